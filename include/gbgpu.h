@@ -1,0 +1,143 @@
+/* gbgpu -- MI355X-native Posdb query scoring, C ABI (the drop-in boundary).
+ *
+ * Replaces the body of PosdbTable::intersectLists10_r (Posdb.cpp:5437-7806)
+ * behind the unchanged Msg39::intersectLists sequence (Msg39.cpp:884-1053):
+ *
+ *   reference call (file:line)                        gbgpu entry point
+ *   ------------------------------------------------  ---------------------------
+ *   PosdbTable::init            Posdb.cpp:722-786      gbgpu_query(...terms, lists)
+ *   PosdbTable::allocTopTree    Posdb.cpp:838-1090     gbgpu_docs_wanted()/internal
+ *   PosdbTable::setQueryTermInfo Posdb.cpp:4354-4869   internal (host plan)
+ *   PosdbTable::intersectLists10_r Posdb.cpp:5437-7806 gbgpu_query / _resident
+ *   TopTree::addNode / getHighNode TopTree.cpp:195-516 gbgpu_result (high -> low)
+ *   Msg3a::mergeLists           Msg3a.cpp:971-1503     gbgpu_merge_topk
+ *   RdbList::posdbMerge_r       RdbList.cpp:3065-3568  gbgpu_merge_posdb
+ *
+ * Conventions: plain pointers and sizes only; the caller owns
+ * every input and output buffer and they are never mutated; the library owns
+ * device memory.  Functions return 0 or a positive errno-style code that the
+ * Msg39 adapter copies into PosdbTable::m_errno; no exceptions cross the ABI.
+ * A context is used by one thread at a time (calls are serialised on an
+ * internal mutex); open one context per INTERSECT thread for concurrency.
+ */
+#ifndef GBGPU_H
+#define GBGPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GBGPU_ABI_VERSION 1
+
+/* error codes beyond errno.h (Errno.h numbering is not reused) */
+#define GBGPU_ENODEVICE   1001 /* no HIP device / extension not usable        */
+#define GBGPU_EUNSUPPORTED 1002 /* request mode outside the GPU path */
+#define GBGPU_ECORRUPT    1003 /* corrupt posdb list (Posdb.cpp:6289-6302)    */
+#define GBGPU_EHIP        1004 /* HIP runtime error                           */
+#define GBGPU_ECAPACITY   1005 /* a fixed device capacity was exceeded        */
+
+typedef struct gbgpu_ctx gbgpu_ctx;
+
+/* One query term, as Query::set2 leaves Query::m_qterms[i] (Query.h:404-580)
+ * and Msg39Request::ptr_termFreqWeights[i] (Msg39.h:152). */
+typedef struct gbgpu_qterm {
+  int32_t is_required;              /* m_isRequired                                  */
+  int32_t term_sign;                /* m_termSign: '-' -> BF_NEGATIVE (Posdb.cpp:4570) */
+  int32_t field_code;               /* m_fieldCode: 0 only (numeric/facet: EUNSUPPORTED) */
+  int32_t piped;                    /* m_piped                                       */
+  int32_t synonym_of;               /* index of m_synonymOf, -1 if none              */
+  int32_t left_phrase_term;         /* m_leftPhraseTermNum, -1 if none               */
+  int32_t right_phrase_term;        /* m_rightPhraseTermNum, -1 if none              */
+  int32_t is_wiki_half_stop_bigram; /* m_isWikiHalfStopBigram                        */
+  int32_t qpos;                     /* m_qword->m_posNum                             */
+  int32_t wiki_phrase_id;           /* m_qword->m_wikiPhraseId                       */
+  int32_t quote_start;              /* m_qword->m_quoteStart, -1 if none             */
+  float   tf_weight;                /* ptr_termFreqWeights[i]                        */
+} gbgpu_qterm;
+
+/* Msg39Request scalars read by PosdbTable (Msg39.h:94-147) */
+typedef struct gbgpu_params {
+  int32_t docs_to_get;      /* m_docsToGet                                        */
+  int32_t real_max_top;     /* m_realMaxTop (clamped to MAX_TOP = 10)              */
+  int32_t language;         /* m_language                                         */
+  int32_t site_clustering;  /* m_doSiteClustering: must be 0 (EUNSUPPORTED)        */
+  int32_t num_docid_splits; /* m_numDocIdSplits: must be 1                         */
+  float   same_lang_weight; /* m_sameLangWeight                                   */
+} gbgpu_params;
+
+/* A posdb termlist exactly as Msg2::getList(i) holds it: first key 18 bytes,
+ * then 12/6-byte compressed keys (RdbList.cpp:282-327).  Host memory. */
+typedef struct gbgpu_list {
+  const uint8_t *bytes;
+  int64_t size;
+} gbgpu_list;
+
+/* The observable PosdbTable state Msg39 reads (Msg39.cpp:402-435, 1346-1420). */
+typedef struct gbgpu_result {
+  int64_t *docids;     /* caller-owned, `capacity` entries; TopTree high -> low   */
+  float   *scores;     /* caller-owned, `capacity` entries (TopNode::m_score)     */
+  int32_t  capacity;
+  int32_t  n;          /* entries written (<= docs_wanted, <= capacity)           */
+  int64_t  hits;       /* m_docIdVoteBuf.length()/6: exact intersection size       */
+  int32_t  filtered;   /* m_filtered                                               */
+  int32_t  docs_wanted;/* TopTree::m_docsWanted (0: no tree was allocated)          */
+} gbgpu_result;
+
+int         gbgpu_open(int device, gbgpu_ctx **out);
+void        gbgpu_close(gbgpu_ctx *ctx);
+const char *gbgpu_strerror(int code);
+int         gbgpu_abi_version(void);
+
+/* allocTopTree sizing (Posdb.cpp:838-930): TopTree::m_docsWanted for a query */
+int32_t gbgpu_docs_wanted(const gbgpu_params *p, const int64_t *list_sizes, int nterms);
+
+/* Full drop-in: lists[] are 1-1 with terms[] (Msg2::getList(i)).  Uploads the
+ * lists, intersects, scores and returns the top tree.  Synchronous. */
+int gbgpu_query(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms, const gbgpu_list *lists,
+                const gbgpu_params *p, gbgpu_result *out);
+
+/* Device-resident index: upload a termlist once (the first-key swap of
+ * Posdb.cpp:5671-5703 is applied to the device copy) and query it many times. */
+int gbgpu_list_upload(gbgpu_ctx *ctx, const uint8_t *bytes, int64_t size, int32_t *handle);
+int gbgpu_list_free(gbgpu_ctx *ctx, int32_t handle);
+int gbgpu_query_resident(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms,
+                         const int32_t *handles, const gbgpu_params *p, gbgpu_result *out);
+
+/* Asynchronous form used by the benchmark: enqueue a resident query on the
+ * context's stream (no host synchronisation), then collect its result.  At
+ * most one query may be in flight per context. */
+int gbgpu_query_resident_enqueue(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms,
+                                 const int32_t *handles, const gbgpu_params *p);
+int gbgpu_query_collect(gbgpu_ctx *ctx, gbgpu_result *out);
+/* the context's HIP stream (hipStream_t), for callers that order work on it */
+void *gbgpu_stream(gbgpu_ctx *ctx);
+/* device copy of the last query's top tree as 16-byte records
+ * {uint32 score_bits, uint32 valid, int64 docid} (the Msg39Reply payload for an
+ * RCCL allgather); returns count via *n after gbgpu_query_collect. */
+int gbgpu_last_topk_device(gbgpu_ctx *ctx, void **dev_ptr, int32_t *n);
+
+/* Msg3a::mergeLists (Msg3a.cpp:1315-1467) without site clustering: k-way merge
+ * of per-shard top lists by (score desc, docid asc), duplicate docids dropped,
+ * first `k` kept.  Scores are widened to double as on the Msg39 wire. */
+int gbgpu_merge_topk(const int64_t *const *shard_docids, const float *const *shard_scores,
+                     const int32_t *shard_counts, int nshards, int32_t k,
+                     int64_t *out_docids, double *out_scores, int32_t *out_n);
+
+/* RdbList::posdbMerge_r (RdbList.cpp:3065-3568): merge n sorted posdb lists
+ * (oldest first; ties keep the newest), optionally annihilating negative
+ * keys, recompressing the output.  out must hold the sum of input sizes. */
+int gbgpu_merge_posdb(gbgpu_ctx *ctx, const gbgpu_list *lists, int n, int remove_neg_keys,
+                      int64_t min_rec_sizes, uint8_t *out, int64_t out_cap, int64_t *out_size);
+
+/* Per-query device timings of the last query (HIP events on the ctx stream),
+ * in milliseconds: [0]=total, [1]=candidate extraction, [2]=list probe scan,
+ * [3]=compaction, [4]=scoring, [5]=top-k.  Enable with gbgpu_set_profiling. */
+int gbgpu_set_profiling(gbgpu_ctx *ctx, int enable);
+int gbgpu_last_timings(gbgpu_ctx *ctx, float *ms6, int64_t *scan_bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,93 @@
+// Query plan: the host-side restatement of PosdbTable::setQueryTermInfo
+// (Posdb.cpp:4354-4869) and allocTopTree sizing (Posdb.cpp:838-930), plus the
+// POD image of it that the kernels read from device memory.
+#ifndef GBGPU_PLAN_H
+#define GBGPU_PLAN_H
+
+#include <stdint.h>
+
+#include "../../include/gbgpu.h"
+
+namespace gbgpu {
+
+// Posdb.h:102-108
+enum : uint8_t {
+  BF_HALFSTOPWIKIBIGRAM = 0x01,
+  BF_PIPED = 0x02,
+  BF_SYNONYM = 0x04,
+  BF_NEGATIVE = 0x08,
+  BF_BIGRAM = 0x10,
+  BF_NUMBER = 0x20,
+  BF_FACET = 0x40,
+};
+constexpr uint8_t BF_EXCLUDE = BF_PIPED | BF_NEGATIVE | BF_NUMBER | BF_FACET;
+
+constexpr int REF_MAX_SUBLISTS = 50;  // Posdb.h:417
+// GPU-path capacities (EUNSUPPORTED beyond)
+constexpr int MAXG = 16;     // QueryTermInfos (required term groups)
+constexpr int MAXSUB = 16;   // sublists per group
+constexpr int MAXL = 32;     // distinct lists referenced by one query
+constexpr int MAXG0 = 8;     // sublists of the smallest group (candidate arrays)
+constexpr uint32_t NEG_BIT = 0x80000000u;
+
+// One QueryTermInfo (Posdb.h:421-451), host form.
+struct GroupInfo {
+  int qterm;                       // m_qtermNum
+  int nsub;                        // m_numSubLists
+  int sub_term[REF_MAX_SUBLISTS];  // query-term index of each sublist
+  uint8_t flags[REF_MAX_SUBLISTS]; // m_bigramFlags (incl. written-but-uncounted slots)
+  int64_t total;                   // m_totalSubListsSize (pre-swap sizes)
+  float tfw;
+  int qpos, wiki, quote;
+};
+
+struct HostPlan {
+  int nqt = 0;
+  int ngroups = 0;
+  GroupInfo g[MAXG * 4];
+  int min_listi = -1;
+  int64_t min_list_size = 0;
+  int32_t docs_wanted = 0;
+  int real_max_top = 10;
+};
+
+// Device image.  Lists are addressed by a dense id 0..nlists-1.
+struct DevList {
+  const uint8_t *p;     // swapped list (12-byte first key), 16-B aligned, zero padded
+  uint32_t units;       // (size-6)/6
+  uint32_t group_bits;  // positive groups containing this list (+NEG_BIT if in a negative group)
+  int32_t g0_array;     // index among the smallest group's candidate arrays, -1 if none
+  int32_t probe;        // 1: scanned by the probe kernel
+};
+
+struct DevPlan {
+  int ngroups;
+  int nlists;
+  uint32_t pos_mask;
+  int real_max_top;
+  int language;
+  float same_lang_weight;
+  float site_rank_multiplier;
+  int nqt;  // Query::m_numTerms (scoreMatrix stride)
+  // groups, in QueryTermInfo order
+  uint8_t gflags0[MAXG];            // m_bigramFlags[0]
+  uint8_t gnsub[MAXG];
+  uint8_t gsub[MAXG][MAXSUB];       // dense list id per original sublist index
+  uint8_t gsubflags[MAXG][MAXSUB];  // m_bigramFlags[x]
+  float tfw[MAXG];
+  int32_t qpos[MAXG], wiki[MAXG], quote[MAXG];
+  // candidate arrays (sublists of m_minListi, distinct lists, in order)
+  int g0n;
+  int g0list[MAXG0];
+  uint64_t g0base[MAXG0 + 1];  // slot base of each array (prefix of upper bounds)
+  DevList lists[MAXL];
+};
+
+// setQueryTermInfo + minListi; returns 0 or error.
+int build_host_plan(const gbgpu_qterm *terms, int nterms, const int64_t *sizes,
+                    const gbgpu_params *p, HostPlan *hp);
+int32_t docs_wanted(const gbgpu_params *p, const int64_t *sizes, int nterms);
+
+}  // namespace gbgpu
+
+#endif

@@ -1,0 +1,350 @@
+"""ctypes binding of the gbgpu C ABI (include/gbgpu.h, include/gbgpu_synth.h).
+
+The product is the C-ABI library ``lib/libgbgpu.so``; this module is the thin
+Python view of it that the tests and ``bench.py`` use (the Gigablast host would
+bind the same symbols from C++).  Loading fails loudly if
+the library is missing: there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_DIR = os.path.dirname(_HERE)
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libgbgpu.so")
+
+GBGPU_ENODEVICE = 1001
+GBGPU_EUNSUPPORTED = 1002
+GBGPU_ECORRUPT = 1003
+GBGPU_EHIP = 1004
+GBGPU_ECAPACITY = 1005
+
+
+class QTerm(ctypes.Structure):
+    """gbgpu_qterm == Query::m_qterms[i] (+ its tf weight)."""
+
+    _fields_ = [
+        ("is_required", ctypes.c_int32),
+        ("term_sign", ctypes.c_int32),
+        ("field_code", ctypes.c_int32),
+        ("piped", ctypes.c_int32),
+        ("synonym_of", ctypes.c_int32),
+        ("left_phrase_term", ctypes.c_int32),
+        ("right_phrase_term", ctypes.c_int32),
+        ("is_wiki_half_stop_bigram", ctypes.c_int32),
+        ("qpos", ctypes.c_int32),
+        ("wiki_phrase_id", ctypes.c_int32),
+        ("quote_start", ctypes.c_int32),
+        ("tf_weight", ctypes.c_float),
+    ]
+
+
+class Params(ctypes.Structure):
+    _fields_ = [
+        ("docs_to_get", ctypes.c_int32),
+        ("real_max_top", ctypes.c_int32),
+        ("language", ctypes.c_int32),
+        ("site_clustering", ctypes.c_int32),
+        ("num_docid_splits", ctypes.c_int32),
+        ("same_lang_weight", ctypes.c_float),
+    ]
+
+
+class ListRef(ctypes.Structure):
+    _fields_ = [("bytes", ctypes.c_void_p), ("size", ctypes.c_int64)]
+
+
+class Result(ctypes.Structure):
+    _fields_ = [
+        ("docids", ctypes.POINTER(ctypes.c_int64)),
+        ("scores", ctypes.POINTER(ctypes.c_float)),
+        ("capacity", ctypes.c_int32),
+        ("n", ctypes.c_int32),
+        ("hits", ctypes.c_int64),
+        ("filtered", ctypes.c_int32),
+        ("docs_wanted", ctypes.c_int32),
+    ]
+
+
+class SynthCorpus(ctypes.Structure):
+    _fields_ = [
+        ("num_docs", ctypes.c_int64),
+        ("seed", ctypes.c_uint64),
+        ("doc_begin", ctypes.c_int64),
+        ("doc_end", ctypes.c_int64),
+        ("max_positions", ctypes.c_int32),
+        ("num_threads", ctypes.c_int32),
+    ]
+
+
+class SynthTerm(ctypes.Structure):
+    _fields_ = [
+        ("term_id", ctypes.c_uint64),
+        ("p", ctypes.c_double),
+        ("kind", ctypes.c_int32),
+        ("a", ctypes.c_int32),
+        ("b", ctypes.c_int32),
+        ("align_to", ctypes.c_int32),
+        ("syn_frac_pct", ctypes.c_int32),
+    ]
+
+
+SYNTH_WORD, SYNTH_SYNONYM, SYNTH_BIGRAM = 0, 1, 2
+
+# every symbol include/gbgpu.h and include/gbgpu_synth.h declare
+EXPORTS = [
+    "gbgpu_open", "gbgpu_close", "gbgpu_strerror", "gbgpu_abi_version", "gbgpu_docs_wanted",
+    "gbgpu_query", "gbgpu_list_upload", "gbgpu_list_free", "gbgpu_query_resident",
+    "gbgpu_query_resident_enqueue", "gbgpu_query_collect", "gbgpu_stream",
+    "gbgpu_last_topk_device", "gbgpu_merge_topk", "gbgpu_merge_posdb", "gbgpu_set_profiling",
+    "gbgpu_last_timings",
+    "gb_synth_lists", "gb_synth_free", "gb_synth_docid", "gb_posdb_compress", "gb_posdb_make_key",
+]
+
+_lib: Optional[ctypes.CDLL] = None
+
+
+def load(path: str = LIB_PATH) -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError(f"gbgpu native library not built: {path} (run __graft_entry__.build())")
+    lib = ctypes.CDLL(path)
+    vp, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
+    lib.gbgpu_open.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
+    lib.gbgpu_close.argtypes = [vp]
+    lib.gbgpu_close.restype = None
+    lib.gbgpu_strerror.argtypes = [ctypes.c_int]
+    lib.gbgpu_strerror.restype = ctypes.c_char_p
+    lib.gbgpu_docs_wanted.argtypes = [ctypes.POINTER(Params), ctypes.POINTER(i64), ctypes.c_int]
+    lib.gbgpu_docs_wanted.restype = i32
+    lib.gbgpu_query.argtypes = [vp, ctypes.POINTER(QTerm), ctypes.c_int, ctypes.POINTER(ListRef),
+                                ctypes.POINTER(Params), ctypes.POINTER(Result)]
+    lib.gbgpu_list_upload.argtypes = [vp, vp, i64, ctypes.POINTER(i32)]
+    lib.gbgpu_list_free.argtypes = [vp, i32]
+    lib.gbgpu_query_resident.argtypes = [vp, ctypes.POINTER(QTerm), ctypes.c_int, ctypes.POINTER(i32),
+                                         ctypes.POINTER(Params), ctypes.POINTER(Result)]
+    lib.gbgpu_query_resident_enqueue.argtypes = [vp, ctypes.POINTER(QTerm), ctypes.c_int,
+                                                 ctypes.POINTER(i32), ctypes.POINTER(Params)]
+    lib.gbgpu_query_collect.argtypes = [vp, ctypes.POINTER(Result)]
+    lib.gbgpu_stream.argtypes = [vp]
+    lib.gbgpu_stream.restype = vp
+    lib.gbgpu_last_topk_device.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(i32)]
+    lib.gbgpu_merge_topk.argtypes = [ctypes.POINTER(ctypes.POINTER(i64)),
+                                     ctypes.POINTER(ctypes.POINTER(ctypes.c_float)),
+                                     ctypes.POINTER(i32), ctypes.c_int, i32, ctypes.POINTER(i64),
+                                     ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i32)]
+    lib.gbgpu_merge_posdb.argtypes = [vp, ctypes.POINTER(ListRef), ctypes.c_int, ctypes.c_int, i64, vp,
+                                      i64, ctypes.POINTER(i64)]
+    lib.gbgpu_set_profiling.argtypes = [vp, ctypes.c_int]
+    lib.gbgpu_last_timings.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(i64)]
+    lib.gb_synth_lists.argtypes = [ctypes.POINTER(SynthCorpus), ctypes.POINTER(SynthTerm), ctypes.c_int,
+                                   ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(i64)]
+    lib.gb_synth_free.argtypes = [vp]
+    lib.gb_synth_free.restype = None
+    lib.gb_synth_docid.argtypes = [ctypes.POINTER(SynthCorpus), i64]
+    lib.gb_synth_docid.restype = ctypes.c_uint64
+    lib.gb_posdb_compress.argtypes = [vp, i64, vp]
+    lib.gb_posdb_compress.restype = i64
+    lib.gb_posdb_make_key.argtypes = [vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
+                                      ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                      ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
+                                      ctypes.c_int, ctypes.c_int]
+    lib.gb_posdb_make_key.restype = None
+    _lib = lib
+    return lib
+
+
+class GbgpuError(RuntimeError):
+    def __init__(self, code: int, what: str = ""):
+        self.code = code
+        msg = load().gbgpu_strerror(code).decode()
+        super().__init__(f"gbgpu error {code} ({msg}) {what}")
+
+
+def _check(rc: int, what: str = "") -> None:
+    if rc != 0:
+        raise GbgpuError(rc, what)
+
+
+# ---------------------------------------------------------------- synthesis
+@dataclass
+class TermSpec:
+    term_id: int
+    p: float
+    kind: int = SYNTH_WORD
+    a: int = -1
+    b: int = -1
+    align_to: int = -1
+    syn_frac_pct: int = 0
+
+
+def synth_lists(num_docs: int, specs: Sequence[TermSpec], seed: int = 0x6B1A57, doc_begin: int = 0,
+                doc_end: int = 0, max_positions: int = 64, threads: int = 0) -> List[bytes]:
+    lib = load()
+    c = SynthCorpus(num_docs, seed, doc_begin, doc_end, max_positions, threads)
+    n = len(specs)
+    arr = (SynthTerm * n)(*[SynthTerm(s.term_id, s.p, s.kind, s.a, s.b, s.align_to, s.syn_frac_pct)
+                            for s in specs])
+    bufs = (ctypes.c_void_p * n)()
+    sizes = (ctypes.c_int64 * n)()
+    _check(lib.gb_synth_lists(ctypes.byref(c), arr, n, bufs, sizes), "gb_synth_lists")
+    out = []
+    for i in range(n):
+        if sizes[i]:
+            out.append(ctypes.string_at(bufs[i], sizes[i]))
+            lib.gb_synth_free(bufs[i])
+        else:
+            out.append(b"")
+    return out
+
+
+def make_key(term_id, docid, wordpos, density, diversity, spam, siterank, hashgroup, langid,
+             multiplier=0, syn=0, delkey=0, shard_by_termid=0) -> bytes:
+    buf = ctypes.create_string_buffer(18)
+    load().gb_posdb_make_key(buf, term_id, docid, wordpos, density, diversity, spam, siterank, hashgroup,
+                             langid, multiplier, syn, delkey, shard_by_termid)
+    return buf.raw
+
+
+def compress(keys18: bytes) -> bytes:
+    n = len(keys18) // 18
+    out = ctypes.create_string_buffer(max(1, 18 * n))
+    inb = ctypes.create_string_buffer(keys18, max(1, len(keys18)))
+    m = load().gb_posdb_compress(inb, n, out)
+    return out.raw[:m]
+
+
+def docs_wanted(params: Params, sizes: Sequence[int]) -> int:
+    arr = (ctypes.c_int64 * max(1, len(sizes)))(*sizes)
+    return load().gbgpu_docs_wanted(ctypes.byref(params), arr, len(sizes))
+
+
+# ------------------------------------------------------------------- engine
+@dataclass
+class QueryResult:
+    docids: np.ndarray
+    scores: np.ndarray
+    hits: int
+    filtered: int
+    docs_wanted: int
+
+
+class Engine:
+    """One gbgpu context (one HIP stream) on one device."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load()
+        self.ctx = ctypes.c_void_p()
+        _check(self.lib.gbgpu_open(device, ctypes.byref(self.ctx)), "gbgpu_open")
+        self._keep = {}
+
+    def close(self) -> None:
+        if self.ctx:
+            self.lib.gbgpu_close(self.ctx)
+            self.ctx = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def upload(self, data: bytes) -> int:
+        h = ctypes.c_int32()
+        buf = ctypes.create_string_buffer(data, max(1, len(data)))
+        _check(self.lib.gbgpu_list_upload(self.ctx, buf, len(data), ctypes.byref(h)), "upload")
+        return h.value
+
+    def free(self, handle: int) -> None:
+        _check(self.lib.gbgpu_list_free(self.ctx, handle), "free")
+
+    @staticmethod
+    def _result(cap: int):
+        d = (ctypes.c_int64 * max(cap, 1))()
+        s = (ctypes.c_float * max(cap, 1))()
+        r = Result(ctypes.cast(d, ctypes.POINTER(ctypes.c_int64)), ctypes.cast(s, ctypes.POINTER(ctypes.c_float)),
+                   cap, 0, 0, 0, 0)
+        return r, d, s
+
+    @staticmethod
+    def _pack(r, d, s) -> QueryResult:
+        n = r.n
+        return QueryResult(np.frombuffer(d, dtype=np.int64, count=n).copy(),
+                           np.frombuffer(s, dtype=np.float32, count=n).copy(), r.hits, r.filtered, r.docs_wanted)
+
+    def query(self, terms: Sequence[QTerm], lists: Sequence[bytes], params: Params, cap: int = 4096) -> QueryResult:
+        n = len(terms)
+        qt = (QTerm * max(n, 1))(*terms)
+        keep = [ctypes.create_string_buffer(l, max(1, len(l))) for l in lists]
+        refs = (ListRef * max(n, 1))(*[ListRef(ctypes.cast(k, ctypes.c_void_p), len(l)) for k, l in zip(keep, lists)])
+        r, d, s = self._result(cap)
+        _check(self.lib.gbgpu_query(self.ctx, qt, n, refs, ctypes.byref(params), ctypes.byref(r)), "query")
+        return self._pack(r, d, s)
+
+    def query_resident(self, terms: Sequence[QTerm], handles: Sequence[int], params: Params,
+                       cap: int = 4096) -> QueryResult:
+        n = len(terms)
+        qt = (QTerm * max(n, 1))(*terms)
+        hh = (ctypes.c_int32 * max(n, 1))(*handles)
+        r, d, s = self._result(cap)
+        _check(self.lib.gbgpu_query_resident(self.ctx, qt, n, hh, ctypes.byref(params), ctypes.byref(r)), "query")
+        return self._pack(r, d, s)
+
+    def enqueue(self, terms: Sequence[QTerm], handles: Sequence[int], params: Params) -> None:
+        n = len(terms)
+        qt = (QTerm * max(n, 1))(*terms)
+        hh = (ctypes.c_int32 * max(n, 1))(*handles)
+        _check(self.lib.gbgpu_query_resident_enqueue(self.ctx, qt, n, hh, ctypes.byref(params)), "enqueue")
+
+    def collect(self, cap: int = 4096) -> QueryResult:
+        r, d, s = self._result(cap)
+        _check(self.lib.gbgpu_query_collect(self.ctx, ctypes.byref(r)), "collect")
+        return self._pack(r, d, s)
+
+    def set_profiling(self, on: bool) -> None:
+        _check(self.lib.gbgpu_set_profiling(self.ctx, 1 if on else 0))
+
+    def last_timings(self):
+        ms = (ctypes.c_float * 6)()
+        sb = ctypes.c_int64()
+        _check(self.lib.gbgpu_last_timings(self.ctx, ms, ctypes.byref(sb)))
+        return list(ms), sb.value
+
+    def stream(self) -> int:
+        return self.lib.gbgpu_stream(self.ctx) or 0
+
+    def last_topk_device(self):
+        p = ctypes.c_void_p()
+        n = ctypes.c_int32()
+        _check(self.lib.gbgpu_last_topk_device(self.ctx, ctypes.byref(p), ctypes.byref(n)))
+        return p.value, n.value
+
+
+def merge_topk(shards, k: int):
+    """Msg3a::mergeLists over [(docids int64[], scores float32[]), ...]."""
+    lib = load()
+    ns = len(shards)
+    keep = []
+    dptrs = (ctypes.POINTER(ctypes.c_int64) * max(ns, 1))()
+    sptrs = (ctypes.POINTER(ctypes.c_float) * max(ns, 1))()
+    cnts = (ctypes.c_int32 * max(ns, 1))()
+    for i, (d, s) in enumerate(shards):
+        d = np.ascontiguousarray(d, dtype=np.int64)
+        s = np.ascontiguousarray(s, dtype=np.float32)
+        keep += [d, s]
+        dptrs[i] = d.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))
+        sptrs[i] = s.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+        cnts[i] = len(d)
+    od = np.zeros(max(k, 1), dtype=np.int64)
+    os_ = np.zeros(max(k, 1), dtype=np.float64)
+    n = ctypes.c_int32()
+    _check(lib.gbgpu_merge_topk(dptrs, sptrs, cnts, ns, k, od.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                                os_.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), ctypes.byref(n)))
+    return od[:n.value], os_[:n.value]

@@ -1,0 +1,1348 @@
+/* TEST INFRASTRUCTURE ONLY (see posdb_oracle.h).
+ *
+ * CPU restatement of the reference's Posdb query path, written against the
+ * reference's own byte-level algorithm so that it inherits its exact
+ * behaviour, quirks included.  Compile with -ffp-contract=off: the reference
+ * is x86-64 SSE -O2 (Makefile:101), FLT_EVAL_METHOD 0, no FMA, so every float
+ * expression below is written with the same operand types and order as the
+ * reference expression it restates and rounds the same way.
+ *
+ * Parity unpinned for scoring (no reference fixture exists and the reference
+ * path is unbuildable here without source edits).
+ */
+#include "posdb_oracle.h"
+
+#include <errno.h>
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* Posdb.h:102-108 */
+#define BF_HALFSTOPWIKIBIGRAM 0x01
+#define BF_PIPED              0x02
+#define BF_SYNONYM            0x04
+#define BF_NEGATIVE           0x08
+#define BF_BIGRAM             0x10
+#define BF_NUMBER             0x20
+#define BF_FACET              0x40
+#define BF_EXCLUDE (BF_PIPED | BF_NEGATIVE | BF_NUMBER | BF_FACET)
+
+#define MAX_SUBLISTS 50        /* Posdb.h:417 */
+#define MAX_TOP 10             /* Posdb.h:817 */
+#define FIXED_DISTANCE 400     /* Posdb.h:765 */
+#define SYNONYM_WEIGHT 0.90    /* Posdb.h:94  */
+#define WIKI_WEIGHT 0.10       /* Posdb.h:95  */
+#define SITERANKMULTIPLIER 0.33333333 /* Posdb.h:97 */
+#define WIKI_BIGRAM_WEIGHT 1.40       /* Posdb.h:115 */
+
+#define HASHGROUP_BODY 0
+#define HASHGROUP_TITLE 1
+#define HASHGROUP_HEADING 2
+#define HASHGROUP_INLIST 3
+#define HASHGROUP_INMETATAG 4
+#define HASHGROUP_INLINKTEXT 5
+#define HASHGROUP_INTAG 6
+#define HASHGROUP_NEIGHBORHOOD 7
+#define HASHGROUP_INTERNALINLINKTEXT 8
+#define HASHGROUP_INURL 9
+#define HASHGROUP_INMENU 10
+#define HASHGROUP_END 11
+
+/* ---------------------------------------------------------------- weights */
+/* initWeights, Posdb.cpp:1094-1197 */
+static int s_init = 0;
+static float s_diversityWeights[16];
+static float s_densityWeights[32];
+static float s_wordSpamWeights[16];
+static float s_linkerWeights[16];
+static float s_hashGroupWeights[HASHGROUP_END];
+static char s_isCompatible[HASHGROUP_END][HASHGROUP_END];
+static char s_inBody[HASHGROUP_END];
+
+static void initWeights(void) {
+  if (s_init) return;
+  s_init = 1;
+  float sum = 0.15;
+  for (int i = 0; i <= 15; i++) {
+    s_diversityWeights[i] = 1.0;
+    sum *= 1.135;
+  }
+  sum = 0.35;
+  for (int i = 0; i <= 31; i++) {
+    if (sum > 1.0) sum = 1.0;
+    s_densityWeights[i] = sum;
+    sum *= 1.03445;
+  }
+  for (int i = 0; i <= 15; i++) s_wordSpamWeights[i] = (float)(i + 1) / (15 + 1);
+  for (int i = 0; i <= 15; i++) s_linkerWeights[i] = sqrt(1.0 + i);
+  for (int i = 0; i < HASHGROUP_END; i++) {
+    s_inBody[i] = 0;
+    if (i == HASHGROUP_BODY || i == HASHGROUP_HEADING || i == HASHGROUP_INLIST ||
+        i == HASHGROUP_INMENU)
+      s_inBody[i] = 1;
+    for (int j = 0; j < HASHGROUP_END; j++) {
+      s_isCompatible[i][j] = 0;
+      int inBody1 = 1, inBody2 = 1;
+      if (i != HASHGROUP_BODY && i != HASHGROUP_HEADING && i != HASHGROUP_INLIST &&
+          i != HASHGROUP_INMENU)
+        inBody1 = 0;
+      if (j != HASHGROUP_BODY && j != HASHGROUP_HEADING && j != HASHGROUP_INLIST &&
+          j != HASHGROUP_INMENU)
+        inBody2 = 0;
+      if (inBody1 || inBody2) continue;
+      s_isCompatible[i][j] = 1;
+    }
+  }
+  s_hashGroupWeights[HASHGROUP_BODY] = 1.0;
+  s_hashGroupWeights[HASHGROUP_TITLE] = 8.0;
+  s_hashGroupWeights[HASHGROUP_HEADING] = 1.5;
+  s_hashGroupWeights[HASHGROUP_INLIST] = 0.3;
+  s_hashGroupWeights[HASHGROUP_INMETATAG] = 0.1;
+  s_hashGroupWeights[HASHGROUP_INLINKTEXT] = 16.0;
+  s_hashGroupWeights[HASHGROUP_INTAG] = 1.0;
+  s_hashGroupWeights[HASHGROUP_NEIGHBORHOOD] = 0.0;
+  s_hashGroupWeights[HASHGROUP_INTERNALINLINKTEXT] = 4.0;
+  s_hashGroupWeights[HASHGROUP_INURL] = 1.0;
+  s_hashGroupWeights[HASHGROUP_INMENU] = 0.2;
+}
+
+void orc_weights(float *d32, float *w16, float *l16, float *h11, float *v16) {
+  initWeights();
+  if (d32) memcpy(d32, s_densityWeights, sizeof s_densityWeights);
+  if (w16) memcpy(w16, s_wordSpamWeights, sizeof s_wordSpamWeights);
+  if (l16) memcpy(l16, s_linkerWeights, sizeof s_linkerWeights);
+  if (h11) memcpy(h11, s_hashGroupWeights, sizeof s_hashGroupWeights);
+  if (v16) memcpy(v16, s_diversityWeights, sizeof s_diversityWeights);
+}
+
+/* ------------------------------------------------------------ key getters */
+/* Posdb.h:271-380 */
+static inline uint32_t U32(const uint8_t *p) { uint32_t v; memcpy(&v, p, 4); return v; }
+static inline uint16_t U16(const uint8_t *p) { uint16_t v; memcpy(&v, p, 2); return v; }
+static inline int keySize(const uint8_t *k) { return (k[0] & 0x04) ? 6 : ((k[0] & 0x02) ? 12 : 18); }
+static inline uint64_t getDocId(const uint8_t *k) {
+  uint64_t d = k[11];
+  d <<= 32;
+  d |= U32(k + 7);
+  return d >> 2;
+}
+static inline unsigned char getSiteRank(const uint8_t *k) {
+  uint64_t n1;
+  memcpy(&n1, k + 2, 8);
+  return (n1 >> 37) & 0x0f;
+}
+static inline unsigned char getLangId(const uint8_t *k) {
+  uint64_t n1;
+  memcpy(&n1, k + 2, 8);
+  if (k[0] & 0x08) return ((n1 >> 32) & 0x1f) | 0x20;
+  return (n1 >> 32) & 0x1f;
+}
+static inline unsigned char getHashGroup(const uint8_t *k) { return (k[3] >> 2) & 0x0f; }
+static inline int32_t getWordPos(const uint8_t *k) { return U32(k + 2) >> (8 + 6); }
+static inline unsigned char getWordSpamRank(const uint8_t *k) { return (U16(k + 2) >> 6) & 0x0f; }
+static inline unsigned char getDiversityRank(const uint8_t *k) { return (k[2] >> 2) & 0x0f; }
+static inline unsigned char getIsSynonym(const uint8_t *k) { return k[2] & 0x03; }
+static inline unsigned char getIsHalfStopWikiBigram(const uint8_t *k) { return k[2] & 0x01; }
+static inline unsigned char getDensityRank(const uint8_t *k) { return (U16(k) >> 11) & 0x1f; }
+
+/* ------------------------------------------------------------ structures */
+typedef struct {
+  uint8_t *list; /* RdbList::m_list (mutated by the first-key swap) */
+  int64_t size;  /* RdbList::m_listSize                              */
+} OList;
+
+/* QueryTermInfo, Posdb.h:421-451 (sublists refer to query-term lists) */
+typedef struct {
+  int subList[MAX_SUBLISTS];
+  char bigramFlags[MAX_SUBLISTS];
+  int64_t newSubListSize[MAX_SUBLISTS];
+  uint8_t *newSubListStart[MAX_SUBLISTS];
+  uint8_t *newSubListEnd[MAX_SUBLISTS];
+  uint8_t *cursor[MAX_SUBLISTS];
+  uint8_t *savedCursor[MAX_SUBLISTS];
+  int numNewSubLists;
+  int numSubLists;
+  int64_t totalSubListsSize;
+  float termFreqWeight;
+  int qtermNum, qpos, wikiPhraseId, quotedStartId;
+} QTI;
+
+typedef struct {
+  /* PosdbTable state used by the scorers */
+  int realMaxTop;
+  float *freqWeights;
+  int32_t *qpos, *wikiPhraseIds, *quotedStartIds;
+  char *bflags;
+  int32_t qdist;
+  float bestWindowScore;
+  uint8_t **windowTermPtrs;
+  uint64_t docId;
+  int nqt;
+} PT;
+
+/* TopTree semantics without site clustering (TopTree.cpp:206-516): keep the
+ * best docsWanted by (score desc, docid asc); sorted high -> low here. */
+typedef struct {
+  int cap, n;
+  float *score;
+  int64_t *docid;
+} TopK;
+
+static void topk_add(TopK *t, float score, int64_t docid) {
+  if (t->cap <= 0) return;
+  if (t->n >= t->cap) {
+    float ls = t->score[t->n - 1];
+    int64_t ld = t->docid[t->n - 1];
+    if (score < ls) return;
+    if (!(score > ls) && docid >= ld) return;
+  }
+  int pos = t->n < t->cap ? t->n : t->cap - 1;
+  /* find insertion point: first entry that ranks below (score, docid) */
+  int i = 0;
+  while (i < t->n && i < t->cap) {
+    if (t->score[i] < score || (t->score[i] == score && t->docid[i] > docid)) break;
+    if (t->score[i] == score && t->docid[i] == docid) return; /* "if equal do not replace" */
+    i++;
+  }
+  if (i >= t->cap) return;
+  if (t->n < t->cap) { pos = t->n; t->n++; }
+  for (int k = pos; k > i; k--) {
+    t->score[k] = t->score[k - 1];
+    t->docid[k] = t->docid[k - 1];
+  }
+  t->score[i] = score;
+  t->docid[i] = docid;
+}
+
+/* --------------------------------------------------------------- scorers */
+/* getSingleTermScore, Posdb.cpp:3087-3301 (pdcs == NULL) */
+static float getSingleTermScore(PT *pt, int i, uint8_t *wpi, uint8_t *endi, uint8_t **bestPos) {
+  float nonBodyMax = -1.0;
+  int first = 1;
+  int32_t minx = 0;
+  float bestScores[MAX_TOP];
+  uint8_t *bestwpi[MAX_TOP];
+  char bestmhg[MAX_TOP];
+  int32_t numTop = 0;
+  *bestPos = NULL;
+  if (!wpi) goto done;
+  for (;;) {
+    float score = 100.0;
+    unsigned char div = getDiversityRank(wpi);
+    score *= s_diversityWeights[div];
+    score *= s_diversityWeights[div];
+    unsigned char hg = getHashGroup(wpi);
+    unsigned char mhg = hg;
+    if (s_inBody[mhg]) mhg = HASHGROUP_BODY;
+    score *= s_hashGroupWeights[hg];
+    score *= s_hashGroupWeights[hg];
+    unsigned char dens = getDensityRank(wpi);
+    score *= s_densityWeights[dens];
+    score *= s_densityWeights[dens];
+    unsigned char wspam = getWordSpamRank(wpi);
+    if (hg == HASHGROUP_INLINKTEXT) {
+      score *= s_linkerWeights[wspam];
+      score *= s_linkerWeights[wspam];
+    } else {
+      score *= s_wordSpamWeights[wspam];
+      score *= s_wordSpamWeights[wspam];
+    }
+    if (getIsSynonym(wpi)) {
+      score *= SYNONYM_WEIGHT;
+      score *= SYNONYM_WEIGHT;
+    }
+    int32_t bro = -1;
+    for (int32_t k = 0; k < numTop; k++) {
+      if (bestmhg[k] == mhg && hg != HASHGROUP_INLINKTEXT) {
+        bro = k;
+        break;
+      }
+    }
+    if (bro >= 0) {
+      if (score > bestScores[bro]) {
+        bestScores[bro] = score;
+        bestwpi[bro] = wpi;
+        bestmhg[bro] = mhg;
+      }
+    } else if (numTop < pt->realMaxTop) {
+      bestScores[numTop] = score;
+      bestwpi[numTop] = wpi;
+      bestmhg[numTop] = mhg;
+      numTop++;
+    } else if (score > bestScores[minx]) {
+      bestScores[minx] = score;
+      bestwpi[minx] = wpi;
+      bestmhg[minx] = mhg;
+    }
+    if (numTop >= pt->realMaxTop) {
+      minx = 0;
+      for (int32_t k = 1; k < pt->realMaxTop; k++) {
+        if (bestScores[k] > bestScores[minx]) continue;
+        minx = k;
+      }
+    }
+    if (score > nonBodyMax && !s_inBody[hg]) {
+      nonBodyMax = score;
+      *bestPos = wpi;
+    }
+    if (first) { wpi += 6; first = 0; }
+    wpi += 6;
+    if (wpi < endi && keySize(wpi) == 6) continue;
+    break;
+  }
+done:;
+  float sum = 0.0;
+  for (int32_t k = 0; k < numTop; k++) {
+    if (getIsHalfStopWikiBigram(bestwpi[k]))
+      sum += (bestScores[k] * WIKI_BIGRAM_WEIGHT * WIKI_BIGRAM_WEIGHT);
+    else
+      sum += bestScores[k];
+  }
+  sum *= pt->freqWeights[i];
+  sum *= pt->freqWeights[i];
+  return sum;
+}
+
+/* getTermPairScoreForNonBody, Posdb.cpp:3305-3555 (m_msg2 != NULL) */
+static void getTermPairScoreForNonBody(PT *pt, int i, int j, uint8_t *wpi, uint8_t *wpj,
+                                       uint8_t *endi, uint8_t *endj, int32_t qdist, float *retMax) {
+  (void)pt; (void)i; (void)j;
+  int32_t p1 = getWordPos(wpi);
+  int32_t p2 = getWordPos(wpj);
+  unsigned char hg1 = getHashGroup(wpi);
+  unsigned char hg2 = getHashGroup(wpj);
+  unsigned char wsr1 = getWordSpamRank(wpi);
+  unsigned char wsr2 = getWordSpamRank(wpj);
+  float spamw1, spamw2;
+  if (hg1 == HASHGROUP_INLINKTEXT) spamw1 = s_linkerWeights[wsr1];
+  else spamw1 = s_wordSpamWeights[wsr1];
+  if (hg2 == HASHGROUP_INLINKTEXT) spamw2 = s_linkerWeights[wsr2];
+  else spamw2 = s_wordSpamWeights[wsr2];
+  float denw1 = s_densityWeights[getDensityRank(wpi)];
+  float denw2 = s_densityWeights[getDensityRank(wpj)];
+  int firsti = 1, firstj = 1;
+  float score;
+  float max = -1.0;
+  int32_t dist;
+  for (;;) {
+    if (p1 <= p2) {
+      if (!s_isCompatible[hg1][hg2]) goto skip1;
+      dist = p2 - p1;
+      if (dist < 2) dist = 2;
+      if (dist > 50) dist = FIXED_DISTANCE;
+      if (dist >= qdist) dist = dist - qdist;
+      score = 100 * denw1 * denw2;
+      score *= s_hashGroupWeights[hg1];
+      score *= s_hashGroupWeights[hg2];
+      if (getIsSynonym(wpi)) score *= SYNONYM_WEIGHT;
+      if (getIsSynonym(wpj)) score *= SYNONYM_WEIGHT;
+      score *= spamw1 * spamw2;
+      score /= (dist + 1.0);
+      if (score > max) max = score;
+    skip1:
+      if (firsti) { wpi += 6; firsti = 0; }
+      wpi += 6;
+      if (wpi >= endi) break;
+      if (keySize(wpi) != 6) break;
+      p1 = getWordPos(wpi);
+      hg1 = getHashGroup(wpi);
+      denw1 = s_densityWeights[getDensityRank(wpi)];
+      if (hg1 == HASHGROUP_INLINKTEXT) spamw1 = s_linkerWeights[getWordSpamRank(wpi)];
+      else spamw1 = s_wordSpamWeights[getWordSpamRank(wpi)];
+    } else {
+      if (!s_isCompatible[hg1][hg2]) goto skip2;
+      dist = p1 - p2;
+      if (dist < 2) dist = 2;
+      if (dist > 50) dist = FIXED_DISTANCE;
+      if (dist >= qdist) {
+        dist = dist - qdist;
+        dist += qdist - 1;
+      } else {
+        dist += 1;
+      }
+      score = 100 * denw1 * denw2;
+      score *= s_hashGroupWeights[hg1];
+      score *= s_hashGroupWeights[hg2];
+      if (getIsSynonym(wpi)) score *= SYNONYM_WEIGHT;
+      if (getIsSynonym(wpj)) score *= SYNONYM_WEIGHT;
+      score *= spamw1 * spamw2;
+      score /= (dist + 1.0);
+      if (score > max) max = score;
+    skip2:
+      if (firstj) { wpj += 6; firstj = 0; }
+      wpj += 6;
+      if (wpj >= endj) break;
+      if (keySize(wpj) != 6) break;
+      p2 = getWordPos(wpj);
+      hg2 = getHashGroup(wpj);
+      denw2 = s_densityWeights[getDensityRank(wpj)];
+      if (hg2 == HASHGROUP_INLINKTEXT) spamw2 = s_linkerWeights[getWordSpamRank(wpj)];
+      else spamw2 = s_wordSpamWeights[getWordSpamRank(wpj)];
+    }
+  }
+  *retMax = max;
+}
+
+/* getTermPairScoreForWindow, Posdb.cpp:3557-3625 */
+static float getTermPairScoreForWindow(PT *pt, uint8_t *wpi, uint8_t *wpj, int32_t fixedDistance) {
+  if (!wpi) return -1.00;
+  if (!wpj) return -1.00;
+  int32_t p1 = getWordPos(wpi);
+  int32_t p2 = getWordPos(wpj);
+  unsigned char hg1 = getHashGroup(wpi);
+  unsigned char hg2 = getHashGroup(wpj);
+  unsigned char wsr1 = getWordSpamRank(wpi);
+  unsigned char wsr2 = getWordSpamRank(wpj);
+  float spamw1, spamw2, denw1, denw2, dist, score;
+  if (hg1 == HASHGROUP_INLINKTEXT) spamw1 = s_linkerWeights[wsr1];
+  else spamw1 = s_wordSpamWeights[wsr1];
+  if (hg2 == HASHGROUP_INLINKTEXT) spamw2 = s_linkerWeights[wsr2];
+  else spamw2 = s_wordSpamWeights[wsr2];
+  denw1 = s_densityWeights[getDensityRank(wpi)];
+  denw2 = s_densityWeights[getDensityRank(wpj)];
+  if (fixedDistance != 0) {
+    dist = fixedDistance;
+  } else {
+    if (p2 < p1) dist = p1 - p2;
+    else dist = p2 - p1;
+    if (dist < 2) dist = 2;
+    if (dist >= pt->qdist) dist = dist - pt->qdist;
+    if (p2 < p1) dist += 1;
+  }
+  score = 100 * denw1 * denw2;
+  score *= s_hashGroupWeights[hg1];
+  score *= s_hashGroupWeights[hg2];
+  if (getIsSynonym(wpi)) score *= SYNONYM_WEIGHT;
+  if (getIsSynonym(wpj)) score *= SYNONYM_WEIGHT;
+  score *= spamw1 * spamw2;
+  score /= (dist + 1.0);
+  return score;
+}
+
+/* evalSlidingWindow, Posdb.cpp:1275-1511 */
+static void evalSlidingWindow(PT *pt, uint8_t **ptrs, int32_t nr, uint8_t **bestPos,
+                              float *scoreMatrix) {
+  float wikiWeight;
+  float minTermPairScoreInWindow = 999999999.0;
+  int32_t maxi = nr;
+  for (int32_t i = 0; i < maxi; i++) {
+    if (pt->bflags[i] & BF_EXCLUDE) continue;
+    uint8_t *wpi = ptrs[i];
+    for (int32_t j = i + 1; j < nr; j++) {
+      if (pt->bflags[j] & BF_EXCLUDE) continue;
+      uint8_t *wpj = ptrs[j];
+      if (pt->wikiPhraseIds[j] == pt->wikiPhraseIds[i] && pt->wikiPhraseIds[j]) {
+        pt->qdist = pt->qpos[j] - pt->qpos[i];
+        wikiWeight = WIKI_WEIGHT;
+      } else {
+        pt->qdist = 2;
+        wikiWeight = 1.0;
+      }
+      float max = getTermPairScoreForWindow(pt, wpi, wpj, 0);
+      float score = getTermPairScoreForWindow(pt, bestPos[i], wpj, FIXED_DISTANCE);
+      if (score > max) max = score;
+      score = getTermPairScoreForWindow(pt, bestPos[i], bestPos[j], FIXED_DISTANCE);
+      if (score > max) max = score;
+      score = getTermPairScoreForWindow(pt, wpi, bestPos[j], FIXED_DISTANCE);
+      if (score > max) max = score;
+      if (wikiWeight != 1.0) max *= wikiWeight;
+      max *= pt->freqWeights[i] * pt->freqWeights[j];
+      if (scoreMatrix[pt->nqt * i + j] > max) max = scoreMatrix[pt->nqt * i + j];
+      if (pt->quotedStartIds[j] >= 0 && pt->quotedStartIds[j] == pt->quotedStartIds[i]) {
+        if (!wpi) {
+          max = -1.0;
+        } else if (!wpj) {
+          max = -1.0;
+        } else {
+          int32_t qdist = pt->qpos[j] - pt->qpos[i];
+          int32_t p1 = getWordPos(wpi);
+          int32_t p2 = getWordPos(wpj);
+          int32_t dist = p2 - p1;
+          if (dist < 0) max = -1.0;
+          else if (dist > qdist && dist - qdist > 1) max = -1.0;
+          else if (dist < qdist && qdist - dist > 1) max = -1.0;
+        }
+      }
+      if (max < minTermPairScoreInWindow) minTermPairScoreInWindow = max;
+    }
+  }
+  if (minTermPairScoreInWindow <= pt->bestWindowScore) return;
+  pt->bestWindowScore = minTermPairScoreInWindow;
+  for (int32_t i = 0; i < maxi; i++) pt->windowTermPtrs[i] = ptrs[i];
+}
+
+/* getTermPairScoreForAny, Posdb.cpp:3631-4344 (pdcs == NULL) */
+static float getTermPairScoreForAny(PT *pt, int32_t i, int32_t j, uint8_t *wpi, uint8_t *wpj,
+                                    uint8_t *endi, uint8_t *endj, int *corrupt) {
+  float wts;
+  int32_t qdist;
+  if (pt->wikiPhraseIds[j] == pt->wikiPhraseIds[i] && pt->wikiPhraseIds[j]) {
+    qdist = pt->qpos[j] - pt->qpos[i];
+    wts = (float)WIKI_WEIGHT;
+  } else {
+    qdist = 2;
+    wts = 1.0;
+  }
+  int inSameQuotedPhrase = 0;
+  if (pt->quotedStartIds[i] == pt->quotedStartIds[j] && pt->quotedStartIds[i] >= 0)
+    inSameQuotedPhrase = 1;
+  if (inSameQuotedPhrase) qdist = pt->qpos[j] - pt->qpos[i];
+  int32_t p1 = getWordPos(wpi);
+  int32_t p2 = getWordPos(wpj);
+  unsigned char hg1 = getHashGroup(wpi);
+  unsigned char hg2 = getHashGroup(wpj);
+  unsigned char mhg1 = hg1, mhg2 = hg2;
+  if (s_inBody[mhg1]) mhg1 = HASHGROUP_BODY;
+  if (s_inBody[mhg2]) mhg2 = HASHGROUP_BODY;
+  unsigned char wsr1 = getWordSpamRank(wpi);
+  unsigned char wsr2 = getWordSpamRank(wpj);
+  float spamw1, spamw2;
+  if (hg1 == HASHGROUP_INLINKTEXT) spamw1 = s_linkerWeights[wsr1];
+  else spamw1 = s_wordSpamWeights[wsr1];
+  if (hg2 == HASHGROUP_INLINKTEXT) spamw2 = s_linkerWeights[wsr2];
+  else spamw2 = s_wordSpamWeights[wsr2];
+  float denw1 = s_densityWeights[getDensityRank(wpi)];
+  float denw2 = s_densityWeights[getDensityRank(wpj)];
+  int firsti = 1, firstj = 1;
+  float score;
+  int32_t minx = -1;
+  float bestScores[MAX_TOP];
+  char bestmhg1[MAX_TOP];
+  char bestmhg2[MAX_TOP];
+  int32_t numTop = 0;
+  int32_t dist;
+  int32_t bro;
+  char syn1, syn2;
+  for (;;) {
+    if (s_inBody[hg1] && wpi != pt->windowTermPtrs[i]) goto skip1;
+    if (s_inBody[hg2] && wpj != pt->windowTermPtrs[j]) goto skip2;
+    if (p1 <= p2) {
+      dist = p2 - p1;
+      if (inSameQuotedPhrase) {
+        if (dist > qdist && dist - qdist >= 2) goto skip1;
+        if (dist < qdist && qdist - dist >= 2) goto skip1;
+      }
+      syn1 = getIsSynonym(wpi);
+      syn2 = getIsSynonym(wpj);
+      if (dist < 2) dist = 2;
+      if (dist < 50) {
+      } else if (mhg1 != mhg2) {
+        dist = FIXED_DISTANCE;
+      } else if (mhg1 == HASHGROUP_INLINKTEXT) {
+        dist = FIXED_DISTANCE;
+      }
+      if (dist >= qdist) dist = dist - qdist;
+      score = 100 * denw1 * denw2;
+      score *= s_hashGroupWeights[hg1];
+      score *= s_hashGroupWeights[hg2];
+      if (syn1) score *= SYNONYM_WEIGHT;
+      if (syn2) score *= SYNONYM_WEIGHT;
+      if (getIsHalfStopWikiBigram(wpi)) score *= WIKI_BIGRAM_WEIGHT;
+      if (getIsHalfStopWikiBigram(wpj)) score *= WIKI_BIGRAM_WEIGHT;
+      score *= spamw1 * spamw2;
+      score /= (dist + 1.0);
+      bro = -1;
+      for (int32_t k = 0; k < numTop; k++) {
+        if (bestmhg1[k] == mhg1 && hg1 != HASHGROUP_INLINKTEXT) { bro = k; break; }
+        if (bestmhg2[k] == mhg2 && hg2 != HASHGROUP_INLINKTEXT) { bro = k; break; }
+      }
+      if (bro >= 0) {
+        if (score > bestScores[bro]) {
+          bestScores[bro] = score;
+          bestmhg1[bro] = mhg1;
+          bestmhg2[bro] = mhg2;
+        }
+      } else if (numTop < pt->realMaxTop) {
+        bestScores[numTop] = score;
+        bestmhg1[numTop] = mhg1;
+        bestmhg2[numTop] = mhg2;
+        numTop++;
+      } else if (score > bestScores[minx]) {
+        bestScores[minx] = score;
+        bestmhg1[minx] = mhg1;
+        bestmhg2[minx] = mhg2;
+      }
+      if (numTop >= pt->realMaxTop) {
+        minx = 0;
+        for (int32_t k = 1; k < pt->realMaxTop; k++) {
+          if (bestScores[k] > bestScores[minx]) continue;
+          minx = k;
+        }
+      }
+    skip1:
+      if (firsti) { wpi += 6; firsti = 0; }
+      wpi += 6;
+      if (wpi >= endi) break;
+      if (keySize(wpi) != 6) {
+        if (getDocId(wpi) != pt->docId) { *corrupt = 1; break; }
+        firsti = 1;
+      }
+      p1 = getWordPos(wpi);
+      hg1 = getHashGroup(wpi);
+      mhg1 = hg1;
+      if (s_inBody[mhg1]) mhg1 = HASHGROUP_BODY;
+      denw1 = s_densityWeights[getDensityRank(wpi)];
+      if (hg1 == HASHGROUP_INLINKTEXT) spamw1 = s_linkerWeights[getWordSpamRank(wpi)];
+      else spamw1 = s_wordSpamWeights[getWordSpamRank(wpi)];
+      continue;
+    } else {
+      dist = p1 - p2;
+      if (inSameQuotedPhrase) goto skip2;
+      if (dist < 2) dist = 2;
+      if (dist < 50) {
+      } else if (mhg1 != mhg2) {
+        dist = FIXED_DISTANCE;
+      } else if (mhg1 == HASHGROUP_INLINKTEXT) {
+        dist = FIXED_DISTANCE;
+      }
+      if (dist >= qdist) {
+        dist = dist - qdist;
+        dist += qdist - 1;
+      } else {
+        dist += 1;
+      }
+      score = 100 * denw1 * denw2;
+      score *= s_hashGroupWeights[hg1];
+      score *= s_hashGroupWeights[hg2];
+      if (getIsSynonym(wpi)) score *= SYNONYM_WEIGHT;
+      if (getIsSynonym(wpj)) score *= SYNONYM_WEIGHT;
+      score *= spamw1 * spamw2;
+      score /= (dist + 1.0);
+      bro = -1;
+      for (int32_t k = 0; k < numTop; k++) {
+        if (bestmhg1[k] == mhg1 && hg1 != HASHGROUP_INLINKTEXT) { bro = k; break; }
+        if (bestmhg2[k] == mhg2 && hg2 != HASHGROUP_INLINKTEXT) { bro = k; break; }
+      }
+      if (bro >= 0) {
+        if (score > bestScores[bro]) {
+          bestScores[bro] = score;
+          bestmhg1[bro] = mhg1;
+          bestmhg2[bro] = mhg2;
+        }
+      } else if (numTop < pt->realMaxTop) {
+        bestScores[numTop] = score;
+        bestmhg1[numTop] = mhg1;
+        bestmhg2[numTop] = mhg2;
+        numTop++;
+      } else if (score > bestScores[minx]) {
+        bestScores[minx] = score;
+        bestmhg1[minx] = mhg1;
+        bestmhg2[minx] = mhg2;
+      }
+      if (numTop >= pt->realMaxTop) {
+        minx = 0;
+        for (int32_t k = 1; k < pt->realMaxTop; k++) {
+          if (bestScores[k] > bestScores[minx]) continue;
+          minx = k;
+        }
+      }
+    skip2:
+      if (firstj) { wpj += 6; firstj = 0; }
+      wpj += 6;
+      if (wpj >= endj) break;
+      if (keySize(wpj) != 6) {
+        if (getDocId(wpj) != pt->docId) { *corrupt = 1; break; }
+        firstj = 1;
+      }
+      p2 = getWordPos(wpj);
+      hg2 = getHashGroup(wpj);
+      mhg2 = hg2;
+      if (s_inBody[mhg2]) mhg2 = HASHGROUP_BODY;
+      denw2 = s_densityWeights[getDensityRank(wpj)];
+      if (hg2 == HASHGROUP_INLINKTEXT) spamw2 = s_linkerWeights[getWordSpamRank(wpj)];
+      else spamw2 = s_wordSpamWeights[getWordSpamRank(wpj)];
+      continue;
+    }
+  }
+  float sum = 0.0;
+  for (int32_t k = 0; k < numTop; k++) sum += bestScores[k];
+  sum *= wts;
+  sum *= pt->freqWeights[i];
+  sum *= pt->freqWeights[j];
+  return sum;
+}
+
+/* ------------------------------------------------- setQueryTermInfo etc. */
+/* PosdbTable::setQueryTermInfo, Posdb.cpp:4354-4869 */
+static int setQueryTermInfo(const orc_qterm *qt, int nqt, OList *lists, QTI *qip, int *nrgOut,
+                            int64_t *minListSize, int *minListi) {
+  int nrg = 0;
+  for (int i = 0; i < nqt; i++) {
+    if (!qt[i].is_required) continue;
+    QTI *qti = &qip[nrg];
+    memset(qti, 0, sizeof *qti);
+    qti->qtermNum = i;
+    qti->qpos = qt[i].qpos;
+    qti->wikiPhraseId = qt[i].wiki_phrase_id;
+    qti->quotedStartId = qt[i].quote_start;
+    int nn = 0;
+    int left = qt[i].left_phrase_term, right = qt[i].right_phrase_term;
+    int leftTerm = left, rightTerm = right; /* m_leftPhraseTerm (NULL iff num < 0) */
+    int leftAlreadyAdded = 0, rightAlreadyAdded = 0;
+    char piped = qt[i].piped ? BF_PIPED : 0;
+#define ADD(listIdx, flags)                                   \
+    do {                                                      \
+      if (nn >= MAX_SUBLISTS) return E2BIG;                   \
+      qti->subList[nn] = (listIdx);                           \
+      qti->bigramFlags[nn] = (char)(flags);                   \
+      if (lists[(listIdx)].size) nn++;                        \
+    } while (0)
+    if (left >= 0 && leftTerm >= 0 && qt[leftTerm].is_wiki_half_stop_bigram) {
+      leftAlreadyAdded = 1;
+      ADD(left, BF_HALFSTOPWIKIBIGRAM | piped);
+      for (int k = 0; k < nqt; k++)
+        if (qt[k].synonym_of == leftTerm) ADD(k, BF_HALFSTOPWIKIBIGRAM | BF_SYNONYM | piped);
+    }
+    if (right >= 0 && rightTerm >= 0 && qt[rightTerm].is_wiki_half_stop_bigram) {
+      rightAlreadyAdded = 1;
+      ADD(right, BF_HALFSTOPWIKIBIGRAM | piped);
+      for (int k = 0; k < nqt; k++)
+        if (qt[k].synonym_of == rightTerm) ADD(k, BF_HALFSTOPWIKIBIGRAM | BF_SYNONYM | piped);
+    }
+    {
+      int fl = piped;
+      if (qt[i].term_sign == '-') fl |= BF_NEGATIVE;
+      ADD(i, fl);
+    }
+    if (left >= 0 && !leftAlreadyAdded) {
+      ADD(left, piped | BF_BIGRAM);
+      for (int k = 0; k < nqt; k++)
+        if (leftTerm >= 0 ? qt[k].synonym_of == leftTerm : qt[k].synonym_of < 0)
+          ADD(k, BF_SYNONYM | piped);
+    }
+    if (right >= 0 && !rightAlreadyAdded) {
+      ADD(right, BF_BIGRAM | piped);
+      for (int k = 0; k < nqt; k++)
+        if (rightTerm >= 0 ? qt[k].synonym_of == rightTerm : qt[k].synonym_of < 0)
+          ADD(k, BF_SYNONYM | piped);
+    }
+    for (int k = 0; k < nqt; k++)
+      if (qt[k].synonym_of == i) ADD(k, BF_SYNONYM | piped);
+#undef ADD
+    qti->numSubLists = nn;
+    qti->termFreqWeight = qt[i].tf_weight;
+    if (nn >= MAX_SUBLISTS) return E2BIG; /* "too many sublists" */
+    qti->totalSubListsSize = 0;
+    for (int q = 0; q < nn; q++) qti->totalSubListsSize += lists[qti->subList[q]].size;
+    nrg++;
+  }
+  *minListSize = 0;
+  *minListi = -1;
+  for (int i = 0; i < nrg; i++) {
+    QTI *qti = &qip[i];
+    if (qti->bigramFlags[0] & BF_NEGATIVE) continue;
+    int64_t total = qti->totalSubListsSize;
+    if (total < *minListSize || *minListi == -1) {
+      *minListSize = total;
+      *minListi = i;
+    }
+  }
+  *nrgOut = nrg;
+  return 0;
+}
+
+/* docid-record compare helpers (Posdb.cpp:5100-5113) */
+static inline int vcmp(const uint8_t *dp, const uint8_t *rec) {
+  uint32_t a = U32(dp + 1), b = U32(rec + 8);
+  if (a > b) return 1;
+  if (a < b) return -1;
+  unsigned char x = dp[0], y = rec[7] & 0xfc;
+  if (x > y) return 1;
+  if (x < y) return -1;
+  return 0;
+}
+
+typedef struct {
+  uint8_t *buf;
+  int64_t len;
+} VoteBuf;
+
+/* addDocIdVotes, Posdb.cpp:5043-5332 (no range terms / whitelist) */
+static void addDocIdVotes(QTI *qti, int listGroupNum, OList *lists, VoteBuf *vb) {
+  uint8_t *dp, *dpEnd, *recPtr, *subListEnd;
+  for (int i = 0; i < qti->numSubLists && listGroupNum > 0; i++) {
+    recPtr = lists[qti->subList[i]].list;
+    subListEnd = recPtr + lists[qti->subList[i]].size;
+    dp = vb->buf;
+    dpEnd = dp + vb->len;
+  subLoop:
+    for (; dp < dpEnd; dp += 6) {
+      int c = vcmp(dp, recPtr);
+      if (c > 0) break;
+      if (c < 0) continue;
+      dp[5] = (uint8_t)listGroupNum;
+      dp += 6;
+      break;
+    }
+    if (dp >= dpEnd) continue;
+    recPtr += 12;
+    for (; recPtr < subListEnd && ((*recPtr) & 0x04); recPtr += 6);
+    if (recPtr < subListEnd) goto subLoop;
+  }
+  if (listGroupNum > 0) {
+    dp = vb->buf;
+    dpEnd = dp + vb->len;
+    uint8_t *dst = dp;
+    for (; dp < dpEnd; dp += 6) {
+      if ((signed char)dp[5] != listGroupNum) continue;
+      memmove(dst, dp, 6);
+      dst += 6;
+    }
+    vb->len = dst - vb->buf;
+    return;
+  }
+  uint8_t *cursor[MAX_SUBLISTS], *cursorEnd[MAX_SUBLISTS];
+  for (int i = 0; i < qti->numSubLists; i++) {
+    cursor[i] = lists[qti->subList[i]].list;
+    cursorEnd[i] = cursor[i] + lists[qti->subList[i]].size;
+  }
+  dp = vb->buf;
+  uint8_t *minRecPtr, *lastMinRecPtr = NULL;
+  int mini = -1;
+  for (;;) {
+    minRecPtr = NULL;
+    for (int i = 0; i < qti->numSubLists; i++) {
+      if (!cursor[i]) continue;
+      recPtr = cursor[i];
+      if (!minRecPtr) { minRecPtr = recPtr; mini = i; continue; }
+      if (U32(recPtr + 8) > U32(minRecPtr + 8)) continue;
+      if (U32(recPtr + 8) < U32(minRecPtr + 8)) { minRecPtr = recPtr; mini = i; continue; }
+      if ((recPtr[7] & 0xfc) > (minRecPtr[7] & 0xfc)) continue;
+      if ((recPtr[7] & 0xfc) < (minRecPtr[7] & 0xfc)) { minRecPtr = recPtr; mini = i; continue; }
+    }
+    if (!minRecPtr) {
+      vb->len = dp - vb->buf;
+      return;
+    }
+    cursor[mini] += 12;
+    for (;;) {
+      if (cursor[mini] >= cursorEnd[mini]) { cursor[mini] = NULL; break; }
+      if (!(cursor[mini][0] & 0x04)) break;
+      cursor[mini] += 6;
+    }
+    if (lastMinRecPtr && U32(lastMinRecPtr + 8) == U32(minRecPtr + 8) &&
+        (lastMinRecPtr[7] & 0xfc) == (minRecPtr[7] & 0xfc))
+      continue;
+    lastMinRecPtr = minRecPtr;
+    memcpy(dp + 1, minRecPtr + 8, 4);
+    dp[0] = minRecPtr[7] & 0xfc;
+    dp[5] = 0;
+    dp += 6;
+  }
+}
+
+/* rmDocIdVotes, Posdb.cpp:4871-4946 */
+static void rmDocIdVotes(QTI *qti, OList *lists, VoteBuf *vb) {
+  uint8_t *dp = NULL, *dpEnd, *recPtr, *subListEnd;
+  for (int i = 0; i < qti->numSubLists; i++) {
+    recPtr = lists[qti->subList[i]].list;
+    subListEnd = recPtr + lists[qti->subList[i]].size;
+    dp = vb->buf;
+    dpEnd = dp + vb->len;
+  subLoop:
+    for (; dp < dpEnd; dp += 6) {
+      int c = vcmp(dp, recPtr);
+      if (c > 0) break;
+      if (c < 0) continue;
+      dp[5] = 0xff;
+      dp += 6;
+      break;
+    }
+    if (dp >= dpEnd) continue;
+    recPtr += 12;
+    for (; recPtr < subListEnd && ((*recPtr) & 0x04); recPtr += 6);
+    if (recPtr < subListEnd) goto subLoop;
+  }
+  dp = vb->buf;
+  dpEnd = dp + vb->len;
+  uint8_t *dst = dp;
+  for (; dp < dpEnd; dp += 6) {
+    if (dp[5] == 0xff) continue;
+    memmove(dst, dp, 6);
+    dst += 6;
+  }
+  vb->len = dst - vb->buf;
+}
+
+/* shrinkSubLists, Posdb.cpp:5334-5428 (in place, like the reference) */
+static void shrinkSubLists(QTI *qti, OList *lists, VoteBuf *vb) {
+  qti->numNewSubLists = 0;
+  for (int i = 0; i < qti->numSubLists; i++) {
+    uint8_t *recPtr = lists[qti->subList[i]].list;
+    uint8_t *subListEnd = recPtr + lists[qti->subList[i]].size;
+    uint8_t *dp = vb->buf;
+    uint8_t *dpEnd = dp + vb->len;
+    uint8_t *dst = recPtr;
+    uint8_t *savedDst = dst;
+  subLoop:
+    for (;; dp += 6) {
+      if (dp >= dpEnd) goto doneWithSubList;
+      int c = vcmp(dp, recPtr);
+      if (c > 0) break;
+      if (c < 0) continue;
+      memmove(dst, recPtr, 12);
+      dst += 12;
+      recPtr += 12;
+      for (;;) {
+        if (recPtr >= subListEnd) goto doneWithSubList;
+        if (!(recPtr[0] & 0x04)) break;
+        memmove(dst, recPtr, 6);
+        dst += 6;
+        recPtr += 6;
+      }
+    }
+    recPtr += 12;
+    for (;;) {
+      if (recPtr >= subListEnd) goto doneWithSubList;
+      if (!(recPtr[0] & 0x04)) break;
+      recPtr += 6;
+    }
+    goto subLoop;
+  doneWithSubList:;
+    int x = qti->numNewSubLists;
+    qti->newSubListSize[x] = dst - savedDst;
+    qti->newSubListStart[x] = savedDst;
+    qti->newSubListEnd[x] = dst;
+    qti->cursor[x] = savedDst;
+    qti->savedCursor[x] = savedDst;
+    if (qti->newSubListSize[x]) qti->numNewSubLists++;
+  }
+}
+
+/* ---------------------------------------------------------------- driver */
+#define LIST_PAD 64
+
+static void free_lists(OList *L, uint8_t **alloc, int n) {
+  for (int i = 0; i < n; i++) free(alloc[i]);
+  free(alloc);
+  free(L);
+}
+
+/* copies + Msg39 early outs; returns 0 and fills everything up to the votes */
+typedef struct {
+  OList *lists;
+  uint8_t **alloc;
+  QTI *qip;
+  int nrg;
+  int64_t minListSize;
+  int minListi;
+  VoteBuf vb;
+} Prep;
+
+static int prepare(const orc_qterm *qt, const uint8_t *const *lists, const int64_t *sizes, int nqt,
+                   Prep *P) {
+  memset(P, 0, sizeof *P);
+  P->lists = (OList *)calloc(nqt > 0 ? nqt : 1, sizeof(OList));
+  P->alloc = (uint8_t **)calloc(nqt > 0 ? nqt : 1, sizeof(uint8_t *));
+  P->qip = (QTI *)calloc(nqt > 0 ? nqt : 1, sizeof(QTI));
+  if (!P->lists || !P->alloc || !P->qip) return ENOMEM;
+  for (int i = 0; i < nqt; i++) {
+    int64_t sz = sizes[i];
+    if (sz < 0 || (sz && !lists[i])) return EINVAL;
+    /* zero padding guards the reference's reads just past a list end */
+    P->alloc[i] = (uint8_t *)calloc(1, (size_t)sz + 2 * LIST_PAD);
+    if (!P->alloc[i]) return ENOMEM;
+    if (sz) memcpy(P->alloc[i] + LIST_PAD, lists[i], (size_t)sz);
+    P->lists[i].list = P->alloc[i] + LIST_PAD;
+    P->lists[i].size = sz;
+  }
+  int rc = setQueryTermInfo(qt, nqt, P->lists, P->qip, &P->nrg, &P->minListSize, &P->minListi);
+  if (rc) return rc;
+  /* first-key swap, Posdb.cpp:5671-5703 */
+  for (int k = 0; k < nqt; k++) {
+    OList *l = &P->lists[k];
+    if (!l->size) continue;
+    uint8_t ttt[12];
+    uint8_t *p = l->list;
+    memcpy(ttt, p, 12);
+    memcpy(p, p + 12, 6);
+    memcpy(p + 6, ttt, 12);
+    p += 6;
+    *p |= 0x02;
+    l->size -= 6;
+    l->list = p;
+  }
+  int64_t need = (P->minListSize / 12) * 6 + 8;
+  P->vb.buf = (uint8_t *)calloc(1, (size_t)need + 16);
+  if (!P->vb.buf) return ENOMEM;
+  return 0;
+}
+
+static void unprepare(Prep *P, int nqt) {
+  free(P->vb.buf);
+  free(P->qip);
+  if (P->lists) free_lists(P->lists, P->alloc, nqt);
+}
+
+/* phases 3-4 of intersectLists10_r, Posdb.cpp:5808-5860 */
+static void votes(Prep *P) {
+  QTI *qip = P->qip;
+  int listGroupNum = 0;
+  addDocIdVotes(&qip[P->minListi], listGroupNum, P->lists, &P->vb);
+  for (int i = 0; i < P->nrg; i++) {
+    if (i == P->minListi) continue;
+    if (qip[i].bigramFlags[0] & BF_NEGATIVE) continue;
+    listGroupNum++;
+    if (listGroupNum >= 256) listGroupNum = 1;
+    addDocIdVotes(&qip[i], listGroupNum, P->lists, &P->vb);
+  }
+  for (int i = 0; i < P->nrg; i++) {
+    if (i == P->minListi) continue;
+    if (!(qip[i].bigramFlags[0] & BF_NEGATIVE)) continue;
+    rmDocIdVotes(&qip[i], P->lists, &P->vb);
+  }
+}
+
+int64_t orc_intersect(const orc_qterm *qt, const uint8_t *const *lists, const int64_t *sizes,
+                      int nqt, int64_t *docids, int64_t cap) {
+  initWeights();
+  Prep P;
+  int rc = prepare(qt, lists, sizes, nqt, &P);
+  if (rc) { unprepare(&P, nqt); return -rc; }
+  int64_t n = 0;
+  if (P.nrg > 0 && P.minListSize != 0) {
+    votes(&P);
+    n = P.vb.len / 6;
+    for (int64_t i = 0; i < n && i < cap; i++) {
+      const uint8_t *d = P.vb.buf + 6 * i;
+      uint64_t id = U32(d + 1);
+      id <<= 8;
+      id |= d[0];
+      docids[i] = (int64_t)(id >> 2);
+    }
+  }
+  unprepare(&P, nqt);
+  return n;
+}
+
+/* allocTopTree sizing, Posdb.cpp:838-930 + TopTree::setNumNodes */
+static int64_t docs_wanted(const orc_params *p, const int64_t *sizes, int nqt) {
+  int64_t nn1 = p->docs_to_get, nn2 = 0;
+  for (int k = 0; k < nqt; k++) {
+    if (!sizes[k]) continue;
+    nn2 += (int32_t)sizes[k] / (18 - 6);
+  }
+  int64_t nn = nn2;
+  if (nn1 < nn2) nn = nn1;
+  if (nn == 0) return 0;
+  if (nn < 30) nn = 30;
+  if (nn > 2000000000) nn = 2000000000;
+  if (nn > (int64_t)p->docs_to_get * 2 && nn > 60) nn = (int64_t)p->docs_to_get * 2;
+  return nn;
+}
+
+int orc_query(const orc_qterm *qt, const uint8_t *const *lists, const int64_t *sizes, int nqt,
+              const orc_params *prm, int64_t *docids, float *scores, int cap, orc_result *out) {
+  memset(out, 0, sizeof *out);
+  if (nqt < 0 || !prm) return EINVAL;
+  if (prm->site_clustering || prm->num_docid_splits > 1) return ENOTSUP;
+  if (prm->real_max_top <= 0 || prm->docs_to_get <= 0) return EINVAL;
+  for (int i = 0; i < nqt; i++)
+    if (qt[i].field_code) return ENOTSUP; /* numeric/facet/range terms: DESIGN.md */
+  initWeights();
+
+  int64_t dw = docs_wanted(prm, sizes, nqt);
+  out->docs_wanted = (int32_t)dw;
+  TopK tk;
+  tk.cap = (int)dw;
+  tk.n = 0;
+  tk.score = (float *)calloc(dw > 0 ? dw : 1, sizeof(float));
+  tk.docid = (int64_t *)calloc(dw > 0 ? dw : 1, sizeof(int64_t));
+
+  Prep P;
+  int rc = prepare(qt, lists, sizes, nqt, &P);
+  if (rc) {
+    unprepare(&P, nqt);
+    free(tk.score); free(tk.docid);
+    return rc;
+  }
+  QTI *qip = P.qip;
+  int nqti = P.nrg;
+  if (nqti == 0 || P.minListSize == 0) goto finish;
+
+  votes(&P);
+  out->hits = P.vb.len / 6;
+  for (int i = 0; i < nqti; i++) {
+    if (qip[i].bigramFlags[0] & BF_NEGATIVE) continue;
+    shrinkSubLists(&qip[i], P.lists, &P.vb);
+  }
+
+  {
+    int32_t *wikiPhraseIds = (int32_t *)calloc(nqt, 4);
+    int32_t *quotedStartIds = (int32_t *)calloc(nqt, 4);
+    int32_t *qpos = (int32_t *)calloc(nqt, 4);
+    float *freqWeights = (float *)calloc(nqt, 4);
+    uint8_t **mml = (uint8_t **)calloc(nqt, sizeof(uint8_t *));
+    uint8_t **mme = (uint8_t **)calloc(nqt, sizeof(uint8_t *));
+    uint8_t **bestPos = (uint8_t **)calloc(nqt, sizeof(uint8_t *));
+    uint8_t **winnerStack = (uint8_t **)calloc(nqt, sizeof(uint8_t *));
+    uint8_t **xpos = (uint8_t **)calloc(nqt, sizeof(uint8_t *));
+    char *bflags = (char *)calloc(nqt, 1);
+    float *scoreMatrix = (float *)calloc((size_t)nqt * nqt, 4);
+    uint8_t *mbuf = (uint8_t *)calloc(1, 300000 + 64);
+    uint8_t *mptrEnd = mbuf + 299000;
+    for (int i = 0; i < nqti; i++) {
+      wikiPhraseIds[i] = qip[i].wikiPhraseId;
+      quotedStartIds[i] = qip[i].quotedStartId;
+      qpos[i] = qip[i].qpos;
+      freqWeights[i] = qip[i].termFreqWeight;
+    }
+    PT pt;
+    memset(&pt, 0, sizeof pt);
+    pt.realMaxTop = prm->real_max_top > MAX_TOP ? MAX_TOP : prm->real_max_top;
+    pt.freqWeights = freqWeights;
+    pt.qpos = qpos;
+    pt.wikiPhraseIds = wikiPhraseIds;
+    pt.quotedStartIds = quotedStartIds;
+    pt.bflags = bflags;
+    pt.windowTermPtrs = winnerStack;
+    pt.nqt = nqt;
+    float siteRankMultiplier = SITERANKMULTIPLIER;
+    char siteRank = 0, docLang = 0;
+    uint8_t *nwp[MAX_SUBLISTS], *nwpEnd[MAX_SUBLISTS];
+    char nwpFlags[MAX_SUBLISTS];
+    uint8_t *docIdEnd = P.vb.buf + P.vb.len;
+
+    for (uint8_t *docIdPtr = P.vb.buf; docIdPtr < docIdEnd; docIdPtr += 6) {
+      /* cursor pre-advance, Posdb.cpp:6252-6310 */
+      for (int i = 0; i < nqti; i++) {
+        QTI *qti = &qip[i];
+        if (qti->bigramFlags[0] & BF_NEGATIVE) continue;
+        for (int j = 0; j < qti->numNewSubLists; j++) {
+          uint8_t *xc = qti->cursor[j];
+          uint8_t *xcEnd = qti->newSubListEnd[j];
+          if (xc >= xcEnd || U32(xc + 8) != U32(docIdPtr + 1) ||
+              (xc[7] & 0xfc) != (docIdPtr[0] & 0xfc)) {
+            qti->savedCursor[j] = NULL;
+            continue;
+          }
+          qti->savedCursor[j] = xc;
+          xc += 12;
+          for (;; xc += 6) {
+            if (xc >= xcEnd) break;
+            if ((*xc & 0x06) == 0x00) { out->corrupt = 1; goto doneAll; }
+            if (!(*xc & 0x04)) break;
+          }
+          qti->cursor[j] = xc;
+        }
+      }
+      /* (the max-score and ring-buffer prefilters are inert without site
+       *  clustering: minWinningScore stays -1, Posdb.cpp:7699-7704) */
+
+      /* mini merges, Posdb.cpp:6559-6778 */
+      {
+        uint8_t *mptr = mbuf, *lastMptr = NULL;
+        for (int j = 0; j < nqti; j++) {
+          QTI *qti = &qip[j];
+          bflags[j] = qti->bigramFlags[0];
+          if (qti->bigramFlags[0] & BF_NEGATIVE) { mml[j] = NULL; continue; }
+          mml[j] = mptr;
+          int isFirstKey = 1;
+          int nsub = 0;
+          for (int k = 0; k < qti->numNewSubLists; k++) {
+            if (!qti->savedCursor[k]) continue;
+            nwp[nsub] = qti->savedCursor[k];
+            nwpEnd[nsub] = qti->cursor[k];
+            nwpFlags[nsub] = qti->bigramFlags[k];
+            nsub++;
+          }
+          for (;;) {
+            int mink = -1;
+            for (int k = 0; k < nsub; k++) {
+              if (!nwp[k]) continue;
+              if (mink == -1) { mink = k; continue; }
+              if (U32(nwp[k] + 2) > U32(nwp[mink] + 2)) continue;
+              if (U32(nwp[k] + 2) == U32(nwp[mink] + 2) && U16(nwp[k]) >= U16(nwp[mink])) continue;
+              mink = k;
+            }
+            if (mink == -1) { mme[j] = mptr; break; }
+            int ks = keySize(nwp[mink]);
+            if ((nwpFlags[mink] & BF_BIGRAM) && (nwp[mink][2] & 0x03)) goto skipOver;
+            if (isFirstKey) {
+              memcpy(mptr, nwp[mink], 12);
+              mptr[2] &= 0xfc;
+              if (nwpFlags[mink] & (BF_BIGRAM | BF_SYNONYM)) mptr[2] |= 0x02;
+              if (nwpFlags[mink] & BF_HALFSTOPWIKIBIGRAM) mptr[2] |= 0x01;
+              mptr[0] &= 0xf9;
+              mptr[0] |= 0x02;
+              lastMptr = mptr;
+              mptr += 12;
+              isFirstKey = 0;
+            } else {
+              if (lastMptr[4] == nwp[mink][4] && lastMptr[5] == nwp[mink][5] &&
+                  (lastMptr[3] & 0xc0) == (nwp[mink][3] & 0xc0))
+                goto skipOver;
+              memcpy(mptr, nwp[mink], 6);
+              mptr[2] &= 0xfc;
+              if (nwpFlags[mink] & (BF_BIGRAM | BF_SYNONYM)) mptr[2] |= 0x02;
+              if (nwpFlags[mink] & BF_HALFSTOPWIKIBIGRAM) mptr[2] |= 0x01;
+              mptr[0] |= 0x06;
+              lastMptr = mptr;
+              mptr += 6;
+            }
+          skipOver:
+            nwp[mink] += ks;
+            if (nwp[mink] >= nwpEnd[mink]) nwp[mink] = NULL;
+            else if (keySize(nwp[mink]) != 6) nwp[mink] = NULL;
+            if (mptr < mptrEnd) continue;
+            mme[j] = mptr;
+            break;
+          }
+        }
+      }
+
+      {
+        uint64_t d = U32(docIdPtr + 1);
+        d <<= 8;
+        d |= docIdPtr[0];
+        pt.docId = d >> 2;
+      }
+
+      /* non-body pair scores, Posdb.cpp:6847-6926 */
+      for (int i = 0; i < nqti; i++) {
+        if (bflags[i] & BF_EXCLUDE) continue;
+        for (int j = i + 1; j < nqti; j++) {
+          if (bflags[j] & BF_EXCLUDE) continue;
+          int32_t qdist;
+          float wts;
+          if (wikiPhraseIds[j] == wikiPhraseIds[i] && wikiPhraseIds[j]) {
+            qdist = qpos[j] - qpos[i];
+            wts = (float)WIKI_WEIGHT;
+          } else {
+            qdist = 2;
+            wts = 1.0;
+          }
+          float pss = 0.0;
+          if (mml[i] && mml[j])
+            getTermPairScoreForNonBody(&pt, i, j, mml[i], mml[j], mme[i], mme[j], qdist, &pss);
+          if (pss < 0) {
+            scoreMatrix[i * nqt + j] = -1.00;
+            wts = -1.0;
+          } else {
+            wts *= pss;
+            wts *= freqWeights[i];
+            wts *= freqWeights[j];
+            scoreMatrix[i * nqt + j] = wts;
+          }
+        }
+      }
+
+      /* single term scores, Posdb.cpp:6933-6978 */
+      float minSingleScore = 999999999.0;
+      for (int i = 0; i < nqti; i++) {
+        if (bflags[i] & BF_EXCLUDE) continue;
+        float sts = getSingleTermScore(&pt, i, mml[i], mme[i], &bestPos[i]);
+        if (sts < minSingleScore) minSingleScore = sts;
+      }
+
+      /* siterank / langid, Posdb.cpp:6985-7003 */
+      if (mml[0] && !(qip[0].bigramFlags[0] & (BF_NUMBER | BF_FACET))) {
+        siteRank = getSiteRank(mml[0]);
+        docLang = getLangId(mml[0]);
+      } else {
+        for (int k = 1; k < nqti; k++) {
+          if (!mml[k]) continue;
+          if (qip[k].bigramFlags[0] & (BF_NUMBER | BF_FACET)) continue;
+          siteRank = getSiteRank(mml[k]);
+          docLang = getLangId(mml[k]);
+          break;
+        }
+      }
+
+      /* sliding window, Posdb.cpp:7013-7150 */
+      pt.bestWindowScore = -2.0;
+      for (int i = 0; i < nqti; i++) xpos[i] = mml[i];
+      {
+        int allNull = 1;
+        for (int i = 0; i < nqti; i++) {
+          if (bflags[i] & BF_EXCLUDE) continue;
+          while (xpos[i] && !s_inBody[getHashGroup(xpos[i])]) {
+            if (!(xpos[i][0] & 0x04)) xpos[i] += 12;
+            else xpos[i] += 6;
+            if (xpos[i] < mme[i] && (xpos[i][0] & 0x04)) continue;
+            xpos[i] = NULL;
+          }
+          if (xpos[i]) allNull = 0;
+        }
+        if (!allNull) {
+          int32_t minx, minPos = 0;
+          for (;;) {
+            evalSlidingWindow(&pt, xpos, nqti, bestPos, scoreMatrix);
+          advanceMin:
+            minx = -1;
+            for (int x = 0; x < nqti; x++) {
+              if (bflags[x] & BF_EXCLUDE) continue;
+              if (!xpos[x]) continue;
+              if (minx == -1) {
+                minx = x;
+                minPos = getWordPos(xpos[x]);
+                continue;
+              }
+              if (getWordPos(xpos[x]) >= minPos) continue;
+              minx = x;
+              minPos = getWordPos(xpos[x]);
+            }
+          advanceAgain:
+            if (!(xpos[minx][0] & 0x04)) xpos[minx] += 12;
+            else xpos[minx] += 6;
+            if (xpos[minx] >= mme[minx] || !(xpos[minx][0] & 0x04)) {
+              xpos[minx] = NULL;
+              int k;
+              for (k = 0; k < nqti; k++) {
+                if (bflags[k] & BF_EXCLUDE) continue;
+                if (xpos[k]) break;
+              }
+              if (k >= nqti) break;
+              goto advanceMin;
+            }
+            if (!s_inBody[getHashGroup(xpos[minx])]) goto advanceAgain;
+          }
+        }
+      }
+
+      /* window-restricted pair scores, Posdb.cpp:7159-7219 */
+      float minPairScore = -1.0;
+      for (int i = 0; i < nqti; i++) {
+        if (bflags[i] & BF_EXCLUDE) continue;
+        for (int j = i + 1; j < nqti; j++) {
+          if (bflags[j] & BF_EXCLUDE) continue;
+          if (!mml[i]) continue;
+          if (!mml[j]) continue;
+          float score = getTermPairScoreForAny(&pt, i, j, mml[i], mml[j], mme[i], mme[j],
+                                               &out->corrupt);
+          if (score >= minPairScore && minPairScore >= 0.0) continue;
+          minPairScore = score;
+        }
+      }
+
+      /* final score, Posdb.cpp:7228-7257 */
+      float minScore = 999999999.0;
+      if (minPairScore < minScore && minPairScore >= 0.0) minScore = minPairScore;
+      if (minSingleScore < minScore) minScore = minSingleScore;
+      if (minScore <= 0.0) continue;
+      float score = minScore * (((float)siteRank) * siteRankMultiplier + 1.0);
+      if (prm->language == 0 || docLang == 0 || prm->language == docLang)
+        score *= prm->same_lang_weight;
+      out->filtered++;
+      out->filtered--; /* no maxSerpScore (Posdb.cpp:7327-7347) */
+      topk_add(&tk, score, (int64_t)pt.docId);
+    }
+  doneAll:
+    free(wikiPhraseIds); free(quotedStartIds); free(qpos); free(freqWeights);
+    free(mml); free(mme); free(bestPos); free(winnerStack); free(xpos); free(bflags);
+    free(scoreMatrix); free(mbuf);
+  }
+
+finish:
+  out->n = tk.n < cap ? tk.n : cap;
+  for (int i = 0; i < out->n; i++) {
+    docids[i] = tk.docid[i];
+    scores[i] = tk.score[i];
+  }
+  free(tk.score);
+  free(tk.docid);
+  unprepare(&P, nqt);
+  return 0;
+}
+
+/* posdbMerge_r restatement lives in posdb_merge_oracle.c */

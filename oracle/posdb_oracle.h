@@ -1,0 +1,78 @@
+/* TEST INFRASTRUCTURE ONLY -- the CPU restatement ("oracle") of the
+ * reference's Posdb query-scoring path.  Only tests/, __graft_entry__.smoke()
+ * and bench.py's cpu_baseline leg may load it; the product never does.
+ *
+ * Parity status: the posdb key codec is pinned by the reference's own
+ * known-answer test (Posdb.cpp:24-86, tests/test_codec.py).  The scoring path
+ * (PosdbTable::intersectLists10_r, TopTree, posdbMerge_r) is "parity
+ * unpinned": the reference holds no fixture for it and its path cannot be
+ * built here without editing reference sources.  This
+ * file restates the reference algorithm line by line, citing file:line.
+ */
+#ifndef GB_POSDB_ORACLE_H
+#define GB_POSDB_ORACLE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* one query term as Query::set2 leaves it (Query.h:404-580) */
+typedef struct orc_qterm {
+  int32_t is_required;              /* QueryTerm::m_isRequired                 */
+  int32_t term_sign;                /* m_termSign ('-' -> BF_NEGATIVE)         */
+  int32_t field_code;               /* m_fieldCode (0: plain word/phrase)      */
+  int32_t piped;                    /* m_piped                                 */
+  int32_t synonym_of;               /* index of m_synonymOf, -1 if none        */
+  int32_t left_phrase_term;         /* m_leftPhraseTermNum, -1 if none         */
+  int32_t right_phrase_term;        /* m_rightPhraseTermNum, -1 if none        */
+  int32_t is_wiki_half_stop_bigram; /* m_isWikiHalfStopBigram                  */
+  int32_t qpos;                     /* m_qword->m_posNum                       */
+  int32_t wiki_phrase_id;           /* m_qword->m_wikiPhraseId                 */
+  int32_t quote_start;              /* m_qword->m_quoteStart (-1 none)         */
+  float   tf_weight;                /* Msg39Request::ptr_termFreqWeights[i]    */
+} orc_qterm;
+
+typedef struct orc_params {
+  int32_t docs_to_get;      /* Msg39Request::m_docsToGet               */
+  int32_t real_max_top;     /* m_realMaxTop (clamped to MAX_TOP=10)    */
+  int32_t language;         /* m_language                              */
+  int32_t site_clustering;  /* must be 0               */
+  int32_t num_docid_splits; /* must be 1                               */
+  float   same_lang_weight; /* m_sameLangWeight                        */
+} orc_params;
+
+typedef struct orc_result {
+  int64_t hits;        /* m_docIdVoteBuf.length()/6                          */
+  int32_t filtered;    /* m_filtered                                          */
+  int32_t docs_wanted; /* TopTree::m_docsWanted (0: no tree allocated)        */
+  int32_t n;           /* entries written (TopTree read high -> low)          */
+  int32_t corrupt;     /* intersectLists10_r bailed on a corrupt list          */
+} orc_result;
+
+/* Runs init/allocTopTree/setQueryTermInfo/intersectLists10_r semantics on
+ * copies of the lists (the caller's bytes are not mutated).  docids/scores
+ * must hold `cap` entries.  Returns 0, or an errno-style code. */
+int orc_query(const orc_qterm *terms, const uint8_t *const *lists, const int64_t *sizes,
+              int nterms, const orc_params *p, int64_t *docids, float *scores, int cap,
+              orc_result *out);
+
+/* Bare intersection: the docids surviving addDocIdVotes/rmDocIdVotes, in
+ * vote-buffer order.  Returns count (or -errno); writes up to cap docids. */
+int64_t orc_intersect(const orc_qterm *terms, const uint8_t *const *lists, const int64_t *sizes,
+                      int nterms, int64_t *docids, int64_t cap);
+
+/* RdbList::posdbMerge_r (RdbList.cpp:3065-3568) over n lists already
+ * prepared by prepareForMerge; returns bytes written to out (cap bytes). */
+int64_t orc_posdb_merge(const uint8_t *const *lists, const int64_t *sizes, int n,
+                        int remove_neg_keys, int64_t min_rec_sizes, uint8_t *out, int64_t cap);
+
+/* weight tables of initWeights (Posdb.cpp:1105-1197), for table tests */
+void orc_weights(float *density32, float *wordspam16, float *linker16, float *hashgroup11,
+                 float *diversity16);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

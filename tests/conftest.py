@@ -1,0 +1,35 @@
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG_PY = os.path.join(ROOT, "open-source-search-engine_amd", "python")
+for p in (PKG_PY, os.path.join(ROOT, "tests")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs through the C ABI on the device)")
+
+
+def _ensure_built():
+    lib = os.path.join(ROOT, "open-source-search-engine_amd", "lib", "libgbgpu.so")
+    orc = os.path.join(ROOT, "oracle", "liboracle.so")
+    if not os.path.exists(lib):
+        subprocess.check_call(["make", "-C", os.path.join(ROOT, "open-source-search-engine_amd"), "-j8"])
+    if not os.path.exists(orc):
+        subprocess.check_call(["make", "-C", os.path.join(ROOT, "oracle")])
+
+
+_ensure_built()
+
+
+@pytest.fixture(scope="session")
+def engine():
+    import gbgpu
+    e = gbgpu.Engine(0)
+    yield e
+    e.close()

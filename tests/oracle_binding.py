@@ -1,0 +1,78 @@
+"""ctypes view of oracle/liboracle.so -- the CPU restatement used as the checker.
+
+Test infrastructure only (see oracle/posdb_oracle.h)."""
+import ctypes
+import os
+
+import numpy as np
+
+import gbgpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+_lib = None
+
+
+class OrcResult(ctypes.Structure):
+    _fields_ = [("hits", ctypes.c_int64), ("filtered", ctypes.c_int32), ("docs_wanted", ctypes.c_int32),
+                ("n", ctypes.c_int32), ("corrupt", ctypes.c_int32)]
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        _lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "liboracle.so"))
+        _lib.orc_query.argtypes = [ctypes.POINTER(gbgpu.QTerm), ctypes.POINTER(ctypes.c_void_p),
+                                   ctypes.POINTER(ctypes.c_int64), ctypes.c_int, ctypes.POINTER(gbgpu.Params),
+                                   ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_float), ctypes.c_int,
+                                   ctypes.POINTER(OrcResult)]
+        _lib.orc_intersect.argtypes = [ctypes.POINTER(gbgpu.QTerm), ctypes.POINTER(ctypes.c_void_p),
+                                       ctypes.POINTER(ctypes.c_int64), ctypes.c_int,
+                                       ctypes.POINTER(ctypes.c_int64), ctypes.c_int64]
+        _lib.orc_intersect.restype = ctypes.c_int64
+        _lib.orc_weights.argtypes = [ctypes.POINTER(ctypes.c_float)] * 5
+        _lib.orc_posdb_merge.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_int64),
+                                         ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p,
+                                         ctypes.c_int64]
+        _lib.orc_posdb_merge.restype = ctypes.c_int64
+    return _lib
+
+
+def _lists(lists):
+    keep = [ctypes.create_string_buffer(l, max(1, len(l))) for l in lists]
+    ptrs = (ctypes.c_void_p * max(1, len(lists)))(*[ctypes.cast(k, ctypes.c_void_p) for k in keep])
+    sizes = (ctypes.c_int64 * max(1, len(lists)))(*[len(l) for l in lists])
+    return keep, ptrs, sizes
+
+
+def query(terms, lists, params, cap=4096):
+    L = lib()
+    keep, ptrs, sizes = _lists(lists)
+    qt = (gbgpu.QTerm * max(1, len(terms)))(*terms)
+    d = np.zeros(cap, np.int64)
+    s = np.zeros(cap, np.float32)
+    r = OrcResult()
+    rc = L.orc_query(qt, ptrs, sizes, len(terms), ctypes.byref(params),
+                     d.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                     s.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), cap, ctypes.byref(r))
+    if rc:
+        raise RuntimeError(f"orc_query rc={rc}")
+    return dict(docids=d[:r.n].copy(), scores=s[:r.n].copy(), hits=r.hits, filtered=r.filtered,
+                docs_wanted=r.docs_wanted, corrupt=r.corrupt)
+
+
+def intersect(terms, lists, cap=1 << 24):
+    L = lib()
+    keep, ptrs, sizes = _lists(lists)
+    qt = (gbgpu.QTerm * max(1, len(terms)))(*terms)
+    d = np.zeros(cap, np.int64)
+    n = L.orc_intersect(qt, ptrs, sizes, len(terms), d.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), cap)
+    if n < 0:
+        raise RuntimeError(f"orc_intersect rc={n}")
+    return d[:n].copy()
+
+
+def weights():
+    arrs = [np.zeros(32, np.float32), np.zeros(16, np.float32), np.zeros(16, np.float32),
+            np.zeros(11, np.float32), np.zeros(16, np.float32)]
+    lib().orc_weights(*[a.ctypes.data_as(ctypes.POINTER(ctypes.c_float)) for a in arrs])
+    return dict(density=arrs[0], wordspam=arrs[1], linker=arrs[2], hashgroup=arrs[3], diversity=arrs[4])
