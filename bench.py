@@ -1,0 +1,215 @@
+"""Benchmark: Posdb query scoring on MI355X (BASELINE.json metric).
+
+One step = one query (config 2: 2-term AND + its bigram, top-100) over a
+synthetic Zipfian posdb index resident in HBM.  At N GPUs the index is
+docid-range sharded (100M docs per GPU, weak scaling, mirroring one Msg39 per
+shard); every rank scores its shard, the per-shard top-k lists are
+all-gathered over RCCL and merged Msg3a-style (Msg3a.cpp:1315-1467).
+
+    python bench.py --gpus 1 --steps 20 --warmup 3
+    torchrun --nproc-per-node N bench.py --gpus N ...
+
+Prints one JSON line (rank 0).  value = aggregate posdb list bytes scanned
+per second (GB/s); queries/sec is reported beside it.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "open-source-search-engine_amd", "python"))
+
+import numpy as np  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(q, num_docs_total: int, budget_s: float = 12.0):
+    """Oracle (CPU restatement, 1 thread) on a bounded docid-range slice of the
+    same corpus; reports list GB/s and queries/s on the slice."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_binding as orc
+    from workload import generate
+
+    sample_docs = min(num_docs_total, 2_000_000)
+    lists = generate(q, num_docs_total, doc_begin=0, doc_end=sample_docs, threads=16)
+    p = q.params()
+    nbytes = sum(len(l) for l in lists)
+    t0 = time.perf_counter()
+    reps = 0
+    while True:
+        orc.query(q.terms, lists, p)
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s or reps >= 2000:
+            break
+    per_q = el / reps
+    return {
+        "value": round(nbytes / per_q / 1e9, 4),
+        "unit": "GB/s",
+        "cores": 1,
+        "kind": "port",
+        "qps_on_sample": round(1.0 / per_q, 3),
+        "est_qps_full_index": round((sample_docs / num_docs_total) / per_q, 4),
+        "sample": f"docs [0,{sample_docs}) of the same {num_docs_total}-doc corpus and query "
+                  f"({nbytes/1e6:.1f} MB of lists), oracle/posdb_oracle.c single thread, {reps} reps, "
+                  f"{el:.1f} s",
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--docs-per-gpu", type=int, default=100_000_000)
+    ap.add_argument("--docs-to-get", type=int, default=100)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: WORLD_SIZE={world} != --gpus {args.gpus}; using WORLD_SIZE")
+
+    import torch
+    import torch.distributed as dist
+    import gbgpu
+    from workload import config_two_term, generate
+
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    per = args.docs_per_gpu
+    total = per * world
+    q = config_two_term(total, docs_to_get=args.docs_to_get)
+    t0 = time.time()
+    lists = generate(q, total, doc_begin=rank * per, doc_end=(rank + 1) * per, threads=16)
+    log(f"[rank {rank}] generated {sum(map(len, lists))/1e6:.1f} MB of lists in {time.time()-t0:.1f}s")
+
+    eng = gbgpu.Engine(local_rank)
+    handles = [eng.upload(l) for l in lists]
+    list_bytes = sum(len(l) for l in lists)
+    p = q.params()
+    k = p.docs_to_get
+
+    def one_step(profile=False):
+        eng.enqueue(q.terms, handles, p)
+        r = eng.collect(cap=4096)
+        if world > 1:
+            # Msg39Reply payload: (docid, score) per shard -> RCCL allgather
+            rec = torch.zeros((k, 2), dtype=torch.float64, device="cuda")
+            n = len(r.docids)
+            if n:
+                rec[:n, 0] = torch.from_numpy(r.docids.astype(np.float64)).cuda()
+                rec[:n, 1] = torch.from_numpy(r.scores.astype(np.float64)).cuda()
+            rec[n:, 1] = -1.0
+            cnt = torch.tensor([n, r.hits], dtype=torch.int64, device="cuda")
+            out = torch.empty((world, k, 2), dtype=torch.float64, device="cuda")
+            dist.all_gather_into_tensor(out, rec)
+            cnts = torch.empty((world, 2), dtype=torch.int64, device="cuda")
+            dist.all_gather_into_tensor(cnts, cnt)
+            out_h, cnts_h = out.cpu().numpy(), cnts.cpu().numpy()
+            shards = [(out_h[w, :cnts_h[w, 0], 0].astype(np.int64), out_h[w, :cnts_h[w, 0], 1].astype(np.float32))
+                      for w in range(world)]
+            d, s = gbgpu.merge_topk(shards, p.docs_to_get)
+            return r, int(cnts_h[:, 1].sum()), d
+        return r, r.hits, r.docids[:p.docs_to_get]
+
+    for _ in range(args.warmup):
+        one_step()
+    eng.set_profiling(True)
+    probe_ms, total_dev_ms, phase_ms = [], [], []
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    hits = 0
+    for _ in range(args.steps):
+        r, hits, top = one_step()
+        ms, scan_bytes = eng.last_timings()
+        total_dev_ms.append(ms[0])
+        probe_ms.append(ms[2])
+        phase_ms.append(ms)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+        lb = torch.tensor([list_bytes], dtype=torch.float64, device="cuda")
+        dist.all_reduce(lb)
+        agg_list_bytes = float(lb.item())
+    else:
+        agg_list_bytes = float(list_bytes)
+    eng.set_profiling(False)
+
+    ms_per_step = el * 1000.0 / args.steps
+    qps = args.steps / el
+    gbs = agg_list_bytes * qps / 1e9
+    # dominant kernel: k_probe, algorithmic bytes = bytes of the lists it scans
+    probe_bytes = float(list_bytes - len(lists[1]) if len(lists[1]) else list_bytes)
+    _, scan_bytes = eng.last_timings()
+    avg_probe_ms = float(np.mean(probe_ms))
+    achieved = probe_bytes / (avg_probe_ms / 1000.0) / 1e9 if avg_probe_ms > 0 else 0.0
+    result = {
+        "metric": "queries/sec + posdb keys scanned GB/s (% HBM peak), 1/2/4/8 MI355X",
+        "value": round(gbs, 3),
+        "unit": "GB/s",
+        "queries_per_sec": round(qps, 3),
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "device_ms_per_query": round(float(np.mean(total_dev_ms)), 4),
+        "phase_ms": dict(zip(["total", "candidates", "probe", "compact", "score", "topk"],
+                             [round(float(x), 4) for x in np.mean(np.array(phase_ms), axis=0)])),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic Zipfian posdb lists (SURVEY.md §8(d) generator), resident in HBM",
+        "config": {
+            "workload": "config 2: 2-term AND (+bigram sublist), top-100, 100M docs per GPU, docid-range shards",
+            "docs_per_gpu": per,
+            "docs_total": total,
+            "list_bytes_per_gpu": list_bytes,
+            "hits": int(hits),
+            "pct_hbm_peak_keys_scanned": round(100.0 * gbs / (HBM_PEAK_GBS * world), 2),
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "k_probe",
+            "achieved": round(achieved, 2),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": None,
+        },
+    }
+    if rank == 0 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(q, per if world == 1 else total)
+    for h in handles:
+        eng.free(h)
+    eng.close()
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

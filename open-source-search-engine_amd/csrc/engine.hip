@@ -54,7 +54,7 @@ constexpr int CHUNK_LOAD = CHUNK_BYTES + 16;     // + the tail of a 12-byte key
 constexpr int CHUNKS_PER_PROBE_BLOCK = 8;        // merge-path span of one block
 constexpr int WIN = 256;                         // candidate window (LDS)
 constexpr int TILE = 2048;                       // top-k tile
-constexpr int LIST_PAD = CHUNK_LOAD + 64;
+constexpr int LIST_PAD = CHUNK_LOAD + 128;
 
 struct Counters {
   uint32_t nsurv;
@@ -242,103 +242,176 @@ __global__ void __launch_bounds__(BLOCK) k_write_runs(const DevPlan *pl, const G
 }
 
 // ------------------------------------------------------------- probe scan
+// Per-thread view of its UPT=8 units: 64 bytes read from the LDS chunk with
+// four conflict-free ds_read_b128 (thread t at byte 48t: dword 12t mod 64
+// tiles all 64 banks over 16 lanes), so classification and docid extraction
+// run from registers.  Bytes 48..63 belong to the next thread and supply the
+// docid bytes of a 12-byte key starting at the last unit.
+struct UnitRegs {
+  uint32_t w[16];
+  __device__ __forceinline__ uint32_t byte(int i) const { return (w[i >> 2] >> ((i & 3) * 8)) & 0xff; }
+};
+
+__device__ __forceinline__ void load_units(const uint8_t *lds, UnitRegs &r) {
+  const uint4 *p = reinterpret_cast<const uint4 *>(lds + threadIdx.x * 48);
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    uint4 v = p[i];
+    r.w[4 * i] = v.x;
+    r.w[4 * i + 1] = v.y;
+    r.w[4 * i + 2] = v.z;
+    r.w[4 * i + 3] = v.w;
+  }
+}
+
+// docid of a key starting at unit q of this thread (bytes 6q+7 .. 6q+11)
+__device__ __forceinline__ uint64_t regs_docid(const UnitRegs &r, int q) {
+  const int b = 6 * q + 7;
+  uint64_t d = 0;
+#pragma unroll
+  for (int i = 4; i >= 0; i--) d = (d << 8) | r.byte(b + i);
+  return d >> 2;
+}
+
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    uint64_t y = __shfl_xor(v, o, 64);
+    v = y < v ? y : v;
+  }
+  return v;
+}
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    uint64_t y = __shfl_xor(v, o, 64);
+    v = y > v ? y : v;
+  }
+  return v;
+}
+
+// MODE (diagnostic builds only, GBGPU_PROBE_MODE): 0 full, 1 stop after the
+// unit classification, 2 stop after staging the chunk in LDS.
+template <int MODE>
 __global__ void __launch_bounds__(BLOCK) k_probe(const DevPlan *pl, const ProbeWork *work,
                                                  const uint64_t *cand, uint32_t *mask, uint32_t *loc,
                                                  uint64_t slot_ub, const Counters *ctr) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[CHUNK_LOAD];
+  __shared__ __attribute__((aligned(16))) uint8_t lds[CHUNK_LOAD + 32];
   __shared__ uint64_t win[WIN];
   __shared__ uint32_t s_lo[MAXG0];
-  __shared__ uint32_t s_minu, s_maxu;
+  __shared__ uint64_t s_red[2][BLOCK / 64];
   const ProbeWork w = work[blockIdx.x];
   const DevList &L = pl->lists[w.list];
   const uint32_t bits = L.group_bits;
   const int g0n = pl->g0n;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   bool first_chunk = true;
   for (uint32_t u0 = w.u0; u0 < w.u1; u0 += CHUNK_UNITS) {
     load_chunk(L.p, u0, lds);
-    if (threadIdx.x == 0) { s_minu = 0xffffffffu; s_maxu = 0; }
     __syncthreads();
-    uint32_t starts = thread_starts(lds, u0, L.units);
-    if (u0 + threadIdx.x * UPT >= w.u1) starts = 0;
-    // restrict to units < w.u1 (blocks own [u0,u1) exactly)
-#pragma unroll
-    for (int q = 0; q < UPT; q++)
-      if (u0 + threadIdx.x * UPT + q >= w.u1) starts &= ~(1u << q);
-    uint64_t dk[UPT];
-#pragma unroll
-    for (int q = 0; q < UPT; q++) dk[q] = (starts >> q & 1) ? unit_docid(lds + (threadIdx.x * UPT + q) * 6) : 0;
-    if (starts) {
-      atomicMin(&s_minu, threadIdx.x * UPT + (__ffs(starts) - 1));
-      atomicMax(&s_maxu, threadIdx.x * UPT + (31 - __clz(starts)));
-    }
-    __syncthreads();
-    if (s_minu == 0xffffffffu) {  // no run starts in this chunk
+    if (MODE == 2) {
+      if (lds[threadIdx.x * 48] == 0xee && lds[threadIdx.x * 48 + 1] == 0x77) mask[0] = 1;
       __syncthreads();
       continue;
     }
-    const uint64_t dmin = unit_docid(lds + s_minu * 6);
-    const uint64_t dmax = unit_docid(lds + s_maxu * 6);
+    UnitRegs r;
+    load_units(lds, r);
+    uint32_t starts = 0;
+    uint64_t dk[UPT];
+    uint64_t tmin = ~0ull, tmax = 0;
+#pragma unroll
+    for (int q = 0; q < UPT; q++) {
+      const uint32_t gu = u0 + threadIdx.x * UPT + q;
+      const bool st = gu < w.u1 && (r.byte(6 * q + 1) & 0x02) && !(r.byte(6 * q) & 0x04);
+      dk[q] = st ? regs_docid(r, q) : 0;
+      if (st) {
+        starts |= 1u << q;
+        tmin = dk[q] < tmin ? dk[q] : tmin;
+        tmax = dk[q] > tmax ? dk[q] : tmax;
+      }
+    }
+    tmin = wave_min_u64(tmin);
+    tmax = wave_max_u64(tmax);
+    if (lane == 0) {
+      s_red[0][wid] = tmin;
+      s_red[1][wid] = tmax;
+    }
+    __syncthreads();
+    uint64_t dmin = s_red[0][0], dmax = s_red[1][0];
+#pragma unroll
+    for (int i = 1; i < BLOCK / 64; i++) {
+      dmin = s_red[0][i] < dmin ? s_red[0][i] : dmin;
+      dmax = s_red[1][i] > dmax ? s_red[1][i] : dmax;
+    }
+    if (dmin == ~0ull || MODE == 1) {  // no run starts in this chunk
+      if (MODE == 1 && dk[0] == 0x123456789ull) mask[0] = 1;
+      __syncthreads();
+      continue;
+    }
     uint32_t found = 0;
     for (int k = 0; k < g0n; k++) {
       const uint32_t nk = ctr->g0count[k];
       const uint64_t *ck = cand + pl->g0base[k];
       if (first_chunk) {
-        uint32_t lo = block_lower_bound(ck, nk, dmin);
-        if (threadIdx.x == 0) s_lo[k] = lo;
+        uint32_t lo0 = block_lower_bound(ck, nk, dmin);
+        if (threadIdx.x == 0) s_lo[k] = lo0;
         __syncthreads();
       }
-      uint32_t todo = starts & ~found;
-      for (;;) {
-        const uint32_t lo = s_lo[k];
-        const uint32_t wc = (nk > lo) ? min((uint32_t)WIN, nk - lo) : 0u;
-        __syncthreads();
-        if (threadIdx.x < wc) win[threadIdx.x] = ck[lo + threadIdx.x];
-        __syncthreads();
-        const bool lastw = (lo + wc >= nk);
-        const uint64_t wmax = wc ? win[wc - 1] : 0;
-        uint32_t still = 0;
-        uint32_t t = todo;
-        while (t) {
-          int q = __ffs(t) - 1;
-          t &= t - 1;
-          const uint64_t d = dk[q];
-          if (!lastw && d > wmax) { still |= 1u << q; continue; }
-          // binary search in the window
-          uint32_t a = 0, b = wc;
+      const uint32_t lo = s_lo[k];
+      const uint32_t wc = (nk > lo) ? min((uint32_t)WIN, nk - lo) : 0u;
+      if (threadIdx.x < wc) win[threadIdx.x] = ck[lo + threadIdx.x];
+      __syncthreads();
+      const bool covered = (lo + wc >= nk) || (win[wc - 1] >= dmax);
+      uint32_t hi;  // one past the last candidate <= dmax
+      if (covered) {
+        uint32_t a = 0, b = wc;
+        while (a < b) {
+          uint32_t mid = (a + b) >> 1;
+          if (win[mid] <= dmax) a = mid + 1;
+          else b = mid;
+        }
+        hi = lo + a;
+      } else {
+        hi = lo + block_lower_bound(ck + lo, nk - lo, dmax + 1);
+      }
+#pragma unroll
+      for (int q = 0; q < UPT; q++) {
+        if (!((starts & ~found) >> q & 1)) continue;
+        const uint64_t d = dk[q];
+        uint32_t a, b;
+        bool hit;
+        if (covered) {
+          a = 0;
+          b = hi - lo;
           while (a < b) {
             uint32_t mid = (a + b) >> 1;
             if (win[mid] < d) a = mid + 1;
             else b = mid;
           }
-          if (a < wc && win[a] == d) {
-            const uint64_t slot = pl->g0base[k] + lo + a;
-            found |= 1u << q;
-            loc[(uint64_t)w.list * slot_ub + slot] = u0 + threadIdx.x * UPT + q;
-            atomicOr(&mask[slot], bits);
+          hit = (a < hi - lo) && win[a] == d;
+        } else {
+          a = lo;
+          b = hi;
+          while (a < b) {
+            uint32_t mid = (a + b) >> 1;
+            if (ck[mid] < d) a = mid + 1;
+            else b = mid;
           }
+          hit = (a < hi) && ck[a] == d;
+          a -= lo;
         }
-        todo = still;
-        int any = __syncthreads_or(todo != 0);
-        if (!any) {
-          // next chunk starts after dmax: advance to upper_bound(dmax) in window
-          if (threadIdx.x == 0) {
-            uint32_t a = 0, b = wc;
-            while (a < b) {
-              uint32_t mid = (a + b) >> 1;
-              if (win[mid] <= dmax) a = mid + 1;
-              else b = mid;
-            }
-            s_lo[k] = lo + a;
-          }
-          __syncthreads();
-          break;
+        if (hit) {
+          const uint64_t slot = pl->g0base[k] + lo + a;
+          found |= 1u << q;
+          loc[(uint64_t)w.list * slot_ub + slot] = u0 + threadIdx.x * UPT + q;
+          atomicOr(&mask[slot], bits);
         }
-        if (threadIdx.x == 0) s_lo[k] = lo + wc;
-        __syncthreads();
       }
+      __syncthreads();
+      if (threadIdx.x == 0) s_lo[k] = hi;  // next chunk's docids are > dmax
+      __syncthreads();
     }
     first_chunk = false;
-    __syncthreads();
   }
 }
 
@@ -358,60 +431,68 @@ __device__ __forceinline__ bool valid_run(const DevList &L, uint32_t u, uint64_t
   return unit_docid(k) == docid;
 }
 
+constexpr int CSPT = 16;                        // compaction slots per thread
+constexpr int CTILE = BLOCK * CSPT;              // 4096 slots per block
+
+// Survivors of one contiguous tile of candidate slots, appended with ONE
+// pair of atomics per block (a single device counter cannot take one atomic
+// per wave: MI355X_MICROARCH.md "dequeue" row, ~88 per us per word).
 __global__ void __launch_bounds__(BLOCK) k_compact(const DevPlan *pl, const uint64_t *cand,
                                                    const uint32_t *mask, const uint32_t *loc,
                                                    uint64_t slot_ub, Counters *ctr, uint32_t *surv,
                                                    unsigned long long *surv_off) {
+  __shared__ uint32_t tmp[BLOCK / 64];
+  __shared__ uint32_t s_base_i;
+  __shared__ unsigned long long s_base_u;
   const uint32_t pos = pl->pos_mask;
-  const int lane = threadIdx.x & 63;
-  for (uint64_t s0 = (uint64_t)blockIdx.x * BLOCK; s0 < slot_ub; s0 += (uint64_t)gridDim.x * BLOCK) {
-    const uint64_t s = s0 + threadIdx.x;
-    bool ok = false;
-    uint32_t units = 0;
-    if (s < slot_ub) {
-      int k = 0;
-      while (k + 1 < pl->g0n && s >= pl->g0base[k + 1]) k++;
-      if (s - pl->g0base[k] < ctr->g0count[k]) {
-        const uint32_t m = mask[s];
-        ok = ((m & pos) == pos) && !(m & NEG_BIT);
+  const uint64_t s0 = (uint64_t)blockIdx.x * CTILE + (uint64_t)threadIdx.x * CSPT;
+  uint32_t okm = 0, nok = 0, utot = 0;
+  uint32_t units[CSPT];
+#pragma unroll
+  for (int q = 0; q < CSPT; q++) {
+    const uint64_t s = s0 + q;
+    units[q] = 0;
+    if (s >= slot_ub) continue;
+    int k = 0;
+    while (k + 1 < pl->g0n && s >= pl->g0base[k + 1]) k++;
+    if (s - pl->g0base[k] >= ctr->g0count[k]) continue;
+    const uint32_t m = mask[s];
+    if (!(((m & pos) == pos) && !(m & NEG_BIT))) continue;
+    const uint64_t d = cand[s];
+    uint32_t u_s = 0;
+    for (int j = 0; j < pl->ngroups; j++) {
+      if (pl->gflags0[j] & BF_NEGATIVE) continue;
+      for (int x = 0; x < pl->gnsub[j]; x++) {
+        const int lid = pl->gsub[j][x];
+        const DevList &L = pl->lists[lid];
+        const uint32_t u = loc[(uint64_t)lid * slot_ub + s];
+        if (!valid_run(L, u, d)) continue;
+        u_s += run_units(L.p, L.units, u);
+        if (!ctr->anysurv[lid]) atomicOr((uint32_t *)&ctr->anysurv[lid], 1u);
       }
-      if (ok) {
-        const uint64_t d = cand[s];
-        for (int j = 0; j < pl->ngroups; j++) {
-          if (pl->gflags0[j] & BF_NEGATIVE) continue;
-          for (int x = 0; x < pl->gnsub[j]; x++) {
-            const int lid = pl->gsub[j][x];
-            const DevList &L = pl->lists[lid];
-            const uint32_t u = loc[(uint64_t)lid * slot_ub + s];
-            if (!valid_run(L, u, d)) continue;
-            units += run_units(L.p, L.units, u);
-            if (!ctr->anysurv[lid]) atomicOr((uint32_t *)&ctr->anysurv[lid], 1u);
-          }
-        }
-      }
     }
-    // wave-aggregated append of survivors and their scratch
-    unsigned long long bal = __ballot(ok);
-    uint32_t u_incl = units;
-    for (int o = 1; o < 64; o <<= 1) {
-      uint32_t y = __shfl_up(u_incl, o, 64);
-      if (lane >= o) u_incl += y;
-    }
-    const uint32_t u_tot = __shfl(u_incl, 63, 64);
-    const uint32_t n_tot = __popcll(bal);
-    uint32_t base_i = 0;
-    unsigned long long base_u = 0;
-    if (lane == 0 && n_tot) {
-      base_i = atomicAdd(&ctr->nsurv, n_tot);
-      base_u = atomicAdd(&ctr->scratch_top, (unsigned long long)u_tot);
-    }
-    base_i = __shfl(base_i, 0, 64);
-    base_u = __shfl(base_u, 0, 64);
-    if (ok) {
-      const uint32_t rank = __popcll(bal & ((1ull << lane) - 1));
-      surv[base_i + rank] = (uint32_t)s;
-      surv_off[base_i + rank] = base_u + (u_incl - units);
-    }
+    units[q] = u_s;
+    okm |= 1u << q;
+    nok++;
+    utot += u_s;
+  }
+  uint32_t tot_n, tot_u;
+  const uint32_t ex_n = block_exclusive_scan(nok, tmp, &tot_n);
+  const uint32_t ex_u = block_exclusive_scan(utot, tmp, &tot_u);
+  if (threadIdx.x == 0) {
+    s_base_i = tot_n ? atomicAdd(&ctr->nsurv, tot_n) : 0;
+    s_base_u = tot_n ? atomicAdd(&ctr->scratch_top, (unsigned long long)tot_u) : 0;
+  }
+  __syncthreads();
+  uint32_t i = s_base_i + ex_n;
+  unsigned long long off = s_base_u + ex_u;
+#pragma unroll
+  for (int q = 0; q < CSPT; q++) {
+    if (!(okm >> q & 1)) continue;
+    surv[i] = (uint32_t)(s0 + q);
+    surv_off[i] = off;
+    i++;
+    off += units[q];
   }
 }
 
@@ -553,6 +634,13 @@ __global__ void __launch_bounds__(1024) k_topk_tile(const uint32_t *in_key, cons
   __shared__ uint64_t sd[TILE];
   const uint32_t n_in = n_in_ptr ? *n_in_ptr : n_in_const;
   const uint64_t base = (uint64_t)blockIdx.x * TILE;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && n_out_ptr) {
+    const uint32_t tiles = (n_in + TILE - 1) / TILE;
+    *n_out_ptr = tiles * (uint32_t)k;
+  }
+  // tiles past the live count exit (grid sized by an upper bound); tile 0
+  // always runs so an empty input still yields an all-invalid output
+  if (base >= n_in && blockIdx.x != 0) return;
   for (int t = threadIdx.x; t < TILE; t += blockDim.x) {
     const uint64_t g = base + t;
     if (g < n_in) {
@@ -586,10 +674,6 @@ __global__ void __launch_bounds__(1024) k_topk_tile(const uint32_t *in_key, cons
   for (int t = threadIdx.x; t < k; t += blockDim.x) {
     out_key[obase + t] = sk[t];
     out_doc[obase + t] = sd[t];
-  }
-  if (blockIdx.x == 0 && threadIdx.x == 0 && n_out_ptr) {
-    const uint32_t tiles = (n_in + TILE - 1) / TILE;
-    *n_out_ptr = tiles * (uint32_t)k;
   }
 }
 
@@ -676,6 +760,8 @@ struct gbgpu_ctx {
   std::vector<G0Chunk> g0c;
   std::vector<ProbeWork> pw;
   std::vector<uint32_t> afirst;
+  uint8_t *h_stage = nullptr;  // pinned staging for the per-query tables
+  size_t stage_cap = 0;
   // state of the in-flight query
   bool pending = false;
   bool early = false;
@@ -684,6 +770,7 @@ struct gbgpu_ctx {
   int32_t docs_wanted = 0;
   int64_t scan_bytes = 0;
   bool profiling = false;
+  int probe_mode = 0;  // diagnostic only (GBGPU_PROBE_MODE)
   hipEvent_t ev[7] = {};
   float last_ms[6] = {0, 0, 0, 0, 0, 0};
   // per-query temporary lists (gbgpu_query with host lists)
@@ -825,7 +912,11 @@ static int enqueue(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms, const i
     const uint32_t units = P.lists[id].units;
     scan += (int64_t)units * 6;
     if (!P.lists[id].probe) continue;
-    const uint32_t span = CHUNK_UNITS * CHUNKS_PER_PROBE_BLOCK;
+    // long lists: 8 chunks per block amortise the candidate search; short
+    // lists: 1 chunk per block so they do not form the kernel's tail
+    const uint32_t nch = (units + CHUNK_UNITS - 1) / CHUNK_UNITS;
+    const uint32_t cpb = std::max(1u, std::min<uint32_t>(CHUNKS_PER_PROBE_BLOCK, nch / 1024));
+    const uint32_t span = CHUNK_UNITS * cpb;
     for (uint32_t u = 0; u < units; u += span) ctx->pw.push_back({(uint32_t)id, u, std::min(units, u + span)});
   }
   ctx->scan_bytes = scan;
@@ -867,13 +958,25 @@ static int enqueue(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms, const i
   hipStream_t st = ctx->stream;
   if (ctx->profiling) HIPCHECK(hipEventRecord(ctx->ev[0], st));
   HIPCHECK(hipMemcpyAsync(ctx->plan.p, ctx->h_plan, sizeof(DevPlan), hipMemcpyHostToDevice, st));
-  if (!ctx->g0c.empty())
-    HIPCHECK(hipMemcpyAsync(ctx->g0chunks.p, ctx->g0c.data(), sizeof(G0Chunk) * ctx->g0c.size(),
-                            hipMemcpyHostToDevice, st));
-  HIPCHECK(hipMemcpyAsync(ctx->arrfirst.p, ctx->afirst.data(), 4 * MAXG0, hipMemcpyHostToDevice, st));
-  if (!ctx->pw.empty())
-    HIPCHECK(hipMemcpyAsync(ctx->work.p, ctx->pw.data(), sizeof(ProbeWork) * ctx->pw.size(),
-                            hipMemcpyHostToDevice, st));
+  {
+    // the tables go through pinned memory: a pageable source makes the copy
+    // synchronous with the host and stalls the stream
+    const size_t b1 = sizeof(G0Chunk) * ctx->g0c.size(), b2 = 4 * MAXG0, b3 = sizeof(ProbeWork) * ctx->pw.size();
+    const size_t need = b1 + b2 + b3 + 64;
+    if (need > ctx->stage_cap) {
+      if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
+      ctx->h_stage = nullptr;
+      ctx->stage_cap = 0;
+      HIPCHECK(hipHostMalloc((void **)&ctx->h_stage, need * 2));
+      ctx->stage_cap = need * 2;
+    }
+    std::memcpy(ctx->h_stage, ctx->g0c.data(), b1);
+    std::memcpy(ctx->h_stage + b1, ctx->afirst.data(), b2);
+    std::memcpy(ctx->h_stage + b1 + b2, ctx->pw.data(), b3);
+    if (b1) HIPCHECK(hipMemcpyAsync(ctx->g0chunks.p, ctx->h_stage, b1, hipMemcpyHostToDevice, st));
+    HIPCHECK(hipMemcpyAsync(ctx->arrfirst.p, ctx->h_stage + b1, b2, hipMemcpyHostToDevice, st));
+    if (b3) HIPCHECK(hipMemcpyAsync(ctx->work.p, ctx->h_stage + b1 + b2, b3, hipMemcpyHostToDevice, st));
+  }
   HIPCHECK(hipMemsetAsync(ctx->counters.p, 0, sizeof(Counters), st));
   HIPCHECK(hipMemsetAsync(ctx->mask.p, 0, 4 * slot_ub, st));
   const DevPlan *dpl = ctx->plan.as<DevPlan>();
@@ -889,12 +992,14 @@ static int enqueue(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms, const i
                        ctx->mask.as<uint32_t>(), ctx->loc.as<uint32_t>(), slot_ub, dctr, ng0);
   }
   if (ctx->profiling) HIPCHECK(hipEventRecord(ctx->ev[1], st));
-  if (!ctx->pw.empty())
-    hipLaunchKernelGGL(k_probe, dim3((uint32_t)ctx->pw.size()), dim3(BLOCK), 0, st, dpl,
+  if (!ctx->pw.empty()) {
+    auto kp = ctx->probe_mode == 1 ? k_probe<1> : (ctx->probe_mode == 2 ? k_probe<2> : k_probe<0>);
+    hipLaunchKernelGGL(kp, dim3((uint32_t)ctx->pw.size()), dim3(BLOCK), 0, st, dpl,
                        ctx->work.as<ProbeWork>(), ctx->cand.as<uint64_t>(), ctx->mask.as<uint32_t>(),
                        ctx->loc.as<uint32_t>(), slot_ub, dctr);
+  }
   if (ctx->profiling) HIPCHECK(hipEventRecord(ctx->ev[2], st));
-  const uint32_t cgrid = (uint32_t)std::min<uint64_t>((slot_ub + BLOCK - 1) / BLOCK, 4096);
+  const uint32_t cgrid = (uint32_t)((slot_ub + CTILE - 1) / CTILE);
   hipLaunchKernelGGL(k_compact, dim3(std::max(cgrid, 1u)), dim3(BLOCK), 0, st, dpl, ctx->cand.as<uint64_t>(),
                      ctx->mask.as<uint32_t>(), ctx->loc.as<uint32_t>(), slot_ub, dctr, ctx->surv.as<uint32_t>(),
                      ctx->survoff.as<unsigned long long>());
@@ -1010,6 +1115,7 @@ int gbgpu_open(int device, gbgpu_ctx **out) {
     return ENOMEM;
   }
   for (auto &e : ctx->ev) (void)hipEventCreate(&e);
+  if (const char *pm = std::getenv("GBGPU_PROBE_MODE")) ctx->probe_mode = std::atoi(pm);
   *out = ctx;
   return 0;
 }
@@ -1028,6 +1134,7 @@ void gbgpu_close(gbgpu_ctx *ctx) {
   if (ctx->h_ctr) (void)hipHostFree(ctx->h_ctr);
   if (ctx->h_out_key) (void)hipHostFree(ctx->h_out_key);
   if (ctx->h_out_doc) (void)hipHostFree(ctx->h_out_doc);
+  if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
   for (auto &e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(ctx->stream);

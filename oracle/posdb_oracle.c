@@ -1197,6 +1197,16 @@ int orc_query(const orc_qterm *qt, const uint8_t *const *lists, const int64_t *s
         d |= docIdPtr[0];
         pt.docId = d >> 2;
       }
+      /* A positive group whose mini-merged list came out empty (all of its
+       * keys for this docid were BF_BIGRAM keys with syn bits, skipped at
+       * Posdb.cpp:6687-6692) makes the reference score stale mbuf bytes
+       * (undefined behaviour).  Defined here, as on the GPU: skip the docid. */
+      {
+        int emptyGroup = 0;
+        for (int j = 0; j < nqti; j++)
+          if (mml[j] && mml[j] == mme[j]) emptyGroup = 1;
+        if (emptyGroup) continue;
+      }
 
       /* non-body pair scores, Posdb.cpp:6847-6926 */
       for (int i = 0; i < nqti; i++) {
