@@ -3,7 +3,8 @@
  * Restatement of RdbList::posdbMerge_r (RdbList.cpp:3065-3568) with the
  * bfcmpPosdb comparator (RdbList.h:620-641), for lists already prepared by
  * prepareForMerge (every input list starts with an 18-byte key) merging into
- * an empty output list.  Parity unpinned.
+ * an empty output list.  Pinned bit-exact against the reference's own
+ * RdbList::merge_r (oracle/ref.mk, tests/golden/m_*.npz).
  */
 #include "posdb_oracle.h"
 
@@ -37,6 +38,7 @@ int64_t orc_posdb_merge(const uint8_t *const *lists, const int64_t *sizes, int n
                         int removeNegKeys, int64_t minRecSizes, uint8_t *out, int64_t cap) {
   if (numLists < 0 || numLists > MAXL) return -EINVAL;
   if (minRecSizes == 0) return 0;
+  const int numListsIn = numLists;
   const uint8_t *ptrs[MAXL], *ends[MAXL], *hiKeys[MAXL], *loKeys[MAXL];
   int n = 0;
   for (int i = 0; i < numLists; i++) {
@@ -50,8 +52,19 @@ int64_t orc_posdb_merge(const uint8_t *const *lists, const int64_t *sizes, int n
   }
   numLists = n;
   if (numLists <= 0) return 0;
-  /* maxPtr = m_list + minRecSizes, capped to the allocation */
-  int64_t maxOff = minRecSizes < 0 ? cap : minRecSizes;
+  /* prepareForMerge (RdbList.cpp:410-491) and merge_r (RdbList.cpp:1658-1756)
+   * turn the caller's minRecSizes into the bound posdbMerge_r receives:
+   * m_mergeMinListSize = min(sum of list sizes, minRecSizes + 2 * 18) for
+   * posdb (18-byte keys, fixedDataSize 0), or the sum when minRecSizes < 0.
+   * maxPtr = m_list + that, capped to the allocation (RdbList.cpp:3127-3133). */
+  int64_t total = 0;
+  for (int i = 0; i < numListsIn; i++) total += sizes[i] > 0 ? sizes[i] : 0;
+  int64_t maxOff = total;
+  if (minRecSizes > 0) {
+    int64_t nm = (int64_t)(int32_t)((uint32_t)minRecSizes + 36u);
+    if (nm < minRecSizes) nm = 0x7fffffff;
+    if (maxOff > nm) maxOff = nm;
+  }
   if (maxOff > cap) maxOff = cap;
   uint8_t *listPtr = out;
   uint8_t *listPtrLo = NULL, *listPtrHi = NULL, *pp = NULL;

@@ -7,8 +7,8 @@
  * expression below is written with the same operand types and order as the
  * reference expression it restates and rounds the same way.
  *
- * Parity unpinned for scoring (no reference fixture exists and the reference
- * path is unbuildable here without source edits).
+ * Pinned bit-exact against the reference's own PosdbTable (oracle/ref.mk,
+ * tests/golden/, tests/test_reference.py).
  */
 #include "posdb_oracle.h"
 

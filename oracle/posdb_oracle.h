@@ -2,12 +2,14 @@
  * reference's Posdb query-scoring path.  Only tests/, __graft_entry__.smoke()
  * and bench.py's cpu_baseline leg may load it; the product never does.
  *
- * Parity status: the posdb key codec is pinned by the reference's own
- * known-answer test (Posdb.cpp:24-86, tests/test_codec.py).  The scoring path
- * (PosdbTable::intersectLists10_r, TopTree, posdbMerge_r) is "parity
- * unpinned": the reference holds no fixture for it and its path cannot be
- * built here without editing reference sources.  This
- * file restates the reference algorithm line by line, citing file:line.
+ * Parity status: PINNED.  The posdb key codec is pinned by the reference's
+ * own known-answer test (Posdb.cpp:24-86, tests/test_codec.py).  The query
+ * path (intersectLists10_r + TopTree) and the list merge (merge_r ->
+ * posdbMerge_r) are pinned against the reference's own code, compiled
+ * unmodified into oracle/_ref/gbref (oracle/ref.mk): bit-exact on the
+ * committed golden vectors (tests/golden/, tests/test_golden.py) and on fresh
+ * seeds (tests/test_reference.py).  This file restates the reference
+ * algorithm line by line, citing file:line.
  */
 #ifndef GB_POSDB_ORACLE_H
 #define GB_POSDB_ORACLE_H
@@ -63,8 +65,10 @@ int orc_query(const orc_qterm *terms, const uint8_t *const *lists, const int64_t
 int64_t orc_intersect(const orc_qterm *terms, const uint8_t *const *lists, const int64_t *sizes,
                       int nterms, int64_t *docids, int64_t cap);
 
-/* RdbList::posdbMerge_r (RdbList.cpp:3065-3568) over n lists already
- * prepared by prepareForMerge; returns bytes written to out (cap bytes). */
+/* RdbList::merge_r -> posdbMerge_r (RdbList.cpp:1658-1756, 3065-3568) into an
+ * empty list, with prepareForMerge's bound (RdbList.cpp:410-491): min_rec_sizes
+ * is the caller's minRecSizes (-1: no limit).  Lists oldest first, each
+ * starting with an 18-byte key.  Returns bytes written to out (cap bytes). */
 int64_t orc_posdb_merge(const uint8_t *const *lists, const int64_t *sizes, int n,
                         int remove_neg_keys, int64_t min_rec_sizes, uint8_t *out, int64_t cap);
 

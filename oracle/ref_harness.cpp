@@ -1,0 +1,356 @@
+// TEST INFRASTRUCTURE ONLY -- drives the REFERENCE's own PosdbTable,
+// TopTree and RdbList::merge_r, compiled unmodified from /root/reference by
+// oracle/ref.mk into oracle/_ref/gbref.  Tests use it to pin the
+// restatement (posdb_oracle.c) and to generate tests/golden/ fixtures; the
+// product never loads it, and it is built only where /root/reference exists.
+//
+// The harness plays the part of main.cpp + Msg39 for one query: it fills a
+// Query/QueryTerm/QueryWord array the way Query::set2 leaves it (the fields
+// PosdbTable reads, Posdb.cpp:4354-4869), wraps the caller's lists in a Msg2,
+// and runs the same sequence as Msg39::intersectLists (Msg39.cpp:884-1053):
+//   PosdbTable::init -> allocTopTree -> allocWhiteListTable ->
+//   setQueryTermInfo -> intersectLists10_r
+// then reads TopTree high -> low (Msg39.cpp:1346-1420 readout order).
+//
+// Lists are copied before every run because intersectLists10_r mutates them
+// (first-key swap Posdb.cpp:5671-5703, shrinkSubLists Posdb.cpp:5334-5428).
+#include "gb-include.h"
+
+#include "Collectiondb.h"
+#include "Mem.h"
+#include "Msg2.h"
+#include "Msg39.h"
+#include "Posdb.h"
+#include "Query.h"
+#include "RdbList.h"
+#include "TopTree.h"
+
+#include <stdint.h>
+#include <string.h>
+
+#include "posdb_oracle.h"  // orc_qterm / orc_params / orc_result
+
+// Symbols main.cpp defines for the gb binary (main.cpp:155,197,199); the
+// harness is this program's main module.
+int g_inMemcpy = 0;
+bool g_recoveryMode = false;
+int32_t g_recoveryLevel = 0;
+
+extern bool hashinit();
+
+// A fault inside the reference (or a call into a unit ref.mk did not link)
+// prints a backtrace instead of dying silently.  Installed before any static
+// initialiser of the reference units runs.
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
+#include <stdio.h>
+#include <ucontext.h>
+static void on_fault(int sig, siginfo_t *si, void *uc) {
+  void *bt[64];
+  int n = backtrace(bt, 64);
+  const ucontext_t *u = (const ucontext_t *)uc;
+  const unsigned long pc = u->uc_mcontext.gregs[REG_RIP];
+  const unsigned long sp = u->uc_mcontext.gregs[REG_RSP];
+  char msg[160];
+  // pc 0 = a call into a unit ref.mk does not link: [sp] is its caller
+  int m = snprintf(msg, sizeof msg, "gbref: fatal signal %d at pc=%#lx addr=%p caller=%#lx; backtrace:\n", sig,
+                   pc, si->si_addr, pc == 0 ? *(const unsigned long *)sp : 0ul);
+  write(2, msg, m);
+  backtrace_symbols_fd(bt, n, 2);
+  _exit(128 + sig);
+}
+__attribute__((constructor(101))) static void install_fault_handler() {
+  struct sigaction sa;
+  memset(&sa, 0, sizeof sa);
+  sa.sa_sigaction = on_fault;
+  sa.sa_flags = SA_SIGINFO;
+  sigaction(SIGSEGV, &sa, NULL);
+  sigaction(SIGBUS, &sa, NULL);
+  sigaction(SIGFPE, &sa, NULL);
+}
+
+static bool s_inited = false;
+static CollectionRec *s_crPtr[1];
+
+static void ref_init() {
+  if (s_inited) return;
+  // gb.conf "maxmem" (Conf.h m_maxMem, read by Mem's operator new): no
+  // gb.conf is loaded here, so give the allocator the whole box
+  g_conf.m_maxMem = (int64_t)1 << 40;
+  g_mem.init();
+  hashinit();
+  // one collection, collnum 0 (PosdbTable::init requires getRec(collnum))
+  static CollectionRec *cr = new CollectionRec();
+  s_crPtr[0] = cr;
+  g_collectiondb.m_recs = s_crPtr;
+  g_collectiondb.m_numRecs = 1;
+  s_inited = true;
+}
+
+enum { MAXT = 64 };
+
+static int ref_query(const orc_qterm *terms, const uint8_t *const *lists, const int64_t *sizes, int nterms,
+                         const orc_params *p, int64_t *docids, float *scores, int cap, orc_result *out,
+                         int64_t *vote_docids, int64_t vote_cap) {
+  ref_init();
+  if (nterms < 0 || nterms > MAXT) return EINVAL;
+  static Query q;
+  static QueryTerm qts[MAXT];
+  static QueryWord qws[MAXT];
+  static RdbList rl[MAXT];
+  static Msg2 msg2;
+  static Msg39Request req;
+  static TopTree tree;
+  static float tfw[MAXT];
+  static PosdbTable *tab = NULL;
+
+  for (int i = 0; i < nterms; i++) {
+    rl[i].freeList();
+    // RdbList::set(list, size, alloc, allocSize, fixedDataSize, ownData,
+    // useHalfKeys, keySize=18): a fresh mutable copy per run
+    char *buf = NULL;
+    int32_t sz = (int32_t)sizes[i];
+    if (sz > 0) {
+      buf = (char *)mmalloc(sz + 64, "refharness");
+      memcpy(buf, lists[i], sz);
+    }
+    rl[i].set(buf, sz, buf, sz ? sz + 64 : 0, 0, true, true, 18);
+  }
+
+  memset((void *)qts, 0, sizeof(qts));
+  memset((void *)qws, 0, sizeof(qws));
+  for (int i = 0; i < nterms; i++) {
+    const orc_qterm &t = terms[i];
+    QueryTerm *qt = &qts[i];
+    QueryWord *qw = &qws[i];
+    qw->m_posNum = t.qpos;
+    qw->m_wikiPhraseId = t.wiki_phrase_id;
+    qw->m_quoteStart = t.quote_start;
+    qt->m_qword = qw;
+    qt->m_isRequired = t.is_required != 0;
+    qt->m_termSign = (char)t.term_sign;
+    qt->m_fieldCode = (char)t.field_code;
+    qt->m_piped = t.piped != 0;
+    qt->m_synonymOf = t.synonym_of >= 0 ? &qts[t.synonym_of] : NULL;
+    qt->m_leftPhraseTermNum = t.left_phrase_term;
+    qt->m_rightPhraseTermNum = t.right_phrase_term;
+    qt->m_leftPhraseTerm = t.left_phrase_term >= 0 ? &qts[t.left_phrase_term] : NULL;
+    qt->m_rightPhraseTerm = t.right_phrase_term >= 0 ? &qts[t.right_phrase_term] : NULL;
+    qt->m_isWikiHalfStopBigram = t.is_wiki_half_stop_bigram != 0;
+    tfw[i] = t.tf_weight;
+  }
+  q.m_qterms = qts;
+  q.m_numTerms = nterms;
+  q.m_isBoolean = false;
+
+  msg2.m_query = &q;
+  msg2.m_lists = rl;
+  msg2.m_numLists = nterms;  // Msg2::getLists sets it (Msg2.cpp:121-347)
+  msg2.m_w = 0;
+
+  req.reset();
+  req.m_docsToGet = p->docs_to_get;
+  req.m_realMaxTop = p->real_max_top;
+  req.m_language = (uint8_t)p->language;
+  req.m_sameLangWeight = p->same_lang_weight;
+  req.m_doSiteClustering = p->site_clustering != 0;
+  req.m_numDocIdSplits = p->num_docid_splits;
+  req.m_getDocIdScoringInfo = false;
+  req.m_collnum = 0;
+  req.ptr_termFreqWeights = (char *)tfw;
+  req.size_termFreqWeights = 4 * nterms;
+
+  if (tab) {
+    tab->~PosdbTable();
+    mfree(tab, sizeof(PosdbTable), "refharness");
+  }
+  tab = (PosdbTable *)mmalloc(sizeof(PosdbTable), "refharness");
+  new (tab) PosdbTable();
+  tree.~TopTree();
+  memset((void *)&tree, 0, sizeof tree);  // m_docsWanted is only set by setNumNodes
+  new (&tree) TopTree();
+
+  // Msg39::intersectLists sequence (Msg39.cpp:922-1027)
+  tab->init(&q, 0, NULL, &tree, 0, &msg2, &req);
+  if (!tab->allocTopTree()) return ENOMEM;
+  if (!tab->allocWhiteListTable()) return ENOMEM;
+  if (!tab->setQueryTermInfo()) return ENOMEM;
+  tab->intersectLists10_r();
+
+  out->hits = tab->m_docIdVoteBuf.length() / 6;
+  out->filtered = tab->m_filtered;
+  // allocTopTree returns before setNumNodes when every list is empty
+  // (Posdb.cpp:889-890): no tree, reported as 0 like the oracle
+  out->docs_wanted = tree.m_numNodes > 0 ? tree.m_docsWanted : 0;
+  out->corrupt = tab->m_errno;
+  int n = 0;
+  if (tree.m_numNodes > 0) {
+    for (int32_t ti = tree.getHighNode(); ti >= 0 && n < cap; ti = tree.getPrev(ti)) {
+      TopNode *t = tree.getNode(ti);
+      docids[n] = t->m_docId;
+      scores[n] = t->m_score;
+      n++;
+    }
+  }
+  out->n = n;
+  if (vote_docids) {
+    // m_docIdVoteBuf records: [b7&0xfc, b8..b11, vote] (Posdb.cpp:5281-5290)
+    const uint8_t *v = (const uint8_t *)tab->m_docIdVoteBuf.getBufStart();
+    int64_t nv = tab->m_docIdVoteBuf.length() / 6;
+    for (int64_t i = 0; i < nv && i < vote_cap; i++) {
+      const uint8_t *r = v + 6 * i;
+      uint64_t d = (uint64_t)r[0] | ((uint64_t)r[1] << 8) | ((uint64_t)r[2] << 16) |
+                   ((uint64_t)r[3] << 24) | ((uint64_t)r[4] << 32);
+      vote_docids[i] = (int64_t)(d >> 2);
+    }
+  }
+  return 0;
+}
+
+// RdbList::merge_r -> posdbMerge_r (RdbList.cpp:1658,1745-1756,3065) on
+// copies of n posdb lists (oldest first), as Msg5::mergeLists_r calls it.
+static int64_t ref_posdb_merge(const uint8_t *const *lists, const int64_t *sizes, int n, int remove_neg_keys,
+                                   int64_t min_rec_sizes, uint8_t *out, int64_t cap) {
+  ref_init();
+  if (n < 0 || n > 256) return -EINVAL;
+  static RdbList in[256];
+  RdbList *ptrs[256];
+  for (int i = 0; i < n; i++) {
+    in[i].freeList();
+    int32_t sz = (int32_t)sizes[i];
+    char *buf = NULL;
+    if (sz > 0) {
+      buf = (char *)mmalloc(sz, "refharness");
+      memcpy(buf, lists[i], sz);
+    }
+    in[i].set(buf, sz, buf, sz, 0, true, true, 18);
+    ptrs[i] = &in[i];
+  }
+  RdbList dst;
+  dst.set(NULL, 0, NULL, 0, 0, true, true, 18);
+  char startKey[18], endKey[18];
+  memset(startKey, 0, 18);
+  memset(endKey, 0xff, 18);
+  int32_t mrs = min_rec_sizes < 0 ? -1 : (int32_t)min_rec_sizes;
+  if (!dst.prepareForMerge(ptrs, n, mrs)) return -ENOMEM;
+  int32_t filtered = 0;
+  dst.merge_r(ptrs, n, startKey, endKey, mrs, remove_neg_keys != 0, RDB_POSDB, &filtered, NULL, NULL, false, 0);
+  int64_t sz = dst.m_listSize;
+  if (sz > cap) return -ENOSPC;
+  memcpy(out, dst.m_list, sz);
+  dst.freeList();
+  return sz;
+}
+
+// ------------------------------------------------------------------ driver
+// Binary request on stdin, response on stdout (little-endian, host layout):
+//   op=1 query: i32 nterms, orc_params, nterms x orc_qterm,
+//               nterms x (i64 size, bytes), i32 cap, i32 want_votes, i32 reps
+//        ->     orc_result, n x i64 docid, n x f32 score,
+//               i64 nvotes, nvotes x i64 docid, f64 seconds per run (median)
+//   op=2 merge: i32 n, i32 remove_neg, i64 min_rec_sizes, n x (i64 size, bytes)
+//        ->     i64 size (or -errno), bytes
+#include <stdio.h>
+#include <stdlib.h>
+#include <time.h>
+
+#include <algorithm>
+#include <vector>
+
+static void rd(void *p, size_t n) {
+  if (n && fread(p, 1, n, stdin) != n) {
+    fprintf(stderr, "gbref: short read\n");
+    exit(2);
+  }
+}
+static void wr(const void *p, size_t n) {
+  if (n && fwrite(p, 1, n, stdout) != n) exit(3);
+}
+static double now_s() {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+int main(int argc, char **argv) {
+  ref_init();  // Mem's global operator new needs g_mem before any allocation
+  int32_t op;
+  while (fread(&op, 4, 1, stdin) == 1) {
+    if (op == 1) {
+      int32_t nt;
+      rd(&nt, 4);
+      if (nt < 0 || nt > MAXT) return 4;
+      orc_params p;
+      rd(&p, sizeof p);
+      std::vector<orc_qterm> t(nt);
+      rd(t.data(), sizeof(orc_qterm) * nt);
+      std::vector<std::vector<uint8_t> > bufs(nt);
+      std::vector<const uint8_t *> ptrs(nt);
+      std::vector<int64_t> sizes(nt);
+      for (int i = 0; i < nt; i++) {
+        rd(&sizes[i], 8);
+        bufs[i].resize(sizes[i] + 1);
+        rd(bufs[i].data(), sizes[i]);
+        ptrs[i] = bufs[i].data();
+      }
+      int32_t cap, want_votes, reps;
+      rd(&cap, 4);
+      rd(&want_votes, 4);
+      rd(&reps, 4);
+      std::vector<int64_t> d(cap > 0 ? cap : 1);
+      std::vector<float> s(cap > 0 ? cap : 1);
+      int64_t vcap = 0;
+      for (int i = 0; i < nt; i++) vcap += sizes[i] / 12 + 1;
+      std::vector<int64_t> votes(want_votes ? vcap : 1);
+      orc_result r;
+      memset(&r, 0, sizeof r);
+      std::vector<double> times;
+      if (reps < 1) reps = 1;
+      int rc = 0;
+      for (int k = 0; k < reps; k++) {
+        double t0 = now_s();
+        rc = ref_query(t.data(), ptrs.data(), sizes.data(), nt, &p, d.data(), s.data(), cap, &r,
+                       want_votes ? votes.data() : NULL, vcap);
+        times.push_back(now_s() - t0);
+        if (rc) break;
+      }
+      if (rc) r.corrupt = -rc;
+      std::sort(times.begin(), times.end());
+      double med = times[times.size() / 2];
+      wr(&r, sizeof r);
+      wr(d.data(), 8 * (size_t)r.n);
+      wr(s.data(), 4 * (size_t)r.n);
+      int64_t nv = want_votes ? std::min<int64_t>(r.hits, vcap) : 0;
+      wr(&nv, 8);
+      wr(votes.data(), 8 * (size_t)nv);
+      wr(&med, 8);
+    } else if (op == 2) {
+      int32_t n, rm;
+      int64_t mrs;
+      rd(&n, 4);
+      rd(&rm, 4);
+      rd(&mrs, 8);
+      if (n < 0 || n > 256) return 4;
+      std::vector<std::vector<uint8_t> > bufs(n);
+      std::vector<const uint8_t *> ptrs(n);
+      std::vector<int64_t> sizes(n);
+      int64_t tot = 0;
+      for (int i = 0; i < n; i++) {
+        rd(&sizes[i], 8);
+        bufs[i].resize(sizes[i] + 1);
+        rd(bufs[i].data(), sizes[i]);
+        ptrs[i] = bufs[i].data();
+        tot += sizes[i];
+      }
+      std::vector<uint8_t> out(tot + 64);
+      int64_t sz = ref_posdb_merge(ptrs.data(), sizes.data(), n, rm, mrs, out.data(), tot + 64);
+      wr(&sz, 8);
+      if (sz > 0) wr(out.data(), sz);
+    } else {
+      return 5;
+    }
+    fflush(stdout);
+  }
+  return 0;
+}

@@ -1,0 +1,101 @@
+"""Regenerates tests/golden/ from the REFERENCE itself (oracle/_ref/gbref,
+built by `make -f oracle/ref.mk` from the unmodified /root/reference sources).
+
+    python tests/make_golden.py
+
+Each fixture is data only (numpy .npz, no pickles): the inputs (posdb lists,
+query plan, Msg39Request scalars; or merge runs) and what the reference's own
+PosdbTable::intersectLists10_r / TopTree / RdbList::merge_r produced for them
+(top-k docids, score bit patterns, hit count, the docid vote buffer; merged
+bytes).  tests/test_golden.py checks the oracle and the GPU path against them.
+"""
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), "open-source-search-engine_amd", "python"))
+sys.path.insert(0, HERE)
+
+import qkinds  # noqa: E402
+import ref_binding as ref  # noqa: E402
+from mergegen import tiered_runs  # noqa: E402
+from workload import generate  # noqa: E402
+
+OUT = os.path.join(HERE, "golden")
+QFIELDS = ["is_required", "term_sign", "field_code", "piped", "synonym_of", "left_phrase_term",
+           "right_phrase_term", "is_wiki_half_stop_bigram", "qpos", "wiki_phrase_id", "quote_start"]
+
+
+def pack_lists(lists):
+    sizes = np.array([len(l) for l in lists], np.int64)
+    blob = np.frombuffer(b"".join(lists), np.uint8) if sizes.sum() else np.zeros(0, np.uint8)
+    return sizes, blob
+
+
+def save_query(name, terms, lists, params):
+    r = ref.query(terms, lists, params, votes=True)
+    sizes, blob = pack_lists(lists)
+    qt = np.array([[getattr(t, f) for f in QFIELDS] for t in terms], np.int32).reshape(len(terms), len(QFIELDS))
+    tfw = np.array([t.tf_weight for t in terms], np.float32)
+    pr = np.array([params.docs_to_get, params.real_max_top, params.language, params.site_clustering,
+                   params.num_docid_splits], np.int32)
+    np.savez_compressed(os.path.join(OUT, f"q_{name}.npz"), qterms=qt, tfw=tfw, params=pr,
+                        same_lang_weight=np.float32(params.same_lang_weight), list_sizes=sizes, list_blob=blob,
+                        docids=r["docids"], score_bits=r["scores"].view(np.uint32), hits=np.int64(r["hits"]),
+                        docs_wanted=np.int32(r["docs_wanted"]), votes=r["votes"])
+    return r
+
+
+def save_merge(name, runs, cases):
+    sizes, blob = pack_lists(runs)
+    outs, osz, rms, mrss = [], [], [], []
+    for rm, mrs in cases:
+        o = ref.posdb_merge(runs, rm, mrs)
+        outs.append(o)
+        osz.append(len(o))
+        rms.append(rm)
+        mrss.append(mrs)
+    np.savez_compressed(os.path.join(OUT, f"m_{name}.npz"), run_sizes=sizes, run_blob=blob,
+                        remove_neg=np.array(rms, np.int32), min_rec_sizes=np.array(mrss, np.int64),
+                        out_sizes=np.array(osz, np.int64),
+                        out_blob=np.frombuffer(b"".join(outs), np.uint8))
+
+
+def main():
+    if not ref.available():
+        sys.exit("oracle/_ref/gbref missing: run `make -f oracle/ref.mk` where /root/reference exists")
+    os.makedirs(OUT, exist_ok=True)
+    N = 6000
+    for seed in (1, 2):
+        for q in qkinds.kinds(N, seed=seed):
+            lists = generate(q, N, seed=2000 + seed)
+            r = save_query(f"{q.name}_s{seed}", q.terms, lists, q.params())
+            print(f"q_{q.name}_s{seed}: hits={r['hits']} n={len(r['docids'])}")
+    # request-parameter variants (realMaxTop, language, docsToGet floor of 30)
+    q = qkinds.kinds(N, seed=4)[2]
+    lists = generate(q, N, seed=77)
+    for dtg, rmt, lang in ((10, 10, 0), (300, 3, 1), (1, 1, 7)):
+        q.docs_to_get = dtg
+        save_query(f"params_{dtg}_{rmt}_{lang}", q.terms, lists, q.params(real_max_top=rmt, language=lang))
+    # empty and partially empty term lists
+    q = qkinds.kinds(N, seed=1)[0]
+    lists = generate(q, N)
+    save_query("empty_bigram", q.terms, [lists[0], lists[1], b""], q.params())
+    # NOT [lists[0], b"", lists[2]]: the second word's group then holds only
+    # BF_BIGRAM keys, some docids mini-merge to an empty list, and the
+    # reference scores stale stack bytes of mbuf (Posdb.cpp:6007, 6687-6692;
+    # undefined behaviour, DESIGN.md "Known divergences")
+    save_query("empty_all", q.terms, [b"", b"", b""], q.params())
+    save_query("empty_required", q.terms, [lists[0], b"", b""], q.params())
+    cases = [(0, -1), (1, -1), (0, 5000), (1, 5000), (0, 1)]
+    for seed, (keys, nterms) in enumerate([(4000, 50), (12000, 3), (8000, 1)]):
+        save_merge(f"tiered_s{seed}", tiered_runs(keys, seed=seed, nterms=nterms), cases)
+    save_merge("two_runs", tiered_runs(3000, nruns=2, seed=9, dup_frac=0.3, neg_frac=0.2), cases)
+    total = sum(os.path.getsize(os.path.join(OUT, f)) for f in os.listdir(OUT))
+    print(f"{len(os.listdir(OUT))} fixtures, {total / 1e6:.2f} MB")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,95 @@
+"""Golden vectors produced by the REFERENCE's own PosdbTable / TopTree /
+RdbList::merge_r (tests/make_golden.py, oracle/_ref/gbref).
+
+CPU tests pin the oracle (oracle/posdb_oracle.c, posdb_merge_oracle.c) to the
+reference; GPU tests check the HIP path against the same vectors through the
+C ABI.  Bar: docid sets and top-k order bit-exact, scores bit-exact (the
+north_star tolerance 1e-5 relative is asserted too)."""
+import ctypes
+import glob
+import os
+
+import numpy as np
+import pytest
+
+import gbgpu
+import oracle_binding as orc
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+QCASES = sorted(glob.glob(os.path.join(HERE, "golden", "q_*.npz")))
+MCASES = sorted(glob.glob(os.path.join(HERE, "golden", "m_*.npz")))
+REL_TOL = 1e-5
+
+
+def split_blob(sizes, blob):
+    out, off = [], 0
+    for s in sizes:
+        out.append(blob[off:off + s].tobytes())
+        off += s
+    return out
+
+
+def load_query(path):
+    z = np.load(path, allow_pickle=False)
+    terms = [gbgpu.QTerm(*[int(x) for x in row], float(w)) for row, w in zip(z["qterms"], z["tfw"])]
+    pr = z["params"]
+    params = gbgpu.Params(int(pr[0]), int(pr[1]), int(pr[2]), int(pr[3]), int(pr[4]), float(z["same_lang_weight"]))
+    lists = split_blob(z["list_sizes"], z["list_blob"])
+    exp = dict(docids=z["docids"], scores=z["score_bits"].view(np.float32), hits=int(z["hits"]),
+               docs_wanted=int(z["docs_wanted"]), votes=z["votes"])
+    return terms, lists, params, exp
+
+
+def check(got, exp, label):
+    assert got["hits"] == exp["hits"], label
+    assert got["docs_wanted"] == exp["docs_wanted"], label
+    assert np.array_equal(got["docids"], exp["docids"]), label
+    g = np.asarray(got["scores"], np.float32)
+    rel = np.abs(g.astype(np.float64) - exp["scores"]) / np.maximum(1e-30, np.abs(exp["scores"]))
+    assert np.all(rel <= REL_TOL), (label, rel.max() if len(rel) else 0)
+    assert np.array_equal(g.view(np.uint32), exp["scores"].view(np.uint32)), label
+
+
+def orc_merge(lists, rm, mrs):
+    keep, ptrs, sizes = orc._lists(lists)
+    cap = sum(map(len, lists)) + 64
+    out = ctypes.create_string_buffer(cap)
+    n = orc.lib().orc_posdb_merge(ptrs, sizes, len(lists), rm, mrs, out, cap)
+    assert n >= 0, n
+    return out.raw[:n]
+
+
+def test_fixtures_present():
+    assert len(QCASES) >= 30 and len(MCASES) >= 4
+
+
+@pytest.mark.parametrize("path", QCASES, ids=[os.path.basename(p)[2:-4] for p in QCASES])
+def test_oracle_query_vs_reference(path):
+    terms, lists, params, exp = load_query(path)
+    got = orc.query(terms, lists, params)
+    check(got, exp, os.path.basename(path))
+
+
+@pytest.mark.parametrize("path", QCASES, ids=[os.path.basename(p)[2:-4] for p in QCASES])
+def test_oracle_intersection_vs_reference(path):
+    terms, lists, params, exp = load_query(path)
+    # m_docIdVoteBuf after intersectLists10_r: the exact intersected docid set
+    assert np.array_equal(orc.intersect(terms, lists), exp["votes"])
+
+
+@pytest.mark.parametrize("path", MCASES, ids=[os.path.basename(p)[2:-4] for p in MCASES])
+def test_oracle_merge_vs_reference(path):
+    z = np.load(path, allow_pickle=False)
+    runs = split_blob(z["run_sizes"], z["run_blob"])
+    outs = split_blob(z["out_sizes"], z["out_blob"])
+    for rm, mrs, want in zip(z["remove_neg"], z["min_rec_sizes"], outs):
+        assert orc_merge(runs, int(rm), int(mrs)) == want, (int(rm), int(mrs))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("path", QCASES, ids=[os.path.basename(p)[2:-4] for p in QCASES])
+def test_gpu_query_vs_reference(engine, path):
+    terms, lists, params, exp = load_query(path)
+    r = engine.query(terms, lists, params)
+    check(dict(docids=r.docids, scores=r.scores, hits=r.hits, docs_wanted=r.docs_wanted), exp,
+          os.path.basename(path))
