@@ -113,9 +113,9 @@ int gbgpu_query_resident_enqueue(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int n
 int gbgpu_query_collect(gbgpu_ctx *ctx, gbgpu_result *out);
 /* the context's HIP stream (hipStream_t), for callers that order work on it */
 void *gbgpu_stream(gbgpu_ctx *ctx);
-/* device copy of the last query's top tree as 16-byte records
- * {uint32 score_bits, uint32 valid, int64 docid} (the Msg39Reply payload for an
- * RCCL allgather); returns count via *n after gbgpu_query_collect. */
+/* device copy of the last query's top list (the Msg39Reply payload for an RCCL
+ * allgather): *n uint32 order-preserving score keys (0 = empty slot), then at
+ * the next 256-byte boundary *n int64 docids.  Valid after gbgpu_query_collect. */
 int gbgpu_last_topk_device(gbgpu_ctx *ctx, void **dev_ptr, int32_t *n);
 
 /* Msg3a::mergeLists (Msg3a.cpp:1315-1467) without site clustering: k-way merge

@@ -2,32 +2,36 @@
 // and the C-ABI around them (include/gbgpu.h).
 //
 // Per query, with every list resident in HBM (first key swapped to 12 bytes
-// at upload, Posdb.cpp:5671-5703), the stream runs:
+// at upload, Posdb.cpp:5671-5703), ONE host->device copy of the query tables
+// is followed by these launches on the context's stream:
 //
+//   k_reset            zero the per-query counters and top-k select state
 //   k_count_runs / k_scan_runs / k_write_runs
 //        candidate docids = run starts of the sublists of the smallest group
 //        (addDocIdVotes group 0, Posdb.cpp:5178-5332), one sorted array per
-//        sublist; sublist 0's own locations and group bits are recorded here.
+//        sublist; array 0's own run locations are recorded here.
 //   k_probe
-//        merge-path scan of every other list (and the remaining smallest-group
-//        sublists): each block owns a contiguous span of one list, stages
-//        12 KiB chunks in LDS, classifies every 6-byte unit by the alignment
-//        bit, and matches each docid run against a sliding LDS window of the
-//        candidate array (addDocIdVotes g>0 / rmDocIdVotes, Posdb.cpp:5086-
-//        5171, 4871-4946).  Matches OR the list's group bits into the
-//        candidate's mask and record the run location.
+//        merge-path scan of every other list: each block owns a contiguous
+//        span of one list, classifies every 6-byte unit of a 12 KiB chunk by
+//        the alignment bit, compacts the run starts in LDS and lets the
+//        chunk's candidates binary-search them (addDocIdVotes g>0 /
+//        rmDocIdVotes, Posdb.cpp:5086-5171, 4871-4946).  A hit sets the
+//        list's bit in the candidate's list mask and records (unit, length)
+//        of the docid's run.
 //   k_compact
-//        survivors = candidates holding every positive group bit and no
-//        negative bit (the final m_docIdVoteBuf); per-list "shrunk sublist is
-//        non-empty" flags (shrinkSubLists, Posdb.cpp:5334-5428).
+//        survivors = candidates whose lists cover every positive group and
+//        no negative one (the final m_docIdVoteBuf), plus the shrunk-sublist
+//        non-empty flags (shrinkSubLists, Posdb.cpp:5334-5428).
 //   k_score
 //        one lane per survivor: mini-merge (Posdb.cpp:6559-6778) into scratch
 //        records, then the scorers of scoring.h.
-//   k_topk_tile (x stages)
-//        LDS bitonic selection replacing TopTree (score desc, docid asc).
+//   k_select_hist x3 / k_select_gather / k_select_final
+//        radix select of the k best (score desc, docid asc) replacing TopTree
+//        (TopTree.cpp:195-516), then one small LDS sort.
 //
-// No host synchronisation happens between kernels: counts live in device
-// memory and grids are sized from host-known upper bounds.
+// ONE device->host copy returns counters + top list.  No host
+// synchronisation happens between kernels: counts live in device memory and
+// grids are sized from host-known upper bounds.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -52,8 +56,10 @@ constexpr int CHUNK_UNITS = BLOCK * UPT;         // 2048 units = 12 KiB per chun
 constexpr int CHUNK_BYTES = CHUNK_UNITS * 6;
 constexpr int CHUNK_LOAD = CHUNK_BYTES + 16;     // + the tail of a 12-byte key
 constexpr int CHUNKS_PER_PROBE_BLOCK = 8;        // merge-path span of one block
-constexpr int WIN = 256;                         // candidate window (LDS)
-constexpr int TILE = 2048;                       // top-k tile
+constexpr int MAX_RUNS = CHUNK_UNITS / 2;        // a run is >= 2 units
+constexpr int TILE = 2048;                       // final top-k sort capacity
+constexpr int MAX_K = 1536;                      // TILE - MAX_K ties merged per round
+constexpr int SEL_BINS = 4096;                   // radix-select bins per pass
 constexpr int LIST_PAD = CHUNK_LOAD + 128;
 
 struct Counters {
@@ -61,8 +67,24 @@ struct Counters {
   uint32_t corrupt;
   unsigned long long scratch_top;
   uint32_t g0count[MAXG0];
-  uint32_t anysurv[MAXL];
-  uint32_t topk_n[8];
+  uint32_t anysurv;  // bit l: list l has a run in some survivor
+  uint32_t pad[5];
+};
+
+// radix-select state (3 passes over the 32-bit score keys: 12+12+8 bits)
+struct Select {
+  uint32_t hist[3][SEL_BINS];
+  uint32_t ticket[3];
+  uint32_t prefix;  // selected key prefix so far
+  uint32_t need;    // entries still to take inside the selected prefix
+  uint32_t all;     // fewer valid entries than k: take them all
+  uint32_t thr;     // final threshold key T
+  uint32_t na, nb;  // gathered: keys > T, keys == T
+};
+
+// where a docid's run sits in one list: first unit and length in units
+struct Loc {
+  uint32_t unit, len;
 };
 
 struct G0Chunk {
@@ -152,6 +174,22 @@ __device__ uint32_t block_lower_bound(const uint64_t *a, uint32_t n, uint64_t ke
   return lo;
 }
 
+
+// first run start at or after unit e (the end of the run before it); the
+// continuation units of a run are the second half of its 12-byte key and
+// its 6-byte keys, none of which classify as a run start (Posdb.h:887-889)
+__device__ __forceinline__ uint32_t run_end(const DevList &L, uint32_t e) {
+  while (e < L.units && !gb_unit_is_run_start(L.p + (size_t)e * 6)) e++;
+  return e;
+}
+
+__global__ void k_reset(uint32_t *a, uint32_t na, uint32_t *b, uint32_t nb) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < na + nb; i += gridDim.x * blockDim.x) {
+    if (i < na) a[i] = 0;
+    else b[i - na] = 0;
+  }
+}
+
 // ----------------------------------------------- candidate extraction (G0)
 __global__ void __launch_bounds__(BLOCK) k_count_runs(const DevPlan *pl, const G0Chunk *chunks,
                                                       uint32_t *chunk_count) {
@@ -167,21 +205,17 @@ __global__ void __launch_bounds__(BLOCK) k_count_runs(const DevPlan *pl, const G
   if (threadIdx.x == 0) chunk_count[blockIdx.x] = tot;
 }
 
-// exclusive scan of per-chunk counts, per candidate array (single block)
-__global__ void __launch_bounds__(1024) k_scan_runs(const G0Chunk *chunks, uint32_t nchunks,
-                                                    uint32_t *chunk_count, Counters *ctr) {
+// exclusive scan of the per-chunk counts (single block); k_write_runs
+// subtracts the prefix at each array's first chunk
+__global__ void __launch_bounds__(1024) k_scan_runs(uint32_t nchunks, uint32_t *chunk_count) {
   __shared__ uint32_t tmp[16];
   __shared__ uint32_t carry;
-  __shared__ uint32_t carry_array;
-  if (threadIdx.x == 0) { carry = 0; carry_array = 0; }
+  if (threadIdx.x == 0) carry = 0;
   __syncthreads();
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   for (uint32_t base = 0; base < nchunks; base += 1024) {
-    uint32_t i = base + threadIdx.x;
-    uint32_t v = i < nchunks ? chunk_count[i] : 0;
-    uint32_t arr = i < nchunks ? chunks[i].array : 0xffffffffu;
-    // segmented by array: chunks are grouped by array in order; handle the
-    // segment start by subtracting the array's running base on the host side
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t i = base + threadIdx.x;
+    const uint32_t v = i < nchunks ? chunk_count[i] : 0;
     uint32_t x = v;
     for (int o = 1; o < 64; o <<= 1) {
       uint32_t y = __shfl_up(x, o, 64);
@@ -191,53 +225,67 @@ __global__ void __launch_bounds__(1024) k_scan_runs(const G0Chunk *chunks, uint3
     __syncthreads();
     uint32_t pre = 0;
     for (int w = 0; w < wid; w++) pre += tmp[w];
-    uint32_t incl = carry + pre + x;
+    const uint32_t incl = carry + pre + x;
     __syncthreads();
-    if (i < nchunks) chunk_count[i] = incl - v;  // global exclusive prefix
+    if (i < nchunks) chunk_count[i] = incl - v;
     if (threadIdx.x == 1023) carry = incl;
-    (void)arr;
     __syncthreads();
   }
-  (void)carry_array;
-  (void)ctr;
 }
 
+// Writes every candidate slot of every array (docid; list mask = the array's
+// own list bit for array 0, which is never probed, else 0 -- so no per-query
+// clear of the mask is needed) and array 0's run locations.
 __global__ void __launch_bounds__(BLOCK) k_write_runs(const DevPlan *pl, const G0Chunk *chunks,
                                                       const uint32_t *chunk_off,
                                                       const uint32_t *array_first_chunk,
-                                                      uint64_t *cand, uint32_t *mask, uint32_t *loc,
+                                                      uint64_t *cand, uint32_t *lmask, Loc *loc,
                                                       uint64_t slot_ub, Counters *ctr,
                                                       uint32_t nchunks) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[CHUNK_LOAD];
   __shared__ uint32_t tmp[BLOCK / 64];
+  __shared__ uint16_t rs_unit[MAX_RUNS];
   const G0Chunk c = chunks[blockIdx.x];
   const int lid = pl->g0list[c.array];
   const DevList &L = pl->lists[lid];
   load_chunk(L.p, c.u0, lds);
   __syncthreads();
-  uint32_t m = thread_starts(lds, c.u0, L.units);
+  const uint32_t m0 = thread_starts(lds, c.u0, L.units);
   uint32_t tot;
-  uint32_t ex = block_exclusive_scan(__popc(m), tmp, &tot);
+  const uint32_t ex = block_exclusive_scan(__popc(m0), tmp, &tot);
+  uint32_t m = m0, o = ex;
+  while (m) {
+    const int q = __ffs(m) - 1;
+    m &= m - 1;
+    rs_unit[o++] = (uint16_t)(threadIdx.x * UPT + q);
+  }
+  __syncthreads();
   // offset inside this array = global prefix - prefix at the array's first chunk
   const uint32_t arr_base_off = chunk_off[array_first_chunk[c.array]];
   uint32_t pos = chunk_off[blockIdx.x] - arr_base_off + ex;
   const uint64_t base = pl->g0base[c.array];
-  const bool own = (c.array == 0);  // array 0 is never probed: record it here
+  const bool own = (c.array == 0);
+  const uint32_t own_bit = 1u << lid;
+  Loc *loc_l = loc + (uint64_t)lid * slot_ub;
+  m = m0;
+  o = ex;
   while (m) {
-    int q = __ffs(m) - 1;
+    const int q = __ffs(m) - 1;
     m &= m - 1;
-    uint32_t lu = threadIdx.x * UPT + q;
-    uint64_t d = unit_docid(lds + lu * 6);
-    uint64_t slot = base + pos;
-    cand[slot] = d;
+    const uint32_t lu = threadIdx.x * UPT + q;
+    const uint64_t slot = base + pos;
+    cand[slot] = unit_docid(lds + lu * 6);
+    lmask[slot] = own ? own_bit : 0u;
     if (own) {
-      loc[(uint64_t)lid * slot_ub + slot] = c.u0 + lu;
-      mask[slot] = L.group_bits;
+      const uint32_t u = c.u0 + lu;
+      const uint32_t e = (o + 1 < tot) ? c.u0 + rs_unit[o + 1] : run_end(L, u + 2);
+      loc_l[slot] = Loc{u, e - u};
     }
     pos++;
+    o++;
   }
   // the last chunk of each array publishes the array's count
-  bool last = (blockIdx.x + 1 == nchunks) || (chunks[blockIdx.x + 1].array != c.array);
+  const bool last = (blockIdx.x + 1 == nchunks) || (chunks[blockIdx.x + 1].array != c.array);
   if (last && threadIdx.x == 0) ctr->g0count[c.array] = chunk_off[blockIdx.x] - arr_base_off + tot;
 }
 
@@ -273,202 +321,179 @@ __device__ __forceinline__ uint64_t regs_docid(const UnitRegs &r, int q) {
   return d >> 2;
 }
 
-__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+// Register-prefetched chunk copy: each thread holds 48 bytes of the next
+// chunk (3 x uint4) while the block works on the current one, so the HBM
+// latency of chunk i+1 overlaps the search of chunk i.  The 16-byte tail
+// (the docid bytes of a 12-byte key starting at the last unit) is one extra
+// uint4 that thread 0 carries.
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+struct ChunkRegs {
+  v4u v[3];
+  v4u tail;
+};
+__device__ __forceinline__ void chunk_fetch(const uint8_t *list, uint32_t u0, ChunkRegs &r) {
+  const v4u *src = reinterpret_cast<const v4u *>(list + (size_t)u0 * 6);
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    uint64_t y = __shfl_xor(v, o, 64);
-    v = y < v ? y : v;
-  }
-  return v;
+  for (int i = 0; i < 3; i++) r.v[i] = __builtin_nontemporal_load(src + threadIdx.x + i * BLOCK);
+  if (threadIdx.x == 0) r.tail = src[3 * BLOCK];
 }
-__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+__device__ __forceinline__ void chunk_store(uint8_t *lds, const ChunkRegs &r) {
+  v4u *dst = reinterpret_cast<v4u *>(lds);
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    uint64_t y = __shfl_xor(v, o, 64);
-    v = y > v ? y : v;
-  }
-  return v;
+  for (int i = 0; i < 3; i++) dst[threadIdx.x + i * BLOCK] = r.v[i];
+  if (threadIdx.x == 0) dst[3 * BLOCK] = r.tail;
 }
 
-// MODE (diagnostic builds only, GBGPU_PROBE_MODE): 0 full, 1 stop after the
-// unit classification, 2 stop after staging the chunk in LDS.
+
+// k_probe -- addDocIdVotes for groups g>0 and rmDocIdVotes (Posdb.cpp:5086-
+// 5171, 4871-4946), all lists in one launch.  A block owns a contiguous span
+// of one list.  Per 12 KiB chunk:
+//   1. classify the 2048 units (Posdb.h:887-889) from registers and compact
+//      the run starts (sorted docids + unit offsets) into LDS with one block
+//      scan;
+//   2. per candidate array k (the smallest group's sublists, in sublist
+//      order), the candidates in [first docid, last docid] of the chunk --
+//      a contiguous slice continuing where the previous chunk stopped --
+//      each binary-search the chunk's run starts.  A run is credited to the
+//      first array holding its docid only (claim flag), which is how the
+//      k-way union of addDocIdVotes' group 0 keeps each docid once.
+//   A hit records the run's (unit, length) in loc[list][slot] and sets the
+//   list's bit in the slot's list mask.
+// MODE (diagnostic, GBGPU_PROBE_MODE): 0 full, 2 stage chunks only.
 template <int MODE>
 __global__ void __launch_bounds__(BLOCK) k_probe(const DevPlan *pl, const ProbeWork *work,
-                                                 const uint64_t *cand, uint32_t *mask, uint32_t *loc,
+                                                 const uint64_t *cand, uint32_t *lmask, Loc *loc,
                                                  uint64_t slot_ub, const Counters *ctr) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[CHUNK_LOAD + 32];
-  __shared__ uint64_t win[WIN];
+  __shared__ uint64_t rs_doc[MAX_RUNS];
+  __shared__ uint16_t rs_unit[MAX_RUNS];
+  __shared__ uint8_t rs_claim[MAX_RUNS];
   __shared__ uint32_t s_lo[MAXG0];
-  __shared__ uint64_t s_red[2][BLOCK / 64];
+  __shared__ uint32_t tmp[BLOCK / 64];
   const ProbeWork w = work[blockIdx.x];
   const DevList &L = pl->lists[w.list];
-  const uint32_t bits = L.group_bits;
+  const uint32_t bit = 1u << w.list;
   const int g0n = pl->g0n;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  Loc *loc_l = loc + (uint64_t)w.list * slot_ub;
   bool first_chunk = true;
+  ChunkRegs cr;
+  chunk_fetch(L.p, w.u0, cr);
   for (uint32_t u0 = w.u0; u0 < w.u1; u0 += CHUNK_UNITS) {
-    load_chunk(L.p, u0, lds);
+    chunk_store(lds, cr);
     __syncthreads();
+    if (u0 + CHUNK_UNITS < w.u1) chunk_fetch(L.p, u0 + CHUNK_UNITS, cr);
     if (MODE == 2) {
-      if (lds[threadIdx.x * 48] == 0xee && lds[threadIdx.x * 48 + 1] == 0x77) mask[0] = 1;
+      if (lds[threadIdx.x * 48] == 0xee && lds[threadIdx.x * 48 + 1] == 0x77 && lds[threadIdx.x * 48 + 2] == 0x55)
+        lmask[0] = 1;
       __syncthreads();
       continue;
     }
     UnitRegs r;
     load_units(lds, r);
     uint32_t starts = 0;
-    uint64_t dk[UPT];
-    uint64_t tmin = ~0ull, tmax = 0;
 #pragma unroll
     for (int q = 0; q < UPT; q++) {
       const uint32_t gu = u0 + threadIdx.x * UPT + q;
-      const bool st = gu < w.u1 && (r.byte(6 * q + 1) & 0x02) && !(r.byte(6 * q) & 0x04);
-      dk[q] = st ? regs_docid(r, q) : 0;
-      if (st) {
-        starts |= 1u << q;
-        tmin = dk[q] < tmin ? dk[q] : tmin;
-        tmax = dk[q] > tmax ? dk[q] : tmax;
-      }
+      if (gu < w.u1 && (r.byte(6 * q + 1) & 0x02) && !(r.byte(6 * q) & 0x04)) starts |= 1u << q;
     }
-    tmin = wave_min_u64(tmin);
-    tmax = wave_max_u64(tmax);
-    if (lane == 0) {
-      s_red[0][wid] = tmin;
-      s_red[1][wid] = tmax;
+    uint32_t nrun;
+    uint32_t o = block_exclusive_scan(__popc(starts), tmp, &nrun);
+#pragma unroll
+    for (int q = 0; q < UPT; q++) {
+      if (!(starts >> q & 1)) continue;
+      rs_doc[o] = regs_docid(r, q);
+      rs_unit[o] = (uint16_t)(threadIdx.x * UPT + q);
+      rs_claim[o] = 0;
+      o++;
     }
     __syncthreads();
-    uint64_t dmin = s_red[0][0], dmax = s_red[1][0];
-#pragma unroll
-    for (int i = 1; i < BLOCK / 64; i++) {
-      dmin = s_red[0][i] < dmin ? s_red[0][i] : dmin;
-      dmax = s_red[1][i] > dmax ? s_red[1][i] : dmax;
-    }
-    if (dmin == ~0ull || MODE == 1) {  // no run starts in this chunk
-      if (MODE == 1 && dk[0] == 0x123456789ull) mask[0] = 1;
-      __syncthreads();
-      continue;
-    }
-    uint32_t found = 0;
+    if (nrun == 0) continue;  // uniform: every thread saw the same total
+    const uint64_t dmin = rs_doc[0], dmax = rs_doc[nrun - 1];
     for (int k = 0; k < g0n; k++) {
       const uint32_t nk = ctr->g0count[k];
       const uint64_t *ck = cand + pl->g0base[k];
+      uint32_t lo;
       if (first_chunk) {
-        uint32_t lo0 = block_lower_bound(ck, nk, dmin);
-        if (threadIdx.x == 0) s_lo[k] = lo0;
-        __syncthreads();
-      }
-      const uint32_t lo = s_lo[k];
-      const uint32_t wc = (nk > lo) ? min((uint32_t)WIN, nk - lo) : 0u;
-      if (threadIdx.x < wc) win[threadIdx.x] = ck[lo + threadIdx.x];
-      __syncthreads();
-      const bool covered = (lo + wc >= nk) || (win[wc - 1] >= dmax);
-      uint32_t hi;  // one past the last candidate <= dmax
-      if (covered) {
-        uint32_t a = 0, b = wc;
-        while (a < b) {
-          uint32_t mid = (a + b) >> 1;
-          if (win[mid] <= dmax) a = mid + 1;
-          else b = mid;
-        }
-        hi = lo + a;
+        lo = block_lower_bound(ck, nk, dmin);
       } else {
-        hi = lo + block_lower_bound(ck + lo, nk - lo, dmax + 1);
+        lo = s_lo[k];
       }
-#pragma unroll
-      for (int q = 0; q < UPT; q++) {
-        if (!((starts & ~found) >> q & 1)) continue;
-        const uint64_t d = dk[q];
-        uint32_t a, b;
-        bool hit;
-        if (covered) {
-          a = 0;
-          b = hi - lo;
+      for (;;) {
+        const uint32_t idx = lo + threadIdx.x;
+        const uint64_t d = idx < nk ? ck[idx] : ~0ull;
+        const bool in = d <= dmax;
+        if (in) {
+          uint32_t a = 0, b = nrun;
           while (a < b) {
-            uint32_t mid = (a + b) >> 1;
-            if (win[mid] < d) a = mid + 1;
+            const uint32_t mid = (a + b) >> 1;
+            if (rs_doc[mid] < d) a = mid + 1;
             else b = mid;
           }
-          hit = (a < hi - lo) && win[a] == d;
-        } else {
-          a = lo;
-          b = hi;
-          while (a < b) {
-            uint32_t mid = (a + b) >> 1;
-            if (ck[mid] < d) a = mid + 1;
-            else b = mid;
+          if (a < nrun && rs_doc[a] == d && !rs_claim[a]) {
+            rs_claim[a] = 1;
+            const uint64_t slot = pl->g0base[k] + idx;
+            const uint32_t u = u0 + rs_unit[a];
+            const uint32_t e = (a + 1 < nrun) ? u0 + rs_unit[a + 1] : run_end(L, u + 2);
+            loc_l[slot] = Loc{u, e - u};
+            atomicOr(&lmask[slot], bit);
           }
-          hit = (a < hi) && ck[a] == d;
-          a -= lo;
         }
-        if (hit) {
-          const uint64_t slot = pl->g0base[k] + lo + a;
-          found |= 1u << q;
-          loc[(uint64_t)w.list * slot_ub + slot] = u0 + threadIdx.x * UPT + q;
-          atomicOr(&mask[slot], bits);
-        }
+        const uint32_t nin = (uint32_t)__syncthreads_count(in);
+        lo += nin;
+        if (nin < (uint32_t)BLOCK) break;
       }
-      __syncthreads();
-      if (threadIdx.x == 0) s_lo[k] = hi;  // next chunk's docids are > dmax
-      __syncthreads();
+      if (threadIdx.x == 0) s_lo[k] = lo;
     }
     first_chunk = false;
+    __syncthreads();
   }
 }
 
 // ------------------------------------------------------------- compaction
-__device__ __forceinline__ uint32_t run_units(const uint8_t *p, uint32_t units, uint32_t u) {
-  // a docid run: 12-byte key (2 units) then 6-byte keys (Posdb.cpp:5141-5145)
-  uint32_t e = u + 2;
-  while (e < units && (p[(size_t)e * 6] & 0x04)) e++;
-  return e - u;
-}
-
-__device__ __forceinline__ bool valid_run(const DevList &L, uint32_t u, uint64_t docid) {
-  if (u >= L.units) return false;
-  const uint8_t *k = L.p + (size_t)u * 6;
-  if (!((k[1] & 0x02) && !(k[0] & 0x04))) return false;
-  if (u + 1 >= L.units) return false;
-  return unit_docid(k) == docid;
-}
-
 constexpr int CSPT = 16;                        // compaction slots per thread
 constexpr int CTILE = BLOCK * CSPT;              // 4096 slots per block
 
-// Survivors of one contiguous tile of candidate slots, appended with ONE
-// pair of atomics per block (a single device counter cannot take one atomic
-// per wave: MI355X_MICROARCH.md "dequeue" row, ~88 per us per word).
-__global__ void __launch_bounds__(BLOCK) k_compact(const DevPlan *pl, const uint64_t *cand,
-                                                   const uint32_t *mask, const uint32_t *loc,
+// Survivors of one contiguous tile of candidate slots (slot = tile base +
+// q*BLOCK + thread: coalesced), appended with ONE pair of atomics per block
+// (a single device counter cannot take one atomic per wave:
+// MI355X_MICROARCH.md "dequeue" row, ~88 per us per word).  A slot's groups
+// are the union of its lists' group bits; its mini-merge arena size is the
+// sum of its runs' lengths (every group instance of a list counts, as the
+// reference merges a shared bigram sublist into both groups).  The shrunk-
+// sublist-non-empty flags (shrinkSubLists, Posdb.cpp:5334-5428) are a list
+// bitmask OR-reduced in the block and published with one atomic.
+__global__ void __launch_bounds__(BLOCK) k_compact(const DevPlan *pl, const uint32_t *lmask, const Loc *loc,
                                                    uint64_t slot_ub, Counters *ctr, uint32_t *surv,
                                                    unsigned long long *surv_off) {
   __shared__ uint32_t tmp[BLOCK / 64];
   __shared__ uint32_t s_base_i;
+  __shared__ uint32_t s_any;
   __shared__ unsigned long long s_base_u;
   const uint32_t pos = pl->pos_mask;
-  const uint64_t s0 = (uint64_t)blockIdx.x * CTILE + (uint64_t)threadIdx.x * CSPT;
-  uint32_t okm = 0, nok = 0, utot = 0;
+  const uint64_t s0 = (uint64_t)blockIdx.x * CTILE + threadIdx.x;
+  if (threadIdx.x == 0) s_any = 0;
+  uint32_t okm = 0, nok = 0, utot = 0, any = 0;
   uint32_t units[CSPT];
 #pragma unroll
   for (int q = 0; q < CSPT; q++) {
-    const uint64_t s = s0 + q;
+    const uint64_t s = s0 + (uint64_t)q * BLOCK;
     units[q] = 0;
     if (s >= slot_ub) continue;
     int k = 0;
     while (k + 1 < pl->g0n && s >= pl->g0base[k + 1]) k++;
     if (s - pl->g0base[k] >= ctr->g0count[k]) continue;
-    const uint32_t m = mask[s];
-    if (!(((m & pos) == pos) && !(m & NEG_BIT))) continue;
-    const uint64_t d = cand[s];
+    const uint32_t lm = lmask[s];
+    uint32_t gm = 0;
+    for (uint32_t x = lm; x; x &= x - 1) gm |= pl->lists[__ffs(x) - 1].group_bits;
+    if (!(((gm & pos) == pos) && !(gm & NEG_BIT))) continue;
     uint32_t u_s = 0;
     for (int j = 0; j < pl->ngroups; j++) {
       if (pl->gflags0[j] & BF_NEGATIVE) continue;
       for (int x = 0; x < pl->gnsub[j]; x++) {
         const int lid = pl->gsub[j][x];
-        const DevList &L = pl->lists[lid];
-        const uint32_t u = loc[(uint64_t)lid * slot_ub + s];
-        if (!valid_run(L, u, d)) continue;
-        u_s += run_units(L.p, L.units, u);
-        if (!ctr->anysurv[lid]) atomicOr((uint32_t *)&ctr->anysurv[lid], 1u);
+        if (!(lm >> lid & 1)) continue;
+        u_s += loc[(uint64_t)lid * slot_ub + s].len;
+        any |= 1u << lid;
       }
     }
     units[q] = u_s;
@@ -479,9 +504,12 @@ __global__ void __launch_bounds__(BLOCK) k_compact(const DevPlan *pl, const uint
   uint32_t tot_n, tot_u;
   const uint32_t ex_n = block_exclusive_scan(nok, tmp, &tot_n);
   const uint32_t ex_u = block_exclusive_scan(utot, tmp, &tot_u);
+  if (any) atomicOr(&s_any, any);
+  __syncthreads();
   if (threadIdx.x == 0) {
     s_base_i = tot_n ? atomicAdd(&ctr->nsurv, tot_n) : 0;
     s_base_u = tot_n ? atomicAdd(&ctr->scratch_top, (unsigned long long)tot_u) : 0;
+    if (s_any) atomicOr(&ctr->anysurv, s_any);
   }
   __syncthreads();
   uint32_t i = s_base_i + ex_n;
@@ -489,7 +517,7 @@ __global__ void __launch_bounds__(BLOCK) k_compact(const DevPlan *pl, const uint
 #pragma unroll
   for (int q = 0; q < CSPT; q++) {
     if (!(okm >> q & 1)) continue;
-    surv[i] = (uint32_t)(s0 + q);
+    surv[i] = (uint32_t)(s0 + (uint64_t)q * BLOCK);
     surv_off[i] = off;
     i++;
     off += units[q];
@@ -513,7 +541,7 @@ __device__ __forceinline__ uint64_t load6(const uint8_t *k) {
 }
 
 __global__ void __launch_bounds__(BLOCK) k_score(const DevPlan *pl, const uint64_t *cand,
-                                                 const uint32_t *loc, uint64_t slot_ub,
+                                                 const uint32_t *lmask, const Loc *loc, uint64_t slot_ub,
                                                  const Counters *ctr, const uint32_t *surv,
                                                  const unsigned long long *surv_off,
                                                  uint64_t *scratch, uint32_t *skey,
@@ -522,6 +550,7 @@ __global__ void __launch_bounds__(BLOCK) k_score(const DevPlan *pl, const uint64
   for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < nsurv; i += gridDim.x * BLOCK) {
     const uint32_t s = surv[i];
     const uint64_t docid = cand[s];
+    const uint32_t lm = lmask[s];
     uint64_t *rec = scratch + surv_off[i];
     DocView dv;
     dv.rec = rec;
@@ -540,16 +569,15 @@ __global__ void __launch_bounds__(BLOCK) k_score(const DevPlan *pl, const uint64
       int nsub = 0, newIdx = 0;
       for (int x = 0; x < pl->gnsub[j]; x++) {
         const int lid = pl->gsub[j][x];
-        if (!ctr->anysurv[lid]) continue;  // shrunk to empty: not a new sublist
+        if (!(ctr->anysurv >> lid & 1)) continue;  // shrunk to empty: not a new sublist
         const uint8_t fl = pl->gsubflags[j][newIdx];  // m_bigramFlags[new index]
         newIdx++;
-        const DevList &L = pl->lists[lid];
-        const uint32_t u = loc[(uint64_t)lid * slot_ub + s];
-        if (!valid_run(L, u, docid)) continue;
+        if (!(lm >> lid & 1)) continue;  // no run of this docid in the list
+        const Loc lc = loc[(uint64_t)lid * slot_ub + s];
         MCur &c = cur[nsub++];
-        c.p = L.p;
-        c.u = u;
-        c.end = u + run_units(L.p, L.units, u);
+        c.p = pl->lists[lid].p;
+        c.u = lc.unit;
+        c.end = lc.unit + lc.len;
         c.flags = fl;
         c.first = true;
         c.live = true;
@@ -624,40 +652,132 @@ __global__ void __launch_bounds__(BLOCK) k_score(const DevPlan *pl, const uint64
 }
 
 // ------------------------------------------------------------------ top-k
-// Each block sorts one tile of up to TILE (key, docid) pairs in LDS by
-// (key desc, docid asc) and writes its best k.  Invalid entries have key 0.
-__global__ void __launch_bounds__(1024) k_topk_tile(const uint32_t *in_key, const uint64_t *in_doc,
-                                                    const uint32_t *n_in_ptr, uint32_t n_in_const,
-                                                    uint32_t *out_key, uint64_t *out_doc,
-                                                    uint32_t *n_out_ptr, int k) {
-  __shared__ uint32_t sk[TILE];
-  __shared__ uint64_t sd[TILE];
-  const uint32_t n_in = n_in_ptr ? *n_in_ptr : n_in_const;
-  const uint64_t base = (uint64_t)blockIdx.x * TILE;
-  if (blockIdx.x == 0 && threadIdx.x == 0 && n_out_ptr) {
-    const uint32_t tiles = (n_in + TILE - 1) / TILE;
-    *n_out_ptr = tiles * (uint32_t)k;
-  }
-  // tiles past the live count exit (grid sized by an upper bound); tile 0
-  // always runs so an empty input still yields an all-invalid output
-  if (base >= n_in && blockIdx.x != 0) return;
-  for (int t = threadIdx.x; t < TILE; t += blockDim.x) {
-    const uint64_t g = base + t;
-    if (g < n_in) {
-      sk[t] = in_key[g];
-      sd[t] = in_doc[g];
+// TopTree replacement (TopTree.cpp:195-516 without clustering): the k best
+// survivors by (score desc, docid asc).  Scores travel as order-preserving
+// uint32 keys (0 = not scored).  A three-pass radix select (key bits 31..20,
+// 19..8, 7..0) finds the k-th key T; keys > T (fewer than k) and keys == T
+// (the ties, of which the smallest docids win) are gathered and sorted in
+// LDS by one block.  Each histogram pass keeps a 4096-bin histogram per block
+// in LDS; the last block to finish (ticket) scans the merged histogram.
+template <int PASS>
+__global__ void __launch_bounds__(BLOCK) k_select_hist(const uint32_t *skey, const Counters *ctr, Select *sel,
+                                                       uint32_t k) {
+  __shared__ uint32_t h[SEL_BINS];
+  __shared__ uint32_t tmp[BLOCK / 64];
+  __shared__ bool s_last;
+  if (PASS > 0 && sel->all) return;  // uniform
+  constexpr int NB = PASS == 2 ? 256 : SEL_BINS;
+  for (int b = threadIdx.x; b < NB; b += BLOCK) h[b] = 0;
+  __syncthreads();
+  const uint32_t n = ctr->nsurv;
+  const uint32_t pre = PASS > 0 ? sel->prefix : 0;
+  for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) {
+    const uint32_t key = skey[i];
+    if (key == 0) continue;
+    uint32_t bin;
+    if (PASS == 0) {
+      bin = key >> 20;
+    } else if (PASS == 1) {
+      if ((key >> 20) != pre) continue;
+      bin = (key >> 8) & 0xfff;
     } else {
-      sk[t] = 0;
-      sd[t] = ~0ull;
+      if ((key >> 8) != pre) continue;
+      bin = key & 0xff;
     }
+    atomicAdd(&h[bin], 1u);
   }
   __syncthreads();
-  // bitonic sort, "greater" = better rank
-  for (int size = 2; size <= TILE; size <<= 1) {
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int t = threadIdx.x; t < TILE / 2; t += blockDim.x) {
-        const int i = 2 * t - (t & (stride - 1));
-        const int j = i + stride;
+  for (int b = threadIdx.x; b < NB; b += BLOCK)
+    if (h[b]) atomicAdd(&sel->hist[PASS][b], h[b]);
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) s_last = atomicAdd(&sel->ticket[PASS], 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();
+  // last block: bins from the top, BPT per thread
+  constexpr int BPT = NB / BLOCK;
+  uint32_t c[BPT], sum = 0;
+#pragma unroll
+  for (int q = 0; q < BPT; q++) {
+    const int b = NB - 1 - (threadIdx.x * BPT + q);
+    c[q] = __hip_atomic_load(&sel->hist[PASS][b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sum += c[q];
+  }
+  uint32_t total;
+  const uint32_t before = block_exclusive_scan(sum, tmp, &total);
+  const uint32_t need = PASS == 0 ? k : sel->need;
+  if (PASS == 0 && total <= need) {
+    if (threadIdx.x == 0) sel->all = 1;
+    return;
+  }
+  if (before < need && need <= before + sum) {
+    uint32_t cum = before;
+#pragma unroll
+    for (int q = 0; q < BPT; q++) {
+      if (cum + c[q] >= need) {
+        const uint32_t b = NB - 1 - (threadIdx.x * BPT + q);
+        if (PASS == 0) sel->prefix = b;
+        else if (PASS == 1) sel->prefix = (pre << 12) | b;
+        else sel->thr = (pre << 8) | b;
+        sel->need = need - cum;
+        break;
+      }
+      cum += c[q];
+    }
+  }
+}
+
+// keys > T -> A (fewer than k), keys == T -> B (ties); one atomic per wave
+__global__ void __launch_bounds__(BLOCK) k_select_gather(const uint32_t *skey, const uint64_t *sdoc,
+                                                         const Counters *ctr, Select *sel, uint32_t *akey,
+                                                         uint64_t *adoc, uint32_t *bkey, uint64_t *bdoc) {
+  const uint32_t n = ctr->nsurv;
+  const bool all = sel->all != 0;
+  const uint32_t T = all ? 1u : sel->thr;
+  const int lane = threadIdx.x & 63;
+  const uint32_t lim = (n + 63) & ~63u;  // whole waves iterate together
+  for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < lim; i += gridDim.x * BLOCK) {
+    const uint32_t key = i < n ? skey[i] : 0;
+    const bool ga = key != 0 && (all ? key >= T : key > T);
+    const bool gb = key != 0 && !all && key == T;
+    const uint64_t ma = __ballot(ga), mb = __ballot(gb);
+    uint32_t ba = 0, bb = 0;
+    if (lane == 0) {
+      if (ma) ba = atomicAdd(&sel->na, (uint32_t)__popcll(ma));
+      if (mb) bb = atomicAdd(&sel->nb, (uint32_t)__popcll(mb));
+    }
+    ba = __shfl(ba, 0, 64);
+    bb = __shfl(bb, 0, 64);
+    const uint64_t below = (1ull << lane) - 1;
+    if (ga) {
+      const uint32_t o = ba + (uint32_t)__popcll(ma & below);
+      akey[o] = key;
+      adoc[o] = sdoc[i];
+    }
+    if (gb) {
+      const uint32_t o = bb + (uint32_t)__popcll(mb & below);
+      bkey[o] = key;
+      bdoc[o] = sdoc[i];
+    }
+  }
+}
+
+// bitonic sort of sk/sd[0, n) in LDS, n rounded up to a power of two with
+// sentinels; "first" = better = key desc, docid asc
+__device__ void lds_sort_best_first(uint32_t *sk, uint64_t *sd, uint32_t n) {
+  uint32_t S = 1;
+  while (S < n) S <<= 1;
+  for (uint32_t t = n + threadIdx.x; t < S; t += blockDim.x) {
+    sk[t] = 0;
+    sd[t] = ~0ull;
+  }
+  __syncthreads();
+  for (uint32_t size = 2; size <= S; size <<= 1) {
+    for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+      for (uint32_t t = threadIdx.x; t < S / 2; t += blockDim.x) {
+        const uint32_t i = 2 * t - (t & (stride - 1));
+        const uint32_t j = i + stride;
         const bool desc = ((i & size) == 0);
         const uint32_t ki = sk[i], kj = sk[j];
         const uint64_t di = sd[i], dj = sd[j];
@@ -670,10 +790,36 @@ __global__ void __launch_bounds__(1024) k_topk_tile(const uint32_t *in_key, cons
       __syncthreads();
     }
   }
-  const uint64_t obase = (uint64_t)blockIdx.x * k;
-  for (int t = threadIdx.x; t < k; t += blockDim.x) {
-    out_key[obase + t] = sk[t];
-    out_doc[obase + t] = sd[t];
+}
+
+// One block: A plus the ties, merged TILE-k at a time (ties beyond one tile
+// only with huge exact-score ties), best k written to the result block.
+__global__ void __launch_bounds__(1024) k_select_final(const Select *sel, const uint32_t *akey, const uint64_t *adoc,
+                                                       const uint32_t *bkey, const uint64_t *bdoc, uint32_t k,
+                                                       uint32_t *out_key, uint64_t *out_doc) {
+  __shared__ uint32_t sk[TILE];
+  __shared__ uint64_t sd[TILE];
+  const uint32_t na = sel->na, nb = sel->nb;
+  for (uint32_t t = threadIdx.x; t < na; t += blockDim.x) {
+    sk[t] = akey[t];
+    sd[t] = adoc[t];
+  }
+  uint32_t kept = na, tb = 0;
+  for (;;) {
+    const uint32_t take = min(nb - tb, (uint32_t)TILE - kept);
+    for (uint32_t t = threadIdx.x; t < take; t += blockDim.x) {
+      sk[kept + t] = bkey[tb + t];
+      sd[kept + t] = bdoc[tb + t];
+    }
+    tb += take;
+    __syncthreads();
+    lds_sort_best_first(sk, sd, kept + take);
+    kept = min(k, kept + take);
+    if (tb >= nb) break;
+  }
+  for (uint32_t t = threadIdx.x; t < k; t += blockDim.x) {
+    out_key[t] = t < kept ? sk[t] : 0u;
+    out_doc[t] = t < kept ? sd[t] : ~0ull;
   }
 }
 
@@ -726,7 +872,7 @@ struct DevBuf {
     cap = want;
     return 0;
   }
-  template <class T> T *as() const { return reinterpret_cast<T *>(p); }
+  template <class T> T *as(size_t off = 0) const { return reinterpret_cast<T *>(static_cast<uint8_t *>(p) + off); }
   void release() {
     if (p) (void)hipFree(p);
     p = nullptr;
@@ -741,6 +887,8 @@ struct ListEntry {
   bool live = false;
 };
 
+static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
 }  // namespace gbgpu
 
 using namespace gbgpu;
@@ -750,32 +898,32 @@ struct gbgpu_ctx {
   hipStream_t stream = nullptr;
   std::mutex mu;
   std::vector<ListEntry> lists;
-  DevBuf plan, counters, g0chunks, chunkcnt, arrfirst, work, cand, mask, loc, surv, survoff, scratch,
-      skey, sdoc, tk_key[2], tk_doc[2];
-  DevPlan *h_plan = nullptr;   // pinned
-  Counters *h_ctr = nullptr;   // pinned
-  uint32_t *h_out_key = nullptr;
-  uint64_t *h_out_doc = nullptr;
-  int out_cap = 0;
+  // per-query device buffers (grown, then reused)
+  DevBuf tables, chunkcnt, cand, lmask, loc, surv, survoff, scratch, skey, sdoc, sel, gath, res;
+  uint8_t *h_stage = nullptr;  // pinned: query tables (host -> device, one copy)
+  size_t stage_cap = 0;
+  uint8_t *h_res = nullptr;    // pinned: counters + top list (device -> host, one copy)
+  size_t hres_cap = 0;
   std::vector<G0Chunk> g0c;
   std::vector<ProbeWork> pw;
   std::vector<uint32_t> afirst;
-  uint8_t *h_stage = nullptr;  // pinned staging for the per-query tables
-  size_t stage_cap = 0;
   // state of the in-flight query
   bool pending = false;
   bool early = false;
   int k = 0;
-  int final_buf = 0;
+  size_t res_bytes = 0;
   int32_t docs_wanted = 0;
   int64_t scan_bytes = 0;
   bool profiling = false;
   int probe_mode = 0;  // diagnostic only (GBGPU_PROBE_MODE)
   hipEvent_t ev[7] = {};
   float last_ms[6] = {0, 0, 0, 0, 0, 0};
-  // per-query temporary lists (gbgpu_query with host lists)
-  std::vector<int32_t> temp_handles;
 };
+
+// result block layout: [Counters | keys k | docids k]
+static size_t res_keys_off() { return align256(sizeof(Counters)); }
+static size_t res_docs_off(int k) { return res_keys_off() + align256(4 * (size_t)std::max(k, 1)); }
+static size_t res_size(int k) { return res_docs_off(k) + 8 * (size_t)std::max(k, 1); }
 
 static int upload_list(gbgpu_ctx *ctx, const uint8_t *bytes, int64_t size, int32_t *handle) {
   if (size < 0 || (size > 0 && size < 18) || (size > 0 && (size - 18) % 6 != 0)) return EINVAL;
@@ -784,7 +932,7 @@ static int upload_list(gbgpu_ctx *ctx, const uint8_t *bytes, int64_t size, int32
   e.size = size;
   e.units = size ? (uint32_t)((size - 6) / 6) : 0;
   size_t alloc = (size_t)(size ? size - 6 : 0) + LIST_PAD;
-  alloc = (alloc + 255) & ~(size_t)255;
+  alloc = align256(alloc);
   if (hipMalloc(&e.d, alloc) != hipSuccess) return ENOMEM;
   HIPCHECK(hipMemsetAsync(e.d, 0, alloc, ctx->stream));
   if (size) {
@@ -816,6 +964,7 @@ static int enqueue(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms, const i
   if (!p || nterms < 0 || (nterms && (!terms || !handles))) return EINVAL;
   if (p->site_clustering || p->num_docid_splits > 1) return GBGPU_EUNSUPPORTED;
   if (p->docs_to_get <= 0 || p->real_max_top <= 0) return EINVAL;
+  if (nterms > 1024) return GBGPU_EUNSUPPORTED;
   std::vector<int64_t> sizes(nterms);
   for (int i = 0; i < nterms; i++) {
     if (terms[i].field_code) return GBGPU_EUNSUPPORTED;
@@ -828,14 +977,18 @@ static int enqueue(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms, const i
   if (rc) return rc;
   ctx->docs_wanted = hp.docs_wanted;
   ctx->k = hp.docs_wanted;
-  ctx->pending = true;
   ctx->early = (hp.ngroups == 0 || hp.min_list_size == 0);
   ctx->scan_bytes = 0;
-  if (ctx->early) return 0;
-  if (hp.ngroups > MAXG) { ctx->pending = false; return GBGPU_EUNSUPPORTED; }
-  if (ctx->k > TILE) { ctx->pending = false; return GBGPU_EUNSUPPORTED; }
+  if (ctx->early) {
+    ctx->pending = true;
+    return 0;
+  }
+  if (hp.ngroups > MAXG) return GBGPU_EUNSUPPORTED;
+  if (ctx->k > MAX_K) return GBGPU_EUNSUPPORTED;
 
-  DevPlan &P = *ctx->h_plan;
+  // ---- query tables, built straight into the pinned staging buffer
+  // layout: [DevPlan | G0Chunk[] | afirst[MAXG0] | ProbeWork[]]
+  DevPlan P;
   std::memset(&P, 0, sizeof P);
   P.ngroups = hp.ngroups;
   P.real_max_top = hp.real_max_top;
@@ -844,15 +997,12 @@ static int enqueue(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms, const i
   P.site_rank_multiplier = GB_SITERANKMULTIPLIER;
   P.nqt = nterms;
   int dense[1024];
-  std::vector<int> term_of(0);
-  if (nterms > 1024) { ctx->pending = false; return GBGPU_EUNSUPPORTED; }
   for (int i = 0; i < nterms; i++) dense[i] = -1;
   auto dense_id = [&](int term) -> int {
     if (dense[term] >= 0) return dense[term];
     if (P.nlists >= MAXL) return -1;
     int id = P.nlists++;
     dense[term] = id;
-    term_of.push_back(term);
     const ListEntry &e = ctx->lists[handles[term]];
     P.lists[id].p = e.d;
     P.lists[id].units = e.units;
@@ -863,7 +1013,7 @@ static int enqueue(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms, const i
   };
   for (int j = 0; j < hp.ngroups; j++) {
     const GroupInfo &g = hp.g[j];
-    if (g.nsub > MAXSUB) { ctx->pending = false; return GBGPU_EUNSUPPORTED; }
+    if (g.nsub > MAXSUB) return GBGPU_EUNSUPPORTED;
     P.gflags0[j] = g.flags[0];
     P.gnsub[j] = (uint8_t)g.nsub;
     P.tfw[j] = g.tfw;
@@ -875,7 +1025,7 @@ static int enqueue(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms, const i
     if (!neg) P.pos_mask |= 1u << j;
     for (int x = 0; x < g.nsub; x++) {
       int id = dense_id(g.sub_term[x]);
-      if (id < 0) { ctx->pending = false; return GBGPU_EUNSUPPORTED; }
+      if (id < 0) return GBGPU_EUNSUPPORTED;
       P.gsub[j][x] = (uint8_t)id;
       P.lists[id].group_bits |= neg ? NEG_BIT : (1u << j);
     }
@@ -887,7 +1037,7 @@ static int enqueue(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms, const i
   for (int x = 0; x < g0.nsub; x++) {
     int id = dense[g0.sub_term[x]];
     if (P.lists[id].g0_array >= 0) continue;
-    if (P.g0n >= MAXG0) { ctx->pending = false; return GBGPU_EUNSUPPORTED; }
+    if (P.g0n >= MAXG0) return GBGPU_EUNSUPPORTED;
     P.lists[id].g0_array = P.g0n;
     P.g0list[P.g0n] = id;
     P.g0base[P.g0n] = slot;
@@ -896,9 +1046,9 @@ static int enqueue(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms, const i
   }
   P.g0base[P.g0n] = slot;
   const uint64_t slot_ub = slot;
+  if (slot_ub >= 0xffffffffull) return GBGPU_ECAPACITY;
   for (int id = 0; id < P.nlists; id++) P.lists[id].probe = (P.lists[id].g0_array != 0);
 
-  // work tables
   ctx->g0c.clear();
   ctx->afirst.assign(MAXG0, 0);
   for (int a = 0; a < P.g0n; a++) {
@@ -927,117 +1077,101 @@ static int enqueue(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms, const i
     for (int x = 0; x < P.gnsub[j]; x++) scratch_ub += P.lists[P.gsub[j][x]].units;
   }
   const int k = ctx->k;
-  const uint64_t tiles0 = (slot_ub + TILE - 1) / TILE;
+  const size_t o_chunks = align256(sizeof(DevPlan));
+  const size_t o_afirst = o_chunks + align256(sizeof(G0Chunk) * ctx->g0c.size());
+  const size_t o_work = o_afirst + align256(4 * MAXG0);
+  const size_t tbytes = o_work + align256(sizeof(ProbeWork) * ctx->pw.size());
+  ctx->res_bytes = res_size(k);
   int rc2 = 0;
-  rc2 |= ctx->plan.ensure(sizeof(DevPlan));
-  rc2 |= ctx->counters.ensure(sizeof(Counters));
-  rc2 |= ctx->g0chunks.ensure(sizeof(G0Chunk) * std::max<size_t>(1, ctx->g0c.size()));
+  rc2 |= ctx->tables.ensure(tbytes);
   rc2 |= ctx->chunkcnt.ensure(4 * std::max<size_t>(1, ctx->g0c.size()));
-  rc2 |= ctx->arrfirst.ensure(4 * MAXG0);
-  rc2 |= ctx->work.ensure(sizeof(ProbeWork) * std::max<size_t>(1, ctx->pw.size()));
   rc2 |= ctx->cand.ensure(8 * slot_ub);
-  rc2 |= ctx->mask.ensure(4 * slot_ub);
-  rc2 |= ctx->loc.ensure(4 * slot_ub * (uint64_t)P.nlists);
+  rc2 |= ctx->lmask.ensure(4 * slot_ub);
+  rc2 |= ctx->loc.ensure(sizeof(Loc) * slot_ub * (uint64_t)P.nlists);
   rc2 |= ctx->surv.ensure(4 * slot_ub);
   rc2 |= ctx->survoff.ensure(8 * slot_ub);
   rc2 |= ctx->scratch.ensure(8 * scratch_ub);
   rc2 |= ctx->skey.ensure(4 * slot_ub);
   rc2 |= ctx->sdoc.ensure(8 * slot_ub);
-  rc2 |= ctx->tk_key[0].ensure(4 * (tiles0 * k + TILE));
-  rc2 |= ctx->tk_doc[0].ensure(8 * (tiles0 * k + TILE));
-  rc2 |= ctx->tk_key[1].ensure(4 * (tiles0 * k + TILE));
-  rc2 |= ctx->tk_doc[1].ensure(8 * (tiles0 * k + TILE));
-  if (rc2) { ctx->pending = false; return ENOMEM; }
-  if (ctx->out_cap < k) {
-    if (ctx->h_out_key) (void)hipHostFree(ctx->h_out_key);
-    if (ctx->h_out_doc) (void)hipHostFree(ctx->h_out_doc);
-    HIPCHECK(hipHostMalloc((void **)&ctx->h_out_key, 4 * (size_t)std::max(k, 1)));
-    HIPCHECK(hipHostMalloc((void **)&ctx->h_out_doc, 8 * (size_t)std::max(k, 1)));
-    ctx->out_cap = std::max(k, 1);
+  rc2 |= ctx->sel.ensure(sizeof(Select));
+  rc2 |= ctx->gath.ensure(12 * (slot_ub + MAX_K) + 1024);
+  rc2 |= ctx->res.ensure(ctx->res_bytes);
+  if (rc2) return ENOMEM;
+  if (tbytes > ctx->stage_cap) {
+    if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
+    ctx->h_stage = nullptr;
+    ctx->stage_cap = 0;
+    HIPCHECK(hipHostMalloc((void **)&ctx->h_stage, tbytes * 2));
+    ctx->stage_cap = tbytes * 2;
   }
+  if (ctx->res_bytes > ctx->hres_cap) {
+    if (ctx->h_res) (void)hipHostFree(ctx->h_res);
+    ctx->h_res = nullptr;
+    ctx->hres_cap = 0;
+    HIPCHECK(hipHostMalloc((void **)&ctx->h_res, ctx->res_bytes));
+    ctx->hres_cap = ctx->res_bytes;
+  }
+  // the staging buffer may still feed the previous query's copy: the stream
+  // has been synchronised by collect() (one query in flight per context)
+  std::memcpy(ctx->h_stage, &P, sizeof P);
+  std::memcpy(ctx->h_stage + o_chunks, ctx->g0c.data(), sizeof(G0Chunk) * ctx->g0c.size());
+  std::memcpy(ctx->h_stage + o_afirst, ctx->afirst.data(), 4 * MAXG0);
+  std::memcpy(ctx->h_stage + o_work, ctx->pw.data(), sizeof(ProbeWork) * ctx->pw.size());
+
   hipStream_t st = ctx->stream;
   if (ctx->profiling) HIPCHECK(hipEventRecord(ctx->ev[0], st));
-  HIPCHECK(hipMemcpyAsync(ctx->plan.p, ctx->h_plan, sizeof(DevPlan), hipMemcpyHostToDevice, st));
-  {
-    // the tables go through pinned memory: a pageable source makes the copy
-    // synchronous with the host and stalls the stream
-    const size_t b1 = sizeof(G0Chunk) * ctx->g0c.size(), b2 = 4 * MAXG0, b3 = sizeof(ProbeWork) * ctx->pw.size();
-    const size_t need = b1 + b2 + b3 + 64;
-    if (need > ctx->stage_cap) {
-      if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
-      ctx->h_stage = nullptr;
-      ctx->stage_cap = 0;
-      HIPCHECK(hipHostMalloc((void **)&ctx->h_stage, need * 2));
-      ctx->stage_cap = need * 2;
-    }
-    std::memcpy(ctx->h_stage, ctx->g0c.data(), b1);
-    std::memcpy(ctx->h_stage + b1, ctx->afirst.data(), b2);
-    std::memcpy(ctx->h_stage + b1 + b2, ctx->pw.data(), b3);
-    if (b1) HIPCHECK(hipMemcpyAsync(ctx->g0chunks.p, ctx->h_stage, b1, hipMemcpyHostToDevice, st));
-    HIPCHECK(hipMemcpyAsync(ctx->arrfirst.p, ctx->h_stage + b1, b2, hipMemcpyHostToDevice, st));
-    if (b3) HIPCHECK(hipMemcpyAsync(ctx->work.p, ctx->h_stage + b1 + b2, b3, hipMemcpyHostToDevice, st));
-  }
-  HIPCHECK(hipMemsetAsync(ctx->counters.p, 0, sizeof(Counters), st));
-  HIPCHECK(hipMemsetAsync(ctx->mask.p, 0, 4 * slot_ub, st));
-  const DevPlan *dpl = ctx->plan.as<DevPlan>();
-  Counters *dctr = ctx->counters.as<Counters>();
+  HIPCHECK(hipMemcpyAsync(ctx->tables.p, ctx->h_stage, tbytes, hipMemcpyHostToDevice, st));
+  const DevPlan *dpl = ctx->tables.as<DevPlan>();
+  const G0Chunk *dchunks = ctx->tables.as<G0Chunk>(o_chunks);
+  const uint32_t *dafirst = ctx->tables.as<uint32_t>(o_afirst);
+  const ProbeWork *dwork = ctx->tables.as<ProbeWork>(o_work);
+  Counters *dctr = ctx->res.as<Counters>();
+  Select *dsel = ctx->sel.as<Select>();
+  uint32_t *lmask = ctx->lmask.as<uint32_t>();
+  Loc *loc = ctx->loc.as<Loc>();
+  hipLaunchKernelGGL(k_reset, dim3(16), dim3(BLOCK), 0, st, reinterpret_cast<uint32_t *>(dctr),
+                     (uint32_t)(sizeof(Counters) / 4), reinterpret_cast<uint32_t *>(dsel),
+                     (uint32_t)(sizeof(Select) / 4));
   const uint32_t ng0 = (uint32_t)ctx->g0c.size();
-  if (ng0) {
-    hipLaunchKernelGGL(k_count_runs, dim3(ng0), dim3(BLOCK), 0, st, dpl, ctx->g0chunks.as<G0Chunk>(),
-                       ctx->chunkcnt.as<uint32_t>());
-    hipLaunchKernelGGL(k_scan_runs, dim3(1), dim3(1024), 0, st, ctx->g0chunks.as<G0Chunk>(), ng0,
-                       ctx->chunkcnt.as<uint32_t>(), dctr);
-    hipLaunchKernelGGL(k_write_runs, dim3(ng0), dim3(BLOCK), 0, st, dpl, ctx->g0chunks.as<G0Chunk>(),
-                       ctx->chunkcnt.as<uint32_t>(), ctx->arrfirst.as<uint32_t>(), ctx->cand.as<uint64_t>(),
-                       ctx->mask.as<uint32_t>(), ctx->loc.as<uint32_t>(), slot_ub, dctr, ng0);
-  }
+  hipLaunchKernelGGL(k_count_runs, dim3(ng0), dim3(BLOCK), 0, st, dpl, dchunks, ctx->chunkcnt.as<uint32_t>());
+  hipLaunchKernelGGL(k_scan_runs, dim3(1), dim3(1024), 0, st, ng0, ctx->chunkcnt.as<uint32_t>());
+  hipLaunchKernelGGL(k_write_runs, dim3(ng0), dim3(BLOCK), 0, st, dpl, dchunks, ctx->chunkcnt.as<uint32_t>(),
+                     dafirst, ctx->cand.as<uint64_t>(), lmask, loc, slot_ub, dctr, ng0);
   if (ctx->profiling) HIPCHECK(hipEventRecord(ctx->ev[1], st));
   if (!ctx->pw.empty()) {
-    auto kp = ctx->probe_mode == 1 ? k_probe<1> : (ctx->probe_mode == 2 ? k_probe<2> : k_probe<0>);
-    hipLaunchKernelGGL(kp, dim3((uint32_t)ctx->pw.size()), dim3(BLOCK), 0, st, dpl,
-                       ctx->work.as<ProbeWork>(), ctx->cand.as<uint64_t>(), ctx->mask.as<uint32_t>(),
-                       ctx->loc.as<uint32_t>(), slot_ub, dctr);
+    auto kp = ctx->probe_mode == 2 ? k_probe<2> : k_probe<0>;
+    hipLaunchKernelGGL(kp, dim3((uint32_t)ctx->pw.size()), dim3(BLOCK), 0, st, dpl, dwork,
+                       ctx->cand.as<uint64_t>(), lmask, loc, slot_ub, dctr);
   }
   if (ctx->profiling) HIPCHECK(hipEventRecord(ctx->ev[2], st));
   const uint32_t cgrid = (uint32_t)((slot_ub + CTILE - 1) / CTILE);
-  hipLaunchKernelGGL(k_compact, dim3(std::max(cgrid, 1u)), dim3(BLOCK), 0, st, dpl, ctx->cand.as<uint64_t>(),
-                     ctx->mask.as<uint32_t>(), ctx->loc.as<uint32_t>(), slot_ub, dctr, ctx->surv.as<uint32_t>(),
-                     ctx->survoff.as<unsigned long long>());
+  hipLaunchKernelGGL(k_compact, dim3(std::max(cgrid, 1u)), dim3(BLOCK), 0, st, dpl, lmask, loc, slot_ub, dctr,
+                     ctx->surv.as<uint32_t>(), ctx->survoff.as<unsigned long long>());
   if (ctx->profiling) HIPCHECK(hipEventRecord(ctx->ev[3], st));
   const uint32_t sgrid = (uint32_t)std::min<uint64_t>((slot_ub + BLOCK - 1) / BLOCK, 2048);
-  hipLaunchKernelGGL(k_score, dim3(std::max(sgrid, 1u)), dim3(BLOCK), 0, st, dpl, ctx->cand.as<uint64_t>(),
-                     ctx->loc.as<uint32_t>(), slot_ub, dctr, ctx->surv.as<uint32_t>(),
-                     ctx->survoff.as<unsigned long long>(), ctx->scratch.as<uint64_t>(), ctx->skey.as<uint32_t>(),
-                     ctx->sdoc.as<uint64_t>());
+  hipLaunchKernelGGL(k_score, dim3(std::max(sgrid, 1u)), dim3(BLOCK), 0, st, dpl, ctx->cand.as<uint64_t>(), lmask,
+                     loc, slot_ub, dctr, ctx->surv.as<uint32_t>(), ctx->survoff.as<unsigned long long>(),
+                     ctx->scratch.as<uint64_t>(), ctx->skey.as<uint32_t>(), ctx->sdoc.as<uint64_t>());
   if (ctx->profiling) HIPCHECK(hipEventRecord(ctx->ev[4], st));
-  // top-k stages: survivors -> tiles -> ... -> one tile
-  uint64_t n_ub = slot_ub;
-  const uint32_t *in_key = ctx->skey.as<uint32_t>();
-  const uint64_t *in_doc = ctx->sdoc.as<uint64_t>();
-  const uint32_t *in_n = &dctr->nsurv;
-  int buf = 0, stage = 0;
-  for (;;) {
-    uint64_t tiles = (n_ub + TILE - 1) / TILE;
-    if (tiles == 0) tiles = 1;
-    uint32_t *ok = ctx->tk_key[buf].as<uint32_t>();
-    uint64_t *od = ctx->tk_doc[buf].as<uint64_t>();
-    uint32_t *on = &dctr->topk_n[stage & 7];
-    hipLaunchKernelGGL(k_topk_tile, dim3((uint32_t)tiles), dim3(1024), 0, st, in_key, in_doc, in_n, 0u, ok, od,
-                       on, k);
-    ctx->final_buf = buf;
-    if (tiles == 1) break;
-    n_ub = tiles * (uint64_t)k;
-    in_key = ok;
-    in_doc = od;
-    in_n = on;
-    buf ^= 1;
-    stage++;
-  }
+  // top-k: radix select over the survivors' keys, then one LDS sort
+  const uint32_t hgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(256, (slot_ub + 1023) / 1024));
+  const uint32_t *skey = ctx->skey.as<uint32_t>();
+  hipLaunchKernelGGL(k_select_hist<0>, dim3(hgrid), dim3(BLOCK), 0, st, skey, dctr, dsel, (uint32_t)k);
+  hipLaunchKernelGGL(k_select_hist<1>, dim3(hgrid), dim3(BLOCK), 0, st, skey, dctr, dsel, (uint32_t)k);
+  hipLaunchKernelGGL(k_select_hist<2>, dim3(hgrid), dim3(BLOCK), 0, st, skey, dctr, dsel, (uint32_t)k);
+  uint32_t *akey = ctx->gath.as<uint32_t>();
+  uint64_t *adoc = ctx->gath.as<uint64_t>(align256(4 * (size_t)MAX_K));
+  uint32_t *bkey = ctx->gath.as<uint32_t>(align256(4 * (size_t)MAX_K) + align256(8 * (size_t)MAX_K));
+  uint64_t *bdoc = ctx->gath.as<uint64_t>(align256(4 * (size_t)MAX_K) + align256(8 * (size_t)MAX_K) +
+                                          align256(4 * slot_ub));
+  hipLaunchKernelGGL(k_select_gather, dim3(hgrid), dim3(BLOCK), 0, st, skey, ctx->sdoc.as<uint64_t>(), dctr, dsel,
+                     akey, adoc, bkey, bdoc);
+  hipLaunchKernelGGL(k_select_final, dim3(1), dim3(1024), 0, st, dsel, akey, adoc, bkey, bdoc, (uint32_t)k,
+                     ctx->res.as<uint32_t>(res_keys_off()), ctx->res.as<uint64_t>(res_docs_off(k)));
   if (ctx->profiling) HIPCHECK(hipEventRecord(ctx->ev[5], st));
-  HIPCHECK(hipMemcpyAsync(ctx->h_out_key, ctx->tk_key[ctx->final_buf].p, 4 * (size_t)k, hipMemcpyDeviceToHost, st));
-  HIPCHECK(hipMemcpyAsync(ctx->h_out_doc, ctx->tk_doc[ctx->final_buf].p, 8 * (size_t)k, hipMemcpyDeviceToHost, st));
-  HIPCHECK(hipMemcpyAsync(ctx->h_ctr, ctx->counters.p, sizeof(Counters), hipMemcpyDeviceToHost, st));
+  HIPCHECK(hipMemcpyAsync(ctx->h_res, ctx->res.p, ctx->res_bytes, hipMemcpyDeviceToHost, st));
   if (ctx->profiling) HIPCHECK(hipEventRecord(ctx->ev[6], st));
+  ctx->pending = true;
   return 0;
 }
 
@@ -1059,15 +1193,18 @@ static int collect(gbgpu_ctx *ctx, gbgpu_result *out) {
       ctx->last_ms[i] = t;
     }
   }
-  out->hits = ctx->h_ctr->nsurv;
+  const Counters *c = reinterpret_cast<const Counters *>(ctx->h_res);
+  const uint32_t *keys = reinterpret_cast<const uint32_t *>(ctx->h_res + res_keys_off());
+  const uint64_t *docs = reinterpret_cast<const uint64_t *>(ctx->h_res + res_docs_off(ctx->k));
+  out->hits = c->nsurv;
   int n = 0;
   for (int i = 0; i < ctx->k && n < out->capacity; i++) {
-    uint32_t key = ctx->h_out_key[i];
+    const uint32_t key = keys[i];
     if (key == 0) break;
-    uint32_t b = (key & 0x80000000u) ? (key & 0x7fffffffu) : ~key;
+    const uint32_t b = (key & 0x80000000u) ? (key & 0x7fffffffu) : ~key;
     float f;
     std::memcpy(&f, &b, 4);
-    if (out->docids) out->docids[n] = (int64_t)ctx->h_out_doc[i];
+    if (out->docids) out->docids[n] = (int64_t)docs[i];
     if (out->scores) out->scores[n] = f;
     n++;
   }
@@ -1109,11 +1246,6 @@ int gbgpu_open(int device, gbgpu_ctx **out) {
     delete ctx;
     return GBGPU_EHIP;
   }
-  if (hipHostMalloc((void **)&ctx->h_plan, sizeof(DevPlan)) != hipSuccess ||
-      hipHostMalloc((void **)&ctx->h_ctr, sizeof(Counters)) != hipSuccess) {
-    delete ctx;
-    return ENOMEM;
-  }
   for (auto &e : ctx->ev) (void)hipEventCreate(&e);
   if (const char *pm = std::getenv("GBGPU_PROBE_MODE")) ctx->probe_mode = std::atoi(pm);
   *out = ctx;
@@ -1126,15 +1258,11 @@ void gbgpu_close(gbgpu_ctx *ctx) {
   (void)hipStreamSynchronize(ctx->stream);
   for (auto &e : ctx->lists)
     if (e.live) (void)hipFree(e.d);
-  DevBuf *bufs[] = {&ctx->plan, &ctx->counters, &ctx->g0chunks, &ctx->chunkcnt, &ctx->arrfirst, &ctx->work,
-                    &ctx->cand, &ctx->mask, &ctx->loc, &ctx->surv, &ctx->survoff, &ctx->scratch, &ctx->skey,
-                    &ctx->sdoc, &ctx->tk_key[0], &ctx->tk_doc[0], &ctx->tk_key[1], &ctx->tk_doc[1]};
+  DevBuf *bufs[] = {&ctx->tables, &ctx->chunkcnt, &ctx->cand, &ctx->lmask, &ctx->loc, &ctx->surv,
+                    &ctx->survoff, &ctx->scratch, &ctx->skey, &ctx->sdoc, &ctx->sel, &ctx->gath, &ctx->res};
   for (auto *b : bufs) b->release();
-  if (ctx->h_plan) (void)hipHostFree(ctx->h_plan);
-  if (ctx->h_ctr) (void)hipHostFree(ctx->h_ctr);
-  if (ctx->h_out_key) (void)hipHostFree(ctx->h_out_key);
-  if (ctx->h_out_doc) (void)hipHostFree(ctx->h_out_doc);
   if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
+  if (ctx->h_res) (void)hipHostFree(ctx->h_res);
   for (auto &e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(ctx->stream);
@@ -1211,7 +1339,7 @@ void *gbgpu_stream(gbgpu_ctx *ctx) { return ctx ? (void *)ctx->stream : nullptr;
 
 int gbgpu_last_topk_device(gbgpu_ctx *ctx, void **dev_ptr, int32_t *n) {
   if (!ctx || !dev_ptr || !n) return EINVAL;
-  *dev_ptr = ctx->tk_key[ctx->final_buf].p;
+  *dev_ptr = ctx->res.p ? ctx->res.as<uint8_t>(res_keys_off()) : nullptr;
   *n = ctx->k;
   return 0;
 }
