@@ -22,9 +22,11 @@
 //        survivors = candidates whose lists cover every positive group and
 //        no negative one (the final m_docIdVoteBuf), plus the shrunk-sublist
 //        non-empty flags (shrinkSubLists, Posdb.cpp:5334-5428).
-//   k_score
-//        one lane per survivor: mini-merge (Posdb.cpp:6559-6778) into scratch
-//        records, then the scorers of scoring.h.
+//   k_minimerge
+//        one lane per (survivor, group): mini-merge (Posdb.cpp:6559-6778) of
+//        the group's sublist runs into arena records.
+//   k_score<NQ>
+//        one lane per survivor: the scorers of scoring.h, register-resident.
 //   k_select_hist x3 / k_select_gather / k_select_final
 //        radix select of the k best (score desc, docid asc) replacing TopTree
 //        (TopTree.cpp:195-516), then one small LDS sort.
@@ -74,7 +76,6 @@ struct Counters {
 // radix-select state (3 passes over the 32-bit score keys: 12+12+8 bits)
 struct Select {
   uint32_t hist[3][SEL_BINS];
-  uint32_t ticket[3];
   uint32_t prefix;  // selected key prefix so far
   uint32_t need;    // entries still to take inside the selected prefix
   uint32_t all;     // fewer valid entries than k: take them all
@@ -527,119 +528,191 @@ __global__ void __launch_bounds__(BLOCK) k_compact(const DevPlan *pl, const uint
 // ------------------------------------------------------------------ score
 __constant__ Weights c_weights;
 
-struct MCur {
-  const uint8_t *p;
-  uint32_t u, end;
-  uint8_t flags;
-  bool first;
-  bool live;
+// one (survivor, group) mini-merge result: record range in the arena and the
+// group's first key's siteRank/langId (Posdb.cpp:6985-7003)
+struct GRange {
+  uint32_t start;
+  uint32_t info;  // count(16) | hasFirst(1) | siteRank(4) | langId(6) | positive(1)
 };
+constexpr uint32_t GR_HASFIRST = 1u << 16;
+constexpr uint32_t GR_POSITIVE = 1u << 27;
 
 __device__ __forceinline__ uint64_t load6(const uint8_t *k) {
   const uint16_t *h = reinterpret_cast<const uint16_t *>(k);
   return (uint64_t)h[0] | ((uint64_t)h[1] << 16) | ((uint64_t)h[2] << 32);
 }
 
-__global__ void __launch_bounds__(BLOCK) k_score(const DevPlan *pl, const uint64_t *cand,
-                                                 const uint32_t *lmask, const Loc *loc, uint64_t slot_ub,
-                                                 const Counters *ctr, const uint32_t *surv,
-                                                 const unsigned long long *surv_off,
-                                                 uint64_t *scratch, uint32_t *skey,
-                                                 uint64_t *sdoc) {
+// Mini-merge (Posdb.cpp:6559-6778) of one group's sublist runs for one
+// survivor, one lane per (survivor, group): blockIdx.y = group.  Runs are
+// merged by (u32@+2, u16@0), ties to the lower sublist; BF_BIGRAM keys with
+// F bits set are skipped; the first key becomes 12 bytes, later keys 6 bytes
+// and are dropped when their word position repeats; byte 2's F bits are
+// rewritten from the sublist flags; output capped at 299000 bytes.  NS =
+// sublist capacity (cursors live in registers, indexed by sublist).
+template <int NS>
+__global__ void __launch_bounds__(BLOCK) k_minimerge(const DevPlan *pl, const uint32_t *lmask, const Loc *loc,
+                                                     uint64_t slot_ub, const Counters *ctr, const uint32_t *surv,
+                                                     const unsigned long long *surv_off, uint64_t *arena,
+                                                     GRange *grange) {
+  const int j = blockIdx.y;
+  const int ng = pl->ngroups;
   const uint32_t nsurv = ctr->nsurv;
+  const uint32_t anys = ctr->anysurv;
+  const uint8_t gf0 = pl->gflags0[j];
+  const int gns = pl->gnsub[j];
   for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < nsurv; i += gridDim.x * BLOCK) {
+    if (gf0 & BF_NEGATIVE) {
+      grange[(size_t)i * ng + j] = GRange{0, 0};
+      continue;
+    }
     const uint32_t s = surv[i];
-    const uint64_t docid = cand[s];
     const uint32_t lm = lmask[s];
-    uint64_t *rec = scratch + surv_off[i];
-    DocView dv;
-    dv.rec = rec;
-    int nrec = 0;
-    uint32_t mbytes = 0;  // emulates mptr - mbuf (cap 299000, Posdb.cpp:6007-6008)
-    bool empty_pos = false;
-    int siteRank = -1, docLang = 0;
-    for (int j = 0; j < pl->ngroups; j++) {
-      dv.beg[j] = dv.end[j] = nrec;
-      if (pl->gflags0[j] & BF_NEGATIVE) {
-        dv.present[j] = false;
-        continue;
+    // arena offset: the runs of the groups before this one (k_compact's order)
+    unsigned long long off = surv_off[i];
+    for (int jj = 0; jj < j; jj++) {
+      if (pl->gflags0[jj] & BF_NEGATIVE) continue;
+      for (int x = 0; x < pl->gnsub[jj]; x++) {
+        const int lid = pl->gsub[jj][x];
+        if (lm >> lid & 1) off += loc[(uint64_t)lid * slot_ub + s].len;
       }
-      dv.present[j] = true;
-      MCur cur[MAXSUB];
-      int nsub = 0, newIdx = 0;
-      for (int x = 0; x < pl->gnsub[j]; x++) {
+    }
+    const uint8_t *cp[NS];
+    uint32_t cu[NS], ce[NS];
+    uint64_t ck[NS];
+    uint8_t cfl[NS];
+    bool cfirst[NS], live[NS];
+    int newIdx = 0;
+#pragma unroll
+    for (int x = 0; x < NS; x++) {
+      live[x] = false;
+      cp[x] = nullptr;
+      cu[x] = ce[x] = 0;
+      ck[x] = 0;
+      cfl[x] = 0;
+      cfirst[x] = false;
+      if (x < gns) {
         const int lid = pl->gsub[j][x];
-        if (!(ctr->anysurv >> lid & 1)) continue;  // shrunk to empty: not a new sublist
-        const uint8_t fl = pl->gsubflags[j][newIdx];  // m_bigramFlags[new index]
-        newIdx++;
-        if (!(lm >> lid & 1)) continue;  // no run of this docid in the list
-        const Loc lc = loc[(uint64_t)lid * slot_ub + s];
-        MCur &c = cur[nsub++];
-        c.p = pl->lists[lid].p;
-        c.u = lc.unit;
-        c.end = lc.unit + lc.len;
-        c.flags = fl;
-        c.first = true;
-        c.live = true;
-      }
-      bool isFirstKey = true;
-      uint64_t last = 0;
-      const uint8_t *firstSrc = nullptr;
-      for (;;) {
-        int mink = -1;
-        uint32_t mhi = 0, mlo = 0;
-        for (int k = 0; k < nsub; k++) {
-          if (!cur[k].live) continue;
-          const uint8_t *kp = cur[k].p + (size_t)cur[k].u * 6;
-          const uint32_t hi = gb_u32(kp + 2), lo = gb_u16(kp);
-          if (mink == -1) { mink = k; mhi = hi; mlo = lo; continue; }
-          if (hi > mhi) continue;
-          if (hi == mhi && lo >= mlo) continue;
-          mink = k; mhi = hi; mlo = lo;
-        }
-        if (mink == -1) break;
-        MCur &c = cur[mink];
-        const uint8_t *src = c.p + (size_t)c.u * 6;
-        const bool hack = (c.flags & BF_BIGRAM) && (src[2] & 0x03);  // Posdb.cpp:6687-6692
-        if (!hack) {
-          uint64_t r = load6(src);
-          uint64_t b2 = (r >> 16) & 0xfc;
-          if (c.flags & (BF_BIGRAM | BF_SYNONYM)) b2 |= 0x02;
-          if (c.flags & BF_HALFSTOPWIKIBIGRAM) b2 |= 0x01;
-          r = (r & ~(0xffull << 16)) | (b2 << 16);
-          if (isFirstKey) {
-            r = (r & ~0xffull) | (((r & 0xff) & 0xf9) | 0x02);
-            rec[nrec++] = r;
-            last = r;
-            mbytes += 12;
-            isFirstKey = false;
-            firstSrc = src;
-          } else {
-            const bool dup = (((last >> 32) & 0xffff) == ((r >> 32) & 0xffff)) &&
-                             (((last >> 24) & 0xc0) == ((r >> 24) & 0xc0));
-            if (!dup) {
-              r |= 0x06;
-              rec[nrec++] = r;
-              last = r;
-              mbytes += 6;
-            }
+        if (anys >> lid & 1) {  // shrunk to empty: not a new sublist
+          cfl[x] = pl->gsubflags[j][newIdx];  // m_bigramFlags[new index]
+          newIdx++;
+          if (lm >> lid & 1) {
+            const Loc lc = loc[(uint64_t)lid * slot_ub + s];
+            cp[x] = pl->lists[lid].p;
+            cu[x] = lc.unit;
+            ce[x] = lc.unit + lc.len;
+            ck[x] = load6(cp[x] + (size_t)lc.unit * 6);
+            cfirst[x] = true;
+            live[x] = true;
           }
         }
-        c.u += c.first ? 2 : 1;
-        c.first = false;
-        if (c.u >= c.end) c.live = false;
-        if (mbytes >= 299000) break;
       }
-      dv.end[j] = nrec;
-      if (nrec == dv.beg[j]) empty_pos = true;  // reference reads stale mbuf here (UB)
-      if (siteRank < 0 && firstSrc && !(pl->gflags0[j] & (BF_NUMBER | BF_FACET))) {
-        // Posdb.cpp:6985-7003: group 0 if present, else first present k >= 1
-        siteRank = gb_siterank(firstSrc);
-        docLang = (int)gb_langid(firstSrc);
+    }
+    uint64_t *rec = arena + off;
+    uint32_t nrec = 0;
+    uint32_t mbytes = 0;  // emulates mptr - mbuf (cap 299000, Posdb.cpp:6007-6008)
+    bool isFirstKey = true;
+    uint64_t last = 0;
+    const uint8_t *firstSrc = nullptr;
+    for (;;) {
+      int mink = -1;
+      uint32_t mhi = 0, mlo = 0;
+#pragma unroll
+      for (int x = 0; x < NS; x++) {
+        if (!live[x]) continue;
+        const uint32_t hi = (uint32_t)(ck[x] >> 16), lo = (uint32_t)(ck[x] & 0xffff);
+        if (mink == -1 || hi < mhi || (hi == mhi && lo < mlo)) {
+          mink = x;
+          mhi = hi;
+          mlo = lo;
+        }
+      }
+      if (mink == -1) break;
+      uint64_t r = 0;
+      uint8_t fl = 0;
+      const uint8_t *src = nullptr;
+#pragma unroll
+      for (int x = 0; x < NS; x++) {
+        if (x == mink) {
+          r = ck[x];
+          fl = cfl[x];
+          src = cp[x] + (size_t)cu[x] * 6;
+        }
+      }
+      const bool hack = (fl & BF_BIGRAM) && ((r >> 16) & 0x03);  // Posdb.cpp:6687-6692
+      if (!hack) {
+        uint64_t b2 = (r >> 16) & 0xfc;
+        if (fl & (BF_BIGRAM | BF_SYNONYM)) b2 |= 0x02;
+        if (fl & BF_HALFSTOPWIKIBIGRAM) b2 |= 0x01;
+        r = (r & ~(0xffull << 16)) | (b2 << 16);
+        if (isFirstKey) {
+          r = (r & ~0xffull) | (((r & 0xff) & 0xf9) | 0x02);
+          rec[nrec++] = r;
+          last = r;
+          mbytes += 12;
+          isFirstKey = false;
+          firstSrc = src;
+        } else {
+          const bool dup = (((last >> 32) & 0xffff) == ((r >> 32) & 0xffff)) &&
+                           (((last >> 24) & 0xc0) == ((r >> 24) & 0xc0));
+          if (!dup) {
+            r |= 0x06;
+            rec[nrec++] = r;
+            last = r;
+            mbytes += 6;
+          }
+        }
+      }
+#pragma unroll
+      for (int x = 0; x < NS; x++) {
+        if (x == mink) {
+          cu[x] += cfirst[x] ? 2 : 1;
+          cfirst[x] = false;
+          if (cu[x] >= ce[x]) live[x] = false;
+          else ck[x] = load6(cp[x] + (size_t)cu[x] * 6);
+        }
+      }
+      if (mbytes >= 299000) break;
+    }
+    uint32_t info = nrec | GR_POSITIVE;
+    if (firstSrc) info |= GR_HASFIRST | (gb_siterank(firstSrc) << 17) | (gb_langid(firstSrc) << 21);
+    grange[(size_t)i * ng + j] = GRange{(uint32_t)off, info};
+  }
+}
+
+// Scoring, one lane per survivor (Posdb.cpp:6847-7257 via scoring.h).  NQ =
+// group capacity of this instance; the pair score matrix is an LDS column
+// per lane.
+template <int NQ, int TPB>
+__global__ void __launch_bounds__(TPB) k_score(const DevPlan *pl, const uint64_t *cand, const Counters *ctr,
+                                               const uint32_t *surv, const GRange *grange, const uint64_t *arena,
+                                               uint32_t *skey, uint64_t *sdoc) {
+  __shared__ float s_sm[npairs<NQ>() * TPB];
+  const uint32_t nsurv = ctr->nsurv;
+  const int ng = pl->ngroups;
+  for (uint32_t i = blockIdx.x * TPB + threadIdx.x; i < nsurv; i += gridDim.x * TPB) {
+    DocView<NQ> dv;
+    dv.rec = arena;
+    dv.present = 0;
+    bool empty_pos = false;
+    int siteRank = -1, docLang = 0;
+#pragma unroll
+    for (int j = 0; j < NQ; j++) {
+      dv.beg[j] = dv.end[j] = 0;
+      if (j >= ng) continue;
+      const GRange g = grange[(size_t)i * ng + j];
+      dv.beg[j] = (int)g.start;
+      dv.end[j] = (int)(g.start + (g.info & 0xffff));
+      if (!(g.info & GR_POSITIVE)) continue;
+      dv.present |= 1u << j;
+      if ((g.info & 0xffff) == 0) empty_pos = true;  // reference reads stale mbuf here (UB)
+      if (siteRank < 0 && (g.info & GR_HASFIRST) && !(pl->gflags0[j] & (BF_NUMBER | BF_FACET))) {
+        siteRank = (int)((g.info >> 17) & 0xf);
+        docLang = (int)((g.info >> 21) & 0x3f);
       }
     }
     float score = 0.0f;
-    bool ok = !empty_pos && score_doc(&c_weights, pl, dv, siteRank < 0 ? 0 : siteRank, docLang, &score);
+    const bool ok = !empty_pos && score_doc<NQ>(&c_weights, pl, dv, siteRank < 0 ? 0 : siteRank, docLang,
+                                                s_sm + threadIdx.x, TPB, &score);
     uint32_t key = 0;
     if (ok) {
       const uint32_t b = __float_as_uint(score);
@@ -647,7 +720,7 @@ __global__ void __launch_bounds__(BLOCK) k_score(const DevPlan *pl, const uint64
       if (key == 0) key = 1;
     }
     skey[i] = key;
-    sdoc[i] = docid;
+    sdoc[i] = cand[surv[i]];
   }
 }
 
@@ -658,13 +731,11 @@ __global__ void __launch_bounds__(BLOCK) k_score(const DevPlan *pl, const uint64
 // 19..8, 7..0) finds the k-th key T; keys > T (fewer than k) and keys == T
 // (the ties, of which the smallest docids win) are gathered and sorted in
 // LDS by one block.  Each histogram pass keeps a 4096-bin histogram per block
-// in LDS; the last block to finish (ticket) scans the merged histogram.
+// in LDS, merged with one atomic per non-empty bin; a one-block kernel scans
+// the merged histogram.
 template <int PASS>
-__global__ void __launch_bounds__(BLOCK) k_select_hist(const uint32_t *skey, const Counters *ctr, Select *sel,
-                                                       uint32_t k) {
+__global__ void __launch_bounds__(BLOCK) k_select_hist(const uint32_t *skey, const Counters *ctr, Select *sel) {
   __shared__ uint32_t h[SEL_BINS];
-  __shared__ uint32_t tmp[BLOCK / 64];
-  __shared__ bool s_last;
   if (PASS > 0 && sel->all) return;  // uniform
   constexpr int NB = PASS == 2 ? 256 : SEL_BINS;
   for (int b = threadIdx.x; b < NB; b += BLOCK) h[b] = 0;
@@ -689,24 +760,27 @@ __global__ void __launch_bounds__(BLOCK) k_select_hist(const uint32_t *skey, con
   __syncthreads();
   for (int b = threadIdx.x; b < NB; b += BLOCK)
     if (h[b]) atomicAdd(&sel->hist[PASS][b], h[b]);
-  __threadfence();
-  __syncthreads();
-  if (threadIdx.x == 0) s_last = atomicAdd(&sel->ticket[PASS], 1u) == gridDim.x - 1;
-  __syncthreads();
-  if (!s_last) return;
-  __threadfence();
-  // last block: bins from the top, BPT per thread
+}
+
+// one block: walk the merged histogram from the top to the bin holding the
+// k-th key (the kernel boundary orders it after every block's adds)
+template <int PASS>
+__global__ void __launch_bounds__(BLOCK) k_select_scan(Select *sel, uint32_t k) {
+  __shared__ uint32_t tmp[BLOCK / 64];
+  if (PASS > 0 && sel->all) return;
+  constexpr int NB = PASS == 2 ? 256 : SEL_BINS;
   constexpr int BPT = NB / BLOCK;
   uint32_t c[BPT], sum = 0;
 #pragma unroll
   for (int q = 0; q < BPT; q++) {
-    const int b = NB - 1 - (threadIdx.x * BPT + q);
-    c[q] = __hip_atomic_load(&sel->hist[PASS][b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    c[q] = sel->hist[PASS][NB - 1 - (threadIdx.x * BPT + q)];
     sum += c[q];
   }
   uint32_t total;
   const uint32_t before = block_exclusive_scan(sum, tmp, &total);
   const uint32_t need = PASS == 0 ? k : sel->need;
+  const uint32_t pre = PASS > 0 ? sel->prefix : 0;
+  __syncthreads();  // every thread has read prefix/need before they change
   if (PASS == 0 && total <= need) {
     if (threadIdx.x == 0) sel->all = 1;
     return;
@@ -899,7 +973,7 @@ struct gbgpu_ctx {
   std::mutex mu;
   std::vector<ListEntry> lists;
   // per-query device buffers (grown, then reused)
-  DevBuf tables, chunkcnt, cand, lmask, loc, surv, survoff, scratch, skey, sdoc, sel, gath, res;
+  DevBuf tables, chunkcnt, cand, lmask, loc, surv, survoff, scratch, grange, skey, sdoc, sel, gath, res;
   uint8_t *h_stage = nullptr;  // pinned: query tables (host -> device, one copy)
   size_t stage_cap = 0;
   uint8_t *h_res = nullptr;    // pinned: counters + top list (device -> host, one copy)
@@ -1091,6 +1165,7 @@ static int enqueue(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms, const i
   rc2 |= ctx->surv.ensure(4 * slot_ub);
   rc2 |= ctx->survoff.ensure(8 * slot_ub);
   rc2 |= ctx->scratch.ensure(8 * scratch_ub);
+  rc2 |= ctx->grange.ensure(sizeof(GRange) * slot_ub * (uint64_t)hp.ngroups);
   rc2 |= ctx->skey.ensure(4 * slot_ub);
   rc2 |= ctx->sdoc.ensure(8 * slot_ub);
   rc2 |= ctx->sel.ensure(sizeof(Select));
@@ -1148,17 +1223,48 @@ static int enqueue(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms, const i
   hipLaunchKernelGGL(k_compact, dim3(std::max(cgrid, 1u)), dim3(BLOCK), 0, st, dpl, lmask, loc, slot_ub, dctr,
                      ctx->surv.as<uint32_t>(), ctx->survoff.as<unsigned long long>());
   if (ctx->profiling) HIPCHECK(hipEventRecord(ctx->ev[3], st));
-  const uint32_t sgrid = (uint32_t)std::min<uint64_t>((slot_ub + BLOCK - 1) / BLOCK, 2048);
-  hipLaunchKernelGGL(k_score, dim3(std::max(sgrid, 1u)), dim3(BLOCK), 0, st, dpl, ctx->cand.as<uint64_t>(), lmask,
-                     loc, slot_ub, dctr, ctx->surv.as<uint32_t>(), ctx->survoff.as<unsigned long long>(),
-                     ctx->scratch.as<uint64_t>(), ctx->skey.as<uint32_t>(), ctx->sdoc.as<uint64_t>());
+  {
+    int maxsub = 0;
+    for (int j = 0; j < hp.ngroups; j++)
+      if (!(P.gflags0[j] & BF_NEGATIVE)) maxsub = std::max(maxsub, (int)P.gnsub[j]);
+    const uint32_t mgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((slot_ub + BLOCK - 1) / BLOCK, 1024));
+    GRange *dgr = ctx->grange.as<GRange>();
+    uint64_t *arena = ctx->scratch.as<uint64_t>();
+    const uint32_t *dsurv = ctx->surv.as<uint32_t>();
+    if (maxsub <= 4)
+      hipLaunchKernelGGL(k_minimerge<4>, dim3(mgrid, hp.ngroups), dim3(BLOCK), 0, st, dpl, lmask, loc, slot_ub, dctr,
+                         dsurv, ctx->survoff.as<unsigned long long>(), arena, dgr);
+    else
+      hipLaunchKernelGGL(k_minimerge<MAXSUB>, dim3(mgrid, hp.ngroups), dim3(BLOCK), 0, st, dpl, lmask, loc, slot_ub,
+                         dctr, dsurv, ctx->survoff.as<unsigned long long>(), arena, dgr);
+    const uint32_t sg256 = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((slot_ub + 255) / 256, 2048));
+    const uint32_t sg64 = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((slot_ub + 63) / 64, 8192));
+    const uint64_t *dcand = ctx->cand.as<uint64_t>();
+    uint32_t *dskey = ctx->skey.as<uint32_t>();
+    uint64_t *dsdoc = ctx->sdoc.as<uint64_t>();
+    if (hp.ngroups <= 2)
+      hipLaunchKernelGGL((k_score<2, 256>), dim3(sg256), dim3(256), 0, st, dpl, dcand, dctr, dsurv, dgr, arena, dskey,
+                         dsdoc);
+    else if (hp.ngroups <= 4)
+      hipLaunchKernelGGL((k_score<4, 256>), dim3(sg256), dim3(256), 0, st, dpl, dcand, dctr, dsurv, dgr, arena, dskey,
+                         dsdoc);
+    else if (hp.ngroups <= 8)
+      hipLaunchKernelGGL((k_score<8, 256>), dim3(sg256), dim3(256), 0, st, dpl, dcand, dctr, dsurv, dgr, arena, dskey,
+                         dsdoc);
+    else
+      hipLaunchKernelGGL((k_score<MAXG, 64>), dim3(sg64), dim3(64), 0, st, dpl, dcand, dctr, dsurv, dgr, arena, dskey,
+                         dsdoc);
+  }
   if (ctx->profiling) HIPCHECK(hipEventRecord(ctx->ev[4], st));
   // top-k: radix select over the survivors' keys, then one LDS sort
-  const uint32_t hgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(256, (slot_ub + 1023) / 1024));
+  const uint32_t hgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(64, (slot_ub + 4095) / 4096));
   const uint32_t *skey = ctx->skey.as<uint32_t>();
-  hipLaunchKernelGGL(k_select_hist<0>, dim3(hgrid), dim3(BLOCK), 0, st, skey, dctr, dsel, (uint32_t)k);
-  hipLaunchKernelGGL(k_select_hist<1>, dim3(hgrid), dim3(BLOCK), 0, st, skey, dctr, dsel, (uint32_t)k);
-  hipLaunchKernelGGL(k_select_hist<2>, dim3(hgrid), dim3(BLOCK), 0, st, skey, dctr, dsel, (uint32_t)k);
+  hipLaunchKernelGGL(k_select_hist<0>, dim3(hgrid), dim3(BLOCK), 0, st, skey, dctr, dsel);
+  hipLaunchKernelGGL(k_select_scan<0>, dim3(1), dim3(BLOCK), 0, st, dsel, (uint32_t)k);
+  hipLaunchKernelGGL(k_select_hist<1>, dim3(hgrid), dim3(BLOCK), 0, st, skey, dctr, dsel);
+  hipLaunchKernelGGL(k_select_scan<1>, dim3(1), dim3(BLOCK), 0, st, dsel, (uint32_t)k);
+  hipLaunchKernelGGL(k_select_hist<2>, dim3(hgrid), dim3(BLOCK), 0, st, skey, dctr, dsel);
+  hipLaunchKernelGGL(k_select_scan<2>, dim3(1), dim3(BLOCK), 0, st, dsel, (uint32_t)k);
   uint32_t *akey = ctx->gath.as<uint32_t>();
   uint64_t *adoc = ctx->gath.as<uint64_t>(align256(4 * (size_t)MAX_K));
   uint32_t *bkey = ctx->gath.as<uint32_t>(align256(4 * (size_t)MAX_K) + align256(8 * (size_t)MAX_K));
@@ -1259,7 +1365,7 @@ void gbgpu_close(gbgpu_ctx *ctx) {
   for (auto &e : ctx->lists)
     if (e.live) (void)hipFree(e.d);
   DevBuf *bufs[] = {&ctx->tables, &ctx->chunkcnt, &ctx->cand, &ctx->lmask, &ctx->loc, &ctx->surv,
-                    &ctx->survoff, &ctx->scratch, &ctx->skey, &ctx->sdoc, &ctx->sel, &ctx->gath, &ctx->res};
+                    &ctx->survoff, &ctx->scratch, &ctx->grange, &ctx->skey, &ctx->sdoc, &ctx->sel, &ctx->gath, &ctx->res};
   for (auto *b : bufs) b->release();
   if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
   if (ctx->h_res) (void)hipHostFree(ctx->h_res);

@@ -7,6 +7,13 @@
 // char pointers; expression shapes (float vs double promotion, operand
 // order) follow the reference exactly so results round identically
 // (compiled with -ffp-contract=off).
+//
+// Register residency: the per-docid state of the reference (top-10 score
+// slots, window cursors, per-term best positions) is kept in fixed-size
+// register arrays -- every loop over them is unrolled to a compile-time bound
+// and runtime indices go through rget/rset select chains -- so nothing spills
+// to scratch.  NQ (the kernel's group capacity) is a template parameter; the
+// term-pair score matrix lives in LDS, one column per lane.
 #ifndef GBGPU_SCORING_H
 #define GBGPU_SCORING_H
 
@@ -43,50 +50,89 @@ __host__ __device__ __forceinline__ uint32_t r_syn(uint64_t r) { return (uint32_
 __host__ __device__ __forceinline__ uint32_t r_hswb(uint64_t r) { return (uint32_t)(r >> 16) & 0x1; }
 __host__ __device__ __forceinline__ uint32_t r_dens(uint64_t r) { return (uint32_t)(r >> 11) & 0x1f; }
 
+// register-array access with a runtime index (unrolled select chains)
+template <int N, class T>
+__device__ __forceinline__ T rget(const T (&a)[N], int i) {
+  T v = a[0];
+#pragma unroll
+  for (int q = 1; q < N; q++) v = (q == i) ? a[q] : v;
+  return v;
+}
+template <int N, class T>
+__device__ __forceinline__ void rset(T (&a)[N], int i, T v) {
+#pragma unroll
+  for (int q = 0; q < N; q++)
+    if (q == i) a[q] = v;
+}
+
+// index of pair (i, j), i < j, in the upper triangle of an NQ x NQ matrix
+template <int NQ>
+__device__ __forceinline__ int pair_index(int i, int j) {
+  return i * (2 * NQ - i - 1) / 2 + (j - i - 1);
+}
+template <int NQ>
+constexpr int npairs() {
+  return NQ * (NQ - 1) / 2;
+}
+
 // What one docid's scorer sees: nq groups, each a record range.
+template <int NQ>
 struct DocView {
-  const uint64_t *rec;  // records of this docid (all groups back to back)
-  int beg[MAXG], end[MAXG];
-  bool present[MAXG];   // miniMergedList[j] != NULL (positive group)
+  const uint64_t *rec;  // record arena (ranges are absolute indices)
+  int beg[NQ], end[NQ];
+  uint32_t present;     // bit i: miniMergedList[i] != NULL (positive group)
 };
 
+template <int NQ>
 struct ScoreCtx {
   const Weights *w;
   const DevPlan *pl;
   int nq;
-  uint8_t bflags[MAXG];
   int realMaxTop;
   int qdist;             // PosdbTable::m_qdist (set by evalSlidingWindow)
   float bestWindowScore; // m_bestWindowScore
-  int window[MAXG];      // m_windowTermPtrs (record index, -1 = NULL)
+  int window[NQ];        // m_windowTermPtrs (record index, -1 = NULL)
+  float *sm;             // score matrix column of this lane (LDS), stride smStride
+  int smStride;
+  uint32_t excl;         // bit i: group i is piped/negative/number/facet (BF_EXCLUDE)
 };
 
 // getSingleTermScore, Posdb.cpp:3087-3301 (pdcs == NULL).  bestPos = record
 // index of the best non-body occurrence or -1.
-__device__ inline float single_term_score(const ScoreCtx &c, const DocView &d, int i, int *bestPos) {
+template <int NQ>
+__device__ __forceinline__ float single_term_score(const ScoreCtx<NQ> &c, const DocView<NQ> &d, int i, int *bestPos) {
   const Weights &W = *c.w;
   float nonBodyMax = -1.0;
   int minx = 0;
+  float minv = 0.0f;  // bestScores[minx]
   float bestScores[MAX_TOP];
   int bestwpi[MAX_TOP];
-  uint8_t bestmhg[MAX_TOP];
+  uint32_t bestmhg[MAX_TOP];
+#pragma unroll
+  for (int q = 0; q < MAX_TOP; q++) {
+    bestScores[q] = 0.0f;
+    bestwpi[q] = 0;
+    bestmhg[q] = 0xff;
+  }
   int numTop = 0;
-  *bestPos = -1;
-  for (int r = d.beg[i]; r < d.end[i]; r++) {
-    uint64_t k = d.rec[r];
+  int bp = -1;
+  const int rmt = c.realMaxTop;
+  const int e = rget(d.end, i);
+  for (int r = rget(d.beg, i); r < e; r++) {
+    const uint64_t k = d.rec[r];
     float score = 100.0;
-    uint32_t div = r_div(k);
+    const uint32_t div = r_div(k);
     score *= W.diversity[div];
     score *= W.diversity[div];
-    uint32_t hg = r_hg(k);
+    const uint32_t hg = r_hg(k);
     uint32_t mhg = hg;
     if (W.in_body[mhg]) mhg = GB_HG_BODY;
     score *= W.hashgroup[hg];
     score *= W.hashgroup[hg];
-    uint32_t dens = r_dens(k);
+    const uint32_t dens = r_dens(k);
     score *= W.density[dens];
     score *= W.density[dens];
-    uint32_t wspam = r_wsr(k);
+    const uint32_t wspam = r_wsr(k);
     if (hg == GB_HG_INLINKTEXT) {
       score *= W.linker[wspam];
       score *= W.linker[wspam];
@@ -98,44 +144,61 @@ __device__ inline float single_term_score(const ScoreCtx &c, const DocView &d, i
       score *= GB_SYNONYM_WEIGHT;
       score *= GB_SYNONYM_WEIGHT;
     }
+    // same modified hash group already in the top list (not inlink text)
     int bro = -1;
-    for (int q = 0; q < numTop; q++) {
-      if (bestmhg[q] == mhg && hg != GB_HG_INLINKTEXT) { bro = q; break; }
-    }
-    if (bro >= 0) {
-      if (score > bestScores[bro]) {
-        bestScores[bro] = score;
-        bestwpi[bro] = r;
-        bestmhg[bro] = (uint8_t)mhg;
+    float broScore = 0.0f;
+    if (hg != GB_HG_INLINKTEXT) {
+#pragma unroll
+      for (int q = MAX_TOP - 1; q >= 0; q--) {
+        if (q < numTop && bestmhg[q] == mhg) {  // lowest matching slot
+          bro = q;
+          broScore = bestScores[q];
+        }
       }
-    } else if (numTop < c.realMaxTop) {
-      bestScores[numTop] = score;
-      bestwpi[numTop] = r;
-      bestmhg[numTop] = (uint8_t)mhg;
-      numTop++;
-    } else if (score > bestScores[minx]) {
-      bestScores[minx] = score;
-      bestwpi[minx] = r;
-      bestmhg[minx] = (uint8_t)mhg;
     }
-    if (numTop >= c.realMaxTop) {
+    int slot = -1;
+    if (bro >= 0) {
+      if (score > broScore) slot = bro;
+    } else if (numTop < rmt) {
+      slot = numTop;
+      numTop++;
+    } else if (score > minv) {
+      slot = minx;
+    }
+#pragma unroll
+    for (int q = 0; q < MAX_TOP; q++) {
+      if (q == slot) {
+        bestScores[q] = score;
+        bestwpi[q] = r;
+        bestmhg[q] = mhg;
+      }
+    }
+    if (numTop >= rmt) {
       minx = 0;
-      for (int q = 1; q < c.realMaxTop; q++) {
-        if (bestScores[q] > bestScores[minx]) continue;
-        minx = q;
+      minv = bestScores[0];
+#pragma unroll
+      for (int q = 1; q < MAX_TOP; q++) {
+        if (q < rmt && !(bestScores[q] > minv)) {
+          minx = q;
+          minv = bestScores[q];
+        }
       }
     }
     if (score > nonBodyMax && !W.in_body[hg]) {
       nonBodyMax = score;
-      *bestPos = r;
+      bp = r;
     }
   }
+  *bestPos = bp;
   float sum = 0.0;
-  for (int q = 0; q < numTop; q++) {
-    if (r_hswb(d.rec[bestwpi[q]]))
-      sum += (bestScores[q] * GB_WIKI_BIGRAM_WEIGHT * GB_WIKI_BIGRAM_WEIGHT);
-    else
-      sum += bestScores[q];
+#pragma unroll
+  for (int q = 0; q < MAX_TOP; q++) {
+    if (q < numTop) {
+      if (r_hswb(d.rec[bestwpi[q]]))
+        sum += (bestScores[q] * GB_WIKI_BIGRAM_WEIGHT * GB_WIKI_BIGRAM_WEIGHT);
+      else
+        sum += bestScores[q];
+    }
   }
   sum *= c.pl->tfw[i];
   sum *= c.pl->tfw[i];
@@ -143,10 +206,11 @@ __device__ inline float single_term_score(const ScoreCtx &c, const DocView &d, i
 }
 
 // getTermPairScoreForNonBody, Posdb.cpp:3305-3555
-__device__ inline float pair_score_nonbody(const ScoreCtx &c, const DocView &d, int i, int j, int qdist) {
+template <int NQ>
+__device__ __forceinline__ float pair_score_nonbody(const ScoreCtx<NQ> &c, const DocView<NQ> &d, int i, int j, int qdist) {
   const Weights &W = *c.w;
-  int wi = d.beg[i], wj = d.beg[j];
-  const int endi = d.end[i], endj = d.end[j];
+  int wi = rget(d.beg, i), wj = rget(d.beg, j);
+  const int endi = rget(d.end, i), endj = rget(d.end, j);
   uint64_t ki = d.rec[wi], kj = d.rec[wj];
   int32_t p1 = (int32_t)r_wordpos(ki), p2 = (int32_t)r_wordpos(kj);
   uint32_t hg1 = r_hg(ki), hg2 = r_hg(kj);
@@ -211,18 +275,17 @@ __device__ inline float pair_score_nonbody(const ScoreCtx &c, const DocView &d, 
 }
 
 // getTermPairScoreForWindow, Posdb.cpp:3557-3625 (record index -1 = NULL)
-__device__ inline float pair_score_window(const ScoreCtx &c, const DocView &d, int wpi, int wpj,
+__device__ __forceinline__ float pair_score_window(const Weights &W, int cqdist, const uint64_t *rec, int wpi, int wpj,
                                           int32_t fixedDistance) {
   if (wpi < 0) return -1.00;
   if (wpj < 0) return -1.00;
-  const Weights &W = *c.w;
-  uint64_t ki = d.rec[wpi], kj = d.rec[wpj];
-  int32_t p1 = (int32_t)r_wordpos(ki), p2 = (int32_t)r_wordpos(kj);
-  uint32_t hg1 = r_hg(ki), hg2 = r_hg(kj);
-  float spamw1 = (hg1 == GB_HG_INLINKTEXT) ? W.linker[r_wsr(ki)] : W.wordspam[r_wsr(ki)];
-  float spamw2 = (hg2 == GB_HG_INLINKTEXT) ? W.linker[r_wsr(kj)] : W.wordspam[r_wsr(kj)];
-  float denw1 = W.density[r_dens(ki)];
-  float denw2 = W.density[r_dens(kj)];
+  const uint64_t ki = rec[wpi], kj = rec[wpj];
+  const int32_t p1 = (int32_t)r_wordpos(ki), p2 = (int32_t)r_wordpos(kj);
+  const uint32_t hg1 = r_hg(ki), hg2 = r_hg(kj);
+  const float spamw1 = (hg1 == GB_HG_INLINKTEXT) ? W.linker[r_wsr(ki)] : W.wordspam[r_wsr(ki)];
+  const float spamw2 = (hg2 == GB_HG_INLINKTEXT) ? W.linker[r_wsr(kj)] : W.wordspam[r_wsr(kj)];
+  const float denw1 = W.density[r_dens(ki)];
+  const float denw2 = W.density[r_dens(kj)];
   float dist, score;
   if (fixedDistance != 0) {
     dist = fixedDistance;
@@ -230,7 +293,7 @@ __device__ inline float pair_score_window(const ScoreCtx &c, const DocView &d, i
     if (p2 < p1) dist = p1 - p2;
     else dist = p2 - p1;
     if (dist < 2) dist = 2;
-    if (dist >= c.qdist) dist = dist - c.qdist;
+    if (dist >= cqdist) dist = dist - cqdist;
     if (p2 < p1) dist += 1;
   }
   score = 100 * denw1 * denw2;
@@ -244,44 +307,50 @@ __device__ inline float pair_score_window(const ScoreCtx &c, const DocView &d, i
 }
 
 // evalSlidingWindow, Posdb.cpp:1275-1511
-__device__ inline void eval_window(ScoreCtx &c, const DocView &d, const int *ptrs, const int *bestPos,
-                                   const float *scoreMatrix) {
+template <int NQ>
+__device__ __forceinline__ void eval_window(ScoreCtx<NQ> &c, const DocView<NQ> &d, const int (&ptrs)[NQ],
+                                   const int (&bestPos)[NQ]) {
+  const Weights &W = *c.w;
+  const DevPlan *pl = c.pl;
   float minTermPairScoreInWindow = 999999999.0;
   const int nr = c.nq;
   for (int i = 0; i < nr; i++) {
-    if (c.bflags[i] & BF_EXCLUDE) continue;
-    int wpi = ptrs[i];
+    if ((c.excl >> i & 1)) continue;
+    const int wpi = rget(ptrs, i);
+    const int bpi = rget(bestPos, i);
     for (int j = i + 1; j < nr; j++) {
-      if (c.bflags[j] & BF_EXCLUDE) continue;
-      int wpj = ptrs[j];
+      if ((c.excl >> j & 1)) continue;
+      const int wpj = rget(ptrs, j);
+      const int bpj = rget(bestPos, j);
       float wikiWeight;
-      if (c.pl->wiki[j] == c.pl->wiki[i] && c.pl->wiki[j]) {
-        c.qdist = c.pl->qpos[j] - c.pl->qpos[i];
+      if (pl->wiki[j] == pl->wiki[i] && pl->wiki[j]) {
+        c.qdist = pl->qpos[j] - pl->qpos[i];
         wikiWeight = GB_WIKI_WEIGHT;
       } else {
         c.qdist = 2;
         wikiWeight = 1.0;
       }
-      float max = pair_score_window(c, d, wpi, wpj, 0);
-      float score = pair_score_window(c, d, bestPos[i], wpj, FIXED_DISTANCE);
+      float max = pair_score_window(W, c.qdist, d.rec, wpi, wpj, 0);
+      float score = pair_score_window(W, c.qdist, d.rec, bpi, wpj, FIXED_DISTANCE);
       if (score > max) max = score;
-      score = pair_score_window(c, d, bestPos[i], bestPos[j], FIXED_DISTANCE);
+      score = pair_score_window(W, c.qdist, d.rec, bpi, bpj, FIXED_DISTANCE);
       if (score > max) max = score;
-      score = pair_score_window(c, d, wpi, bestPos[j], FIXED_DISTANCE);
+      score = pair_score_window(W, c.qdist, d.rec, wpi, bpj, FIXED_DISTANCE);
       if (score > max) max = score;
       if (wikiWeight != 1.0) max *= wikiWeight;
-      max *= c.pl->tfw[i] * c.pl->tfw[j];
-      if (scoreMatrix[i * MAXG + j] > max) max = scoreMatrix[i * MAXG + j];
-      if (c.pl->quote[j] >= 0 && c.pl->quote[j] == c.pl->quote[i]) {
+      max *= pl->tfw[i] * pl->tfw[j];
+      const float smv = c.sm[pair_index<NQ>(i, j) * c.smStride];
+      if (smv > max) max = smv;
+      if (pl->quote[j] >= 0 && pl->quote[j] == pl->quote[i]) {
         if (wpi < 0) {
           max = -1.0;
         } else if (wpj < 0) {
           max = -1.0;
         } else {
-          int32_t qd = c.pl->qpos[j] - c.pl->qpos[i];
-          int32_t p1 = (int32_t)r_wordpos(d.rec[wpi]);
-          int32_t p2 = (int32_t)r_wordpos(d.rec[wpj]);
-          int32_t dist = p2 - p1;
+          const int32_t qd = pl->qpos[j] - pl->qpos[i];
+          const int32_t p1 = (int32_t)r_wordpos(d.rec[wpi]);
+          const int32_t p2 = (int32_t)r_wordpos(d.rec[wpj]);
+          const int32_t dist = p2 - p1;
           if (dist < 0) max = -1.0;
           else if (dist > qd && dist - qd > 1) max = -1.0;
           else if (dist < qd && qd - dist > 1) max = -1.0;
@@ -292,25 +361,29 @@ __device__ inline void eval_window(ScoreCtx &c, const DocView &d, const int *ptr
   }
   if (minTermPairScoreInWindow <= c.bestWindowScore) return;
   c.bestWindowScore = minTermPairScoreInWindow;
-  for (int i = 0; i < nr; i++) c.window[i] = ptrs[i];
+#pragma unroll
+  for (int q = 0; q < NQ; q++) c.window[q] = ptrs[q];
 }
 
 // getTermPairScoreForAny, Posdb.cpp:3631-4344 (pdcs == NULL)
-__device__ inline float pair_score_any(const ScoreCtx &c, const DocView &d, int i, int j) {
+template <int NQ>
+__device__ __forceinline__ float pair_score_any(const ScoreCtx<NQ> &c, const DocView<NQ> &d, int i, int j) {
   const Weights &W = *c.w;
+  const DevPlan *pl = c.pl;
   float wts;
   int32_t qdist;
-  if (c.pl->wiki[j] == c.pl->wiki[i] && c.pl->wiki[j]) {
-    qdist = c.pl->qpos[j] - c.pl->qpos[i];
+  if (pl->wiki[j] == pl->wiki[i] && pl->wiki[j]) {
+    qdist = pl->qpos[j] - pl->qpos[i];
     wts = (float)GB_WIKI_WEIGHT;
   } else {
     qdist = 2;
     wts = 1.0;
   }
-  const bool inSameQuotedPhrase = (c.pl->quote[i] == c.pl->quote[j] && c.pl->quote[i] >= 0);
-  if (inSameQuotedPhrase) qdist = c.pl->qpos[j] - c.pl->qpos[i];
-  int wi = d.beg[i], wj = d.beg[j];
-  const int endi = d.end[i], endj = d.end[j];
+  const bool inSameQuotedPhrase = (pl->quote[i] == pl->quote[j] && pl->quote[i] >= 0);
+  if (inSameQuotedPhrase) qdist = pl->qpos[j] - pl->qpos[i];
+  const int wini = rget(c.window, i), winj = rget(c.window, j);
+  int wi = rget(d.beg, i), wj = rget(d.beg, j);
+  const int endi = rget(d.end, i), endj = rget(d.end, j);
   uint64_t ki = d.rec[wi], kj = d.rec[wj];
   int32_t p1 = (int32_t)r_wordpos(ki), p2 = (int32_t)r_wordpos(kj);
   uint32_t hg1 = r_hg(ki), hg2 = r_hg(kj);
@@ -320,17 +393,26 @@ __device__ inline float pair_score_any(const ScoreCtx &c, const DocView &d, int 
   float spamw2 = (hg2 == GB_HG_INLINKTEXT) ? W.linker[r_wsr(kj)] : W.wordspam[r_wsr(kj)];
   float denw1 = W.density[r_dens(ki)];
   float denw2 = W.density[r_dens(kj)];
-  float score;
+  float score = 0.0f;
   int minx = -1;
+  float minv = 0.0f;  // bestScores[minx]
   float bestScores[MAX_TOP];
-  uint8_t bestmhg1[MAX_TOP], bestmhg2[MAX_TOP];
+  uint32_t bestmhg1[MAX_TOP], bestmhg2[MAX_TOP];
+#pragma unroll
+  for (int q = 0; q < MAX_TOP; q++) {
+    bestScores[q] = 0.0f;
+    bestmhg1[q] = 0xff;
+    bestmhg2[q] = 0xff;
+  }
   int numTop = 0;
+  const int rmt = c.realMaxTop;
   int32_t dist;
   for (;;) {
     bool adv1;
-    if (W.in_body[hg1] && wi != c.window[i]) {
+    bool scored = false;
+    if (W.in_body[hg1] && wi != wini) {
       adv1 = true;
-    } else if (W.in_body[hg2] && wj != c.window[j]) {
+    } else if (W.in_body[hg2] && wj != winj) {
       adv1 = false;
     } else if (p1 <= p2) {
       adv1 = true;
@@ -341,7 +423,7 @@ __device__ inline float pair_score_any(const ScoreCtx &c, const DocView &d, int 
         if (dist < qdist && qdist - dist >= 2) skip = true;
       }
       if (!skip) {
-        uint32_t syn1 = r_syn(ki), syn2 = r_syn(kj);
+        const uint32_t syn1 = r_syn(ki), syn2 = r_syn(kj);
         if (dist < 2) dist = 2;
         if (dist < 50) {
         } else if (mhg1 != mhg2) {
@@ -359,7 +441,7 @@ __device__ inline float pair_score_any(const ScoreCtx &c, const DocView &d, int 
         if (r_hswb(kj)) score *= GB_WIKI_BIGRAM_WEIGHT;
         score *= spamw1 * spamw2;
         score /= (dist + 1.0);
-        goto topScores;
+        scored = true;
       }
     } else {
       adv1 = false;
@@ -385,41 +467,49 @@ __device__ inline float pair_score_any(const ScoreCtx &c, const DocView &d, int 
         if (r_syn(kj)) score *= GB_SYNONYM_WEIGHT;
         score *= spamw1 * spamw2;
         score /= (dist + 1.0);
-        goto topScores;
+        scored = true;
       }
     }
-    goto advance;
-  topScores : {
-    int bro = -1;
-    for (int q = 0; q < numTop; q++) {
-      if (bestmhg1[q] == mhg1 && hg1 != GB_HG_INLINKTEXT) { bro = q; break; }
-      if (bestmhg2[q] == mhg2 && hg2 != GB_HG_INLINKTEXT) { bro = q; break; }
-    }
-    if (bro >= 0) {
-      if (score > bestScores[bro]) {
-        bestScores[bro] = score;
-        bestmhg1[bro] = (uint8_t)mhg1;
-        bestmhg2[bro] = (uint8_t)mhg2;
+    if (scored) {  // the topScores block, Posdb.cpp:3875-3922
+      int bro = -1;
+      float broScore = 0.0f;
+#pragma unroll
+      for (int q = MAX_TOP - 1; q >= 0; q--) {
+        if (q < numTop && ((bestmhg1[q] == mhg1 && hg1 != GB_HG_INLINKTEXT) ||
+                           (bestmhg2[q] == mhg2 && hg2 != GB_HG_INLINKTEXT))) {
+          bro = q;  // lowest matching slot
+          broScore = bestScores[q];
+        }
       }
-    } else if (numTop < c.realMaxTop) {
-      bestScores[numTop] = score;
-      bestmhg1[numTop] = (uint8_t)mhg1;
-      bestmhg2[numTop] = (uint8_t)mhg2;
-      numTop++;
-    } else if (score > bestScores[minx]) {
-      bestScores[minx] = score;
-      bestmhg1[minx] = (uint8_t)mhg1;
-      bestmhg2[minx] = (uint8_t)mhg2;
-    }
-    if (numTop >= c.realMaxTop) {
-      minx = 0;
-      for (int q = 1; q < c.realMaxTop; q++) {
-        if (bestScores[q] > bestScores[minx]) continue;
-        minx = q;
+      int slot = -1;
+      if (bro >= 0) {
+        if (score > broScore) slot = bro;
+      } else if (numTop < rmt) {
+        slot = numTop;
+        numTop++;
+      } else if (score > minv) {
+        slot = minx;
+      }
+#pragma unroll
+      for (int q = 0; q < MAX_TOP; q++) {
+        if (q == slot) {
+          bestScores[q] = score;
+          bestmhg1[q] = mhg1;
+          bestmhg2[q] = mhg2;
+        }
+      }
+      if (numTop >= rmt) {
+        minx = 0;
+        minv = bestScores[0];
+#pragma unroll
+        for (int q = 1; q < MAX_TOP; q++) {
+          if (q < rmt && !(bestScores[q] > minv)) {
+            minx = q;
+            minv = bestScores[q];
+          }
+        }
       }
     }
-  }
-  advance:
     if (adv1) {
       if (++wi >= endi) break;
       ki = d.rec[wi];
@@ -439,33 +529,40 @@ __device__ inline float pair_score_any(const ScoreCtx &c, const DocView &d, int 
     }
   }
   float sum = 0.0;
-  for (int q = 0; q < numTop; q++) sum += bestScores[q];
+#pragma unroll
+  for (int q = 0; q < MAX_TOP; q++)
+    if (q < numTop) sum += bestScores[q];
   sum *= wts;
-  sum *= c.pl->tfw[i];
-  sum *= c.pl->tfw[j];
+  sum *= pl->tfw[i];
+  sum *= pl->tfw[j];
   return sum;
 }
 
 // The per-docid body of intersectLists10_r after the mini merges
 // (Posdb.cpp:6847-7257).  Returns false when the docid is not scored
 // (minScore <= 0); siteRank/docLang come from the first key of the first
-// present group (Posdb.cpp:6985-7003).
-__device__ inline bool score_doc(const Weights *w, const DevPlan *pl, const DocView &d, int siteRank,
-                                 int docLang, float *outScore) {
-  ScoreCtx c;
+// present group (Posdb.cpp:6985-7003).  sm: this lane's score-matrix column
+// (npairs<NQ>() floats at stride smStride).
+template <int NQ>
+__device__ __forceinline__ bool score_doc(const Weights *w, const DevPlan *pl, const DocView<NQ> &d, int siteRank, int docLang,
+                                 float *sm, int smStride, float *outScore) {
+  ScoreCtx<NQ> c;
   c.w = w;
   c.pl = pl;
   c.nq = pl->ngroups;
   c.realMaxTop = pl->real_max_top;
   c.qdist = 2;
-  for (int i = 0; i < c.nq; i++) c.bflags[i] = pl->gflags0[i];
-  float scoreMatrix[MAXG * MAXG];
-  int bestPos[MAXG];
+  c.sm = sm;
+  c.smStride = smStride;
+  c.excl = 0;
+  for (int i = 0; i < c.nq; i++)
+    if (pl->gflags0[i] & BF_EXCLUDE) c.excl |= 1u << i;
+  int bestPos[NQ];
   // non-body pair scores, Posdb.cpp:6847-6926
   for (int i = 0; i < c.nq; i++) {
-    if (c.bflags[i] & BF_EXCLUDE) continue;
+    if ((c.excl >> i & 1)) continue;
     for (int j = i + 1; j < c.nq; j++) {
-      if (c.bflags[j] & BF_EXCLUDE) continue;
+      if ((c.excl >> j & 1)) continue;
       int32_t qdist;
       float wts;
       if (pl->wiki[j] == pl->wiki[i] && pl->wiki[j]) {
@@ -476,76 +573,87 @@ __device__ inline bool score_doc(const Weights *w, const DevPlan *pl, const DocV
         wts = 1.0;
       }
       float pss = 0.0;
-      if (d.present[i] && d.present[j]) pss = pair_score_nonbody(c, d, i, j, qdist);
+      if ((d.present >> i & 1) && (d.present >> j & 1)) pss = pair_score_nonbody(c, d, i, j, qdist);
+      float v;
       if (pss < 0) {
-        scoreMatrix[i * MAXG + j] = -1.00;
+        v = -1.00;
       } else {
         wts *= pss;
         wts *= pl->tfw[i];
         wts *= pl->tfw[j];
-        scoreMatrix[i * MAXG + j] = wts;
+        v = wts;
       }
+      sm[pair_index<NQ>(i, j) * smStride] = v;
     }
   }
   // single term scores, Posdb.cpp:6933-6978
   float minSingleScore = 999999999.0;
+#pragma unroll
+  for (int i = 0; i < NQ; i++) bestPos[i] = -1;
   for (int i = 0; i < c.nq; i++) {
-    bestPos[i] = -1;
-    if (c.bflags[i] & BF_EXCLUDE) continue;
-    float sts = single_term_score(c, d, i, &bestPos[i]);
+    if ((c.excl >> i & 1)) continue;
+    int bp;
+    const float sts = single_term_score(c, d, i, &bp);
+    rset(bestPos, i, bp);
     if (sts < minSingleScore) minSingleScore = sts;
   }
   // sliding window, Posdb.cpp:7013-7150
   c.bestWindowScore = -2.0;
-  int xpos[MAXG];
-  for (int i = 0; i < c.nq; i++) {
-    xpos[i] = d.present[i] ? d.beg[i] : -1;
+  int xpos[NQ];
+#pragma unroll
+  for (int i = 0; i < NQ; i++) {
+    xpos[i] = (i < c.nq && (d.present >> i & 1)) ? d.beg[i] : -1;
     c.window[i] = -1;
   }
   bool allNull = true;
-  for (int i = 0; i < c.nq; i++) {
-    if (c.bflags[i] & BF_EXCLUDE) continue;
-    while (xpos[i] >= 0 && !w->in_body[r_hg(d.rec[xpos[i]])]) {
-      xpos[i]++;
-      if (xpos[i] < d.end[i]) continue;
-      xpos[i] = -1;
+#pragma unroll
+  for (int i = 0; i < NQ; i++) {
+    if (i < c.nq && !(c.excl >> i & 1)) {
+      int xp = xpos[i];
+      while (xp >= 0 && !w->in_body[r_hg(d.rec[xp])]) {
+        xp++;
+        if (xp >= d.end[i]) xp = -1;
+      }
+      xpos[i] = xp;
+      if (xp >= 0) allNull = false;
     }
-    if (xpos[i] >= 0) allNull = false;
   }
   if (!allNull) {
     for (;;) {
-      eval_window(c, d, xpos, bestPos, scoreMatrix);
+      eval_window(c, d, xpos, bestPos);
       bool done = false;
       for (;;) {  // advanceMin
         int minx = -1;
         uint32_t minPos = 0;
-        for (int x = 0; x < c.nq; x++) {
-          if (c.bflags[x] & BF_EXCLUDE) continue;
-          if (xpos[x] < 0) continue;
-          uint32_t wp = r_wordpos(d.rec[xpos[x]]);
-          if (minx == -1) { minx = x; minPos = wp; continue; }
-          if (wp >= minPos) continue;
-          minx = x;
-          minPos = wp;
+#pragma unroll
+        for (int x = 0; x < NQ; x++) {
+          if (x < c.nq && !(c.excl >> x & 1) && xpos[x] >= 0) {
+            const uint32_t wp = r_wordpos(d.rec[xpos[x]]);
+            if (minx == -1 || wp < minPos) {
+              minx = x;
+              minPos = wp;
+            }
+          }
         }
-        bool again = true;
+        int xp = rget(xpos, minx);
+        const int xe = rget(d.end, minx);
         bool exhausted = false;
-        while (again) {  // advanceAgain
-          xpos[minx]++;
-          if (xpos[minx] >= d.end[minx]) {
-            xpos[minx] = -1;
+        for (;;) {  // advanceAgain
+          xp++;
+          if (xp >= xe) {
+            xp = -1;
             exhausted = true;
             break;
           }
-          again = !w->in_body[r_hg(d.rec[xpos[minx]])];
+          if (w->in_body[r_hg(d.rec[xp])]) break;
         }
+        rset(xpos, minx, xp);
         if (!exhausted) break;  // -> slideMore
-        int k;
-        for (k = 0; k < c.nq; k++) {
-          if (c.bflags[k] & BF_EXCLUDE) continue;
-          if (xpos[k] >= 0) break;
-        }
-        if (k >= c.nq) { done = true; break; }
+        bool any = false;
+#pragma unroll
+        for (int k = 0; k < NQ; k++)
+          if (k < c.nq && !(c.excl >> k & 1) && xpos[k] >= 0) any = true;
+        if (!any) { done = true; break; }
       }
       if (done) break;
     }
@@ -553,12 +661,12 @@ __device__ inline bool score_doc(const Weights *w, const DevPlan *pl, const DocV
   // window-restricted pair scores, Posdb.cpp:7159-7219
   float minPairScore = -1.0;
   for (int i = 0; i < c.nq; i++) {
-    if (c.bflags[i] & BF_EXCLUDE) continue;
+    if ((c.excl >> i & 1)) continue;
     for (int j = i + 1; j < c.nq; j++) {
-      if (c.bflags[j] & BF_EXCLUDE) continue;
-      if (!d.present[i]) continue;
-      if (!d.present[j]) continue;
-      float score = pair_score_any(c, d, i, j);
+      if ((c.excl >> j & 1)) continue;
+      if (!(d.present >> i & 1)) continue;
+      if (!(d.present >> j & 1)) continue;
+      const float score = pair_score_any(c, d, i, j);
       if (score >= minPairScore && minPairScore >= 0.0) continue;
       minPairScore = score;
     }
