@@ -65,9 +65,9 @@ constexpr int SEL_BINS = 4096;                   // radix-select bins per pass
 constexpr int LIST_PAD = CHUNK_LOAD + 128;
 
 struct Counters {
-  uint32_t nsurv;
+  uint32_t pad0;
   uint32_t corrupt;
-  unsigned long long scratch_top;
+  unsigned long long surv_top;  // k_compact's packed bump pointer: survivors << 36 | arena units
   uint32_t g0count[MAXG0];
   uint32_t anysurv;  // bit l: list l has a run in some survivor
   uint32_t pad[5];
@@ -241,7 +241,7 @@ __global__ void __launch_bounds__(BLOCK) k_write_runs(const DevPlan *pl, const G
                                                       const uint32_t *chunk_off,
                                                       const uint32_t *array_first_chunk,
                                                       uint64_t *cand, uint32_t *lmask, Loc *loc,
-                                                      uint64_t slot_ub, Counters *ctr,
+                                                      uint32_t *ulen, uint64_t slot_ub, Counters *ctr,
                                                       uint32_t nchunks) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[CHUNK_LOAD];
   __shared__ uint32_t tmp[BLOCK / 64];
@@ -267,6 +267,7 @@ __global__ void __launch_bounds__(BLOCK) k_write_runs(const DevPlan *pl, const G
   const uint64_t base = pl->g0base[c.array];
   const bool own = (c.array == 0);
   const uint32_t own_bit = 1u << lid;
+  const uint32_t own_mult = __popc(L.group_bits & pl->pos_mask & ~NEG_BIT);
   Loc *loc_l = loc + (uint64_t)lid * slot_ub;
   m = m0;
   o = ex;
@@ -277,11 +278,14 @@ __global__ void __launch_bounds__(BLOCK) k_write_runs(const DevPlan *pl, const G
     const uint64_t slot = base + pos;
     cand[slot] = unit_docid(lds + lu * 6);
     lmask[slot] = own ? own_bit : 0u;
+    uint32_t ul = 0;
     if (own) {
       const uint32_t u = c.u0 + lu;
       const uint32_t e = (o + 1 < tot) ? c.u0 + rs_unit[o + 1] : run_end(L, u + 2);
       loc_l[slot] = Loc{u, e - u};
+      ul = (e - u) * own_mult;
     }
+    ulen[slot] = ul;
     pos++;
     o++;
   }
@@ -360,22 +364,41 @@ __device__ __forceinline__ void chunk_store(uint8_t *lds, const ChunkRegs &r) {
 //      k-way union of addDocIdVotes' group 0 keeps each docid once.
 //   A hit records the run's (unit, length) in loc[list][slot] and sets the
 //   list's bit in the slot's list mask.
-// MODE (diagnostic, GBGPU_PROBE_MODE): 0 full, 2 stage chunks only.
+// MODE (diagnostic, GBGPU_PROBE_MODE): 0 full, 1 stop after the run-start
+// compaction, 2 stage chunks only.
 template <int MODE>
 __global__ void __launch_bounds__(BLOCK) k_probe(const DevPlan *pl, const ProbeWork *work,
                                                  const uint64_t *cand, uint32_t *lmask, Loc *loc,
-                                                 uint64_t slot_ub, const Counters *ctr) {
+                                                 uint32_t *ulen, uint64_t slot_ub, const Counters *ctr) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[CHUNK_LOAD + 32];
   __shared__ uint64_t rs_doc[MAX_RUNS];
   __shared__ uint16_t rs_unit[MAX_RUNS];
   __shared__ uint8_t rs_claim[MAX_RUNS];
-  __shared__ uint32_t s_lo[MAXG0];
+  __shared__ uint32_t s_nk[MAXG0];
+  __shared__ uint64_t s_base[MAXG0];
   __shared__ uint32_t tmp[BLOCK / 64];
   const ProbeWork w = work[blockIdx.x];
   const DevList &L = pl->lists[w.list];
   const uint32_t bit = 1u << w.list;
+  // arena units this list adds per matched run: one copy per positive group
+  // it belongs to (a shared bigram sublist is merged into both groups)
+  const uint32_t mult = __popc(L.group_bits & pl->pos_mask & ~NEG_BIT);
   const int g0n = pl->g0n;
   Loc *loc_l = loc + (uint64_t)w.list * slot_ub;
+  if (threadIdx.x < MAXG0) {
+    s_nk[threadIdx.x] = threadIdx.x < (unsigned)g0n ? ctr->g0count[threadIdx.x] : 0;
+    s_base[threadIdx.x] = threadIdx.x < (unsigned)g0n ? pl->g0base[threadIdx.x] : 0;
+  }
+  __shared__ uint64_t s_pend_slot;  // slot whose run length waits for the next run start
+  __shared__ uint32_t s_pend_u;
+  if (threadIdx.x == 0) s_pend_slot = ~0ull;
+  uint32_t lok[MAXG0];  // next candidate of each array (uniform)
+  uint64_t pf[MAXG0];   // candidate lok[k] + thread, prefetched
+#pragma unroll
+  for (int k = 0; k < MAXG0; k++) {
+    lok[k] = 0;
+    pf[k] = ~0ull;
+  }
   bool first_chunk = true;
   ChunkRegs cr;
   chunk_fetch(L.p, w.u0, cr);
@@ -409,44 +432,74 @@ __global__ void __launch_bounds__(BLOCK) k_probe(const DevPlan *pl, const ProbeW
     }
     __syncthreads();
     if (nrun == 0) continue;  // uniform: every thread saw the same total
+    if (threadIdx.x == 0 && s_pend_slot != ~0ull) {
+      const uint32_t len = u0 + rs_unit[0] - s_pend_u;
+      loc_l[s_pend_slot].len = len;
+      if (mult) atomicAdd(&ulen[s_pend_slot], len * mult);
+      s_pend_slot = ~0ull;
+    }
     const uint64_t dmin = rs_doc[0], dmax = rs_doc[nrun - 1];
-    for (int k = 0; k < g0n; k++) {
-      const uint32_t nk = ctr->g0count[k];
-      const uint64_t *ck = cand + pl->g0base[k];
-      uint32_t lo;
-      if (first_chunk) {
-        lo = block_lower_bound(ck, nk, dmin);
-      } else {
-        lo = s_lo[k];
-      }
-      for (;;) {
-        const uint32_t idx = lo + threadIdx.x;
-        const uint64_t d = idx < nk ? ck[idx] : ~0ull;
-        const bool in = d <= dmax;
-        if (in) {
-          uint32_t a = 0, b = nrun;
-          while (a < b) {
-            const uint32_t mid = (a + b) >> 1;
-            if (rs_doc[mid] < d) a = mid + 1;
-            else b = mid;
-          }
-          if (a < nrun && rs_doc[a] == d && !rs_claim[a]) {
-            rs_claim[a] = 1;
-            const uint64_t slot = pl->g0base[k] + idx;
-            const uint32_t u = u0 + rs_unit[a];
-            const uint32_t e = (a + 1 < nrun) ? u0 + rs_unit[a + 1] : run_end(L, u + 2);
-            loc_l[slot] = Loc{u, e - u};
-            atomicOr(&lmask[slot], bit);
-          }
+    if (MODE == 1) {
+      if (dmin == 0x123456789ull && dmax == 7) lmask[0] = 1;
+      continue;
+    }
+#pragma unroll
+    for (int k = 0; k < MAXG0; k++) {
+      if (k < g0n) {
+        const uint32_t nk = s_nk[k];
+        const uint64_t *ck = cand + s_base[k];
+        if (first_chunk) {
+          lok[k] = block_lower_bound(ck, nk, dmin);
+          pf[k] = lok[k] + threadIdx.x < nk ? ck[lok[k] + threadIdx.x] : ~0ull;
         }
-        const uint32_t nin = (uint32_t)__syncthreads_count(in);
-        lo += nin;
-        if (nin < (uint32_t)BLOCK) break;
+        uint32_t lo = lok[k];
+        uint64_t d = pf[k];
+        for (;;) {
+          const uint32_t idx = lo + threadIdx.x;
+          const bool in = d <= dmax;
+          if (in) {
+            uint32_t a = 0, b = nrun;
+            while (a < b) {
+              const uint32_t mid = (a + b) >> 1;
+              if (rs_doc[mid] < d) a = mid + 1;
+              else b = mid;
+            }
+            if (a < nrun && rs_doc[a] == d && !rs_claim[a]) {
+              rs_claim[a] = 1;
+              const uint64_t slot = s_base[k] + idx;
+              const uint32_t u = u0 + rs_unit[a];
+              if (a + 1 < nrun) {
+                const uint32_t len = u0 + rs_unit[a + 1] - u;
+                loc_l[slot] = Loc{u, len};
+                if (mult) atomicAdd(&ulen[slot], len * mult);
+              } else {
+                // the chunk's last run ends at the next chunk's first run
+                // start: patched there (or after the span), not walked here
+                loc_l[slot] = Loc{u, 0};
+                s_pend_slot = slot;
+                s_pend_u = u;
+              }
+              atomicOr(&lmask[slot], bit);
+            }
+          }
+          const uint32_t nin = (uint32_t)__syncthreads_count(in);
+          lo += nin;
+          if (nin < (uint32_t)BLOCK) break;
+          d = lo + threadIdx.x < nk ? ck[lo + threadIdx.x] : ~0ull;
+        }
+        lok[k] = lo;
+        // the next chunk starts at lo: fetch its first candidate now so the
+        // load overlaps the next chunk's staging and classification
+        pf[k] = lo + threadIdx.x < nk ? ck[lo + threadIdx.x] : ~0ull;
       }
-      if (threadIdx.x == 0) s_lo[k] = lo;
     }
     first_chunk = false;
     __syncthreads();
+  }
+  if (threadIdx.x == 0 && s_pend_slot != ~0ull) {
+    const uint32_t len = run_end(L, s_pend_u + 2) - s_pend_u;
+    loc_l[s_pend_slot].len = len;
+    if (mult) atomicAdd(&ulen[s_pend_slot], len * mult);
   }
 }
 
@@ -463,16 +516,31 @@ constexpr int CTILE = BLOCK * CSPT;              // 4096 slots per block
 // reference merges a shared bigram sublist into both groups).  The shrunk-
 // sublist-non-empty flags (shrinkSubLists, Posdb.cpp:5334-5428) are a list
 // bitmask OR-reduced in the block and published with one atomic.
-__global__ void __launch_bounds__(BLOCK) k_compact(const DevPlan *pl, const uint32_t *lmask, const Loc *loc,
+__global__ void __launch_bounds__(BLOCK) k_compact(const DevPlan *pl, const uint32_t *lmask, const uint32_t *ulen,
                                                    uint64_t slot_ub, Counters *ctr, uint32_t *surv,
                                                    unsigned long long *surv_off) {
   __shared__ uint32_t tmp[BLOCK / 64];
   __shared__ uint32_t s_base_i;
   __shared__ uint32_t s_any;
   __shared__ unsigned long long s_base_u;
+  __shared__ uint32_t s_gbits[MAXL];     // group bits per list
+  __shared__ uint64_t s_end[MAXG0];      // live end slot of each candidate array
+  __shared__ uint64_t s_beg[MAXG0 + 1];
   const uint32_t pos = pl->pos_mask;
-  const uint64_t s0 = (uint64_t)blockIdx.x * CTILE + threadIdx.x;
+  const int g0n = pl->g0n;
+  if (threadIdx.x < MAXL) s_gbits[threadIdx.x] = threadIdx.x < (unsigned)pl->nlists ? pl->lists[threadIdx.x].group_bits : 0;
+  if (threadIdx.x < MAXG0 + 1) s_beg[threadIdx.x] = threadIdx.x <= (unsigned)g0n ? pl->g0base[threadIdx.x] : ~0ull;
+  if (threadIdx.x < MAXG0) s_end[threadIdx.x] = threadIdx.x < (unsigned)g0n ? pl->g0base[threadIdx.x] + ctr->g0count[threadIdx.x] : 0;
   if (threadIdx.x == 0) s_any = 0;
+  __syncthreads();
+  const uint64_t s0 = (uint64_t)blockIdx.x * CTILE + threadIdx.x;
+  // all of this thread's list masks in flight at once
+  uint32_t lmv[CSPT];
+#pragma unroll
+  for (int q = 0; q < CSPT; q++) {
+    const uint64_t s = s0 + (uint64_t)q * BLOCK;
+    lmv[q] = s < slot_ub ? lmask[s] : 0u;
+  }
   uint32_t okm = 0, nok = 0, utot = 0, any = 0;
   uint32_t units[CSPT];
 #pragma unroll
@@ -481,22 +549,14 @@ __global__ void __launch_bounds__(BLOCK) k_compact(const DevPlan *pl, const uint
     units[q] = 0;
     if (s >= slot_ub) continue;
     int k = 0;
-    while (k + 1 < pl->g0n && s >= pl->g0base[k + 1]) k++;
-    if (s - pl->g0base[k] >= ctr->g0count[k]) continue;
-    const uint32_t lm = lmask[s];
+    while (k + 1 < g0n && s >= s_beg[k + 1]) k++;
+    if (s >= s_end[k]) continue;
+    const uint32_t lm = lmv[q];
     uint32_t gm = 0;
-    for (uint32_t x = lm; x; x &= x - 1) gm |= pl->lists[__ffs(x) - 1].group_bits;
+    for (uint32_t x = lm; x; x &= x - 1) gm |= s_gbits[__ffs(x) - 1];
     if (!(((gm & pos) == pos) && !(gm & NEG_BIT))) continue;
-    uint32_t u_s = 0;
-    for (int j = 0; j < pl->ngroups; j++) {
-      if (pl->gflags0[j] & BF_NEGATIVE) continue;
-      for (int x = 0; x < pl->gnsub[j]; x++) {
-        const int lid = pl->gsub[j][x];
-        if (!(lm >> lid & 1)) continue;
-        u_s += loc[(uint64_t)lid * slot_ub + s].len;
-        any |= 1u << lid;
-      }
-    }
+    const uint32_t u_s = ulen[s];
+    any |= lm;  // a survivor's lists are all in positive groups
     units[q] = u_s;
     okm |= 1u << q;
     nok++;
@@ -508,9 +568,14 @@ __global__ void __launch_bounds__(BLOCK) k_compact(const DevPlan *pl, const uint
   if (any) atomicOr(&s_any, any);
   __syncthreads();
   if (threadIdx.x == 0) {
-    s_base_i = tot_n ? atomicAdd(&ctr->nsurv, tot_n) : 0;
-    s_base_u = tot_n ? atomicAdd(&ctr->scratch_top, (unsigned long long)tot_u) : 0;
-    if (s_any) atomicOr(&ctr->anysurv, s_any);
+    // ONE atomic per block for both bump pointers (survivor index and arena
+    // offset), 28 + 36 bits; the host caps slot_ub and the arena to fit
+    const unsigned long long old =
+        tot_n ? atomicAdd(&ctr->surv_top, ((unsigned long long)tot_n << 36) | (unsigned long long)tot_u) : 0ull;
+    s_base_i = (uint32_t)(old >> 36);
+    s_base_u = old & ((1ull << 36) - 1);
+    if (s_any & ~__hip_atomic_load(&ctr->anysurv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+      atomicOr(&ctr->anysurv, s_any);
   }
   __syncthreads();
   uint32_t i = s_base_i + ex_n;
@@ -556,7 +621,7 @@ __global__ void __launch_bounds__(BLOCK) k_minimerge(const DevPlan *pl, const ui
                                                      GRange *grange) {
   const int j = blockIdx.y;
   const int ng = pl->ngroups;
-  const uint32_t nsurv = ctr->nsurv;
+  const uint32_t nsurv = (uint32_t)(ctr->surv_top >> 36);
   const uint32_t anys = ctr->anysurv;
   const uint8_t gf0 = pl->gflags0[j];
   const int gns = pl->gnsub[j];
@@ -687,7 +752,7 @@ __global__ void __launch_bounds__(TPB) k_score(const DevPlan *pl, const uint64_t
                                                const uint32_t *surv, const GRange *grange, const uint64_t *arena,
                                                uint32_t *skey, uint64_t *sdoc) {
   __shared__ float s_sm[npairs<NQ>() * TPB];
-  const uint32_t nsurv = ctr->nsurv;
+  const uint32_t nsurv = (uint32_t)(ctr->surv_top >> 36);
   const int ng = pl->ngroups;
   for (uint32_t i = blockIdx.x * TPB + threadIdx.x; i < nsurv; i += gridDim.x * TPB) {
     DocView<NQ> dv;
@@ -740,7 +805,7 @@ __global__ void __launch_bounds__(BLOCK) k_select_hist(const uint32_t *skey, con
   constexpr int NB = PASS == 2 ? 256 : SEL_BINS;
   for (int b = threadIdx.x; b < NB; b += BLOCK) h[b] = 0;
   __syncthreads();
-  const uint32_t n = ctr->nsurv;
+  const uint32_t n = (uint32_t)(ctr->surv_top >> 36);
   const uint32_t pre = PASS > 0 ? sel->prefix : 0;
   for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) {
     const uint32_t key = skey[i];
@@ -806,7 +871,7 @@ __global__ void __launch_bounds__(BLOCK) k_select_scan(Select *sel, uint32_t k) 
 __global__ void __launch_bounds__(BLOCK) k_select_gather(const uint32_t *skey, const uint64_t *sdoc,
                                                          const Counters *ctr, Select *sel, uint32_t *akey,
                                                          uint64_t *adoc, uint32_t *bkey, uint64_t *bdoc) {
-  const uint32_t n = ctr->nsurv;
+  const uint32_t n = (uint32_t)(ctr->surv_top >> 36);
   const bool all = sel->all != 0;
   const uint32_t T = all ? 1u : sel->thr;
   const int lane = threadIdx.x & 63;
@@ -973,7 +1038,7 @@ struct gbgpu_ctx {
   std::mutex mu;
   std::vector<ListEntry> lists;
   // per-query device buffers (grown, then reused)
-  DevBuf tables, chunkcnt, cand, lmask, loc, surv, survoff, scratch, grange, skey, sdoc, sel, gath, res;
+  DevBuf tables, chunkcnt, cand, lmask, ulen, loc, surv, survoff, scratch, grange, skey, sdoc, sel, gath, res;
   uint8_t *h_stage = nullptr;  // pinned: query tables (host -> device, one copy)
   size_t stage_cap = 0;
   uint8_t *h_res = nullptr;    // pinned: counters + top list (device -> host, one copy)
@@ -1120,7 +1185,7 @@ static int enqueue(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms, const i
   }
   P.g0base[P.g0n] = slot;
   const uint64_t slot_ub = slot;
-  if (slot_ub >= 0xffffffffull) return GBGPU_ECAPACITY;
+  if (slot_ub >= (1ull << 28)) return GBGPU_ECAPACITY;  // k_compact's packed bump pointer
   for (int id = 0; id < P.nlists; id++) P.lists[id].probe = (P.lists[id].g0_array != 0);
 
   ctx->g0c.clear();
@@ -1150,6 +1215,7 @@ static int enqueue(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms, const i
     if (P.gflags0[j] & BF_NEGATIVE) continue;
     for (int x = 0; x < P.gnsub[j]; x++) scratch_ub += P.lists[P.gsub[j][x]].units;
   }
+  if (scratch_ub >= (1ull << 36)) return GBGPU_ECAPACITY;
   const int k = ctx->k;
   const size_t o_chunks = align256(sizeof(DevPlan));
   const size_t o_afirst = o_chunks + align256(sizeof(G0Chunk) * ctx->g0c.size());
@@ -1161,6 +1227,7 @@ static int enqueue(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms, const i
   rc2 |= ctx->chunkcnt.ensure(4 * std::max<size_t>(1, ctx->g0c.size()));
   rc2 |= ctx->cand.ensure(8 * slot_ub);
   rc2 |= ctx->lmask.ensure(4 * slot_ub);
+  rc2 |= ctx->ulen.ensure(4 * slot_ub);
   rc2 |= ctx->loc.ensure(sizeof(Loc) * slot_ub * (uint64_t)P.nlists);
   rc2 |= ctx->surv.ensure(4 * slot_ub);
   rc2 |= ctx->survoff.ensure(8 * slot_ub);
@@ -1211,16 +1278,16 @@ static int enqueue(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms, const i
   hipLaunchKernelGGL(k_count_runs, dim3(ng0), dim3(BLOCK), 0, st, dpl, dchunks, ctx->chunkcnt.as<uint32_t>());
   hipLaunchKernelGGL(k_scan_runs, dim3(1), dim3(1024), 0, st, ng0, ctx->chunkcnt.as<uint32_t>());
   hipLaunchKernelGGL(k_write_runs, dim3(ng0), dim3(BLOCK), 0, st, dpl, dchunks, ctx->chunkcnt.as<uint32_t>(),
-                     dafirst, ctx->cand.as<uint64_t>(), lmask, loc, slot_ub, dctr, ng0);
+                     dafirst, ctx->cand.as<uint64_t>(), lmask, loc, ctx->ulen.as<uint32_t>(), slot_ub, dctr, ng0);
   if (ctx->profiling) HIPCHECK(hipEventRecord(ctx->ev[1], st));
   if (!ctx->pw.empty()) {
-    auto kp = ctx->probe_mode == 2 ? k_probe<2> : k_probe<0>;
+    auto kp = ctx->probe_mode == 2 ? k_probe<2> : (ctx->probe_mode == 1 ? k_probe<1> : k_probe<0>);
     hipLaunchKernelGGL(kp, dim3((uint32_t)ctx->pw.size()), dim3(BLOCK), 0, st, dpl, dwork,
-                       ctx->cand.as<uint64_t>(), lmask, loc, slot_ub, dctr);
+                       ctx->cand.as<uint64_t>(), lmask, loc, ctx->ulen.as<uint32_t>(), slot_ub, dctr);
   }
   if (ctx->profiling) HIPCHECK(hipEventRecord(ctx->ev[2], st));
   const uint32_t cgrid = (uint32_t)((slot_ub + CTILE - 1) / CTILE);
-  hipLaunchKernelGGL(k_compact, dim3(std::max(cgrid, 1u)), dim3(BLOCK), 0, st, dpl, lmask, loc, slot_ub, dctr,
+  hipLaunchKernelGGL(k_compact, dim3(std::max(cgrid, 1u)), dim3(BLOCK), 0, st, dpl, lmask, ctx->ulen.as<uint32_t>(), slot_ub, dctr,
                      ctx->surv.as<uint32_t>(), ctx->survoff.as<unsigned long long>());
   if (ctx->profiling) HIPCHECK(hipEventRecord(ctx->ev[3], st));
   {
@@ -1302,7 +1369,7 @@ static int collect(gbgpu_ctx *ctx, gbgpu_result *out) {
   const Counters *c = reinterpret_cast<const Counters *>(ctx->h_res);
   const uint32_t *keys = reinterpret_cast<const uint32_t *>(ctx->h_res + res_keys_off());
   const uint64_t *docs = reinterpret_cast<const uint64_t *>(ctx->h_res + res_docs_off(ctx->k));
-  out->hits = c->nsurv;
+  out->hits = (int64_t)(c->surv_top >> 36);
   int n = 0;
   for (int i = 0; i < ctx->k && n < out->capacity; i++) {
     const uint32_t key = keys[i];
@@ -1364,7 +1431,7 @@ void gbgpu_close(gbgpu_ctx *ctx) {
   (void)hipStreamSynchronize(ctx->stream);
   for (auto &e : ctx->lists)
     if (e.live) (void)hipFree(e.d);
-  DevBuf *bufs[] = {&ctx->tables, &ctx->chunkcnt, &ctx->cand, &ctx->lmask, &ctx->loc, &ctx->surv,
+  DevBuf *bufs[] = {&ctx->tables, &ctx->chunkcnt, &ctx->cand, &ctx->lmask, &ctx->ulen, &ctx->loc, &ctx->surv,
                     &ctx->survoff, &ctx->scratch, &ctx->grange, &ctx->skey, &ctx->sdoc, &ctx->sel, &ctx->gath, &ctx->res};
   for (auto *b : bufs) b->release();
   if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
