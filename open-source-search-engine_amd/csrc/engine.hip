@@ -57,7 +57,6 @@ constexpr int UPT = 8;                           // units per thread
 constexpr int CHUNK_UNITS = BLOCK * UPT;         // 2048 units = 12 KiB per chunk
 constexpr int CHUNK_BYTES = CHUNK_UNITS * 6;
 constexpr int CHUNK_LOAD = CHUNK_BYTES + 16;     // + the tail of a 12-byte key
-constexpr int CHUNKS_PER_PROBE_BLOCK = 8;        // merge-path span of one block
 constexpr int MAX_RUNS = CHUNK_UNITS / 2;        // a run is >= 2 units
 constexpr int TILE = 2048;                       // final top-k sort capacity
 constexpr int MAX_K = 1536;                      // TILE - MAX_K ties merged per round
@@ -108,6 +107,18 @@ struct ProbeWork {
   } while (0)
 
 // ------------------------------------------------------------------ helpers
+// List bytes are reached through pointers kept in the plan, which the
+// compiler cannot prove global: it would emit FLAT accesses, and every flat
+// load makes the next wait drain vmcnt AND lgkmcnt to zero (in-flight chunk
+// prefetches included).  Every list access goes through gl().
+typedef const __attribute__((address_space(1))) uint8_t gu8;
+__device__ __forceinline__ gu8 *gl(const uint8_t *p) { return (gu8 *)p; }
+template <class T>
+__device__ __forceinline__ const __attribute__((address_space(1))) T *glc(const uint8_t *p) {
+  return (const __attribute__((address_space(1))) T *)p;
+}
+__device__ __forceinline__ bool unit_is_run_start(gu8 *u) { return (u[1] & 0x02) && !(u[0] & 0x04); }
+
 __device__ __forceinline__ uint64_t unit_docid(const uint8_t *k) {  // Posdb.h:295
   uint64_t d = (uint64_t)k[11];
   d = (d << 32) | ((uint32_t)k[7] | ((uint32_t)k[8] << 8) | ((uint32_t)k[9] << 16) | ((uint32_t)k[10] << 24));
@@ -116,8 +127,9 @@ __device__ __forceinline__ uint64_t unit_docid(const uint8_t *k) {  // Posdb.h:2
 
 // Stage CHUNK_LOAD bytes of a list (16-B aligned, zero padded) into LDS.
 __device__ __forceinline__ void load_chunk(const uint8_t *list, uint32_t u0, uint8_t *lds) {
-  const uint4 *src = reinterpret_cast<const uint4 *>(list + (size_t)u0 * 6);
-  uint4 *dst = reinterpret_cast<uint4 *>(lds);
+  typedef uint32_t v4 __attribute__((ext_vector_type(4)));
+  const auto *src = glc<v4>(list + (size_t)u0 * 6);
+  v4 *dst = reinterpret_cast<v4 *>(lds);
   for (int i = threadIdx.x; i < CHUNK_LOAD / 16; i += BLOCK) dst[i] = src[i];
 }
 
@@ -180,7 +192,7 @@ __device__ uint32_t block_lower_bound(const uint64_t *a, uint32_t n, uint64_t ke
 // continuation units of a run are the second half of its 12-byte key and
 // its 6-byte keys, none of which classify as a run start (Posdb.h:887-889)
 __device__ __forceinline__ uint32_t run_end(const DevList &L, uint32_t e) {
-  while (e < L.units && !gb_unit_is_run_start(L.p + (size_t)e * 6)) e++;
+  while (e < L.units && !unit_is_run_start(gl(L.p) + (size_t)e * 6)) e++;
   return e;
 }
 
@@ -242,7 +254,7 @@ __global__ void __launch_bounds__(BLOCK) k_write_runs(const DevPlan *pl, const G
                                                       const uint32_t *array_first_chunk,
                                                       uint64_t *cand, uint32_t *lmask, Loc *loc,
                                                       uint32_t *ulen, uint64_t slot_ub, Counters *ctr,
-                                                      uint32_t nchunks) {
+                                                      uint32_t nchunks, uint64_t *dir) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[CHUNK_LOAD];
   __shared__ uint32_t tmp[BLOCK / 64];
   __shared__ uint16_t rs_unit[MAX_RUNS];
@@ -269,6 +281,10 @@ __global__ void __launch_bounds__(BLOCK) k_write_runs(const DevPlan *pl, const G
   const uint32_t own_bit = 1u << lid;
   const uint32_t own_mult = __popc(L.group_bits & pl->pos_mask & ~NEG_BIT);
   Loc *loc_l = loc + (uint64_t)lid * slot_ub;
+  uint64_t *dir_a = dir + pl->g0dir[c.array];
+  const uint64_t dmin = pl->g0dmin[c.array];
+  const uint32_t sh = pl->g0sh[c.array];
+  const uint64_t tag = (uint64_t)pl->epoch << 32;
   m = m0;
   o = ex;
   while (m) {
@@ -276,7 +292,12 @@ __global__ void __launch_bounds__(BLOCK) k_write_runs(const DevPlan *pl, const G
     m &= m - 1;
     const uint32_t lu = threadIdx.x * UPT + q;
     const uint64_t slot = base + pos;
-    cand[slot] = unit_docid(lds + lu * 6);
+    const uint64_t d = unit_docid(lds + lu * 6);
+    cand[slot] = d;
+    // directory: the first candidate of each bucket within this chunk (a
+    // bucket straddling two chunks gets two writers; either names it)
+    const uint64_t bkt = (d - dmin) >> sh;
+    if (o == 0 || ((unit_docid(lds + rs_unit[o - 1] * 6) - dmin) >> sh) != bkt) dir_a[bkt] = tag | pos;
     lmask[slot] = own ? own_bit : 0u;
     uint32_t ul = 0;
     if (own) {
@@ -295,211 +316,464 @@ __global__ void __launch_bounds__(BLOCK) k_write_runs(const DevPlan *pl, const G
 }
 
 // ------------------------------------------------------------- probe scan
-// Per-thread view of its UPT=8 units: 64 bytes read from the LDS chunk with
-// four conflict-free ds_read_b128 (thread t at byte 48t: dword 12t mod 64
-// tiles all 64 banks over 16 lanes), so classification and docid extraction
-// run from registers.  Bytes 48..63 belong to the next thread and supply the
-// docid bytes of a 12-byte key starting at the last unit.
-struct UnitRegs {
-  uint32_t w[16];
-  __device__ __forceinline__ uint32_t byte(int i) const { return (w[i >> 2] >> ((i & 3) * 8)) & 0xff; }
-};
-
-__device__ __forceinline__ void load_units(const uint8_t *lds, UnitRegs &r) {
-  const uint4 *p = reinterpret_cast<const uint4 *>(lds + threadIdx.x * 48);
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    uint4 v = p[i];
-    r.w[4 * i] = v.x;
-    r.w[4 * i + 1] = v.y;
-    r.w[4 * i + 2] = v.z;
-    r.w[4 * i + 3] = v.w;
-  }
-}
-
-// docid of a key starting at unit q of this thread (bytes 6q+7 .. 6q+11)
-__device__ __forceinline__ uint64_t regs_docid(const UnitRegs &r, int q) {
-  const int b = 6 * q + 7;
-  uint64_t d = 0;
-#pragma unroll
-  for (int i = 4; i >= 0; i--) d = (d << 8) | r.byte(b + i);
-  return d >> 2;
-}
-
-// Register-prefetched chunk copy: each thread holds 48 bytes of the next
-// chunk (3 x uint4) while the block works on the current one, so the HBM
-// latency of chunk i+1 overlaps the search of chunk i.  The 16-byte tail
-// (the docid bytes of a 12-byte key starting at the last unit) is one extra
-// uint4 that thread 0 carries.
-typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-struct ChunkRegs {
-  v4u v[3];
-  v4u tail;
-};
-__device__ __forceinline__ void chunk_fetch(const uint8_t *list, uint32_t u0, ChunkRegs &r) {
-  const v4u *src = reinterpret_cast<const v4u *>(list + (size_t)u0 * 6);
-#pragma unroll
-  for (int i = 0; i < 3; i++) r.v[i] = __builtin_nontemporal_load(src + threadIdx.x + i * BLOCK);
-  if (threadIdx.x == 0) r.tail = src[3 * BLOCK];
-}
-__device__ __forceinline__ void chunk_store(uint8_t *lds, const ChunkRegs &r) {
-  v4u *dst = reinterpret_cast<v4u *>(lds);
-#pragma unroll
-  for (int i = 0; i < 3; i++) dst[threadIdx.x + i * BLOCK] = r.v[i];
-  if (threadIdx.x == 0) dst[3 * BLOCK] = r.tail;
-}
-
-
 // k_probe -- addDocIdVotes for groups g>0 and rmDocIdVotes (Posdb.cpp:5086-
-// 5171, 4871-4946), all lists in one launch.  A block owns a contiguous span
-// of one list.  Per 12 KiB chunk:
-//   1. classify the 2048 units (Posdb.h:887-889) from registers and compact
-//      the run starts (sorted docids + unit offsets) into LDS with one block
-//      scan;
+// 5171, 4871-4946), all lists in one launch.  Every WAVE works alone (no
+// block barrier anywhere): it owns a contiguous span of one list and walks it
+// in 3 KiB chunks (512 six-byte units, 48 bytes = 8 whole units per lane),
+// loaded straight into registers two chunks ahead of use.  Per chunk:
+//   1. each lane classifies its 8 units by the alignment bit (Posdb.h:887-
+//      889); the run starts (<= 4 per lane: a run's 12-byte head is 2 units)
+//      are compacted into the wave's LDS list with a ballot prefix sum
+//      (sorted docids + unit offsets);
 //   2. per candidate array k (the smallest group's sublists, in sublist
-//      order), the candidates in [first docid, last docid] of the chunk --
-//      a contiguous slice continuing where the previous chunk stopped --
-//      each binary-search the chunk's run starts.  A run is credited to the
-//      first array holding its docid only (claim flag), which is how the
-//      k-way union of addDocIdVotes' group 0 keeps each docid once.
-//   A hit records the run's (unit, length) in loc[list][slot] and sets the
-//   list's bit in the slot's list mask.
+//      order), the next candidates up to the chunk's last docid -- a
+//      contiguous slice continuing where the previous chunk stopped -- each
+//      binary-search the run starts.  A run is credited to the first array
+//      holding its docid only (claim byte), which is how the k-way union of
+//      addDocIdVotes' group 0 keeps each docid once.
+//   A hit records the run's (unit, length) in loc[list][slot], adds the
+//   length to the slot's arena size and sets the list's bit in the slot's
+//   list mask.  The last run of a chunk ends at the next chunk's first run
+//   start: its length is patched there (or walked after the span).
 // MODE (diagnostic, GBGPU_PROBE_MODE): 0 full, 1 stop after the run-start
-// compaction, 2 stage chunks only.
-template <int MODE>
-__global__ void __launch_bounds__(BLOCK) k_probe(const DevPlan *pl, const ProbeWork *work,
-                                                 const uint64_t *cand, uint32_t *lmask, Loc *loc,
-                                                 uint32_t *ulen, uint64_t slot_ub, const Counters *ctr) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[CHUNK_LOAD + 32];
-  __shared__ uint64_t rs_doc[MAX_RUNS];
-  __shared__ uint16_t rs_unit[MAX_RUNS];
-  __shared__ uint8_t rs_claim[MAX_RUNS];
-  __shared__ uint32_t s_nk[MAXG0];
-  __shared__ uint64_t s_base[MAXG0];
-  __shared__ uint32_t tmp[BLOCK / 64];
-  const ProbeWork w = work[blockIdx.x];
-  const DevList &L = pl->lists[w.list];
-  const uint32_t bit = 1u << w.list;
-  // arena units this list adds per matched run: one copy per positive group
-  // it belongs to (a shared bigram sublist is merged into both groups)
-  const uint32_t mult = __popc(L.group_bits & pl->pos_mask & ~NEG_BIT);
-  const int g0n = pl->g0n;
-  Loc *loc_l = loc + (uint64_t)w.list * slot_ub;
-  if (threadIdx.x < MAXG0) {
-    s_nk[threadIdx.x] = threadIdx.x < (unsigned)g0n ? ctr->g0count[threadIdx.x] : 0;
-    s_base[threadIdx.x] = threadIdx.x < (unsigned)g0n ? pl->g0base[threadIdx.x] : 0;
-  }
-  __shared__ uint64_t s_pend_slot;  // slot whose run length waits for the next run start
-  __shared__ uint32_t s_pend_u;
-  if (threadIdx.x == 0) s_pend_slot = ~0ull;
-  uint32_t lok[MAXG0];  // next candidate of each array (uniform)
-  uint64_t pf[MAXG0];   // candidate lok[k] + thread, prefetched
+// compaction, 2 load chunks only, 3 skip the run-driven lists.
+constexpr int PW = 4;                      // waves per probe block
+constexpr int WCH_UNITS = 512;             // units per wave chunk
+constexpr int WCH_BYTES = WCH_UNITS * 6;   // 3 KiB
+constexpr int WMAX_RUNS = WCH_UNITS / 2;
+constexpr uint32_t PROBE_WAVES = 256 * 16;
+
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+struct WChunk {
+  v4u v[3];   // this lane's 48 bytes
+  uint2 nb;   // lane 63: the 8 bytes after the chunk (docid of a 12-byte key at unit 511)
+};
+
+__device__ __forceinline__ void wchunk_fetch(const uint8_t *list, uint32_t u0, int lane, WChunk &c) {
+  const auto *src = glc<v4u>(list + (size_t)u0 * 6 + lane * 48);
 #pragma unroll
-  for (int k = 0; k < MAXG0; k++) {
-    lok[k] = 0;
-    pf[k] = ~0ull;
+  for (int i = 0; i < 3; i++) c.v[i] = __builtin_nontemporal_load(src + i);
+  c.nb = make_uint2(0, 0);
+  if (lane == 63) {
+    typedef uint32_t v2 __attribute__((ext_vector_type(2)));
+    const v2 t = *glc<v2>(list + (size_t)u0 * 6 + WCH_BYTES);
+    c.nb = make_uint2(t.x, t.y);
   }
-  bool first_chunk = true;
-  ChunkRegs cr;
-  chunk_fetch(L.p, w.u0, cr);
-  for (uint32_t u0 = w.u0; u0 < w.u1; u0 += CHUNK_UNITS) {
-    chunk_store(lds, cr);
-    __syncthreads();
-    if (u0 + CHUNK_UNITS < w.u1) chunk_fetch(L.p, u0 + CHUNK_UNITS, cr);
+}
+
+// first index in [0,n) with a[i] >= key, cooperatively by one wave (64-ary)
+__device__ uint32_t wave_lower_bound(const uint64_t *a, uint32_t n, uint64_t key, int lane) {
+  uint32_t lo = 0, hi = n;  // answer in [lo, hi]
+  while (hi - lo > 64) {
+    const uint32_t step = (hi - lo + 63) / 64;
+    const uint32_t idx = lo + lane * step;
+    const uint64_t m = __ballot(idx < hi && a[idx] < key);
+    const uint32_t c = (uint32_t)__popcll(m);
+    if (c == 0) return lo;
+    const uint32_t nlo = lo + (c - 1) * step + 1;
+    const uint32_t nhi = min(hi, lo + c * step);
+    lo = nlo;
+    hi = nhi;
+  }
+  const uint32_t idx = lo + lane;
+  const uint64_t m = __ballot(idx < hi && a[idx] < key);
+  return lo + (uint32_t)__popcll(m);
+}
+
+// Candidate lookup for run-driven probing, split so a wave issues every
+// lookup's loads before it waits on any: dir_entry() gives the directory
+// entry of d's bucket in array k (some candidate of that bucket, or empty);
+// cand_resolve() finds d from there -- the four candidates from the entry on
+// are loaded together, a walk beyond them (a crowded bucket, or a bucket
+// whose entry came from a later chunk) is the rare case.
+__device__ __forceinline__ uint64_t dir_entry(const DevPlan *pl, int k, uint32_t n, const uint64_t *dir, uint64_t d) {
+  const uint64_t dmin = pl->g0dmin[k];
+  if (n == 0 || d < dmin || d > pl->g0dmax[k]) return 0;
+  return dir[pl->g0dir[k] + ((d - dmin) >> pl->g0sh[k])];
+}
+__device__ __forceinline__ int64_t cand_resolve(const DevPlan *pl, uint64_t e, const uint64_t *ck, uint32_t n,
+                                                uint64_t d) {
+  if ((uint32_t)(e >> 32) != pl->epoch) return -1;  // empty bucket
+  uint32_t i = (uint32_t)e;
+  uint64_t c4[4];
+#pragma unroll
+  for (int x = 0; x < 4; x++) c4[x] = i + x < n ? ck[i + x] : ~0ull;
+  if (c4[0] > d) {
+    while (i > 0) {
+      const uint64_t c = ck[--i];
+      if (c <= d) return c == d ? (int64_t)i : -1;
+    }
+    return -1;
+  }
+#pragma unroll
+  for (int x = 0; x < 4; x++)
+    if (c4[x] >= d) return c4[x] == d ? (int64_t)(i + x) : -1;
+  for (i += 4; i < n; i++) {
+    const uint64_t c = ck[i];
+    if (c >= d) return c == d ? (int64_t)i : -1;
+  }
+  return -1;
+}
+
+// first index of candidate array k with docid >= key, by one wave: the
+// directory entry of key's bucket (or of the next non-empty one of 64) lands
+// within a few slots of the answer; a 64-wide window settles it.  Falls back
+// to the 64-ary search when the window misses.
+__device__ uint32_t wave_lower_bound_dir(const DevPlan *pl, int k, const uint64_t *ck, uint32_t n,
+                                         const uint64_t *dir, uint64_t key, int lane) {
+  const uint64_t dmin = pl->g0dmin[k];
+  if (n == 0 || key <= dmin) return 0;
+  if (key > pl->g0dmax[k]) return n;
+  const uint32_t sh = pl->g0sh[k];
+  const uint64_t h = (key - dmin) >> sh;
+  const uint64_t hmax = (pl->g0dmax[k] - dmin) >> sh;
+  const uint64_t e = h + lane <= hmax ? dir[pl->g0dir[k] + h + lane] : 0;
+  const uint64_t v = __ballot((uint32_t)(e >> 32) == pl->epoch);
+  if (v) {
+    const int f = __ffsll((unsigned long long)v) - 1;
+    const uint32_t i = (uint32_t)__shfl(e, f, 64);
+    const uint32_t b0 = i > 32 ? i - 32 : 0;
+    const uint32_t idx = b0 + lane;
+    const uint32_t c = (uint32_t)__popcll(__ballot(idx < n && ck[idx] < key));
+    if (c < 64 && (c > 0 || b0 == 0)) return b0 + c;
+  }
+  return wave_lower_bound(ck, n, key, lane);
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+  // one wave's LDS accesses execute in order; keep the compiler from moving
+  // them across this point
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Wave-private probe state: the chunk's run starts and the matches found so
+// far (buffered so the scan loop issues no store or atomic: those would share
+// the in-order vmcnt counter with the chunk prefetches and force full drains).
+constexpr int MBUF = 256;
+struct ProbeLds {
+  uint64_t doc[WMAX_RUNS];
+  uint32_t mslot[MBUF], mu[MBUF], mlen[MBUF];
+  uint16_t unit[WMAX_RUNS];
+  uint8_t claim[WMAX_RUNS];
+};
+
+struct ProbeOut {
+  uint32_t *lmask;
+  uint32_t *ulen;
+  Loc *loc_l;
+  uint32_t bit, mult;
+};
+
+// append up to 64 matches (one per lane), wave-wide
+__device__ __forceinline__ void mbuf_push(ProbeLds &S, uint32_t &nbuf, bool hit, uint32_t slot, uint32_t u,
+                                          uint32_t len, int lane) {
+  const uint64_t m = __ballot(hit);
+  if (hit) {
+    const uint32_t o = nbuf + (uint32_t)__popcll(m & ((1ull << lane) - 1));
+    S.mslot[o] = slot;
+    S.mu[o] = u;
+    S.mlen[o] = len;
+  }
+  nbuf += (uint32_t)__popcll(m);
+}
+
+// publish buffered matches: run location, arena units, list bit
+// (out of line, with every argument by value: a by-reference counter would
+// live in scratch, and scratch loads wait on vmcnt like any global load)
+__device__ __noinline__ void mbuf_flush_n(ProbeLds *S, uint32_t nbuf, uint32_t *lmask, uint32_t *ulen, Loc *loc_l,
+                                          uint32_t bit, uint32_t mult, int lane) {
+  wave_lds_sync();
+  for (uint32_t i = lane; i < nbuf; i += 64) {
+    const uint32_t slot = S->mslot[i], len = S->mlen[i];
+    loc_l[slot] = Loc{S->mu[i], len};
+    if (mult) atomicAdd(&ulen[slot], len * mult);
+    atomicOr(&lmask[slot], bit);
+  }
+  wave_lds_sync();
+}
+__device__ __forceinline__ void mbuf_flush(ProbeLds &S, uint32_t &nbuf, const ProbeOut &o, int lane) {
+  mbuf_flush_n(&S, nbuf, o.lmask, o.ulen, o.loc_l, o.bit, o.mult, lane);
+  nbuf = 0;
+}
+
+// Classify this lane's 8 units, compact the wave's run starts into S (sorted
+// docids + unit offsets within the chunk).  Returns the run count.
+__device__ __forceinline__ uint32_t chunk_runs(const WChunk &cur, uint32_t u0, uint32_t u1, int lane, ProbeLds &S) {
+  uint32_t r[14];
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    r[4 * i] = cur.v[i].x;
+    r[4 * i + 1] = cur.v[i].y;
+    r[4 * i + 2] = cur.v[i].z;
+    r[4 * i + 3] = cur.v[i].w;
+  }
+  // bytes 48..55 of this lane = the next lane's first 8 bytes
+  r[12] = __shfl_down(r[0], 1, 64);
+  r[13] = __shfl_down(r[1], 1, 64);
+  if (lane == 63) {
+    r[12] = cur.nb.x;
+    r[13] = cur.nb.y;
+  }
+  auto byte = [&](int i) -> uint32_t { return (r[i >> 2] >> ((i & 3) * 8)) & 0xff; };
+  uint32_t starts = 0;
+#pragma unroll
+  for (int q = 0; q < 8; q++) {
+    const uint32_t gu = u0 + lane * 8 + q;
+    if (gu < u1 && (byte(6 * q + 1) & 0x02) && !(byte(6 * q) & 0x04)) starts |= 1u << q;
+  }
+  const uint32_t cnt = __popc(starts);
+  const uint64_t lt = (1ull << lane) - 1;
+  const uint64_t b0 = __ballot(cnt & 1), b1 = __ballot(cnt & 2), b2 = __ballot(cnt & 4);
+  const uint32_t nrun = (uint32_t)(__popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2));
+  uint32_t o = (uint32_t)(__popcll(b0 & lt) + 2 * __popcll(b1 & lt) + 4 * __popcll(b2 & lt));
+#pragma unroll
+  for (int q = 0; q < 8; q++) {
+    if (!(starts >> q & 1)) continue;
+    uint64_t d = 0;
+#pragma unroll
+    for (int i = 4; i >= 0; i--) d = (d << 8) | byte(6 * q + 7 + i);
+    S.doc[o] = d >> 2;
+    S.unit[o] = (uint16_t)(lane * 8 + q);
+    S.claim[o] = 0;
+    o++;
+  }
+  wave_lds_sync();
+  return nrun;
+}
+
+// docid of the first run start at or after unit u (< u1), ~0 if none
+__device__ uint64_t first_run_doc(const DevList &L, uint32_t u, uint32_t u1, int lane) {
+  gu8 *p = gl(L.p);
+  for (; u < u1; u += 64) {
+    const uint32_t x = u + lane;
+    const bool st = x < u1 && unit_is_run_start(p + (size_t)x * 6);
+    const uint64_t m = __ballot(st);
+    if (m) {
+      const int f = __ffsll((unsigned long long)m) - 1;
+      uint64_t d = 0;
+      if (lane == f) {
+        gu8 *k = p + (size_t)x * 6;
+        for (int i = 11; i >= 7; i--) d = (d << 8) | k[i];
+        d >>= 2;
+      }
+      return __shfl(d, f, 64);
+    }
+  }
+  return ~0ull;
+}
+
+// Dense list: candidates search the run starts.  Loop body VMEM ops are the
+// next-but-one chunk and one candidate block per array, both unconditional.
+template <int MODE, int G0>
+__device__ void probe_by_cand(const DevPlan *pl, const ProbeWork &w, const DevList &L, const uint64_t *cand,
+                              const Counters *ctr, const uint64_t *dir, ProbeLds &S, const ProbeOut &po, int lane) {
+  const int g0n = G0 <= 2 ? G0 : pl->g0n;
+  const uint8_t *lp = L.p;
+  uint32_t nk[G0], lok[G0];
+  // pf[k]: candidate lok[k] + lane as loaded (clamped index); its validity
+  // (lok[k] + lane < nk[k]) is applied at the use, not after the load, so no
+  // wait lands at the loop latch
+  uint64_t base[G0], pf[G0];
+  const uint32_t last_u0 = w.u0 + ((w.u1 - w.u0 - 1) / WCH_UNITS) * WCH_UNITS;
+  WChunk c0, c1;
+  wchunk_fetch(lp, w.u0, lane, c0);
+  wchunk_fetch(lp, min(w.u0 + WCH_UNITS, last_u0), lane, c1);
+  // where each array's candidates meet this span (peeled out of the loop)
+  const uint64_t dfirst = MODE == 0 ? first_run_doc(L, w.u0, w.u1, lane) : 0;
+#pragma unroll
+  for (int k = 0; k < G0; k++) {
+    nk[k] = k < g0n ? ctr->g0count[k] : 0;
+    base[k] = k < g0n ? pl->g0base[k] : 0;
+    lok[k] = (MODE == 0 && k < g0n) ? wave_lower_bound_dir(pl, k, cand + base[k], nk[k], dir, dfirst, lane) : 0;
+    pf[k] = cand[base[k] + min(lok[k] + lane, max(nk[k], 1u) - 1)];
+  }
+  uint32_t nbuf = 0;
+  uint64_t pend_slot = ~0ull;  // slot whose run length waits for the next run start
+  uint32_t pend_u = 0;
+  for (uint32_t u0 = w.u0; u0 < w.u1; u0 += WCH_UNITS) {
+    const WChunk cur = c0;
+    c0 = c1;
+    wchunk_fetch(lp, min(u0 + 2 * WCH_UNITS, last_u0), lane, c1);
     if (MODE == 2) {
-      if (lds[threadIdx.x * 48] == 0xee && lds[threadIdx.x * 48 + 1] == 0x77 && lds[threadIdx.x * 48 + 2] == 0x55)
-        lmask[0] = 1;
-      __syncthreads();
+      if (cur.v[0].x == 0x557713eeu && cur.v[1].y == 7u && cur.nb.x == 3u) po.lmask[0] = 1;
       continue;
     }
-    UnitRegs r;
-    load_units(lds, r);
-    uint32_t starts = 0;
-#pragma unroll
-    for (int q = 0; q < UPT; q++) {
-      const uint32_t gu = u0 + threadIdx.x * UPT + q;
-      if (gu < w.u1 && (r.byte(6 * q + 1) & 0x02) && !(r.byte(6 * q) & 0x04)) starts |= 1u << q;
+    const uint32_t nrun = chunk_runs(cur, u0, w.u1, lane, S);
+    if (nrun && pend_slot != ~0ull) {
+      if (nbuf + 1 > MBUF) mbuf_flush(S, nbuf, po, lane);
+      mbuf_push(S, nbuf, lane == 0, (uint32_t)pend_slot, pend_u, u0 + S.unit[0] - pend_u, lane);
+      pend_slot = ~0ull;
     }
-    uint32_t nrun;
-    uint32_t o = block_exclusive_scan(__popc(starts), tmp, &nrun);
-#pragma unroll
-    for (int q = 0; q < UPT; q++) {
-      if (!(starts >> q & 1)) continue;
-      rs_doc[o] = regs_docid(r, q);
-      rs_unit[o] = (uint16_t)(threadIdx.x * UPT + q);
-      rs_claim[o] = 0;
-      o++;
-    }
-    __syncthreads();
-    if (nrun == 0) continue;  // uniform: every thread saw the same total
-    if (threadIdx.x == 0 && s_pend_slot != ~0ull) {
-      const uint32_t len = u0 + rs_unit[0] - s_pend_u;
-      loc_l[s_pend_slot].len = len;
-      if (mult) atomicAdd(&ulen[s_pend_slot], len * mult);
-      s_pend_slot = ~0ull;
-    }
-    const uint64_t dmin = rs_doc[0], dmax = rs_doc[nrun - 1];
     if (MODE == 1) {
-      if (dmin == 0x123456789ull && dmax == 7) lmask[0] = 1;
+      if (nrun && S.doc[0] == 0x123456789ull) po.lmask[0] = 1;
       continue;
     }
+    const uint64_t dmax = nrun ? S.doc[nrun - 1] : 0;
 #pragma unroll
-    for (int k = 0; k < MAXG0; k++) {
-      if (k < g0n) {
-        const uint32_t nk = s_nk[k];
-        const uint64_t *ck = cand + s_base[k];
-        if (first_chunk) {
-          lok[k] = block_lower_bound(ck, nk, dmin);
-          pf[k] = lok[k] + threadIdx.x < nk ? ck[lok[k] + threadIdx.x] : ~0ull;
-        }
-        uint32_t lo = lok[k];
-        uint64_t d = pf[k];
-        for (;;) {
-          const uint32_t idx = lo + threadIdx.x;
-          const bool in = d <= dmax;
-          if (in) {
-            uint32_t a = 0, b = nrun;
-            while (a < b) {
-              const uint32_t mid = (a + b) >> 1;
-              if (rs_doc[mid] < d) a = mid + 1;
-              else b = mid;
-            }
-            if (a < nrun && rs_doc[a] == d && !rs_claim[a]) {
-              rs_claim[a] = 1;
-              const uint64_t slot = s_base[k] + idx;
-              const uint32_t u = u0 + rs_unit[a];
-              if (a + 1 < nrun) {
-                const uint32_t len = u0 + rs_unit[a + 1] - u;
-                loc_l[slot] = Loc{u, len};
-                if (mult) atomicAdd(&ulen[slot], len * mult);
-              } else {
-                // the chunk's last run ends at the next chunk's first run
-                // start: patched there (or after the span), not walked here
-                loc_l[slot] = Loc{u, 0};
-                s_pend_slot = slot;
-                s_pend_u = u;
-              }
-              atomicOr(&lmask[slot], bit);
+    for (int k = 0; k < G0; k++) {
+      if (k >= g0n) break;
+      const uint64_t *ck = cand + base[k];
+      uint32_t lo = lok[k];
+      // one pass: the 64 candidates from lo (one per lane) against the runs
+      auto pass = [&](uint64_t d) -> uint32_t {
+        const bool in = nrun && d <= dmax;
+        bool hit = false, last = false;
+        uint32_t u = 0, len = 0;
+        if (in) {
+          uint32_t a = 0, b = nrun;
+          while (a < b) {
+            const uint32_t mid = (a + b) >> 1;
+            if (S.doc[mid] < d) a = mid + 1;
+            else b = mid;
+          }
+          if (a < nrun && S.doc[a] == d && !S.claim[a]) {
+            S.claim[a] = 1;
+            u = u0 + S.unit[a];
+            if (a + 1 < nrun) {
+              hit = true;
+              len = S.unit[a + 1] - S.unit[a];
+            } else {
+              last = true;  // ends at the next chunk's first run start
             }
           }
-          const uint32_t nin = (uint32_t)__syncthreads_count(in);
-          lo += nin;
-          if (nin < (uint32_t)BLOCK) break;
-          d = lo + threadIdx.x < nk ? ck[lo + threadIdx.x] : ~0ull;
         }
-        lok[k] = lo;
-        // the next chunk starts at lo: fetch its first candidate now so the
-        // load overlaps the next chunk's staging and classification
-        pf[k] = lo + threadIdx.x < nk ? ck[lo + threadIdx.x] : ~0ull;
+        if (nbuf + 64 > MBUF) mbuf_flush(S, nbuf, po, lane);
+        mbuf_push(S, nbuf, hit, (uint32_t)(base[k] + lo + lane), u, len, lane);
+        const uint64_t pm = __ballot(last);
+        if (pm) {
+          pend_slot = base[k] + lo + (uint32_t)(__ffsll((unsigned long long)pm) - 1);
+          pend_u = u0 + S.unit[nrun - 1];
+        }
+        const uint32_t nin = (uint32_t)__popcll(__ballot(in));
+        lo += nin;
+        return nin;
+      };
+      // the first pass reads the prefetched block; a chunk meeting more than
+      // 64 candidates (dense arrays) reloads in a loop of its own, so the
+      // prefetched register never merges with a just-loaded one
+      if (pass(lo + lane < nk[k] ? pf[k] : ~0ull) == 64u) {
+        for (;;) {
+          const uint64_t d = lo + lane < nk[k] ? ck[lo + lane] : ~0ull;
+          if (pass(d) < 64u) break;
+        }
+      }
+      lok[k] = lo;
+      // the next chunk starts at lo
+      pf[k] = ck[min(lo + lane, max(nk[k], 1u) - 1)];
+    }
+    wave_lds_sync();  // the next chunk rewrites the run list
+  }
+  if (pend_slot != ~0ull) {
+    const uint32_t len = lane == 0 ? run_end(L, pend_u + 2) - pend_u : 0;
+    if (nbuf + 1 > MBUF) mbuf_flush(S, nbuf, po, lane);
+    mbuf_push(S, nbuf, lane == 0, (uint32_t)pend_slot, pend_u, len, lane);
+  }
+  mbuf_flush(S, nbuf, po, lane);
+}
+
+// Sparse list: each run start looks its docid up in the arrays, in order;
+// the first array holding it takes the run.
+template <int G0>
+__device__ void probe_by_run(const DevPlan *pl, const ProbeWork &w, const DevList &L, const uint64_t *cand,
+                             const Counters *ctr, const uint64_t *dir, ProbeLds &S, const ProbeOut &po, int lane) {
+  const int g0n = G0 <= 2 ? G0 : pl->g0n;
+  uint32_t nk[G0];
+  uint64_t base[G0];
+#pragma unroll
+  for (int k = 0; k < G0; k++) {
+    nk[k] = k < g0n ? ctr->g0count[k] : 0;
+    base[k] = k < g0n ? pl->g0base[k] : 0;
+  }
+  uint32_t nbuf = 0;
+  uint64_t pend_slot = ~0ull;
+  uint32_t pend_u = 0;
+  WChunk cur;
+  for (uint32_t u0 = w.u0; u0 < w.u1; u0 += WCH_UNITS) {
+    wchunk_fetch(L.p, u0, lane, cur);
+    const uint32_t nrun = chunk_runs(cur, u0, w.u1, lane, S);
+    if (!nrun) continue;
+    if (pend_slot != ~0ull) {
+      if (nbuf + 1 > MBUF) mbuf_flush(S, nbuf, po, lane);
+      mbuf_push(S, nbuf, lane == 0, (uint32_t)pend_slot, pend_u, u0 + S.unit[0] - pend_u, lane);
+      pend_slot = ~0ull;
+    }
+    for (uint32_t j0 = 0; j0 < nrun; j0 += 64) {
+      const uint32_t j = j0 + lane;
+      bool hit = false, last = false;
+      uint32_t slot = 0, u = 0, len = 0;
+      if (j < nrun) {
+        const uint64_t d = S.doc[j];
+        uint64_t e[G0];
+#pragma unroll
+        for (int k = 0; k < G0; k++) e[k] = k < g0n ? dir_entry(pl, k, nk[k], dir, d) : 0;
+        int64_t i = -1;
+        int kh = 0;
+#pragma unroll
+        for (int k = 0; k < G0; k++) {
+          if (i >= 0 || k >= g0n) continue;
+          i = cand_resolve(pl, e[k], cand + base[k], nk[k], d);
+          kh = k;
+        }
+        if (i >= 0) {
+          slot = (uint32_t)(base[kh] + (uint64_t)i);
+          u = u0 + S.unit[j];
+          if (j + 1 < nrun) {
+            hit = true;
+            len = S.unit[j + 1] - S.unit[j];
+          } else {
+            last = true;
+          }
+        }
+      }
+      if (nbuf + 64 > MBUF) mbuf_flush(S, nbuf, po, lane);
+      mbuf_push(S, nbuf, hit, slot, u, len, lane);
+      const uint64_t pm = __ballot(last);
+      if (pm) {
+        const int f = __ffsll((unsigned long long)pm) - 1;
+        pend_slot = __shfl(slot, f, 64);
+        pend_u = u0 + S.unit[nrun - 1];
       }
     }
-    first_chunk = false;
-    __syncthreads();
+    wave_lds_sync();
   }
-  if (threadIdx.x == 0 && s_pend_slot != ~0ull) {
-    const uint32_t len = run_end(L, s_pend_u + 2) - s_pend_u;
-    loc_l[s_pend_slot].len = len;
-    if (mult) atomicAdd(&ulen[s_pend_slot], len * mult);
+  if (pend_slot != ~0ull) {
+    const uint32_t len = lane == 0 ? run_end(L, pend_u + 2) - pend_u : 0;
+    if (nbuf + 1 > MBUF) mbuf_flush(S, nbuf, po, lane);
+    mbuf_push(S, nbuf, lane == 0, (uint32_t)pend_slot, pend_u, len, lane);
+  }
+  mbuf_flush(S, nbuf, po, lane);
+}
+
+// k_probe -- addDocIdVotes for groups g>0 and rmDocIdVotes (Posdb.cpp:5086-
+// 5171, 4871-4946): one wave per work item, each wave alone (no block
+// barrier).  The direction is per list (the host's choice, DevList::probe).
+// MODE (diagnostic, GBGPU_PROBE_MODE): 0 full, 1 stop after the run-start
+// compaction, 2 load chunks only, 3 skip the run-driven lists.
+template <int MODE, int G0>
+__global__ void __launch_bounds__(64 * PW) k_probe(const DevPlan *pl, const ProbeWork *work, uint32_t nwork,
+                                                   const uint64_t *cand, uint32_t *lmask, Loc *loc,
+                                                   uint32_t *ulen, uint64_t slot_ub, const Counters *ctr,
+                                                   const uint64_t *dir) {
+  __shared__ ProbeLds s_lds[PW];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const uint32_t wi = blockIdx.x * PW + wid;
+  if (wi >= nwork) return;  // the whole wave: no block barrier follows
+  const ProbeWork w = work[wi];
+  const DevList &L = pl->lists[w.list];
+  ProbeOut po;
+  po.lmask = lmask;
+  po.ulen = ulen;
+  po.loc_l = loc + (uint64_t)w.list * slot_ub;
+  po.bit = 1u << w.list;
+  // arena units this list adds per matched run: one copy per positive group
+  // it belongs to (a shared bigram sublist is merged into both groups)
+  po.mult = __popc(L.group_bits & pl->pos_mask & ~NEG_BIT);
+  if (L.probe == PROBE_BY_RUN) {
+    if (MODE == 0) probe_by_run<G0>(pl, w, L, cand, ctr, dir, s_lds[wid], po, lane);
+  } else {
+    probe_by_cand<MODE == 3 ? 0 : MODE, G0>(pl, w, L, cand, ctr, dir, s_lds[wid], po, lane);
   }
 }
 
@@ -602,8 +876,8 @@ struct GRange {
 constexpr uint32_t GR_HASFIRST = 1u << 16;
 constexpr uint32_t GR_POSITIVE = 1u << 27;
 
-__device__ __forceinline__ uint64_t load6(const uint8_t *k) {
-  const uint16_t *h = reinterpret_cast<const uint16_t *>(k);
+__device__ __forceinline__ uint64_t load6(gu8 *k) {
+  const auto *h = (const __attribute__((address_space(1))) uint16_t *)k;
   return (uint64_t)h[0] | ((uint64_t)h[1] << 16) | ((uint64_t)h[2] << 32);
 }
 
@@ -641,7 +915,7 @@ __global__ void __launch_bounds__(BLOCK) k_minimerge(const DevPlan *pl, const ui
         if (lm >> lid & 1) off += loc[(uint64_t)lid * slot_ub + s].len;
       }
     }
-    const uint8_t *cp[NS];
+    gu8 *cp[NS];
     uint32_t cu[NS], ce[NS];
     uint64_t ck[NS];
     uint8_t cfl[NS];
@@ -662,7 +936,7 @@ __global__ void __launch_bounds__(BLOCK) k_minimerge(const DevPlan *pl, const ui
           newIdx++;
           if (lm >> lid & 1) {
             const Loc lc = loc[(uint64_t)lid * slot_ub + s];
-            cp[x] = pl->lists[lid].p;
+            cp[x] = gl(pl->lists[lid].p);
             cu[x] = lc.unit;
             ce[x] = lc.unit + lc.len;
             ck[x] = load6(cp[x] + (size_t)lc.unit * 6);
@@ -677,7 +951,7 @@ __global__ void __launch_bounds__(BLOCK) k_minimerge(const DevPlan *pl, const ui
     uint32_t mbytes = 0;  // emulates mptr - mbuf (cap 299000, Posdb.cpp:6007-6008)
     bool isFirstKey = true;
     uint64_t last = 0;
-    const uint8_t *firstSrc = nullptr;
+    gu8 *firstSrc = nullptr;
     for (;;) {
       int mink = -1;
       uint32_t mhi = 0, mlo = 0;
@@ -694,7 +968,7 @@ __global__ void __launch_bounds__(BLOCK) k_minimerge(const DevPlan *pl, const ui
       if (mink == -1) break;
       uint64_t r = 0;
       uint8_t fl = 0;
-      const uint8_t *src = nullptr;
+      gu8 *src = nullptr;
 #pragma unroll
       for (int x = 0; x < NS; x++) {
         if (x == mink) {
@@ -739,7 +1013,11 @@ __global__ void __launch_bounds__(BLOCK) k_minimerge(const DevPlan *pl, const ui
       if (mbytes >= 299000) break;
     }
     uint32_t info = nrec | GR_POSITIVE;
-    if (firstSrc) info |= GR_HASFIRST | (gb_siterank(firstSrc) << 17) | (gb_langid(firstSrc) << 21);
+    if (firstSrc) {
+      uint8_t k12[12];
+      for (int b = 0; b < 12; b++) k12[b] = firstSrc[b];
+      info |= GR_HASFIRST | (gb_siterank(k12) << 17) | (gb_langid(k12) << 21);
+    }
     grange[(size_t)i * ng + j] = GRange{(uint32_t)off, info};
   }
 }
@@ -1023,8 +1301,16 @@ struct ListEntry {
   uint8_t *d = nullptr;
   int64_t size = 0;   // original bytes (18-byte first key)
   uint32_t units = 0; // swapped units
+  uint64_t dmin = 0, dmax = 0;  // docid of the first and of the last run
   bool live = false;
 };
+
+// docid of the key starting at p (Posdb.h:295)
+static uint64_t host_docid(const uint8_t *p) {
+  uint64_t d = 0;
+  for (int i = 11; i >= 7; i--) d = (d << 8) | p[i];
+  return d >> 2;
+}
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
@@ -1039,6 +1325,8 @@ struct gbgpu_ctx {
   std::vector<ListEntry> lists;
   // per-query device buffers (grown, then reused)
   DevBuf tables, chunkcnt, cand, lmask, ulen, loc, surv, survoff, scratch, grange, skey, sdoc, sel, gath, res;
+  DevBuf dir;           // candidate directories, epoch-tagged (never cleared per query)
+  uint32_t epoch = 0;
   uint8_t *h_stage = nullptr;  // pinned: query tables (host -> device, one copy)
   size_t stage_cap = 0;
   uint8_t *h_res = nullptr;    // pinned: counters + top list (device -> host, one copy)
@@ -1085,6 +1373,16 @@ static int upload_list(gbgpu_ctx *ctx, const uint8_t *bytes, int64_t size, int32
       HIPCHECK(hipMemcpyAsync(e.d + 12, bytes + 18, (size_t)(size - 18), hipMemcpyHostToDevice, ctx->stream));
   }
   HIPCHECK(hipStreamSynchronize(ctx->stream));
+  if (size) {
+    // the list's docid range (directory sizing): first key, last run start
+    e.dmin = e.dmax = host_docid(bytes);
+    for (int64_t q = size - 6; q >= 18; q -= 6) {
+      if ((bytes[q + 1] & 0x02) && !(bytes[q] & 0x04)) {
+        e.dmax = host_docid(bytes + q);
+        break;
+      }
+    }
+  }
   e.live = true;
   for (size_t i = 0; i < ctx->lists.size(); i++) {
     if (!ctx->lists[i].live) {
@@ -1136,6 +1434,7 @@ static int enqueue(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms, const i
   P.site_rank_multiplier = GB_SITERANKMULTIPLIER;
   P.nqt = nterms;
   int dense[1024];
+  uint64_t list_dmin[MAXL], list_dmax[MAXL];
   for (int i = 0; i < nterms; i++) dense[i] = -1;
   auto dense_id = [&](int term) -> int {
     if (dense[term] >= 0) return dense[term];
@@ -1145,6 +1444,8 @@ static int enqueue(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms, const i
     const ListEntry &e = ctx->lists[handles[term]];
     P.lists[id].p = e.d;
     P.lists[id].units = e.units;
+    list_dmin[id] = e.dmin;
+    list_dmax[id] = e.dmax;
     P.lists[id].group_bits = 0;
     P.lists[id].g0_array = -1;
     P.lists[id].probe = 0;
@@ -1186,7 +1487,30 @@ static int enqueue(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms, const i
   P.g0base[P.g0n] = slot;
   const uint64_t slot_ub = slot;
   if (slot_ub >= (1ull << 28)) return GBGPU_ECAPACITY;  // k_compact's packed bump pointer
-  for (int id = 0; id < P.nlists; id++) P.lists[id].probe = (P.lists[id].g0_array != 0);
+  // directories: about 8 units (2-4 docids) per bucket, power-of-two count
+  uint64_t dir_entries = 0;
+  for (int a = 0; a < P.g0n; a++) {
+    const int id = P.g0list[a];
+    const uint32_t units = P.lists[id].units;
+    uint64_t nb = 64;
+    while (nb < units / 8) nb <<= 1;
+    const uint64_t lo = list_dmin[id], hi = list_dmax[id];
+    uint32_t sh = 0;
+    while (((hi - lo) >> sh) >= nb) sh++;
+    P.g0dmin[a] = lo;
+    P.g0dmax[a] = hi;
+    P.g0sh[a] = sh;
+    P.g0dir[a] = dir_entries;
+    dir_entries += ((hi - lo) >> sh) + 1;
+  }
+  // probe direction per list: candidate-driven while a 3 KiB chunk meets
+  // about one wave-width of candidates, else run-driven
+  for (int id = 0; id < P.nlists; id++) {
+    P.lists[id].probe = 0;
+    if (P.lists[id].g0_array == 0) continue;
+    const double per_chunk = (double)slot_ub * WCH_UNITS / std::max<uint32_t>(1, P.lists[id].units);
+    P.lists[id].probe = per_chunk > 64.0 ? PROBE_BY_RUN : PROBE_BY_CAND;
+  }
 
   ctx->g0c.clear();
   ctx->afirst.assign(MAXG0, 0);
@@ -1197,15 +1521,20 @@ static int enqueue(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms, const i
   }
   ctx->pw.clear();
   int64_t scan = 0;
+  uint64_t probe_chunks = 0;
   for (int id = 0; id < P.nlists; id++) {
-    const uint32_t units = P.lists[id].units;
-    scan += (int64_t)units * 6;
+    scan += (int64_t)P.lists[id].units * 6;
+    if (P.lists[id].probe == PROBE_BY_CAND) probe_chunks += (P.lists[id].units + WCH_UNITS - 1) / WCH_UNITS;
+  }
+  // one wave per span of S chunks: about PROBE_WAVES spans over all probed
+  // lists, so every CU holds ~24 waves and each amortises its initial
+  // candidate search over several chunks
+  const uint32_t S = (uint32_t)std::max<uint64_t>(1, (probe_chunks + PROBE_WAVES - 1) / PROBE_WAVES);
+  for (int id = 0; id < P.nlists; id++) {
     if (!P.lists[id].probe) continue;
-    // long lists: 8 chunks per block amortise the candidate search; short
-    // lists: 1 chunk per block so they do not form the kernel's tail
-    const uint32_t nch = (units + CHUNK_UNITS - 1) / CHUNK_UNITS;
-    const uint32_t cpb = std::max(1u, std::min<uint32_t>(CHUNKS_PER_PROBE_BLOCK, nch / 1024));
-    const uint32_t span = CHUNK_UNITS * cpb;
+    const uint32_t units = P.lists[id].units;
+    // a run-driven chunk costs a few dependent lookups: one chunk per wave
+    const uint32_t span = WCH_UNITS * (P.lists[id].probe == PROBE_BY_RUN ? 1 : S);
     for (uint32_t u = 0; u < units; u += span) ctx->pw.push_back({(uint32_t)id, u, std::min(units, u + span)});
   }
   ctx->scan_bytes = scan;
@@ -1238,7 +1567,15 @@ static int enqueue(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms, const i
   rc2 |= ctx->sel.ensure(sizeof(Select));
   rc2 |= ctx->gath.ensure(12 * (slot_ub + MAX_K) + 1024);
   rc2 |= ctx->res.ensure(ctx->res_bytes);
+  const void *dir_before = ctx->dir.p;
+  rc2 |= ctx->dir.ensure(8 * std::max<uint64_t>(1, dir_entries));
   if (rc2) return ENOMEM;
+  if (ctx->dir.p != dir_before || ctx->epoch == 0xffffffffu) {
+    // fresh directory memory: no entry may carry a live epoch
+    HIPCHECK(hipMemsetAsync(ctx->dir.p, 0, ctx->dir.cap, ctx->stream));
+    ctx->epoch = 0;
+  }
+  P.epoch = ++ctx->epoch;
   if (tbytes > ctx->stage_cap) {
     if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
     ctx->h_stage = nullptr;
@@ -1278,12 +1615,21 @@ static int enqueue(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms, const i
   hipLaunchKernelGGL(k_count_runs, dim3(ng0), dim3(BLOCK), 0, st, dpl, dchunks, ctx->chunkcnt.as<uint32_t>());
   hipLaunchKernelGGL(k_scan_runs, dim3(1), dim3(1024), 0, st, ng0, ctx->chunkcnt.as<uint32_t>());
   hipLaunchKernelGGL(k_write_runs, dim3(ng0), dim3(BLOCK), 0, st, dpl, dchunks, ctx->chunkcnt.as<uint32_t>(),
-                     dafirst, ctx->cand.as<uint64_t>(), lmask, loc, ctx->ulen.as<uint32_t>(), slot_ub, dctr, ng0);
+                     dafirst, ctx->cand.as<uint64_t>(), lmask, loc, ctx->ulen.as<uint32_t>(), slot_ub, dctr, ng0,
+                     ctx->dir.as<uint64_t>());
   if (ctx->profiling) HIPCHECK(hipEventRecord(ctx->ev[1], st));
   if (!ctx->pw.empty()) {
-    auto kp = ctx->probe_mode == 2 ? k_probe<2> : (ctx->probe_mode == 1 ? k_probe<1> : k_probe<0>);
-    hipLaunchKernelGGL(kp, dim3((uint32_t)ctx->pw.size()), dim3(BLOCK), 0, st, dpl, dwork,
-                       ctx->cand.as<uint64_t>(), lmask, loc, ctx->ulen.as<uint32_t>(), slot_ub, dctr);
+    auto kp = ctx->probe_mode == 3   ? k_probe<3, MAXG0>
+              : ctx->probe_mode == 2 ? k_probe<2, MAXG0>
+              : ctx->probe_mode == 1 ? k_probe<1, MAXG0>
+              : P.g0n == 1           ? k_probe<0, 1>
+              : P.g0n == 2           ? k_probe<0, 2>
+              : P.g0n <= 4           ? k_probe<0, 4>
+                                     : k_probe<0, MAXG0>;
+    const uint32_t nwork = (uint32_t)ctx->pw.size();
+    hipLaunchKernelGGL(kp, dim3((nwork + PW - 1) / PW), dim3(64 * PW), 0, st, dpl, dwork, nwork,
+                       ctx->cand.as<uint64_t>(), lmask, loc, ctx->ulen.as<uint32_t>(), slot_ub, dctr,
+                       ctx->dir.as<uint64_t>());
   }
   if (ctx->profiling) HIPCHECK(hipEventRecord(ctx->ev[2], st));
   const uint32_t cgrid = (uint32_t)((slot_ub + CTILE - 1) / CTILE);
@@ -1432,7 +1778,8 @@ void gbgpu_close(gbgpu_ctx *ctx) {
   for (auto &e : ctx->lists)
     if (e.live) (void)hipFree(e.d);
   DevBuf *bufs[] = {&ctx->tables, &ctx->chunkcnt, &ctx->cand, &ctx->lmask, &ctx->ulen, &ctx->loc, &ctx->surv,
-                    &ctx->survoff, &ctx->scratch, &ctx->grange, &ctx->skey, &ctx->sdoc, &ctx->sel, &ctx->gath, &ctx->res};
+                    &ctx->survoff, &ctx->scratch, &ctx->grange, &ctx->skey, &ctx->sdoc, &ctx->sel, &ctx->gath, &ctx->res,
+                    &ctx->dir};
   for (auto *b : bufs) b->release();
   if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
   if (ctx->h_res) (void)hipHostFree(ctx->h_res);

@@ -57,8 +57,10 @@ struct DevList {
   uint32_t units;       // (size-6)/6
   uint32_t group_bits;  // positive groups containing this list (+NEG_BIT if in a negative group)
   int32_t g0_array;     // index among the smallest group's candidate arrays, -1 if none
-  int32_t probe;        // 1: scanned by the probe kernel
+  int32_t probe;        // k_probe direction: 0 not scanned, PROBE_BY_CAND, PROBE_BY_RUN
 };
+constexpr int32_t PROBE_BY_CAND = 1;  // dense list: candidates search the chunk's run starts
+constexpr int32_t PROBE_BY_RUN = 2;   // sparse list: run starts look up the candidate directory
 
 struct DevPlan {
   int ngroups;
@@ -80,6 +82,13 @@ struct DevPlan {
   int g0n;
   int g0list[MAXG0];
   uint64_t g0base[MAXG0 + 1];  // slot base of each array (prefix of upper bounds)
+  // per candidate array, a docid-bucket directory: entry (epoch << 32 | i)
+  // at bucket (docid - g0dmin) >> g0sh names SOME candidate i of that bucket
+  // (k_write_runs); entries of older queries carry an older epoch
+  uint32_t epoch;
+  uint32_t g0sh[MAXG0];
+  uint64_t g0dmin[MAXG0], g0dmax[MAXG0];
+  uint64_t g0dir[MAXG0];       // first entry of each array's directory
   DevList lists[MAXL];
 };
 
