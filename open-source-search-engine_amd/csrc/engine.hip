@@ -11,22 +11,23 @@
 //        (addDocIdVotes group 0, Posdb.cpp:5178-5332), one sorted array per
 //        sublist; array 0's own run locations are recorded here.
 //   k_probe
-//        merge-path scan of every other list: each block owns a contiguous
-//        span of one list, classifies every 6-byte unit of a 12 KiB chunk by
-//        the alignment bit, compacts the run starts in LDS and lets the
-//        chunk's candidates binary-search them (addDocIdVotes g>0 /
-//        rmDocIdVotes, Posdb.cpp:5086-5171, 4871-4946).  A hit sets the
+//        scan of every other list, one wave per contiguous span, no block
+//        barrier: each lane classifies 8 six-byte units by the alignment bit
+//        (Posdb.h:887-889), the wave compacts the run starts into LDS with a
+//        ballot prefix sum, and either the chunk's candidates binary-search
+//        them (dense lists) or each run start looks its docid up in the
+//        candidate arrays' bucket directory (sparse lists) -- addDocIdVotes
+//        g>0 / rmDocIdVotes, Posdb.cpp:5086-5171, 4871-4946.  A hit sets the
 //        list's bit in the candidate's list mask and records (unit, length)
 //        of the docid's run.
 //   k_compact
 //        survivors = candidates whose lists cover every positive group and
 //        no negative one (the final m_docIdVoteBuf), plus the shrunk-sublist
 //        non-empty flags (shrinkSubLists, Posdb.cpp:5334-5428).
-//   k_minimerge
-//        one lane per (survivor, group): mini-merge (Posdb.cpp:6559-6778) of
-//        the group's sublist runs into arena records.
-//   k_score<NQ>
-//        one lane per survivor: the scorers of scoring.h, register-resident.
+//   k_score<NQ, NS>
+//        one lane per survivor: mini-merge of each group (Posdb.cpp:6559-
+//        6778) into the survivor's arena records, then the scorers of
+//        scoring.h (weight tables staged in LDS).
 //   k_select_hist x3 / k_select_gather / k_select_final
 //        radix select of the k best (score desc, docid asc) replacing TopTree
 //        (TopTree.cpp:195-516), then one small LDS sort.
@@ -792,7 +793,7 @@ constexpr int CTILE = BLOCK * CSPT;              // 4096 slots per block
 // bitmask OR-reduced in the block and published with one atomic.
 __global__ void __launch_bounds__(BLOCK) k_compact(const DevPlan *pl, const uint32_t *lmask, const uint32_t *ulen,
                                                    uint64_t slot_ub, Counters *ctr, uint32_t *surv,
-                                                   unsigned long long *surv_off) {
+                                                   unsigned long long *surv_off, uint32_t *surv_lm) {
   __shared__ uint32_t tmp[BLOCK / 64];
   __shared__ uint32_t s_base_i;
   __shared__ uint32_t s_any;
@@ -859,6 +860,7 @@ __global__ void __launch_bounds__(BLOCK) k_compact(const DevPlan *pl, const uint
     if (!(okm >> q & 1)) continue;
     surv[i] = (uint32_t)(s0 + (uint64_t)q * BLOCK);
     surv_off[i] = off;
+    surv_lm[i] = lmv[q];
     i++;
     off += units[q];
   }
@@ -867,91 +869,78 @@ __global__ void __launch_bounds__(BLOCK) k_compact(const DevPlan *pl, const uint
 // ------------------------------------------------------------------ score
 __constant__ Weights c_weights;
 
-// one (survivor, group) mini-merge result: record range in the arena and the
-// group's first key's siteRank/langId (Posdb.cpp:6985-7003)
-struct GRange {
-  uint32_t start;
-  uint32_t info;  // count(16) | hasFirst(1) | siteRank(4) | langId(6) | positive(1)
-};
-constexpr uint32_t GR_HASFIRST = 1u << 16;
-constexpr uint32_t GR_POSITIVE = 1u << 27;
+// Per-survivor work, one lane per survivor (Posdb.cpp:6252-7257): for each
+// group, mini-merge (Posdb.cpp:6559-6778) its sublist runs into records in
+// the survivor's arena range (k_compact's prefix sum of its run units), then
+// score_doc (scoring.h) over them.
+constexpr int SCORE_TPB = 64;
 
 __device__ __forceinline__ uint64_t load6(gu8 *k) {
   const auto *h = (const __attribute__((address_space(1))) uint16_t *)k;
   return (uint64_t)h[0] | ((uint64_t)h[1] << 16) | ((uint64_t)h[2] << 32);
 }
 
-// Mini-merge (Posdb.cpp:6559-6778) of one group's sublist runs for one
-// survivor, one lane per (survivor, group): blockIdx.y = group.  Runs are
-// merged by (u32@+2, u16@0), ties to the lower sublist; BF_BIGRAM keys with
-// F bits set are skipped; the first key becomes 12 bytes, later keys 6 bytes
-// and are dropped when their word position repeats; byte 2's F bits are
-// rewritten from the sublist flags; output capped at 299000 bytes.  NS =
-// sublist capacity (cursors live in registers, indexed by sublist).
-template <int NS>
-__global__ void __launch_bounds__(BLOCK) k_minimerge(const DevPlan *pl, const uint32_t *lmask, const Loc *loc,
-                                                     uint64_t slot_ub, const Counters *ctr, const uint32_t *surv,
-                                                     const unsigned long long *surv_off, uint64_t *arena,
-                                                     GRange *grange) {
-  const int j = blockIdx.y;
+template <int NQ, int NS, class RP>
+__device__ __forceinline__ void score_survivor(const DevPlan *pl, uint32_t s, uint32_t lm, uint32_t anys,
+                                               const Loc *loc, uint64_t slot_ub, RP rec, float *smcol,
+                                               uint32_t *key_out, int diag) {
   const int ng = pl->ngroups;
-  const uint32_t nsurv = (uint32_t)(ctr->surv_top >> 36);
-  const uint32_t anys = ctr->anysurv;
-  const uint8_t gf0 = pl->gflags0[j];
-  const int gns = pl->gnsub[j];
-  for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < nsurv; i += gridDim.x * BLOCK) {
-    if (gf0 & BF_NEGATIVE) {
-      grange[(size_t)i * ng + j] = GRange{0, 0};
-      continue;
-    }
-    const uint32_t s = surv[i];
-    const uint32_t lm = lmask[s];
-    // arena offset: the runs of the groups before this one (k_compact's order)
-    unsigned long long off = surv_off[i];
-    for (int jj = 0; jj < j; jj++) {
-      if (pl->gflags0[jj] & BF_NEGATIVE) continue;
-      for (int x = 0; x < pl->gnsub[jj]; x++) {
-        const int lid = pl->gsub[jj][x];
-        if (lm >> lid & 1) off += loc[(uint64_t)lid * slot_ub + s].len;
-      }
-    }
-    gu8 *cp[NS];
+  DocView<NQ, RP> dv;
+  dv.rec = rec;
+  dv.present = 0;
+  bool empty_pos = false;
+  int siteRank = -1, docLang = 0;
+  uint32_t nrec = 0;
+#pragma unroll
+  for (int j = 0; j < NQ; j++) {
+    dv.beg[j] = dv.end[j] = (int)nrec;
+    if (j >= ng) continue;
+    const uint8_t gf0 = pl->gflags0[j];
+    if (gf0 & BF_NEGATIVE) continue;
+    const int gns = pl->gnsub[j];
+    // this group's runs: cursor, end, flags (m_bigramFlags of the shrunk
+    // sublist index: lists shrunk to empty are not sublists any more)
     uint32_t cu[NS], ce[NS];
-    uint64_t ck[NS];
     uint8_t cfl[NS];
-    bool cfirst[NS], live[NS];
+    bool live[NS];
+    gu8 *src[NS];
     int newIdx = 0;
 #pragma unroll
     for (int x = 0; x < NS; x++) {
       live[x] = false;
-      cp[x] = nullptr;
       cu[x] = ce[x] = 0;
-      ck[x] = 0;
       cfl[x] = 0;
-      cfirst[x] = false;
+      src[x] = nullptr;
       if (x < gns) {
         const int lid = pl->gsub[j][x];
-        if (anys >> lid & 1) {  // shrunk to empty: not a new sublist
-          cfl[x] = pl->gsubflags[j][newIdx];  // m_bigramFlags[new index]
+        if (anys >> lid & 1) {
+          cfl[x] = pl->gsubflags[j][newIdx];
           newIdx++;
           if (lm >> lid & 1) {
             const Loc lc = loc[(uint64_t)lid * slot_ub + s];
-            cp[x] = gl(pl->lists[lid].p);
-            cu[x] = lc.unit;
-            ce[x] = lc.unit + lc.len;
-            ck[x] = load6(cp[x] + (size_t)lc.unit * 6);
-            cfirst[x] = true;
+            src[x] = gl(pl->lists[lid].p) + (size_t)lc.unit * 6;
+            cu[x] = 0;
+            ce[x] = lc.len;
             live[x] = true;
           }
         }
       }
     }
-    uint64_t *rec = arena + off;
-    uint32_t nrec = 0;
+    // x must be a compile-time index (unrolled loops): a runtime one would
+    // put src[] in scratch
+    auto unit_at = [&](int x, uint32_t c) -> uint64_t { return load6(src[x] + (size_t)c * 6); };
+    uint64_t ck[NS];
+    bool cfirst[NS];
+#pragma unroll
+    for (int x = 0; x < NS; x++) {
+      cfirst[x] = live[x];
+      ck[x] = live[x] ? unit_at(x, cu[x]) : 0;
+    }
+    const uint32_t start = nrec;
     uint32_t mbytes = 0;  // emulates mptr - mbuf (cap 299000, Posdb.cpp:6007-6008)
     bool isFirstKey = true;
     uint64_t last = 0;
-    gu8 *firstSrc = nullptr;
+    bool hasFirst = false;
     for (;;) {
       int mink = -1;
       uint32_t mhi = 0, mlo = 0;
@@ -966,15 +955,15 @@ __global__ void __launch_bounds__(BLOCK) k_minimerge(const DevPlan *pl, const ui
         }
       }
       if (mink == -1) break;
-      uint64_t r = 0;
+      uint64_t r = 0, hi6 = 0;
       uint8_t fl = 0;
-      gu8 *src = nullptr;
 #pragma unroll
       for (int x = 0; x < NS; x++) {
         if (x == mink) {
           r = ck[x];
           fl = cfl[x];
-          src = cp[x] + (size_t)cu[x] * 6;
+          // the bytes after the first emitted key (its siteRank / langId)
+          if (isFirstKey) hi6 = unit_at(x, cu[x] + 1);
         }
       }
       const bool hack = (fl & BF_BIGRAM) && ((r >> 16) & 0x03);  // Posdb.cpp:6687-6692
@@ -984,12 +973,20 @@ __global__ void __launch_bounds__(BLOCK) k_minimerge(const DevPlan *pl, const ui
         if (fl & BF_HALFSTOPWIKIBIGRAM) b2 |= 0x01;
         r = (r & ~(0xffull << 16)) | (b2 << 16);
         if (isFirstKey) {
+          // siteRank / langId of the key copied as 12 bytes (Posdb.h:308-315)
+          const uint32_t b0 = (uint32_t)(r & 0xff), b6 = (uint32_t)(hi6 & 0xff), b7 = (uint32_t)((hi6 >> 8) & 0xff);
+          const int sr = (int)(((b6 >> 5) | ((b7 & 1) << 3)) & 0x0f);
+          const int lg = (int)((b6 & 0x1f) | ((b0 & 0x08) ? 0x20 : 0));
           r = (r & ~0xffull) | (((r & 0xff) & 0xf9) | 0x02);
           rec[nrec++] = r;
           last = r;
           mbytes += 12;
           isFirstKey = false;
-          firstSrc = src;
+          hasFirst = true;
+          if (siteRank < 0 && !(gf0 & (BF_NUMBER | BF_FACET))) {
+            siteRank = sr;
+            docLang = lg;
+          }
         } else {
           const bool dup = (((last >> 32) & 0xffff) == ((r >> 32) & 0xffff)) &&
                            (((last >> 24) & 0xc0) == ((r >> 24) & 0xc0));
@@ -1007,63 +1004,53 @@ __global__ void __launch_bounds__(BLOCK) k_minimerge(const DevPlan *pl, const ui
           cu[x] += cfirst[x] ? 2 : 1;
           cfirst[x] = false;
           if (cu[x] >= ce[x]) live[x] = false;
-          else ck[x] = load6(cp[x] + (size_t)cu[x] * 6);
+          else ck[x] = unit_at(x, cu[x]);
         }
       }
       if (mbytes >= 299000) break;
     }
-    uint32_t info = nrec | GR_POSITIVE;
-    if (firstSrc) {
-      uint8_t k12[12];
-      for (int b = 0; b < 12; b++) k12[b] = firstSrc[b];
-      info |= GR_HASFIRST | (gb_siterank(k12) << 17) | (gb_langid(k12) << 21);
-    }
-    grange[(size_t)i * ng + j] = GRange{(uint32_t)off, info};
+    (void)hasFirst;
+    dv.beg[j] = (int)start;
+    dv.end[j] = (int)nrec;
+    dv.present |= 1u << j;
+    if (nrec == start) empty_pos = true;  // reference reads stale mbuf here (UB)
   }
+  float score = 0.0f;
+  if (diag == 1) {  // diagnostic: mini-merge only
+    *key_out = nrec + 1;
+    return;
+  }
+  const bool ok = !empty_pos && score_doc<NQ>(&c_weights, pl, dv, siteRank < 0 ? 0 : siteRank, docLang, smcol,
+                                              SCORE_TPB, &score);
+  uint32_t key = 0;
+  if (ok) {
+    const uint32_t b = __float_as_uint(score);
+    key = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+    if (key == 0) key = 1;
+  }
+  *key_out = key;
 }
 
-// Scoring, one lane per survivor (Posdb.cpp:6847-7257 via scoring.h).  NQ =
-// group capacity of this instance; the pair score matrix is an LDS column
-// per lane.
-template <int NQ, int TPB>
-__global__ void __launch_bounds__(TPB) k_score(const DevPlan *pl, const uint64_t *cand, const Counters *ctr,
-                                               const uint32_t *surv, const GRange *grange, const uint64_t *arena,
-                                               uint32_t *skey, uint64_t *sdoc) {
-  __shared__ float s_sm[npairs<NQ>() * TPB];
+// One lane per survivor, grid-stride.  (Measured alternatives: staging each
+// survivor's runs and records in lane-private LDS halves occupancy for no
+// gain -- the scorers are bound by their per-record instruction chains, not
+// by record reads -- and splitting survivors into size tiers adds one launch
+// tail per tier.)
+template <int NQ, int NS>
+__global__ void __launch_bounds__(SCORE_TPB) k_score(const DevPlan *pl, const uint64_t *cand, const Counters *ctr,
+                                                     const uint32_t *surv, const uint32_t *surv_lm,
+                                                     const unsigned long long *surv_off, const Loc *loc,
+                                                     uint64_t slot_ub, uint64_t *arena, uint32_t *skey,
+                                                     uint64_t *sdoc, int diag) {
+  __shared__ float s_sm[npairs<NQ>() * SCORE_TPB];
+  stage_weights(&c_weights);
   const uint32_t nsurv = (uint32_t)(ctr->surv_top >> 36);
-  const int ng = pl->ngroups;
-  for (uint32_t i = blockIdx.x * TPB + threadIdx.x; i < nsurv; i += gridDim.x * TPB) {
-    DocView<NQ> dv;
-    dv.rec = arena;
-    dv.present = 0;
-    bool empty_pos = false;
-    int siteRank = -1, docLang = 0;
-#pragma unroll
-    for (int j = 0; j < NQ; j++) {
-      dv.beg[j] = dv.end[j] = 0;
-      if (j >= ng) continue;
-      const GRange g = grange[(size_t)i * ng + j];
-      dv.beg[j] = (int)g.start;
-      dv.end[j] = (int)(g.start + (g.info & 0xffff));
-      if (!(g.info & GR_POSITIVE)) continue;
-      dv.present |= 1u << j;
-      if ((g.info & 0xffff) == 0) empty_pos = true;  // reference reads stale mbuf here (UB)
-      if (siteRank < 0 && (g.info & GR_HASFIRST) && !(pl->gflags0[j] & (BF_NUMBER | BF_FACET))) {
-        siteRank = (int)((g.info >> 17) & 0xf);
-        docLang = (int)((g.info >> 21) & 0x3f);
-      }
-    }
-    float score = 0.0f;
-    const bool ok = !empty_pos && score_doc<NQ>(&c_weights, pl, dv, siteRank < 0 ? 0 : siteRank, docLang,
-                                                s_sm + threadIdx.x, TPB, &score);
-    uint32_t key = 0;
-    if (ok) {
-      const uint32_t b = __float_as_uint(score);
-      key = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
-      if (key == 0) key = 1;
-    }
-    skey[i] = key;
-    sdoc[i] = cand[surv[i]];
+  const uint32_t anys = ctr->anysurv;
+  for (uint32_t i = blockIdx.x * SCORE_TPB + threadIdx.x; i < nsurv; i += gridDim.x * SCORE_TPB) {
+    const uint32_t s = surv[i];
+    auto *rec = (__attribute__((address_space(1))) uint64_t *)(arena + surv_off[i]);
+    score_survivor<NQ, NS>(pl, s, surv_lm[i], anys, loc, slot_ub, rec, s_sm + threadIdx.x, &skey[i], diag);
+    sdoc[i] = cand[s];
   }
 }
 
@@ -1324,7 +1311,7 @@ struct gbgpu_ctx {
   std::mutex mu;
   std::vector<ListEntry> lists;
   // per-query device buffers (grown, then reused)
-  DevBuf tables, chunkcnt, cand, lmask, ulen, loc, surv, survoff, scratch, grange, skey, sdoc, sel, gath, res;
+  DevBuf tables, chunkcnt, cand, lmask, ulen, loc, surv, survoff, survlm, scratch, skey, sdoc, sel, gath, res;
   DevBuf dir;           // candidate directories, epoch-tagged (never cleared per query)
   uint32_t epoch = 0;
   uint8_t *h_stage = nullptr;  // pinned: query tables (host -> device, one copy)
@@ -1343,6 +1330,7 @@ struct gbgpu_ctx {
   int64_t scan_bytes = 0;
   bool profiling = false;
   int probe_mode = 0;  // diagnostic only (GBGPU_PROBE_MODE)
+  int score_mode = 0;  // diagnostic only (GBGPU_SCORE_MODE): 1 mini-merge without scoring
   hipEvent_t ev[7] = {};
   float last_ms[6] = {0, 0, 0, 0, 0, 0};
 };
@@ -1561,7 +1549,7 @@ static int enqueue(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms, const i
   rc2 |= ctx->surv.ensure(4 * slot_ub);
   rc2 |= ctx->survoff.ensure(8 * slot_ub);
   rc2 |= ctx->scratch.ensure(8 * scratch_ub);
-  rc2 |= ctx->grange.ensure(sizeof(GRange) * slot_ub * (uint64_t)hp.ngroups);
+  rc2 |= ctx->survlm.ensure(4 * slot_ub);
   rc2 |= ctx->skey.ensure(4 * slot_ub);
   rc2 |= ctx->sdoc.ensure(8 * slot_ub);
   rc2 |= ctx->sel.ensure(sizeof(Select));
@@ -1634,39 +1622,23 @@ static int enqueue(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms, const i
   if (ctx->profiling) HIPCHECK(hipEventRecord(ctx->ev[2], st));
   const uint32_t cgrid = (uint32_t)((slot_ub + CTILE - 1) / CTILE);
   hipLaunchKernelGGL(k_compact, dim3(std::max(cgrid, 1u)), dim3(BLOCK), 0, st, dpl, lmask, ctx->ulen.as<uint32_t>(), slot_ub, dctr,
-                     ctx->surv.as<uint32_t>(), ctx->survoff.as<unsigned long long>());
+                     ctx->surv.as<uint32_t>(), ctx->survoff.as<unsigned long long>(), ctx->survlm.as<uint32_t>());
   if (ctx->profiling) HIPCHECK(hipEventRecord(ctx->ev[3], st));
   {
     int maxsub = 0;
     for (int j = 0; j < hp.ngroups; j++)
       if (!(P.gflags0[j] & BF_NEGATIVE)) maxsub = std::max(maxsub, (int)P.gnsub[j]);
-    const uint32_t mgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((slot_ub + BLOCK - 1) / BLOCK, 1024));
-    GRange *dgr = ctx->grange.as<GRange>();
-    uint64_t *arena = ctx->scratch.as<uint64_t>();
-    const uint32_t *dsurv = ctx->surv.as<uint32_t>();
-    if (maxsub <= 4)
-      hipLaunchKernelGGL(k_minimerge<4>, dim3(mgrid, hp.ngroups), dim3(BLOCK), 0, st, dpl, lmask, loc, slot_ub, dctr,
-                         dsurv, ctx->survoff.as<unsigned long long>(), arena, dgr);
-    else
-      hipLaunchKernelGGL(k_minimerge<MAXSUB>, dim3(mgrid, hp.ngroups), dim3(BLOCK), 0, st, dpl, lmask, loc, slot_ub,
-                         dctr, dsurv, ctx->survoff.as<unsigned long long>(), arena, dgr);
-    const uint32_t sg256 = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((slot_ub + 255) / 256, 2048));
-    const uint32_t sg64 = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((slot_ub + 63) / 64, 8192));
-    const uint64_t *dcand = ctx->cand.as<uint64_t>();
-    uint32_t *dskey = ctx->skey.as<uint32_t>();
-    uint64_t *dsdoc = ctx->sdoc.as<uint64_t>();
-    if (hp.ngroups <= 2)
-      hipLaunchKernelGGL((k_score<2, 256>), dim3(sg256), dim3(256), 0, st, dpl, dcand, dctr, dsurv, dgr, arena, dskey,
-                         dsdoc);
-    else if (hp.ngroups <= 4)
-      hipLaunchKernelGGL((k_score<4, 256>), dim3(sg256), dim3(256), 0, st, dpl, dcand, dctr, dsurv, dgr, arena, dskey,
-                         dsdoc);
-    else if (hp.ngroups <= 8)
-      hipLaunchKernelGGL((k_score<8, 256>), dim3(sg256), dim3(256), 0, st, dpl, dcand, dctr, dsurv, dgr, arena, dskey,
-                         dsdoc);
-    else
-      hipLaunchKernelGGL((k_score<MAXG, 64>), dim3(sg64), dim3(64), 0, st, dpl, dcand, dctr, dsurv, dgr, arena, dskey,
-                         dsdoc);
+    const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((slot_ub + SCORE_TPB - 1) / SCORE_TPB, 8192));
+    auto launch = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(SCORE_TPB), 0, st, dpl, ctx->cand.as<uint64_t>(), dctr,
+                         ctx->surv.as<uint32_t>(), ctx->survlm.as<uint32_t>(), ctx->survoff.as<unsigned long long>(),
+                         loc, slot_ub, ctx->scratch.as<uint64_t>(), ctx->skey.as<uint32_t>(),
+                         ctx->sdoc.as<uint64_t>(), ctx->score_mode);
+    };
+    if (hp.ngroups <= 2 && maxsub <= 4) launch(k_score<2, 4>);
+    else if (hp.ngroups <= 4 && maxsub <= 4) launch(k_score<4, 4>);
+    else if (hp.ngroups <= 8 && maxsub <= 4) launch(k_score<8, 4>);
+    else launch(k_score<MAXG, MAXSUB>);
   }
   if (ctx->profiling) HIPCHECK(hipEventRecord(ctx->ev[4], st));
   // top-k: radix select over the survivors' keys, then one LDS sort
@@ -1767,6 +1739,7 @@ int gbgpu_open(int device, gbgpu_ctx **out) {
   }
   for (auto &e : ctx->ev) (void)hipEventCreate(&e);
   if (const char *pm = std::getenv("GBGPU_PROBE_MODE")) ctx->probe_mode = std::atoi(pm);
+  if (const char *sm = std::getenv("GBGPU_SCORE_MODE")) ctx->score_mode = std::atoi(sm);
   *out = ctx;
   return 0;
 }
@@ -1778,7 +1751,7 @@ void gbgpu_close(gbgpu_ctx *ctx) {
   for (auto &e : ctx->lists)
     if (e.live) (void)hipFree(e.d);
   DevBuf *bufs[] = {&ctx->tables, &ctx->chunkcnt, &ctx->cand, &ctx->lmask, &ctx->ulen, &ctx->loc, &ctx->surv,
-                    &ctx->survoff, &ctx->scratch, &ctx->grange, &ctx->skey, &ctx->sdoc, &ctx->sel, &ctx->gath, &ctx->res,
+                    &ctx->survoff, &ctx->survlm, &ctx->scratch, &ctx->skey, &ctx->sdoc, &ctx->sel, &ctx->gath, &ctx->res,
                     &ctx->dir};
   for (auto *b : bufs) b->release();
   if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);

@@ -41,6 +41,18 @@ struct Weights {
   uint8_t compatible[16][16];
 };
 
+// The tables as every scoring kernel reads them: staged into LDS at kernel
+// start (stage_weights), so a lookup by a per-lane index is one ds_read
+// instead of a dependent global load.
+__shared__ Weights s_weights;
+
+__device__ __forceinline__ void stage_weights(const Weights *src) {
+  static_assert(sizeof(Weights) % 4 == 0, "Weights is copied as words");
+  for (int i = threadIdx.x; i < (int)(sizeof(Weights) / 4); i += blockDim.x)
+    reinterpret_cast<uint32_t *>(&s_weights)[i] = reinterpret_cast<const uint32_t *>(src)[i];
+  __syncthreads();
+}
+
 // record field accessors (Posdb.h:319-361 on key bytes 0..5)
 __host__ __device__ __forceinline__ uint32_t r_wordpos(uint64_t r) { return (uint32_t)(r >> 30) & 0x3ffff; }
 __host__ __device__ __forceinline__ uint32_t r_hg(uint64_t r) { return (uint32_t)(r >> 26) & 0xf; }
@@ -75,10 +87,12 @@ constexpr int npairs() {
   return NQ * (NQ - 1) / 2;
 }
 
-// What one docid's scorer sees: nq groups, each a record range.
-template <int NQ>
+// What one docid's scorer sees: nq groups, each a record range.  RP is the
+// record pointer type: an LDS (address space 3) or global (1) pointer, so
+// every record read compiles to a ds_read or global_load, never a flat one.
+template <int NQ, class RP = const uint64_t *>
 struct DocView {
-  const uint64_t *rec;  // record arena (ranges are absolute indices)
+  RP rec;  // records (ranges are indices into rec)
   int beg[NQ], end[NQ];
   uint32_t present;     // bit i: miniMergedList[i] != NULL (positive group)
 };
@@ -99,9 +113,9 @@ struct ScoreCtx {
 
 // getSingleTermScore, Posdb.cpp:3087-3301 (pdcs == NULL).  bestPos = record
 // index of the best non-body occurrence or -1.
-template <int NQ>
-__device__ __forceinline__ float single_term_score(const ScoreCtx<NQ> &c, const DocView<NQ> &d, int i, int *bestPos) {
-  const Weights &W = *c.w;
+template <int NQ, class RP>
+__device__ __forceinline__ float single_term_score(const ScoreCtx<NQ> &c, const DocView<NQ, RP> &d, int i, int *bestPos) {
+  const Weights &W = s_weights;
   float nonBodyMax = -1.0;
   int minx = 0;
   float minv = 0.0f;  // bestScores[minx]
@@ -206,9 +220,9 @@ __device__ __forceinline__ float single_term_score(const ScoreCtx<NQ> &c, const 
 }
 
 // getTermPairScoreForNonBody, Posdb.cpp:3305-3555
-template <int NQ>
-__device__ __forceinline__ float pair_score_nonbody(const ScoreCtx<NQ> &c, const DocView<NQ> &d, int i, int j, int qdist) {
-  const Weights &W = *c.w;
+template <int NQ, class RP>
+__device__ __forceinline__ float pair_score_nonbody(const ScoreCtx<NQ> &c, const DocView<NQ, RP> &d, int i, int j, int qdist) {
+  const Weights &W = s_weights;
   int wi = rget(d.beg, i), wj = rget(d.beg, j);
   const int endi = rget(d.end, i), endj = rget(d.end, j);
   uint64_t ki = d.rec[wi], kj = d.rec[wj];
@@ -275,7 +289,8 @@ __device__ __forceinline__ float pair_score_nonbody(const ScoreCtx<NQ> &c, const
 }
 
 // getTermPairScoreForWindow, Posdb.cpp:3557-3625 (record index -1 = NULL)
-__device__ __forceinline__ float pair_score_window(const Weights &W, int cqdist, const uint64_t *rec, int wpi, int wpj,
+template <class RP>
+__device__ __forceinline__ float pair_score_window(const Weights &W, int cqdist, RP rec, int wpi, int wpj,
                                           int32_t fixedDistance) {
   if (wpi < 0) return -1.00;
   if (wpj < 0) return -1.00;
@@ -307,10 +322,10 @@ __device__ __forceinline__ float pair_score_window(const Weights &W, int cqdist,
 }
 
 // evalSlidingWindow, Posdb.cpp:1275-1511
-template <int NQ>
-__device__ __forceinline__ void eval_window(ScoreCtx<NQ> &c, const DocView<NQ> &d, const int (&ptrs)[NQ],
+template <int NQ, class RP>
+__device__ __forceinline__ void eval_window(ScoreCtx<NQ> &c, const DocView<NQ, RP> &d, const int (&ptrs)[NQ],
                                    const int (&bestPos)[NQ]) {
-  const Weights &W = *c.w;
+  const Weights &W = s_weights;
   const DevPlan *pl = c.pl;
   float minTermPairScoreInWindow = 999999999.0;
   const int nr = c.nq;
@@ -366,9 +381,9 @@ __device__ __forceinline__ void eval_window(ScoreCtx<NQ> &c, const DocView<NQ> &
 }
 
 // getTermPairScoreForAny, Posdb.cpp:3631-4344 (pdcs == NULL)
-template <int NQ>
-__device__ __forceinline__ float pair_score_any(const ScoreCtx<NQ> &c, const DocView<NQ> &d, int i, int j) {
-  const Weights &W = *c.w;
+template <int NQ, class RP>
+__device__ __forceinline__ float pair_score_any(const ScoreCtx<NQ> &c, const DocView<NQ, RP> &d, int i, int j) {
+  const Weights &W = s_weights;
   const DevPlan *pl = c.pl;
   float wts;
   int32_t qdist;
@@ -543,8 +558,8 @@ __device__ __forceinline__ float pair_score_any(const ScoreCtx<NQ> &c, const Doc
 // (minScore <= 0); siteRank/docLang come from the first key of the first
 // present group (Posdb.cpp:6985-7003).  sm: this lane's score-matrix column
 // (npairs<NQ>() floats at stride smStride).
-template <int NQ>
-__device__ __forceinline__ bool score_doc(const Weights *w, const DevPlan *pl, const DocView<NQ> &d, int siteRank, int docLang,
+template <int NQ, class RP>
+__device__ __forceinline__ bool score_doc(const Weights *w, const DevPlan *pl, const DocView<NQ, RP> &d, int siteRank, int docLang,
                                  float *sm, int smStride, float *outScore) {
   ScoreCtx<NQ> c;
   c.w = w;
@@ -610,7 +625,7 @@ __device__ __forceinline__ bool score_doc(const Weights *w, const DevPlan *pl, c
   for (int i = 0; i < NQ; i++) {
     if (i < c.nq && !(c.excl >> i & 1)) {
       int xp = xpos[i];
-      while (xp >= 0 && !w->in_body[r_hg(d.rec[xp])]) {
+      while (xp >= 0 && !s_weights.in_body[r_hg(d.rec[xp])]) {
         xp++;
         if (xp >= d.end[i]) xp = -1;
       }
@@ -645,7 +660,7 @@ __device__ __forceinline__ bool score_doc(const Weights *w, const DevPlan *pl, c
             exhausted = true;
             break;
           }
-          if (w->in_body[r_hg(d.rec[xp])]) break;
+          if (s_weights.in_body[r_hg(d.rec[xp])]) break;
         }
         rset(xpos, minx, xp);
         if (!exhausted) break;  // -> slideMore
