@@ -69,10 +69,11 @@ def cpu_baseline(q, num_docs_total: int, budget_s: float = 12.0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--docs-per-gpu", type=int, default=100_000_000)
     ap.add_argument("--docs-to-get", type=int, default=100)
+    ap.add_argument("--slots", type=int, default=2, help="queries in flight per GPU (query slots)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -85,6 +86,7 @@ def main():
     import torch
     import torch.distributed as dist
     import gbgpu
+    from shard_merge import gather_merge
     from workload import config_two_term, generate
 
     torch.cuda.set_device(local_rank)
@@ -104,44 +106,49 @@ def main():
     p = q.params()
     k = p.docs_to_get
 
-    def one_step(profile=False):
-        eng.enqueue(q.terms, handles, p)
-        r = eng.collect(cap=4096)
-        if world > 1:
-            # Msg39Reply payload: (docid, score) per shard -> RCCL allgather
-            rec = torch.zeros((k, 2), dtype=torch.float64, device="cuda")
-            n = len(r.docids)
-            if n:
-                rec[:n, 0] = torch.from_numpy(r.docids.astype(np.float64)).cuda()
-                rec[:n, 1] = torch.from_numpy(r.scores.astype(np.float64)).cuda()
-            rec[n:, 1] = -1.0
-            cnt = torch.tensor([n, r.hits], dtype=torch.int64, device="cuda")
-            out = torch.empty((world, k, 2), dtype=torch.float64, device="cuda")
-            dist.all_gather_into_tensor(out, rec)
-            cnts = torch.empty((world, 2), dtype=torch.int64, device="cuda")
-            dist.all_gather_into_tensor(cnts, cnt)
-            out_h, cnts_h = out.cpu().numpy(), cnts.cpu().numpy()
-            shards = [(out_h[w, :cnts_h[w, 0], 0].astype(np.int64), out_h[w, :cnts_h[w, 0], 1].astype(np.float32))
-                      for w in range(world)]
-            d, s = gbgpu.merge_topk(shards, p.docs_to_get)
-            return r, int(cnts_h[:, 1].sum()), d
-        return r, r.hits, r.docids[:p.docs_to_get]
+    slots = max(1, args.slots)
+    eng.set_slots(slots)
 
-    for _ in range(args.warmup):
-        one_step()
+    def finish(r):
+        """Msg39Reply -> Msg3a: per-shard top lists all-gathered over RCCL and
+        merged (shard_merge.py); returns (total hits, merged docids)."""
+        if world == 1:
+            return r.hits, r.docids[:k]
+        hits, d, _ = gather_merge(r.docids, r.scores, r.hits, k, device="cuda")
+        return hits, d
+
+    def run(nq):
+        """nq queries with `slots` of them in flight (round-robin over the
+        slots: a slot's previous query is collected before it is reused)."""
+        hits, top = 0, None
+        for i in range(nq):
+            slot = i % slots
+            if i >= slots:
+                hits, top = finish(eng.collect(cap=4096, slot=slot))
+            eng.enqueue(q.terms, handles, p, slot=slot)
+        for i in range(max(0, nq - slots), nq):
+            hits, top = finish(eng.collect(cap=4096, slot=i % slots))
+        return hits, top
+
+    run(args.warmup * slots)
+    # per-phase device times and the probe roofline: queries one at a time
+    # (untimed; concurrent queries would overlap each other's events)
     eng.set_profiling(True)
-    probe_ms, total_dev_ms, phase_ms = [], [], []
+    phase_ms = []
+    for _ in range(max(5, args.steps // 2)):
+        eng.enqueue(q.terms, handles, p, slot=0)
+        finish(eng.collect(cap=4096, slot=0))
+        ms, scan_bytes = eng.last_timings(slot=0)
+        phase_ms.append(ms)
+    eng.set_profiling(False)
+    probe_ms = [m[2] for m in phase_ms]
+    total_dev_ms = [m[0] for m in phase_ms]
+
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    hits = 0
-    for _ in range(args.steps):
-        r, hits, top = one_step()
-        ms, scan_bytes = eng.last_timings()
-        total_dev_ms.append(ms[0])
-        probe_ms.append(ms[2])
-        phase_ms.append(ms)
+    hits, top = run(args.steps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -155,7 +162,6 @@ def main():
         agg_list_bytes = float(lb.item())
     else:
         agg_list_bytes = float(list_bytes)
-    eng.set_profiling(False)
 
     ms_per_step = el * 1000.0 / args.steps
     qps = args.steps / el
@@ -174,6 +180,7 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 4),
+        "queries_in_flight": slots,
         "device_ms_per_query": round(float(np.mean(total_dev_ms)), 4),
         "phase_ms": dict(zip(["total", "candidates", "probe", "compact", "score", "topk"],
                              [round(float(x), 4) for x in np.mean(np.array(phase_ms), axis=0)])),

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define GBGPU_ABI_VERSION 1
+#define GBGPU_ABI_VERSION 2
 
 /* error codes beyond errno.h (Errno.h numbering is not reused) */
 #define GBGPU_ENODEVICE   1001 /* no HIP device / extension not usable        */
@@ -102,17 +102,31 @@ int gbgpu_query(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms, const gbgp
  * Posdb.cpp:5671-5703 is applied to the device copy) and query it many times. */
 int gbgpu_list_upload(gbgpu_ctx *ctx, const uint8_t *bytes, int64_t size, int32_t *handle);
 int gbgpu_list_free(gbgpu_ctx *ctx, int32_t handle);
+/* gbgpu_query and gbgpu_query_resident are re-entrant: Msg39 runs several
+ * intersect threads at once (Msg39.cpp:1019-1027, Parms.cpp:12356); each call
+ * takes a free query slot (its own HIP stream and buffers over the shared
+ * resident lists) and waits for one when all are busy. */
 int gbgpu_query_resident(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms,
                          const int32_t *handles, const gbgpu_params *p, gbgpu_result *out);
 
-/* Asynchronous form used by the benchmark: enqueue a resident query on the
- * context's stream (no host synchronisation), then collect its result.  At
- * most one query may be in flight per context. */
+/* Query slots: a context starts with one; grow the pool to n (<= 64) so that
+ * n queries can be in flight at once.  Returns 0 or an errno-style code. */
+int gbgpu_set_query_slots(gbgpu_ctx *ctx, int n);
+int gbgpu_query_slots(gbgpu_ctx *ctx);
+
+/* Asynchronous form: enqueue a resident query on a slot's stream (no host
+ * synchronisation; EBUSY if that slot still holds an uncollected query),
+ * then collect its result (waits for that slot's stream only). */
+int gbgpu_query_slot_enqueue(gbgpu_ctx *ctx, int slot, const gbgpu_qterm *terms, int nterms,
+                             const int32_t *handles, const gbgpu_params *p);
+int gbgpu_query_slot_collect(gbgpu_ctx *ctx, int slot, gbgpu_result *out);
+/* slot 0 shorthands */
 int gbgpu_query_resident_enqueue(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms,
                                  const int32_t *handles, const gbgpu_params *p);
 int gbgpu_query_collect(gbgpu_ctx *ctx, gbgpu_result *out);
-/* the context's HIP stream (hipStream_t), for callers that order work on it */
-void *gbgpu_stream(gbgpu_ctx *ctx);
+/* a slot's HIP stream (hipStream_t), for callers that order work on it */
+void *gbgpu_slot_stream(gbgpu_ctx *ctx, int slot);
+void *gbgpu_stream(gbgpu_ctx *ctx); /* slot 0 */
 /* device copy of the last query's top list (the Msg39Reply payload for an RCCL
  * allgather): *n uint32 order-preserving score keys (0 = empty slot), then at
  * the next 256-byte boundary *n int64 docids.  Valid after gbgpu_query_collect. */
@@ -131,11 +145,12 @@ int gbgpu_merge_topk(const int64_t *const *shard_docids, const float *const *sha
 int gbgpu_merge_posdb(gbgpu_ctx *ctx, const gbgpu_list *lists, int n, int remove_neg_keys,
                       int64_t min_rec_sizes, uint8_t *out, int64_t out_cap, int64_t *out_size);
 
-/* Per-query device timings of the last query (HIP events on the ctx stream),
+/* Per-query device timings of a slot's last query (HIP events on its stream),
  * in milliseconds: [0]=total, [1]=candidate extraction, [2]=list probe scan,
  * [3]=compaction, [4]=scoring, [5]=top-k.  Enable with gbgpu_set_profiling. */
 int gbgpu_set_profiling(gbgpu_ctx *ctx, int enable);
-int gbgpu_last_timings(gbgpu_ctx *ctx, float *ms6, int64_t *scan_bytes);
+int gbgpu_slot_timings(gbgpu_ctx *ctx, int slot, float *ms6, int64_t *scan_bytes);
+int gbgpu_last_timings(gbgpu_ctx *ctx, float *ms6, int64_t *scan_bytes); /* slot 0 */
 
 #ifdef __cplusplus
 }

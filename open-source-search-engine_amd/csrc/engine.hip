@@ -43,6 +43,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
 #include <mutex>
 #include <vector>
 
@@ -1305,12 +1306,12 @@ static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 using namespace gbgpu;
 
-struct gbgpu_ctx {
-  int device = 0;
-  hipStream_t stream = nullptr;
+// One query in flight: its stream, device buffers (grown, then reused),
+// pinned staging and result state.  A context owns one or more slots; the
+// resident lists are shared by all of them.
+struct QuerySlot {
   std::mutex mu;
-  std::vector<ListEntry> lists;
-  // per-query device buffers (grown, then reused)
+  hipStream_t stream = nullptr;
   DevBuf tables, chunkcnt, cand, lmask, ulen, loc, surv, survoff, survlm, scratch, skey, sdoc, sel, gath, res;
   DevBuf dir;           // candidate directories, epoch-tagged (never cleared per query)
   uint32_t epoch = 0;
@@ -1328,11 +1329,43 @@ struct gbgpu_ctx {
   size_t res_bytes = 0;
   int32_t docs_wanted = 0;
   int64_t scan_bytes = 0;
+  hipEvent_t ev[7] = {};
+  float last_ms[6] = {0, 0, 0, 0, 0, 0};
+
+  int init() {
+    if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return GBGPU_EHIP;
+    for (auto &e : ev)
+      if (hipEventCreate(&e) != hipSuccess) return GBGPU_EHIP;
+    return 0;
+  }
+  void release() {
+    if (stream) (void)hipStreamSynchronize(stream);
+    DevBuf *bufs[] = {&tables, &chunkcnt, &cand, &lmask, &ulen, &loc, &surv, &survoff, &survlm,
+                      &scratch, &skey, &sdoc, &sel, &gath, &res, &dir};
+    for (auto *b : bufs) b->release();
+    if (h_stage) (void)hipHostFree(h_stage);
+    if (h_res) (void)hipHostFree(h_res);
+    h_stage = h_res = nullptr;
+    for (auto &e : ev)
+      if (e) (void)hipEventDestroy(e);
+    if (stream) (void)hipStreamDestroy(stream);
+    stream = nullptr;
+  }
+};
+
+constexpr int MAX_SLOTS = 64;
+
+struct gbgpu_ctx {
+  int device = 0;
+  hipStream_t upload_stream = nullptr;
+  std::mutex lists_mu;
+  std::vector<ListEntry> lists;
+  std::mutex slots_mu;  // guards growth of the slot table
+  QuerySlot *slots[MAX_SLOTS] = {};
+  int nslots = 0;
   bool profiling = false;
   int probe_mode = 0;  // diagnostic only (GBGPU_PROBE_MODE)
   int score_mode = 0;  // diagnostic only (GBGPU_SCORE_MODE): 1 mini-merge without scoring
-  hipEvent_t ev[7] = {};
-  float last_ms[6] = {0, 0, 0, 0, 0, 0};
 };
 
 // result block layout: [Counters | keys k | docids k]
@@ -1349,18 +1382,18 @@ static int upload_list(gbgpu_ctx *ctx, const uint8_t *bytes, int64_t size, int32
   size_t alloc = (size_t)(size ? size - 6 : 0) + LIST_PAD;
   alloc = align256(alloc);
   if (hipMalloc(&e.d, alloc) != hipSuccess) return ENOMEM;
-  HIPCHECK(hipMemsetAsync(e.d, 0, alloc, ctx->stream));
+  HIPCHECK(hipMemsetAsync(e.d, 0, alloc, ctx->upload_stream));
   if (size) {
     // device image = the list after the first-key swap (Posdb.cpp:5689-5698):
     // original bytes 0..11 with the half bit set, then bytes 18..size-1
     uint8_t first[12];
     std::memcpy(first, bytes, 12);
     first[0] |= 0x02;
-    HIPCHECK(hipMemcpyAsync(e.d, first, 12, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHECK(hipMemcpyAsync(e.d, first, 12, hipMemcpyHostToDevice, ctx->upload_stream));
     if (size > 18)
-      HIPCHECK(hipMemcpyAsync(e.d + 12, bytes + 18, (size_t)(size - 18), hipMemcpyHostToDevice, ctx->stream));
+      HIPCHECK(hipMemcpyAsync(e.d + 12, bytes + 18, (size_t)(size - 18), hipMemcpyHostToDevice, ctx->upload_stream));
   }
-  HIPCHECK(hipStreamSynchronize(ctx->stream));
+  HIPCHECK(hipStreamSynchronize(ctx->upload_stream));
   if (size) {
     // the list's docid range (directory sizing): first key, last run start
     e.dmin = e.dmax = host_docid(bytes);
@@ -1384,32 +1417,37 @@ static int upload_list(gbgpu_ctx *ctx, const uint8_t *bytes, int64_t size, int32
   return 0;
 }
 
-static int enqueue(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms, const int32_t *handles,
+static int enqueue(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *terms, int nterms, const int32_t *handles,
                    const gbgpu_params *p) {
   if (!p || nterms < 0 || (nterms && (!terms || !handles))) return EINVAL;
   if (p->site_clustering || p->num_docid_splits > 1) return GBGPU_EUNSUPPORTED;
   if (p->docs_to_get <= 0 || p->real_max_top <= 0) return EINVAL;
   if (nterms > 1024) return GBGPU_EUNSUPPORTED;
   std::vector<int64_t> sizes(nterms);
-  for (int i = 0; i < nterms; i++) {
-    if (terms[i].field_code) return GBGPU_EUNSUPPORTED;
-    int32_t h = handles[i];
-    if (h < 0 || h >= (int32_t)ctx->lists.size() || !ctx->lists[h].live) return EINVAL;
-    sizes[i] = ctx->lists[h].size;
+  std::vector<ListEntry> ents(nterms);  // snapshot: the table may grow under us
+  {
+    std::lock_guard<std::mutex> g(ctx->lists_mu);
+    for (int i = 0; i < nterms; i++) {
+      if (terms[i].field_code) return GBGPU_EUNSUPPORTED;
+      int32_t h = handles[i];
+      if (h < 0 || h >= (int32_t)ctx->lists.size() || !ctx->lists[h].live) return EINVAL;
+      ents[i] = ctx->lists[h];
+      sizes[i] = ents[i].size;
+    }
   }
   HostPlan hp;
   int rc = build_host_plan(terms, nterms, sizes.data(), p, &hp);
   if (rc) return rc;
-  ctx->docs_wanted = hp.docs_wanted;
-  ctx->k = hp.docs_wanted;
-  ctx->early = (hp.ngroups == 0 || hp.min_list_size == 0);
-  ctx->scan_bytes = 0;
-  if (ctx->early) {
-    ctx->pending = true;
+  q.docs_wanted = hp.docs_wanted;
+  q.k = hp.docs_wanted;
+  q.early = (hp.ngroups == 0 || hp.min_list_size == 0);
+  q.scan_bytes = 0;
+  if (q.early) {
+    q.pending = true;
     return 0;
   }
   if (hp.ngroups > MAXG) return GBGPU_EUNSUPPORTED;
-  if (ctx->k > MAX_K) return GBGPU_EUNSUPPORTED;
+  if (q.k > MAX_K) return GBGPU_EUNSUPPORTED;
 
   // ---- query tables, built straight into the pinned staging buffer
   // layout: [DevPlan | G0Chunk[] | afirst[MAXG0] | ProbeWork[]]
@@ -1429,7 +1467,7 @@ static int enqueue(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms, const i
     if (P.nlists >= MAXL) return -1;
     int id = P.nlists++;
     dense[term] = id;
-    const ListEntry &e = ctx->lists[handles[term]];
+    const ListEntry &e = ents[term];
     P.lists[id].p = e.d;
     P.lists[id].units = e.units;
     list_dmin[id] = e.dmin;
@@ -1500,14 +1538,14 @@ static int enqueue(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms, const i
     P.lists[id].probe = per_chunk > 64.0 ? PROBE_BY_RUN : PROBE_BY_CAND;
   }
 
-  ctx->g0c.clear();
-  ctx->afirst.assign(MAXG0, 0);
+  q.g0c.clear();
+  q.afirst.assign(MAXG0, 0);
   for (int a = 0; a < P.g0n; a++) {
-    ctx->afirst[a] = (uint32_t)ctx->g0c.size();
+    q.afirst[a] = (uint32_t)q.g0c.size();
     const uint32_t units = P.lists[P.g0list[a]].units;
-    for (uint32_t u = 0; u < units; u += CHUNK_UNITS) ctx->g0c.push_back({(uint32_t)a, u});
+    for (uint32_t u = 0; u < units; u += CHUNK_UNITS) q.g0c.push_back({(uint32_t)a, u});
   }
-  ctx->pw.clear();
+  q.pw.clear();
   int64_t scan = 0;
   uint64_t probe_chunks = 0;
   for (int id = 0; id < P.nlists; id++) {
@@ -1523,9 +1561,9 @@ static int enqueue(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms, const i
     const uint32_t units = P.lists[id].units;
     // a run-driven chunk costs a few dependent lookups: one chunk per wave
     const uint32_t span = WCH_UNITS * (P.lists[id].probe == PROBE_BY_RUN ? 1 : S);
-    for (uint32_t u = 0; u < units; u += span) ctx->pw.push_back({(uint32_t)id, u, std::min(units, u + span)});
+    for (uint32_t u = 0; u < units; u += span) q.pw.push_back({(uint32_t)id, u, std::min(units, u + span)});
   }
-  ctx->scan_bytes = scan;
+  q.scan_bytes = scan;
   // scratch upper bound: every group instance can use all of its list once
   uint64_t scratch_ub = 1;
   for (int j = 0; j < hp.ngroups; j++) {
@@ -1533,80 +1571,80 @@ static int enqueue(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms, const i
     for (int x = 0; x < P.gnsub[j]; x++) scratch_ub += P.lists[P.gsub[j][x]].units;
   }
   if (scratch_ub >= (1ull << 36)) return GBGPU_ECAPACITY;
-  const int k = ctx->k;
+  const int k = q.k;
   const size_t o_chunks = align256(sizeof(DevPlan));
-  const size_t o_afirst = o_chunks + align256(sizeof(G0Chunk) * ctx->g0c.size());
+  const size_t o_afirst = o_chunks + align256(sizeof(G0Chunk) * q.g0c.size());
   const size_t o_work = o_afirst + align256(4 * MAXG0);
-  const size_t tbytes = o_work + align256(sizeof(ProbeWork) * ctx->pw.size());
-  ctx->res_bytes = res_size(k);
+  const size_t tbytes = o_work + align256(sizeof(ProbeWork) * q.pw.size());
+  q.res_bytes = res_size(k);
   int rc2 = 0;
-  rc2 |= ctx->tables.ensure(tbytes);
-  rc2 |= ctx->chunkcnt.ensure(4 * std::max<size_t>(1, ctx->g0c.size()));
-  rc2 |= ctx->cand.ensure(8 * slot_ub);
-  rc2 |= ctx->lmask.ensure(4 * slot_ub);
-  rc2 |= ctx->ulen.ensure(4 * slot_ub);
-  rc2 |= ctx->loc.ensure(sizeof(Loc) * slot_ub * (uint64_t)P.nlists);
-  rc2 |= ctx->surv.ensure(4 * slot_ub);
-  rc2 |= ctx->survoff.ensure(8 * slot_ub);
-  rc2 |= ctx->scratch.ensure(8 * scratch_ub);
-  rc2 |= ctx->survlm.ensure(4 * slot_ub);
-  rc2 |= ctx->skey.ensure(4 * slot_ub);
-  rc2 |= ctx->sdoc.ensure(8 * slot_ub);
-  rc2 |= ctx->sel.ensure(sizeof(Select));
-  rc2 |= ctx->gath.ensure(12 * (slot_ub + MAX_K) + 1024);
-  rc2 |= ctx->res.ensure(ctx->res_bytes);
-  const void *dir_before = ctx->dir.p;
-  rc2 |= ctx->dir.ensure(8 * std::max<uint64_t>(1, dir_entries));
+  rc2 |= q.tables.ensure(tbytes);
+  rc2 |= q.chunkcnt.ensure(4 * std::max<size_t>(1, q.g0c.size()));
+  rc2 |= q.cand.ensure(8 * slot_ub);
+  rc2 |= q.lmask.ensure(4 * slot_ub);
+  rc2 |= q.ulen.ensure(4 * slot_ub);
+  rc2 |= q.loc.ensure(sizeof(Loc) * slot_ub * (uint64_t)P.nlists);
+  rc2 |= q.surv.ensure(4 * slot_ub);
+  rc2 |= q.survoff.ensure(8 * slot_ub);
+  rc2 |= q.scratch.ensure(8 * scratch_ub);
+  rc2 |= q.survlm.ensure(4 * slot_ub);
+  rc2 |= q.skey.ensure(4 * slot_ub);
+  rc2 |= q.sdoc.ensure(8 * slot_ub);
+  rc2 |= q.sel.ensure(sizeof(Select));
+  rc2 |= q.gath.ensure(12 * (slot_ub + MAX_K) + 1024);
+  rc2 |= q.res.ensure(q.res_bytes);
+  const void *dir_before = q.dir.p;
+  rc2 |= q.dir.ensure(8 * std::max<uint64_t>(1, dir_entries));
   if (rc2) return ENOMEM;
-  if (ctx->dir.p != dir_before || ctx->epoch == 0xffffffffu) {
+  if (q.dir.p != dir_before || q.epoch == 0xffffffffu) {
     // fresh directory memory: no entry may carry a live epoch
-    HIPCHECK(hipMemsetAsync(ctx->dir.p, 0, ctx->dir.cap, ctx->stream));
-    ctx->epoch = 0;
+    HIPCHECK(hipMemsetAsync(q.dir.p, 0, q.dir.cap, q.stream));
+    q.epoch = 0;
   }
-  P.epoch = ++ctx->epoch;
-  if (tbytes > ctx->stage_cap) {
-    if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
-    ctx->h_stage = nullptr;
-    ctx->stage_cap = 0;
-    HIPCHECK(hipHostMalloc((void **)&ctx->h_stage, tbytes * 2));
-    ctx->stage_cap = tbytes * 2;
+  P.epoch = ++q.epoch;
+  if (tbytes > q.stage_cap) {
+    if (q.h_stage) (void)hipHostFree(q.h_stage);
+    q.h_stage = nullptr;
+    q.stage_cap = 0;
+    HIPCHECK(hipHostMalloc((void **)&q.h_stage, tbytes * 2));
+    q.stage_cap = tbytes * 2;
   }
-  if (ctx->res_bytes > ctx->hres_cap) {
-    if (ctx->h_res) (void)hipHostFree(ctx->h_res);
-    ctx->h_res = nullptr;
-    ctx->hres_cap = 0;
-    HIPCHECK(hipHostMalloc((void **)&ctx->h_res, ctx->res_bytes));
-    ctx->hres_cap = ctx->res_bytes;
+  if (q.res_bytes > q.hres_cap) {
+    if (q.h_res) (void)hipHostFree(q.h_res);
+    q.h_res = nullptr;
+    q.hres_cap = 0;
+    HIPCHECK(hipHostMalloc((void **)&q.h_res, q.res_bytes));
+    q.hres_cap = q.res_bytes;
   }
   // the staging buffer may still feed the previous query's copy: the stream
   // has been synchronised by collect() (one query in flight per context)
-  std::memcpy(ctx->h_stage, &P, sizeof P);
-  std::memcpy(ctx->h_stage + o_chunks, ctx->g0c.data(), sizeof(G0Chunk) * ctx->g0c.size());
-  std::memcpy(ctx->h_stage + o_afirst, ctx->afirst.data(), 4 * MAXG0);
-  std::memcpy(ctx->h_stage + o_work, ctx->pw.data(), sizeof(ProbeWork) * ctx->pw.size());
+  std::memcpy(q.h_stage, &P, sizeof P);
+  std::memcpy(q.h_stage + o_chunks, q.g0c.data(), sizeof(G0Chunk) * q.g0c.size());
+  std::memcpy(q.h_stage + o_afirst, q.afirst.data(), 4 * MAXG0);
+  std::memcpy(q.h_stage + o_work, q.pw.data(), sizeof(ProbeWork) * q.pw.size());
 
-  hipStream_t st = ctx->stream;
-  if (ctx->profiling) HIPCHECK(hipEventRecord(ctx->ev[0], st));
-  HIPCHECK(hipMemcpyAsync(ctx->tables.p, ctx->h_stage, tbytes, hipMemcpyHostToDevice, st));
-  const DevPlan *dpl = ctx->tables.as<DevPlan>();
-  const G0Chunk *dchunks = ctx->tables.as<G0Chunk>(o_chunks);
-  const uint32_t *dafirst = ctx->tables.as<uint32_t>(o_afirst);
-  const ProbeWork *dwork = ctx->tables.as<ProbeWork>(o_work);
-  Counters *dctr = ctx->res.as<Counters>();
-  Select *dsel = ctx->sel.as<Select>();
-  uint32_t *lmask = ctx->lmask.as<uint32_t>();
-  Loc *loc = ctx->loc.as<Loc>();
+  hipStream_t st = q.stream;
+  if (ctx->profiling) HIPCHECK(hipEventRecord(q.ev[0], st));
+  HIPCHECK(hipMemcpyAsync(q.tables.p, q.h_stage, tbytes, hipMemcpyHostToDevice, st));
+  const DevPlan *dpl = q.tables.as<DevPlan>();
+  const G0Chunk *dchunks = q.tables.as<G0Chunk>(o_chunks);
+  const uint32_t *dafirst = q.tables.as<uint32_t>(o_afirst);
+  const ProbeWork *dwork = q.tables.as<ProbeWork>(o_work);
+  Counters *dctr = q.res.as<Counters>();
+  Select *dsel = q.sel.as<Select>();
+  uint32_t *lmask = q.lmask.as<uint32_t>();
+  Loc *loc = q.loc.as<Loc>();
   hipLaunchKernelGGL(k_reset, dim3(16), dim3(BLOCK), 0, st, reinterpret_cast<uint32_t *>(dctr),
                      (uint32_t)(sizeof(Counters) / 4), reinterpret_cast<uint32_t *>(dsel),
                      (uint32_t)(sizeof(Select) / 4));
-  const uint32_t ng0 = (uint32_t)ctx->g0c.size();
-  hipLaunchKernelGGL(k_count_runs, dim3(ng0), dim3(BLOCK), 0, st, dpl, dchunks, ctx->chunkcnt.as<uint32_t>());
-  hipLaunchKernelGGL(k_scan_runs, dim3(1), dim3(1024), 0, st, ng0, ctx->chunkcnt.as<uint32_t>());
-  hipLaunchKernelGGL(k_write_runs, dim3(ng0), dim3(BLOCK), 0, st, dpl, dchunks, ctx->chunkcnt.as<uint32_t>(),
-                     dafirst, ctx->cand.as<uint64_t>(), lmask, loc, ctx->ulen.as<uint32_t>(), slot_ub, dctr, ng0,
-                     ctx->dir.as<uint64_t>());
-  if (ctx->profiling) HIPCHECK(hipEventRecord(ctx->ev[1], st));
-  if (!ctx->pw.empty()) {
+  const uint32_t ng0 = (uint32_t)q.g0c.size();
+  hipLaunchKernelGGL(k_count_runs, dim3(ng0), dim3(BLOCK), 0, st, dpl, dchunks, q.chunkcnt.as<uint32_t>());
+  hipLaunchKernelGGL(k_scan_runs, dim3(1), dim3(1024), 0, st, ng0, q.chunkcnt.as<uint32_t>());
+  hipLaunchKernelGGL(k_write_runs, dim3(ng0), dim3(BLOCK), 0, st, dpl, dchunks, q.chunkcnt.as<uint32_t>(),
+                     dafirst, q.cand.as<uint64_t>(), lmask, loc, q.ulen.as<uint32_t>(), slot_ub, dctr, ng0,
+                     q.dir.as<uint64_t>());
+  if (ctx->profiling) HIPCHECK(hipEventRecord(q.ev[1], st));
+  if (!q.pw.empty()) {
     auto kp = ctx->probe_mode == 3   ? k_probe<3, MAXG0>
               : ctx->probe_mode == 2 ? k_probe<2, MAXG0>
               : ctx->probe_mode == 1 ? k_probe<1, MAXG0>
@@ -1614,82 +1652,82 @@ static int enqueue(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms, const i
               : P.g0n == 2           ? k_probe<0, 2>
               : P.g0n <= 4           ? k_probe<0, 4>
                                      : k_probe<0, MAXG0>;
-    const uint32_t nwork = (uint32_t)ctx->pw.size();
+    const uint32_t nwork = (uint32_t)q.pw.size();
     hipLaunchKernelGGL(kp, dim3((nwork + PW - 1) / PW), dim3(64 * PW), 0, st, dpl, dwork, nwork,
-                       ctx->cand.as<uint64_t>(), lmask, loc, ctx->ulen.as<uint32_t>(), slot_ub, dctr,
-                       ctx->dir.as<uint64_t>());
+                       q.cand.as<uint64_t>(), lmask, loc, q.ulen.as<uint32_t>(), slot_ub, dctr,
+                       q.dir.as<uint64_t>());
   }
-  if (ctx->profiling) HIPCHECK(hipEventRecord(ctx->ev[2], st));
+  if (ctx->profiling) HIPCHECK(hipEventRecord(q.ev[2], st));
   const uint32_t cgrid = (uint32_t)((slot_ub + CTILE - 1) / CTILE);
-  hipLaunchKernelGGL(k_compact, dim3(std::max(cgrid, 1u)), dim3(BLOCK), 0, st, dpl, lmask, ctx->ulen.as<uint32_t>(), slot_ub, dctr,
-                     ctx->surv.as<uint32_t>(), ctx->survoff.as<unsigned long long>(), ctx->survlm.as<uint32_t>());
-  if (ctx->profiling) HIPCHECK(hipEventRecord(ctx->ev[3], st));
+  hipLaunchKernelGGL(k_compact, dim3(std::max(cgrid, 1u)), dim3(BLOCK), 0, st, dpl, lmask, q.ulen.as<uint32_t>(), slot_ub, dctr,
+                     q.surv.as<uint32_t>(), q.survoff.as<unsigned long long>(), q.survlm.as<uint32_t>());
+  if (ctx->profiling) HIPCHECK(hipEventRecord(q.ev[3], st));
   {
     int maxsub = 0;
     for (int j = 0; j < hp.ngroups; j++)
       if (!(P.gflags0[j] & BF_NEGATIVE)) maxsub = std::max(maxsub, (int)P.gnsub[j]);
     const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((slot_ub + SCORE_TPB - 1) / SCORE_TPB, 8192));
     auto launch = [&](auto kern) {
-      hipLaunchKernelGGL(kern, dim3(grid), dim3(SCORE_TPB), 0, st, dpl, ctx->cand.as<uint64_t>(), dctr,
-                         ctx->surv.as<uint32_t>(), ctx->survlm.as<uint32_t>(), ctx->survoff.as<unsigned long long>(),
-                         loc, slot_ub, ctx->scratch.as<uint64_t>(), ctx->skey.as<uint32_t>(),
-                         ctx->sdoc.as<uint64_t>(), ctx->score_mode);
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(SCORE_TPB), 0, st, dpl, q.cand.as<uint64_t>(), dctr,
+                         q.surv.as<uint32_t>(), q.survlm.as<uint32_t>(), q.survoff.as<unsigned long long>(),
+                         loc, slot_ub, q.scratch.as<uint64_t>(), q.skey.as<uint32_t>(),
+                         q.sdoc.as<uint64_t>(), ctx->score_mode);
     };
     if (hp.ngroups <= 2 && maxsub <= 4) launch(k_score<2, 4>);
     else if (hp.ngroups <= 4 && maxsub <= 4) launch(k_score<4, 4>);
     else if (hp.ngroups <= 8 && maxsub <= 4) launch(k_score<8, 4>);
     else launch(k_score<MAXG, MAXSUB>);
   }
-  if (ctx->profiling) HIPCHECK(hipEventRecord(ctx->ev[4], st));
+  if (ctx->profiling) HIPCHECK(hipEventRecord(q.ev[4], st));
   // top-k: radix select over the survivors' keys, then one LDS sort
   const uint32_t hgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(64, (slot_ub + 4095) / 4096));
-  const uint32_t *skey = ctx->skey.as<uint32_t>();
+  const uint32_t *skey = q.skey.as<uint32_t>();
   hipLaunchKernelGGL(k_select_hist<0>, dim3(hgrid), dim3(BLOCK), 0, st, skey, dctr, dsel);
   hipLaunchKernelGGL(k_select_scan<0>, dim3(1), dim3(BLOCK), 0, st, dsel, (uint32_t)k);
   hipLaunchKernelGGL(k_select_hist<1>, dim3(hgrid), dim3(BLOCK), 0, st, skey, dctr, dsel);
   hipLaunchKernelGGL(k_select_scan<1>, dim3(1), dim3(BLOCK), 0, st, dsel, (uint32_t)k);
   hipLaunchKernelGGL(k_select_hist<2>, dim3(hgrid), dim3(BLOCK), 0, st, skey, dctr, dsel);
   hipLaunchKernelGGL(k_select_scan<2>, dim3(1), dim3(BLOCK), 0, st, dsel, (uint32_t)k);
-  uint32_t *akey = ctx->gath.as<uint32_t>();
-  uint64_t *adoc = ctx->gath.as<uint64_t>(align256(4 * (size_t)MAX_K));
-  uint32_t *bkey = ctx->gath.as<uint32_t>(align256(4 * (size_t)MAX_K) + align256(8 * (size_t)MAX_K));
-  uint64_t *bdoc = ctx->gath.as<uint64_t>(align256(4 * (size_t)MAX_K) + align256(8 * (size_t)MAX_K) +
+  uint32_t *akey = q.gath.as<uint32_t>();
+  uint64_t *adoc = q.gath.as<uint64_t>(align256(4 * (size_t)MAX_K));
+  uint32_t *bkey = q.gath.as<uint32_t>(align256(4 * (size_t)MAX_K) + align256(8 * (size_t)MAX_K));
+  uint64_t *bdoc = q.gath.as<uint64_t>(align256(4 * (size_t)MAX_K) + align256(8 * (size_t)MAX_K) +
                                           align256(4 * slot_ub));
-  hipLaunchKernelGGL(k_select_gather, dim3(hgrid), dim3(BLOCK), 0, st, skey, ctx->sdoc.as<uint64_t>(), dctr, dsel,
+  hipLaunchKernelGGL(k_select_gather, dim3(hgrid), dim3(BLOCK), 0, st, skey, q.sdoc.as<uint64_t>(), dctr, dsel,
                      akey, adoc, bkey, bdoc);
   hipLaunchKernelGGL(k_select_final, dim3(1), dim3(1024), 0, st, dsel, akey, adoc, bkey, bdoc, (uint32_t)k,
-                     ctx->res.as<uint32_t>(res_keys_off()), ctx->res.as<uint64_t>(res_docs_off(k)));
-  if (ctx->profiling) HIPCHECK(hipEventRecord(ctx->ev[5], st));
-  HIPCHECK(hipMemcpyAsync(ctx->h_res, ctx->res.p, ctx->res_bytes, hipMemcpyDeviceToHost, st));
-  if (ctx->profiling) HIPCHECK(hipEventRecord(ctx->ev[6], st));
-  ctx->pending = true;
+                     q.res.as<uint32_t>(res_keys_off()), q.res.as<uint64_t>(res_docs_off(k)));
+  if (ctx->profiling) HIPCHECK(hipEventRecord(q.ev[5], st));
+  HIPCHECK(hipMemcpyAsync(q.h_res, q.res.p, q.res_bytes, hipMemcpyDeviceToHost, st));
+  if (ctx->profiling) HIPCHECK(hipEventRecord(q.ev[6], st));
+  q.pending = true;
   return 0;
 }
 
-static int collect(gbgpu_ctx *ctx, gbgpu_result *out) {
-  if (!ctx->pending) return EINVAL;
-  ctx->pending = false;
+static int collect(gbgpu_ctx *ctx, QuerySlot &q, gbgpu_result *out) {
+  if (!q.pending) return EINVAL;
+  q.pending = false;
   out->n = 0;
   out->hits = 0;
   out->filtered = 0;
-  out->docs_wanted = ctx->docs_wanted;
-  if (ctx->early) return 0;
-  HIPCHECK(hipStreamSynchronize(ctx->stream));
+  out->docs_wanted = q.docs_wanted;
+  if (q.early) return 0;
+  HIPCHECK(hipStreamSynchronize(q.stream));
   if (ctx->profiling) {
     float t;
-    (void)hipEventElapsedTime(&t, ctx->ev[0], ctx->ev[6]);
-    ctx->last_ms[0] = t;
+    (void)hipEventElapsedTime(&t, q.ev[0], q.ev[6]);
+    q.last_ms[0] = t;
     for (int i = 1; i < 6; i++) {
-      (void)hipEventElapsedTime(&t, ctx->ev[i - 1], ctx->ev[i]);
-      ctx->last_ms[i] = t;
+      (void)hipEventElapsedTime(&t, q.ev[i - 1], q.ev[i]);
+      q.last_ms[i] = t;
     }
   }
-  const Counters *c = reinterpret_cast<const Counters *>(ctx->h_res);
-  const uint32_t *keys = reinterpret_cast<const uint32_t *>(ctx->h_res + res_keys_off());
-  const uint64_t *docs = reinterpret_cast<const uint64_t *>(ctx->h_res + res_docs_off(ctx->k));
+  const Counters *c = reinterpret_cast<const Counters *>(q.h_res);
+  const uint32_t *keys = reinterpret_cast<const uint32_t *>(q.h_res + res_keys_off());
+  const uint64_t *docs = reinterpret_cast<const uint64_t *>(q.h_res + res_docs_off(q.k));
   out->hits = (int64_t)(c->surv_top >> 36);
   int n = 0;
-  for (int i = 0; i < ctx->k && n < out->capacity; i++) {
+  for (int i = 0; i < q.k && n < out->capacity; i++) {
     const uint32_t key = keys[i];
     if (key == 0) break;
     const uint32_t b = (key & 0x80000000u) ? (key & 0x7fffffffu) : ~key;
@@ -1720,6 +1758,28 @@ const char *gbgpu_strerror(int code) {
   }
 }
 
+static QuerySlot *slot_of(gbgpu_ctx *ctx, int slot) {
+  if (!ctx || slot < 0) return nullptr;
+  std::lock_guard<std::mutex> g(ctx->slots_mu);
+  return slot < ctx->nslots ? ctx->slots[slot] : nullptr;
+}
+
+static int grow_slots(gbgpu_ctx *ctx, int n) {
+  std::lock_guard<std::mutex> g(ctx->slots_mu);
+  if (n > MAX_SLOTS) return EINVAL;
+  while (ctx->nslots < n) {
+    QuerySlot *q = new QuerySlot();
+    int rc = q->init();
+    if (rc) {
+      q->release();
+      delete q;
+      return rc;
+    }
+    ctx->slots[ctx->nslots++] = q;
+  }
+  return 0;
+}
+
 int gbgpu_open(int device, gbgpu_ctx **out) {
   if (!out) return EINVAL;
   *out = nullptr;
@@ -1728,16 +1788,12 @@ int gbgpu_open(int device, gbgpu_ctx **out) {
   if (hipSetDevice(device) != hipSuccess) return GBGPU_ENODEVICE;
   gbgpu_ctx *ctx = new gbgpu_ctx();
   ctx->device = device;
-  if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
-    delete ctx;
-    return GBGPU_EHIP;
-  }
   Weights w = host_weights();
-  if (hipMemcpyToSymbol(HIP_SYMBOL(c_weights), &w, sizeof w) != hipSuccess) {
-    delete ctx;
+  if (hipStreamCreateWithFlags(&ctx->upload_stream, hipStreamNonBlocking) != hipSuccess ||
+      hipMemcpyToSymbol(HIP_SYMBOL(c_weights), &w, sizeof w) != hipSuccess || grow_slots(ctx, 1) != 0) {
+    gbgpu_close(ctx);
     return GBGPU_EHIP;
   }
-  for (auto &e : ctx->ev) (void)hipEventCreate(&e);
   if (const char *pm = std::getenv("GBGPU_PROBE_MODE")) ctx->probe_mode = std::atoi(pm);
   if (const char *sm = std::getenv("GBGPU_SCORE_MODE")) ctx->score_mode = std::atoi(sm);
   *out = ctx;
@@ -1747,19 +1803,26 @@ int gbgpu_open(int device, gbgpu_ctx **out) {
 void gbgpu_close(gbgpu_ctx *ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
-  (void)hipStreamSynchronize(ctx->stream);
+  for (int i = 0; i < ctx->nslots; i++) {
+    ctx->slots[i]->release();
+    delete ctx->slots[i];
+  }
   for (auto &e : ctx->lists)
     if (e.live) (void)hipFree(e.d);
-  DevBuf *bufs[] = {&ctx->tables, &ctx->chunkcnt, &ctx->cand, &ctx->lmask, &ctx->ulen, &ctx->loc, &ctx->surv,
-                    &ctx->survoff, &ctx->survlm, &ctx->scratch, &ctx->skey, &ctx->sdoc, &ctx->sel, &ctx->gath, &ctx->res,
-                    &ctx->dir};
-  for (auto *b : bufs) b->release();
-  if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
-  if (ctx->h_res) (void)hipHostFree(ctx->h_res);
-  for (auto &e : ctx->ev)
-    if (e) (void)hipEventDestroy(e);
-  (void)hipStreamDestroy(ctx->stream);
+  if (ctx->upload_stream) (void)hipStreamDestroy(ctx->upload_stream);
   delete ctx;
+}
+
+int gbgpu_set_query_slots(gbgpu_ctx *ctx, int n) {
+  if (!ctx || n < 1) return EINVAL;
+  (void)hipSetDevice(ctx->device);
+  return grow_slots(ctx, n);
+}
+
+int gbgpu_query_slots(gbgpu_ctx *ctx) {
+  if (!ctx) return 0;
+  std::lock_guard<std::mutex> g(ctx->slots_mu);
+  return ctx->nslots;
 }
 
 int32_t gbgpu_docs_wanted(const gbgpu_params *p, const int64_t *sizes, int nterms) {
@@ -1769,51 +1832,79 @@ int32_t gbgpu_docs_wanted(const gbgpu_params *p, const int64_t *sizes, int nterm
 
 int gbgpu_list_upload(gbgpu_ctx *ctx, const uint8_t *bytes, int64_t size, int32_t *handle) {
   if (!ctx || !handle || (size > 0 && !bytes)) return EINVAL;
-  std::lock_guard<std::mutex> g(ctx->mu);
+  std::lock_guard<std::mutex> g(ctx->lists_mu);
   (void)hipSetDevice(ctx->device);
   return upload_list(ctx, bytes, size, handle);
 }
 
 int gbgpu_list_free(gbgpu_ctx *ctx, int32_t h) {
   if (!ctx) return EINVAL;
-  std::lock_guard<std::mutex> g(ctx->mu);
+  std::lock_guard<std::mutex> g(ctx->lists_mu);
   if (h < 0 || h >= (int32_t)ctx->lists.size() || !ctx->lists[h].live) return EINVAL;
-  (void)hipStreamSynchronize(ctx->stream);
+  (void)hipSetDevice(ctx->device);
+  // a query still in flight may read the list: drain every slot's stream
+  for (int i = 0; i < gbgpu_query_slots(ctx); i++) (void)hipStreamSynchronize(slot_of(ctx, i)->stream);
   (void)hipFree(ctx->lists[h].d);
   ctx->lists[h] = ListEntry();
   return 0;
 }
 
-int gbgpu_query_resident_enqueue(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms, const int32_t *handles,
-                                 const gbgpu_params *p) {
-  if (!ctx) return EINVAL;
-  std::lock_guard<std::mutex> g(ctx->mu);
+int gbgpu_query_slot_enqueue(gbgpu_ctx *ctx, int slot, const gbgpu_qterm *terms, int nterms,
+                             const int32_t *handles, const gbgpu_params *p) {
+  QuerySlot *q = slot_of(ctx, slot);
+  if (!q) return EINVAL;
+  std::lock_guard<std::mutex> g(q->mu);
   (void)hipSetDevice(ctx->device);
-  if (ctx->pending) return EBUSY;
-  int rc = enqueue(ctx, terms, nterms, handles, p);
-  if (rc) ctx->pending = false;
+  if (q->pending) return EBUSY;
+  int rc = enqueue(ctx, *q, terms, nterms, handles, p);
+  if (rc) q->pending = false;
   return rc;
 }
 
-int gbgpu_query_collect(gbgpu_ctx *ctx, gbgpu_result *out) {
-  if (!ctx || !out) return EINVAL;
-  std::lock_guard<std::mutex> g(ctx->mu);
+int gbgpu_query_slot_collect(gbgpu_ctx *ctx, int slot, gbgpu_result *out) {
+  QuerySlot *q = slot_of(ctx, slot);
+  if (!q || !out) return EINVAL;
+  std::lock_guard<std::mutex> g(q->mu);
   (void)hipSetDevice(ctx->device);
-  return collect(ctx, out);
+  return collect(ctx, *q, out);
 }
 
+int gbgpu_query_resident_enqueue(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms, const int32_t *handles,
+                                 const gbgpu_params *p) {
+  return gbgpu_query_slot_enqueue(ctx, 0, terms, nterms, handles, p);
+}
+
+int gbgpu_query_collect(gbgpu_ctx *ctx, gbgpu_result *out) { return gbgpu_query_slot_collect(ctx, 0, out); }
+
+// Blocking query on whichever slot is free (re-entrant: Msg39 runs several
+// intersect threads); waits on one slot when all are busy.
 int gbgpu_query_resident(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms, const int32_t *handles,
                          const gbgpu_params *p, gbgpu_result *out) {
   if (!ctx || !out) return EINVAL;
-  std::lock_guard<std::mutex> g(ctx->mu);
+  const int n = gbgpu_query_slots(ctx);
+  QuerySlot *q = nullptr;
+  std::unique_lock<std::mutex> lk;
+  for (int i = 0; i < n && !q; i++) {
+    QuerySlot *c = slot_of(ctx, i);
+    std::unique_lock<std::mutex> t(c->mu, std::try_to_lock);
+    if (t.owns_lock() && !c->pending) {
+      q = c;
+      lk = std::move(t);
+    }
+  }
+  if (!q) {
+    static std::atomic<unsigned> rr{0};
+    q = slot_of(ctx, (int)(rr++ % (unsigned)n));
+    lk = std::unique_lock<std::mutex>(q->mu);
+    if (q->pending) return EBUSY;  // held by an enqueue/collect caller
+  }
   (void)hipSetDevice(ctx->device);
-  if (ctx->pending) return EBUSY;
-  int rc = enqueue(ctx, terms, nterms, handles, p);
+  int rc = enqueue(ctx, *q, terms, nterms, handles, p);
   if (rc) {
-    ctx->pending = false;
+    q->pending = false;
     return rc;
   }
-  return collect(ctx, out);
+  return collect(ctx, *q, out);
 }
 
 int gbgpu_query(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms, const gbgpu_list *lists,
@@ -1828,12 +1919,18 @@ int gbgpu_query(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms, const gbgp
   return rc;
 }
 
-void *gbgpu_stream(gbgpu_ctx *ctx) { return ctx ? (void *)ctx->stream : nullptr; }
+void *gbgpu_stream(gbgpu_ctx *ctx) { return gbgpu_slot_stream(ctx, 0); }
+
+void *gbgpu_slot_stream(gbgpu_ctx *ctx, int slot) {
+  QuerySlot *q = slot_of(ctx, slot);
+  return q ? (void *)q->stream : nullptr;
+}
 
 int gbgpu_last_topk_device(gbgpu_ctx *ctx, void **dev_ptr, int32_t *n) {
-  if (!ctx || !dev_ptr || !n) return EINVAL;
-  *dev_ptr = ctx->res.p ? ctx->res.as<uint8_t>(res_keys_off()) : nullptr;
-  *n = ctx->k;
+  QuerySlot *q = slot_of(ctx, 0);
+  if (!q || !dev_ptr || !n) return EINVAL;
+  *dev_ptr = q->res.p ? q->res.as<uint8_t>(res_keys_off()) : nullptr;
+  *n = q->k;
   return 0;
 }
 
@@ -1843,11 +1940,16 @@ int gbgpu_set_profiling(gbgpu_ctx *ctx, int enable) {
   return 0;
 }
 
-int gbgpu_last_timings(gbgpu_ctx *ctx, float *ms6, int64_t *scan_bytes) {
-  if (!ctx) return EINVAL;
-  if (ms6) std::memcpy(ms6, ctx->last_ms, sizeof ctx->last_ms);
-  if (scan_bytes) *scan_bytes = ctx->scan_bytes;
+int gbgpu_slot_timings(gbgpu_ctx *ctx, int slot, float *ms6, int64_t *scan_bytes) {
+  QuerySlot *q = slot_of(ctx, slot);
+  if (!q) return EINVAL;
+  if (ms6) std::memcpy(ms6, q->last_ms, sizeof q->last_ms);
+  if (scan_bytes) *scan_bytes = q->scan_bytes;
   return 0;
+}
+
+int gbgpu_last_timings(gbgpu_ctx *ctx, float *ms6, int64_t *scan_bytes) {
+  return gbgpu_slot_timings(ctx, 0, ms6, scan_bytes);
 }
 
 int gbgpu_merge_topk(const int64_t *const *sd, const float *const *ss, const int32_t *cnt, int nshards, int32_t k,

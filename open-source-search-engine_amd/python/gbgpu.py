@@ -102,7 +102,8 @@ EXPORTS = [
     "gbgpu_query", "gbgpu_list_upload", "gbgpu_list_free", "gbgpu_query_resident",
     "gbgpu_query_resident_enqueue", "gbgpu_query_collect", "gbgpu_stream",
     "gbgpu_last_topk_device", "gbgpu_merge_topk", "gbgpu_merge_posdb", "gbgpu_set_profiling",
-    "gbgpu_last_timings",
+    "gbgpu_last_timings", "gbgpu_set_query_slots", "gbgpu_query_slots", "gbgpu_query_slot_enqueue",
+    "gbgpu_query_slot_collect", "gbgpu_slot_stream", "gbgpu_slot_timings",
     "gb_synth_lists", "gb_synth_free", "gb_synth_docid", "gb_posdb_compress", "gb_posdb_make_key",
 ]
 
@@ -144,6 +145,14 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
                                       i64, ctypes.POINTER(i64)]
     lib.gbgpu_set_profiling.argtypes = [vp, ctypes.c_int]
     lib.gbgpu_last_timings.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(i64)]
+    lib.gbgpu_set_query_slots.argtypes = [vp, ctypes.c_int]
+    lib.gbgpu_query_slots.argtypes = [vp]
+    lib.gbgpu_query_slot_enqueue.argtypes = [vp, ctypes.c_int, ctypes.POINTER(QTerm), ctypes.c_int,
+                                             ctypes.POINTER(i32), ctypes.POINTER(Params)]
+    lib.gbgpu_query_slot_collect.argtypes = [vp, ctypes.c_int, ctypes.POINTER(Result)]
+    lib.gbgpu_slot_stream.argtypes = [vp, ctypes.c_int]
+    lib.gbgpu_slot_stream.restype = vp
+    lib.gbgpu_slot_timings.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(i64)]
     lib.gb_synth_lists.argtypes = [ctypes.POINTER(SynthCorpus), ctypes.POINTER(SynthTerm), ctypes.c_int,
                                    ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(i64)]
     lib.gb_synth_free.argtypes = [vp]
@@ -237,7 +246,8 @@ class QueryResult:
 
 
 class Engine:
-    """One gbgpu context (one HIP stream) on one device."""
+    """One gbgpu context on one device: resident lists shared by its query
+    slots (one HIP stream each; a context starts with one slot)."""
 
     def __init__(self, device: int = 0):
         self.lib = load()
@@ -297,24 +307,30 @@ class Engine:
         _check(self.lib.gbgpu_query_resident(self.ctx, qt, n, hh, ctypes.byref(params), ctypes.byref(r)), "query")
         return self._pack(r, d, s)
 
-    def enqueue(self, terms: Sequence[QTerm], handles: Sequence[int], params: Params) -> None:
+    def set_slots(self, n: int) -> None:
+        _check(self.lib.gbgpu_set_query_slots(self.ctx, n), "set_query_slots")
+
+    def slots(self) -> int:
+        return self.lib.gbgpu_query_slots(self.ctx)
+
+    def enqueue(self, terms: Sequence[QTerm], handles: Sequence[int], params: Params, slot: int = 0) -> None:
         n = len(terms)
         qt = (QTerm * max(n, 1))(*terms)
         hh = (ctypes.c_int32 * max(n, 1))(*handles)
-        _check(self.lib.gbgpu_query_resident_enqueue(self.ctx, qt, n, hh, ctypes.byref(params)), "enqueue")
+        _check(self.lib.gbgpu_query_slot_enqueue(self.ctx, slot, qt, n, hh, ctypes.byref(params)), "enqueue")
 
-    def collect(self, cap: int = 4096) -> QueryResult:
+    def collect(self, cap: int = 4096, slot: int = 0) -> QueryResult:
         r, d, s = self._result(cap)
-        _check(self.lib.gbgpu_query_collect(self.ctx, ctypes.byref(r)), "collect")
+        _check(self.lib.gbgpu_query_slot_collect(self.ctx, slot, ctypes.byref(r)), "collect")
         return self._pack(r, d, s)
 
     def set_profiling(self, on: bool) -> None:
         _check(self.lib.gbgpu_set_profiling(self.ctx, 1 if on else 0))
 
-    def last_timings(self):
+    def last_timings(self, slot: int = 0):
         ms = (ctypes.c_float * 6)()
         sb = ctypes.c_int64()
-        _check(self.lib.gbgpu_last_timings(self.ctx, ms, ctypes.byref(sb)))
+        _check(self.lib.gbgpu_slot_timings(self.ctx, slot, ms, ctypes.byref(sb)))
         return list(ms), sb.value
 
     def stream(self) -> int:

@@ -86,3 +86,43 @@ def test_unsupported_modes_fail_loudly(engine):
     with pytest.raises(gbgpu.GbgpuError) as e:
         engine.query(q.terms, lists, p)
     assert e.value.code == gbgpu.GBGPU_EUNSUPPORTED
+
+
+def test_query_slots_in_flight_together(engine):
+    # four different queries in flight at once, one per slot, each checked
+    engine.set_slots(4)
+    assert engine.slots() >= 4
+    kinds = qkinds.kinds(20000, seed=6)
+    jobs = []
+    for slot in range(4):
+        q = kinds[slot % len(kinds)]
+        lists = generate(q, 20000, seed=300 + slot)
+        hs = [engine.upload(l) for l in lists]
+        jobs.append((slot, q, lists, hs))
+    try:
+        for slot, q, _, hs in jobs:
+            engine.enqueue(q.terms, hs, q.params(), slot=slot)
+        for slot, q, lists, _ in reversed(jobs):
+            check(engine.collect(slot=slot), orc.query(q.terms, lists, q.params()), f"slot {slot} {q.name}")
+    finally:
+        for *_, hs in jobs:
+            for h in hs:
+                engine.free(h)
+
+
+def test_query_resident_reentrant_from_threads(engine):
+    # Msg39's intersect threads call in concurrently
+    from concurrent.futures import ThreadPoolExecutor
+    engine.set_slots(4)
+    q = qkinds.kinds(20000, seed=7)[2]
+    lists = generate(q, 20000, seed=71)
+    hs = [engine.upload(l) for l in lists]
+    try:
+        exp = orc.query(q.terms, lists, q.params())
+        with ThreadPoolExecutor(6) as ex:
+            results = list(ex.map(lambda _: engine.query_resident(q.terms, hs, q.params()), range(24)))
+        for r in results:
+            check(r, exp, "threaded")
+    finally:
+        for h in hs:
+            engine.free(h)
