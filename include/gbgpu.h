@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define GBGPU_ABI_VERSION 2
+#define GBGPU_ABI_VERSION 3
 
 /* error codes beyond errno.h (Errno.h numbering is not reused) */
 #define GBGPU_ENODEVICE   1001 /* no HIP device / extension not usable        */
@@ -139,11 +139,26 @@ int gbgpu_merge_topk(const int64_t *const *shard_docids, const float *const *sha
                      const int32_t *shard_counts, int nshards, int32_t k,
                      int64_t *out_docids, double *out_scores, int32_t *out_n);
 
-/* RdbList::posdbMerge_r (RdbList.cpp:3065-3568): merge n sorted posdb lists
- * (oldest first; ties keep the newest), optionally annihilating negative
- * keys, recompressing the output.  out must hold the sum of input sizes. */
+/* RdbList::posdbMerge_r (RdbList.cpp:3065-3568), as RdbList::merge_r
+ * (RdbList.cpp:1658-1756) calls it after prepareForMerge (410-491): merge n
+ * (<= 256) sorted posdb lists, oldest first, each starting with an 18-byte
+ * key (else EINVAL); on equal keys (bfcmpPosdb, RdbList.h:620-641) only the
+ * newest list's survives; remove_neg_keys drops surviving delete keys; the
+ * output is re-compressed and stops after the first key that reaches
+ * min(sum of sizes, min_rec_sizes + 36, out_cap) bytes (min_rec_sizes < 0:
+ * no bound; 0: nothing).  ENOSPC if a key would start within 18 bytes of
+ * out_cap (give out_cap >= sum of sizes + 64).  Host buffers. */
 int gbgpu_merge_posdb(gbgpu_ctx *ctx, const gbgpu_list *lists, int n, int remove_neg_keys,
                       int64_t min_rec_sizes, uint8_t *out, int64_t out_cap, int64_t *out_size);
+/* Same on device-resident runs (each 16-byte aligned, readable up to its size
+ * rounded up to 16) into a device buffer (2-byte aligned).  Synchronous. */
+int gbgpu_merge_posdb_device(gbgpu_ctx *ctx, const uint8_t *const *dev_lists, const int64_t *sizes, int n,
+                             int remove_neg_keys, int64_t min_rec_sizes, uint8_t *dev_out,
+                             int64_t out_cap, int64_t *out_size);
+/* Device timings of the last merge (HIP events), ms: [0] total, [1] decode,
+ * [2] partition, [3] tile count pass, [4] tile offset scan, [5] tile write
+ * pass; and the number of keys decoded and of merge tiles. */
+int gbgpu_merge_timings(gbgpu_ctx *ctx, float *ms6, int64_t *nkeys, int64_t *ntiles);
 
 /* Per-query device timings of a slot's last query (HIP events on its stream),
  * in milliseconds: [0]=total, [1]=candidate extraction, [2]=list probe scan,

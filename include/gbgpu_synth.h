@@ -52,6 +52,16 @@ void gb_synth_free(void *p);
 /* docid of document i of the corpus */
 uint64_t gb_synth_docid(const gb_synth_corpus *corpus, int64_t i);
 
+/* Config 5: nruns sorted, compressed posdb runs ("tiered
+ * files", oldest first) of relative sizes 1:2:4:...; about total_keys keys
+ * over nterms Zipf-weighted termids, ~1+Geometric(0.5) positions per
+ * (term, doc); each key is a delete key with probability neg_frac and also
+ * copied (delete bit flipped half the time) into another run with
+ * probability dup_frac.  Deterministic for a seed, whatever nthreads.
+ * out_bufs[r] are malloc'd (gb_synth_free). */
+int gb_synth_merge_runs(int64_t total_keys, int nruns, uint64_t seed, double dup_frac, double neg_frac,
+                        int nterms, int nthreads, uint8_t **out_bufs, int64_t *out_sizes);
+
 /* RdbList::addRecord posdb compression of a sorted array of 18-byte keys
  * (RdbList.cpp:282-327).  out must hold 18*n bytes; returns bytes written. */
 int64_t gb_posdb_compress(const uint8_t *keys18, int64_t n, uint8_t *out);

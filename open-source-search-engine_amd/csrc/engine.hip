@@ -48,6 +48,7 @@
 #include <vector>
 
 #include "../../include/gbgpu.h"
+#include "merge.h"
 #include "plan.h"
 #include "posdb_key.h"
 #include "scoring.h"
@@ -1366,6 +1367,8 @@ struct gbgpu_ctx {
   bool profiling = false;
   int probe_mode = 0;  // diagnostic only (GBGPU_PROBE_MODE)
   int score_mode = 0;  // diagnostic only (GBGPU_SCORE_MODE): 1 mini-merge without scoring
+  std::mutex merge_mu;
+  gbmerge::MergeState *merge = nullptr;  // created on first use (merge.hip)
 };
 
 // result block layout: [Counters | keys k | docids k]
@@ -1809,6 +1812,7 @@ void gbgpu_close(gbgpu_ctx *ctx) {
   }
   for (auto &e : ctx->lists)
     if (e.live) (void)hipFree(e.d);
+  gbmerge::state_free(ctx->merge);
   if (ctx->upload_stream) (void)hipStreamDestroy(ctx->upload_stream);
   delete ctx;
 }
@@ -1986,11 +1990,45 @@ int gbgpu_merge_topk(const int64_t *const *sd, const float *const *ss, const int
   return 0;
 }
 
+static gbmerge::MergeState *merge_state(gbgpu_ctx *ctx) {
+  std::lock_guard<std::mutex> g(ctx->merge_mu);
+  if (!ctx->merge && gbmerge::state_new(&ctx->merge) != 0) ctx->merge = nullptr;
+  return ctx->merge;
+}
+
 int gbgpu_merge_posdb(gbgpu_ctx *ctx, const gbgpu_list *lists, int n, int remove_neg_keys, int64_t min_rec_sizes,
                       uint8_t *out, int64_t out_cap, int64_t *out_size) {
-  (void)ctx; (void)lists; (void)n; (void)remove_neg_keys; (void)min_rec_sizes; (void)out; (void)out_cap;
-  if (out_size) *out_size = 0;
-  return GBGPU_EUNSUPPORTED;  // next milestone
+  if (!ctx || !out_size || n < 0 || (n > 0 && !lists) || (out_cap > 0 && !out)) return EINVAL;
+  *out_size = 0;
+  (void)hipSetDevice(ctx->device);
+  gbmerge::MergeState *m = merge_state(ctx);
+  if (!m) return GBGPU_EHIP;
+  std::vector<const uint8_t *> p(n);
+  std::vector<int64_t> sz(n);
+  for (int i = 0; i < n; i++) {
+    p[i] = lists[i].bytes;
+    sz[i] = lists[i].bytes ? lists[i].size : 0;
+  }
+  return gbmerge::merge_host(m, p.data(), sz.data(), n, remove_neg_keys, min_rec_sizes, out, out_cap, out_size);
+}
+
+int gbgpu_merge_posdb_device(gbgpu_ctx *ctx, const uint8_t *const *dev_lists, const int64_t *sizes, int n,
+                             int remove_neg_keys, int64_t min_rec_sizes, uint8_t *dev_out, int64_t out_cap,
+                             int64_t *out_size) {
+  if (!ctx || !out_size) return EINVAL;
+  *out_size = 0;
+  (void)hipSetDevice(ctx->device);
+  gbmerge::MergeState *m = merge_state(ctx);
+  if (!m) return GBGPU_EHIP;
+  return gbmerge::merge_device(m, dev_lists, sizes, n, remove_neg_keys, min_rec_sizes, dev_out, out_cap, out_size);
+}
+
+int gbgpu_merge_timings(gbgpu_ctx *ctx, float *ms6, int64_t *nkeys, int64_t *ntiles) {
+  if (!ctx) return EINVAL;
+  gbmerge::MergeState *m = merge_state(ctx);
+  if (!m) return GBGPU_EHIP;
+  gbmerge::last_timings(m, ms6, nkeys, ntiles);
+  return 0;
 }
 
 }  // extern "C"

@@ -221,6 +221,153 @@ extern "C" int gb_synth_lists(const gb_synth_corpus *c, const gb_synth_term *ter
 
 extern "C" void gb_synth_free(void *p) { std::free(p); }
 
+// ------------------------------------------------ tiered runs (config 5)
+namespace {
+
+struct Rng {  // splitmix64 stream
+  uint64_t s;
+  uint64_t next() { return mix64(s += 0x9e3779b97f4a7c15ULL); }
+  double u() { return U01(next()); }
+};
+
+// RdbList::addRecord compression (RdbList.cpp:282-327) into one run
+struct RunOut {
+  std::vector<uint8_t> b;
+  uint8_t hi[6], lo[6];
+  bool any = false;
+  void add(const uint8_t *k) {
+    if (any && std::memcmp(hi, k + 12, 6) == 0) {
+      if (std::memcmp(lo, k + 6, 6) == 0) {
+        b.insert(b.end(), k, k + 6);
+        b[b.size() - 6] = (uint8_t)((k[0] & 0xf9) | 0x06);
+        return;
+      }
+      b.insert(b.end(), k, k + 12);
+      b[b.size() - 12] = (uint8_t)((k[0] & 0xf9) | 0x02);
+      std::memcpy(lo, k + 6, 6);
+      return;
+    }
+    b.insert(b.end(), k, k + 18);
+    b[b.size() - 18] = (uint8_t)(k[0] & 0xf9);
+    std::memcpy(lo, k + 6, 6);
+    std::memcpy(hi, k + 12, 6);
+    any = true;
+  }
+};
+
+}  // namespace
+
+extern "C" int gb_synth_merge_runs(int64_t total_keys, int nruns, uint64_t seed, double dup_frac, double neg_frac,
+                                   int nterms, int nthreads, uint8_t **out_bufs, int64_t *out_sizes) {
+  if (total_keys < 0 || nruns < 1 || nruns > 30 || nterms < 1 || !out_bufs || !out_sizes) return EINVAL;
+  // termids sorted; Zipf weight by a random rank, so key counts are not
+  // correlated with termid order
+  std::vector<uint64_t> tid(nterms);
+  std::vector<double> w(nterms);
+  for (int j = 0; j < nterms; j++) tid[j] = (H(seed, (uint64_t)j, 11) & GB_TERMID_MASK) | 1;
+  std::sort(tid.begin(), tid.end());
+  std::vector<int> rank(nterms);
+  for (int j = 0; j < nterms; j++) rank[j] = j;
+  for (int j = nterms - 1; j > 0; j--) std::swap(rank[j], rank[H(seed, (uint64_t)j, 12) % (uint64_t)(j + 1)]);
+  double ws = 0;
+  for (int j = 0; j < nterms; j++) ws += (w[j] = 1.0 / (1.0 + rank[j]));
+  std::vector<int64_t> cnt(nterms);
+  for (int j = 0; j < nterms; j++) cnt[j] = (int64_t)((double)total_keys * w[j] / ws);
+  // run r gets 2^r / (2^nruns - 1) of the keys
+  std::vector<double> cum(nruns);
+  double acc = 0, tw = (double)((1ULL << nruns) - 1);
+  for (int r = 0; r < nruns; r++) cum[r] = (acc += (double)(1ULL << r) / tw);
+  int nth = nthreads > 0 ? nthreads : (int)std::thread::hardware_concurrency();
+  nth = std::max(1, std::min(nth, nterms));
+  // contiguous term ranges of about equal key counts
+  std::vector<int> cut(nth + 1, nterms);
+  cut[0] = 0;
+  {
+    int64_t tot = 0, run = 0;
+    for (auto c : cnt) tot += c;
+    int t = 1;
+    for (int j = 0; j < nterms && t < nth; j++) {
+      run += cnt[j];
+      while (t < nth && run >= tot * t / nth) cut[t++] = j + 1;
+    }
+  }
+  std::vector<std::vector<RunOut>> parts(nth, std::vector<RunOut>(nruns));
+  std::vector<std::thread> th;
+  for (int t = 0; t < nth; t++) {
+    th.emplace_back([&, t] {
+      auto &R = parts[t];
+      uint8_t k[18];
+      for (int j = cut[t]; j < cut[t + 1]; j++) {
+        Rng g{H(seed, (uint64_t)j, 13)};
+        const int64_t want = cnt[j];
+        if (want <= 0) continue;
+        // ~1+Geometric(0.5) positions per doc: docs = want/2, sorted by
+        // uniform gaps over the 38-bit docid space
+        const uint64_t ndoc = std::max<int64_t>(1, want / 2);
+        const uint64_t gap = std::max<uint64_t>(1, ((1ULL << 38) - 1) / ndoc * 2);
+        uint64_t docid = 0;
+        int64_t made = 0;
+        while (made < want) {
+          docid += 1 + g.next() % gap;
+          if (docid >= (1ULL << 38)) break;
+          const uint32_t sr = (uint32_t)(g.next() % 16);
+          const uint32_t lang = g.u() < 0.9 ? 1u : (uint32_t)(g.next() % 64);
+          int P = 1;
+          while (P < 64 && g.u() < 0.5) P++;
+          uint32_t pos = (uint32_t)(g.next() % (GB_MAXWORDPOS - 64 * 40));
+          for (int q = 0; q < P && made < want; q++, made++) {
+            pos += 2 + (uint32_t)(g.next() % 39);
+            const double uh = g.u();
+            const uint32_t hg = pick_hashgroup(uh);
+            const uint32_t dens = (uint32_t)(g.next() % 32);
+            const uint32_t spam = g.u() < 0.8 ? 15u : (uint32_t)(g.next() % 16);
+            const int syn = g.u() < 0.05;
+            gb_make_key(k, tid[j], docid, pos, dens, 15, spam, sr, hg, lang, 0, syn, 0, 0);
+            const double ur = g.u();
+            int r = 0;
+            while (r < nruns - 1 && ur >= cum[r]) r++;
+            if (g.u() < neg_frac) k[0] &= 0xfe;  // delete key
+            R[r].add(k);
+            if (g.u() < dup_frac) {  // a copy in another run; its delete bit may flip
+              int r2 = (int)(g.next() % (uint64_t)nruns);
+              if (r2 == r) r2 = (r2 + 1) % nruns;
+              if (nruns > 1) {
+                uint8_t d[18];
+                std::memcpy(d, k, 18);
+                if (g.u() < 0.5) d[0] ^= 0x01;
+                R[r2].add(d);
+              }
+            }
+          }
+        }
+      }
+    });
+  }
+  for (auto &x : th) x.join();
+  for (int r = 0; r < nruns; r++) {
+    int64_t tot = 0;
+    for (int t = 0; t < nth; t++) tot += (int64_t)parts[t][r].b.size();
+    out_bufs[r] = nullptr;
+    out_sizes[r] = 0;
+    if (!tot) continue;
+    uint8_t *p = (uint8_t *)std::malloc((size_t)tot);
+    if (!p) {
+      for (int q = 0; q < r; q++) std::free(out_bufs[q]);
+      return ENOMEM;
+    }
+    int64_t off = 0;
+    for (int t = 0; t < nth; t++) {
+      auto &v = parts[t][r].b;
+      if (!v.empty()) std::memcpy(p + off, v.data(), v.size());
+      off += (int64_t)v.size();
+      std::vector<uint8_t>().swap(v);
+    }
+    out_bufs[r] = p;
+    out_sizes[r] = off;
+  }
+  return 0;
+}
+
 extern "C" int64_t gb_posdb_compress(const uint8_t *keys, int64_t n, uint8_t *out) {
   int64_t o = 0;
   const uint8_t *hi = nullptr, *lo = nullptr;  // RdbList m_listPtrHi / m_listPtrLo

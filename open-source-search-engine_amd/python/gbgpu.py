@@ -104,6 +104,7 @@ EXPORTS = [
     "gbgpu_last_topk_device", "gbgpu_merge_topk", "gbgpu_merge_posdb", "gbgpu_set_profiling",
     "gbgpu_last_timings", "gbgpu_set_query_slots", "gbgpu_query_slots", "gbgpu_query_slot_enqueue",
     "gbgpu_query_slot_collect", "gbgpu_slot_stream", "gbgpu_slot_timings",
+    "gbgpu_merge_posdb_device", "gbgpu_merge_timings", "gb_synth_merge_runs",
     "gb_synth_lists", "gb_synth_free", "gb_synth_docid", "gb_posdb_compress", "gb_posdb_make_key",
 ]
 
@@ -143,6 +144,12 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
                                      ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i32)]
     lib.gbgpu_merge_posdb.argtypes = [vp, ctypes.POINTER(ListRef), ctypes.c_int, ctypes.c_int, i64, vp,
                                       i64, ctypes.POINTER(i64)]
+    lib.gbgpu_merge_posdb_device.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(i64), ctypes.c_int,
+                                             ctypes.c_int, i64, vp, i64, ctypes.POINTER(i64)]
+    lib.gbgpu_merge_timings.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(i64),
+                                        ctypes.POINTER(i64)]
+    lib.gb_synth_merge_runs.argtypes = [i64, ctypes.c_int, ctypes.c_uint64, ctypes.c_double, ctypes.c_double,
+                                        ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp), ctypes.POINTER(i64)]
     lib.gbgpu_set_profiling.argtypes = [vp, ctypes.c_int]
     lib.gbgpu_last_timings.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(i64)]
     lib.gbgpu_set_query_slots.argtypes = [vp, ctypes.c_int]
@@ -212,6 +219,48 @@ def synth_lists(num_docs: int, specs: Sequence[TermSpec], seed: int = 0x6B1A57, 
         else:
             out.append(b"")
     return out
+
+
+class MergeRuns:
+    """Config-5 tiered runs made by gb_synth_merge_runs (csrc/synth.cpp), kept in
+    the generator's own buffers: .arrays are numpy uint8 views; free() releases."""
+
+    def __init__(self, total_keys: int, nruns: int = 8, seed: int = 5, dup_frac: float = 0.05,
+                 neg_frac: float = 0.01, nterms: int = 20000, nthreads: int = 0):
+        import numpy as np
+        lib = load()
+        self._lib = lib
+        self._bufs = (ctypes.c_void_p * nruns)()
+        self.sizes = (ctypes.c_int64 * nruns)()
+        _check(lib.gb_synth_merge_runs(int(total_keys), nruns, seed, dup_frac, neg_frac, nterms, nthreads,
+                                       self._bufs, self.sizes), "gb_synth_merge_runs")
+        self.arrays = []
+        for i in range(nruns):
+            n = self.sizes[i]
+            if n:
+                a = np.ctypeslib.as_array((ctypes.c_uint8 * n).from_address(self._bufs[i]))
+            else:
+                a = np.zeros(0, np.uint8)
+            self.arrays.append(a)
+
+    def as_bytes(self):
+        return [a.tobytes() for a in self.arrays]
+
+    def free(self):
+        for i in range(len(self.arrays)):
+            if self._bufs[i]:
+                self._lib.gb_synth_free(self._bufs[i])
+                self._bufs[i] = None
+        self.arrays = []
+
+
+def synth_merge_runs(total_keys: int, **kw):
+    """Config-5 runs as bytes (small sizes; see MergeRuns for large ones)."""
+    m = MergeRuns(total_keys, **kw)
+    try:
+        return m.as_bytes()
+    finally:
+        m.free()
 
 
 def make_key(term_id, docid, wordpos, density, diversity, spam, siterank, hashgroup, langid,
@@ -335,6 +384,42 @@ class Engine:
 
     def stream(self) -> int:
         return self.lib.gbgpu_stream(self.ctx) or 0
+
+    def merge_posdb(self, runs: Sequence[bytes], remove_neg_keys: bool, min_rec_sizes: int = -1,
+                    cap: Optional[int] = None) -> bytes:
+        """RdbList::merge_r -> posdbMerge_r (RdbList.cpp:3065-3568) of host runs, oldest first."""
+        n = len(runs)
+        refs = (ListRef * max(n, 1))()
+        keep = []
+        for i, r in enumerate(runs):
+            b = ctypes.create_string_buffer(bytes(r), max(len(r), 1))
+            keep.append(b)
+            refs[i].bytes = ctypes.cast(b, ctypes.c_void_p)
+            refs[i].size = len(r)
+        if cap is None:
+            cap = sum(len(r) for r in runs) + 64
+        out = ctypes.create_string_buffer(max(cap, 1))
+        osz = ctypes.c_int64()
+        _check(self.lib.gbgpu_merge_posdb(self.ctx, refs, n, int(bool(remove_neg_keys)), int(min_rec_sizes), out,
+                                          cap, ctypes.byref(osz)), "gbgpu_merge_posdb")
+        return out.raw[:osz.value]
+
+    def merge_posdb_device(self, ptrs: Sequence[int], sizes: Sequence[int], remove_neg_keys: bool,
+                           min_rec_sizes: int, out_ptr: int, cap: int) -> int:
+        """Device-resident form (pointers from torch tensors); returns the output size."""
+        n = len(ptrs)
+        p = (ctypes.c_void_p * max(n, 1))(*ptrs)
+        sz = (ctypes.c_int64 * max(n, 1))(*sizes)
+        osz = ctypes.c_int64()
+        _check(self.lib.gbgpu_merge_posdb_device(self.ctx, p, sz, n, int(bool(remove_neg_keys)), int(min_rec_sizes),
+                                                 out_ptr, cap, ctypes.byref(osz)), "gbgpu_merge_posdb_device")
+        return osz.value
+
+    def merge_timings(self):
+        ms = (ctypes.c_float * 6)()
+        nk, nt = ctypes.c_int64(), ctypes.c_int64()
+        _check(self.lib.gbgpu_merge_timings(self.ctx, ms, ctypes.byref(nk), ctypes.byref(nt)))
+        return list(ms), nk.value, nt.value
 
     def last_topk_device(self):
         p = ctypes.c_void_p()
