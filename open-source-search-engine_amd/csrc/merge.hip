@@ -54,7 +54,7 @@ constexpr int MUPT = 8;                          // units per thread (decode)
 constexpr int MCH = MB * MUPT;                   // 2048 units = 12 KiB per decode chunk
 constexpr int WIN_LO = 16;                       // bytes staged before a chunk (2 units + pad)
 constexpr int WIN_BYTES = WIN_LO + MCH * 6 + 16; // + 2 units after it
-constexpr int TCAP = 1024;                       // keys per merge tile
+constexpr int TCAP = 512;                        // keys per merge tile
 constexpr int KPT = TCAP / MB;                   // keys per thread in a tile
 constexpr int MAXN = 256;                        // runs per merge (oracle MAXL)
 constexpr int SCAN_TPB = MB * 4;                 // tiles per scan block
@@ -101,7 +101,6 @@ struct MCtl {
   uint32_t flags, pad;
   unsigned long long out_end;     // end of the last key written (the list size)
   unsigned long long last_start;  // start of that key (ENOSPC check)
-  unsigned long long arena_top;   // bump allocator of the tile byte arena
 };
 
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
@@ -281,58 +280,78 @@ __global__ void __launch_bounds__(1024) k_mscan(MList *lists, DSum *sum) {
   if (threadIdx.x == 0) L.nkeys = carry[0];
 }
 
+// Units are taken in 8 rounds of 256 consecutive units (lane i of wave w
+// holds unit u0 + 256q + 64w + i), so the keys a round decodes are written to
+// consecutive slots by consecutive lanes.  Within a wave, key ranks and the
+// last lo / hi unit before a lane come from ballots; across waves and rounds
+// from per-wave totals in LDS and the chunk carries of k_mscan.
 __global__ void __launch_bounds__(MB) k_mdecode(const MList *lists, int n, const DSum *sum, Keys K, MCtl *ctl) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[WIN_BYTES];
-  __shared__ uint32_t t0[MB / 64], t1[MB / 64], t2[MB / 64];
+  __shared__ uint32_t wk[MUPT][MB / 64], wlo[MUPT][MB / 64], whi[MUPT][MB / 64];
   const int li = list_of_chunk(lists, n, blockIdx.x);
   const MList L = lists[li];
   const uint32_t u0 = (blockIdx.x - L.c0) * MCH;
   stage(L, u0, lds);
   __syncthreads();
-  uint32_t types = 0, cnt = 0, llo = 0, lhi = 0;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const uint64_t below = (1ull << lane) - 1;
+  uint32_t types = 0;
 #pragma unroll
   for (int q = 0; q < MUPT; q++) {
-    const uint32_t u = u0 + threadIdx.x * MUPT + q;
+    const uint32_t u = u0 + q * MB + threadIdx.x;
     const int t = u < L.units ? utype(lds, u0, u) : 3;
     types |= (uint32_t)t << (2 * q);
-    if (t == 0) cnt++;
-    else if (t == 1) llo = u + 1;
-    else if (t == 2) lhi = u + 1;
+    const uint64_t bk = __ballot(t == 0), bl = __ballot(t == 1), bh = __ballot(t == 2);
+    if (lane == 0) {
+      const uint32_t w0 = u0 + q * MB + wid * 64;
+      wk[q][wid] = (uint32_t)__popcll(bk);
+      wlo[q][wid] = bl ? w0 + (63 - __clzll(bl)) + 1 : 0;
+      whi[q][wid] = bh ? w0 + (63 - __clzll(bh)) + 1 : 0;
+    }
   }
-  uint32_t a;
-  const uint32_t ek = block_scan<MB>(cnt, 0u, OpAdd(), t0, &a);
-  const uint32_t elo = block_scan<MB>(llo, 0u, OpMax(), t1, &a);
-  const uint32_t ehi = block_scan<MB>(lhi, 0u, OpMax(), t2, &a);
+  __syncthreads();
   const DSum c = sum[blockIdx.x];
-  uint64_t kidx = L.koff + c.nkeys + ek;
-  uint32_t curlo = elo > c.lastlo ? elo : c.lastlo;
-  uint32_t curhi = ehi > c.lasthi ? ehi : c.lasthi;
+  uint64_t kbase = L.koff + c.nkeys;
+  uint32_t clo = c.lastlo, chi = c.lasthi;
   bool bad = false;
-  const int64_t wlo = (int64_t)u0 - 2, whi = (int64_t)u0 + MCH + 2;
+  const int64_t wlo_u = (int64_t)u0 - 2, whi_u = (int64_t)u0 + MCH + 2;
 #pragma unroll
   for (int q = 0; q < MUPT; q++) {
-    const uint32_t u = u0 + threadIdx.x * MUPT + q;
+    const uint32_t u = u0 + q * MB + threadIdx.x;
     const int t = (types >> (2 * q)) & 3;
-    if (t == 1) {
-      curlo = u + 1;
-    } else if (t == 2) {
-      curhi = u + 1;
-    } else if (t == 0) {
+    const uint64_t bk = __ballot(t == 0), bl = __ballot(t == 1), bh = __ballot(t == 2);
+    uint64_t kb = kbase;
+    uint32_t lo = clo, hi = chi;
+    for (int w = 0; w < MB / 64; w++) {
+      if (w < wid) {
+        kb += wk[q][w];
+        lo = lo > wlo[q][w] ? lo : wlo[q][w];
+        hi = hi > whi[q][w] ? hi : whi[q][w];
+      }
+      kbase += wk[q][w];
+      clo = clo > wlo[q][w] ? clo : wlo[q][w];
+      chi = chi > whi[q][w] ? chi : whi[q][w];
+    }
+    if (t == 0) {
+      const uint32_t w0 = u0 + q * MB + wid * 64;
+      const uint64_t ml = bl & below, mh = bh & below;
+      if (ml) lo = w0 + (63 - __clzll(ml)) + 1;
+      if (mh) hi = w0 + (63 - __clzll(mh)) + 1;
+      const uint64_t kidx = kb + __popcll(bk & below);
       const uint8_t *bp = lunit(lds, u0, u);
       const uint32_t ku = kunits(bp[0]);
-      const int64_t lu = ku >= 2 ? (int64_t)u + 1 : (int64_t)curlo - 1;
-      const int64_t hu = ku == 3 ? (int64_t)u + 2 : (int64_t)curhi - 1;
-      uint64_t lo = 0, hi = 0;
+      const int64_t lu = ku >= 2 ? (int64_t)u + 1 : (int64_t)lo - 1;
+      const int64_t hu = ku == 3 ? (int64_t)u + 2 : (int64_t)hi - 1;
+      uint64_t lov = 0, hiv = 0;
       if (lu < 0 || hu < 0 || (uint64_t)u + ku > L.units) {
         bad = true;
       } else {
-        lo = (lu >= wlo && lu < whi) ? rd48(lunit(lds, u0, lu)) : rd48g(L.p + (size_t)lu * 6);
-        hi = (hu >= wlo && hu < whi) ? rd48(lunit(lds, u0, hu)) : rd48g(L.p + (size_t)hu * 6);
+        lov = (lu >= wlo_u && lu < whi_u) ? rd48(lunit(lds, u0, lu)) : rd48g(L.p + (size_t)lu * 6);
+        hiv = (hu >= wlo_u && hu < whi_u) ? rd48(lunit(lds, u0, hu)) : rd48g(L.p + (size_t)hu * 6);
       }
-      K.hi[kidx] = hi;
-      K.lo[kidx] = lo;
+      K.hi[kidx] = hiv;
+      K.lo[kidx] = lov;
       K.b[kidx] = rd48(bp);
-      kidx++;
     }
   }
   if (bad) atomicOr(&ctl->flags, (uint32_t)F_CORRUPT);
@@ -411,14 +430,13 @@ struct TileLds {
   uint64_t h[TCAP], l[TCAP], b[TCAP];
   uint16_t E[TCAP + 1];  // exclusive survivor count in segment order
   uint16_t ord[TCAP];    // entry of merged rank r
-  uint16_t off[TCAP];    // tile-relative byte offset of rank r (ranks >= 1)
   uint8_t run[TCAP];
   uint8_t keep[TCAP];
   uint32_t seg[MAXN + 1];
   uint32_t beg[MAXN];
   uint64_t koff[MAXN];
   uint32_t tmp[MB / 64];
-  uint64_t arena;
+  uint64_t tmp64[MB / 64];
 };
 
 __device__ __forceinline__ uint32_t lbound(const TileLds &s, uint32_t a, uint32_t z, uint64_t vh, uint64_t vl,
@@ -449,19 +467,25 @@ __device__ __forceinline__ void put_key(uint16_t *o, uint32_t sz, uint64_t h, ui
 // Survivors (no equal key in a newer run, RdbList.cpp:3254-3274; not a delete
 // key under removeNegKeys, 3276-3279), their merged order, and the bytes of
 // survivors 2..n compressed against their predecessor, appended to the arena.
+template <int NL>
 __global__ void __launch_bounds__(MB) k_mtile(const MList *lists, int n, const uint32_t *off, Keys K, TileSum *ts,
                                               int rm, uint8_t *arena, MCtl *ctl) {
   __shared__ TileLds s;
   const uint32_t t = blockIdx.x;
   uint32_t len = 0;
+  uint64_t before = 0;
   if (threadIdx.x < n) {
     const uint32_t b = off[(size_t)t * n + threadIdx.x], e = off[(size_t)(t + 1) * n + threadIdx.x];
     s.beg[threadIdx.x] = b;
     s.koff[threadIdx.x] = lists[threadIdx.x].koff;
     len = e - b;
+    before = b;
   }
   uint32_t tot;
   const uint32_t ex = block_scan<MB>(len, 0u, OpAdd(), s.tmp, &tot);
+  // keys of all runs before this tile: the tile's arena bytes start at 18x that
+  uint64_t kbefore;
+  block_scan<MB>(before, (uint64_t)0, OpAdd(), s.tmp64, &kbefore);
   if (threadIdx.x < n) s.seg[threadIdx.x] = ex;
   if (threadIdx.x == 0) s.seg[n] = tot;
   if (tot > TCAP || tot == 0) {
@@ -486,17 +510,62 @@ __global__ void __launch_bounds__(MB) k_mtile(const MList *lists, int n, const u
     s.run[e] = (uint8_t)lo;
   }
   __syncthreads();
-  for (uint32_t e = threadIdx.x; e < tot; e += MB) {
-    const int l = s.run[e];
-    const uint64_t vh = s.h[e], vl = s.l[e], vb = s.b[e];
-    bool drop = rm && !(vb & 1);
-    for (int l2 = l + 1; !drop && l2 < n; l2++) {
-      const uint32_t a = s.seg[l2], z = s.seg[l2 + 1];
-      if (a == z) continue;
-      const uint32_t p = lbound(s, a, z, vh, vl, vb);
-      drop = p < z && key_eq(s.h[p], s.l[p], s.b[p], vh, vl, vb);
+  // lower bound of every entry in every other run's segment: NL > 0 searches
+  // all segments in lockstep (independent LDS loads in flight) and keeps the
+  // bounds in registers for the rank; NL == 0 (more than 8 runs) searches
+  // one segment at a time, twice
+  uint16_t P[NL > 0 ? KPT : 1][NL > 0 ? NL : 1];
+  if (NL > 0) {
+#pragma unroll
+    for (int j = 0; j < KPT; j++) {
+      const uint32_t e = threadIdx.x + MB * j;
+      if (e >= tot) break;
+      const int l = s.run[e];
+      const uint64_t vh = s.h[e], vl = s.l[e], vb = s.b[e];
+      uint32_t base[NL > 0 ? NL : 1], len[NL > 0 ? NL : 1];
+#pragma unroll
+      for (int q = 0; q < NL; q++) {
+        base[q] = q < n ? s.seg[q] : 0;
+        len[q] = (q < n && q != l) ? s.seg[q + 1] - s.seg[q] : 0;
+      }
+      for (;;) {
+        bool any = false;
+#pragma unroll
+        for (int q = 0; q < NL; q++) {
+          if (!len[q]) continue;
+          any = true;
+          const uint32_t half = len[q] >> 1, m = base[q] + half;
+          if (key_lt(s.h[m], s.l[m], s.b[m], vh, vl, vb)) {
+            base[q] = m + 1;
+            len[q] -= half + 1;
+          } else {
+            len[q] = half;
+          }
+        }
+        if (!any) break;
+      }
+      bool drop = rm && !(vb & 1);
+#pragma unroll
+      for (int q = 0; q < NL; q++) {
+        P[j][q] = (uint16_t)base[q];
+        if (q > l && q < n && base[q] < s.seg[q + 1] && key_eq(s.h[base[q]], s.l[base[q]], s.b[base[q]], vh, vl, vb))
+          drop = true;
+      }
+      s.keep[e] = !drop;
     }
-    s.keep[e] = !drop;
+  } else {
+    for (uint32_t e = threadIdx.x; e < tot; e += MB) {
+      const int l = s.run[e];
+      const uint64_t vh = s.h[e], vl = s.l[e], vb = s.b[e];
+      bool drop = rm && !(vb & 1);
+      for (int l2 = l + 1; !drop && l2 < n; l2++) {
+        const uint32_t a = s.seg[l2], z = s.seg[l2 + 1];
+        if (a == z) continue;
+        const uint32_t p = lbound(s, a, z, vh, vl, vb);
+        drop = p < z && key_eq(s.h[p], s.l[p], s.b[p], vh, vl, vb);
+      }
+      s.keep[e] = !drop;
+    }
   }
   __syncthreads();
   uint32_t em = 0;
@@ -521,17 +590,32 @@ __global__ void __launch_bounds__(MB) k_mtile(const MList *lists, int n, const u
   // merged rank of each survivor: survivors before it in its own segment +
   // survivors with a smaller key in every other segment (equal keys of other
   // runs are never survivors)
-  for (uint32_t e = threadIdx.x; e < tot; e += MB) {
-    if (!s.keep[e]) continue;
-    const int l = s.run[e];
-    const uint64_t vh = s.h[e], vl = s.l[e], vb = s.b[e];
-    uint32_t r = s.E[e] - s.E[s.seg[l]];
-    for (int l2 = 0; l2 < n; l2++) {
-      const uint32_t a = s.seg[l2], z = s.seg[l2 + 1];
-      if (l2 == l || a == z) continue;
-      r += s.E[lbound(s, a, z, vh, vl, vb)] - s.E[a];
+  if (NL > 0) {
+#pragma unroll
+    for (int j = 0; j < KPT; j++) {
+      const uint32_t e = threadIdx.x + MB * j;
+      if (e >= tot) break;
+      if (!s.keep[e]) continue;
+      const int l = s.run[e];
+      uint32_t r = s.E[e] - s.E[s.seg[l]];
+#pragma unroll
+      for (int q = 0; q < NL; q++)
+        if (q < n && q != l) r += s.E[P[j][q]] - s.E[s.seg[q]];
+      s.ord[r] = (uint16_t)e;
     }
-    s.ord[r] = (uint16_t)e;
+  } else {
+    for (uint32_t e = threadIdx.x; e < tot; e += MB) {
+      if (!s.keep[e]) continue;
+      const int l = s.run[e];
+      const uint64_t vh = s.h[e], vl = s.l[e], vb = s.b[e];
+      uint32_t r = s.E[e] - s.E[s.seg[l]];
+      for (int l2 = 0; l2 < n; l2++) {
+        const uint32_t a = s.seg[l2], z = s.seg[l2 + 1];
+        if (l2 == l || a == z) continue;
+        r += s.E[lbound(s, a, z, vh, vl, vb)] - s.E[a];
+      }
+      s.ord[r] = (uint16_t)e;
+    }
   }
   __syncthreads();
   // sizes of ranks 1..n-1 against their predecessor, their tile offsets
@@ -547,14 +631,12 @@ __global__ void __launch_bounds__(MB) k_mtile(const MList *lists, int n, const u
   }
   uint32_t inner;
   uint32_t o = block_scan<MB>(mine, 0u, OpAdd(), s.tmp, &inner);
+  const uint64_t at = 18 * kbefore;
   if (threadIdx.x == 0) {
-    const uint64_t at = inner ? atomicAdd(&ctl->arena_top, (unsigned long long)inner) : 0;
-    s.arena = at;
     const uint32_t f = s.ord[0], z = s.ord[nemit - 1];
     ts[t] = TileSum{nemit, inner, s.h[f], s.l[f], s.b[f], s.h[z], s.l[z], at};
   }
-  __syncthreads();
-  uint8_t *dst = arena + s.arena;
+  uint8_t *dst = arena + at;
 #pragma unroll
   for (int j = 0; j < KPT; j++) {
     const uint32_t r = threadIdx.x * KPT + j;
@@ -897,7 +979,8 @@ static int run(MergeState *s, const uint8_t *const *lists, const int64_t *sizes,
                                                  s->off.as<uint32_t>());
     MCHECK(hipGetLastError());
     MCHECK(hipEventRecord(s->ev[2], st));
-    k_mtile<<<T32, MB, 0, st>>>(dl, n, s->off.as<uint32_t>(), K, ts, rm, arena, dctl);
+    if (n <= 8) k_mtile<8><<<T32, MB, 0, st>>>(dl, n, s->off.as<uint32_t>(), K, ts, rm, arena, dctl);
+    else k_mtile<0><<<T32, MB, 0, st>>>(dl, n, s->off.as<uint32_t>(), K, ts, rm, arena, dctl);
     MCHECK(hipEventRecord(s->ev[3], st));
     k_tscan1<<<nblk, MB, 0, st>>>(ts, T32, s->bs.as<BlkSum>());
     k_tscan2<<<1, 1024, 0, st>>>(ts, s->bs.as<BlkSum>(), nblk, s->bo.as<TileOff>());

@@ -11,6 +11,7 @@ import torch  # noqa: E402
 import gbgpu  # noqa: E402
 
 keys = int(float(sys.argv[1])) if len(sys.argv) > 1 else 400_000_000
+iters = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 t0 = time.time()
 m = gbgpu.MergeRuns(keys, nruns=8, seed=5, nterms=20000, nthreads=16)
 sizes = [len(a) for a in m.arrays]
@@ -21,8 +22,8 @@ m.free()
 cap = sum(sizes) + 64
 out = torch.empty(cap, dtype=torch.uint8, device="cuda")
 eng = gbgpu.Engine(0)
-for rm in (0, 1):
-    for it in range(3):
+for rm in ((0, 1) if iters >= 3 else (0,)):
+    for it in range(iters):
         torch.cuda.synchronize()
         t = time.perf_counter()
         n = eng.merge_posdb_device([d.data_ptr() for d in dev], sizes, rm, -1, out.data_ptr(), cap)
