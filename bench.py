@@ -66,6 +66,145 @@ def cpu_baseline(q, num_docs_total: int, budget_s: float = 12.0):
     }
 
 
+def bench_config3(eng, num_docs: int, steps: int, slots: int):
+    """Config 3 (BASELINE.json): the ten fixed 3-5 word queries, three with a
+    quoted phrase (term-pair proximity path), over a 100M-doc index resident in
+    HBM; queries run round-robin with `slots` of them in flight."""
+    from workload import config3_queries, generate
+
+    qs = config3_queries(num_docs, docs_to_get=100)
+    t0 = time.time()
+    hs, qbytes = [], []
+    for q in qs:
+        lists = generate(q, num_docs, threads=16)
+        hs.append([eng.upload(l) for l in lists])
+        qbytes.append(sum(len(l) for l in lists))
+    log(f"[config3] generated + uploaded {sum(qbytes)/1e9:.2f} GB of lists in {time.time()-t0:.1f}s")
+    ps = [q.params() for q in qs]
+
+    def run(nq):
+        hits = []
+        for i in range(nq):
+            slot = i % slots
+            if i >= slots:
+                hits.append(eng.collect(cap=4096, slot=slot).hits)
+            j = i % len(qs)
+            eng.enqueue(qs[j].terms, hs[j], ps[j], slot=slot)
+        for i in range(max(0, nq - slots), nq):
+            hits.append(eng.collect(cap=4096, slot=i % slots).hits)
+        return hits
+
+    run(len(qs))
+    eng.set_profiling(True)
+    dev = []
+    for j, q in enumerate(qs):
+        eng.enqueue(q.terms, hs[j], ps[j], slot=0)
+        eng.collect(cap=4096, slot=0)
+        dev.append(eng.last_timings(slot=0)[0][0])
+    eng.set_profiling(False)
+    nq = max(steps, len(qs)) // len(qs) * len(qs)
+    t = time.perf_counter()
+    run(nq)
+    el = time.perf_counter() - t
+    scanned = sum(qbytes) * (nq // len(qs))
+    for h in hs:
+        for x in h:
+            eng.free(x)
+    return {
+        "workload": "config 3: 10 fixed 3-5 word queries (3 with a quoted phrase), top-100, 100M docs",
+        "queries": nq,
+        "queries_per_sec": round(nq / el, 2),
+        "keys_scanned_GBps": round(scanned / el / 1e9, 2),
+        "pct_hbm_peak_keys_scanned": round(100.0 * scanned / el / 1e9 / HBM_PEAK_GBS, 2),
+        "avg_list_bytes_per_query": int(np.mean(qbytes)),
+        "device_ms_per_query": [round(float(x), 4) for x in dev],
+    }
+
+
+def bench_merge(eng, steps: int, total_keys: int, with_cpu: bool):
+    """Config 5 (BASELINE.json): RdbList::posdbMerge_r of 8 tiered posdb runs
+    (sizes 1:2:..:128, 5% of keys repeated across runs, 1% delete keys),
+    runs and output resident in HBM (gbgpu_merge_posdb_device).  Reports the
+    merge rate (input bytes/s and (input+output) bytes/s), per-phase device
+    times, a size-independent check (merging the output alone returns it) and
+    the oracle's single-thread rate on a bounded sample of the same generator."""
+    import torch
+    import gbgpu
+
+    t0 = time.time()
+    m = gbgpu.MergeRuns(total_keys, nruns=8, seed=5, nterms=20000, nthreads=16)
+    sizes = [len(a) for a in m.arrays]
+    dev = [torch.from_numpy(a).to("cuda") if len(a) else torch.zeros(16, dtype=torch.uint8, device="cuda")
+           for a in m.arrays]
+    m.free()
+    log(f"[merge] generated + uploaded {sum(sizes)/1e9:.2f} GB of runs in {time.time()-t0:.1f}s")
+    cap = sum(sizes) + 64
+    out = torch.empty(cap, dtype=torch.uint8, device="cuda")
+    ptrs = [d.data_ptr() for d in dev]
+    res = {}
+    for rm in (1, 0):  # removeNegKeys=0 (the disk merge) last: its output stays in `out`
+        eng.merge_posdb_device(ptrs, sizes, rm, -1, out.data_ptr(), cap)  # warmup
+        wall, dev_ms = [], []
+        for _ in range(steps):
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            n = eng.merge_posdb_device(ptrs, sizes, rm, -1, out.data_ptr(), cap)
+            wall.append(time.perf_counter() - t)
+            ms, nkeys, ntiles = eng.merge_timings()
+            dev_ms.append(ms)
+        res[rm] = (n, float(np.median(wall)), np.mean(np.array(dev_ms), axis=0), nkeys, ntiles)
+    n, w, ms, nkeys, ntiles = res[0]
+    # size-independent property: the merged list is canonical, so merging it
+    # alone reproduces it byte for byte
+    out2 = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+    n2 = eng.merge_posdb_device([out.data_ptr()], [n], 0, -1, out2.data_ptr(), n + 64)
+    idem = bool(n2 == n and torch.equal(out[:n], out2[:n]))
+    in_b = float(sum(sizes))
+    r = {
+        "workload": "config 5: RdbList::posdbMerge_r of 8 tiered posdb runs (1:2:..:128), 5% cross-run "
+                    "duplicates, 1% delete keys, removeNegKeys=0 (disk merge), resident in HBM",
+        "input_bytes": int(in_b),
+        "output_bytes": int(n),
+        "keys": int(nkeys),
+        "ms_per_merge": round(w * 1e3, 3),
+        "input_GBps": round(in_b / w / 1e9, 2),
+        "in_plus_out_GBps": round((in_b + n) / w / 1e9, 2),
+        "keys_per_s": round(nkeys / w, 1),
+        "phase_ms": dict(zip(["total", "decode", "partition", "tile_merge", "offsets", "copy"],
+                             [round(float(x), 3) for x in ms])),
+        "tiles": int(ntiles),
+        "remove_neg_keys_ms": round(res[1][1] * 1e3, 3),
+        "idempotent": idem,
+        "roofline": {"bound": "hbm", "achieved": round((in_b + n) / (ms[0] / 1e3) / 1e9, 2), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round((in_b + n) / (ms[0] / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                     "note": "whole merge, algorithmic bytes = input + output"},
+    }
+    del dev, out, out2
+    if with_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import ctypes
+        import oracle_binding as orc
+        sample_keys = 20_000_000
+        runs = gbgpu.synth_merge_runs(sample_keys, nruns=8, seed=5, nterms=20000, nthreads=16)
+        keep, p, sz = orc._lists(runs)
+        scap = sum(map(len, runs)) + 64
+        buf = ctypes.create_string_buffer(scap)
+        t = time.perf_counter()
+        reps = 0
+        while True:
+            orc.lib().orc_posdb_merge(p, sz, len(runs), 0, -1, buf, scap)
+            reps += 1
+            el = time.perf_counter() - t
+            if el > 8.0 or reps >= 20:
+                break
+        sb = sum(map(len, runs))
+        r["cpu_baseline"] = {"value": round(sb / (el / reps) / 1e9, 4), "unit": "GB/s (input)", "cores": 1,
+                             "kind": "port",
+                             "sample": f"{sample_keys} keys ({sb/1e6:.0f} MB) of the same generator, "
+                                       f"oracle/posdb_merge_oracle.c single thread, {reps} reps, {el:.1f} s"}
+    return r
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -75,6 +214,9 @@ def main():
     ap.add_argument("--docs-to-get", type=int, default=100)
     ap.add_argument("--slots", type=int, default=2, help="queries in flight per GPU (query slots)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-merge", action="store_true", help="skip the config-5 list merge measurement")
+    ap.add_argument("--no-config3", action="store_true", help="skip the config-3 query-mix measurement")
+    ap.add_argument("--merge-keys", type=int, default=400_000_000, help="config-5 keys (~4.4 GB of runs)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -211,6 +353,11 @@ def main():
         result["cpu_baseline"] = cpu_baseline(q, per if world == 1 else total)
     for h in handles:
         eng.free(h)
+    if rank == 0 and world == 1 and not args.no_config3:
+        result["config3"] = bench_config3(eng, per, max(args.steps, 50), slots)
+    if rank == 0 and world == 1 and not args.no_merge:
+        result["config5_merge"] = bench_merge(eng, max(3, min(args.steps, 10)), args.merge_keys,
+                                              not args.no_cpu_baseline)
     eng.close()
     if rank == 0:
         print(json.dumps(result), flush=True)
