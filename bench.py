@@ -205,6 +205,20 @@ def bench_merge(eng, steps: int, total_keys: int, with_cpu: bool):
     return r
 
 
+def pmc_traffic(kernel_prefix: str):
+    """HBM bytes per launch of a kernel from the committed rocprofv3 PMC passes
+    (profiles/*pmc_traffic.json, newest), corrected per MI355X_MICROARCH.md."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic.json")))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    for k, v in d["kernels"].items():
+        if k.startswith(kernel_prefix):
+            return v.get("hbm_bytes_per_launch_corrected"), os.path.basename(files[-1])
+    return None, None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -313,6 +327,7 @@ def main():
     _, scan_bytes = eng.last_timings()
     avg_probe_ms = float(np.mean(probe_ms))
     achieved = probe_bytes / (avg_probe_ms / 1000.0) / 1e9 if avg_probe_ms > 0 else 0.0
+    traffic, traffic_src = pmc_traffic("k_probe")
     result = {
         "metric": "queries/sec + posdb keys scanned GB/s (% HBM peak), 1/2/4/8 MI355X",
         "value": round(gbs, 3),
@@ -346,7 +361,9 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": None,
+            "traffic": traffic,
+            "traffic_source": traffic_src,
+            "algorithmic_bytes_per_launch": int(probe_bytes),
         },
     }
     if rank == 0 and not args.no_cpu_baseline:

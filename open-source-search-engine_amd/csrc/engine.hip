@@ -278,7 +278,6 @@ __global__ void __launch_bounds__(BLOCK) k_write_runs(const DevPlan *pl, const G
   __syncthreads();
   // offset inside this array = global prefix - prefix at the array's first chunk
   const uint32_t arr_base_off = chunk_off[array_first_chunk[c.array]];
-  uint32_t pos = chunk_off[blockIdx.x] - arr_base_off + ex;
   const uint64_t base = pl->g0base[c.array];
   const bool own = (c.array == 0);
   const uint32_t own_bit = 1u << lid;
@@ -288,30 +287,28 @@ __global__ void __launch_bounds__(BLOCK) k_write_runs(const DevPlan *pl, const G
   const uint64_t dmin = pl->g0dmin[c.array];
   const uint32_t sh = pl->g0sh[c.array];
   const uint64_t tag = (uint64_t)pl->epoch << 32;
-  m = m0;
-  o = ex;
-  while (m) {
-    const int q = __ffs(m) - 1;
-    m &= m - 1;
-    const uint32_t lu = threadIdx.x * UPT + q;
-    const uint64_t slot = base + pos;
+  // runs in chunk order, strided over the block: consecutive lanes write
+  // consecutive slots (coalesced stores)
+  const uint32_t pos0 = chunk_off[blockIdx.x] - arr_base_off;
+  for (uint32_t o2 = threadIdx.x; o2 < tot; o2 += BLOCK) {
+    const uint32_t lu = rs_unit[o2];
+    const uint32_t p2 = pos0 + o2;
+    const uint64_t slot = base + p2;
     const uint64_t d = unit_docid(lds + lu * 6);
     cand[slot] = d;
     // directory: the first candidate of each bucket within this chunk (a
     // bucket straddling two chunks gets two writers; either names it)
     const uint64_t bkt = (d - dmin) >> sh;
-    if (o == 0 || ((unit_docid(lds + rs_unit[o - 1] * 6) - dmin) >> sh) != bkt) dir_a[bkt] = tag | pos;
+    if (o2 == 0 || ((unit_docid(lds + rs_unit[o2 - 1] * 6) - dmin) >> sh) != bkt) dir_a[bkt] = tag | p2;
     lmask[slot] = own ? own_bit : 0u;
     uint32_t ul = 0;
     if (own) {
       const uint32_t u = c.u0 + lu;
-      const uint32_t e = (o + 1 < tot) ? c.u0 + rs_unit[o + 1] : run_end(L, u + 2);
+      const uint32_t e = (o2 + 1 < tot) ? c.u0 + rs_unit[o2 + 1] : run_end(L, u + 2);
       loc_l[slot] = Loc{u, e - u};
       ul = (e - u) * own_mult;
     }
     ulen[slot] = ul;
-    pos++;
-    o++;
   }
   // the last chunk of each array publishes the array's count
   const bool last = (blockIdx.x + 1 == nchunks) || (chunks[blockIdx.x + 1].array != c.array);
