@@ -155,6 +155,11 @@ int gbgpu_merge_posdb(gbgpu_ctx *ctx, const gbgpu_list *lists, int n, int remove
 int gbgpu_merge_posdb_device(gbgpu_ctx *ctx, const uint8_t *const *dev_lists, const int64_t *sizes, int n,
                              int remove_neg_keys, int64_t min_rec_sizes, uint8_t *dev_out,
                              int64_t out_cap, int64_t *out_size);
+/* The last key the last merge wrote, as 18 bytes with the compression bits
+ * cleared -- what posdbMerge_r leaves in RdbList::m_lastKey (RdbList.cpp:
+ * 3521-3535), from which merge_r's caller shrinks m_endKey (3544-3565).
+ * 0, or ENOENT if the merge wrote no key. */
+int gbgpu_merge_last_key(gbgpu_ctx *ctx, uint8_t *key18);
 /* Device timings of the last merge (HIP events), ms: [0] total, [1] decode,
  * [2] partition, [3] tile count pass, [4] tile offset scan, [5] tile write
  * pass; and the number of keys decoded and of merge tiles. */

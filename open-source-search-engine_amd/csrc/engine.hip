@@ -2020,6 +2020,13 @@ int gbgpu_merge_posdb_device(gbgpu_ctx *ctx, const uint8_t *const *dev_lists, co
   return gbmerge::merge_device(m, dev_lists, sizes, n, remove_neg_keys, min_rec_sizes, dev_out, out_cap, out_size);
 }
 
+int gbgpu_merge_last_key(gbgpu_ctx *ctx, uint8_t *key18) {
+  if (!ctx || !key18) return EINVAL;
+  gbmerge::MergeState *m = merge_state(ctx);
+  if (!m) return GBGPU_EHIP;
+  return gbmerge::last_key(m, key18);
+}
+
 int gbgpu_merge_timings(gbgpu_ctx *ctx, float *ms6, int64_t *nkeys, int64_t *ntiles) {
   if (!ctx) return EINVAL;
   gbmerge::MergeState *m = merge_state(ctx);

@@ -23,9 +23,14 @@ int merge_device(MergeState *s, const uint8_t *const *lists, const int64_t *size
 int merge_host(MergeState *s, const uint8_t *const *lists, const int64_t *sizes, int n, int remove_neg_keys,
                int64_t min_rec_sizes, uint8_t *out, int64_t out_cap, int64_t *out_size);
 
+// The last key the last merge wrote, decompressed (RdbList::m_lastKey):
+// 0, or ENOENT when it wrote nothing.
+int last_key(MergeState *s, uint8_t *key18);
+
 // Phase timings of the last merge (HIP events), ms: [0] total, [1] decode
 // (count + scan + decode), [2] partition (samples, rank, offsets), [3] tile
-// pass A (count), [4] tile scan, [5] tile pass B (write).  Plus the key count.
+// merge, [4] tile offsets + cut, [5] copy to the output.  Plus the key and
+// tile counts.
 void last_timings(MergeState *s, float *ms6, int64_t *nkeys, int64_t *ntiles);
 
 }  // namespace gbmerge

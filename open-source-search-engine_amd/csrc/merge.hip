@@ -101,6 +101,7 @@ struct MCtl {
   uint32_t flags, pad;
   unsigned long long out_end;     // end of the last key written (the list size)
   unsigned long long last_start;  // start of that key (ENOSPC check)
+  uint64_t lk_hi, lk_lo, lk_b;    // that key, decompressed (RdbList::m_lastKey)
 };
 
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
@@ -772,15 +773,23 @@ __global__ void k_mcut(const TileSum *ts, const TileOff *to, uint32_t T, const u
   const TileSum &S = ts[t];
   uint64_t pos = to[t].off, start = pos;
   pos += to[t].fsize;
+  uint64_t kh = S.fhi, kl = S.flo, kb = S.fb;
   const uint8_t *p = arena + S.arena;
   for (uint32_t k = 1; k < S.n && pos < maxoff; k++) {
     start = pos;
     const uint32_t sz = (p[0] & 0x04) ? 6u : ((p[0] & 0x02) ? 12u : 18u);
+    kb = rd48(p);
+    if (sz >= 12) kl = rd48(p + 6);
+    if (sz == 18) kh = rd48(p + 12);
     pos += sz;
     p += sz;
   }
   ctl->out_end = pos;
   ctl->last_start = start;
+  // m_lastKey: base with the compression bits cleared (RdbList.cpp:3526-3535)
+  ctl->lk_hi = kh;
+  ctl->lk_lo = kl;
+  ctl->lk_b = kb & ~(uint64_t)0x06;
 }
 
 // out[off, off + bytes) of every tile, below the cut: its first key, then its
@@ -845,6 +854,8 @@ struct MergeState {
   MCtl *h_ctl = nullptr;     // pinned
   float ms[6] = {0, 0, 0, 0, 0, 0};
   int64_t nkeys = 0, ntiles = 0;
+  bool has_last = false;
+  uint8_t last_key[18] = {};
 };
 
 int state_new(MergeState **out) {
@@ -892,6 +903,7 @@ static int run(MergeState *s, const uint8_t *const *lists, const int64_t *sizes,
                uint8_t *out, int64_t cap, int64_t *out_size) {
   *out_size = 0;
   s->nkeys = s->ntiles = 0;
+  s->has_last = false;
   std::fill(s->ms, s->ms + 6, 0.f);
   if (nin < 0 || nin > MAXN || cap < 0) return EINVAL;
   if (mrs == 0) return 0;
@@ -1004,6 +1016,12 @@ static int run(MergeState *s, const uint8_t *const *lists, const int64_t *sizes,
   // end of the buffer (oracle/posdb_merge_oracle.c)
   if (s->h_ctl->out_end && s->h_ctl->last_start + 18 > (uint64_t)cap) return ENOSPC;
   *out_size = (int64_t)s->h_ctl->out_end;
+  if (*out_size) {
+    const uint64_t v[3] = {s->h_ctl->lk_b, s->h_ctl->lk_lo, s->h_ctl->lk_hi};
+    for (int i = 0; i < 3; i++)
+      for (int j = 0; j < 6; j++) s->last_key[6 * i + j] = (uint8_t)(v[i] >> (8 * j));
+    s->has_last = true;
+  }
   return 0;
 }
 
@@ -1043,6 +1061,13 @@ int merge_host(MergeState *s, const uint8_t *const *lists, const int64_t *sizes,
   int rc = run(s, dptr.data(), sizes, n, rm, mrs, s->out.as<uint8_t>(), cap, out_size);
   if (rc) return rc;
   if (*out_size) MCHECK(hipMemcpy(out, s->out.p, (size_t)*out_size, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int last_key(MergeState *s, uint8_t *key18) {
+  std::lock_guard<std::mutex> g(s->mu);
+  if (!s->has_last) return ENOENT;
+  std::memcpy(key18, s->last_key, 18);
   return 0;
 }
 

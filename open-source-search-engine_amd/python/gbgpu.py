@@ -104,7 +104,7 @@ EXPORTS = [
     "gbgpu_last_topk_device", "gbgpu_merge_topk", "gbgpu_merge_posdb", "gbgpu_set_profiling",
     "gbgpu_last_timings", "gbgpu_set_query_slots", "gbgpu_query_slots", "gbgpu_query_slot_enqueue",
     "gbgpu_query_slot_collect", "gbgpu_slot_stream", "gbgpu_slot_timings",
-    "gbgpu_merge_posdb_device", "gbgpu_merge_timings", "gb_synth_merge_runs",
+    "gbgpu_merge_posdb_device", "gbgpu_merge_timings", "gbgpu_merge_last_key", "gb_synth_merge_runs",
     "gb_synth_lists", "gb_synth_free", "gb_synth_docid", "gb_posdb_compress", "gb_posdb_make_key",
 ]
 
@@ -146,6 +146,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
                                       i64, ctypes.POINTER(i64)]
     lib.gbgpu_merge_posdb_device.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(i64), ctypes.c_int,
                                              ctypes.c_int, i64, vp, i64, ctypes.POINTER(i64)]
+    lib.gbgpu_merge_last_key.argtypes = [vp, vp]
     lib.gbgpu_merge_timings.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(i64),
                                         ctypes.POINTER(i64)]
     lib.gb_synth_merge_runs.argtypes = [i64, ctypes.c_int, ctypes.c_uint64, ctypes.c_double, ctypes.c_double,
@@ -414,6 +415,15 @@ class Engine:
         _check(self.lib.gbgpu_merge_posdb_device(self.ctx, p, sz, n, int(bool(remove_neg_keys)), int(min_rec_sizes),
                                                  out_ptr, cap, ctypes.byref(osz)), "gbgpu_merge_posdb_device")
         return osz.value
+
+    def merge_last_key(self):
+        """RdbList::m_lastKey after the last merge (18 bytes), None if it wrote nothing."""
+        k = ctypes.create_string_buffer(18)
+        rc = self.lib.gbgpu_merge_last_key(self.ctx, k)
+        if rc == 2:  # ENOENT
+            return None
+        _check(rc, "gbgpu_merge_last_key")
+        return k.raw
 
     def merge_timings(self):
         ms = (ctypes.c_float * 6)()

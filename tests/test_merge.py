@@ -83,6 +83,12 @@ def gpu_vs_oracle(engine, runs, rm, mrs, cap=None):
         return
     got = engine.merge_posdb(runs, rm, mrs, cap)
     assert got == want, (len(got), len(want), rm, mrs)
+    lk = engine.merge_last_key()
+    if not want:
+        assert lk is None
+    else:
+        h, l, b = key_stream(want)[-1]
+        assert lk == (b & ~0x06).to_bytes(6, "little") + l.to_bytes(6, "little") + h.to_bytes(6, "little")
 
 
 @pytest.mark.gpu
