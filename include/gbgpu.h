@@ -63,7 +63,12 @@ typedef struct gbgpu_params {
   int32_t real_max_top;     /* m_realMaxTop (clamped to MAX_TOP = 10)              */
   int32_t language;         /* m_language                                         */
   int32_t site_clustering;  /* m_doSiteClustering: must be 0 (EUNSUPPORTED)        */
-  int32_t num_docid_splits; /* m_numDocIdSplits: must be 1                         */
+  int32_t num_docid_splits; /* m_numDocIdSplits: >1 runs Msg39's docid-split loop
+                               (Msg39.cpp:345-457) inside gbgpu_query/_resident:
+                               one pass per docid piece [d0, d1+2] into one TopTree
+                               sized at the first piece (Posdb.cpp:859-877); hits
+                               and filtered are the sums over pieces.  The
+                               enqueue/collect form returns EUNSUPPORTED for it */
   float   same_lang_weight; /* m_sameLangWeight                                   */
 } gbgpu_params;
 
@@ -90,7 +95,8 @@ void        gbgpu_close(gbgpu_ctx *ctx);
 const char *gbgpu_strerror(int code);
 int         gbgpu_abi_version(void);
 
-/* allocTopTree sizing (Posdb.cpp:838-930): TopTree::m_docsWanted for a query */
+/* allocTopTree sizing (Posdb.cpp:838-930): TopTree::m_docsWanted for a query
+ * (with docid splits: list_sizes are the first piece's lists) */
 int32_t gbgpu_docs_wanted(const gbgpu_params *p, const int64_t *list_sizes, int nterms);
 
 /* Full drop-in: lists[] are 1-1 with terms[] (Msg2::getList(i)).  Uploads the

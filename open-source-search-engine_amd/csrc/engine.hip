@@ -1262,6 +1262,63 @@ static Weights host_weights() {  // initWeights, Posdb.cpp:1105-1197
   return w;
 }
 
+// ---------------------------------------------------------- docid splits
+// Msg39::controlLoop's docid-range pieces (Msg39.cpp:345-457) over a
+// resident list: the units of the runs whose docid lies in [d0, d1], found
+// by binary search over run starts (no serial walk), and the docids of the
+// first and last run in that window (directory sizing).
+struct SplitWin {
+  uint32_t lo, hi;
+  uint64_t dmin, dmax;
+};
+
+__device__ __forceinline__ uint32_t next_run_start(gu8 *p, uint32_t x, uint32_t n) {
+  while (x < n && !unit_is_run_start(p + (size_t)x * 6)) x++;
+  return x;
+}
+
+// first run start whose docid >= v (n if none): predicate "f(x) == n or
+// docid(f(x)) >= v" with f = next_run_start is monotone in x
+__device__ uint32_t run_lower_bound(gu8 *p, uint32_t n, uint64_t v) {
+  uint32_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint32_t mid = lo + (hi - lo) / 2;
+    const uint32_t r = next_run_start(p, mid, n);
+    uint8_t k[12];
+    if (r < n) {
+      for (int b = 0; b < 12; b++) k[b] = p[(size_t)r * 6 + b];
+    }
+    if (r == n || unit_docid(k) >= v) hi = mid;
+    else lo = r + 1;
+  }
+  return next_run_start(p, lo, n);
+}
+
+__global__ void k_split_windows(const uint64_t *lp, const uint64_t *units, int nl, const uint64_t *d0,
+                                const uint64_t *d1, int ns, SplitWin *out) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nl * ns) return;
+  const int i = t / ns, j = t % ns;
+  const uint32_t n = (uint32_t)units[i];
+  SplitWin w{0, 0, 0, 0};
+  if (n) {
+    gu8 *p = gl(reinterpret_cast<const uint8_t *>(lp[i]));
+    w.lo = run_lower_bound(p, n, d0[j]);
+    w.hi = run_lower_bound(p, n, d1[j] + 1);
+    if (w.hi < w.lo) w.hi = w.lo;
+    if (w.lo < w.hi) {
+      uint8_t k[12];
+      for (int b = 0; b < 12; b++) k[b] = p[(size_t)w.lo * 6 + b];
+      w.dmin = unit_docid(k);
+      uint32_t x = w.hi - 1;
+      while (x > w.lo && !unit_is_run_start(p + (size_t)x * 6)) x--;
+      for (int b = 0; b < 12; b++) k[b] = p[(size_t)x * 6 + b];
+      w.dmax = unit_docid(k);
+    }
+  }
+  out[t] = w;
+}
+
 struct DevBuf {
   void *p = nullptr;
   size_t cap = 0;
@@ -1312,6 +1369,7 @@ struct QuerySlot {
   hipStream_t stream = nullptr;
   DevBuf tables, chunkcnt, cand, lmask, ulen, loc, surv, survoff, survlm, scratch, skey, sdoc, sel, gath, res;
   DevBuf dir;           // candidate directories, epoch-tagged (never cleared per query)
+  DevBuf split, swin;   // docid splits: one piece's list windows; window table
   uint32_t epoch = 0;
   uint8_t *h_stage = nullptr;  // pinned: query tables (host -> device, one copy)
   size_t stage_cap = 0;
@@ -1339,7 +1397,7 @@ struct QuerySlot {
   void release() {
     if (stream) (void)hipStreamSynchronize(stream);
     DevBuf *bufs[] = {&tables, &chunkcnt, &cand, &lmask, &ulen, &loc, &surv, &survoff, &survlm,
-                      &scratch, &skey, &sdoc, &sel, &gath, &res, &dir};
+                      &scratch, &skey, &sdoc, &sel, &gath, &res, &dir, &split, &swin};
     for (auto *b : bufs) b->release();
     if (h_stage) (void)hipHostFree(h_stage);
     if (h_res) (void)hipHostFree(h_res);
@@ -1417,27 +1475,49 @@ static int upload_list(gbgpu_ctx *ctx, const uint8_t *bytes, int64_t size, int32
   return 0;
 }
 
+// Validates a request and copies the list-table entries it names (the table
+// may grow under us).
+static int snapshot_lists(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms, const int32_t *handles,
+                          const gbgpu_params *p, std::vector<ListEntry> &ents) {
+  if (!p || nterms < 0 || (nterms && (!terms || !handles))) return EINVAL;
+  if (p->site_clustering) return GBGPU_EUNSUPPORTED;
+  if (p->docs_to_get <= 0 || p->real_max_top <= 0 || p->num_docid_splits <= 0) return EINVAL;
+  if (nterms > 1024) return GBGPU_EUNSUPPORTED;
+  ents.resize(nterms);
+  std::lock_guard<std::mutex> g(ctx->lists_mu);
+  for (int i = 0; i < nterms; i++) {
+    if (terms[i].field_code) return GBGPU_EUNSUPPORTED;
+    int32_t h = handles[i];
+    if (h < 0 || h >= (int32_t)ctx->lists.size() || !ctx->lists[h].live) return EINVAL;
+    ents[i] = ctx->lists[h];
+  }
+  return 0;
+}
+
+static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *terms, int nterms,
+                           const ListEntry *ents, const gbgpu_params *p, int32_t dw_override);
+
+// One whole-range query (no docid splits) on slot q's stream.
 static int enqueue(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *terms, int nterms, const int32_t *handles,
                    const gbgpu_params *p) {
-  if (!p || nterms < 0 || (nterms && (!terms || !handles))) return EINVAL;
-  if (p->site_clustering || p->num_docid_splits > 1) return GBGPU_EUNSUPPORTED;
-  if (p->docs_to_get <= 0 || p->real_max_top <= 0) return EINVAL;
-  if (nterms > 1024) return GBGPU_EUNSUPPORTED;
+  std::vector<ListEntry> ents;
+  int rc = snapshot_lists(ctx, terms, nterms, handles, p, ents);
+  if (rc) return rc;
+  if (p->num_docid_splits > 1) return GBGPU_EUNSUPPORTED;  // blocking entry points only
+  return enqueue_entries(ctx, q, terms, nterms, ents.data(), p, 0);
+}
+
+// One PosdbTable pass over the given lists on slot q's stream.  dw_override
+// > 0 fixes TopTree::m_docsWanted (docid splits size the tree once, at the
+// first piece: Msg39.cpp:938-966).
+static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *terms, int nterms,
+                           const ListEntry *ents, const gbgpu_params *p, int32_t dw_override) {
   std::vector<int64_t> sizes(nterms);
-  std::vector<ListEntry> ents(nterms);  // snapshot: the table may grow under us
-  {
-    std::lock_guard<std::mutex> g(ctx->lists_mu);
-    for (int i = 0; i < nterms; i++) {
-      if (terms[i].field_code) return GBGPU_EUNSUPPORTED;
-      int32_t h = handles[i];
-      if (h < 0 || h >= (int32_t)ctx->lists.size() || !ctx->lists[h].live) return EINVAL;
-      ents[i] = ctx->lists[h];
-      sizes[i] = ents[i].size;
-    }
-  }
+  for (int i = 0; i < nterms; i++) sizes[i] = ents[i].size;
   HostPlan hp;
   int rc = build_host_plan(terms, nterms, sizes.data(), p, &hp);
   if (rc) return rc;
+  if (dw_override > 0) hp.docs_wanted = dw_override;
   q.docs_wanted = hp.docs_wanted;
   q.k = hp.docs_wanted;
   q.early = (hp.ngroups == 0 || hp.min_list_size == 0);
@@ -1741,6 +1821,140 @@ static int collect(gbgpu_ctx *ctx, QuerySlot &q, gbgpu_result *out) {
   return 0;
 }
 
+constexpr uint64_t GB_MAX_DOCID = 0x3fffffffffULL;  // MAX_DOCID = DOCID_MASK (Titledb.h:10-11)
+
+// Msg39::controlLoop's docid-split loop (Msg39.cpp:345-457) on one slot: piece
+// j reads docids [d0, d1+2] (getLists, Msg39.cpp:573-615, one stripe), so
+// neighbouring pieces overlap; each piece is one PosdbTable pass over its
+// windows of the resident lists (copied to 16-B aligned, zero-padded device
+// buffers), into ONE TopTree sized at the first piece (allocTopTree's split
+// branch, Posdb.cpp:859-877) and never reset; hits and m_filtered add up.
+// Without site clustering the tree is the best docs_wanted by (score desc,
+// docid asc), each docid once, whatever the insertion order -- so the pieces'
+// top lists merge exactly on the host.
+static int query_splits(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *terms, int nterms,
+                        const std::vector<ListEntry> &ents, const gbgpu_params *p, gbgpu_result *out) {
+  std::vector<uint64_t> d0, d1;
+  {
+    const uint64_t delta = GB_MAX_DOCID / (uint64_t)p->num_docid_splits;
+    uint64_t ddd = 0;
+    do {
+      const uint64_t a = ddd;
+      ddd += delta;
+      uint64_t b = ddd;
+      if (b + 20 > GB_MAX_DOCID) {
+        b = GB_MAX_DOCID;
+        ddd = GB_MAX_DOCID;
+      }
+      d0.push_back(a);
+      d1.push_back(std::min(b + 2, GB_MAX_DOCID));
+    } while (ddd < GB_MAX_DOCID);
+  }
+  const int ns = (int)d0.size(), nl = nterms;
+  if ((int64_t)ns * std::max(nl, 1) > (1 << 22)) return GBGPU_EUNSUPPORTED;
+  // window search: in [list ptr nl | units nl | d0 ns | d1 ns], out SplitWin[nl][ns]
+  std::vector<uint64_t> hin(2 * (size_t)nl + 2 * (size_t)ns);
+  for (int i = 0; i < nl; i++) {
+    hin[i] = (uint64_t)(uintptr_t)ents[i].d;
+    hin[nl + i] = ents[i].units;
+  }
+  for (int j = 0; j < ns; j++) {
+    hin[2 * nl + j] = d0[j];
+    hin[2 * nl + ns + j] = d1[j];
+  }
+  const size_t in_bytes = 8 * hin.size();
+  const size_t out_off = align256(in_bytes);
+  const int nt = nl * ns;
+  if (q.swin.ensure(out_off + sizeof(SplitWin) * (size_t)std::max(nt, 1))) return ENOMEM;
+  std::vector<SplitWin> win((size_t)std::max(nt, 1));
+  if (nt) {
+    HIPCHECK(hipMemcpyAsync(q.swin.p, hin.data(), in_bytes, hipMemcpyHostToDevice, q.stream));
+    const uint64_t *b = q.swin.as<uint64_t>();
+    hipLaunchKernelGGL(k_split_windows, dim3((nt + 255) / 256), dim3(256), 0, q.stream, b, b + nl, nl, b + 2 * nl,
+                       b + 2 * nl + ns, ns, q.swin.as<SplitWin>(out_off));
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipMemcpyAsync(win.data(), q.swin.as<uint8_t>(out_off), sizeof(SplitWin) * nt, hipMemcpyDeviceToHost,
+                            q.stream));
+    HIPCHECK(hipStreamSynchronize(q.stream));
+  }
+  std::vector<std::pair<float, int64_t>> top;
+  int32_t dw = 0;
+  int64_t hits = 0;
+  int32_t filtered = 0;
+  std::vector<ListEntry> we(nl);
+  std::vector<size_t> off(nl);
+  std::vector<int64_t> td;
+  std::vector<float> ts;
+  for (int j = 0; j < ns; j++) {
+    size_t total = 0;
+    for (int i = 0; i < nl; i++) {
+      const SplitWin &w = win[(size_t)i * ns + j];
+      off[i] = total;
+      total += align256((size_t)(w.hi - w.lo) * 6 + LIST_PAD);
+    }
+    if (q.split.ensure(std::max<size_t>(total, 256))) return ENOMEM;
+    if (total) HIPCHECK(hipMemsetAsync(q.split.p, 0, total, q.stream));
+    for (int i = 0; i < nl; i++) {
+      const SplitWin &w = win[(size_t)i * ns + j];
+      const uint32_t n = w.hi - w.lo;
+      ListEntry e;
+      e.d = q.split.as<uint8_t>(off[i]);
+      e.units = n;
+      e.size = n ? (int64_t)n * 6 + 6 : 0;  // as Msg2 holds it: first key 18 bytes
+      e.dmin = w.dmin;
+      e.dmax = w.dmax;
+      e.live = true;
+      if (n)
+        HIPCHECK(hipMemcpyAsync(e.d, ents[i].d + (size_t)w.lo * 6, (size_t)n * 6, hipMemcpyDeviceToDevice, q.stream));
+      we[i] = e;
+    }
+    if (j == 0) {
+      std::vector<int64_t> sz(nl);
+      for (int i = 0; i < nl; i++) sz[i] = we[i].size;
+      dw = docs_wanted(p, sz.data(), nl);
+    }
+    int rc = enqueue_entries(ctx, q, terms, nterms, we.data(), p, dw);
+    if (rc) {
+      q.pending = false;
+      return rc;
+    }
+    td.assign(std::max(dw, 1), 0);
+    ts.assign(std::max(dw, 1), 0.f);
+    gbgpu_result r;
+    std::memset(&r, 0, sizeof r);
+    r.docids = td.data();
+    r.scores = ts.data();
+    r.capacity = dw;
+    rc = collect(ctx, q, &r);
+    if (rc) return rc;
+    hits += r.hits;
+    filtered += r.filtered;
+    for (int x = 0; x < r.n; x++) top.push_back({ts[x], td[x]});
+    std::sort(top.begin(), top.end(), [](const std::pair<float, int64_t> &a, const std::pair<float, int64_t> &b) {
+      return a.first > b.first || (a.first == b.first && a.second < b.second);
+    });
+    // a docid read by two overlapping pieces scores the same in both
+    top.erase(std::unique(top.begin(), top.end(),
+                          [](const std::pair<float, int64_t> &a, const std::pair<float, int64_t> &b) {
+                            return a.second == b.second;
+                          }),
+              top.end());
+    if ((int32_t)top.size() > dw) top.resize(dw);
+  }
+  out->hits = hits;
+  out->filtered = filtered;
+  out->docs_wanted = dw;
+  int n = 0;
+  for (const auto &t : top) {
+    if (n >= out->capacity) break;
+    if (out->docids) out->docids[n] = t.second;
+    if (out->scores) out->scores[n] = t.first;
+    n++;
+  }
+  out->n = n;
+  return 0;
+}
+
 // ------------------------------------------------------------------ C ABI
 extern "C" {
 
@@ -1900,6 +2114,13 @@ int gbgpu_query_resident(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms, c
     if (q->pending) return EBUSY;  // held by an enqueue/collect caller
   }
   (void)hipSetDevice(ctx->device);
+  if (p && p->num_docid_splits > 1) {
+    std::vector<ListEntry> ents;
+    int rc = snapshot_lists(ctx, terms, nterms, handles, p, ents);
+    if (!rc) rc = query_splits(ctx, *q, terms, nterms, ents, p, out);
+    q->pending = false;
+    return rc;
+  }
   int rc = enqueue(ctx, *q, terms, nterms, handles, p);
   if (rc) {
     q->pending = false;

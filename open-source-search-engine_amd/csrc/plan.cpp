@@ -14,6 +14,14 @@ int32_t docs_wanted(const gbgpu_params *p, const int64_t *sizes, int nterms) {
     if (sizes[k] <= 0) continue;                    // empty list
     nn2 += (int64_t)(int32_t)sizes[k] / (18 - 6);   // m_listSize / (sizeof(POSDBKEY)-6)
   }
+  if (p->num_docid_splits > 1) {      // Posdb.cpp:859-877 (sizes: the first piece's lists)
+    if (nn2 < 100) nn2 = 100;
+    nn2 *= p->num_docid_splits;
+    nn2 *= 2;
+    if (nn1 < 100) nn1 = 100;
+    nn1 *= p->num_docid_splits;
+    nn1 *= 2;
+  }
   int64_t nn = nn2;
   if (nn1 < nn2) nn = nn1;
   if (nn == 0) return 0;              // no tree allocated

@@ -1022,6 +1022,14 @@ static int64_t docs_wanted(const orc_params *p, const int64_t *sizes, int nqt) {
     if (!sizes[k]) continue;
     nn2 += (int32_t)sizes[k] / (18 - 6);
   }
+  if (p->num_docid_splits > 1) { /* Posdb.cpp:859-877 */
+    if (nn2 < 100) nn2 = 100;
+    nn2 *= p->num_docid_splits;
+    nn2 *= 2;
+    if (nn1 < 100) nn1 = 100;
+    nn1 *= p->num_docid_splits;
+    nn1 *= 2;
+  }
   int64_t nn = nn2;
   if (nn1 < nn2) nn = nn1;
   if (nn == 0) return 0;
@@ -1031,29 +1039,15 @@ static int64_t docs_wanted(const orc_params *p, const int64_t *sizes, int nqt) {
   return nn;
 }
 
-int orc_query(const orc_qterm *qt, const uint8_t *const *lists, const int64_t *sizes, int nqt,
-              const orc_params *prm, int64_t *docids, float *scores, int cap, orc_result *out) {
-  memset(out, 0, sizeof *out);
-  if (nqt < 0 || !prm) return EINVAL;
-  if (prm->site_clustering || prm->num_docid_splits > 1) return ENOTSUP;
-  if (prm->real_max_top <= 0 || prm->docs_to_get <= 0) return EINVAL;
-  for (int i = 0; i < nqt; i++)
-    if (qt[i].field_code) return ENOTSUP; /* numeric/facet/range terms: DESIGN.md */
-  initWeights();
-
-  int64_t dw = docs_wanted(prm, sizes, nqt);
-  out->docs_wanted = (int32_t)dw;
-  TopK tk;
-  tk.cap = (int)dw;
-  tk.n = 0;
-  tk.score = (float *)calloc(dw > 0 ? dw : 1, sizeof(float));
-  tk.docid = (int64_t *)calloc(dw > 0 ? dw : 1, sizeof(int64_t));
-
+/* One PosdbTable pass (init .. intersectLists10_r, Posdb.cpp:5437-7806) over
+ * one docid range's lists, adding its winners to the caller's TopTree. */
+static int run_range(const orc_qterm *qt, const uint8_t *const *lists, const int64_t *sizes, int nqt,
+                     const orc_params *prm, TopK *tkp, orc_result *out) {
+  TopK tk = *tkp;
   Prep P;
   int rc = prepare(qt, lists, sizes, nqt, &P);
   if (rc) {
     unprepare(&P, nqt);
-    free(tk.score); free(tk.docid);
     return rc;
   }
   QTI *qip = P.qip;
@@ -1344,6 +1338,109 @@ int orc_query(const orc_qterm *qt, const uint8_t *const *lists, const int64_t *s
   }
 
 finish:
+  *tkp = tk;
+  unprepare(&P, nqt);
+  return 0;
+}
+
+/* RdbList::constrain (RdbList.cpp:1328-1560) of a posdb list to the keys with
+ * docid in [d0, d1]: the first kept key is written out whole (18 bytes), the
+ * rest keep their compressed form.  Returns the restricted size. */
+static int64_t constrain_docids(const uint8_t *l, int64_t n, uint64_t d0, uint64_t d1, uint8_t *out) {
+  uint8_t hi[6] = {0}, lo[6] = {0};
+  int64_t o = 0;
+  for (int64_t p = 0; p < n;) {
+    const int ks = keySize(l + p);
+    if (ks == 18) memcpy(hi, l + p + 12, 6);
+    if (ks >= 12) memcpy(lo, l + p + 6, 6);
+    uint8_t k[18];
+    memcpy(k, l + p, 6);
+    memcpy(k + 6, lo, 6);
+    memcpy(k + 12, hi, 6);
+    const uint64_t d = getDocId(k);
+    if (d > d1) break;
+    if (d >= d0) {
+      if (o == 0) {
+        memcpy(out, k, 18);
+        out[0] &= 0xf9;
+        o = 18;
+      } else {
+        memcpy(out + o, l + p, ks);
+        o += ks;
+      }
+    }
+    p += ks;
+  }
+  return o;
+}
+
+#define ORC_MAX_DOCID 0x3fffffffffULL /* MAX_DOCID = DOCID_MASK, Titledb.h:10-11 */
+
+/* Msg39::controlLoop (Msg39.cpp:345-457) + getLists' range (573-615): the
+ * docid range is cut into m_numDocIdSplits pieces; each piece's lists are
+ * read constrained to it and intersected into ONE TopTree, allocated once at
+ * the first piece with allocTopTree's split sizing (Posdb.cpp:859-877) and
+ * never reset; hit counts and m_filtered add up over the pieces.  A piece
+ * reads docids [d0, d1+2] (getLists adds 1 twice), so neighbours overlap. */
+int orc_query(const orc_qterm *qt, const uint8_t *const *lists, const int64_t *sizes, int nqt,
+              const orc_params *prm, int64_t *docids, float *scores, int cap, orc_result *out) {
+  memset(out, 0, sizeof *out);
+  if (nqt < 0 || !prm) return EINVAL;
+  if (prm->site_clustering) return ENOTSUP;
+  if (prm->real_max_top <= 0 || prm->docs_to_get <= 0 || prm->num_docid_splits <= 0) return EINVAL;
+  for (int i = 0; i < nqt; i++)
+    if (qt[i].field_code) return ENOTSUP; /* numeric/facet/range terms: DESIGN.md */
+  initWeights();
+
+  const int splits = prm->num_docid_splits;
+  TopK tk = {0, 0, NULL, NULL};
+  int alloced = 0, rc = 0;
+  const uint8_t **pl = (const uint8_t **)calloc(nqt > 0 ? nqt : 1, sizeof(uint8_t *));
+  int64_t *ps = (int64_t *)calloc(nqt > 0 ? nqt : 1, sizeof(int64_t));
+  uint8_t **own = (uint8_t **)calloc(nqt > 0 ? nqt : 1, sizeof(uint8_t *));
+  const uint64_t delta = ORC_MAX_DOCID / (uint64_t)splits;
+  uint64_t ddd = 0;
+  do {
+    const uint64_t d0 = ddd;
+    ddd += delta;
+    uint64_t d1 = ddd;
+    if (d1 + 20 > ORC_MAX_DOCID) {
+      d1 = ORC_MAX_DOCID;
+      ddd = ORC_MAX_DOCID;
+    }
+    uint64_t dend = d1 + 2;
+    if (dend > ORC_MAX_DOCID) dend = ORC_MAX_DOCID;
+    for (int i = 0; i < nqt; i++) {
+      if (splits == 1) {
+        pl[i] = lists[i];
+        ps[i] = sizes[i];
+        continue;
+      }
+      free(own[i]);
+      own[i] = (uint8_t *)malloc(sizes[i] + 24);
+      ps[i] = constrain_docids(lists[i], sizes[i], d0, dend, own[i]);
+      pl[i] = own[i];
+    }
+    if (!alloced) {
+      /* Msg39::intersectLists: no tree while it would have no nodes (938-947) */
+      int64_t dw = docs_wanted(prm, ps, nqt);
+      if (dw == 0) continue;
+      alloced = 1;
+      out->docs_wanted = (int32_t)dw;
+      tk.cap = (int)dw;
+      tk.score = (float *)calloc(dw, sizeof(float));
+      tk.docid = (int64_t *)calloc(dw, sizeof(int64_t));
+    }
+    orc_result r;
+    memset(&r, 0, sizeof r);
+    rc = run_range(qt, pl, ps, nqt, prm, &tk, &r);
+    if (rc) break;
+    out->hits += r.hits;
+    out->filtered += r.filtered;
+    if (r.corrupt) out->corrupt = r.corrupt;
+  } while (ddd < ORC_MAX_DOCID);
+  for (int i = 0; i < nqt; i++) free(own[i]);
+  free(own); free(pl); free(ps);
   out->n = tk.n < cap ? tk.n : cap;
   for (int i = 0; i < out->n; i++) {
     docids[i] = tk.docid[i];
@@ -1351,8 +1448,7 @@ finish:
   }
   free(tk.score);
   free(tk.docid);
-  unprepare(&P, nqt);
-  return 0;
+  return rc;
 }
 
 /* posdbMerge_r restatement lives in posdb_merge_oracle.c */

@@ -41,7 +41,7 @@ typedef struct orc_params {
   int32_t real_max_top;     /* m_realMaxTop (clamped to MAX_TOP=10)    */
   int32_t language;         /* m_language                              */
   int32_t site_clustering;  /* must be 0               */
-  int32_t num_docid_splits; /* must be 1                               */
+  int32_t num_docid_splits; /* m_numDocIdSplits: Msg39's split loop      */
   float   same_lang_weight; /* m_sameLangWeight                        */
 } orc_params;
 

@@ -105,19 +105,6 @@ static int ref_query(const orc_qterm *terms, const uint8_t *const *lists, const 
   static float tfw[MAXT];
   static PosdbTable *tab = NULL;
 
-  for (int i = 0; i < nterms; i++) {
-    rl[i].freeList();
-    // RdbList::set(list, size, alloc, allocSize, fixedDataSize, ownData,
-    // useHalfKeys, keySize=18): a fresh mutable copy per run
-    char *buf = NULL;
-    int32_t sz = (int32_t)sizes[i];
-    if (sz > 0) {
-      buf = (char *)mmalloc(sz + 64, "refharness");
-      memcpy(buf, lists[i], sz);
-    }
-    rl[i].set(buf, sz, buf, sz ? sz + 64 : 0, 0, true, true, 18);
-  }
-
   memset((void *)qts, 0, sizeof(qts));
   memset((void *)qws, 0, sizeof(qws));
   for (int i = 0; i < nterms; i++) {
@@ -161,29 +148,79 @@ static int ref_query(const orc_qterm *terms, const uint8_t *const *lists, const 
   req.ptr_termFreqWeights = (char *)tfw;
   req.size_termFreqWeights = 4 * nterms;
 
-  if (tab) {
-    tab->~PosdbTable();
-    mfree(tab, sizeof(PosdbTable), "refharness");
-  }
-  tab = (PosdbTable *)mmalloc(sizeof(PosdbTable), "refharness");
-  new (tab) PosdbTable();
   tree.~TopTree();
   memset((void *)&tree, 0, sizeof tree);  // m_docsWanted is only set by setNumNodes
   new (&tree) TopTree();
+  out->hits = 0;
+  out->filtered = 0;
+  out->corrupt = 0;
 
-  // Msg39::intersectLists sequence (Msg39.cpp:922-1027)
-  tab->init(&q, 0, NULL, &tree, 0, &msg2, &req);
-  if (!tab->allocTopTree()) return ENOMEM;
-  if (!tab->allocWhiteListTable()) return ENOMEM;
-  if (!tab->setQueryTermInfo()) return ENOMEM;
-  tab->intersectLists10_r();
-
-  out->hits = tab->m_docIdVoteBuf.length() / 6;
-  out->filtered = tab->m_filtered;
+  // Msg39::controlLoop's docid-split loop (Msg39.cpp:345-457): one TopTree
+  // (reset once, Msg39.cpp:263) filled by one PosdbTable pass per docid range;
+  // each pass gets its lists as Msg2 reads them for getLists' range
+  // (Msg39.cpp:573-647: [d0, d1+2] with one stripe), here by the reference's
+  // own RdbList::constrain on a fresh copy of the whole list.
+  bool alloced = false;
+  int64_t ddd = 0;
+  const int64_t dddEnd = MAX_DOCID;
+  const int32_t splits = p->num_docid_splits;
+  do {
+    const int64_t d0 = ddd;
+    const int64_t delta = MAX_DOCID / (int64_t)splits;
+    ddd += delta;
+    int64_t d1 = ddd;
+    if (d1 + 20LL > MAX_DOCID) {
+      d1 = MAX_DOCID;
+      ddd = MAX_DOCID;
+    }
+    int64_t docIdEnd = d1 + 1 + 1;
+    if (docIdEnd > MAX_DOCID) docIdEnd = MAX_DOCID;
+    for (int i = 0; i < nterms; i++) {
+      rl[i].freeList();
+      // RdbList::set(list, size, alloc, allocSize, fixedDataSize, ownData,
+      // useHalfKeys, keySize=18): a fresh mutable copy per pass
+      char *buf = NULL;
+      int32_t sz = (int32_t)sizes[i];
+      if (sz > 0) {
+        buf = (char *)mmalloc(sz + 64, "refharness");
+        memcpy(buf, lists[i], sz);
+      }
+      rl[i].set(buf, sz, buf, sz ? sz + 64 : 0, 0, true, true, 18);
+      if (splits > 1 && sz > 0) {
+        char first[18], sk[18], ek[18];
+        memcpy(first, lists[i], 18);
+        const int64_t tid = g_posdb.getTermId(first);
+        g_posdb.makeStartKey(sk, tid, d0);
+        g_posdb.makeEndKey(ek, tid, docIdEnd);
+        if (!rl[i].constrain(sk, ek, -1, 0, first, (char *)"refharness", 0)) return EIO;
+      }
+    }
+    // one PosdbTable over all pieces: reset per piece (Msg39::reset2,
+    // Msg39.cpp:51-69), its allocTopTree buffers (m_stackBuf) kept
+    if (d0 == 0) {
+      if (tab) {
+        tab->~PosdbTable();
+        mfree(tab, sizeof(PosdbTable), "refharness");
+      }
+      tab = (PosdbTable *)mmalloc(sizeof(PosdbTable), "refharness");
+      new (tab) PosdbTable();
+    }
+    tab->reset();
+    // Msg39::intersectLists sequence (Msg39.cpp:922-1027)
+    tab->init(&q, 0, NULL, &tree, 0, &msg2, &req);
+    if (!alloced && !tab->allocTopTree()) return ENOMEM;
+    if (tree.m_numNodes == 0) continue;  // all lists empty: no pass (Msg39.cpp:945-948)
+    alloced = true;
+    if (!tab->allocWhiteListTable()) return ENOMEM;
+    if (!tab->setQueryTermInfo()) return ENOMEM;
+    tab->intersectLists10_r();
+    out->hits += tab->m_docIdVoteBuf.length() / 6;
+    out->filtered += tab->m_filtered;
+    if (tab->m_errno) out->corrupt = tab->m_errno;
+  } while (ddd < dddEnd);
   // allocTopTree returns before setNumNodes when every list is empty
   // (Posdb.cpp:889-890): no tree, reported as 0 like the oracle
   out->docs_wanted = tree.m_numNodes > 0 ? tree.m_docsWanted : 0;
-  out->corrupt = tab->m_errno;
   int n = 0;
   if (tree.m_numNodes > 0) {
     for (int32_t ti = tree.getHighNode(); ti >= 0 && n < cap; ti = tree.getPrev(ti)) {

@@ -36,6 +36,12 @@ def pack_lists(lists):
 
 def save_query(name, terms, lists, params):
     r = ref.query(terms, lists, params, votes=True)
+    if params.num_docid_splits > 1:
+        # the vote buffer of one whole-range pass: the exact intersection
+        import copy
+        p1 = copy.copy(params)
+        p1.num_docid_splits = 1
+        r["votes"] = ref.query(terms, lists, p1, votes=True)["votes"]
     sizes, blob = pack_lists(lists)
     qt = np.array([[getattr(t, f) for f in QFIELDS] for t in terms], np.int32).reshape(len(terms), len(QFIELDS))
     tfw = np.array([t.tf_weight for t in terms], np.float32)
@@ -46,6 +52,49 @@ def save_query(name, terms, lists, params):
                         docids=r["docids"], score_bits=r["scores"].view(np.uint32), hits=np.int64(r["hits"]),
                         docs_wanted=np.int32(r["docs_wanted"]), votes=r["votes"])
     return r
+
+
+def split_boundary_docids(n, seed, splits=(2, 5)):
+    """n sorted distinct docids holding, for each piece boundary d1 of
+    Msg39's docid-split loop (Msg39.cpp:362-373), d1-1 .. d1+3: d1..d1+2 are
+    read by both neighbouring pieces (getLists' docIdEnd = d1+2)."""
+    maxd = (1 << 38) - 1
+    want = set()
+    for s in splits:
+        delta = maxd // s
+        for j in range(1, s):
+            want.update(j * delta + k for k in (-1, 0, 1, 2, 3))
+    rng = np.random.default_rng(seed)
+    while len(want) < n:
+        want.update(int(x) for x in rng.integers(0, maxd + 1, n - len(want)))
+    bnd = sorted(want)
+    # spread the boundary docids over the union (every k-th doc, so hits land on them)
+    return bnd[:n]
+
+
+def save_splits():
+    """Msg39's docid-split loop: m_numDocIdSplits pieces into one TopTree."""
+    import posdb_py
+    N = 6000
+    for seed in (1, 2):
+        ks = qkinds.kinds(N, seed=seed)
+        for q in (ks[0], ks[2], ks[3], ks[9]):
+            lists = generate(q, N, seed=3000 + seed)
+            nd = len({int(d) for l in lists for d in posdb_py.docids(l)})
+            lists = posdb_py.remap_docids(lists, split_boundary_docids(nd, seed))
+            for S in (2, 5):
+                p = q.params()
+                p.num_docid_splits = S
+                r = save_query(f"splits{S}_{q.name}_s{seed}", q.terms, lists, p)
+                print(f"q_splits{S}_{q.name}_s{seed}: hits={r['hits']} n={len(r['docids'])} dw={r['docs_wanted']}")
+    # tree sized from the first piece's lists (Posdb.cpp:859-877): a big
+    # docsToGet where that piece is nearly empty
+    q = qkinds.kinds(N, seed=5)[9]
+    q.docs_to_get = 900
+    lists = generate(q, N, seed=3100)
+    p = q.params()
+    p.num_docid_splits = 3
+    save_query("splits3_sizing", q.terms, lists, p)
 
 
 def save_merge(name, runs, cases):
@@ -89,6 +138,7 @@ def main():
     # undefined behaviour, DESIGN.md "Known divergences")
     save_query("empty_all", q.terms, [b"", b"", b""], q.params())
     save_query("empty_required", q.terms, [lists[0], b"", b""], q.params())
+    save_splits()
     cases = [(0, -1), (1, -1), (0, 5000), (1, 5000), (0, 1)]
     for seed, (keys, nterms) in enumerate([(4000, 50), (12000, 3), (8000, 1)]):
         save_merge(f"tiered_s{seed}", tiered_runs(keys, seed=seed, nterms=nterms), cases)
@@ -98,4 +148,7 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["splits"]:
+        save_splits()
+    else:
+        main()

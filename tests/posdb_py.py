@@ -61,3 +61,56 @@ def decode_keys(data: bytes):
         ))
         off += ks
     return keys
+
+
+def full_keys(data: bytes):
+    """The list's keys as whole 18-byte keys, compression bits cleared."""
+    out, off, hi, lo = [], 0, b"", b""
+    while off < len(data):
+        ks = key_size(data[off])
+        if ks == 18:
+            hi = bytes(data[off + 12:off + 18])
+        if ks >= 12:
+            lo = bytes(data[off + 6:off + 12])
+        k = bytearray(bytes(data[off:off + 6]) + lo + hi)
+        k[0] &= 0xf9
+        out.append(bytes(k))
+        off += ks
+    return out
+
+
+def encode_keys(keys) -> bytes:
+    """RdbList::addRecord's posdb compression (RdbList.cpp:282-327) of sorted
+    whole keys: same bytes 6..17 -> 6 bytes, same 12..17 -> 12, else 18."""
+    out, prev = bytearray(), None
+    for k in keys:
+        k = bytearray(k)
+        if prev is not None and prev[6:18] == k[6:18]:
+            k[0] |= 0x06
+            out += k[:6]
+        elif prev is not None and prev[12:18] == k[12:18]:
+            k[0] |= 0x02
+            out += k[:12]
+        else:
+            out += k
+        prev = bytes(k)
+    return bytes(out)
+
+
+def with_docid(k: bytes, d: int) -> bytes:
+    """Key k with its docid (bytes 7..11 >> 2, Posdb.h:295) replaced."""
+    k = bytearray(k)
+    v = (int.from_bytes(k[7:12], "little") & 0x3) | (d << 2)
+    k[7:12] = v.to_bytes(5, "little")
+    return bytes(k)
+
+
+def remap_docids(lists, new_docids):
+    """Relabel the union of the lists' docids, in order, with the sorted
+    new_docids (at least as many): every list keeps its key order."""
+    ks = [full_keys(l) for l in lists]
+    old = sorted({int.from_bytes(k[7:12], "little") >> 2 for kl in ks for k in kl})
+    new = sorted(new_docids)[:len(old)]
+    assert len(new) == len(old)
+    m = dict(zip(old, new))
+    return [encode_keys([with_docid(k, m[int.from_bytes(k[7:12], "little") >> 2]) for k in kl]) for kl in ks]

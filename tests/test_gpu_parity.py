@@ -126,3 +126,30 @@ def test_query_resident_reentrant_from_threads(engine):
     finally:
         for h in hs:
             engine.free(h)
+
+
+@pytest.mark.parametrize("splits", [2, 5, 16])
+@pytest.mark.parametrize("kind", [0, 2, 3, 9, 12])
+def test_parity_docid_splits(engine, kind, splits):
+    # Msg39's docid-split loop: pieces found on the device by binary search
+    # over run starts, one TopTree over all pieces
+    q = qkinds.kinds(20000, seed=6)[kind]
+    lists = generate(q, 20000, seed=600 + splits)
+    p = q.params()
+    p.num_docid_splits = splits
+    check(engine.query(q.terms, lists, p), orc.query(q.terms, lists, p), f"{q.name} S={splits}")
+
+
+def test_parity_docid_splits_resident_large(engine):
+    q = config_two_term(2_000_000, docs_to_get=100, seed=9)
+    lists = generate(q, 2_000_000, seed=5)
+    p = q.params()
+    p.num_docid_splits = 5
+    hs = [engine.upload(l) for l in lists]
+    try:
+        exp = orc.query(q.terms, lists, p)
+        for _ in range(2):
+            check(engine.query_resident(q.terms, hs, p), exp, "two_term 2M S=5")
+    finally:
+        for h in hs:
+            engine.free(h)

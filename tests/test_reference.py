@@ -50,3 +50,17 @@ def test_merge_vs_reference(seed):
             out = ctypes.create_string_buffer(cap)
             n = orc.lib().orc_posdb_merge(ptrs, sizes, len(runs), rm, mrs, out, cap)
             assert out.raw[:n] == ref.posdb_merge(runs, rm, mrs), (seed, rm, mrs)
+
+
+@pytest.mark.parametrize("splits", [2, 3, 7])
+def test_docid_splits_vs_reference(splits):
+    # Msg39's docid-split loop (Msg39.cpp:345-457) played by the harness with
+    # the reference's own RdbList::constrain per piece
+    N = 8000
+    for q in qkinds.kinds(N, seed=31):
+        lists = generate(q, N, seed=splits)
+        for dtg in (q.docs_to_get, 700):
+            q.docs_to_get = dtg
+            p = q.params()
+            p.num_docid_splits = splits
+            same(orc.query(q.terms, lists, p), ref.query(q.terms, lists, p), f"{q.name} S={splits} dtg={dtg}")
