@@ -88,13 +88,23 @@ def save_splits():
                 r = save_query(f"splits{S}_{q.name}_s{seed}", q.terms, lists, p)
                 print(f"q_splits{S}_{q.name}_s{seed}: hits={r['hits']} n={len(r['docids'])} dw={r['docs_wanted']}")
     # tree sized from the first piece's lists (Posdb.cpp:859-877): a big
-    # docsToGet where that piece is nearly empty
+    # docsToGet while the first piece holds only a few docids, so
+    # nn2 = 100 x splits x 2 (600) sizes the tree, not docsToGet x 2
     q = qkinds.kinds(N, seed=5)[9]
-    q.docs_to_get = 900
+    q.docs_to_get = 700
     lists = generate(q, N, seed=3100)
+    nd = len({int(d) for l in lists for d in posdb_py.docids(l)})
+    third = ((1 << 38) - 1) // 3
+    rng = np.random.default_rng(5)
+    few = set(int(x) for x in rng.integers(0, third, 4))
+    rest = set()
+    while len(rest) < nd - len(few):
+        rest.update(int(x) for x in rng.integers(third + 8, (1 << 38) - 1, nd))
+    lists = posdb_py.remap_docids(lists, sorted(few) + sorted(rest)[:nd - len(few)])
     p = q.params()
     p.num_docid_splits = 3
-    save_query("splits3_sizing", q.terms, lists, p)
+    r = save_query("splits3_sizing", q.terms, lists, p)
+    print(f"q_splits3_sizing: hits={r['hits']} n={len(r['docids'])} dw={r['docs_wanted']}")
 
 
 def save_merge(name, runs, cases):
