@@ -53,7 +53,7 @@ def cpu_baseline(q, num_docs_total: int, budget_s: float = 12.0):
         if el >= budget_s or reps >= 2000:
             break
     per_q = el / reps
-    return {
+    out = {
         "value": round(nbytes / per_q / 1e9, 4),
         "unit": "GB/s",
         "cores": 1,
@@ -64,6 +64,33 @@ def cpu_baseline(q, num_docs_total: int, budget_s: float = 12.0):
                   f"({nbytes/1e6:.1f} MB of lists), oracle/posdb_oracle.c single thread, {reps} reps, "
                   f"{el:.1f} s",
     }
+    # the reference's own PosdbTable::intersectLists10_r (oracle/_ref/gbref,
+    # built from the unmodified sources) on the same slice, when it was built
+    try:
+        import ref_binding as ref
+        if ref.available():
+            exp = orc.query(q.terms, lists, p)
+            r1 = ref.query(q.terms, lists, p, reps=1)
+            assert r1["hits"] == exp["hits"] and np.array_equal(r1["docids"], exp["docids"])
+            nrep = int(max(3, min(2000, budget_s / max(r1["seconds"], 1e-6))))
+            t0 = time.perf_counter()
+            rr = ref.query(q.terms, lists, p, reps=nrep)
+            el2 = time.perf_counter() - t0
+            per_r = rr["seconds"]  # median of nrep runs, timed inside the harness
+            out.update({
+                "value": round(nbytes / per_r / 1e9, 4),
+                "kind": "reference",
+                "qps_on_sample": round(1.0 / per_r, 3),
+                "est_qps_full_index": round((sample_docs / num_docs_total) / per_r, 4),
+                "port_value": round(nbytes / per_q / 1e9, 4),
+                "sample": f"docs [0,{sample_docs}) of the same {num_docs_total}-doc corpus and query "
+                          f"({nbytes/1e6:.1f} MB of lists), the reference's PosdbTable (oracle/_ref/gbref, "
+                          f"-O2 as its Makefile) single thread, median of {nrep} runs incl. the per-run "
+                          f"list copy, {el2:.1f} s; port_value = oracle/posdb_oracle.c, {reps} reps",
+            })
+    except Exception as e:  # the reference build is optional (absent where /root/reference was)
+        out["reference_error"] = repr(e)[:200]
+    return out
 
 
 def bench_config3(eng, num_docs: int, steps: int, slots: int):
