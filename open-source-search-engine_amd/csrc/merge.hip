@@ -429,7 +429,6 @@ __global__ void __launch_bounds__(MB) k_moff(const MList *lists, int n, uint32_t
 // ------------------------------------------------------------ tile merge
 struct TileLds {
   uint64_t h[TCAP], l[TCAP], b[TCAP];
-  uint16_t E[TCAP + 1];  // exclusive survivor count in segment order
   uint16_t ord[TCAP];    // entry of merged rank r
   uint8_t run[TCAP];
   uint8_t keep[TCAP];
@@ -445,6 +444,15 @@ __device__ __forceinline__ uint32_t lbound(const TileLds &s, uint32_t a, uint32_
   while (a < z) {
     const uint32_t m = (a + z) >> 1;
     if (key_lt(s.h[m], s.l[m], s.b[m], vh, vl, vb)) a = m + 1;
+    else z = m;
+  }
+  return a;
+}
+__device__ __forceinline__ uint32_t ubound(const TileLds &s, uint32_t a, uint32_t z, uint64_t vh, uint64_t vl,
+                                           uint64_t vb) {
+  while (a < z) {
+    const uint32_t m = (a + z) >> 1;
+    if (!key_lt(vh, vl, vb, s.h[m], s.l[m], s.b[m])) a = m + 1;
     else z = m;
   }
   return a;
@@ -468,7 +476,6 @@ __device__ __forceinline__ void put_key(uint16_t *o, uint32_t sz, uint64_t h, ui
 // Survivors (no equal key in a newer run, RdbList.cpp:3254-3274; not a delete
 // key under removeNegKeys, 3276-3279), their merged order, and the bytes of
 // survivors 2..n compressed against their predecessor, appended to the arena.
-template <int NL>
 __global__ void __launch_bounds__(MB) k_mtile(const MList *lists, int n, const uint32_t *off, Keys K, TileSum *ts,
                                               int rm, uint8_t *arena, MCtl *ctl) {
   __shared__ TileLds s;
@@ -511,62 +518,56 @@ __global__ void __launch_bounds__(MB) k_mtile(const MList *lists, int n, const u
     s.run[e] = (uint8_t)lo;
   }
   __syncthreads();
-  // lower bound of every entry in every other run's segment: NL > 0 searches
-  // all segments in lockstep (independent LDS loads in flight) and keeps the
-  // bounds in registers for the rank; NL == 0 (more than 8 runs) searches
-  // one segment at a time, twice
-  uint16_t P[NL > 0 ? KPT : 1][NL > 0 ? NL : 1];
-  if (NL > 0) {
+  // Merge the n sorted segments in place, pairwise: the round with width w
+  // merges each group of w segments (A, older runs) with the next w (B).  An
+  // entry's new position is its index in its own half plus its rank in the
+  // other half -- strict in B for an A entry, inclusive in A for a B entry --
+  // so keys equal under bfcmpPosdb stay in run order (older first).
+  for (int w = 1; w < n; w <<= 1) {
+    uint64_t rh[KPT], rl[KPT], rb[KPT];
+    uint32_t np[KPT];
+    uint8_t rr[KPT];
 #pragma unroll
     for (int j = 0; j < KPT; j++) {
       const uint32_t e = threadIdx.x + MB * j;
-      if (e >= tot) break;
-      const int l = s.run[e];
-      const uint64_t vh = s.h[e], vl = s.l[e], vb = s.b[e];
-      uint32_t base[NL > 0 ? NL : 1], len[NL > 0 ? NL : 1];
-#pragma unroll
-      for (int q = 0; q < NL; q++) {
-        base[q] = q < n ? s.seg[q] : 0;
-        len[q] = (q < n && q != l) ? s.seg[q + 1] - s.seg[q] : 0;
+      np[j] = 0xffffffffu;
+      if (e >= tot) continue;
+      int lo = 0, hi = n - 1;  // last segment starting at or before e
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (s.seg[mid] <= e) lo = mid;
+        else hi = mid - 1;
       }
-      for (;;) {
-        bool any = false;
-#pragma unroll
-        for (int q = 0; q < NL; q++) {
-          if (!len[q]) continue;
-          any = true;
-          const uint32_t half = len[q] >> 1, m = base[q] + half;
-          if (key_lt(s.h[m], s.l[m], s.b[m], vh, vl, vb)) {
-            base[q] = m + 1;
-            len[q] -= half + 1;
-          } else {
-            len[q] = half;
-          }
-        }
-        if (!any) break;
-      }
-      bool drop = rm && !(vb & 1);
-#pragma unroll
-      for (int q = 0; q < NL; q++) {
-        P[j][q] = (uint16_t)base[q];
-        if (q > l && q < n && base[q] < s.seg[q + 1] && key_eq(s.h[base[q]], s.l[base[q]], s.b[base[q]], vh, vl, vb))
-          drop = true;
-      }
-      s.keep[e] = !drop;
+      const int g0 = lo & ~(2 * w - 1);
+      const int gm = g0 + w < n ? g0 + w : n, g1 = g0 + 2 * w < n ? g0 + 2 * w : n;
+      const uint32_t am = s.seg[gm];
+      rh[j] = s.h[e];
+      rl[j] = s.l[e];
+      rb[j] = s.b[e];
+      rr[j] = s.run[e];
+      if (lo < gm) np[j] = e + (lbound(s, am, s.seg[g1], rh[j], rl[j], rb[j]) - am);
+      else np[j] = e - am + ubound(s, s.seg[g0], am, rh[j], rl[j], rb[j]);
     }
-  } else {
-    for (uint32_t e = threadIdx.x; e < tot; e += MB) {
-      const int l = s.run[e];
-      const uint64_t vh = s.h[e], vl = s.l[e], vb = s.b[e];
-      bool drop = rm && !(vb & 1);
-      for (int l2 = l + 1; !drop && l2 < n; l2++) {
-        const uint32_t a = s.seg[l2], z = s.seg[l2 + 1];
-        if (a == z) continue;
-        const uint32_t p = lbound(s, a, z, vh, vl, vb);
-        drop = p < z && key_eq(s.h[p], s.l[p], s.b[p], vh, vl, vb);
-      }
-      s.keep[e] = !drop;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < KPT; j++) {
+      const uint32_t d = np[j];
+      if (d == 0xffffffffu) continue;
+      s.h[d] = rh[j];
+      s.l[d] = rl[j];
+      s.b[d] = rb[j];
+      s.run[d] = rr[j];
     }
+    __syncthreads();
+  }
+  // a survivor has no equal key in a newer run (RdbList.cpp:3254-3274): the
+  // equal keys after it are in run order, so look for one from another run
+  for (uint32_t e = threadIdx.x; e < tot; e += MB) {
+    const uint64_t vh = s.h[e], vl = s.l[e], vb = s.b[e];
+    bool drop = rm && !(vb & 1);
+    for (uint32_t f = e + 1; !drop && f < tot && key_eq(s.h[f], s.l[f], s.b[f], vh, vl, vb); f++)
+      drop = s.run[f] != s.run[e];
+    s.keep[e] = !drop;
   }
   __syncthreads();
   uint32_t em = 0;
@@ -577,46 +578,15 @@ __global__ void __launch_bounds__(MB) k_mtile(const MList *lists, int n, const u
   }
   uint32_t nemit;
   const uint32_t eb = block_scan<MB>((uint32_t)__popc(em), 0u, OpAdd(), s.tmp, &nemit);
+  // entries are in merged order: a survivor's rank is the survivors before it
 #pragma unroll
   for (int j = 0; j < KPT; j++) {
     const uint32_t e = threadIdx.x * KPT + j;
-    if (e < tot) s.E[e] = (uint16_t)(eb + __popc(em & ((1u << j) - 1)));
+    if (e < tot && (em >> j & 1)) s.ord[eb + __popc(em & ((1u << j) - 1))] = (uint16_t)e;
   }
-  if (threadIdx.x == 0) s.E[tot] = (uint16_t)nemit;
-  __syncthreads();
   if (nemit == 0) {
     if (threadIdx.x == 0) ts[t] = TileSum{0, 0, 0, 0, 0, 0, 0, 0};
     return;
-  }
-  // merged rank of each survivor: survivors before it in its own segment +
-  // survivors with a smaller key in every other segment (equal keys of other
-  // runs are never survivors)
-  if (NL > 0) {
-#pragma unroll
-    for (int j = 0; j < KPT; j++) {
-      const uint32_t e = threadIdx.x + MB * j;
-      if (e >= tot) break;
-      if (!s.keep[e]) continue;
-      const int l = s.run[e];
-      uint32_t r = s.E[e] - s.E[s.seg[l]];
-#pragma unroll
-      for (int q = 0; q < NL; q++)
-        if (q < n && q != l) r += s.E[P[j][q]] - s.E[s.seg[q]];
-      s.ord[r] = (uint16_t)e;
-    }
-  } else {
-    for (uint32_t e = threadIdx.x; e < tot; e += MB) {
-      if (!s.keep[e]) continue;
-      const int l = s.run[e];
-      const uint64_t vh = s.h[e], vl = s.l[e], vb = s.b[e];
-      uint32_t r = s.E[e] - s.E[s.seg[l]];
-      for (int l2 = 0; l2 < n; l2++) {
-        const uint32_t a = s.seg[l2], z = s.seg[l2 + 1];
-        if (l2 == l || a == z) continue;
-        r += s.E[lbound(s, a, z, vh, vl, vb)] - s.E[a];
-      }
-      s.ord[r] = (uint16_t)e;
-    }
   }
   __syncthreads();
   // sizes of ranks 1..n-1 against their predecessor, their tile offsets
@@ -991,8 +961,7 @@ static int run(MergeState *s, const uint8_t *const *lists, const int64_t *sizes,
                                                  s->off.as<uint32_t>());
     MCHECK(hipGetLastError());
     MCHECK(hipEventRecord(s->ev[2], st));
-    if (n <= 8) k_mtile<8><<<T32, MB, 0, st>>>(dl, n, s->off.as<uint32_t>(), K, ts, rm, arena, dctl);
-    else k_mtile<0><<<T32, MB, 0, st>>>(dl, n, s->off.as<uint32_t>(), K, ts, rm, arena, dctl);
+    k_mtile<<<T32, MB, 0, st>>>(dl, n, s->off.as<uint32_t>(), K, ts, rm, arena, dctl);
     MCHECK(hipEventRecord(s->ev[3], st));
     k_tscan1<<<nblk, MB, 0, st>>>(ts, T32, s->bs.as<BlkSum>());
     k_tscan2<<<1, 1024, 0, st>>>(ts, s->bs.as<BlkSum>(), nblk, s->bo.as<TileOff>());
