@@ -55,7 +55,8 @@ constexpr int MCH = MB * MUPT;                   // 2048 units = 12 KiB per deco
 constexpr int WIN_LO = 16;                       // bytes staged before a chunk (2 units + pad)
 constexpr int WIN_BYTES = WIN_LO + MCH * 6 + 16; // + 2 units after it
 constexpr int TCAP = 512;                        // keys per merge tile
-constexpr int KPT = TCAP / MB;                   // keys per thread in a tile
+constexpr int TB = 256;                          // threads per merge-tile block
+constexpr int KPT = TCAP / TB;                   // keys per thread in a tile
 constexpr int MAXN = 256;                        // runs per merge (oracle MAXL)
 constexpr int SCAN_TPB = MB * 4;                 // tiles per scan block
 
@@ -146,6 +147,11 @@ __device__ __forceinline__ bool key_lt(uint64_t h1, uint64_t l1, uint64_t b1, ui
   if (h1 != h2) return h1 < h2;
   if (l1 != l2) return l1 < l2;
   return (b1 | 7) < (b2 | 7);
+}
+// the same order without short-circuits: all three words are loaded up front
+__device__ __forceinline__ bool key_lt_bl(uint64_t h1, uint64_t l1, uint64_t b1, uint64_t h2, uint64_t l2,
+                                          uint64_t b2) {
+  return (h1 < h2) | ((h1 == h2) & ((l1 < l2) | ((l1 == l2) & ((b1 | 7) < (b2 | 7)))));
 }
 __device__ __forceinline__ bool key_eq(uint64_t h1, uint64_t l1, uint64_t b1, uint64_t h2, uint64_t l2, uint64_t b2) {
   return h1 == h2 && l1 == l2 && (b1 | 7) == (b2 | 7);
@@ -435,8 +441,8 @@ struct TileLds {
   uint32_t seg[MAXN + 1];
   uint32_t beg[MAXN];
   uint64_t koff[MAXN];
-  uint32_t tmp[MB / 64];
-  uint64_t tmp64[MB / 64];
+  uint32_t tmp[TB / 64];
+  uint64_t tmp64[TB / 64];
 };
 
 __device__ __forceinline__ uint32_t lbound(const TileLds &s, uint32_t a, uint32_t z, uint64_t vh, uint64_t vl,
@@ -476,7 +482,7 @@ __device__ __forceinline__ void put_key(uint16_t *o, uint32_t sz, uint64_t h, ui
 // Survivors (no equal key in a newer run, RdbList.cpp:3254-3274; not a delete
 // key under removeNegKeys, 3276-3279), their merged order, and the bytes of
 // survivors 2..n compressed against their predecessor, appended to the arena.
-__global__ void __launch_bounds__(MB) k_mtile(const MList *lists, int n, const uint32_t *off, Keys K, TileSum *ts,
+__global__ void __launch_bounds__(TB) k_mtile(const MList *lists, int n, const uint32_t *off, Keys K, TileSum *ts,
                                               int rm, uint8_t *arena, MCtl *ctl) {
   __shared__ TileLds s;
   const uint32_t t = blockIdx.x;
@@ -490,10 +496,10 @@ __global__ void __launch_bounds__(MB) k_mtile(const MList *lists, int n, const u
     before = b;
   }
   uint32_t tot;
-  const uint32_t ex = block_scan<MB>(len, 0u, OpAdd(), s.tmp, &tot);
+  const uint32_t ex = block_scan<TB>(len, 0u, OpAdd(), s.tmp, &tot);
   // keys of all runs before this tile: the tile's arena bytes start at 18x that
   uint64_t kbefore;
-  block_scan<MB>(before, (uint64_t)0, OpAdd(), s.tmp64, &kbefore);
+  block_scan<TB>(before, (uint64_t)0, OpAdd(), s.tmp64, &kbefore);
   if (threadIdx.x < n) s.seg[threadIdx.x] = ex;
   if (threadIdx.x == 0) s.seg[n] = tot;
   if (tot > TCAP || tot == 0) {
@@ -504,7 +510,7 @@ __global__ void __launch_bounds__(MB) k_mtile(const MList *lists, int n, const u
     return;
   }
   __syncthreads();
-  for (uint32_t e = threadIdx.x; e < tot; e += MB) {
+  for (uint32_t e = threadIdx.x; e < tot; e += TB) {
     int lo = 0, hi = n - 1;  // last run whose segment starts at or before e
     while (lo < hi) {
       const int mid = (lo + hi + 1) >> 1;
@@ -525,12 +531,14 @@ __global__ void __launch_bounds__(MB) k_mtile(const MList *lists, int n, const u
   // so keys equal under bfcmpPosdb stay in run order (older first).
   for (int w = 1; w < n; w <<= 1) {
     uint64_t rh[KPT], rl[KPT], rb[KPT];
-    uint32_t np[KPT];
+    uint32_t np[KPT], base[KPT], len[KPT];
+    bool ub[KPT];
     uint8_t rr[KPT];
 #pragma unroll
     for (int j = 0; j < KPT; j++) {
-      const uint32_t e = threadIdx.x + MB * j;
+      const uint32_t e = threadIdx.x + TB * j;
       np[j] = 0xffffffffu;
+      len[j] = 0;
       if (e >= tot) continue;
       int lo = 0, hi = n - 1;  // last segment starting at or before e
       while (lo < hi) {
@@ -545,9 +553,40 @@ __global__ void __launch_bounds__(MB) k_mtile(const MList *lists, int n, const u
       rl[j] = s.l[e];
       rb[j] = s.b[e];
       rr[j] = s.run[e];
-      if (lo < gm) np[j] = e + (lbound(s, am, s.seg[g1], rh[j], rl[j], rb[j]) - am);
-      else np[j] = e - am + ubound(s, s.seg[g0], am, rh[j], rl[j], rb[j]);
+      if (lo < gm) {  // A entry: index in A + keys of B strictly below it
+        np[j] = e - am;
+        base[j] = am;
+        len[j] = s.seg[g1] - am;
+        ub[j] = false;
+      } else {  // B entry: index in B + keys of A at or below it
+        np[j] = e - am;
+        base[j] = s.seg[g0];
+        len[j] = am - s.seg[g0];
+        ub[j] = true;
+      }
     }
+    // the KPT searches in lockstep, each step's three key words loaded together
+    for (;;) {
+      bool any = false;
+#pragma unroll
+      for (int j = 0; j < KPT; j++) {
+        if (!len[j]) continue;
+        any = true;
+        const uint32_t half = len[j] >> 1, m = base[j] + half;
+        const uint64_t xh = s.h[m], xl = s.l[m], xb = s.b[m];
+        const bool go = ub[j] ? !key_lt_bl(rh[j], rl[j], rb[j], xh, xl, xb) : key_lt_bl(xh, xl, xb, rh[j], rl[j], rb[j]);
+        if (go) {
+          base[j] = m + 1;
+          len[j] -= half + 1;
+        } else {
+          len[j] = half;
+        }
+      }
+      if (!any) break;
+    }
+#pragma unroll
+    for (int j = 0; j < KPT; j++)
+      if (threadIdx.x + TB * j < tot) np[j] += base[j];  // (e - am wraps for A entries)
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < KPT; j++) {
@@ -562,7 +601,7 @@ __global__ void __launch_bounds__(MB) k_mtile(const MList *lists, int n, const u
   }
   // a survivor has no equal key in a newer run (RdbList.cpp:3254-3274): the
   // equal keys after it are in run order, so look for one from another run
-  for (uint32_t e = threadIdx.x; e < tot; e += MB) {
+  for (uint32_t e = threadIdx.x; e < tot; e += TB) {
     const uint64_t vh = s.h[e], vl = s.l[e], vb = s.b[e];
     bool drop = rm && !(vb & 1);
     for (uint32_t f = e + 1; !drop && f < tot && key_eq(s.h[f], s.l[f], s.b[f], vh, vl, vb); f++)
@@ -577,7 +616,7 @@ __global__ void __launch_bounds__(MB) k_mtile(const MList *lists, int n, const u
     if (e < tot && s.keep[e]) em |= 1u << j;
   }
   uint32_t nemit;
-  const uint32_t eb = block_scan<MB>((uint32_t)__popc(em), 0u, OpAdd(), s.tmp, &nemit);
+  const uint32_t eb = block_scan<TB>((uint32_t)__popc(em), 0u, OpAdd(), s.tmp, &nemit);
   // entries are in merged order: a survivor's rank is the survivors before it
 #pragma unroll
   for (int j = 0; j < KPT; j++) {
@@ -601,7 +640,7 @@ __global__ void __launch_bounds__(MB) k_mtile(const MList *lists, int n, const u
     mine += sz[j];
   }
   uint32_t inner;
-  uint32_t o = block_scan<MB>(mine, 0u, OpAdd(), s.tmp, &inner);
+  uint32_t o = block_scan<TB>(mine, 0u, OpAdd(), s.tmp, &inner);
   const uint64_t at = 18 * kbefore;
   if (threadIdx.x == 0) {
     const uint32_t f = s.ord[0], z = s.ord[nemit - 1];
@@ -961,7 +1000,7 @@ static int run(MergeState *s, const uint8_t *const *lists, const int64_t *sizes,
                                                  s->off.as<uint32_t>());
     MCHECK(hipGetLastError());
     MCHECK(hipEventRecord(s->ev[2], st));
-    k_mtile<<<T32, MB, 0, st>>>(dl, n, s->off.as<uint32_t>(), K, ts, rm, arena, dctl);
+    k_mtile<<<T32, TB, 0, st>>>(dl, n, s->off.as<uint32_t>(), K, ts, rm, arena, dctl);
     MCHECK(hipEventRecord(s->ev[3], st));
     k_tscan1<<<nblk, MB, 0, st>>>(ts, T32, s->bs.as<BlkSum>());
     k_tscan2<<<1, 1024, 0, st>>>(ts, s->bs.as<BlkSum>(), nblk, s->bo.as<TileOff>());
