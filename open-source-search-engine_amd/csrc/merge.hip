@@ -259,7 +259,9 @@ __global__ void __launch_bounds__(MB) k_mcount(const MList *lists, int n, DSum *
   if (threadIdx.x == 0) sum[blockIdx.x] = DSum{a, b, c, 0};
 }
 
-// per run (one block each): exclusive key count and lo/hi carries per chunk
+// per run (one block each): exclusive key count and lo/hi carries per chunk;
+// each thread takes SCH consecutive chunks per pass
+constexpr int SCH = 8;
 __global__ void __launch_bounds__(1024) k_mscan(MList *lists, DSum *sum) {
   __shared__ uint32_t t0[16], t1[16], t2[16];
   __shared__ uint32_t carry[3];
@@ -267,15 +269,30 @@ __global__ void __launch_bounds__(1024) k_mscan(MList *lists, DSum *sum) {
   const uint32_t nch = (L.units + MCH - 1) / MCH;
   if (threadIdx.x == 0) carry[0] = carry[1] = carry[2] = 0;
   __syncthreads();
-  for (uint32_t base = 0; base < nch; base += 1024) {
-    const uint32_t i = base + threadIdx.x;
-    DSum v = i < nch ? sum[L.c0 + i] : DSum{0, 0, 0, 0};
+  for (uint32_t base = 0; base < nch; base += 1024 * SCH) {
+    const uint32_t i0 = base + threadIdx.x * SCH;
+    DSum v[SCH];
+    uint32_t x0 = 0, x1 = 0, x2 = 0;
+#pragma unroll
+    for (int q = 0; q < SCH; q++) {
+      v[q] = i0 + q < nch ? sum[L.c0 + i0 + q] : DSum{0, 0, 0, 0};
+      x0 += v[q].nkeys;
+      x1 = v[q].lastlo > x1 ? v[q].lastlo : x1;
+      x2 = v[q].lasthi > x2 ? v[q].lasthi : x2;
+    }
     uint32_t a, b, c;
     const uint32_t c0 = carry[0], c1 = carry[1], c2 = carry[2];
-    uint32_t e0 = block_scan<1024>(v.nkeys, 0u, OpAdd(), t0, &a);
-    uint32_t e1 = block_scan<1024>(v.lastlo, 0u, OpMax(), t1, &b);
-    uint32_t e2 = block_scan<1024>(v.lasthi, 0u, OpMax(), t2, &c);
-    if (i < nch) sum[L.c0 + i] = DSum{c0 + e0, e1 > c1 ? e1 : c1, e2 > c2 ? e2 : c2, 0};
+    const uint32_t e0 = block_scan<1024>(x0, 0u, OpAdd(), t0, &a);
+    const uint32_t e1 = block_scan<1024>(x1, 0u, OpMax(), t1, &b);
+    const uint32_t e2 = block_scan<1024>(x2, 0u, OpMax(), t2, &c);
+    uint32_t r0 = c0 + e0, r1 = e1 > c1 ? e1 : c1, r2 = e2 > c2 ? e2 : c2;
+#pragma unroll
+    for (int q = 0; q < SCH; q++) {
+      if (i0 + q < nch) sum[L.c0 + i0 + q] = DSum{r0, r1, r2, 0};
+      r0 += v[q].nkeys;
+      r1 = v[q].lastlo > r1 ? v[q].lastlo : r1;
+      r2 = v[q].lasthi > r2 ? v[q].lasthi : r2;
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
       carry[0] = c0 + a;
@@ -365,15 +382,19 @@ __global__ void __launch_bounds__(MB) k_mdecode(const MList *lists, int n, const
 }
 
 // ------------------------------------------------------------ partition
-__global__ void __launch_bounds__(MB) k_msample(const MList *lists, int n, uint32_t S, Keys K, Keys Sm,
+// a splitter: the three key words side by side, so one step of a search over
+// splitters touches one 32-byte sector instead of three cache lines
+struct __attribute__((aligned(32))) SKey {
+  uint64_t h, l, b, pad;
+};
+
+__global__ void __launch_bounds__(MB) k_msample(const MList *lists, int n, uint32_t S, Keys K, SKey *Sm,
                                                 uint32_t nsamples) {
   const uint32_t g = blockIdx.x * MB + threadIdx.x;
   if (g >= nsamples) return;
   const MList &L = lists[list_of_sample(lists, n, g)];
   const uint64_t idx = L.koff + (uint64_t)(g - L.soff) * S;
-  Sm.hi[g] = K.hi[idx];
-  Sm.lo[g] = K.lo[idx];
-  Sm.b[g] = K.b[idx];
+  Sm[g] = SKey{K.hi[idx], K.lo[idx], K.b[idx], 0};
 }
 
 // first index in [a, z) of K whose key is >= v (UB: > v)
@@ -389,17 +410,31 @@ __device__ __forceinline__ uint64_t gbound(const Keys &K, uint64_t a, uint64_t z
   return a;
 }
 
+template <bool UB>
+__device__ __forceinline__ uint64_t sbound(const SKey *Sm, uint64_t a, uint64_t z, uint64_t vh, uint64_t vl,
+                                           uint64_t vb) {
+  while (a < z) {
+    const uint64_t m = (a + z) >> 1;
+    const SKey x = Sm[m];
+    const bool go = UB ? !key_lt(vh, vl, vb, x.h, x.l, x.b) : key_lt(x.h, x.l, x.b, vh, vl, vb);
+    if (go) a = m + 1;
+    else z = m;
+  }
+  return a;
+}
+
 // sorted order of all samples by (key, run, index): scatter sample ids
-__global__ void __launch_bounds__(MB) k_mrank(const MList *lists, int n, Keys Sm, uint32_t nsamples, uint32_t *tiles) {
+__global__ void __launch_bounds__(MB) k_mrank(const MList *lists, int n, const SKey *Sm, uint32_t nsamples, uint32_t *tiles) {
   const uint32_t g = blockIdx.x * MB + threadIdx.x;
   if (g >= nsamples) return;
   const int l = list_of_sample(lists, n, g);
-  const uint64_t vh = Sm.hi[g], vl = Sm.lo[g], vb = Sm.b[g];
+  const SKey v = Sm[g];
+  const uint64_t vh = v.h, vl = v.l, vb = v.b;
   uint64_t pos = g - lists[l].soff;
   for (int l2 = 0; l2 < n; l2++) {
     if (l2 == l) continue;
     const uint64_t a = lists[l2].soff, z = a + lists[l2].ns;
-    pos += (l2 < l ? gbound<true>(Sm, a, z, vh, vl, vb) : gbound<false>(Sm, a, z, vh, vl, vb)) - a;
+    pos += (l2 < l ? sbound<true>(Sm, a, z, vh, vl, vb) : sbound<false>(Sm, a, z, vh, vl, vb)) - a;
   }
   tiles[pos] = g;
 }
@@ -408,7 +443,7 @@ __global__ void __launch_bounds__(MB) k_mrank(const MList *lists, int n, Keys Sm
 // boundary, the sorted sample at position t*J; row T holds the run lengths.
 // Run l2's segment then holds at most (samples of l2 among the J + 1)*S keys,
 // so a tile holds at most (J + n)*S keys -- TCAP for J = n, S = TCAP/2n.
-__global__ void __launch_bounds__(MB) k_moff(const MList *lists, int n, uint32_t S, uint32_t J, Keys K, Keys Sm,
+__global__ void __launch_bounds__(MB) k_moff(const MList *lists, int n, uint32_t S, uint32_t J, Keys K, const SKey *Sm,
                                              const uint32_t *tiles, uint32_t T, uint32_t *off) {
   const uint64_t i = (uint64_t)blockIdx.x * MB + threadIdx.x;
   if (i >= (uint64_t)(T + 1) * n) return;
@@ -420,8 +455,9 @@ __global__ void __launch_bounds__(MB) k_moff(const MList *lists, int n, uint32_t
     return;
   }
   const uint32_t g = tiles[(size_t)t * J];
-  const uint64_t vh = Sm.hi[g], vl = Sm.lo[g], vb = Sm.b[g];
-  const uint64_t q = gbound<false>(Sm, L.soff, (uint64_t)L.soff + L.ns, vh, vl, vb) - L.soff;
+  const SKey v = Sm[g];
+  const uint64_t vh = v.h, vl = v.l, vb = v.b;
+  const uint64_t q = sbound<false>(Sm, L.soff, (uint64_t)L.soff + L.ns, vh, vl, vb) - L.soff;
   uint64_t r = 0;
   if (q > 0) {
     // samples q-1 < v <= sample q: the bound is in ((q-1)S, qS]
@@ -984,11 +1020,11 @@ static int run(MergeState *s, const uint8_t *const *lists, const int64_t *sizes,
     if (NS >= 0x7fffffffULL || (T + 1) * (uint64_t)n >= 0xffffffffULL) return GBGPU_ECAPACITY;
     s->ntiles = (int64_t)T;
     const uint32_t nblk = cdiv(T, SCAN_TPB);
-    if (s->shi.ensure(8 * NS) || s->slo.ensure(8 * NS) || s->sb.ensure(8 * NS) || s->tiles.ensure(4 * NS) ||
+    if (s->shi.ensure(sizeof(SKey) * NS) || s->tiles.ensure(4 * NS) ||
         s->off.ensure(4 * (T + 1) * n) || s->ts.ensure(sizeof(TileSum) * T) || s->to.ensure(sizeof(TileOff) * T) ||
         s->bs.ensure(sizeof(BlkSum) * nblk) || s->bo.ensure(sizeof(TileOff) * nblk))
       return ENOMEM;
-    Keys Sm{s->shi.as<uint64_t>(), s->slo.as<uint64_t>(), s->sb.as<uint64_t>()};
+    SKey *Sm = s->shi.as<SKey>();
     const uint32_t T32 = (uint32_t)T, NS32 = (uint32_t)NS;
     TileSum *ts = s->ts.as<TileSum>();
     TileOff *to = s->to.as<TileOff>();
