@@ -840,22 +840,44 @@ __global__ void k_mcut(const TileSum *ts, const TileOff *to, uint32_t T, const u
 // out[off, off + bytes) of every tile, below the cut: its first key, then its
 // arena bytes.  Byte offsets are even (keys are 6-byte multiples).
 __global__ void __launch_bounds__(MB) k_mcopy(const TileSum *ts, const TileOff *to, const uint8_t *arena,
-                                              const MCtl *ctl, uint64_t cap, uint8_t *out) {
-  const uint32_t t = blockIdx.x;
+                                              const MCtl *ctl, uint64_t cap, uint8_t *out, uint32_t T) {
+  // one wave per tile
+  const uint32_t t = blockIdx.x * (MB / 64) + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (t >= T) return;
   const TileSum S = ts[t];
   if (S.n == 0) return;
   const TileOff o = to[t];
   uint64_t lim = ctl->out_end;
   if (lim > cap) lim = cap;
   if (o.off >= lim) return;
-  if (threadIdx.x == 0 && o.off + o.fsize <= lim)
+  if (lane == 0 && o.off + o.fsize <= lim)
     put_key(reinterpret_cast<uint16_t *>(out + o.off), o.fsize, S.fhi, S.flo, S.fb);
   const uint64_t d0 = o.off + o.fsize;
   if (d0 >= lim) return;
   const uint32_t nb = (uint32_t)((d0 + S.inner <= lim ? d0 + S.inner : lim) - d0);
-  const uint16_t *src = reinterpret_cast<const uint16_t *>(arena + S.arena);
-  uint16_t *dst = reinterpret_cast<uint16_t *>(out + d0);
-  for (uint32_t i = threadIdx.x; i < nb / 2; i += MB) dst[i] = src[i];
+  // 2-byte stores up to an 8-byte aligned destination and after the last
+  // whole word (the bytes either side belong to the neighbouring tiles), 8-byte
+  // stores in between, each assembled from two aligned source words (the
+  // arena has slack past its last tile, so reading one word beyond is safe)
+  const uint8_t *sp = arena + S.arena;
+  uint8_t *dp = out + d0;
+  uint32_t head = (uint32_t)((8 - ((uintptr_t)dp & 7)) & 7);
+  if (head > nb) head = nb;
+  if (lane < head / 2)
+    reinterpret_cast<uint16_t *>(dp)[lane] = reinterpret_cast<const uint16_t *>(sp)[lane];
+  const uint32_t nw = (nb - head) >> 3, tail = (nb - head) & 7;
+  const uintptr_t sa = (uintptr_t)(sp + head);
+  const uint64_t *sw = reinterpret_cast<const uint64_t *>(sa & ~(uintptr_t)7);
+  const uint32_t sh = (uint32_t)(sa & 7) * 8;
+  uint64_t *dw = reinterpret_cast<uint64_t *>(dp + head);
+  if (sh == 0) {
+    for (uint32_t w = lane; w < nw; w += 64) dw[w] = sw[w];
+  } else {
+    for (uint32_t w = lane; w < nw; w += 64) dw[w] = (sw[w] >> sh) | (sw[w + 1] << (64 - sh));
+  }
+  const uint32_t t0 = head + nw * 8;
+  if (lane < tail / 2)
+    reinterpret_cast<uint16_t *>(dp + t0)[lane] = reinterpret_cast<const uint16_t *>(sp + t0)[lane];
 }
 
 // ------------------------------------------------------------------ host
@@ -1005,7 +1027,7 @@ static int run(MergeState *s, const uint8_t *const *lists, const int64_t *sizes,
   // list); the tile pass then flags F_CAPACITY and the partition is redone
   // with a smaller S.
   const uint32_t J = (uint32_t)n;
-  if (s->arena.ensure(18 * (size_t)std::max<uint64_t>(units, 1))) return ENOMEM;
+  if (s->arena.ensure(18 * (size_t)std::max<uint64_t>(units, 1) + 16)) return ENOMEM;  // + k_mcopy read slack
   for (uint32_t S = (uint32_t)std::max(1, TCAP / (2 * n));; S /= 2) {
     uint64_t NS = 0;
     s->nkeys = 0;
@@ -1043,7 +1065,7 @@ static int run(MergeState *s, const uint8_t *const *lists, const int64_t *sizes,
     k_tscan3<<<nblk, MB, 0, st>>>(ts, T32, s->bo.as<TileOff>(), to);
     k_mcut<<<1, 64, 0, st>>>(ts, to, T32, arena, (uint64_t)maxoff, dctl);
     MCHECK(hipEventRecord(s->ev[4], st));
-    k_mcopy<<<T32, MB, 0, st>>>(ts, to, arena, dctl, (uint64_t)cap, out);
+    k_mcopy<<<cdiv(T, MB / 64), MB, 0, st>>>(ts, to, arena, dctl, (uint64_t)cap, out, T32);
     MCHECK(hipGetLastError());
     MCHECK(hipEventRecord(s->ev[5], st));
     MCHECK(hipMemcpyAsync(s->h_ctl, dctl, sizeof(MCtl), hipMemcpyDeviceToHost, st));
