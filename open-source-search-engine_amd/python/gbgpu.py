@@ -339,11 +339,20 @@ class Engine:
         return QueryResult(np.frombuffer(d, dtype=np.int64, count=n).copy(),
                            np.frombuffer(s, dtype=np.float32, count=n).copy(), r.hits, r.filtered, r.docs_wanted)
 
-    def query(self, terms: Sequence[QTerm], lists: Sequence[bytes], params: Params, cap: int = 4096) -> QueryResult:
+    @staticmethod
+    def host_lists(lists: Sequence[bytes]):
+        """Host copies of the lists and the gbgpu_list array naming them
+        (keep the returned tuple alive while the refs are in use)."""
+        keep = [ctypes.create_string_buffer(bytes(l), max(1, len(l))) for l in lists]
+        refs = (ListRef * max(len(lists), 1))(*[ListRef(ctypes.cast(k, ctypes.c_void_p), len(l))
+                                                for k, l in zip(keep, lists)])
+        return keep, refs
+
+    def query(self, terms: Sequence[QTerm], lists, params: Params, cap: int = 4096) -> QueryResult:
+        """gbgpu_query over host lists: a sequence of bytes, or host_lists()'s tuple."""
         n = len(terms)
         qt = (QTerm * max(n, 1))(*terms)
-        keep = [ctypes.create_string_buffer(l, max(1, len(l))) for l in lists]
-        refs = (ListRef * max(n, 1))(*[ListRef(ctypes.cast(k, ctypes.c_void_p), len(l)) for k, l in zip(keep, lists)])
+        keep, refs = lists if isinstance(lists, tuple) else self.host_lists(lists)
         r, d, s = self._result(cap)
         _check(self.lib.gbgpu_query(self.ctx, qt, n, refs, ctypes.byref(params), ctypes.byref(r)), "query")
         return self._pack(r, d, s)
