@@ -17,8 +17,14 @@
  * every input and output buffer and they are never mutated; the library owns
  * device memory.  Functions return 0 or a positive errno-style code that the
  * Msg39 adapter copies into PosdbTable::m_errno; no exceptions cross the ABI.
- * A context is used by one thread at a time (calls are serialised on an
- * internal mutex); open one context per INTERSECT thread for concurrency.
+ *
+ * Concurrency: one context per GPU, shared by every INTERSECT thread of the
+ * process.  A context owns 1..64 query slots (gbgpu_set_query_slots), each
+ * with its own HIP stream and buffers over the shared resident lists; the
+ * blocking entry points (gbgpu_query, gbgpu_query_resident) are re-entrant
+ * and take a free slot, waiting for one when all are busy.  The slot-explicit
+ * enqueue/collect pair is for a single caller per slot.  A list freed while a
+ * query in flight still reads it is released when that query is collected.
  */
 #ifndef GBGPU_H
 #define GBGPU_H
@@ -29,7 +35,7 @@
 extern "C" {
 #endif
 
-#define GBGPU_ABI_VERSION 3
+#define GBGPU_ABI_VERSION 4
 
 /* error codes beyond errno.h (Errno.h numbering is not reused) */
 #define GBGPU_ENODEVICE   1001 /* no HIP device / extension not usable        */
@@ -57,12 +63,18 @@ typedef struct gbgpu_qterm {
   float   tf_weight;                /* ptr_termFreqWeights[i]                        */
 } gbgpu_qterm;
 
-/* Msg39Request scalars read by PosdbTable (Msg39.h:94-147) */
+/* Msg39Request scalars read by PosdbTable (Msg39.h:94-147).  Zero-filled
+ * trailing fields reproduce a request without paging and without the max-score
+ * prefilter; Msg39Request::reset() (Msg39.h:36-82) sets do_max_score_algo=1. */
 typedef struct gbgpu_params {
   int32_t docs_to_get;      /* m_docsToGet                                        */
   int32_t real_max_top;     /* m_realMaxTop (clamped to MAX_TOP = 10)              */
   int32_t language;         /* m_language                                         */
-  int32_t site_clustering;  /* m_doSiteClustering: must be 0 (EUNSUPPORTED)        */
+  int32_t site_clustering;  /* m_doSiteClustering: TopTree domain caps
+                               (TopTree.cpp:64-186, 312-516) and the pruning they
+                               make live (minWinningScore, Posdb.cpp:7699-7704;
+                               getMaxPossibleScore 7811-7960; ring buffer
+                               6365-6504), replayed in docid order on the GPU   */
   int32_t num_docid_splits; /* m_numDocIdSplits: >1 runs Msg39's docid-split loop
                                (Msg39.cpp:345-457) inside gbgpu_query/_resident:
                                one pass per docid piece [d0, d1+2] into one TopTree
@@ -70,6 +82,13 @@ typedef struct gbgpu_params {
                                and filtered are the sums over pieces.  The
                                enqueue/collect form returns EUNSUPPORTED for it */
   float   same_lang_weight; /* m_sameLangWeight                                   */
+  int32_t do_max_score_algo;/* m_doMaxScoreAlgo: per-term getMaxPossibleScore
+                               prefilter (Posdb.cpp:6046-6047, 6327-6346)         */
+  int32_t reserved0;        /* 0                                                  */
+  double  max_serp_score;   /* m_maxSerpScore  } paging of a widget's next page:   */
+  int64_t min_serp_docid;   /* m_minSerpDocId  } nonzero enables the filter of
+                               Posdb.cpp:4379-4381, 7327-7347 (counted in
+                               gbgpu_result::filtered)                           */
 } gbgpu_params;
 
 /* A posdb termlist exactly as Msg2::getList(i) holds it: first key 18 bytes,
@@ -84,10 +103,18 @@ typedef struct gbgpu_result {
   int64_t *docids;     /* caller-owned, `capacity` entries; TopTree high -> low   */
   float   *scores;     /* caller-owned, `capacity` entries (TopNode::m_score)     */
   int32_t  capacity;
-  int32_t  n;          /* entries written (<= docs_wanted, <= capacity)           */
+  int32_t  n;          /* entries written: every TopTree node (m_numUsedNodes;
+                          <= docs_wanted without site clustering), <= capacity */
   int64_t  hits;       /* m_docIdVoteBuf.length()/6: exact intersection size       */
   int32_t  filtered;   /* m_filtered                                               */
   int32_t  docs_wanted;/* TopTree::m_docsWanted (0: no tree was allocated)          */
+  /* optional: the intersected docid set itself -- the docids of
+   * m_docIdVoteBuf after addDocIdVotes/rmDocIdVotes (Posdb.cpp:5154-5171,
+   * 5281-5290, 4871-4946), ascending.  NULL to skip.  With docid splits it is
+   * the union over the pieces (boundary docids once). */
+  int64_t *hit_docids;   /* caller-owned, hit_capacity entries                     */
+  int64_t  hit_capacity;
+  int64_t  n_hit_docids; /* entries written (min(set size, hit_capacity))          */
 } gbgpu_result;
 
 int         gbgpu_open(int device, gbgpu_ctx **out);
@@ -96,8 +123,11 @@ const char *gbgpu_strerror(int code);
 int         gbgpu_abi_version(void);
 
 /* allocTopTree sizing (Posdb.cpp:838-930): TopTree::m_docsWanted for a query
- * (with docid splits: list_sizes are the first piece's lists) */
+ * (with docid splits: list_sizes are the first piece's lists).  With site
+ * clustering the tree may hold more nodes than this (TopTree.cpp:64-186):
+ * gbgpu_tree_capacity() is the most a result can carry. */
 int32_t gbgpu_docs_wanted(const gbgpu_params *p, const int64_t *list_sizes, int nterms);
+int32_t gbgpu_tree_capacity(const gbgpu_params *p, const int64_t *list_sizes, int nterms);
 
 /* Full drop-in: lists[] are 1-1 with terms[] (Msg2::getList(i)).  Uploads the
  * lists, intersects, scores and returns the top tree.  Synchronous. */

@@ -44,6 +44,9 @@
 #include <cstdlib>
 #include <cstring>
 #include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <memory>
 #include <mutex>
 #include <vector>
 
@@ -64,15 +67,18 @@ constexpr int MAX_RUNS = CHUNK_UNITS / 2;        // a run is >= 2 units
 constexpr int TILE = 2048;                       // final top-k sort capacity
 constexpr int MAX_K = 1536;                      // TILE - MAX_K ties merged per round
 constexpr int SEL_BINS = 4096;                   // radix-select bins per pass
+constexpr int TREE_CAP = 4096;                   // site-clustering TopTree nodes held in LDS
 constexpr int LIST_PAD = CHUNK_LOAD + 128;
 
 struct Counters {
-  uint32_t pad0;
+  uint32_t filtered;  // m_filtered: scored docids dropped by the paging filter (Posdb.cpp:7327-7347)
   uint32_t corrupt;
   unsigned long long surv_top;  // k_compact's packed bump pointer: survivors << 36 | arena units
   uint32_t g0count[MAXG0];
   uint32_t anysurv;  // bit l: list l has a run in some survivor
-  uint32_t pad[5];
+  uint32_t tree_n;   // site clustering: TopTree nodes written by k_tree_replay
+  uint32_t tree_err; // site clustering: the tree outgrew the replay's LDS (TC nodes)
+  uint32_t pad[3];
 };
 
 // radix-select state (3 passes over the 32-bit score keys: 12+12+8 bits)
@@ -790,9 +796,21 @@ constexpr int CTILE = BLOCK * CSPT;              // 4096 slots per block
 // reference merges a shared bigram sublist into both groups).  The shrunk-
 // sublist-non-empty flags (shrinkSubLists, Posdb.cpp:5334-5428) are a list
 // bitmask OR-reduced in the block and published with one atomic.
+//
+// ORDERED (site clustering, whose TopTree replay walks the survivors in docid
+// order like the vote buffer, Posdb.cpp:6137-6140): two launches instead of
+// the bump pointer -- CMODE 1 publishes each block's totals (blk[]), a one-
+// block scan (k_compact_scan) turns them into offsets, and CMODE 2 writes
+// the survivors at them, so survivors come out in slot order.
+struct BlkTot {
+  uint32_t n, pad;
+  unsigned long long u;
+};
+
+template <int CMODE>
 __global__ void __launch_bounds__(BLOCK) k_compact(const DevPlan *pl, const uint32_t *lmask, const uint32_t *ulen,
                                                    uint64_t slot_ub, Counters *ctr, uint32_t *surv,
-                                                   unsigned long long *surv_off, uint32_t *surv_lm) {
+                                                   unsigned long long *surv_off, uint32_t *surv_lm, BlkTot *blk) {
   __shared__ uint32_t tmp[BLOCK / 64];
   __shared__ uint32_t s_base_i;
   __shared__ uint32_t s_any;
@@ -807,19 +825,22 @@ __global__ void __launch_bounds__(BLOCK) k_compact(const DevPlan *pl, const uint
   if (threadIdx.x < MAXG0) s_end[threadIdx.x] = threadIdx.x < (unsigned)g0n ? pl->g0base[threadIdx.x] + ctr->g0count[threadIdx.x] : 0;
   if (threadIdx.x == 0) s_any = 0;
   __syncthreads();
-  const uint64_t s0 = (uint64_t)blockIdx.x * CTILE + threadIdx.x;
+  // a thread's slots: strided over the block (coalesced) -- or, ordered, 16
+  // consecutive ones, so thread order is slot order inside the block
+  const uint64_t s0 = (uint64_t)blockIdx.x * CTILE + (CMODE ? threadIdx.x * CSPT : threadIdx.x);
+  constexpr uint64_t SSTEP = CMODE ? 1 : BLOCK;
   // all of this thread's list masks in flight at once
   uint32_t lmv[CSPT];
 #pragma unroll
   for (int q = 0; q < CSPT; q++) {
-    const uint64_t s = s0 + (uint64_t)q * BLOCK;
+    const uint64_t s = s0 + (uint64_t)q * SSTEP;
     lmv[q] = s < slot_ub ? lmask[s] : 0u;
   }
   uint32_t okm = 0, nok = 0, utot = 0, any = 0;
   uint32_t units[CSPT];
 #pragma unroll
   for (int q = 0; q < CSPT; q++) {
-    const uint64_t s = s0 + (uint64_t)q * BLOCK;
+    const uint64_t s = s0 + (uint64_t)q * SSTEP;
     units[q] = 0;
     if (s >= slot_ub) continue;
     int k = 0;
@@ -839,30 +860,98 @@ __global__ void __launch_bounds__(BLOCK) k_compact(const DevPlan *pl, const uint
   uint32_t tot_n, tot_u;
   const uint32_t ex_n = block_exclusive_scan(nok, tmp, &tot_n);
   const uint32_t ex_u = block_exclusive_scan(utot, tmp, &tot_u);
-  if (any) atomicOr(&s_any, any);
+  if (CMODE != 2 && any) atomicOr(&s_any, any);
   __syncthreads();
   if (threadIdx.x == 0) {
-    // ONE atomic per block for both bump pointers (survivor index and arena
-    // offset), 28 + 36 bits; the host caps slot_ub and the arena to fit
-    const unsigned long long old =
-        tot_n ? atomicAdd(&ctr->surv_top, ((unsigned long long)tot_n << 36) | (unsigned long long)tot_u) : 0ull;
-    s_base_i = (uint32_t)(old >> 36);
-    s_base_u = old & ((1ull << 36) - 1);
-    if (s_any & ~__hip_atomic_load(&ctr->anysurv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+    if (CMODE == 0) {
+      // ONE atomic per block for both bump pointers (survivor index and arena
+      // offset), 28 + 36 bits; the host caps slot_ub and the arena to fit
+      const unsigned long long old =
+          tot_n ? atomicAdd(&ctr->surv_top, ((unsigned long long)tot_n << 36) | (unsigned long long)tot_u) : 0ull;
+      s_base_i = (uint32_t)(old >> 36);
+      s_base_u = old & ((1ull << 36) - 1);
+    } else if (CMODE == 1) {
+      blk[blockIdx.x].n = tot_n;
+      blk[blockIdx.x].u = tot_u;
+    } else {
+      s_base_i = blk[blockIdx.x].n;
+      s_base_u = blk[blockIdx.x].u;
+    }
+    if (CMODE != 2 && (s_any & ~__hip_atomic_load(&ctr->anysurv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)))
       atomicOr(&ctr->anysurv, s_any);
   }
+  if (CMODE == 1) return;  // uniform
   __syncthreads();
   uint32_t i = s_base_i + ex_n;
   unsigned long long off = s_base_u + ex_u;
 #pragma unroll
   for (int q = 0; q < CSPT; q++) {
     if (!(okm >> q & 1)) continue;
-    surv[i] = (uint32_t)(s0 + (uint64_t)q * BLOCK);
+    surv[i] = (uint32_t)(s0 + (uint64_t)q * SSTEP);
     surv_off[i] = off;
     surv_lm[i] = lmv[q];
     i++;
     off += units[q];
   }
+}
+
+// exclusive scan of the blocks' (survivors, arena units) -> their offsets,
+// and the totals into the counters (one block)
+__global__ void __launch_bounds__(1024) k_compact_scan(uint32_t nblk, BlkTot *blk, Counters *ctr) {
+  __shared__ uint32_t tn[16];
+  __shared__ unsigned long long tu[16];
+  __shared__ uint32_t cn;
+  __shared__ unsigned long long cu;
+  if (threadIdx.x == 0) {
+    cn = 0;
+    cu = 0;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (uint32_t base = 0; base < nblk; base += 1024) {
+    const uint32_t i = base + threadIdx.x;
+    const uint32_t vn = i < nblk ? blk[i].n : 0;
+    const unsigned long long vu = i < nblk ? blk[i].u : 0;
+    uint32_t xn = vn;
+    unsigned long long xu = vu;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t yn = __shfl_up(xn, o, 64);
+      const unsigned long long yu = __shfl_up(xu, o, 64);
+      if (lane >= o) {
+        xn += yn;
+        xu += yu;
+      }
+    }
+    if (lane == 63) {
+      tn[wid] = xn;
+      tu[wid] = xu;
+    }
+    __syncthreads();
+    uint32_t pn = 0;
+    unsigned long long pu = 0;
+    for (int w = 0; w < wid; w++) {
+      pn += tn[w];
+      pu += tu[w];
+    }
+    const uint32_t in_n = cn + pn + xn;
+    const unsigned long long in_u = cu + pu + xu;
+    __syncthreads();
+    if (i < nblk) {
+      blk[i].n = in_n - vn;
+      blk[i].u = in_u - vu;
+    }
+    if (threadIdx.x == 1023) {
+      cn = in_n;
+      cu = in_u;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) ctr->surv_top = ((unsigned long long)cn << 36) | cu;
+}
+
+// docids of the survivors (the vote buffer's docids, unordered)
+__global__ void k_gather_hits(const uint32_t *surv, const uint64_t *cand, uint32_t n, uint64_t *out) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) out[i] = cand[surv[i]];
 }
 
 // ------------------------------------------------------------------ score
@@ -1040,16 +1129,555 @@ __global__ void __launch_bounds__(SCORE_TPB) k_score(const DevPlan *pl, const ui
                                                      const uint32_t *surv, const uint32_t *surv_lm,
                                                      const unsigned long long *surv_off, const Loc *loc,
                                                      uint64_t slot_ub, uint64_t *arena, uint32_t *skey,
-                                                     uint64_t *sdoc, int diag) {
+                                                     uint64_t *sdoc, uint8_t *sflag, int diag) {
   __shared__ float s_sm[npairs<NQ>() * SCORE_TPB];
   stage_weights(&c_weights);
   const uint32_t nsurv = (uint32_t)(ctr->surv_top >> 36);
   const uint32_t anys = ctr->anysurv;
-  for (uint32_t i = blockIdx.x * SCORE_TPB + threadIdx.x; i < nsurv; i += gridDim.x * SCORE_TPB) {
-    const uint32_t s = surv[i];
-    auto *rec = (__attribute__((address_space(1))) uint64_t *)(arena + surv_off[i]);
-    score_survivor<NQ, NS>(pl, s, surv_lm[i], anys, loc, slot_ub, rec, s_sm + threadIdx.x, &skey[i], diag);
-    sdoc[i] = cand[s];
+  const uint32_t lim = (nsurv + 63) & ~63u;  // whole waves iterate together (ballot below)
+  uint32_t nfilt = 0;
+  for (uint32_t i = blockIdx.x * SCORE_TPB + threadIdx.x; i < lim; i += gridDim.x * SCORE_TPB) {
+    bool filt = false;
+    if (i < nsurv) {
+      const uint32_t s = surv[i];
+      auto *rec = (__attribute__((address_space(1))) uint64_t *)(arena + surv_off[i]);
+      uint32_t key;
+      score_survivor<NQ, NS>(pl, s, surv_lm[i], anys, loc, slot_ub, rec, s_sm + threadIdx.x, &key, diag);
+      const uint64_t d = cand[s];
+      // the paging filter of a widget's next page (Posdb.cpp:7327-7347):
+      // m_filtered counts the scored docids it drops
+      if (pl->has_serp && key) {
+        const uint32_t b = (key & 0x80000000u) ? (key & 0x7fffffffu) : ~key;
+        const float score = __uint_as_float(b);
+        if (score > (float)pl->max_serp_score) filt = true;
+        else if ((double)score == pl->max_serp_score && (int64_t)d <= pl->min_serp_docid) filt = true;
+        if (filt) key = 0;
+      }
+      skey[i] = key;
+      sdoc[i] = d;
+      // site clustering: the replay counts m_filtered, since a docid the
+      // prefilters skip never reaches the paging test (Posdb.cpp:6341-6345)
+      if (pl->clustering) sflag[i] = filt ? 1 : 0;
+    }
+    nfilt += (uint32_t)__popcll(__ballot(filt));
+  }
+  if (!pl->clustering && (threadIdx.x & 63) == 0 && nfilt) atomicAdd((uint32_t *)&ctr->filtered, nfilt);
+}
+
+// ------------------------------------------------------- site clustering
+// With m_doSiteClustering (the Msg39Request default, Msg39.h:41) the TopTree
+// keeps per-domain caps (TopTree.cpp:64-186, 312-516), so it holds more than
+// docsWanted nodes, minWinningScore becomes live (Posdb.cpp:7699-7704) and
+// the two prefilters skip docids whose bound cannot beat it (Posdb.cpp:
+// 6322-6504).  The reference decides docid by docid in vote-buffer order.
+// Here every survivor is scored in parallel as usual, and additionally
+//   k_bound        its prefilter bound B = min of the getMaxPossibleScore
+//                  values of both prefilters (-1, "has inlink text", ignored),
+//                  one wave per survivor, the 4096-slot ring buffer in LDS;
+//   k_rank         (several candidate arrays) its position in docid order;
+//   k_tree_replay  ONE wave replays the docid-order loop exactly: a docid is
+//                  skipped iff B <= minWinningScore, else offered to the
+//                  TopTree with the domain caps.  Offers that cannot change
+//                  the tree (skipped, unscored, or not better than the low
+//                  node of a full tree) are ruled out 64 at a time with a
+//                  ballot; only the others take the sequential path.
+constexpr int BND_WAVES = 4;
+constexpr int RING = 4096;     // RINGBUFSIZE, Posdb.cpp:6019
+constexpr int TC = 10240;      // TopTree nodes the replay keeps in LDS
+
+// getMaxPossibleScore (Posdb.cpp:7811-7960) up to its request- and
+// pair-specific tail: the best hash-group weight and density rank over the
+// group's runs, scanned backwards (12-byte run head last), and the siteRank /
+// langId of its first run.  state: -1 inlink text (returns -1.0), 0 nothing
+// found (returns 0.0), 1 a score (base = 100*hgw^2*dw^2*... *tfw_i)
+struct BoundCore {
+  int state;
+  float base;
+};
+
+__device__ __forceinline__ float max_score_tail(const DevPlan *pl, BoundCore c, float tfw_m, int32_t bestDist,
+                                                int32_t qdist) {
+  if (c.state <= 0) return c.state < 0 ? -1.0f : 0.0f;
+  float score = c.base;
+  if (qdist) {  // Posdb.cpp:7935-7946
+    score *= tfw_m;
+    bestDist -= qdist;
+    if (bestDist < 0) bestDist *= -1;
+    if (bestDist > 1) score /= (float)bestDist;
+  }
+  if (pl->all_same_wiki) score *= GB_WIKI_WEIGHT;
+  return score;
+}
+
+__device__ BoundCore group_bound_core(const DevPlan *pl, int g, uint32_t s, uint32_t lm, const Loc *loc,
+                                      uint64_t slot_ub) {
+  const Weights &W = s_weights;
+  float best = -1.0f;
+  unsigned bestDR = 0;
+  int sr = -1, lang = 0;
+  bool hs = false;
+  const int gns = pl->gnsub[g];
+  for (int x = 0; x < gns; x++) {
+    const int lid = pl->gsub[g][x];
+    if (!(lm >> lid & 1)) continue;  // m_savedCursor[j] == NULL
+    if (pl->gflags0[g] & BF_HALFSTOPWIKIBIGRAM) hs = true;
+    const Loc lc = loc[(uint64_t)lid * slot_ub + s];
+    gu8 *run = gl(pl->lists[lid].p) + (size_t)lc.unit * 6;
+    if (sr == -1) {  // getSiteRank / getLangId of the 12-byte run head
+      const uint32_t b0 = run[0], b6 = run[6], b7 = run[7];
+      sr = (int)(((b6 >> 5) | ((b7 & 1) << 3)) & 0x0f);
+      lang = (int)((b6 & 0x1f) | ((b0 & 0x08) ? 0x20 : 0));
+    }
+    // keys from the last 6-byte key down to the first one, then the head
+    // (Posdb.cpp:7851-7897); a body key weaker than the best ends the list
+    for (int k = (int)lc.len - 1; k >= 0; k--) {
+      if (k == 1) continue;  // second half of the 12-byte head
+      gu8 *dc = run + (size_t)k * 6;
+      const uint32_t hg = (dc[3] >> 2) & 0x0f;
+      if (hg == GB_HG_INLINKTEXT) return BoundCore{-1, 0.0f};
+      const float w = W.hashgroup[hg];
+      if (w < best) {
+        if (hg == GB_HG_BODY) break;
+        continue;
+      }
+      const unsigned dr = ((uint32_t)dc[1] >> 3) & 0x1f;
+      if (w > best) {
+        best = w;
+        bestDR = dr;
+        continue;
+      }
+      if (dr < bestDR) continue;
+      if (dr > bestDR) bestDR = dr;
+    }
+  }
+  if (best < 0) return BoundCore{0, 0.0f};
+  float score = 100.0;
+  score *= best;
+  score *= best;
+  score *= W.density[bestDR];
+  score *= W.density[bestDR];
+  if (hs) {
+    score *= GB_WIKI_BIGRAM_WEIGHT;
+    score *= GB_WIKI_BIGRAM_WEIGHT;
+  }
+  score *= (((float)sr) * pl->site_rank_multiplier + 1.0);
+  if (pl->language == lang || pl->language == 0 || lang == 0) score *= pl->same_lang_weight;
+  score *= pl->tfw[g];
+  return BoundCore{1, score};
+}
+
+// ring-buffer slots this wave's lanes write for one group's runs (value v);
+// returns the slot of the head of the group's last run (ourFirstPos)
+__device__ int ring_fill(const DevPlan *pl, int g, uint32_t s, uint32_t lm, const Loc *loc, uint64_t slot_ub,
+                         uint8_t *ring, uint8_t v, int lane) {
+  int first = -1;
+  const int gns = pl->gnsub[g];
+  for (int x = 0; x < gns; x++) {
+    const int lid = pl->gsub[g][x];
+    if (!(lm >> lid & 1)) continue;
+    const Loc lc = loc[(uint64_t)lid * slot_ub + s];
+    gu8 *run = gl(pl->lists[lid].p) + (size_t)lc.unit * 6;
+    for (uint32_t k = lane; k < lc.len; k += 64) {
+      if (k == 1) continue;
+      gu8 *kp = run + (size_t)k * 6;
+      const uint32_t wp = ((uint32_t)kp[2] | ((uint32_t)kp[3] << 8) | ((uint32_t)kp[4] << 16) |
+                           ((uint32_t)kp[5] << 24)) >> 14;
+      ring[wp & (RING - 1)] = v;
+    }
+    first = (int)((((uint32_t)run[2] | ((uint32_t)run[3] << 8) | ((uint32_t)run[4] << 16) |
+                    ((uint32_t)run[5] << 24)) >> 14) & (RING - 1));
+  }
+  return first;
+}
+
+// ordered summary of a stretch of ring slots holding the min group (type 0)
+// or the probed group (type 1): the closest different-type neighbours
+struct RingSum {
+  int fpos, ftype, lpos, ltype, gap, lastm;  // fpos < 0: nothing
+};
+__device__ __forceinline__ RingSum ring_join(RingSum a, RingSum b) {
+  if (a.fpos < 0) return RingSum{b.fpos, b.ftype, b.lpos, b.ltype, b.gap, b.lastm >= 0 ? b.lastm : a.lastm};
+  if (b.fpos < 0) return a;
+  RingSum r;
+  r.fpos = a.fpos;
+  r.ftype = a.ftype;
+  r.lpos = b.lpos;
+  r.ltype = b.ltype;
+  r.gap = min(a.gap, b.gap);
+  if (a.ltype != b.ftype) r.gap = min(r.gap, b.fpos - a.lpos);
+  r.lastm = b.lastm >= 0 ? b.lastm : a.lastm;
+  return r;
+}
+
+// Posdb.cpp:6445-6485 for group i: the smallest distance between a slot of
+// the min group and a slot of group i (scan order), and the wrap distance
+__device__ int32_t ring_best_dist(const uint8_t *ring, uint8_t m, uint8_t i, int ourFirstPos, int lane) {
+  RingSum r{-1, 0, -1, 0, 0x7fffffff, -1};
+  const uint32_t *w = reinterpret_cast<const uint32_t *>(ring) + lane * 16;
+  for (int q = 0; q < 16; q++) {
+    const uint32_t v4 = w[q];
+    if (v4 == 0xffffffffu) continue;
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+      const uint8_t v = (uint8_t)(v4 >> (8 * b));
+      if (v != m && v != i) continue;
+      const int pos = lane * 64 + q * 4 + b;
+      const int t = v == m ? 0 : 1;
+      if (r.fpos < 0) {
+        r.fpos = pos;
+        r.ftype = t;
+      } else if (t != r.ltype) {
+        r.gap = min(r.gap, pos - r.lpos);
+      }
+      r.lpos = pos;
+      r.ltype = t;
+      if (t == 0) r.lastm = pos;
+    }
+  }
+  // ordered reduction: lane l joins lane l+off, lane 0 ends with the whole ring
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    RingSum o;
+    o.fpos = __shfl_down(r.fpos, off, 64);
+    o.ftype = __shfl_down(r.ftype, off, 64);
+    o.lpos = __shfl_down(r.lpos, off, 64);
+    o.ltype = __shfl_down(r.ltype, off, 64);
+    o.gap = __shfl_down(r.gap, off, 64);
+    o.lastm = __shfl_down(r.lastm, off, 64);
+    if ((lane & (2 * off - 1)) == 0) r = ring_join(r, o);
+  }
+  int32_t bestDist = __shfl(r.gap, 0, 64);
+  const int hisLastPos = __shfl(r.lastm, 0, 64);
+  const int32_t wrapDist = ourFirstPos + (RING - hisLastPos);
+  if (wrapDist < bestDist) bestDist = wrapDist;
+  return bestDist;
+}
+
+__global__ void __launch_bounds__(64 * BND_WAVES) k_bound(const DevPlan *pl, const Counters *ctr, const uint32_t *surv,
+                                                       const uint32_t *surv_lm, const Loc *loc, uint64_t slot_ub,
+                                                       float *sbound) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_ring[BND_WAVES][RING];
+  stage_weights(&c_weights);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint8_t *ring = s_ring[wid];
+  const uint32_t nsurv = (uint32_t)(ctr->surv_top >> 36);
+  const int ng = pl->ngroups, m = pl->min_listi;
+  const float INF = __int_as_float(0x7f800000);
+  for (uint32_t i = blockIdx.x * BND_WAVES + wid; i < nsurv; i += gridDim.x * BND_WAVES) {
+    const uint32_t s = surv[i], lm = surv_lm[i];
+    // lane g: getMaxPossibleScore's scan of group g
+    BoundCore core{0, 0.0f};
+    if (lane < ng && !(pl->gflags0[lane] & (BF_NEGATIVE | BF_FACET)))
+      core = group_bound_core(pl, lane, s, lm, loc, slot_ub);
+    float B = INF;
+    // filter 1 (m_doMaxScoreAlgo): bestDist 0, qdist 0 (Posdb.cpp:6327-6346)
+    if (pl->do_max_score && lane < ng && !(pl->gflags0[lane] & (BF_NEGATIVE | BF_FACET))) {
+      const float v = max_score_tail(pl, core, 1.0f, 0, 0);
+      if (v != -1.0f) B = v;
+    }
+    // filter 2, the ring buffer (Posdb.cpp:6364-6504): the min group's word
+    // positions mod 4096, then each other group's over them in turn (the
+    // buffer is not cleared between groups)
+    {
+      uint4 *r4 = reinterpret_cast<uint4 *>(ring);
+      for (int q = lane; q < RING / 16; q += 64) r4[q] = make_uint4(~0u, ~0u, ~0u, ~0u);
+      wave_lds_sync();
+      const int ourFirstPos = ring_fill(pl, m, s, lm, loc, slot_ub, ring, (uint8_t)m, lane);
+      const float tfw_m = pl->tfw[m];
+      for (int g = 0; g < ng; g++) {
+        if (g == m || (pl->gflags0[g] & (BF_NEGATIVE | BF_FACET))) continue;
+        wave_lds_sync();
+        ring_fill(pl, g, s, lm, loc, slot_ub, ring, (uint8_t)g, lane);
+        wave_lds_sync();
+        BoundCore cg;
+        cg.state = __shfl(core.state, g, 64);
+        cg.base = __shfl(core.base, g, 64);
+        if (cg.state < 0) continue;  // -1: not applied
+        const int32_t bestDist = ring_best_dist(ring, (uint8_t)m, (uint8_t)g, ourFirstPos, lane);
+        const float v = max_score_tail(pl, cg, tfw_m, bestDist, pl->qpos[m] - pl->qpos[g]);
+        if (lane == 0 && v != -1.0f) B = fminf(B, v);
+      }
+      wave_lds_sync();
+    }
+    // min over the wave
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) B = fminf(B, __shfl_xor(B, off, 64));
+    if (lane == 0) sbound[i] = B;
+  }
+}
+
+// position of each survivor in docid order when the smallest group has
+// several candidate arrays (each array's survivors are docid-sorted and no
+// docid survives in two arrays: the probe credits it to the first)
+__device__ __forceinline__ uint32_t lower_bound_u32(const uint32_t *a, uint32_t n, uint32_t v) {
+  uint32_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (a[mid] < v) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+__device__ __forceinline__ uint32_t lower_bound_u64(const uint64_t *a, uint32_t lo, uint32_t hi, uint64_t v) {
+  const uint32_t b = lo;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (a[mid] < v) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo - b;
+}
+
+__global__ void k_rank(const DevPlan *pl, const Counters *ctr, const uint32_t *surv, const uint64_t *sdoc,
+                       uint32_t *order) {
+  const uint32_t nsurv = (uint32_t)(ctr->surv_top >> 36);
+  const int g0n = pl->g0n;
+  uint32_t sb[MAXG0 + 1];
+  for (int k = 0; k <= g0n; k++)
+    sb[k] = k == g0n ? nsurv : lower_bound_u32(surv, nsurv, (uint32_t)pl->g0base[k]);
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nsurv; i += gridDim.x * blockDim.x) {
+    int k = 0;
+    while (k + 1 < g0n && i >= sb[k + 1]) k++;
+    const uint64_t d = sdoc[i];
+    uint32_t pos = i - sb[k];
+    for (int k2 = 0; k2 < g0n; k2++)
+      if (k2 != k) pos += lower_bound_u64(sdoc, sb[k2], sb[k2 + 1], d);
+    order[pos] = i;
+  }
+}
+
+// TopTree state carried between the pieces of a docid-split query (Msg39's
+// one tree over every piece, Msg39.cpp:345-457)
+struct TreeState {
+  uint32_t n;
+  float vcount;
+  int32_t dom[256];
+  float score[TC];
+  uint64_t docid[TC];
+};
+
+struct TreeParams {
+  int32_t docs_wanted;  // m_docsWanted
+  int32_t cap;          // m_cap
+  float partial;        // m_partial
+  int32_t pad;
+  int64_t ridiculous;   // m_ridiculousMax
+  int64_t num_nodes;    // m_numNodes
+  uint32_t init, final; // first / last piece
+};
+
+__device__ __forceinline__ bool node_better(float s1, uint64_t d1, float s2, uint64_t d2) {
+  return s1 > s2 || (s1 == s2 && d1 < d2);
+}
+__device__ __forceinline__ uint32_t dom_hash8(uint64_t d) { return (uint32_t)((d & 0x3fc0ull) >> 6); }  // Titledb.h:114-115
+
+// index of the first node (best-first order) not better than (s, d)
+__device__ uint32_t tree_lower_bound(const float *ts, const uint64_t *td, uint32_t n, float s, uint64_t d, int lane) {
+  uint32_t lo = 0, hi = n;
+  while (hi - lo > 64) {
+    const uint32_t step = (hi - lo + 63) / 64;
+    const uint32_t idx = lo + lane * step;
+    const uint32_t c = (uint32_t)__popcll(__ballot(idx < hi && node_better(ts[idx], td[idx], s, d)));
+    if (c == 0) return lo;
+    const uint32_t nlo = lo + (c - 1) * step + 1;
+    hi = min(hi, lo + c * step);
+    lo = nlo;
+  }
+  const uint32_t idx = lo + lane;
+  return lo + (uint32_t)__popcll(__ballot(idx < hi && node_better(ts[idx], td[idx], s, d)));
+}
+
+// deleteNode's count bookkeeping (TopTree.cpp:543-547) and removal of node q
+__device__ void tree_delete(float *ts, uint64_t *td, int32_t *dom, uint32_t &n, float &vcount, const TreeParams &tp,
+                            uint32_t q, uint32_t dh, int lane) {
+  if (dom[dh] < tp.cap) vcount -= 1.0;
+  else if (dom[dh] == tp.cap) vcount -= tp.partial;
+  wave_lds_sync();
+  if (lane == 0) dom[dh]--;
+  for (uint32_t b = q; b + 1 < n; b += 64) {
+    const uint32_t idx = b + 1 + lane;
+    float v = 0.0f;
+    uint64_t w = 0;
+    if (idx < n) {
+      v = ts[idx];
+      w = td[idx];
+    }
+    wave_lds_sync();
+    if (idx < n) {
+      ts[idx - 1] = v;
+      td[idx - 1] = w;
+    }
+    wave_lds_sync();
+  }
+  n--;
+  wave_lds_sync();
+}
+
+// TopTree::addNode (TopTree.cpp:206-516) on the best-first node array; every
+// lane runs it (uniform), the array work is spread over the wave
+__device__ void tree_add(float *ts, uint64_t *td, int32_t *dom, uint32_t &n, float &vcount, const TreeParams &tp,
+                         float s, uint64_t d, uint32_t &err, int lane) {
+  const uint32_t dh = dom_hash8(d);
+  if (vcount >= tp.docs_wanted) {
+    if (!node_better(s, d, ts[n - 1], td[n - 1])) return;
+  }
+  const uint32_t p = tree_lower_bound(ts, td, n, s, d, lane);
+  if (p < n && ts[p] == s && td[p] == d) return;  // "if equal do not replace"
+  const uint32_t cs = (uint32_t)s;
+  bool del = false;
+  float delS = 0.0f;
+  uint64_t delD = 0;
+  if (dom[dh] >= tp.ridiculous) {
+    // m_domMinNode[domHash]: the domain's minimum m_t2 key (uint32 score, docid)
+    uint32_t mc = 0xffffffffu;
+    uint64_t md = ~0ull;
+    float ms = 0.0f;
+    for (uint32_t t = lane; t < n; t += 64) {
+      const uint64_t dt = td[t];
+      if (dom_hash8(dt) != dh) continue;
+      const uint32_t ct = (uint32_t)ts[t];
+      if (ct < mc || (ct == mc && dt < md)) {
+        mc = ct;
+        md = dt;
+        ms = ts[t];
+      }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const uint32_t oc = __shfl_xor(mc, off, 64);
+      const uint64_t od = __shfl_xor(md, off, 64);
+      const float os = __shfl_xor(ms, off, 64);
+      if (oc < mc || (oc == mc && od < md)) {
+        mc = oc;
+        md = od;
+        ms = os;
+      }
+    }
+    if (cs < mc || (cs == mc && d <= md)) return;  // k <= *m_t2.getKey(min)
+    del = true;
+    delS = ms;
+    delD = md;
+  }
+  if (n >= TC) {
+    err = 1;
+    return;
+  }
+  // insert at p
+  for (int64_t e = (int64_t)n; e > (int64_t)p; e -= 64) {
+    const int64_t idx = e - 64 + lane;
+    float v = 0.0f;
+    uint64_t w = 0;
+    const bool act = idx >= (int64_t)p && idx < (int64_t)n;
+    if (act) {
+      v = ts[idx];
+      w = td[idx];
+    }
+    wave_lds_sync();
+    if (act) {
+      ts[idx + 1] = v;
+      td[idx + 1] = w;
+    }
+    wave_lds_sync();
+  }
+  if (lane == 0) {
+    ts[p] = s;
+    td[p] = d;
+    dom[dh]++;
+  }
+  n++;
+  wave_lds_sync();
+  if (dom[dh] < tp.cap) vcount += 1.0;
+  else if (dom[dh] == tp.cap) vcount += tp.partial;
+  if (del) tree_delete(ts, td, dom, n, vcount, tp, tree_lower_bound(ts, td, n, delS, delD, lane), dh, lane);
+  while (n > 0 && (vcount - 1.0 >= tp.docs_wanted || (int64_t)n == tp.num_nodes))
+    tree_delete(ts, td, dom, n, vcount, tp, n - 1, dom_hash8(td[n - 1]), lane);
+}
+
+__device__ __forceinline__ float key_score(uint32_t key) {
+  return __uint_as_float((key & 0x80000000u) ? (key & 0x7fffffffu) : ~key);
+}
+
+// one wave: the docid-order loop of intersectLists10_r with the TopTree
+// (Posdb.cpp:6137-7706, minWinningScore per pass)
+__global__ void __launch_bounds__(64) k_tree_replay(Counters *ctr, const uint32_t *order, const uint32_t *skey,
+                                                    const uint64_t *sdoc, const uint8_t *sflag, const float *sbound,
+                                                    TreeState *T, TreeParams tp, uint32_t *out_key,
+                                                    uint64_t *out_doc) {
+  __shared__ float ts[TC];
+  __shared__ uint64_t td[TC];
+  __shared__ int32_t dom[256];
+  const int lane = threadIdx.x;
+  uint32_t n = 0;
+  float vcount = 0.0f;
+  if (tp.init) {
+    for (int q = lane; q < 256; q += 64) dom[q] = 0;
+  } else {
+    n = T->n;
+    vcount = T->vcount;
+    for (int q = lane; q < 256; q += 64) dom[q] = T->dom[q];
+    for (uint32_t q = lane; q < n; q += 64) {
+      ts[q] = T->score[q];
+      td[q] = T->docid[q];
+    }
+  }
+  wave_lds_sync();
+  const uint32_t ns = (uint32_t)(ctr->surv_top >> 36);
+  float mws = -1.0f;  // minWinningScore, Posdb.cpp:6012
+  bool called = false;
+  uint32_t filtered = 0, err = 0;
+  for (uint32_t base = 0; base < ns && !err;) {
+    const uint32_t pidx = base + lane;
+    const bool valid = pidx < ns;
+    const uint32_t i = valid ? (order ? order[pidx] : pidx) : 0;
+    const uint32_t key = valid ? skey[i] : 0;
+    const bool serp = valid && sflag[i];
+    const float B = valid ? sbound[i] : 0.0f;
+    const uint64_t d = valid ? sdoc[i] : 0;
+    const float sc = key_score(key);
+    const bool live = valid && !(B <= mws);  // not skipped by the prefilters
+    const bool ok = live && key != 0;        // scored, not filtered by paging
+    const bool full = vcount >= tp.docs_wanted;
+    const bool rej = called && full && n > 0 && !node_better(sc, d, ts[n - 1], td[n - 1]);
+    const uint64_t slow = __ballot(ok && !rej);
+    const int j = slow ? __ffsll((unsigned long long)slow) - 1 : 64;
+    const uint64_t below = j >= 64 ? ~0ull : ((1ull << j) - 1);
+    filtered += (uint32_t)__popcll(__ballot(live && serp) & below);
+    if (!slow) {
+      base += 64;
+      continue;
+    }
+    const float s = __shfl(sc, j, 64);
+    const uint64_t dd = __shfl(d, j, 64);
+    tree_add(ts, td, dom, n, vcount, tp, s, dd, err, lane);
+    called = true;
+    if (n > (uint32_t)tp.docs_wanted) mws = ts[n - 1];  // Posdb.cpp:7699-7704
+    base += (uint32_t)j + 1;
+  }
+  if (lane == 0) {
+    ctr->filtered = filtered;
+    if (err) ctr->tree_err = 1;
+  }
+  if (tp.final) {
+    for (uint32_t q = lane; q < n; q += 64) {
+      const uint32_t b = __float_as_uint(ts[q]);
+      uint32_t k = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+      out_key[q] = k ? k : 1u;
+      out_doc[q] = td[q];
+    }
+    if (lane == 0) {
+      if (n < TC) out_key[n] = 0;
+      ctr->tree_n = n;
+    }
+  } else {
+    for (uint32_t q = lane; q < n; q += 64) {
+      T->score[q] = ts[q];
+      T->docid[q] = td[q];
+    }
+    for (int q = lane; q < 256; q += 64) T->dom[q] = dom[q];
+    if (lane == 0) {
+      T->n = n;
+      T->vcount = vcount;
+    }
   }
 }
 
@@ -1340,13 +1968,51 @@ struct DevBuf {
   }
 };
 
+// Device memory of one resident list.  Shared by the list table and every
+// query in flight that reads it: gbgpu_list_free drops the table's reference,
+// and the memory goes when the last in-flight query holding it is collected.
+struct ListMem {
+  uint8_t *d = nullptr;
+  ~ListMem() {
+    if (d) (void)hipFree(d);
+  }
+};
+
 struct ListEntry {
   uint8_t *d = nullptr;
+  std::shared_ptr<ListMem> mem;  // owner of d (null for docid-split windows)
   int64_t size = 0;   // original bytes (18-byte first key)
   uint32_t units = 0; // swapped units
   uint64_t dmin = 0, dmax = 0;  // docid of the first and of the last run
   bool live = false;
 };
+
+// Upload-time check of a swapped list's unit structure.  A valid list
+// classifies every unit independently (Posdb.h:887-889): a unit with the
+// half bit (byte1 & 0x02) starts a key, and a key start is either a 12-byte
+// run head (byte0 & 0x06 == 0x02), which the next unit (its docid half,
+// whose byte-1 bit is the mandatory zero, Posdb.cpp:410-412) must follow, or
+// a 6-byte key (byte0 & 0x04).  A key start with neither compression bit is
+// an 18-byte key inside the list -- the corruption intersectLists10_r bails
+// on (Posdb.cpp:6289-6302); a run head followed by a key start, or ending the
+// list, is a truncated key.  Either sets *bad, so no scan kernel ever sees a
+// list whose run count could exceed units/2 (the sizing of every run buffer).
+__global__ void k_validate(const uint8_t *list, uint32_t units, uint32_t *bad) {
+  gu8 *p = gl(list);
+  uint32_t b = 0;
+  for (uint32_t u = blockIdx.x * blockDim.x + threadIdx.x; u < units; u += gridDim.x * blockDim.x) {
+    const uint8_t b0 = p[(size_t)u * 6], b1 = p[(size_t)u * 6 + 1];
+    if (!(b1 & 0x02)) {
+      if (u == 0) b = 1;  // the list must start with a key
+      continue;
+    }
+    if (!(b0 & 0x06)) b = 1;
+    if (!(b0 & 0x04)) {
+      if (u + 1 >= units || (p[(size_t)(u + 1) * 6 + 1] & 0x02)) b = 1;
+    }
+  }
+  if (__ballot(b) && (threadIdx.x & 63) == 0) atomicOr(bad, 1u);
+}
 
 // docid of the key starting at p (Posdb.h:295)
 static uint64_t host_docid(const uint8_t *p) {
@@ -1370,6 +2036,7 @@ struct QuerySlot {
   DevBuf tables, chunkcnt, cand, lmask, ulen, loc, surv, survoff, survlm, scratch, skey, sdoc, sel, gath, res;
   DevBuf dir;           // candidate directories, epoch-tagged (never cleared per query)
   DevBuf split, swin;   // docid splits: one piece's list windows; window table
+  DevBuf blk, sflag, sbound, order, tree;  // site clustering: ordered compaction, bounds, TopTree state
   uint32_t epoch = 0;
   uint8_t *h_stage = nullptr;  // pinned: query tables (host -> device, one copy)
   size_t stage_cap = 0;
@@ -1378,8 +2045,11 @@ struct QuerySlot {
   std::vector<G0Chunk> g0c;
   std::vector<ProbeWork> pw;
   std::vector<uint32_t> afirst;
+  std::vector<std::shared_ptr<ListMem>> held;  // lists the in-flight query reads
   // state of the in-flight query
   bool pending = false;
+  bool replayed = false;  // site clustering: the pass ran the TopTree replay
+  uint64_t slot_ub = 0;
   bool early = false;
   int k = 0;
   size_t res_bytes = 0;
@@ -1397,7 +2067,8 @@ struct QuerySlot {
   void release() {
     if (stream) (void)hipStreamSynchronize(stream);
     DevBuf *bufs[] = {&tables, &chunkcnt, &cand, &lmask, &ulen, &loc, &surv, &survoff, &survlm,
-                      &scratch, &skey, &sdoc, &sel, &gath, &res, &dir, &split, &swin};
+                      &scratch, &skey, &sdoc, &sel, &gath, &res, &dir, &split, &swin,
+                      &blk, &sflag, &sbound, &order, &tree};
     for (auto *b : bufs) b->release();
     if (h_stage) (void)hipHostFree(h_stage);
     if (h_res) (void)hipHostFree(h_res);
@@ -1414,6 +2085,10 @@ constexpr int MAX_SLOTS = 64;
 struct gbgpu_ctx {
   int device = 0;
   hipStream_t upload_stream = nullptr;
+  uint32_t *d_flag = nullptr;  // upload validation result (device / pinned host)
+  uint32_t *h_flag = nullptr;
+  std::mutex free_mu;          // a slot became free (gbgpu_query_resident waits on it)
+  std::condition_variable free_cv;
   std::mutex lists_mu;
   std::vector<ListEntry> lists;
   std::mutex slots_mu;  // guards growth of the slot table
@@ -1434,12 +2109,16 @@ static size_t res_size(int k) { return res_docs_off(k) + 8 * (size_t)std::max(k,
 static int upload_list(gbgpu_ctx *ctx, const uint8_t *bytes, int64_t size, int32_t *handle) {
   if (size < 0 || (size > 0 && size < 18) || (size > 0 && (size - 18) % 6 != 0)) return EINVAL;
   if ((size - 6) / 6 > 0xfffffff0LL) return GBGPU_ECAPACITY;
+  // the first key must be a whole 18-byte key (Posdb.cpp:5671-5703 swaps it)
+  if (size > 0 && (bytes[0] & 0x06)) return GBGPU_ECORRUPT;
   ListEntry e;
   e.size = size;
   e.units = size ? (uint32_t)((size - 6) / 6) : 0;
   size_t alloc = (size_t)(size ? size - 6 : 0) + LIST_PAD;
   alloc = align256(alloc);
-  if (hipMalloc(&e.d, alloc) != hipSuccess) return ENOMEM;
+  e.mem = std::make_shared<ListMem>();
+  if (hipMalloc(&e.mem->d, alloc) != hipSuccess) return ENOMEM;
+  e.d = e.mem->d;
   HIPCHECK(hipMemsetAsync(e.d, 0, alloc, ctx->upload_stream));
   if (size) {
     // device image = the list after the first-key swap (Posdb.cpp:5689-5698):
@@ -1450,8 +2129,15 @@ static int upload_list(gbgpu_ctx *ctx, const uint8_t *bytes, int64_t size, int32
     HIPCHECK(hipMemcpyAsync(e.d, first, 12, hipMemcpyHostToDevice, ctx->upload_stream));
     if (size > 18)
       HIPCHECK(hipMemcpyAsync(e.d + 12, bytes + 18, (size_t)(size - 18), hipMemcpyHostToDevice, ctx->upload_stream));
+    HIPCHECK(hipMemsetAsync(ctx->d_flag, 0, 4, ctx->upload_stream));
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(4096, (e.units + 255) / 256);
+    hipLaunchKernelGGL(k_validate, dim3(std::max(grid, 1u)), dim3(256), 0, ctx->upload_stream, e.d, e.units,
+                       ctx->d_flag);
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipMemcpyAsync(ctx->h_flag, ctx->d_flag, 4, hipMemcpyDeviceToHost, ctx->upload_stream));
   }
   HIPCHECK(hipStreamSynchronize(ctx->upload_stream));
+  if (size && *ctx->h_flag) return GBGPU_ECORRUPT;  // e.mem frees the copy
   if (size) {
     // the list's docid range (directory sizing): first key, last run start
     e.dmin = e.dmax = host_docid(bytes);
@@ -1480,7 +2166,6 @@ static int upload_list(gbgpu_ctx *ctx, const uint8_t *bytes, int64_t size, int32
 static int snapshot_lists(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms, const int32_t *handles,
                           const gbgpu_params *p, std::vector<ListEntry> &ents) {
   if (!p || nterms < 0 || (nterms && (!terms || !handles))) return EINVAL;
-  if (p->site_clustering) return GBGPU_EUNSUPPORTED;
   if (p->docs_to_get <= 0 || p->real_max_top <= 0 || p->num_docid_splits <= 0) return EINVAL;
   if (nterms > 1024) return GBGPU_EUNSUPPORTED;
   ents.resize(nterms);
@@ -1494,8 +2179,13 @@ static int snapshot_lists(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms, 
   return 0;
 }
 
+// site clustering: which part of Msg39's one-tree-over-all-pieces a pass is
+constexpr int TREE_INIT = 1;   // the pass starts the TopTree
+constexpr int TREE_FINAL = 2;  // the pass ends it: the tree is the result
+
 static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *terms, int nterms,
-                           const ListEntry *ents, const gbgpu_params *p, int32_t dw_override);
+                           const ListEntry *ents, const gbgpu_params *p, int32_t dw_override,
+                           int tree_phase = TREE_INIT | TREE_FINAL);
 
 // One whole-range query (no docid splits) on slot q's stream.
 static int enqueue(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *terms, int nterms, const int32_t *handles,
@@ -1504,30 +2194,89 @@ static int enqueue(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *terms, int n
   int rc = snapshot_lists(ctx, terms, nterms, handles, p, ents);
   if (rc) return rc;
   if (p->num_docid_splits > 1) return GBGPU_EUNSUPPORTED;  // blocking entry points only
-  return enqueue_entries(ctx, q, terms, nterms, ents.data(), p, 0);
+  rc = enqueue_entries(ctx, q, terms, nterms, ents.data(), p, 0);
+  if (!rc)
+    for (auto &e : ents)
+      if (e.mem) q.held.push_back(e.mem);
+  return rc;
 }
 
 // One PosdbTable pass over the given lists on slot q's stream.  dw_override
 // > 0 fixes TopTree::m_docsWanted (docid splits size the tree once, at the
 // first piece: Msg39.cpp:938-966).
+// TopTree::setNumNodes' sizing (TopTree.cpp:64-101) for the replay
+static TreeParams tree_params(int32_t dw, int phase) {
+  TreeParams tp;
+  std::memset(&tp, 0, sizeof tp);
+  tp.docs_wanted = dw;
+  int64_t rmax = std::max<int64_t>(50, (int64_t)dw * 2);
+  tp.ridiculous = rmax;
+  tp.num_nodes = tree_nodes(dw, true);
+  tp.cap = std::max(2, dw / 50);
+  tp.partial = (float)(dw % 50) / 50.0;
+  tp.init = (phase & TREE_INIT) ? 1 : 0;
+  tp.final = (phase & TREE_FINAL) ? 1 : 0;
+  return tp;
+}
+
+// result block of a clustering query: up to TC nodes
+static int ensure_result(QuerySlot &q) {
+  q.res_bytes = res_size(q.k);
+  if (q.res.ensure(q.res_bytes)) return ENOMEM;
+  if (q.res_bytes > q.hres_cap) {
+    if (q.h_res) (void)hipHostFree(q.h_res);
+    q.h_res = nullptr;
+    q.hres_cap = 0;
+    HIPCHECK(hipHostMalloc((void **)&q.h_res, q.res_bytes));
+    q.hres_cap = q.res_bytes;
+  }
+  return 0;
+}
+
+// The last piece of a docid-split clustering query scored nothing: the tree
+// the earlier pieces left is the result (no survivors to replay).
+static int enqueue_tree_emit(QuerySlot &q, int32_t dw) {
+  q.k = TC;
+  q.docs_wanted = dw;
+  q.early = false;
+  q.scan_bytes = 0;
+  q.slot_ub = 0;
+  int rc = ensure_result(q);
+  if (rc) return rc;
+  hipStream_t st = q.stream;
+  Counters *dctr = q.res.as<Counters>();
+  hipLaunchKernelGGL(k_reset, dim3(1), dim3(BLOCK), 0, st, reinterpret_cast<uint32_t *>(dctr),
+                     (uint32_t)(sizeof(Counters) / 4), reinterpret_cast<uint32_t *>(dctr), 0u);
+  hipLaunchKernelGGL(k_tree_replay, dim3(1), dim3(64), 0, st, dctr, (const uint32_t *)nullptr,
+                     (const uint32_t *)nullptr, (const uint64_t *)nullptr, (const uint8_t *)nullptr,
+                     (const float *)nullptr, q.tree.as<TreeState>(), tree_params(dw, TREE_FINAL),
+                     q.res.as<uint32_t>(res_keys_off()), q.res.as<uint64_t>(res_docs_off(q.k)));
+  HIPCHECK(hipGetLastError());
+  HIPCHECK(hipMemcpyAsync(q.h_res, q.res.p, q.res_bytes, hipMemcpyDeviceToHost, st));
+  q.pending = true;
+  return 0;
+}
+
 static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *terms, int nterms,
-                           const ListEntry *ents, const gbgpu_params *p, int32_t dw_override) {
+                           const ListEntry *ents, const gbgpu_params *p, int32_t dw_override, int tree_phase) {
   std::vector<int64_t> sizes(nterms);
   for (int i = 0; i < nterms; i++) sizes[i] = ents[i].size;
   HostPlan hp;
   int rc = build_host_plan(terms, nterms, sizes.data(), p, &hp);
   if (rc) return rc;
   if (dw_override > 0) hp.docs_wanted = dw_override;
+  const bool clus = p->site_clustering != 0;
   q.docs_wanted = hp.docs_wanted;
-  q.k = hp.docs_wanted;
+  q.k = clus ? TC : hp.docs_wanted;
   q.early = (hp.ngroups == 0 || hp.min_list_size == 0);
   q.scan_bytes = 0;
+  q.replayed = false;
   if (q.early) {
     q.pending = true;
     return 0;
   }
   if (hp.ngroups > MAXG) return GBGPU_EUNSUPPORTED;
-  if (q.k > MAX_K) return GBGPU_EUNSUPPORTED;
+  if (!clus && q.k > MAX_K) return GBGPU_EUNSUPPORTED;
 
   // ---- query tables, built straight into the pinned staging buffer
   // layout: [DevPlan | G0Chunk[] | afirst[MAXG0] | ProbeWork[]]
@@ -1539,6 +2288,19 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   P.same_lang_weight = p->same_lang_weight;
   P.site_rank_multiplier = GB_SITERANKMULTIPLIER;
   P.nqt = nterms;
+  P.has_serp = p->min_serp_docid != 0;  // Posdb.cpp:4379-4381
+  P.max_serp_score = p->max_serp_score;
+  P.min_serp_docid = p->min_serp_docid;
+  P.clustering = clus;
+  P.do_max_score = p->do_max_score_algo != 0;
+  P.min_listi = hp.min_listi;
+  P.all_same_wiki = 1;  // m_allInSameWikiPhrase, Posdb.cpp:5764-5778
+  for (int j = 0; j < hp.ngroups; j++) {
+    if (hp.g[j].flags[0] & (BF_NEGATIVE | BF_NUMBER | BF_FACET)) continue;
+    if (hp.g[j].wiki == 1) continue;
+    P.all_same_wiki = 0;
+    break;
+  }
   int dense[1024];
   uint64_t list_dmin[MAXL], list_dmax[MAXL];
   for (int i = 0; i < nterms; i++) dense[i] = -1;
@@ -1593,6 +2355,7 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   P.g0base[P.g0n] = slot;
   const uint64_t slot_ub = slot;
   if (slot_ub >= (1ull << 28)) return GBGPU_ECAPACITY;  // k_compact's packed bump pointer
+  q.slot_ub = slot_ub;
   // directories: about 8 units (2-4 docids) per bucket, power-of-two count
   uint64_t dir_entries = 0;
   for (int a = 0; a < P.g0n; a++) {
@@ -1673,6 +2436,13 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   rc2 |= q.sel.ensure(sizeof(Select));
   rc2 |= q.gath.ensure(12 * (slot_ub + MAX_K) + 1024);
   rc2 |= q.res.ensure(q.res_bytes);
+  if (clus) {
+    rc2 |= q.blk.ensure(sizeof(BlkTot) * (size_t)std::max<uint64_t>(1, (slot_ub + CTILE - 1) / CTILE));
+    rc2 |= q.sflag.ensure(slot_ub);
+    rc2 |= q.sbound.ensure(4 * slot_ub);
+    if (P.g0n > 1) rc2 |= q.order.ensure(4 * slot_ub);
+    if (!(tree_phase & TREE_FINAL)) rc2 |= q.tree.ensure(sizeof(TreeState));
+  }
   const void *dir_before = q.dir.p;
   rc2 |= q.dir.ensure(8 * std::max<uint64_t>(1, dir_entries));
   if (rc2) return ENOMEM;
@@ -1738,9 +2508,19 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
                        q.dir.as<uint64_t>());
   }
   if (ctx->profiling) HIPCHECK(hipEventRecord(q.ev[2], st));
-  const uint32_t cgrid = (uint32_t)((slot_ub + CTILE - 1) / CTILE);
-  hipLaunchKernelGGL(k_compact, dim3(std::max(cgrid, 1u)), dim3(BLOCK), 0, st, dpl, lmask, q.ulen.as<uint32_t>(), slot_ub, dctr,
-                     q.surv.as<uint32_t>(), q.survoff.as<unsigned long long>(), q.survlm.as<uint32_t>());
+  const uint32_t cgrid = std::max(1u, (uint32_t)((slot_ub + CTILE - 1) / CTILE));
+  if (!P.clustering) {
+    hipLaunchKernelGGL(k_compact<0>, dim3(cgrid), dim3(BLOCK), 0, st, dpl, lmask, q.ulen.as<uint32_t>(), slot_ub,
+                       dctr, q.surv.as<uint32_t>(), q.survoff.as<unsigned long long>(), q.survlm.as<uint32_t>(),
+                       (BlkTot *)nullptr);
+  } else {
+    BlkTot *blk = q.blk.as<BlkTot>();
+    hipLaunchKernelGGL(k_compact<1>, dim3(cgrid), dim3(BLOCK), 0, st, dpl, lmask, q.ulen.as<uint32_t>(), slot_ub,
+                       dctr, q.surv.as<uint32_t>(), q.survoff.as<unsigned long long>(), q.survlm.as<uint32_t>(), blk);
+    hipLaunchKernelGGL(k_compact_scan, dim3(1), dim3(1024), 0, st, cgrid, blk, dctr);
+    hipLaunchKernelGGL(k_compact<2>, dim3(cgrid), dim3(BLOCK), 0, st, dpl, lmask, q.ulen.as<uint32_t>(), slot_ub,
+                       dctr, q.surv.as<uint32_t>(), q.survoff.as<unsigned long long>(), q.survlm.as<uint32_t>(), blk);
+  }
   if (ctx->profiling) HIPCHECK(hipEventRecord(q.ev[3], st));
   {
     int maxsub = 0;
@@ -1751,7 +2531,7 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
       hipLaunchKernelGGL(kern, dim3(grid), dim3(SCORE_TPB), 0, st, dpl, q.cand.as<uint64_t>(), dctr,
                          q.surv.as<uint32_t>(), q.survlm.as<uint32_t>(), q.survoff.as<unsigned long long>(),
                          loc, slot_ub, q.scratch.as<uint64_t>(), q.skey.as<uint32_t>(),
-                         q.sdoc.as<uint64_t>(), ctx->score_mode);
+                         q.sdoc.as<uint64_t>(), q.sflag.as<uint8_t>(), ctx->score_mode);
     };
     if (hp.ngroups <= 2 && maxsub <= 4) launch(k_score<2, 4>);
     else if (hp.ngroups <= 4 && maxsub <= 4) launch(k_score<4, 4>);
@@ -1759,6 +2539,30 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
     else launch(k_score<MAXG, MAXSUB>);
   }
   if (ctx->profiling) HIPCHECK(hipEventRecord(q.ev[4], st));
+  if (clus) {
+    // site clustering: prefilter bounds, docid order, the TopTree replay
+    const uint32_t bgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((slot_ub + BND_WAVES - 1) / BND_WAVES, 4096));
+    hipLaunchKernelGGL(k_bound, dim3(bgrid), dim3(64 * BND_WAVES), 0, st, dpl, dctr, q.surv.as<uint32_t>(),
+                       q.survlm.as<uint32_t>(), loc, slot_ub, q.sbound.as<float>());
+    const uint32_t *order = nullptr;
+    if (P.g0n > 1) {
+      const uint32_t rgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((slot_ub + 255) / 256, 4096));
+      hipLaunchKernelGGL(k_rank, dim3(rgrid), dim3(256), 0, st, dpl, dctr, q.surv.as<uint32_t>(),
+                         q.sdoc.as<uint64_t>(), q.order.as<uint32_t>());
+      order = q.order.as<uint32_t>();
+    }
+    hipLaunchKernelGGL(k_tree_replay, dim3(1), dim3(64), 0, st, dctr, order, q.skey.as<uint32_t>(),
+                       q.sdoc.as<uint64_t>(), q.sflag.as<uint8_t>(), q.sbound.as<float>(),
+                       (tree_phase & TREE_FINAL) ? (TreeState *)q.tree.p : q.tree.as<TreeState>(),
+                       tree_params(q.docs_wanted, tree_phase), q.res.as<uint32_t>(res_keys_off()),
+                       q.res.as<uint64_t>(res_docs_off(k)));
+    q.replayed = true;
+    if (ctx->profiling) HIPCHECK(hipEventRecord(q.ev[5], st));
+    HIPCHECK(hipMemcpyAsync(q.h_res, q.res.p, q.res_bytes, hipMemcpyDeviceToHost, st));
+    if (ctx->profiling) HIPCHECK(hipEventRecord(q.ev[6], st));
+    q.pending = true;
+    return 0;
+  }
   // top-k: radix select over the survivors' keys, then one LDS sort
   const uint32_t hgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(64, (slot_ub + 4095) / 4096));
   const uint32_t *skey = q.skey.as<uint32_t>();
@@ -1784,15 +2588,54 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   return 0;
 }
 
-static int collect(gbgpu_ctx *ctx, QuerySlot &q, gbgpu_result *out) {
+// the sorted intersected docid set of the slot's last query (its vote buffer)
+static int fetch_hits(QuerySlot &q, uint32_t nsurv, std::vector<int64_t> &out) {
+  const size_t base = out.size();
+  if (!nsurv) return 0;
+  out.resize(base + nsurv);
+  uint64_t *tmp = q.gath.as<uint64_t>();  // >= 8 * slot_ub bytes; free after the query
+  hipLaunchKernelGGL(k_gather_hits, dim3(std::min<uint32_t>(1024, (nsurv + 255) / 256)), dim3(256), 0, q.stream,
+                     q.surv.as<uint32_t>(), q.cand.as<uint64_t>(), nsurv, tmp);
+  HIPCHECK(hipGetLastError());
+  HIPCHECK(hipMemcpyAsync(out.data() + base, tmp, 8 * (size_t)nsurv, hipMemcpyDeviceToHost, q.stream));
+  HIPCHECK(hipStreamSynchronize(q.stream));
+  std::sort(out.begin() + base, out.end());
+  return 0;
+}
+
+static void write_hits(const std::vector<int64_t> &h, gbgpu_result *out) {
+  out->n_hit_docids = 0;
+  if (!out->hit_docids) return;
+  const int64_t n = std::min<int64_t>((int64_t)h.size(), std::max<int64_t>(0, out->hit_capacity));
+  if (n) std::memcpy(out->hit_docids, h.data(), 8 * (size_t)n);
+  out->n_hit_docids = n;
+}
+
+static void slot_released(gbgpu_ctx *ctx) {
+  { std::lock_guard<std::mutex> g(ctx->free_mu); }
+  ctx->free_cv.notify_all();
+}
+
+// hits_acc: when non-null, the query's intersected docids are appended to it
+// (docid splits gather them over the pieces) instead of being written to out
+static int collect(gbgpu_ctx *ctx, QuerySlot &q, gbgpu_result *out, std::vector<int64_t> *hits_acc = nullptr) {
   if (!q.pending) return EINVAL;
   q.pending = false;
   out->n = 0;
   out->hits = 0;
   out->filtered = 0;
+  out->n_hit_docids = 0;
   out->docs_wanted = q.docs_wanted;
-  if (q.early) return 0;
-  HIPCHECK(hipStreamSynchronize(q.stream));
+  if (q.early) {
+    q.held.clear();
+    return 0;
+  }
+  const hipError_t se = hipStreamSynchronize(q.stream);
+  q.held.clear();  // the lists may go now (gbgpu_list_free while in flight)
+  if (se != hipSuccess) {
+    std::fprintf(stderr, "gbgpu: query stream failed: %s\n", hipGetErrorString(se));
+    return GBGPU_EHIP;
+  }
   if (ctx->profiling) {
     float t;
     (void)hipEventElapsedTime(&t, q.ev[0], q.ev[6]);
@@ -1806,6 +2649,16 @@ static int collect(gbgpu_ctx *ctx, QuerySlot &q, gbgpu_result *out) {
   const uint32_t *keys = reinterpret_cast<const uint32_t *>(q.h_res + res_keys_off());
   const uint64_t *docs = reinterpret_cast<const uint64_t *>(q.h_res + res_docs_off(q.k));
   out->hits = (int64_t)(c->surv_top >> 36);
+  out->filtered = (int32_t)c->filtered;
+  if (c->corrupt) return GBGPU_ECORRUPT;
+  if (c->tree_err) return GBGPU_ECAPACITY;
+  if (hits_acc || out->hit_docids) {
+    std::vector<int64_t> local;
+    std::vector<int64_t> &h = hits_acc ? *hits_acc : local;
+    int rc = fetch_hits(q, (uint32_t)out->hits, h);
+    if (rc) return rc;
+    if (!hits_acc) write_hits(h, out);
+  }
   int n = 0;
   for (int i = 0; i < q.k && n < out->capacity; i++) {
     const uint32_t key = keys[i];
@@ -1885,6 +2738,9 @@ static int query_splits(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *terms, 
   std::vector<size_t> off(nl);
   std::vector<int64_t> td;
   std::vector<float> ts;
+  std::vector<int64_t> hit_ids;
+  const bool clus = p->site_clustering != 0;
+  bool tree_started = false, emitted = false;
   for (int j = 0; j < ns; j++) {
     size_t total = 0;
     for (int i = 0; i < nl; i++) {
@@ -1908,27 +2764,42 @@ static int query_splits(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *terms, 
         HIPCHECK(hipMemcpyAsync(e.d, ents[i].d + (size_t)w.lo * 6, (size_t)n * 6, hipMemcpyDeviceToDevice, q.stream));
       we[i] = e;
     }
-    if (j == 0) {
+    if (dw == 0) {
+      // allocTopTree at the first piece whose lists are not all empty; until
+      // then Msg39 skips the pieces (Msg39.cpp:938-948, Posdb.cpp:890-891)
       std::vector<int64_t> sz(nl);
       for (int i = 0; i < nl; i++) sz[i] = we[i].size;
       dw = docs_wanted(p, sz.data(), nl);
+      if (dw == 0) continue;
     }
-    int rc = enqueue_entries(ctx, q, terms, nterms, we.data(), p, dw);
+    const int phase = clus ? ((tree_started ? 0 : TREE_INIT) | (j == ns - 1 ? TREE_FINAL : 0)) : (TREE_INIT | TREE_FINAL);
+    int rc = enqueue_entries(ctx, q, terms, nterms, we.data(), p, dw, phase);
     if (rc) {
       q.pending = false;
       return rc;
     }
-    td.assign(std::max(dw, 1), 0);
-    ts.assign(std::max(dw, 1), 0.f);
+    const bool replayed = q.replayed;
+    if (replayed) tree_started = true;
+    const int cap = clus ? TC : dw;
+    td.assign(std::max(cap, 1), 0);
+    ts.assign(std::max(cap, 1), 0.f);
     gbgpu_result r;
     std::memset(&r, 0, sizeof r);
     r.docids = td.data();
     r.scores = ts.data();
-    r.capacity = dw;
-    rc = collect(ctx, q, &r);
+    r.capacity = cap;
+    rc = collect(ctx, q, &r, out->hit_docids ? &hit_ids : nullptr);
     if (rc) return rc;
     hits += r.hits;
     filtered += r.filtered;
+    if (clus) {
+      // one TopTree over every piece, carried on the device between them
+      if (replayed && (phase & TREE_FINAL)) {
+        emitted = true;
+        for (int x = 0; x < r.n; x++) top.push_back({ts[x], td[x]});
+      }
+      continue;
+    }
     for (int x = 0; x < r.n; x++) top.push_back({ts[x], td[x]});
     std::sort(top.begin(), top.end(), [](const std::pair<float, int64_t> &a, const std::pair<float, int64_t> &b) {
       return a.first > b.first || (a.first == b.first && a.second < b.second);
@@ -1941,9 +2812,33 @@ static int query_splits(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *terms, 
               top.end());
     if ((int32_t)top.size() > dw) top.resize(dw);
   }
+  if (clus && tree_started && !emitted) {
+    // the last piece scored nothing: the tree as the earlier pieces left it
+    int rc = enqueue_tree_emit(q, dw);
+    if (rc) {
+      q.pending = false;
+      return rc;
+    }
+    td.assign(TC, 0);
+    ts.assign(TC, 0.f);
+    gbgpu_result r;
+    std::memset(&r, 0, sizeof r);
+    r.docids = td.data();
+    r.scores = ts.data();
+    r.capacity = TC;
+    rc = collect(ctx, q, &r);
+    if (rc) return rc;
+    for (int x = 0; x < r.n; x++) top.push_back({ts[x], td[x]});
+  }
   out->hits = hits;
   out->filtered = filtered;
   out->docs_wanted = dw;
+  if (out->hit_docids) {
+    // pieces overlap by two docids (getLists' [d0, d1+2]): the set has each once
+    std::sort(hit_ids.begin(), hit_ids.end());
+    hit_ids.erase(std::unique(hit_ids.begin(), hit_ids.end()), hit_ids.end());
+    write_hits(hit_ids, out);
+  }
   int n = 0;
   for (const auto &t : top) {
     if (n >= out->capacity) break;
@@ -2004,6 +2899,8 @@ int gbgpu_open(int device, gbgpu_ctx **out) {
   ctx->device = device;
   Weights w = host_weights();
   if (hipStreamCreateWithFlags(&ctx->upload_stream, hipStreamNonBlocking) != hipSuccess ||
+      hipMalloc((void **)&ctx->d_flag, 4) != hipSuccess ||
+      hipHostMalloc((void **)&ctx->h_flag, 4) != hipSuccess ||
       hipMemcpyToSymbol(HIP_SYMBOL(c_weights), &w, sizeof w) != hipSuccess || grow_slots(ctx, 1) != 0) {
     gbgpu_close(ctx);
     return GBGPU_EHIP;
@@ -2021,9 +2918,10 @@ void gbgpu_close(gbgpu_ctx *ctx) {
     ctx->slots[i]->release();
     delete ctx->slots[i];
   }
-  for (auto &e : ctx->lists)
-    if (e.live) (void)hipFree(e.d);
+  ctx->lists.clear();  // the last references: ListMem frees the device copies
   gbmerge::state_free(ctx->merge);
+  if (ctx->d_flag) (void)hipFree(ctx->d_flag);
+  if (ctx->h_flag) (void)hipHostFree(ctx->h_flag);
   if (ctx->upload_stream) (void)hipStreamDestroy(ctx->upload_stream);
   delete ctx;
 }
@@ -2045,6 +2943,13 @@ int32_t gbgpu_docs_wanted(const gbgpu_params *p, const int64_t *sizes, int nterm
   return docs_wanted(p, sizes, nterms);
 }
 
+int32_t gbgpu_tree_capacity(const gbgpu_params *p, const int64_t *sizes, int nterms) {
+  if (!p || (nterms && !sizes)) return 0;
+  const int32_t dw = docs_wanted(p, sizes, nterms);
+  if (!p->site_clustering) return dw;
+  return (int32_t)std::min<int64_t>(tree_nodes(dw, true), TREE_CAP);
+}
+
 int gbgpu_list_upload(gbgpu_ctx *ctx, const uint8_t *bytes, int64_t size, int32_t *handle) {
   if (!ctx || !handle || (size > 0 && !bytes)) return EINVAL;
   std::lock_guard<std::mutex> g(ctx->lists_mu);
@@ -2054,13 +2959,17 @@ int gbgpu_list_upload(gbgpu_ctx *ctx, const uint8_t *bytes, int64_t size, int32_
 
 int gbgpu_list_free(gbgpu_ctx *ctx, int32_t h) {
   if (!ctx) return EINVAL;
-  std::lock_guard<std::mutex> g(ctx->lists_mu);
-  if (h < 0 || h >= (int32_t)ctx->lists.size() || !ctx->lists[h].live) return EINVAL;
+  std::shared_ptr<ListMem> last;  // released outside the lock
+  {
+    std::lock_guard<std::mutex> g(ctx->lists_mu);
+    if (h < 0 || h >= (int32_t)ctx->lists.size() || !ctx->lists[h].live) return EINVAL;
+    // queries in flight hold their own references (QuerySlot::held), so the
+    // memory outlives them; nothing is drained here
+    last = std::move(ctx->lists[h].mem);
+    ctx->lists[h] = ListEntry();
+  }
   (void)hipSetDevice(ctx->device);
-  // a query still in flight may read the list: drain every slot's stream
-  for (int i = 0; i < gbgpu_query_slots(ctx); i++) (void)hipStreamSynchronize(slot_of(ctx, i)->stream);
-  (void)hipFree(ctx->lists[h].d);
-  ctx->lists[h] = ListEntry();
+  last.reset();
   return 0;
 }
 
@@ -2079,9 +2988,14 @@ int gbgpu_query_slot_enqueue(gbgpu_ctx *ctx, int slot, const gbgpu_qterm *terms,
 int gbgpu_query_slot_collect(gbgpu_ctx *ctx, int slot, gbgpu_result *out) {
   QuerySlot *q = slot_of(ctx, slot);
   if (!q || !out) return EINVAL;
-  std::lock_guard<std::mutex> g(q->mu);
-  (void)hipSetDevice(ctx->device);
-  return collect(ctx, *q, out);
+  int rc;
+  {
+    std::lock_guard<std::mutex> g(q->mu);
+    (void)hipSetDevice(ctx->device);
+    rc = collect(ctx, *q, out);
+  }
+  slot_released(ctx);
+  return rc;
 }
 
 int gbgpu_query_resident_enqueue(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms, const int32_t *handles,
@@ -2093,26 +3007,33 @@ int gbgpu_query_collect(gbgpu_ctx *ctx, gbgpu_result *out) { return gbgpu_query_
 
 // Blocking query on whichever slot is free (re-entrant: Msg39 runs several
 // intersect threads); waits on one slot when all are busy.
+static int query_resident_on(gbgpu_ctx *ctx, QuerySlot *q, const gbgpu_qterm *terms, int nterms,
+                             const int32_t *handles, const gbgpu_params *p, gbgpu_result *out);
+
 int gbgpu_query_resident(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms, const int32_t *handles,
                          const gbgpu_params *p, gbgpu_result *out) {
   if (!ctx || !out) return EINVAL;
-  const int n = gbgpu_query_slots(ctx);
-  QuerySlot *q = nullptr;
-  std::unique_lock<std::mutex> lk;
-  for (int i = 0; i < n && !q; i++) {
-    QuerySlot *c = slot_of(ctx, i);
-    std::unique_lock<std::mutex> t(c->mu, std::try_to_lock);
-    if (t.owns_lock() && !c->pending) {
-      q = c;
-      lk = std::move(t);
+  // take a free slot; when every slot is busy (other intersect threads, or
+  // an enqueue/collect caller's uncollected query) wait until one is released
+  for (;;) {
+    const int n = gbgpu_query_slots(ctx);
+    for (int i = 0; i < n; i++) {
+      QuerySlot *c = slot_of(ctx, i);
+      std::unique_lock<std::mutex> t(c->mu, std::try_to_lock);
+      if (t.owns_lock() && !c->pending) {
+        const int rc = query_resident_on(ctx, c, terms, nterms, handles, p, out);
+        t.unlock();
+        slot_released(ctx);
+        return rc;
+      }
     }
+    std::unique_lock<std::mutex> w(ctx->free_mu);
+    ctx->free_cv.wait_for(w, std::chrono::milliseconds(1));
   }
-  if (!q) {
-    static std::atomic<unsigned> rr{0};
-    q = slot_of(ctx, (int)(rr++ % (unsigned)n));
-    lk = std::unique_lock<std::mutex>(q->mu);
-    if (q->pending) return EBUSY;  // held by an enqueue/collect caller
-  }
+}
+
+static int query_resident_on(gbgpu_ctx *ctx, QuerySlot *q, const gbgpu_qterm *terms, int nterms,
+                             const int32_t *handles, const gbgpu_params *p, gbgpu_result *out) {
   (void)hipSetDevice(ctx->device);
   if (p && p->num_docid_splits > 1) {
     std::vector<ListEntry> ents;

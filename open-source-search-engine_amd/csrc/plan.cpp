@@ -26,9 +26,19 @@ int32_t docs_wanted(const gbgpu_params *p, const int64_t *sizes, int nterms) {
   if (nn1 < nn2) nn = nn1;
   if (nn == 0) return 0;              // no tree allocated
   if (nn < 30) nn = 30;               // Posdb.cpp:897
+  if (p->site_clustering) nn *= 2;    // Posdb.cpp:900
   if (nn > 2000000000) nn = 2000000000;
   if (nn > (int64_t)p->docs_to_get * 2 && nn > 60) nn = (int64_t)p->docs_to_get * 2;
   return (int32_t)nn;                 // TopTree::setNumNodes -> m_docsWanted
+}
+
+int64_t tree_nodes(int32_t dw, bool site_clustering) {
+  if (!site_clustering) return (int64_t)dw + 1;  // TopTree.cpp:88
+  int64_t rmax = (int64_t)dw * 2;                // m_ridiculousMax, TopTree.cpp:76-77
+  if (rmax < 50) rmax = 50;
+  int64_t n = rmax * 256;
+  if (n > 2000000000LL) n = 2000000000LL;        // MAXDOCIDSTOCOMPUTE (Msg40.h:25)
+  return n;
 }
 
 int build_host_plan(const gbgpu_qterm *qt, int nqt, const int64_t *sizes, const gbgpu_params *p,

@@ -71,6 +71,15 @@ struct DevPlan {
   float same_lang_weight;
   float site_rank_multiplier;
   int nqt;  // Query::m_numTerms (scoreMatrix stride)
+  // paging filter (Posdb.cpp:4379-4381, 7327-7347): m_hasMaxSerpScore
+  int has_serp;
+  double max_serp_score;
+  int64_t min_serp_docid;
+  // site clustering: the pruning bounds (Posdb.cpp:6327-6504, 7811-7960)
+  int clustering;
+  int do_max_score;        // m_doMaxScoreAlgo
+  int min_listi;           // m_minListi (group whose positions seed the ring buffer)
+  int all_same_wiki;       // m_allInSameWikiPhrase (Posdb.cpp:5764-5778)
   // groups, in QueryTermInfo order
   uint8_t gflags0[MAXG];            // m_bigramFlags[0]
   uint8_t gnsub[MAXG];
@@ -96,6 +105,9 @@ struct DevPlan {
 int build_host_plan(const gbgpu_qterm *terms, int nterms, const int64_t *sizes,
                     const gbgpu_params *p, HostPlan *hp);
 int32_t docs_wanted(const gbgpu_params *p, const int64_t *sizes, int nterms);
+// TopTree::setNumNodes (TopTree.cpp:64-101): node count of a tree of
+// docs_wanted entries (docs_wanted+1 without site clustering)
+int64_t tree_nodes(int32_t docs_wanted, bool site_clustering);
 
 }  // namespace gbgpu
 

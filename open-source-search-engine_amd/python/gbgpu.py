@@ -52,6 +52,10 @@ class Params(ctypes.Structure):
         ("site_clustering", ctypes.c_int32),
         ("num_docid_splits", ctypes.c_int32),
         ("same_lang_weight", ctypes.c_float),
+        ("do_max_score_algo", ctypes.c_int32),
+        ("reserved0", ctypes.c_int32),
+        ("max_serp_score", ctypes.c_double),
+        ("min_serp_docid", ctypes.c_int64),
     ]
 
 
@@ -68,6 +72,9 @@ class Result(ctypes.Structure):
         ("hits", ctypes.c_int64),
         ("filtered", ctypes.c_int32),
         ("docs_wanted", ctypes.c_int32),
+        ("hit_docids", ctypes.POINTER(ctypes.c_int64)),
+        ("hit_capacity", ctypes.c_int64),
+        ("n_hit_docids", ctypes.c_int64),
     ]
 
 
@@ -99,6 +106,7 @@ SYNTH_WORD, SYNTH_SYNONYM, SYNTH_BIGRAM = 0, 1, 2
 # every symbol include/gbgpu.h and include/gbgpu_synth.h declare
 EXPORTS = [
     "gbgpu_open", "gbgpu_close", "gbgpu_strerror", "gbgpu_abi_version", "gbgpu_docs_wanted",
+    "gbgpu_tree_capacity",
     "gbgpu_query", "gbgpu_list_upload", "gbgpu_list_free", "gbgpu_query_resident",
     "gbgpu_query_resident_enqueue", "gbgpu_query_collect", "gbgpu_stream",
     "gbgpu_last_topk_device", "gbgpu_merge_topk", "gbgpu_merge_posdb", "gbgpu_set_profiling",
@@ -126,6 +134,8 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.gbgpu_strerror.restype = ctypes.c_char_p
     lib.gbgpu_docs_wanted.argtypes = [ctypes.POINTER(Params), ctypes.POINTER(i64), ctypes.c_int]
     lib.gbgpu_docs_wanted.restype = i32
+    lib.gbgpu_tree_capacity.argtypes = [ctypes.POINTER(Params), ctypes.POINTER(i64), ctypes.c_int]
+    lib.gbgpu_tree_capacity.restype = i32
     lib.gbgpu_query.argtypes = [vp, ctypes.POINTER(QTerm), ctypes.c_int, ctypes.POINTER(ListRef),
                                 ctypes.POINTER(Params), ctypes.POINTER(Result)]
     lib.gbgpu_list_upload.argtypes = [vp, vp, i64, ctypes.POINTER(i32)]
@@ -285,6 +295,11 @@ def docs_wanted(params: Params, sizes: Sequence[int]) -> int:
     return load().gbgpu_docs_wanted(ctypes.byref(params), arr, len(sizes))
 
 
+def tree_capacity(params: Params, sizes: Sequence[int]) -> int:
+    arr = (ctypes.c_int64 * max(1, len(sizes)))(*sizes)
+    return load().gbgpu_tree_capacity(ctypes.byref(params), arr, len(sizes))
+
+
 # ------------------------------------------------------------------- engine
 @dataclass
 class QueryResult:
@@ -293,6 +308,7 @@ class QueryResult:
     hits: int
     filtered: int
     docs_wanted: int
+    hit_docids: Optional[np.ndarray] = None  # the intersected docid set (when asked for)
 
 
 class Engine:
@@ -326,18 +342,24 @@ class Engine:
         _check(self.lib.gbgpu_list_free(self.ctx, handle), "free")
 
     @staticmethod
-    def _result(cap: int):
+    def _result(cap: int, hit_cap: int = 0):
         d = (ctypes.c_int64 * max(cap, 1))()
         s = (ctypes.c_float * max(cap, 1))()
         r = Result(ctypes.cast(d, ctypes.POINTER(ctypes.c_int64)), ctypes.cast(s, ctypes.POINTER(ctypes.c_float)),
                    cap, 0, 0, 0, 0)
-        return r, d, s
+        h = None
+        if hit_cap > 0:
+            h = np.zeros(hit_cap, np.int64)
+            r.hit_docids = h.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))
+            r.hit_capacity = hit_cap
+        return r, d, s, h
 
     @staticmethod
-    def _pack(r, d, s) -> QueryResult:
+    def _pack(r, d, s, h=None) -> QueryResult:
         n = r.n
         return QueryResult(np.frombuffer(d, dtype=np.int64, count=n).copy(),
-                           np.frombuffer(s, dtype=np.float32, count=n).copy(), r.hits, r.filtered, r.docs_wanted)
+                           np.frombuffer(s, dtype=np.float32, count=n).copy(), r.hits, r.filtered, r.docs_wanted,
+                           None if h is None else h[:r.n_hit_docids].copy())
 
     @staticmethod
     def host_lists(lists: Sequence[bytes]):
@@ -348,23 +370,25 @@ class Engine:
                                                 for k, l in zip(keep, lists)])
         return keep, refs
 
-    def query(self, terms: Sequence[QTerm], lists, params: Params, cap: int = 4096) -> QueryResult:
-        """gbgpu_query over host lists: a sequence of bytes, or host_lists()'s tuple."""
+    def query(self, terms: Sequence[QTerm], lists, params: Params, cap: int = 4096,
+              hit_cap: int = 0) -> QueryResult:
+        """gbgpu_query over host lists: a sequence of bytes, or host_lists()'s tuple.
+        hit_cap > 0 also returns the intersected docid set (up to hit_cap)."""
         n = len(terms)
         qt = (QTerm * max(n, 1))(*terms)
         keep, refs = lists if isinstance(lists, tuple) else self.host_lists(lists)
-        r, d, s = self._result(cap)
+        r, d, s, h = self._result(cap, hit_cap)
         _check(self.lib.gbgpu_query(self.ctx, qt, n, refs, ctypes.byref(params), ctypes.byref(r)), "query")
-        return self._pack(r, d, s)
+        return self._pack(r, d, s, h)
 
     def query_resident(self, terms: Sequence[QTerm], handles: Sequence[int], params: Params,
-                       cap: int = 4096) -> QueryResult:
+                       cap: int = 4096, hit_cap: int = 0) -> QueryResult:
         n = len(terms)
         qt = (QTerm * max(n, 1))(*terms)
         hh = (ctypes.c_int32 * max(n, 1))(*handles)
-        r, d, s = self._result(cap)
+        r, d, s, h = self._result(cap, hit_cap)
         _check(self.lib.gbgpu_query_resident(self.ctx, qt, n, hh, ctypes.byref(params), ctypes.byref(r)), "query")
-        return self._pack(r, d, s)
+        return self._pack(r, d, s, h)
 
     def set_slots(self, n: int) -> None:
         _check(self.lib.gbgpu_set_query_slots(self.ctx, n), "set_query_slots")
@@ -378,10 +402,10 @@ class Engine:
         hh = (ctypes.c_int32 * max(n, 1))(*handles)
         _check(self.lib.gbgpu_query_slot_enqueue(self.ctx, slot, qt, n, hh, ctypes.byref(params)), "enqueue")
 
-    def collect(self, cap: int = 4096, slot: int = 0) -> QueryResult:
-        r, d, s = self._result(cap)
+    def collect(self, cap: int = 4096, slot: int = 0, hit_cap: int = 0) -> QueryResult:
+        r, d, s, h = self._result(cap, hit_cap)
         _check(self.lib.gbgpu_query_slot_collect(self.ctx, slot, ctypes.byref(r)), "collect")
-        return self._pack(r, d, s)
+        return self._pack(r, d, s, h)
 
     def set_profiling(self, on: bool) -> None:
         _check(self.lib.gbgpu_set_profiling(self.ctx, 1 if on else 0))

@@ -49,8 +49,12 @@ class Query:
     spec_of_term: List[int]
     docs_to_get: int = 100
 
-    def params(self, real_max_top=10, language=0, same_lang_weight=20.0) -> Params:
-        return Params(self.docs_to_get, real_max_top, language, 0, 1, same_lang_weight)
+    def params(self, real_max_top=10, language=0, same_lang_weight=20.0, site_clustering=0,
+               num_docid_splits=1, max_serp_score=0.0, min_serp_docid=0) -> Params:
+        """Msg39Request as reset() (Msg39.h:36-82) leaves it, but clustering off
+        unless asked (the parity default, SURVEY.md §7 hard part 1)."""
+        return Params(self.docs_to_get, real_max_top, language, site_clustering, num_docid_splits,
+                      same_lang_weight, 1, 0, max_serp_score, min_serp_docid)
 
 
 def _tid(seed: int, k: int) -> int:

@@ -180,38 +180,130 @@ typedef struct {
   int nqt;
 } PT;
 
-/* TopTree semantics without site clustering (TopTree.cpp:206-516): keep the
- * best docsWanted by (score desc, docid asc); sorted high -> low here. */
+/* TopTree (TopTree.h:65-154, TopTree.cpp:64-516).  Its readout (getHighNode /
+ * getPrev) and low node only depend on the SET of nodes, ordered by (score
+ * asc, docid desc) -- the AVL shape does not show -- so the nodes are kept as
+ * an array sorted best first (score desc, docid asc).  The embedded m_t2
+ * RdbTree holds exactly the same nodes (every add to one is an add to the
+ * other, every delete likewise), keyed per domain by (uint32 score, docid)
+ * (TopTree.cpp:337-342), so m_domMinNode[] is the minimum of that key over the
+ * domain's nodes and is found by a scan here. */
 typedef struct {
-  int cap, n;
-  float *score;
+  int64_t numNodes;      /* m_numNodes                                   */
+  int32_t docsWanted;    /* m_docsWanted                                 */
+  int clustering;        /* m_doSiteClustering                           */
+  int64_t ridiculousMax; /* m_ridiculousMax                              */
+  int32_t cap;           /* m_cap                                        */
+  float partial;         /* m_partial                                    */
+  float vcount;          /* m_vcount                                     */
+  int32_t domCount[256]; /* m_domCount                                   */
+  int64_t n;             /* m_numUsedNodes                               */
+  float *score;          /* sorted best first                            */
   int64_t *docid;
-} TopK;
+} TTree;
 
-static void topk_add(TopK *t, float score, int64_t docid) {
-  if (t->cap <= 0) return;
-  if (t->n >= t->cap) {
-    float ls = t->score[t->n - 1];
-    int64_t ld = t->docid[t->n - 1];
-    if (score < ls) return;
-    if (!(score > ls) && docid >= ld) return;
+/* TopTree::setNumNodes, TopTree.cpp:64-101 */
+static int tt_init(TTree *t, int32_t docsWanted, int clustering) {
+  memset(t, 0, sizeof *t);
+  t->docsWanted = docsWanted;
+  t->clustering = clustering;
+  t->ridiculousMax = (int64_t)docsWanted * 2;
+  if (t->ridiculousMax < 50) t->ridiculousMax = 50;
+  int64_t numNodes = t->ridiculousMax * 256;
+  if (numNodes > 2000000000LL) numNodes = 2000000000LL; /* MAXDOCIDSTOCOMPUTE, Msg40.h:25 */
+  if (!clustering) t->ridiculousMax = 0x7fffffff;
+  if (!clustering) numNodes = t->docsWanted + 1;
+  t->vcount = 0.0;
+  t->cap = t->docsWanted / 50;
+  if (t->cap < 2) t->cap = 2;
+  if (!clustering) t->cap = 0x7fffffff;
+  t->partial = (float)(t->docsWanted % 50) / 50.0;
+  t->numNodes = numNodes;
+  /* the array grows on demand (numNodes can be 2 * docsWanted * 256) */
+  return 0;
+}
+
+static void tt_free(TTree *t) {
+  free(t->score);
+  free(t->docid);
+  t->score = NULL;
+  t->docid = NULL;
+}
+
+static inline uint8_t domHash8(int64_t d) { return (uint8_t)((d & ~0xffffffffffffc03fULL) >> 6); } /* Titledb.h:114-115 */
+
+/* deleteNode's count bookkeeping (TopTree.cpp:543-547) + removal of node i */
+static void tt_delete(TTree *t, int64_t i, uint8_t domHash) {
+  if (t->domCount[domHash] < t->cap) t->vcount -= 1.0;
+  else if (t->domCount[domHash] == t->cap) t->vcount -= t->partial;
+  t->domCount[domHash]--;
+  memmove(t->score + i, t->score + i + 1, sizeof(float) * (size_t)(t->n - i - 1));
+  memmove(t->docid + i, t->docid + i + 1, sizeof(int64_t) * (size_t)(t->n - i - 1));
+  t->n--;
+}
+
+/* TopTree::addNode, TopTree.cpp:206-516; returns 1 if the node was added */
+static int tt_add(TTree *t, float score, int64_t docid) {
+  const uint8_t domHash = domHash8(docid);
+  if (t->vcount >= t->docsWanted) {
+    const float ls = t->score[t->n - 1];
+    const int64_t ld = t->docid[t->n - 1];
+    if (score < ls) return 0;
+    if (score > ls) goto addIt;
+    if (docid >= ld) return 0;
   }
-  int pos = t->n < t->cap ? t->n : t->cap - 1;
-  /* find insertion point: first entry that ranks below (score, docid) */
-  int i = 0;
-  while (i < t->n && i < t->cap) {
-    if (t->score[i] < score || (t->score[i] == score && t->docid[i] > docid)) break;
-    if (t->score[i] == score && t->docid[i] == docid) return; /* "if equal do not replace" */
-    i++;
+addIt:;
+  /* position: after every node that ranks above (score desc, docid asc) */
+  int64_t pos = 0;
+  {
+    int64_t lo = 0, hi = t->n;
+    while (lo < hi) {
+      int64_t mid = (lo + hi) / 2;
+      if (t->score[mid] > score || (t->score[mid] == score && t->docid[mid] < docid)) lo = mid + 1;
+      else hi = mid;
+    }
+    pos = lo;
+    if (pos < t->n && t->score[pos] == score && t->docid[pos] == docid) return 0; /* equal: not replaced */
   }
-  if (i >= t->cap) return;
-  if (t->n < t->cap) { pos = t->n; t->n++; }
-  for (int k = pos; k > i; k--) {
-    t->score[k] = t->score[k - 1];
-    t->docid[k] = t->docid[k - 1];
+  const uint32_t cs = (uint32_t)score;
+  int64_t deleteMe = -1; /* docid of the domain's m_t2 minimum to delete */
+  if (t->domCount[domHash] >= t->ridiculousMax) {
+    /* m_domMinNode[domHash]: minimum (uint32 score, docid) of the domain */
+    int64_t m = -1;
+    uint32_t mcs = 0;
+    for (int64_t i = 0; i < t->n; i++) {
+      if (domHash8(t->docid[i]) != domHash) continue;
+      const uint32_t c = (uint32_t)t->score[i];
+      if (m < 0 || c < mcs || (c == mcs && t->docid[i] < t->docid[m])) {
+        m = i;
+        mcs = c;
+      }
+    }
+    if (cs < mcs || (cs == mcs && docid <= t->docid[m])) return 0; /* k <= key(min) */
+    deleteMe = t->docid[m];
   }
-  t->score[i] = score;
-  t->docid[i] = docid;
+  if (t->n % 4096 == 0) {
+    t->score = (float *)realloc(t->score, sizeof(float) * (size_t)(t->n + 4096));
+    t->docid = (int64_t *)realloc(t->docid, sizeof(int64_t) * (size_t)(t->n + 4096));
+  }
+  memmove(t->score + pos + 1, t->score + pos, sizeof(float) * (size_t)(t->n - pos));
+  memmove(t->docid + pos + 1, t->docid + pos, sizeof(int64_t) * (size_t)(t->n - pos));
+  t->score[pos] = score;
+  t->docid[pos] = docid;
+  t->n++;
+  t->domCount[domHash]++;
+  if (t->domCount[domHash] < t->cap) t->vcount += 1.0;
+  else if (t->domCount[domHash] == t->cap) t->vcount += t->partial;
+  if (deleteMe >= 0) {
+    int64_t i = 0;
+    while (t->docid[i] != deleteMe) i++;
+    tt_delete(t, i, domHash);
+  }
+  while (t->vcount - 1.0 >= t->docsWanted || t->n == t->numNodes) {
+    const int64_t tn = t->n - 1; /* m_lowNode */
+    tt_delete(t, tn, domHash8(t->docid[tn]));
+  }
+  return 1;
 }
 
 /* --------------------------------------------------------------- scorers */
@@ -909,6 +1001,178 @@ static void shrinkSubLists(QTI *qti, OList *lists, VoteBuf *vb) {
   }
 }
 
+/* --------------------------------------------------- pruning (clustering) */
+typedef struct {
+  float siteRankMultiplier;
+  int language;
+  float sameLangWeight;
+  int allInSameWikiPhrase; /* m_allInSameWikiPhrase, Posdb.cpp:5764-5778 */
+} MaxCtx;
+
+/* getMaxPossibleScore, Posdb.cpp:7811-7960 (over the docid's shrunk-sublist
+ * runs [m_savedCursor, m_cursor)) */
+static float getMaxPossibleScore(const MaxCtx *c, QTI *qti, int32_t bestDist, int32_t qdist, QTI *qtm) {
+  float bestHashGroupWeight = -1.0;
+  unsigned char bestDensityRank = 0;
+  char siteRank = -1;
+  char docLang = 0;
+  unsigned char hgrp;
+  int hadHalfStopWikiBigram = 0;
+  for (int j = 0; j < qti->numNewSubLists; j++) {
+    uint8_t *start = qti->savedCursor[j];
+    if (!start) continue;
+    if (qti->bigramFlags[0] & BF_HALFSTOPWIKIBIGRAM) hadHalfStopWikiBigram = 1;
+    if (start >= qti->newSubListEnd[j]) continue;
+    if (siteRank == -1) {
+      siteRank = (char)getSiteRank(start);
+      docLang = (char)getLangId(start);
+    }
+    start += 12;
+    uint8_t *dc = qti->cursor[j];
+    dc -= 6;
+    int retried = 0;
+    for (; dc >= start; dc -= 6) {
+    retry:
+      hgrp = getHashGroup(dc);
+      if (hgrp == HASHGROUP_INLINKTEXT) return -1.0;
+      if (s_hashGroupWeights[hgrp] < bestHashGroupWeight) {
+        if (hgrp == HASHGROUP_BODY) goto nextTermList;
+        continue;
+      }
+      {
+        char dr = (char)getDensityRank(dc);
+        if (s_hashGroupWeights[hgrp] > bestHashGroupWeight) {
+          if (hgrp == HASHGROUP_INLINKTEXT) return -1.0;
+          bestHashGroupWeight = s_hashGroupWeights[hgrp];
+          bestDensityRank = dr;
+          continue;
+        }
+        if (dr < bestDensityRank) continue;
+        if (dr > bestDensityRank) bestDensityRank = dr;
+      }
+    }
+    /* the run's 12-byte key last (Posdb.cpp:7893-7897) */
+    if (!retried) {
+      retried = 1;
+      dc = qti->savedCursor[j];
+      goto retry;
+    }
+  nextTermList:
+    continue;
+  }
+  if (bestHashGroupWeight < 0) return 0.0;
+  float score = 100.0;
+  score *= bestHashGroupWeight;
+  score *= bestHashGroupWeight;
+  score *= s_densityWeights[bestDensityRank];
+  score *= s_densityWeights[bestDensityRank];
+  if (hadHalfStopWikiBigram) {
+    score *= WIKI_BIGRAM_WEIGHT;
+    score *= WIKI_BIGRAM_WEIGHT;
+  }
+  score *= (((float)siteRank) * c->siteRankMultiplier + 1.0);
+  if (c->language == (unsigned char)docLang || c->language == 0 || docLang == 0) score *= c->sameLangWeight;
+  score *= qti->termFreqWeight;
+  if (qdist) {
+    score *= qtm->termFreqWeight;
+    bestDist -= qdist;
+    if (qdist < 0) qdist *= -1;
+    if (bestDist < 0) bestDist *= -1;
+    if (bestDist > 1) score /= (float)bestDist;
+  }
+  if (c->allInSameWikiPhrase) score *= WIKI_WEIGHT;
+  return score;
+}
+
+#define RINGBUFSIZE 4096
+
+/* The two prefilters of the per-docid loop, Posdb.cpp:6322-6504: 1 if the
+ * docid is skipped (its bound cannot beat minWinningScore). */
+static int prefilter_skip(const MaxCtx *c, QTI *qip, int nqti, int minListi, int doMaxScoreAlgo,
+                          float minWinningScore, unsigned char *ringBuf, int32_t *ourFirstPos) {
+  const int nnn = doMaxScoreAlgo ? nqti : 0;
+  for (int i = 0; i < nnn; i++) {
+    if (qip[i].bigramFlags[0] & (BF_NEGATIVE | BF_FACET)) continue;
+    float maxScore = getMaxPossibleScore(c, &qip[i], 0, 0, NULL);
+    if (maxScore == -1.0) continue;
+    if (maxScore <= minWinningScore) return 1;
+  }
+  memset(ringBuf, 0xff, RINGBUFSIZE);
+  QTI *qtx = &qip[minListi];
+  for (int k = 0; k < qtx->numNewSubLists; k++) {
+    uint8_t *sub = qtx->savedCursor[k];
+    if (!sub) continue;
+    uint8_t *end = qtx->cursor[k];
+    uint32_t wx = U32(sub + 3) >> 6;
+    wx &= (RINGBUFSIZE - 1);
+    ringBuf[wx] = (unsigned char)minListi;
+    *ourFirstPos = (int32_t)wx;
+    sub += 12;
+    for (; sub < end; sub += 6) {
+      wx = U32(sub + 3) >> 6;
+      wx &= (RINGBUFSIZE - 1);
+      ringBuf[wx] = (unsigned char)minListi;
+    }
+  }
+  for (int i = 0; i < nqti; i++) {
+    if (i == minListi) continue;
+    QTI *qti = &qip[i];
+    if (qti->bigramFlags[0] & (BF_NEGATIVE | BF_FACET)) continue;
+    for (int k = 0; k < qti->numNewSubLists; k++) {
+      uint8_t *sub = qti->savedCursor[k];
+      if (!sub) continue;
+      uint8_t *end = qti->cursor[k];
+      uint32_t wx = U32(sub + 3) >> 6;
+      wx &= (RINGBUFSIZE - 1);
+      ringBuf[wx] = (unsigned char)i;
+      sub += 12;
+      for (; sub < end; sub += 6) {
+        wx = U32(sub + 3) >> 6;
+        wx &= (RINGBUFSIZE - 1);
+        ringBuf[wx] = (unsigned char)i;
+      }
+    }
+    int32_t ourLastPos = -1;
+    int32_t hisLastPos = -1;
+    int32_t bestDist = 0x7fffffff;
+    for (int32_t x = 0; x < (int32_t)RINGBUFSIZE;) {
+      if (U32(ringBuf + x) == 0xffffffff) {
+        x += 4;
+        continue;
+      }
+      if (ringBuf[x] == 0xff) {
+        x++;
+        continue;
+      }
+      unsigned char qt = ringBuf[x];
+      if (qt == minListi) {
+        hisLastPos = x;
+        if (ourLastPos == -1) {
+          x++;
+          continue;
+        }
+        if (x - ourLastPos < bestDist) bestDist = x - ourLastPos;
+      } else if (qt == i) {
+        ourLastPos = x;
+        if (hisLastPos == -1) {
+          x++;
+          continue;
+        }
+        ourLastPos = x;
+        if (x - hisLastPos < bestDist) bestDist = x - hisLastPos;
+      }
+      x++;
+    }
+    int32_t wrapDist = *ourFirstPos + ((int32_t)RINGBUFSIZE - hisLastPos);
+    if (wrapDist < bestDist) bestDist = wrapDist;
+    int32_t qdist = qip[minListi].qpos - qip[i].qpos;
+    float maxScore2 = getMaxPossibleScore(c, &qip[i], bestDist, qdist, &qip[minListi]);
+    if (maxScore2 == -1.0) continue;
+    if (maxScore2 <= minWinningScore) return 1;
+  }
+  return 0;
+}
+
 /* ---------------------------------------------------------------- driver */
 #define LIST_PAD 64
 
@@ -1034,6 +1298,7 @@ static int64_t docs_wanted(const orc_params *p, const int64_t *sizes, int nqt) {
   if (nn1 < nn2) nn = nn1;
   if (nn == 0) return 0;
   if (nn < 30) nn = 30;
+  if (p->site_clustering) nn *= 2; /* Posdb.cpp:900 */
   if (nn > 2000000000) nn = 2000000000;
   if (nn > (int64_t)p->docs_to_get * 2 && nn > 60) nn = (int64_t)p->docs_to_get * 2;
   return nn;
@@ -1042,8 +1307,7 @@ static int64_t docs_wanted(const orc_params *p, const int64_t *sizes, int nqt) {
 /* One PosdbTable pass (init .. intersectLists10_r, Posdb.cpp:5437-7806) over
  * one docid range's lists, adding its winners to the caller's TopTree. */
 static int run_range(const orc_qterm *qt, const uint8_t *const *lists, const int64_t *sizes, int nqt,
-                     const orc_params *prm, TopK *tkp, orc_result *out) {
-  TopK tk = *tkp;
+                     const orc_params *prm, TTree *tree, orc_result *out) {
   Prep P;
   int rc = prepare(qt, lists, sizes, nqt, &P);
   if (rc) {
@@ -1093,6 +1357,20 @@ static int run_range(const orc_qterm *qt, const uint8_t *const *lists, const int
     pt.nqt = nqt;
     float siteRankMultiplier = SITERANKMULTIPLIER;
     char siteRank = 0, docLang = 0;
+    float minWinningScore = -1.0; /* Posdb.cpp:6012: per pass */
+    int32_t ourFirstPos = -1;
+    unsigned char ringBuf[RINGBUFSIZE + 10];
+    MaxCtx mc;
+    mc.siteRankMultiplier = siteRankMultiplier;
+    mc.language = prm->language;
+    mc.sameLangWeight = prm->same_lang_weight;
+    mc.allInSameWikiPhrase = 1;
+    for (int i = 0; i < nqti; i++) {
+      if (qip[i].bigramFlags[0] & (BF_NEGATIVE | BF_NUMBER | BF_FACET)) continue;
+      if (qip[i].wikiPhraseId == 1) continue;
+      mc.allInSameWikiPhrase = 0;
+      break;
+    }
     uint8_t *nwp[MAX_SUBLISTS], *nwpEnd[MAX_SUBLISTS];
     char nwpFlags[MAX_SUBLISTS];
     uint8_t *docIdEnd = P.vb.buf + P.vb.len;
@@ -1120,8 +1398,12 @@ static int run_range(const orc_qterm *qt, const uint8_t *const *lists, const int
           qti->cursor[j] = xc;
         }
       }
-      /* (the max-score and ring-buffer prefilters are inert without site
-       *  clustering: minWinningScore stays -1, Posdb.cpp:7699-7704) */
+      /* the max-score and ring-buffer prefilters, Posdb.cpp:6322-6504 (live
+       * only once the TopTree holds more than docsWanted nodes, i.e. with
+       * site clustering: minWinningScore is -1 until then) */
+      if (prefilter_skip(&mc, qip, nqti, P.minListi, prm->do_max_score_algo, minWinningScore, ringBuf,
+                         &ourFirstPos))
+        continue;
 
       /* mini merges, Posdb.cpp:6559-6778 */
       {
@@ -1328,8 +1610,13 @@ static int run_range(const orc_qterm *qt, const uint8_t *const *lists, const int
       if (prm->language == 0 || docLang == 0 || prm->language == docLang)
         score *= prm->same_lang_weight;
       out->filtered++;
-      out->filtered--; /* no maxSerpScore (Posdb.cpp:7327-7347) */
-      topk_add(&tk, score, (int64_t)pt.docId);
+      if (prm->min_serp_docid) { /* m_hasMaxSerpScore, Posdb.cpp:4379-4381, 7327-7347 */
+        if (score > (float)prm->max_serp_score) continue;
+        if (score == prm->max_serp_score && (int64_t)pt.docId <= prm->min_serp_docid) continue;
+      }
+      out->filtered--;
+      tt_add(tree, score, (int64_t)pt.docId);
+      if (tree->n > tree->docsWanted) minWinningScore = tree->score[tree->n - 1]; /* 7699-7704 */
     }
   doneAll:
     free(wikiPhraseIds); free(quotedStartIds); free(qpos); free(freqWeights);
@@ -1338,7 +1625,6 @@ static int run_range(const orc_qterm *qt, const uint8_t *const *lists, const int
   }
 
 finish:
-  *tkp = tk;
   unprepare(&P, nqt);
   return 0;
 }
@@ -1386,14 +1672,14 @@ int orc_query(const orc_qterm *qt, const uint8_t *const *lists, const int64_t *s
               const orc_params *prm, int64_t *docids, float *scores, int cap, orc_result *out) {
   memset(out, 0, sizeof *out);
   if (nqt < 0 || !prm) return EINVAL;
-  if (prm->site_clustering) return ENOTSUP;
   if (prm->real_max_top <= 0 || prm->docs_to_get <= 0 || prm->num_docid_splits <= 0) return EINVAL;
   for (int i = 0; i < nqt; i++)
     if (qt[i].field_code) return ENOTSUP; /* numeric/facet/range terms: DESIGN.md */
   initWeights();
 
   const int splits = prm->num_docid_splits;
-  TopK tk = {0, 0, NULL, NULL};
+  TTree tk;
+  memset(&tk, 0, sizeof tk);
   int alloced = 0, rc = 0;
   const uint8_t **pl = (const uint8_t **)calloc(nqt > 0 ? nqt : 1, sizeof(uint8_t *));
   int64_t *ps = (int64_t *)calloc(nqt > 0 ? nqt : 1, sizeof(int64_t));
@@ -1427,9 +1713,7 @@ int orc_query(const orc_qterm *qt, const uint8_t *const *lists, const int64_t *s
       if (dw == 0) continue;
       alloced = 1;
       out->docs_wanted = (int32_t)dw;
-      tk.cap = (int)dw;
-      tk.score = (float *)calloc(dw, sizeof(float));
-      tk.docid = (int64_t *)calloc(dw, sizeof(int64_t));
+      tt_init(&tk, (int32_t)dw, prm->site_clustering != 0);
     }
     orc_result r;
     memset(&r, 0, sizeof r);
@@ -1441,13 +1725,12 @@ int orc_query(const orc_qterm *qt, const uint8_t *const *lists, const int64_t *s
   } while (ddd < ORC_MAX_DOCID);
   for (int i = 0; i < nqt; i++) free(own[i]);
   free(own); free(pl); free(ps);
-  out->n = tk.n < cap ? tk.n : cap;
+  out->n = tk.n < cap ? (int32_t)tk.n : cap;
   for (int i = 0; i < out->n; i++) {
     docids[i] = tk.docid[i];
     scores[i] = tk.score[i];
   }
-  free(tk.score);
-  free(tk.docid);
+  tt_free(&tk);
   return rc;
 }
 

@@ -36,20 +36,26 @@ typedef struct orc_qterm {
   float   tf_weight;                /* Msg39Request::ptr_termFreqWeights[i]    */
 } orc_qterm;
 
+/* same layout as gbgpu_params (include/gbgpu.h) */
 typedef struct orc_params {
   int32_t docs_to_get;      /* Msg39Request::m_docsToGet               */
   int32_t real_max_top;     /* m_realMaxTop (clamped to MAX_TOP=10)    */
   int32_t language;         /* m_language                              */
-  int32_t site_clustering;  /* must be 0               */
+  int32_t site_clustering;  /* m_doSiteClustering (TopTree domain caps) */
   int32_t num_docid_splits; /* m_numDocIdSplits: Msg39's split loop      */
   float   same_lang_weight; /* m_sameLangWeight                        */
+  int32_t do_max_score_algo;/* m_doMaxScoreAlgo                        */
+  int32_t reserved0;
+  double  max_serp_score;   /* m_maxSerpScore                          */
+  int64_t min_serp_docid;   /* m_minSerpDocId (nonzero: paging filter) */
 } orc_params;
 
 typedef struct orc_result {
   int64_t hits;        /* m_docIdVoteBuf.length()/6                          */
   int32_t filtered;    /* m_filtered                                          */
   int32_t docs_wanted; /* TopTree::m_docsWanted (0: no tree allocated)        */
-  int32_t n;           /* entries written (TopTree read high -> low)          */
+  int32_t n;           /* entries written (TopTree read high -> low; all of
+                          m_numUsedNodes with site clustering)            */
   int32_t corrupt;     /* intersectLists10_r bailed on a corrupt list          */
 } orc_result;
 

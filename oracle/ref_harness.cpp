@@ -143,6 +143,9 @@ static int ref_query(const orc_qterm *terms, const uint8_t *const *lists, const 
   req.m_sameLangWeight = p->same_lang_weight;
   req.m_doSiteClustering = p->site_clustering != 0;
   req.m_numDocIdSplits = p->num_docid_splits;
+  req.m_doMaxScoreAlgo = p->do_max_score_algo != 0;
+  req.m_maxSerpScore = p->max_serp_score;
+  req.m_minSerpDocId = p->min_serp_docid;
   req.m_getDocIdScoringInfo = false;
   req.m_collnum = 0;
   req.ptr_termFreqWeights = (char *)tfw;

@@ -35,7 +35,7 @@ def pack_lists(lists):
 
 
 def save_query(name, terms, lists, params):
-    r = ref.query(terms, lists, params, votes=True)
+    r = ref.query(terms, lists, params, votes=True, cap=1 << 16)
     if params.num_docid_splits > 1:
         # the vote buffer of one whole-range pass: the exact intersection
         import copy
@@ -46,11 +46,13 @@ def save_query(name, terms, lists, params):
     qt = np.array([[getattr(t, f) for f in QFIELDS] for t in terms], np.int32).reshape(len(terms), len(QFIELDS))
     tfw = np.array([t.tf_weight for t in terms], np.float32)
     pr = np.array([params.docs_to_get, params.real_max_top, params.language, params.site_clustering,
-                   params.num_docid_splits], np.int32)
+                   params.num_docid_splits, params.do_max_score_algo], np.int32)
     np.savez_compressed(os.path.join(OUT, f"q_{name}.npz"), qterms=qt, tfw=tfw, params=pr,
-                        same_lang_weight=np.float32(params.same_lang_weight), list_sizes=sizes, list_blob=blob,
+                        same_lang_weight=np.float32(params.same_lang_weight),
+                        max_serp_score=np.float64(params.max_serp_score),
+                        min_serp_docid=np.int64(params.min_serp_docid), list_sizes=sizes, list_blob=blob,
                         docids=r["docids"], score_bits=r["scores"].view(np.uint32), hits=np.int64(r["hits"]),
-                        docs_wanted=np.int32(r["docs_wanted"]), votes=r["votes"])
+                        filtered=np.int32(r["filtered"]), docs_wanted=np.int32(r["docs_wanted"]), votes=r["votes"])
     return r
 
 
@@ -107,6 +109,77 @@ def save_splits():
     print(f"q_splits3_sizing: hits={r['hits']} n={len(r['docids'])} dw={r['docs_wanted']}")
 
 
+def skewed_docids(n, seed, ndom=3, frac=0.7):
+    """n distinct sorted docids, `frac` of them in `ndom` domains (domHash8 =
+    docid bits 6..13, Titledb.h:114-115): TopTree's per-domain caps."""
+    rng = np.random.default_rng(seed)
+    doms = rng.choice(256, ndom, replace=False)
+    out = set()
+    while len(out) < n:
+        d = int(rng.integers(0, 1 << 38))
+        if rng.random() < frac:
+            d = (d & ~0x3fc0) | (int(doms[rng.integers(0, ndom)]) << 6)
+        out.add(d)
+    return sorted(out)
+
+
+def save_clustering():
+    """Site clustering on (the Msg39Request default, Msg39.h:41): TopTree
+    domain caps (TopTree.cpp:64-186, 312-516) and the minWinningScore pruning
+    they make live (Posdb.cpp:6322-6504, 7699-7704, 7811-7960)."""
+    import posdb_py
+    from workload import Word, build_query
+    N = 6000
+    for q in qkinds.kinds(N, seed=3):
+        lists = generate(q, N, seed=4000)
+        r = save_query(f"clus_{q.name}", q.terms, lists, q.params(site_clustering=1))
+        print(f"q_clus_{q.name}: hits={r['hits']} n={len(r['docids'])} dw={r['docs_wanted']}")
+    # few domains: m_ridiculousMax / m_cap / m_partial (docsWanted % 50 != 0)
+    for ndom, frac, dtg in ((1, 0.9, 10), (3, 0.7, 17), (12, 0.5, 60)):
+        for q in (qkinds.kinds(N, seed=5)[0], qkinds.kinds(N, seed=5)[2]):
+            lists = generate(q, N, seed=4100 + ndom)
+            nd = len({int(d) for l in lists for d in posdb_py.docids(l)})
+            lists = posdb_py.remap_docids(lists, skewed_docids(nd, seed=ndom, ndom=ndom, frac=frac))
+            q.docs_to_get = dtg
+            for mx in (1, 0):
+                r = save_query(f"clus_dom{ndom}_{q.name}_mx{mx}", q.terms, lists, _mx(q.params(site_clustering=1), mx))
+                print(f"  dom{ndom} {q.name} mx={mx}: hits={r['hits']} n={len(r['docids'])} dw={r['docs_wanted']}")
+    # clustering with docid splits: one tree across the pieces
+    for S in (2, 5):
+        q = qkinds.kinds(N, seed=6)[1]
+        lists = generate(q, N, seed=4200 + S)
+        r = save_query(f"clus_splits{S}_{q.name}", q.terms, lists, q.params(site_clustering=1, num_docid_splits=S))
+        print(f"  splits{S}: hits={r['hits']} n={len(r['docids'])}")
+    # large enough that the prefilters change the tree (vs scoring every docid)
+    N2 = 100000
+    q = build_query("three_prune", [Word("a", 0.3), Word("b", 0.2), Word("c", 0.25)], N2, seed=3)
+    q.docs_to_get = 50
+    lists = generate(q, N2, seed=3)
+    r = save_query("clus_prune_100k", q.terms, lists, q.params(site_clustering=1))
+    print(f"  prune 100k: hits={r['hits']} n={len(r['docids'])}")
+
+
+def _mx(p, mx):
+    p.do_max_score_algo = mx
+    return p
+
+
+def save_paging():
+    """m_maxSerpScore / m_minSerpDocId (Posdb.cpp:4379-4381, 7327-7347)."""
+    N = 6000
+    for q in qkinds.kinds(N, seed=7)[:6]:
+        lists = generate(q, N, seed=4300)
+        full = ref.query(q.terms, lists, q.params())
+        if len(full["docids"]) < 3:
+            continue
+        pos = len(full["docids"]) // 3
+        for clus in (0, 1):
+            p = q.params(site_clustering=clus, max_serp_score=float(full["scores"][pos]),
+                         min_serp_docid=int(full["docids"][pos]))
+            r = save_query(f"serp_{q.name}_c{clus}", q.terms, lists, p)
+            print(f"  serp {q.name} clus={clus}: n={len(r['docids'])} filtered={r['filtered']}")
+
+
 def save_merge(name, runs, cases):
     sizes, blob = pack_lists(runs)
     outs, osz, rms, mrss = [], [], [], []
@@ -149,6 +222,8 @@ def main():
     save_query("empty_all", q.terms, [b"", b"", b""], q.params())
     save_query("empty_required", q.terms, [lists[0], b"", b""], q.params())
     save_splits()
+    save_clustering()
+    save_paging()
     cases = [(0, -1), (1, -1), (0, 5000), (1, 5000), (0, 1)]
     for seed, (keys, nterms) in enumerate([(4000, 50), (12000, 3), (8000, 1)]):
         save_merge(f"tiered_s{seed}", tiered_runs(keys, seed=seed, nterms=nterms), cases)
@@ -160,5 +235,8 @@ def main():
 if __name__ == "__main__":
     if sys.argv[1:] == ["splits"]:
         save_splits()
+    elif sys.argv[1:] == ["clustering"]:
+        save_clustering()
+        save_paging()
     else:
         main()

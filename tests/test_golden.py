@@ -33,16 +33,27 @@ def load_query(path):
     z = np.load(path, allow_pickle=False)
     terms = [gbgpu.QTerm(*[int(x) for x in row], float(w)) for row, w in zip(z["qterms"], z["tfw"])]
     pr = z["params"]
-    params = gbgpu.Params(int(pr[0]), int(pr[1]), int(pr[2]), int(pr[3]), int(pr[4]), float(z["same_lang_weight"]))
+    # the harness ran Msg39Request::reset() (m_doMaxScoreAlgo = true) before
+    # the fields a fixture names
+    do_max = int(pr[5]) if len(pr) > 5 else 1
+    params = gbgpu.Params(int(pr[0]), int(pr[1]), int(pr[2]), int(pr[3]), int(pr[4]), float(z["same_lang_weight"]),
+                          do_max, 0, float(z["max_serp_score"]) if "max_serp_score" in z else 0.0,
+                          int(z["min_serp_docid"]) if "min_serp_docid" in z else 0)
     lists = split_blob(z["list_sizes"], z["list_blob"])
     exp = dict(docids=z["docids"], scores=z["score_bits"].view(np.float32), hits=int(z["hits"]),
-               docs_wanted=int(z["docs_wanted"]), votes=z["votes"])
+               docs_wanted=int(z["docs_wanted"]), votes=z["votes"],
+               filtered=int(z["filtered"]) if "filtered" in z else None)
     return terms, lists, params, exp
 
 
 def check(got, exp, label):
     assert got["hits"] == exp["hits"], label
     assert got["docs_wanted"] == exp["docs_wanted"], label
+    if exp.get("filtered") is not None:
+        assert got["filtered"] == exp["filtered"], label
+    if got.get("hit_docids") is not None:
+        # the intersected docid set itself (m_docIdVoteBuf), bit-exact
+        assert np.array_equal(got["hit_docids"], exp["votes"]), label
     assert np.array_equal(got["docids"], exp["docids"]), label
     g = np.asarray(got["scores"], np.float32)
     rel = np.abs(g.astype(np.float64) - exp["scores"]) / np.maximum(1e-30, np.abs(exp["scores"]))
@@ -66,7 +77,7 @@ def test_fixtures_present():
 @pytest.mark.parametrize("path", QCASES, ids=[os.path.basename(p)[2:-4] for p in QCASES])
 def test_oracle_query_vs_reference(path):
     terms, lists, params, exp = load_query(path)
-    got = orc.query(terms, lists, params)
+    got = orc.query(terms, lists, params, cap=1 << 16)
     check(got, exp, os.path.basename(path))
 
 
@@ -90,6 +101,6 @@ def test_oracle_merge_vs_reference(path):
 @pytest.mark.parametrize("path", QCASES, ids=[os.path.basename(p)[2:-4] for p in QCASES])
 def test_gpu_query_vs_reference(engine, path):
     terms, lists, params, exp = load_query(path)
-    r = engine.query(terms, lists, params)
-    check(dict(docids=r.docids, scores=r.scores, hits=r.hits, docs_wanted=r.docs_wanted), exp,
-          os.path.basename(path))
+    r = engine.query(terms, lists, params, cap=1 << 16, hit_cap=max(1, exp["hits"]))
+    check(dict(docids=r.docids, scores=r.scores, hits=r.hits, docs_wanted=r.docs_wanted, filtered=r.filtered,
+               hit_docids=r.hit_docids), exp, os.path.basename(path))

@@ -19,11 +19,26 @@ REL_TOL = 1e-5
 def check(res, exp, label=""):
     assert res.hits == exp["hits"], label
     assert res.docs_wanted == exp["docs_wanted"], label
+    if "filtered" in exp:
+        assert res.filtered == exp["filtered"], label
+    if res.hit_docids is not None and "votes" in exp:
+        # the intersected docid set itself (m_docIdVoteBuf), not only its size
+        assert np.array_equal(res.hit_docids, exp["votes"]), label
     assert len(res.docids) == len(exp["docids"]), label
     assert np.array_equal(res.docids, exp["docids"]), label
     rel = np.abs(res.scores.astype(np.float64) - exp["scores"]) / np.maximum(1e-30, np.abs(exp["scores"]))
     assert np.all(rel <= REL_TOL), (label, rel.max())
     assert np.array_equal(res.scores.view(np.uint32), exp["scores"].view(np.uint32)), label
+
+
+def oracle(terms, lists, p, cap=1 << 16):
+    exp = orc.query(terms, lists, p, cap=cap)
+    exp["votes"] = orc.intersect(terms, lists)
+    return exp
+
+
+def gpu(engine, terms, lists, p, cap=1 << 16):
+    return engine.query(terms, lists, p, cap=cap, hit_cap=1 << 22)
 
 
 @pytest.mark.parametrize("seed", [1, 2, 3])
@@ -32,9 +47,43 @@ def test_parity_kinds(engine, kind, seed):
     q = qkinds.kinds(20000, seed=seed)[kind]
     lists = generate(q, 20000, seed=1000 + seed)
     p = q.params()
-    exp = orc.query(q.terms, lists, p)
-    res = engine.query(q.terms, lists, p)
-    check(res, exp, f"{q.name} seed={seed}")
+    check(gpu(engine, q.terms, lists, p), oracle(q.terms, lists, p), f"{q.name} seed={seed}")
+
+
+@pytest.mark.parametrize("kind", [0, 1, 2, 3, 4])
+def test_parity_paging_filter(engine, kind):
+    # m_maxSerpScore / m_minSerpDocId (Posdb.cpp:4379-4381, 7327-7347)
+    q = qkinds.kinds(20000, seed=8)[kind]
+    lists = generate(q, 20000, seed=800 + kind)
+    full = orc.query(q.terms, lists, q.params())
+    for pos in (0, len(full["docids"]) // 2):
+        if not len(full["docids"]):
+            break
+        p = q.params(max_serp_score=float(full["scores"][pos]), min_serp_docid=int(full["docids"][pos]))
+        check(gpu(engine, q.terms, lists, p), oracle(q.terms, lists, p), f"{q.name} pos={pos}")
+
+
+def test_corrupt_list_fails_loudly(engine):
+    # an 18-byte key inside a termlist is what intersectLists10_r bails on
+    # (Posdb.cpp:6289-6302); the GPU path refuses the list (GBGPU_ECORRUPT)
+    # instead of scanning it, and a truncated 12-byte key likewise
+    q = qkinds.kinds(5000, seed=1)[0]
+    lists = generate(q, 5000)
+    import posdb_py
+    runs = posdb_py.decode_runs(lists[0])
+    off = runs[len(runs) // 2][1]                 # a 12-byte run head mid-list
+    bad = bytearray(lists[0])
+    bad[off] &= 0xf9                              # -> reads as an 18-byte key
+    trunc = lists[0][:runs[1][1] + 6]              # ends inside a 12-byte key
+    for ls in ([bytes(bad), lists[1], lists[2]], [trunc, lists[1], lists[2]]):
+        with pytest.raises(gbgpu.GbgpuError) as e:
+            engine.query(q.terms, ls, q.params())
+        assert e.value.code == gbgpu.GBGPU_ECORRUPT
+    with pytest.raises(gbgpu.GbgpuError) as e:
+        engine.upload(bytes(bad))
+    assert e.value.code == gbgpu.GBGPU_ECORRUPT
+    # the context stays usable
+    check(gpu(engine, q.terms, lists, q.params()), oracle(q.terms, lists, q.params()), "after corrupt")
 
 
 @pytest.mark.parametrize("docs_to_get,real_max_top,language", [(10, 10, 0), (300, 3, 1), (1, 1, 7)])
@@ -51,7 +100,7 @@ def test_parity_larger_lists(engine):
     q = config_two_term(2_000_000, docs_to_get=100, seed=9)
     lists = generate(q, 2_000_000, seed=5)
     p = q.params()
-    check(engine.query(q.terms, lists, p), orc.query(q.terms, lists, p))
+    check(gpu(engine, q.terms, lists, p), oracle(q.terms, lists, p))
 
 
 def test_resident_repeat_is_idempotent(engine):
@@ -82,9 +131,11 @@ def test_unsupported_modes_fail_loudly(engine):
     q = qkinds.kinds(5000, seed=1)[0]
     lists = generate(q, 5000)
     p = q.params()
-    p.site_clustering = 1
+    terms = list(q.terms)
+    terms[0] = gbgpu.QTerm(*[getattr(terms[0], f) for f, _ in gbgpu.QTerm._fields_])
+    terms[0].field_code = 3  # a numeric/facet field term (gbsortby:, gbfacet*: ...)
     with pytest.raises(gbgpu.GbgpuError) as e:
-        engine.query(q.terms, lists, p)
+        engine.query(terms, lists, p)
     assert e.value.code == gbgpu.GBGPU_EUNSUPPORTED
 
 
@@ -137,7 +188,7 @@ def test_parity_docid_splits(engine, kind, splits):
     lists = generate(q, 20000, seed=600 + splits)
     p = q.params()
     p.num_docid_splits = splits
-    check(engine.query(q.terms, lists, p), orc.query(q.terms, lists, p), f"{q.name} S={splits}")
+    check(gpu(engine, q.terms, lists, p), oracle(q.terms, lists, p), f"{q.name} S={splits}")
 
 
 def test_parity_docid_splits_resident_large(engine):
@@ -153,3 +204,68 @@ def test_parity_docid_splits_resident_large(engine):
     finally:
         for h in hs:
             engine.free(h)
+
+
+# ---------------------------------------------------------- site clustering
+# m_doSiteClustering (the Msg39Request default): TopTree domain caps and the
+# minWinningScore pruning they make live, replayed in docid order on the GPU
+
+@pytest.mark.parametrize("seed", [1, 2])
+@pytest.mark.parametrize("kind", range(len(qkinds.kinds())))
+def test_parity_site_clustering(engine, kind, seed):
+    q = qkinds.kinds(20000, seed=seed)[kind]
+    lists = generate(q, 20000, seed=1100 + seed)
+    for dtg in (q.docs_to_get, 13):
+        q.docs_to_get = dtg
+        p = q.params(site_clustering=1)
+        check(gpu(engine, q.terms, lists, p), oracle(q.terms, lists, p), f"{q.name} seed={seed} dtg={dtg}")
+
+
+def _skewed(n, seed, ndom, frac):
+    rng = np.random.default_rng(seed)
+    doms = rng.choice(256, ndom, replace=False)
+    out = set()
+    while len(out) < n:
+        d = int(rng.integers(0, 1 << 38))
+        if rng.random() < frac:
+            d = (d & ~0x3fc0) | (int(doms[rng.integers(0, ndom)]) << 6)
+        out.add(d)
+    return sorted(out)
+
+
+@pytest.mark.parametrize("ndom,frac,dtg", [(1, 0.9, 10), (2, 0.8, 37), (5, 0.6, 60), (20, 0.5, 100)])
+def test_parity_site_clustering_skewed_domains(engine, ndom, frac, dtg):
+    # m_ridiculousMax / m_cap / m_partial (TopTree.cpp:64-186, 355-418)
+    import posdb_py
+    for kind in (0, 1, 3):
+        q = qkinds.kinds(8000, seed=9)[kind]
+        lists = generate(q, 8000, seed=900 + ndom)
+        nd = len({int(d) for l in lists for d in posdb_py.docids(l)})
+        lists = posdb_py.remap_docids(lists, _skewed(nd, ndom, ndom, frac))
+        q.docs_to_get = dtg
+        for mx in (1, 0):
+            p = q.params(site_clustering=1)
+            p.do_max_score_algo = mx
+            check(gpu(engine, q.terms, lists, p), oracle(q.terms, lists, p), f"{q.name} ndom={ndom} mx={mx}")
+
+
+@pytest.mark.parametrize("splits", [2, 5, 16])
+def test_parity_site_clustering_docid_splits(engine, splits):
+    for kind in (0, 2, 3, 9):
+        q = qkinds.kinds(20000, seed=10)[kind]
+        lists = generate(q, 20000, seed=1200 + splits)
+        p = q.params(site_clustering=1, num_docid_splits=splits)
+        check(gpu(engine, q.terms, lists, p), oracle(q.terms, lists, p), f"{q.name} S={splits}")
+
+
+def test_parity_site_clustering_pruning_large(engine):
+    # 300k docs: the prefilters prune and change the tree vs scoring every docid
+    q = build_query("three", [Word("a", 0.3), Word("b", 0.2), Word("c", 0.25)], 300_000, seed=1)
+    q.docs_to_get = 50
+    lists = generate(q, 300_000, seed=1)
+    p = q.params(site_clustering=1)
+    check(gpu(engine, q.terms, lists, p), oracle(q.terms, lists, p), "three 300k")
+    q2 = config_two_term(2_000_000, docs_to_get=100, seed=9)
+    lists2 = generate(q2, 2_000_000, seed=5)
+    p2 = q2.params(site_clustering=1)
+    check(gpu(engine, q2.terms, lists2, p2), oracle(q2.terms, lists2, p2), "two_term 2M")
