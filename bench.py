@@ -1,23 +1,28 @@
 """Benchmark: Posdb query scoring on MI355X (BASELINE.json metric).
 
-One step = one query (config 2: 2-term AND + its bigram, top-100) over a
-synthetic Zipfian posdb index resident in HBM.  At N GPUs the index is
-docid-range sharded (100M docs per GPU, weak scaling, mirroring one Msg39 per
-shard); every rank scores its shard, the per-shard top-k lists are
-all-gathered over RCCL and merged Msg3a-style (Msg3a.cpp:1315-1467).
+One step = one query over a synthetic Zipfian posdb index resident in HBM.
+At N=1 the workload is config 2 (100M docs, 2-term AND + bigram, top-100),
+rotating over 16 distinct 2-term queries (distinct termIds, ~3.5 GB of lists,
+far above the 256 MiB Infinity Cache, so the list scan reads HBM).  At N>1 the
+index is docid-range sharded, 125M docs per GPU -- at N=8 exactly config 4's
+1B-doc index -- every rank scores its shard and the shards' top lists are
+all-gathered over RCCL and merged on the device Msg3a-style
+(gbgpu_allgather_topk, Msg3a.cpp:1315-1467).
 
-    python bench.py --gpus 1 --steps 20 --warmup 3
+    python bench.py --gpus 1 --steps 400 --warmup 5
     torchrun --nproc-per-node N bench.py --gpus N ...
 
 Prints one JSON line (rank 0).  value = aggregate posdb list bytes scanned
-per second (GB/s); queries/sec is reported beside it.
+per second (GB/s, all ranks); queries/sec beside it.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import subprocess
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -26,6 +31,8 @@ sys.path.insert(0, os.path.join(ROOT, "open-source-search-engine_amd", "python")
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+CFG2_DOCS = 100_000_000
+CFG4_DOCS_PER_GPU = 125_000_000  # 1B docs over 8 GPUs
 
 
 def log(*a):
@@ -33,67 +40,127 @@ def log(*a):
         print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(q, num_docs_total: int, budget_s: float = 12.0):
-    """Oracle (CPU restatement, 1 thread) on a bounded docid-range slice of the
-    same corpus; reports list GB/s and queries/s on the slice."""
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import oracle_binding as orc
-    from workload import generate
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
-    sample_docs = min(num_docs_total, 2_000_000)
-    lists = generate(q, num_docs_total, doc_begin=0, doc_end=sample_docs, threads=16)
+
+def cpu_threads():
+    """The host threads this process may use (the GPU box gives a share of a
+    larger machine: `nproc` overstates it; the box exports OMP_NUM_THREADS)."""
+    n = len(os.sched_getaffinity(0))
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return max(1, min(n, share) if share > 0 else n)
+
+
+# ------------------------------------------------------------ CPU baselines
+def _gbref_requests(terms, lists, params, reps):
+    """op=1 request bytes of oracle/_ref/gbref (see tests/ref_binding.py)."""
+    import ctypes
+    import struct
+    import gbgpu
+    qt = (gbgpu.QTerm * max(1, len(terms)))(*terms)
+    req = [struct.pack("<ii", 1, len(terms)), bytes(params), bytes(qt)[:ctypes.sizeof(gbgpu.QTerm) * len(terms)]]
+    for l in lists:
+        req.append(struct.pack("<q", len(l)))
+        req.append(bytes(l))
+    req.append(struct.pack("<iii", 128, 0, reps))
+    return b"".join(req)
+
+
+def _gbref_run(exe, req, nproc):
+    """nproc gbref processes each serving the same request; returns the per
+    process median seconds inside intersectLists10_r and the hit counts."""
+    import ctypes
+    import struct
+    procs = [subprocess.Popen([exe], stdin=subprocess.PIPE, stdout=subprocess.PIPE) for _ in range(nproc)]
+    outs = [None] * nproc
+
+    def drive(i):
+        p = procs[i]
+        p.stdin.write(req)
+        p.stdin.close()
+        outs[i] = p.stdout.read()
+        p.wait()
+
+    th = [threading.Thread(target=drive, args=(i,)) for i in range(nproc)]
+    t0 = time.perf_counter()
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    wall = time.perf_counter() - t0
+    res = []
+    for o in outs:
+        # orc_result: hits i64, filtered i32, docs_wanted i32, n i32, corrupt i32
+        hits, _, _, n, corrupt = struct.unpack_from("<qiiii", o, 0)
+        off = 24 + 12 * n
+        (nv,) = struct.unpack_from("<q", o, off)
+        (sec,) = struct.unpack_from("<d", o, off + 8 + 8 * nv)
+        if corrupt < 0:
+            raise RuntimeError(f"gbref rc {-corrupt}")
+        res.append((sec, hits))
+    return res, wall
+
+
+def cpu_baseline_query(q, lists, budget_s=20.0):
+    """The reference's own PosdbTable::intersectLists10_r (oracle/_ref/gbref,
+    compiled from the unmodified sources, -O2 as its Makefile) on the SAME
+    full-size lists as the GPU, timed inside the harness (list copies, which
+    the reference mutates, excluded): 1 thread, then one process per host
+    thread of this box's share running the same query.  Falls back to the C
+    restatement (kind "port") where the reference was not built."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
     p = q.params()
     nbytes = sum(len(l) for l in lists)
+    exe = os.path.join(ROOT, "oracle", "_ref", "gbref")
+    threads = cpu_threads()
+    out = {"unit": "GB/s", "cpu_model": cpu_model(), "host_threads_available": threads,
+           "sample": f"the full config-2 query ({nbytes/1e6:.1f} MB of lists, the GPU's first rotation query)"}
+    if os.access(exe, os.X_OK):
+        one, _ = _gbref_run(exe, _gbref_requests(q.terms, lists, p, 1), 1)
+        t1 = max(one[0][0], 1e-6)
+        reps1 = int(max(3, min(50, budget_s * 0.3 / t1)))
+        r1, _ = _gbref_run(exe, _gbref_requests(q.terms, lists, p, reps1), 1)
+        per1 = r1[0][0]
+        repsn = int(max(2, min(50, budget_s * 0.6 / t1)))
+        rn, wall = _gbref_run(exe, _gbref_requests(q.terms, lists, p, repsn), threads)
+        qps_n = sum(1.0 / max(s, 1e-9) for s, _ in rn)
+        out.update({
+            "kind": "reference",
+            "value": round(nbytes / per1 / 1e9, 4),
+            "cores": 1,
+            "queries_per_sec": round(1.0 / per1, 3),
+            "throughput": {"cores": threads, "queries_per_sec": round(qps_n, 3),
+                           "value": round(nbytes * qps_n / 1e9, 4), "unit": "GB/s",
+                           "note": f"{threads} gbref processes, each the same query {repsn}x "
+                                   f"(median per process), {wall:.1f} s wall"},
+            "hits": int(r1[0][1]),
+            "detail": f"oracle/_ref/gbref: median of {reps1} runs inside intersectLists10_r, 1 thread",
+        })
+        return out
+    import oracle_binding as orc
     t0 = time.perf_counter()
     reps = 0
     while True:
         orc.query(q.terms, lists, p)
         reps += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s or reps >= 2000:
+        if time.perf_counter() - t0 > budget_s * 0.5 or reps >= 20:
             break
-    per_q = el / reps
-    out = {
-        "value": round(nbytes / per_q / 1e9, 4),
-        "unit": "GB/s",
-        "cores": 1,
-        "kind": "port",
-        "qps_on_sample": round(1.0 / per_q, 3),
-        "est_qps_full_index": round((sample_docs / num_docs_total) / per_q, 4),
-        "sample": f"docs [0,{sample_docs}) of the same {num_docs_total}-doc corpus and query "
-                  f"({nbytes/1e6:.1f} MB of lists), oracle/posdb_oracle.c single thread, {reps} reps, "
-                  f"{el:.1f} s",
-    }
-    # the reference's own PosdbTable::intersectLists10_r (oracle/_ref/gbref,
-    # built from the unmodified sources) on the same slice, when it was built
-    try:
-        import ref_binding as ref
-        if ref.available():
-            exp = orc.query(q.terms, lists, p)
-            r1 = ref.query(q.terms, lists, p, reps=1)
-            assert r1["hits"] == exp["hits"] and np.array_equal(r1["docids"], exp["docids"])
-            nrep = int(max(3, min(2000, budget_s / max(r1["seconds"], 1e-6))))
-            t0 = time.perf_counter()
-            rr = ref.query(q.terms, lists, p, reps=nrep)
-            el2 = time.perf_counter() - t0
-            per_r = rr["seconds"]  # median of nrep runs, timed inside the harness
-            out.update({
-                "value": round(nbytes / per_r / 1e9, 4),
-                "kind": "reference",
-                "qps_on_sample": round(1.0 / per_r, 3),
-                "est_qps_full_index": round((sample_docs / num_docs_total) / per_r, 4),
-                "port_value": round(nbytes / per_q / 1e9, 4),
-                "sample": f"docs [0,{sample_docs}) of the same {num_docs_total}-doc corpus and query "
-                          f"({nbytes/1e6:.1f} MB of lists), the reference's PosdbTable (oracle/_ref/gbref, "
-                          f"-O2 as its Makefile) single thread, median of {nrep} runs incl. the per-run "
-                          f"list copy, {el2:.1f} s; port_value = oracle/posdb_oracle.c, {reps} reps",
-            })
-    except Exception as e:  # the reference build is optional (absent where /root/reference was)
-        out["reference_error"] = repr(e)[:200]
+    per = (time.perf_counter() - t0) / reps
+    out.update({"kind": "port", "value": round(nbytes / per / 1e9, 4), "cores": 1,
+                "queries_per_sec": round(1.0 / per, 3),
+                "detail": f"oracle/posdb_oracle.c (reference not built here), {reps} reps"})
     return out
 
 
-def bench_config3(eng, num_docs: int, steps: int, slots: int):
+# ---------------------------------------------------------------- config 3
+def bench_config3(eng, num_docs, steps, slots, with_cpu):
     """Config 3 (BASELINE.json): the ten fixed 3-5 word queries, three with a
     quoted phrase (term-pair proximity path), over a 100M-doc index resident in
     HBM; queries run round-robin with `slots` of them in flight."""
@@ -101,25 +168,25 @@ def bench_config3(eng, num_docs: int, steps: int, slots: int):
 
     qs = config3_queries(num_docs, docs_to_get=100)
     t0 = time.time()
-    hs, qbytes = [], []
+    hs, qbytes, first_lists = [], [], None
     for q in qs:
         lists = generate(q, num_docs, threads=16)
+        if first_lists is None:
+            first_lists = lists
         hs.append([eng.upload(l) for l in lists])
         qbytes.append(sum(len(l) for l in lists))
     log(f"[config3] generated + uploaded {sum(qbytes)/1e9:.2f} GB of lists in {time.time()-t0:.1f}s")
     ps = [q.params() for q in qs]
 
     def run(nq):
-        hits = []
         for i in range(nq):
             slot = i % slots
             if i >= slots:
-                hits.append(eng.collect(cap=4096, slot=slot).hits)
+                eng.collect(cap=4096, slot=slot)
             j = i % len(qs)
             eng.enqueue(qs[j].terms, hs[j], ps[j], slot=slot)
         for i in range(max(0, nq - slots), nq):
-            hits.append(eng.collect(cap=4096, slot=i % slots).hits)
-        return hits
+            eng.collect(cap=4096, slot=i % slots)
 
     run(len(qs))
     eng.set_profiling(True)
@@ -127,7 +194,7 @@ def bench_config3(eng, num_docs: int, steps: int, slots: int):
     for j, q in enumerate(qs):
         eng.enqueue(q.terms, hs[j], ps[j], slot=0)
         eng.collect(cap=4096, slot=0)
-        dev.append(eng.last_timings(slot=0)[0][0])
+        dev.append(eng.last_timings(slot=0)[0])
     eng.set_profiling(False)
     nq = max(steps, len(qs)) // len(qs) * len(qs)
     t = time.perf_counter()
@@ -137,24 +204,34 @@ def bench_config3(eng, num_docs: int, steps: int, slots: int):
     for h in hs:
         for x in h:
             eng.free(x)
-    return {
+    r = {
         "workload": "config 3: 10 fixed 3-5 word queries (3 with a quoted phrase), top-100, 100M docs",
         "queries": nq,
         "queries_per_sec": round(nq / el, 2),
         "keys_scanned_GBps": round(scanned / el / 1e9, 2),
         "pct_hbm_peak_keys_scanned": round(100.0 * scanned / el / 1e9 / HBM_PEAK_GBS, 2),
         "avg_list_bytes_per_query": int(np.mean(qbytes)),
-        "device_ms_per_query": [round(float(x), 4) for x in dev],
+        "device_ms_per_query": [round(float(x[0]), 4) for x in dev],
+        "phase_ms_mean": dict(zip(["total", "candidates", "probe", "compact", "score", "topk"],
+                                  [round(float(v), 4) for v in np.mean(np.array(dev), axis=0)])),
     }
+    if with_cpu:
+        exe = os.path.join(ROOT, "oracle", "_ref", "gbref")
+        if os.access(exe, os.X_OK):
+            res, _ = _gbref_run(exe, _gbref_requests(qs[0].terms, first_lists, ps[0], 2), 1)
+            sec = res[0][0]
+            r["cpu_baseline"] = {"value": round(qbytes[0] / sec / 1e9, 4), "unit": "GB/s", "cores": 1,
+                                 "kind": "reference", "queries_per_sec": round(1.0 / sec, 3),
+                                 "sample": f"config-3 query {qs[0].name} at full size ({qbytes[0]/1e6:.0f} MB), "
+                                           f"oracle/_ref/gbref median of 2 runs inside intersectLists10_r"}
+    return r
 
 
-def bench_merge(eng, steps: int, total_keys: int, with_cpu: bool):
+# ---------------------------------------------------------------- config 5
+def bench_merge(eng, steps, total_keys, with_cpu):
     """Config 5 (BASELINE.json): RdbList::posdbMerge_r of 8 tiered posdb runs
-    (sizes 1:2:..:128, 5% of keys repeated across runs, 1% delete keys),
-    runs and output resident in HBM (gbgpu_merge_posdb_device).  Reports the
-    merge rate (input bytes/s and (input+output) bytes/s), per-phase device
-    times, a size-independent check (merging the output alone returns it) and
-    the oracle's single-thread rate on a bounded sample of the same generator."""
+    (sizes 1:2:..:128, 5% of keys repeated across runs, 1% delete keys), runs
+    and output resident in HBM (gbgpu_merge_posdb_device)."""
     import torch
     import gbgpu
 
@@ -181,8 +258,6 @@ def bench_merge(eng, steps: int, total_keys: int, with_cpu: bool):
             dev_ms.append(ms)
         res[rm] = (n, float(np.median(wall)), np.mean(np.array(dev_ms), axis=0), nkeys, ntiles)
     n, w, ms, nkeys, ntiles = res[0]
-    # size-independent property: the merged list is canonical, so merging it
-    # alone reproduces it byte for byte
     out2 = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
     n2 = eng.merge_posdb_device([out.data_ptr()], [n], 0, -1, out2.data_ptr(), n + 64)
     idem = bool(n2 == n and torch.equal(out[:n], out2[:n]))
@@ -209,34 +284,39 @@ def bench_merge(eng, steps: int, total_keys: int, with_cpu: bool):
     del dev, out, out2
     if with_cpu:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
-        import ctypes
-        import oracle_binding as orc
         sample_keys = 20_000_000
         runs = gbgpu.synth_merge_runs(sample_keys, nruns=8, seed=5, nterms=20000, nthreads=16)
-        keep, p, sz = orc._lists(runs)
-        scap = sum(map(len, runs)) + 64
-        buf = ctypes.create_string_buffer(scap)
-        t = time.perf_counter()
-        reps = 0
-        while True:
-            orc.lib().orc_posdb_merge(p, sz, len(runs), 0, -1, buf, scap)
-            reps += 1
-            el = time.perf_counter() - t
-            if el > 8.0 or reps >= 20:
-                break
         sb = sum(map(len, runs))
-        r["cpu_baseline"] = {"value": round(sb / (el / reps) / 1e9, 4), "unit": "GB/s (input)", "cores": 1,
-                             "kind": "port",
-                             "sample": f"{sample_keys} keys ({sb/1e6:.0f} MB) of the same generator, "
-                                       f"oracle/posdb_merge_oracle.c single thread, {reps} reps, {el:.1f} s"}
+        try:
+            import ref_binding as ref
+            if not ref.available():
+                raise RuntimeError("gbref not built")
+            secs = [ref.posdb_merge(runs, False, -1, timed=True)[1] for _ in range(3)]
+            ref.close()
+            sec = float(np.median(secs))
+            r["cpu_baseline"] = {"value": round(sb / sec / 1e9, 4), "unit": "GB/s (input)", "cores": 1,
+                                 "kind": "reference",
+                                 "sample": f"{sample_keys} keys ({sb/1e6:.0f} MB) of the same generator, the "
+                                           f"reference's own RdbList::merge_r (oracle/_ref/gbref), median of 3"}
+        except Exception as e:  # reference not built: the C restatement
+            import ctypes
+            import oracle_binding as orc
+            keep, p, sz = orc._lists(runs)
+            buf = ctypes.create_string_buffer(sb + 64)
+            t = time.perf_counter()
+            orc.lib().orc_posdb_merge(p, sz, len(runs), 0, -1, buf, sb + 64)
+            el = time.perf_counter() - t
+            r["cpu_baseline"] = {"value": round(sb / el / 1e9, 4), "unit": "GB/s (input)", "cores": 1,
+                                 "kind": "port", "reference_error": repr(e)[:120],
+                                 "sample": f"{sample_keys} keys ({sb/1e6:.0f} MB), oracle/posdb_merge_oracle.c"}
     return r
 
 
 def pmc_traffic(kernel_prefix: str):
-    """HBM bytes per launch of a kernel from the committed rocprofv3 PMC passes
-    (profiles/*pmc_traffic.json, newest), corrected per MI355X_MICROARCH.md."""
+    """HBM bytes per launch of a kernel from the newest committed rocprofv3 PMC
+    pass (profiles/r02_*pmc_traffic.json), corrected per MI355X_MICROARCH.md."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic.json")))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r02_*pmc_traffic.json")))
     if not files:
         return None, None
     d = json.load(open(files[-1]))
@@ -249,15 +329,19 @@ def pmc_traffic(kernel_prefix: str):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--docs-per-gpu", type=int, default=100_000_000)
+    ap.add_argument("--docs-per-gpu", type=int, default=0, help="0: 100M at N=1 (config 2), 125M at N>1 (config 4)")
     ap.add_argument("--docs-to-get", type=int, default=100)
+    ap.add_argument("--queries", type=int, default=16, help="distinct config-2 queries the steps rotate over")
     ap.add_argument("--slots", type=int, default=2, help="queries in flight per GPU (query slots)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-merge", action="store_true", help="skip the config-5 list merge measurement")
     ap.add_argument("--no-config3", action="store_true", help="skip the config-3 query-mix measurement")
+    ap.add_argument("--no-ceiling", action="store_true", help="skip the streaming-bandwidth ceiling")
     ap.add_argument("--merge-keys", type=int, default=400_000_000, help="config-5 keys (~4.4 GB of runs)")
+    ap.add_argument("--exchange", action="store_true",
+                    help="run the RCCL Msg3a exchange even on one GPU (a one-rank communicator)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -269,91 +353,127 @@ def main():
     import torch
     import torch.distributed as dist
     import gbgpu
-    from shard_merge import gather_merge
     from workload import config_two_term, generate
 
     torch.cuda.set_device(local_rank)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
-    per = args.docs_per_gpu
+    per = args.docs_per_gpu or (CFG2_DOCS if world == 1 else CFG4_DOCS_PER_GPU)
     total = per * world
-    q = config_two_term(total, docs_to_get=args.docs_to_get)
-    t0 = time.time()
-    lists = generate(q, total, doc_begin=rank * per, doc_end=(rank + 1) * per, threads=16)
-    log(f"[rank {rank}] generated {sum(map(len, lists))/1e6:.1f} MB of lists in {time.time()-t0:.1f}s")
-
     eng = gbgpu.Engine(local_rank)
-    handles = [eng.upload(l) for l in lists]
-    list_bytes = sum(len(l) for l in lists)
-    p = q.params()
-    k = p.docs_to_get
+    exchange = world > 1 or args.exchange
+    if exchange and world == 1:
+        eng.comm_init(1, 0, gbgpu.Engine.comm_unique_id())
+    if world > 1:
+        # the library's own communicator for the Msg3a exchange
+        uid = torch.zeros(128, dtype=torch.uint8, device="cuda")
+        if rank == 0:
+            uid.copy_(torch.frombuffer(bytearray(gbgpu.Engine.comm_unique_id()), dtype=torch.uint8))
+        dist.broadcast(uid, 0)
+        eng.comm_init(world, rank, bytes(uid.cpu().numpy()))
 
+    # the rotation: distinct 2-term queries (distinct termIds), each with its
+    # own lists; every rank holds its docid range of each list
+    qs = [config_two_term(total, docs_to_get=args.docs_to_get, seed=s + 1) for s in range(args.queries)]
+    t0 = time.time()
+    handles, qbytes, first_lists = [], [], None
+    for q in qs:
+        lists = generate(q, total, doc_begin=rank * per, doc_end=(rank + 1) * per, threads=16)
+        if first_lists is None:
+            first_lists = lists
+        handles.append([eng.upload(l) for l in lists])
+        qbytes.append(sum(len(l) for l in lists))
+    log(f"[rank {rank}] generated + uploaded {len(qs)} queries, {sum(qbytes)/1e9:.2f} GB of lists "
+        f"in {time.time()-t0:.1f}s")
+    ps = [q.params() for q in qs]
+    k = ps[0].docs_to_get
     slots = max(1, args.slots)
     eng.set_slots(slots)
 
-    def finish(r):
-        """Msg39Reply -> Msg3a: per-shard top lists all-gathered over RCCL and
-        merged (shard_merge.py); returns (total hits, merged docids)."""
-        if world == 1:
-            return r.hits, r.docids[:k]
-        hits, d, _ = gather_merge(r.docids, r.scores, r.hits, k, device="cuda")
-        return hits, d
+    def finish(slot):
+        if not exchange:
+            return eng.collect(cap=4096, slot=slot).hits
+        _, _, hits = eng.allgather_topk(k, slot=slot)
+        return hits
 
     def run(nq):
-        """nq queries with `slots` of them in flight (round-robin over the
-        slots: a slot's previous query is collected before it is reused)."""
-        hits, top = 0, None
+        """nq queries round-robin over the rotation with `slots` in flight (a
+        slot's previous query is collected before it is reused)."""
+        hits = 0
         for i in range(nq):
             slot = i % slots
             if i >= slots:
-                hits, top = finish(eng.collect(cap=4096, slot=slot))
-            eng.enqueue(q.terms, handles, p, slot=slot)
+                hits = finish(slot)
+            j = i % len(qs)
+            eng.enqueue(qs[j].terms, handles[j], ps[j], slot=slot)
         for i in range(max(0, nq - slots), nq):
-            hits, top = finish(eng.collect(cap=4096, slot=i % slots))
-        return hits, top
+            hits = finish(i % slots)
+        return hits
 
     run(args.warmup * slots)
-    # per-phase device times and the probe roofline: queries one at a time
-    # (untimed; concurrent queries would overlap each other's events)
+    # per-phase device times (HIP events on the slot stream) and work counts,
+    # one query at a time over the whole rotation (untimed)
     eng.set_profiling(True)
-    phase_ms = []
-    for _ in range(max(5, args.steps // 2)):
-        eng.enqueue(q.terms, handles, p, slot=0)
-        finish(eng.collect(cap=4096, slot=0))
-        ms, scan_bytes = eng.last_timings(slot=0)
-        phase_ms.append(ms)
+    phase, stats = [], []
+    for rep in range(2):
+        for j, q in enumerate(qs):
+            eng.enqueue(q.terms, handles[j], ps[j], slot=0)
+            finish(0)
+            if rep:
+                phase.append(eng.last_timings(slot=0)[0])
+                stats.append(eng.stats(slot=0))
     eng.set_profiling(False)
-    probe_ms = [m[2] for m in phase_ms]
-    total_dev_ms = [m[0] for m in phase_ms]
 
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    hits, top = run(args.steps)
+    hits = run(args.steps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
+    # bytes of the steps actually run on this rank (round-robin rotation)
+    my_bytes = float(sum(qbytes[i % len(qs)] for i in range(args.steps)))
     if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
-        lb = torch.tensor([list_bytes], dtype=torch.float64, device="cuda")
-        dist.all_reduce(lb)
-        agg_list_bytes = float(lb.item())
+        t = torch.tensor([el, my_bytes], dtype=torch.float64, device="cuda")
+        tt = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(tt, t)
+        el = max(float(x[0]) for x in tt)
+        agg_bytes = sum(float(x[1]) for x in tt)
     else:
-        agg_list_bytes = float(list_bytes)
+        agg_bytes = my_bytes
 
     ms_per_step = el * 1000.0 / args.steps
     qps = args.steps / el
-    gbs = agg_list_bytes * qps / 1e9
-    # dominant kernel: k_probe, algorithmic bytes = bytes of the lists it scans
-    probe_bytes = float(list_bytes - len(lists[1]) if len(lists[1]) else list_bytes)
-    _, scan_bytes = eng.last_timings()
-    avg_probe_ms = float(np.mean(probe_ms))
-    achieved = probe_bytes / (avg_probe_ms / 1000.0) / 1e9 if avg_probe_ms > 0 else 0.0
+    gbs = agg_bytes / el / 1e9
+
+    ph = np.array(phase)
+    names = ["total", "candidates", "probe", "compact", "score", "topk"]
+    sum_ms = ph.sum(axis=0)
+    tot = {key: float(sum(st[key] for st in stats)) for key in stats[0]}
+    # algorithmic bytes per kernel (SURVEY.md §8(d)), summed over the rotation
+    kern_bytes = {
+        "candidates": tot["g0_bytes"] + 8.0 * tot["candidates"],
+        "probe": tot["probe_bytes"],
+        "compact": 8.0 * tot["candidates"] + 16.0 * tot["survivors"],
+        "score": tot["survivor_run_bytes"] + 12.0 * tot["survivors"],
+    }
+    kernels = {}
+    for i, nm in enumerate(names[1:], start=1):
+        entry = {"ms_per_query": round(float(sum_ms[i]) / len(phase), 4)}
+        if nm in kern_bytes and sum_ms[i] > 0:
+            a = kern_bytes[nm] / (sum_ms[i] / 1e3) / 1e9
+            entry.update({"algorithmic_bytes_per_query": int(kern_bytes[nm] / len(phase)),
+                          "achieved_GBps": round(a, 1), "frac_of_peak": round(a / HBM_PEAK_GBS, 4)})
+        kernels[nm] = entry
+    probe_achieved = kern_bytes["probe"] / (sum_ms[2] / 1e3) / 1e9
+    ceiling = None
+    if rank == 0 and not args.no_ceiling:
+        rd, cp = eng.bandwidth_ceiling(4 << 30, 8)
+        ceiling = {"read_GBps": round(rd, 1), "copy_GBps": round(cp, 1),
+                   "kernel": "k_stream_read / k_stream_copy (16 B/lane, 4 GiB buffers, 8 passes)"}
     traffic, traffic_src = pmc_traffic("k_probe")
     result = {
         "metric": "queries/sec + posdb keys scanned GB/s (% HBM peak), 1/2/4/8 MI355X",
@@ -365,57 +485,67 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 4),
         "queries_in_flight": slots,
-        "device_ms_per_query": round(float(np.mean(total_dev_ms)), 4),
-        "phase_ms": dict(zip(["total", "candidates", "probe", "compact", "score", "topk"],
-                             [round(float(x), 4) for x in np.mean(np.array(phase_ms), axis=0)])),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic Zipfian posdb lists (SURVEY.md §8(d) generator), resident in HBM",
         "config": {
-            "workload": "config 2: 2-term AND (+bigram sublist), top-100, 100M docs per GPU, docid-range shards",
+            "workload": ("config 2: 2-term AND (+bigram sublist), top-100, 100M docs" if world == 1 else
+                         f"config 4: {total/1e9:.3g}B-doc index docid-sharded, {per/1e6:.0f}M docs per GPU, "
+                         f"per-GPU top-100 + RCCL allgather + device Msg3a merge"),
+            "rotation": f"{len(qs)} distinct 2-term queries (distinct termIds), round-robin",
             "docs_per_gpu": per,
             "docs_total": total,
-            "list_bytes_per_gpu": list_bytes,
-            "hits": int(hits),
+            "list_bytes_per_gpu_rotation": int(sum(qbytes)),
+            "list_bytes_per_query_mean": int(np.mean(qbytes)),
+            "hits_last": int(hits),
             "pct_hbm_peak_keys_scanned": round(100.0 * gbs / (HBM_PEAK_GBS * world), 2),
         },
+        "device_ms_per_query": round(float(sum_ms[0]) / len(phase), 4),
+        "phase_ms": {nm: round(float(sum_ms[i]) / len(phase), 4) for i, nm in enumerate(names)},
+        "kernels": kernels,
         "roofline": {
             "bound": "hbm",
-            "kernel": "k_probe",
-            "achieved": round(achieved, 2),
+            "kernel": "k_probe (the list scan: every sublist but the candidate array's)",
+            "achieved": round(probe_achieved, 2),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "frac": round(probe_achieved / HBM_PEAK_GBS, 4),
+            "ceiling": ceiling,
+            "frac_of_ceiling": round(probe_achieved / ceiling["read_GBps"], 4) if ceiling else None,
             "traffic": traffic,
             "traffic_source": traffic_src,
-            "algorithmic_bytes_per_launch": int(probe_bytes),
+            "algorithmic_bytes_per_launch": int(kern_bytes["probe"] / len(phase)),
+            "timing": "HIP events around the launch on the slot stream, mean over the rotation",
         },
     }
     if rank == 0 and world == 1:
         # the C-ABI's host-buffer entry (gbgpu_query: lists in pageable host
         # memory, uploaded per call) -- PCIe-inclusive, reported beside `value`
         n_pc = 10
-        host = eng.host_lists(lists)
-        eng.query(q.terms, host, p)
+        host = eng.host_lists(first_lists)
+        r0 = eng.query(qs[0].terms, host, ps[0])
         t_pc = time.perf_counter()
         for _ in range(n_pc):
-            r_pc = eng.query(q.terms, host, p)
+            r_pc = eng.query(qs[0].terms, host, ps[0])
         el_pc = time.perf_counter() - t_pc
-        if r_pc.hits != hits:
-            raise RuntimeError(f"host-buffer query hits {r_pc.hits} != resident {hits}")
+        if r_pc.hits != r0.hits:
+            raise RuntimeError("host-buffer query results differ between calls")
         result["pcie_inclusive"] = {
             "queries_per_sec": round(n_pc / el_pc, 3),
-            "keys_scanned_GBps": round(list_bytes * n_pc / el_pc / 1e9, 3),
+            "keys_scanned_GBps": round(qbytes[0] * n_pc / el_pc / 1e9, 3),
             "note": "gbgpu_query with the lists in pageable host memory, uploaded every call; not `value`",
         }
-    if rank == 0 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(q, per if world == 1 else total)
-    for h in handles:
-        eng.free(h)
+        del host
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline_query(qs[0], first_lists)
+    for hs in handles:
+        for h in hs:
+            eng.free(h)
+    del first_lists
     if rank == 0 and world == 1 and not args.no_config3:
-        result["config3"] = bench_config3(eng, per, max(args.steps, 50), slots)
+        result["config3"] = bench_config3(eng, CFG2_DOCS, max(args.steps // 4, 50), slots, not args.no_cpu_baseline)
     if rank == 0 and world == 1 and not args.no_merge:
         result["config5_merge"] = bench_merge(eng, max(3, min(args.steps, 10)), args.merge_keys,
                                               not args.no_cpu_baseline)

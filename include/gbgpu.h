@@ -10,7 +10,8 @@
  *   PosdbTable::setQueryTermInfo Posdb.cpp:4354-4869   internal (host plan)
  *   PosdbTable::intersectLists10_r Posdb.cpp:5437-7806 gbgpu_query / _resident
  *   TopTree::addNode / getHighNode TopTree.cpp:195-516 gbgpu_result (high -> low)
- *   Msg3a::mergeLists           Msg3a.cpp:971-1503     gbgpu_merge_topk
+ *   Msg3a::mergeLists           Msg3a.cpp:971-1503     gbgpu_allgather_topk (RCCL) /
+ *                                                      gbgpu_merge_topk (host lists)
  *   RdbList::posdbMerge_r       RdbList.cpp:3065-3568  gbgpu_merge_posdb
  *
  * Conventions: plain pointers and sizes only; the caller owns
@@ -175,6 +176,30 @@ int gbgpu_merge_topk(const int64_t *const *shard_docids, const float *const *sha
                      const int32_t *shard_counts, int nshards, int32_t k,
                      int64_t *out_docids, double *out_scores, int32_t *out_n);
 
+/* Msg39 -> Msg3a over RCCL: one context per GPU, each
+ * holding one docid range of the index (a shard).  Rank 0 makes the id with
+ * gbgpu_comm_unique_id and the caller ships it to every rank; each rank then
+ * calls gbgpu_comm_init (collective).  gbgpu_allgather_topk replaces the
+ * collect of a slot's enqueued query: that shard's reply -- the first
+ * min(nodes, k) of its TopTree and its hit count -- is all-gathered over
+ * xGMI and merged on the device by Msg3a::mergeLists' rules (Msg3a.cpp:
+ * 1315-1467: score desc as double, ties to the lower docid, a docid taken
+ * once, first k; the clusterdb site cap of 1342-1379 needs cluster records
+ * and is not applied).  Every rank receives the same merged list and the
+ * summed hit count; `local` (may be NULL) receives the shard's own result.
+ * Collective: every rank calls it once per query, in the same order. */
+/* The device merge gbgpu_allgather_topk runs after its all-gather, on replies
+ * given from the host (one per shard: counts[r] entries, best first, and the
+ * shard's hit count); for checking the merge without a multi-GPU node. */
+int gbgpu_merge_replies_device(gbgpu_ctx *ctx, int nranks, int32_t k, const int32_t *counts, const int64_t *shard_hits,
+                               const int64_t *const *shard_docids, const float *const *shard_scores,
+                               int64_t *docids, double *scores, int32_t *n, int64_t *hits);
+#define GBGPU_COMM_ID_BYTES 128
+int gbgpu_comm_unique_id(uint8_t *id);
+int gbgpu_comm_init(gbgpu_ctx *ctx, int nranks, int rank, const uint8_t *id);
+int gbgpu_allgather_topk(gbgpu_ctx *ctx, int slot, int32_t k, int64_t *docids, double *scores, int32_t *n,
+                         int64_t *hits, gbgpu_result *local);
+
 /* RdbList::posdbMerge_r (RdbList.cpp:3065-3568), as RdbList::merge_r
  * (RdbList.cpp:1658-1756) calls it after prepareForMerge (410-491): merge n
  * (<= 256) sorted posdb lists, oldest first, each starting with an 18-byte
@@ -207,6 +232,17 @@ int gbgpu_merge_timings(gbgpu_ctx *ctx, float *ms6, int64_t *nkeys, int64_t *nti
 int gbgpu_set_profiling(gbgpu_ctx *ctx, int enable);
 int gbgpu_slot_timings(gbgpu_ctx *ctx, int slot, float *ms6, int64_t *scan_bytes);
 int gbgpu_last_timings(gbgpu_ctx *ctx, float *ms6, int64_t *scan_bytes); /* slot 0 */
+/* Work counts of a slot's last collected query, for per-kernel rooflines:
+ * [0] bytes of every list it scanned, [1] of the smallest group's lists
+ * (candidate extraction), [2] of the probed lists, [3] candidates,
+ * [4] survivors (hits), [5] bytes of the survivors' runs (mini-merge input,
+ * one copy per group a list serves), [6] TopTree nodes (site clustering). */
+int gbgpu_slot_stats(gbgpu_ctx *ctx, int slot, int64_t *stats8);
+
+/* The achievable-HBM ceiling of SURVEY.md §8(d): 16-B/lane streaming read and
+ * copy kernels over `bytes`-sized buffers (give >> 256 MiB), `iters` passes
+ * each; GB/s of bytes read (read) and read + written (copy). */
+int gbgpu_bandwidth_ceiling(gbgpu_ctx *ctx, int64_t bytes, int iters, double *read_gbps, double *copy_gbps);
 
 #ifdef __cplusplus
 }

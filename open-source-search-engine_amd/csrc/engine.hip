@@ -36,6 +36,7 @@
 // synchronisation happens between kernels: counts live in device memory and
 // grids are sized from host-known upper bounds.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cerrno>
@@ -70,6 +71,21 @@ constexpr int SEL_BINS = 4096;                   // radix-select bins per pass
 constexpr int TREE_CAP = 4096;                   // site-clustering TopTree nodes held in LDS
 constexpr int LIST_PAD = CHUNK_LOAD + 128;
 
+// A list re-shrunk by a later group (DevList::owner_group): its buffer then
+// holds the first shrink's output P (the survivors' runs) followed by the
+// list's own bytes from offset |P| on, and the re-shrink's copy of the LAST
+// survivor run takes every following unit whose byte 0 has the 6-byte bit
+// (Posdb.cpp:5384-5395 reads past P): that run grows by E units.
+struct ListExt {
+  unsigned long long units;  // |P| in 6-byte units
+  unsigned long long dmax;   // docid of the last survivor with a run in the list
+  unsigned long long off;    // arena offset of that survivor's relocated records (reloc)
+  uint32_t E;                // units the re-shrunk copy of that run gains
+  uint32_t slot1;            // its candidate slot + 1 (0: none)
+  uint32_t reloc;            // its mini-merge records live at `off` (room for the extra units)
+  uint32_t pad;
+};
+
 struct Counters {
   uint32_t filtered;  // m_filtered: scored docids dropped by the paging filter (Posdb.cpp:7327-7347)
   uint32_t corrupt;
@@ -78,7 +94,10 @@ struct Counters {
   uint32_t anysurv;  // bit l: list l has a run in some survivor
   uint32_t tree_n;   // site clustering: TopTree nodes written by k_tree_replay
   uint32_t tree_err; // site clustering: the tree outgrew the replay's LDS (TC nodes)
-  uint32_t pad[3];
+  uint32_t unsup;    // a re-shrink would copy a misparsed run (not emulated): EUNSUPPORTED
+  uint32_t pad[2];
+  unsigned long long dmax_all;  // largest survivor docid
+  ListExt ext[MAXL];
 };
 
 // radix-select state (3 passes over the 32-bit score keys: 12+12+8 bits)
@@ -810,8 +829,12 @@ struct BlkTot {
 template <int CMODE>
 __global__ void __launch_bounds__(BLOCK) k_compact(const DevPlan *pl, const uint32_t *lmask, const uint32_t *ulen,
                                                    uint64_t slot_ub, Counters *ctr, uint32_t *surv,
-                                                   unsigned long long *surv_off, uint32_t *surv_lm, BlkTot *blk) {
+                                                   unsigned long long *surv_off, uint32_t *surv_lm, BlkTot *blk,
+                                                   const Loc *loc, const uint64_t *cand) {
   __shared__ uint32_t tmp[BLOCK / 64];
+  __shared__ uint32_t s_xu[MAXL];            // CMODE 0/1: re-shrunk lists' survivor run units
+  __shared__ unsigned long long s_xd[MAXL];  // ... and their last survivor docid
+  __shared__ unsigned long long s_dall;
   __shared__ uint32_t s_base_i;
   __shared__ uint32_t s_any;
   __shared__ unsigned long long s_base_u;
@@ -823,8 +846,16 @@ __global__ void __launch_bounds__(BLOCK) k_compact(const DevPlan *pl, const uint
   if (threadIdx.x < MAXL) s_gbits[threadIdx.x] = threadIdx.x < (unsigned)pl->nlists ? pl->lists[threadIdx.x].group_bits : 0;
   if (threadIdx.x < MAXG0 + 1) s_beg[threadIdx.x] = threadIdx.x <= (unsigned)g0n ? pl->g0base[threadIdx.x] : ~0ull;
   if (threadIdx.x < MAXG0) s_end[threadIdx.x] = threadIdx.x < (unsigned)g0n ? pl->g0base[threadIdx.x] + ctr->g0count[threadIdx.x] : 0;
-  if (threadIdx.x == 0) s_any = 0;
+  if (threadIdx.x == 0) {
+    s_any = 0;
+    s_dall = 0;
+  }
+  if (CMODE != 2 && threadIdx.x < MAXL) {
+    s_xu[threadIdx.x] = 0;
+    s_xd[threadIdx.x] = 0;
+  }
   __syncthreads();
+  const uint32_t xmask = pl->reshare_mask;
   // a thread's slots: strided over the block (coalesced) -- or, ordered, 16
   // consecutive ones, so thread order is slot order inside the block
   const uint64_t s0 = (uint64_t)blockIdx.x * CTILE + (CMODE ? threadIdx.x * CSPT : threadIdx.x);
@@ -856,6 +887,15 @@ __global__ void __launch_bounds__(BLOCK) k_compact(const DevPlan *pl, const uint
     okm |= 1u << q;
     nok++;
     utot += u_s;
+    if (CMODE != 2 && xmask) {
+      const unsigned long long d = cand[s];
+      atomicMax(&s_dall, d);
+      for (uint32_t x = lm & xmask; x; x &= x - 1) {
+        const int l = __ffs(x) - 1;
+        atomicAdd(&s_xu[l], loc[(uint64_t)l * slot_ub + s].len);
+        atomicMax(&s_xd[l], d);
+      }
+    }
   }
   uint32_t tot_n, tot_u;
   const uint32_t ex_n = block_exclusive_scan(nok, tmp, &tot_n);
@@ -879,6 +919,11 @@ __global__ void __launch_bounds__(BLOCK) k_compact(const DevPlan *pl, const uint
     }
     if (CMODE != 2 && (s_any & ~__hip_atomic_load(&ctr->anysurv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)))
       atomicOr(&ctr->anysurv, s_any);
+    if (CMODE != 2 && xmask && s_dall) atomicMax(&ctr->dmax_all, s_dall);
+  }
+  if (CMODE != 2 && xmask && threadIdx.x < MAXL && s_xu[threadIdx.x]) {
+    atomicAdd(&ctr->ext[threadIdx.x].units, (unsigned long long)s_xu[threadIdx.x]);
+    atomicMax(&ctr->ext[threadIdx.x].dmax, s_xd[threadIdx.x]);
   }
   if (CMODE == 1) return;  // uniform
   __syncthreads();
@@ -893,6 +938,128 @@ __global__ void __launch_bounds__(BLOCK) k_compact(const DevPlan *pl, const uint
     i++;
     off += units[q];
   }
+}
+
+// The re-shrink of each list several groups use (ListExt): E = the units
+// from |P| on whose byte 0 has the 6-byte bit (stopping at the list end),
+// added to the last survivor run's copy for every use but the first -- its
+// slot's arena units grow accordingly before the offsets are scanned.  The
+// re-shrink then parses on from |P|+E: an aligned parse (a true run head
+// there) can match no survivor any more (every survivor run of the list is
+// in P); a misaligned one reads garbage docids, and one equal to a later
+// survivor would copy a misparsed run -- not emulated, flagged instead
+// (GBGPU_EUNSUPPORTED; about 2^-20 per query).  One wave per list.
+__device__ bool slot_is_survivor(const DevPlan *pl, const uint32_t *lmask, uint64_t s) {
+  uint32_t gm = 0;
+  for (uint32_t x = lmask[s]; x; x &= x - 1) gm |= pl->lists[__ffs(x) - 1].group_bits;
+  return ((gm & pl->pos_mask) == pl->pos_mask) && !(gm & NEG_BIT);
+}
+
+// slot of candidate docid d in any array, if that slot survived; ~0 if none
+__device__ uint64_t survivor_slot(const DevPlan *pl, const Counters *ctr, const uint64_t *cand,
+                                  const uint32_t *lmask, uint64_t d, int lane) {
+  for (int k = 0; k < pl->g0n; k++) {
+    const uint64_t *ck = cand + pl->g0base[k];
+    const uint32_t n = ctr->g0count[k];
+    const uint32_t i = wave_lower_bound(ck, n, d, lane);
+    if (i < n && ck[i] == d && slot_is_survivor(pl, lmask, pl->g0base[k] + i)) return pl->g0base[k] + i;
+  }
+  return ~0ull;
+}
+
+__global__ void __launch_bounds__(64) k_ext_walk(const DevPlan *pl, Counters *ctr, const uint64_t *cand,
+                                                 const uint32_t *lmask, const uint32_t *ulen,
+                                                 unsigned long long arena_cap) {
+  const int lane = threadIdx.x;
+  for (uint32_t xm = pl->reshare_mask; xm; xm &= xm - 1) {
+    const int l = __ffs(xm) - 1;
+    ListExt &x = ctr->ext[l];
+    if (x.units == 0) continue;  // no survivor run in the list
+    const DevList &L = pl->lists[l];
+    gu8 *p = gl(L.p);
+    const uint64_t P = x.units;
+    uint64_t u = P;
+    for (;;) {  // E: consecutive 6-byte-bit units from |P|
+      const uint64_t v = u + lane;
+      const bool six = v < L.units && (p[v * 6] & 0x04);
+      const uint64_t m = __ballot(!six);
+      if (m) {
+        u += (uint64_t)(__ffsll((unsigned long long)m) - 1);
+        break;
+      }
+      u += 64;
+    }
+    const uint64_t s = survivor_slot(pl, ctr, cand, lmask, x.dmax, lane);
+    if (lane == 0) {
+      x.E = (uint32_t)(u - P);
+      x.slot1 = s == ~0ull ? 0u : (uint32_t)(s + 1);
+      x.reloc = 0;
+    }
+    // the parse after the copy: only a misaligned one can match again
+    if (x.dmax >= ctr->dmax_all) continue;  // that run was the last survivor: done
+    uint64_t h = u;
+    bool settled = false;
+    for (int step = 0; step < 4096 && !settled; step++) {
+      if (h >= L.units) {
+        settled = true;
+        break;
+      }
+      gu8 *k = p + h * 6;
+      if ((k[1] & 0x02) && !(k[0] & 0x04)) {  // a true run head: aligned
+        settled = true;
+        break;
+      }
+      // the docid shrinkSubLists compares: u32 at +8 and byte 7 & 0xfc
+      uint64_t g = 0;
+      const uint64_t hb = h * 6 + 7;
+      for (int b = 4; b >= 0; b--) g = (g << 8) | p[hb + b];
+      g = (g & ~3ull) >> 2;
+      if (g > ctr->dmax_all) {  // past every survivor: the loop ends
+        settled = true;
+        break;
+      }
+      if (g > x.dmax && survivor_slot(pl, ctr, cand, lmask, g, lane) != ~0ull) break;
+      h += 2;
+      for (;;) {
+        const uint64_t v = h + lane;
+        const bool six = v < L.units && (p[v * 6] & 0x04);
+        const uint64_t m = __ballot(!six);
+        if (m) {
+          h += (uint64_t)(__ffsll((unsigned long long)m) - 1);
+          break;
+        }
+        h += 64;
+      }
+    }
+    if (!settled && lane == 0) ctr->unsup = 1;  // a misparsed run would be copied
+  }
+  // the survivors whose re-shrunk copies grow get their records moved to the
+  // arena's end, with room for the extra units of every list extending them
+  if (lane != 0) return;
+  unsigned long long top = ctr->surv_top & ((1ull << 36) - 1);
+  for (uint32_t xm = pl->reshare_mask; xm; xm &= xm - 1) {
+    const int l = __ffs(xm) - 1;
+    ListExt &x = ctr->ext[l];
+    if (!x.slot1 || !x.E || x.reloc) continue;
+    unsigned long long need = ulen[x.slot1 - 1];
+    for (uint32_t ym = pl->reshare_mask; ym; ym &= ym - 1) {
+      const int l2 = __ffs(ym) - 1;
+      if (ctr->ext[l2].slot1 == x.slot1) need += (unsigned long long)ctr->ext[l2].E * (uint32_t)(pl->lists[l2].uses - 1);
+    }
+    if (top + need > arena_cap) {
+      ctr->unsup = 1;
+      return;
+    }
+    for (uint32_t ym = pl->reshare_mask; ym; ym &= ym - 1) {
+      const int l2 = __ffs(ym) - 1;
+      if (ctr->ext[l2].slot1 == x.slot1) {
+        ctr->ext[l2].reloc = 1;
+        ctr->ext[l2].off = top;
+      }
+    }
+    top += need;
+  }
+  ctr->surv_top = (ctr->surv_top & ~((1ull << 36) - 1)) | top;
 }
 
 // exclusive scan of the blocks' (survivors, arena units) -> their offsets,
@@ -949,6 +1116,31 @@ __global__ void __launch_bounds__(1024) k_compact_scan(uint32_t nblk, BlkTot *bl
   if (threadIdx.x == 0) ctr->surv_top = ((unsigned long long)cn << 36) | cu;
 }
 
+// A survivor's run in list lid as group g's sublist x sees it: its own
+// units, and -- for a re-shrunk copy of the list's last survivor run
+// (ListExt) -- the E units that followed the first shrink's output in the
+// buffer, i.e. the list's units [|P|, |P|+E).  Key k of the run is at
+// k < len0 ? own + k : ext + (k - len0).
+struct SubRun {
+  gu8 *own, *ext;
+  uint32_t len0, len;
+  __device__ __forceinline__ gu8 *key(uint32_t k) const {
+    return k < len0 ? own + (size_t)k * 6 : ext + (size_t)(k - len0) * 6;
+  }
+};
+__device__ __forceinline__ SubRun sub_run(const DevPlan *pl, const Counters *ctr, const Loc *loc, uint64_t slot_ub,
+                                          int lid, int g, int x, uint64_t s) {
+  const Loc lc = loc[(uint64_t)lid * slot_ub + s];
+  gu8 *base = gl(pl->lists[lid].p);
+  SubRun r{base + (size_t)lc.unit * 6, base, lc.len, lc.len};
+  if ((pl->reshare_mask >> lid & 1) && !(g == pl->lists[lid].owner_group && x == pl->lists[lid].owner_sub) &&
+      ctr->ext[lid].slot1 == (uint32_t)(s + 1)) {
+    r.ext = base + (size_t)ctr->ext[lid].units * 6;
+    r.len += ctr->ext[lid].E;
+  }
+  return r;
+}
+
 // docids of the survivors (the vote buffer's docids, unordered)
 __global__ void k_gather_hits(const uint32_t *surv, const uint64_t *cand, uint32_t n, uint64_t *out) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) out[i] = cand[surv[i]];
@@ -969,8 +1161,8 @@ __device__ __forceinline__ uint64_t load6(gu8 *k) {
 }
 
 template <int NQ, int NS, class RP>
-__device__ __forceinline__ void score_survivor(const DevPlan *pl, uint32_t s, uint32_t lm, uint32_t anys,
-                                               const Loc *loc, uint64_t slot_ub, RP rec, float *smcol,
+__device__ __forceinline__ void score_survivor(const DevPlan *pl, const Counters *ctr, uint32_t s, uint32_t lm,
+                                               uint32_t anys, const Loc *loc, uint64_t slot_ub, RP rec, float *smcol,
                                                uint32_t *key_out, int diag) {
   const int ng = pl->ngroups;
   DocView<NQ, RP> dv;
@@ -988,27 +1180,30 @@ __device__ __forceinline__ void score_survivor(const DevPlan *pl, uint32_t s, ui
     const int gns = pl->gnsub[j];
     // this group's runs: cursor, end, flags (m_bigramFlags of the shrunk
     // sublist index: lists shrunk to empty are not sublists any more)
-    uint32_t cu[NS], ce[NS];
+    uint32_t cu[NS], ce[NS], c0[NS];
     uint8_t cfl[NS];
     bool live[NS];
-    gu8 *src[NS];
+    gu8 *src[NS], *xsrc[NS];
     int newIdx = 0;
 #pragma unroll
     for (int x = 0; x < NS; x++) {
       live[x] = false;
       cu[x] = ce[x] = 0;
       cfl[x] = 0;
-      src[x] = nullptr;
+      src[x] = xsrc[x] = nullptr;
+      c0[x] = 0;
       if (x < gns) {
         const int lid = pl->gsub[j][x];
         if (anys >> lid & 1) {
           cfl[x] = pl->gsubflags[j][newIdx];
           newIdx++;
           if (lm >> lid & 1) {
-            const Loc lc = loc[(uint64_t)lid * slot_ub + s];
-            src[x] = gl(pl->lists[lid].p) + (size_t)lc.unit * 6;
+            const SubRun sr = sub_run(pl, ctr, loc, slot_ub, lid, j, x, s);
+            src[x] = sr.own;
+            xsrc[x] = sr.ext;
+            c0[x] = sr.len0;
             cu[x] = 0;
-            ce[x] = lc.len;
+            ce[x] = sr.len;
             live[x] = true;
           }
         }
@@ -1016,7 +1211,9 @@ __device__ __forceinline__ void score_survivor(const DevPlan *pl, uint32_t s, ui
     }
     // x must be a compile-time index (unrolled loops): a runtime one would
     // put src[] in scratch
-    auto unit_at = [&](int x, uint32_t c) -> uint64_t { return load6(src[x] + (size_t)c * 6); };
+    auto unit_at = [&](int x, uint32_t c) -> uint64_t {
+      return load6(c < c0[x] ? src[x] + (size_t)c * 6 : xsrc[x] + (size_t)(c - c0[x]) * 6);
+    };
     uint64_t ck[NS];
     bool cfirst[NS];
 #pragma unroll
@@ -1140,9 +1337,15 @@ __global__ void __launch_bounds__(SCORE_TPB) k_score(const DevPlan *pl, const ui
     bool filt = false;
     if (i < nsurv) {
       const uint32_t s = surv[i];
-      auto *rec = (__attribute__((address_space(1))) uint64_t *)(arena + surv_off[i]);
+      const uint32_t lm = surv_lm[i];
+      unsigned long long off = surv_off[i];
+      for (uint32_t x = lm & pl->reshare_mask; x; x &= x - 1) {  // relocated (k_ext_walk)
+        const ListExt &e = ctr->ext[__ffs(x) - 1];
+        if (e.reloc && e.slot1 == s + 1) off = e.off;
+      }
+      auto *rec = (__attribute__((address_space(1))) uint64_t *)(arena + off);
       uint32_t key;
-      score_survivor<NQ, NS>(pl, s, surv_lm[i], anys, loc, slot_ub, rec, s_sm + threadIdx.x, &key, diag);
+      score_survivor<NQ, NS>(pl, ctr, s, lm, anys, loc, slot_ub, rec, s_sm + threadIdx.x, &key, diag);
       const uint64_t d = cand[s];
       // the paging filter of a widget's next page (Posdb.cpp:7327-7347):
       // m_filtered counts the scored docids it drops
@@ -1209,8 +1412,8 @@ __device__ __forceinline__ float max_score_tail(const DevPlan *pl, BoundCore c, 
   return score;
 }
 
-__device__ BoundCore group_bound_core(const DevPlan *pl, int g, uint32_t s, uint32_t lm, const Loc *loc,
-                                      uint64_t slot_ub) {
+__device__ BoundCore group_bound_core(const DevPlan *pl, const Counters *ctr, int g, uint32_t s, uint32_t lm,
+                                      const Loc *loc, uint64_t slot_ub) {
   const Weights &W = s_weights;
   float best = -1.0f;
   unsigned bestDR = 0;
@@ -1221,18 +1424,18 @@ __device__ BoundCore group_bound_core(const DevPlan *pl, int g, uint32_t s, uint
     const int lid = pl->gsub[g][x];
     if (!(lm >> lid & 1)) continue;  // m_savedCursor[j] == NULL
     if (pl->gflags0[g] & BF_HALFSTOPWIKIBIGRAM) hs = true;
-    const Loc lc = loc[(uint64_t)lid * slot_ub + s];
-    gu8 *run = gl(pl->lists[lid].p) + (size_t)lc.unit * 6;
+    const SubRun run = sub_run(pl, ctr, loc, slot_ub, lid, g, x, s);
     if (sr == -1) {  // getSiteRank / getLangId of the 12-byte run head
-      const uint32_t b0 = run[0], b6 = run[6], b7 = run[7];
+      gu8 *h = run.own;
+      const uint32_t b0 = h[0], b6 = h[6], b7 = h[7];
       sr = (int)(((b6 >> 5) | ((b7 & 1) << 3)) & 0x0f);
       lang = (int)((b6 & 0x1f) | ((b0 & 0x08) ? 0x20 : 0));
     }
     // keys from the last 6-byte key down to the first one, then the head
     // (Posdb.cpp:7851-7897); a body key weaker than the best ends the list
-    for (int k = (int)lc.len - 1; k >= 0; k--) {
+    for (int k = (int)run.len - 1; k >= 0; k--) {
       if (k == 1) continue;  // second half of the 12-byte head
-      gu8 *dc = run + (size_t)k * 6;
+      gu8 *dc = run.key((uint32_t)k);
       const uint32_t hg = (dc[3] >> 2) & 0x0f;
       if (hg == GB_HG_INLINKTEXT) return BoundCore{-1, 0.0f};
       const float w = W.hashgroup[hg];
@@ -1268,24 +1471,24 @@ __device__ BoundCore group_bound_core(const DevPlan *pl, int g, uint32_t s, uint
 
 // ring-buffer slots this wave's lanes write for one group's runs (value v);
 // returns the slot of the head of the group's last run (ourFirstPos)
-__device__ int ring_fill(const DevPlan *pl, int g, uint32_t s, uint32_t lm, const Loc *loc, uint64_t slot_ub,
-                         uint8_t *ring, uint8_t v, int lane) {
+__device__ int ring_fill(const DevPlan *pl, const Counters *ctr, int g, uint32_t s, uint32_t lm, const Loc *loc,
+                         uint64_t slot_ub, uint8_t *ring, uint8_t v, int lane) {
   int first = -1;
   const int gns = pl->gnsub[g];
   for (int x = 0; x < gns; x++) {
     const int lid = pl->gsub[g][x];
     if (!(lm >> lid & 1)) continue;
-    const Loc lc = loc[(uint64_t)lid * slot_ub + s];
-    gu8 *run = gl(pl->lists[lid].p) + (size_t)lc.unit * 6;
-    for (uint32_t k = lane; k < lc.len; k += 64) {
+    const SubRun run = sub_run(pl, ctr, loc, slot_ub, lid, g, x, s);
+    for (uint32_t k = lane; k < run.len; k += 64) {
       if (k == 1) continue;
-      gu8 *kp = run + (size_t)k * 6;
+      gu8 *kp = run.key(k);
       const uint32_t wp = ((uint32_t)kp[2] | ((uint32_t)kp[3] << 8) | ((uint32_t)kp[4] << 16) |
                            ((uint32_t)kp[5] << 24)) >> 14;
       ring[wp & (RING - 1)] = v;
     }
-    first = (int)((((uint32_t)run[2] | ((uint32_t)run[3] << 8) | ((uint32_t)run[4] << 16) |
-                    ((uint32_t)run[5] << 24)) >> 14) & (RING - 1));
+    gu8 *h = run.own;
+    first = (int)((((uint32_t)h[2] | ((uint32_t)h[3] << 8) | ((uint32_t)h[4] << 16) |
+                    ((uint32_t)h[5] << 24)) >> 14) & (RING - 1));
   }
   return first;
 }
@@ -1368,7 +1571,7 @@ __global__ void __launch_bounds__(64 * BND_WAVES) k_bound(const DevPlan *pl, con
     // lane g: getMaxPossibleScore's scan of group g
     BoundCore core{0, 0.0f};
     if (lane < ng && !(pl->gflags0[lane] & (BF_NEGATIVE | BF_FACET)))
-      core = group_bound_core(pl, lane, s, lm, loc, slot_ub);
+      core = group_bound_core(pl, ctr, lane, s, lm, loc, slot_ub);
     float B = INF;
     // filter 1 (m_doMaxScoreAlgo): bestDist 0, qdist 0 (Posdb.cpp:6327-6346)
     if (pl->do_max_score && lane < ng && !(pl->gflags0[lane] & (BF_NEGATIVE | BF_FACET))) {
@@ -1382,12 +1585,12 @@ __global__ void __launch_bounds__(64 * BND_WAVES) k_bound(const DevPlan *pl, con
       uint4 *r4 = reinterpret_cast<uint4 *>(ring);
       for (int q = lane; q < RING / 16; q += 64) r4[q] = make_uint4(~0u, ~0u, ~0u, ~0u);
       wave_lds_sync();
-      const int ourFirstPos = ring_fill(pl, m, s, lm, loc, slot_ub, ring, (uint8_t)m, lane);
+      const int ourFirstPos = ring_fill(pl, ctr, m, s, lm, loc, slot_ub, ring, (uint8_t)m, lane);
       const float tfw_m = pl->tfw[m];
       for (int g = 0; g < ng; g++) {
         if (g == m || (pl->gflags0[g] & (BF_NEGATIVE | BF_FACET))) continue;
         wave_lds_sync();
-        ring_fill(pl, g, s, lm, loc, slot_ub, ring, (uint8_t)g, lane);
+        ring_fill(pl, ctr, g, s, lm, loc, slot_ub, ring, (uint8_t)g, lane);
         wave_lds_sync();
         BoundCore cg;
         cg.state = __shfl(core.state, g, 64);
@@ -1854,6 +2057,116 @@ __global__ void __launch_bounds__(1024) k_select_final(const Select *sel, const 
   }
 }
 
+// ------------------------------------------------- Msg3a exchange (RCCL)
+// Every GPU holds one docid range of the index (one Msg39 shard each); its
+// reply -- the top of its TopTree and its hit count -- is all-gathered over
+// xGMI and every rank merges the replies as Msg3a::mergeLists does
+// (Msg3a.cpp:1315-1467): the highest score (as double) first, ties to the
+// lower docid, a docid already taken skipped, until docsToGet.
+struct XHead {
+  int32_t n;
+  int32_t pad;
+  int64_t hits;
+};
+constexpr uint32_t XMAX = 4096;  // merged entries (docsToGet) the exchange handles
+struct XRec {
+  uint32_t key;  // order-preserving float score key
+  uint32_t pad;
+  uint64_t docid;
+};
+
+// this shard's Msg39Reply: min(nodes, docsToGet) entries of its result block
+__global__ void k_xpack(const Counters *ctr, const uint32_t *keys, const uint64_t *docs, uint32_t k, uint32_t kq,
+                        uint8_t *send) {
+  XHead *h = reinterpret_cast<XHead *>(send);
+  XRec *r = reinterpret_cast<XRec *>(send + sizeof(XHead));
+  __shared__ uint32_t s_n;
+  if (threadIdx.x == 0) s_n = 0;
+  __syncthreads();
+  const uint32_t lim = min(k, kq);
+  for (uint32_t i = threadIdx.x; i < lim; i += blockDim.x) {
+    const uint32_t key = keys[i];
+    r[i].key = key;
+    r[i].pad = 0;
+    r[i].docid = docs[i];
+    // keys are written best first and end at the first 0 (empty) key
+    if (key && (i + 1 == lim || keys[i + 1] == 0)) s_n = i + 1;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    h->n = (int32_t)s_n;
+    h->pad = 0;
+    h->hits = (int64_t)(ctr->surv_top >> 36);
+  }
+}
+
+// one wave: the k-way merge of the shards' replies (each sorted best first)
+__global__ void __launch_bounds__(64) k_xmerge(const uint8_t *recv, int nranks, uint32_t k, size_t stride,
+                                               uint8_t *out) {
+  const int lane = threadIdx.x;
+  XHead *oh = reinterpret_cast<XHead *>(out);
+  double *osc = reinterpret_cast<double *>(out + sizeof(XHead));
+  int64_t *odoc = reinterpret_cast<int64_t *>(out + sizeof(XHead) + 8 * (size_t)k);
+  // lane r < nranks follows shard r
+  uint32_t cur = 0, n = 0;
+  const XRec *rr = nullptr;
+  int64_t hits = 0;
+  if (lane < nranks) {
+    const XHead *h = reinterpret_cast<const XHead *>(recv + stride * lane);
+    n = (uint32_t)h->n;
+    hits = h->hits;
+    rr = reinterpret_cast<const XRec *>(recv + stride * lane + sizeof(XHead));
+  }
+  for (int off = 32; off > 0; off >>= 1) hits += __shfl_xor(hits, off, 64);
+  __shared__ uint64_t s_doc[XMAX];
+  __shared__ uint32_t s_key[XMAX];
+  uint32_t taken = 0;
+  for (;;) {
+    if (taken >= k) break;
+    // maxj: the shard whose head has the highest score, ties to the lower docid
+    const bool has = lane < nranks && cur < n;
+    const uint32_t key = has ? rr[cur].key : 0;
+    const uint64_t doc = has ? rr[cur].docid : ~0ull;
+    uint32_t bk = key;
+    uint64_t bd = doc;
+    int bl = has ? lane : 64;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const uint32_t ok = __shfl_xor(bk, off, 64);
+      const uint64_t od = __shfl_xor(bd, off, 64);
+      const int ol = __shfl_xor(bl, off, 64);
+      if (ol < 64 && (bl == 64 || ok > bk || (ok == bk && (od < bd || (od == bd && ol < bl))))) {
+        bk = ok;
+        bd = od;
+        bl = ol;
+      }
+    }
+    if (bl == 64) break;  // every shard exhausted
+    if (lane == bl) cur++;
+    // a docid already in the merged list is skipped (Msg3a.cpp:1381-1385)
+    bool dup = false;
+    for (uint32_t t = lane; t < taken; t += 64) dup |= s_doc[t] == bd;
+    if (__ballot(dup)) continue;
+    if (lane == 0) {
+      s_key[taken] = bk;
+      s_doc[taken] = bd;
+    }
+    wave_lds_sync();
+    taken++;
+  }
+  for (uint32_t t = lane; t < taken; t += 64) {
+    const uint32_t bk = s_key[t];
+    const uint32_t b = (bk & 0x80000000u) ? (bk & 0x7fffffffu) : ~bk;
+    osc[t] = (double)__uint_as_float(b);  // the wire's double score (Msg3a.cpp:1443)
+    odoc[t] = (int64_t)s_doc[t];
+  }
+  if (lane == 0) {
+    oh->n = (int32_t)taken;
+    oh->pad = 0;
+    oh->hits = hits;
+  }
+}
+
 // ------------------------------------------------------------- host side
 static Weights host_weights() {  // initWeights, Posdb.cpp:1105-1197
   Weights w;
@@ -2055,13 +2368,17 @@ struct QuerySlot {
   size_t res_bytes = 0;
   int32_t docs_wanted = 0;
   int64_t scan_bytes = 0;
+  int64_t g0_bytes = 0, probe_bytes = 0;  // list bytes of candidate extraction / of the probe scan
+  int64_t stats[8] = {};                   // gbgpu_slot_stats of the last collected query
   hipEvent_t ev[7] = {};
+  hipEvent_t ev_done = nullptr;  // the query's device work is done (the exchange waits on it)
   float last_ms[6] = {0, 0, 0, 0, 0, 0};
 
   int init() {
     if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return GBGPU_EHIP;
     for (auto &e : ev)
       if (hipEventCreate(&e) != hipSuccess) return GBGPU_EHIP;
+    if (hipEventCreateWithFlags(&ev_done, hipEventDisableTiming) != hipSuccess) return GBGPU_EHIP;
     return 0;
   }
   void release() {
@@ -2075,6 +2392,7 @@ struct QuerySlot {
     h_stage = h_res = nullptr;
     for (auto &e : ev)
       if (e) (void)hipEventDestroy(e);
+    if (ev_done) (void)hipEventDestroy(ev_done);
     if (stream) (void)hipStreamDestroy(stream);
     stream = nullptr;
   }
@@ -2097,8 +2415,17 @@ struct gbgpu_ctx {
   bool profiling = false;
   int probe_mode = 0;  // diagnostic only (GBGPU_PROBE_MODE)
   int score_mode = 0;  // diagnostic only (GBGPU_SCORE_MODE): 1 mini-merge without scoring
+  int debug_ext = 0;   // diagnostic only (GBGPU_DEBUG_EXT): print the re-shrink table per query
   std::mutex merge_mu;
   gbmerge::MergeState *merge = nullptr;  // created on first use (merge.hip)
+  // Msg3a exchange over RCCL (gbgpu_comm_init / gbgpu_allgather_topk)
+  std::mutex x_mu;
+  ncclComm_t comm = nullptr;
+  int nranks = 1, rank = 0;
+  hipStream_t xstream = nullptr;
+  DevBuf xsend, xrecv, xout;
+  uint8_t *h_xout = nullptr;
+  size_t h_xout_cap = 0;
 };
 
 // result block layout: [Counters | keys k | docids k]
@@ -2252,6 +2579,7 @@ static int enqueue_tree_emit(QuerySlot &q, int32_t dw) {
                      (const float *)nullptr, q.tree.as<TreeState>(), tree_params(dw, TREE_FINAL),
                      q.res.as<uint32_t>(res_keys_off()), q.res.as<uint64_t>(res_docs_off(q.k)));
   HIPCHECK(hipGetLastError());
+  HIPCHECK(hipEventRecord(q.ev_done, st));
   HIPCHECK(hipMemcpyAsync(q.h_res, q.res.p, q.res_bytes, hipMemcpyDeviceToHost, st));
   q.pending = true;
   return 0;
@@ -2317,6 +2645,9 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
     P.lists[id].group_bits = 0;
     P.lists[id].g0_array = -1;
     P.lists[id].probe = 0;
+    P.lists[id].owner_group = -1;
+    P.lists[id].owner_sub = -1;
+    P.lists[id].uses = 0;
     return id;
   };
   for (int j = 0; j < hp.ngroups; j++) {
@@ -2336,6 +2667,16 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
       if (id < 0) return GBGPU_EUNSUPPORTED;
       P.gsub[j][x] = (uint8_t)id;
       P.lists[id].group_bits |= neg ? NEG_BIT : (1u << j);
+      if (!neg) {
+        // shrinkSubLists' in-place order: groups in index order, sublists in
+        // order (Posdb.cpp:5906-5914); the first use sees the list clean
+        if (P.lists[id].uses++ == 0) {
+          P.lists[id].owner_group = (int16_t)j;
+          P.lists[id].owner_sub = (int16_t)x;
+        } else {
+          P.reshare_mask |= 1u << id;
+        }
+      }
     }
   }
   // candidate arrays: distinct lists of the smallest group, in sublist order
@@ -2407,12 +2748,21 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
     for (uint32_t u = 0; u < units; u += span) q.pw.push_back({(uint32_t)id, u, std::min(units, u + span)});
   }
   q.scan_bytes = scan;
+  q.g0_bytes = 0;
+  q.probe_bytes = 0;
+  for (int id = 0; id < P.nlists; id++) {
+    if (P.lists[id].g0_array >= 0) q.g0_bytes += (int64_t)P.lists[id].units * 6;
+    if (P.lists[id].probe) q.probe_bytes += (int64_t)P.lists[id].units * 6;
+  }
   // scratch upper bound: every group instance can use all of its list once
   uint64_t scratch_ub = 1;
   for (int j = 0; j < hp.ngroups; j++) {
     if (P.gflags0[j] & BF_NEGATIVE) continue;
     for (int x = 0; x < P.gnsub[j]; x++) scratch_ub += P.lists[P.gsub[j][x]].units;
   }
+  // re-shrunk lists: one survivor per list has its records relocated to the
+  // arena's end with room for the extra units (k_ext_walk checks the fit)
+  if (P.reshare_mask) scratch_ub += scratch_ub / 2 + 4096;
   if (scratch_ub >= (1ull << 36)) return GBGPU_ECAPACITY;
   const int k = q.k;
   const size_t o_chunks = align256(sizeof(DevPlan));
@@ -2509,18 +2859,25 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   }
   if (ctx->profiling) HIPCHECK(hipEventRecord(q.ev[2], st));
   const uint32_t cgrid = std::max(1u, (uint32_t)((slot_ub + CTILE - 1) / CTILE));
+  const uint64_t *dcand = q.cand.as<uint64_t>();
   if (!P.clustering) {
     hipLaunchKernelGGL(k_compact<0>, dim3(cgrid), dim3(BLOCK), 0, st, dpl, lmask, q.ulen.as<uint32_t>(), slot_ub,
                        dctr, q.surv.as<uint32_t>(), q.survoff.as<unsigned long long>(), q.survlm.as<uint32_t>(),
-                       (BlkTot *)nullptr);
+                       (BlkTot *)nullptr, loc, dcand);
   } else {
+    // ordered: site clustering's replay walks the survivors in docid order
     BlkTot *blk = q.blk.as<BlkTot>();
     hipLaunchKernelGGL(k_compact<1>, dim3(cgrid), dim3(BLOCK), 0, st, dpl, lmask, q.ulen.as<uint32_t>(), slot_ub,
-                       dctr, q.surv.as<uint32_t>(), q.survoff.as<unsigned long long>(), q.survlm.as<uint32_t>(), blk);
+                       dctr, q.surv.as<uint32_t>(), q.survoff.as<unsigned long long>(), q.survlm.as<uint32_t>(), blk,
+                       loc, dcand);
     hipLaunchKernelGGL(k_compact_scan, dim3(1), dim3(1024), 0, st, cgrid, blk, dctr);
     hipLaunchKernelGGL(k_compact<2>, dim3(cgrid), dim3(BLOCK), 0, st, dpl, lmask, q.ulen.as<uint32_t>(), slot_ub,
-                       dctr, q.surv.as<uint32_t>(), q.survoff.as<unsigned long long>(), q.survlm.as<uint32_t>(), blk);
+                       dctr, q.surv.as<uint32_t>(), q.survoff.as<unsigned long long>(), q.survlm.as<uint32_t>(), blk,
+                       loc, dcand);
   }
+  if (P.reshare_mask)
+    hipLaunchKernelGGL(k_ext_walk, dim3(1), dim3(64), 0, st, dpl, dctr, dcand, lmask, q.ulen.as<uint32_t>(),
+                       (unsigned long long)(q.scratch.cap / 8));
   if (ctx->profiling) HIPCHECK(hipEventRecord(q.ev[3], st));
   {
     int maxsub = 0;
@@ -2558,6 +2915,7 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
                        q.res.as<uint64_t>(res_docs_off(k)));
     q.replayed = true;
     if (ctx->profiling) HIPCHECK(hipEventRecord(q.ev[5], st));
+    HIPCHECK(hipEventRecord(q.ev_done, st));
     HIPCHECK(hipMemcpyAsync(q.h_res, q.res.p, q.res_bytes, hipMemcpyDeviceToHost, st));
     if (ctx->profiling) HIPCHECK(hipEventRecord(q.ev[6], st));
     q.pending = true;
@@ -2582,6 +2940,7 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   hipLaunchKernelGGL(k_select_final, dim3(1), dim3(1024), 0, st, dsel, akey, adoc, bkey, bdoc, (uint32_t)k,
                      q.res.as<uint32_t>(res_keys_off()), q.res.as<uint64_t>(res_docs_off(k)));
   if (ctx->profiling) HIPCHECK(hipEventRecord(q.ev[5], st));
+  HIPCHECK(hipEventRecord(q.ev_done, st));
   HIPCHECK(hipMemcpyAsync(q.h_res, q.res.p, q.res_bytes, hipMemcpyDeviceToHost, st));
   if (ctx->profiling) HIPCHECK(hipEventRecord(q.ev[6], st));
   q.pending = true;
@@ -2650,8 +3009,22 @@ static int collect(gbgpu_ctx *ctx, QuerySlot &q, gbgpu_result *out, std::vector<
   const uint64_t *docs = reinterpret_cast<const uint64_t *>(q.h_res + res_docs_off(q.k));
   out->hits = (int64_t)(c->surv_top >> 36);
   out->filtered = (int32_t)c->filtered;
+  {
+    int64_t ncand = 0;
+    for (int a = 0; a < MAXG0; a++) ncand += c->g0count[a];
+    const int64_t st[8] = {q.scan_bytes, q.g0_bytes, q.probe_bytes, ncand, out->hits,
+                           (int64_t)(c->surv_top & ((1ull << 36) - 1)) * 6, (int64_t)c->tree_n, 0};
+    std::memcpy(q.stats, st, sizeof st);
+  }
   if (c->corrupt) return GBGPU_ECORRUPT;
   if (c->tree_err) return GBGPU_ECAPACITY;
+  if (c->unsup) return GBGPU_EUNSUPPORTED;
+  if (ctx->debug_ext) {
+    for (int l = 0; l < MAXL; l++)
+      if (c->ext[l].units || c->ext[l].E)
+        std::fprintf(stderr, "gbgpu ext list %d units %llu dmax %llu E %u slot1 %u\n", l, c->ext[l].units,
+                     c->ext[l].dmax, c->ext[l].E, c->ext[l].slot1);
+  }
   if (hits_acc || out->hit_docids) {
     std::vector<int64_t> local;
     std::vector<int64_t> &h = hits_acc ? *hits_acc : local;
@@ -2907,6 +3280,7 @@ int gbgpu_open(int device, gbgpu_ctx **out) {
   }
   if (const char *pm = std::getenv("GBGPU_PROBE_MODE")) ctx->probe_mode = std::atoi(pm);
   if (const char *sm = std::getenv("GBGPU_SCORE_MODE")) ctx->score_mode = std::atoi(sm);
+  if (const char *de = std::getenv("GBGPU_DEBUG_EXT")) ctx->debug_ext = std::atoi(de);
   *out = ctx;
   return 0;
 }
@@ -2918,6 +3292,12 @@ void gbgpu_close(gbgpu_ctx *ctx) {
     ctx->slots[i]->release();
     delete ctx->slots[i];
   }
+  if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
+  if (ctx->xstream) (void)hipStreamDestroy(ctx->xstream);
+  ctx->xsend.release();
+  ctx->xrecv.release();
+  ctx->xout.release();
+  if (ctx->h_xout) (void)hipHostFree(ctx->h_xout);
   ctx->lists.clear();  // the last references: ListMem frees the device copies
   gbmerge::state_free(ctx->merge);
   if (ctx->d_flag) (void)hipFree(ctx->d_flag);
@@ -3091,8 +3471,212 @@ int gbgpu_slot_timings(gbgpu_ctx *ctx, int slot, float *ms6, int64_t *scan_bytes
   return 0;
 }
 
+int gbgpu_slot_stats(gbgpu_ctx *ctx, int slot, int64_t *stats8) {
+  QuerySlot *q = slot_of(ctx, slot);
+  if (!q || !stats8) return EINVAL;
+  std::memcpy(stats8, q->stats, sizeof q->stats);
+  return 0;
+}
+
+// ------------------------------------------------ bandwidth ceiling (§8(d))
+// The achievable-HBM reference the roofline is reported against beside the
+// 8 TB/s spec: 16-byte-per-lane streaming kernels over buffers far larger
+// than the 256 MiB Infinity Cache.
+__global__ void __launch_bounds__(256) k_stream_read(const v4u *a, size_t n, uint32_t *sink) {
+  uint32_t x = 0;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const v4u v = __builtin_nontemporal_load(a + i);
+    x ^= v.x ^ v.y ^ v.z ^ v.w;
+  }
+  if (x == 0x9e3779b9u) sink[0] = x;  // keeps the loads; practically never stores
+}
+__global__ void __launch_bounds__(256) k_stream_copy(const v4u *a, v4u *b, size_t n) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    __builtin_nontemporal_store(__builtin_nontemporal_load(a + i), b + i);
+}
+
+int gbgpu_bandwidth_ceiling(gbgpu_ctx *ctx, int64_t bytes, int iters, double *read_gbps, double *copy_gbps) {
+  if (!ctx || bytes < (1 << 20) || iters < 1) return EINVAL;
+  (void)hipSetDevice(ctx->device);
+  const size_t n = (size_t)bytes / 16;
+  v4u *a = nullptr, *b = nullptr;
+  uint32_t *sink = nullptr;
+  hipStream_t st = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  int rc = 0;
+  float ms = 0.0f;
+  if (hipMalloc(&a, n * 16) != hipSuccess || hipMalloc(&b, n * 16) != hipSuccess || hipMalloc(&sink, 4) != hipSuccess) {
+    rc = ENOMEM;
+    goto out;
+  }
+  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess || hipEventCreate(&e0) != hipSuccess ||
+      hipEventCreate(&e1) != hipSuccess) {
+    rc = GBGPU_EHIP;
+    goto out;
+  }
+  (void)hipMemsetAsync(a, 1, n * 16, st);
+  (void)hipMemsetAsync(b, 0, n * 16, st);
+  {
+    const uint32_t grid = 256 * 8;  // 8 blocks of 256 per CU
+    hipLaunchKernelGGL(k_stream_read, dim3(grid), dim3(256), 0, st, a, n, sink);
+    (void)hipEventRecord(e0, st);
+    for (int i = 0; i < iters; i++) hipLaunchKernelGGL(k_stream_read, dim3(grid), dim3(256), 0, st, a, n, sink);
+    (void)hipEventRecord(e1, st);
+    (void)hipEventSynchronize(e1);
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    if (read_gbps) *read_gbps = (double)n * 16 * iters / (ms * 1e-3) / 1e9;
+    hipLaunchKernelGGL(k_stream_copy, dim3(grid), dim3(256), 0, st, a, b, n);
+    (void)hipEventRecord(e0, st);
+    for (int i = 0; i < iters; i++) hipLaunchKernelGGL(k_stream_copy, dim3(grid), dim3(256), 0, st, a, b, n);
+    (void)hipEventRecord(e1, st);
+    (void)hipEventSynchronize(e1);
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    if (copy_gbps) *copy_gbps = 2.0 * (double)n * 16 * iters / (ms * 1e-3) / 1e9;
+    if (hipGetLastError() != hipSuccess) rc = GBGPU_EHIP;
+  }
+out:
+  if (e0) (void)hipEventDestroy(e0);
+  if (e1) (void)hipEventDestroy(e1);
+  if (st) (void)hipStreamDestroy(st);
+  if (a) (void)hipFree(a);
+  if (b) (void)hipFree(b);
+  if (sink) (void)hipFree(sink);
+  return rc;
+}
+
 int gbgpu_last_timings(gbgpu_ctx *ctx, float *ms6, int64_t *scan_bytes) {
   return gbgpu_slot_timings(ctx, 0, ms6, scan_bytes);
+}
+
+int gbgpu_comm_unique_id(uint8_t *id) {
+  if (!id) return EINVAL;
+  ncclUniqueId u;
+  if (ncclGetUniqueId(&u) != ncclSuccess) return GBGPU_EHIP;
+  static_assert(sizeof(u) == GBGPU_COMM_ID_BYTES, "ncclUniqueId size");
+  std::memcpy(id, &u, sizeof u);
+  return 0;
+}
+
+int gbgpu_comm_init(gbgpu_ctx *ctx, int nranks, int rank, const uint8_t *id) {
+  if (!ctx || !id || nranks < 1 || rank < 0 || rank >= nranks || nranks > 64) return EINVAL;
+  std::lock_guard<std::mutex> g(ctx->x_mu);
+  if (ctx->comm) return EBUSY;
+  (void)hipSetDevice(ctx->device);
+  ncclUniqueId u;
+  std::memcpy(&u, id, sizeof u);
+  if (!ctx->xstream && hipStreamCreateWithFlags(&ctx->xstream, hipStreamNonBlocking) != hipSuccess) return GBGPU_EHIP;
+  if (ncclCommInitRank(&ctx->comm, nranks, u, rank) != ncclSuccess) {
+    ctx->comm = nullptr;
+    return GBGPU_EHIP;
+  }
+  ctx->nranks = nranks;
+  ctx->rank = rank;
+  return 0;
+}
+
+int gbgpu_allgather_topk(gbgpu_ctx *ctx, int slot, int32_t k, int64_t *docids, double *scores, int32_t *n,
+                         int64_t *hits, gbgpu_result *local) {
+  if (!ctx || k < 1 || (uint32_t)k > XMAX || !n || !hits) return EINVAL;
+  QuerySlot *q = slot_of(ctx, slot);
+  if (!q) return EINVAL;
+  std::lock_guard<std::mutex> xg(ctx->x_mu);
+  if (!ctx->comm) return EINVAL;
+  std::unique_lock<std::mutex> lk(q->mu);
+  if (!q->pending) return EINVAL;
+  (void)hipSetDevice(ctx->device);
+  const size_t stride = align256(sizeof(XHead) + sizeof(XRec) * (size_t)k);
+  const size_t out_bytes = sizeof(XHead) + 16 * (size_t)k;
+  if (ctx->xsend.ensure(stride) || ctx->xrecv.ensure(stride * ctx->nranks) || ctx->xout.ensure(out_bytes))
+    return ENOMEM;
+  if (out_bytes > ctx->h_xout_cap) {
+    if (ctx->h_xout) (void)hipHostFree(ctx->h_xout);
+    ctx->h_xout = nullptr;
+    ctx->h_xout_cap = 0;
+    HIPCHECK(hipHostMalloc((void **)&ctx->h_xout, out_bytes));
+    ctx->h_xout_cap = out_bytes;
+  }
+  hipStream_t xs = ctx->xstream;
+  if (q->early) {
+    HIPCHECK(hipMemsetAsync(ctx->xsend.p, 0, sizeof(XHead), xs));  // an empty reply
+  } else {
+    HIPCHECK(hipStreamWaitEvent(xs, q->ev_done, 0));
+    hipLaunchKernelGGL(k_xpack, dim3(1), dim3(256), 0, xs, q->res.as<Counters>(), q->res.as<uint32_t>(res_keys_off()),
+                       q->res.as<uint64_t>(res_docs_off(q->k)), (uint32_t)k, (uint32_t)q->k, ctx->xsend.as<uint8_t>());
+  }
+  if (ncclAllGather(ctx->xsend.p, ctx->xrecv.p, stride, ncclUint8, ctx->comm, xs) != ncclSuccess) return GBGPU_EHIP;
+  hipLaunchKernelGGL(k_xmerge, dim3(1), dim3(64), 0, xs, ctx->xrecv.as<uint8_t>(), ctx->nranks, (uint32_t)k, stride,
+                     ctx->xout.as<uint8_t>());
+  HIPCHECK(hipMemcpyAsync(ctx->h_xout, ctx->xout.p, out_bytes, hipMemcpyDeviceToHost, xs));
+  HIPCHECK(hipStreamSynchronize(xs));
+  // finish the slot's own query (its result block was read on the device)
+  gbgpu_result tmp;
+  std::memset(&tmp, 0, sizeof tmp);
+  int rc = collect(ctx, *q, local ? local : &tmp);
+  lk.unlock();
+  slot_released(ctx);
+  if (rc) return rc;
+  const XHead *h = reinterpret_cast<const XHead *>(ctx->h_xout);
+  const double *sc = reinterpret_cast<const double *>(ctx->h_xout + sizeof(XHead));
+  const int64_t *dc = reinterpret_cast<const int64_t *>(ctx->h_xout + sizeof(XHead) + 8 * (size_t)k);
+  *n = h->n;
+  *hits = h->hits;
+  for (int i = 0; i < h->n; i++) {
+    if (docids) docids[i] = dc[i];
+    if (scores) scores[i] = sc[i];
+  }
+  return 0;
+}
+
+int gbgpu_merge_replies_device(gbgpu_ctx *ctx, int nranks, int32_t k, const int32_t *counts, const int64_t *shard_hits,
+                               const int64_t *const *shard_docids, const float *const *shard_scores,
+                               int64_t *docids, double *scores, int32_t *n, int64_t *hits) {
+  if (!ctx || nranks < 1 || nranks > 64 || k < 1 || (uint32_t)k > XMAX || !counts || !n || !hits) return EINVAL;
+  (void)hipSetDevice(ctx->device);
+  const size_t stride = align256(sizeof(XHead) + sizeof(XRec) * (size_t)k);
+  std::vector<uint8_t> recv(stride * nranks, 0);
+  for (int r = 0; r < nranks; r++) {
+    XHead *h = reinterpret_cast<XHead *>(recv.data() + stride * r);
+    XRec *rec = reinterpret_cast<XRec *>(recv.data() + stride * r + sizeof(XHead));
+    const int m = std::min(counts[r], k);
+    h->n = m;
+    h->hits = shard_hits ? shard_hits[r] : 0;
+    for (int i = 0; i < m; i++) {
+      uint32_t b;
+      std::memcpy(&b, &shard_scores[r][i], 4);
+      uint32_t key = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+      rec[i].key = key ? key : 1u;
+      rec[i].docid = (uint64_t)shard_docids[r][i];
+    }
+  }
+  const size_t out_bytes = sizeof(XHead) + 16 * (size_t)k;
+  DevBuf din, dout;
+  if (din.ensure(recv.size()) || dout.ensure(out_bytes)) {
+    din.release();
+    dout.release();
+    return ENOMEM;
+  }
+  std::vector<uint8_t> out(out_bytes);
+  int rc = 0;
+  if (hipMemcpy(din.p, recv.data(), recv.size(), hipMemcpyHostToDevice) != hipSuccess) rc = GBGPU_EHIP;
+  if (!rc) {
+    hipLaunchKernelGGL(k_xmerge, dim3(1), dim3(64), 0, 0, din.as<uint8_t>(), nranks, (uint32_t)k, stride,
+                       dout.as<uint8_t>());
+    if (hipGetLastError() != hipSuccess || hipMemcpy(out.data(), dout.p, out_bytes, hipMemcpyDeviceToHost) != hipSuccess)
+      rc = GBGPU_EHIP;
+  }
+  din.release();
+  dout.release();
+  if (rc) return rc;
+  const XHead *h = reinterpret_cast<const XHead *>(out.data());
+  const double *sc = reinterpret_cast<const double *>(out.data() + sizeof(XHead));
+  const int64_t *dc = reinterpret_cast<const int64_t *>(out.data() + sizeof(XHead) + 8 * (size_t)k);
+  *n = h->n;
+  *hits = h->hits;
+  for (int i = 0; i < h->n; i++) {
+    if (docids) docids[i] = dc[i];
+    if (scores) scores[i] = sc[i];
+  }
+  return 0;
 }
 
 int gbgpu_merge_topk(const int64_t *const *sd, const float *const *ss, const int32_t *cnt, int nshards, int32_t k,

@@ -58,6 +58,11 @@ struct DevList {
   uint32_t group_bits;  // positive groups containing this list (+NEG_BIT if in a negative group)
   int32_t g0_array;     // index among the smallest group's candidate arrays, -1 if none
   int32_t probe;        // k_probe direction: 0 not scanned, PROBE_BY_CAND, PROBE_BY_RUN
+  // a list several positive groups use is shrunk in place once per use
+  // (shrinkSubLists, Posdb.cpp:5334-5428): the first use (owner_group,
+  // owner_sub) sees it clean, every later one sees the re-shrunk buffer
+  int16_t owner_group, owner_sub;
+  int32_t uses;         // positive group sublist positions naming this list
 };
 constexpr int32_t PROBE_BY_CAND = 1;  // dense list: candidates search the chunk's run starts
 constexpr int32_t PROBE_BY_RUN = 2;   // sparse list: run starts look up the candidate directory
@@ -76,6 +81,7 @@ struct DevPlan {
   double max_serp_score;
   int64_t min_serp_docid;
   // site clustering: the pruning bounds (Posdb.cpp:6327-6504, 7811-7960)
+  uint32_t reshare_mask;   // bit l: list l is shrunk more than once (uses >= 2)
   int clustering;
   int do_max_score;        // m_doMaxScoreAlgo
   int min_listi;           // m_minListi (group whose positions seed the ring buffer)

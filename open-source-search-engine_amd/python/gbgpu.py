@@ -111,7 +111,9 @@ EXPORTS = [
     "gbgpu_query_resident_enqueue", "gbgpu_query_collect", "gbgpu_stream",
     "gbgpu_last_topk_device", "gbgpu_merge_topk", "gbgpu_merge_posdb", "gbgpu_set_profiling",
     "gbgpu_last_timings", "gbgpu_set_query_slots", "gbgpu_query_slots", "gbgpu_query_slot_enqueue",
-    "gbgpu_query_slot_collect", "gbgpu_slot_stream", "gbgpu_slot_timings",
+    "gbgpu_query_slot_collect", "gbgpu_slot_stream", "gbgpu_slot_timings", "gbgpu_slot_stats",
+    "gbgpu_bandwidth_ceiling", "gbgpu_comm_unique_id", "gbgpu_comm_init", "gbgpu_allgather_topk",
+    "gbgpu_merge_replies_device",
     "gbgpu_merge_posdb_device", "gbgpu_merge_timings", "gbgpu_merge_last_key", "gb_synth_merge_runs",
     "gb_synth_lists", "gb_synth_free", "gb_synth_docid", "gb_posdb_compress", "gb_posdb_make_key",
 ]
@@ -171,6 +173,18 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.gbgpu_slot_stream.argtypes = [vp, ctypes.c_int]
     lib.gbgpu_slot_stream.restype = vp
     lib.gbgpu_slot_timings.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(i64)]
+    lib.gbgpu_slot_stats.argtypes = [vp, ctypes.c_int, ctypes.POINTER(i64)]
+    lib.gbgpu_comm_unique_id.argtypes = [vp]
+    lib.gbgpu_comm_init.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp]
+    lib.gbgpu_allgather_topk.argtypes = [vp, ctypes.c_int, i32, ctypes.POINTER(i64), ctypes.POINTER(ctypes.c_double),
+                                         ctypes.POINTER(i32), ctypes.POINTER(i64), ctypes.POINTER(Result)]
+    lib.gbgpu_merge_replies_device.argtypes = [vp, ctypes.c_int, i32, ctypes.POINTER(i32), ctypes.POINTER(i64),
+                                               ctypes.POINTER(ctypes.POINTER(i64)),
+                                               ctypes.POINTER(ctypes.POINTER(ctypes.c_float)),
+                                               ctypes.POINTER(i64), ctypes.POINTER(ctypes.c_double),
+                                               ctypes.POINTER(i32), ctypes.POINTER(i64)]
+    lib.gbgpu_bandwidth_ceiling.argtypes = [vp, i64, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+                                            ctypes.POINTER(ctypes.c_double)]
     lib.gb_synth_lists.argtypes = [ctypes.POINTER(SynthCorpus), ctypes.POINTER(SynthTerm), ctypes.c_int,
                                    ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(i64)]
     lib.gb_synth_free.argtypes = [vp]
@@ -415,6 +429,64 @@ class Engine:
         sb = ctypes.c_int64()
         _check(self.lib.gbgpu_slot_timings(self.ctx, slot, ms, ctypes.byref(sb)))
         return list(ms), sb.value
+
+    def stats(self, slot: int = 0):
+        """gbgpu_slot_stats: work counts of the slot's last collected query."""
+        st = (ctypes.c_int64 * 8)()
+        _check(self.lib.gbgpu_slot_stats(self.ctx, slot, st))
+        keys = ["scan_bytes", "g0_bytes", "probe_bytes", "candidates", "survivors", "survivor_run_bytes",
+                "tree_nodes"]
+        return dict(zip(keys, list(st)))
+
+    def bandwidth_ceiling(self, nbytes: int = 2 << 30, iters: int = 10):
+        r, c = ctypes.c_double(), ctypes.c_double()
+        _check(self.lib.gbgpu_bandwidth_ceiling(self.ctx, nbytes, iters, ctypes.byref(r), ctypes.byref(c)))
+        return r.value, c.value
+
+    # ------------------------------------------------ Msg3a exchange (RCCL)
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        buf = ctypes.create_string_buffer(128)
+        _check(load().gbgpu_comm_unique_id(buf), "gbgpu_comm_unique_id")
+        return buf.raw
+
+    def comm_init(self, nranks: int, rank: int, uid: bytes) -> None:
+        b = ctypes.create_string_buffer(bytes(uid), 128)
+        _check(self.lib.gbgpu_comm_init(self.ctx, nranks, rank, b), "gbgpu_comm_init")
+
+    def allgather_topk(self, k: int, slot: int = 0):
+        """Collects the slot's query as this shard's reply and returns the
+        Msg3a merge of every rank's reply: (docids, scores float64, total hits)."""
+        d = np.zeros(k, np.int64)
+        sc = np.zeros(k, np.float64)
+        n, h = ctypes.c_int32(), ctypes.c_int64()
+        _check(self.lib.gbgpu_allgather_topk(self.ctx, slot, k, d.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                                             sc.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), ctypes.byref(n),
+                                             ctypes.byref(h), None), "gbgpu_allgather_topk")
+        return d[:n.value], sc[:n.value], h.value
+
+    def merge_replies_device(self, shards, k: int, shard_hits=None):
+        ns = len(shards)
+        keep = []
+        dptrs = (ctypes.POINTER(ctypes.c_int64) * ns)()
+        sptrs = (ctypes.POINTER(ctypes.c_float) * ns)()
+        cnts = (ctypes.c_int32 * ns)()
+        hh = (ctypes.c_int64 * ns)(*(shard_hits or [0] * ns))
+        for i, (dd, ss) in enumerate(shards):
+            dd = np.ascontiguousarray(dd, dtype=np.int64)
+            ss = np.ascontiguousarray(ss, dtype=np.float32)
+            keep += [dd, ss]
+            dptrs[i] = dd.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))
+            sptrs[i] = ss.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+            cnts[i] = len(dd)
+        od = np.zeros(k, np.int64)
+        osc = np.zeros(k, np.float64)
+        n, h = ctypes.c_int32(), ctypes.c_int64()
+        _check(self.lib.gbgpu_merge_replies_device(self.ctx, ns, k, cnts, hh, dptrs, sptrs,
+                                                   od.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                                                   osc.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                                                   ctypes.byref(n), ctypes.byref(h)), "gbgpu_merge_replies_device")
+        return od[:n.value], osc[:n.value], h.value
 
     def stream(self) -> int:
         return self.lib.gbgpu_stream(self.ctx) or 0

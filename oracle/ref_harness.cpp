@@ -71,6 +71,9 @@ __attribute__((constructor(101))) static void install_fault_handler() {
 }
 
 static bool s_inited = false;
+static double s_isect_s = 0;  // seconds inside intersectLists10_r (list copies excluded)
+static double s_merge_s = 0;  // seconds inside RdbList::merge_r
+static double now_s();
 static CollectionRec *s_crPtr[1];
 
 static void ref_init() {
@@ -216,7 +219,9 @@ static int ref_query(const orc_qterm *terms, const uint8_t *const *lists, const 
     alloced = true;
     if (!tab->allocWhiteListTable()) return ENOMEM;
     if (!tab->setQueryTermInfo()) return ENOMEM;
+    const double t0 = now_s();
     tab->intersectLists10_r();
+    s_isect_s += now_s() - t0;
     out->hits += tab->m_docIdVoteBuf.length() / 6;
     out->filtered += tab->m_filtered;
     if (tab->m_errno) out->corrupt = tab->m_errno;
@@ -275,7 +280,9 @@ static int64_t ref_posdb_merge(const uint8_t *const *lists, const int64_t *sizes
   int32_t mrs = min_rec_sizes < 0 ? -1 : (int32_t)min_rec_sizes;
   if (!dst.prepareForMerge(ptrs, n, mrs)) return -ENOMEM;
   int32_t filtered = 0;
+  const double t0 = now_s();
   dst.merge_r(ptrs, n, startKey, endKey, mrs, remove_neg_keys != 0, RDB_POSDB, &filtered, NULL, NULL, false, 0);
+  s_merge_s = now_s() - t0;
   int64_t sz = dst.m_listSize;
   if (sz > cap) return -ENOSPC;
   memcpy(out, dst.m_list, sz);
@@ -288,9 +295,11 @@ static int64_t ref_posdb_merge(const uint8_t *const *lists, const int64_t *sizes
 //   op=1 query: i32 nterms, orc_params, nterms x orc_qterm,
 //               nterms x (i64 size, bytes), i32 cap, i32 want_votes, i32 reps
 //        ->     orc_result, n x i64 docid, n x f32 score,
-//               i64 nvotes, nvotes x i64 docid, f64 seconds per run (median)
+//               i64 nvotes, nvotes x i64 docid, f64 seconds per run (median of
+//               the time inside intersectLists10_r: the per-run list copies,
+//               which the reference mutates, are not timed)
 //   op=2 merge: i32 n, i32 remove_neg, i64 min_rec_sizes, n x (i64 size, bytes)
-//        ->     i64 size (or -errno), bytes
+//        ->     i64 size (or -errno), bytes, f64 seconds inside merge_r
 #include <stdio.h>
 #include <stdlib.h>
 #include <time.h>
@@ -349,10 +358,10 @@ int main(int argc, char **argv) {
       if (reps < 1) reps = 1;
       int rc = 0;
       for (int k = 0; k < reps; k++) {
-        double t0 = now_s();
+        s_isect_s = 0;
         rc = ref_query(t.data(), ptrs.data(), sizes.data(), nt, &p, d.data(), s.data(), cap, &r,
                        want_votes ? votes.data() : NULL, vcap);
-        times.push_back(now_s() - t0);
+        times.push_back(s_isect_s);
         if (rc) break;
       }
       if (rc) r.corrupt = -rc;
@@ -387,6 +396,7 @@ int main(int argc, char **argv) {
       int64_t sz = ref_posdb_merge(ptrs.data(), sizes.data(), n, rm, mrs, out.data(), tot + 64);
       wr(&sz, 8);
       if (sz > 0) wr(out.data(), sz);
+      wr(&s_merge_s, 8);
     } else {
       return 5;
     }

@@ -80,7 +80,7 @@ def query(terms, lists, params, cap=4096, votes=False, reps=1):
                 corrupt=r.corrupt, votes=v, seconds=sec)
 
 
-def posdb_merge(lists, remove_neg_keys, min_rec_sizes=-1):
+def posdb_merge(lists, remove_neg_keys, min_rec_sizes=-1, timed=False):
     p = _p()
     req = [struct.pack("<iiiq", 2, len(lists), 1 if remove_neg_keys else 0, min_rec_sizes)]
     for l in lists:
@@ -89,6 +89,10 @@ def posdb_merge(lists, remove_neg_keys, min_rec_sizes=-1):
     p.stdin.write(b"".join(req))
     p.stdin.flush()
     (n,) = struct.unpack("<q", _read(8))
+    out = _read(n) if n > 0 else b""
+    (sec,) = struct.unpack("<d", _read(8))
     if n < 0:
         raise RuntimeError(f"gbref merge rc={n}")
-    return _read(n)
+    if timed:
+        return out, sec
+    return out

@@ -269,3 +269,39 @@ def test_parity_site_clustering_pruning_large(engine):
     lists2 = generate(q2, 2_000_000, seed=5)
     p2 = q2.params(site_clustering=1)
     check(gpu(engine, q2.terms, lists2, p2), oracle(q2.terms, lists2, p2), "two_term 2M")
+
+
+# ------------------------------------------- every survivor's score, exactly
+# docs_to_get large enough that the TopTree holds every scored survivor, so
+# each docid's score is compared, not only the top's.  The seeds include
+# queries whose shared bigram lists are shrunk in place twice by the
+# reference (shrinkSubLists re-reads the list's original extent, Posdb.cpp:
+# 5334-5428): the second group's copy of the list's last survivor run picks
+# up the stale 6-byte units that follow the first shrink's output.
+RESHRINK_CASES = [(2, "q3_0"), (8, "three_word"), (8, "piped"), (11, "five_word"), (14, "q3_0"),
+                  (16, "wiki_halfstop"), (17, "five_word")]
+
+
+@pytest.mark.parametrize("seed,name", RESHRINK_CASES)
+def test_parity_every_survivor_reshrunk_lists(engine, seed, name):
+    q = [k for k in qkinds.kinds(20000, seed=seed) if k.name == name][0]
+    lists = generate(q, 20000, seed=seed)
+    q.docs_to_get = 1500
+    p = q.params()
+    exp = oracle(q.terms, lists, p)
+    assert exp["hits"] <= 1500
+    check(gpu(engine, q.terms, lists, p), exp, f"{name} seed={seed}")
+    p = q.params(site_clustering=1)
+    check(gpu(engine, q.terms, lists, p), oracle(q.terms, lists, p), f"{name} seed={seed} clustering")
+
+
+@pytest.mark.parametrize("kind", range(len(qkinds.kinds())))
+def test_parity_every_survivor(engine, kind):
+    q = qkinds.kinds(12000, seed=21)[kind]
+    lists = generate(q, 12000, seed=21)
+    q.docs_to_get = 1500
+    p = q.params()
+    exp = oracle(q.terms, lists, p)
+    if exp["hits"] > 1500:
+        pytest.skip("more survivors than one TopTree can hold here")
+    check(gpu(engine, q.terms, lists, p), exp, q.name)
