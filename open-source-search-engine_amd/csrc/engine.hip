@@ -869,6 +869,9 @@ __global__ void __launch_bounds__(BLOCK) k_compact(const DevPlan *pl, const uint
   }
   uint32_t okm = 0, nok = 0, utot = 0, any = 0;
   uint32_t units[CSPT];
+  constexpr int XR = 4;  // re-shrunk lists accumulated in registers
+  uint32_t txu[XR] = {0, 0, 0, 0};
+  unsigned long long txd[XR] = {0, 0, 0, 0}, tdall = 0;
 #pragma unroll
   for (int q = 0; q < CSPT; q++) {
     const uint64_t s = s0 + (uint64_t)q * SSTEP;
@@ -888,12 +891,53 @@ __global__ void __launch_bounds__(BLOCK) k_compact(const DevPlan *pl, const uint
     nok++;
     utot += u_s;
     if (CMODE != 2 && xmask) {
+      // accumulated per thread in registers for the first XR re-shrunk lists
+      // (reduced over the wave below), LDS atomics beyond
       const unsigned long long d = cand[s];
-      atomicMax(&s_dall, d);
-      for (uint32_t x = lm & xmask; x; x &= x - 1) {
+      if (d > tdall) tdall = d;
+      int r = 0;
+      for (uint32_t x = xmask; x; x &= x - 1, r++) {
         const int l = __ffs(x) - 1;
-        atomicAdd(&s_xu[l], loc[(uint64_t)l * slot_ub + s].len);
-        atomicMax(&s_xd[l], d);
+        if (!(lm >> l & 1)) continue;
+        const uint32_t len = loc[(uint64_t)l * slot_ub + s].len;
+        if (r < XR) {
+#pragma unroll
+          for (int t = 0; t < XR; t++)
+            if (t == r) {
+              txu[t] += len;
+              txd[t] = d > txd[t] ? d : txd[t];
+            }
+        } else {
+          atomicAdd(&s_xu[l], len);
+          atomicMax(&s_xd[l], d);
+        }
+      }
+    }
+  }
+  if (CMODE != 2 && xmask) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const unsigned long long o = __shfl_xor(tdall, off, 64);
+      tdall = o > tdall ? o : tdall;
+#pragma unroll
+      for (int t = 0; t < XR; t++) {
+        txu[t] += __shfl_xor(txu[t], off, 64);
+        const unsigned long long od = __shfl_xor(txd[t], off, 64);
+        txd[t] = od > txd[t] ? od : txd[t];
+      }
+    }
+    if (lane == 0) {
+      if (tdall) atomicMax(&s_dall, tdall);
+      int r = 0;
+      for (uint32_t x = xmask; x && r < XR; x &= x - 1, r++) {
+        const int l = __ffs(x) - 1;
+#pragma unroll
+        for (int t = 0; t < XR; t++)
+          if (t == r && txu[t]) {
+            atomicAdd(&s_xu[l], txu[t]);
+            atomicMax(&s_xd[l], txd[t]);
+          }
       }
     }
   }
@@ -1163,7 +1207,7 @@ __device__ __forceinline__ uint64_t load6(gu8 *k) {
 template <int NQ, int NS, class RP>
 __device__ __forceinline__ void score_survivor(const DevPlan *pl, const Counters *ctr, uint32_t s, uint32_t lm,
                                                uint32_t anys, const Loc *loc, uint64_t slot_ub, RP rec, float *smcol,
-                                               uint32_t *key_out, int diag) {
+                                               uint32_t *key_out, int diag, uint32_t *nrec_out) {
   const int ng = pl->ngroups;
   DocView<NQ, RP> dv;
   dv.rec = rec;
@@ -1301,6 +1345,7 @@ __device__ __forceinline__ void score_survivor(const DevPlan *pl, const Counters
     if (nrec == start) empty_pos = true;  // reference reads stale mbuf here (UB)
   }
   float score = 0.0f;
+  *nrec_out = nrec;
   if (diag == 1) {  // diagnostic: mini-merge only
     *key_out = nrec + 1;
     return;
@@ -1326,8 +1371,11 @@ __global__ void __launch_bounds__(SCORE_TPB) k_score(const DevPlan *pl, const ui
                                                      const uint32_t *surv, const uint32_t *surv_lm,
                                                      const unsigned long long *surv_off, const Loc *loc,
                                                      uint64_t slot_ub, uint64_t *arena, uint32_t *skey,
-                                                     uint64_t *sdoc, uint8_t *sflag, int diag) {
+                                                     uint64_t *sdoc, uint8_t *sflag, int diag, uint64_t *dbg) {
   __shared__ float s_sm[npairs<NQ>() * SCORE_TPB];
+  // diagnostic (GBGPU_SCORE_MODE=2): per-wave start/end clock, records
+  const uint64_t t0 = dbg ? __builtin_amdgcn_s_memrealtime() : 0;
+  uint32_t dmax = 0, dsum = 0, dits = 0;
   stage_weights(&c_weights);
   const uint32_t nsurv = (uint32_t)(ctr->surv_top >> 36);
   const uint32_t anys = ctr->anysurv;
@@ -1344,8 +1392,13 @@ __global__ void __launch_bounds__(SCORE_TPB) k_score(const DevPlan *pl, const ui
         if (e.reloc && e.slot1 == s + 1) off = e.off;
       }
       auto *rec = (__attribute__((address_space(1))) uint64_t *)(arena + off);
-      uint32_t key;
-      score_survivor<NQ, NS>(pl, ctr, s, lm, anys, loc, slot_ub, rec, s_sm + threadIdx.x, &key, diag);
+      uint32_t key, nr;
+      score_survivor<NQ, NS>(pl, ctr, s, lm, anys, loc, slot_ub, rec, s_sm + threadIdx.x, &key, diag, &nr);
+      if (dbg) {
+        dmax = nr > dmax ? nr : dmax;
+        dsum += nr;
+        dits++;
+      }
       const uint64_t d = cand[s];
       // the paging filter of a widget's next page (Posdb.cpp:7327-7347):
       // m_filtered counts the scored docids it drops
@@ -1365,6 +1418,21 @@ __global__ void __launch_bounds__(SCORE_TPB) k_score(const DevPlan *pl, const ui
     nfilt += (uint32_t)__popcll(__ballot(filt));
   }
   if (!pl->clustering && (threadIdx.x & 63) == 0 && nfilt) atomicAdd((uint32_t *)&ctr->filtered, nfilt);
+  if (dbg) {
+    for (int o = 32; o > 0; o >>= 1) {
+      const uint32_t m = __shfl_xor(dmax, o, 64);
+      dmax = m > dmax ? m : dmax;
+      dsum += __shfl_xor(dsum, o, 64);
+      dits += __shfl_xor(dits, o, 64);
+    }
+    const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0) {
+      dbg[blockIdx.x * 4 + 0] = t0;
+      dbg[blockIdx.x * 4 + 1] = t1;
+      dbg[blockIdx.x * 4 + 2] = dmax;
+      dbg[blockIdx.x * 4 + 3] = ((uint64_t)dits << 32) | dsum;
+    }
+  }
 }
 
 // ------------------------------------------------------- site clustering
@@ -2416,6 +2484,8 @@ struct gbgpu_ctx {
   int probe_mode = 0;  // diagnostic only (GBGPU_PROBE_MODE)
   int score_mode = 0;  // diagnostic only (GBGPU_SCORE_MODE): 1 mini-merge without scoring
   int debug_ext = 0;   // diagnostic only (GBGPU_DEBUG_EXT): print the re-shrink table per query
+  uint64_t *d_sdbg = nullptr;  // GBGPU_SCORE_MODE=2: per-wave k_score timing (GBGPU_SCORE_DUMP file)
+  uint32_t sdbg_grid = 0;
   std::mutex merge_mu;
   gbmerge::MergeState *merge = nullptr;  // created on first use (merge.hip)
   // Msg3a exchange over RCCL (gbgpu_comm_init / gbgpu_allgather_topk)
@@ -2884,11 +2954,15 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
     for (int j = 0; j < hp.ngroups; j++)
       if (!(P.gflags0[j] & BF_NEGATIVE)) maxsub = std::max(maxsub, (int)P.gnsub[j]);
     const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((slot_ub + SCORE_TPB - 1) / SCORE_TPB, 8192));
+    if (ctx->d_sdbg) {
+      ctx->sdbg_grid = grid;
+      HIPCHECK(hipMemsetAsync(ctx->d_sdbg, 0, 8192 * 32, st));
+    }
     auto launch = [&](auto kern) {
       hipLaunchKernelGGL(kern, dim3(grid), dim3(SCORE_TPB), 0, st, dpl, q.cand.as<uint64_t>(), dctr,
                          q.surv.as<uint32_t>(), q.survlm.as<uint32_t>(), q.survoff.as<unsigned long long>(),
                          loc, slot_ub, q.scratch.as<uint64_t>(), q.skey.as<uint32_t>(),
-                         q.sdoc.as<uint64_t>(), q.sflag.as<uint8_t>(), ctx->score_mode);
+                         q.sdoc.as<uint64_t>(), q.sflag.as<uint8_t>(), ctx->score_mode, ctx->d_sdbg);
     };
     if (hp.ngroups <= 2 && maxsub <= 4) launch(k_score<2, 4>);
     else if (hp.ngroups <= 4 && maxsub <= 4) launch(k_score<4, 4>);
@@ -3019,6 +3093,15 @@ static int collect(gbgpu_ctx *ctx, QuerySlot &q, gbgpu_result *out, std::vector<
   if (c->corrupt) return GBGPU_ECORRUPT;
   if (c->tree_err) return GBGPU_ECAPACITY;
   if (c->unsup) return GBGPU_EUNSUPPORTED;
+  if (ctx->d_sdbg && ctx->sdbg_grid) {
+    std::vector<uint64_t> h((size_t)ctx->sdbg_grid * 4);
+    if (hipMemcpy(h.data(), ctx->d_sdbg, h.size() * 8, hipMemcpyDeviceToHost) == hipSuccess)
+      if (const char *fn = std::getenv("GBGPU_SCORE_DUMP"))
+        if (FILE *f = std::fopen(fn, "ab")) {
+          std::fwrite(h.data(), 8, h.size(), f);
+          std::fclose(f);
+        }
+  }
   if (ctx->debug_ext) {
     for (int l = 0; l < MAXL; l++)
       if (c->ext[l].units || c->ext[l].E)
@@ -3280,6 +3363,7 @@ int gbgpu_open(int device, gbgpu_ctx **out) {
   }
   if (const char *pm = std::getenv("GBGPU_PROBE_MODE")) ctx->probe_mode = std::atoi(pm);
   if (const char *sm = std::getenv("GBGPU_SCORE_MODE")) ctx->score_mode = std::atoi(sm);
+  if (ctx->score_mode == 2) HIPCHECK(hipMalloc(&ctx->d_sdbg, 8192 * 32));
   if (const char *de = std::getenv("GBGPU_DEBUG_EXT")) ctx->debug_ext = std::atoi(de);
   *out = ctx;
   return 0;
@@ -3301,6 +3385,7 @@ void gbgpu_close(gbgpu_ctx *ctx) {
   ctx->lists.clear();  // the last references: ListMem frees the device copies
   gbmerge::state_free(ctx->merge);
   if (ctx->d_flag) (void)hipFree(ctx->d_flag);
+  if (ctx->d_sdbg) (void)hipFree(ctx->d_sdbg);
   if (ctx->h_flag) (void)hipHostFree(ctx->h_flag);
   if (ctx->upload_stream) (void)hipStreamDestroy(ctx->upload_stream);
   delete ctx;
