@@ -85,7 +85,10 @@ typedef struct gbgpu_params {
   float   same_lang_weight; /* m_sameLangWeight                                   */
   int32_t do_max_score_algo;/* m_doMaxScoreAlgo: per-term getMaxPossibleScore
                                prefilter (Posdb.cpp:6046-6047, 6327-6346)         */
-  int32_t reserved0;        /* 0                                                  */
+  int32_t get_docid_scoring_info; /* m_getDocIdScoringInfo: the per-docid score
+                               breakdown second pass (Posdb.cpp:942-948, 3058,
+                               7752-7806) is not on the GPU path: nonzero returns
+                               GBGPU_EUNSUPPORTED (the adapter runs the CPU body) */
   double  max_serp_score;   /* m_maxSerpScore  } paging of a widget's next page:   */
   int64_t min_serp_docid;   /* m_minSerpDocId  } nonzero enables the filter of
                                Posdb.cpp:4379-4381, 7327-7347 (counted in

@@ -39,6 +39,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <cerrno>
 #include <cmath>
 #include <cstdio>
@@ -98,6 +99,8 @@ struct Counters {
   uint32_t pad[2];
   unsigned long long dmax_all;  // largest survivor docid
   ListExt ext[MAXL];
+  uint32_t bcnt[8];  // survivors per size bucket (k_compact), NBKT
+  uint32_t pad2[8];
 };
 
 // radix-select state (3 passes over the 32-bit score keys: 12+12+8 bits)
@@ -826,12 +829,26 @@ struct BlkTot {
   unsigned long long u;
 };
 
+// Survivors are also counted by size (their run units, an upper bound on
+// their records) so k_score can give each wave survivors of one size: a
+// wave's lanes run the scorers in lockstep, so its time is its largest
+// lane's.  Bucket 0 holds the largest and is scored first.
+// Buckets 0-2 (more units than a lane's rc records) are scored 8, 16 and 32
+// to a wave, so each survivor gets 8, 4 or 2 lanes' worth of LDS records.
+constexpr int NBKT = 8;
+__host__ __device__ __forceinline__ int size_bucket(uint32_t u, uint32_t rc) {
+  return u > 4 * rc ? 0 : u > 2 * rc ? 1 : u > rc ? 2 : 2 * u > rc ? 3 : 3 * u > rc ? 4 : 4 * u > rc ? 5 : 6 * u > rc ? 6 : 7;
+}
+__host__ __device__ __forceinline__ int bucket_shift(int b) { return b == 0 ? 3 : b == 1 ? 4 : b == 2 ? 5 : 6; }
+
 template <int CMODE>
 __global__ void __launch_bounds__(BLOCK) k_compact(const DevPlan *pl, const uint32_t *lmask, const uint32_t *ulen,
                                                    uint64_t slot_ub, Counters *ctr, uint32_t *surv,
                                                    unsigned long long *surv_off, uint32_t *surv_lm, BlkTot *blk,
-                                                   const Loc *loc, const uint64_t *cand) {
+                                                   const Loc *loc, const uint64_t *cand, uint32_t *surv_u,
+                                                   uint32_t rc, uint32_t *perm) {
   __shared__ uint32_t tmp[BLOCK / 64];
+  __shared__ uint32_t s_bcnt[NBKT], s_bbase[NBKT], s_bcur[NBKT];
   __shared__ uint32_t s_xu[MAXL];            // CMODE 0/1: re-shrunk lists' survivor run units
   __shared__ unsigned long long s_xd[MAXL];  // ... and their last survivor docid
   __shared__ unsigned long long s_dall;
@@ -849,6 +866,10 @@ __global__ void __launch_bounds__(BLOCK) k_compact(const DevPlan *pl, const uint
   if (threadIdx.x == 0) {
     s_any = 0;
     s_dall = 0;
+  }
+  if (threadIdx.x < NBKT) {
+    s_bcnt[threadIdx.x] = 0;
+    s_bcur[threadIdx.x] = 0;
   }
   if (CMODE != 2 && threadIdx.x < MAXL) {
     s_xu[threadIdx.x] = 0;
@@ -890,6 +911,7 @@ __global__ void __launch_bounds__(BLOCK) k_compact(const DevPlan *pl, const uint
     okm |= 1u << q;
     nok++;
     utot += u_s;
+    if (CMODE != 1) atomicAdd(&s_bcnt[size_bucket(u_s, rc)], 1u);
     if (CMODE != 2 && xmask) {
       // accumulated per thread in registers for the first XR re-shrunk lists
       // (reduced over the wave below), LDS atomics beyond
@@ -970,6 +992,8 @@ __global__ void __launch_bounds__(BLOCK) k_compact(const DevPlan *pl, const uint
     atomicMax(&ctr->ext[threadIdx.x].dmax, s_xd[threadIdx.x]);
   }
   if (CMODE == 1) return;  // uniform
+  if (threadIdx.x < NBKT)
+    s_bbase[threadIdx.x] = s_bcnt[threadIdx.x] ? atomicAdd(&ctr->bcnt[threadIdx.x], s_bcnt[threadIdx.x]) : 0u;
   __syncthreads();
   uint32_t i = s_base_i + ex_n;
   unsigned long long off = s_base_u + ex_u;
@@ -979,6 +1003,11 @@ __global__ void __launch_bounds__(BLOCK) k_compact(const DevPlan *pl, const uint
     surv[i] = (uint32_t)(s0 + (uint64_t)q * SSTEP);
     surv_off[i] = off;
     surv_lm[i] = lmv[q];
+    surv_u[i] = units[q];
+    // size bucket b's region of perm starts at b * slot_ub; the block's
+    // range in it was reserved above
+    const int b = size_bucket(units[q], rc);
+    perm[(uint64_t)b * slot_ub + s_bbase[b] + atomicAdd(&s_bcur[b], 1u)] = i;
     i++;
     off += units[q];
   }
@@ -1172,9 +1201,14 @@ struct SubRun {
     return k < len0 ? own + (size_t)k * 6 : ext + (size_t)(k - len0) * 6;
   }
 };
+__device__ __forceinline__ SubRun sub_run_at(const DevPlan *pl, const Counters *ctr, Loc lc, int lid, int g, int x,
+                                             uint64_t s);
 __device__ __forceinline__ SubRun sub_run(const DevPlan *pl, const Counters *ctr, const Loc *loc, uint64_t slot_ub,
                                           int lid, int g, int x, uint64_t s) {
-  const Loc lc = loc[(uint64_t)lid * slot_ub + s];
+  return sub_run_at(pl, ctr, loc[(uint64_t)lid * slot_ub + s], lid, g, x, s);
+}
+__device__ __forceinline__ SubRun sub_run_at(const DevPlan *pl, const Counters *ctr, Loc lc, int lid, int g, int x,
+                                             uint64_t s) {
   gu8 *base = gl(pl->lists[lid].p);
   SubRun r{base + (size_t)lc.unit * 6, base, lc.len, lc.len};
   if ((pl->reshare_mask >> lid & 1) && !(g == pl->lists[lid].owner_group && x == pl->lists[lid].owner_sub) &&
@@ -1199,15 +1233,21 @@ __constant__ Weights c_weights;
 // score_doc (scoring.h) over them.
 constexpr int SCORE_TPB = 64;
 
+// a unit's 6 bytes as one u16 and one u32 load (units are 2-byte aligned;
+// which half is 4-byte aligned depends on the unit's parity)
 __device__ __forceinline__ uint64_t load6(gu8 *k) {
-  const auto *h = (const __attribute__((address_space(1))) uint16_t *)k;
-  return (uint64_t)h[0] | ((uint64_t)h[1] << 16) | ((uint64_t)h[2] << 32);
+  const bool odd = ((uintptr_t)k & 2) != 0;
+  const auto *h = (const __attribute__((address_space(1))) uint16_t *)(odd ? k : k + 4);
+  const auto *w = (const __attribute__((address_space(1))) uint32_t *)(odd ? k + 2 : k);
+  const uint64_t hv = *h, wv = *w;
+  return odd ? (hv | (wv << 16)) : (wv | (hv << 32));
 }
 
 template <int NQ, int NS, class RP>
 __device__ __forceinline__ void score_survivor(const DevPlan *pl, const Counters *ctr, uint32_t s, uint32_t lm,
                                                uint32_t anys, const Loc *loc, uint64_t slot_ub, RP rec, float *smcol,
-                                               uint32_t *key_out, int diag, uint32_t *nrec_out) {
+                                               uint32_t *key_out, int diag, uint32_t *nrec_out,
+                                               bool stamp, uint64_t &tmerge, uint64_t (&tm)[3]) {
   const int ng = pl->ngroups;
   DocView<NQ, RP> dv;
   dv.rec = rec;
@@ -1222,6 +1262,8 @@ __device__ __forceinline__ void score_survivor(const DevPlan *pl, const Counters
     const uint8_t gf0 = pl->gflags0[j];
     if (gf0 & BF_NEGATIVE) continue;
     const int gns = pl->gnsub[j];
+    uint64_t ta = 0;
+    if (stamp) ta = __builtin_amdgcn_s_memtime();
     // this group's runs: cursor, end, flags (m_bigramFlags of the shrunk
     // sublist index: lists shrunk to empty are not sublists any more)
     uint32_t cu[NS], ce[NS], c0[NS];
@@ -1253,48 +1295,110 @@ __device__ __forceinline__ void score_survivor(const DevPlan *pl, const Counters
         }
       }
     }
-    // x must be a compile-time index (unrolled loops): a runtime one would
-    // put src[] in scratch
+    // Stage the group's run units in the lane's LDS column at its tail
+    // [cap - U, cap), every sublist's next SK units in flight together: the
+    // records written meanwhile stay below it when nrec + 2U <= cap, as each
+    // record consumes at least one unit.  Otherwise the merge reads the
+    // units from global memory one by one.
+    constexpr int SK = NS >= 16 ? 1 : 16 / NS;
+    if (stamp) {
+      __asm__ volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      const uint64_t tb = __builtin_amdgcn_s_memtime();
+      tm[0] += tb - ta;
+      ta = tb;
+    }
+    uint32_t offx[NS], U = 0, cmax = 0;
+#pragma unroll
+    for (int x = 0; x < NS; x++) {
+      offx[x] = U;
+      U += live[x] ? ce[x] : 0;
+      cmax = live[x] && ce[x] > cmax ? ce[x] : cmax;
+    }
+    bool staged = false;
+    int R = 0;
+    if constexpr (std::is_same<RP, LdsRecs>::value) {
+      if (nrec + 2 * U <= (uint32_t)rec.cap && !(diag & 0x200)) {
+        staged = true;
+        R = rec.cap - (int)U;
+        for (uint32_t b = 0; b < cmax; b += SK) {
+          uint64_t v[NS][SK];
+#pragma unroll
+          for (int x = 0; x < NS; x++)
+#pragma unroll
+            for (int q = 0; q < SK; q++) {
+              const uint32_t c = b + q;
+              v[x][q] = (live[x] && c < ce[x])
+                            ? load6(c < c0[x] ? src[x] + (size_t)c * 6 : xsrc[x] + (size_t)(c - c0[x]) * 6)
+                            : 0;
+            }
+#pragma unroll
+          for (int x = 0; x < NS; x++)
+#pragma unroll
+            for (int q = 0; q < SK; q++)
+              if (live[x] && b + q < ce[x]) rec.put(R + (int)(offx[x] + b + q), v[x][q]);
+        }
+      }
+    }
+    // unit c of sublist x, x a runtime index: one LDS read (staged) or one
+    // global unit load, its address picked by select chains
+    if (stamp) {
+      __asm__ volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      const uint64_t tb = __builtin_amdgcn_s_memtime();
+      tm[1] += tb - ta;
+      ta = tb;
+    }
     auto unit_at = [&](int x, uint32_t c) -> uint64_t {
-      return load6(c < c0[x] ? src[x] + (size_t)c * 6 : xsrc[x] + (size_t)(c - c0[x]) * 6);
+      uint32_t o = 0, cz = 0;
+      gu8 *a = nullptr, *b = nullptr;
+#pragma unroll
+      for (int y = 0; y < NS; y++)
+        if (y == x) {
+          o = offx[y];
+          cz = c0[y];
+          a = src[y];
+          b = xsrc[y];
+        }
+      if (staged) return rec[R + (int)(o + c)];
+      return load6(c < cz ? a + (size_t)c * 6 : b + (size_t)(c - cz) * 6);
     };
     uint64_t ck[NS];
     bool cfirst[NS];
 #pragma unroll
     for (int x = 0; x < NS; x++) {
       cfirst[x] = live[x];
-      ck[x] = live[x] ? unit_at(x, cu[x]) : 0;
+      ck[x] = 0;
+      if (live[x]) {
+        if (staged) ck[x] = rec[R + (int)offx[x]];
+        else ck[x] = load6(src[x]);  // cu == 0 < c0 (a run has its own units)
+      }
     }
     const uint32_t start = nrec;
     uint32_t mbytes = 0;  // emulates mptr - mbuf (cap 299000, Posdb.cpp:6007-6008)
     bool isFirstKey = true;
     uint64_t last = 0;
-    bool hasFirst = false;
     for (;;) {
+      // the smallest current key (6-byte keys compare as 48-bit numbers;
+      // ties go to the lowest sublist)
       int mink = -1;
-      uint32_t mhi = 0, mlo = 0;
+      uint64_t r = 0;
 #pragma unroll
-      for (int x = 0; x < NS; x++) {
-        if (!live[x]) continue;
-        const uint32_t hi = (uint32_t)(ck[x] >> 16), lo = (uint32_t)(ck[x] & 0xffff);
-        if (mink == -1 || hi < mhi || (hi == mhi && lo < mlo)) {
+      for (int x = 0; x < NS; x++)
+        if (live[x] && (mink == -1 || ck[x] < r)) {
           mink = x;
-          mhi = hi;
-          mlo = lo;
-        }
-      }
-      if (mink == -1) break;
-      uint64_t r = 0, hi6 = 0;
-      uint8_t fl = 0;
-#pragma unroll
-      for (int x = 0; x < NS; x++) {
-        if (x == mink) {
           r = ck[x];
-          fl = cfl[x];
-          // the bytes after the first emitted key (its siteRank / langId)
-          if (isFirstKey) hi6 = unit_at(x, cu[x] + 1);
         }
-      }
+      if (mink == -1) break;
+      uint8_t fl = 0;
+      uint32_t cx = 0, cex = 0;
+      bool cf = false;
+#pragma unroll
+      for (int x = 0; x < NS; x++)
+        if (x == mink) {
+          fl = cfl[x];
+          cx = cu[x];
+          cex = ce[x];
+          cf = cfirst[x];
+        }
       const bool hack = (fl & BF_BIGRAM) && ((r >> 16) & 0x03);  // Posdb.cpp:6687-6692
       if (!hack) {
         uint64_t b2 = (r >> 16) & 0xfc;
@@ -1302,16 +1406,17 @@ __device__ __forceinline__ void score_survivor(const DevPlan *pl, const Counters
         if (fl & BF_HALFSTOPWIKIBIGRAM) b2 |= 0x01;
         r = (r & ~(0xffull << 16)) | (b2 << 16);
         if (isFirstKey) {
-          // siteRank / langId of the key copied as 12 bytes (Posdb.h:308-315)
+          // siteRank / langId of the key copied as 12 bytes (Posdb.h:308-315):
+          // the bytes after the first emitted key
+          const uint64_t hi6 = unit_at(mink, cx + 1);
           const uint32_t b0 = (uint32_t)(r & 0xff), b6 = (uint32_t)(hi6 & 0xff), b7 = (uint32_t)((hi6 >> 8) & 0xff);
           const int sr = (int)(((b6 >> 5) | ((b7 & 1) << 3)) & 0x0f);
           const int lg = (int)((b6 & 0x1f) | ((b0 & 0x08) ? 0x20 : 0));
           r = (r & ~0xffull) | (((r & 0xff) & 0xf9) | 0x02);
-          rec[nrec++] = r;
+          rec.put(nrec++, r);
           last = r;
           mbytes += 12;
           isFirstKey = false;
-          hasFirst = true;
           if (siteRank < 0 && !(gf0 & (BF_NUMBER | BF_FACET))) {
             siteRank = sr;
             docLang = lg;
@@ -1321,24 +1426,29 @@ __device__ __forceinline__ void score_survivor(const DevPlan *pl, const Counters
                            (((last >> 24) & 0xc0) == ((r >> 24) & 0xc0));
           if (!dup) {
             r |= 0x06;
-            rec[nrec++] = r;
+            rec.put(nrec++, r);
             last = r;
             mbytes += 6;
           }
         }
       }
+      const uint32_t ncx = cx + (cf ? 2 : 1);
+      const bool more = ncx < cex;
+      const uint64_t nk = more ? unit_at(mink, ncx) : 0;
 #pragma unroll
-      for (int x = 0; x < NS; x++) {
+      for (int x = 0; x < NS; x++)
         if (x == mink) {
-          cu[x] += cfirst[x] ? 2 : 1;
+          cu[x] = ncx;
           cfirst[x] = false;
-          if (cu[x] >= ce[x]) live[x] = false;
-          else ck[x] = unit_at(x, cu[x]);
+          live[x] = more;
+          ck[x] = nk;
         }
-      }
       if (mbytes >= 299000) break;
     }
-    (void)hasFirst;
+    if (stamp) {
+      __asm__ volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      tm[2] += __builtin_amdgcn_s_memtime() - ta;
+    }
     dv.beg[j] = (int)start;
     dv.end[j] = (int)nrec;
     dv.present |= 1u << j;
@@ -1346,12 +1456,16 @@ __device__ __forceinline__ void score_survivor(const DevPlan *pl, const Counters
   }
   float score = 0.0f;
   *nrec_out = nrec;
-  if (diag == 1) {  // diagnostic: mini-merge only
+  if (stamp) {  // diagnostic stamp (GBGPU_SCORE_MODE=2)
+    __asm__ volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    tmerge = __builtin_amdgcn_s_memtime();
+  }
+  if ((diag & 0xff) == 1) {  // diagnostic: mini-merge only
     *key_out = nrec + 1;
     return;
   }
   const bool ok = !empty_pos && score_doc<NQ>(&c_weights, pl, dv, siteRank < 0 ? 0 : siteRank, docLang, smcol,
-                                              SCORE_TPB, &score);
+                                              SCORE_TPB, &score, diag & 0xff);
   uint32_t key = 0;
   if (ok) {
     const uint32_t b = __float_as_uint(score);
@@ -1361,43 +1475,111 @@ __device__ __forceinline__ void score_survivor(const DevPlan *pl, const Counters
   *key_out = key;
 }
 
-// One lane per survivor, grid-stride.  (Measured alternatives: staging each
-// survivor's runs and records in lane-private LDS halves occupancy for no
-// gain -- the scorers are bound by their per-record instruction chains, not
-// by record reads -- and splitting survivors into size tiers adds one launch
-// tail per tier.)
-template <int NQ, int NS>
+// Scored in size-bucketed order (k_compact's perm), so a wave's survivors have
+// similar work (its lanes run the scorers in lockstep).  Waves of buckets
+// 3-7 score 64 survivors, one per lane, each keeping its records in its
+// lane's column of the wave's LDS record arrays (RC records); waves of
+// buckets 0-2 score 8/16/32 larger survivors with 8/4/2 columns each.  A
+// survivor that still does not fit (or whose re-shrunk copies grow it past
+// that) uses its range of the global record arena instead.
+template <int NQ, int NS, int RC>
 __global__ void __launch_bounds__(SCORE_TPB) k_score(const DevPlan *pl, const uint64_t *cand, const Counters *ctr,
                                                      const uint32_t *surv, const uint32_t *surv_lm,
-                                                     const unsigned long long *surv_off, const Loc *loc,
-                                                     uint64_t slot_ub, uint64_t *arena, uint32_t *skey,
-                                                     uint64_t *sdoc, uint8_t *sflag, int diag, uint64_t *dbg) {
+                                                     const unsigned long long *surv_off, const uint32_t *surv_u,
+                                                     const uint32_t *perm, const Loc *loc, uint64_t slot_ub,
+                                                     uint64_t *arena, uint32_t *skey, uint64_t *sdoc, uint8_t *sflag,
+                                                     int diag, uint64_t *dbg) {
+  static_assert(SCORE_TPB == 64, "LdsRecs columns are one wave wide");
   __shared__ float s_sm[npairs<NQ>() * SCORE_TPB];
+  __shared__ uint32_t s_rlo[RC * 64];
+  __shared__ uint16_t s_rhi[RC * 64];
   // diagnostic (GBGPU_SCORE_MODE=2): per-wave start/end clock, records
   const uint64_t t0 = dbg ? __builtin_amdgcn_s_memrealtime() : 0;
   uint32_t dmax = 0, dsum = 0, dits = 0;
+  uint64_t tseg[3] = {0, 0, 0};  // diagnostic: cycles in setup loads, mini-merge, scorers
+  uint64_t tmm[3] = {0, 0, 0};   // ... and in the mini-merge: run locations, staging, merge loop
   stage_weights(&c_weights);
-  const uint32_t nsurv = (uint32_t)(ctr->surv_top >> 36);
   const uint32_t anys = ctr->anysurv;
-  const uint32_t lim = (nsurv + 63) & ~63u;  // whole waves iterate together (ballot below)
+  const int lane = threadIdx.x;
+  // waves per bucket: bucket b packs 1 << bucket_shift(b) survivors a wave
+  uint32_t wend[NBKT], bstart[NBKT];
+  uint32_t nw = 0, acc = 0;
+#pragma unroll
+  for (int b = 0; b < NBKT; b++) {
+    const uint32_t c = ctr->bcnt[b];
+    bstart[b] = acc;
+    acc += c;
+    nw += (c + (1u << bucket_shift(b)) - 1) >> bucket_shift(b);
+    wend[b] = nw;
+  }
+  // diagnostic bit 0x100: survivors in compaction order, 64 a wave
+  const bool natural = (diag & 0x100) != 0;
+  if (natural) nw = (acc + 63) >> 6;
   uint32_t nfilt = 0;
-  for (uint32_t i = blockIdx.x * SCORE_TPB + threadIdx.x; i < lim; i += gridDim.x * SCORE_TPB) {
+  for (uint32_t w = blockIdx.x; w < nw; w += gridDim.x) {  // uniform over the wave
+    int b = 0;
+#pragma unroll
+    for (int q = 0; q < NBKT - 1; q++) b += w >= wend[q];
+    if (natural) b = NBKT - 1;
+    uint32_t wb = 0, st = 0, cnt = 0, wprev = 0;
+#pragma unroll
+    for (int q = 0; q < NBKT; q++)
+      if (q == b) {
+        wb = wend[q];
+        st = bstart[q];
+        cnt = (q + 1 < NBKT ? bstart[q + 1] : acc) - st;
+        wprev = q ? wend[q - 1] : 0;
+      }
+    (void)wb;
+    if (natural) {
+      st = 0;
+      cnt = acc;
+      wprev = 0;
+    }
+    const int sh = bucket_shift(b);
+    const uint32_t j = ((w - wprev) << sh) + (uint32_t)lane;
     bool filt = false;
-    if (i < nsurv) {
+    if (lane < (1 << sh) && j < cnt) {
+      uint64_t ts0 = 0, ts1 = 0, ts2 = 0, ts3 = 0;
+      if (dbg) ts0 = __builtin_amdgcn_s_memtime();
+      const uint32_t i = natural ? j : perm[(uint64_t)b * slot_ub + j];
       const uint32_t s = surv[i];
       const uint32_t lm = surv_lm[i];
+      uint32_t units = surv_u[i];
       unsigned long long off = surv_off[i];
-      for (uint32_t x = lm & pl->reshare_mask; x; x &= x - 1) {  // relocated (k_ext_walk)
-        const ListExt &e = ctr->ext[__ffs(x) - 1];
-        if (e.reloc && e.slot1 == s + 1) off = e.off;
+      for (uint32_t x = lm & pl->reshare_mask; x; x &= x - 1) {  // re-shrunk copies (k_ext_walk)
+        const int l = __ffs(x) - 1;
+        const ListExt &e = ctr->ext[l];
+        if (e.slot1 == s + 1) {
+          units += e.E * (uint32_t)(pl->lists[l].uses - 1);
+          if (e.reloc) off = e.off;
+        }
       }
-      auto *rec = (__attribute__((address_space(1))) uint64_t *)(arena + off);
       uint32_t key, nr;
-      score_survivor<NQ, NS>(pl, ctr, s, lm, anys, loc, slot_ub, rec, s_sm + threadIdx.x, &key, diag, &nr);
       if (dbg) {
+        __asm__ volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        ts1 = __builtin_amdgcn_s_memtime();
+      }
+      if (units <= ((uint32_t)RC << (6 - sh))) {
+        const LdsRecs lrec{(__attribute__((address_space(3))) uint32_t *)(s_rlo + lane),
+                           (__attribute__((address_space(3))) uint16_t *)(s_rhi + lane), sh, RC << (6 - sh)};
+        score_survivor<NQ, NS>(pl, ctr, s, lm, anys, loc, slot_ub, lrec, s_sm + lane, &key, diag, &nr,
+                               dbg != nullptr, ts2, tmm);
+      } else {
+        const GlobalRecs grec{(__attribute__((address_space(1))) uint64_t *)(arena + off)};
+        score_survivor<NQ, NS>(pl, ctr, s, lm, anys, loc, slot_ub, grec, s_sm + lane, &key, diag, &nr,
+                               dbg != nullptr, ts2, tmm);
+      }
+      if (dbg) {
+        __asm__ volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        ts3 = __builtin_amdgcn_s_memtime();
         dmax = nr > dmax ? nr : dmax;
         dsum += nr;
         dits++;
+        if (ts2 == 0) ts2 = ts3;
+        tseg[0] += ts1 - ts0;
+        tseg[1] += ts2 - ts1;
+        tseg[2] += ts3 - ts2;
       }
       const uint64_t d = cand[s];
       // the paging filter of a widget's next page (Posdb.cpp:7327-7347):
@@ -1426,11 +1608,22 @@ __global__ void __launch_bounds__(SCORE_TPB) k_score(const DevPlan *pl, const ui
       dits += __shfl_xor(dits, o, 64);
     }
     const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+    for (int o = 32; o > 0; o >>= 1)
+      for (int q = 0; q < 3; q++) {
+        const uint64_t m = __shfl_xor(tseg[q], o, 64);
+        tseg[q] = m > tseg[q] ? m : tseg[q];
+        const uint64_t m2 = __shfl_xor(tmm[q], o, 64);
+        tmm[q] = m2 > tmm[q] ? m2 : tmm[q];
+      }
     if (threadIdx.x == 0) {
-      dbg[blockIdx.x * 4 + 0] = t0;
-      dbg[blockIdx.x * 4 + 1] = t1;
-      dbg[blockIdx.x * 4 + 2] = dmax;
-      dbg[blockIdx.x * 4 + 3] = ((uint64_t)dits << 32) | dsum;
+      dbg[blockIdx.x * 8 + 0] = t0;
+      dbg[blockIdx.x * 8 + 1] = t1;
+      dbg[blockIdx.x * 8 + 2] = dmax;
+      dbg[blockIdx.x * 8 + 3] = ((uint64_t)dits << 32) | dsum;
+      dbg[blockIdx.x * 8 + 4] = tseg[0];
+      dbg[blockIdx.x * 8 + 5] = tseg[1];
+      dbg[blockIdx.x * 8 + 6] = tseg[2];
+      dbg[blockIdx.x * 8 + 7] = (tmm[0] & 0xfffff) | ((tmm[1] & 0xfffff) << 20) | ((tmm[2] & 0xfffff) << 40);
     }
   }
 }
@@ -2414,7 +2607,7 @@ using namespace gbgpu;
 struct QuerySlot {
   std::mutex mu;
   hipStream_t stream = nullptr;
-  DevBuf tables, chunkcnt, cand, lmask, ulen, loc, surv, survoff, survlm, scratch, skey, sdoc, sel, gath, res;
+  DevBuf tables, chunkcnt, cand, lmask, ulen, loc, surv, survoff, survlm, survu, perm, scratch, skey, sdoc, sel, gath, res;
   DevBuf dir;           // candidate directories, epoch-tagged (never cleared per query)
   DevBuf split, swin;   // docid splits: one piece's list windows; window table
   DevBuf blk, sflag, sbound, order, tree;  // site clustering: ordered compaction, bounds, TopTree state
@@ -2451,7 +2644,7 @@ struct QuerySlot {
   }
   void release() {
     if (stream) (void)hipStreamSynchronize(stream);
-    DevBuf *bufs[] = {&tables, &chunkcnt, &cand, &lmask, &ulen, &loc, &surv, &survoff, &survlm,
+    DevBuf *bufs[] = {&tables, &chunkcnt, &cand, &lmask, &ulen, &loc, &surv, &survoff, &survlm, &survu, &perm,
                       &scratch, &skey, &sdoc, &sel, &gath, &res, &dir, &split, &swin,
                       &blk, &sflag, &sbound, &order, &tree};
     for (auto *b : bufs) b->release();
@@ -2565,6 +2758,7 @@ static int snapshot_lists(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms, 
   if (!p || nterms < 0 || (nterms && (!terms || !handles))) return EINVAL;
   if (p->docs_to_get <= 0 || p->real_max_top <= 0 || p->num_docid_splits <= 0) return EINVAL;
   if (nterms > 1024) return GBGPU_EUNSUPPORTED;
+  if (p->get_docid_scoring_info) return GBGPU_EUNSUPPORTED;  // second scoring pass: CPU body
   ents.resize(nterms);
   std::lock_guard<std::mutex> g(ctx->lists_mu);
   for (int i = 0; i < nterms; i++) {
@@ -2851,6 +3045,8 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   rc2 |= q.survoff.ensure(8 * slot_ub);
   rc2 |= q.scratch.ensure(8 * scratch_ub);
   rc2 |= q.survlm.ensure(4 * slot_ub);
+  rc2 |= q.survu.ensure(4 * slot_ub);
+  rc2 |= q.perm.ensure(4 * slot_ub * NBKT);  // NBKT bucket regions of slot_ub entries
   rc2 |= q.skey.ensure(4 * slot_ub);
   rc2 |= q.sdoc.ensure(8 * slot_ub);
   rc2 |= q.sel.ensure(sizeof(Select));
@@ -2928,46 +3124,52 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
                        q.dir.as<uint64_t>());
   }
   if (ctx->profiling) HIPCHECK(hipEventRecord(q.ev[2], st));
+  // k_score variant: group / sublist capacity and LDS records per lane
+  int maxsub = 0;
+  for (int j = 0; j < hp.ngroups; j++)
+    if (!(P.gflags0[j] & BF_NEGATIVE)) maxsub = std::max(maxsub, (int)P.gnsub[j]);
+  const int variant = (hp.ngroups <= 2 && maxsub <= 4) ? 0 : (hp.ngroups <= 4 && maxsub <= 4) ? 1
+                      : (hp.ngroups <= 8 && maxsub <= 4) ? 2 : 3;
+  static constexpr uint32_t kRC[4] = {24, 48, 64, 64};  // LDS records per lane
+  const uint32_t rcap = kRC[variant] / 2;  // size buckets: a column holds 2x a bucket-3 survivor's units
   const uint32_t cgrid = std::max(1u, (uint32_t)((slot_ub + CTILE - 1) / CTILE));
   const uint64_t *dcand = q.cand.as<uint64_t>();
   if (!P.clustering) {
     hipLaunchKernelGGL(k_compact<0>, dim3(cgrid), dim3(BLOCK), 0, st, dpl, lmask, q.ulen.as<uint32_t>(), slot_ub,
                        dctr, q.surv.as<uint32_t>(), q.survoff.as<unsigned long long>(), q.survlm.as<uint32_t>(),
-                       (BlkTot *)nullptr, loc, dcand);
+                       (BlkTot *)nullptr, loc, dcand, q.survu.as<uint32_t>(), rcap, q.perm.as<uint32_t>());
   } else {
     // ordered: site clustering's replay walks the survivors in docid order
     BlkTot *blk = q.blk.as<BlkTot>();
     hipLaunchKernelGGL(k_compact<1>, dim3(cgrid), dim3(BLOCK), 0, st, dpl, lmask, q.ulen.as<uint32_t>(), slot_ub,
                        dctr, q.surv.as<uint32_t>(), q.survoff.as<unsigned long long>(), q.survlm.as<uint32_t>(), blk,
-                       loc, dcand);
+                       loc, dcand, q.survu.as<uint32_t>(), rcap, q.perm.as<uint32_t>());
     hipLaunchKernelGGL(k_compact_scan, dim3(1), dim3(1024), 0, st, cgrid, blk, dctr);
     hipLaunchKernelGGL(k_compact<2>, dim3(cgrid), dim3(BLOCK), 0, st, dpl, lmask, q.ulen.as<uint32_t>(), slot_ub,
                        dctr, q.surv.as<uint32_t>(), q.survoff.as<unsigned long long>(), q.survlm.as<uint32_t>(), blk,
-                       loc, dcand);
+                       loc, dcand, q.survu.as<uint32_t>(), rcap, q.perm.as<uint32_t>());
   }
   if (P.reshare_mask)
     hipLaunchKernelGGL(k_ext_walk, dim3(1), dim3(64), 0, st, dpl, dctr, dcand, lmask, q.ulen.as<uint32_t>(),
                        (unsigned long long)(q.scratch.cap / 8));
   if (ctx->profiling) HIPCHECK(hipEventRecord(q.ev[3], st));
   {
-    int maxsub = 0;
-    for (int j = 0; j < hp.ngroups; j++)
-      if (!(P.gflags0[j] & BF_NEGATIVE)) maxsub = std::max(maxsub, (int)P.gnsub[j]);
     const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((slot_ub + SCORE_TPB - 1) / SCORE_TPB, 8192));
     if (ctx->d_sdbg) {
       ctx->sdbg_grid = grid;
-      HIPCHECK(hipMemsetAsync(ctx->d_sdbg, 0, 8192 * 32, st));
+      HIPCHECK(hipMemsetAsync(ctx->d_sdbg, 0, 8192 * 64, st));
     }
     auto launch = [&](auto kern) {
       hipLaunchKernelGGL(kern, dim3(grid), dim3(SCORE_TPB), 0, st, dpl, q.cand.as<uint64_t>(), dctr,
                          q.surv.as<uint32_t>(), q.survlm.as<uint32_t>(), q.survoff.as<unsigned long long>(),
-                         loc, slot_ub, q.scratch.as<uint64_t>(), q.skey.as<uint32_t>(),
-                         q.sdoc.as<uint64_t>(), q.sflag.as<uint8_t>(), ctx->score_mode, ctx->d_sdbg);
+                         q.survu.as<uint32_t>(), q.perm.as<uint32_t>(), loc, slot_ub, q.scratch.as<uint64_t>(),
+                         q.skey.as<uint32_t>(), q.sdoc.as<uint64_t>(), q.sflag.as<uint8_t>(), ctx->score_mode,
+                         ctx->d_sdbg);
     };
-    if (hp.ngroups <= 2 && maxsub <= 4) launch(k_score<2, 4>);
-    else if (hp.ngroups <= 4 && maxsub <= 4) launch(k_score<4, 4>);
-    else if (hp.ngroups <= 8 && maxsub <= 4) launch(k_score<8, 4>);
-    else launch(k_score<MAXG, MAXSUB>);
+    if (variant == 0) launch(k_score<2, 4, kRC[0]>);
+    else if (variant == 1) launch(k_score<4, 4, kRC[1]>);
+    else if (variant == 2) launch(k_score<8, 4, kRC[2]>);
+    else launch(k_score<MAXG, MAXSUB, kRC[3]>);
   }
   if (ctx->profiling) HIPCHECK(hipEventRecord(q.ev[4], st));
   if (clus) {
@@ -3094,7 +3296,7 @@ static int collect(gbgpu_ctx *ctx, QuerySlot &q, gbgpu_result *out, std::vector<
   if (c->tree_err) return GBGPU_ECAPACITY;
   if (c->unsup) return GBGPU_EUNSUPPORTED;
   if (ctx->d_sdbg && ctx->sdbg_grid) {
-    std::vector<uint64_t> h((size_t)ctx->sdbg_grid * 4);
+    std::vector<uint64_t> h((size_t)ctx->sdbg_grid * 8);
     if (hipMemcpy(h.data(), ctx->d_sdbg, h.size() * 8, hipMemcpyDeviceToHost) == hipSuccess)
       if (const char *fn = std::getenv("GBGPU_SCORE_DUMP"))
         if (FILE *f = std::fopen(fn, "ab")) {
@@ -3363,7 +3565,7 @@ int gbgpu_open(int device, gbgpu_ctx **out) {
   }
   if (const char *pm = std::getenv("GBGPU_PROBE_MODE")) ctx->probe_mode = std::atoi(pm);
   if (const char *sm = std::getenv("GBGPU_SCORE_MODE")) ctx->score_mode = std::atoi(sm);
-  if (ctx->score_mode == 2) HIPCHECK(hipMalloc(&ctx->d_sdbg, 8192 * 32));
+  if (ctx->score_mode == 2) HIPCHECK(hipMalloc(&ctx->d_sdbg, 8192 * 64));
   if (const char *de = std::getenv("GBGPU_DEBUG_EXT")) ctx->debug_ext = std::atoi(de);
   *out = ctx;
   return 0;

@@ -62,6 +62,17 @@ __host__ __device__ __forceinline__ uint32_t r_syn(uint64_t r) { return (uint32_
 __host__ __device__ __forceinline__ uint32_t r_hswb(uint64_t r) { return (uint32_t)(r >> 16) & 0x1; }
 __host__ __device__ __forceinline__ uint32_t r_dens(uint64_t r) { return (uint32_t)(r >> 11) & 0x1f; }
 
+// score /= (dist + 1.0) of the reference: a float promoted to double,
+// divided, rounded back to float.  dist + 1 is an integer below 2^24, exact
+// in either precision, and rounding a double quotient of two floats to float
+// gives the correctly rounded float quotient (53 >= 2 * 24 + 2: double
+// rounding is innocuous for division), so one IEEE float division yields the
+// same bits without the f64 divide sequence.
+template <class D>
+__device__ __forceinline__ float div_dist(float score, D dist) {
+  return score / (float)(dist + 1);
+}
+
 // register-array access with a runtime index (unrolled select chains)
 template <int N, class T>
 __device__ __forceinline__ T rget(const T (&a)[N], int i) {
@@ -87,10 +98,35 @@ constexpr int npairs() {
   return NQ * (NQ - 1) / 2;
 }
 
-// What one docid's scorer sees: nq groups, each a record range.  RP is the
-// record pointer type: an LDS (address space 3) or global (1) pointer, so
-// every record read compiles to a ds_read or global_load, never a flat one.
-template <int NQ, class RP = const uint64_t *>
+// Where one docid's records live.  RP is one of these two record stores, so
+// every record access compiles to a ds_read/ds_write or a global load/store,
+// never a flat one.
+//  LdsRecs:    the lane's column of the wave's LDS record arrays, [cap][S]
+//              for S survivors per wave (48-bit records split 32 + 16 bits;
+//              consecutive lanes hit consecutive banks, so a wave's record
+//              reads are conflict-free);
+//  GlobalRecs: a contiguous range of the global record arena.
+struct LdsRecs {
+  __attribute__((address_space(3))) uint32_t *lo;
+  __attribute__((address_space(3))) uint16_t *hi;
+  int sh;   // log2 of the column stride (the survivors sharing the wave's arrays)
+  int cap;  // records the column holds
+  __device__ __forceinline__ uint64_t operator[](int r) const {
+    return (uint64_t)lo[r << sh] | ((uint64_t)hi[r << sh] << 32);
+  }
+  __device__ __forceinline__ void put(int r, uint64_t v) const {
+    lo[r << sh] = (uint32_t)v;
+    hi[r << sh] = (uint16_t)(v >> 32);
+  }
+};
+struct GlobalRecs {
+  __attribute__((address_space(1))) uint64_t *p;
+  __device__ __forceinline__ uint64_t operator[](int r) const { return p[r]; }
+  __device__ __forceinline__ void put(int r, uint64_t v) const { p[r] = v; }
+};
+
+// What one docid's scorer sees: nq groups, each a record range in rec.
+template <int NQ, class RP>
 struct DocView {
   RP rec;  // records (ranges are indices into rec)
   int beg[NQ], end[NQ];
@@ -248,7 +284,7 @@ __device__ __forceinline__ float pair_score_nonbody(const ScoreCtx<NQ> &c, const
         if (r_syn(ki)) score *= GB_SYNONYM_WEIGHT;
         if (r_syn(kj)) score *= GB_SYNONYM_WEIGHT;
         score *= spamw1 * spamw2;
-        score /= (dist + 1.0);
+        score = div_dist(score, dist);
         if (score > max) max = score;
       }
       if (++wi >= endi) break;
@@ -274,7 +310,7 @@ __device__ __forceinline__ float pair_score_nonbody(const ScoreCtx<NQ> &c, const
         if (r_syn(ki)) score *= GB_SYNONYM_WEIGHT;
         if (r_syn(kj)) score *= GB_SYNONYM_WEIGHT;
         score *= spamw1 * spamw2;
-        score /= (dist + 1.0);
+        score = div_dist(score, dist);
         if (score > max) max = score;
       }
       if (++wj >= endj) break;
@@ -317,7 +353,50 @@ __device__ __forceinline__ float pair_score_window(const Weights &W, int cqdist,
   if (r_syn(ki)) score *= GB_SYNONYM_WEIGHT;
   if (r_syn(kj)) score *= GB_SYNONYM_WEIGHT;
   score *= spamw1 * spamw2;
-  score /= (dist + 1.0);
+  score = div_dist(score, dist);
+  return score;
+}
+
+// One occurrence as getTermPairScoreForWindow reads it: its word position
+// and weight factors, looked up once per record instead of per pair call.
+struct WinRec {
+  int32_t p;
+  float spamw, denw, hgw;
+  bool syn, valid;
+};
+__device__ __forceinline__ WinRec win_rec(const Weights &W, uint64_t k) {
+  WinRec r;
+  const uint32_t hg = r_hg(k);
+  r.p = (int32_t)r_wordpos(k);
+  r.spamw = (hg == GB_HG_INLINKTEXT) ? W.linker[r_wsr(k)] : W.wordspam[r_wsr(k)];
+  r.denw = W.density[r_dens(k)];
+  r.hgw = W.hashgroup[hg];
+  r.syn = r_syn(k) != 0;
+  r.valid = true;
+  return r;
+}
+// pair_score_window on WinRecs (same expression order, so the same bits)
+__device__ __forceinline__ float pair_score_window_rec(int cqdist, const WinRec &a, const WinRec &b,
+                                                      int32_t fixedDistance) {
+  if (!a.valid) return -1.00;
+  if (!b.valid) return -1.00;
+  float dist, score;
+  if (fixedDistance != 0) {
+    dist = fixedDistance;
+  } else {
+    if (b.p < a.p) dist = a.p - b.p;
+    else dist = b.p - a.p;
+    if (dist < 2) dist = 2;
+    if (dist >= cqdist) dist = dist - cqdist;
+    if (b.p < a.p) dist += 1;
+  }
+  score = 100 * a.denw * b.denw;
+  score *= a.hgw;
+  score *= b.hgw;
+  if (a.syn) score *= GB_SYNONYM_WEIGHT;
+  if (b.syn) score *= GB_SYNONYM_WEIGHT;
+  score *= a.spamw * b.spamw;
+  score = div_dist(score, dist);
   return score;
 }
 
@@ -455,7 +534,7 @@ __device__ __forceinline__ float pair_score_any(const ScoreCtx<NQ> &c, const Doc
         if (r_hswb(ki)) score *= GB_WIKI_BIGRAM_WEIGHT;
         if (r_hswb(kj)) score *= GB_WIKI_BIGRAM_WEIGHT;
         score *= spamw1 * spamw2;
-        score /= (dist + 1.0);
+        score = div_dist(score, dist);
         scored = true;
       }
     } else {
@@ -481,7 +560,7 @@ __device__ __forceinline__ float pair_score_any(const ScoreCtx<NQ> &c, const Doc
         if (r_syn(ki)) score *= GB_SYNONYM_WEIGHT;
         if (r_syn(kj)) score *= GB_SYNONYM_WEIGHT;
         score *= spamw1 * spamw2;
-        score /= (dist + 1.0);
+        score = div_dist(score, dist);
         scored = true;
       }
     }
@@ -560,7 +639,7 @@ __device__ __forceinline__ float pair_score_any(const ScoreCtx<NQ> &c, const Doc
 // (npairs<NQ>() floats at stride smStride).
 template <int NQ, class RP>
 __device__ __forceinline__ bool score_doc(const Weights *w, const DevPlan *pl, const DocView<NQ, RP> &d, int siteRank, int docLang,
-                                 float *sm, int smStride, float *outScore) {
+                                 float *sm, int smStride, float *outScore, int stop = 0) {
   ScoreCtx<NQ> c;
   c.w = w;
   c.pl = pl;
@@ -601,6 +680,10 @@ __device__ __forceinline__ bool score_doc(const Weights *w, const DevPlan *pl, c
       sm[pair_index<NQ>(i, j) * smStride] = v;
     }
   }
+  if (stop == 3) {  // diagnostic (GBGPU_SCORE_MODE=3): stop after the non-body pairs
+    *outScore = sm[0];
+    return true;
+  }
   // single term scores, Posdb.cpp:6933-6978
   float minSingleScore = 999999999.0;
 #pragma unroll
@@ -611,6 +694,10 @@ __device__ __forceinline__ bool score_doc(const Weights *w, const DevPlan *pl, c
     const float sts = single_term_score(c, d, i, &bp);
     rset(bestPos, i, bp);
     if (sts < minSingleScore) minSingleScore = sts;
+  }
+  if (stop == 4) {  // diagnostic: stop after the single-term scores
+    *outScore = minSingleScore + (float)bestPos[0];
+    return true;
   }
   // sliding window, Posdb.cpp:7013-7150
   c.bestWindowScore = -2.0;
@@ -633,7 +720,103 @@ __device__ __forceinline__ bool score_doc(const Weights *w, const DevPlan *pl, c
       if (xp >= 0) allNull = false;
     }
   }
-  if (!allNull) {
+  bool fast2 = false;
+  if constexpr (NQ == 2) fast2 = c.nq == 2 && c.excl == 0;
+  if (!allNull && fast2) {
+    // Two groups, one pair: the same walk with the pair's four window terms
+    // kept in registers.  (best, best) never changes and (best, window) /
+    // (window, best) only when that window pointer moves, so a step scores
+    // two of the four; each pointer's record fields are read once.
+    const Weights &W = s_weights;
+    float wikiWeight;
+    int cq;
+    if (pl->wiki[1] == pl->wiki[0] && pl->wiki[1]) {
+      cq = pl->qpos[1] - pl->qpos[0];
+      wikiWeight = GB_WIKI_WEIGHT;
+    } else {
+      cq = 2;
+      wikiWeight = 1.0;
+    }
+    const float tf = pl->tfw[0] * pl->tfw[1];
+    const float smv = sm[0];
+    const bool quoted = pl->quote[1] >= 0 && pl->quote[1] == pl->quote[0];
+    const int32_t qd = pl->qpos[1] - pl->qpos[0];
+    WinRec b0{0, 0, 0, 0, false, false}, b1{0, 0, 0, 0, false, false};
+    if (bestPos[0] >= 0) b0 = win_rec(W, d.rec[bestPos[0]]);
+    if (bestPos[1] >= 0) b1 = win_rec(W, d.rec[bestPos[1]]);
+    WinRec w0{0, 0, 0, 0, false, false}, w1{0, 0, 0, 0, false, false};
+    int x0 = xpos[0], x1 = xpos[1];
+    if (x0 >= 0) w0 = win_rec(W, d.rec[x0]);
+    if (x1 >= 0) w1 = win_rec(W, d.rec[x1]);
+    const float sbb = pair_score_window_rec(cq, b0, b1, FIXED_DISTANCE);
+    float sbw = pair_score_window_rec(cq, b0, w1, FIXED_DISTANCE);
+    float swb = pair_score_window_rec(cq, w0, b1, FIXED_DISTANCE);
+    const int e0 = d.end[0], e1 = d.end[1];
+    for (;;) {
+      float mx = pair_score_window_rec(cq, w0, w1, 0);
+      if (sbw > mx) mx = sbw;
+      if (sbb > mx) mx = sbb;
+      if (swb > mx) mx = swb;
+      if (wikiWeight != 1.0) mx *= wikiWeight;
+      mx *= tf;
+      if (smv > mx) mx = smv;
+      if (quoted) {
+        if (x0 < 0) {
+          mx = -1.0;
+        } else if (x1 < 0) {
+          mx = -1.0;
+        } else {
+          const int32_t dist = w1.p - w0.p;
+          if (dist < 0) mx = -1.0;
+          else if (dist > qd && dist - qd > 1) mx = -1.0;
+          else if (dist < qd && qd - dist > 1) mx = -1.0;
+        }
+      }
+      float minTPS = 999999999.0;
+      if (mx < minTPS) minTPS = mx;
+      if (!(minTPS <= c.bestWindowScore)) {
+        c.bestWindowScore = minTPS;
+        c.window[0] = x0;
+        c.window[1] = x1;
+      }
+      bool done = false;
+      for (;;) {  // advanceMin: the lower position moves (term 0 on ties)
+        const bool m0 = x0 >= 0 && (x1 < 0 || (uint32_t)w0.p <= (uint32_t)w1.p);
+        int xp = m0 ? x0 : x1;
+        const int xe = m0 ? e0 : e1;
+        bool exhausted = false;
+        uint64_t k = 0;
+        for (;;) {  // advanceAgain
+          xp++;
+          if (xp >= xe) {
+            xp = -1;
+            exhausted = true;
+            break;
+          }
+          k = d.rec[xp];
+          if (W.in_body[r_hg(k)]) break;
+        }
+        WinRec nr{0, 0, 0, 0, false, false};
+        if (!exhausted) nr = win_rec(W, k);
+        if (m0) {
+          x0 = xp;
+          w0 = nr;
+          swb = pair_score_window_rec(cq, w0, b1, FIXED_DISTANCE);
+        } else {
+          x1 = xp;
+          w1 = nr;
+          sbw = pair_score_window_rec(cq, b0, w1, FIXED_DISTANCE);
+        }
+        if (!exhausted) break;  // -> slideMore
+        if (x0 < 0 && x1 < 0) {
+          done = true;
+          break;
+        }
+      }
+      if (done) break;
+    }
+  }
+  if (!allNull && !fast2) {
     for (;;) {
       eval_window(c, d, xpos, bestPos);
       bool done = false;
@@ -672,6 +855,10 @@ __device__ __forceinline__ bool score_doc(const Weights *w, const DevPlan *pl, c
       }
       if (done) break;
     }
+  }
+  if (stop == 5) {  // diagnostic: stop after the sliding window
+    *outScore = c.bestWindowScore + (float)c.window[0];
+    return true;
   }
   // window-restricted pair scores, Posdb.cpp:7159-7219
   float minPairScore = -1.0;

@@ -53,7 +53,7 @@ class Params(ctypes.Structure):
         ("num_docid_splits", ctypes.c_int32),
         ("same_lang_weight", ctypes.c_float),
         ("do_max_score_algo", ctypes.c_int32),
-        ("reserved0", ctypes.c_int32),
+        ("get_docid_scoring_info", ctypes.c_int32),
         ("max_serp_score", ctypes.c_double),
         ("min_serp_docid", ctypes.c_int64),
     ]

@@ -137,6 +137,20 @@ def test_unsupported_modes_fail_loudly(engine):
     with pytest.raises(gbgpu.GbgpuError) as e:
         engine.query(terms, lists, p)
     assert e.value.code == gbgpu.GBGPU_EUNSUPPORTED
+    # the per-docid scoring-info second pass (m_getDocIdScoringInfo) stays on the CPU
+    p2 = q.params()
+    p2.get_docid_scoring_info = 1
+    with pytest.raises(gbgpu.GbgpuError) as e:
+        engine.query(q.terms, lists, p2)
+    assert e.value.code == gbgpu.GBGPU_EUNSUPPORTED
+    hs = [engine.upload(l) for l in lists]
+    try:
+        with pytest.raises(gbgpu.GbgpuError) as e:
+            engine.query_resident(q.terms, hs, p2)
+        assert e.value.code == gbgpu.GBGPU_EUNSUPPORTED
+    finally:
+        for h in hs:
+            engine.free(h)
 
 
 def test_query_slots_in_flight_together(engine):
