@@ -347,7 +347,7 @@ __global__ void __launch_bounds__(BLOCK) k_write_runs(const DevPlan *pl, const G
 // k_probe -- addDocIdVotes for groups g>0 and rmDocIdVotes (Posdb.cpp:5086-
 // 5171, 4871-4946), all lists in one launch.  Every WAVE works alone (no
 // block barrier anywhere): it owns a contiguous span of one list and walks it
-// in 3 KiB chunks (512 six-byte units, 48 bytes = 8 whole units per lane),
+// in 3 KiB chunks (512 six-byte units as three coalesced 1 KiB wave loads),
 // loaded straight into registers two chunks ahead of use.  Per chunk:
 //   1. each lane classifies its 8 units by the alignment bit (Posdb.h:887-
 //      889); the run starts (<= 4 per lane: a run's 12-byte head is 2 units)
@@ -366,21 +366,26 @@ __global__ void __launch_bounds__(BLOCK) k_write_runs(const DevPlan *pl, const G
 // MODE (diagnostic, GBGPU_PROBE_MODE): 0 full, 1 stop after the run-start
 // compaction, 2 load chunks only, 3 skip the run-driven lists.
 constexpr int PW = 4;                      // waves per probe block
-constexpr int WCH_UNITS = 512;             // units per wave chunk
-constexpr int WCH_BYTES = WCH_UNITS * 6;   // 3 KiB
+constexpr int WPIECES = 3;                 // 1 KiB wave loads per chunk
+constexpr int WCH_BYTES = WPIECES * 1024;  // 3 KiB
+constexpr int WCH_UNITS = WCH_BYTES / 6;   // units per wave chunk
+static_assert(WCH_BYTES % 6 == 0, "a chunk holds whole units");
 constexpr int WMAX_RUNS = WCH_UNITS / 2;
 constexpr uint32_t PROBE_WAVES = 256 * 16;
 
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 struct WChunk {
-  v4u v[3];   // this lane's 48 bytes
+  v4u v[WPIECES];  // piece i: bytes i*1024 + 16*lane
   uint2 nb;   // lane 63: the 8 bytes after the chunk (docid of a 12-byte key at unit 511)
 };
 
+// The chunk as three fully coalesced 1 KiB wave loads: piece i of lane L is
+// bytes i*1024 + 16L .. +16 (a 48-byte-per-lane layout would make each load
+// instruction touch the whole 3 KiB; measured 1.5x slower as a pure scan).
 __device__ __forceinline__ void wchunk_fetch(const uint8_t *list, uint32_t u0, int lane, WChunk &c) {
-  const auto *src = glc<v4u>(list + (size_t)u0 * 6 + lane * 48);
+  const auto *src = glc<v4u>(list + (size_t)u0 * 6 + lane * 16);
 #pragma unroll
-  for (int i = 0; i < 3; i++) c.v[i] = __builtin_nontemporal_load(src + i);
+  for (int i = 0; i < WPIECES; i++) c.v[i] = __builtin_nontemporal_load(src + i * 64);
   c.nb = make_uint2(0, 0);
   if (lane == 63) {
     typedef uint32_t v2 __attribute__((ext_vector_type(2)));
@@ -513,6 +518,7 @@ __device__ __forceinline__ void mbuf_push(ProbeLds &S, uint32_t &nbuf, bool hit,
 __device__ __noinline__ void mbuf_flush_n(ProbeLds *S, uint32_t nbuf, uint32_t *lmask, uint32_t *ulen, Loc *loc_l,
                                           uint32_t bit, uint32_t mult, int lane) {
   wave_lds_sync();
+  if (!bit) nbuf = 0;  // diagnostic (GBGPU_PROBE_MODE=5): matches not published
   for (uint32_t i = lane; i < nbuf; i += 64) {
     const uint32_t slot = S->mslot[i], len = S->mlen[i];
     loc_l[slot] = Loc{S->mu[i], len};
@@ -526,46 +532,69 @@ __device__ __forceinline__ void mbuf_flush(ProbeLds &S, uint32_t &nbuf, const Pr
   nbuf = 0;
 }
 
-// Classify this lane's 8 units, compact the wave's run starts into S (sorted
-// docids + unit offsets within the chunk).  Returns the run count.
+// Classify the chunk's units and compact the wave's run starts into S (sorted
+// docids + unit offsets within the chunk).  Returns the run count.  Piece by
+// piece (wchunk_fetch's layout): lane L's 16 bytes plus the 12 that follow
+// (the next lane's, or the next piece's lane 0, or the bytes after the chunk)
+// hold every unit starting in its 16 bytes -- 2 or 3 of them, the first at
+// byte o0 = (-P) mod 6 in {0, 2, 4} -- whole, docid bytes included; the window
+// is realigned to o0 with byte funnel shifts, so every byte is then read at a
+// compile-time offset.
 __device__ __forceinline__ uint32_t chunk_runs(const WChunk &cur, uint32_t u0, uint32_t u1, int lane, ProbeLds &S) {
-  uint32_t r[14];
-#pragma unroll
-  for (int i = 0; i < 3; i++) {
-    r[4 * i] = cur.v[i].x;
-    r[4 * i + 1] = cur.v[i].y;
-    r[4 * i + 2] = cur.v[i].z;
-    r[4 * i + 3] = cur.v[i].w;
-  }
-  // bytes 48..55 of this lane = the next lane's first 8 bytes
-  r[12] = __shfl_down(r[0], 1, 64);
-  r[13] = __shfl_down(r[1], 1, 64);
-  if (lane == 63) {
-    r[12] = cur.nb.x;
-    r[13] = cur.nb.y;
-  }
-  auto byte = [&](int i) -> uint32_t { return (r[i >> 2] >> ((i & 3) * 8)) & 0xff; };
-  uint32_t starts = 0;
-#pragma unroll
-  for (int q = 0; q < 8; q++) {
-    const uint32_t gu = u0 + lane * 8 + q;
-    if (gu < u1 && (byte(6 * q + 1) & 0x02) && !(byte(6 * q) & 0x04)) starts |= 1u << q;
-  }
-  const uint32_t cnt = __popc(starts);
   const uint64_t lt = (1ull << lane) - 1;
-  const uint64_t b0 = __ballot(cnt & 1), b1 = __ballot(cnt & 2), b2 = __ballot(cnt & 4);
-  const uint32_t nrun = (uint32_t)(__popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2));
-  uint32_t o = (uint32_t)(__popcll(b0 & lt) + 2 * __popcll(b1 & lt) + 4 * __popcll(b2 & lt));
+  uint32_t nrun = 0;
 #pragma unroll
-  for (int q = 0; q < 8; q++) {
-    if (!(starts >> q & 1)) continue;
-    uint64_t d = 0;
+  for (int i = 0; i < WPIECES; i++) {
+    uint32_t r[7];
+    r[0] = cur.v[i].x;
+    r[1] = cur.v[i].y;
+    r[2] = cur.v[i].z;
+    r[3] = cur.v[i].w;
+    r[4] = __shfl_down(cur.v[i].x, 1, 64);
+    r[5] = __shfl_down(cur.v[i].y, 1, 64);
+    r[6] = __shfl_down(cur.v[i].z, 1, 64);
+    if (i + 1 < WPIECES) {
+      const uint32_t m0 = __shfl(cur.v[i + 1].x, 0, 64), m1 = __shfl(cur.v[i + 1].y, 0, 64),
+                     m2 = __shfl(cur.v[i + 1].z, 0, 64);
+      if (lane == 63) {
+        r[4] = m0;
+        r[5] = m1;
+        r[6] = m2;
+      }
+    } else if (lane == 63) {
+      r[4] = cur.nb.x;
+      r[5] = cur.nb.y;
+      r[6] = 0;
+    }
+    const uint32_t P = (uint32_t)i * 1024 + (uint32_t)lane * 16;
+    const uint32_t k0 = (P + 5) / 6;  // first unit starting in [P, P + 16)
+    const uint32_t o0 = k0 * 6 - P;
+    uint32_t a[6];
 #pragma unroll
-    for (int i = 4; i >= 0; i--) d = (d << 8) | byte(6 * q + 7 + i);
-    S.doc[o] = d >> 2;
-    S.unit[o] = (uint16_t)(lane * 8 + q);
-    S.claim[o] = 0;
-    o++;
+    for (int j = 0; j < 6; j++)  // v_alignbyte shifts by 0-3 bytes: o0 = 4 is a whole dword
+      a[j] = o0 == 4 ? r[j + 1] : __builtin_amdgcn_alignbyte(r[j + 1], r[j], o0);
+    auto byte = [&](int b) -> uint32_t { return (a[b >> 2] >> ((b & 3) * 8)) & 0xff; };
+    uint32_t starts = 0;
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+      const bool in = 6 * q + o0 < 16 && u0 + k0 + q < u1;
+      if (in && (byte(6 * q + 1) & 0x02) && !(byte(6 * q) & 0x04)) starts |= 1u << q;
+    }
+    const uint32_t cnt = __popc(starts);  // <= 2: a run head spans two units
+    const uint64_t b0 = __ballot(cnt & 1), b1 = __ballot(cnt & 2);
+    uint32_t o = nrun + (uint32_t)(__popcll(b0 & lt) + 2 * __popcll(b1 & lt));
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+      if (!(starts >> q & 1)) continue;
+      uint64_t d = 0;
+#pragma unroll
+      for (int b = 4; b >= 0; b--) d = (d << 8) | byte(6 * q + 7 + b);
+      S.doc[o] = d >> 2;
+      S.unit[o] = (uint16_t)(k0 + q);
+      S.claim[o] = 0;
+      o++;
+    }
+    nrun += (uint32_t)(__popcll(b0) + 2 * __popcll(b1));
   }
   wave_lds_sync();
   return nrun;
@@ -609,12 +638,13 @@ __device__ void probe_by_cand(const DevPlan *pl, const ProbeWork &w, const DevLi
   wchunk_fetch(lp, w.u0, lane, c0);
   wchunk_fetch(lp, min(w.u0 + WCH_UNITS, last_u0), lane, c1);
   // where each array's candidates meet this span (peeled out of the loop)
-  const uint64_t dfirst = MODE == 0 ? first_run_doc(L, w.u0, w.u1, lane) : 0;
+  constexpr bool FULL = MODE == 0 || MODE == 5;
+  const uint64_t dfirst = FULL ? first_run_doc(L, w.u0, w.u1, lane) : 0;
 #pragma unroll
   for (int k = 0; k < G0; k++) {
     nk[k] = k < g0n ? ctr->g0count[k] : 0;
     base[k] = k < g0n ? pl->g0base[k] : 0;
-    lok[k] = (MODE == 0 && k < g0n) ? wave_lower_bound_dir(pl, k, cand + base[k], nk[k], dir, dfirst, lane) : 0;
+    lok[k] = (FULL && k < g0n) ? wave_lower_bound_dir(pl, k, cand + base[k], nk[k], dir, dfirst, lane) : 0;
     pf[k] = cand[base[k] + min(lok[k] + lane, max(nk[k], 1u) - 1)];
   }
   uint32_t nbuf = 0;
@@ -623,9 +653,9 @@ __device__ void probe_by_cand(const DevPlan *pl, const ProbeWork &w, const DevLi
   for (uint32_t u0 = w.u0; u0 < w.u1; u0 += WCH_UNITS) {
     const WChunk cur = c0;
     c0 = c1;
-    wchunk_fetch(lp, min(u0 + 2 * WCH_UNITS, last_u0), lane, c1);
     if (MODE == 2) {
-      if (cur.v[0].x == 0x557713eeu && cur.v[1].y == 7u && cur.nb.x == 3u) po.lmask[0] = 1;
+      if (cur.v[0].x == 0x557713eeu && cur.v[1].y == 7u && cur.v[2].z == 3u) po.lmask[0] = 1;
+      wchunk_fetch(lp, min(u0 + 2 * WCH_UNITS, last_u0), lane, c1);
       continue;
     }
     const uint32_t nrun = chunk_runs(cur, u0, w.u1, lane, S);
@@ -636,35 +666,49 @@ __device__ void probe_by_cand(const DevPlan *pl, const ProbeWork &w, const DevLi
     }
     if (MODE == 1) {
       if (nrun && S.doc[0] == 0x123456789ull) po.lmask[0] = 1;
+      wchunk_fetch(lp, min(u0 + 2 * WCH_UNITS, last_u0), lane, c1);
       continue;
     }
     const uint64_t dmax = nrun ? S.doc[nrun - 1] : 0;
+    // every array's prefetched block is searched at once (the arrays' LDS
+    // round trips overlap); claims are then settled array by array, in order
+    uint64_t dk[G0];
+    uint32_t pa[G0];
+#pragma unroll
+    for (int k = 0; k < G0; k++) {
+      dk[k] = (k < g0n && lok[k] + lane < nk[k]) ? pf[k] : ~0ull;
+      pa[k] = 0;
+    }
+    // branchless lower bound (nrun <= WMAX_RUNS): no divergence, no
+    // exec-mask bookkeeping, every array's read of a step issued together
+#pragma unroll
+    for (uint32_t step = WMAX_RUNS; step > 0; step >>= 1) {
+#pragma unroll
+      for (int k = 0; k < G0; k++) {
+        const uint32_t t = pa[k] + step;
+        const uint64_t v = S.doc[min(t, max(nrun, 1u)) - 1];
+        if (t <= nrun && v < dk[k]) pa[k] = t;
+      }
+    }
 #pragma unroll
     for (int k = 0; k < G0; k++) {
       if (k >= g0n) break;
       const uint64_t *ck = cand + base[k];
       uint32_t lo = lok[k];
-      // one pass: the 64 candidates from lo (one per lane) against the runs
-      auto pass = [&](uint64_t d) -> uint32_t {
+      // one pass: the 64 candidates from lo (one per lane) against the runs;
+      // a is d's lower bound in the runs (searched by the caller)
+      auto settle = [&](uint64_t d, uint32_t a) -> uint32_t {
         const bool in = nrun && d <= dmax;
         bool hit = false, last = false;
         uint32_t u = 0, len = 0;
-        if (in) {
-          uint32_t a = 0, b = nrun;
-          while (a < b) {
-            const uint32_t mid = (a + b) >> 1;
-            if (S.doc[mid] < d) a = mid + 1;
-            else b = mid;
-          }
-          if (a < nrun && S.doc[a] == d && !S.claim[a]) {
-            S.claim[a] = 1;
-            u = u0 + S.unit[a];
-            if (a + 1 < nrun) {
-              hit = true;
-              len = S.unit[a + 1] - S.unit[a];
-            } else {
-              last = true;  // ends at the next chunk's first run start
-            }
+        if (in && a < nrun && S.doc[a] == d && !S.claim[a]) {
+          S.claim[a] = 1;
+          u = u0 + S.unit[a];
+          if (a + 1 < nrun) {
+            hit = true;
+            len = S.unit[a + 1] - S.unit[a];
+          } else {
+            last = true;  // ends at the next chunk's first run start
           }
         }
         if (nbuf + 64 > MBUF) mbuf_flush(S, nbuf, po, lane);
@@ -678,19 +722,29 @@ __device__ void probe_by_cand(const DevPlan *pl, const ProbeWork &w, const DevLi
         lo += nin;
         return nin;
       };
-      // the first pass reads the prefetched block; a chunk meeting more than
-      // 64 candidates (dense arrays) reloads in a loop of its own, so the
-      // prefetched register never merges with a just-loaded one
-      if (pass(lo + lane < nk[k] ? pf[k] : ~0ull) == 64u) {
+      // a chunk meeting more than 64 candidates (dense arrays) reloads in a
+      // loop of its own, so the prefetched register never merges with a
+      // just-loaded one
+      if (settle(dk[k], pa[k]) == 64u) {
         for (;;) {
           const uint64_t d = lo + lane < nk[k] ? ck[lo + lane] : ~0ull;
-          if (pass(d) < 64u) break;
+          uint32_t a = 0;
+#pragma unroll
+          for (uint32_t step = WMAX_RUNS; step > 0; step >>= 1) {
+            const uint32_t t = a + step;
+            const uint64_t v = S.doc[min(t, max(nrun, 1u)) - 1];
+            if (t <= nrun && v < d) a = t;
+          }
+          if (settle(d, a) < 64u) break;
         }
       }
       lok[k] = lo;
       // the next chunk starts at lo
       pf[k] = ck[min(lo + lane, max(nk[k], 1u) - 1)];
     }
+    // the next-but-one chunk, issued after the candidate blocks: vmcnt is in
+    // order, so the next chunk's wait on them does not wait for this fetch
+    wchunk_fetch(lp, min(u0 + 2 * WCH_UNITS, last_u0), lane, c1);
     wave_lds_sync();  // the next chunk rewrites the run list
   }
   if (pend_slot != ~0ull) {
@@ -794,7 +848,7 @@ __global__ void __launch_bounds__(64 * PW) k_probe(const DevPlan *pl, const Prob
   po.lmask = lmask;
   po.ulen = ulen;
   po.loc_l = loc + (uint64_t)w.list * slot_ub;
-  po.bit = 1u << w.list;
+  po.bit = MODE == 5 ? 0u : 1u << w.list;
   // arena units this list adds per matched run: one copy per positive group
   // it belongs to (a shared bigram sublist is merged into both groups)
   po.mult = __popc(L.group_bits & pl->pos_mask & ~NEG_BIT);
@@ -3111,7 +3165,8 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
                      q.dir.as<uint64_t>());
   if (ctx->profiling) HIPCHECK(hipEventRecord(q.ev[1], st));
   if (!q.pw.empty()) {
-    auto kp = ctx->probe_mode == 3   ? k_probe<3, MAXG0>
+    auto kp = ctx->probe_mode == 5   ? k_probe<5, 2>
+              : ctx->probe_mode == 3 ? k_probe<3, MAXG0>
               : ctx->probe_mode == 2 ? k_probe<2, MAXG0>
               : ctx->probe_mode == 1 ? k_probe<1, MAXG0>
               : P.g0n == 1           ? k_probe<0, 1>
