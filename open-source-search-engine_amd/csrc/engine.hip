@@ -176,8 +176,9 @@ __device__ __forceinline__ uint32_t thread_starts(const uint8_t *lds, uint32_t u
   return m;
 }
 
+template <int NT = BLOCK>
 __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t *tmp, uint32_t *total) {
-  // tmp: BLOCK/64 words of LDS
+  // tmp: NT/64 words of LDS
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   uint32_t x = v;
 #pragma unroll
@@ -188,7 +189,7 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t *t
   if (lane == 63) tmp[wid] = x;
   __syncthreads();
   uint32_t base = 0, tot = 0;
-  for (int w = 0; w < BLOCK / 64; w++) {
+  for (int w = 0; w < NT / 64; w++) {
     if (w < wid) base += tmp[w];
     tot += tmp[w];
   }
@@ -861,7 +862,8 @@ __global__ void __launch_bounds__(64 * PW) k_probe(const DevPlan *pl, const Prob
 
 // ------------------------------------------------------------- compaction
 constexpr int CSPT = 16;                        // compaction slots per thread
-constexpr int CTILE = BLOCK * CSPT;              // 4096 slots per block
+constexpr int CBLOCK = 1024;                     // compaction threads per block
+constexpr int CTILE = CBLOCK * CSPT;             // 16384 slots per block (few blocks: few global atomics)
 
 // Survivors of one contiguous tile of candidate slots (slot = tile base +
 // q*BLOCK + thread: coalesced), appended with ONE pair of atomics per block
@@ -896,12 +898,12 @@ __host__ __device__ __forceinline__ int size_bucket(uint32_t u, uint32_t rc) {
 __host__ __device__ __forceinline__ int bucket_shift(int b) { return b == 0 ? 3 : b == 1 ? 4 : b == 2 ? 5 : 6; }
 
 template <int CMODE>
-__global__ void __launch_bounds__(BLOCK) k_compact(const DevPlan *pl, const uint32_t *lmask, const uint32_t *ulen,
+__global__ void __launch_bounds__(CBLOCK) k_compact(const DevPlan *pl, const uint32_t *lmask, const uint32_t *ulen,
                                                    uint64_t slot_ub, Counters *ctr, uint32_t *surv,
                                                    unsigned long long *surv_off, uint32_t *surv_lm, BlkTot *blk,
                                                    const Loc *loc, const uint64_t *cand, uint32_t *surv_u,
                                                    uint32_t rc, uint32_t *perm) {
-  __shared__ uint32_t tmp[BLOCK / 64];
+  __shared__ uint32_t tmp[CBLOCK / 64];
   __shared__ uint32_t s_bcnt[NBKT], s_bbase[NBKT], s_bcur[NBKT];
   __shared__ uint32_t s_xu[MAXL];            // CMODE 0/1: re-shrunk lists' survivor run units
   __shared__ unsigned long long s_xd[MAXL];  // ... and their last survivor docid
@@ -934,7 +936,7 @@ __global__ void __launch_bounds__(BLOCK) k_compact(const DevPlan *pl, const uint
   // a thread's slots: strided over the block (coalesced) -- or, ordered, 16
   // consecutive ones, so thread order is slot order inside the block
   const uint64_t s0 = (uint64_t)blockIdx.x * CTILE + (CMODE ? threadIdx.x * CSPT : threadIdx.x);
-  constexpr uint64_t SSTEP = CMODE ? 1 : BLOCK;
+  constexpr uint64_t SSTEP = CMODE ? 1 : CBLOCK;
   // all of this thread's list masks in flight at once
   uint32_t lmv[CSPT];
 #pragma unroll
@@ -1018,8 +1020,8 @@ __global__ void __launch_bounds__(BLOCK) k_compact(const DevPlan *pl, const uint
     }
   }
   uint32_t tot_n, tot_u;
-  const uint32_t ex_n = block_exclusive_scan(nok, tmp, &tot_n);
-  const uint32_t ex_u = block_exclusive_scan(utot, tmp, &tot_u);
+  const uint32_t ex_n = block_exclusive_scan<CBLOCK>(nok, tmp, &tot_n);
+  const uint32_t ex_u = block_exclusive_scan<CBLOCK>(utot, tmp, &tot_u);
   if (CMODE != 2 && any) atomicOr(&s_any, any);
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -3190,17 +3192,17 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   const uint32_t cgrid = std::max(1u, (uint32_t)((slot_ub + CTILE - 1) / CTILE));
   const uint64_t *dcand = q.cand.as<uint64_t>();
   if (!P.clustering) {
-    hipLaunchKernelGGL(k_compact<0>, dim3(cgrid), dim3(BLOCK), 0, st, dpl, lmask, q.ulen.as<uint32_t>(), slot_ub,
+    hipLaunchKernelGGL(k_compact<0>, dim3(cgrid), dim3(CBLOCK), 0, st, dpl, lmask, q.ulen.as<uint32_t>(), slot_ub,
                        dctr, q.surv.as<uint32_t>(), q.survoff.as<unsigned long long>(), q.survlm.as<uint32_t>(),
                        (BlkTot *)nullptr, loc, dcand, q.survu.as<uint32_t>(), rcap, q.perm.as<uint32_t>());
   } else {
     // ordered: site clustering's replay walks the survivors in docid order
     BlkTot *blk = q.blk.as<BlkTot>();
-    hipLaunchKernelGGL(k_compact<1>, dim3(cgrid), dim3(BLOCK), 0, st, dpl, lmask, q.ulen.as<uint32_t>(), slot_ub,
+    hipLaunchKernelGGL(k_compact<1>, dim3(cgrid), dim3(CBLOCK), 0, st, dpl, lmask, q.ulen.as<uint32_t>(), slot_ub,
                        dctr, q.surv.as<uint32_t>(), q.survoff.as<unsigned long long>(), q.survlm.as<uint32_t>(), blk,
                        loc, dcand, q.survu.as<uint32_t>(), rcap, q.perm.as<uint32_t>());
     hipLaunchKernelGGL(k_compact_scan, dim3(1), dim3(1024), 0, st, cgrid, blk, dctr);
-    hipLaunchKernelGGL(k_compact<2>, dim3(cgrid), dim3(BLOCK), 0, st, dpl, lmask, q.ulen.as<uint32_t>(), slot_ub,
+    hipLaunchKernelGGL(k_compact<2>, dim3(cgrid), dim3(CBLOCK), 0, st, dpl, lmask, q.ulen.as<uint32_t>(), slot_ub,
                        dctr, q.surv.as<uint32_t>(), q.survoff.as<unsigned long long>(), q.survlm.as<uint32_t>(), blk,
                        loc, dcand, q.survu.as<uint32_t>(), rcap, q.perm.as<uint32_t>());
   }
@@ -4101,6 +4103,13 @@ int gbgpu_merge_timings(gbgpu_ctx *ctx, float *ms6, int64_t *nkeys, int64_t *nti
   if (!m) return GBGPU_EHIP;
   gbmerge::last_timings(m, ms6, nkeys, ntiles);
   return 0;
+}
+
+int gbgpu_merge_path(gbgpu_ctx *ctx) {
+  if (!ctx) return -EINVAL;
+  gbmerge::MergeState *m = merge_state(ctx);
+  if (!m) return -GBGPU_EHIP;
+  return gbmerge::last_path(m);
 }
 
 }  // extern "C"

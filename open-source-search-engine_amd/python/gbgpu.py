@@ -114,7 +114,7 @@ EXPORTS = [
     "gbgpu_query_slot_collect", "gbgpu_slot_stream", "gbgpu_slot_timings", "gbgpu_slot_stats",
     "gbgpu_bandwidth_ceiling", "gbgpu_comm_unique_id", "gbgpu_comm_init", "gbgpu_allgather_topk",
     "gbgpu_merge_replies_device",
-    "gbgpu_merge_posdb_device", "gbgpu_merge_timings", "gbgpu_merge_last_key", "gb_synth_merge_runs",
+    "gbgpu_merge_posdb_device", "gbgpu_merge_timings", "gbgpu_merge_path", "gbgpu_merge_last_key", "gb_synth_merge_runs",
     "gb_synth_lists", "gb_synth_free", "gb_synth_docid", "gb_posdb_compress", "gb_posdb_make_key",
 ]
 
@@ -159,6 +159,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.gbgpu_merge_posdb_device.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(i64), ctypes.c_int,
                                              ctypes.c_int, i64, vp, i64, ctypes.POINTER(i64)]
     lib.gbgpu_merge_last_key.argtypes = [vp, vp]
+    lib.gbgpu_merge_path.argtypes = [vp]
     lib.gbgpu_merge_timings.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(i64),
                                         ctypes.POINTER(i64)]
     lib.gb_synth_merge_runs.argtypes = [i64, ctypes.c_int, ctypes.c_uint64, ctypes.c_double, ctypes.c_double,
@@ -535,6 +536,10 @@ class Engine:
         nk, nt = ctypes.c_int64(), ctypes.c_int64()
         _check(self.lib.gbgpu_merge_timings(self.ctx, ms, ctypes.byref(nk), ctypes.byref(nt)))
         return list(ms), nk.value, nt.value
+
+    def merge_path(self):
+        """1: the last merge ran the tile path, 2: the legacy (decoded keys) path."""
+        return self.lib.gbgpu_merge_path(self.ctx)
 
     def last_topk_device(self):
         p = ctypes.c_void_p()

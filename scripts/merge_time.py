@@ -30,5 +30,5 @@ for rm in ((0, 1) if iters >= 3 else (0,)):
         el = time.perf_counter() - t
         ms, nk, nt = eng.merge_timings()
         print(f"rm={rm} out {n/1e9:.3f} GB wall {el*1e3:.1f} ms dev {[round(x,2) for x in ms]} keys {nk} tiles {nt} "
-              f"alg GB/s {(sum(sizes)+n)/ (ms[0]/1e3) / 1e9:.0f}", flush=True)
+              f"alg GB/s {(sum(sizes)+n)/ (ms[0]/1e3) / 1e9:.0f} path {eng.merge_path()}", flush=True)
 eng.close()

@@ -30,6 +30,14 @@ _ensure_built()
 @pytest.fixture(scope="session")
 def engine():
     import gbgpu
+    # torch (device tensors in some tests) brings its own HIP runtime, which
+    # must initialise before the library's on the GPU box
+    try:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.init()
+    except ImportError:
+        pass
     e = gbgpu.Engine(0)
     yield e
     e.close()

@@ -86,9 +86,13 @@ def test_config4_shards_and_merge(engine):
     assert np.array_equal(d, alld[order]) and np.array_equal(s, alls[order])
 
 
-def test_config5_fullsize_merge(engine):
-    # 400M keys in 8 tiered runs (1:2:..:128), ~4.4 GB: GPU bytes == oracle bytes
+@pytest.mark.parametrize("path", ["decoded", "tiles"])
+def test_config5_fullsize_merge(engine, path, monkeypatch):
+    # 400M keys in 8 tiered runs (1:2:..:128), ~4.4 GB: GPU bytes == oracle
+    # bytes, under both merge pipelines (GBGPU_MERGE_PATH)
     import torch
+    if path == "tiles":
+        monkeypatch.setenv("GBGPU_MERGE_PATH", "tiles")
     m = gbgpu.MergeRuns(400_000_000, nruns=8, seed=5, nterms=20000, nthreads=16)
     try:
         sizes = [len(a) for a in m.arrays]

@@ -104,7 +104,7 @@ def test_gpu_merge_vs_reference(engine, path):
 @pytest.mark.gpu
 @pytest.mark.parametrize("seed", [11, 12, 13])
 @pytest.mark.parametrize("rm", [0, 1])
-def test_gpu_merge_tiered_runs(engine, seed, rm):
+def test_gpu_merge_tiered_runs(engine, merge_path, seed, rm):
     runs = tiered_runs(20000, nruns=8, seed=seed, dup_frac=0.1, neg_frac=0.05, nterms=50)
     total = sum(map(len, runs))
     for mrs in (-1, 1, 6, 100, 4099, total // 3, total - 7, total + 100):
@@ -113,7 +113,7 @@ def test_gpu_merge_tiered_runs(engine, seed, rm):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("nruns", [1, 2, 3, 5, 20, 64])
-def test_gpu_merge_run_counts(engine, nruns):
+def test_gpu_merge_run_counts(engine, merge_path, nruns):
     runs = tiered_runs(6000, nruns=nruns, seed=20 + nruns, dup_frac=0.3, neg_frac=0.1, nterms=20)
     for rm in (0, 1):
         gpu_vs_oracle(engine, runs, rm, -1)
@@ -121,7 +121,7 @@ def test_gpu_merge_run_counts(engine, nruns):
 
 
 @pytest.mark.gpu
-def test_gpu_merge_heavy_duplicates(engine):
+def test_gpu_merge_heavy_duplicates(engine, merge_path):
     # half the keys repeated across runs: long tie chains, flipped delete bits
     runs = tiered_runs(30000, nruns=6, seed=3, dup_frac=0.5, neg_frac=0.2, nterms=5)
     for rm in (0, 1):
@@ -129,7 +129,7 @@ def test_gpu_merge_heavy_duplicates(engine):
 
 
 @pytest.mark.gpu
-def test_gpu_merge_generator_runs(engine):
+def test_gpu_merge_generator_runs(engine, merge_path):
     runs = gbgpu.synth_merge_runs(400000, nruns=8, seed=9, nterms=2000)
     for rm in (0, 1):
         gpu_vs_oracle(engine, runs, rm, -1)
@@ -137,7 +137,7 @@ def test_gpu_merge_generator_runs(engine):
 
 
 @pytest.mark.gpu
-def test_gpu_merge_edge_cases(engine):
+def test_gpu_merge_edge_cases(engine, merge_path):
     k1 = gbgpu.make_key(5, 1000, 10, 1, 15, 15, 3, 0, 1, 0, 0, 0, 0)
     k2 = gbgpu.make_key(5, 1000, 20, 1, 15, 15, 3, 0, 1, 0, 0, 0, 0)
     k3 = gbgpu.make_key(5, 2000, 30, 1, 15, 15, 3, 0, 1, 0, 0, 0, 0)
@@ -183,3 +183,57 @@ def test_gpu_merge_large_vs_oracle_and_properties(engine):
     assert engine.merge_posdb([got1], True, -1) == got1
     _, nk, nt = engine.merge_timings()
     assert nk > 0 and nt > 0
+
+
+@pytest.fixture(params=["decoded", "tiles"])
+def merge_path(request, monkeypatch):
+    """Run a test under both merge pipelines (GBGPU_MERGE_PATH)."""
+    if request.param == "tiles":
+        monkeypatch.setenv("GBGPU_MERGE_PATH", "tiles")
+    else:
+        monkeypatch.delenv("GBGPU_MERGE_PATH", raising=False)
+    return 1 if request.param == "tiles" else 2
+
+
+@pytest.mark.gpu
+def test_gpu_merge_paths_agree(engine, merge_path):
+    # the tile path (<= 28 runs) and the decoded-key path give the same
+    # bytes, both equal to the oracle's; more runs than the tile path takes
+    # fall back to the decoded-key path
+    runs = tiered_runs(30000, nruns=8, seed=31, dup_frac=0.2, neg_frac=0.05, nterms=30)
+    total = sum(map(len, runs))
+    for rm in (0, 1):
+        gpu_vs_oracle(engine, runs, rm, -1)
+        assert engine.merge_path() == merge_path
+    gpu_vs_oracle(engine, runs, 0, total // 3)
+    many = tiered_runs(8000, nruns=40, seed=32, dup_frac=0.2, neg_frac=0.05, nterms=30)
+    gpu_vs_oracle(engine, many, 0, -1)
+    assert engine.merge_path() == 2
+
+
+def _run(term, docid, wordpos):
+    from mergegen import pack_keys, to_bytes, _order
+    n = len(docid)
+    z = np.zeros(n, dtype=np.uint32)
+    n0, n1, n2 = pack_keys(np.full(n, term, dtype=np.uint64), np.asarray(docid, dtype=np.uint64),
+                           np.asarray(wordpos, dtype=np.uint32), z + 3, z + 15, z + 15, z + 2, z, z + 1, z, z + 1)
+    o = _order(n0, n1, n2)
+    return gbgpu.compress(to_bytes(n0[o], n1[o], n2[o]))
+
+
+@pytest.mark.gpu
+def test_gpu_merge_long_carries(engine, merge_path):
+    # one docid with 30000 positions: 6-byte keys whose lo and hi units lie
+    # hundreds of granules back (the tile path decodes a granule with the
+    # run's carries, not its own bytes); a newer run interleaves docids around
+    # it and repeats some of its keys
+    d = 1 << 30
+    a = _run(77, np.full(30000, d), np.arange(30000))
+    b = _run(77, np.concatenate([np.arange(d - 3000, d + 3000), np.full(500, d)]),
+             np.concatenate([np.full(6000, 7), np.arange(0, 30000, 60)]))
+    c = _run(78, np.arange(1, 4000), np.full(3999, 1))
+    for runs in ([a, b, c], [c, a, b], [a]):
+        for rm in (0, 1):
+            gpu_vs_oracle(engine, runs, rm, -1)
+            assert engine.merge_path() == merge_path
+        gpu_vs_oracle(engine, runs, 0, sum(map(len, runs)) // 2)
