@@ -1356,7 +1356,7 @@ __device__ __forceinline__ void score_survivor(const DevPlan *pl, const Counters
     // records written meanwhile stay below it when nrec + 2U <= cap, as each
     // record consumes at least one unit.  Otherwise the merge reads the
     // units from global memory one by one.
-    constexpr int SK = NS >= 16 ? 1 : 16 / NS;
+    constexpr int SK = NS >= 16 ? 1 : NS >= 4 ? 16 / NS : 4;
     if (stamp) {
       __asm__ volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       const uint64_t tb = __builtin_amdgcn_s_memtime();
@@ -2731,6 +2731,7 @@ struct gbgpu_ctx {
   int nslots = 0;
   bool profiling = false;
   int probe_mode = 0;  // diagnostic only (GBGPU_PROBE_MODE)
+  int probe_waves = 0;  // diagnostic: probe spans (GBGPU_PROBE_WAVES; 0 = PROBE_WAVES)
   int score_mode = 0;  // diagnostic only (GBGPU_SCORE_MODE): 1 mini-merge without scoring
   int debug_ext = 0;   // diagnostic only (GBGPU_DEBUG_EXT): print the re-shrink table per query
   uint64_t *d_sdbg = nullptr;  // GBGPU_SCORE_MODE=2: per-wave k_score timing (GBGPU_SCORE_DUMP file)
@@ -3059,7 +3060,8 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   // one wave per span of S chunks: about PROBE_WAVES spans over all probed
   // lists, so every CU holds ~24 waves and each amortises its initial
   // candidate search over several chunks
-  const uint32_t S = (uint32_t)std::max<uint64_t>(1, (probe_chunks + PROBE_WAVES - 1) / PROBE_WAVES);
+  const uint64_t pwaves = ctx->probe_waves ? (uint64_t)ctx->probe_waves : PROBE_WAVES;
+  const uint32_t S = (uint32_t)std::max<uint64_t>(1, (probe_chunks + pwaves - 1) / pwaves);
   for (int id = 0; id < P.nlists; id++) {
     if (!P.lists[id].probe) continue;
     const uint32_t units = P.lists[id].units;
@@ -3185,9 +3187,12 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   int maxsub = 0;
   for (int j = 0; j < hp.ngroups; j++)
     if (!(P.gflags0[j] & BF_NEGATIVE)) maxsub = std::max(maxsub, (int)P.gnsub[j]);
-  const int variant = (hp.ngroups <= 2 && maxsub <= 4) ? 0 : (hp.ngroups <= 4 && maxsub <= 4) ? 1
-                      : (hp.ngroups <= 8 && maxsub <= 4) ? 2 : 3;
-  static constexpr uint32_t kRC[4] = {24, 48, 64, 64};  // LDS records per lane
+  const int variant = (hp.ngroups <= 2 && maxsub <= 2)   ? 4
+                      : (hp.ngroups <= 2 && maxsub <= 4) ? 0
+                      : (hp.ngroups <= 4 && maxsub <= 4) ? 1
+                      : (hp.ngroups <= 8 && maxsub <= 4) ? 2
+                                                         : 3;
+  static constexpr uint32_t kRC[5] = {24, 48, 64, 64, 24};  // LDS records per lane
   const uint32_t rcap = kRC[variant] / 2;  // size buckets: a column holds 2x a bucket-3 survivor's units
   const uint32_t cgrid = std::max(1u, (uint32_t)((slot_ub + CTILE - 1) / CTILE));
   const uint64_t *dcand = q.cand.as<uint64_t>();
@@ -3223,7 +3228,8 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
                          q.skey.as<uint32_t>(), q.sdoc.as<uint64_t>(), q.sflag.as<uint8_t>(), ctx->score_mode,
                          ctx->d_sdbg);
     };
-    if (variant == 0) launch(k_score<2, 4, kRC[0]>);
+    if (variant == 4) launch(k_score<2, 2, kRC[4]>);  // two groups of <= 2 sublists (config 2)
+    else if (variant == 0) launch(k_score<2, 4, kRC[0]>);
     else if (variant == 1) launch(k_score<4, 4, kRC[1]>);
     else if (variant == 2) launch(k_score<8, 4, kRC[2]>);
     else launch(k_score<MAXG, MAXSUB, kRC[3]>);
@@ -3621,6 +3627,7 @@ int gbgpu_open(int device, gbgpu_ctx **out) {
     return GBGPU_EHIP;
   }
   if (const char *pm = std::getenv("GBGPU_PROBE_MODE")) ctx->probe_mode = std::atoi(pm);
+  if (const char *pw = std::getenv("GBGPU_PROBE_WAVES")) ctx->probe_waves = std::atoi(pw);
   if (const char *sm = std::getenv("GBGPU_SCORE_MODE")) ctx->score_mode = std::atoi(sm);
   if (ctx->score_mode == 2) HIPCHECK(hipMalloc(&ctx->d_sdbg, 8192 * 64));
   if (const char *de = std::getenv("GBGPU_DEBUG_EXT")) ctx->debug_ext = std::atoi(de);
