@@ -69,7 +69,7 @@ def _gbref_requests(terms, lists, params, reps):
     for l in lists:
         req.append(struct.pack("<q", len(l)))
         req.append(bytes(l))
-    req.append(struct.pack("<iii", 128, 0, reps))
+    req.append(struct.pack("<iiii", 128, 0, reps, 0))  # no whitelist lists
     return b"".join(req)
 
 

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define GBGPU_ABI_VERSION 4
+#define GBGPU_ABI_VERSION 5
 
 /* error codes beyond errno.h (Errno.h numbering is not reused) */
 #define GBGPU_ENODEVICE   1001 /* no HIP device / extension not usable        */
@@ -63,6 +63,13 @@ typedef struct gbgpu_qterm {
   int32_t quote_start;              /* m_qword->m_quoteStart, -1 if none             */
   float   tf_weight;                /* ptr_termFreqWeights[i]                        */
 } gbgpu_qterm;
+
+/* A posdb termlist exactly as Msg2::getList(i) holds it: first key 18 bytes,
+ * then 12/6-byte compressed keys (RdbList.cpp:282-327).  Host memory. */
+typedef struct gbgpu_list {
+  const uint8_t *bytes;
+  int64_t size;
+} gbgpu_list;
 
 /* Msg39Request scalars read by PosdbTable (Msg39.h:94-147).  Zero-filled
  * trailing fields reproduce a request without paging and without the max-score
@@ -93,14 +100,17 @@ typedef struct gbgpu_params {
   int64_t min_serp_docid;   /* m_minSerpDocId  } nonzero enables the filter of
                                Posdb.cpp:4379-4381, 7327-7347 (counted in
                                gbgpu_result::filtered)                           */
+  /* The "&sites=" whitelist: use_whitelist = (Msg39Request::size_whiteList > 1)
+   * (Posdb.cpp:800-801); white_lists = Msg2::m_whiteLists[0..m_w), host
+   * memory, not mutated.  A docid is voted only if the 5 bytes at rec+7 of its
+   * smallest-group key (docid and siteRank's top bit) are those of some record
+   * of a whitelist list (Posdb.cpp:5294, 5544-5572); with no records at all,
+   * nothing is.  Zero-filled: no whitelist. */
+  int32_t use_whitelist;
+  int32_t n_white_lists;
+  const struct gbgpu_list *white_lists;
 } gbgpu_params;
 
-/* A posdb termlist exactly as Msg2::getList(i) holds it: first key 18 bytes,
- * then 12/6-byte compressed keys (RdbList.cpp:282-327).  Host memory. */
-typedef struct gbgpu_list {
-  const uint8_t *bytes;
-  int64_t size;
-} gbgpu_list;
 
 /* The observable PosdbTable state Msg39 reads (Msg39.cpp:402-435, 1346-1420). */
 typedef struct gbgpu_result {

@@ -329,6 +329,20 @@ __global__ void __launch_bounds__(BLOCK) k_write_runs(const DevPlan *pl, const G
     // bucket straddling two chunks gets two writers; either names it)
     const uint64_t bkt = (d - dmin) >> sh;
     if (o2 == 0 || ((unit_docid(lds + rs_unit[o2 - 1] * 6) - dmin) >> sh) != bkt) dir_a[bkt] = tag | p2;
+    if (pl->use_white) {
+      // Posdb.cpp:5294: the 5 bytes at minRecPtr+7 (the run head's docid
+      // bytes, siteRank's top bit included) must be in the whitelist table
+      const uint8_t *k = lds + lu * 6;
+      uint64_t x = 0;
+      for (int b = 4; b >= 0; b--) x = (x << 8) | k[7 + b];
+      uint32_t lo = 0, hi = pl->nwhite;
+      while (lo < hi) {
+        const uint32_t m = (lo + hi) >> 1;
+        if (pl->white[m] < x) lo = m + 1;
+        else hi = m;
+      }
+      pl->wrej[slot] = !(lo < pl->nwhite && pl->white[lo] == x);
+    }
     lmask[slot] = own ? own_bit : 0u;
     uint32_t ul = 0;
     if (own) {
@@ -957,6 +971,7 @@ __global__ void __launch_bounds__(CBLOCK) k_compact(const DevPlan *pl, const uin
     int k = 0;
     while (k + 1 < g0n && s >= s_beg[k + 1]) k++;
     if (s >= s_end[k]) continue;
+    if (pl->use_white && pl->wrej[s]) continue;  // not voted (Posdb.cpp:5294)
     const uint32_t lm = lmv[q];
     uint32_t gm = 0;
     for (uint32_t x = lm; x; x &= x - 1) gm |= s_gbits[__ffs(x) - 1];
@@ -1079,6 +1094,7 @@ __global__ void __launch_bounds__(CBLOCK) k_compact(const DevPlan *pl, const uin
 // survivor would copy a misparsed run -- not emulated, flagged instead
 // (GBGPU_EUNSUPPORTED; about 2^-20 per query).  One wave per list.
 __device__ bool slot_is_survivor(const DevPlan *pl, const uint32_t *lmask, uint64_t s) {
+  if (pl->use_white && pl->wrej[s]) return false;
   uint32_t gm = 0;
   for (uint32_t x = lmask[s]; x; x &= x - 1) gm |= pl->lists[__ffs(x) - 1].group_bits;
   return ((gm & pl->pos_mask) == pl->pos_mask) && !(gm & NEG_BIT);
@@ -2667,6 +2683,8 @@ struct QuerySlot {
   DevBuf dir;           // candidate directories, epoch-tagged (never cleared per query)
   DevBuf split, swin;   // docid splits: one piece's list windows; window table
   DevBuf blk, sflag, sbound, order, tree;  // site clustering: ordered compaction, bounds, TopTree state
+  DevBuf white, wrej;                       // "&sites=" whitelist: sorted 5-byte values; rejected slots
+  std::vector<uint64_t> h_white;            // its host copy (the upload's source)
   uint32_t epoch = 0;
   uint8_t *h_stage = nullptr;  // pinned: query tables (host -> device, one copy)
   size_t stage_cap = 0;
@@ -2906,6 +2924,32 @@ static int enqueue_tree_emit(QuerySlot &q, int32_t dw) {
   return 0;
 }
 
+// The whitelist table of allocWhiteListTable / Posdb.cpp:5544-5572: the 5
+// bytes at rec+7 of every record of every whitelist list, records walked with
+// RdbList::skipCurrentRecord's posdb sizes (18 first, then 6 / 12 / 18 by the
+// compression bits) -- for a 6-byte record rec+7 lies in the next record, as
+// in the reference; past the list's end (the reference reads its allocation
+// slack, undefined) bytes read as 0.  Membership is exact (HashTableX
+// compares the 5 bytes), so a sorted unique array serves.
+static int white_set(const gbgpu_params *p, std::vector<uint64_t> &out) {
+  out.clear();
+  if (p->n_white_lists < 0 || (p->n_white_lists > 0 && !p->white_lists)) return EINVAL;
+  for (int i = 0; i < p->n_white_lists; i++) {
+    const gbgpu_list &l = p->white_lists[i];
+    if (l.size < 0 || (l.size > 0 && !l.bytes)) return EINVAL;
+    const uint8_t *b = l.bytes, *end = b + l.size;
+    for (const uint8_t *r = b; r < end;) {
+      uint64_t x = 0;
+      for (int k = 4; k >= 0; k--) x = (x << 8) | (r + 7 + k < end ? r[7 + k] : 0);
+      out.push_back(x);
+      r += r == b ? 18 : ((r[0] & 0x04) ? 6 : ((r[0] & 0x02) ? 12 : 18));
+    }
+  }
+  std::sort(out.begin(), out.end());
+  out.erase(std::unique(out.begin(), out.end()), out.end());
+  return 0;
+}
+
 static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *terms, int nterms,
                            const ListEntry *ents, const gbgpu_params *p, int32_t dw_override, int tree_phase) {
   std::vector<int64_t> sizes(nterms);
@@ -2941,6 +2985,12 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   P.max_serp_score = p->max_serp_score;
   P.min_serp_docid = p->min_serp_docid;
   P.clustering = clus;
+  P.use_white = p->use_whitelist != 0;
+  if (P.use_white) {
+    rc = white_set(p, q.h_white);
+    if (rc) return rc;
+    P.nwhite = (uint32_t)q.h_white.size();
+  }
   P.do_max_score = p->do_max_score_algo != 0;
   P.min_listi = hp.min_listi;
   P.all_same_wiki = 1;  // m_allInSameWikiPhrase, Posdb.cpp:5764-5778
@@ -3117,9 +3167,19 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
     if (P.g0n > 1) rc2 |= q.order.ensure(4 * slot_ub);
     if (!(tree_phase & TREE_FINAL)) rc2 |= q.tree.ensure(sizeof(TreeState));
   }
+  if (P.use_white) {
+    rc2 |= q.white.ensure(8 * std::max<size_t>(1, q.h_white.size()));
+    rc2 |= q.wrej.ensure(slot_ub);
+  }
   const void *dir_before = q.dir.p;
   rc2 |= q.dir.ensure(8 * std::max<uint64_t>(1, dir_entries));
   if (rc2) return ENOMEM;
+  if (P.use_white) {
+    P.white = q.white.as<uint64_t>();
+    P.wrej = q.wrej.as<uint8_t>();
+    if (!q.h_white.empty())
+      HIPCHECK(hipMemcpyAsync(q.white.p, q.h_white.data(), 8 * q.h_white.size(), hipMemcpyHostToDevice, q.stream));
+  }
   if (q.dir.p != dir_before || q.epoch == 0xffffffffu) {
     // fresh directory memory: no entry may carry a live epoch
     HIPCHECK(hipMemsetAsync(q.dir.p, 0, q.dir.cap, q.stream));

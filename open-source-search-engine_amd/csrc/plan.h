@@ -80,6 +80,14 @@ struct DevPlan {
   int has_serp;
   double max_serp_score;
   int64_t min_serp_docid;
+  // the "&sites=" whitelist (Posdb.cpp:793-835, 5294, 5544-5572): sorted
+  // 5-byte values (bytes 7..11 of a key: docid + siteRank's top bit); a
+  // group-0 candidate whose run head is not among them is rejected
+  // (k_write_runs writes wrej[slot], k_compact skips it)
+  int use_white;
+  uint32_t nwhite;
+  const uint64_t *white;
+  uint8_t *wrej;
   // site clustering: the pruning bounds (Posdb.cpp:6327-6504, 7811-7960)
   uint32_t reshare_mask;   // bit l: list l is shrunk more than once (uses >= 2)
   int clustering;

@@ -56,7 +56,25 @@ class Params(ctypes.Structure):
         ("get_docid_scoring_info", ctypes.c_int32),
         ("max_serp_score", ctypes.c_double),
         ("min_serp_docid", ctypes.c_int64),
+        ("use_whitelist", ctypes.c_int32),
+        ("n_white_lists", ctypes.c_int32),
+        ("white_lists", ctypes.c_void_p),
     ]
+
+    def with_whitelist(self, lists):
+        """A copy of these params carrying the "&sites=" whitelist lists
+        (Msg2::m_whiteLists; Posdb.cpp:793-835, 5294).  The copy keeps the
+        list buffers alive."""
+        q = Params.from_buffer_copy(self)
+        q._keep = [ctypes.create_string_buffer(bytes(l), max(1, len(l))) for l in lists]
+        arr = (ListRef * max(1, len(lists)))(*[ListRef(ctypes.cast(k, ctypes.c_void_p), len(l))
+                                               for k, l in zip(q._keep, lists)])
+        q._keep.append(arr)
+        q.use_whitelist = 1
+        q.n_white_lists = len(lists)
+        q.white_lists = ctypes.cast(arr, ctypes.c_void_p) if lists else None
+        q._white = [bytes(l) for l in lists]
+        return q
 
 
 class ListRef(ctypes.Structure):

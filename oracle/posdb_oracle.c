@@ -849,8 +849,60 @@ typedef struct {
   int64_t len;
 } VoteBuf;
 
-/* addDocIdVotes, Posdb.cpp:5043-5332 (no range terms / whitelist) */
-static void addDocIdVotes(QTI *qti, int listGroupNum, OList *lists, VoteBuf *vb) {
+/* The whitelist table (allocWhiteListTable + the fill of Posdb.cpp:5544-
+ * 5572): the 5 bytes at rec+7 of every record of every whitelist list,
+ * walked with RdbList::skipCurrentRecord's posdb record sizes (18 first, then
+ * 6 if byte0&0x04, 12 if byte0&0x02, else 18).  For a 6-byte record rec+7
+ * lies in the record after it, as in the reference; bytes past the list end
+ * (read from the reference's allocation slack: undefined) read as 0 here.
+ * Membership is exact (HashTableX compares the 5 key bytes), so a sorted
+ * array stands in for the hash table. */
+typedef struct {
+  uint64_t *v;
+  int64_t n;
+} WhiteSet;
+
+static uint64_t five_at(const uint8_t *p, const uint8_t *end) {
+  uint64_t x = 0;
+  for (int b = 4; b >= 0; b--) x = (x << 8) | (p + b < end ? p[b] : 0);
+  return x;
+}
+static int cmp_u64(const void *a, const void *b) {
+  const uint64_t x = *(const uint64_t *)a, y = *(const uint64_t *)b;
+  return x < y ? -1 : x > y;
+}
+static int white_build(const orc_params *prm, WhiteSet *ws) {
+  ws->v = NULL;
+  ws->n = 0;
+  int64_t cap = 0;
+  for (int i = 0; i < prm->n_white_lists; i++) cap += prm->white_lists[i].size / 6 + 1;
+  ws->v = (uint64_t *)malloc(8 * (size_t)(cap > 0 ? cap : 1));
+  if (!ws->v) return ENOMEM;
+  for (int i = 0; i < prm->n_white_lists; i++) {
+    const uint8_t *p = prm->white_lists[i].bytes, *end = p + prm->white_lists[i].size;
+    for (int first = 1; p < end; first = 0) {
+      ws->v[ws->n++] = five_at(p + 7, end);
+      p += first ? 18 : ((p[0] & 0x04) ? 6 : ((p[0] & 0x02) ? 12 : 18));
+    }
+  }
+  qsort(ws->v, (size_t)ws->n, 8, cmp_u64);
+  return 0;
+}
+static int white_has(const WhiteSet *ws, const uint8_t *p) {
+  uint64_t x = 0;
+  for (int b = 4; b >= 0; b--) x = (x << 8) | p[b];
+  int64_t lo = 0, hi = ws->n;
+  while (lo < hi) {
+    const int64_t m = (lo + hi) >> 1;
+    if (ws->v[m] < x) lo = m + 1;
+    else hi = m;
+  }
+  return lo < ws->n && ws->v[lo] == x;
+}
+
+/* addDocIdVotes, Posdb.cpp:5043-5332 (no range terms); ws: the whitelist
+ * table when the request has one (Posdb.cpp:5294), else NULL */
+static void addDocIdVotes(QTI *qti, int listGroupNum, OList *lists, VoteBuf *vb, const WhiteSet *ws) {
   uint8_t *dp, *dpEnd, *recPtr, *subListEnd;
   for (int i = 0; i < qti->numSubLists && listGroupNum > 0; i++) {
     recPtr = lists[qti->subList[i]].list;
@@ -915,6 +967,8 @@ static void addDocIdVotes(QTI *qti, int listGroupNum, OList *lists, VoteBuf *vb)
     if (lastMinRecPtr && U32(lastMinRecPtr + 8) == U32(minRecPtr + 8) &&
         (lastMinRecPtr[7] & 0xfc) == (minRecPtr[7] & 0xfc))
       continue;
+    /* not in the whitelist: not stored, lastMinRecPtr unchanged (5294) */
+    if (ws && !white_has(ws, minRecPtr + 7)) continue;
     lastMinRecPtr = minRecPtr;
     memcpy(dp + 1, minRecPtr + 8, 4);
     dp[0] = minRecPtr[7] & 0xfc;
@@ -1239,16 +1293,16 @@ static void unprepare(Prep *P, int nqt) {
 }
 
 /* phases 3-4 of intersectLists10_r, Posdb.cpp:5808-5860 */
-static void votes(Prep *P) {
+static void votes(Prep *P, const WhiteSet *ws) {
   QTI *qip = P->qip;
   int listGroupNum = 0;
-  addDocIdVotes(&qip[P->minListi], listGroupNum, P->lists, &P->vb);
+  addDocIdVotes(&qip[P->minListi], listGroupNum, P->lists, &P->vb, ws);
   for (int i = 0; i < P->nrg; i++) {
     if (i == P->minListi) continue;
     if (qip[i].bigramFlags[0] & BF_NEGATIVE) continue;
     listGroupNum++;
     if (listGroupNum >= 256) listGroupNum = 1;
-    addDocIdVotes(&qip[i], listGroupNum, P->lists, &P->vb);
+    addDocIdVotes(&qip[i], listGroupNum, P->lists, &P->vb, NULL);
   }
   for (int i = 0; i < P->nrg; i++) {
     if (i == P->minListi) continue;
@@ -1258,14 +1312,16 @@ static void votes(Prep *P) {
 }
 
 int64_t orc_intersect(const orc_qterm *qt, const uint8_t *const *lists, const int64_t *sizes,
-                      int nqt, int64_t *docids, int64_t cap) {
+                      int nqt, int64_t *docids, int64_t cap, const orc_params *prm) {
   initWeights();
+  WhiteSet ws = {NULL, 0};
+  if (prm && prm->use_whitelist && white_build(prm, &ws)) return -ENOMEM;
   Prep P;
   int rc = prepare(qt, lists, sizes, nqt, &P);
-  if (rc) { unprepare(&P, nqt); return -rc; }
+  if (rc) { unprepare(&P, nqt); free(ws.v); return -rc; }
   int64_t n = 0;
   if (P.nrg > 0 && P.minListSize != 0) {
-    votes(&P);
+    votes(&P, (prm && prm->use_whitelist) ? &ws : NULL);
     n = P.vb.len / 6;
     for (int64_t i = 0; i < n && i < cap; i++) {
       const uint8_t *d = P.vb.buf + 6 * i;
@@ -1276,6 +1332,7 @@ int64_t orc_intersect(const orc_qterm *qt, const uint8_t *const *lists, const in
     }
   }
   unprepare(&P, nqt);
+  free(ws.v);
   return n;
 }
 
@@ -1307,7 +1364,7 @@ static int64_t docs_wanted(const orc_params *p, const int64_t *sizes, int nqt) {
 /* One PosdbTable pass (init .. intersectLists10_r, Posdb.cpp:5437-7806) over
  * one docid range's lists, adding its winners to the caller's TopTree. */
 static int run_range(const orc_qterm *qt, const uint8_t *const *lists, const int64_t *sizes, int nqt,
-                     const orc_params *prm, TTree *tree, orc_result *out) {
+                     const orc_params *prm, const WhiteSet *ws, TTree *tree, orc_result *out) {
   Prep P;
   int rc = prepare(qt, lists, sizes, nqt, &P);
   if (rc) {
@@ -1318,7 +1375,7 @@ static int run_range(const orc_qterm *qt, const uint8_t *const *lists, const int
   int nqti = P.nrg;
   if (nqti == 0 || P.minListSize == 0) goto finish;
 
-  votes(&P);
+  votes(&P, ws);
   out->hits = P.vb.len / 6;
   for (int i = 0; i < nqti; i++) {
     if (qip[i].bigramFlags[0] & BF_NEGATIVE) continue;
@@ -1678,6 +1735,8 @@ int orc_query(const orc_qterm *qt, const uint8_t *const *lists, const int64_t *s
   initWeights();
 
   const int splits = prm->num_docid_splits;
+  WhiteSet ws = {NULL, 0};
+  if (prm->use_whitelist && white_build(prm, &ws)) return ENOMEM;
   TTree tk;
   memset(&tk, 0, sizeof tk);
   int alloced = 0, rc = 0;
@@ -1717,7 +1776,7 @@ int orc_query(const orc_qterm *qt, const uint8_t *const *lists, const int64_t *s
     }
     orc_result r;
     memset(&r, 0, sizeof r);
-    rc = run_range(qt, pl, ps, nqt, prm, &tk, &r);
+    rc = run_range(qt, pl, ps, nqt, prm, prm->use_whitelist ? &ws : NULL, &tk, &r);
     if (rc) break;
     out->hits += r.hits;
     out->filtered += r.filtered;
@@ -1725,6 +1784,7 @@ int orc_query(const orc_qterm *qt, const uint8_t *const *lists, const int64_t *s
   } while (ddd < ORC_MAX_DOCID);
   for (int i = 0; i < nqt; i++) free(own[i]);
   free(own); free(pl); free(ps);
+  free(ws.v);
   out->n = tk.n < cap ? (int32_t)tk.n : cap;
   for (int i = 0; i < out->n; i++) {
     docids[i] = tk.docid[i];

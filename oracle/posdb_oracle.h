@@ -48,7 +48,17 @@ typedef struct orc_params {
   int32_t reserved0;
   double  max_serp_score;   /* m_maxSerpScore                          */
   int64_t min_serp_docid;   /* m_minSerpDocId (nonzero: paging filter) */
+  /* the "&sites=" whitelist (Msg39Request::size_whiteList > 1 and
+   * Msg2::m_whiteLists[0..m_w), Posdb.cpp:793-835, 5294, 5544-5572) */
+  int32_t use_whitelist;
+  int32_t n_white_lists;
+  const struct orc_list *white_lists;
 } orc_params;
+
+typedef struct orc_list {
+  const uint8_t *bytes;
+  int64_t size;
+} orc_list;
 
 typedef struct orc_result {
   int64_t hits;        /* m_docIdVoteBuf.length()/6                          */
@@ -69,7 +79,7 @@ int orc_query(const orc_qterm *terms, const uint8_t *const *lists, const int64_t
 /* Bare intersection: the docids surviving addDocIdVotes/rmDocIdVotes, in
  * vote-buffer order.  Returns count (or -errno); writes up to cap docids. */
 int64_t orc_intersect(const orc_qterm *terms, const uint8_t *const *lists, const int64_t *sizes,
-                      int nterms, int64_t *docids, int64_t cap);
+                      int nterms, int64_t *docids, int64_t cap, const orc_params *prm);
 
 /* RdbList::merge_r -> posdbMerge_r (RdbList.cpp:1658-1756, 3065-3568) into an
  * empty list, with prepareForMerge's bound (RdbList.cpp:410-491): min_rec_sizes

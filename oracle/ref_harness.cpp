@@ -153,6 +153,13 @@ static int ref_query(const orc_qterm *terms, const uint8_t *const *lists, const 
   req.m_collnum = 0;
   req.ptr_termFreqWeights = (char *)tfw;
   req.size_termFreqWeights = 4 * nterms;
+  // the "&sites=" whitelist: allocWhiteListTable only tests size_whiteList > 1
+  // (Posdb.cpp:800-801); the lists are Msg2::m_whiteLists[0..m_w)
+  static char s_sites[] = "x";
+  req.ptr_whiteList = p->use_whitelist ? s_sites : NULL;
+  req.size_whiteList = p->use_whitelist ? 2 : 0;
+  const int nw = p->use_whitelist ? p->n_white_lists : 0;
+  if (nw < 0 || nw > MAX_WHITELISTS) return EINVAL;
 
   tree.~TopTree();
   memset((void *)&tree, 0, sizeof tree);  // m_docsWanted is only set by setNumNodes
@@ -201,6 +208,20 @@ static int ref_query(const orc_qterm *terms, const uint8_t *const *lists, const 
         if (!rl[i].constrain(sk, ek, -1, 0, first, (char *)"refharness", 0)) return EIO;
       }
     }
+    // whitelist lists as Msg2 reads them for each piece: fresh (their cursor
+    // is walked by the table fill, Posdb.cpp:5550-5571)
+    for (int i = 0; i < MAX_WHITELISTS && i < (nw > msg2.m_w ? nw : msg2.m_w); i++) msg2.m_whiteLists[i].freeList();
+    for (int i = 0; i < nw; i++) {
+      char *buf = NULL;
+      const int32_t sz = (int32_t)p->white_lists[i].size;
+      if (sz > 0) {
+        buf = (char *)mmalloc(sz + 64, "refharness");
+        memcpy(buf, p->white_lists[i].bytes, sz);
+        memset(buf + sz, 0, 64);
+      }
+      msg2.m_whiteLists[i].set(buf, sz, buf, sz ? sz + 64 : 0, 0, true, true, 18);
+    }
+    msg2.m_w = nw;
     // one PosdbTable over all pieces: reset per piece (Msg39::reset2,
     // Msg39.cpp:51-69), its allocTopTree buffers (m_stackBuf) kept
     if (d0 == 0) {
@@ -292,7 +313,7 @@ static int64_t ref_posdb_merge(const uint8_t *const *lists, const int64_t *sizes
 
 // ------------------------------------------------------------------ driver
 // Binary request on stdin, response on stdout (little-endian, host layout):
-//   op=1 query: i32 nterms, orc_params, nterms x orc_qterm,
+//   op=1 query: i32 nterms, orc_params (its white_lists pointer ignored), nterms x orc_qterm,
 //               nterms x (i64 size, bytes), i32 cap, i32 want_votes, i32 reps
 //        ->     orc_result, n x i64 docid, n x f32 score,
 //               i64 nvotes, nvotes x i64 docid, f64 seconds per run (median of
@@ -343,10 +364,24 @@ int main(int argc, char **argv) {
         rd(bufs[i].data(), sizes[i]);
         ptrs[i] = bufs[i].data();
       }
-      int32_t cap, want_votes, reps;
+      int32_t cap, want_votes, reps, nw;
       rd(&cap, 4);
       rd(&want_votes, 4);
       rd(&reps, 4);
+      rd(&nw, 4);  // whitelist lists follow
+      if (nw < 0 || nw > MAX_WHITELISTS) return 4;
+      std::vector<std::vector<uint8_t> > wbufs(nw);
+      std::vector<orc_list> wl(nw);
+      for (int i = 0; i < nw; i++) {
+        int64_t sz;
+        rd(&sz, 8);
+        wbufs[i].resize(sz + 1);
+        rd(wbufs[i].data(), sz);
+        wl[i].bytes = wbufs[i].data();
+        wl[i].size = sz;
+      }
+      p.n_white_lists = nw;
+      p.white_lists = nw ? wl.data() : NULL;
       std::vector<int64_t> d(cap > 0 ? cap : 1);
       std::vector<float> s(cap > 0 ? cap : 1);
       int64_t vcap = 0;

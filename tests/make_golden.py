@@ -18,6 +18,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(os.path.dirname(HERE), "open-source-search-engine_amd", "python"))
 sys.path.insert(0, HERE)
 
+import gbgpu  # noqa: E402
 import qkinds  # noqa: E402
 import ref_binding as ref  # noqa: E402
 from mergegen import tiered_runs  # noqa: E402
@@ -35,13 +36,13 @@ def pack_lists(lists):
 
 
 def save_query(name, terms, lists, params):
-    r = ref.query(terms, lists, params, votes=True, cap=1 << 16)
+    white = getattr(params, "_white", None) if params.use_whitelist else None
+    r = ref.query(terms, lists, params, votes=True, cap=1 << 16, white=white)
     if params.num_docid_splits > 1:
         # the vote buffer of one whole-range pass: the exact intersection
-        import copy
-        p1 = copy.copy(params)
+        p1 = gbgpu.Params.from_buffer_copy(params)  # (keeps white_lists' pointer; its buffers live in params)
         p1.num_docid_splits = 1
-        r["votes"] = ref.query(terms, lists, p1, votes=True)["votes"]
+        r["votes"] = ref.query(terms, lists, p1, votes=True, white=white)["votes"]
     sizes, blob = pack_lists(lists)
     qt = np.array([[getattr(t, f) for f in QFIELDS] for t in terms], np.int32).reshape(len(terms), len(QFIELDS))
     tfw = np.array([t.tf_weight for t in terms], np.float32)
@@ -52,8 +53,39 @@ def save_query(name, terms, lists, params):
                         max_serp_score=np.float64(params.max_serp_score),
                         min_serp_docid=np.int64(params.min_serp_docid), list_sizes=sizes, list_blob=blob,
                         docids=r["docids"], score_bits=r["scores"].view(np.uint32), hits=np.int64(r["hits"]),
-                        filtered=np.int32(r["filtered"]), docs_wanted=np.int32(r["docs_wanted"]), votes=r["votes"])
+                        filtered=np.int32(r["filtered"]), docs_wanted=np.int32(r["docs_wanted"]), votes=r["votes"],
+                        **white_arrays(params))
     return r
+
+
+def white_arrays(params):
+    if not params.use_whitelist:
+        return {}
+    sizes, blob = pack_lists(params._white)
+    return dict(use_whitelist=np.int32(1), white_sizes=sizes, white_blob=blob)
+
+
+def save_whitelist():
+    """The "&sites=" whitelist (Posdb.cpp:793-835, 5294, 5544-5572): site
+    lists over part of the query's docids, some with siteRank's top bit
+    flipped (rejected by the 5-byte compare), 6-byte keys inside a site list
+    (rec+7 then reads the next record), an empty whitelist (nothing voted),
+    and with docid splits and site clustering."""
+    from posdb_py import site_lists
+    N = 20000
+    ks = qkinds.kinds(N, seed=9)
+    cases = [(0, 2, 0.3, 0.05, 0.0, {}), (1, 1, 0.5, 0.1, 0.3, {}), (2, 3, 0.2, 0.0, 0.2, {}),
+             (0, 0, 0.0, 0.0, 0.0, {}), (0, 2, 0.4, 0.05, 0.0, dict(num_docid_splits=3)),
+             (0, 2, 0.4, 0.05, 0.0, dict(site_clustering=1)), (4, 2, 0.5, 0.05, 0.1, {})]
+    for j, (kind, ns, fr, ff, mf, kw) in enumerate(cases):
+        q = ks[kind]
+        lists = generate(q, N, seed=5100 + j)
+        wl = site_lists(lists, ns, fr, seed=31 + j, flip_frac=ff, multi_frac=mf)
+        if j == 2:
+            wl = wl[:1] + [b""] + wl[1:]  # an empty whitelist list among them
+        p = q.params(**kw).with_whitelist(wl)
+        r = save_query(f"white{j}_{q.name}", q.terms, lists, p)
+        print(f"  white{j} {q.name}: sites={ns} hits={r['hits']} n={len(r['docids'])}")
 
 
 def split_boundary_docids(n, seed, splits=(2, 5)):
@@ -224,6 +256,7 @@ def main():
     save_splits()
     save_clustering()
     save_paging()
+    save_whitelist()
     cases = [(0, -1), (1, -1), (0, 5000), (1, 5000), (0, 1)]
     for seed, (keys, nterms) in enumerate([(4000, 50), (12000, 3), (8000, 1)]):
         save_merge(f"tiered_s{seed}", tiered_runs(keys, seed=seed, nterms=nterms), cases)
@@ -238,5 +271,7 @@ if __name__ == "__main__":
     elif sys.argv[1:] == ["clustering"]:
         save_clustering()
         save_paging()
+    elif sys.argv[1:] == ["whitelist"]:
+        save_whitelist()
     else:
         main()

@@ -27,7 +27,8 @@ def lib():
                                    ctypes.POINTER(OrcResult)]
         _lib.orc_intersect.argtypes = [ctypes.POINTER(gbgpu.QTerm), ctypes.POINTER(ctypes.c_void_p),
                                        ctypes.POINTER(ctypes.c_int64), ctypes.c_int,
-                                       ctypes.POINTER(ctypes.c_int64), ctypes.c_int64]
+                                       ctypes.POINTER(ctypes.c_int64), ctypes.c_int64,
+                                       ctypes.POINTER(gbgpu.Params)]
         _lib.orc_intersect.restype = ctypes.c_int64
         _lib.orc_weights.argtypes = [ctypes.POINTER(ctypes.c_float)] * 5
         _lib.orc_posdb_merge.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_int64),
@@ -60,12 +61,13 @@ def query(terms, lists, params, cap=4096):
                 docs_wanted=r.docs_wanted, corrupt=r.corrupt)
 
 
-def intersect(terms, lists, cap=1 << 24):
+def intersect(terms, lists, cap=1 << 24, params=None):
     L = lib()
     keep, ptrs, sizes = _lists(lists)
     qt = (gbgpu.QTerm * max(1, len(terms)))(*terms)
     d = np.zeros(cap, np.int64)
-    n = L.orc_intersect(qt, ptrs, sizes, len(terms), d.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), cap)
+    n = L.orc_intersect(qt, ptrs, sizes, len(terms), d.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), cap,
+                        ctypes.byref(params) if params is not None else None)
     if n < 0:
         raise RuntimeError(f"orc_intersect rc={n}")
     return d[:n].copy()

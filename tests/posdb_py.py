@@ -114,3 +114,34 @@ def remap_docids(lists, new_docids):
     assert len(new) == len(old)
     m = dict(zip(old, new))
     return [encode_keys([with_docid(k, m[int.from_bytes(k[7:12], "little") >> 2]) for k in kl]) for kl in ks]
+
+
+def site_lists(lists, nsites=2, frac=0.3, seed=5, flip_frac=0.05, multi_frac=0.0):
+    """Whitelist ("&sites=") termlists for a query's lists: each of nsites
+    site terms holds a random fraction of the query's docids, one key per doc
+    (18 then 12 bytes) carrying the doc's own siteRank, so byte 7 (docid low
+    bits + siteRank's top bit) matches the query keys -- except a flip_frac
+    share whose siteRank top bit is flipped, which the reference's 5-byte
+    table compare rejects.  multi_frac docs get 2-3 keys (6-byte keys inside
+    a list; never the last key)."""
+    import gbgpu
+    rng = np.random.default_rng(seed)
+    docs = {}
+    for l in lists:
+        for k in decode_keys(l):
+            docs.setdefault(k["docid"], (k["siterank"], k["langid"]))
+    ids = np.array(sorted(docs), dtype=np.int64)
+    out = []
+    for s in range(nsites):
+        tid = (0x5173 + 977 * s + (seed << 20)) & ((1 << 48) - 1)
+        pick = ids[rng.random(len(ids)) < frac]
+        keys = []
+        for j, d in enumerate(pick):
+            sr, lang = docs[int(d)]
+            if rng.random() < flip_frac:
+                sr ^= 0x8
+            npos = 1 if (j == len(pick) - 1 or rng.random() >= multi_frac) else int(rng.integers(2, 4))
+            for w in range(npos):
+                keys.append(gbgpu.make_key(tid, int(d), 5 + 7 * w, 20, 15, 15, sr, 7, lang & 0x3f))
+        out.append(gbgpu.compress(b"".join(keys)))
+    return out

@@ -57,8 +57,9 @@ def _read(n):
     return b
 
 
-def query(terms, lists, params, cap=4096, votes=False, reps=1):
-    """Same result dict as oracle_binding.query (+ 'votes', 'seconds')."""
+def query(terms, lists, params, cap=4096, votes=False, reps=1, white=None):
+    """Same result dict as oracle_binding.query (+ 'votes', 'seconds').
+    white: the whitelist lists (Msg2::m_whiteLists) when params.use_whitelist."""
     p = _p()
     qt = (gbgpu.QTerm * max(1, len(terms)))(*terms)
     req = [struct.pack("<ii", 1, len(terms)), bytes(params), bytes(qt)[:ctypes.sizeof(gbgpu.QTerm) * len(terms)]]
@@ -66,6 +67,11 @@ def query(terms, lists, params, cap=4096, votes=False, reps=1):
         req.append(struct.pack("<q", len(l)))
         req.append(bytes(l))
     req.append(struct.pack("<iii", cap, 1 if votes else 0, reps))
+    white = list(white or [])
+    req.append(struct.pack("<i", len(white)))
+    for l in white:
+        req.append(struct.pack("<q", len(l)))
+        req.append(bytes(l))
     p.stdin.write(b"".join(req))
     p.stdin.flush()
     r = OrcResult.from_buffer_copy(_read(ctypes.sizeof(OrcResult)))

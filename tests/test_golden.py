@@ -39,6 +39,8 @@ def load_query(path):
     params = gbgpu.Params(int(pr[0]), int(pr[1]), int(pr[2]), int(pr[3]), int(pr[4]), float(z["same_lang_weight"]),
                           do_max, 0, float(z["max_serp_score"]) if "max_serp_score" in z else 0.0,
                           int(z["min_serp_docid"]) if "min_serp_docid" in z else 0)
+    if "use_whitelist" in z and int(z["use_whitelist"]):
+        params = params.with_whitelist(split_blob(z["white_sizes"], z["white_blob"]))
     lists = split_blob(z["list_sizes"], z["list_blob"])
     exp = dict(docids=z["docids"], scores=z["score_bits"].view(np.float32), hits=int(z["hits"]),
                docs_wanted=int(z["docs_wanted"]), votes=z["votes"],
@@ -85,7 +87,7 @@ def test_oracle_query_vs_reference(path):
 def test_oracle_intersection_vs_reference(path):
     terms, lists, params, exp = load_query(path)
     # m_docIdVoteBuf after intersectLists10_r: the exact intersected docid set
-    assert np.array_equal(orc.intersect(terms, lists), exp["votes"])
+    assert np.array_equal(orc.intersect(terms, lists, params=params), exp["votes"])
 
 
 @pytest.mark.parametrize("path", MCASES, ids=[os.path.basename(p)[2:-4] for p in MCASES])

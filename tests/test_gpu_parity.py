@@ -33,7 +33,7 @@ def check(res, exp, label=""):
 
 def oracle(terms, lists, p, cap=1 << 16):
     exp = orc.query(terms, lists, p, cap=cap)
-    exp["votes"] = orc.intersect(terms, lists)
+    exp["votes"] = orc.intersect(terms, lists, params=p)
     return exp
 
 
@@ -319,3 +319,28 @@ def test_parity_every_survivor(engine, kind):
     if exp["hits"] > 1500:
         pytest.skip("more survivors than one TopTree can hold here")
     check(gpu(engine, q.terms, lists, p), exp, q.name)
+
+
+@pytest.mark.parametrize("kind", [0, 1, 2, 4, 6])
+@pytest.mark.parametrize("clus,splits", [(0, 1), (1, 1), (0, 4)])
+def test_parity_whitelist(engine, kind, clus, splits):
+    # the "&sites=" whitelist (Posdb.cpp:793-835, 5294, 5544-5572): site lists
+    # over part of the docids, some with siteRank's top bit flipped, 6-byte
+    # keys inside; through gbgpu_query and the resident path
+    from posdb_py import site_lists
+    q = qkinds.kinds(30000, seed=4)[kind]
+    lists = generate(q, 30000, seed=6100 + kind)
+    wl = site_lists(lists, 2 + kind % 2, 0.35, seed=kind, flip_frac=0.05, multi_frac=0.2)
+    p = q.params(site_clustering=clus, num_docid_splits=splits).with_whitelist(wl)
+    exp = oracle(q.terms, lists, p)
+    check(gpu(engine, q.terms, lists, p), exp, f"{q.name} white")
+    hs = [engine.upload(l) for l in lists]
+    try:
+        check(engine.query_resident(q.terms, hs, p, cap=1 << 16), exp, f"{q.name} white resident")
+    finally:
+        for h in hs:
+            engine.free(h)
+    # an empty whitelist votes nothing
+    p0 = q.params(site_clustering=clus, num_docid_splits=splits).with_whitelist([])
+    r0 = gpu(engine, q.terms, lists, p0)
+    assert r0.hits == 0 and len(r0.docids) == 0
