@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define GBGPU_ABI_VERSION 5
+#define GBGPU_ABI_VERSION 6
 
 /* error codes beyond errno.h (Errno.h numbering is not reused) */
 #define GBGPU_ENODEVICE   1001 /* no HIP device / extension not usable        */
@@ -93,8 +93,10 @@ typedef struct gbgpu_params {
   int32_t do_max_score_algo;/* m_doMaxScoreAlgo: per-term getMaxPossibleScore
                                prefilter (Posdb.cpp:6046-6047, 6327-6346)         */
   int32_t get_docid_scoring_info; /* m_getDocIdScoringInfo: the per-docid score
-                               breakdown second pass (Posdb.cpp:942-948, 3058,
-                               7752-7806) is not on the GPU path: nonzero returns
+                               breakdown second pass (Posdb.cpp:6116-6244,
+                               7554-7665, 7752-7775) into gbgpu_result's
+                               docid/pair/single score arrays.  With site
+                               clustering, docid splits or paging it returns
                                GBGPU_EUNSUPPORTED (the adapter runs the CPU body) */
   double  max_serp_score;   /* m_maxSerpScore  } paging of a widget's next page:   */
   int64_t min_serp_docid;   /* m_minSerpDocId  } nonzero enables the filter of
@@ -111,6 +113,45 @@ typedef struct gbgpu_params {
   const struct gbgpu_list *white_lists;
 } gbgpu_params;
 
+
+/* The second pass's score info (m_getDocIdScoringInfo, Posdb.cpp:6116-6244,
+ * 7554-7665): byte-for-byte the layout of the reference's DocIdScore /
+ * PairScore / SingleScore (Posdb.h:767-866) on x86-64, so the adapter copies
+ * the three arrays into m_scoreInfoBuf / m_pairScoreBuf / m_singleScoreBuf.
+ * Fields the reference leaves unset (m_termFreq*, the two pointers, padding)
+ * are zero here. */
+typedef struct gbgpu_pair_score {
+  float   final_score;
+  int8_t  is_synonym1, is_synonym2, is_half_stop_wiki_bigram1, is_half_stop_wiki_bigram2;
+  int8_t  diversity_rank1, diversity_rank2, density_rank1, density_rank2;
+  int8_t  word_spam_rank1, word_spam_rank2, hash_group1, hash_group2;
+  int8_t  in_same_wiki_phrase, fixed_distance;
+  int32_t word_pos1, word_pos2;
+  int64_t term_freq1, term_freq2;
+  float   tf_weight1, tf_weight2;
+  int32_t qterm_num1, qterm_num2;
+  int8_t  bflags1, bflags2;
+  int32_t qdist;
+} gbgpu_pair_score;
+typedef struct gbgpu_single_score {
+  float   final_score;
+  int8_t  is_synonym, is_half_stop_wiki_bigram, diversity_rank, density_rank, word_spam_rank, hash_group;
+  int32_t word_pos;
+  int64_t term_freq;
+  float   tf_weight;
+  int32_t qterm_num;
+  int8_t  bflags;
+} gbgpu_single_score;
+typedef struct gbgpu_docid_score {
+  int64_t docid;
+  double  final_score;
+  int8_t  site_rank;
+  int32_t doc_lang;
+  int32_t num_required_terms;
+  int32_t num_pairs, num_singles;
+  int32_t pairs_offset, singles_offset;  /* byte offsets into the pair / single arrays, -1 if none */
+  void   *pair_scores, *single_scores;   /* NULL */
+} gbgpu_docid_score;
 
 /* The observable PosdbTable state Msg39 reads (Msg39.cpp:402-435, 1346-1420). */
 typedef struct gbgpu_result {
@@ -129,6 +170,14 @@ typedef struct gbgpu_result {
   int64_t *hit_docids;   /* caller-owned, hit_capacity entries                     */
   int64_t  hit_capacity;
   int64_t  n_hit_docids; /* entries written (min(set size, hit_capacity))          */
+  /* with gbgpu_params::get_docid_scoring_info: the second pass's records for
+   * the first min(n, docs_to_get) docids of the tree, high -> low, one
+   * DocIdScore each, their PairScores / SingleScores in the reference's append
+   * order.  Caller-owned arrays of *_cap entries; *_n = entries written
+   * (ENOSPC if an array is too small). */
+  gbgpu_docid_score  *docid_scores;  int32_t docid_scores_cap;  int32_t n_docid_scores;
+  gbgpu_pair_score   *pair_scores;   int32_t pair_scores_cap;   int32_t n_pair_scores;
+  gbgpu_single_score *single_scores; int32_t single_scores_cap; int32_t n_single_scores;
 } gbgpu_result;
 
 int         gbgpu_open(int device, gbgpu_ctx **out);

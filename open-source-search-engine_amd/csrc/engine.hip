@@ -57,6 +57,7 @@
 #include "plan.h"
 #include "posdb_key.h"
 #include "scoring.h"
+#include "sisort.h"
 
 namespace gbgpu {
 
@@ -1315,11 +1316,19 @@ __device__ __forceinline__ uint64_t load6(gu8 *k) {
   return odd ? (hv | (wv << 16)) : (wv | (hv << 32));
 }
 
-template <int NQ, int NS, class RP>
+// what the second pass's DocIdScore takes from a scored docid (Posdb.cpp:7555-7563)
+struct SurvOut {
+  float score;
+  int32_t site_rank, doc_lang, ok;
+};
+
+template <int NQ, int NS, class RP, class REC = NoRec>
 __device__ __forceinline__ void score_survivor(const DevPlan *pl, const Counters *ctr, uint32_t s, uint32_t lm,
                                                uint32_t anys, const Loc *loc, uint64_t slot_ub, RP rec, float *smcol,
                                                uint32_t *key_out, int diag, uint32_t *nrec_out,
-                                               bool stamp, uint64_t &tmerge, uint64_t (&tm)[3]) {
+                                               bool stamp, uint64_t &tmerge, uint64_t (&tm)[3],
+                                               REC *srec = nullptr, SurvOut *so = nullptr,
+                                               const uint16_t *kill = nullptr) {
   const int ng = pl->ngroups;
   DocView<NQ, RP> dv;
   dv.rec = rec;
@@ -1355,7 +1364,8 @@ __device__ __forceinline__ void score_survivor(const DevPlan *pl, const Counters
         if (anys >> lid & 1) {
           cfl[x] = pl->gsubflags[j][newIdx];
           newIdx++;
-          if (lm >> lid & 1) {
+          // kill: sublists the second pass's lookup misses (k_scoreinfo)
+          if ((lm >> lid & 1) && !(kill && (kill[j] >> x & 1))) {
             const SubRun sr = sub_run(pl, ctr, loc, slot_ub, lid, j, x, s);
             src[x] = sr.own;
             xsrc[x] = sr.ext;
@@ -1524,7 +1534,12 @@ __device__ __forceinline__ void score_survivor(const DevPlan *pl, const Counters
     dv.beg[j] = (int)start;
     dv.end[j] = (int)nrec;
     dv.present |= 1u << j;
-    if (nrec == start) empty_pos = true;  // reference reads stale mbuf here (UB)
+    // An empty mini-merged list still has one key read by every scorer
+    // (do-while loops): what mbuf holds there.  When a later group writes
+    // records, that is its first key (groups are merged back to back from
+    // the same place), which rec[start] is here too; when none does, it is
+    // stale bytes of an earlier docid (not replayed: the docid is dropped)
+    empty_pos = nrec == start;
   }
   float score = 0.0f;
   *nrec_out = nrec;
@@ -1536,8 +1551,14 @@ __device__ __forceinline__ void score_survivor(const DevPlan *pl, const Counters
     *key_out = nrec + 1;
     return;
   }
-  const bool ok = !empty_pos && score_doc<NQ>(&c_weights, pl, dv, siteRank < 0 ? 0 : siteRank, docLang, smcol,
-                                              SCORE_TPB, &score, diag & 0xff);
+  const bool ok = !empty_pos && score_doc<NQ, RP, REC>(&c_weights, pl, dv, siteRank < 0 ? 0 : siteRank, docLang,
+                                                       smcol, SCORE_TPB, &score, diag & 0xff, srec);
+  if (so) {
+    so->score = score;
+    so->site_rank = siteRank < 0 ? 0 : siteRank;
+    so->doc_lang = docLang;
+    so->ok = empty_pos ? -2 : ok;
+  }
   uint32_t key = 0;
   if (ok) {
     const uint32_t b = __float_as_uint(score);
@@ -1698,6 +1719,281 @@ __global__ void __launch_bounds__(SCORE_TPB) k_score(const DevPlan *pl, const ui
       dbg[blockIdx.x * 8 + 7] = (tmm[0] & 0xfffff) | ((tmm[1] & 0xfffff) << 20) | ((tmm[2] & 0xfffff) << 40);
     }
   }
+}
+
+// ------------------------------------------- the second pass's score info
+// m_getDocIdScoringInfo (Posdb.cpp:6116-6244, 7554-7665, 7752-7770): after
+// the first pass, the top min(m_numUsedNodes, m_docsToGet) docids of the tree
+// are scored again, high -> low, with the scorers recording their top lists.
+// Here the tree's docids find their survivor entry (k_si_find), and
+// k_scoreinfo re-runs score_survivor for them -- one lane per docid, the
+// records in the survivor's own range of the global arena -- with ScoreRec
+// attached; the host lays out DocIdScore and the offsets.
+
+// getSingleTermScore's / getTermPairScoreForAny's recording (Posdb.cpp:
+// 3247-3298, 4195-4280) into one docid's slices of the output arrays, in the
+// reference's append order.  The host sizes the slices for the worst case.
+struct ScoreRec {
+  static constexpr bool on = true;
+  gbgpu_single_score *ss;
+  gbgpu_pair_score *ps;
+  int ns, np, scap, pcap;
+  __device__ void single(const DevPlan *pl, int i, float best, uint64_t r) {
+    if (ns < scap) {
+      gbgpu_single_score x;
+      __builtin_memset(&x, 0, sizeof x);
+      x.is_synonym = (int8_t)r_syn(r);
+      x.is_half_stop_wiki_bigram = (int8_t)r_hswb(r);
+      x.diversity_rank = (int8_t)r_div(r);
+      x.word_spam_rank = (int8_t)r_wsr(r);
+      x.hash_group = (int8_t)r_hg(r);
+      x.word_pos = (int32_t)r_wordpos(r);
+      x.density_rank = (int8_t)r_dens(r);
+      float score = best;
+      score *= pl->tfw[i];
+      score *= pl->tfw[i];
+      if (x.is_half_stop_wiki_bigram) {
+        score *= GB_WIKI_BIGRAM_WEIGHT;
+        score *= GB_WIKI_BIGRAM_WEIGHT;
+      }
+      x.final_score = score;
+      x.tf_weight = pl->tfw[i];
+      x.qterm_num = pl->qterm[i];
+      x.bflags = (int8_t)pl->gflags0[i];
+      __builtin_memcpy(ss + ns, &x, sizeof x);
+    }
+    ns++;
+  }
+  __device__ void pair(const DevPlan *pl, int i, int j, float best, float wts, int32_t qdist, uint64_t r1,
+                       uint64_t r2, bool fixed) {
+    if (np < pcap) {
+      gbgpu_pair_score x;
+      __builtin_memset(&x, 0, sizeof x);
+      float score = best;
+      score *= wts;
+      score *= pl->tfw[i];
+      score *= pl->tfw[j];
+      if (r_hswb(r1)) score *= GB_WIKI_BIGRAM_WEIGHT;
+      if (r_hswb(r2)) score *= GB_WIKI_BIGRAM_WEIGHT;
+      x.final_score = score;
+      x.word_pos1 = (int32_t)r_wordpos(r1);
+      x.word_pos2 = (int32_t)r_wordpos(r2);
+      x.is_synonym1 = (int8_t)r_syn(r1);
+      x.is_synonym2 = (int8_t)r_syn(r2);
+      x.is_half_stop_wiki_bigram1 = (int8_t)r_hswb(r1);
+      x.is_half_stop_wiki_bigram2 = (int8_t)r_hswb(r2);
+      x.diversity_rank1 = (int8_t)r_div(r1);
+      x.diversity_rank2 = (int8_t)r_div(r2);
+      x.word_spam_rank1 = (int8_t)r_wsr(r1);
+      x.word_spam_rank2 = (int8_t)r_wsr(r2);
+      x.hash_group1 = (int8_t)r_hg(r1);
+      x.hash_group2 = (int8_t)r_hg(r2);
+      x.qdist = qdist;
+      x.density_rank1 = (int8_t)r_dens(r1);
+      x.density_rank2 = (int8_t)r_dens(r2);
+      x.fixed_distance = fixed ? 1 : 0;
+      x.qterm_num1 = pl->qterm[i];
+      x.qterm_num2 = pl->qterm[j];
+      x.tf_weight1 = pl->tfw[i];
+      x.tf_weight2 = pl->tfw[j];
+      x.bflags1 = (int8_t)pl->gflags0[i];
+      x.bflags2 = (int8_t)pl->gflags0[j];
+      x.in_same_wiki_phrase = (wts == (float)GB_WIKI_WEIGHT) ? 1 : 0;
+      __builtin_memcpy(ps + np, &x, sizeof x);
+    }
+    np++;
+  }
+};
+
+// The second pass does not walk the vote buffer: it looks each tree docid up
+// in every shrunk sublist with getWordPosList (Posdb.h:873-956), a binary
+// search that can miss a docid that is there (its step bottoms out at one
+// unit after three probes, and a probe landing on a run's first unit
+// resolves to the previous run).  A miss drops that sublist from the
+// docid's mini merge.  shrinkSubLists (Posdb.cpp:5334-5428) made each
+// sublist the survivors' runs in docid order, in place, so the search is
+// replayed over a directory: survivors sorted by docid (k_si_keys + hipcub),
+// and per list the exclusive prefix of their run units (k_si_dir).  Past the
+// shrunk end the in-place buffer still holds the list's own bytes.
+__global__ void k_si_keys(const uint32_t *surv, const uint64_t *cand, uint32_t nsurv, uint64_t *key, uint32_t *val) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nsurv; i += gridDim.x * blockDim.x) {
+    key[i] = cand[surv[i]];
+    val[i] = i;
+  }
+}
+
+// one block per list: cum[l][k] = units, in list l, of the survivors ranked
+// below k (k = 0..nsurv)
+__global__ void __launch_bounds__(1024) k_si_dir(const DevPlan *pl, const Loc *loc, uint64_t slot_ub,
+                                                 const uint32_t *surv, const uint32_t *surv_lm,
+                                                 const uint32_t *sperm, uint32_t nsurv, uint32_t *cum) {
+  __shared__ uint32_t s_w[16];
+  const int l = blockIdx.x;
+  uint32_t *c = cum + (size_t)l * (nsurv + 1);
+  uint32_t carry = 0;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (uint32_t b = 0; b < nsurv; b += 1024) {
+    const uint32_t k = b + threadIdx.x;
+    uint32_t u = 0;
+    if (k < nsurv) {
+      const uint32_t i = sperm[k];
+      if (surv_lm[i] >> l & 1) u = loc[(uint64_t)l * slot_ub + surv[i]].len;
+    }
+    uint32_t x = u;  // inclusive wave scan
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) s_w[w] = x;
+    __syncthreads();
+    uint32_t wb = 0, tot = 0;
+    for (int q = 0; q < 16; q++) {
+      wb += q < w ? s_w[q] : 0;
+      tot += s_w[q];
+    }
+    if (k < nsurv) c[k] = carry + wb + x - u;
+    carry += tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) c[nsurv] = carry;
+}
+
+// list lid's in-place buffer as getWordPosList reads it: unit u of the
+// shrunk image (u < S), else the list's own unit u (zero past its end)
+struct SiList {
+  const DevPlan *pl;
+  const Loc *loc;
+  uint64_t slot_ub;
+  const uint32_t *surv, *sperm, *cum;
+  uint32_t nsurv;
+  int lid;
+  __device__ uint32_t run_of(uint32_t u) const {  // last k with cum[k] <= u
+    uint32_t lo = 0, hi = nsurv;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi + 1) >> 1;
+      if (cum[mid] <= u) lo = mid;
+      else hi = mid - 1;
+    }
+    return lo;
+  }
+  __device__ uint64_t unit(int64_t u) const {
+    gu8 *base = gl(pl->lists[lid].p);
+    if (u < (int64_t)cum[nsurv]) {
+      const uint32_t k = run_of((uint32_t)u);
+      const Loc lc = loc[(uint64_t)lid * slot_ub + surv[sperm[k]]];
+      return load6(base + ((size_t)lc.unit + (size_t)(u - cum[k])) * 6);
+    }
+    if (u < (int64_t)pl->lists[lid].units) return load6(base + (size_t)u * 6);
+    return 0;
+  }
+};
+
+// getWordPosList(docId) over the shrunk list of U units: 1 found (the
+// docid's own run, which starts at unit `own`), 0 NULL, -1 a path not
+// replayed (a match at a negative key or off the list's start, or somewhere
+// else than `own`).  A list shared by several groups is shrunk again in
+// place for each later use; that pass re-copies the runs onto themselves and
+// then parses the stale bytes after them, extending the last run by E units
+// (k_ext_walk) -- the buffer's bytes stay those of SiList::unit, only the
+// later uses' U grows.
+__device__ int si_word_pos_list(const SiList &L, uint64_t docId, uint32_t own, int64_t U) {
+  int64_t step = (6 * U / 12) * 6;  // bytes
+  int64_t p = step / 6;              // units
+  int count = 0;
+  for (int it = 0; it < 256; it++) {
+    const int64_t origp = p;
+    while (p > 0 && ((L.unit(p) >> 8) & 0x02)) p--;
+    p -= 1;
+    const uint64_t d = ((L.unit(p + 1) >> 8) & 0xffffffffffull) >> 2;
+    if (d == docId) {
+      if (p < 0) return -1;
+      if (!(L.unit(p) & 0x01)) return -1;
+      return p == (int64_t)own ? 1 : -1;
+    }
+    step >>= 1;
+    step -= step % 6;
+    if (step <= 0) {
+      step = 6;
+      if (count++ >= 2) return 0;
+    }
+    if (d < docId) {
+      p = origp + step / 6;
+      if (p > U) p = U - 1;
+    } else {
+      p = origp - step / 6;
+      if (p < 0) p = 0;
+    }
+  }
+  return -1;
+}
+
+// one lane per tree docid: the first pass's score_survivor again, with the
+// recorder, over the survivor's arena range (k_score's fallback store)
+__global__ void __launch_bounds__(SCORE_TPB) k_scoreinfo(const DevPlan *pl, const Counters *ctr, const uint32_t *surv,
+                                                         const uint32_t *surv_lm,
+                                                         const unsigned long long *surv_off, const Loc *loc,
+                                                         uint64_t slot_ub, uint64_t *arena, const uint64_t *tdoc,
+                                                         const uint64_t *sdoc, const uint32_t *sperm,
+                                                         const uint32_t *cum, uint32_t nsurv,
+                                                         uint32_t n, SurvOut *info, int32_t *counts,
+                                                         gbgpu_single_score *ss, int scap, gbgpu_pair_score *ps,
+                                                         int pcap) {
+  __shared__ float s_sm[npairs<MAXG>() * SCORE_TPB];
+  stage_weights(&c_weights);
+  const uint32_t t = blockIdx.x * SCORE_TPB + threadIdx.x;
+  if (t >= n) return;
+  SurvOut so{0.0f, 0, 0, -1};
+  const uint64_t d = tdoc[t];
+  uint32_t lo = 0, hi = nsurv;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (sdoc[mid] < d) lo = mid + 1;
+    else hi = mid;
+  }
+  if (lo >= nsurv || sdoc[lo] != d) {  // not a survivor: reported as ECORRUPT
+    info[t] = so;
+    return;
+  }
+  const uint32_t i = sperm[lo];
+  const uint32_t s = surv[i];
+  // the sublists getWordPosList finds the docid in (Posdb.cpp:6195-6241)
+  const uint32_t lm = surv_lm[i];
+  uint16_t kill[MAXG];
+  for (int j = 0; j < MAXG; j++) kill[j] = 0;
+  const uint32_t anys = ctr->anysurv;
+  for (int j = 0; j < pl->ngroups; j++) {
+    if (pl->gflags0[j] & BF_NEGATIVE) continue;
+    for (int x = 0; x < pl->gnsub[j]; x++) {
+      const int lid = pl->gsub[j][x];
+      if (!(anys >> lid & 1) || !(lm >> lid & 1)) continue;
+      const SiList L{pl, loc, slot_ub, surv, sperm, cum + (size_t)lid * (nsurv + 1), nsurv, lid};
+      const bool later = (pl->reshare_mask >> lid & 1) &&
+                         !(j == pl->lists[lid].owner_group && x == pl->lists[lid].owner_sub);
+      const int64_t U = (int64_t)L.cum[nsurv] + ((later && ctr->ext[lid].slot1) ? ctr->ext[lid].E : 0);
+      const int f = si_word_pos_list(L, d, L.cum[lo], U);
+      if (f < 0) {
+        so.ok = -2;
+        info[t] = so;
+        return;
+      }
+      if (f == 0) kill[j] |= (uint16_t)(1u << x);
+    }
+  }
+  unsigned long long off = surv_off[i];
+  for (uint32_t x = lm & pl->reshare_mask; x; x &= x - 1) {  // as k_score: re-shrunk copies
+    const int l = __ffs(x) - 1;
+    const ListExt &e = ctr->ext[l];
+    if (e.slot1 == s + 1 && e.reloc) off = e.off;
+  }
+  ScoreRec rec{ss + (size_t)t * scap, ps + (size_t)t * pcap, 0, 0, scap, pcap};
+  uint32_t key, nr;
+  uint64_t tmerge = 0, tm[3] = {0, 0, 0};
+  const GlobalRecs grec{(__attribute__((address_space(1))) uint64_t *)(arena + off)};
+  score_survivor<MAXG, MAXSUB>(pl, ctr, s, lm, anys, loc, slot_ub, grec, s_sm + threadIdx.x, &key, 0, &nr,
+                               false, tmerge, tm, &rec, &so, kill);
+  info[t] = so;
+  counts[2 * t] = rec.ns;
+  counts[2 * t + 1] = rec.np;
 }
 
 // ------------------------------------------------------- site clustering
@@ -2684,6 +2980,7 @@ struct QuerySlot {
   DevBuf split, swin;   // docid splits: one piece's list windows; window table
   DevBuf blk, sflag, sbound, order, tree;  // site clustering: ordered compaction, bounds, TopTree state
   DevBuf white, wrej;                       // "&sites=" whitelist: sorted 5-byte values; rejected slots
+  DevBuf si;                                // second pass's score info (score_info)
   std::vector<uint64_t> h_white;            // its host copy (the upload's source)
   uint32_t epoch = 0;
   uint8_t *h_stage = nullptr;  // pinned: query tables (host -> device, one copy)
@@ -2702,6 +2999,10 @@ struct QuerySlot {
   int k = 0;
   size_t res_bytes = 0;
   int32_t docs_wanted = 0;
+  bool want_info = false;   // m_getDocIdScoringInfo
+  int info_docs = 0;        // m_docsToGet: the second pass's docid limit
+  int info_ng = 0;          // m_numQueryTermInfos
+  int info_scap = 0, info_pcap = 0;  // singles / pairs one docid can record
   int64_t scan_bytes = 0;
   int64_t g0_bytes = 0, probe_bytes = 0;  // list bytes of candidate extraction / of the probe scan
   int64_t stats[8] = {};                   // gbgpu_slot_stats of the last collected query
@@ -2720,7 +3021,7 @@ struct QuerySlot {
     if (stream) (void)hipStreamSynchronize(stream);
     DevBuf *bufs[] = {&tables, &chunkcnt, &cand, &lmask, &ulen, &loc, &surv, &survoff, &survlm, &survu, &perm,
                       &scratch, &skey, &sdoc, &sel, &gath, &res, &dir, &split, &swin,
-                      &blk, &sflag, &sbound, &order, &tree};
+                      &blk, &sflag, &sbound, &order, &tree, &white, &wrej, &si};
     for (auto *b : bufs) b->release();
     if (h_stage) (void)hipHostFree(h_stage);
     if (h_res) (void)hipHostFree(h_res);
@@ -2833,7 +3134,10 @@ static int snapshot_lists(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms, 
   if (!p || nterms < 0 || (nterms && (!terms || !handles))) return EINVAL;
   if (p->docs_to_get <= 0 || p->real_max_top <= 0 || p->num_docid_splits <= 0) return EINVAL;
   if (nterms > 1024) return GBGPU_EUNSUPPORTED;
-  if (p->get_docid_scoring_info) return GBGPU_EUNSUPPORTED;  // second scoring pass: CPU body
+  // the second scoring pass with the tree's domain caps, over docid-split
+  // pieces, or under the paging filter: the CPU body
+  if (p->get_docid_scoring_info && (p->site_clustering || p->num_docid_splits > 1 || p->min_serp_docid))
+    return GBGPU_EUNSUPPORTED;
   ents.resize(nterms);
   std::lock_guard<std::mutex> g(ctx->lists_mu);
   for (int i = 0; i < nterms; i++) {
@@ -2964,6 +3268,22 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   q.early = (hp.ngroups == 0 || hp.min_list_size == 0);
   q.scan_bytes = 0;
   q.replayed = false;
+  q.want_info = p->get_docid_scoring_info != 0;
+  q.info_docs = p->docs_to_get;
+  q.info_ng = hp.ngroups;
+  q.info_scap = hp.ngroups * hp.real_max_top;
+  q.info_pcap = hp.ngroups * (hp.ngroups - 1) / 2 * hp.real_max_top;
+  if (q.want_info) {
+    // allocTopTree's reservations (Posdb.cpp:931-975): a call whose records
+    // would not fit is dropped there ("CRITICAL ... overflow"); not emulated,
+    // so refuse any request whose worst case could reach it
+    const int64_t xx = std::max<int64_t>(hp.docs_wanted, 32);
+    const int64_t nt = std::min(nterms, 10);
+    const int64_t pcap_ref = nt * nt / 2 * hp.real_max_top * xx;
+    const int64_t scap_ref = nt * hp.real_max_top * xx;
+    if ((int64_t)p->docs_to_get * q.info_pcap > pcap_ref || (int64_t)p->docs_to_get * q.info_scap > scap_ref)
+      return GBGPU_EUNSUPPORTED;
+  }
   if (q.early) {
     q.pending = true;
     return 0;
@@ -3030,6 +3350,7 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
     P.qpos[j] = g.qpos;
     P.wiki[j] = g.wiki;
     P.quote[j] = g.quote;
+    P.qterm[j] = g.qterm;
     for (int x = 0; x < MAXSUB; x++) P.gsubflags[j][x] = x < 50 ? g.flags[x] : 0;
     const bool neg = (g.flags[0] & BF_NEGATIVE) != 0;
     if (!neg) P.pos_mask |= 1u << j;
@@ -3374,6 +3695,100 @@ static void slot_released(gbgpu_ctx *ctx) {
   ctx->free_cv.notify_all();
 }
 
+// The second pass (see k_scoreinfo) for the first min(tree size, docs_to_get)
+// docids of the collected tree, and the three buffers' host layout: one
+// DocIdScore per docid in tree order, its PairScores / SingleScores appended
+// in scoring order, m_pairsOffset / m_singlesOffset the byte offsets where
+// its first record went (-1: none).  A docid the scorer rejects (minScore <=
+// 0, never a tree member) would append records without a DocIdScore, as
+// Posdb.cpp:7228-7230 jumps past the bookkeeping.
+static int score_info(QuerySlot &q, const uint32_t *keys, const uint64_t *docs, uint32_t nsurv, gbgpu_result *out) {
+  int n = 0;
+  while (n < q.k && n < q.info_docs && keys[n]) n++;
+  if (!n) return 0;
+  const DevPlan *hpl = reinterpret_cast<const DevPlan *>(q.h_stage);  // this query's plan (enqueue's staging copy)
+  const int scap = std::max(q.info_scap, 1), pcap = std::max(q.info_pcap, 1);
+  const int nl = std::max(hpl->nlists, 1);
+  size_t sort_tmp = 0;
+  HIPCHECK(si_sort_pairs(nullptr, sort_tmp, nullptr, nullptr, nullptr, nullptr, nsurv, q.stream));
+  const size_t o_key = 0;
+  const size_t o_val = o_key + align256(8 * (size_t)nsurv);
+  const size_t o_skey = o_val + align256(4 * (size_t)nsurv);
+  const size_t o_sval = o_skey + align256(8 * (size_t)nsurv);
+  const size_t o_cum = o_sval + align256(4 * (size_t)nsurv);
+  const size_t o_tmp = o_cum + align256(4 * (size_t)nl * (nsurv + 1));
+  const size_t o_tdoc = o_tmp + align256(sort_tmp);
+  const size_t o_info = o_tdoc + align256(8 * (size_t)n);
+  const size_t o_cnt = o_info + align256(sizeof(SurvOut) * (size_t)n);
+  const size_t o_ss = o_cnt + align256(8 * (size_t)n);
+  const size_t o_ps = o_ss + align256(sizeof(gbgpu_single_score) * (size_t)n * scap);
+  const size_t total = o_ps + sizeof(gbgpu_pair_score) * (size_t)n * pcap;
+  if (q.si.ensure(total)) return ENOMEM;
+  hipStream_t st = q.stream;
+  const uint32_t g = std::max(1u, std::min<uint32_t>(1024, (nsurv + 255) / 256));
+  hipLaunchKernelGGL(k_si_keys, dim3(g), dim3(256), 0, st, q.surv.as<uint32_t>(), q.cand.as<uint64_t>(), nsurv,
+                     q.si.as<uint64_t>(o_key), q.si.as<uint32_t>(o_val));
+  HIPCHECK(si_sort_pairs(q.si.as<uint8_t>(o_tmp), sort_tmp, q.si.as<uint64_t>(o_key), q.si.as<uint64_t>(o_skey),
+                         q.si.as<uint32_t>(o_val), q.si.as<uint32_t>(o_sval), nsurv, st));
+  hipLaunchKernelGGL(k_si_dir, dim3(nl), dim3(1024), 0, st, q.tables.as<DevPlan>(), q.loc.as<Loc>(), q.slot_ub,
+                     q.surv.as<uint32_t>(), q.survlm.as<uint32_t>(), q.si.as<uint32_t>(o_sval), nsurv,
+                     q.si.as<uint32_t>(o_cum));
+  HIPCHECK(hipMemcpyAsync(q.si.as<uint8_t>(o_tdoc), docs, 8 * (size_t)n, hipMemcpyHostToDevice, st));
+  hipLaunchKernelGGL(k_scoreinfo, dim3((n + SCORE_TPB - 1) / SCORE_TPB), dim3(SCORE_TPB), 0, st,
+                     q.tables.as<DevPlan>(), q.res.as<Counters>(), q.surv.as<uint32_t>(), q.survlm.as<uint32_t>(),
+                     q.survoff.as<unsigned long long>(), q.loc.as<Loc>(), q.slot_ub, q.scratch.as<uint64_t>(),
+                     q.si.as<uint64_t>(o_tdoc), q.si.as<uint64_t>(o_skey), q.si.as<uint32_t>(o_sval),
+                     q.si.as<uint32_t>(o_cum), nsurv, (uint32_t)n, q.si.as<SurvOut>(o_info),
+                     q.si.as<int32_t>(o_cnt), q.si.as<gbgpu_single_score>(o_ss), scap,
+                     q.si.as<gbgpu_pair_score>(o_ps), pcap);
+  HIPCHECK(hipGetLastError());
+  std::vector<SurvOut> info((size_t)n);
+  std::vector<int32_t> cnt(2 * (size_t)n);
+  std::vector<gbgpu_single_score> hs((size_t)n * scap);
+  std::vector<gbgpu_pair_score> hp((size_t)n * pcap);
+  HIPCHECK(hipMemcpyAsync(info.data(), q.si.as<uint8_t>(o_info), sizeof(SurvOut) * (size_t)n, hipMemcpyDeviceToHost, st));
+  HIPCHECK(hipMemcpyAsync(cnt.data(), q.si.as<uint8_t>(o_cnt), 8 * (size_t)n, hipMemcpyDeviceToHost, st));
+  HIPCHECK(hipMemcpyAsync(hs.data(), q.si.as<uint8_t>(o_ss), sizeof(gbgpu_single_score) * hs.size(),
+                          hipMemcpyDeviceToHost, st));
+  HIPCHECK(hipMemcpyAsync(hp.data(), q.si.as<uint8_t>(o_ps), sizeof(gbgpu_pair_score) * hp.size(),
+                          hipMemcpyDeviceToHost, st));
+  HIPCHECK(hipStreamSynchronize(st));
+  int nd = 0, np = 0, ns = 0;
+  bool room = true;
+  for (int t = 0; t < n; t++) {
+    if (info[t].ok == -1) return GBGPU_ECORRUPT;      // a tree docid with no survivor entry
+    if (info[t].ok == -2) return GBGPU_EUNSUPPORTED;  // a getWordPosList path not replayed
+    const int cs = cnt[2 * t], cp = cnt[2 * t + 1];
+    if (cs > scap || cp > pcap) return GBGPU_ECAPACITY;
+    gbgpu_docid_score d;
+    std::memset(&d, 0, sizeof d);
+    d.docid = (int64_t)docs[t];
+    d.final_score = (double)info[t].score;
+    d.site_rank = (int8_t)info[t].site_rank;
+    d.doc_lang = info[t].doc_lang;
+    d.num_required_terms = q.info_ng;
+    d.num_pairs = cp;
+    d.num_singles = cs;
+    d.pairs_offset = cp ? np * (int32_t)sizeof(gbgpu_pair_score) : -1;
+    d.singles_offset = cs ? ns * (int32_t)sizeof(gbgpu_single_score) : -1;
+    if (ns + cs > out->single_scores_cap || np + cp > out->pair_scores_cap ||
+        (info[t].ok && nd + 1 > out->docid_scores_cap))
+      room = false;
+    if (room) {
+      if (cs) std::memcpy(out->single_scores + ns, &hs[(size_t)t * scap], sizeof(gbgpu_single_score) * cs);
+      if (cp) std::memcpy(out->pair_scores + np, &hp[(size_t)t * pcap], sizeof(gbgpu_pair_score) * cp);
+      if (info[t].ok) out->docid_scores[nd] = d;
+    }
+    ns += cs;
+    np += cp;
+    nd += info[t].ok ? 1 : 0;
+  }
+  out->n_docid_scores = nd;
+  out->n_pair_scores = np;
+  out->n_single_scores = ns;
+  return room ? 0 : ENOSPC;
+}
+
 // hits_acc: when non-null, the query's intersected docids are appended to it
 // (docid splits gather them over the pieces) instead of being written to out
 static int collect(gbgpu_ctx *ctx, QuerySlot &q, gbgpu_result *out, std::vector<int64_t> *hits_acc = nullptr) {
@@ -3383,6 +3798,7 @@ static int collect(gbgpu_ctx *ctx, QuerySlot &q, gbgpu_result *out, std::vector<
   out->hits = 0;
   out->filtered = 0;
   out->n_hit_docids = 0;
+  out->n_docid_scores = out->n_pair_scores = out->n_single_scores = 0;
   out->docs_wanted = q.docs_wanted;
   if (q.early) {
     q.held.clear();
@@ -3452,6 +3868,7 @@ static int collect(gbgpu_ctx *ctx, QuerySlot &q, gbgpu_result *out, std::vector<
     n++;
   }
   out->n = n;
+  if (q.want_info) return score_info(q, keys, docs, (uint32_t)out->hits, out);
   return 0;
 }
 

@@ -101,6 +101,7 @@ struct DevPlan {
   uint8_t gsubflags[MAXG][MAXSUB];  // m_bigramFlags[x]
   float tfw[MAXG];
   int32_t qpos[MAXG], wiki[MAXG], quote[MAXG];
+  int32_t qterm[MAXG];  // m_qtermNum (the second pass's score info)
   // candidate arrays (sublists of m_minListi, distinct lists, in order)
   int g0n;
   int g0list[MAXG0];

@@ -147,10 +147,21 @@ struct ScoreCtx {
   uint32_t excl;         // bit i: group i is piped/negative/number/facet (BF_EXCLUDE)
 };
 
-// getSingleTermScore, Posdb.cpp:3087-3301 (pdcs == NULL).  bestPos = record
-// index of the best non-body occurrence or -1.
-template <int NQ, class RP>
-__device__ __forceinline__ float single_term_score(const ScoreCtx<NQ> &c, const DocView<NQ, RP> &d, int i, int *bestPos) {
+// The second pass's score info (pdcs != NULL, Posdb.cpp:3247-3298,
+// 4195-4280): a recorder receives each scorer's top list.  NoRec (the first
+// pass) compiles away; ScoreRec writes the reference's SingleScore /
+// PairScore records (include/gbgpu.h mirrors) for one docid.
+struct NoRec {
+  static constexpr bool on = false;
+  __device__ void single(const DevPlan *, int, float, uint64_t) {}
+  __device__ void pair(const DevPlan *, int, int, float, float, int32_t, uint64_t, uint64_t, bool) {}
+};
+
+// getSingleTermScore, Posdb.cpp:3087-3301.  bestPos = record index of the
+// best non-body occurrence or -1; REC receives the top list (pdcs path).
+template <int NQ, class RP, class REC = NoRec>
+__device__ __forceinline__ float single_term_score(const ScoreCtx<NQ> &c, const DocView<NQ, RP> &d, int i, int *bestPos,
+                                                  REC *rec = nullptr) {
   const Weights &W = s_weights;
   float nonBodyMax = -1.0;
   int minx = 0;
@@ -167,8 +178,12 @@ __device__ __forceinline__ float single_term_score(const ScoreCtx<NQ> &c, const 
   int numTop = 0;
   int bp = -1;
   const int rmt = c.realMaxTop;
+  // a do-while, as the reference's loop (Posdb.cpp:3117-3206): an empty
+  // mini-merged list still has its first key read -- the next group's
+  // first key, written at the same place (see score_survivor)
   const int e = rget(d.end, i);
-  for (int r = rget(d.beg, i); r < e; r++) {
+  int r = rget(d.beg, i);
+  do {
     const uint64_t k = d.rec[r];
     float score = 100.0;
     const uint32_t div = r_div(k);
@@ -238,7 +253,7 @@ __device__ __forceinline__ float single_term_score(const ScoreCtx<NQ> &c, const 
       nonBodyMax = score;
       bp = r;
     }
-  }
+  } while (++r < e);
   *bestPos = bp;
   float sum = 0.0;
 #pragma unroll
@@ -252,6 +267,10 @@ __device__ __forceinline__ float single_term_score(const ScoreCtx<NQ> &c, const 
   }
   sum *= c.pl->tfw[i];
   sum *= c.pl->tfw[i];
+  if constexpr (REC::on) {
+    for (int q = 0; q < MAX_TOP; q++)
+      if (q < numTop) rec->single(c.pl, i, bestScores[q], d.rec[rget(bestwpi, q)]);
+  }
   return sum;
 }
 
@@ -459,9 +478,14 @@ __device__ __forceinline__ void eval_window(ScoreCtx<NQ> &c, const DocView<NQ, R
   for (int q = 0; q < NQ; q++) c.window[q] = ptrs[q];
 }
 
-// getTermPairScoreForAny, Posdb.cpp:3631-4344 (pdcs == NULL)
-template <int NQ, class RP>
-__device__ __forceinline__ float pair_score_any(const ScoreCtx<NQ> &c, const DocView<NQ, RP> &d, int i, int j) {
+// getTermPairScoreForAny, Posdb.cpp:3631-4344; REC receives the top pairs
+// (pdcs path, 4195-4280) with their record indices and fixedDistance flag --
+// which the reference only assigns when dist < 50 or the distance is fixed,
+// so it carries over from the previous scored pair otherwise (false at the
+// start, where the reference's is uninitialised)
+template <int NQ, class RP, class REC = NoRec>
+__device__ __forceinline__ float pair_score_any(const ScoreCtx<NQ> &c, const DocView<NQ, RP> &d, int i, int j,
+                                               REC *rec = nullptr) {
   const Weights &W = s_weights;
   const DevPlan *pl = c.pl;
   float wts;
@@ -492,11 +516,18 @@ __device__ __forceinline__ float pair_score_any(const ScoreCtx<NQ> &c, const Doc
   float minv = 0.0f;  // bestScores[minx]
   float bestScores[MAX_TOP];
   uint32_t bestmhg1[MAX_TOP], bestmhg2[MAX_TOP];
+  int bestwpi[REC::on ? MAX_TOP : 1], bestwpj[REC::on ? MAX_TOP : 1];
+  bool bestFixed[REC::on ? MAX_TOP : 1];
+  bool fixedDistance = false;
 #pragma unroll
   for (int q = 0; q < MAX_TOP; q++) {
     bestScores[q] = 0.0f;
     bestmhg1[q] = 0xff;
     bestmhg2[q] = 0xff;
+    if constexpr (REC::on) {
+      bestwpi[q] = bestwpj[q] = 0;
+      bestFixed[q] = false;
+    }
   }
   int numTop = 0;
   const int rmt = c.realMaxTop;
@@ -520,10 +551,13 @@ __device__ __forceinline__ float pair_score_any(const ScoreCtx<NQ> &c, const Doc
         const uint32_t syn1 = r_syn(ki), syn2 = r_syn(kj);
         if (dist < 2) dist = 2;
         if (dist < 50) {
+          fixedDistance = false;
         } else if (mhg1 != mhg2) {
           dist = FIXED_DISTANCE;
+          fixedDistance = true;
         } else if (mhg1 == GB_HG_INLINKTEXT) {
           dist = FIXED_DISTANCE;
+          fixedDistance = true;
         }
         if (dist >= qdist) dist = dist - qdist;
         score = 100 * denw1 * denw2;
@@ -543,10 +577,13 @@ __device__ __forceinline__ float pair_score_any(const ScoreCtx<NQ> &c, const Doc
       if (!inSameQuotedPhrase) {
         if (dist < 2) dist = 2;
         if (dist < 50) {
+          fixedDistance = false;
         } else if (mhg1 != mhg2) {
           dist = FIXED_DISTANCE;
+          fixedDistance = true;
         } else if (mhg1 == GB_HG_INLINKTEXT) {
           dist = FIXED_DISTANCE;
+          fixedDistance = true;
         }
         if (dist >= qdist) {
           dist = dist - qdist;
@@ -590,6 +627,11 @@ __device__ __forceinline__ float pair_score_any(const ScoreCtx<NQ> &c, const Doc
           bestScores[q] = score;
           bestmhg1[q] = mhg1;
           bestmhg2[q] = mhg2;
+          if constexpr (REC::on) {
+            bestwpi[q] = wi;
+            bestwpj[q] = wj;
+            bestFixed[q] = fixedDistance;
+          }
         }
       }
       if (numTop >= rmt) {
@@ -629,6 +671,12 @@ __device__ __forceinline__ float pair_score_any(const ScoreCtx<NQ> &c, const Doc
   sum *= wts;
   sum *= pl->tfw[i];
   sum *= pl->tfw[j];
+  if constexpr (REC::on) {
+    for (int q = 0; q < MAX_TOP; q++)
+      if (q < numTop)
+        rec->pair(pl, i, j, bestScores[q], wts, qdist, d.rec[rget(bestwpi, q)], d.rec[rget(bestwpj, q)],
+                  rget(bestFixed, q));
+  }
   return sum;
 }
 
@@ -637,9 +685,9 @@ __device__ __forceinline__ float pair_score_any(const ScoreCtx<NQ> &c, const Doc
 // (minScore <= 0); siteRank/docLang come from the first key of the first
 // present group (Posdb.cpp:6985-7003).  sm: this lane's score-matrix column
 // (npairs<NQ>() floats at stride smStride).
-template <int NQ, class RP>
+template <int NQ, class RP, class REC = NoRec>
 __device__ __forceinline__ bool score_doc(const Weights *w, const DevPlan *pl, const DocView<NQ, RP> &d, int siteRank, int docLang,
-                                 float *sm, int smStride, float *outScore, int stop = 0) {
+                                 float *sm, int smStride, float *outScore, int stop = 0, REC *rec = nullptr) {
   ScoreCtx<NQ> c;
   c.w = w;
   c.pl = pl;
@@ -691,7 +739,7 @@ __device__ __forceinline__ bool score_doc(const Weights *w, const DevPlan *pl, c
   for (int i = 0; i < c.nq; i++) {
     if ((c.excl >> i & 1)) continue;
     int bp;
-    const float sts = single_term_score(c, d, i, &bp);
+    const float sts = single_term_score<NQ, RP, REC>(c, d, i, &bp, rec);
     rset(bestPos, i, bp);
     if (sts < minSingleScore) minSingleScore = sts;
   }
@@ -868,7 +916,7 @@ __device__ __forceinline__ bool score_doc(const Weights *w, const DevPlan *pl, c
       if ((c.excl >> j & 1)) continue;
       if (!(d.present >> i & 1)) continue;
       if (!(d.present >> j & 1)) continue;
-      const float score = pair_score_any(c, d, i, j);
+      const float score = pair_score_any<NQ, RP, REC>(c, d, i, j, rec);
       if (score >= minPairScore && minPairScore >= 0.0) continue;
       minPairScore = score;
     }

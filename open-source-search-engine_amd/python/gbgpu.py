@@ -81,6 +81,61 @@ class ListRef(ctypes.Structure):
     _fields_ = [("bytes", ctypes.c_void_p), ("size", ctypes.c_int64)]
 
 
+class PairScore(ctypes.Structure):
+    """gbgpu_pair_score == the reference's PairScore (Posdb.h:767-800)."""
+
+    _fields_ = [
+        ("final_score", ctypes.c_float),
+        ("is_synonym1", ctypes.c_int8), ("is_synonym2", ctypes.c_int8),
+        ("is_half_stop_wiki_bigram1", ctypes.c_int8), ("is_half_stop_wiki_bigram2", ctypes.c_int8),
+        ("diversity_rank1", ctypes.c_int8), ("diversity_rank2", ctypes.c_int8),
+        ("density_rank1", ctypes.c_int8), ("density_rank2", ctypes.c_int8),
+        ("word_spam_rank1", ctypes.c_int8), ("word_spam_rank2", ctypes.c_int8),
+        ("hash_group1", ctypes.c_int8), ("hash_group2", ctypes.c_int8),
+        ("in_same_wiki_phrase", ctypes.c_int8), ("fixed_distance", ctypes.c_int8),
+        ("word_pos1", ctypes.c_int32), ("word_pos2", ctypes.c_int32),
+        ("term_freq1", ctypes.c_int64), ("term_freq2", ctypes.c_int64),
+        ("tf_weight1", ctypes.c_float), ("tf_weight2", ctypes.c_float),
+        ("qterm_num1", ctypes.c_int32), ("qterm_num2", ctypes.c_int32),
+        ("bflags1", ctypes.c_int8), ("bflags2", ctypes.c_int8),
+        ("qdist", ctypes.c_int32),
+    ]
+
+
+class SingleScore(ctypes.Structure):
+    """gbgpu_single_score == the reference's SingleScore (Posdb.h:802-816)."""
+
+    _fields_ = [
+        ("final_score", ctypes.c_float),
+        ("is_synonym", ctypes.c_int8), ("is_half_stop_wiki_bigram", ctypes.c_int8),
+        ("diversity_rank", ctypes.c_int8), ("density_rank", ctypes.c_int8),
+        ("word_spam_rank", ctypes.c_int8), ("hash_group", ctypes.c_int8),
+        ("word_pos", ctypes.c_int32),
+        ("term_freq", ctypes.c_int64),
+        ("tf_weight", ctypes.c_float),
+        ("qterm_num", ctypes.c_int32),
+        ("bflags", ctypes.c_int8),
+    ]
+
+
+class DocIdScore(ctypes.Structure):
+    """gbgpu_docid_score == the reference's DocIdScore (Posdb.h:818-866)."""
+
+    _fields_ = [
+        ("docid", ctypes.c_int64),
+        ("final_score", ctypes.c_double),
+        ("site_rank", ctypes.c_int8),
+        ("doc_lang", ctypes.c_int32),
+        ("num_required_terms", ctypes.c_int32),
+        ("num_pairs", ctypes.c_int32), ("num_singles", ctypes.c_int32),
+        ("pairs_offset", ctypes.c_int32), ("singles_offset", ctypes.c_int32),
+        ("pair_scores", ctypes.c_void_p), ("single_scores", ctypes.c_void_p),
+    ]
+
+
+PAIR_DT, SINGLE_DT, DOCID_DT = np.dtype(PairScore), np.dtype(SingleScore), np.dtype(DocIdScore)
+
+
 class Result(ctypes.Structure):
     _fields_ = [
         ("docids", ctypes.POINTER(ctypes.c_int64)),
@@ -93,6 +148,10 @@ class Result(ctypes.Structure):
         ("hit_docids", ctypes.POINTER(ctypes.c_int64)),
         ("hit_capacity", ctypes.c_int64),
         ("n_hit_docids", ctypes.c_int64),
+        ("docid_scores", ctypes.c_void_p), ("docid_scores_cap", ctypes.c_int32), ("n_docid_scores", ctypes.c_int32),
+        ("pair_scores", ctypes.c_void_p), ("pair_scores_cap", ctypes.c_int32), ("n_pair_scores", ctypes.c_int32),
+        ("single_scores", ctypes.c_void_p), ("single_scores_cap", ctypes.c_int32),
+        ("n_single_scores", ctypes.c_int32),
     ]
 
 
@@ -342,6 +401,11 @@ class QueryResult:
     filtered: int
     docs_wanted: int
     hit_docids: Optional[np.ndarray] = None  # the intersected docid set (when asked for)
+    # the second pass's score info (get_docid_scoring_info): structured arrays
+    # of DOCID_DT / PAIR_DT / SINGLE_DT
+    docid_scores: Optional[np.ndarray] = None
+    pair_scores: Optional[np.ndarray] = None
+    single_scores: Optional[np.ndarray] = None
 
 
 class Engine:
@@ -375,7 +439,19 @@ class Engine:
         _check(self.lib.gbgpu_list_free(self.ctx, handle), "free")
 
     @staticmethod
-    def _result(cap: int, hit_cap: int = 0):
+    def info_arrays(params: Params, nterms: int):
+        """Score-info output arrays sized for the request's worst case
+        (every group pair and group recording real_max_top entries)."""
+        if not params.get_docid_scoring_info:
+            return None
+        nd = max(1, params.docs_to_get)
+        ng = max(1, min(nterms, 16))
+        rmt = max(1, params.real_max_top)
+        return (np.zeros(nd, DOCID_DT), np.zeros(max(1, nd * ng * (ng - 1) // 2 * rmt), PAIR_DT),
+                np.zeros(nd * ng * rmt, SINGLE_DT))
+
+    @staticmethod
+    def _result(cap: int, hit_cap: int = 0, info=None):
         d = (ctypes.c_int64 * max(cap, 1))()
         s = (ctypes.c_float * max(cap, 1))()
         r = Result(ctypes.cast(d, ctypes.POINTER(ctypes.c_int64)), ctypes.cast(s, ctypes.POINTER(ctypes.c_float)),
@@ -385,14 +461,23 @@ class Engine:
             h = np.zeros(hit_cap, np.int64)
             r.hit_docids = h.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))
             r.hit_capacity = hit_cap
+        if info is not None:
+            r.docid_scores, r.docid_scores_cap = info[0].ctypes.data, len(info[0])
+            r.pair_scores, r.pair_scores_cap = info[1].ctypes.data, len(info[1])
+            r.single_scores, r.single_scores_cap = info[2].ctypes.data, len(info[2])
         return r, d, s, h
 
     @staticmethod
-    def _pack(r, d, s, h=None) -> QueryResult:
+    def _pack(r, d, s, h=None, info=None) -> QueryResult:
         n = r.n
-        return QueryResult(np.frombuffer(d, dtype=np.int64, count=n).copy(),
-                           np.frombuffer(s, dtype=np.float32, count=n).copy(), r.hits, r.filtered, r.docs_wanted,
-                           None if h is None else h[:r.n_hit_docids].copy())
+        q = QueryResult(np.frombuffer(d, dtype=np.int64, count=n).copy(),
+                        np.frombuffer(s, dtype=np.float32, count=n).copy(), r.hits, r.filtered, r.docs_wanted,
+                        None if h is None else h[:r.n_hit_docids].copy())
+        if info is not None:
+            q.docid_scores = info[0][:r.n_docid_scores].copy()
+            q.pair_scores = info[1][:r.n_pair_scores].copy()
+            q.single_scores = info[2][:r.n_single_scores].copy()
+        return q
 
     @staticmethod
     def host_lists(lists: Sequence[bytes]):
@@ -410,18 +495,20 @@ class Engine:
         n = len(terms)
         qt = (QTerm * max(n, 1))(*terms)
         keep, refs = lists if isinstance(lists, tuple) else self.host_lists(lists)
-        r, d, s, h = self._result(cap, hit_cap)
+        info = self.info_arrays(params, n)
+        r, d, s, h = self._result(cap, hit_cap, info)
         _check(self.lib.gbgpu_query(self.ctx, qt, n, refs, ctypes.byref(params), ctypes.byref(r)), "query")
-        return self._pack(r, d, s, h)
+        return self._pack(r, d, s, h, info)
 
     def query_resident(self, terms: Sequence[QTerm], handles: Sequence[int], params: Params,
                        cap: int = 4096, hit_cap: int = 0) -> QueryResult:
         n = len(terms)
         qt = (QTerm * max(n, 1))(*terms)
         hh = (ctypes.c_int32 * max(n, 1))(*handles)
-        r, d, s, h = self._result(cap, hit_cap)
+        info = self.info_arrays(params, n)
+        r, d, s, h = self._result(cap, hit_cap, info)
         _check(self.lib.gbgpu_query_resident(self.ctx, qt, n, hh, ctypes.byref(params), ctypes.byref(r)), "query")
-        return self._pack(r, d, s, h)
+        return self._pack(r, d, s, h, info)
 
     def set_slots(self, n: int) -> None:
         _check(self.lib.gbgpu_set_query_slots(self.ctx, n), "set_query_slots")

@@ -45,7 +45,8 @@ typedef struct orc_params {
   int32_t num_docid_splits; /* m_numDocIdSplits: Msg39's split loop      */
   float   same_lang_weight; /* m_sameLangWeight                        */
   int32_t do_max_score_algo;/* m_doMaxScoreAlgo                        */
-  int32_t reserved0;
+  int32_t get_docid_scoring_info; /* m_getDocIdScoringInfo (gbref only; the oracle
+                                     does not restate the second pass)  */
   double  max_serp_score;   /* m_maxSerpScore                          */
   int64_t min_serp_docid;   /* m_minSerpDocId (nonzero: paging filter) */
   /* the "&sites=" whitelist (Msg39Request::size_whiteList > 1 and

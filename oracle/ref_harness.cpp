@@ -28,6 +28,8 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <vector>
+
 #include "posdb_oracle.h"  // orc_qterm / orc_params / orc_result
 
 // Symbols main.cpp defines for the gb binary (main.cpp:155,197,199); the
@@ -71,6 +73,9 @@ __attribute__((constructor(101))) static void install_fault_handler() {
 }
 
 static bool s_inited = false;
+// the second pass's score info (Posdb.cpp:6116-6244, 7554-7665): the last
+// query's m_scoreInfoBuf / m_pairScoreBuf / m_singleScoreBuf bytes
+static std::vector<char> s_info[3];
 static double s_isect_s = 0;  // seconds inside intersectLists10_r (list copies excluded)
 static double s_merge_s = 0;  // seconds inside RdbList::merge_r
 static double now_s();
@@ -149,7 +154,7 @@ static int ref_query(const orc_qterm *terms, const uint8_t *const *lists, const 
   req.m_doMaxScoreAlgo = p->do_max_score_algo != 0;
   req.m_maxSerpScore = p->max_serp_score;
   req.m_minSerpDocId = p->min_serp_docid;
-  req.m_getDocIdScoringInfo = false;
+  req.m_getDocIdScoringInfo = p->get_docid_scoring_info != 0;
   req.m_collnum = 0;
   req.ptr_termFreqWeights = (char *)tfw;
   req.size_termFreqWeights = 4 * nterms;
@@ -260,6 +265,11 @@ static int ref_query(const orc_qterm *terms, const uint8_t *const *lists, const 
     }
   }
   out->n = n;
+  for (int b = 0; b < 3; b++) s_info[b].clear();
+  if (p->get_docid_scoring_info && tab) {
+    SafeBuf *sb[3] = {&tab->m_scoreInfoBuf, &tab->m_pairScoreBuf, &tab->m_singleScoreBuf};
+    for (int b = 0; b < 3; b++) s_info[b].assign(sb[b]->getBufStart(), sb[b]->getBufStart() + sb[b]->length());
+  }
   if (vote_docids) {
     // m_docIdVoteBuf records: [b7&0xfc, b8..b11, vote] (Posdb.cpp:5281-5290)
     const uint8_t *v = (const uint8_t *)tab->m_docIdVoteBuf.getBufStart();
@@ -409,6 +419,12 @@ int main(int argc, char **argv) {
       wr(&nv, 8);
       wr(votes.data(), 8 * (size_t)nv);
       wr(&med, 8);
+      // score info buffers: DocIdScore[], PairScore[], SingleScore[] bytes
+      for (int b = 0; b < 3; b++) {
+        const int64_t nb = (int64_t)s_info[b].size();
+        wr(&nb, 8);
+        wr(s_info[b].data(), (size_t)nb);
+      }
     } else if (op == 2) {
       int32_t n, rm;
       int64_t mrs;

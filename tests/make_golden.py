@@ -35,7 +35,7 @@ def pack_lists(lists):
     return sizes, blob
 
 
-def save_query(name, terms, lists, params):
+def save_query(name, terms, lists, params, prefix="q"):
     white = getattr(params, "_white", None) if params.use_whitelist else None
     r = ref.query(terms, lists, params, votes=True, cap=1 << 16, white=white)
     if params.num_docid_splits > 1:
@@ -48,13 +48,19 @@ def save_query(name, terms, lists, params):
     tfw = np.array([t.tf_weight for t in terms], np.float32)
     pr = np.array([params.docs_to_get, params.real_max_top, params.language, params.site_clustering,
                    params.num_docid_splits, params.do_max_score_algo], np.int32)
-    np.savez_compressed(os.path.join(OUT, f"q_{name}.npz"), qterms=qt, tfw=tfw, params=pr,
+    extra = {}
+    if params.get_docid_scoring_info:
+        # the three SafeBufs of the second pass, as the reference left them
+        for k in ("score_info", "pair_scores", "single_scores"):
+            extra[k] = np.frombuffer(r[k], np.uint8)
+        extra["get_docid_scoring_info"] = np.int32(1)
+    np.savez_compressed(os.path.join(OUT, f"{prefix}_{name}.npz"), qterms=qt, tfw=tfw, params=pr,
                         same_lang_weight=np.float32(params.same_lang_weight),
                         max_serp_score=np.float64(params.max_serp_score),
                         min_serp_docid=np.int64(params.min_serp_docid), list_sizes=sizes, list_blob=blob,
                         docids=r["docids"], score_bits=r["scores"].view(np.uint32), hits=np.int64(r["hits"]),
                         filtered=np.int32(r["filtered"]), docs_wanted=np.int32(r["docs_wanted"]), votes=r["votes"],
-                        **white_arrays(params))
+                        **white_arrays(params), **extra)
     return r
 
 
@@ -86,6 +92,33 @@ def save_whitelist():
         p = q.params(**kw).with_whitelist(wl)
         r = save_query(f"white{j}_{q.name}", q.terms, lists, p)
         print(f"  white{j} {q.name}: sites={ns} hits={r['hits']} n={len(r['docids'])}")
+
+
+def save_scoreinfo():
+    """m_getDocIdScoringInfo's second pass (Posdb.cpp:6116-6244, 3247-3298,
+    4195-4280, 7554-7665): every query kind, plus realMaxTop / docsToGet
+    variants and a whitelist; the reference's DocIdScore / PairScore /
+    SingleScore buffers are kept byte for byte."""
+    from posdb_py import site_lists
+    N = 6000
+    ks = qkinds.kinds(N, seed=11)
+    for q in ks:
+        lists = generate(q, N, seed=5200)
+        p = q.params()
+        p.get_docid_scoring_info = 1
+        r = save_query(q.name, q.terms, lists, p, prefix="s")
+        print(f"  s_{q.name}: n={len(r['docids'])} info={len(r['score_info'])} pairs={len(r['pair_scores'])} "
+              f"singles={len(r['single_scores'])}")
+    for j, (kind, dtg, rmt) in enumerate(((1, 7, 3), (5, 12, 1), (8, 3, 10), (4, 40, 2))):
+        q = ks[kind]
+        q.docs_to_get = dtg
+        lists = generate(q, N, seed=5300 + j)
+        p = q.params(real_max_top=rmt)
+        p.get_docid_scoring_info = 1
+        if j == 3:
+            p = p.with_whitelist(site_lists(lists, 2, 0.5, seed=77))
+        r = save_query(f"v{j}_{q.name}", q.terms, lists, p, prefix="s")
+        print(f"  s_v{j}_{q.name}: n={len(r['docids'])} info={len(r['score_info'])}")
 
 
 def split_boundary_docids(n, seed, splits=(2, 5)):
@@ -257,6 +290,7 @@ def main():
     save_clustering()
     save_paging()
     save_whitelist()
+    save_scoreinfo()
     cases = [(0, -1), (1, -1), (0, 5000), (1, 5000), (0, 1)]
     for seed, (keys, nterms) in enumerate([(4000, 50), (12000, 3), (8000, 1)]):
         save_merge(f"tiered_s{seed}", tiered_runs(keys, seed=seed, nterms=nterms), cases)
@@ -273,5 +307,7 @@ if __name__ == "__main__":
         save_paging()
     elif sys.argv[1:] == ["whitelist"]:
         save_whitelist()
+    elif sys.argv[1:] == ["scoreinfo"]:
+        save_scoreinfo()
     else:
         main()

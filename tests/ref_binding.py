@@ -80,10 +80,15 @@ def query(terms, lists, params, cap=4096, votes=False, reps=1, white=None):
     (nv,) = struct.unpack("<q", _read(8))
     v = np.frombuffer(_read(8 * nv), np.int64).copy()
     (sec,) = struct.unpack("<d", _read(8))
+    info = []
+    for _ in range(3):  # m_scoreInfoBuf, m_pairScoreBuf, m_singleScoreBuf
+        (nb,) = struct.unpack("<q", _read(8))
+        info.append(_read(nb) if nb else b"")
     if r.corrupt < 0:
         raise RuntimeError(f"gbref query rc={-r.corrupt}")
     return dict(docids=d, scores=s, hits=r.hits, filtered=r.filtered, docs_wanted=r.docs_wanted,
-                corrupt=r.corrupt, votes=v, seconds=sec)
+                corrupt=r.corrupt, votes=v, seconds=sec, score_info=info[0], pair_scores=info[1],
+                single_scores=info[2])
 
 
 def posdb_merge(lists, remove_neg_keys, min_rec_sizes=-1, timed=False):
