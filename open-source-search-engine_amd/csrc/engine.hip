@@ -3702,6 +3702,25 @@ static void slot_released(gbgpu_ctx *ctx) {
 // its first record went (-1: none).  A docid the scorer rejects (minScore <=
 // 0, never a tree member) would append records without a DocIdScore, as
 // Posdb.cpp:7228-7230 jumps past the bookkeeping.
+// padding bytes of the three records, zeroed after the copy (struct stores
+// may leave them unspecified)
+static void zero_gap(void *rec, size_t from, size_t to) {
+  if (to > from) std::memset(static_cast<char *>(rec) + from, 0, to - from);
+}
+static void zero_pads(gbgpu_docid_score *d) {
+  zero_gap(d, offsetof(gbgpu_docid_score, site_rank) + 1, offsetof(gbgpu_docid_score, doc_lang));
+  zero_gap(d, offsetof(gbgpu_docid_score, singles_offset) + 4, offsetof(gbgpu_docid_score, pair_scores));
+}
+static void zero_pads(gbgpu_pair_score *p) {
+  zero_gap(p, offsetof(gbgpu_pair_score, fixed_distance) + 1, offsetof(gbgpu_pair_score, word_pos1));
+  zero_gap(p, offsetof(gbgpu_pair_score, word_pos2) + 4, offsetof(gbgpu_pair_score, term_freq1));
+  zero_gap(p, offsetof(gbgpu_pair_score, bflags2) + 1, offsetof(gbgpu_pair_score, qdist));
+}
+static void zero_pads(gbgpu_single_score *s) {
+  zero_gap(s, offsetof(gbgpu_single_score, hash_group) + 1, offsetof(gbgpu_single_score, word_pos));
+  zero_gap(s, offsetof(gbgpu_single_score, bflags) + 1, sizeof(gbgpu_single_score));
+}
+
 static int score_info(QuerySlot &q, const uint32_t *keys, const uint64_t *docs, uint32_t nsurv, gbgpu_result *out) {
   int n = 0;
   while (n < q.k && n < q.info_docs && keys[n]) n++;
@@ -3777,7 +3796,12 @@ static int score_info(QuerySlot &q, const uint32_t *keys, const uint64_t *docs, 
     if (room) {
       if (cs) std::memcpy(out->single_scores + ns, &hs[(size_t)t * scap], sizeof(gbgpu_single_score) * cs);
       if (cp) std::memcpy(out->pair_scores + np, &hp[(size_t)t * pcap], sizeof(gbgpu_pair_score) * cp);
-      if (info[t].ok) out->docid_scores[nd] = d;
+      for (int k = 0; k < cs; k++) zero_pads(out->single_scores + ns + k);
+      for (int k = 0; k < cp; k++) zero_pads(out->pair_scores + np + k);
+      if (info[t].ok) {
+        std::memcpy(out->docid_scores + nd, &d, sizeof d);
+        zero_pads(out->docid_scores + nd);
+      }
     }
     ns += cs;
     np += cp;

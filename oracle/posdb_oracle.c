@@ -1532,13 +1532,19 @@ static int run_range(const orc_qterm *qt, const uint8_t *const *lists, const int
       }
       /* A positive group whose mini-merged list came out empty (all of its
        * keys for this docid were BF_BIGRAM keys with syn bits, skipped at
-       * Posdb.cpp:6687-6692) makes the reference score stale mbuf bytes
-       * (undefined behaviour).  Defined here, as on the GPU: skip the docid. */
+       * Posdb.cpp:6687-6692) still has its first key read by every scorer
+       * (their loops test the end after a key).  When a later group wrote
+       * records, that key is the later group's first (groups are merged back
+       * to back), scored here as there.  When none did, the reference reads
+       * stale mbuf bytes of an earlier docid (undefined behaviour); defined
+       * here, as on the GPU: skip the docid. */
       {
-        int emptyGroup = 0;
-        for (int j = 0; j < nqti; j++)
-          if (mml[j] && mml[j] == mme[j]) emptyGroup = 1;
-        if (emptyGroup) continue;
+        int trailingEmpty = 0;
+        for (int j = 0; j < nqti; j++) {
+          if (!mml[j]) continue;
+          trailingEmpty = (mml[j] == mme[j]);
+        }
+        if (trailingEmpty) continue;
       }
 
       /* non-body pair scores, Posdb.cpp:6847-6926 */

@@ -286,6 +286,10 @@ def main():
     # undefined behaviour, DESIGN.md "Known divergences")
     save_query("empty_all", q.terms, [b"", b"", b""], q.params())
     save_query("empty_required", q.terms, [lists[0], b"", b""], q.params())
+    # the FIRST word's list empty: group 0 then holds only bigram keys, and a
+    # docid whose bigram keys all carry syn bits mini-merges it empty; its
+    # scorers read the key at that place, group 1's first key (defined)
+    save_query("empty_first_word", q.terms, [b"", lists[1], lists[2]], q.params())
     save_splits()
     save_clustering()
     save_paging()

@@ -137,17 +137,30 @@ def test_unsupported_modes_fail_loudly(engine):
     with pytest.raises(gbgpu.GbgpuError) as e:
         engine.query(terms, lists, p)
     assert e.value.code == gbgpu.GBGPU_EUNSUPPORTED
-    # the per-docid scoring-info second pass (m_getDocIdScoringInfo) stays on the CPU
-    p2 = q.params()
+    # the scoring-info second pass runs on the GPU except with site
+    # clustering / docid splits / paging (test_scoreinfo.py); resident lists
+    # take the same path
+    p2 = q.params(site_clustering=1)
     p2.get_docid_scoring_info = 1
     with pytest.raises(gbgpu.GbgpuError) as e:
         engine.query(q.terms, lists, p2)
     assert e.value.code == gbgpu.GBGPU_EUNSUPPORTED
+    p3 = q.params()
+    p3.get_docid_scoring_info = 1
     hs = [engine.upload(l) for l in lists]
     try:
-        with pytest.raises(gbgpu.GbgpuError) as e:
-            engine.query_resident(q.terms, hs, p2)
-        assert e.value.code == gbgpu.GBGPU_EUNSUPPORTED
+        try:
+            a = engine.query(q.terms, lists, p3)
+        except gbgpu.GbgpuError as e:  # a getWordPosList path not replayed
+            assert e.code == gbgpu.GBGPU_EUNSUPPORTED
+            with pytest.raises(gbgpu.GbgpuError):
+                engine.query_resident(q.terms, hs, p3)
+            return
+        b = engine.query_resident(q.terms, hs, p3)
+        assert len(a.docid_scores) == min(len(a.docids), p3.docs_to_get)
+        assert a.docid_scores.tobytes() == b.docid_scores.tobytes()
+        assert a.pair_scores.tobytes() == b.pair_scores.tobytes()
+        assert a.single_scores.tobytes() == b.single_scores.tobytes()
     finally:
         for h in hs:
             engine.free(h)

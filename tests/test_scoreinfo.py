@@ -106,6 +106,7 @@ def test_gpu_scoreinfo_declines_bounded(engine):
     """Runs after the parametrized cases: most fixtures are answered."""
     if len(DECLINED) == 0 and not SCASES:
         pytest.skip("no fixtures")
+    print("declined:", sorted(DECLINED))
     assert len(DECLINED) <= len(SCASES) // 2, sorted(DECLINED)
 
 
