@@ -52,7 +52,9 @@ typedef struct gbgpu_ctx gbgpu_ctx;
 typedef struct gbgpu_qterm {
   int32_t is_required;              /* m_isRequired                                  */
   int32_t term_sign;                /* m_termSign: '-' -> BF_NEGATIVE (Posdb.cpp:4570) */
-  int32_t field_code;               /* m_fieldCode: 0 only (numeric/facet: EUNSUPPORTED) */
+  int32_t field_code;               /* m_fieldCode: plain fields and gbsortby:/gbrevsortby:
+                                       float (54/55); range, int sortby, facets (56-57,
+                                       59-67): EUNSUPPORTED */
   int32_t piped;                    /* m_piped                                       */
   int32_t synonym_of;               /* index of m_synonymOf, -1 if none              */
   int32_t left_phrase_term;         /* m_leftPhraseTermNum, -1 if none               */

@@ -1335,6 +1335,8 @@ __device__ __forceinline__ void score_survivor(const DevPlan *pl, const Counters
   dv.present = 0;
   bool empty_pos = false;
   int siteRank = -1, docLang = 0;
+  uint64_t sortby_raw = 0;  // gbsortby: the unmerged first key (see below)
+  bool sortby_is_raw = false;
   uint32_t nrec = 0;
 #pragma unroll
   for (int j = 0; j < NQ; j++) {
@@ -1454,6 +1456,24 @@ __device__ __forceinline__ void score_survivor(const DevPlan *pl, const Counters
         else ck[x] = load6(src[x]);  // cu == 0 < c0 (a run has its own units)
       }
     }
+    // a numeric group with the docid in ONE sublist is not merged: its
+    // miniMergedList points into the termlist, keys unrewritten
+    // (Posdb.cpp:6638-6647); only gbsortby reads it (its first key's float)
+    if (j == pl->sortby_group) {
+      int nl = 0;
+      uint64_t rk = 0;
+      uint8_t f = 0;
+#pragma unroll
+      for (int x = 0; x < NS; x++)
+        if (live[x] && nl++ == 0) {
+          rk = ck[x];
+          f = cfl[x];
+        }
+      if (nl == 1 && (f & (BF_FACET | BF_NUMBER)) && !(f & (BF_SYNONYM | BF_HALFSTOPWIKIBIGRAM))) {
+        sortby_raw = rk;
+        sortby_is_raw = true;
+      }
+    }
     const uint32_t start = nrec;
     uint32_t mbytes = 0;  // emulates mptr - mbuf (cap 299000, Posdb.cpp:6007-6008)
     bool isFirstKey = true;
@@ -1553,6 +1573,10 @@ __device__ __forceinline__ void score_survivor(const DevPlan *pl, const Counters
   }
   const bool ok = !empty_pos && score_doc<NQ, RP, REC>(&c_weights, pl, dv, siteRank < 0 ? 0 : siteRank, docLang,
                                                        smcol, SCORE_TPB, &score, diag & 0xff, srec);
+  // gbsortby: the score is the float of the group's first key, bytes 2..5 as
+  // the mini-merge left them (Posdb.cpp:7265-7269)
+  if (ok && pl->sortby_group >= 0)
+    score = __uint_as_float((uint32_t)((sortby_is_raw ? sortby_raw : dv.rec[rget(dv.beg, pl->sortby_group)]) >> 16));
   if (so) {
     so->score = score;
     so->site_rank = siteRank < 0 ? 0 : siteRank;
@@ -2197,6 +2221,10 @@ __global__ void __launch_bounds__(64 * BND_WAVES) k_bound(const DevPlan *pl, con
   const float INF = __int_as_float(0x7f800000);
   for (uint32_t i = blockIdx.x * BND_WAVES + wid; i < nsurv; i += gridDim.x * BND_WAVES) {
     const uint32_t s = surv[i], lm = surv_lm[i];
+    if (pl->sortby_group >= 0) {  // gbsortby: both prefilters are skipped (Posdb.cpp:6050-6051, 6350)
+      if (lane == 0) sbound[i] = INF;
+      continue;
+    }
     // lane g: getMaxPossibleScore's scan of group g
     BoundCore core{0, 0.0f};
     if (lane < ng && !(pl->gflags0[lane] & (BF_NEGATIVE | BF_FACET)))
@@ -3141,7 +3169,7 @@ static int snapshot_lists(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms, 
   ents.resize(nterms);
   std::lock_guard<std::mutex> g(ctx->lists_mu);
   for (int i = 0; i < nterms; i++) {
-    if (terms[i].field_code) return GBGPU_EUNSUPPORTED;
+    if (field_unsupported(terms[i].field_code)) return GBGPU_EUNSUPPORTED;
     int32_t h = handles[i];
     if (h < 0 || h >= (int32_t)ctx->lists.size() || !ctx->lists[h].live) return EINVAL;
     ents[i] = ctx->lists[h];
@@ -3312,6 +3340,7 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
     P.nwhite = (uint32_t)q.h_white.size();
   }
   P.do_max_score = p->do_max_score_algo != 0;
+  P.sortby_group = hp.sortby_group;
   P.min_listi = hp.min_listi;
   P.all_same_wiki = 1;  // m_allInSameWikiPhrase, Posdb.cpp:5764-5778
   for (int j = 0; j < hp.ngroups; j++) {

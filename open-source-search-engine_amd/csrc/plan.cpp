@@ -48,6 +48,7 @@ int build_host_plan(const gbgpu_qterm *qt, int nqt, const int64_t *sizes, const 
   hp->min_listi = -1;
   hp->min_list_size = 0;
   hp->real_max_top = p->real_max_top > 10 ? 10 : p->real_max_top;
+  hp->sortby_group = -1;
   int nrg = 0;
   for (int i = 0; i < nqt; i++) {
     if (!qt[i].is_required) continue;
@@ -84,7 +85,11 @@ int build_host_plan(const gbgpu_qterm *qt, int nqt, const int64_t *sizes, const 
       for (int k = 0; k < nqt; k++)
         if (qt[k].synonym_of == right) ok &= add(k, BF_HALFSTOPWIKIBIGRAM | BF_SYNONYM | piped);
     }
-    ok &= add(i, (uint8_t)(piped | (qt[i].term_sign == '-' ? BF_NEGATIVE : 0)));
+    // numeric term lists carry a float where the word position is
+    // (Posdb.cpp:4572-4577); gbsortby: scores by it (4413-4417, 7265-7269)
+    const bool sortby = qt[i].field_code == FIELD_GBSORTBYFLOAT || qt[i].field_code == FIELD_GBREVSORTBYFLOAT;
+    if (sortby) hp->sortby_group = nrg;
+    ok &= add(i, (uint8_t)(piped | (qt[i].term_sign == '-' ? BF_NEGATIVE : 0) | (sortby ? BF_NUMBER : 0)));
     if (left >= 0 && !leftAdded) {
       ok &= add(left, piped | BF_BIGRAM);
       for (int k = 0; k < nqt; k++)

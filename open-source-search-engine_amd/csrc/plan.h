@@ -49,7 +49,30 @@ struct HostPlan {
   int64_t min_list_size = 0;
   int32_t docs_wanted = 0;
   int real_max_top = 10;
+  int sortby_group = -1;  // m_sortByTermInfoNum (gbsortby:/gbrevsortby: float, Posdb.cpp:4413-4417)
 };
+
+// Query::m_fieldCode values PosdbTable treats specially (Query.h:118-132);
+// every other field code is an ordinary term list to it
+enum : int32_t {
+  FIELD_GBSORTBYFLOAT = 54,
+  FIELD_GBREVSORTBYFLOAT = 55,
+  FIELD_GBNUMBERMIN = 56,
+  FIELD_GBNUMBERMAX = 57,
+  FIELD_GBSORTBYINT = 59,
+  FIELD_GBREVSORTBYINT = 60,
+  FIELD_GBNUMBERMININT = 61,
+  FIELD_GBNUMBERMAXINT = 62,
+  FIELD_GBFACETSTR = 63,
+  FIELD_GBFACETINT = 64,
+  FIELD_GBFACETFLOAT = 65,
+  FIELD_GBNUMBEREQUALINT = 66,
+  FIELD_GBNUMBEREQUALFLOAT = 67,
+};
+// a field code the GPU path does not implement (range, int sortby, facets)
+inline bool field_unsupported(int32_t fc) {
+  return fc >= FIELD_GBNUMBERMIN && fc <= FIELD_GBNUMBEREQUALFLOAT && fc != 58;  // 58: gbparenturl, a text field
+}
 
 // Device image.  Lists are addressed by a dense id 0..nlists-1.
 struct DevList {
@@ -102,6 +125,7 @@ struct DevPlan {
   float tfw[MAXG];
   int32_t qpos[MAXG], wiki[MAXG], quote[MAXG];
   int32_t qterm[MAXG];  // m_qtermNum (the second pass's score info)
+  int32_t sortby_group;  // gbsortby float: the group whose first key's float is the score (-1: none)
   // candidate arrays (sublists of m_minListi, distinct lists, in order)
   int g0n;
   int g0list[MAXG0];

@@ -121,6 +121,60 @@ def save_scoreinfo():
         print(f"  s_v{j}_{q.name}: n={len(r['docids'])} info={len(r['score_info'])}")
 
 
+def sortby_list(lists, frac, seed, termid=0x5A5A5A5A5A5, neg_frac=0.0):
+    """A numeric gbsortby: termlist (Posdb.cpp:4572-4577): one key per docid
+    for a `frac` share of the query's docids, a float where the word position
+    is (Posdb.h:213-219 setFloat: bytes 2..5), the rest of each key taken
+    from one of the docid's own keys."""
+    import struct
+    import posdb_py
+    rng = np.random.default_rng(seed)
+    first = {}
+    for l in lists:
+        for k in posdb_py.full_keys(l):
+            d = int.from_bytes(k[7:12], "little") >> 2
+            first.setdefault(d, k)
+    keys = []
+    for d in sorted(first):
+        if rng.random() >= frac:
+            continue
+        k = bytearray(first[d])
+        v = float(rng.integers(0, 400)) / 4.0 if rng.random() < 0.5 else float(rng.random() * 1000.0)
+        if rng.random() < neg_frac:
+            v = -v
+        k[2:6] = struct.pack("<f", v)
+        k[12:18] = termid.to_bytes(6, "little")
+        keys.append(bytes(k))
+    return posdb_py.encode_keys(keys)
+
+
+def save_sortby():
+    """gbsortby:/gbrevsortby: float terms (Posdb.cpp:4413-4417, 6050-6051,
+    6350, 7265-7269): the score is the float of the term's first key; plain
+    text field terms (title:, site: ...) are ordinary lists to PosdbTable."""
+    N = 6000
+    ks = qkinds.kinds(N, seed=13)
+    for j, (kind, fc, frac, neg, kw) in enumerate([(0, 54, 0.6, 0.0, {}), (1, 55, 0.4, 0.2, {}),
+                                                   (4, 54, 0.8, 0.0, {}), (0, 54, 0.5, 0.1, dict(site_clustering=1)),
+                                                   (7, 54, 0.7, 0.0, {})]):
+        q = ks[kind]
+        lists = generate(q, N, seed=5400 + j)
+        terms = list(q.terms)
+        qpos = max(t.qpos for t in terms) + 2
+        terms.append(gbgpu.QTerm(1, 0, fc, 0, -1, -1, -1, 0, qpos, 0, -1, 1.0))
+        lists = list(lists) + [sortby_list(lists, frac, seed=61 + j, neg_frac=neg)]
+        r = save_query(f"sortby{j}_{q.name}", terms, lists, q.params(**kw), prefix="f")
+        print(f"  f_sortby{j}_{q.name}: hits={r['hits']} n={len(r['docids'])} top={r['scores'][:3]}")
+    # a text field term (FIELD_TITLE = 6): nothing special to PosdbTable
+    q = ks[1]
+    lists = generate(q, N, seed=5500)
+    terms = list(q.terms)
+    terms[0] = gbgpu.QTerm(*[getattr(terms[0], f) for f, _ in gbgpu.QTerm._fields_])
+    terms[0].field_code = 6
+    r = save_query(f"field_title_{q.name}", terms, lists, q.params(), prefix="f")
+    print(f"  f_field_title: hits={r['hits']} n={len(r['docids'])}")
+
+
 def split_boundary_docids(n, seed, splits=(2, 5)):
     """n sorted distinct docids holding, for each piece boundary d1 of
     Msg39's docid-split loop (Msg39.cpp:362-373), d1-1 .. d1+3: d1..d1+2 are
@@ -295,6 +349,7 @@ def main():
     save_paging()
     save_whitelist()
     save_scoreinfo()
+    save_sortby()
     cases = [(0, -1), (1, -1), (0, 5000), (1, 5000), (0, 1)]
     for seed, (keys, nterms) in enumerate([(4000, 50), (12000, 3), (8000, 1)]):
         save_merge(f"tiered_s{seed}", tiered_runs(keys, seed=seed, nterms=nterms), cases)
@@ -313,5 +368,7 @@ if __name__ == "__main__":
         save_whitelist()
     elif sys.argv[1:] == ["scoreinfo"]:
         save_scoreinfo()
+    elif sys.argv[1:] == ["sortby"]:
+        save_sortby()
     else:
         main()

@@ -1,0 +1,61 @@
+"""Field terms (row f4): gbsortby:/gbrevsortby: float terms score a docid
+by the float its numeric termlist stores where the word position is
+(Posdb.cpp:4413-4417, 4572-4577, 6050-6051, 6350, 7265-7269), and plain
+text field terms (title:, site: ...) are ordinary lists to PosdbTable.
+Fixtures: tests/golden/f_*.npz, made by `python3 tests/make_golden.py
+sortby` from the reference harness (oracle/_ref/gbref).  The C oracle does
+not restate these modes: the fixtures are the only pin.  Range (gbmin:/
+gbmax:), int sortby and facet terms return GBGPU_EUNSUPPORTED."""
+import glob
+import os
+import struct
+
+import numpy as np
+import pytest
+
+import gbgpu
+from test_golden import check, load_query
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+FCASES = sorted(glob.glob(os.path.join(HERE, "golden", "f_*.npz")))
+IDS = [os.path.basename(p)[2:-4] for p in FCASES]
+
+
+def test_fixtures_present():
+    assert len(FCASES) >= 6
+
+
+@pytest.mark.parametrize("path", [p for p in FCASES if "sortby" in p],
+                         ids=[i for i in IDS if "sortby" in i])
+def test_sortby_scores_are_the_stored_floats(path):
+    """The reference's scores are the sortby keys' floats, unrewritten: a
+    numeric group found in one sublist is not mini-merged (Posdb.cpp:
+    6638-6647)."""
+    terms, lists, params, exp = load_query(path)
+    import posdb_py
+    floats = set()
+    for key in posdb_py.full_keys(lists[-1]):
+        floats.add(struct.unpack("<f", bytes(key[2:6]))[0])
+    assert all(float(s) in floats for s in exp["scores"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("path", FCASES, ids=IDS)
+def test_gpu_fields_vs_reference(engine, path):
+    terms, lists, params, exp = load_query(path)
+    r = engine.query(terms, lists, params, cap=1 << 16, hit_cap=max(1, exp["hits"]))
+    check(dict(docids=r.docids, scores=r.scores, hits=r.hits, docs_wanted=r.docs_wanted, filtered=r.filtered,
+               hit_docids=r.hit_docids), exp, os.path.basename(path))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fc", [56, 57, 59, 60, 61, 62, 63, 64, 65, 66, 67])
+def test_gpu_unsupported_field_codes(engine, fc):
+    terms, lists, params, _ = load_query(FCASES[0])
+    terms = list(terms)
+    last = gbgpu.QTerm(*[getattr(terms[-1], f) for f, _ in gbgpu.QTerm._fields_])
+    last.field_code = fc
+    terms[-1] = last
+    with pytest.raises(gbgpu.GbgpuError) as e:
+        engine.query(terms, lists, params)
+    assert e.value.code == gbgpu.GBGPU_EUNSUPPORTED
