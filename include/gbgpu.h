@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define GBGPU_ABI_VERSION 6
+#define GBGPU_ABI_VERSION 7
 
 /* error codes beyond errno.h (Errno.h numbering is not reused) */
 #define GBGPU_ENODEVICE   1001 /* no HIP device / extension not usable        */
@@ -52,9 +52,10 @@ typedef struct gbgpu_ctx gbgpu_ctx;
 typedef struct gbgpu_qterm {
   int32_t is_required;              /* m_isRequired                                  */
   int32_t term_sign;                /* m_termSign: '-' -> BF_NEGATIVE (Posdb.cpp:4570) */
-  int32_t field_code;               /* m_fieldCode: plain fields and gbsortby:/gbrevsortby:
-                                       float (54/55); range, int sortby, facets (56-57,
-                                       59-67): EUNSUPPORTED */
+  int32_t field_code;               /* m_fieldCode: plain fields, gbsortby:/gbrevsortby:
+                                       float (54/55), range terms gbmin:/gbmax:/gbequal:
+                                       (56-57, 61-62, 66-67; own list only, positive);
+                                       int sortby and facets (59-60, 63-65): EUNSUPPORTED */
   int32_t piped;                    /* m_piped                                       */
   int32_t synonym_of;               /* index of m_synonymOf, -1 if none              */
   int32_t left_phrase_term;         /* m_leftPhraseTermNum, -1 if none               */
@@ -64,6 +65,9 @@ typedef struct gbgpu_qterm {
   int32_t wiki_phrase_id;           /* m_qword->m_wikiPhraseId                       */
   int32_t quote_start;              /* m_qword->m_quoteStart, -1 if none             */
   float   tf_weight;                /* ptr_termFreqWeights[i]                        */
+  float    number_float;            /* m_qword->m_float: gbmin:/gbmax:/gbequal: float bound  */
+  int32_t  number_int;              /* m_qword->m_int: the int range terms' bound (56-57, 61-62,
+                                       66-67 filter votes by the key's number, Posdb.cpp:4948-4999) */
 } gbgpu_qterm;
 
 /* A posdb termlist exactly as Msg2::getList(i) holds it: first key 18 bytes,

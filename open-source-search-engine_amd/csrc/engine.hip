@@ -279,6 +279,39 @@ __global__ void __launch_bounds__(1024) k_scan_runs(uint32_t nchunks, uint32_t *
   }
 }
 
+// Range terms (gbmin:/gbmax:/gbequal:, Posdb.cpp:4948-4999): isInRange on
+// one key, the number where the word position is (bytes 2..5 as float or int)
+__device__ __forceinline__ bool in_range_key(const DevList &L, gu8 *k) {
+  const uint32_t v = (uint32_t)k[2] | ((uint32_t)k[3] << 8) | ((uint32_t)k[4] << 16) | ((uint32_t)k[5] << 24);
+  if (L.rint) {
+    const int32_t x = (int32_t)v;
+    return L.rmode == 1 ? x >= L.ri : L.rmode == 2 ? x <= L.ri : x == L.ri;
+  }
+  const float x = __uint_as_float(v);
+  return L.rmode == 1 ? x >= L.rf : L.rmode == 2 ? x <= L.rf : x == L.rf;
+}
+// isInRange2 at a run head u, run [u, e): the head, then its 6-byte keys
+__device__ bool run_in_range(const DevList &L, uint32_t u, uint32_t e) {
+  gu8 *p = gl(L.p);
+  if (in_range_key(L, p + (size_t)u * 6)) return true;
+  for (uint32_t x = u + 2; x < e; x++)
+    if (in_range_key(L, p + (size_t)x * 6)) return true;
+  return false;
+}
+// addDocIdVotes' first-group test (Posdb.cpp:5249-5277): isInRange2 at the
+// head and again at every 6-byte key.  From the run's last 6-byte key that
+// skips 12 bytes -- onto the next run's second unit -- and goes on over
+// units with the 6-byte bit, so the next run's keys can count too.
+__device__ bool run_in_range_first(const DevList &L, uint32_t u, uint32_t e) {
+  if (run_in_range(L, u, e)) return true;
+  if (e - u > 2) {
+    gu8 *p = gl(L.p);
+    for (uint32_t x = e + 1; x < L.units && (p[(size_t)x * 6] & 0x04); x++)
+      if (in_range_key(L, p + (size_t)x * 6)) return true;
+  }
+  return false;
+}
+
 // Writes every candidate slot of every array (docid; list mask = the array's
 // own list bit for array 0, which is never probed, else 0 -- so no per-query
 // clear of the mask is needed) and array 0's run locations.
@@ -330,6 +363,7 @@ __global__ void __launch_bounds__(BLOCK) k_write_runs(const DevPlan *pl, const G
     // bucket straddling two chunks gets two writers; either names it)
     const uint64_t bkt = (d - dmin) >> sh;
     if (o2 == 0 || ((unit_docid(lds + rs_unit[o2 - 1] * 6) - dmin) >> sh) != bkt) dir_a[bkt] = tag | p2;
+    bool rej = false;
     if (pl->use_white) {
       // Posdb.cpp:5294: the 5 bytes at minRecPtr+7 (the run head's docid
       // bytes, siteRank's top bit included) must be in the whitelist table
@@ -342,7 +376,7 @@ __global__ void __launch_bounds__(BLOCK) k_write_runs(const DevPlan *pl, const G
         if (pl->white[m] < x) lo = m + 1;
         else hi = m;
       }
-      pl->wrej[slot] = !(lo < pl->nwhite && pl->white[lo] == x);
+      rej = !(lo < pl->nwhite && pl->white[lo] == x);
     }
     lmask[slot] = own ? own_bit : 0u;
     uint32_t ul = 0;
@@ -351,7 +385,9 @@ __global__ void __launch_bounds__(BLOCK) k_write_runs(const DevPlan *pl, const G
       const uint32_t e = (o2 + 1 < tot) ? c.u0 + rs_unit[o2 + 1] : run_end(L, u + 2);
       loc_l[slot] = Loc{u, e - u};
       ul = (e - u) * own_mult;
+      if (L.rmode && !run_in_range_first(L, u, e)) rej = true;  // Posdb.cpp:5249-5277, 5297
     }
+    if (pl->use_rej) pl->wrej[slot] = rej;
     ulen[slot] = ul;
   }
   // the last chunk of each array publishes the array's count
@@ -513,6 +549,7 @@ struct ProbeOut {
   uint32_t *ulen;
   Loc *loc_l;
   uint32_t bit, mult;
+  const DevList *rl;  // the list, when it is a range term's (else nullptr)
 };
 
 // append up to 64 matches (one per lane), wave-wide
@@ -532,11 +569,13 @@ __device__ __forceinline__ void mbuf_push(ProbeLds &S, uint32_t &nbuf, bool hit,
 // (out of line, with every argument by value: a by-reference counter would
 // live in scratch, and scratch loads wait on vmcnt like any global load)
 __device__ __noinline__ void mbuf_flush_n(ProbeLds *S, uint32_t nbuf, uint32_t *lmask, uint32_t *ulen, Loc *loc_l,
-                                          uint32_t bit, uint32_t mult, int lane) {
+                                          uint32_t bit, uint32_t mult, int lane, const DevList *rl) {
   wave_lds_sync();
   if (!bit) nbuf = 0;  // diagnostic (GBGPU_PROBE_MODE=5): matches not published
   for (uint32_t i = lane; i < nbuf; i += 64) {
     const uint32_t slot = S->mslot[i], len = S->mlen[i];
+    // a range term's run votes only in range (Posdb.cpp:5115-5121)
+    if (rl && !run_in_range(*rl, S->mu[i], S->mu[i] + len)) continue;
     loc_l[slot] = Loc{S->mu[i], len};
     if (mult) atomicAdd(&ulen[slot], len * mult);
     atomicOr(&lmask[slot], bit);
@@ -544,7 +583,7 @@ __device__ __noinline__ void mbuf_flush_n(ProbeLds *S, uint32_t nbuf, uint32_t *
   wave_lds_sync();
 }
 __device__ __forceinline__ void mbuf_flush(ProbeLds &S, uint32_t &nbuf, const ProbeOut &o, int lane) {
-  mbuf_flush_n(&S, nbuf, o.lmask, o.ulen, o.loc_l, o.bit, o.mult, lane);
+  mbuf_flush_n(&S, nbuf, o.lmask, o.ulen, o.loc_l, o.bit, o.mult, lane, o.rl);
   nbuf = 0;
 }
 
@@ -868,6 +907,7 @@ __global__ void __launch_bounds__(64 * PW) k_probe(const DevPlan *pl, const Prob
   // arena units this list adds per matched run: one copy per positive group
   // it belongs to (a shared bigram sublist is merged into both groups)
   po.mult = __popc(L.group_bits & pl->pos_mask & ~NEG_BIT);
+  po.rl = L.rmode ? &L : nullptr;
   if (L.probe == PROBE_BY_RUN) {
     if (MODE == 0) probe_by_run<G0>(pl, w, L, cand, ctr, dir, s_lds[wid], po, lane);
   } else {
@@ -972,7 +1012,7 @@ __global__ void __launch_bounds__(CBLOCK) k_compact(const DevPlan *pl, const uin
     int k = 0;
     while (k + 1 < g0n && s >= s_beg[k + 1]) k++;
     if (s >= s_end[k]) continue;
-    if (pl->use_white && pl->wrej[s]) continue;  // not voted (Posdb.cpp:5294)
+    if (pl->use_rej && pl->wrej[s]) continue;  // not voted (Posdb.cpp:5294, 5297)
     const uint32_t lm = lmv[q];
     uint32_t gm = 0;
     for (uint32_t x = lm; x; x &= x - 1) gm |= s_gbits[__ffs(x) - 1];
@@ -1095,7 +1135,7 @@ __global__ void __launch_bounds__(CBLOCK) k_compact(const DevPlan *pl, const uin
 // survivor would copy a misparsed run -- not emulated, flagged instead
 // (GBGPU_EUNSUPPORTED; about 2^-20 per query).  One wave per list.
 __device__ bool slot_is_survivor(const DevPlan *pl, const uint32_t *lmask, uint64_t s) {
-  if (pl->use_white && pl->wrej[s]) return false;
+  if (pl->use_rej && pl->wrej[s]) return false;
   uint32_t gm = 0;
   for (uint32_t x = lmask[s]; x; x &= x - 1) gm |= pl->lists[__ffs(x) - 1].group_bits;
   return ((gm & pl->pos_mask) == pl->pos_mask) && !(gm & NEG_BIT);
@@ -3368,6 +3408,7 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
     P.lists[id].owner_group = -1;
     P.lists[id].owner_sub = -1;
     P.lists[id].uses = 0;
+    P.lists[id].rmode = 0;
     return id;
   };
   for (int j = 0; j < hp.ngroups; j++) {
@@ -3380,6 +3421,13 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
     P.wiki[j] = g.wiki;
     P.quote[j] = g.quote;
     P.qterm[j] = g.qterm;
+    int rint = 0;
+    const int rmode = range_mode(terms[g.qterm].field_code, &rint);
+    if (rmode) {
+      // a range term's group: its own list only (no synonyms / bigrams), voted
+      // by the keys' numbers (Posdb.cpp:5056-5073, 5115-5121, 5242-5298)
+      if (g.nsub != 1 || g.sub_term[0] != g.qterm || (g.flags[0] & BF_NEGATIVE)) return GBGPU_EUNSUPPORTED;
+    }
     for (int x = 0; x < MAXSUB; x++) P.gsubflags[j][x] = x < 50 ? g.flags[x] : 0;
     const bool neg = (g.flags[0] & BF_NEGATIVE) != 0;
     if (!neg) P.pos_mask |= 1u << j;
@@ -3387,6 +3435,13 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
       int id = dense_id(g.sub_term[x]);
       if (id < 0) return GBGPU_EUNSUPPORTED;
       P.gsub[j][x] = (uint8_t)id;
+      if (rmode) {
+        if (P.lists[id].uses) return GBGPU_EUNSUPPORTED;  // shared with another group
+        P.lists[id].rmode = rmode;
+        P.lists[id].rint = rint;
+        P.lists[id].rf = terms[g.qterm].number_float;
+        P.lists[id].ri = terms[g.qterm].number_int;
+      }
       P.lists[id].group_bits |= neg ? NEG_BIT : (1u << j);
       if (!neg) {
         // shrinkSubLists' in-place order: groups in index order, sublists in
@@ -3416,6 +3471,11 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   }
   P.g0base[P.g0n] = slot;
   const uint64_t slot_ub = slot;
+  // slots k_write_runs may reject: the whitelist, or a range term in the
+  // smallest group (its first-group vote test)
+  P.use_rej = P.use_white;
+  for (int a = 0; a < P.g0n; a++)
+    if (P.lists[P.g0list[a]].rmode) P.use_rej = 1;
   if (slot_ub >= (1ull << 28)) return GBGPU_ECAPACITY;  // k_compact's packed bump pointer
   q.slot_ub = slot_ub;
   // directories: about 8 units (2-4 docids) per bucket, power-of-two count
@@ -3517,16 +3577,14 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
     if (P.g0n > 1) rc2 |= q.order.ensure(4 * slot_ub);
     if (!(tree_phase & TREE_FINAL)) rc2 |= q.tree.ensure(sizeof(TreeState));
   }
-  if (P.use_white) {
-    rc2 |= q.white.ensure(8 * std::max<size_t>(1, q.h_white.size()));
-    rc2 |= q.wrej.ensure(slot_ub);
-  }
+  if (P.use_white) rc2 |= q.white.ensure(8 * std::max<size_t>(1, q.h_white.size()));
+  if (P.use_rej) rc2 |= q.wrej.ensure(slot_ub);
   const void *dir_before = q.dir.p;
   rc2 |= q.dir.ensure(8 * std::max<uint64_t>(1, dir_entries));
   if (rc2) return ENOMEM;
+  if (P.use_rej) P.wrej = q.wrej.as<uint8_t>();
   if (P.use_white) {
     P.white = q.white.as<uint64_t>();
-    P.wrej = q.wrej.as<uint8_t>();
     if (!q.h_white.empty())
       HIPCHECK(hipMemcpyAsync(q.white.p, q.h_white.data(), 8 * q.h_white.size(), hipMemcpyHostToDevice, q.stream));
   }

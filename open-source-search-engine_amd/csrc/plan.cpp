@@ -88,8 +88,10 @@ int build_host_plan(const gbgpu_qterm *qt, int nqt, const int64_t *sizes, const 
     // numeric term lists carry a float where the word position is
     // (Posdb.cpp:4572-4577); gbsortby: scores by it (4413-4417, 7265-7269)
     const bool sortby = qt[i].field_code == FIELD_GBSORTBYFLOAT || qt[i].field_code == FIELD_GBREVSORTBYFLOAT;
+    int rint;
+    const bool number = sortby || range_mode(qt[i].field_code, &rint) != 0;
     if (sortby) hp->sortby_group = nrg;
-    ok &= add(i, (uint8_t)(piped | (qt[i].term_sign == '-' ? BF_NEGATIVE : 0) | (sortby ? BF_NUMBER : 0)));
+    ok &= add(i, (uint8_t)(piped | (qt[i].term_sign == '-' ? BF_NEGATIVE : 0) | (number ? BF_NUMBER : 0)));
     if (left >= 0 && !leftAdded) {
       ok &= add(left, piped | BF_BIGRAM);
       for (int k = 0; k < nqt; k++)

@@ -71,7 +71,16 @@ enum : int32_t {
 };
 // a field code the GPU path does not implement (range, int sortby, facets)
 inline bool field_unsupported(int32_t fc) {
-  return fc >= FIELD_GBNUMBERMIN && fc <= FIELD_GBNUMBEREQUALFLOAT && fc != 58;  // 58: gbparenturl, a text field
+  return fc == FIELD_GBSORTBYINT || fc == FIELD_GBREVSORTBYINT ||
+         (fc >= FIELD_GBFACETSTR && fc <= FIELD_GBFACETFLOAT);
+}
+// range terms: (mode, int?) of a field code, mode 0 if not one
+inline int range_mode(int32_t fc, int *is_int) {
+  *is_int = fc == FIELD_GBNUMBERMININT || fc == FIELD_GBNUMBERMAXINT || fc == FIELD_GBNUMBEREQUALINT;
+  if (fc == FIELD_GBNUMBERMIN || fc == FIELD_GBNUMBERMININT) return 1;
+  if (fc == FIELD_GBNUMBERMAX || fc == FIELD_GBNUMBERMAXINT) return 2;
+  if (fc == FIELD_GBNUMBEREQUALFLOAT || fc == FIELD_GBNUMBEREQUALINT) return 3;
+  return 0;
 }
 
 // Device image.  Lists are addressed by a dense id 0..nlists-1.
@@ -86,6 +95,12 @@ struct DevList {
   // owner_sub) sees it clean, every later one sees the re-shrunk buffer
   int16_t owner_group, owner_sub;
   int32_t uses;         // positive group sublist positions naming this list
+  // range term (gbmin:/gbmax:/gbequal:, Posdb.cpp:4948-4999): a docid is voted
+  // by this list only if a key of its run holds a number in range
+  int32_t rmode;        // 0 none, 1 min (>=), 2 max (<=), 3 equal
+  int32_t rint;         // compare getInt (1) or getFloat (0)
+  float rf;             // m_qword->m_float
+  int32_t ri;           // m_qword->m_int
 };
 constexpr int32_t PROBE_BY_CAND = 1;  // dense list: candidates search the chunk's run starts
 constexpr int32_t PROBE_BY_RUN = 2;   // sparse list: run starts look up the candidate directory
@@ -108,6 +123,7 @@ struct DevPlan {
   // group-0 candidate whose run head is not among them is rejected
   // (k_write_runs writes wrej[slot], k_compact skips it)
   int use_white;
+  int use_rej;          // wrej[] marks slots not voted (whitelist or a range term's first group)
   uint32_t nwhite;
   const uint64_t *white;
   uint8_t *wrej;

@@ -41,6 +41,8 @@ class QTerm(ctypes.Structure):
         ("wiki_phrase_id", ctypes.c_int32),
         ("quote_start", ctypes.c_int32),
         ("tf_weight", ctypes.c_float),
+        ("number_float", ctypes.c_float),  # m_qword->m_float (range terms)
+        ("number_int", ctypes.c_int32),    # m_qword->m_int
     ]
 
 

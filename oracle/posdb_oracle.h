@@ -34,6 +34,8 @@ typedef struct orc_qterm {
   int32_t wiki_phrase_id;           /* m_qword->m_wikiPhraseId                 */
   int32_t quote_start;              /* m_qword->m_quoteStart (-1 none)         */
   float   tf_weight;                /* Msg39Request::ptr_termFreqWeights[i]    */
+  float   number_float;             /* m_qword->m_float (range terms; gbref only) */
+  int32_t number_int;               /* m_qword->m_int                          */
 } orc_qterm;
 
 /* same layout as gbgpu_params (include/gbgpu.h) */

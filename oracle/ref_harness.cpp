@@ -122,6 +122,8 @@ static int ref_query(const orc_qterm *terms, const uint8_t *const *lists, const 
     qw->m_posNum = t.qpos;
     qw->m_wikiPhraseId = t.wiki_phrase_id;
     qw->m_quoteStart = t.quote_start;
+    qw->m_float = t.number_float;  // gbmin:/gbmax:/gbequal: bounds (Posdb.cpp:4948-4979)
+    qw->m_int = t.number_int;
     qt->m_qword = qw;
     qt->m_isRequired = t.is_required != 0;
     qt->m_termSign = (char)t.term_sign;

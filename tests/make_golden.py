@@ -46,6 +46,11 @@ def save_query(name, terms, lists, params, prefix="q"):
     sizes, blob = pack_lists(lists)
     qt = np.array([[getattr(t, f) for f in QFIELDS] for t in terms], np.int32).reshape(len(terms), len(QFIELDS))
     tfw = np.array([t.tf_weight for t in terms], np.float32)
+    if any(t.number_float or t.number_int for t in terms):
+        extra_num = dict(qnum_f=np.array([t.number_float for t in terms], np.float32),
+                         qnum_i=np.array([t.number_int for t in terms], np.int32))
+    else:
+        extra_num = {}
     pr = np.array([params.docs_to_get, params.real_max_top, params.language, params.site_clustering,
                    params.num_docid_splits, params.do_max_score_algo], np.int32)
     extra = {}
@@ -60,7 +65,7 @@ def save_query(name, terms, lists, params, prefix="q"):
                         min_serp_docid=np.int64(params.min_serp_docid), list_sizes=sizes, list_blob=blob,
                         docids=r["docids"], score_bits=r["scores"].view(np.uint32), hits=np.int64(r["hits"]),
                         filtered=np.int32(r["filtered"]), docs_wanted=np.int32(r["docs_wanted"]), votes=r["votes"],
-                        **white_arrays(params), **extra)
+                        **white_arrays(params), **extra, **extra_num)
     return r
 
 
@@ -146,6 +151,59 @@ def sortby_list(lists, frac, seed, termid=0x5A5A5A5A5A5, neg_frac=0.0):
         k[12:18] = termid.to_bytes(6, "little")
         keys.append(bytes(k))
     return posdb_py.encode_keys(keys)
+
+
+def number_list(lists, frac, seed, termid=0x3C3C3C3C3C3, kmax=1, ints=False):
+    """A numeric termlist of 1..kmax keys per docid for a `frac` share of
+    the query's docids: a float (or int32) in bytes 2..5 of each key."""
+    import struct
+    import posdb_py
+    rng = np.random.default_rng(seed)
+    first = {}
+    for l in lists:
+        for k in posdb_py.full_keys(l):
+            first.setdefault(int.from_bytes(k[7:12], "little") >> 2, k)
+    keys = []
+    for d in sorted(first):
+        if rng.random() >= frac:
+            continue
+        vals = set()
+        for _ in range(int(rng.integers(1, kmax + 1))):
+            vals.add(struct.pack("<i", int(rng.integers(-20, 200))) if ints else
+                     struct.pack("<f", float(rng.integers(0, 400)) / 4.0))
+        run = []
+        for v in vals:
+            k = bytearray(first[d])
+            k[2:6] = v
+            k[12:18] = termid.to_bytes(6, "little")
+            run.append(bytes(k))
+        keys += sorted(run, key=lambda k: int.from_bytes(k[0:6], "little"))
+    return posdb_py.encode_keys(keys)
+
+
+def save_range():
+    """gbmin:/gbmax:/gbequal: float and int terms (Posdb.cpp:4948-4999,
+    5056-5121, 5242-5298): a docid is voted only if a key of its run holds a
+    number in range; in the smallest group the test also reads on past the
+    run from its last 6-byte key.  The bounds travel in the qterms'
+    number_float / number_int (m_qword->m_float / m_int)."""
+    N = 6000
+    ks = qkinds.kinds(N, seed=17)
+    cases = [(0, 56, 50.0, 0, 0.3, 4, False), (0, 57, 25.0, 0, 0.95, 8, False), (1, 61, 0.0, 100, 0.5, 3, True),
+             (4, 62, 0.0, 50, 0.9, 6, True), (0, 67, 12.5, 0, 0.9, 6, False), (0, 66, 0.0, 7, 0.9, 6, True),
+             (7, 56, 80.0, 0, 0.5, 5, False), (2, 57, 60.0, 0, 0.7, 3, False)]
+    for j, (kind, fc, vf, vi, frac, kmax, ints) in enumerate(cases):
+        q = ks[kind]
+        lists = generate(q, N, seed=5600 + j)
+        terms = list(q.terms)
+        qpos = max(t.qpos for t in terms) + 2
+        t = gbgpu.QTerm(1, 0, fc, 0, -1, -1, -1, 0, qpos, 0, -1, 1.0)
+        t.number_float = vf
+        t.number_int = vi
+        terms.append(t)
+        lists = list(lists) + [number_list(lists, frac, seed=71 + j, kmax=kmax, ints=ints)]
+        r = save_query(f"range{j}_{q.name}", terms, lists, q.params(), prefix="f")
+        print(f"  f_range{j}_{q.name}: fc={fc} hits={r['hits']} n={len(r['docids'])} sizes={[len(l) for l in lists]}")
 
 
 def save_sortby():
@@ -350,6 +408,7 @@ def main():
     save_whitelist()
     save_scoreinfo()
     save_sortby()
+    save_range()
     cases = [(0, -1), (1, -1), (0, 5000), (1, 5000), (0, 1)]
     for seed, (keys, nterms) in enumerate([(4000, 50), (12000, 3), (8000, 1)]):
         save_merge(f"tiered_s{seed}", tiered_runs(keys, seed=seed, nterms=nterms), cases)
@@ -370,5 +429,7 @@ if __name__ == "__main__":
         save_scoreinfo()
     elif sys.argv[1:] == ["sortby"]:
         save_sortby()
+    elif sys.argv[1:] == ["range"]:
+        save_range()
     else:
         main()

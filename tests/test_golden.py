@@ -32,6 +32,9 @@ def split_blob(sizes, blob):
 def load_query(path):
     z = np.load(path, allow_pickle=False)
     terms = [gbgpu.QTerm(*[int(x) for x in row], float(w)) for row, w in zip(z["qterms"], z["tfw"])]
+    if "qnum_f" in z:  # range terms' bounds (m_qword->m_float / m_int)
+        for t, f, i in zip(terms, z["qnum_f"], z["qnum_i"]):
+            t.number_float, t.number_int = float(f), int(i)
     pr = z["params"]
     # the harness ran Msg39Request::reset() (m_doMaxScoreAlgo = true) before
     # the fields a fixture names
