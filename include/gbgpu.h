@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define GBGPU_ABI_VERSION 7
+#define GBGPU_ABI_VERSION 8
 
 /* error codes beyond errno.h (Errno.h numbering is not reused) */
 #define GBGPU_ENODEVICE   1001 /* no HIP device / extension not usable        */
@@ -54,8 +54,9 @@ typedef struct gbgpu_qterm {
   int32_t term_sign;                /* m_termSign: '-' -> BF_NEGATIVE (Posdb.cpp:4570) */
   int32_t field_code;               /* m_fieldCode: plain fields, gbsortby:/gbrevsortby:
                                        float (54/55), range terms gbmin:/gbmax:/gbequal:
-                                       (56-57, 61-62, 66-67; own list only, positive);
-                                       int sortby and facets (59-60, 63-65): EUNSUPPORTED */
+                                       (56-57, 61-62, 66-67; own list only, positive),
+                                       gbsortby: int (59/60: gbgpu_result::int_scores);
+                                       facets (63-65): EUNSUPPORTED */
   int32_t piped;                    /* m_piped                                       */
   int32_t synonym_of;               /* index of m_synonymOf, -1 if none              */
   int32_t left_phrase_term;         /* m_leftPhraseTermNum, -1 if none               */
@@ -184,6 +185,10 @@ typedef struct gbgpu_result {
   gbgpu_docid_score  *docid_scores;  int32_t docid_scores_cap;  int32_t n_docid_scores;
   gbgpu_pair_score   *pair_scores;   int32_t pair_scores_cap;   int32_t n_pair_scores;
   gbgpu_single_score *single_scores; int32_t single_scores_cap; int32_t n_single_scores;
+  /* optional, `capacity` entries: TopNode::m_intScore when a gbsortby int
+   * term makes the tree use integer scores (scores[] are then 0.0, as the
+   * reference's m_score); 0 otherwise.  NULL to skip. */
+  int32_t *int_scores;
 } gbgpu_result;
 
 int         gbgpu_open(int device, gbgpu_ctx **out);

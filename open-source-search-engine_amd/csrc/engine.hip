@@ -1615,8 +1615,12 @@ __device__ __forceinline__ void score_survivor(const DevPlan *pl, const Counters
                                                        smcol, SCORE_TPB, &score, diag & 0xff, srec);
   // gbsortby: the score is the float of the group's first key, bytes 2..5 as
   // the mini-merge left them (Posdb.cpp:7265-7269)
-  if (ok && pl->sortby_group >= 0)
-    score = __uint_as_float((uint32_t)((sortby_is_raw ? sortby_raw : dv.rec[rget(dv.beg, pl->sortby_group)]) >> 16));
+  uint32_t ival = 0;  // gbsortby int: m_intScore's bits
+  if (ok && pl->sortby_group >= 0) {
+    const uint32_t v = (uint32_t)((sortby_is_raw ? sortby_raw : dv.rec[rget(dv.beg, pl->sortby_group)]) >> 16);
+    if (pl->sortby_int) ival = v;  // getInt (Posdb.cpp:7271-7279)
+    else score = __uint_as_float(v);
+  }
   if (so) {
     so->score = score;
     so->site_rank = siteRank < 0 ? 0 : siteRank;
@@ -1627,6 +1631,7 @@ __device__ __forceinline__ void score_survivor(const DevPlan *pl, const Counters
   if (ok) {
     const uint32_t b = __float_as_uint(score);
     key = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+    if (pl->sortby_group >= 0 && pl->sortby_int) key = ival ^ 0x80000000u;  // int32 order
     if (key == 0) key = 1;
   }
   *key_out = key;
@@ -3068,6 +3073,7 @@ struct QuerySlot {
   size_t res_bytes = 0;
   int32_t docs_wanted = 0;
   bool want_info = false;   // m_getDocIdScoringInfo
+  bool int_scores = false;  // gbsortby int: keys are m_intScore, TopNode::m_score 0
   int info_docs = 0;        // m_docsToGet: the second pass's docid limit
   int info_ng = 0;          // m_numQueryTermInfos
   int info_scap = 0, info_pcap = 0;  // singles / pairs one docid can record
@@ -3337,6 +3343,7 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   q.scan_bytes = 0;
   q.replayed = false;
   q.want_info = p->get_docid_scoring_info != 0;
+  q.int_scores = false;
   q.info_docs = p->docs_to_get;
   q.info_ng = hp.ngroups;
   q.info_scap = hp.ngroups * hp.real_max_top;
@@ -3381,6 +3388,13 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   }
   P.do_max_score = p->do_max_score_algo != 0;
   P.sortby_group = hp.sortby_group;
+  P.sortby_int = hp.sortby_int;
+  q.int_scores = hp.sortby_int != 0;
+  // integer TopTree scores: with the domain-cap tree, the paging filter or
+  // the score info they take other reference paths (TopTree.cpp:332-333,
+  // Posdb.cpp:7330-7336, 7559-7560): not on the GPU
+  if (hp.sortby_int && (clus || P.has_serp || p->get_docid_scoring_info || p->num_docid_splits > 1))
+    return GBGPU_EUNSUPPORTED;
   P.min_listi = hp.min_listi;
   P.all_same_wiki = 1;  // m_allInSameWikiPhrase, Posdb.cpp:5764-5778
   for (int j = 0; j < hp.ngroups; j++) {
@@ -3974,8 +3988,10 @@ static int collect(gbgpu_ctx *ctx, QuerySlot &q, gbgpu_result *out, std::vector<
     const uint32_t b = (key & 0x80000000u) ? (key & 0x7fffffffu) : ~key;
     float f;
     std::memcpy(&f, &b, 4);
+    if (q.int_scores) f = 0.0f;  // TopNode::m_score with integer scores (Posdb.cpp:7680-7683)
     if (out->docids) out->docids[n] = (int64_t)docs[i];
     if (out->scores) out->scores[n] = f;
+    if (out->int_scores) out->int_scores[n] = q.int_scores ? (int32_t)(key ^ 0x80000000u) : 0;
     n++;
   }
   out->n = n;
@@ -4522,6 +4538,7 @@ int gbgpu_allgather_topk(gbgpu_ctx *ctx, int slot, int32_t k, int64_t *docids, d
   if (!ctx->comm) return EINVAL;
   std::unique_lock<std::mutex> lk(q->mu);
   if (!q->pending) return EINVAL;
+  if (q->int_scores) return GBGPU_EUNSUPPORTED;  // Msg3a merges double scores; int ones not emulated
   (void)hipSetDevice(ctx->device);
   const size_t stride = align256(sizeof(XHead) + sizeof(XRec) * (size_t)k);
   const size_t out_bytes = sizeof(XHead) + 16 * (size_t)k;

@@ -49,6 +49,7 @@ int build_host_plan(const gbgpu_qterm *qt, int nqt, const int64_t *sizes, const 
   hp->min_list_size = 0;
   hp->real_max_top = p->real_max_top > 10 ? 10 : p->real_max_top;
   hp->sortby_group = -1;
+  hp->sortby_int = 0;
   int nrg = 0;
   for (int i = 0; i < nqt; i++) {
     if (!qt[i].is_required) continue;
@@ -87,10 +88,19 @@ int build_host_plan(const gbgpu_qterm *qt, int nqt, const int64_t *sizes, const 
     }
     // numeric term lists carry a float where the word position is
     // (Posdb.cpp:4572-4577); gbsortby: scores by it (4413-4417, 7265-7269)
-    const bool sortby = qt[i].field_code == FIELD_GBSORTBYFLOAT || qt[i].field_code == FIELD_GBREVSORTBYFLOAT;
+    const bool sortbyf = qt[i].field_code == FIELD_GBSORTBYFLOAT || qt[i].field_code == FIELD_GBREVSORTBYFLOAT;
+    const bool sortbyi = qt[i].field_code == FIELD_GBSORTBYINT || qt[i].field_code == FIELD_GBREVSORTBYINT;
+    const bool sortby = sortbyf || sortbyi;
     int rint;
     const bool number = sortby || range_mode(qt[i].field_code, &rint) != 0;
-    if (sortby) hp->sortby_group = nrg;
+    // the last sortby term wins; the int form also switches the tree
+    // (m_sortByTermNum and m_sortByTermNumInt are separate in the reference:
+    // with both, the float sets `score` and the int the tree -- not emulated)
+    if (sortby) {
+      if (hp->sortby_group >= 0 && hp->sortby_int != (int)sortbyi) return GBGPU_EUNSUPPORTED;
+      hp->sortby_group = nrg;
+      hp->sortby_int = sortbyi;
+    }
     ok &= add(i, (uint8_t)(piped | (qt[i].term_sign == '-' ? BF_NEGATIVE : 0) | (number ? BF_NUMBER : 0)));
     if (left >= 0 && !leftAdded) {
       ok &= add(left, piped | BF_BIGRAM);

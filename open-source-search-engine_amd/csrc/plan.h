@@ -49,7 +49,8 @@ struct HostPlan {
   int64_t min_list_size = 0;
   int32_t docs_wanted = 0;
   int real_max_top = 10;
-  int sortby_group = -1;  // m_sortByTermInfoNum (gbsortby:/gbrevsortby: float, Posdb.cpp:4413-4417)
+  int sortby_group = -1;  // m_sortByTermInfoNum(Int) (gbsortby:/gbrevsortby:, Posdb.cpp:4413-4425)
+  int sortby_int = 0;     // the int form: TopTree integer scores (m_useIntScores)
 };
 
 // Query::m_fieldCode values PosdbTable treats specially (Query.h:118-132);
@@ -70,10 +71,7 @@ enum : int32_t {
   FIELD_GBNUMBEREQUALFLOAT = 67,
 };
 // a field code the GPU path does not implement (range, int sortby, facets)
-inline bool field_unsupported(int32_t fc) {
-  return fc == FIELD_GBSORTBYINT || fc == FIELD_GBREVSORTBYINT ||
-         (fc >= FIELD_GBFACETSTR && fc <= FIELD_GBFACETFLOAT);
-}
+inline bool field_unsupported(int32_t fc) { return fc >= FIELD_GBFACETSTR && fc <= FIELD_GBFACETFLOAT; }
 // range terms: (mode, int?) of a field code, mode 0 if not one
 inline int range_mode(int32_t fc, int *is_int) {
   *is_int = fc == FIELD_GBNUMBERMININT || fc == FIELD_GBNUMBERMAXINT || fc == FIELD_GBNUMBEREQUALINT;
@@ -141,7 +139,8 @@ struct DevPlan {
   float tfw[MAXG];
   int32_t qpos[MAXG], wiki[MAXG], quote[MAXG];
   int32_t qterm[MAXG];  // m_qtermNum (the second pass's score info)
-  int32_t sortby_group;  // gbsortby float: the group whose first key's float is the score (-1: none)
+  int32_t sortby_group;  // gbsortby: the group whose first key's number is the score (-1: none)
+  int32_t sortby_int;    // ... read as int32: the TopTree orders by m_intScore (TopTree.cpp:216-219, 270-274)
   // candidate arrays (sublists of m_minListi, distinct lists, in order)
   int g0n;
   int g0list[MAXG0];

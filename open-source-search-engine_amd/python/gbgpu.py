@@ -154,6 +154,7 @@ class Result(ctypes.Structure):
         ("pair_scores", ctypes.c_void_p), ("pair_scores_cap", ctypes.c_int32), ("n_pair_scores", ctypes.c_int32),
         ("single_scores", ctypes.c_void_p), ("single_scores_cap", ctypes.c_int32),
         ("n_single_scores", ctypes.c_int32),
+        ("int_scores", ctypes.POINTER(ctypes.c_int32)),
     ]
 
 
@@ -408,6 +409,8 @@ class QueryResult:
     docid_scores: Optional[np.ndarray] = None
     pair_scores: Optional[np.ndarray] = None
     single_scores: Optional[np.ndarray] = None
+    # TopNode::m_intScore under a gbsortby int term (scores are then 0.0)
+    int_scores: Optional[np.ndarray] = None
 
 
 class Engine:
@@ -463,6 +466,8 @@ class Engine:
             h = np.zeros(hit_cap, np.int64)
             r.hit_docids = h.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))
             r.hit_capacity = hit_cap
+        r._ints = (ctypes.c_int32 * max(cap, 1))()
+        r.int_scores = ctypes.cast(r._ints, ctypes.POINTER(ctypes.c_int32))
         if info is not None:
             r.docid_scores, r.docid_scores_cap = info[0].ctypes.data, len(info[0])
             r.pair_scores, r.pair_scores_cap = info[1].ctypes.data, len(info[1])
@@ -475,6 +480,7 @@ class Engine:
         q = QueryResult(np.frombuffer(d, dtype=np.int64, count=n).copy(),
                         np.frombuffer(s, dtype=np.float32, count=n).copy(), r.hits, r.filtered, r.docs_wanted,
                         None if h is None else h[:r.n_hit_docids].copy())
+        q.int_scores = np.frombuffer(r._ints, dtype=np.int32, count=n).copy()
         if info is not None:
             q.docid_scores = info[0][:r.n_docid_scores].copy()
             q.pair_scores = info[1][:r.n_pair_scores].copy()

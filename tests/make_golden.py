@@ -223,6 +223,16 @@ def save_sortby():
         lists = list(lists) + [sortby_list(lists, frac, seed=61 + j, neg_frac=neg)]
         r = save_query(f"sortby{j}_{q.name}", terms, lists, q.params(**kw), prefix="f")
         print(f"  f_sortby{j}_{q.name}: hits={r['hits']} n={len(r['docids'])} top={r['scores'][:3]}")
+    # gbsortby int (59) / gbrevsortby int (60): TopTree integer scores
+    for j, (kind, fc, frac) in enumerate([(0, 59, 0.7), (4, 60, 0.8), (1, 59, 0.6)]):
+        q = ks[kind]
+        lists = generate(q, N, seed=5450 + j)
+        terms = list(q.terms)
+        qpos = max(t.qpos for t in terms) + 2
+        terms.append(gbgpu.QTerm(1, 0, fc, 0, -1, -1, -1, 0, qpos, 0, -1, 1.0))
+        lists = list(lists) + [number_list(lists, frac, seed=81 + j, kmax=1 + j, ints=True)]
+        r = save_query(f"sortbyint{j}_{q.name}", terms, lists, q.params(), prefix="f")
+        print(f"  f_sortbyint{j}_{q.name}: hits={r['hits']} n={len(r['docids'])} scores={r['scores'][:2]}")
     # a text field term (FIELD_TITLE = 6): nothing special to PosdbTable
     q = ks[1]
     lists = generate(q, N, seed=5500)

@@ -133,7 +133,7 @@ def test_unsupported_modes_fail_loudly(engine):
     p = q.params()
     terms = list(q.terms)
     terms[0] = gbgpu.QTerm(*[getattr(terms[0], f) for f, _ in gbgpu.QTerm._fields_])
-    terms[0].field_code = 59  # gbsortby int (integer TopTree scores); facets likewise (test_fields.py)
+    terms[0].field_code = 63  # a facet term (gbfacetstr:); test_fields.py covers the others
     with pytest.raises(gbgpu.GbgpuError) as e:
         engine.query(terms, lists, p)
     assert e.value.code == gbgpu.GBGPU_EUNSUPPORTED
