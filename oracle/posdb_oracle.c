@@ -165,7 +165,24 @@ typedef struct {
   int64_t totalSubListsSize;
   float termFreqWeight;
   int qtermNum, qpos, wikiPhraseId, quotedStartId;
+  int fieldCode;     /* m_qt->m_fieldCode                                   */
+  float qwFloat;     /* m_qt->m_qword->m_float (range terms)                */
+  int32_t qwInt;     /* m_qt->m_qword->m_int                                */
 } QTI;
+
+/* Query::m_fieldCode values PosdbTable treats specially (Query.h:118-132) */
+enum { F_SORTBYFLOAT = 54, F_REVSORTBYFLOAT = 55, F_NUMBERMIN = 56, F_NUMBERMAX = 57, F_SORTBYINT = 59,
+       F_REVSORTBYINT = 60, F_NUMBERMININT = 61, F_NUMBERMAXINT = 62, F_FACETSTR = 63, F_FACETINT = 64,
+       F_FACETFLOAT = 65, F_NUMBEREQUALINT = 66, F_NUMBEREQUALFLOAT = 67 };
+static int isNumberField(int fc) { /* Posdb.cpp:4572-4594 */
+  return fc == F_SORTBYFLOAT || fc == F_REVSORTBYFLOAT || fc == F_NUMBERMIN || fc == F_NUMBERMAX ||
+         fc == F_NUMBEREQUALFLOAT || fc == F_SORTBYINT || fc == F_REVSORTBYINT || fc == F_NUMBERMININT ||
+         fc == F_NUMBERMAXINT || fc == F_NUMBEREQUALINT;
+}
+static int isRangeField(int fc) { /* Posdb.cpp:5056-5073 */
+  return fc == F_NUMBERMIN || fc == F_NUMBERMAX || fc == F_NUMBEREQUALFLOAT || fc == F_NUMBERMININT ||
+         fc == F_NUMBERMAXINT || fc == F_NUMBEREQUALINT;
+}
 
 typedef struct {
   /* PosdbTable state used by the scorers */
@@ -198,7 +215,7 @@ typedef struct {
   float vcount;          /* m_vcount                                     */
   int32_t domCount[256]; /* m_domCount                                   */
   int64_t n;             /* m_numUsedNodes                               */
-  float *score;          /* sorted best first                            */
+  double *score;         /* sorted best first (an int score is exact)     */
   int64_t *docid;
 } TTree;
 
@@ -237,16 +254,16 @@ static void tt_delete(TTree *t, int64_t i, uint8_t domHash) {
   if (t->domCount[domHash] < t->cap) t->vcount -= 1.0;
   else if (t->domCount[domHash] == t->cap) t->vcount -= t->partial;
   t->domCount[domHash]--;
-  memmove(t->score + i, t->score + i + 1, sizeof(float) * (size_t)(t->n - i - 1));
+  memmove(t->score + i, t->score + i + 1, sizeof(double) * (size_t)(t->n - i - 1));
   memmove(t->docid + i, t->docid + i + 1, sizeof(int64_t) * (size_t)(t->n - i - 1));
   t->n--;
 }
 
 /* TopTree::addNode, TopTree.cpp:206-516; returns 1 if the node was added */
-static int tt_add(TTree *t, float score, int64_t docid) {
+static int tt_add(TTree *t, double score, int64_t docid) {
   const uint8_t domHash = domHash8(docid);
   if (t->vcount >= t->docsWanted) {
-    const float ls = t->score[t->n - 1];
+    const double ls = t->score[t->n - 1];
     const int64_t ld = t->docid[t->n - 1];
     if (score < ls) return 0;
     if (score > ls) goto addIt;
@@ -283,10 +300,10 @@ addIt:;
     deleteMe = t->docid[m];
   }
   if (t->n % 4096 == 0) {
-    t->score = (float *)realloc(t->score, sizeof(float) * (size_t)(t->n + 4096));
+    t->score = (double *)realloc(t->score, sizeof(double) * (size_t)(t->n + 4096));
     t->docid = (int64_t *)realloc(t->docid, sizeof(int64_t) * (size_t)(t->n + 4096));
   }
-  memmove(t->score + pos + 1, t->score + pos, sizeof(float) * (size_t)(t->n - pos));
+  memmove(t->score + pos + 1, t->score + pos, sizeof(double) * (size_t)(t->n - pos));
   memmove(t->docid + pos + 1, t->docid + pos, sizeof(int64_t) * (size_t)(t->n - pos));
   t->score[pos] = score;
   t->docid[pos] = docid;
@@ -794,8 +811,12 @@ static int setQueryTermInfo(const orc_qterm *qt, int nqt, OList *lists, QTI *qip
     {
       int fl = piped;
       if (qt[i].term_sign == '-') fl |= BF_NEGATIVE;
+      if (isNumberField(qt[i].field_code)) fl |= BF_NUMBER; /* Posdb.cpp:4572-4594 */
       ADD(i, fl);
     }
+    qti->fieldCode = qt[i].field_code;
+    qti->qwFloat = qt[i].number_float;
+    qti->qwInt = qt[i].number_int;
     if (left >= 0 && !leftAlreadyAdded) {
       ADD(left, piped | BF_BIGRAM);
       for (int k = 0; k < nqt; k++)
@@ -900,9 +921,34 @@ static int white_has(const WhiteSet *ws, const uint8_t *p) {
   return lo < ws->n && ws->v[lo] == x;
 }
 
-/* addDocIdVotes, Posdb.cpp:5043-5332 (no range terms); ws: the whitelist
- * table when the request has one (Posdb.cpp:5294), else NULL */
+/* isInRange / isInRange2, Posdb.cpp:4948-4999 */
+static int isInRange(const uint8_t *p, const QTI *qti) {
+  float f;
+  int32_t v;
+  memcpy(&f, p + 2, 4);
+  memcpy(&v, p + 2, 4);
+  switch (qti->fieldCode) {
+    case F_NUMBERMIN: return f >= qti->qwFloat;
+    case F_NUMBERMAX: return f <= qti->qwFloat;
+    case F_NUMBEREQUALFLOAT: return f == qti->qwFloat;
+    case F_NUMBERMININT: return v >= qti->qwInt;
+    case F_NUMBERMAXINT: return v <= qti->qwInt;
+    case F_NUMBEREQUALINT: return v == qti->qwInt;
+  }
+  return 1;
+}
+static int isInRange2(const uint8_t *recPtr, const uint8_t *subListEnd, const QTI *qti) {
+  if (isInRange(recPtr, qti)) return 1;
+  recPtr += 12;
+  for (; recPtr < subListEnd && ((*recPtr) & 0x04); recPtr += 6)
+    if (isInRange(recPtr, qti)) return 1;
+  return 0;
+}
+
+/* addDocIdVotes, Posdb.cpp:5043-5332; ws: the whitelist table when the
+ * request has one (Posdb.cpp:5294), else NULL */
 static void addDocIdVotes(QTI *qti, int listGroupNum, OList *lists, VoteBuf *vb, const WhiteSet *ws) {
+  const int isRangeTerm = isRangeField(qti->fieldCode);
   uint8_t *dp, *dpEnd, *recPtr, *subListEnd;
   for (int i = 0; i < qti->numSubLists && listGroupNum > 0; i++) {
     recPtr = lists[qti->subList[i]].list;
@@ -914,6 +960,7 @@ static void addDocIdVotes(QTI *qti, int listGroupNum, OList *lists, VoteBuf *vb,
       int c = vcmp(dp, recPtr);
       if (c > 0) break;
       if (c < 0) continue;
+      if (isRangeTerm && !isInRange2(recPtr, subListEnd, qti)) break; /* 5120-5121 */
       dp[5] = (uint8_t)listGroupNum;
       dp += 6;
       break;
@@ -958,10 +1005,13 @@ static void addDocIdVotes(QTI *qti, int listGroupNum, OList *lists, VoteBuf *vb,
       vb->len = dp - vb->buf;
       return;
     }
+    int inRange = 0; /* Posdb.cpp:5242-5277 */
+    if (isRangeTerm && isInRange2(cursor[mini], cursorEnd[mini], qti)) inRange = 1;
     cursor[mini] += 12;
     for (;;) {
       if (cursor[mini] >= cursorEnd[mini]) { cursor[mini] = NULL; break; }
       if (!(cursor[mini][0] & 0x04)) break;
+      if (isRangeTerm && isInRange2(cursor[mini], cursorEnd[mini], qti)) inRange = 1;
       cursor[mini] += 6;
     }
     if (lastMinRecPtr && U32(lastMinRecPtr + 8) == U32(minRecPtr + 8) &&
@@ -969,6 +1019,7 @@ static void addDocIdVotes(QTI *qti, int listGroupNum, OList *lists, VoteBuf *vb,
       continue;
     /* not in the whitelist: not stored, lastMinRecPtr unchanged (5294) */
     if (ws && !white_has(ws, minRecPtr + 7)) continue;
+    if (isRangeTerm && !inRange) continue; /* 5297-5298 */
     lastMinRecPtr = minRecPtr;
     memcpy(dp + 1, minRecPtr + 8, 4);
     dp[0] = minRecPtr[7] & 0xfc;
@@ -1415,6 +1466,11 @@ static int run_range(const orc_qterm *qt, const uint8_t *const *lists, const int
     float siteRankMultiplier = SITERANKMULTIPLIER;
     char siteRank = 0, docLang = 0;
     float minWinningScore = -1.0; /* Posdb.cpp:6012: per pass */
+    int sortByF = -1, sortByI = -1; /* m_sortByTermInfoNum(Int), Posdb.cpp:4413-4425 */
+    for (int i = 0; i < nqti; i++) {
+      if (qip[i].fieldCode == F_SORTBYFLOAT || qip[i].fieldCode == F_REVSORTBYFLOAT) sortByF = i;
+      if (qip[i].fieldCode == F_SORTBYINT || qip[i].fieldCode == F_REVSORTBYINT) sortByI = i;
+    }
     int32_t ourFirstPos = -1;
     unsigned char ringBuf[RINGBUFSIZE + 10];
     MaxCtx mc;
@@ -1458,7 +1514,9 @@ static int run_range(const orc_qterm *qt, const uint8_t *const *lists, const int
       /* the max-score and ring-buffer prefilters, Posdb.cpp:6322-6504 (live
        * only once the TopTree holds more than docsWanted nodes, i.e. with
        * site clustering: minWinningScore is -1 until then) */
-      if (prefilter_skip(&mc, qip, nqti, P.minListi, prm->do_max_score_algo, minWinningScore, ringBuf,
+      /* gbsortby: both prefilters off (Posdb.cpp:6050-6051, 6350-6351) */
+      if (sortByF < 0 && sortByI < 0 &&
+          prefilter_skip(&mc, qip, nqti, P.minListi, prm->do_max_score_algo, minWinningScore, ringBuf,
                          &ourFirstPos))
         continue;
 
@@ -1478,6 +1536,15 @@ static int run_range(const orc_qterm *qt, const uint8_t *const *lists, const int
             nwpEnd[nsub] = qti->cursor[k];
             nwpFlags[nsub] = qti->bigramFlags[k];
             nsub++;
+          }
+          /* one sublist of a numeric/facet group: not merged, the list
+           * itself (Posdb.cpp:6638-6647) */
+          if (nsub == 1 && (nwpFlags[0] & (BF_FACET | BF_NUMBER)) && !(nwpFlags[0] & BF_SYNONYM) &&
+              !(nwpFlags[0] & BF_HALFSTOPWIKIBIGRAM)) {
+            mml[j] = nwp[0];
+            mme[j] = nwpEnd[0];
+            bflags[j] = nwpFlags[0];
+            continue;
           }
           for (;;) {
             int mink = -1;
@@ -1673,12 +1740,22 @@ static int run_range(const orc_qterm *qt, const uint8_t *const *lists, const int
       if (prm->language == 0 || docLang == 0 || prm->language == docLang)
         score *= prm->same_lang_weight;
       out->filtered++;
+      int32_t intScore = 0;
+      if (sortByF >= 0) { /* Posdb.cpp:7265-7269 */
+        if (!mml[sortByF]) continue;
+        memcpy(&score, mml[sortByF] + 2, 4);
+      }
+      if (sortByI >= 0) { /* 7271-7279 */
+        if (!mml[sortByI]) continue;
+        memcpy(&intScore, mml[sortByI] + 2, 4);
+      }
       if (prm->min_serp_docid) { /* m_hasMaxSerpScore, Posdb.cpp:4379-4381, 7327-7347 */
         if (score > (float)prm->max_serp_score) continue;
         if (score == prm->max_serp_score && (int64_t)pt.docId <= prm->min_serp_docid) continue;
       }
       out->filtered--;
-      tt_add(tree, score, (int64_t)pt.docId);
+      /* with m_useIntScores the tree orders by m_intScore (TopTree.cpp:216-219, 270-274) */
+      tt_add(tree, sortByI >= 0 ? (double)intScore : (double)score, (int64_t)pt.docId);
       if (tree->n > tree->docsWanted) minWinningScore = tree->score[tree->n - 1]; /* 7699-7704 */
     }
   doneAll:
@@ -1736,8 +1813,16 @@ int orc_query(const orc_qterm *qt, const uint8_t *const *lists, const int64_t *s
   memset(out, 0, sizeof *out);
   if (nqt < 0 || !prm) return EINVAL;
   if (prm->real_max_top <= 0 || prm->docs_to_get <= 0 || prm->num_docid_splits <= 0) return EINVAL;
-  for (int i = 0; i < nqt; i++)
-    if (qt[i].field_code) return ENOTSUP; /* numeric/facet/range terms: DESIGN.md */
+  int intMode = 0;
+  for (int i = 0; i < nqt; i++) {
+    const int fc = qt[i].field_code;
+    if ((fc == F_SORTBYINT || fc == F_REVSORTBYINT) && qt[i].is_required) intMode = 1;
+    if (fc == F_FACETSTR || fc == F_FACETINT || fc == F_FACETFLOAT) return ENOTSUP; /* facets: DESIGN.md */
+    /* integer tree scores with the domain caps / paging / pieces: not restated */
+    if ((fc == F_SORTBYINT || fc == F_REVSORTBYINT) &&
+        (prm->site_clustering || prm->min_serp_docid || prm->num_docid_splits > 1))
+      return ENOTSUP;
+  }
   initWeights();
 
   const int splits = prm->num_docid_splits;
@@ -1794,7 +1879,7 @@ int orc_query(const orc_qterm *qt, const uint8_t *const *lists, const int64_t *s
   out->n = tk.n < cap ? (int32_t)tk.n : cap;
   for (int i = 0; i < out->n; i++) {
     docids[i] = tk.docid[i];
-    scores[i] = tk.score[i];
+    scores[i] = intMode ? 0.0f : (float)tk.score[i]; /* TopNode::m_score is 0 with int scores */
   }
   tt_free(&tk);
   return rc;

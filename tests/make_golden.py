@@ -22,6 +22,7 @@ import gbgpu  # noqa: E402
 import qkinds  # noqa: E402
 import ref_binding as ref  # noqa: E402
 from mergegen import tiered_runs  # noqa: E402
+from numlists import number_list  # noqa: E402
 from workload import generate  # noqa: E402
 
 OUT = os.path.join(HERE, "golden")
@@ -150,34 +151,6 @@ def sortby_list(lists, frac, seed, termid=0x5A5A5A5A5A5, neg_frac=0.0):
         k[2:6] = struct.pack("<f", v)
         k[12:18] = termid.to_bytes(6, "little")
         keys.append(bytes(k))
-    return posdb_py.encode_keys(keys)
-
-
-def number_list(lists, frac, seed, termid=0x3C3C3C3C3C3, kmax=1, ints=False):
-    """A numeric termlist of 1..kmax keys per docid for a `frac` share of
-    the query's docids: a float (or int32) in bytes 2..5 of each key."""
-    import struct
-    import posdb_py
-    rng = np.random.default_rng(seed)
-    first = {}
-    for l in lists:
-        for k in posdb_py.full_keys(l):
-            first.setdefault(int.from_bytes(k[7:12], "little") >> 2, k)
-    keys = []
-    for d in sorted(first):
-        if rng.random() >= frac:
-            continue
-        vals = set()
-        for _ in range(int(rng.integers(1, kmax + 1))):
-            vals.add(struct.pack("<i", int(rng.integers(-20, 200))) if ints else
-                     struct.pack("<f", float(rng.integers(0, 400)) / 4.0))
-        run = []
-        for v in vals:
-            k = bytearray(first[d])
-            k[2:6] = v
-            k[12:18] = termid.to_bytes(6, "little")
-            run.append(bytes(k))
-        keys += sorted(run, key=lambda k: int.from_bytes(k[0:6], "little"))
     return posdb_py.encode_keys(keys)
 
 

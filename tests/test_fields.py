@@ -6,8 +6,8 @@ Fixtures: tests/golden/f_*.npz, made by `python3 tests/make_golden.py
 sortby` / `range` from the reference harness (oracle/_ref/gbref).  Range
 terms (gbmin:/gbmax:/gbequal:, float and int; Posdb.cpp:4948-4999,
 5056-5121, 5242-5298) vote a docid only if a key of its run holds a number
-in range.  The C oracle does not restate these modes: the fixtures are the
-only pin.  gbsortby int terms make the TopTree order by m_intScore
+in range.  The C oracle restates them too and is pinned to the same
+fixtures (CPU tests below).  gbsortby int terms make the TopTree order by m_intScore
 (gbgpu_result::int_scores).  Facet terms return GBGPU_EUNSUPPORTED."""
 import glob
 import os
@@ -17,6 +17,7 @@ import numpy as np
 import pytest
 
 import gbgpu
+import oracle_binding as orc
 from test_golden import check, load_query
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -26,6 +27,13 @@ IDS = [os.path.basename(p)[2:-4] for p in FCASES]
 
 def test_fixtures_present():
     assert len(FCASES) >= 6
+
+
+@pytest.mark.parametrize("path", FCASES, ids=IDS)
+def test_oracle_fields_vs_reference(path):
+    terms, lists, params, exp = load_query(path)
+    check(orc.query(terms, lists, params, cap=1 << 16), exp, os.path.basename(path))
+    assert np.array_equal(orc.intersect(terms, lists, params=params), exp["votes"])
 
 
 def first_numbers(lst, fmt):
@@ -77,3 +85,34 @@ def test_gpu_unsupported_field_codes(engine, fc):
     with pytest.raises(gbgpu.GbgpuError) as e:
         engine.query(terms, lists, params)
     assert e.value.code == gbgpu.GBGPU_EUNSUPPORTED
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [1, 2, 3])
+@pytest.mark.parametrize("fc,vf,vi,ints", [(56, 40.0, 0, False), (57, 60.0, 0, False), (67, 12.5, 0, False),
+                                           (61, 0, 90, True), (62, 0, 30, True), (54, 0, 0, False),
+                                           (59, 0, 0, True)])
+def test_gpu_fields_vs_oracle(engine, seed, fc, vf, vi, ints):
+    """Larger seeded corpora (40 k docs) than the fixtures, GPU vs the oracle:
+    top tree, hits, the intersected docid set."""
+    import qkinds
+    from numlists import number_list
+    from workload import generate
+    N = 40000
+    for q in qkinds.kinds(N, seed=seed)[:5]:
+        lists = generate(q, N, seed=7000 + seed)
+        terms = list(q.terms)
+        t = gbgpu.QTerm(1, 0, fc, 0, -1, -1, -1, 0, max(x.qpos for x in terms) + 2, 0, -1, 1.0)
+        t.number_float, t.number_int = vf, vi
+        terms.append(t)
+        lists = list(lists) + [number_list(lists, 0.6, seed=seed, kmax=3, ints=ints)]
+        params = q.params()
+        o = orc.query(terms, lists, params, cap=1 << 16)
+        ov = orc.intersect(terms, lists, params=params)
+        r = engine.query(terms, lists, params, cap=1 << 16, hit_cap=max(1, o["hits"]))
+        label = f"{q.name} fc={fc} seed={seed}"
+        assert r.hits == o["hits"], label
+        assert np.array_equal(r.hit_docids, ov), label
+        assert np.array_equal(r.docids, o["docids"]), label
+        assert np.array_equal(np.asarray(r.scores, np.float32).view(np.uint32),
+                              np.asarray(o["scores"], np.float32).view(np.uint32)), label
