@@ -3208,10 +3208,12 @@ static int snapshot_lists(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms, 
   if (!p || nterms < 0 || (nterms && (!terms || !handles))) return EINVAL;
   if (p->docs_to_get <= 0 || p->real_max_top <= 0 || p->num_docid_splits <= 0) return EINVAL;
   if (nterms > 1024) return GBGPU_EUNSUPPORTED;
-  // the second scoring pass with the tree's domain caps, over docid-split
-  // pieces, or under the paging filter: the CPU body
-  if (p->get_docid_scoring_info && (p->site_clustering || p->num_docid_splits > 1 || p->min_serp_docid))
-    return GBGPU_EUNSUPPORTED;
+  // the second scoring pass over docid-split pieces (its per-range skip and
+  // the kicked-out-docid bookkeeping, Posdb.cpp:6189-6193, 7588-7665): the
+  // CPU body.  With site clustering or paging it reads the same tree order
+  // (the prefilters are off in that pass, and every tree docid passed the
+  // paging filter already), so those run here.
+  if (p->get_docid_scoring_info && p->num_docid_splits > 1) return GBGPU_EUNSUPPORTED;
   ents.resize(nterms);
   std::lock_guard<std::mutex> g(ctx->lists_mu);
   for (int i = 0; i < nterms; i++) {

@@ -115,6 +115,25 @@ def save_scoreinfo():
         r = save_query(q.name, q.terms, lists, p, prefix="s")
         print(f"  s_{q.name}: n={len(r['docids'])} info={len(r['score_info'])} pairs={len(r['pair_scores'])} "
               f"singles={len(r['single_scores'])}")
+    # with site clustering (the default request) and with paging
+    for j, kind in enumerate((0, 1, 4, 8)):
+        q = ks[kind]
+        lists = generate(q, N, seed=5250 + j)
+        p = q.params(site_clustering=1)
+        p.get_docid_scoring_info = 1
+        r = save_query(f"clus{j}_{q.name}", q.terms, lists, p, prefix="s")
+        print(f"  s_clus{j}_{q.name}: n={len(r['docids'])} info={len(r['score_info'])}")
+    for j, kind in enumerate((0, 2)):
+        q = ks[kind]
+        lists = generate(q, N, seed=5280 + j)
+        full = ref.query(q.terms, lists, q.params())
+        if len(full["docids"]) < 3:
+            continue
+        pos = len(full["docids"]) // 3
+        p = q.params(max_serp_score=float(full["scores"][pos]), min_serp_docid=int(full["docids"][pos]))
+        p.get_docid_scoring_info = 1
+        r = save_query(f"serp{j}_{q.name}", q.terms, lists, p, prefix="s")
+        print(f"  s_serp{j}_{q.name}: n={len(r['docids'])} info={len(r['score_info'])}")
     for j, (kind, dtg, rmt) in enumerate(((1, 7, 3), (5, 12, 1), (8, 3, 10), (4, 40, 2))):
         q = ks[kind]
         q.docs_to_get = dtg

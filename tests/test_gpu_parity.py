@@ -137,10 +137,9 @@ def test_unsupported_modes_fail_loudly(engine):
     with pytest.raises(gbgpu.GbgpuError) as e:
         engine.query(terms, lists, p)
     assert e.value.code == gbgpu.GBGPU_EUNSUPPORTED
-    # the scoring-info second pass runs on the GPU except with site
-    # clustering / docid splits / paging (test_scoreinfo.py); resident lists
-    # take the same path
-    p2 = q.params(site_clustering=1)
+    # the scoring-info second pass runs on the GPU except over docid splits
+    # (test_scoreinfo.py); resident lists take the same path
+    p2 = q.params(num_docid_splits=2)
     p2.get_docid_scoring_info = 1
     with pytest.raises(gbgpu.GbgpuError) as e:
         engine.query(q.terms, lists, p2)

@@ -114,7 +114,7 @@ def test_gpu_scoreinfo_declines_bounded(engine):
 def test_gpu_scoreinfo_refusals(engine):
     """The combinations left to the CPU body return GBGPU_EUNSUPPORTED."""
     terms, lists, params, _ = load_query(SCASES[0])
-    for kw in (dict(site_clustering=1), dict(num_docid_splits=2), dict(min_serp_docid=5)):
+    for kw in (dict(num_docid_splits=2),):
         p = gbgpu.Params.from_buffer_copy(params)
         p.get_docid_scoring_info = 1
         for k, v in kw.items():
