@@ -102,9 +102,9 @@ typedef struct gbgpu_params {
   int32_t get_docid_scoring_info; /* m_getDocIdScoringInfo: the per-docid score
                                breakdown second pass (Posdb.cpp:6116-6244,
                                7554-7665, 7752-7775) into gbgpu_result's
-                               docid/pair/single score arrays.  With site
-                               clustering, docid splits or paging it returns
-                               GBGPU_EUNSUPPORTED (the adapter runs the CPU body) */
+                               docid/pair/single score arrays.  With docid splits
+                               it returns GBGPU_EUNSUPPORTED (the adapter runs the
+                               CPU body) */
   double  max_serp_score;   /* m_maxSerpScore  } paging of a widget's next page:   */
   int64_t min_serp_docid;   /* m_minSerpDocId  } nonzero enables the filter of
                                Posdb.cpp:4379-4381, 7327-7347 (counted in
