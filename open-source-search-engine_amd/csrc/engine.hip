@@ -549,7 +549,6 @@ struct ProbeOut {
   uint32_t *ulen;
   Loc *loc_l;
   uint32_t bit, mult;
-  const DevList *rl;  // the list, when it is a range term's (else nullptr)
 };
 
 // append up to 64 matches (one per lane), wave-wide
@@ -569,13 +568,11 @@ __device__ __forceinline__ void mbuf_push(ProbeLds &S, uint32_t &nbuf, bool hit,
 // (out of line, with every argument by value: a by-reference counter would
 // live in scratch, and scratch loads wait on vmcnt like any global load)
 __device__ __noinline__ void mbuf_flush_n(ProbeLds *S, uint32_t nbuf, uint32_t *lmask, uint32_t *ulen, Loc *loc_l,
-                                          uint32_t bit, uint32_t mult, int lane, const DevList *rl) {
+                                          uint32_t bit, uint32_t mult, int lane) {
   wave_lds_sync();
   if (!bit) nbuf = 0;  // diagnostic (GBGPU_PROBE_MODE=5): matches not published
   for (uint32_t i = lane; i < nbuf; i += 64) {
     const uint32_t slot = S->mslot[i], len = S->mlen[i];
-    // a range term's run votes only in range (Posdb.cpp:5115-5121)
-    if (rl && !run_in_range(*rl, S->mu[i], S->mu[i] + len)) continue;
     loc_l[slot] = Loc{S->mu[i], len};
     if (mult) atomicAdd(&ulen[slot], len * mult);
     atomicOr(&lmask[slot], bit);
@@ -583,7 +580,7 @@ __device__ __noinline__ void mbuf_flush_n(ProbeLds *S, uint32_t nbuf, uint32_t *
   wave_lds_sync();
 }
 __device__ __forceinline__ void mbuf_flush(ProbeLds &S, uint32_t &nbuf, const ProbeOut &o, int lane) {
-  mbuf_flush_n(&S, nbuf, o.lmask, o.ulen, o.loc_l, o.bit, o.mult, lane, o.rl);
+  mbuf_flush_n(&S, nbuf, o.lmask, o.ulen, o.loc_l, o.bit, o.mult, lane);
   nbuf = 0;
 }
 
@@ -907,11 +904,38 @@ __global__ void __launch_bounds__(64 * PW) k_probe(const DevPlan *pl, const Prob
   // arena units this list adds per matched run: one copy per positive group
   // it belongs to (a shared bigram sublist is merged into both groups)
   po.mult = __popc(L.group_bits & pl->pos_mask & ~NEG_BIT);
-  po.rl = L.rmode ? &L : nullptr;
   if (L.probe == PROBE_BY_RUN) {
     if (MODE == 0) probe_by_run<G0>(pl, w, L, cand, ctr, dir, s_lds[wid], po, lane);
   } else {
     probe_by_cand<MODE == 3 ? 0 : MODE, G0>(pl, w, L, cand, ctr, dir, s_lds[wid], po, lane);
+  }
+}
+
+// A range term's list in a later group votes a docid only if a key of its
+// run holds a number in range (Posdb.cpp:5115-5121): k_probe publishes every
+// run it matches, and this pass (launched only for such queries) withdraws
+// the out-of-range ones -- their list bit and arena units.
+__global__ void k_range_filter(const DevPlan *pl, uint32_t rbits, uint32_t *lmask, uint32_t *ulen, const Loc *loc,
+                               uint64_t slot_ub) {
+  for (uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; s < slot_ub;
+       s += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t lm = lmask[s];
+    uint32_t hit = lm & rbits;
+    if (!hit) continue;
+    uint32_t drop = 0, du = 0;
+    for (; hit; hit &= hit - 1) {
+      const int l = __ffs(hit) - 1;
+      const DevList &L = pl->lists[l];
+      const Loc lc = loc[(uint64_t)l * slot_ub + s];
+      if (!run_in_range(L, lc.unit, lc.unit + lc.len)) {
+        drop |= 1u << l;
+        du += lc.len * (uint32_t)__popc(L.group_bits & pl->pos_mask & ~NEG_BIT);
+      }
+    }
+    if (drop) {
+      lmask[s] = lm & ~drop;
+      ulen[s] -= du;
+    }
   }
 }
 
@@ -3665,6 +3689,16 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
     hipLaunchKernelGGL(kp, dim3((nwork + PW - 1) / PW), dim3(64 * PW), 0, st, dpl, dwork, nwork,
                        q.cand.as<uint64_t>(), lmask, loc, q.ulen.as<uint32_t>(), slot_ub, dctr,
                        q.dir.as<uint64_t>());
+  }
+  {
+    uint32_t rbits = 0;  // range terms' lists outside the smallest group
+    for (int l = 0; l < P.nlists; l++)
+      if (P.lists[l].rmode && P.lists[l].g0_array < 0) rbits |= 1u << l;
+    if (rbits) {
+      const uint32_t g = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(4096, (slot_ub + 255) / 256));
+      hipLaunchKernelGGL(k_range_filter, dim3(g), dim3(256), 0, st, dpl, rbits, lmask, q.ulen.as<uint32_t>(), loc,
+                         slot_ub);
+    }
   }
   if (ctx->profiling) HIPCHECK(hipEventRecord(q.ev[2], st));
   // k_score variant: group / sublist capacity and LDS records per lane
