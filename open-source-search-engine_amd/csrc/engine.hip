@@ -915,10 +915,14 @@ __global__ void __launch_bounds__(64 * PW) k_probe(const DevPlan *pl, const Prob
 // run holds a number in range (Posdb.cpp:5115-5121): k_probe publishes every
 // run it matches, and this pass (launched only for such queries) withdraws
 // the out-of-range ones -- their list bit and arena units.
-__global__ void k_range_filter(const DevPlan *pl, uint32_t rbits, uint32_t *lmask, uint32_t *ulen, const Loc *loc,
-                               uint64_t slot_ub) {
+__global__ void k_range_filter(const DevPlan *pl, const Counters *ctr, uint32_t rbits, uint32_t *lmask, uint32_t *ulen,
+                               const Loc *loc, uint64_t slot_ub) {
   for (uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; s < slot_ub;
        s += (uint64_t)gridDim.x * blockDim.x) {
+    // only written slots: each candidate array fills [g0base, g0base + g0count)
+    int a = 0;
+    while (a + 1 < pl->g0n && s >= pl->g0base[a + 1]) a++;
+    if (s - pl->g0base[a] >= ctr->g0count[a]) continue;
     const uint32_t lm = lmask[s];
     uint32_t hit = lm & rbits;
     if (!hit) continue;
@@ -927,7 +931,7 @@ __global__ void k_range_filter(const DevPlan *pl, uint32_t rbits, uint32_t *lmas
       const int l = __ffs(hit) - 1;
       const DevList &L = pl->lists[l];
       const Loc lc = loc[(uint64_t)l * slot_ub + s];
-      if (!run_in_range(L, lc.unit, lc.unit + lc.len)) {
+      if (lc.len < 2 || (uint64_t)lc.unit + lc.len > L.units || !run_in_range(L, lc.unit, lc.unit + lc.len)) {
         drop |= 1u << l;
         du += lc.len * (uint32_t)__popc(L.group_bits & pl->pos_mask & ~NEG_BIT);
       }
@@ -3696,8 +3700,8 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
       if (P.lists[l].rmode && P.lists[l].g0_array < 0) rbits |= 1u << l;
     if (rbits) {
       const uint32_t g = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(4096, (slot_ub + 255) / 256));
-      hipLaunchKernelGGL(k_range_filter, dim3(g), dim3(256), 0, st, dpl, rbits, lmask, q.ulen.as<uint32_t>(), loc,
-                         slot_ub);
+      hipLaunchKernelGGL(k_range_filter, dim3(g), dim3(256), 0, st, dpl, dctr, rbits, lmask, q.ulen.as<uint32_t>(),
+                         loc, slot_ub);
     }
   }
   if (ctx->profiling) HIPCHECK(hipEventRecord(q.ev[2], st));
