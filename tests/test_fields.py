@@ -116,3 +116,30 @@ def test_gpu_fields_vs_oracle(engine, seed, fc, vf, vi, ints):
         assert np.array_equal(r.docids, o["docids"]), label
         assert np.array_equal(np.asarray(r.scores, np.float32).view(np.uint32),
                               np.asarray(o["scores"], np.float32).view(np.uint32)), label
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fc,vf,vi,ints", [(54, 0, 0, False), (56, 40.0, 0, False), (62, 0, 30, True)])
+def test_gpu_fields_clustering_vs_oracle(engine, fc, vf, vi, ints):
+    """Field terms under site clustering (the default request): the TopTree
+    domain caps with the sortby float score, and the prefilters off for
+    gbsortby (Posdb.cpp:6050-6051, 6350)."""
+    import qkinds
+    from numlists import number_list
+    from workload import generate
+    N = 40000
+    for q in qkinds.kinds(N, seed=4)[:5]:
+        lists = generate(q, N, seed=7100)
+        terms = list(q.terms)
+        t = gbgpu.QTerm(1, 0, fc, 0, -1, -1, -1, 0, max(x.qpos for x in terms) + 2, 0, -1, 1.0)
+        t.number_float, t.number_int = vf, vi
+        terms.append(t)
+        lists = list(lists) + [number_list(lists, 0.6, seed=5, kmax=3, ints=ints)]
+        params = q.params(site_clustering=1)
+        o = orc.query(terms, lists, params, cap=1 << 16)
+        r = engine.query(terms, lists, params, cap=1 << 16)
+        label = f"{q.name} fc={fc}"
+        assert (r.hits, r.filtered, r.docs_wanted) == (o["hits"], o["filtered"], o["docs_wanted"]), label
+        assert np.array_equal(r.docids, o["docids"]), label
+        assert np.array_equal(np.asarray(r.scores, np.float32).view(np.uint32),
+                              np.asarray(o["scores"], np.float32).view(np.uint32)), label
