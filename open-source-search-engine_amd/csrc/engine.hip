@@ -2832,7 +2832,7 @@ __global__ void k_xpack(const Counters *ctr, const uint32_t *keys, const uint64_
 
 // one wave: the k-way merge of the shards' replies (each sorted best first)
 __global__ void __launch_bounds__(64) k_xmerge(const uint8_t *recv, int nranks, uint32_t k, size_t stride,
-                                               uint8_t *out) {
+                                               uint8_t *out, int int_scores) {
   const int lane = threadIdx.x;
   XHead *oh = reinterpret_cast<XHead *>(out);
   double *osc = reinterpret_cast<double *>(out + sizeof(XHead));
@@ -2887,7 +2887,9 @@ __global__ void __launch_bounds__(64) k_xmerge(const uint8_t *recv, int nranks, 
   for (uint32_t t = lane; t < taken; t += 64) {
     const uint32_t bk = s_key[t];
     const uint32_t b = (bk & 0x80000000u) ? (bk & 0x7fffffffu) : ~bk;
-    osc[t] = (double)__uint_as_float(b);  // the wire's double score (Msg3a.cpp:1443)
+    // the wire's double score (Msg3a.cpp:1443); with integer tree scores
+    // Msg39 sends (double)m_intScore (Msg39.cpp:1663-1664)
+    osc[t] = int_scores ? (double)(int32_t)(bk ^ 0x80000000u) : (double)__uint_as_float(b);
     odoc[t] = (int64_t)s_doc[t];
   }
   if (lane == 0) {
@@ -4578,7 +4580,6 @@ int gbgpu_allgather_topk(gbgpu_ctx *ctx, int slot, int32_t k, int64_t *docids, d
   if (!ctx->comm) return EINVAL;
   std::unique_lock<std::mutex> lk(q->mu);
   if (!q->pending) return EINVAL;
-  if (q->int_scores) return GBGPU_EUNSUPPORTED;  // Msg3a merges double scores; int ones not emulated
   (void)hipSetDevice(ctx->device);
   const size_t stride = align256(sizeof(XHead) + sizeof(XRec) * (size_t)k);
   const size_t out_bytes = sizeof(XHead) + 16 * (size_t)k;
@@ -4601,7 +4602,7 @@ int gbgpu_allgather_topk(gbgpu_ctx *ctx, int slot, int32_t k, int64_t *docids, d
   }
   if (ncclAllGather(ctx->xsend.p, ctx->xrecv.p, stride, ncclUint8, ctx->comm, xs) != ncclSuccess) return GBGPU_EHIP;
   hipLaunchKernelGGL(k_xmerge, dim3(1), dim3(64), 0, xs, ctx->xrecv.as<uint8_t>(), ctx->nranks, (uint32_t)k, stride,
-                     ctx->xout.as<uint8_t>());
+                     ctx->xout.as<uint8_t>(), q->int_scores ? 1 : 0);
   HIPCHECK(hipMemcpyAsync(ctx->h_xout, ctx->xout.p, out_bytes, hipMemcpyDeviceToHost, xs));
   HIPCHECK(hipStreamSynchronize(xs));
   // finish the slot's own query (its result block was read on the device)
@@ -4656,7 +4657,7 @@ int gbgpu_merge_replies_device(gbgpu_ctx *ctx, int nranks, int32_t k, const int3
   if (hipMemcpy(din.p, recv.data(), recv.size(), hipMemcpyHostToDevice) != hipSuccess) rc = GBGPU_EHIP;
   if (!rc) {
     hipLaunchKernelGGL(k_xmerge, dim3(1), dim3(64), 0, 0, din.as<uint8_t>(), nranks, (uint32_t)k, stride,
-                       dout.as<uint8_t>());
+                       dout.as<uint8_t>(), 0);
     if (hipGetLastError() != hipSuccess || hipMemcpy(out.data(), dout.p, out_bytes, hipMemcpyDeviceToHost) != hipSuccess)
       rc = GBGPU_EHIP;
   }

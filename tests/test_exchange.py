@@ -64,6 +64,20 @@ def test_allgather_topk_one_rank():
             assert h == exp["hits"]
             assert np.array_equal(d, exp["docids"][:m])
             assert np.array_equal(s, exp["scores"][:m].astype(np.float64))
+        # gbsortby int: the tree orders by m_intScore and the wire carries
+        # (double)m_intScore (Msg39.cpp:1663-1664)
+        from numlists import number_list
+        terms = list(q.terms)
+        t = gbgpu.QTerm(1, 0, 59, 0, -1, -1, -1, 0, max(x.qpos for x in terms) + 2, 0, -1, 1.0)
+        terms.append(t)
+        lists3 = list(lists) + [number_list(lists, 0.7, seed=9, ints=True)]
+        hs3 = [eng.upload(l) for l in lists3]
+        ref = eng.query_resident(terms, hs3, p, cap=1 << 12)
+        eng.enqueue(terms, hs3, p, slot=0)
+        d, s, h = eng.allgather_topk(q.docs_to_get, slot=0)
+        m = min(q.docs_to_get, len(ref.docids))
+        assert np.array_equal(d, ref.docids[:m])
+        assert np.array_equal(s, ref.int_scores[:m].astype(np.float64))
         # an empty shard (all lists empty) replies with nothing
         hs2 = [eng.upload(b"") for _ in lists]
         eng.enqueue(q.terms, hs2, p, slot=0)
