@@ -1775,10 +1775,16 @@ __global__ void __launch_bounds__(SCORE_TPB) k_score(const DevPlan *pl, const ui
       // the paging filter of a widget's next page (Posdb.cpp:7327-7347):
       // m_filtered counts the scored docids it drops
       if (pl->has_serp && key) {
-        const uint32_t b = (key & 0x80000000u) ? (key & 0x7fffffffu) : ~key;
-        const float score = __uint_as_float(b);
-        if (score > (float)pl->max_serp_score) filt = true;
-        else if ((double)score == pl->max_serp_score && (int64_t)d <= pl->min_serp_docid) filt = true;
+        if (pl->sortby_group >= 0 && pl->sortby_int) {  // intScore vs (int32_t)m_maxSerpScore
+          const int32_t iv = (int32_t)(key ^ 0x80000000u);
+          if (iv > pl->max_serp_int) filt = true;
+          else if (iv == pl->max_serp_int && (int64_t)d <= pl->min_serp_docid) filt = true;
+        } else {
+          const uint32_t b = (key & 0x80000000u) ? (key & 0x7fffffffu) : ~key;
+          const float score = __uint_as_float(b);
+          if (score > (float)pl->max_serp_score) filt = true;
+          else if ((double)score == pl->max_serp_score && (int64_t)d <= pl->min_serp_docid) filt = true;
+        }
         if (filt) key = 0;
       }
       skey[i] = key;
@@ -3411,6 +3417,9 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   P.has_serp = p->min_serp_docid != 0;  // Posdb.cpp:4379-4381
   P.max_serp_score = p->max_serp_score;
   P.min_serp_docid = p->min_serp_docid;
+  P.max_serp_int = (p->max_serp_score >= -2147483648.0 && p->max_serp_score < 2147483648.0)
+                       ? (int32_t)p->max_serp_score
+                       : (p->max_serp_score < 0 ? INT32_MIN : INT32_MAX);
   P.clustering = clus;
   P.use_white = p->use_whitelist != 0;
   if (P.use_white) {
@@ -3425,7 +3434,7 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   // integer TopTree scores: with the domain-cap tree, the paging filter or
   // the score info they take other reference paths (TopTree.cpp:332-333,
   // Posdb.cpp:7330-7336, 7559-7560): not on the GPU
-  if (hp.sortby_int && (clus || P.has_serp || p->get_docid_scoring_info || p->num_docid_splits > 1))
+  if (hp.sortby_int && (clus || p->get_docid_scoring_info || p->num_docid_splits > 1))
     return GBGPU_EUNSUPPORTED;
   P.min_listi = hp.min_listi;
   P.all_same_wiki = 1;  // m_allInSameWikiPhrase, Posdb.cpp:5764-5778

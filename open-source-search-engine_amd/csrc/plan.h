@@ -116,6 +116,7 @@ struct DevPlan {
   int has_serp;
   double max_serp_score;
   int64_t min_serp_docid;
+  int32_t max_serp_int;  // (int32_t)m_maxSerpScore, the bound for integer scores (Posdb.cpp:7330-7336)
   // the "&sites=" whitelist (Posdb.cpp:793-835, 5294, 5544-5572): sorted
   // 5-byte values (bytes 7..11 of a key: docid + siteRank's top bit); a
   // group-0 candidate whose run head is not among them is rejected

@@ -1750,8 +1750,14 @@ static int run_range(const orc_qterm *qt, const uint8_t *const *lists, const int
         memcpy(&intScore, mml[sortByI] + 2, 4);
       }
       if (prm->min_serp_docid) { /* m_hasMaxSerpScore, Posdb.cpp:4379-4381, 7327-7347 */
-        if (score > (float)prm->max_serp_score) continue;
-        if (score == prm->max_serp_score && (int64_t)pt.docId <= prm->min_serp_docid) continue;
+        if (sortByI >= 0) {
+          const int32_t m = (int32_t)prm->max_serp_score;
+          if (intScore > m) continue;
+          if (intScore == m && (int64_t)pt.docId <= prm->min_serp_docid) continue;
+        } else {
+          if (score > (float)prm->max_serp_score) continue;
+          if (score == prm->max_serp_score && (int64_t)pt.docId <= prm->min_serp_docid) continue;
+        }
       }
       out->filtered--;
       /* with m_useIntScores the tree orders by m_intScore (TopTree.cpp:216-219, 270-274) */
@@ -1819,8 +1825,7 @@ int orc_query(const orc_qterm *qt, const uint8_t *const *lists, const int64_t *s
     if ((fc == F_SORTBYINT || fc == F_REVSORTBYINT) && qt[i].is_required) intMode = 1;
     if (fc == F_FACETSTR || fc == F_FACETINT || fc == F_FACETFLOAT) return ENOTSUP; /* facets: DESIGN.md */
     /* integer tree scores with the domain caps / paging / pieces: not restated */
-    if ((fc == F_SORTBYINT || fc == F_REVSORTBYINT) &&
-        (prm->site_clustering || prm->min_serp_docid || prm->num_docid_splits > 1))
+    if ((fc == F_SORTBYINT || fc == F_REVSORTBYINT) && (prm->site_clustering || prm->num_docid_splits > 1))
       return ENOTSUP;
   }
   initWeights();

@@ -225,6 +225,24 @@ def save_sortby():
         lists = list(lists) + [number_list(lists, frac, seed=81 + j, kmax=1 + j, ints=True)]
         r = save_query(f"sortbyint{j}_{q.name}", terms, lists, q.params(), prefix="f")
         print(f"  f_sortbyint{j}_{q.name}: hits={r['hits']} n={len(r['docids'])} scores={r['scores'][:2]}")
+    # gbsortby int with paging: intScore vs (int32_t)m_maxSerpScore (7330-7336)
+    q = ks[0]
+    lists = generate(q, N, seed=5470)
+    terms = list(q.terms)
+    terms.append(gbgpu.QTerm(1, 0, 59, 0, -1, -1, -1, 0, max(t.qpos for t in terms) + 2, 0, -1, 1.0))
+    lists = list(lists) + [number_list(lists, 0.7, seed=91, ints=True)]
+    r0 = save_query("sortbyint_full", terms, lists, q.params(), prefix="tmp")
+    os.remove(os.path.join(OUT, "tmp_sortbyint_full.npz"))
+    import struct
+    import posdb_py
+    vals = {}
+    for key in posdb_py.full_keys(lists[-1]):
+        vals.setdefault(int.from_bytes(key[7:12], "little") >> 2, struct.unpack("<i", bytes(key[2:6]))[0])
+    pos = len(r0["docids"]) // 3
+    d = int(r0["docids"][pos])
+    p = q.params(max_serp_score=float(vals[d]) + 0.75, min_serp_docid=d)
+    r = save_query("sortbyint_serp_two_term", terms, lists, p, prefix="f")
+    print(f"  f_sortbyint_serp: n={len(r['docids'])} filtered={r['filtered']}")
     # a text field term (FIELD_TITLE = 6): nothing special to PosdbTable
     q = ks[1]
     lists = generate(q, N, seed=5500)
