@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define GBGPU_ABI_VERSION 8
+#define GBGPU_ABI_VERSION 9
 
 /* error codes beyond errno.h (Errno.h numbering is not reused) */
 #define GBGPU_ENODEVICE   1001 /* no HIP device / extension not usable        */
@@ -242,36 +242,67 @@ void *gbgpu_stream(gbgpu_ctx *ctx); /* slot 0 */
  * the next 256-byte boundary *n int64 docids.  Valid after gbgpu_query_collect. */
 int gbgpu_last_topk_device(gbgpu_ctx *ctx, void **dev_ptr, int32_t *n);
 
-/* Msg3a::mergeLists (Msg3a.cpp:1315-1467) without site clustering: k-way merge
- * of per-shard top lists by (score desc, docid asc), duplicate docids dropped,
- * first `k` kept.  Scores are widened to double as on the Msg39 wire. */
-int gbgpu_merge_topk(const int64_t *const *shard_docids, const float *const *shard_scores,
+/* Msg3a::mergeLists (Msg3a.cpp:1315-1467) without site clustering, on the
+ * host: the shards' replies as Msg39 sends them (docids, double scores --
+ * m_score, or (double)m_intScore for gbsortby int queries, Msg39.cpp:
+ * 1661-1664).  The loop takes the best shard head each step (higher double
+ * score; on equal scores the lower docid; on equal docids the earlier
+ * shard), passes over a docid already merged, and stops at `k` entries; a
+ * reply need not be sorted.  Pinned to the reference's own mergeLists
+ * (tests/golden/x_*.npz). */
+int gbgpu_merge_topk(const int64_t *const *shard_docids, const double *const *shard_scores,
                      const int32_t *shard_counts, int nshards, int32_t k,
                      int64_t *out_docids, double *out_scores, int32_t *out_n);
+
+/* The device merge gbgpu_allgather_topk runs after its all-gather, on replies
+ * given from the host (one per shard: counts[r] entries as Msg39 sends them,
+ * double scores, and the shard's hit count); for checking the merge without
+ * a multi-GPU node.  Same rules as gbgpu_merge_topk. */
+int gbgpu_merge_replies_device(gbgpu_ctx *ctx, int nranks, int32_t k, const int32_t *counts, const int64_t *shard_hits,
+                               const int64_t *const *shard_docids, const double *const *shard_scores,
+                               int64_t *docids, double *scores, int32_t *n, int64_t *hits);
+
+/* Exchange ordering.  Every rank must issue its collectives in the same
+ * order, but a process runs several INTERSECT threads (Msg39.cpp:1019-1027,
+ * up to `mct`) whose queries finish in any order.  A sequencer admits
+ * exactly one caller at a time, in increasing sequence number: the caller
+ * holding query `seq` waits in gbgpu_seq_enter until every smaller number
+ * has left.  Sequence numbers are agreed across ranks (the front end that
+ * sends one Msg39Request to every shard numbers it) and
+ * each must be entered and left on every rank exactly once, starting at
+ * `first`.  gbgpu_seq_enter returns 0 when admitted, ETIMEDOUT after
+ * timeout_ms (< 0: wait forever), EINVAL for a number already past or
+ * already admitted; gbgpu_seq_leave returns EINVAL unless `seq` is the one
+ * admitted.  Host code only (no device): the context's own sequencer orders
+ * gbgpu_allgather_topk, and a caller with its own transport may use one. */
+typedef struct gbgpu_seq gbgpu_seq;
+int gbgpu_seq_open(uint64_t first, gbgpu_seq **out);
+int gbgpu_seq_enter(gbgpu_seq *s, uint64_t seq, int timeout_ms);
+int gbgpu_seq_leave(gbgpu_seq *s, uint64_t seq);
+uint64_t gbgpu_seq_next(const gbgpu_seq *s); /* the number admitted next */
+void gbgpu_seq_close(gbgpu_seq *s);
 
 /* Msg39 -> Msg3a over RCCL: one context per GPU, each
  * holding one docid range of the index (a shard).  Rank 0 makes the id with
  * gbgpu_comm_unique_id and the caller ships it to every rank; each rank then
- * calls gbgpu_comm_init (collective).  gbgpu_allgather_topk replaces the
- * collect of a slot's enqueued query: that shard's reply -- the first
- * min(nodes, k) of its TopTree and its hit count -- is all-gathered over
- * xGMI and merged on the device by Msg3a::mergeLists' rules (Msg3a.cpp:
- * 1315-1467: score desc as double, ties to the lower docid, a docid taken
- * once, first k; the clusterdb site cap of 1342-1379 needs cluster records
- * and is not applied).  Every rank receives the same merged list and the
- * summed hit count; `local` (may be NULL) receives the shard's own result.
- * Collective: every rank calls it once per query, in the same order. */
-/* The device merge gbgpu_allgather_topk runs after its all-gather, on replies
- * given from the host (one per shard: counts[r] entries, best first, and the
- * shard's hit count); for checking the merge without a multi-GPU node. */
-int gbgpu_merge_replies_device(gbgpu_ctx *ctx, int nranks, int32_t k, const int32_t *counts, const int64_t *shard_hits,
-                               const int64_t *const *shard_docids, const float *const *shard_scores,
-                               int64_t *docids, double *scores, int32_t *n, int64_t *hits);
+ * calls gbgpu_comm_init (collective; the exchange sequence starts at 0).
+ * gbgpu_allgather_topk replaces the collect of a slot's enqueued query:
+ * that shard's reply -- the first min(nodes, k) of its TopTree as Msg39
+ * sends it (double scores: m_score, or (double)m_intScore for gbsortby int)
+ * and its hit count -- is all-gathered over xGMI and merged on the device by
+ * Msg3a::mergeLists' rules (gbgpu_merge_topk; the clusterdb site cap of
+ * Msg3a.cpp:1342-1379 needs cluster records and is not applied).  Every
+ * rank receives the same merged list and the summed hit count; `local` (may
+ * be NULL) receives the shard's own result.  `seq` is the query's exchange
+ * sequence number: the call waits (timeout_ms, as gbgpu_seq_enter) until
+ * every smaller number has been exchanged on this rank, so concurrent
+ * callers issue the collectives in the same order on every rank.  slot < 0
+ * sends an empty reply (a shard whose query failed still takes part). */
 #define GBGPU_COMM_ID_BYTES 128
 int gbgpu_comm_unique_id(uint8_t *id);
 int gbgpu_comm_init(gbgpu_ctx *ctx, int nranks, int rank, const uint8_t *id);
-int gbgpu_allgather_topk(gbgpu_ctx *ctx, int slot, int32_t k, int64_t *docids, double *scores, int32_t *n,
-                         int64_t *hits, gbgpu_result *local);
+int gbgpu_allgather_topk(gbgpu_ctx *ctx, int slot, uint64_t seq, int timeout_ms, int32_t k, int64_t *docids,
+                         double *scores, int32_t *n, int64_t *hits, gbgpu_result *local);
 
 /* RdbList::posdbMerge_r (RdbList.cpp:3065-3568), as RdbList::merge_r
  * (RdbList.cpp:1658-1756) calls it after prepareForMerge (410-491): merge n

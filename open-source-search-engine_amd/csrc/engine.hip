@@ -2805,15 +2805,17 @@ struct XHead {
   int64_t hits;
 };
 constexpr uint32_t XMAX = 4096;  // merged entries (docsToGet) the exchange handles
+// one entry of a shard's reply as Msg39 sends it: the double score
+// (Msg39.cpp:1661-1664: m_score, or (double)m_intScore with integer tree
+// scores) and the docid
 struct XRec {
-  uint32_t key;  // order-preserving float score key
-  uint32_t pad;
+  double score;
   uint64_t docid;
 };
 
 // this shard's Msg39Reply: min(nodes, docsToGet) entries of its result block
 __global__ void k_xpack(const Counters *ctr, const uint32_t *keys, const uint64_t *docs, uint32_t k, uint32_t kq,
-                        uint8_t *send) {
+                        int int_scores, uint8_t *send) {
   XHead *h = reinterpret_cast<XHead *>(send);
   XRec *r = reinterpret_cast<XRec *>(send + sizeof(XHead));
   __shared__ uint32_t s_n;
@@ -2822,8 +2824,8 @@ __global__ void k_xpack(const Counters *ctr, const uint32_t *keys, const uint64_
   const uint32_t lim = min(k, kq);
   for (uint32_t i = threadIdx.x; i < lim; i += blockDim.x) {
     const uint32_t key = keys[i];
-    r[i].key = key;
-    r[i].pad = 0;
+    const uint32_t b = (key & 0x80000000u) ? (key & 0x7fffffffu) : ~key;
+    r[i].score = int_scores ? (double)(int32_t)(key ^ 0x80000000u) : (double)__uint_as_float(b);
     r[i].docid = docs[i];
     // keys are written best first and end at the first 0 (empty) key
     if (key && (i + 1 == lim || keys[i + 1] == 0)) s_n = i + 1;
@@ -2836,14 +2838,27 @@ __global__ void k_xpack(const Counters *ctr, const uint32_t *keys, const uint64_
   }
 }
 
-// one wave: the k-way merge of the shards' replies (each sorted best first)
+// one wave: Msg3a::mergeLists' loop over the shards' replies (Msg3a.cpp:
+// 1315-1467).  Lane r < nranks holds shard r's head; the wave's reduction
+// picks what the reference's scan over j picks -- the highest double score,
+// on equal scores the lower docid, on equal docids the lower shard (a later
+// shard replaces maxj only if strictly better) -- so a reply need not be
+// sorted.  A docid already merged is passed over (htable, Msg3a.cpp:1381-
+// 1385), and the loop stops at k entries.
+__device__ __forceinline__ bool xhead_better(double s1, uint64_t d1, int l1, double s2, uint64_t d2, int l2) {
+  if (l2 >= 64) return l1 < 64;
+  if (l1 >= 64) return false;
+  if (s1 > s2) return true;
+  if (s1 < s2) return false;
+  if (d1 != d2) return d1 < d2;
+  return l1 < l2;
+}
 __global__ void __launch_bounds__(64) k_xmerge(const uint8_t *recv, int nranks, uint32_t k, size_t stride,
-                                               uint8_t *out, int int_scores) {
+                                               uint8_t *out) {
   const int lane = threadIdx.x;
   XHead *oh = reinterpret_cast<XHead *>(out);
   double *osc = reinterpret_cast<double *>(out + sizeof(XHead));
   int64_t *odoc = reinterpret_cast<int64_t *>(out + sizeof(XHead) + 8 * (size_t)k);
-  // lane r < nranks follows shard r
   uint32_t cur = 0, n = 0;
   const XRec *rr = nullptr;
   int64_t hits = 0;
@@ -2855,47 +2870,38 @@ __global__ void __launch_bounds__(64) k_xmerge(const uint8_t *recv, int nranks, 
   }
   for (int off = 32; off > 0; off >>= 1) hits += __shfl_xor(hits, off, 64);
   __shared__ uint64_t s_doc[XMAX];
-  __shared__ uint32_t s_key[XMAX];
+  __shared__ double s_sc[XMAX];
   uint32_t taken = 0;
-  for (;;) {
-    if (taken >= k) break;
-    // maxj: the shard whose head has the highest score, ties to the lower docid
+  while (taken < k) {
     const bool has = lane < nranks && cur < n;
-    const uint32_t key = has ? rr[cur].key : 0;
-    const uint64_t doc = has ? rr[cur].docid : ~0ull;
-    uint32_t bk = key;
-    uint64_t bd = doc;
+    double bs = has ? rr[cur].score : 0.0;
+    uint64_t bd = has ? rr[cur].docid : ~0ull;
     int bl = has ? lane : 64;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
-      const uint32_t ok = __shfl_xor(bk, off, 64);
+      const double os = __shfl_xor(bs, off, 64);
       const uint64_t od = __shfl_xor(bd, off, 64);
       const int ol = __shfl_xor(bl, off, 64);
-      if (ol < 64 && (bl == 64 || ok > bk || (ok == bk && (od < bd || (od == bd && ol < bl))))) {
-        bk = ok;
+      if (xhead_better(os, od, ol, bs, bd, bl)) {
+        bs = os;
         bd = od;
         bl = ol;
       }
     }
     if (bl == 64) break;  // every shard exhausted
     if (lane == bl) cur++;
-    // a docid already in the merged list is skipped (Msg3a.cpp:1381-1385)
     bool dup = false;
     for (uint32_t t = lane; t < taken; t += 64) dup |= s_doc[t] == bd;
     if (__ballot(dup)) continue;
     if (lane == 0) {
-      s_key[taken] = bk;
+      s_sc[taken] = bs;
       s_doc[taken] = bd;
     }
     wave_lds_sync();
     taken++;
   }
   for (uint32_t t = lane; t < taken; t += 64) {
-    const uint32_t bk = s_key[t];
-    const uint32_t b = (bk & 0x80000000u) ? (bk & 0x7fffffffu) : ~bk;
-    // the wire's double score (Msg3a.cpp:1443); with integer tree scores
-    // Msg39 sends (double)m_intScore (Msg39.cpp:1663-1664)
-    osc[t] = int_scores ? (double)(int32_t)(bk ^ 0x80000000u) : (double)__uint_as_float(b);
+    osc[t] = s_sc[t];
     odoc[t] = (int64_t)s_doc[t];
   }
   if (lane == 0) {
@@ -3146,6 +3152,39 @@ struct QuerySlot {
 
 constexpr int MAX_SLOTS = 64;
 
+// Exchange sequencer (gbgpu.h "Exchange ordering"): one caller at a time,
+// admitted in increasing sequence number.
+struct gbgpu_seq {
+  std::mutex mu;
+  std::condition_variable cv;
+  uint64_t next = 0;  // the number admitted next
+  bool busy = false;  // `next` has been admitted and not yet left
+};
+
+static int seq_enter(gbgpu_seq *s, uint64_t seq, int timeout_ms) {
+  std::unique_lock<std::mutex> g(s->mu);
+  if (seq < s->next || (seq == s->next && s->busy)) return EINVAL;
+  auto ready = [&] { return s->next == seq && !s->busy; };
+  if (timeout_ms < 0) {
+    s->cv.wait(g, ready);
+  } else if (!s->cv.wait_for(g, std::chrono::milliseconds(timeout_ms), ready)) {
+    return ETIMEDOUT;
+  }
+  s->busy = true;
+  return 0;
+}
+
+static int seq_leave(gbgpu_seq *s, uint64_t seq) {
+  {
+    std::lock_guard<std::mutex> g(s->mu);
+    if (!s->busy || s->next != seq) return EINVAL;
+    s->busy = false;
+    s->next++;
+  }
+  s->cv.notify_all();
+  return 0;
+}
+
 struct gbgpu_ctx {
   int device = 0;
   hipStream_t upload_stream = nullptr;
@@ -3171,6 +3210,7 @@ struct gbgpu_ctx {
   std::mutex x_mu;
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
+  gbgpu_seq xseq;  // orders gbgpu_allgather_topk across this rank's threads
   hipStream_t xstream = nullptr;
   DevBuf xsend, xrecv, xout;
   uint8_t *h_xout = nullptr;
@@ -4577,18 +4617,25 @@ int gbgpu_comm_init(gbgpu_ctx *ctx, int nranks, int rank, const uint8_t *id) {
   }
   ctx->nranks = nranks;
   ctx->rank = rank;
+  {
+    std::lock_guard<std::mutex> sg(ctx->xseq.mu);
+    ctx->xseq.next = 0;
+    ctx->xseq.busy = false;
+  }
   return 0;
 }
 
-int gbgpu_allgather_topk(gbgpu_ctx *ctx, int slot, int32_t k, int64_t *docids, double *scores, int32_t *n,
-                         int64_t *hits, gbgpu_result *local) {
-  if (!ctx || k < 1 || (uint32_t)k > XMAX || !n || !hits) return EINVAL;
-  QuerySlot *q = slot_of(ctx, slot);
-  if (!q) return EINVAL;
+// One exchange, admitted by the context's sequencer: the collectives of
+// every rank run in sequence-number order whichever thread gets here first.
+static int allgather_admitted(gbgpu_ctx *ctx, QuerySlot *q, int32_t k, int64_t *docids, double *scores, int32_t *n,
+                              int64_t *hits, gbgpu_result *local) {
   std::lock_guard<std::mutex> xg(ctx->x_mu);
   if (!ctx->comm) return EINVAL;
-  std::unique_lock<std::mutex> lk(q->mu);
-  if (!q->pending) return EINVAL;
+  std::unique_lock<std::mutex> lk;
+  if (q) {
+    lk = std::unique_lock<std::mutex>(q->mu);
+    if (!q->pending) return EINVAL;
+  }
   (void)hipSetDevice(ctx->device);
   const size_t stride = align256(sizeof(XHead) + sizeof(XRec) * (size_t)k);
   const size_t out_bytes = sizeof(XHead) + 16 * (size_t)k;
@@ -4602,24 +4649,28 @@ int gbgpu_allgather_topk(gbgpu_ctx *ctx, int slot, int32_t k, int64_t *docids, d
     ctx->h_xout_cap = out_bytes;
   }
   hipStream_t xs = ctx->xstream;
-  if (q->early) {
+  if (!q || q->early) {
     HIPCHECK(hipMemsetAsync(ctx->xsend.p, 0, sizeof(XHead), xs));  // an empty reply
   } else {
     HIPCHECK(hipStreamWaitEvent(xs, q->ev_done, 0));
     hipLaunchKernelGGL(k_xpack, dim3(1), dim3(256), 0, xs, q->res.as<Counters>(), q->res.as<uint32_t>(res_keys_off()),
-                       q->res.as<uint64_t>(res_docs_off(q->k)), (uint32_t)k, (uint32_t)q->k, ctx->xsend.as<uint8_t>());
+                       q->res.as<uint64_t>(res_docs_off(q->k)), (uint32_t)k, (uint32_t)q->k, q->int_scores ? 1 : 0,
+                       ctx->xsend.as<uint8_t>());
   }
   if (ncclAllGather(ctx->xsend.p, ctx->xrecv.p, stride, ncclUint8, ctx->comm, xs) != ncclSuccess) return GBGPU_EHIP;
   hipLaunchKernelGGL(k_xmerge, dim3(1), dim3(64), 0, xs, ctx->xrecv.as<uint8_t>(), ctx->nranks, (uint32_t)k, stride,
-                     ctx->xout.as<uint8_t>(), q->int_scores ? 1 : 0);
+                     ctx->xout.as<uint8_t>());
   HIPCHECK(hipMemcpyAsync(ctx->h_xout, ctx->xout.p, out_bytes, hipMemcpyDeviceToHost, xs));
   HIPCHECK(hipStreamSynchronize(xs));
-  // finish the slot's own query (its result block was read on the device)
-  gbgpu_result tmp;
-  std::memset(&tmp, 0, sizeof tmp);
-  int rc = collect(ctx, *q, local ? local : &tmp);
-  lk.unlock();
-  slot_released(ctx);
+  int rc = 0;
+  if (q) {
+    // finish the slot's own query (its result block was read on the device)
+    gbgpu_result tmp;
+    std::memset(&tmp, 0, sizeof tmp);
+    rc = collect(ctx, *q, local ? local : &tmp);
+    lk.unlock();
+    slot_released(ctx);
+  }
   if (rc) return rc;
   const XHead *h = reinterpret_cast<const XHead *>(ctx->h_xout);
   const double *sc = reinterpret_cast<const double *>(ctx->h_xout + sizeof(XHead));
@@ -4633,8 +4684,39 @@ int gbgpu_allgather_topk(gbgpu_ctx *ctx, int slot, int32_t k, int64_t *docids, d
   return 0;
 }
 
+int gbgpu_allgather_topk(gbgpu_ctx *ctx, int slot, uint64_t seq, int timeout_ms, int32_t k, int64_t *docids,
+                         double *scores, int32_t *n, int64_t *hits, gbgpu_result *local) {
+  if (!ctx || k < 1 || (uint32_t)k > XMAX || !n || !hits) return EINVAL;
+  QuerySlot *q = nullptr;
+  if (slot >= 0) {
+    q = slot_of(ctx, slot);
+    if (!q) return EINVAL;
+  }
+  int rc = seq_enter(&ctx->xseq, seq, timeout_ms);
+  if (rc) return rc;
+  rc = allgather_admitted(ctx, q, k, docids, scores, n, hits, local);
+  seq_leave(&ctx->xseq, seq);
+  return rc;
+}
+
+int gbgpu_seq_open(uint64_t first, gbgpu_seq **out) {
+  if (!out) return EINVAL;
+  gbgpu_seq *s = new gbgpu_seq();
+  s->next = first;
+  *out = s;
+  return 0;
+}
+int gbgpu_seq_enter(gbgpu_seq *s, uint64_t seq, int timeout_ms) { return s ? seq_enter(s, seq, timeout_ms) : EINVAL; }
+int gbgpu_seq_leave(gbgpu_seq *s, uint64_t seq) { return s ? seq_leave(s, seq) : EINVAL; }
+uint64_t gbgpu_seq_next(const gbgpu_seq *s) {
+  if (!s) return 0;
+  std::lock_guard<std::mutex> g(const_cast<gbgpu_seq *>(s)->mu);
+  return s->next;
+}
+void gbgpu_seq_close(gbgpu_seq *s) { delete s; }
+
 int gbgpu_merge_replies_device(gbgpu_ctx *ctx, int nranks, int32_t k, const int32_t *counts, const int64_t *shard_hits,
-                               const int64_t *const *shard_docids, const float *const *shard_scores,
+                               const int64_t *const *shard_docids, const double *const *shard_scores,
                                int64_t *docids, double *scores, int32_t *n, int64_t *hits) {
   if (!ctx || nranks < 1 || nranks > 64 || k < 1 || (uint32_t)k > XMAX || !counts || !n || !hits) return EINVAL;
   (void)hipSetDevice(ctx->device);
@@ -4647,10 +4729,7 @@ int gbgpu_merge_replies_device(gbgpu_ctx *ctx, int nranks, int32_t k, const int3
     h->n = m;
     h->hits = shard_hits ? shard_hits[r] : 0;
     for (int i = 0; i < m; i++) {
-      uint32_t b;
-      std::memcpy(&b, &shard_scores[r][i], 4);
-      uint32_t key = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
-      rec[i].key = key ? key : 1u;
+      rec[i].score = shard_scores[r][i];
       rec[i].docid = (uint64_t)shard_docids[r][i];
     }
   }
@@ -4666,7 +4745,7 @@ int gbgpu_merge_replies_device(gbgpu_ctx *ctx, int nranks, int32_t k, const int3
   if (hipMemcpy(din.p, recv.data(), recv.size(), hipMemcpyHostToDevice) != hipSuccess) rc = GBGPU_EHIP;
   if (!rc) {
     hipLaunchKernelGGL(k_xmerge, dim3(1), dim3(64), 0, 0, din.as<uint8_t>(), nranks, (uint32_t)k, stride,
-                       dout.as<uint8_t>(), 0);
+                       dout.as<uint8_t>());
     if (hipGetLastError() != hipSuccess || hipMemcpy(out.data(), dout.p, out_bytes, hipMemcpyDeviceToHost) != hipSuccess)
       rc = GBGPU_EHIP;
   }
@@ -4685,34 +4764,32 @@ int gbgpu_merge_replies_device(gbgpu_ctx *ctx, int nranks, int32_t k, const int3
   return 0;
 }
 
-int gbgpu_merge_topk(const int64_t *const *sd, const float *const *ss, const int32_t *cnt, int nshards, int32_t k,
+int gbgpu_merge_topk(const int64_t *const *sd, const double *const *ss, const int32_t *cnt, int nshards, int32_t k,
                      int64_t *od, double *os, int32_t *on) {
-  // Msg3a::mergeLists, Msg3a.cpp:1315-1467: repeatedly take the shard head
-  // with the max (double) score, ties -> lower docid, skip duplicate docids
+  // Msg3a::mergeLists, Msg3a.cpp:1315-1467: scanning the shards in order,
+  // a later head replaces the best one only with a higher (double) score,
+  // or an equal score and a lower docid; a docid already merged is skipped
   if (!on || nshards < 0 || k < 0) return EINVAL;
   std::vector<int32_t> cur(nshards, 0);
   std::vector<int64_t> seen;
   int32_t n = 0;
   while (n < k) {
     int best = -1;
-    double bs = 0;
-    int64_t bd = 0;
     for (int s = 0; s < nshards; s++) {
       if (cur[s] >= cnt[s]) continue;
-      double sc = (double)ss[s][cur[s]];
-      int64_t d = sd[s][cur[s]];
-      if (best < 0 || sc > bs || (sc == bs && d < bd)) {
-        best = s;
-        bs = sc;
-        bd = d;
-      }
+      if (best < 0) { best = s; continue; }
+      const double sc = ss[s][cur[s]], bs = ss[best][cur[best]];
+      if (sc < bs) continue;
+      if (sc > bs || sd[s][cur[s]] < sd[best][cur[best]]) best = s;
     }
     if (best < 0) break;
+    const int64_t bd = sd[best][cur[best]];
+    const double bsc = ss[best][cur[best]];
     cur[best]++;
     if (std::find(seen.begin(), seen.end(), bd) != seen.end()) continue;
     seen.push_back(bd);
     od[n] = bd;
-    os[n] = bs;
+    os[n] = bsc;
     n++;
   }
   *on = n;

@@ -193,7 +193,8 @@ EXPORTS = [
     "gbgpu_last_timings", "gbgpu_set_query_slots", "gbgpu_query_slots", "gbgpu_query_slot_enqueue",
     "gbgpu_query_slot_collect", "gbgpu_slot_stream", "gbgpu_slot_timings", "gbgpu_slot_stats",
     "gbgpu_bandwidth_ceiling", "gbgpu_comm_unique_id", "gbgpu_comm_init", "gbgpu_allgather_topk",
-    "gbgpu_merge_replies_device",
+    "gbgpu_merge_replies_device", "gbgpu_seq_open", "gbgpu_seq_enter", "gbgpu_seq_leave", "gbgpu_seq_next",
+    "gbgpu_seq_close",
     "gbgpu_merge_posdb_device", "gbgpu_merge_timings", "gbgpu_merge_path", "gbgpu_merge_last_key", "gb_synth_merge_runs",
     "gb_synth_lists", "gb_synth_free", "gb_synth_docid", "gb_posdb_compress", "gb_posdb_make_key",
 ]
@@ -231,7 +232,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.gbgpu_stream.restype = vp
     lib.gbgpu_last_topk_device.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(i32)]
     lib.gbgpu_merge_topk.argtypes = [ctypes.POINTER(ctypes.POINTER(i64)),
-                                     ctypes.POINTER(ctypes.POINTER(ctypes.c_float)),
+                                     ctypes.POINTER(ctypes.POINTER(ctypes.c_double)),
                                      ctypes.POINTER(i32), ctypes.c_int, i32, ctypes.POINTER(i64),
                                      ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i32)]
     lib.gbgpu_merge_posdb.argtypes = [vp, ctypes.POINTER(ListRef), ctypes.c_int, ctypes.c_int, i64, vp,
@@ -255,13 +256,21 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.gbgpu_slot_stream.restype = vp
     lib.gbgpu_slot_timings.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(i64)]
     lib.gbgpu_slot_stats.argtypes = [vp, ctypes.c_int, ctypes.POINTER(i64)]
+    lib.gbgpu_seq_open.argtypes = [ctypes.c_uint64, ctypes.POINTER(vp)]
+    lib.gbgpu_seq_enter.argtypes = [vp, ctypes.c_uint64, ctypes.c_int]
+    lib.gbgpu_seq_leave.argtypes = [vp, ctypes.c_uint64]
+    lib.gbgpu_seq_next.argtypes = [vp]
+    lib.gbgpu_seq_next.restype = ctypes.c_uint64
+    lib.gbgpu_seq_close.argtypes = [vp]
+    lib.gbgpu_seq_close.restype = None
     lib.gbgpu_comm_unique_id.argtypes = [vp]
     lib.gbgpu_comm_init.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp]
-    lib.gbgpu_allgather_topk.argtypes = [vp, ctypes.c_int, i32, ctypes.POINTER(i64), ctypes.POINTER(ctypes.c_double),
-                                         ctypes.POINTER(i32), ctypes.POINTER(i64), ctypes.POINTER(Result)]
+    lib.gbgpu_allgather_topk.argtypes = [vp, ctypes.c_int, ctypes.c_uint64, ctypes.c_int, i32, ctypes.POINTER(i64),
+                                         ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i32), ctypes.POINTER(i64),
+                                         ctypes.POINTER(Result)]
     lib.gbgpu_merge_replies_device.argtypes = [vp, ctypes.c_int, i32, ctypes.POINTER(i32), ctypes.POINTER(i64),
                                                ctypes.POINTER(ctypes.POINTER(i64)),
-                                               ctypes.POINTER(ctypes.POINTER(ctypes.c_float)),
+                                               ctypes.POINTER(ctypes.POINTER(ctypes.c_double)),
                                                ctypes.POINTER(i64), ctypes.POINTER(ctypes.c_double),
                                                ctypes.POINTER(i32), ctypes.POINTER(i64)]
     lib.gbgpu_bandwidth_ceiling.argtypes = [vp, i64, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
@@ -422,6 +431,7 @@ class Engine:
         self.ctx = ctypes.c_void_p()
         _check(self.lib.gbgpu_open(device, ctypes.byref(self.ctx)), "gbgpu_open")
         self._keep = {}
+        self._xseq = 0  # next exchange sequence number (allgather_topk)
 
     def close(self) -> None:
         if self.ctx:
@@ -567,14 +577,22 @@ class Engine:
     def comm_init(self, nranks: int, rank: int, uid: bytes) -> None:
         b = ctypes.create_string_buffer(bytes(uid), 128)
         _check(self.lib.gbgpu_comm_init(self.ctx, nranks, rank, b), "gbgpu_comm_init")
+        self._xseq = 0
 
-    def allgather_topk(self, k: int, slot: int = 0):
+    def allgather_topk(self, k: int, slot: int = 0, seq: Optional[int] = None, timeout_ms: int = -1):
         """Collects the slot's query as this shard's reply and returns the
-        Msg3a merge of every rank's reply: (docids, scores float64, total hits)."""
+        Msg3a merge of every rank's reply: (docids, scores float64, total hits).
+        seq: the query's exchange sequence number, agreed by every rank (None:
+        this engine's next, for single-threaded callers); slot < 0 sends an
+        empty reply."""
+        if seq is None:
+            seq = self._xseq
+        self._xseq = max(self._xseq, seq + 1)
         d = np.zeros(k, np.int64)
         sc = np.zeros(k, np.float64)
         n, h = ctypes.c_int32(), ctypes.c_int64()
-        _check(self.lib.gbgpu_allgather_topk(self.ctx, slot, k, d.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+        _check(self.lib.gbgpu_allgather_topk(self.ctx, slot, seq, timeout_ms,
+                                             k, d.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
                                              sc.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), ctypes.byref(n),
                                              ctypes.byref(h), None), "gbgpu_allgather_topk")
         return d[:n.value], sc[:n.value], h.value
@@ -583,15 +601,15 @@ class Engine:
         ns = len(shards)
         keep = []
         dptrs = (ctypes.POINTER(ctypes.c_int64) * ns)()
-        sptrs = (ctypes.POINTER(ctypes.c_float) * ns)()
+        sptrs = (ctypes.POINTER(ctypes.c_double) * ns)()
         cnts = (ctypes.c_int32 * ns)()
         hh = (ctypes.c_int64 * ns)(*(shard_hits or [0] * ns))
         for i, (dd, ss) in enumerate(shards):
             dd = np.ascontiguousarray(dd, dtype=np.int64)
-            ss = np.ascontiguousarray(ss, dtype=np.float32)
+            ss = np.ascontiguousarray(ss, dtype=np.float64)
             keep += [dd, ss]
             dptrs[i] = dd.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))
-            sptrs[i] = ss.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+            sptrs[i] = ss.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
             cnts[i] = len(dd)
         od = np.zeros(k, np.int64)
         osc = np.zeros(k, np.float64)
@@ -661,20 +679,52 @@ class Engine:
         return p.value, n.value
 
 
+class Seq:
+    """gbgpu_seq: admits one caller at a time in increasing sequence number
+    (include/gbgpu.h "Exchange ordering").  Host code only."""
+
+    def __init__(self, first: int = 0):
+        self.lib = load()
+        h = ctypes.c_void_p()
+        _check(self.lib.gbgpu_seq_open(first, ctypes.byref(h)), "gbgpu_seq_open")
+        self.h = h
+
+    def enter(self, seq: int, timeout_ms: int = -1) -> None:
+        _check(self.lib.gbgpu_seq_enter(self.h, seq, timeout_ms), "gbgpu_seq_enter")
+
+    def leave(self, seq: int) -> None:
+        _check(self.lib.gbgpu_seq_leave(self.h, seq), "gbgpu_seq_leave")
+
+    def next(self) -> int:
+        return int(self.lib.gbgpu_seq_next(self.h))
+
+    def close(self) -> None:
+        if self.h:
+            self.lib.gbgpu_seq_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def merge_topk(shards, k: int):
-    """Msg3a::mergeLists over [(docids int64[], scores float32[]), ...]."""
+    """Msg3a::mergeLists over [(docids int64[], scores float64[]), ...] (the
+    Msg39 reply's double scores; float32 input is widened as Msg39 does)."""
     lib = load()
     ns = len(shards)
     keep = []
     dptrs = (ctypes.POINTER(ctypes.c_int64) * max(ns, 1))()
-    sptrs = (ctypes.POINTER(ctypes.c_float) * max(ns, 1))()
+    sptrs = (ctypes.POINTER(ctypes.c_double) * max(ns, 1))()
     cnts = (ctypes.c_int32 * max(ns, 1))()
     for i, (d, s) in enumerate(shards):
         d = np.ascontiguousarray(d, dtype=np.int64)
-        s = np.ascontiguousarray(s, dtype=np.float32)
+        s = np.ascontiguousarray(s, dtype=np.float64)
         keep += [d, s]
         dptrs[i] = d.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))
-        sptrs[i] = s.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+        sptrs[i] = s.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
         cnts[i] = len(d)
     od = np.zeros(max(k, 1), dtype=np.int64)
     os_ = np.zeros(max(k, 1), dtype=np.float64)

@@ -92,6 +92,11 @@ int64_t orc_posdb_merge(const uint8_t *const *lists, const int64_t *sizes, int n
                         int remove_neg_keys, int64_t min_rec_sizes, uint8_t *out, int64_t cap);
 
 /* weight tables of initWeights (Posdb.cpp:1105-1197), for table tests */
+/* Msg3a::mergeLists (Msg3a.cpp:971-1503), no site clustering / facets:
+ * returns the merged count, or -errno; out arrays hold docs_to_get entries */
+int32_t orc_msg3a_merge(const int64_t *const *docids, const double *const *scores, const int32_t *counts,
+                        int nshards, int32_t docs_to_get, int64_t *out_docids, double *out_scores);
+
 void orc_weights(float *density32, float *wordspam16, float *linker16, float *hashgroup11,
                  float *diversity16);
 

@@ -323,6 +323,49 @@ static int64_t ref_posdb_merge(const uint8_t *const *lists, const int64_t *sizes
   return sz;
 }
 
+// Msg3a::mergeLists (Msg3a.cpp:971-1503) over n fake shard replies, as
+// Msg3a::gotAllShardReplies calls it: each reply is a Msg39Reply whose
+// ptr_docIds / ptr_scores (double, Msg39.cpp:1661-1664) are the caller's
+// arrays; no cluster recs (m_doSiteClustering off: the clusterdb site caps
+// need Msg51 recs, out of scope), no facets (a query with no terms), no
+// score info.  Output: the merged m_docIds / m_scores.
+#include "Msg3a.h"
+static int ref_msg3a_merge(int nshards, int32_t docs_to_get, const int32_t *counts,
+                           const int64_t *const *docids, const double *const *scores,
+                           std::vector<int64_t> &od, std::vector<double> &os) {
+  ref_init();
+  if (nshards < 0 || nshards > MAX_SHARDS || docs_to_get <= 0) return EINVAL;
+  static Msg3a *m = NULL;
+  static Msg39Request req;
+  static Query q;
+  static Msg39Reply rep[MAX_SHARDS];
+  if (!m) m = new Msg3a();
+  req.reset();
+  req.m_doSiteClustering = false;
+  req.m_getDocIdScoringInfo = false;
+  q.m_numTerms = 0;
+  m->m_q = &q;
+  m->m_r = &req;
+  m->m_debug = 0;
+  m->m_docsToGet = docs_to_get;
+  m->m_numHosts = nshards;
+  for (int j = 0; j < nshards; j++) {
+    Msg39Reply &r = rep[j];
+    memset((void *)&r, 0, sizeof r);
+    r.m_numDocIds = counts[j];
+    r.ptr_docIds = (char *)docids[j];
+    r.ptr_scores = (char *)scores[j];
+    r.size_docIds = 8 * counts[j];
+    r.size_scores = 8 * counts[j];
+    m->m_reply[j] = &r;
+  }
+  m->mergeLists();
+  od.assign(m->m_docIds, m->m_docIds + m->m_numDocIds);
+  os.assign(m->m_scores, m->m_scores + m->m_numDocIds);
+  for (int j = 0; j < nshards; j++) m->m_reply[j] = NULL;  // not Msg3a's to free
+  return 0;
+}
+
 // ------------------------------------------------------------------ driver
 // Binary request on stdin, response on stdout (little-endian, host layout):
 //   op=1 query: i32 nterms, orc_params (its white_lists pointer ignored), nterms x orc_qterm,
@@ -450,6 +493,37 @@ int main(int argc, char **argv) {
       wr(&sz, 8);
       if (sz > 0) wr(out.data(), sz);
       wr(&s_merge_s, 8);
+    } else if (op == 3) {
+      // Msg3a merge: i32 nshards, i32 docs_to_get, per shard i32 n,
+      // n x i64 docid, n x f64 score  ->  i32 n (or -errno), n x i64, n x f64
+      int32_t ns, dtg;
+      rd(&ns, 4);
+      rd(&dtg, 4);
+      if (ns < 0 || ns > MAX_SHARDS) return 4;
+      std::vector<int32_t> cnt(ns);
+      std::vector<std::vector<int64_t> > dd(ns);
+      std::vector<std::vector<double> > ss(ns);
+      std::vector<const int64_t *> dp(ns);
+      std::vector<const double *> sp(ns);
+      for (int j = 0; j < ns; j++) {
+        rd(&cnt[j], 4);
+        if (cnt[j] < 0) return 4;
+        dd[j].resize(cnt[j] + 1);
+        ss[j].resize(cnt[j] + 1);
+        rd(dd[j].data(), 8 * (size_t)cnt[j]);
+        rd(ss[j].data(), 8 * (size_t)cnt[j]);
+        dp[j] = dd[j].data();
+        sp[j] = ss[j].data();
+      }
+      std::vector<int64_t> od;
+      std::vector<double> os;
+      int rc = ref_msg3a_merge(ns, dtg, cnt.data(), dp.data(), sp.data(), od, os);
+      int32_t n = rc ? -rc : (int32_t)od.size();
+      wr(&n, 4);
+      if (n > 0) {
+        wr(od.data(), 8 * (size_t)n);
+        wr(os.data(), 8 * (size_t)n);
+      }
     } else {
       return 5;
     }

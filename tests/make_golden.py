@@ -392,6 +392,20 @@ def save_merge(name, runs, cases):
                         out_blob=np.frombuffer(b"".join(outs), np.uint8))
 
 
+def save_msg3a():
+    """Msg3a::mergeLists fixtures: the reference's own merge of the shard
+    reply sets in msg3a_cases.py (x_<name>.npz)."""
+    import msg3a_cases
+    for name, shards, k in msg3a_cases.cases():
+        d, s = ref.msg3a_merge(shards, k)
+        cnt = np.array([len(x[0]) for x in shards], np.int32)
+        np.savez_compressed(os.path.join(OUT, f"x_{name}.npz"), counts=cnt,
+                            docids=np.concatenate([x[0] for x in shards]).astype(np.int64),
+                            scores=np.concatenate([x[1] for x in shards]).astype(np.float64),
+                            docs_to_get=np.int32(k), exp_docids=d, exp_scores=s)
+        print(f"x_{name}: shards={len(shards)} k={k} merged={len(d)}")
+
+
 def main():
     if not ref.available():
         sys.exit("oracle/_ref/gbref missing: run `make -f oracle/ref.mk` where /root/reference exists")
@@ -429,6 +443,7 @@ def main():
     save_scoreinfo()
     save_sortby()
     save_range()
+    save_msg3a()
     cases = [(0, -1), (1, -1), (0, 5000), (1, 5000), (0, 1)]
     for seed, (keys, nterms) in enumerate([(4000, 50), (12000, 3), (8000, 1)]):
         save_merge(f"tiered_s{seed}", tiered_runs(keys, seed=seed, nterms=nterms), cases)
@@ -451,5 +466,7 @@ if __name__ == "__main__":
         save_sortby()
     elif sys.argv[1:] == ["range"]:
         save_range()
+    elif sys.argv[1:] == ["msg3a"]:
+        save_msg3a()
     else:
         main()

@@ -35,6 +35,11 @@ def lib():
                                          ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p,
                                          ctypes.c_int64]
         _lib.orc_posdb_merge.restype = ctypes.c_int64
+        _lib.orc_msg3a_merge.argtypes = [ctypes.POINTER(ctypes.POINTER(ctypes.c_int64)),
+                                         ctypes.POINTER(ctypes.POINTER(ctypes.c_double)),
+                                         ctypes.POINTER(ctypes.c_int32), ctypes.c_int, ctypes.c_int32,
+                                         ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double)]
+        _lib.orc_msg3a_merge.restype = ctypes.c_int32
     return _lib
 
 
@@ -78,3 +83,27 @@ def weights():
             np.zeros(11, np.float32), np.zeros(16, np.float32)]
     lib().orc_weights(*[a.ctypes.data_as(ctypes.POINTER(ctypes.c_float)) for a in arrs])
     return dict(density=arrs[0], wordspam=arrs[1], linker=arrs[2], hashgroup=arrs[3], diversity=arrs[4])
+
+
+def msg3a_merge(shards, docs_to_get):
+    """oracle/msg3a_oracle.c: Msg3a::mergeLists over [(docids, scores float64), ...]."""
+    L = lib()
+    ns = len(shards)
+    keep = []
+    dp = (ctypes.POINTER(ctypes.c_int64) * max(ns, 1))()
+    sp = (ctypes.POINTER(ctypes.c_double) * max(ns, 1))()
+    cnt = (ctypes.c_int32 * max(ns, 1))()
+    for i, (d, s) in enumerate(shards):
+        d = np.ascontiguousarray(d, np.int64)
+        s = np.ascontiguousarray(s, np.float64)
+        keep += [d, s]
+        dp[i] = d.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))
+        sp[i] = s.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+        cnt[i] = len(d)
+    od = np.zeros(max(docs_to_get, 1), np.int64)
+    os_ = np.zeros(max(docs_to_get, 1), np.float64)
+    n = L.orc_msg3a_merge(dp, sp, cnt, ns, docs_to_get, od.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                          os_.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+    if n < 0:
+        raise RuntimeError(f"orc_msg3a_merge rc={n}")
+    return od[:n].copy(), os_[:n].copy()

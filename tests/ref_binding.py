@@ -107,3 +107,24 @@ def posdb_merge(lists, remove_neg_keys, min_rec_sizes=-1, timed=False):
     if timed:
         return out, sec
     return out
+
+
+def msg3a_merge(shards, docs_to_get):
+    """The reference's own Msg3a::mergeLists (Msg3a.cpp:971-1503) over
+    [(docids int64[], scores float64[]), ...] replies; no site clustering.
+    Returns (docids int64[], scores float64[])."""
+    p = _p()
+    req = [struct.pack("<iii", 3, len(shards), docs_to_get)]
+    for d, s in shards:
+        d = np.ascontiguousarray(d, np.int64)
+        s = np.ascontiguousarray(s, np.float64)
+        assert len(d) == len(s)
+        req += [struct.pack("<i", len(d)), d.tobytes(), s.tobytes()]
+    p.stdin.write(b"".join(req))
+    p.stdin.flush()
+    (n,) = struct.unpack("<i", _read(4))
+    if n < 0:
+        raise RuntimeError(f"gbref msg3a rc={-n}")
+    d = np.frombuffer(_read(8 * n), np.int64).copy()
+    s = np.frombuffer(_read(8 * n), np.float64).copy()
+    return d, s

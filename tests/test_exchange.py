@@ -1,51 +1,45 @@
 """Msg39 -> Msg3a exchange through the C ABI on the GPU.
 
 gbgpu_allgather_topk all-gathers every shard's reply over RCCL and merges
-them on the device by Msg3a::mergeLists' rules (Msg3a.cpp:1315-1467).  One
-GPU box cannot run several ranks, so the device merge is checked on its own
-against the host restatement (gbgpu_merge_topk) for 1-8 shards with ties and
-duplicate docids, and the whole collective runs as a one-rank communicator.
-The multi-rank exchange semantics are covered on CPU (test_shards_gloo.py)."""
+them on the device (k_xmerge) by Msg3a::mergeLists' rules (Msg3a.cpp:
+971-1503).  One GPU box cannot run several ranks, so the device merge is
+checked on its own (gbgpu_merge_replies_device) against the reference's own
+mergeLists (tests/golden/x_*.npz) and against the oracle restatement on
+seeded reply sets, and the whole collective runs as a one-rank communicator.
+The multi-rank ordering (gbgpu_seq) is covered on CPU (test_shards_gloo.py)."""
 import numpy as np
 import pytest
 
 import gbgpu
+import msg3a_cases
 import oracle_binding as orc
 import qkinds
+from test_msg3a import FIX, load_fixture, same
 from workload import generate
 
 pytestmark = pytest.mark.gpu
 
 
-def random_replies(rng, nranks, k, ties, dup):
-    shards = []
-    pool = rng.choice(1 << 38, size=nranks * k * 2, replace=False)
-    for r in range(nranks):
-        n = int(rng.integers(0, k + 1))
-        sc = np.sort(rng.choice(np.arange(1, 50 if ties else 100000), size=n).astype(np.float32))[::-1]
-        dd = pool[r * 2 * k:r * 2 * k + n].copy()
-        if dup and r > 0 and n:
-            m = int(rng.integers(0, n))
-            dd[:m] = shards[0][0][:m] if len(shards[0][0]) >= m else dd[:m]
-            sc[:m] = shards[0][1][:m] if len(shards[0][1]) >= m else sc[:m]
-        # each reply sorted best first: score desc, docid asc
-        o = np.lexsort((dd, -sc.astype(np.float64)))
-        shards.append((dd[o], sc[o]))
-    return shards
+@pytest.mark.parametrize("path", FIX, ids=[p.rsplit("/", 1)[1][:-4] for p in FIX])
+def test_device_merge_matches_reference_fixture(engine, path):
+    shards, k, ed, es = load_fixture(path)
+    hits = list(range(1, len(shards) + 1))
+    d, s, h = engine.merge_replies_device(shards, k, hits)
+    assert h == sum(hits)
+    assert same(d, s, ed, es)
 
 
-@pytest.mark.parametrize("nranks", [1, 2, 3, 8])
-@pytest.mark.parametrize("ties,dup", [(False, False), (True, False), (True, True)])
-def test_device_merge_matches_msg3a(engine, nranks, ties, dup):
-    rng = np.random.default_rng(nranks * 7 + ties * 3 + dup)
-    for k in (1, 10, 100, 300):
-        shards = random_replies(rng, nranks, k, ties, dup)
-        hits = [int(x) for x in rng.integers(0, 1 << 40, nranks)]
-        d, s, h = engine.merge_replies_device(shards, k, hits)
-        ed, es = gbgpu.merge_topk(shards, k)
-        assert h == sum(hits)
-        assert np.array_equal(d, ed), (nranks, k)
-        assert np.array_equal(s, es), (nranks, k)
+@pytest.mark.parametrize("nranks", [1, 2, 3, 8, 64])
+def test_device_merge_matches_oracle(engine, nranks):
+    rng = np.random.default_rng(nranks * 7)
+    for it, k in enumerate((1, 10, 100, 300, 4096)):
+        shards = msg3a_cases.partitioned(rng, nranks, int(rng.integers(0, 200)), int(rng.integers(1, 40)),
+                                         int_scores=bool(it % 2))
+        if it == 3:  # replicas
+            shards = (shards + shards)[:max(nranks, 2)]
+        ed, es = orc.msg3a_merge(shards, k)
+        d, s, _ = engine.merge_replies_device(shards, k, [0] * len(shards))
+        assert same(d, s, ed, es), (nranks, k)
 
 
 def test_allgather_topk_one_rank():
@@ -61,6 +55,8 @@ def test_allgather_topk_one_rank():
             eng.enqueue(q.terms, hs, p, slot=0)
             d, s, h = eng.allgather_topk(k, slot=0)
             m = min(k, len(exp["docids"]))
+            ed, es = orc.msg3a_merge([(exp["docids"][:m], exp["scores"][:m].astype(np.float64))], k)
+            assert same(d, s, ed, es)
             assert h == exp["hits"]
             assert np.array_equal(d, exp["docids"][:m])
             assert np.array_equal(s, exp["scores"][:m].astype(np.float64))
@@ -83,3 +79,9 @@ def test_allgather_topk_one_rank():
         eng.enqueue(q.terms, hs2, p, slot=0)
         d, s, h = eng.allgather_topk(10, slot=0)
         assert len(d) == 0 and h == 0
+        # a shard with no query of its own (slot < 0) sends an empty reply
+        d, s, h = eng.allgather_topk(10, slot=-1)
+        assert len(d) == 0 and h == 0
+        # sequence numbers: an explicit number already past is refused
+        with pytest.raises(gbgpu.GbgpuError):
+            eng.allgather_topk(10, slot=-1, seq=0, timeout_ms=0)

@@ -6,8 +6,9 @@
   score bits; also with site clustering (the Msg39Request default);
 * config 3: the bench's ten 3-5 word queries (config3_queries(1e8, seed=3),
   628 MB of lists each on average);
-* config 4: 125M-doc shards of the 1B-doc index (docid-range sharding), each
-  shard checked on its own, then the Msg3a merge of the shards' top lists;
+* config 4: all eight 125M-doc shards of the 1B-doc index (docid-range
+  sharding), each checked on its own, then the device Msg3a merge of their
+  replies against the oracle's mergeLists and the unsharded query;
 * config 5: the 4.4 GB eight-run merge, output bytes vs the oracle.
 
 The oracle runs at ~1 GB/s of lists, so each case costs a few seconds."""
@@ -69,21 +70,31 @@ def test_config3_bench_queries(engine, k):
 
 
 def test_config4_shards_and_merge(engine):
-    # 1B docs, docid-range shards of 125M docs (one per GPU on the 8-GPU node);
-    # two shards here (first and last), each bit-exact, then Msg3a's merge
+    # 1B docs, docid-range shards of 125M docs (one per GPU on the 8-GPU node):
+    # all 8 shards in turn on this GPU, each bit-exact against the oracle, then
+    # the device Msg3a merge (k_xmerge, the kernel gbgpu_allgather_topk runs
+    # after its all-gather) of the 8 replies == the oracle's mergeLists of
+    # them == the unsharded 1B-doc query's top 100 and hit count
     total, per = 1_000_000_000, 125_000_000
     q = config_two_term(total, docs_to_get=100, seed=1)
-    shards = []
-    for r in (0, 7):
+    p = q.params()
+    replies, hits = [], []
+    for r in range(8):
         lists = generate(q, total, doc_begin=r * per, doc_end=(r + 1) * per, threads=16)
-        res = resident(engine, lists, q.terms, q.params())
-        check_full(res, q.terms, lists, q.params(), f"config4 shard {r}")
-        shards.append((res.docids, res.scores))
-    d, s = gbgpu.merge_topk(shards, 100)
-    alld = np.concatenate([x[0] for x in shards])
-    alls = np.concatenate([x[1] for x in shards]).astype(np.float64)
-    order = np.lexsort((alld, -alls))[:100]
-    assert np.array_equal(d, alld[order]) and np.array_equal(s, alls[order])
+        res = resident(engine, lists, q.terms, p)
+        check_full(res, q.terms, lists, p, f"config4 shard {r}")
+        n = min(len(res.docids), p.docs_to_get)
+        replies.append((res.docids[:n], res.scores[:n].astype(np.float64)))
+        hits.append(res.hits)
+        del lists
+    d, s, h = engine.merge_replies_device(replies, 100, hits)
+    ed, es = orc.msg3a_merge(replies, 100)
+    assert np.array_equal(d, ed) and np.array_equal(s, es)
+    full = generate(q, total, threads=16)
+    exp = orc.query(q.terms, full, p, cap=1 << 12)
+    assert h == exp["hits"]
+    assert np.array_equal(d, exp["docids"][:100])
+    assert np.array_equal(s, exp["scores"][:100].astype(np.float64))
 
 
 @pytest.mark.parametrize("path", ["decoded", "tiles"])
