@@ -91,7 +91,7 @@ struct ListExt {
 struct Counters {
   uint32_t filtered;  // m_filtered: scored docids dropped by the paging filter (Posdb.cpp:7327-7347)
   uint32_t corrupt;
-  unsigned long long surv_top;  // k_compact's packed bump pointer: survivors << 36 | arena units
+  unsigned long long surv_top;  // survivors << 36 | their run units (k_cmp_scan)
   uint32_t g0count[MAXG0];
   uint32_t anysurv;  // bit l: list l has a run in some survivor
   uint32_t tree_n;   // site clustering: TopTree nodes written by k_tree_replay
@@ -100,8 +100,9 @@ struct Counters {
   uint32_t pad[2];
   unsigned long long dmax_all;  // largest survivor docid
   ListExt ext[MAXL];
-  uint32_t bcnt[8];  // survivors per size bucket (k_compact), NBKT
-  uint32_t pad2[8];
+  uint32_t bcnt[8];    // survivors per size bucket (k_cmp_scan), NBKT
+  uint32_t bstart[8];  // each bucket's first survivor position
+  unsigned long long arena_top;  // global record arena: units handed out (k_ext_walk, k_score, k_scoreinfo)
 };
 
 // radix-select state (3 passes over the 32-bit score keys: 12+12+8 bits)
@@ -229,10 +230,11 @@ __device__ __forceinline__ uint32_t run_end(const DevList &L, uint32_t e) {
   return e;
 }
 
-__global__ void k_reset(uint32_t *a, uint32_t na, uint32_t *b, uint32_t nb) {
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < na + nb; i += gridDim.x * blockDim.x) {
+__global__ void k_reset(uint32_t *a, uint32_t na, uint32_t *b, uint32_t nb, uint32_t *c = nullptr, uint32_t nc = 0) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < na + nb + nc; i += gridDim.x * blockDim.x) {
     if (i < na) a[i] = 0;
-    else b[i - na] = 0;
+    else if (i < na + nb) b[i - na] = 0;
+    else c[i - na - nb] = 0;
   }
 }
 
@@ -312,14 +314,15 @@ __device__ bool run_in_range_first(const DevList &L, uint32_t u, uint32_t e) {
   return false;
 }
 
-// Writes every candidate slot of every array (docid; list mask = the array's
-// own list bit for array 0, which is never probed, else 0 -- so no per-query
-// clear of the mask is needed) and array 0's run locations.
+// Writes every candidate slot of every array: its docid, the unit of its run
+// start in the array's own list (cunit: array 0's run locations, whose run
+// ends where the next candidate's starts), the directory, and the
+// whitelist / range-term rejections.  Match state lives in per-list bitmaps
+// (k_probe) cleared by k_reset, so no per-slot mask is written here.
 __global__ void __launch_bounds__(BLOCK) k_write_runs(const DevPlan *pl, const G0Chunk *chunks,
                                                       const uint32_t *chunk_off,
                                                       const uint32_t *array_first_chunk,
-                                                      uint64_t *cand, uint32_t *lmask, Loc *loc,
-                                                      uint32_t *ulen, uint64_t slot_ub, Counters *ctr,
+                                                      uint64_t *cand, uint32_t *cunit, Counters *ctr,
                                                       uint32_t nchunks, uint64_t *dir) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[CHUNK_LOAD];
   __shared__ uint32_t tmp[BLOCK / 64];
@@ -342,10 +345,6 @@ __global__ void __launch_bounds__(BLOCK) k_write_runs(const DevPlan *pl, const G
   // offset inside this array = global prefix - prefix at the array's first chunk
   const uint32_t arr_base_off = chunk_off[array_first_chunk[c.array]];
   const uint64_t base = pl->g0base[c.array];
-  const bool own = (c.array == 0);
-  const uint32_t own_bit = 1u << lid;
-  const uint32_t own_mult = __popc(L.group_bits & pl->pos_mask & ~NEG_BIT);
-  Loc *loc_l = loc + (uint64_t)lid * slot_ub;
   uint64_t *dir_a = dir + pl->g0dir[c.array];
   const uint64_t dmin = pl->g0dmin[c.array];
   const uint32_t sh = pl->g0sh[c.array];
@@ -359,6 +358,7 @@ __global__ void __launch_bounds__(BLOCK) k_write_runs(const DevPlan *pl, const G
     const uint64_t slot = base + p2;
     const uint64_t d = unit_docid(lds + lu * 6);
     cand[slot] = d;
+    cunit[slot] = c.u0 + lu;
     // directory: the first candidate of each bucket within this chunk (a
     // bucket straddling two chunks gets two writers; either names it)
     const uint64_t bkt = (d - dmin) >> sh;
@@ -378,17 +378,12 @@ __global__ void __launch_bounds__(BLOCK) k_write_runs(const DevPlan *pl, const G
       }
       rej = !(lo < pl->nwhite && pl->white[lo] == x);
     }
-    lmask[slot] = own ? own_bit : 0u;
-    uint32_t ul = 0;
-    if (own) {
+    if (c.array == 0 && L.rmode) {
       const uint32_t u = c.u0 + lu;
       const uint32_t e = (o2 + 1 < tot) ? c.u0 + rs_unit[o2 + 1] : run_end(L, u + 2);
-      loc_l[slot] = Loc{u, e - u};
-      ul = (e - u) * own_mult;
-      if (L.rmode && !run_in_range_first(L, u, e)) rej = true;  // Posdb.cpp:5249-5277, 5297
+      if (!run_in_range_first(L, u, e)) rej = true;  // Posdb.cpp:5249-5277, 5297
     }
     if (pl->use_rej) pl->wrej[slot] = rej;
-    ulen[slot] = ul;
   }
   // the last chunk of each array publishes the array's count
   const bool last = (blockIdx.x + 1 == nchunks) || (chunks[blockIdx.x + 1].array != c.array);
@@ -545,10 +540,10 @@ struct ProbeLds {
 };
 
 struct ProbeOut {
-  uint32_t *lmask;
-  uint32_t *ulen;
-  Loc *loc_l;
-  uint32_t bit, mult;
+  uint32_t *bits;  // list l's match bitmap (bit s of word s >> 5: slot s)
+  Loc *loc;        // run locations, [slot][nl]
+  uint32_t nl, l;
+  int on;          // 0: diagnostic GBGPU_PROBE_MODE=5, matches not published
 };
 
 // append up to 64 matches (one per lane), wave-wide
@@ -564,23 +559,38 @@ __device__ __forceinline__ void mbuf_push(ProbeLds &S, uint32_t &nbuf, bool hit,
   nbuf += (uint32_t)__popcll(m);
 }
 
-// publish buffered matches: run location, arena units, list bit
+// publish buffered matches: each run location, and the list's bit of each
+// slot -- the bits of consecutive matches in one bitmap word are OR-ed over
+// the wave first (a segmented reduction; buffered slots ascend within each
+// candidate array), so one atomicOr goes out per word and batch
 // (out of line, with every argument by value: a by-reference counter would
 // live in scratch, and scratch loads wait on vmcnt like any global load)
-__device__ __noinline__ void mbuf_flush_n(ProbeLds *S, uint32_t nbuf, uint32_t *lmask, uint32_t *ulen, Loc *loc_l,
-                                          uint32_t bit, uint32_t mult, int lane) {
+__device__ __noinline__ void mbuf_flush_n(ProbeLds *S, uint32_t nbuf, uint32_t *bits, Loc *loc, uint32_t nl,
+                                          uint32_t l, int on, int lane) {
   wave_lds_sync();
-  if (!bit) nbuf = 0;  // diagnostic (GBGPU_PROBE_MODE=5): matches not published
-  for (uint32_t i = lane; i < nbuf; i += 64) {
-    const uint32_t slot = S->mslot[i], len = S->mlen[i];
-    loc_l[slot] = Loc{S->mu[i], len};
-    if (mult) atomicAdd(&ulen[slot], len * mult);
-    atomicOr(&lmask[slot], bit);
+  if (!on) nbuf = 0;  // diagnostic (GBGPU_PROBE_MODE=5): matches not published
+  for (uint32_t i0 = 0; i0 < nbuf; i0 += 64) {
+    const uint32_t i = i0 + lane;
+    const bool act = i < nbuf;
+    const uint32_t slot = act ? S->mslot[i] : 0xffffffffu;
+    if (act) loc[(uint64_t)slot * nl + l] = Loc{S->mu[i], S->mlen[i]};
+    const uint32_t word = slot >> 5;
+    uint32_t v = act ? 1u << (slot & 31) : 0u;
+    const uint32_t wprev = __shfl_up(word, 1, 64);
+    const bool head = act && (lane == 0 || wprev != word);
+    const uint64_t H = __ballot(head);
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t vv = __shfl_down(v, off, 64);
+      // lane + off is in this lane's segment: no head in (lane, lane + off]
+      if (lane + off < 64 && !(H & (((1ull << off) - 1) << (lane + 1)))) v |= vv;
+    }
+    if (head) atomicOr(&bits[word], v);
   }
   wave_lds_sync();
 }
 __device__ __forceinline__ void mbuf_flush(ProbeLds &S, uint32_t &nbuf, const ProbeOut &o, int lane) {
-  mbuf_flush_n(&S, nbuf, o.lmask, o.ulen, o.loc_l, o.bit, o.mult, lane);
+  mbuf_flush_n(&S, nbuf, o.bits, o.loc, o.nl, o.l, o.on, lane);
   nbuf = 0;
 }
 
@@ -706,7 +716,7 @@ __device__ void probe_by_cand(const DevPlan *pl, const ProbeWork &w, const DevLi
     const WChunk cur = c0;
     c0 = c1;
     if (MODE == 2) {
-      if (cur.v[0].x == 0x557713eeu && cur.v[1].y == 7u && cur.v[2].z == 3u) po.lmask[0] = 1;
+      if (cur.v[0].x == 0x557713eeu && cur.v[1].y == 7u && cur.v[2].z == 3u) po.bits[0] = 1;
       wchunk_fetch(lp, min(u0 + 2 * WCH_UNITS, last_u0), lane, c1);
       continue;
     }
@@ -717,7 +727,7 @@ __device__ void probe_by_cand(const DevPlan *pl, const ProbeWork &w, const DevLi
       pend_slot = ~0ull;
     }
     if (MODE == 1) {
-      if (nrun && S.doc[0] == 0x123456789ull) po.lmask[0] = 1;
+      if (nrun && S.doc[0] == 0x123456789ull) po.bits[0] = 1;
       wchunk_fetch(lp, min(u0 + 2 * WCH_UNITS, last_u0), lane, c1);
       continue;
     }
@@ -887,9 +897,8 @@ __device__ void probe_by_run(const DevPlan *pl, const ProbeWork &w, const DevLis
 // compaction, 2 load chunks only, 3 skip the run-driven lists.
 template <int MODE, int G0>
 __global__ void __launch_bounds__(64 * PW) k_probe(const DevPlan *pl, const ProbeWork *work, uint32_t nwork,
-                                                   const uint64_t *cand, uint32_t *lmask, Loc *loc,
-                                                   uint32_t *ulen, uint64_t slot_ub, const Counters *ctr,
-                                                   const uint64_t *dir) {
+                                                   const uint64_t *cand, uint32_t *bits, uint32_t nwords, Loc *loc,
+                                                   const Counters *ctr, const uint64_t *dir) {
   __shared__ ProbeLds s_lds[PW];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const uint32_t wi = blockIdx.x * PW + wid;
@@ -897,13 +906,11 @@ __global__ void __launch_bounds__(64 * PW) k_probe(const DevPlan *pl, const Prob
   const ProbeWork w = work[wi];
   const DevList &L = pl->lists[w.list];
   ProbeOut po;
-  po.lmask = lmask;
-  po.ulen = ulen;
-  po.loc_l = loc + (uint64_t)w.list * slot_ub;
-  po.bit = MODE == 5 ? 0u : 1u << w.list;
-  // arena units this list adds per matched run: one copy per positive group
-  // it belongs to (a shared bigram sublist is merged into both groups)
-  po.mult = __popc(L.group_bits & pl->pos_mask & ~NEG_BIT);
+  po.bits = bits + (uint64_t)w.list * nwords;
+  po.loc = loc;
+  po.nl = (uint32_t)pl->nlists;
+  po.l = w.list;
+  po.on = MODE == 5 ? 0 : 1;
   if (L.probe == PROBE_BY_RUN) {
     if (MODE == 0) probe_by_run<G0>(pl, w, L, cand, ctr, dir, s_lds[wid], po, lane);
   } else {
@@ -914,154 +921,215 @@ __global__ void __launch_bounds__(64 * PW) k_probe(const DevPlan *pl, const Prob
 // A range term's list in a later group votes a docid only if a key of its
 // run holds a number in range (Posdb.cpp:5115-5121): k_probe publishes every
 // run it matches, and this pass (launched only for such queries) withdraws
-// the out-of-range ones -- their list bit and arena units.
-__global__ void k_range_filter(const DevPlan *pl, const Counters *ctr, uint32_t rbits, uint32_t *lmask, uint32_t *ulen,
-                               const Loc *loc, uint64_t slot_ub) {
-  for (uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; s < slot_ub;
-       s += (uint64_t)gridDim.x * blockDim.x) {
-    // only written slots: each candidate array fills [g0base, g0base + g0count)
-    int a = 0;
-    while (a + 1 < pl->g0n && s >= pl->g0base[a + 1]) a++;
-    if (s - pl->g0base[a] >= ctr->g0count[a]) continue;
-    const uint32_t lm = lmask[s];
-    uint32_t hit = lm & rbits;
-    if (!hit) continue;
-    uint32_t drop = 0, du = 0;
-    for (; hit; hit &= hit - 1) {
-      const int l = __ffs(hit) - 1;
+// the out-of-range ones from the list's bitmap.  One thread per bitmap word
+// (32 slots), so no atomics: the probe is over.
+__global__ void k_range_filter(const DevPlan *pl, uint32_t rbits, uint32_t *bits, uint32_t nwords, const Loc *loc) {
+  const uint32_t nl = (uint32_t)pl->nlists;
+  for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < nwords; w += gridDim.x * blockDim.x) {
+    for (uint32_t rb = rbits; rb; rb &= rb - 1) {
+      const int l = __ffs(rb) - 1;
       const DevList &L = pl->lists[l];
-      const Loc lc = loc[(uint64_t)l * slot_ub + s];
-      if (lc.len < 2 || (uint64_t)lc.unit + lc.len > L.units || !run_in_range(L, lc.unit, lc.unit + lc.len)) {
-        drop |= 1u << l;
-        du += lc.len * (uint32_t)__popc(L.group_bits & pl->pos_mask & ~NEG_BIT);
+      uint32_t *bw = bits + (uint64_t)l * nwords + w;
+      const uint32_t v = *bw;
+      uint32_t keep = v;
+      for (uint32_t x = v; x; x &= x - 1) {
+        const uint64_t s = (uint64_t)w * 32 + (uint32_t)(__ffs(x) - 1);
+        const Loc lc = loc[s * nl + l];
+        if (lc.len < 2 || (uint64_t)lc.unit + lc.len > L.units || !run_in_range(L, lc.unit, lc.unit + lc.len))
+          keep &= ~(1u << (s & 31));
       }
-    }
-    if (drop) {
-      lmask[s] = lm & ~drop;
-      ulen[s] -= du;
+      if (keep != v) *bw = keep;
     }
   }
 }
 
 // ------------------------------------------------------------- compaction
-constexpr int CSPT = 16;                        // compaction slots per thread
-constexpr int CBLOCK = 1024;                     // compaction threads per block
-constexpr int CTILE = CBLOCK * CSPT;             // 16384 slots per block (few blocks: few global atomics)
-
-// Survivors of one contiguous tile of candidate slots (slot = tile base +
-// q*BLOCK + thread: coalesced), appended with ONE pair of atomics per block
-// (a single device counter cannot take one atomic per wave:
-// MI355X_MICROARCH.md "dequeue" row, ~88 per us per word).  A slot's groups
-// are the union of its lists' group bits; its mini-merge arena size is the
-// sum of its runs' lengths (every group instance of a list counts, as the
-// reference merges a shared bigram sublist into both groups).  The shrunk-
-// sublist-non-empty flags (shrinkSubLists, Posdb.cpp:5334-5428) are a list
-// bitmask OR-reduced in the block and published with one atomic.
+// Survivors: candidates whose lists cover every positive group and no
+// negative one (the final m_docIdVoteBuf, Posdb.cpp:5154-5171), plus the
+// shrunk-sublist non-empty flags (shrinkSubLists, Posdb.cpp:5334-5428).
+// A slot's list mask is its array's own list (array 0 only: a later array's
+// slot is voted by its own list only through the probe, which credits a
+// docid to the first array holding it) and its bits in the probe bitmaps.
 //
-// ORDERED (site clustering, whose TopTree replay walks the survivors in docid
-// order like the vote buffer, Posdb.cpp:6137-6140): two launches instead of
-// the bump pointer -- CMODE 1 publishes each block's totals (blk[]), a one-
-// block scan (k_compact_scan) turns them into offsets, and CMODE 2 writes
-// the survivors at them, so survivors come out in slot order.
-struct BlkTot {
-  uint32_t n, pad;
-  unsigned long long u;
-};
-
-// Survivors are also counted by size (their run units, an upper bound on
-// their records) so k_score can give each wave survivors of one size: a
-// wave's lanes run the scorers in lockstep, so its time is its largest
-// lane's.  Bucket 0 holds the largest and is scored first.
-// Buckets 0-2 (more units than a lane's rc records) are scored 8, 16 and 32
-// to a wave, so each survivor gets 8, 4 or 2 lanes' worth of LDS records.
+// Two passes over the slots, CB threads x CSPT consecutive slots a block:
+//   k_cmp_count  survivors per size bucket of each block, the lists with a
+//                run in some survivor, the re-shrink partials (BlkInfo);
+//   k_cmp_scan   one block: each bucket's start, each block's offset in
+//                every bucket, the totals;
+//   k_cmp_write  every survivor's record at its final position -- buckets
+//                in order, slot order inside a bucket: slot, list mask, run
+//                units, docid, and its run locations ([pos][nl]), so k_score
+//                reads its survivors' data contiguously.
+// Survivors are counted by size (their run units, an upper bound on their
+// records) so k_score can give each wave survivors of one size: a wave's
+// lanes run the scorers in lockstep, so its time is its largest lane's.
+// Bucket 0 holds the largest and is scored first.  Buckets 0-2 (more units
+// than a lane's rc records) are scored 8, 16 and 32 to a wave, so each
+// survivor gets 8, 4 or 2 lanes' worth of LDS records.  ORDERED (site
+// clustering: the TopTree replay walks survivors in docid order, Posdb.cpp:
+// 6137-6140) puts every survivor in one bucket, in slot order.
 constexpr int NBKT = 8;
 __host__ __device__ __forceinline__ int size_bucket(uint32_t u, uint32_t rc) {
   return u > 4 * rc ? 0 : u > 2 * rc ? 1 : u > rc ? 2 : 2 * u > rc ? 3 : 3 * u > rc ? 4 : 4 * u > rc ? 5 : 6 * u > rc ? 6 : 7;
 }
 __host__ __device__ __forceinline__ int bucket_shift(int b) { return b == 0 ? 3 : b == 1 ? 4 : b == 2 ? 5 : 6; }
 
-template <int CMODE>
-__global__ void __launch_bounds__(CBLOCK) k_compact(const DevPlan *pl, const uint32_t *lmask, const uint32_t *ulen,
-                                                   uint64_t slot_ub, Counters *ctr, uint32_t *surv,
-                                                   unsigned long long *surv_off, uint32_t *surv_lm, BlkTot *blk,
-                                                   const Loc *loc, const uint64_t *cand, uint32_t *surv_u,
-                                                   uint32_t rc, uint32_t *perm) {
-  __shared__ uint32_t tmp[CBLOCK / 64];
-  __shared__ uint32_t s_bcnt[NBKT], s_bbase[NBKT], s_bcur[NBKT];
-  __shared__ uint32_t s_xu[MAXL];            // CMODE 0/1: re-shrunk lists' survivor run units
-  __shared__ unsigned long long s_xd[MAXL];  // ... and their last survivor docid
-  __shared__ unsigned long long s_dall;
-  __shared__ uint32_t s_base_i;
+constexpr int CB = 256;            // compaction threads per block
+constexpr int CSPT = 8;            // consecutive slots per thread (a quarter bitmap word)
+constexpr int CTILE = CB * CSPT;   // 2048 slots per block
+constexpr int XR = 4;              // re-shrunk lists reduced per block (more: global atomics)
+
+struct BlkInfo {
+  uint32_t cnt[NBKT];  // survivors per bucket; k_cmp_scan turns them into the block's offsets
+  uint32_t any, pad;   // lists with a run in some survivor of the block
+  unsigned long long usum;       // the survivors' run units (their records' upper bound)
+  unsigned long long dall;       // largest survivor docid (re-shrink queries)
+  unsigned long long xu[XR];     // re-shrunk list r: its runs' units over the block's survivors
+  unsigned long long xd[XR];     // ... and the last survivor docid with a run in it
+};
+
+// bit l: list l holds the docid of slot s (array a's slot)
+__device__ __forceinline__ uint32_t slot_lmask(const DevPlan *pl, const uint32_t *bits, uint32_t nwords, uint64_t s,
+                                               int a) {
+  uint32_t lm = a == 0 ? 1u << pl->g0list[0] : 0u;
+  for (uint32_t pm = pl->probed_mask; pm; pm &= pm - 1) {
+    const int l = __ffs(pm) - 1;
+    lm |= ((bits[(uint64_t)l * nwords + (s >> 5)] >> (s & 31)) & 1u) << l;
+  }
+  return lm;
+}
+// slot s's run in list l (l in its mask): array 0's own list from the
+// candidates' run starts (a run ends where the next one starts), the others
+// as k_probe recorded them
+__device__ __forceinline__ Loc slot_loc(const DevPlan *pl, const Counters *ctr, const uint32_t *cunit, const Loc *loc,
+                                        uint64_t s, int l) {
+  if (l == pl->g0list[0] && s < pl->g0base[1]) {
+    const uint32_t u = cunit[s];
+    const uint32_t e = s + 1 < pl->g0base[0] + ctr->g0count[0] ? cunit[s + 1] : pl->lists[l].units;
+    return Loc{u, e - u};
+  }
+  return loc[s * (uint32_t)pl->nlists + l];
+}
+// a docid survives when a list of every positive group and none of a
+// negative group holds it: a loop over the (wave-uniform) groups' list masks
+__device__ __forceinline__ bool lm_survives(const DevPlan *pl, uint32_t lm) {
+  if (lm & pl->neg_lists) return false;
+  for (uint32_t pm = pl->pos_mask; pm; pm &= pm - 1)
+    if (!(lm & pl->group_lists[__ffs(pm) - 1])) return false;
+  return true;
+}
+// array of slot s, or -1 past every array's written slots
+__device__ __forceinline__ int slot_array(const DevPlan *pl, const Counters *ctr, uint64_t s) {
+  int a = 0;
+  while (a + 1 < pl->g0n && s >= pl->g0base[a + 1]) a++;
+  return s - pl->g0base[a] < ctr->g0count[a] ? a : -1;
+}
+__device__ bool slot_is_survivor(const DevPlan *pl, const Counters *ctr, const uint32_t *bits, uint32_t nwords,
+                                 uint64_t s, uint32_t *lm_out = nullptr) {
+  const int a = slot_array(pl, ctr, s);
+  if (a < 0) return false;
+  if (pl->use_rej && pl->wrej[s]) return false;  // not voted (Posdb.cpp:5294, 5297)
+  const uint32_t lm = slot_lmask(pl, bits, nwords, s, a);
+  if (lm_out) *lm_out = lm;
+  return lm_survives(pl, lm);
+}
+// arena units of slot s's records: each run once per positive group its
+// list belongs to (a shared bigram sublist is merged into both groups); the
+// lists are walked in a wave-uniform loop
+__device__ uint32_t slot_units(const DevPlan *pl, const Counters *ctr, const uint32_t *cunit, const Loc *loc, uint64_t s,
+                               uint32_t lm) {
+  uint32_t u = 0;
+  for (int l = 0; l < pl->nlists; l++)
+    if (lm >> l & 1) u += slot_loc(pl, ctr, cunit, loc, s, l).len * (uint32_t)pl->list_mult[l];
+  return u;
+}
+
+// the survivors among this thread's CSPT slots: bit q of the result
+template <bool ORDERED>
+__device__ __forceinline__ uint32_t cmp_thread(const DevPlan *pl, const Counters *ctr, const uint32_t *cunit,
+                                               const uint32_t *bits, uint32_t nwords, const Loc *loc,
+                                               uint64_t slot_ub, uint32_t rc, uint64_t s0, uint32_t (&lmv)[CSPT],
+                                               uint32_t (&uv)[CSPT], uint32_t (&bk)[CSPT]) {
+  uint32_t ok = 0;
+  // the probed lists' bits of the thread's slots (CSPT consecutive slots
+  // inside one bitmap word)
+#pragma unroll
+  for (int q = 0; q < CSPT; q++) lmv[q] = 0;
+  if (s0 < slot_ub) {
+    for (uint32_t pm = pl->probed_mask; pm; pm &= pm - 1) {
+      const int l = __ffs(pm) - 1;
+      const uint32_t sub = bits[(uint64_t)l * nwords + (s0 >> 5)] >> (s0 & 31);
+#pragma unroll
+      for (int q = 0; q < CSPT; q++) lmv[q] |= ((sub >> q) & 1u) << l;
+    }
+  }
+  int a = 0;
+  while (a + 1 < pl->g0n && s0 >= pl->g0base[a + 1]) a++;
+#pragma unroll
+  for (int q = 0; q < CSPT; q++) {
+    const uint64_t s = s0 + q;
+    uv[q] = 0;
+    bk[q] = 0;
+    if (s >= slot_ub) {
+      lmv[q] = 0;
+      continue;
+    }
+    while (a + 1 < pl->g0n && s >= pl->g0base[a + 1]) a++;
+    if (s - pl->g0base[a] >= ctr->g0count[a] || (pl->use_rej && pl->wrej[s])) {
+      lmv[q] = 0;
+      continue;
+    }
+    const uint32_t lm = lmv[q] | (a == 0 ? 1u << pl->g0list[0] : 0u);
+    lmv[q] = lm;
+    if (!lm_survives(pl, lm)) continue;
+    const uint32_t u = slot_units(pl, ctr, cunit, loc, s, lm);
+    uv[q] = u;
+    bk[q] = ORDERED ? 0u : (uint32_t)size_bucket(u, rc);
+    ok |= 1u << q;
+  }
+  return ok;
+}
+
+template <bool ORDERED>
+__global__ void __launch_bounds__(CB) k_cmp_count(const DevPlan *pl, Counters *ctr, const uint32_t *cunit,
+                                                  const uint32_t *bits, uint32_t nwords, const Loc *loc,
+                                                  const uint64_t *cand, uint64_t slot_ub, uint32_t rc, BlkInfo *blk) {
+  __shared__ uint32_t s_cnt[NBKT];
   __shared__ uint32_t s_any;
-  __shared__ unsigned long long s_base_u;
-  __shared__ uint32_t s_gbits[MAXL];     // group bits per list
-  __shared__ uint64_t s_end[MAXG0];      // live end slot of each candidate array
-  __shared__ uint64_t s_beg[MAXG0 + 1];
-  const uint32_t pos = pl->pos_mask;
-  const int g0n = pl->g0n;
-  if (threadIdx.x < MAXL) s_gbits[threadIdx.x] = threadIdx.x < (unsigned)pl->nlists ? pl->lists[threadIdx.x].group_bits : 0;
-  if (threadIdx.x < MAXG0 + 1) s_beg[threadIdx.x] = threadIdx.x <= (unsigned)g0n ? pl->g0base[threadIdx.x] : ~0ull;
-  if (threadIdx.x < MAXG0) s_end[threadIdx.x] = threadIdx.x < (unsigned)g0n ? pl->g0base[threadIdx.x] + ctr->g0count[threadIdx.x] : 0;
-  if (threadIdx.x == 0) {
-    s_any = 0;
-    s_dall = 0;
-  }
-  if (threadIdx.x < NBKT) {
-    s_bcnt[threadIdx.x] = 0;
-    s_bcur[threadIdx.x] = 0;
-  }
-  if (CMODE != 2 && threadIdx.x < MAXL) {
+  __shared__ unsigned long long s_dall, s_usum, s_xu[XR], s_xd[XR];
+  if (threadIdx.x < NBKT) s_cnt[threadIdx.x] = 0;
+  if (threadIdx.x < XR) {
     s_xu[threadIdx.x] = 0;
     s_xd[threadIdx.x] = 0;
   }
-  __syncthreads();
-  const uint32_t xmask = pl->reshare_mask;
-  // a thread's slots: strided over the block (coalesced) -- or, ordered, 16
-  // consecutive ones, so thread order is slot order inside the block
-  const uint64_t s0 = (uint64_t)blockIdx.x * CTILE + (CMODE ? threadIdx.x * CSPT : threadIdx.x);
-  constexpr uint64_t SSTEP = CMODE ? 1 : CBLOCK;
-  // all of this thread's list masks in flight at once
-  uint32_t lmv[CSPT];
-#pragma unroll
-  for (int q = 0; q < CSPT; q++) {
-    const uint64_t s = s0 + (uint64_t)q * SSTEP;
-    lmv[q] = s < slot_ub ? lmask[s] : 0u;
+  if (threadIdx.x == 0) {
+    s_any = 0;
+    s_dall = 0;
+    s_usum = 0;
   }
-  uint32_t okm = 0, nok = 0, utot = 0, any = 0;
-  uint32_t units[CSPT];
-  constexpr int XR = 4;  // re-shrunk lists accumulated in registers
-  uint32_t txu[XR] = {0, 0, 0, 0};
-  unsigned long long txd[XR] = {0, 0, 0, 0}, tdall = 0;
+  __syncthreads();
+  const uint64_t s0 = (uint64_t)blockIdx.x * CTILE + threadIdx.x * CSPT;
+  uint32_t lmv[CSPT], uv[CSPT], bk[CSPT];
+  const uint32_t ok = cmp_thread<ORDERED>(pl, ctr, cunit, bits, nwords, loc, slot_ub, rc, s0, lmv, uv, bk);
+  const uint32_t xmask = pl->reshare_mask;
+  uint32_t any = 0, usum = 0;
+  unsigned long long tdall = 0, txu[XR] = {0, 0, 0, 0}, txd[XR] = {0, 0, 0, 0};
 #pragma unroll
   for (int q = 0; q < CSPT; q++) {
-    const uint64_t s = s0 + (uint64_t)q * SSTEP;
-    units[q] = 0;
-    if (s >= slot_ub) continue;
-    int k = 0;
-    while (k + 1 < g0n && s >= s_beg[k + 1]) k++;
-    if (s >= s_end[k]) continue;
-    if (pl->use_rej && pl->wrej[s]) continue;  // not voted (Posdb.cpp:5294, 5297)
-    const uint32_t lm = lmv[q];
-    uint32_t gm = 0;
-    for (uint32_t x = lm; x; x &= x - 1) gm |= s_gbits[__ffs(x) - 1];
-    if (!(((gm & pos) == pos) && !(gm & NEG_BIT))) continue;
-    const uint32_t u_s = ulen[s];
-    any |= lm;  // a survivor's lists are all in positive groups
-    units[q] = u_s;
-    okm |= 1u << q;
-    nok++;
-    utot += u_s;
-    if (CMODE != 1) atomicAdd(&s_bcnt[size_bucket(u_s, rc)], 1u);
-    if (CMODE != 2 && xmask) {
-      // accumulated per thread in registers for the first XR re-shrunk lists
-      // (reduced over the wave below), LDS atomics beyond
+    if (!(ok >> q & 1)) continue;
+    const uint64_t s = s0 + q;
+    atomicAdd(&s_cnt[bk[q]], 1u);
+    any |= lmv[q];
+    usum += uv[q];
+    if (xmask) {
+      // re-shrunk lists (k_ext_walk): their survivor run units and last docid
       const unsigned long long d = cand[s];
-      if (d > tdall) tdall = d;
+      tdall = d > tdall ? d : tdall;
       int r = 0;
       for (uint32_t x = xmask; x; x &= x - 1, r++) {
         const int l = __ffs(x) - 1;
-        if (!(lm >> l & 1)) continue;
-        const uint32_t len = loc[(uint64_t)l * slot_ub + s].len;
+        if (!(lmv[q] >> l & 1)) continue;
+        const uint32_t len = slot_loc(pl, ctr, cunit, loc, s, l).len;
         if (r < XR) {
 #pragma unroll
           for (int t = 0; t < XR; t++)
@@ -1070,16 +1138,17 @@ __global__ void __launch_bounds__(CBLOCK) k_compact(const DevPlan *pl, const uin
               txd[t] = d > txd[t] ? d : txd[t];
             }
         } else {
-          atomicAdd(&s_xu[l], len);
-          atomicMax(&s_xd[l], d);
+          atomicAdd(&ctr->ext[l].units, (unsigned long long)len);
+          atomicMax(&ctr->ext[l].dmax, d);
         }
       }
     }
   }
-  if (CMODE != 2 && xmask) {
-    const int lane = threadIdx.x & 63;
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
+  for (int off = 32; off > 0; off >>= 1) {
+    any |= __shfl_xor(any, off, 64);
+    usum += __shfl_xor(usum, off, 64);
+    if (xmask) {
       const unsigned long long o = __shfl_xor(tdall, off, 64);
       tdall = o > tdall ? o : tdall;
 #pragma unroll
@@ -1089,101 +1158,244 @@ __global__ void __launch_bounds__(CBLOCK) k_compact(const DevPlan *pl, const uin
         txd[t] = od > txd[t] ? od : txd[t];
       }
     }
-    if (lane == 0) {
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (any) atomicOr(&s_any, any);
+    if (usum) atomicAdd(&s_usum, (unsigned long long)usum);
+    if (xmask) {
       if (tdall) atomicMax(&s_dall, tdall);
-      int r = 0;
-      for (uint32_t x = xmask; x && r < XR; x &= x - 1, r++) {
-        const int l = __ffs(x) - 1;
 #pragma unroll
-        for (int t = 0; t < XR; t++)
-          if (t == r && txu[t]) {
-            atomicAdd(&s_xu[l], txu[t]);
-            atomicMax(&s_xd[l], txd[t]);
-          }
+      for (int t = 0; t < XR; t++)
+        if (txu[t]) {
+          atomicAdd(&s_xu[t], txu[t]);
+          atomicMax(&s_xd[t], txd[t]);
+        }
+    }
+  }
+  __syncthreads();
+  BlkInfo &o = blk[blockIdx.x];
+  if (threadIdx.x < NBKT) o.cnt[threadIdx.x] = s_cnt[threadIdx.x];
+  if (threadIdx.x < XR) {
+    o.xu[threadIdx.x] = s_xu[threadIdx.x];
+    o.xd[threadIdx.x] = s_xd[threadIdx.x];
+  }
+  if (threadIdx.x == 0) {
+    o.any = s_any;
+    o.pad = 0;
+    o.usum = s_usum;
+    o.dall = s_dall;
+  }
+}
+
+// one block: per bucket, the exclusive scan of the blocks' counts (written
+// back as offsets), the bucket starts, and every total into the counters.
+// Each thread loads its blocks' records once; the eight bucket scans run in
+// registers (the loads, not the arithmetic, are the latency).
+__global__ void __launch_bounds__(1024) k_cmp_scan(const DevPlan *pl, uint32_t nblk, BlkInfo *blk, Counters *ctr) {
+  __shared__ uint32_t tw[16][NBKT];
+  __shared__ uint32_t s_carry[NBKT];
+  __shared__ uint32_t s_any;
+  __shared__ unsigned long long s_dall, s_usum, s_xu[XR], s_xd[XR];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (threadIdx.x == 0) {
+    s_any = 0;
+    s_dall = 0;
+    s_usum = 0;
+  }
+  if (threadIdx.x < XR) {
+    s_xu[threadIdx.x] = 0;
+    s_xd[threadIdx.x] = 0;
+  }
+  if (threadIdx.x < NBKT) s_carry[threadIdx.x] = 0;
+  uint32_t any = 0;
+  unsigned long long dall = 0, usum = 0, xu[XR] = {0, 0, 0, 0}, xd[XR] = {0, 0, 0, 0};
+  const bool xm = pl->reshare_mask != 0;
+  __syncthreads();
+  for (uint32_t base = 0; base < nblk; base += 1024) {
+    const uint32_t i = base + threadIdx.x;
+    uint32_t v[NBKT], x[NBKT];
+    if (i < nblk) {
+      const BlkInfo &bi = blk[i];
+#pragma unroll
+      for (int b = 0; b < NBKT; b++) v[b] = bi.cnt[b];
+      any |= bi.any;
+      usum += bi.usum;
+      if (xm) {
+        dall = bi.dall > dall ? bi.dall : dall;
+#pragma unroll
+        for (int t = 0; t < XR; t++) {
+          xu[t] += bi.xu[t];
+          xd[t] = bi.xd[t] > xd[t] ? bi.xd[t] : xd[t];
+        }
+      }
+    } else {
+#pragma unroll
+      for (int b = 0; b < NBKT; b++) v[b] = 0;
+    }
+#pragma unroll
+    for (int b = 0; b < NBKT; b++) x[b] = v[b];
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+#pragma unroll
+      for (int b = 0; b < NBKT; b++) {
+        const uint32_t y = __shfl_up(x[b], o, 64);
+        if (lane >= o) x[b] += y;
       }
     }
+    if (lane == 63) {
+#pragma unroll
+      for (int b = 0; b < NBKT; b++) tw[wid][b] = x[b];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int b = 0; b < NBKT; b++) {
+      uint32_t pre = s_carry[b], tot = 0;
+      for (int w = 0; w < 16; w++) {
+        pre += w < wid ? tw[w][b] : 0u;
+        tot += tw[w][b];
+      }
+      if (i < nblk) blk[i].cnt[b] = pre + x[b] - v[b];
+      x[b] = tot;  // this chunk's total
+    }
+    __syncthreads();
+    if (threadIdx.x < NBKT) s_carry[threadIdx.x] += x[threadIdx.x & (NBKT - 1)];
+    __syncthreads();
   }
-  uint32_t tot_n, tot_u;
-  const uint32_t ex_n = block_exclusive_scan<CBLOCK>(nok, tmp, &tot_n);
-  const uint32_t ex_u = block_exclusive_scan<CBLOCK>(utot, tmp, &tot_u);
-  if (CMODE != 2 && any) atomicOr(&s_any, any);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    any |= __shfl_xor(any, off, 64);
+    usum += __shfl_xor(usum, off, 64);
+  }
+  if (lane == 0) {
+    if (any) atomicOr(&s_any, any);
+    if (usum) atomicAdd(&s_usum, usum);
+  }
+  if (xm) {
+    if (dall) atomicMax(&s_dall, dall);
+#pragma unroll
+    for (int t = 0; t < XR; t++)
+      if (xu[t]) {
+        atomicAdd(&s_xu[t], xu[t]);
+        atomicMax(&s_xd[t], xd[t]);
+      }
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
-    if (CMODE == 0) {
-      // ONE atomic per block for both bump pointers (survivor index and arena
-      // offset), 28 + 36 bits; the host caps slot_ub and the arena to fit
-      const unsigned long long old =
-          tot_n ? atomicAdd(&ctr->surv_top, ((unsigned long long)tot_n << 36) | (unsigned long long)tot_u) : 0ull;
-      s_base_i = (uint32_t)(old >> 36);
-      s_base_u = old & ((1ull << 36) - 1);
-    } else if (CMODE == 1) {
-      blk[blockIdx.x].n = tot_n;
-      blk[blockIdx.x].u = tot_u;
-    } else {
-      s_base_i = blk[blockIdx.x].n;
-      s_base_u = blk[blockIdx.x].u;
+    uint32_t acc = 0;
+    for (int b = 0; b < NBKT; b++) {
+      ctr->bstart[b] = acc;
+      ctr->bcnt[b] = s_carry[b];
+      acc += s_carry[b];
     }
-    if (CMODE != 2 && (s_any & ~__hip_atomic_load(&ctr->anysurv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)))
-      atomicOr(&ctr->anysurv, s_any);
-    if (CMODE != 2 && xmask && s_dall) atomicMax(&ctr->dmax_all, s_dall);
+    ctr->surv_top = ((unsigned long long)acc << 36) | (s_usum & ((1ull << 36) - 1));
+    ctr->anysurv = s_any;
+    ctr->dmax_all = s_dall;
+    int r = 0;
+    for (uint32_t x = pl->reshare_mask; x && r < XR; x &= x - 1, r++) {
+      const int l = __ffs(x) - 1;
+      ctr->ext[l].units += s_xu[r];
+      if (s_xd[r] > ctr->ext[l].dmax) ctr->ext[l].dmax = s_xd[r];
+    }
   }
-  if (CMODE != 2 && xmask && threadIdx.x < MAXL && s_xu[threadIdx.x]) {
-    atomicAdd(&ctr->ext[threadIdx.x].units, (unsigned long long)s_xu[threadIdx.x]);
-    atomicMax(&ctr->ext[threadIdx.x].dmax, s_xd[threadIdx.x]);
-  }
-  if (CMODE == 1) return;  // uniform
-  if (threadIdx.x < NBKT)
-    s_bbase[threadIdx.x] = s_bcnt[threadIdx.x] ? atomicAdd(&ctr->bcnt[threadIdx.x], s_bcnt[threadIdx.x]) : 0u;
-  __syncthreads();
-  uint32_t i = s_base_i + ex_n;
-  unsigned long long off = s_base_u + ex_u;
+}
+
+// the survivors' records at their final positions
+template <bool ORDERED>
+__global__ void __launch_bounds__(CB) k_cmp_write(const DevPlan *pl, const Counters *ctr, const uint32_t *cunit,
+                                                  const uint32_t *bits, uint32_t nwords, const Loc *loc,
+                                                  const uint64_t *cand, uint64_t slot_ub, uint32_t rc,
+                                                  const BlkInfo *blk, uint32_t *sv_slot, uint32_t *sv_lm,
+                                                  uint32_t *sv_u, uint64_t *sv_doc, Loc *sv_loc) {
+  __shared__ uint64_t tw[2][CB / 64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const uint64_t s0 = (uint64_t)blockIdx.x * CTILE + threadIdx.x * CSPT;
+  uint32_t lmv[CSPT], uv[CSPT], bk[CSPT];
+  const uint32_t ok = cmp_thread<ORDERED>(pl, ctr, cunit, bits, nwords, loc, slot_ub, rc, s0, lmv, uv, bk);
+  // this thread's survivors per bucket, 16 bits each, buckets 0-3 / 4-7
+  uint64_t c[2] = {0, 0};
 #pragma unroll
   for (int q = 0; q < CSPT; q++) {
-    if (!(okm >> q & 1)) continue;
-    surv[i] = (uint32_t)(s0 + (uint64_t)q * SSTEP);
-    surv_off[i] = off;
-    surv_lm[i] = lmv[q];
-    surv_u[i] = units[q];
-    // size bucket b's region of perm starts at b * slot_ub; the block's
-    // range in it was reserved above
-    const int b = size_bucket(units[q], rc);
-    perm[(uint64_t)b * slot_ub + s_bbase[b] + atomicAdd(&s_bcur[b], 1u)] = i;
-    i++;
-    off += units[q];
+    if (!(ok >> q & 1)) continue;
+    const uint64_t inc = 1ull << (16 * (bk[q] & 3));
+    if (bk[q] < 4) c[0] += inc;
+    else c[1] += inc;
+  }
+  // block exclusive scan of both packed words (no field overflows: <= CTILE)
+  uint64_t x[2] = {c[0], c[1]};
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const uint64_t y = __shfl_up(x[h], o, 64);
+      if (lane >= o) x[h] += y;
+    }
+  }
+  if (lane == 63) {
+    tw[0][wid] = x[0];
+    tw[1][wid] = x[1];
+  }
+  __syncthreads();
+  uint64_t pre[2] = {0, 0};
+  for (int w = 0; w < wid; w++) {
+    pre[0] += tw[0][w];
+    pre[1] += tw[1][w];
+  }
+  pre[0] += x[0] - c[0];
+  pre[1] += x[1] - c[1];
+  if (!ok) return;
+  const BlkInfo &bi = blk[blockIdx.x];
+  const uint32_t nl = (uint32_t)pl->nlists;
+  // the thread's survivors in slot order: per bucket, the next position
+#pragma unroll
+  for (int q = 0; q < CSPT; q++) {
+    if (!(ok >> q & 1)) continue;
+    const uint32_t b = bk[q];
+    const uint32_t sh16 = 16 * (b & 3);
+    uint32_t r;
+    if (b < 4) {
+      r = (uint32_t)((pre[0] >> sh16) & 0xffff);
+      pre[0] += 1ull << sh16;
+    } else {
+      r = (uint32_t)((pre[1] >> sh16) & 0xffff);
+      pre[1] += 1ull << sh16;
+    }
+    const uint32_t pos = ctr->bstart[b] + bi.cnt[b] + r;
+    const uint64_t s = s0 + q;
+    sv_slot[pos] = (uint32_t)s;
+    sv_lm[pos] = lmv[q];
+    sv_u[pos] = uv[q];
+    sv_doc[pos] = cand[s];
+    for (uint32_t xm = lmv[q]; xm; xm &= xm - 1) {
+      const int l = __ffs(xm) - 1;
+      sv_loc[(uint64_t)pos * nl + l] = slot_loc(pl, ctr, cunit, loc, s, l);
+    }
   }
 }
 
 // The re-shrink of each list several groups use (ListExt): E = the units
 // from |P| on whose byte 0 has the 6-byte bit (stopping at the list end),
 // added to the last survivor run's copy for every use but the first -- its
-// slot's arena units grow accordingly before the offsets are scanned.  The
-// re-shrink then parses on from |P|+E: an aligned parse (a true run head
+// survivor's records are relocated to the arena's end with room for them.
+// The re-shrink then parses on from |P|+E: an aligned parse (a true run head
 // there) can match no survivor any more (every survivor run of the list is
 // in P); a misaligned one reads garbage docids, and one equal to a later
 // survivor would copy a misparsed run -- not emulated, flagged instead
 // (GBGPU_EUNSUPPORTED; about 2^-20 per query).  One wave per list.
-__device__ bool slot_is_survivor(const DevPlan *pl, const uint32_t *lmask, uint64_t s) {
-  if (pl->use_rej && pl->wrej[s]) return false;
-  uint32_t gm = 0;
-  for (uint32_t x = lmask[s]; x; x &= x - 1) gm |= pl->lists[__ffs(x) - 1].group_bits;
-  return ((gm & pl->pos_mask) == pl->pos_mask) && !(gm & NEG_BIT);
-}
-
 // slot of candidate docid d in any array, if that slot survived; ~0 if none
-__device__ uint64_t survivor_slot(const DevPlan *pl, const Counters *ctr, const uint64_t *cand,
-                                  const uint32_t *lmask, uint64_t d, int lane) {
+__device__ uint64_t survivor_slot(const DevPlan *pl, const Counters *ctr, const uint64_t *cand, const uint32_t *bits,
+                                  uint32_t nwords, uint64_t d, int lane) {
   for (int k = 0; k < pl->g0n; k++) {
     const uint64_t *ck = cand + pl->g0base[k];
     const uint32_t n = ctr->g0count[k];
     const uint32_t i = wave_lower_bound(ck, n, d, lane);
-    if (i < n && ck[i] == d && slot_is_survivor(pl, lmask, pl->g0base[k] + i)) return pl->g0base[k] + i;
+    if (i < n && ck[i] == d && slot_is_survivor(pl, ctr, bits, nwords, pl->g0base[k] + i)) return pl->g0base[k] + i;
   }
   return ~0ull;
 }
 
 __global__ void __launch_bounds__(64) k_ext_walk(const DevPlan *pl, Counters *ctr, const uint64_t *cand,
-                                                 const uint32_t *lmask, const uint32_t *ulen,
-                                                 unsigned long long arena_cap) {
+                                                 const uint32_t *cunit, const uint32_t *bits, uint32_t nwords,
+                                                 const Loc *loc, unsigned long long arena_cap) {
   const int lane = threadIdx.x;
   for (uint32_t xm = pl->reshare_mask; xm; xm &= xm - 1) {
     const int l = __ffs(xm) - 1;
@@ -1203,7 +1415,7 @@ __global__ void __launch_bounds__(64) k_ext_walk(const DevPlan *pl, Counters *ct
       }
       u += 64;
     }
-    const uint64_t s = survivor_slot(pl, ctr, cand, lmask, x.dmax, lane);
+    const uint64_t s = survivor_slot(pl, ctr, cand, bits, nwords, x.dmax, lane);
     if (lane == 0) {
       x.E = (uint32_t)(u - P);
       x.slot1 = s == ~0ull ? 0u : (uint32_t)(s + 1);
@@ -1232,7 +1444,7 @@ __global__ void __launch_bounds__(64) k_ext_walk(const DevPlan *pl, Counters *ct
         settled = true;
         break;
       }
-      if (g > x.dmax && survivor_slot(pl, ctr, cand, lmask, g, lane) != ~0ull) break;
+      if (g > x.dmax && survivor_slot(pl, ctr, cand, bits, nwords, g, lane) != ~0ull) break;
       h += 2;
       for (;;) {
         const uint64_t v = h + lane;
@@ -1250,12 +1462,14 @@ __global__ void __launch_bounds__(64) k_ext_walk(const DevPlan *pl, Counters *ct
   // the survivors whose re-shrunk copies grow get their records moved to the
   // arena's end, with room for the extra units of every list extending them
   if (lane != 0) return;
-  unsigned long long top = ctr->surv_top & ((1ull << 36) - 1);
+  unsigned long long top = ctr->arena_top;
   for (uint32_t xm = pl->reshare_mask; xm; xm &= xm - 1) {
     const int l = __ffs(xm) - 1;
     ListExt &x = ctr->ext[l];
     if (!x.slot1 || !x.E || x.reloc) continue;
-    unsigned long long need = ulen[x.slot1 - 1];
+    uint32_t lm = 0;
+    slot_is_survivor(pl, ctr, bits, nwords, x.slot1 - 1, &lm);
+    unsigned long long need = slot_units(pl, ctr, cunit, loc, x.slot1 - 1, lm);
     for (uint32_t ym = pl->reshare_mask; ym; ym &= ym - 1) {
       const int l2 = __ffs(ym) - 1;
       if (ctr->ext[l2].slot1 == x.slot1) need += (unsigned long long)ctr->ext[l2].E * (uint32_t)(pl->lists[l2].uses - 1);
@@ -1273,61 +1487,7 @@ __global__ void __launch_bounds__(64) k_ext_walk(const DevPlan *pl, Counters *ct
     }
     top += need;
   }
-  ctr->surv_top = (ctr->surv_top & ~((1ull << 36) - 1)) | top;
-}
-
-// exclusive scan of the blocks' (survivors, arena units) -> their offsets,
-// and the totals into the counters (one block)
-__global__ void __launch_bounds__(1024) k_compact_scan(uint32_t nblk, BlkTot *blk, Counters *ctr) {
-  __shared__ uint32_t tn[16];
-  __shared__ unsigned long long tu[16];
-  __shared__ uint32_t cn;
-  __shared__ unsigned long long cu;
-  if (threadIdx.x == 0) {
-    cn = 0;
-    cu = 0;
-  }
-  __syncthreads();
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  for (uint32_t base = 0; base < nblk; base += 1024) {
-    const uint32_t i = base + threadIdx.x;
-    const uint32_t vn = i < nblk ? blk[i].n : 0;
-    const unsigned long long vu = i < nblk ? blk[i].u : 0;
-    uint32_t xn = vn;
-    unsigned long long xu = vu;
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t yn = __shfl_up(xn, o, 64);
-      const unsigned long long yu = __shfl_up(xu, o, 64);
-      if (lane >= o) {
-        xn += yn;
-        xu += yu;
-      }
-    }
-    if (lane == 63) {
-      tn[wid] = xn;
-      tu[wid] = xu;
-    }
-    __syncthreads();
-    uint32_t pn = 0;
-    unsigned long long pu = 0;
-    for (int w = 0; w < wid; w++) {
-      pn += tn[w];
-      pu += tu[w];
-    }
-    const uint32_t in_n = cn + pn + xn;
-    const unsigned long long in_u = cu + pu + xu;
-    __syncthreads();
-    if (i < nblk) {
-      blk[i].n = in_n - vn;
-      blk[i].u = in_u - vu;
-    }
-    if (threadIdx.x == 1023) {
-      cn = in_n;
-      cu = in_u;
-    }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) ctr->surv_top = ((unsigned long long)cn << 36) | cu;
+  ctr->arena_top = top;
 }
 
 // A survivor's run in list lid as group g's sublist x sees it: its own
@@ -1343,12 +1503,6 @@ struct SubRun {
   }
 };
 __device__ __forceinline__ SubRun sub_run_at(const DevPlan *pl, const Counters *ctr, Loc lc, int lid, int g, int x,
-                                             uint64_t s);
-__device__ __forceinline__ SubRun sub_run(const DevPlan *pl, const Counters *ctr, const Loc *loc, uint64_t slot_ub,
-                                          int lid, int g, int x, uint64_t s) {
-  return sub_run_at(pl, ctr, loc[(uint64_t)lid * slot_ub + s], lid, g, x, s);
-}
-__device__ __forceinline__ SubRun sub_run_at(const DevPlan *pl, const Counters *ctr, Loc lc, int lid, int g, int x,
                                              uint64_t s) {
   gu8 *base = gl(pl->lists[lid].p);
   SubRun r{base + (size_t)lc.unit * 6, base, lc.len, lc.len};
@@ -1359,10 +1513,10 @@ __device__ __forceinline__ SubRun sub_run_at(const DevPlan *pl, const Counters *
   }
   return r;
 }
-
-// docids of the survivors (the vote buffer's docids, unordered)
-__global__ void k_gather_hits(const uint32_t *surv, const uint64_t *cand, uint32_t n, uint64_t *out) {
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) out[i] = cand[surv[i]];
+// survivor `pos`'s run in list lid (its record's run locations)
+__device__ __forceinline__ SubRun sub_run(const DevPlan *pl, const Counters *ctr, const Loc *sv_loc, uint32_t pos,
+                                          int lid, int g, int x, uint64_t s) {
+  return sub_run_at(pl, ctr, sv_loc[(uint64_t)pos * (uint32_t)pl->nlists + lid], lid, g, x, s);
 }
 
 // ------------------------------------------------------------------ score
@@ -1392,7 +1546,7 @@ struct SurvOut {
 
 template <int NQ, int NS, class RP, class REC = NoRec>
 __device__ __forceinline__ void score_survivor(const DevPlan *pl, const Counters *ctr, uint32_t s, uint32_t lm,
-                                               uint32_t anys, const Loc *loc, uint64_t slot_ub, RP rec, float *smcol,
+                                               uint32_t anys, const Loc *svloc, RP rec, float *smcol,
                                                uint32_t *key_out, int diag, uint32_t *nrec_out,
                                                bool stamp, uint64_t &tmerge, uint64_t (&tm)[3],
                                                REC *srec = nullptr, SurvOut *so = nullptr,
@@ -1436,7 +1590,7 @@ __device__ __forceinline__ void score_survivor(const DevPlan *pl, const Counters
           newIdx++;
           // kill: sublists the second pass's lookup misses (k_scoreinfo)
           if ((lm >> lid & 1) && !(kill && (kill[j] >> x & 1))) {
-            const SubRun sr = sub_run(pl, ctr, loc, slot_ub, lid, j, x, s);
+            const SubRun sr = sub_run_at(pl, ctr, svloc[lid], lid, j, x, s);
             src[x] = sr.own;
             xsrc[x] = sr.ext;
             c0[x] = sr.len0;
@@ -1639,8 +1793,20 @@ __device__ __forceinline__ void score_survivor(const DevPlan *pl, const Counters
     *key_out = nrec + 1;
     return;
   }
-  const bool ok = !empty_pos && score_doc<NQ, RP, REC>(&c_weights, pl, dv, siteRank < 0 ? 0 : siteRank, docLang,
-                                                       smcol, SCORE_TPB, &score, diag & 0xff, srec);
+  // the scorers' top lists fill at most min(m_realMaxTop, records) slots
+  // (a pair's merge walk scores fewer steps than both lists' records; an
+  // empty list is read once): when every lane of the wave has at most
+  // SMALL_TOP records, the bookkeeping runs over SMALL_TOP register slots
+  constexpr int SMALL_TOP = 4;
+  bool ok = false;
+  if (!empty_pos) {
+    const int sr = siteRank < 0 ? 0 : siteRank;
+    if (!REC::on && __ballot(nrec > (uint32_t)SMALL_TOP) == 0)
+      ok = score_doc<NQ, RP, REC, SMALL_TOP>(&c_weights, pl, dv, sr, docLang, smcol, SCORE_TPB, &score, diag & 0xff,
+                                             srec);
+    else
+      ok = score_doc<NQ, RP, REC>(&c_weights, pl, dv, sr, docLang, smcol, SCORE_TPB, &score, diag & 0xff, srec);
+  }
   // gbsortby: the score is the float of the group's first key, bytes 2..5 as
   // the mini-merge left them (Posdb.cpp:7265-7269)
   uint32_t ival = 0;  // gbsortby int: m_intScore's bits
@@ -1665,19 +1831,20 @@ __device__ __forceinline__ void score_survivor(const DevPlan *pl, const Counters
   *key_out = key;
 }
 
-// Scored in size-bucketed order (k_compact's perm), so a wave's survivors have
-// similar work (its lanes run the scorers in lockstep).  Waves of buckets
-// 3-7 score 64 survivors, one per lane, each keeping its records in its
-// lane's column of the wave's LDS record arrays (RC records); waves of
-// buckets 0-2 score 8/16/32 larger survivors with 8/4/2 columns each.  A
-// survivor that still does not fit (or whose re-shrunk copies grow it past
-// that) uses its range of the global record arena instead.
+// Scored in size-bucket order (k_cmp_write's positions), so a wave's
+// survivors have similar work (its lanes run the scorers in lockstep).
+// Waves of buckets 3-7 score 64 survivors, one per lane, each keeping its
+// records in its lane's column of the wave's LDS record arrays (RC records);
+// waves of buckets 0-2 score 8/16/32 larger survivors with 8/4/2 columns
+// each.  A survivor that still does not fit (or whose re-shrunk copies grow
+// it past that) takes a range of the global record arena.  A survivor's
+// data (slot, list mask, units, run locations) is read at its position, so
+// a wave's reads are contiguous; its key goes to skey at the same position.
 template <int NQ, int NS, int RC>
-__global__ void __launch_bounds__(SCORE_TPB) k_score(const DevPlan *pl, const uint64_t *cand, const Counters *ctr,
-                                                     const uint32_t *surv, const uint32_t *surv_lm,
-                                                     const unsigned long long *surv_off, const uint32_t *surv_u,
-                                                     const uint32_t *perm, const Loc *loc, uint64_t slot_ub,
-                                                     uint64_t *arena, uint32_t *skey, uint64_t *sdoc, uint8_t *sflag,
+__global__ void __launch_bounds__(SCORE_TPB) k_score(const DevPlan *pl, const uint64_t *sv_doc, Counters *ctr,
+                                                     const uint32_t *sv_slot, const uint32_t *sv_lm,
+                                                     const uint32_t *sv_u, const Loc *sv_loc, uint64_t *arena,
+                                                     unsigned long long arena_cap, uint32_t *skey, uint8_t *sflag,
                                                      int diag, uint64_t *dbg) {
   static_assert(SCORE_TPB == 64, "LdsRecs columns are one wave wide");
   __shared__ float s_sm[npairs<NQ>() * SCORE_TPB];
@@ -1691,52 +1858,40 @@ __global__ void __launch_bounds__(SCORE_TPB) k_score(const DevPlan *pl, const ui
   stage_weights(&c_weights);
   const uint32_t anys = ctr->anysurv;
   const int lane = threadIdx.x;
+  const uint32_t nl = (uint32_t)pl->nlists;
   // waves per bucket: bucket b packs 1 << bucket_shift(b) survivors a wave
-  uint32_t wend[NBKT], bstart[NBKT];
-  uint32_t nw = 0, acc = 0;
+  uint32_t wend[NBKT];
+  uint32_t nw = 0;
 #pragma unroll
   for (int b = 0; b < NBKT; b++) {
-    const uint32_t c = ctr->bcnt[b];
-    bstart[b] = acc;
-    acc += c;
-    nw += (c + (1u << bucket_shift(b)) - 1) >> bucket_shift(b);
+    nw += (ctr->bcnt[b] + (1u << bucket_shift(b)) - 1) >> bucket_shift(b);
     wend[b] = nw;
   }
-  // diagnostic bit 0x100: survivors in compaction order, 64 a wave
-  const bool natural = (diag & 0x100) != 0;
-  if (natural) nw = (acc + 63) >> 6;
   uint32_t nfilt = 0;
   for (uint32_t w = blockIdx.x; w < nw; w += gridDim.x) {  // uniform over the wave
     int b = 0;
 #pragma unroll
     for (int q = 0; q < NBKT - 1; q++) b += w >= wend[q];
-    if (natural) b = NBKT - 1;
-    uint32_t wb = 0, st = 0, cnt = 0, wprev = 0;
+    uint32_t st = 0, cnt = 0, wprev = 0;
 #pragma unroll
     for (int q = 0; q < NBKT; q++)
       if (q == b) {
-        wb = wend[q];
-        st = bstart[q];
-        cnt = (q + 1 < NBKT ? bstart[q + 1] : acc) - st;
+        st = ctr->bstart[q];
+        cnt = ctr->bcnt[q];
         wprev = q ? wend[q - 1] : 0;
       }
-    (void)wb;
-    if (natural) {
-      st = 0;
-      cnt = acc;
-      wprev = 0;
-    }
     const int sh = bucket_shift(b);
     const uint32_t j = ((w - wprev) << sh) + (uint32_t)lane;
     bool filt = false;
     if (lane < (1 << sh) && j < cnt) {
       uint64_t ts0 = 0, ts1 = 0, ts2 = 0, ts3 = 0;
       if (dbg) ts0 = __builtin_amdgcn_s_memtime();
-      const uint32_t i = natural ? j : perm[(uint64_t)b * slot_ub + j];
-      const uint32_t s = surv[i];
-      const uint32_t lm = surv_lm[i];
-      uint32_t units = surv_u[i];
-      unsigned long long off = surv_off[i];
+      const uint32_t i = st + j;
+      const uint32_t s = sv_slot[i];
+      const uint32_t lm = sv_lm[i];
+      uint32_t units = sv_u[i];
+      const Loc *svl = sv_loc + (uint64_t)i * nl;
+      unsigned long long off = ~0ull;
       for (uint32_t x = lm & pl->reshare_mask; x; x &= x - 1) {  // re-shrunk copies (k_ext_walk)
         const int l = __ffs(x) - 1;
         const ListExt &e = ctr->ext[l];
@@ -1753,12 +1908,18 @@ __global__ void __launch_bounds__(SCORE_TPB) k_score(const DevPlan *pl, const ui
       if (units <= ((uint32_t)RC << (6 - sh))) {
         const LdsRecs lrec{(__attribute__((address_space(3))) uint32_t *)(s_rlo + lane),
                            (__attribute__((address_space(3))) uint16_t *)(s_rhi + lane), sh, RC << (6 - sh)};
-        score_survivor<NQ, NS>(pl, ctr, s, lm, anys, loc, slot_ub, lrec, s_sm + lane, &key, diag, &nr,
+        score_survivor<NQ, NS>(pl, ctr, s, lm, anys, svl, lrec, s_sm + lane, &key, diag, &nr,
                                dbg != nullptr, ts2, tmm);
       } else {
-        const GlobalRecs grec{(__attribute__((address_space(1))) uint64_t *)(arena + off)};
-        score_survivor<NQ, NS>(pl, ctr, s, lm, anys, loc, slot_ub, grec, s_sm + lane, &key, diag, &nr,
-                               dbg != nullptr, ts2, tmm);
+        if (off == ~0ull) off = atomicAdd(&ctr->arena_top, (unsigned long long)units);
+        if (off + units > arena_cap) {
+          ctr->unsup = 1;  // the host sized the arena for every survivor's units: not reached
+          key = 0;
+        } else {
+          const GlobalRecs grec{(__attribute__((address_space(1))) uint64_t *)(arena + off)};
+          score_survivor<NQ, NS>(pl, ctr, s, lm, anys, svl, grec, s_sm + lane, &key, diag, &nr,
+                                 dbg != nullptr, ts2, tmm);
+        }
       }
       if (dbg) {
         __asm__ volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -1771,24 +1932,23 @@ __global__ void __launch_bounds__(SCORE_TPB) k_score(const DevPlan *pl, const ui
         tseg[1] += ts2 - ts1;
         tseg[2] += ts3 - ts2;
       }
-      const uint64_t d = cand[s];
       // the paging filter of a widget's next page (Posdb.cpp:7327-7347):
       // m_filtered counts the scored docids it drops
       if (pl->has_serp && key) {
+        const uint64_t d = sv_doc[i];
         if (pl->sortby_group >= 0 && pl->sortby_int) {  // intScore vs (int32_t)m_maxSerpScore
           const int32_t iv = (int32_t)(key ^ 0x80000000u);
           if (iv > pl->max_serp_int) filt = true;
           else if (iv == pl->max_serp_int && (int64_t)d <= pl->min_serp_docid) filt = true;
         } else {
-          const uint32_t b = (key & 0x80000000u) ? (key & 0x7fffffffu) : ~key;
-          const float score = __uint_as_float(b);
+          const uint32_t b2 = (key & 0x80000000u) ? (key & 0x7fffffffu) : ~key;
+          const float score = __uint_as_float(b2);
           if (score > (float)pl->max_serp_score) filt = true;
           else if ((double)score == pl->max_serp_score && (int64_t)d <= pl->min_serp_docid) filt = true;
         }
         if (filt) key = 0;
       }
       skey[i] = key;
-      sdoc[i] = d;
       // site clustering: the replay counts m_filtered, since a docid the
       // prefilters skip never reaches the paging test (Posdb.cpp:6341-6345)
       if (pl->clustering) sflag[i] = filt ? 1 : 0;
@@ -1918,17 +2078,16 @@ struct ScoreRec {
 // replayed over a directory: survivors sorted by docid (k_si_keys + hipcub),
 // and per list the exclusive prefix of their run units (k_si_dir).  Past the
 // shrunk end the in-place buffer still holds the list's own bytes.
-__global__ void k_si_keys(const uint32_t *surv, const uint64_t *cand, uint32_t nsurv, uint64_t *key, uint32_t *val) {
+__global__ void k_si_keys(const uint64_t *sv_doc, uint32_t nsurv, uint64_t *key, uint32_t *val) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nsurv; i += gridDim.x * blockDim.x) {
-    key[i] = cand[surv[i]];
+    key[i] = sv_doc[i];
     val[i] = i;
   }
 }
 
 // one block per list: cum[l][k] = units, in list l, of the survivors ranked
 // below k (k = 0..nsurv)
-__global__ void __launch_bounds__(1024) k_si_dir(const DevPlan *pl, const Loc *loc, uint64_t slot_ub,
-                                                 const uint32_t *surv, const uint32_t *surv_lm,
+__global__ void __launch_bounds__(1024) k_si_dir(const DevPlan *pl, const Loc *sv_loc, const uint32_t *sv_lm,
                                                  const uint32_t *sperm, uint32_t nsurv, uint32_t *cum) {
   __shared__ uint32_t s_w[16];
   const int l = blockIdx.x;
@@ -1940,7 +2099,7 @@ __global__ void __launch_bounds__(1024) k_si_dir(const DevPlan *pl, const Loc *l
     uint32_t u = 0;
     if (k < nsurv) {
       const uint32_t i = sperm[k];
-      if (surv_lm[i] >> l & 1) u = loc[(uint64_t)l * slot_ub + surv[i]].len;
+      if (sv_lm[i] >> l & 1) u = sv_loc[(uint64_t)i * (uint32_t)pl->nlists + l].len;
     }
     uint32_t x = u;  // inclusive wave scan
     for (int o = 1; o < 64; o <<= 1) {
@@ -1965,9 +2124,8 @@ __global__ void __launch_bounds__(1024) k_si_dir(const DevPlan *pl, const Loc *l
 // shrunk image (u < S), else the list's own unit u (zero past its end)
 struct SiList {
   const DevPlan *pl;
-  const Loc *loc;
-  uint64_t slot_ub;
-  const uint32_t *surv, *sperm, *cum;
+  const Loc *sv_loc;
+  const uint32_t *sperm, *cum;
   uint32_t nsurv;
   int lid;
   __device__ uint32_t run_of(uint32_t u) const {  // last k with cum[k] <= u
@@ -1983,7 +2141,7 @@ struct SiList {
     gu8 *base = gl(pl->lists[lid].p);
     if (u < (int64_t)cum[nsurv]) {
       const uint32_t k = run_of((uint32_t)u);
-      const Loc lc = loc[(uint64_t)lid * slot_ub + surv[sperm[k]]];
+      const Loc lc = sv_loc[(uint64_t)sperm[k] * (uint32_t)pl->nlists + lid];
       return load6(base + ((size_t)lc.unit + (size_t)(u - cum[k])) * 6);
     }
     if (u < (int64_t)pl->lists[lid].units) return load6(base + (size_t)u * 6);
@@ -2032,10 +2190,10 @@ __device__ int si_word_pos_list(const SiList &L, uint64_t docId, uint32_t own, i
 
 // one lane per tree docid: the first pass's score_survivor again, with the
 // recorder, over the survivor's arena range (k_score's fallback store)
-__global__ void __launch_bounds__(SCORE_TPB) k_scoreinfo(const DevPlan *pl, const Counters *ctr, const uint32_t *surv,
-                                                         const uint32_t *surv_lm,
-                                                         const unsigned long long *surv_off, const Loc *loc,
-                                                         uint64_t slot_ub, uint64_t *arena, const uint64_t *tdoc,
+__global__ void __launch_bounds__(SCORE_TPB) k_scoreinfo(const DevPlan *pl, Counters *ctr, const uint32_t *sv_slot,
+                                                         const uint32_t *sv_lm, const uint32_t *sv_u,
+                                                         const Loc *sv_loc, uint64_t *arena,
+                                                         unsigned long long arena_cap, const uint64_t *tdoc,
                                                          const uint64_t *sdoc, const uint32_t *sperm,
                                                          const uint32_t *cum, uint32_t nsurv,
                                                          uint32_t n, SurvOut *info, int32_t *counts,
@@ -2058,9 +2216,9 @@ __global__ void __launch_bounds__(SCORE_TPB) k_scoreinfo(const DevPlan *pl, cons
     return;
   }
   const uint32_t i = sperm[lo];
-  const uint32_t s = surv[i];
+  const uint32_t s = sv_slot[i];
   // the sublists getWordPosList finds the docid in (Posdb.cpp:6195-6241)
-  const uint32_t lm = surv_lm[i];
+  const uint32_t lm = sv_lm[i];
   uint16_t kill[MAXG];
   for (int j = 0; j < MAXG; j++) kill[j] = 0;
   const uint32_t anys = ctr->anysurv;
@@ -2069,7 +2227,7 @@ __global__ void __launch_bounds__(SCORE_TPB) k_scoreinfo(const DevPlan *pl, cons
     for (int x = 0; x < pl->gnsub[j]; x++) {
       const int lid = pl->gsub[j][x];
       if (!(anys >> lid & 1) || !(lm >> lid & 1)) continue;
-      const SiList L{pl, loc, slot_ub, surv, sperm, cum + (size_t)lid * (nsurv + 1), nsurv, lid};
+      const SiList L{pl, sv_loc, sperm, cum + (size_t)lid * (nsurv + 1), nsurv, lid};
       const bool later = (pl->reshare_mask >> lid & 1) &&
                          !(j == pl->lists[lid].owner_group && x == pl->lists[lid].owner_sub);
       const int64_t U = (int64_t)L.cum[nsurv] + ((later && ctr->ext[lid].slot1) ? ctr->ext[lid].E : 0);
@@ -2082,18 +2240,30 @@ __global__ void __launch_bounds__(SCORE_TPB) k_scoreinfo(const DevPlan *pl, cons
       if (f == 0) kill[j] |= (uint16_t)(1u << x);
     }
   }
-  unsigned long long off = surv_off[i];
-  for (uint32_t x = lm & pl->reshare_mask; x; x &= x - 1) {  // as k_score: re-shrunk copies
+  // the records go to a range of the global arena (a re-shrunk copy's
+  // relocated range where k_ext_walk gave it one)
+  uint32_t units = sv_u[i];
+  unsigned long long off = ~0ull;
+  for (uint32_t x = lm & pl->reshare_mask; x; x &= x - 1) {
     const int l = __ffs(x) - 1;
     const ListExt &e = ctr->ext[l];
-    if (e.slot1 == s + 1 && e.reloc) off = e.off;
+    if (e.slot1 == s + 1) {
+      units += e.E * (uint32_t)(pl->lists[l].uses - 1);
+      if (e.reloc) off = e.off;
+    }
+  }
+  if (off == ~0ull) off = atomicAdd(&ctr->arena_top, (unsigned long long)units);
+  if (off + units > arena_cap) {
+    so.ok = -3;  // arena exhausted (not reached: the host sizes it for every survivor)
+    info[t] = so;
+    return;
   }
   ScoreRec rec{ss + (size_t)t * scap, ps + (size_t)t * pcap, 0, 0, scap, pcap};
   uint32_t key, nr;
   uint64_t tmerge = 0, tm[3] = {0, 0, 0};
   const GlobalRecs grec{(__attribute__((address_space(1))) uint64_t *)(arena + off)};
-  score_survivor<MAXG, MAXSUB>(pl, ctr, s, lm, anys, loc, slot_ub, grec, s_sm + threadIdx.x, &key, 0, &nr,
-                               false, tmerge, tm, &rec, &so, kill);
+  score_survivor<MAXG, MAXSUB>(pl, ctr, s, lm, anys, sv_loc + (uint64_t)i * (uint32_t)pl->nlists, grec,
+                               s_sm + threadIdx.x, &key, 0, &nr, false, tmerge, tm, &rec, &so, kill);
   info[t] = so;
   counts[2 * t] = rec.ns;
   counts[2 * t + 1] = rec.np;
@@ -2145,7 +2315,7 @@ __device__ __forceinline__ float max_score_tail(const DevPlan *pl, BoundCore c, 
 }
 
 __device__ BoundCore group_bound_core(const DevPlan *pl, const Counters *ctr, int g, uint32_t s, uint32_t lm,
-                                      const Loc *loc, uint64_t slot_ub) {
+                                      const Loc *svl) {
   const Weights &W = s_weights;
   float best = -1.0f;
   unsigned bestDR = 0;
@@ -2156,7 +2326,7 @@ __device__ BoundCore group_bound_core(const DevPlan *pl, const Counters *ctr, in
     const int lid = pl->gsub[g][x];
     if (!(lm >> lid & 1)) continue;  // m_savedCursor[j] == NULL
     if (pl->gflags0[g] & BF_HALFSTOPWIKIBIGRAM) hs = true;
-    const SubRun run = sub_run(pl, ctr, loc, slot_ub, lid, g, x, s);
+    const SubRun run = sub_run_at(pl, ctr, svl[lid], lid, g, x, s);
     if (sr == -1) {  // getSiteRank / getLangId of the 12-byte run head
       gu8 *h = run.own;
       const uint32_t b0 = h[0], b6 = h[6], b7 = h[7];
@@ -2203,14 +2373,14 @@ __device__ BoundCore group_bound_core(const DevPlan *pl, const Counters *ctr, in
 
 // ring-buffer slots this wave's lanes write for one group's runs (value v);
 // returns the slot of the head of the group's last run (ourFirstPos)
-__device__ int ring_fill(const DevPlan *pl, const Counters *ctr, int g, uint32_t s, uint32_t lm, const Loc *loc,
-                         uint64_t slot_ub, uint8_t *ring, uint8_t v, int lane) {
+__device__ int ring_fill(const DevPlan *pl, const Counters *ctr, int g, uint32_t s, uint32_t lm, const Loc *svl,
+                         uint8_t *ring, uint8_t v, int lane) {
   int first = -1;
   const int gns = pl->gnsub[g];
   for (int x = 0; x < gns; x++) {
     const int lid = pl->gsub[g][x];
     if (!(lm >> lid & 1)) continue;
-    const SubRun run = sub_run(pl, ctr, loc, slot_ub, lid, g, x, s);
+    const SubRun run = sub_run_at(pl, ctr, svl[lid], lid, g, x, s);
     for (uint32_t k = lane; k < run.len; k += 64) {
       if (k == 1) continue;
       gu8 *kp = run.key(k);
@@ -2288,9 +2458,9 @@ __device__ int32_t ring_best_dist(const uint8_t *ring, uint8_t m, uint8_t i, int
   return bestDist;
 }
 
-__global__ void __launch_bounds__(64 * BND_WAVES) k_bound(const DevPlan *pl, const Counters *ctr, const uint32_t *surv,
-                                                       const uint32_t *surv_lm, const Loc *loc, uint64_t slot_ub,
-                                                       float *sbound) {
+__global__ void __launch_bounds__(64 * BND_WAVES) k_bound(const DevPlan *pl, const Counters *ctr,
+                                                       const uint32_t *sv_slot, const uint32_t *sv_lm,
+                                                       const Loc *sv_loc, float *sbound) {
   __shared__ __attribute__((aligned(16))) uint8_t s_ring[BND_WAVES][RING];
   stage_weights(&c_weights);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -2299,7 +2469,8 @@ __global__ void __launch_bounds__(64 * BND_WAVES) k_bound(const DevPlan *pl, con
   const int ng = pl->ngroups, m = pl->min_listi;
   const float INF = __int_as_float(0x7f800000);
   for (uint32_t i = blockIdx.x * BND_WAVES + wid; i < nsurv; i += gridDim.x * BND_WAVES) {
-    const uint32_t s = surv[i], lm = surv_lm[i];
+    const uint32_t s = sv_slot[i], lm = sv_lm[i];
+    const Loc *svl = sv_loc + (uint64_t)i * (uint32_t)pl->nlists;
     if (pl->sortby_group >= 0) {  // gbsortby: both prefilters are skipped (Posdb.cpp:6050-6051, 6350)
       if (lane == 0) sbound[i] = INF;
       continue;
@@ -2307,7 +2478,7 @@ __global__ void __launch_bounds__(64 * BND_WAVES) k_bound(const DevPlan *pl, con
     // lane g: getMaxPossibleScore's scan of group g
     BoundCore core{0, 0.0f};
     if (lane < ng && !(pl->gflags0[lane] & (BF_NEGATIVE | BF_FACET)))
-      core = group_bound_core(pl, ctr, lane, s, lm, loc, slot_ub);
+      core = group_bound_core(pl, ctr, lane, s, lm, svl);
     float B = INF;
     // filter 1 (m_doMaxScoreAlgo): bestDist 0, qdist 0 (Posdb.cpp:6327-6346)
     if (pl->do_max_score && lane < ng && !(pl->gflags0[lane] & (BF_NEGATIVE | BF_FACET))) {
@@ -2321,12 +2492,12 @@ __global__ void __launch_bounds__(64 * BND_WAVES) k_bound(const DevPlan *pl, con
       uint4 *r4 = reinterpret_cast<uint4 *>(ring);
       for (int q = lane; q < RING / 16; q += 64) r4[q] = make_uint4(~0u, ~0u, ~0u, ~0u);
       wave_lds_sync();
-      const int ourFirstPos = ring_fill(pl, ctr, m, s, lm, loc, slot_ub, ring, (uint8_t)m, lane);
+      const int ourFirstPos = ring_fill(pl, ctr, m, s, lm, svl, ring, (uint8_t)m, lane);
       const float tfw_m = pl->tfw[m];
       for (int g = 0; g < ng; g++) {
         if (g == m || (pl->gflags0[g] & (BF_NEGATIVE | BF_FACET))) continue;
         wave_lds_sync();
-        ring_fill(pl, ctr, g, s, lm, loc, slot_ub, ring, (uint8_t)g, lane);
+        ring_fill(pl, ctr, g, s, lm, svl, ring, (uint8_t)g, lane);
         wave_lds_sync();
         BoundCore cg;
         cg.state = __shfl(core.state, g, 64);
@@ -2367,13 +2538,13 @@ __device__ __forceinline__ uint32_t lower_bound_u64(const uint64_t *a, uint32_t 
   return lo - b;
 }
 
-__global__ void k_rank(const DevPlan *pl, const Counters *ctr, const uint32_t *surv, const uint64_t *sdoc,
+__global__ void k_rank(const DevPlan *pl, const Counters *ctr, const uint32_t *sv_slot, const uint64_t *sdoc,
                        uint32_t *order) {
   const uint32_t nsurv = (uint32_t)(ctr->surv_top >> 36);
   const int g0n = pl->g0n;
   uint32_t sb[MAXG0 + 1];
   for (int k = 0; k <= g0n; k++)
-    sb[k] = k == g0n ? nsurv : lower_bound_u32(surv, nsurv, (uint32_t)pl->g0base[k]);
+    sb[k] = k == g0n ? nsurv : lower_bound_u32(sv_slot, nsurv, (uint32_t)pl->g0base[k]);
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nsurv; i += gridDim.x * blockDim.x) {
     int k = 0;
     while (k + 1 < g0n && i >= sb[k + 1]) k++;
@@ -3090,7 +3261,7 @@ using namespace gbgpu;
 struct QuerySlot {
   std::mutex mu;
   hipStream_t stream = nullptr;
-  DevBuf tables, chunkcnt, cand, lmask, ulen, loc, surv, survoff, survlm, survu, perm, scratch, skey, sdoc, sel, gath, res;
+  DevBuf tables, chunkcnt, cand, cunit, bits, loc, svslot, svlm, svu, svdoc, svloc, scratch, skey, sel, gath, res;
   DevBuf dir;           // candidate directories, epoch-tagged (never cleared per query)
   DevBuf split, swin;   // docid splits: one piece's list windows; window table
   DevBuf blk, sflag, sbound, order, tree;  // site clustering: ordered compaction, bounds, TopTree state
@@ -3135,8 +3306,8 @@ struct QuerySlot {
   }
   void release() {
     if (stream) (void)hipStreamSynchronize(stream);
-    DevBuf *bufs[] = {&tables, &chunkcnt, &cand, &lmask, &ulen, &loc, &surv, &survoff, &survlm, &survu, &perm,
-                      &scratch, &skey, &sdoc, &sel, &gath, &res, &dir, &split, &swin,
+    DevBuf *bufs[] = {&tables, &chunkcnt, &cand, &cunit, &bits, &loc, &svslot, &svlm, &svu, &svdoc, &svloc,
+                      &scratch, &skey, &sel, &gath, &res, &dir, &split, &swin,
                       &blk, &sflag, &sbound, &order, &tree, &white, &wrej, &si};
     for (auto *b : bufs) b->release();
     if (h_stage) (void)hipHostFree(h_stage);
@@ -3538,6 +3709,8 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
         P.lists[id].ri = terms[g.qterm].number_int;
       }
       P.lists[id].group_bits |= neg ? NEG_BIT : (1u << j);
+      if (neg) P.neg_lists |= 1u << id;
+      else P.group_lists[j] |= 1u << id;
       if (!neg) {
         // shrinkSubLists' in-place order: groups in index order, sublists in
         // order (Posdb.cpp:5906-5914); the first use sees the list clean
@@ -3591,11 +3764,15 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   }
   // probe direction per list: candidate-driven while a 3 KiB chunk meets
   // about one wave-width of candidates, else run-driven
+  for (int id = 0; id < P.nlists; id++)
+    P.list_mult[id] = (uint8_t)__builtin_popcount(P.lists[id].group_bits & P.pos_mask & ~NEG_BIT);
+  P.probed_mask = 0;
   for (int id = 0; id < P.nlists; id++) {
     P.lists[id].probe = 0;
     if (P.lists[id].g0_array == 0) continue;
     const double per_chunk = (double)slot_ub * WCH_UNITS / std::max<uint32_t>(1, P.lists[id].units);
     P.lists[id].probe = per_chunk > 64.0 ? PROBE_BY_RUN : PROBE_BY_CAND;
+    P.probed_mask |= 1u << id;
   }
 
   q.g0c.clear();
@@ -3650,23 +3827,24 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   int rc2 = 0;
   rc2 |= q.tables.ensure(tbytes);
   rc2 |= q.chunkcnt.ensure(4 * std::max<size_t>(1, q.g0c.size()));
+  const uint32_t nwords = (uint32_t)((slot_ub + 31) / 32);
+  const uint32_t cgrid = std::max(1u, (uint32_t)((slot_ub + CTILE - 1) / CTILE));
   rc2 |= q.cand.ensure(8 * slot_ub);
-  rc2 |= q.lmask.ensure(4 * slot_ub);
-  rc2 |= q.ulen.ensure(4 * slot_ub);
+  rc2 |= q.cunit.ensure(4 * slot_ub);
+  rc2 |= q.bits.ensure(4 * (size_t)nwords * (uint64_t)P.nlists);
   rc2 |= q.loc.ensure(sizeof(Loc) * slot_ub * (uint64_t)P.nlists);
-  rc2 |= q.surv.ensure(4 * slot_ub);
-  rc2 |= q.survoff.ensure(8 * slot_ub);
+  rc2 |= q.svslot.ensure(4 * slot_ub);
+  rc2 |= q.svlm.ensure(4 * slot_ub);
+  rc2 |= q.svu.ensure(4 * slot_ub);
+  rc2 |= q.svdoc.ensure(8 * slot_ub);
+  rc2 |= q.svloc.ensure(sizeof(Loc) * slot_ub * (uint64_t)P.nlists);
   rc2 |= q.scratch.ensure(8 * scratch_ub);
-  rc2 |= q.survlm.ensure(4 * slot_ub);
-  rc2 |= q.survu.ensure(4 * slot_ub);
-  rc2 |= q.perm.ensure(4 * slot_ub * NBKT);  // NBKT bucket regions of slot_ub entries
   rc2 |= q.skey.ensure(4 * slot_ub);
-  rc2 |= q.sdoc.ensure(8 * slot_ub);
+  rc2 |= q.blk.ensure(sizeof(BlkInfo) * (size_t)cgrid);
   rc2 |= q.sel.ensure(sizeof(Select));
   rc2 |= q.gath.ensure(12 * (slot_ub + MAX_K) + 1024);
   rc2 |= q.res.ensure(q.res_bytes);
   if (clus) {
-    rc2 |= q.blk.ensure(sizeof(BlkTot) * (size_t)std::max<uint64_t>(1, (slot_ub + CTILE - 1) / CTILE));
     rc2 |= q.sflag.ensure(slot_ub);
     rc2 |= q.sbound.ensure(4 * slot_ub);
     if (P.g0n > 1) rc2 |= q.order.ensure(4 * slot_ub);
@@ -3719,17 +3897,20 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   const ProbeWork *dwork = q.tables.as<ProbeWork>(o_work);
   Counters *dctr = q.res.as<Counters>();
   Select *dsel = q.sel.as<Select>();
-  uint32_t *lmask = q.lmask.as<uint32_t>();
+  uint32_t *bits = q.bits.as<uint32_t>();
   Loc *loc = q.loc.as<Loc>();
-  hipLaunchKernelGGL(k_reset, dim3(16), dim3(BLOCK), 0, st, reinterpret_cast<uint32_t *>(dctr),
-                     (uint32_t)(sizeof(Counters) / 4), reinterpret_cast<uint32_t *>(dsel),
-                     (uint32_t)(sizeof(Select) / 4));
+  {
+    const uint32_t nb = nwords * (uint32_t)P.nlists;  // the probe bitmaps
+    const uint32_t rg = std::max(16u, std::min(1024u, nb / 2048));
+    hipLaunchKernelGGL(k_reset, dim3(rg), dim3(BLOCK), 0, st, reinterpret_cast<uint32_t *>(dctr),
+                       (uint32_t)(sizeof(Counters) / 4), reinterpret_cast<uint32_t *>(dsel),
+                       (uint32_t)(sizeof(Select) / 4), bits, nb);
+  }
   const uint32_t ng0 = (uint32_t)q.g0c.size();
   hipLaunchKernelGGL(k_count_runs, dim3(ng0), dim3(BLOCK), 0, st, dpl, dchunks, q.chunkcnt.as<uint32_t>());
   hipLaunchKernelGGL(k_scan_runs, dim3(1), dim3(1024), 0, st, ng0, q.chunkcnt.as<uint32_t>());
   hipLaunchKernelGGL(k_write_runs, dim3(ng0), dim3(BLOCK), 0, st, dpl, dchunks, q.chunkcnt.as<uint32_t>(),
-                     dafirst, q.cand.as<uint64_t>(), lmask, loc, q.ulen.as<uint32_t>(), slot_ub, dctr, ng0,
-                     q.dir.as<uint64_t>());
+                     dafirst, q.cand.as<uint64_t>(), q.cunit.as<uint32_t>(), dctr, ng0, q.dir.as<uint64_t>());
   if (ctx->profiling) HIPCHECK(hipEventRecord(q.ev[1], st));
   if (!q.pw.empty()) {
     auto kp = ctx->probe_mode == 5   ? k_probe<5, 2>
@@ -3742,17 +3923,15 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
                                      : k_probe<0, MAXG0>;
     const uint32_t nwork = (uint32_t)q.pw.size();
     hipLaunchKernelGGL(kp, dim3((nwork + PW - 1) / PW), dim3(64 * PW), 0, st, dpl, dwork, nwork,
-                       q.cand.as<uint64_t>(), lmask, loc, q.ulen.as<uint32_t>(), slot_ub, dctr,
-                       q.dir.as<uint64_t>());
+                       q.cand.as<uint64_t>(), bits, nwords, loc, dctr, q.dir.as<uint64_t>());
   }
   {
     uint32_t rbits = 0;  // range terms' lists outside the smallest group
     for (int l = 0; l < P.nlists; l++)
       if (P.lists[l].rmode && P.lists[l].g0_array < 0) rbits |= 1u << l;
     if (rbits) {
-      const uint32_t g = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(4096, (slot_ub + 255) / 256));
-      hipLaunchKernelGGL(k_range_filter, dim3(g), dim3(256), 0, st, dpl, dctr, rbits, lmask, q.ulen.as<uint32_t>(),
-                         loc, slot_ub);
+      const uint32_t g = std::max(1u, std::min(4096u, (nwords + 255) / 256));
+      hipLaunchKernelGGL(k_range_filter, dim3(g), dim3(256), 0, st, dpl, rbits, bits, nwords, loc);
     }
   }
   if (ctx->profiling) HIPCHECK(hipEventRecord(q.ev[2], st));
@@ -3767,26 +3946,32 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
                                                          : 3;
   static constexpr uint32_t kRC[5] = {24, 48, 64, 64, 24};  // LDS records per lane
   const uint32_t rcap = kRC[variant] / 2;  // size buckets: a column holds 2x a bucket-3 survivor's units
-  const uint32_t cgrid = std::max(1u, (uint32_t)((slot_ub + CTILE - 1) / CTILE));
   const uint64_t *dcand = q.cand.as<uint64_t>();
-  if (!P.clustering) {
-    hipLaunchKernelGGL(k_compact<0>, dim3(cgrid), dim3(CBLOCK), 0, st, dpl, lmask, q.ulen.as<uint32_t>(), slot_ub,
-                       dctr, q.surv.as<uint32_t>(), q.survoff.as<unsigned long long>(), q.survlm.as<uint32_t>(),
-                       (BlkTot *)nullptr, loc, dcand, q.survu.as<uint32_t>(), rcap, q.perm.as<uint32_t>());
+  const uint32_t *dcunit = q.cunit.as<uint32_t>();
+  BlkInfo *blk = q.blk.as<BlkInfo>();
+  uint32_t *svslot = q.svslot.as<uint32_t>(), *svlm = q.svlm.as<uint32_t>(), *svu = q.svu.as<uint32_t>();
+  uint64_t *svdoc = q.svdoc.as<uint64_t>();
+  Loc *svloc = q.svloc.as<Loc>();
+  // ordered (site clustering: the replay walks the survivors in docid order)
+  // puts every survivor in one bucket, in slot order
+  if (!clus) {
+    hipLaunchKernelGGL(k_cmp_count<false>, dim3(cgrid), dim3(CB), 0, st, dpl, dctr, dcunit, bits, nwords, loc, dcand,
+                       slot_ub, rcap, blk);
   } else {
-    // ordered: site clustering's replay walks the survivors in docid order
-    BlkTot *blk = q.blk.as<BlkTot>();
-    hipLaunchKernelGGL(k_compact<1>, dim3(cgrid), dim3(CBLOCK), 0, st, dpl, lmask, q.ulen.as<uint32_t>(), slot_ub,
-                       dctr, q.surv.as<uint32_t>(), q.survoff.as<unsigned long long>(), q.survlm.as<uint32_t>(), blk,
-                       loc, dcand, q.survu.as<uint32_t>(), rcap, q.perm.as<uint32_t>());
-    hipLaunchKernelGGL(k_compact_scan, dim3(1), dim3(1024), 0, st, cgrid, blk, dctr);
-    hipLaunchKernelGGL(k_compact<2>, dim3(cgrid), dim3(CBLOCK), 0, st, dpl, lmask, q.ulen.as<uint32_t>(), slot_ub,
-                       dctr, q.surv.as<uint32_t>(), q.survoff.as<unsigned long long>(), q.survlm.as<uint32_t>(), blk,
-                       loc, dcand, q.survu.as<uint32_t>(), rcap, q.perm.as<uint32_t>());
+    hipLaunchKernelGGL(k_cmp_count<true>, dim3(cgrid), dim3(CB), 0, st, dpl, dctr, dcunit, bits, nwords, loc, dcand,
+                       slot_ub, rcap, blk);
   }
+  hipLaunchKernelGGL(k_cmp_scan, dim3(1), dim3(1024), 0, st, dpl, cgrid, blk, dctr);
+  if (!clus) {
+    hipLaunchKernelGGL(k_cmp_write<false>, dim3(cgrid), dim3(CB), 0, st, dpl, dctr, dcunit, bits, nwords, loc, dcand,
+                       slot_ub, rcap, blk, svslot, svlm, svu, svdoc, svloc);
+  } else {
+    hipLaunchKernelGGL(k_cmp_write<true>, dim3(cgrid), dim3(CB), 0, st, dpl, dctr, dcunit, bits, nwords, loc, dcand,
+                       slot_ub, rcap, blk, svslot, svlm, svu, svdoc, svloc);
+  }
+  const unsigned long long arena_cap = (unsigned long long)(q.scratch.cap / 8);
   if (P.reshare_mask)
-    hipLaunchKernelGGL(k_ext_walk, dim3(1), dim3(64), 0, st, dpl, dctr, dcand, lmask, q.ulen.as<uint32_t>(),
-                       (unsigned long long)(q.scratch.cap / 8));
+    hipLaunchKernelGGL(k_ext_walk, dim3(1), dim3(64), 0, st, dpl, dctr, dcand, dcunit, bits, nwords, loc, arena_cap);
   if (ctx->profiling) HIPCHECK(hipEventRecord(q.ev[3], st));
   {
     const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((slot_ub + SCORE_TPB - 1) / SCORE_TPB, 8192));
@@ -3795,11 +3980,10 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
       HIPCHECK(hipMemsetAsync(ctx->d_sdbg, 0, 8192 * 64, st));
     }
     auto launch = [&](auto kern) {
-      hipLaunchKernelGGL(kern, dim3(grid), dim3(SCORE_TPB), 0, st, dpl, q.cand.as<uint64_t>(), dctr,
-                         q.surv.as<uint32_t>(), q.survlm.as<uint32_t>(), q.survoff.as<unsigned long long>(),
-                         q.survu.as<uint32_t>(), q.perm.as<uint32_t>(), loc, slot_ub, q.scratch.as<uint64_t>(),
-                         q.skey.as<uint32_t>(), q.sdoc.as<uint64_t>(), q.sflag.as<uint8_t>(), ctx->score_mode,
-                         ctx->d_sdbg);
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(SCORE_TPB), 0, st, dpl, (const uint64_t *)svdoc, dctr,
+                         (const uint32_t *)svslot, (const uint32_t *)svlm, (const uint32_t *)svu, (const Loc *)svloc,
+                         q.scratch.as<uint64_t>(), arena_cap, q.skey.as<uint32_t>(), q.sflag.as<uint8_t>(),
+                         ctx->score_mode, ctx->d_sdbg);
     };
     if (variant == 4) launch(k_score<2, 2, kRC[4]>);  // two groups of <= 2 sublists (config 2)
     else if (variant == 0) launch(k_score<2, 4, kRC[0]>);
@@ -3811,17 +3995,17 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   if (clus) {
     // site clustering: prefilter bounds, docid order, the TopTree replay
     const uint32_t bgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((slot_ub + BND_WAVES - 1) / BND_WAVES, 4096));
-    hipLaunchKernelGGL(k_bound, dim3(bgrid), dim3(64 * BND_WAVES), 0, st, dpl, dctr, q.surv.as<uint32_t>(),
-                       q.survlm.as<uint32_t>(), loc, slot_ub, q.sbound.as<float>());
+    hipLaunchKernelGGL(k_bound, dim3(bgrid), dim3(64 * BND_WAVES), 0, st, dpl, dctr, (const uint32_t *)svslot,
+                       (const uint32_t *)svlm, (const Loc *)svloc, q.sbound.as<float>());
     const uint32_t *order = nullptr;
     if (P.g0n > 1) {
       const uint32_t rgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((slot_ub + 255) / 256, 4096));
-      hipLaunchKernelGGL(k_rank, dim3(rgrid), dim3(256), 0, st, dpl, dctr, q.surv.as<uint32_t>(),
-                         q.sdoc.as<uint64_t>(), q.order.as<uint32_t>());
+      hipLaunchKernelGGL(k_rank, dim3(rgrid), dim3(256), 0, st, dpl, dctr, (const uint32_t *)svslot,
+                         (const uint64_t *)svdoc, q.order.as<uint32_t>());
       order = q.order.as<uint32_t>();
     }
     hipLaunchKernelGGL(k_tree_replay, dim3(1), dim3(64), 0, st, dctr, order, q.skey.as<uint32_t>(),
-                       q.sdoc.as<uint64_t>(), q.sflag.as<uint8_t>(), q.sbound.as<float>(),
+                       (const uint64_t *)svdoc, q.sflag.as<uint8_t>(), q.sbound.as<float>(),
                        (tree_phase & TREE_FINAL) ? (TreeState *)q.tree.p : q.tree.as<TreeState>(),
                        tree_params(q.docs_wanted, tree_phase), q.res.as<uint32_t>(res_keys_off()),
                        q.res.as<uint64_t>(res_docs_off(k)));
@@ -3847,7 +4031,7 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   uint32_t *bkey = q.gath.as<uint32_t>(align256(4 * (size_t)MAX_K) + align256(8 * (size_t)MAX_K));
   uint64_t *bdoc = q.gath.as<uint64_t>(align256(4 * (size_t)MAX_K) + align256(8 * (size_t)MAX_K) +
                                           align256(4 * slot_ub));
-  hipLaunchKernelGGL(k_select_gather, dim3(hgrid), dim3(BLOCK), 0, st, skey, q.sdoc.as<uint64_t>(), dctr, dsel,
+  hipLaunchKernelGGL(k_select_gather, dim3(hgrid), dim3(BLOCK), 0, st, skey, (const uint64_t *)svdoc, dctr, dsel,
                      akey, adoc, bkey, bdoc);
   hipLaunchKernelGGL(k_select_final, dim3(1), dim3(1024), 0, st, dsel, akey, adoc, bkey, bdoc, (uint32_t)k,
                      q.res.as<uint32_t>(res_keys_off()), q.res.as<uint64_t>(res_docs_off(k)));
@@ -3864,11 +4048,7 @@ static int fetch_hits(QuerySlot &q, uint32_t nsurv, std::vector<int64_t> &out) {
   const size_t base = out.size();
   if (!nsurv) return 0;
   out.resize(base + nsurv);
-  uint64_t *tmp = q.gath.as<uint64_t>();  // >= 8 * slot_ub bytes; free after the query
-  hipLaunchKernelGGL(k_gather_hits, dim3(std::min<uint32_t>(1024, (nsurv + 255) / 256)), dim3(256), 0, q.stream,
-                     q.surv.as<uint32_t>(), q.cand.as<uint64_t>(), nsurv, tmp);
-  HIPCHECK(hipGetLastError());
-  HIPCHECK(hipMemcpyAsync(out.data() + base, tmp, 8 * (size_t)nsurv, hipMemcpyDeviceToHost, q.stream));
+  HIPCHECK(hipMemcpyAsync(out.data() + base, q.svdoc.p, 8 * (size_t)nsurv, hipMemcpyDeviceToHost, q.stream));
   HIPCHECK(hipStreamSynchronize(q.stream));
   std::sort(out.begin() + base, out.end());
   return 0;
@@ -3937,18 +4117,17 @@ static int score_info(QuerySlot &q, const uint32_t *keys, const uint64_t *docs, 
   if (q.si.ensure(total)) return ENOMEM;
   hipStream_t st = q.stream;
   const uint32_t g = std::max(1u, std::min<uint32_t>(1024, (nsurv + 255) / 256));
-  hipLaunchKernelGGL(k_si_keys, dim3(g), dim3(256), 0, st, q.surv.as<uint32_t>(), q.cand.as<uint64_t>(), nsurv,
+  hipLaunchKernelGGL(k_si_keys, dim3(g), dim3(256), 0, st, q.svdoc.as<uint64_t>(), nsurv,
                      q.si.as<uint64_t>(o_key), q.si.as<uint32_t>(o_val));
   HIPCHECK(si_sort_pairs(q.si.as<uint8_t>(o_tmp), sort_tmp, q.si.as<uint64_t>(o_key), q.si.as<uint64_t>(o_skey),
                          q.si.as<uint32_t>(o_val), q.si.as<uint32_t>(o_sval), nsurv, st));
-  hipLaunchKernelGGL(k_si_dir, dim3(nl), dim3(1024), 0, st, q.tables.as<DevPlan>(), q.loc.as<Loc>(), q.slot_ub,
-                     q.surv.as<uint32_t>(), q.survlm.as<uint32_t>(), q.si.as<uint32_t>(o_sval), nsurv,
-                     q.si.as<uint32_t>(o_cum));
+  hipLaunchKernelGGL(k_si_dir, dim3(nl), dim3(1024), 0, st, q.tables.as<DevPlan>(), q.svloc.as<Loc>(),
+                     q.svlm.as<uint32_t>(), q.si.as<uint32_t>(o_sval), nsurv, q.si.as<uint32_t>(o_cum));
   HIPCHECK(hipMemcpyAsync(q.si.as<uint8_t>(o_tdoc), docs, 8 * (size_t)n, hipMemcpyHostToDevice, st));
   hipLaunchKernelGGL(k_scoreinfo, dim3((n + SCORE_TPB - 1) / SCORE_TPB), dim3(SCORE_TPB), 0, st,
-                     q.tables.as<DevPlan>(), q.res.as<Counters>(), q.surv.as<uint32_t>(), q.survlm.as<uint32_t>(),
-                     q.survoff.as<unsigned long long>(), q.loc.as<Loc>(), q.slot_ub, q.scratch.as<uint64_t>(),
-                     q.si.as<uint64_t>(o_tdoc), q.si.as<uint64_t>(o_skey), q.si.as<uint32_t>(o_sval),
+                     q.tables.as<DevPlan>(), q.res.as<Counters>(), q.svslot.as<uint32_t>(), q.svlm.as<uint32_t>(),
+                     q.svu.as<uint32_t>(), q.svloc.as<Loc>(), q.scratch.as<uint64_t>(),
+                     (unsigned long long)(q.scratch.cap / 8), q.si.as<uint64_t>(o_tdoc), q.si.as<uint64_t>(o_skey), q.si.as<uint32_t>(o_sval),
                      q.si.as<uint32_t>(o_cum), nsurv, (uint32_t)n, q.si.as<SurvOut>(o_info),
                      q.si.as<int32_t>(o_cnt), q.si.as<gbgpu_single_score>(o_ss), scap,
                      q.si.as<gbgpu_pair_score>(o_ps), pcap);
@@ -3969,6 +4148,7 @@ static int score_info(QuerySlot &q, const uint32_t *keys, const uint64_t *docs, 
   for (int t = 0; t < n; t++) {
     if (info[t].ok == -1) return GBGPU_ECORRUPT;      // a tree docid with no survivor entry
     if (info[t].ok == -2) return GBGPU_EUNSUPPORTED;  // a getWordPosList path not replayed
+    if (info[t].ok == -3) return GBGPU_ECAPACITY;     // record arena exhausted
     const int cs = cnt[2 * t], cp = cnt[2 * t + 1];
     if (cs > scap || cp > pcap) return GBGPU_ECAPACITY;
     gbgpu_docid_score d;

@@ -153,6 +153,10 @@ struct DevPlan {
   uint32_t g0sh[MAXG0];
   uint64_t g0dmin[MAXG0], g0dmax[MAXG0];
   uint64_t g0dir[MAXG0];       // first entry of each array's directory
+  uint32_t probed_mask;        // bit l: k_probe scans list l (its matches are bitmap bits)
+  uint32_t group_lists[MAXG];  // bit l: list l is a sublist of group g
+  uint32_t neg_lists;          // bit l: list l is a sublist of a negative group
+  uint8_t list_mult[MAXL];     // positive groups list l is a sublist of (its runs' record copies)
   DevList lists[MAXL];
 };
 

@@ -159,20 +159,24 @@ struct NoRec {
 
 // getSingleTermScore, Posdb.cpp:3087-3301.  bestPos = record index of the
 // best non-body occurrence or -1; REC receives the top list (pdcs path).
-template <int NQ, class RP, class REC = NoRec>
+// T: the top list's register capacity, a bound the caller guarantees on the
+// slots it can fill -- min(m_realMaxTop, the group's records) -- so the
+// unrolled bookkeeping below costs T steps per record, not MAX_TOP.
+template <int NQ, class RP, class REC = NoRec, int T = MAX_TOP>
 __device__ __forceinline__ float single_term_score(const ScoreCtx<NQ> &c, const DocView<NQ, RP> &d, int i, int *bestPos,
                                                   REC *rec = nullptr) {
   const Weights &W = s_weights;
   float nonBodyMax = -1.0;
   int minx = 0;
   float minv = 0.0f;  // bestScores[minx]
-  float bestScores[MAX_TOP];
-  int bestwpi[MAX_TOP];
-  uint32_t bestmhg[MAX_TOP];
+  float bestScores[T];
+  int bestwpi[REC::on ? T : 1];
+  uint32_t bestmhg[T];
+  uint32_t besths = 0;  // bit q: slot q's key is a half-stop wiki bigram (r_hswb)
 #pragma unroll
-  for (int q = 0; q < MAX_TOP; q++) {
+  for (int q = 0; q < T; q++) {
     bestScores[q] = 0.0f;
-    bestwpi[q] = 0;
+    if constexpr (REC::on) bestwpi[q] = 0;
     bestmhg[q] = 0xff;
   }
   int numTop = 0;
@@ -214,7 +218,7 @@ __device__ __forceinline__ float single_term_score(const ScoreCtx<NQ> &c, const 
     float broScore = 0.0f;
     if (hg != GB_HG_INLINKTEXT) {
 #pragma unroll
-      for (int q = MAX_TOP - 1; q >= 0; q--) {
+      for (int q = T - 1; q >= 0; q--) {
         if (q < numTop && bestmhg[q] == mhg) {  // lowest matching slot
           bro = q;
           broScore = bestScores[q];
@@ -231,18 +235,19 @@ __device__ __forceinline__ float single_term_score(const ScoreCtx<NQ> &c, const 
       slot = minx;
     }
 #pragma unroll
-    for (int q = 0; q < MAX_TOP; q++) {
+    for (int q = 0; q < T; q++) {
       if (q == slot) {
         bestScores[q] = score;
-        bestwpi[q] = r;
+        if constexpr (REC::on) bestwpi[q] = r;
         bestmhg[q] = mhg;
       }
     }
+    if (slot >= 0) besths = (besths & ~(1u << slot)) | (r_hswb(k) << slot);
     if (numTop >= rmt) {
       minx = 0;
       minv = bestScores[0];
 #pragma unroll
-      for (int q = 1; q < MAX_TOP; q++) {
+      for (int q = 1; q < T; q++) {
         if (q < rmt && !(bestScores[q] > minv)) {
           minx = q;
           minv = bestScores[q];
@@ -257,9 +262,9 @@ __device__ __forceinline__ float single_term_score(const ScoreCtx<NQ> &c, const 
   *bestPos = bp;
   float sum = 0.0;
 #pragma unroll
-  for (int q = 0; q < MAX_TOP; q++) {
+  for (int q = 0; q < T; q++) {
     if (q < numTop) {
-      if (r_hswb(d.rec[bestwpi[q]]))
+      if (besths >> q & 1)
         sum += (bestScores[q] * GB_WIKI_BIGRAM_WEIGHT * GB_WIKI_BIGRAM_WEIGHT);
       else
         sum += bestScores[q];
@@ -268,7 +273,7 @@ __device__ __forceinline__ float single_term_score(const ScoreCtx<NQ> &c, const 
   sum *= c.pl->tfw[i];
   sum *= c.pl->tfw[i];
   if constexpr (REC::on) {
-    for (int q = 0; q < MAX_TOP; q++)
+    for (int q = 0; q < T; q++)
       if (q < numTop) rec->single(c.pl, i, bestScores[q], d.rec[rget(bestwpi, q)]);
   }
   return sum;
@@ -478,12 +483,13 @@ __device__ __forceinline__ void eval_window(ScoreCtx<NQ> &c, const DocView<NQ, R
   for (int q = 0; q < NQ; q++) c.window[q] = ptrs[q];
 }
 
-// getTermPairScoreForAny, Posdb.cpp:3631-4344; REC receives the top pairs
+// getTermPairScoreForAny, Posdb.cpp:3631-4344 (T as in single_term_score:
+// a bound on the slots the pair's records can fill); REC receives the top pairs
 // (pdcs path, 4195-4280) with their record indices and fixedDistance flag --
 // which the reference only assigns when dist < 50 or the distance is fixed,
 // so it carries over from the previous scored pair otherwise (false at the
 // start, where the reference's is uninitialised)
-template <int NQ, class RP, class REC = NoRec>
+template <int NQ, class RP, class REC = NoRec, int T = MAX_TOP>
 __device__ __forceinline__ float pair_score_any(const ScoreCtx<NQ> &c, const DocView<NQ, RP> &d, int i, int j,
                                                REC *rec = nullptr) {
   const Weights &W = s_weights;
@@ -514,13 +520,13 @@ __device__ __forceinline__ float pair_score_any(const ScoreCtx<NQ> &c, const Doc
   float score = 0.0f;
   int minx = -1;
   float minv = 0.0f;  // bestScores[minx]
-  float bestScores[MAX_TOP];
-  uint32_t bestmhg1[MAX_TOP], bestmhg2[MAX_TOP];
-  int bestwpi[REC::on ? MAX_TOP : 1], bestwpj[REC::on ? MAX_TOP : 1];
-  bool bestFixed[REC::on ? MAX_TOP : 1];
+  float bestScores[T];
+  uint32_t bestmhg1[T], bestmhg2[T];
+  int bestwpi[REC::on ? T : 1], bestwpj[REC::on ? T : 1];
+  bool bestFixed[REC::on ? T : 1];
   bool fixedDistance = false;
 #pragma unroll
-  for (int q = 0; q < MAX_TOP; q++) {
+  for (int q = 0; q < T; q++) {
     bestScores[q] = 0.0f;
     bestmhg1[q] = 0xff;
     bestmhg2[q] = 0xff;
@@ -605,7 +611,7 @@ __device__ __forceinline__ float pair_score_any(const ScoreCtx<NQ> &c, const Doc
       int bro = -1;
       float broScore = 0.0f;
 #pragma unroll
-      for (int q = MAX_TOP - 1; q >= 0; q--) {
+      for (int q = T - 1; q >= 0; q--) {
         if (q < numTop && ((bestmhg1[q] == mhg1 && hg1 != GB_HG_INLINKTEXT) ||
                            (bestmhg2[q] == mhg2 && hg2 != GB_HG_INLINKTEXT))) {
           bro = q;  // lowest matching slot
@@ -622,7 +628,7 @@ __device__ __forceinline__ float pair_score_any(const ScoreCtx<NQ> &c, const Doc
         slot = minx;
       }
 #pragma unroll
-      for (int q = 0; q < MAX_TOP; q++) {
+      for (int q = 0; q < T; q++) {
         if (q == slot) {
           bestScores[q] = score;
           bestmhg1[q] = mhg1;
@@ -638,7 +644,7 @@ __device__ __forceinline__ float pair_score_any(const ScoreCtx<NQ> &c, const Doc
         minx = 0;
         minv = bestScores[0];
 #pragma unroll
-        for (int q = 1; q < MAX_TOP; q++) {
+        for (int q = 1; q < T; q++) {
           if (q < rmt && !(bestScores[q] > minv)) {
             minx = q;
             minv = bestScores[q];
@@ -666,13 +672,13 @@ __device__ __forceinline__ float pair_score_any(const ScoreCtx<NQ> &c, const Doc
   }
   float sum = 0.0;
 #pragma unroll
-  for (int q = 0; q < MAX_TOP; q++)
+  for (int q = 0; q < T; q++)
     if (q < numTop) sum += bestScores[q];
   sum *= wts;
   sum *= pl->tfw[i];
   sum *= pl->tfw[j];
   if constexpr (REC::on) {
-    for (int q = 0; q < MAX_TOP; q++)
+    for (int q = 0; q < T; q++)
       if (q < numTop)
         rec->pair(pl, i, j, bestScores[q], wts, qdist, d.rec[rget(bestwpi, q)], d.rec[rget(bestwpj, q)],
                   rget(bestFixed, q));
@@ -685,7 +691,7 @@ __device__ __forceinline__ float pair_score_any(const ScoreCtx<NQ> &c, const Doc
 // (minScore <= 0); siteRank/docLang come from the first key of the first
 // present group (Posdb.cpp:6985-7003).  sm: this lane's score-matrix column
 // (npairs<NQ>() floats at stride smStride).
-template <int NQ, class RP, class REC = NoRec>
+template <int NQ, class RP, class REC = NoRec, int T = MAX_TOP>
 __device__ __forceinline__ bool score_doc(const Weights *w, const DevPlan *pl, const DocView<NQ, RP> &d, int siteRank, int docLang,
                                  float *sm, int smStride, float *outScore, int stop = 0, REC *rec = nullptr) {
   ScoreCtx<NQ> c;
@@ -739,7 +745,7 @@ __device__ __forceinline__ bool score_doc(const Weights *w, const DevPlan *pl, c
   for (int i = 0; i < c.nq; i++) {
     if ((c.excl >> i & 1)) continue;
     int bp;
-    const float sts = single_term_score<NQ, RP, REC>(c, d, i, &bp, rec);
+    const float sts = single_term_score<NQ, RP, REC, T>(c, d, i, &bp, rec);
     rset(bestPos, i, bp);
     if (sts < minSingleScore) minSingleScore = sts;
   }
@@ -916,7 +922,7 @@ __device__ __forceinline__ bool score_doc(const Weights *w, const DevPlan *pl, c
       if ((c.excl >> j & 1)) continue;
       if (!(d.present >> i & 1)) continue;
       if (!(d.present >> j & 1)) continue;
-      const float score = pair_score_any<NQ, RP, REC>(c, d, i, j, rec);
+      const float score = pair_score_any<NQ, RP, REC, T>(c, d, i, j, rec);
       if (score >= minPairScore && minPairScore >= 0.0) continue;
       minPairScore = score;
     }
