@@ -28,9 +28,10 @@
 //        one lane per survivor: mini-merge of each group (Posdb.cpp:6559-
 //        6778) into the survivor's arena records, then the scorers of
 //        scoring.h (weight tables staged in LDS).
-//   k_select_hist x3 / k_select_gather / k_select_final
-//        radix select of the k best (score desc, docid asc) replacing TopTree
-//        (TopTree.cpp:195-516), then one small LDS sort.
+//   k_topk
+//        the k best (score desc, docid asc) replacing TopTree (TopTree.cpp:
+//        195-516): k_score's 16-bit key histogram, one gather, the last block
+//        narrows the k-th key in LDS and sorts.
 //
 // ONE device->host copy returns counters + top list.  No host
 // synchronisation happens between kernels: counts live in device memory and
@@ -69,7 +70,7 @@ constexpr int CHUNK_LOAD = CHUNK_BYTES + 16;     // + the tail of a 12-byte key
 constexpr int MAX_RUNS = CHUNK_UNITS / 2;        // a run is >= 2 units
 constexpr int TILE = 2048;                       // final top-k sort capacity
 constexpr int MAX_K = 1536;                      // TILE - MAX_K ties merged per round
-constexpr int SEL_BINS = 4096;                   // radix-select bins per pass
+constexpr int SEL_HBINS = 65536;                 // top-k histogram bins (key >> 16)
 constexpr int TREE_CAP = 4096;                   // site-clustering TopTree nodes held in LDS
 constexpr int LIST_PAD = CHUNK_LOAD + 128;
 
@@ -91,7 +92,7 @@ struct ListExt {
 struct Counters {
   uint32_t filtered;  // m_filtered: scored docids dropped by the paging filter (Posdb.cpp:7327-7347)
   uint32_t corrupt;
-  unsigned long long surv_top;  // survivors << 36 | their run units (k_cmp_scan)
+  unsigned long long surv_top;  // survivors << 36 | their run units (k_cmp_write block 0)
   uint32_t g0count[MAXG0];
   uint32_t anysurv;  // bit l: list l has a run in some survivor
   uint32_t tree_n;   // site clustering: TopTree nodes written by k_tree_replay
@@ -100,19 +101,17 @@ struct Counters {
   uint32_t pad[2];
   unsigned long long dmax_all;  // largest survivor docid
   ListExt ext[MAXL];
-  uint32_t bcnt[8];    // survivors per size bucket (k_cmp_scan), NBKT
+  uint32_t bcnt[8];    // survivors per size bucket (k_cmp_write block 0), NBKT
   uint32_t bstart[8];  // each bucket's first survivor position
   unsigned long long arena_top;  // global record arena: units handed out (k_ext_walk, k_score, k_scoreinfo)
 };
 
-// radix-select state (3 passes over the 32-bit score keys: 12+12+8 bits)
+// top-k select state (k_score's histogram, k_topk's gathers)
 struct Select {
-  uint32_t hist[3][SEL_BINS];
-  uint32_t prefix;  // selected key prefix so far
-  uint32_t need;    // entries still to take inside the selected prefix
-  uint32_t all;     // fewer valid entries than k: take them all
-  uint32_t thr;     // final threshold key T
-  uint32_t na, nb;  // gathered: keys > T, keys == T
+  uint32_t hist[SEL_HBINS];  // scored keys per top-16-bit prefix (k_score)
+  uint32_t na, nb;           // k_topk's gathers: A (prefix above P), B (prefix P)
+  uint32_t done;             // k_topk blocks finished (the last one selects)
+  uint32_t pad;
 };
 
 // where a docid's run sits in one list: first unit and length in units
@@ -239,7 +238,7 @@ __global__ void k_reset(uint32_t *a, uint32_t na, uint32_t *b, uint32_t nb, uint
 }
 
 // ----------------------------------------------- candidate extraction (G0)
-__global__ void __launch_bounds__(BLOCK) k_count_runs(const DevPlan *pl, const G0Chunk *chunks,
+__global__ void __launch_bounds__(BLOCK) k_count_runs(const DevPlan *__restrict__ pl, const G0Chunk *chunks,
                                                       uint32_t *chunk_count) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[CHUNK_LOAD];
   __shared__ uint32_t tmp[BLOCK / 64];
@@ -319,7 +318,7 @@ __device__ bool run_in_range_first(const DevList &L, uint32_t u, uint32_t e) {
 // ends where the next candidate's starts), the directory, and the
 // whitelist / range-term rejections.  Match state lives in per-list bitmaps
 // (k_probe) cleared by k_reset, so no per-slot mask is written here.
-__global__ void __launch_bounds__(BLOCK) k_write_runs(const DevPlan *pl, const G0Chunk *chunks,
+__global__ void __launch_bounds__(BLOCK) k_write_runs(const DevPlan *__restrict__ pl, const G0Chunk *chunks,
                                                       const uint32_t *chunk_off,
                                                       const uint32_t *array_first_chunk,
                                                       uint64_t *cand, uint32_t *cunit, Counters *ctr,
@@ -466,12 +465,12 @@ __device__ uint32_t wave_lower_bound(const uint64_t *a, uint32_t n, uint64_t key
 // cand_resolve() finds d from there -- the four candidates from the entry on
 // are loaded together, a walk beyond them (a crowded bucket, or a bucket
 // whose entry came from a later chunk) is the rare case.
-__device__ __forceinline__ uint64_t dir_entry(const DevPlan *pl, int k, uint32_t n, const uint64_t *dir, uint64_t d) {
+__device__ __forceinline__ uint64_t dir_entry(const DevPlan *__restrict__ pl, int k, uint32_t n, const uint64_t *dir, uint64_t d) {
   const uint64_t dmin = pl->g0dmin[k];
   if (n == 0 || d < dmin || d > pl->g0dmax[k]) return 0;
   return dir[pl->g0dir[k] + ((d - dmin) >> pl->g0sh[k])];
 }
-__device__ __forceinline__ int64_t cand_resolve(const DevPlan *pl, uint64_t e, const uint64_t *ck, uint32_t n,
+__device__ __forceinline__ int64_t cand_resolve(const DevPlan *__restrict__ pl, uint64_t e, const uint64_t *ck, uint32_t n,
                                                 uint64_t d) {
   if ((uint32_t)(e >> 32) != pl->epoch) return -1;  // empty bucket
   uint32_t i = (uint32_t)e;
@@ -499,7 +498,7 @@ __device__ __forceinline__ int64_t cand_resolve(const DevPlan *pl, uint64_t e, c
 // directory entry of key's bucket (or of the next non-empty one of 64) lands
 // within a few slots of the answer; a 64-wide window settles it.  Falls back
 // to the 64-ary search when the window misses.
-__device__ uint32_t wave_lower_bound_dir(const DevPlan *pl, int k, const uint64_t *ck, uint32_t n,
+__device__ uint32_t wave_lower_bound_dir(const DevPlan *__restrict__ pl, int k, const uint64_t *ck, uint32_t n,
                                          const uint64_t *dir, uint64_t key, int lane) {
   const uint64_t dmin = pl->g0dmin[k];
   if (n == 0 || key <= dmin) return 0;
@@ -686,7 +685,7 @@ __device__ uint64_t first_run_doc(const DevList &L, uint32_t u, uint32_t u1, int
 // Dense list: candidates search the run starts.  Loop body VMEM ops are the
 // next-but-one chunk and one candidate block per array, both unconditional.
 template <int MODE, int G0>
-__device__ void probe_by_cand(const DevPlan *pl, const ProbeWork &w, const DevList &L, const uint64_t *cand,
+__device__ void probe_by_cand(const DevPlan *__restrict__ pl, const ProbeWork &w, const DevList &L, const uint64_t *cand,
                               const Counters *ctr, const uint64_t *dir, ProbeLds &S, const ProbeOut &po, int lane) {
   const int g0n = G0 <= 2 ? G0 : pl->g0n;
   const uint8_t *lp = L.p;
@@ -820,7 +819,7 @@ __device__ void probe_by_cand(const DevPlan *pl, const ProbeWork &w, const DevLi
 // Sparse list: each run start looks its docid up in the arrays, in order;
 // the first array holding it takes the run.
 template <int G0>
-__device__ void probe_by_run(const DevPlan *pl, const ProbeWork &w, const DevList &L, const uint64_t *cand,
+__device__ void probe_by_run(const DevPlan *__restrict__ pl, const ProbeWork &w, const DevList &L, const uint64_t *cand,
                              const Counters *ctr, const uint64_t *dir, ProbeLds &S, const ProbeOut &po, int lane) {
   const int g0n = G0 <= 2 ? G0 : pl->g0n;
   uint32_t nk[G0];
@@ -896,7 +895,7 @@ __device__ void probe_by_run(const DevPlan *pl, const ProbeWork &w, const DevLis
 // MODE (diagnostic, GBGPU_PROBE_MODE): 0 full, 1 stop after the run-start
 // compaction, 2 load chunks only, 3 skip the run-driven lists.
 template <int MODE, int G0>
-__global__ void __launch_bounds__(64 * PW) k_probe(const DevPlan *pl, const ProbeWork *work, uint32_t nwork,
+__global__ void __launch_bounds__(64 * PW) k_probe(const DevPlan *__restrict__ pl, const ProbeWork *work, uint32_t nwork,
                                                    const uint64_t *cand, uint32_t *bits, uint32_t nwords, Loc *loc,
                                                    const Counters *ctr, const uint64_t *dir) {
   __shared__ ProbeLds s_lds[PW];
@@ -923,7 +922,7 @@ __global__ void __launch_bounds__(64 * PW) k_probe(const DevPlan *pl, const Prob
 // run it matches, and this pass (launched only for such queries) withdraws
 // the out-of-range ones from the list's bitmap.  One thread per bitmap word
 // (32 slots), so no atomics: the probe is over.
-__global__ void k_range_filter(const DevPlan *pl, uint32_t rbits, uint32_t *bits, uint32_t nwords, const Loc *loc) {
+__global__ void k_range_filter(const DevPlan *__restrict__ pl, uint32_t rbits, uint32_t *bits, uint32_t nwords, const Loc *loc) {
   const uint32_t nl = (uint32_t)pl->nlists;
   for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < nwords; w += gridDim.x * blockDim.x) {
     for (uint32_t rb = rbits; rb; rb &= rb - 1) {
@@ -954,9 +953,9 @@ __global__ void k_range_filter(const DevPlan *pl, uint32_t rbits, uint32_t *bits
 // Two passes over the slots, CB threads x CSPT consecutive slots a block:
 //   k_cmp_count  survivors per size bucket of each block, the lists with a
 //                run in some survivor, the re-shrink partials (BlkInfo);
-//   k_cmp_scan   one block: each bucket's start, each block's offset in
-//                every bucket, the totals;
-//   k_cmp_write  every survivor's record at its final position -- buckets
+//   k_cmp_write  each block's offset in every bucket and the bucket starts
+//                (from the counts), then every survivor's record at its
+//                final position -- buckets
 //                in order, slot order inside a bucket: slot, list mask, run
 //                units, docid, and its run locations ([pos][nl]), so k_score
 //                reads its survivors' data contiguously.
@@ -975,12 +974,13 @@ __host__ __device__ __forceinline__ int size_bucket(uint32_t u, uint32_t rc) {
 __host__ __device__ __forceinline__ int bucket_shift(int b) { return b == 0 ? 3 : b == 1 ? 4 : b == 2 ? 5 : 6; }
 
 constexpr int CB = 256;            // compaction threads per block
-constexpr int CSPT = 8;            // consecutive slots per thread (a quarter bitmap word)
-constexpr int CTILE = CB * CSPT;   // 2048 slots per block
+constexpr int CSPT = 32;           // consecutive slots per thread: one bitmap word
+constexpr int CTILE = CB * CSPT;   // 8192 slots per block (one block scan: <= 2^16 per bucket)
+static_assert(CTILE < 65536, "packed 16-bit bucket counts");
 constexpr int XR = 4;              // re-shrunk lists reduced per block (more: global atomics)
 
 struct BlkInfo {
-  uint32_t cnt[NBKT];  // survivors per bucket; k_cmp_scan turns them into the block's offsets
+  uint32_t cnt[NBKT];  // survivors per bucket; k_cmp_write sums them into the block's offsets
   uint32_t any, pad;   // lists with a run in some survivor of the block
   unsigned long long usum;       // the survivors' run units (their records' upper bound)
   unsigned long long dall;       // largest survivor docid (re-shrink queries)
@@ -989,7 +989,7 @@ struct BlkInfo {
 };
 
 // bit l: list l holds the docid of slot s (array a's slot)
-__device__ __forceinline__ uint32_t slot_lmask(const DevPlan *pl, const uint32_t *bits, uint32_t nwords, uint64_t s,
+__device__ __forceinline__ uint32_t slot_lmask(const DevPlan *__restrict__ pl, const uint32_t *bits, uint32_t nwords, uint64_t s,
                                                int a) {
   uint32_t lm = a == 0 ? 1u << pl->g0list[0] : 0u;
   for (uint32_t pm = pl->probed_mask; pm; pm &= pm - 1) {
@@ -1001,7 +1001,7 @@ __device__ __forceinline__ uint32_t slot_lmask(const DevPlan *pl, const uint32_t
 // slot s's run in list l (l in its mask): array 0's own list from the
 // candidates' run starts (a run ends where the next one starts), the others
 // as k_probe recorded them
-__device__ __forceinline__ Loc slot_loc(const DevPlan *pl, const Counters *ctr, const uint32_t *cunit, const Loc *loc,
+__device__ __forceinline__ Loc slot_loc(const DevPlan *__restrict__ pl, const Counters *ctr, const uint32_t *cunit, const Loc *loc,
                                         uint64_t s, int l) {
   if (l == pl->g0list[0] && s < pl->g0base[1]) {
     const uint32_t u = cunit[s];
@@ -1012,19 +1012,19 @@ __device__ __forceinline__ Loc slot_loc(const DevPlan *pl, const Counters *ctr, 
 }
 // a docid survives when a list of every positive group and none of a
 // negative group holds it: a loop over the (wave-uniform) groups' list masks
-__device__ __forceinline__ bool lm_survives(const DevPlan *pl, uint32_t lm) {
+__device__ __forceinline__ bool lm_survives(const DevPlan *__restrict__ pl, uint32_t lm) {
   if (lm & pl->neg_lists) return false;
   for (uint32_t pm = pl->pos_mask; pm; pm &= pm - 1)
     if (!(lm & pl->group_lists[__ffs(pm) - 1])) return false;
   return true;
 }
 // array of slot s, or -1 past every array's written slots
-__device__ __forceinline__ int slot_array(const DevPlan *pl, const Counters *ctr, uint64_t s) {
+__device__ __forceinline__ int slot_array(const DevPlan *__restrict__ pl, const Counters *ctr, uint64_t s) {
   int a = 0;
   while (a + 1 < pl->g0n && s >= pl->g0base[a + 1]) a++;
   return s - pl->g0base[a] < ctr->g0count[a] ? a : -1;
 }
-__device__ bool slot_is_survivor(const DevPlan *pl, const Counters *ctr, const uint32_t *bits, uint32_t nwords,
+__device__ bool slot_is_survivor(const DevPlan *__restrict__ pl, const Counters *ctr, const uint32_t *bits, uint32_t nwords,
                                  uint64_t s, uint32_t *lm_out = nullptr) {
   const int a = slot_array(pl, ctr, s);
   if (a < 0) return false;
@@ -1036,7 +1036,7 @@ __device__ bool slot_is_survivor(const DevPlan *pl, const Counters *ctr, const u
 // arena units of slot s's records: each run once per positive group its
 // list belongs to (a shared bigram sublist is merged into both groups); the
 // lists are walked in a wave-uniform loop
-__device__ uint32_t slot_units(const DevPlan *pl, const Counters *ctr, const uint32_t *cunit, const Loc *loc, uint64_t s,
+__device__ uint32_t slot_units(const DevPlan *__restrict__ pl, const Counters *ctr, const uint32_t *cunit, const Loc *loc, uint64_t s,
                                uint32_t lm) {
   uint32_t u = 0;
   for (int l = 0; l < pl->nlists; l++)
@@ -1044,56 +1044,129 @@ __device__ uint32_t slot_units(const DevPlan *pl, const Counters *ctr, const uin
   return u;
 }
 
-// the survivors among this thread's CSPT slots: bit q of the result
-template <bool ORDERED>
-__device__ __forceinline__ uint32_t cmp_thread(const DevPlan *pl, const Counters *ctr, const uint32_t *cunit,
-                                               const uint32_t *bits, uint32_t nwords, const Loc *loc,
-                                               uint64_t slot_ub, uint32_t rc, uint64_t s0, uint32_t (&lmv)[CSPT],
-                                               uint32_t (&uv)[CSPT], uint32_t (&bk)[CSPT]) {
-  uint32_t ok = 0;
-  // the probed lists' bits of the thread's slots (CSPT consecutive slots
-  // inside one bitmap word)
-#pragma unroll
-  for (int q = 0; q < CSPT; q++) lmv[q] = 0;
-  if (s0 < slot_ub) {
-    for (uint32_t pm = pl->probed_mask; pm; pm &= pm - 1) {
-      const int l = __ffs(pm) - 1;
-      const uint32_t sub = bits[(uint64_t)l * nwords + (s0 >> 5)] >> (s0 & 31);
-#pragma unroll
-      for (int q = 0; q < CSPT; q++) lmv[q] |= ((sub >> q) & 1u) << l;
-    }
-  }
-  int a = 0;
-  while (a + 1 < pl->g0n && s0 >= pl->g0base[a + 1]) a++;
-#pragma unroll
-  for (int q = 0; q < CSPT; q++) {
-    const uint64_t s = s0 + q;
-    uv[q] = 0;
-    bk[q] = 0;
-    if (s >= slot_ub) {
-      lmv[q] = 0;
-      continue;
-    }
-    while (a + 1 < pl->g0n && s >= pl->g0base[a + 1]) a++;
-    if (s - pl->g0base[a] >= ctr->g0count[a] || (pl->use_rej && pl->wrej[s])) {
-      lmv[q] = 0;
-      continue;
-    }
-    const uint32_t lm = lmv[q] | (a == 0 ? 1u << pl->g0list[0] : 0u);
-    lmv[q] = lm;
-    if (!lm_survives(pl, lm)) continue;
-    const uint32_t u = slot_units(pl, ctr, cunit, loc, s, lm);
-    uv[q] = u;
-    bk[q] = ORDERED ? 0u : (uint32_t)size_bucket(u, rc);
-    ok |= 1u << q;
-  }
-  return ok;
+// bits q of a 32-slot word (first slot s0) with lo <= s0 + q < hi
+__device__ __forceinline__ uint32_t range_bits(uint64_t s0, uint64_t lo, uint64_t hi) {
+  if (hi <= lo || hi <= s0 || lo >= s0 + 32) return 0u;
+  const uint32_t a = lo > s0 ? (uint32_t)(lo - s0) : 0u;
+  const uint32_t b = hi < s0 + 32 ? (uint32_t)(hi - s0) : 32u;
+  const uint32_t mb = b >= 32 ? 0xffffffffu : ((1u << b) - 1u);
+  return mb & ~((1u << a) - 1u);
 }
 
+// One bitmap word's 32 slots, bit-parallel: the probed lists' bits, the
+// slots of array 0 (whose own list is not probed: its bit is implied), and
+// the survivors -- a written, voted slot whose lists hit every positive group
+// and no negative one (Posdb.cpp:5154-5171, 4871-4946).
+struct CmpWord {
+  uint32_t bw[MAXL];
+  uint32_t own0;
+  uint32_t surv;
+};
+__device__ __forceinline__ void cmp_word(const DevPlan *__restrict__ pl, const Counters *ctr, const uint32_t *bits, uint32_t nwords,
+                                         uint32_t w, CmpWord &c) {
+  const uint64_t s0 = (uint64_t)w * 32;
+  const uint32_t pm = pl->probed_mask;
+#pragma unroll
+  for (int l = 0; l < MAXL; l++) c.bw[l] = (pm >> l & 1) ? bits[(uint64_t)l * nwords + w] : 0u;
+  uint32_t valid = 0;
+  for (int a = 0; a < pl->g0n; a++) valid |= range_bits(s0, pl->g0base[a], pl->g0base[a] + ctr->g0count[a]);
+  c.own0 = range_bits(s0, pl->g0base[0], pl->g0base[0] + ctr->g0count[0]);
+  uint32_t surv = valid;
+  if (surv && pl->use_rej) {  // not voted: whitelist / a range term's first group (k_write_runs)
+    const v4u *r = reinterpret_cast<const v4u *>(pl->wrej + s0);
+    const v4u r0 = r[0], r1 = r[1];
+    const uint32_t wd[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+    uint32_t rej = 0;
+#pragma unroll
+    for (int i = 0; i < 32; i++) rej |= ((wd[i >> 2] >> ((i & 3) * 8)) & 0xffu) ? 1u << i : 0u;
+    surv &= ~rej;
+  }
+  const uint32_t nm = pl->neg_lists;
+#pragma unroll
+  for (int l = 0; l < MAXL; l++)
+    if (nm >> l & 1) surv &= ~c.bw[l];
+  const int l0 = pl->g0list[0];
+  for (uint32_t gm = pl->pos_mask; gm; gm &= gm - 1) {
+    const uint32_t gl = pl->group_lists[__ffs(gm) - 1];
+    uint32_t gh = (gl >> l0 & 1) ? c.own0 : 0u;
+#pragma unroll
+    for (int l = 0; l < MAXL; l++)
+      if (gl >> l & 1) gh |= c.bw[l];
+    surv &= gh;
+  }
+  c.surv = surv;
+}
+// slot s0 + q's list mask
+__device__ __forceinline__ uint32_t cmp_lm(const DevPlan *__restrict__ pl, const CmpWord &c, int q) {
+  uint32_t lm = (c.own0 >> q & 1) ? 1u << pl->g0list[0] : 0u;
+#pragma unroll
+  for (int l = 0; l < MAXL; l++) lm |= ((c.bw[l] >> q) & 1u) << l;
+  return lm;
+}
+// the slot's run in list l (l in its mask): array 0's own list from the
+// candidates' run starts (a run ends where the next one starts), the others
+// as k_probe recorded them
+__device__ __forceinline__ Loc cmp_loc(const DevPlan *__restrict__ pl, const Counters *ctr, const uint32_t *cunit, const Loc *loc,
+                                       uint64_t s, int l, bool own) {
+  if (own && l == pl->g0list[0]) {
+    const uint32_t u = cunit[s];
+    const uint32_t e = s + 1 < pl->g0base[0] + ctr->g0count[0] ? cunit[s + 1] : pl->lists[l].units;
+    return Loc{u, e - u};
+  }
+  return loc[s * (uint32_t)pl->nlists + l];
+}
+// its record units: each run once per positive group its list belongs to
+__device__ __forceinline__ uint32_t cmp_units(const DevPlan *__restrict__ pl, const Counters *ctr, const uint32_t *cunit,
+                                              const Loc *loc, uint64_t s, uint32_t lm, bool own) {
+  uint32_t u = 0;
+  const uint32_t nl = (uint32_t)pl->nlists;
+  const int l0 = pl->g0list[0];
+  if (own) {
+    const uint32_t u0 = cunit[s];
+    const uint32_t e = s + 1 < pl->g0base[0] + ctr->g0count[0] ? cunit[s + 1] : pl->lists[l0].units;
+    u += (e - u0) * (uint32_t)pl->list_mult[l0];
+  }
+  const uint32_t om = own ? lm & ~(1u << l0) : lm;
+#pragma unroll
+  for (int l = 0; l < MAXL; l++)
+    if (om >> l & 1) u += loc[s * nl + l].len * (uint32_t)pl->list_mult[l];
+  return u;
+}
+
+// Both passes stage the block's survivors (slot, list mask), in slot order,
+// in LDS and then work on them one per thread, so every survivor's loads
+// (run locations, docid) go out together instead of one thread walking its
+// word's survivors serially.
+constexpr int CSV = 2048;  // survivors staged per round
+struct CmpStage {
+  uint32_t slot[CSV];
+  uint32_t lm[CSV];
+};
+// stage survivors [base, base + CSV) of the block (ex: this thread's first)
+__device__ __forceinline__ void cmp_stage(const DevPlan *__restrict__ pl, const CmpWord &c, uint32_t w, uint32_t ex,
+                                          uint32_t base, CmpStage &S) {
+  const uint32_t n = __popc(c.surv);
+  if (!n || ex >= base + CSV || ex + n <= base) return;
+  uint32_t idx = ex;
+  for (uint32_t sm = c.surv; sm; sm &= sm - 1, idx++) {
+    if (idx < base || idx >= base + CSV) continue;
+    const int q = __ffs(sm) - 1;
+    S.slot[idx - base] = w * 32 + (uint32_t)q;
+    S.lm[idx - base] = cmp_lm(pl, c, q);
+  }
+}
+
+// Pass 1: per block of CTILE slots (one bitmap word a thread), the survivors
+// per size bucket, the lists with a run in some survivor, the run units and
+// the re-shrink partials.
 template <bool ORDERED>
-__global__ void __launch_bounds__(CB) k_cmp_count(const DevPlan *pl, Counters *ctr, const uint32_t *cunit,
-                                                  const uint32_t *bits, uint32_t nwords, const Loc *loc,
-                                                  const uint64_t *cand, uint64_t slot_ub, uint32_t rc, BlkInfo *blk) {
+__global__ void __launch_bounds__(CB) k_cmp_count(const DevPlan *__restrict__ pl, Counters *ctr,
+                                                  const uint32_t *__restrict__ cunit, const uint32_t *__restrict__ bits,
+                                                  uint32_t nwords, const Loc *__restrict__ loc,
+                                                  const uint64_t *__restrict__ cand, uint32_t rc,
+                                                  BlkInfo *__restrict__ blk) {
+  __shared__ CmpStage S;
+  __shared__ uint32_t tmp[CB / 64];
   __shared__ uint32_t s_cnt[NBKT];
   __shared__ uint32_t s_any;
   __shared__ unsigned long long s_dall, s_usum, s_xu[XR], s_xd[XR];
@@ -1107,42 +1180,51 @@ __global__ void __launch_bounds__(CB) k_cmp_count(const DevPlan *pl, Counters *c
     s_dall = 0;
     s_usum = 0;
   }
-  __syncthreads();
-  const uint64_t s0 = (uint64_t)blockIdx.x * CTILE + threadIdx.x * CSPT;
-  uint32_t lmv[CSPT], uv[CSPT], bk[CSPT];
-  const uint32_t ok = cmp_thread<ORDERED>(pl, ctr, cunit, bits, nwords, loc, slot_ub, rc, s0, lmv, uv, bk);
+  const uint32_t w = blockIdx.x * CB + threadIdx.x;
+  CmpWord c;
+  c.surv = 0;
+  if (w < nwords) cmp_word(pl, ctr, bits, nwords, w, c);
+  uint32_t total;
+  const uint32_t ex = block_exclusive_scan<CB>(__popc(c.surv), tmp, &total);
   const uint32_t xmask = pl->reshare_mask;
   uint32_t any = 0, usum = 0;
   unsigned long long tdall = 0, txu[XR] = {0, 0, 0, 0}, txd[XR] = {0, 0, 0, 0};
+  for (uint32_t base = 0; base < total; base += CSV) {
+    cmp_stage(pl, c, w, ex, base, S);
+    __syncthreads();
+    const uint32_t nr = min((uint32_t)CSV, total - base);
+    for (uint32_t i = threadIdx.x; i < nr; i += CB) {
+      const uint64_t s = S.slot[i];
+      const uint32_t lm = S.lm[i];
+      const bool own = (lm >> pl->g0list[0]) & 1;
+      const uint32_t u = cmp_units(pl, ctr, cunit, loc, s, lm, own);
+      atomicAdd(&s_cnt[ORDERED ? 0 : size_bucket(u, rc)], 1u);
+      any |= lm;
+      usum += u;
+      if (xmask) {
+        // re-shrunk lists (k_ext_walk): their survivor run units and last docid
+        const unsigned long long d = cand[s];
+        tdall = d > tdall ? d : tdall;
+        int r = 0;
+        for (uint32_t x = xmask; x; x &= x - 1, r++) {
+          const int l = __ffs(x) - 1;
+          if (!(lm >> l & 1)) continue;
+          const uint32_t len = cmp_loc(pl, ctr, cunit, loc, s, l, own).len;
+          if (r < XR) {
 #pragma unroll
-  for (int q = 0; q < CSPT; q++) {
-    if (!(ok >> q & 1)) continue;
-    const uint64_t s = s0 + q;
-    atomicAdd(&s_cnt[bk[q]], 1u);
-    any |= lmv[q];
-    usum += uv[q];
-    if (xmask) {
-      // re-shrunk lists (k_ext_walk): their survivor run units and last docid
-      const unsigned long long d = cand[s];
-      tdall = d > tdall ? d : tdall;
-      int r = 0;
-      for (uint32_t x = xmask; x; x &= x - 1, r++) {
-        const int l = __ffs(x) - 1;
-        if (!(lmv[q] >> l & 1)) continue;
-        const uint32_t len = slot_loc(pl, ctr, cunit, loc, s, l).len;
-        if (r < XR) {
-#pragma unroll
-          for (int t = 0; t < XR; t++)
-            if (t == r) {
-              txu[t] += len;
-              txd[t] = d > txd[t] ? d : txd[t];
-            }
-        } else {
-          atomicAdd(&ctr->ext[l].units, (unsigned long long)len);
-          atomicMax(&ctr->ext[l].dmax, d);
+            for (int t = 0; t < XR; t++)
+              if (t == r) {
+                txu[t] += len;
+                txd[t] = d > txd[t] ? d : txd[t];
+              }
+          } else {
+            atomicAdd(&ctr->ext[l].units, (unsigned long long)len);
+            atomicMax(&ctr->ext[l].dmax, d);
+          }
         }
       }
     }
+    __syncthreads();
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
@@ -1187,187 +1269,199 @@ __global__ void __launch_bounds__(CB) k_cmp_count(const DevPlan *pl, Counters *c
   }
 }
 
-// one block: per bucket, the exclusive scan of the blocks' counts (written
-// back as offsets), the bucket starts, and every total into the counters.
-// Each thread loads its blocks' records once; the eight bucket scans run in
-// registers (the loads, not the arithmetic, are the latency).
-__global__ void __launch_bounds__(1024) k_cmp_scan(const DevPlan *pl, uint32_t nblk, BlkInfo *blk, Counters *ctr) {
-  __shared__ uint32_t tw[16][NBKT];
-  __shared__ uint32_t s_carry[NBKT];
-  __shared__ uint32_t s_any;
-  __shared__ unsigned long long s_dall, s_usum, s_xu[XR], s_xd[XR];
+// Pass 2: every survivor's record at its final position -- buckets in
+// order, slot order inside a bucket: slot, list mask, run units, docid, and
+// its run locations ([pos][nl]), so k_score reads its survivors' data
+// contiguously.  Each block sums the counts of the blocks before it (its
+// offsets) and of all blocks (the bucket starts); block 0 publishes the
+// totals.
+template <bool ORDERED>
+__global__ void __launch_bounds__(CB) k_cmp_write(const DevPlan *__restrict__ pl, Counters *__restrict__ ctr,
+                                                  const uint32_t *__restrict__ cunit, const uint32_t *__restrict__ bits,
+                                                  uint32_t nwords, const Loc *__restrict__ loc,
+                                                  const uint64_t *__restrict__ cand, uint32_t rc,
+                                                  const BlkInfo *__restrict__ blk, uint32_t nblk,
+                                                  uint32_t *__restrict__ sv_slot, uint32_t *__restrict__ sv_lm,
+                                                  uint32_t *__restrict__ sv_u, uint64_t *__restrict__ sv_doc,
+                                                  Loc *__restrict__ sv_loc) {
+  __shared__ CmpStage S;
+  __shared__ uint32_t tmp[CB / 64];
+  __shared__ uint32_t s_pre[NBKT], s_tot[NBKT], s_carry[NBKT];
+  __shared__ uint32_t s_wc[CB / 64][NBKT];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  if (threadIdx.x == 0) {
-    s_any = 0;
-    s_dall = 0;
-    s_usum = 0;
+  if (threadIdx.x < NBKT) {
+    s_pre[threadIdx.x] = 0;
+    s_tot[threadIdx.x] = 0;
+    s_carry[threadIdx.x] = 0;
   }
-  if (threadIdx.x < XR) {
-    s_xu[threadIdx.x] = 0;
-    s_xd[threadIdx.x] = 0;
-  }
-  if (threadIdx.x < NBKT) s_carry[threadIdx.x] = 0;
-  uint32_t any = 0;
-  unsigned long long dall = 0, usum = 0, xu[XR] = {0, 0, 0, 0}, xd[XR] = {0, 0, 0, 0};
-  const bool xm = pl->reshare_mask != 0;
   __syncthreads();
-  for (uint32_t base = 0; base < nblk; base += 1024) {
-    const uint32_t i = base + threadIdx.x;
-    uint32_t v[NBKT], x[NBKT];
-    if (i < nblk) {
-      const BlkInfo &bi = blk[i];
+  {
+    uint32_t pre[NBKT], tot[NBKT];
 #pragma unroll
-      for (int b = 0; b < NBKT; b++) v[b] = bi.cnt[b];
-      any |= bi.any;
-      usum += bi.usum;
-      if (xm) {
-        dall = bi.dall > dall ? bi.dall : dall;
-#pragma unroll
-        for (int t = 0; t < XR; t++) {
-          xu[t] += bi.xu[t];
-          xd[t] = bi.xd[t] > xd[t] ? bi.xd[t] : xd[t];
-        }
-      }
-    } else {
-#pragma unroll
-      for (int b = 0; b < NBKT; b++) v[b] = 0;
-    }
-#pragma unroll
-    for (int b = 0; b < NBKT; b++) x[b] = v[b];
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
+    for (int b = 0; b < NBKT; b++) pre[b] = tot[b] = 0;
+    for (uint32_t i = threadIdx.x; i < nblk; i += CB) {
 #pragma unroll
       for (int b = 0; b < NBKT; b++) {
-        const uint32_t y = __shfl_up(x[b], o, 64);
-        if (lane >= o) x[b] += y;
+        const uint32_t v = blk[i].cnt[b];
+        tot[b] += v;
+        pre[b] += i < blockIdx.x ? v : 0u;
       }
     }
-    if (lane == 63) {
-#pragma unroll
-      for (int b = 0; b < NBKT; b++) tw[wid][b] = x[b];
-    }
-    __syncthreads();
 #pragma unroll
     for (int b = 0; b < NBKT; b++) {
-      uint32_t pre = s_carry[b], tot = 0;
-      for (int w = 0; w < 16; w++) {
-        pre += w < wid ? tw[w][b] : 0u;
-        tot += tw[w][b];
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) {
+        pre[b] += __shfl_xor(pre[b], off, 64);
+        tot[b] += __shfl_xor(tot[b], off, 64);
       }
-      if (i < nblk) blk[i].cnt[b] = pre + x[b] - v[b];
-      x[b] = tot;  // this chunk's total
+    }
+    if (lane == 0) {
+#pragma unroll
+      for (int b = 0; b < NBKT; b++) {
+        if (pre[b]) atomicAdd(&s_pre[b], pre[b]);
+        if (tot[b]) atomicAdd(&s_tot[b], tot[b]);
+      }
+    }
+  }
+  if (blockIdx.x == 0) {
+    // the totals: counts, bucket starts, list union, units, re-shrink sums
+    uint32_t any = 0;
+    unsigned long long usum = 0, dall = 0, xu[XR] = {0, 0, 0, 0}, xd[XR] = {0, 0, 0, 0};
+    for (uint32_t i = threadIdx.x; i < nblk; i += CB) {
+      const BlkInfo &bi = blk[i];
+      any |= bi.any;
+      usum += bi.usum;
+      dall = bi.dall > dall ? bi.dall : dall;
+#pragma unroll
+      for (int t = 0; t < XR; t++) {
+        xu[t] += bi.xu[t];
+        xd[t] = bi.xd[t] > xd[t] ? bi.xd[t] : xd[t];
+      }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      any |= __shfl_xor(any, off, 64);
+      usum += __shfl_xor(usum, off, 64);
+      const unsigned long long o = __shfl_xor(dall, off, 64);
+      dall = o > dall ? o : dall;
+#pragma unroll
+      for (int t = 0; t < XR; t++) {
+        xu[t] += __shfl_xor(xu[t], off, 64);
+        const unsigned long long od = __shfl_xor(xd[t], off, 64);
+        xd[t] = od > xd[t] ? od : xd[t];
+      }
+    }
+    __shared__ uint32_t s_any;
+    __shared__ unsigned long long s_usum, s_dall, s_xu[XR], s_xd[XR];
+    if (threadIdx.x == 0) {
+      s_any = 0;
+      s_usum = 0;
+      s_dall = 0;
+    }
+    if (threadIdx.x < XR) {
+      s_xu[threadIdx.x] = 0;
+      s_xd[threadIdx.x] = 0;
     }
     __syncthreads();
-    if (threadIdx.x < NBKT) s_carry[threadIdx.x] += x[threadIdx.x & (NBKT - 1)];
-    __syncthreads();
-  }
+    if (lane == 0) {
+      atomicOr(&s_any, any);
+      atomicAdd(&s_usum, usum);
+      atomicMax(&s_dall, dall);
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    any |= __shfl_xor(any, off, 64);
-    usum += __shfl_xor(usum, off, 64);
-  }
-  if (lane == 0) {
-    if (any) atomicOr(&s_any, any);
-    if (usum) atomicAdd(&s_usum, usum);
-  }
-  if (xm) {
-    if (dall) atomicMax(&s_dall, dall);
-#pragma unroll
-    for (int t = 0; t < XR; t++)
-      if (xu[t]) {
+      for (int t = 0; t < XR; t++) {
         atomicAdd(&s_xu[t], xu[t]);
         atomicMax(&s_xd[t], xd[t]);
       }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t acc = 0;
+      for (int b = 0; b < NBKT; b++) {
+        ctr->bstart[b] = acc;
+        ctr->bcnt[b] = s_tot[b];
+        acc += s_tot[b];
+      }
+      ctr->surv_top = ((unsigned long long)acc << 36) | (s_usum & ((1ull << 36) - 1));
+      ctr->anysurv = s_any;
+      ctr->dmax_all = s_dall;
+      int r = 0;
+      for (uint32_t x = pl->reshare_mask; x && r < XR; x &= x - 1, r++) {
+        const int l = __ffs(x) - 1;
+        ctr->ext[l].units += s_xu[r];
+        if (s_xd[r] > ctr->ext[l].dmax) ctr->ext[l].dmax = s_xd[r];
+      }
+    }
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
+  uint32_t bstart[NBKT], boff[NBKT];
+  {
     uint32_t acc = 0;
+#pragma unroll
     for (int b = 0; b < NBKT; b++) {
-      ctr->bstart[b] = acc;
-      ctr->bcnt[b] = s_carry[b];
-      acc += s_carry[b];
-    }
-    ctr->surv_top = ((unsigned long long)acc << 36) | (s_usum & ((1ull << 36) - 1));
-    ctr->anysurv = s_any;
-    ctr->dmax_all = s_dall;
-    int r = 0;
-    for (uint32_t x = pl->reshare_mask; x && r < XR; x &= x - 1, r++) {
-      const int l = __ffs(x) - 1;
-      ctr->ext[l].units += s_xu[r];
-      if (s_xd[r] > ctr->ext[l].dmax) ctr->ext[l].dmax = s_xd[r];
+      bstart[b] = acc;
+      acc += s_tot[b];
+      boff[b] = s_pre[b];
     }
   }
-}
-
-// the survivors' records at their final positions
-template <bool ORDERED>
-__global__ void __launch_bounds__(CB) k_cmp_write(const DevPlan *pl, const Counters *ctr, const uint32_t *cunit,
-                                                  const uint32_t *bits, uint32_t nwords, const Loc *loc,
-                                                  const uint64_t *cand, uint64_t slot_ub, uint32_t rc,
-                                                  const BlkInfo *blk, uint32_t *sv_slot, uint32_t *sv_lm,
-                                                  uint32_t *sv_u, uint64_t *sv_doc, Loc *sv_loc) {
-  __shared__ uint64_t tw[2][CB / 64];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const uint64_t s0 = (uint64_t)blockIdx.x * CTILE + threadIdx.x * CSPT;
-  uint32_t lmv[CSPT], uv[CSPT], bk[CSPT];
-  const uint32_t ok = cmp_thread<ORDERED>(pl, ctr, cunit, bits, nwords, loc, slot_ub, rc, s0, lmv, uv, bk);
-  // this thread's survivors per bucket, 16 bits each, buckets 0-3 / 4-7
-  uint64_t c[2] = {0, 0};
-#pragma unroll
-  for (int q = 0; q < CSPT; q++) {
-    if (!(ok >> q & 1)) continue;
-    const uint64_t inc = 1ull << (16 * (bk[q] & 3));
-    if (bk[q] < 4) c[0] += inc;
-    else c[1] += inc;
-  }
-  // block exclusive scan of both packed words (no field overflows: <= CTILE)
-  uint64_t x[2] = {c[0], c[1]};
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-#pragma unroll
-    for (int h = 0; h < 2; h++) {
-      const uint64_t y = __shfl_up(x[h], o, 64);
-      if (lane >= o) x[h] += y;
-    }
-  }
-  if (lane == 63) {
-    tw[0][wid] = x[0];
-    tw[1][wid] = x[1];
-  }
-  __syncthreads();
-  uint64_t pre[2] = {0, 0};
-  for (int w = 0; w < wid; w++) {
-    pre[0] += tw[0][w];
-    pre[1] += tw[1][w];
-  }
-  pre[0] += x[0] - c[0];
-  pre[1] += x[1] - c[1];
-  if (!ok) return;
-  const BlkInfo &bi = blk[blockIdx.x];
+  const uint32_t w = blockIdx.x * CB + threadIdx.x;
+  CmpWord c;
+  c.surv = 0;
+  if (w < nwords) cmp_word(pl, ctr, bits, nwords, w, c);
+  uint32_t total;
+  const uint32_t ex = block_exclusive_scan<CB>(__popc(c.surv), tmp, &total);
   const uint32_t nl = (uint32_t)pl->nlists;
-  // the thread's survivors in slot order: per bucket, the next position
+  const int l0 = pl->g0list[0];
+  const uint64_t lt = (1ull << lane) - 1;
+  for (uint32_t base = 0; base < total; base += CSV) {
+    cmp_stage(pl, c, w, ex, base, S);
+    __syncthreads();
+    const uint32_t nr = min((uint32_t)CSV, total - base);
+    // in steps of CB survivors, in order: ranks inside each bucket
+    for (uint32_t i0 = 0; i0 < nr; i0 += CB) {
+      const uint32_t i = i0 + threadIdx.x;
+      const bool act = i < nr;
+      const uint64_t s = act ? S.slot[i] : 0;
+      const uint32_t lm = act ? S.lm[i] : 0;
+      const bool own = (lm >> l0) & 1;
+      const uint32_t u = act ? cmp_units(pl, ctr, cunit, loc, s, lm, own) : 0;
+      const uint32_t b = ORDERED ? 0u : (uint32_t)size_bucket(u, rc);
+      uint32_t rk = 0;
 #pragma unroll
-  for (int q = 0; q < CSPT; q++) {
-    if (!(ok >> q & 1)) continue;
-    const uint32_t b = bk[q];
-    const uint32_t sh16 = 16 * (b & 3);
-    uint32_t r;
-    if (b < 4) {
-      r = (uint32_t)((pre[0] >> sh16) & 0xffff);
-      pre[0] += 1ull << sh16;
-    } else {
-      r = (uint32_t)((pre[1] >> sh16) & 0xffff);
-      pre[1] += 1ull << sh16;
-    }
-    const uint32_t pos = ctr->bstart[b] + bi.cnt[b] + r;
-    const uint64_t s = s0 + q;
-    sv_slot[pos] = (uint32_t)s;
-    sv_lm[pos] = lmv[q];
-    sv_u[pos] = uv[q];
-    sv_doc[pos] = cand[s];
-    for (uint32_t xm = lmv[q]; xm; xm &= xm - 1) {
-      const int l = __ffs(xm) - 1;
-      sv_loc[(uint64_t)pos * nl + l] = slot_loc(pl, ctr, cunit, loc, s, l);
+      for (int bb = 0; bb < NBKT; bb++) {
+        const uint64_t m = __ballot(act && b == (uint32_t)bb);
+        if (b == (uint32_t)bb) rk = (uint32_t)__popcll(m & lt);
+        if (lane == 0) s_wc[wid][bb] = (uint32_t)__popcll(m);
+      }
+      __syncthreads();
+      uint32_t wpre = 0;
+#pragma unroll
+      for (int bb = 0; bb < NBKT; bb++)
+        if (b == (uint32_t)bb) {
+          for (int w2 = 0; w2 < wid; w2++) wpre += s_wc[w2][bb];
+          wpre += s_carry[bb];
+        }
+      if (act) {
+        uint32_t pos = 0;
+#pragma unroll
+        for (int bb = 0; bb < NBKT; bb++)
+          if (b == (uint32_t)bb) pos = bstart[bb] + boff[bb];
+        pos += wpre + rk;
+        sv_slot[pos] = (uint32_t)s;
+        sv_lm[pos] = lm;
+        sv_u[pos] = u;
+        sv_doc[pos] = cand[s];
+        for (uint32_t xm = lm; xm; xm &= xm - 1) {
+          const int l = __ffs(xm) - 1;
+          sv_loc[(uint64_t)pos * nl + l] = cmp_loc(pl, ctr, cunit, loc, s, l, own);
+        }
+      }
+      __syncthreads();
+      if (threadIdx.x < NBKT) {
+        uint32_t add = 0;
+        for (int w2 = 0; w2 < CB / 64; w2++) add += s_wc[w2][threadIdx.x];
+        s_carry[threadIdx.x] += add;
+      }
+      __syncthreads();
     }
   }
 }
@@ -1382,7 +1476,7 @@ __global__ void __launch_bounds__(CB) k_cmp_write(const DevPlan *pl, const Count
 // survivor would copy a misparsed run -- not emulated, flagged instead
 // (GBGPU_EUNSUPPORTED; about 2^-20 per query).  One wave per list.
 // slot of candidate docid d in any array, if that slot survived; ~0 if none
-__device__ uint64_t survivor_slot(const DevPlan *pl, const Counters *ctr, const uint64_t *cand, const uint32_t *bits,
+__device__ uint64_t survivor_slot(const DevPlan *__restrict__ pl, const Counters *ctr, const uint64_t *cand, const uint32_t *bits,
                                   uint32_t nwords, uint64_t d, int lane) {
   for (int k = 0; k < pl->g0n; k++) {
     const uint64_t *ck = cand + pl->g0base[k];
@@ -1393,7 +1487,7 @@ __device__ uint64_t survivor_slot(const DevPlan *pl, const Counters *ctr, const 
   return ~0ull;
 }
 
-__global__ void __launch_bounds__(64) k_ext_walk(const DevPlan *pl, Counters *ctr, const uint64_t *cand,
+__global__ void __launch_bounds__(64) k_ext_walk(const DevPlan *__restrict__ pl, Counters *ctr, const uint64_t *cand,
                                                  const uint32_t *cunit, const uint32_t *bits, uint32_t nwords,
                                                  const Loc *loc, unsigned long long arena_cap) {
   const int lane = threadIdx.x;
@@ -1502,7 +1596,7 @@ struct SubRun {
     return k < len0 ? own + (size_t)k * 6 : ext + (size_t)(k - len0) * 6;
   }
 };
-__device__ __forceinline__ SubRun sub_run_at(const DevPlan *pl, const Counters *ctr, Loc lc, int lid, int g, int x,
+__device__ __forceinline__ SubRun sub_run_at(const DevPlan *__restrict__ pl, const Counters *ctr, Loc lc, int lid, int g, int x,
                                              uint64_t s) {
   gu8 *base = gl(pl->lists[lid].p);
   SubRun r{base + (size_t)lc.unit * 6, base, lc.len, lc.len};
@@ -1514,7 +1608,7 @@ __device__ __forceinline__ SubRun sub_run_at(const DevPlan *pl, const Counters *
   return r;
 }
 // survivor `pos`'s run in list lid (its record's run locations)
-__device__ __forceinline__ SubRun sub_run(const DevPlan *pl, const Counters *ctr, const Loc *sv_loc, uint32_t pos,
+__device__ __forceinline__ SubRun sub_run(const DevPlan *__restrict__ pl, const Counters *ctr, const Loc *sv_loc, uint32_t pos,
                                           int lid, int g, int x, uint64_t s) {
   return sub_run_at(pl, ctr, sv_loc[(uint64_t)pos * (uint32_t)pl->nlists + lid], lid, g, x, s);
 }
@@ -1545,7 +1639,7 @@ struct SurvOut {
 };
 
 template <int NQ, int NS, class RP, class REC = NoRec>
-__device__ __forceinline__ void score_survivor(const DevPlan *pl, const Counters *ctr, uint32_t s, uint32_t lm,
+__device__ __forceinline__ void score_survivor(const DevPlan *__restrict__ pl, const Counters *ctr, uint32_t s, uint32_t lm,
                                                uint32_t anys, const Loc *svloc, RP rec, float *smcol,
                                                uint32_t *key_out, int diag, uint32_t *nrec_out,
                                                bool stamp, uint64_t &tmerge, uint64_t (&tm)[3],
@@ -1841,11 +1935,11 @@ __device__ __forceinline__ void score_survivor(const DevPlan *pl, const Counters
 // data (slot, list mask, units, run locations) is read at its position, so
 // a wave's reads are contiguous; its key goes to skey at the same position.
 template <int NQ, int NS, int RC>
-__global__ void __launch_bounds__(SCORE_TPB) k_score(const DevPlan *pl, const uint64_t *sv_doc, Counters *ctr,
+__global__ void __launch_bounds__(SCORE_TPB) k_score(const DevPlan *__restrict__ pl, const uint64_t *sv_doc, Counters *ctr,
                                                      const uint32_t *sv_slot, const uint32_t *sv_lm,
                                                      const uint32_t *sv_u, const Loc *sv_loc, uint64_t *arena,
                                                      unsigned long long arena_cap, uint32_t *skey, uint8_t *sflag,
-                                                     int diag, uint64_t *dbg) {
+                                                     int diag, uint64_t *dbg, uint32_t *khist) {
   static_assert(SCORE_TPB == 64, "LdsRecs columns are one wave wide");
   __shared__ float s_sm[npairs<NQ>() * SCORE_TPB];
   __shared__ uint32_t s_rlo[RC * 64];
@@ -1949,6 +2043,7 @@ __global__ void __launch_bounds__(SCORE_TPB) k_score(const DevPlan *pl, const ui
         if (filt) key = 0;
       }
       skey[i] = key;
+      if (khist && key) atomicAdd(&khist[key >> 16], 1u);  // k_topk's first pass
       // site clustering: the replay counts m_filtered, since a docid the
       // prefilters skip never reaches the paging test (Posdb.cpp:6341-6345)
       if (pl->clustering) sflag[i] = filt ? 1 : 0;
@@ -2001,7 +2096,7 @@ struct ScoreRec {
   gbgpu_single_score *ss;
   gbgpu_pair_score *ps;
   int ns, np, scap, pcap;
-  __device__ void single(const DevPlan *pl, int i, float best, uint64_t r) {
+  __device__ void single(const DevPlan *__restrict__ pl, int i, float best, uint64_t r) {
     if (ns < scap) {
       gbgpu_single_score x;
       __builtin_memset(&x, 0, sizeof x);
@@ -2027,7 +2122,7 @@ struct ScoreRec {
     }
     ns++;
   }
-  __device__ void pair(const DevPlan *pl, int i, int j, float best, float wts, int32_t qdist, uint64_t r1,
+  __device__ void pair(const DevPlan *__restrict__ pl, int i, int j, float best, float wts, int32_t qdist, uint64_t r1,
                        uint64_t r2, bool fixed) {
     if (np < pcap) {
       gbgpu_pair_score x;
@@ -2087,7 +2182,7 @@ __global__ void k_si_keys(const uint64_t *sv_doc, uint32_t nsurv, uint64_t *key,
 
 // one block per list: cum[l][k] = units, in list l, of the survivors ranked
 // below k (k = 0..nsurv)
-__global__ void __launch_bounds__(1024) k_si_dir(const DevPlan *pl, const Loc *sv_loc, const uint32_t *sv_lm,
+__global__ void __launch_bounds__(1024) k_si_dir(const DevPlan *__restrict__ pl, const Loc *sv_loc, const uint32_t *sv_lm,
                                                  const uint32_t *sperm, uint32_t nsurv, uint32_t *cum) {
   __shared__ uint32_t s_w[16];
   const int l = blockIdx.x;
@@ -2123,7 +2218,7 @@ __global__ void __launch_bounds__(1024) k_si_dir(const DevPlan *pl, const Loc *s
 // list lid's in-place buffer as getWordPosList reads it: unit u of the
 // shrunk image (u < S), else the list's own unit u (zero past its end)
 struct SiList {
-  const DevPlan *pl;
+  const DevPlan *__restrict__ pl;
   const Loc *sv_loc;
   const uint32_t *sperm, *cum;
   uint32_t nsurv;
@@ -2190,7 +2285,7 @@ __device__ int si_word_pos_list(const SiList &L, uint64_t docId, uint32_t own, i
 
 // one lane per tree docid: the first pass's score_survivor again, with the
 // recorder, over the survivor's arena range (k_score's fallback store)
-__global__ void __launch_bounds__(SCORE_TPB) k_scoreinfo(const DevPlan *pl, Counters *ctr, const uint32_t *sv_slot,
+__global__ void __launch_bounds__(SCORE_TPB) k_scoreinfo(const DevPlan *__restrict__ pl, Counters *ctr, const uint32_t *sv_slot,
                                                          const uint32_t *sv_lm, const uint32_t *sv_u,
                                                          const Loc *sv_loc, uint64_t *arena,
                                                          unsigned long long arena_cap, const uint64_t *tdoc,
@@ -2300,7 +2395,7 @@ struct BoundCore {
   float base;
 };
 
-__device__ __forceinline__ float max_score_tail(const DevPlan *pl, BoundCore c, float tfw_m, int32_t bestDist,
+__device__ __forceinline__ float max_score_tail(const DevPlan *__restrict__ pl, BoundCore c, float tfw_m, int32_t bestDist,
                                                 int32_t qdist) {
   if (c.state <= 0) return c.state < 0 ? -1.0f : 0.0f;
   float score = c.base;
@@ -2314,7 +2409,7 @@ __device__ __forceinline__ float max_score_tail(const DevPlan *pl, BoundCore c, 
   return score;
 }
 
-__device__ BoundCore group_bound_core(const DevPlan *pl, const Counters *ctr, int g, uint32_t s, uint32_t lm,
+__device__ BoundCore group_bound_core(const DevPlan *__restrict__ pl, const Counters *ctr, int g, uint32_t s, uint32_t lm,
                                       const Loc *svl) {
   const Weights &W = s_weights;
   float best = -1.0f;
@@ -2373,7 +2468,7 @@ __device__ BoundCore group_bound_core(const DevPlan *pl, const Counters *ctr, in
 
 // ring-buffer slots this wave's lanes write for one group's runs (value v);
 // returns the slot of the head of the group's last run (ourFirstPos)
-__device__ int ring_fill(const DevPlan *pl, const Counters *ctr, int g, uint32_t s, uint32_t lm, const Loc *svl,
+__device__ int ring_fill(const DevPlan *__restrict__ pl, const Counters *ctr, int g, uint32_t s, uint32_t lm, const Loc *svl,
                          uint8_t *ring, uint8_t v, int lane) {
   int first = -1;
   const int gns = pl->gnsub[g];
@@ -2458,7 +2553,7 @@ __device__ int32_t ring_best_dist(const uint8_t *ring, uint8_t m, uint8_t i, int
   return bestDist;
 }
 
-__global__ void __launch_bounds__(64 * BND_WAVES) k_bound(const DevPlan *pl, const Counters *ctr,
+__global__ void __launch_bounds__(64 * BND_WAVES) k_bound(const DevPlan *__restrict__ pl, const Counters *ctr,
                                                        const uint32_t *sv_slot, const uint32_t *sv_lm,
                                                        const Loc *sv_loc, float *sbound) {
   __shared__ __attribute__((aligned(16))) uint8_t s_ring[BND_WAVES][RING];
@@ -2538,7 +2633,7 @@ __device__ __forceinline__ uint32_t lower_bound_u64(const uint64_t *a, uint32_t 
   return lo - b;
 }
 
-__global__ void k_rank(const DevPlan *pl, const Counters *ctr, const uint32_t *sv_slot, const uint64_t *sdoc,
+__global__ void k_rank(const DevPlan *__restrict__ pl, const Counters *ctr, const uint32_t *sv_slot, const uint64_t *sdoc,
                        uint32_t *order) {
   const uint32_t nsurv = (uint32_t)(ctr->surv_top >> 36);
   const int g0n = pl->g0n;
@@ -2794,115 +2889,18 @@ __global__ void __launch_bounds__(64) k_tree_replay(Counters *ctr, const uint32_
 // ------------------------------------------------------------------ top-k
 // TopTree replacement (TopTree.cpp:195-516 without clustering): the k best
 // survivors by (score desc, docid asc).  Scores travel as order-preserving
-// uint32 keys (0 = not scored).  A three-pass radix select (key bits 31..20,
-// 19..8, 7..0) finds the k-th key T; keys > T (fewer than k) and keys == T
-// (the ties, of which the smallest docids win) are gathered and sorted in
-// LDS by one block.  Each histogram pass keeps a 4096-bin histogram per block
-// in LDS, merged with one atomic per non-empty bin; a one-block kernel scans
-// the merged histogram.
-template <int PASS>
-__global__ void __launch_bounds__(BLOCK) k_select_hist(const uint32_t *skey, const Counters *ctr, Select *sel) {
-  __shared__ uint32_t h[SEL_BINS];
-  if (PASS > 0 && sel->all) return;  // uniform
-  constexpr int NB = PASS == 2 ? 256 : SEL_BINS;
-  for (int b = threadIdx.x; b < NB; b += BLOCK) h[b] = 0;
-  __syncthreads();
-  const uint32_t n = (uint32_t)(ctr->surv_top >> 36);
-  const uint32_t pre = PASS > 0 ? sel->prefix : 0;
-  for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) {
-    const uint32_t key = skey[i];
-    if (key == 0) continue;
-    uint32_t bin;
-    if (PASS == 0) {
-      bin = key >> 20;
-    } else if (PASS == 1) {
-      if ((key >> 20) != pre) continue;
-      bin = (key >> 8) & 0xfff;
-    } else {
-      if ((key >> 8) != pre) continue;
-      bin = key & 0xff;
-    }
-    atomicAdd(&h[bin], 1u);
-  }
-  __syncthreads();
-  for (int b = threadIdx.x; b < NB; b += BLOCK)
-    if (h[b]) atomicAdd(&sel->hist[PASS][b], h[b]);
-}
-
-// one block: walk the merged histogram from the top to the bin holding the
-// k-th key (the kernel boundary orders it after every block's adds)
-template <int PASS>
-__global__ void __launch_bounds__(BLOCK) k_select_scan(Select *sel, uint32_t k) {
-  __shared__ uint32_t tmp[BLOCK / 64];
-  if (PASS > 0 && sel->all) return;
-  constexpr int NB = PASS == 2 ? 256 : SEL_BINS;
-  constexpr int BPT = NB / BLOCK;
-  uint32_t c[BPT], sum = 0;
-#pragma unroll
-  for (int q = 0; q < BPT; q++) {
-    c[q] = sel->hist[PASS][NB - 1 - (threadIdx.x * BPT + q)];
-    sum += c[q];
-  }
-  uint32_t total;
-  const uint32_t before = block_exclusive_scan(sum, tmp, &total);
-  const uint32_t need = PASS == 0 ? k : sel->need;
-  const uint32_t pre = PASS > 0 ? sel->prefix : 0;
-  __syncthreads();  // every thread has read prefix/need before they change
-  if (PASS == 0 && total <= need) {
-    if (threadIdx.x == 0) sel->all = 1;
-    return;
-  }
-  if (before < need && need <= before + sum) {
-    uint32_t cum = before;
-#pragma unroll
-    for (int q = 0; q < BPT; q++) {
-      if (cum + c[q] >= need) {
-        const uint32_t b = NB - 1 - (threadIdx.x * BPT + q);
-        if (PASS == 0) sel->prefix = b;
-        else if (PASS == 1) sel->prefix = (pre << 12) | b;
-        else sel->thr = (pre << 8) | b;
-        sel->need = need - cum;
-        break;
-      }
-      cum += c[q];
-    }
-  }
-}
-
-// keys > T -> A (fewer than k), keys == T -> B (ties); one atomic per wave
-__global__ void __launch_bounds__(BLOCK) k_select_gather(const uint32_t *skey, const uint64_t *sdoc,
-                                                         const Counters *ctr, Select *sel, uint32_t *akey,
-                                                         uint64_t *adoc, uint32_t *bkey, uint64_t *bdoc) {
-  const uint32_t n = (uint32_t)(ctr->surv_top >> 36);
-  const bool all = sel->all != 0;
-  const uint32_t T = all ? 1u : sel->thr;
-  const int lane = threadIdx.x & 63;
-  const uint32_t lim = (n + 63) & ~63u;  // whole waves iterate together
-  for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < lim; i += gridDim.x * BLOCK) {
-    const uint32_t key = i < n ? skey[i] : 0;
-    const bool ga = key != 0 && (all ? key >= T : key > T);
-    const bool gb = key != 0 && !all && key == T;
-    const uint64_t ma = __ballot(ga), mb = __ballot(gb);
-    uint32_t ba = 0, bb = 0;
-    if (lane == 0) {
-      if (ma) ba = atomicAdd(&sel->na, (uint32_t)__popcll(ma));
-      if (mb) bb = atomicAdd(&sel->nb, (uint32_t)__popcll(mb));
-    }
-    ba = __shfl(ba, 0, 64);
-    bb = __shfl(bb, 0, 64);
-    const uint64_t below = (1ull << lane) - 1;
-    if (ga) {
-      const uint32_t o = ba + (uint32_t)__popcll(ma & below);
-      akey[o] = key;
-      adoc[o] = sdoc[i];
-    }
-    if (gb) {
-      const uint32_t o = bb + (uint32_t)__popcll(mb & below);
-      bkey[o] = key;
-      bdoc[o] = sdoc[i];
-    }
-  }
-}
+// uint32 keys (0 = not scored).  k_score counts every key in a 65536-bin
+// histogram of its top 16 bits (Select::hist); then ONE launch, k_topk:
+//   1. every block scans the histogram from the top to the bin P holding the
+//      k-th key;
+//   2. the grid gathers keys whose prefix is above P (A, fewer than k) and
+//      equal to P (B), one atomic per wave;
+//   3. the block that finishes last narrows B in LDS with two 8-bit passes to
+//      the k-th key T itself, moves B's keys > T to A and compacts the ties
+//      (== T, of which the smallest docids win) in place, then sorts A and
+//      merges the ties in LDS.
+constexpr int TK_THREADS = 1024;
+constexpr int TK_BLOCKS = 32;
 
 // bitonic sort of sk/sd[0, n) in LDS, n rounded up to a power of two with
 // sentinels; "first" = better = key desc, docid asc
@@ -2933,22 +2931,151 @@ __device__ void lds_sort_best_first(uint32_t *sk, uint64_t *sd, uint32_t n) {
   }
 }
 
-// One block: A plus the ties, merged TILE-k at a time (ties beyond one tile
-// only with huge exact-score ties), best k written to the result block.
-__global__ void __launch_bounds__(1024) k_select_final(const Select *sel, const uint32_t *akey, const uint64_t *adoc,
-                                                       const uint32_t *bkey, const uint64_t *bdoc, uint32_t k,
-                                                       uint32_t *out_key, uint64_t *out_doc) {
+// the bin (of NB, counts h[]) holding the need-th entry counted from the top
+// bin down, and the entries in the bins above it; one block of NT threads,
+// each holding NB/NT consecutive counts in registers; tmp: NT/64 words
+template <int NT, int NB, class P>
+__device__ void top_bin(const P *h, uint32_t need, uint32_t *tmp, uint32_t *s_bin, uint32_t *s_above,
+                        uint32_t *s_total) {
+  constexpr int BPT = NB >= NT ? NB / NT : 1;
+  static_assert(NB < NT || NB % NT == 0, "bins split evenly");
+  // thread t: bins [NB - (t+1) BPT, NB - t BPT), walked from the highest
+  const int lo = NB - ((int)threadIdx.x + 1) * BPT;
+  uint32_t c[BPT], sum = 0;
+#pragma unroll
+  for (int q = 0; q < BPT; q++) {
+    c[q] = lo + q >= 0 ? (uint32_t)h[lo + q] : 0u;
+    sum += c[q];
+  }
+  uint32_t total;
+  const uint32_t before = block_exclusive_scan<NT>(sum, tmp, &total);
+  if (threadIdx.x == 0) *s_total = total;
+  if (need > 0 && before < need && need <= before + sum) {
+    uint32_t cum = before;
+    bool found = false;
+#pragma unroll
+    for (int q = BPT - 1; q >= 0; q--) {
+      if (!found && cum + c[q] >= need) {
+        *s_bin = (uint32_t)(lo + q);
+        *s_above = cum;
+        found = true;
+      }
+      cum += c[q];
+    }
+  }
+  __syncthreads();
+}
+
+// append the flagged entries of one block-wide step to dst (block scan, in
+// index order); returns the new count (every thread)
+__device__ __forceinline__ uint32_t block_append(bool f, uint32_t key, uint64_t doc, uint32_t *dk, uint64_t *dd,
+                                                 uint32_t n, uint32_t *tmp) {
+  uint32_t tot;
+  const uint32_t o = block_exclusive_scan<TK_THREADS>(f ? 1u : 0u, tmp, &tot);
+  if (f) {
+    dk[n + o] = key;
+    dd[n + o] = doc;
+  }
+  return n + tot;
+}
+
+__global__ void __launch_bounds__(TK_THREADS) k_topk(const uint32_t *skey, const uint64_t *sdoc, const Counters *ctr,
+                                                     Select *sel, uint32_t k, uint32_t *akey, uint64_t *adoc,
+                                                     uint32_t *bkey, uint64_t *bdoc, uint32_t *out_key,
+                                                     uint64_t *out_doc) {
+  __shared__ uint32_t tmp[TK_THREADS / 64];
+  __shared__ uint32_t s_bin, s_above, s_total, s_last;
+  __shared__ uint32_t h8[256];
   __shared__ uint32_t sk[TILE];
   __shared__ uint64_t sd[TILE];
-  const uint32_t na = sel->na, nb = sel->nb;
-  for (uint32_t t = threadIdx.x; t < na; t += blockDim.x) {
+  const uint32_t n = (uint32_t)(ctr->surv_top >> 36);
+  // 1. the prefix P of the k-th key
+  if (threadIdx.x == 0) {
+    s_bin = 0;
+    s_above = 0;
+  }
+  __syncthreads();
+  top_bin<TK_THREADS, SEL_HBINS>(sel->hist, k, tmp, &s_bin, &s_above, &s_total);
+  const bool all = s_total <= k;  // every scored key is taken
+  const uint32_t P = s_bin;
+  // 2. A: prefix > P (all: every scored key), B: prefix == P
+  const int lane = threadIdx.x & 63;
+  const uint32_t lim = (n + 63) & ~63u;  // whole waves iterate together
+  for (uint32_t i = blockIdx.x * TK_THREADS + threadIdx.x; i < lim; i += gridDim.x * TK_THREADS) {
+    const uint32_t key = i < n ? skey[i] : 0;
+    const bool ga = key != 0 && (all || (key >> 16) > P);
+    const bool gb = key != 0 && !all && (key >> 16) == P;
+    const uint64_t ma = __ballot(ga), mb = __ballot(gb);
+    uint32_t ba = 0, bb = 0;
+    if (lane == 0) {
+      if (ma) ba = atomicAdd(&sel->na, (uint32_t)__popcll(ma));
+      if (mb) bb = atomicAdd(&sel->nb, (uint32_t)__popcll(mb));
+    }
+    ba = __shfl(ba, 0, 64);
+    bb = __shfl(bb, 0, 64);
+    const uint64_t below = (1ull << lane) - 1;
+    if (ga) {
+      const uint32_t o = ba + (uint32_t)__popcll(ma & below);
+      akey[o] = key;
+      adoc[o] = sdoc[i];
+    }
+    if (gb) {
+      const uint32_t o = bb + (uint32_t)__popcll(mb & below);
+      bkey[o] = key;
+      bdoc[o] = sdoc[i];
+    }
+  }
+  // 3. the last block
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) s_last = atomicAdd(&sel->done, 1u) == gridDim.x - 1 ? 1u : 0u;
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();
+  uint32_t na = __hip_atomic_load(&sel->na, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t nb = __hip_atomic_load(&sel->nb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  uint32_t nt = 0;  // ties of T, compacted to the front of B
+  if (nb) {
+    // T inside B: bits 15..8, then 7..0
+    const uint32_t need = k - na;  // na < k <= s_above + |B|
+    for (int t = threadIdx.x; t < 256; t += TK_THREADS) h8[t] = 0;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nb; i += TK_THREADS) atomicAdd(&h8[(bkey[i] >> 8) & 0xff], 1u);
+    __syncthreads();
+    top_bin<TK_THREADS, 256>(h8, need, tmp, &s_bin, &s_above, &s_total);
+    const uint32_t c1 = s_bin, need2 = need - s_above;
+    __syncthreads();
+    for (int t = threadIdx.x; t < 256; t += TK_THREADS) h8[t] = 0;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nb; i += TK_THREADS) {
+      const uint32_t key = bkey[i];
+      if (((key >> 8) & 0xff) == c1) atomicAdd(&h8[key & 0xff], 1u);
+    }
+    __syncthreads();
+    top_bin<TK_THREADS, 256>(h8, need2, tmp, &s_bin, &s_above, &s_total);
+    const uint32_t T = (P << 16) | (c1 << 8) | s_bin;
+    // B's keys > T join A; its ties move to B's front (in place: a step
+    // writes below the entries it has read)
+    const uint32_t lim2 = (nb + TK_THREADS - 1) / TK_THREADS * TK_THREADS;
+    for (uint32_t i0 = 0; i0 < lim2; i0 += TK_THREADS) {
+      const uint32_t i = i0 + threadIdx.x;
+      const uint32_t key = i < nb ? bkey[i] : 0;
+      const uint64_t doc = i < nb ? bdoc[i] : 0;
+      __syncthreads();
+      na = block_append(key > T, key, doc, akey, adoc, na, tmp);
+      nt = block_append(key == T && i < nb, key, doc, bkey, bdoc, nt, tmp);
+    }
+  }
+  // A (fewer than k entries) plus the ties, merged TILE-k at a time (ties
+  // beyond one tile only with huge exact-score ties)
+  for (uint32_t t = threadIdx.x; t < na; t += TK_THREADS) {
     sk[t] = akey[t];
     sd[t] = adoc[t];
   }
   uint32_t kept = na, tb = 0;
   for (;;) {
-    const uint32_t take = min(nb - tb, (uint32_t)TILE - kept);
-    for (uint32_t t = threadIdx.x; t < take; t += blockDim.x) {
+    const uint32_t take = min(nt - tb, (uint32_t)TILE - kept);
+    for (uint32_t t = threadIdx.x; t < take; t += TK_THREADS) {
       sk[kept + t] = bkey[tb + t];
       sd[kept + t] = bdoc[tb + t];
     }
@@ -2956,9 +3083,9 @@ __global__ void __launch_bounds__(1024) k_select_final(const Select *sel, const 
     __syncthreads();
     lds_sort_best_first(sk, sd, kept + take);
     kept = min(k, kept + take);
-    if (tb >= nb) break;
+    if (tb >= nt) break;
   }
-  for (uint32_t t = threadIdx.x; t < k; t += blockDim.x) {
+  for (uint32_t t = threadIdx.x; t < k; t += TK_THREADS) {
     out_key[t] = t < kept ? sk[t] : 0u;
     out_doc[t] = t < kept ? sd[t] : ~0ull;
   }
@@ -3828,7 +3955,7 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   rc2 |= q.tables.ensure(tbytes);
   rc2 |= q.chunkcnt.ensure(4 * std::max<size_t>(1, q.g0c.size()));
   const uint32_t nwords = (uint32_t)((slot_ub + 31) / 32);
-  const uint32_t cgrid = std::max(1u, (uint32_t)((slot_ub + CTILE - 1) / CTILE));
+  const uint32_t cgrid = std::max(1u, (uint32_t)((nwords + CB - 1) / CB));
   rc2 |= q.cand.ensure(8 * slot_ub);
   rc2 |= q.cunit.ensure(4 * slot_ub);
   rc2 |= q.bits.ensure(4 * (size_t)nwords * (uint64_t)P.nlists);
@@ -3851,7 +3978,7 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
     if (!(tree_phase & TREE_FINAL)) rc2 |= q.tree.ensure(sizeof(TreeState));
   }
   if (P.use_white) rc2 |= q.white.ensure(8 * std::max<size_t>(1, q.h_white.size()));
-  if (P.use_rej) rc2 |= q.wrej.ensure(slot_ub);
+  if (P.use_rej) rc2 |= q.wrej.ensure(align256(slot_ub));  // k_cmp_* read it 32 slots at a time
   const void *dir_before = q.dir.p;
   rc2 |= q.dir.ensure(8 * std::max<uint64_t>(1, dir_entries));
   if (rc2) return ENOMEM;
@@ -3956,18 +4083,17 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   // puts every survivor in one bucket, in slot order
   if (!clus) {
     hipLaunchKernelGGL(k_cmp_count<false>, dim3(cgrid), dim3(CB), 0, st, dpl, dctr, dcunit, bits, nwords, loc, dcand,
-                       slot_ub, rcap, blk);
+                       rcap, blk);
   } else {
     hipLaunchKernelGGL(k_cmp_count<true>, dim3(cgrid), dim3(CB), 0, st, dpl, dctr, dcunit, bits, nwords, loc, dcand,
-                       slot_ub, rcap, blk);
+                       rcap, blk);
   }
-  hipLaunchKernelGGL(k_cmp_scan, dim3(1), dim3(1024), 0, st, dpl, cgrid, blk, dctr);
   if (!clus) {
     hipLaunchKernelGGL(k_cmp_write<false>, dim3(cgrid), dim3(CB), 0, st, dpl, dctr, dcunit, bits, nwords, loc, dcand,
-                       slot_ub, rcap, blk, svslot, svlm, svu, svdoc, svloc);
+                       rcap, blk, cgrid, svslot, svlm, svu, svdoc, svloc);
   } else {
     hipLaunchKernelGGL(k_cmp_write<true>, dim3(cgrid), dim3(CB), 0, st, dpl, dctr, dcunit, bits, nwords, loc, dcand,
-                       slot_ub, rcap, blk, svslot, svlm, svu, svdoc, svloc);
+                       rcap, blk, cgrid, svslot, svlm, svu, svdoc, svloc);
   }
   const unsigned long long arena_cap = (unsigned long long)(q.scratch.cap / 8);
   if (P.reshare_mask)
@@ -3983,7 +4109,7 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
       hipLaunchKernelGGL(kern, dim3(grid), dim3(SCORE_TPB), 0, st, dpl, (const uint64_t *)svdoc, dctr,
                          (const uint32_t *)svslot, (const uint32_t *)svlm, (const uint32_t *)svu, (const Loc *)svloc,
                          q.scratch.as<uint64_t>(), arena_cap, q.skey.as<uint32_t>(), q.sflag.as<uint8_t>(),
-                         ctx->score_mode, ctx->d_sdbg);
+                         ctx->score_mode, ctx->d_sdbg, clus ? nullptr : dsel->hist);
     };
     if (variant == 4) launch(k_score<2, 2, kRC[4]>);  // two groups of <= 2 sublists (config 2)
     else if (variant == 0) launch(k_score<2, 4, kRC[0]>);
@@ -4018,23 +4144,16 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
     return 0;
   }
   // top-k: radix select over the survivors' keys, then one LDS sort
-  const uint32_t hgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(64, (slot_ub + 4095) / 4096));
   const uint32_t *skey = q.skey.as<uint32_t>();
-  hipLaunchKernelGGL(k_select_hist<0>, dim3(hgrid), dim3(BLOCK), 0, st, skey, dctr, dsel);
-  hipLaunchKernelGGL(k_select_scan<0>, dim3(1), dim3(BLOCK), 0, st, dsel, (uint32_t)k);
-  hipLaunchKernelGGL(k_select_hist<1>, dim3(hgrid), dim3(BLOCK), 0, st, skey, dctr, dsel);
-  hipLaunchKernelGGL(k_select_scan<1>, dim3(1), dim3(BLOCK), 0, st, dsel, (uint32_t)k);
-  hipLaunchKernelGGL(k_select_hist<2>, dim3(hgrid), dim3(BLOCK), 0, st, skey, dctr, dsel);
-  hipLaunchKernelGGL(k_select_scan<2>, dim3(1), dim3(BLOCK), 0, st, dsel, (uint32_t)k);
   uint32_t *akey = q.gath.as<uint32_t>();
   uint64_t *adoc = q.gath.as<uint64_t>(align256(4 * (size_t)MAX_K));
   uint32_t *bkey = q.gath.as<uint32_t>(align256(4 * (size_t)MAX_K) + align256(8 * (size_t)MAX_K));
   uint64_t *bdoc = q.gath.as<uint64_t>(align256(4 * (size_t)MAX_K) + align256(8 * (size_t)MAX_K) +
                                           align256(4 * slot_ub));
-  hipLaunchKernelGGL(k_select_gather, dim3(hgrid), dim3(BLOCK), 0, st, skey, (const uint64_t *)svdoc, dctr, dsel,
-                     akey, adoc, bkey, bdoc);
-  hipLaunchKernelGGL(k_select_final, dim3(1), dim3(1024), 0, st, dsel, akey, adoc, bkey, bdoc, (uint32_t)k,
-                     q.res.as<uint32_t>(res_keys_off()), q.res.as<uint64_t>(res_docs_off(k)));
+  const uint32_t tgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(TK_BLOCKS, (slot_ub + TK_THREADS - 1) / TK_THREADS));
+  hipLaunchKernelGGL(k_topk, dim3(tgrid), dim3(TK_THREADS), 0, st, skey, (const uint64_t *)svdoc, dctr, dsel,
+                     (uint32_t)k, akey, adoc, bkey, bdoc, q.res.as<uint32_t>(res_keys_off()),
+                     q.res.as<uint64_t>(res_docs_off(k)));
   if (ctx->profiling) HIPCHECK(hipEventRecord(q.ev[5], st));
   HIPCHECK(hipEventRecord(q.ev_done, st));
   HIPCHECK(hipMemcpyAsync(q.h_res, q.res.p, q.res_bytes, hipMemcpyDeviceToHost, st));
