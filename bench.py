@@ -338,6 +338,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-merge", action="store_true", help="skip the config-5 list merge measurement")
     ap.add_argument("--no-config3", action="store_true", help="skip the config-3 query-mix measurement")
+    ap.add_argument("--no-clustering", action="store_true",
+                    help="skip the config-2 rotation with site clustering (the Msg39 default)")
     ap.add_argument("--no-ceiling", action="store_true", help="skip the streaming-bandwidth ceiling")
     ap.add_argument("--merge-keys", type=int, default=400_000_000, help="config-5 keys (~4.4 GB of runs)")
     ap.add_argument("--exchange", action="store_true",
@@ -538,6 +540,39 @@ def main():
             "note": "gbgpu_query with the lists in pageable host memory, uploaded every call; not `value`",
         }
         del host
+    if rank == 0 and world == 1 and not args.no_clustering:
+        # the same rotation as Msg39 sends it by default: m_doSiteClustering
+        # (Msg39.h:41) -- the prefilter bounds (k_bound) and the in-docid-order
+        # TopTree replay (k_tree_replay) instead of the radix top-k
+        pc = [q.params(site_clustering=1) for q in qs]
+        eng.set_profiling(True)
+        cdev = []
+        for j, q in enumerate(qs):
+            eng.enqueue(q.terms, handles[j], pc[j], slot=0)
+            eng.collect(cap=4096, slot=0)
+            cdev.append(eng.last_timings(slot=0)[0])
+        eng.set_profiling(False)
+        nc = max(len(qs), args.steps // 2)
+        t_c = time.perf_counter()
+        for i in range(nc):
+            slot = i % slots
+            if i >= slots:
+                eng.collect(cap=4096, slot=slot)
+            eng.enqueue(qs[i % len(qs)].terms, handles[i % len(qs)], pc[i % len(qs)], slot=slot)
+        for i in range(max(0, nc - slots), nc):
+            eng.collect(cap=4096, slot=i % slots)
+        el_c = time.perf_counter() - t_c
+        cb = float(sum(qbytes[i % len(qs)] for i in range(nc)))
+        cd = np.array(cdev)
+        result["clustering"] = {
+            "workload": "config 2 with site clustering (Msg39's default request), same rotation",
+            "queries": nc,
+            "queries_per_sec": round(nc / el_c, 3),
+            "keys_scanned_GBps": round(cb / el_c / 1e9, 3),
+            "device_ms_per_query": round(float(cd[:, 0].mean()), 4),
+            "phase_ms": dict(zip(["total", "candidates", "probe", "compact", "score", "bound+replay"],
+                                 [round(float(v), 4) for v in cd.mean(axis=0)])),
+        }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline_query(qs[0], first_lists)
     for hs in handles:

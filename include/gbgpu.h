@@ -108,7 +108,11 @@ typedef struct gbgpu_params {
   double  max_serp_score;   /* m_maxSerpScore  } paging of a widget's next page:   */
   int64_t min_serp_docid;   /* m_minSerpDocId  } nonzero enables the filter of
                                Posdb.cpp:4379-4381, 7327-7347 (counted in
-                               gbgpu_result::filtered)                           */
+                               gbgpu_result::filtered).  With a gbsortby int term
+                               the tree's m_intScore is compared with
+                               (int32_t)max_serp_score as x86-64 truncates it
+                               (INT32_MIN when out of range or NaN), Posdb.cpp:
+                               7330-7336                                         */
   /* The "&sites=" whitelist: use_whitelist = (Msg39Request::size_whiteList > 1)
    * (Posdb.cpp:800-801); white_lists = Msg2::m_whiteLists[0..m_w), host
    * memory, not mutated.  A docid is voted only if the 5 bytes at rec+7 of its

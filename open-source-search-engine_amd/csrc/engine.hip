@@ -6,7 +6,7 @@
 // is followed by these launches on the context's stream:
 //
 //   k_reset            zero the per-query counters and top-k select state
-//   k_count_runs / k_scan_runs / k_write_runs
+//   k_write_runs
 //        candidate docids = run starts of the sublists of the smallest group
 //        (addDocIdVotes group 0, Posdb.cpp:5178-5332), one sorted array per
 //        sublist; array 0's own run locations are recorded here.
@@ -238,31 +238,34 @@ __global__ void k_reset(uint32_t *a, uint32_t na, uint32_t *b, uint32_t nb, uint
 }
 
 // ----------------------------------------------- candidate extraction (G0)
-__global__ void __launch_bounds__(BLOCK) k_count_runs(const DevPlan *__restrict__ pl, const G0Chunk *chunks,
-                                                      uint32_t *chunk_count) {
+// The page map, RdbMap's role (RdbMap.h:48: a list's pages and where each
+// begins) for the GPU: per CHUNK_UNITS-unit page of a swapped list, the run
+// starts before it, and their total at [npages].  Built once when a list is
+// uploaded (k_page_count, k_page_scan), so a query's candidate slots need no
+// counting pass: a run's slot is its page's prefix plus its rank in the page.
+__global__ void __launch_bounds__(BLOCK) k_page_count(const uint8_t *__restrict__ list, uint32_t units,
+                                                      uint32_t *__restrict__ pm) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[CHUNK_LOAD];
   __shared__ uint32_t tmp[BLOCK / 64];
-  const G0Chunk c = chunks[blockIdx.x];
-  const DevList &L = pl->lists[pl->g0list[c.array]];
-  load_chunk(L.p, c.u0, lds);
+  const uint32_t u0 = blockIdx.x * (uint32_t)CHUNK_UNITS;
+  load_chunk(list, u0, lds);
   __syncthreads();
-  uint32_t m = thread_starts(lds, c.u0, L.units);
   uint32_t tot;
-  block_exclusive_scan(__popc(m), tmp, &tot);
-  if (threadIdx.x == 0) chunk_count[blockIdx.x] = tot;
+  block_exclusive_scan(__popc(thread_starts(lds, u0, units)), tmp, &tot);
+  if (threadIdx.x == 0) pm[blockIdx.x] = tot;
 }
 
-// exclusive scan of the per-chunk counts (single block); k_write_runs
-// subtracts the prefix at each array's first chunk
-__global__ void __launch_bounds__(1024) k_scan_runs(uint32_t nchunks, uint32_t *chunk_count) {
+// exclusive scan of the page counts in place (one block); the total lands
+// at pm[npages]
+__global__ void __launch_bounds__(1024) k_page_scan(uint32_t npages, uint32_t *pm) {
   __shared__ uint32_t tmp[16];
   __shared__ uint32_t carry;
   if (threadIdx.x == 0) carry = 0;
   __syncthreads();
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  for (uint32_t base = 0; base < nchunks; base += 1024) {
+  for (uint32_t base = 0; base < npages; base += 1024) {
     const uint32_t i = base + threadIdx.x;
-    const uint32_t v = i < nchunks ? chunk_count[i] : 0;
+    const uint32_t v = i < npages ? pm[i] : 0;
     uint32_t x = v;
     for (int o = 1; o < 64; o <<= 1) {
       uint32_t y = __shfl_up(x, o, 64);
@@ -274,10 +277,11 @@ __global__ void __launch_bounds__(1024) k_scan_runs(uint32_t nchunks, uint32_t *
     for (int w = 0; w < wid; w++) pre += tmp[w];
     const uint32_t incl = carry + pre + x;
     __syncthreads();
-    if (i < nchunks) chunk_count[i] = incl - v;
+    if (i < npages) pm[i] = incl - v;
     if (threadIdx.x == 1023) carry = incl;
     __syncthreads();
   }
+  if (threadIdx.x == 0) pm[npages] = carry;
 }
 
 // Range terms (gbmin:/gbmax:/gbequal:, Posdb.cpp:4948-4999): isInRange on
@@ -318,17 +322,18 @@ __device__ bool run_in_range_first(const DevList &L, uint32_t u, uint32_t e) {
 // ends where the next candidate's starts), the directory, and the
 // whitelist / range-term rejections.  Match state lives in per-list bitmaps
 // (k_probe) cleared by k_reset, so no per-slot mask is written here.
-__global__ void __launch_bounds__(BLOCK) k_write_runs(const DevPlan *__restrict__ pl, const G0Chunk *chunks,
-                                                      const uint32_t *chunk_off,
-                                                      const uint32_t *array_first_chunk,
-                                                      uint64_t *cand, uint32_t *cunit, Counters *ctr,
-                                                      uint32_t nchunks, uint64_t *dir) {
+__global__ void __launch_bounds__(BLOCK) k_write_runs(const DevPlan *__restrict__ pl, const G0Chunk *__restrict__ chunks,
+                                                      uint64_t *__restrict__ cand, uint32_t *__restrict__ cunit,
+                                                      Counters *__restrict__ ctr, uint32_t nchunks,
+                                                      uint64_t *__restrict__ dir) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[CHUNK_LOAD];
   __shared__ uint32_t tmp[BLOCK / 64];
   __shared__ uint16_t rs_unit[MAX_RUNS];
-  const G0Chunk c = chunks[blockIdx.x];
+  const uint32_t me = blockIdx.x;
+  const G0Chunk c = chunks[me];
   const int lid = pl->g0list[c.array];
   const DevList &L = pl->lists[lid];
+  const uint32_t pos0 = L.pm[c.u0 / CHUNK_UNITS];  // the page's slot offset in its array
   load_chunk(L.p, c.u0, lds);
   __syncthreads();
   const uint32_t m0 = thread_starts(lds, c.u0, L.units);
@@ -341,8 +346,6 @@ __global__ void __launch_bounds__(BLOCK) k_write_runs(const DevPlan *__restrict_
     rs_unit[o++] = (uint16_t)(threadIdx.x * UPT + q);
   }
   __syncthreads();
-  // offset inside this array = global prefix - prefix at the array's first chunk
-  const uint32_t arr_base_off = chunk_off[array_first_chunk[c.array]];
   const uint64_t base = pl->g0base[c.array];
   uint64_t *dir_a = dir + pl->g0dir[c.array];
   const uint64_t dmin = pl->g0dmin[c.array];
@@ -350,7 +353,6 @@ __global__ void __launch_bounds__(BLOCK) k_write_runs(const DevPlan *__restrict_
   const uint64_t tag = (uint64_t)pl->epoch << 32;
   // runs in chunk order, strided over the block: consecutive lanes write
   // consecutive slots (coalesced stores)
-  const uint32_t pos0 = chunk_off[blockIdx.x] - arr_base_off;
   for (uint32_t o2 = threadIdx.x; o2 < tot; o2 += BLOCK) {
     const uint32_t lu = rs_unit[o2];
     const uint32_t p2 = pos0 + o2;
@@ -371,9 +373,9 @@ __global__ void __launch_bounds__(BLOCK) k_write_runs(const DevPlan *__restrict_
       for (int b = 4; b >= 0; b--) x = (x << 8) | k[7 + b];
       uint32_t lo = 0, hi = pl->nwhite;
       while (lo < hi) {
-        const uint32_t m = (lo + hi) >> 1;
-        if (pl->white[m] < x) lo = m + 1;
-        else hi = m;
+        const uint32_t mm = (lo + hi) >> 1;
+        if (pl->white[mm] < x) lo = mm + 1;
+        else hi = mm;
       }
       rej = !(lo < pl->nwhite && pl->white[lo] == x);
     }
@@ -385,8 +387,8 @@ __global__ void __launch_bounds__(BLOCK) k_write_runs(const DevPlan *__restrict_
     if (pl->use_rej) pl->wrej[slot] = rej;
   }
   // the last chunk of each array publishes the array's count
-  const bool last = (blockIdx.x + 1 == nchunks) || (chunks[blockIdx.x + 1].array != c.array);
-  if (last && threadIdx.x == 0) ctr->g0count[c.array] = chunk_off[blockIdx.x] - arr_base_off + tot;
+  const bool last = (me + 1 == nchunks) || (chunks[me + 1].array != c.array);
+  if (last && threadIdx.x == 0) ctr->g0count[c.array] = pos0 + tot;
 }
 
 // ------------------------------------------------------------- probe scan
@@ -2665,7 +2667,7 @@ struct TreeParams {
   int32_t docs_wanted;  // m_docsWanted
   int32_t cap;          // m_cap
   float partial;        // m_partial
-  int32_t pad;
+  int32_t emit;         // write the tree out without ending it (the second pass of a docid-split piece)
   int64_t ridiculous;   // m_ridiculousMax
   int64_t num_nodes;    // m_numNodes
   uint32_t init, final; // first / last piece
@@ -2862,7 +2864,7 @@ __global__ void __launch_bounds__(64) k_tree_replay(Counters *ctr, const uint32_
     ctr->filtered = filtered;
     if (err) ctr->tree_err = 1;
   }
-  if (tp.final) {
+  if (tp.final || tp.emit) {
     for (uint32_t q = lane; q < n; q += 64) {
       const uint32_t b = __float_as_uint(ts[q]);
       uint32_t k = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
@@ -2873,7 +2875,8 @@ __global__ void __launch_bounds__(64) k_tree_replay(Counters *ctr, const uint32_
       if (n < TC) out_key[n] = 0;
       ctr->tree_n = n;
     }
-  } else {
+  }
+  if (!tp.final) {
     for (uint32_t q = lane; q < n; q += 64) {
       T->score[q] = ts[q];
       T->docid[q] = td[q];
@@ -2901,6 +2904,7 @@ __global__ void __launch_bounds__(64) k_tree_replay(Counters *ctr, const uint32_
 //      merges the ties in LDS.
 constexpr int TK_THREADS = 1024;
 constexpr int TK_BLOCKS = 32;
+constexpr int TK_E = 16;  // keys per thread and gather round
 
 // bitonic sort of sk/sd[0, n) in LDS, n rounded up to a power of two with
 // sentinels; "first" = better = key desc, docid asc
@@ -2966,6 +2970,17 @@ __device__ void top_bin(const P *h, uint32_t need, uint32_t *tmp, uint32_t *s_bi
   __syncthreads();
 }
 
+// write-through (sc1) stores and L2-served (sc1) loads: the cross-workgroup
+// hand-off of MI355X_MICROARCH.md (no buffer_wbl2 / buffer_inv)
+template <class T>
+__device__ __forceinline__ void st_sc1(T *p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <class T>
+__device__ __forceinline__ T ld_sc1(const T *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // append the flagged entries of one block-wide step to dst (block scan, in
 // index order); returns the new count (every thread)
 __device__ __forceinline__ uint32_t block_append(bool f, uint32_t key, uint64_t doc, uint32_t *dk, uint64_t *dd,
@@ -2973,8 +2988,8 @@ __device__ __forceinline__ uint32_t block_append(bool f, uint32_t key, uint64_t 
   uint32_t tot;
   const uint32_t o = block_exclusive_scan<TK_THREADS>(f ? 1u : 0u, tmp, &tot);
   if (f) {
-    dk[n + o] = key;
-    dd[n + o] = doc;
+    st_sc1(dk + n + o, key);
+    st_sc1(dd + n + o, doc);
   }
   return n + tot;
 }
@@ -2984,7 +2999,7 @@ __global__ void __launch_bounds__(TK_THREADS) k_topk(const uint32_t *skey, const
                                                      uint32_t *bkey, uint64_t *bdoc, uint32_t *out_key,
                                                      uint64_t *out_doc) {
   __shared__ uint32_t tmp[TK_THREADS / 64];
-  __shared__ uint32_t s_bin, s_above, s_total, s_last;
+  __shared__ uint32_t s_bin, s_above, s_total, s_last, s_ba, s_bb;
   __shared__ uint32_t h8[256];
   __shared__ uint32_t sk[TILE];
   __shared__ uint64_t sd[TILE];
@@ -2998,49 +3013,66 @@ __global__ void __launch_bounds__(TK_THREADS) k_topk(const uint32_t *skey, const
   top_bin<TK_THREADS, SEL_HBINS>(sel->hist, k, tmp, &s_bin, &s_above, &s_total);
   const bool all = s_total <= k;  // every scored key is taken
   const uint32_t P = s_bin;
-  // 2. A: prefix > P (all: every scored key), B: prefix == P
-  const int lane = threadIdx.x & 63;
-  const uint32_t lim = (n + 63) & ~63u;  // whole waves iterate together
-  for (uint32_t i = blockIdx.x * TK_THREADS + threadIdx.x; i < lim; i += gridDim.x * TK_THREADS) {
-    const uint32_t key = i < n ? skey[i] : 0;
-    const bool ga = key != 0 && (all || (key >> 16) > P);
-    const bool gb = key != 0 && !all && (key >> 16) == P;
-    const uint64_t ma = __ballot(ga), mb = __ballot(gb);
-    uint32_t ba = 0, bb = 0;
-    if (lane == 0) {
-      if (ma) ba = atomicAdd(&sel->na, (uint32_t)__popcll(ma));
-      if (mb) bb = atomicAdd(&sel->nb, (uint32_t)__popcll(mb));
+  // 2. A: prefix > P (all: every scored key), B: prefix == P.  A block
+  // takes TK_E keys a thread per round: flags, one block scan, ONE atomic
+  // per list and round, then the writes.
+  for (uint32_t r0 = blockIdx.x * TK_THREADS * TK_E; r0 < n; r0 += gridDim.x * TK_THREADS * TK_E) {
+    uint32_t keys[TK_E], fa = 0, fb = 0, cnt = 0;
+#pragma unroll
+    for (int e = 0; e < TK_E; e++) {
+      const uint32_t i = r0 + (uint32_t)e * TK_THREADS + threadIdx.x;
+      keys[e] = i < n ? skey[i] : 0u;
     }
-    ba = __shfl(ba, 0, 64);
-    bb = __shfl(bb, 0, 64);
-    const uint64_t below = (1ull << lane) - 1;
-    if (ga) {
-      const uint32_t o = ba + (uint32_t)__popcll(ma & below);
-      akey[o] = key;
-      adoc[o] = sdoc[i];
+#pragma unroll
+    for (int e = 0; e < TK_E; e++) {
+      const uint32_t key = keys[e];
+      const bool ga = key != 0 && (all || (key >> 16) > P);
+      const bool gb = key != 0 && !all && (key >> 16) == P;
+      fa |= (ga ? 1u : 0u) << e;
+      fb |= (gb ? 1u : 0u) << e;
     }
-    if (gb) {
-      const uint32_t o = bb + (uint32_t)__popcll(mb & below);
-      bkey[o] = key;
-      bdoc[o] = sdoc[i];
+    cnt = (uint32_t)__popc(fa) | ((uint32_t)__popc(fb) << 16);  // <= TK_THREADS * TK_E < 2^16 each
+    uint32_t tot;
+    const uint32_t ex = block_exclusive_scan<TK_THREADS>(cnt, tmp, &tot);
+    if (threadIdx.x == 0) {
+      s_ba = (tot & 0xffff) ? atomicAdd(&sel->na, tot & 0xffff) : 0u;
+      s_bb = (tot >> 16) ? atomicAdd(&sel->nb, tot >> 16) : 0u;
     }
+    __syncthreads();
+    uint32_t oa = s_ba + (ex & 0xffff), ob = s_bb + (ex >> 16);
+#pragma unroll
+    for (int e = 0; e < TK_E; e++) {
+      const uint32_t i = r0 + (uint32_t)e * TK_THREADS + threadIdx.x;
+      if (fa >> e & 1) {
+        st_sc1(akey + oa, keys[e]);
+        st_sc1(adoc + oa++, sdoc[i]);
+      }
+      if (fb >> e & 1) {
+        st_sc1(bkey + ob, keys[e]);
+        st_sc1(bdoc + ob++, sdoc[i]);
+      }
+    }
+    __syncthreads();  // s_ba / s_bb are rewritten next round
   }
-  // 3. the last block
-  __threadfence();
+  // 3. the last block.  Hand-off without L2 write-back (MI355X_MICROARCH.md,
+  // hand-offs): every gathered entry was stored write-through (sc1), each
+  // wave drains its stores, one lane per block adds to the done counter, and
+  // the block whose add came last reads everything with sc1 loads.
+  __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) s_last = atomicAdd(&sel->done, 1u) == gridDim.x - 1 ? 1u : 0u;
+  if (threadIdx.x == 0)
+    s_last = __hip_atomic_fetch_add(&sel->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1 ? 1u : 0u;
   __syncthreads();
   if (!s_last) return;
-  __threadfence();
-  uint32_t na = __hip_atomic_load(&sel->na, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const uint32_t nb = __hip_atomic_load(&sel->nb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  uint32_t na = ld_sc1(&sel->na);
+  const uint32_t nb = ld_sc1(&sel->nb);
   uint32_t nt = 0;  // ties of T, compacted to the front of B
   if (nb) {
     // T inside B: bits 15..8, then 7..0
     const uint32_t need = k - na;  // na < k <= s_above + |B|
     for (int t = threadIdx.x; t < 256; t += TK_THREADS) h8[t] = 0;
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < nb; i += TK_THREADS) atomicAdd(&h8[(bkey[i] >> 8) & 0xff], 1u);
+    for (uint32_t i = threadIdx.x; i < nb; i += TK_THREADS) atomicAdd(&h8[(ld_sc1(bkey + i) >> 8) & 0xff], 1u);
     __syncthreads();
     top_bin<TK_THREADS, 256>(h8, need, tmp, &s_bin, &s_above, &s_total);
     const uint32_t c1 = s_bin, need2 = need - s_above;
@@ -3048,7 +3080,7 @@ __global__ void __launch_bounds__(TK_THREADS) k_topk(const uint32_t *skey, const
     for (int t = threadIdx.x; t < 256; t += TK_THREADS) h8[t] = 0;
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < nb; i += TK_THREADS) {
-      const uint32_t key = bkey[i];
+      const uint32_t key = ld_sc1(bkey + i);
       if (((key >> 8) & 0xff) == c1) atomicAdd(&h8[key & 0xff], 1u);
     }
     __syncthreads();
@@ -3059,8 +3091,8 @@ __global__ void __launch_bounds__(TK_THREADS) k_topk(const uint32_t *skey, const
     const uint32_t lim2 = (nb + TK_THREADS - 1) / TK_THREADS * TK_THREADS;
     for (uint32_t i0 = 0; i0 < lim2; i0 += TK_THREADS) {
       const uint32_t i = i0 + threadIdx.x;
-      const uint32_t key = i < nb ? bkey[i] : 0;
-      const uint64_t doc = i < nb ? bdoc[i] : 0;
+      const uint32_t key = i < nb ? ld_sc1(bkey + i) : 0;
+      const uint64_t doc = i < nb ? ld_sc1(bdoc + i) : 0;
       __syncthreads();
       na = block_append(key > T, key, doc, akey, adoc, na, tmp);
       nt = block_append(key == T && i < nb, key, doc, bkey, bdoc, nt, tmp);
@@ -3068,16 +3100,18 @@ __global__ void __launch_bounds__(TK_THREADS) k_topk(const uint32_t *skey, const
   }
   // A (fewer than k entries) plus the ties, merged TILE-k at a time (ties
   // beyond one tile only with huge exact-score ties)
+  __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // this block's own appends are in place
   for (uint32_t t = threadIdx.x; t < na; t += TK_THREADS) {
-    sk[t] = akey[t];
-    sd[t] = adoc[t];
+    sk[t] = ld_sc1(akey + t);
+    sd[t] = ld_sc1(adoc + t);
   }
   uint32_t kept = na, tb = 0;
   for (;;) {
     const uint32_t take = min(nt - tb, (uint32_t)TILE - kept);
     for (uint32_t t = threadIdx.x; t < take; t += TK_THREADS) {
-      sk[kept + t] = bkey[tb + t];
-      sd[kept + t] = bdoc[tb + t];
+      sk[kept + t] = ld_sc1(bkey + tb + t);
+      sd[kept + t] = ld_sc1(bdoc + tb + t);
     }
     tb += take;
     __syncthreads();
@@ -3335,6 +3369,7 @@ struct ListMem {
 
 struct ListEntry {
   uint8_t *d = nullptr;
+  uint32_t *pm = nullptr;        // its page map (k_page_count / k_page_scan), in the same allocation
   std::shared_ptr<ListMem> mem;  // owner of d (null for docid-split windows)
   int64_t size = 0;   // original bytes (18-byte first key)
   uint32_t units = 0; // swapped units
@@ -3415,6 +3450,8 @@ struct QuerySlot {
   bool want_info = false;   // m_getDocIdScoringInfo
   bool int_scores = false;  // gbsortby int: keys are m_intScore, TopNode::m_score 0
   int info_docs = 0;        // m_docsToGet: the second pass's docid limit
+  int info_nterms = 0;      // m_q->m_numTerms and m_realMaxTop (allocTopTree's reservations)
+  int info_rmt = 0;
   int info_ng = 0;          // m_numQueryTermInfos
   int info_scap = 0, info_pcap = 0;  // singles / pairs one docid can record
   int64_t scan_bytes = 0;
@@ -3498,6 +3535,7 @@ struct gbgpu_ctx {
   bool profiling = false;
   int probe_mode = 0;  // diagnostic only (GBGPU_PROBE_MODE)
   int probe_waves = 0;  // diagnostic: probe spans (GBGPU_PROBE_WAVES; 0 = PROBE_WAVES)
+  int probe_runspan = 0;  // diagnostic: chunks per run-driven probe wave (GBGPU_PROBE_RUNSPAN; 0 = 1)
   int score_mode = 0;  // diagnostic only (GBGPU_SCORE_MODE): 1 mini-merge without scoring
   int debug_ext = 0;   // diagnostic only (GBGPU_DEBUG_EXT): print the re-shrink table per query
   uint64_t *d_sdbg = nullptr;  // GBGPU_SCORE_MODE=2: per-wave k_score timing (GBGPU_SCORE_DUMP file)
@@ -3520,6 +3558,20 @@ static size_t res_keys_off() { return align256(sizeof(Counters)); }
 static size_t res_docs_off(int k) { return res_keys_off() + align256(4 * (size_t)std::max(k, 1)); }
 static size_t res_size(int k) { return res_docs_off(k) + 8 * (size_t)std::max(k, 1); }
 
+// the page map of a swapped list of `units` units: bytes to reserve, and its
+// build (two launches on `st`; an empty list's map is its zeroed total)
+static size_t page_map_bytes(uint32_t units) {
+  return align256(4 * ((size_t)(units + CHUNK_UNITS - 1) / CHUNK_UNITS + 1));
+}
+static int build_page_map(const uint8_t *d, uint32_t units, uint32_t *pm, hipStream_t st) {
+  const uint32_t np = (units + CHUNK_UNITS - 1) / CHUNK_UNITS;
+  if (!np) return 0;
+  hipLaunchKernelGGL(k_page_count, dim3(np), dim3(BLOCK), 0, st, d, units, pm);
+  hipLaunchKernelGGL(k_page_scan, dim3(1), dim3(1024), 0, st, np, pm);
+  HIPCHECK(hipGetLastError());
+  return 0;
+}
+
 static int upload_list(gbgpu_ctx *ctx, const uint8_t *bytes, int64_t size, int32_t *handle) {
   if (size < 0 || (size > 0 && size < 18) || (size > 0 && (size - 18) % 6 != 0)) return EINVAL;
   if ((size - 6) / 6 > 0xfffffff0LL) return GBGPU_ECAPACITY;
@@ -3528,11 +3580,12 @@ static int upload_list(gbgpu_ctx *ctx, const uint8_t *bytes, int64_t size, int32
   ListEntry e;
   e.size = size;
   e.units = size ? (uint32_t)((size - 6) / 6) : 0;
-  size_t alloc = (size_t)(size ? size - 6 : 0) + LIST_PAD;
-  alloc = align256(alloc);
+  const size_t lbytes = align256((size_t)(size ? size - 6 : 0) + LIST_PAD);
+  const size_t alloc = lbytes + page_map_bytes(e.units);
   e.mem = std::make_shared<ListMem>();
   if (hipMalloc(&e.mem->d, alloc) != hipSuccess) return ENOMEM;
   e.d = e.mem->d;
+  e.pm = reinterpret_cast<uint32_t *>(e.d + lbytes);
   HIPCHECK(hipMemsetAsync(e.d, 0, alloc, ctx->upload_stream));
   if (size) {
     // device image = the list after the first-key swap (Posdb.cpp:5689-5698):
@@ -3548,6 +3601,8 @@ static int upload_list(gbgpu_ctx *ctx, const uint8_t *bytes, int64_t size, int32
     hipLaunchKernelGGL(k_validate, dim3(std::max(grid, 1u)), dim3(256), 0, ctx->upload_stream, e.d, e.units,
                        ctx->d_flag);
     HIPCHECK(hipGetLastError());
+    int rc = build_page_map(e.d, e.units, e.pm, ctx->upload_stream);
+    if (rc) return rc;
     HIPCHECK(hipMemcpyAsync(ctx->h_flag, ctx->d_flag, 4, hipMemcpyDeviceToHost, ctx->upload_stream));
   }
   HIPCHECK(hipStreamSynchronize(ctx->upload_stream));
@@ -3582,12 +3637,6 @@ static int snapshot_lists(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms, 
   if (!p || nterms < 0 || (nterms && (!terms || !handles))) return EINVAL;
   if (p->docs_to_get <= 0 || p->real_max_top <= 0 || p->num_docid_splits <= 0) return EINVAL;
   if (nterms > 1024) return GBGPU_EUNSUPPORTED;
-  // the second scoring pass over docid-split pieces (its per-range skip and
-  // the kicked-out-docid bookkeeping, Posdb.cpp:6189-6193, 7588-7665): the
-  // CPU body.  With site clustering or paging it reads the same tree order
-  // (the prefilters are off in that pass, and every tree docid passed the
-  // paging filter already), so those run here.
-  if (p->get_docid_scoring_info && p->num_docid_splits > 1) return GBGPU_EUNSUPPORTED;
   ents.resize(nterms);
   std::lock_guard<std::mutex> g(ctx->lists_mu);
   for (int i = 0; i < nterms; i++) {
@@ -3602,6 +3651,7 @@ static int snapshot_lists(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms, 
 // site clustering: which part of Msg39's one-tree-over-all-pieces a pass is
 constexpr int TREE_INIT = 1;   // the pass starts the TopTree
 constexpr int TREE_FINAL = 2;  // the pass ends it: the tree is the result
+constexpr int TREE_EMIT = 4;   // the pass also writes the tree out (score info over docid splits)
 
 static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *terms, int nterms,
                            const ListEntry *ents, const gbgpu_params *p, int32_t dw_override,
@@ -3636,6 +3686,7 @@ static TreeParams tree_params(int32_t dw, int phase) {
   tp.partial = (float)(dw % 50) / 50.0;
   tp.init = (phase & TREE_INIT) ? 1 : 0;
   tp.final = (phase & TREE_FINAL) ? 1 : 0;
+  tp.emit = (phase & TREE_EMIT) ? 1 : 0;
   return tp;
 }
 
@@ -3721,6 +3772,8 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   q.want_info = p->get_docid_scoring_info != 0;
   q.int_scores = false;
   q.info_docs = p->docs_to_get;
+  q.info_nterms = nterms;
+  q.info_rmt = hp.real_max_top;
   q.info_ng = hp.ngroups;
   q.info_scap = hp.ngroups * hp.real_max_top;
   q.info_pcap = hp.ngroups * (hp.ngroups - 1) / 2 * hp.real_max_top;
@@ -3755,9 +3808,11 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   P.has_serp = p->min_serp_docid != 0;  // Posdb.cpp:4379-4381
   P.max_serp_score = p->max_serp_score;
   P.min_serp_docid = p->min_serp_docid;
-  P.max_serp_int = (p->max_serp_score >= -2147483648.0 && p->max_serp_score < 2147483648.0)
+  // (int32_t)m_maxSerpScore as the reference's x86-64 build computes it
+  // (cvttsd2si): truncation, or INT32_MIN when out of range or NaN
+  P.max_serp_int = (p->max_serp_score > -2147483649.0 && p->max_serp_score < 2147483648.0)
                        ? (int32_t)p->max_serp_score
-                       : (p->max_serp_score < 0 ? INT32_MIN : INT32_MAX);
+                       : INT32_MIN;
   P.clustering = clus;
   P.use_white = p->use_whitelist != 0;
   if (P.use_white) {
@@ -3792,6 +3847,7 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
     dense[term] = id;
     const ListEntry &e = ents[term];
     P.lists[id].p = e.d;
+    P.lists[id].pm = e.pm;
     P.lists[id].units = e.units;
     list_dmin[id] = e.dmin;
     list_dmax[id] = e.dmax;
@@ -3925,7 +3981,8 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
     if (!P.lists[id].probe) continue;
     const uint32_t units = P.lists[id].units;
     // a run-driven chunk costs a few dependent lookups: one chunk per wave
-    const uint32_t span = WCH_UNITS * (P.lists[id].probe == PROBE_BY_RUN ? 1 : S);
+    const uint32_t rspan = ctx->probe_runspan > 0 ? (uint32_t)ctx->probe_runspan : 1u;
+    const uint32_t span = WCH_UNITS * (P.lists[id].probe == PROBE_BY_RUN ? rspan : S);
     for (uint32_t u = 0; u < units; u += span) q.pw.push_back({(uint32_t)id, u, std::min(units, u + span)});
   }
   q.scan_bytes = scan;
@@ -3953,7 +4010,6 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   q.res_bytes = res_size(k);
   int rc2 = 0;
   rc2 |= q.tables.ensure(tbytes);
-  rc2 |= q.chunkcnt.ensure(4 * std::max<size_t>(1, q.g0c.size()));
   const uint32_t nwords = (uint32_t)((slot_ub + 31) / 32);
   const uint32_t cgrid = std::max(1u, (uint32_t)((nwords + CB - 1) / CB));
   rc2 |= q.cand.ensure(8 * slot_ub);
@@ -4020,7 +4076,6 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   HIPCHECK(hipMemcpyAsync(q.tables.p, q.h_stage, tbytes, hipMemcpyHostToDevice, st));
   const DevPlan *dpl = q.tables.as<DevPlan>();
   const G0Chunk *dchunks = q.tables.as<G0Chunk>(o_chunks);
-  const uint32_t *dafirst = q.tables.as<uint32_t>(o_afirst);
   const ProbeWork *dwork = q.tables.as<ProbeWork>(o_work);
   Counters *dctr = q.res.as<Counters>();
   Select *dsel = q.sel.as<Select>();
@@ -4034,10 +4089,8 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
                        (uint32_t)(sizeof(Select) / 4), bits, nb);
   }
   const uint32_t ng0 = (uint32_t)q.g0c.size();
-  hipLaunchKernelGGL(k_count_runs, dim3(ng0), dim3(BLOCK), 0, st, dpl, dchunks, q.chunkcnt.as<uint32_t>());
-  hipLaunchKernelGGL(k_scan_runs, dim3(1), dim3(1024), 0, st, ng0, q.chunkcnt.as<uint32_t>());
-  hipLaunchKernelGGL(k_write_runs, dim3(ng0), dim3(BLOCK), 0, st, dpl, dchunks, q.chunkcnt.as<uint32_t>(),
-                     dafirst, q.cand.as<uint64_t>(), q.cunit.as<uint32_t>(), dctr, ng0, q.dir.as<uint64_t>());
+  hipLaunchKernelGGL(k_write_runs, dim3(ng0), dim3(BLOCK), 0, st, dpl, dchunks, q.cand.as<uint64_t>(),
+                     q.cunit.as<uint32_t>(), dctr, ng0, q.dir.as<uint64_t>());
   if (ctx->profiling) HIPCHECK(hipEventRecord(q.ev[1], st));
   if (!q.pw.empty()) {
     auto kp = ctx->probe_mode == 5   ? k_probe<5, 2>
@@ -4212,9 +4265,16 @@ static void zero_pads(gbgpu_single_score *s) {
   zero_gap(s, offsetof(gbgpu_single_score, bflags) + 1, sizeof(gbgpu_single_score));
 }
 
-static int score_info(QuerySlot &q, const uint32_t *keys, const uint64_t *docs, uint32_t nsurv, gbgpu_result *out) {
-  int n = 0;
-  while (n < q.k && n < q.info_docs && keys[n]) n++;
+// the score info records of several second passes, appended in order (the
+// reference's buffers persist over docid-split pieces)
+struct InfoAcc {
+  int nd = 0, np = 0, ns = 0;
+  bool room = true;
+};
+// the second pass over docs[0, n) (tree docids, high -> low) against the
+// slot's last query: DocIdScore / PairScore / SingleScore appended to out
+static int score_info_docs(QuerySlot &q, const uint64_t *docs, int n, uint32_t nsurv, gbgpu_result *out,
+                           InfoAcc &acc) {
   if (!n) return 0;
   const DevPlan *hpl = reinterpret_cast<const DevPlan *>(q.h_stage);  // this query's plan (enqueue's staging copy)
   const int scap = std::max(q.info_scap, 1), pcap = std::max(q.info_pcap, 1);
@@ -4262,8 +4322,8 @@ static int score_info(QuerySlot &q, const uint32_t *keys, const uint64_t *docs, 
   HIPCHECK(hipMemcpyAsync(hp.data(), q.si.as<uint8_t>(o_ps), sizeof(gbgpu_pair_score) * hp.size(),
                           hipMemcpyDeviceToHost, st));
   HIPCHECK(hipStreamSynchronize(st));
-  int nd = 0, np = 0, ns = 0;
-  bool room = true;
+  int nd = acc.nd, np = acc.np, ns = acc.ns;
+  bool room = acc.room;
   for (int t = 0; t < n; t++) {
     if (info[t].ok == -1) return GBGPU_ECORRUPT;      // a tree docid with no survivor entry
     if (info[t].ok == -2) return GBGPU_EUNSUPPORTED;  // a getWordPosList path not replayed
@@ -4298,10 +4358,21 @@ static int score_info(QuerySlot &q, const uint32_t *keys, const uint64_t *docs, 
     np += cp;
     nd += info[t].ok ? 1 : 0;
   }
-  out->n_docid_scores = nd;
-  out->n_pair_scores = np;
-  out->n_single_scores = ns;
-  return room ? 0 : ENOSPC;
+  acc.nd = nd;
+  acc.np = np;
+  acc.ns = ns;
+  acc.room = room;
+  return 0;
+}
+static int score_info(QuerySlot &q, const uint32_t *keys, const uint64_t *docs, uint32_t nsurv, gbgpu_result *out) {
+  int n = 0;
+  while (n < q.k && n < q.info_docs && keys[n]) n++;
+  InfoAcc acc;
+  const int rc = score_info_docs(q, docs, n, nsurv, out, acc);
+  out->n_docid_scores = acc.nd;
+  out->n_pair_scores = acc.np;
+  out->n_single_scores = acc.ns;
+  return rc ? rc : (acc.room ? 0 : ENOSPC);
 }
 
 // hits_acc: when non-null, the query's intersected docids are appended to it
@@ -4400,9 +4471,32 @@ constexpr uint64_t GB_MAX_DOCID = 0x3fffffffffULL;  // MAX_DOCID = DOCID_MASK (T
 // Without site clustering the tree is the best docs_wanted by (score desc,
 // docid asc), each docid once, whatever the insertion order -- so the pieces'
 // top lists merge exactly on the host.
+// One docid-split piece's second pass: the tree's first m_docsToGet nodes
+// (tree[0, n), high -> low) whose docid lies in the piece's [lo, hi) are
+// scored again against the piece's survivors.  allocTopTree reserved the
+// buffers for xx = max(docsWanted, 32) docids (Posdb.cpp:931-975); a piece
+// that could reach the kicked-out-docid path (a full m_scoreInfoBuf,
+// Posdb.cpp:7588-7665) or a pair/single overflow is refused.
+static int split_info(QuerySlot &q, const int64_t *tree, int n, uint64_t lo, uint64_t hi, uint32_t nsurv,
+                      gbgpu_result *out, InfoAcc &acc, std::vector<uint64_t> &sel) {
+  sel.clear();
+  for (int x = 0; x < n && x < q.info_docs; x++) {
+    const uint64_t d = (uint64_t)tree[x];
+    if (d >= lo && d < hi) sel.push_back(d);
+  }
+  if (sel.empty()) return 0;
+  const int64_t xx = std::max<int64_t>(q.docs_wanted, 32);
+  const int64_t nt = std::min<int64_t>(q.info_nterms, 10);
+  const int64_t pairs_ref = nt * nt / 2 * q.info_rmt * xx, singles_ref = nt * q.info_rmt * xx;
+  const int64_t m = (int64_t)sel.size();
+  if (acc.nd + m >= xx || acc.np + m * q.info_pcap > pairs_ref || acc.ns + m * q.info_scap > singles_ref)
+    return GBGPU_EUNSUPPORTED;
+  return score_info_docs(q, sel.data(), (int)m, nsurv, out, acc);
+}
+
 static int query_splits(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *terms, int nterms,
                         const std::vector<ListEntry> &ents, const gbgpu_params *p, gbgpu_result *out) {
-  std::vector<uint64_t> d0, d1;
+  std::vector<uint64_t> d0, d1, dmx;  // dmx: the piece's m_maxDocId (its second pass's range end)
   {
     const uint64_t delta = GB_MAX_DOCID / (uint64_t)p->num_docid_splits;
     uint64_t ddd = 0;
@@ -4416,6 +4510,7 @@ static int query_splits(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *terms, 
       }
       d0.push_back(a);
       d1.push_back(std::min(b + 2, GB_MAX_DOCID));
+      dmx.push_back(b);
     } while (ddd < GB_MAX_DOCID);
   }
   const int ns = (int)d0.size(), nl = nterms;
@@ -4456,12 +4551,23 @@ static int query_splits(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *terms, 
   std::vector<int64_t> hit_ids;
   const bool clus = p->site_clustering != 0;
   bool tree_started = false, emitted = false;
+  // m_getDocIdScoringInfo over the pieces: after each piece's first pass,
+  // the reference walks the tree from its best node, counting at most
+  // m_docsToGet nodes, and scores again the ones inside the piece's range
+  // [m_minDocId, m_maxDocId) (Posdb.cpp:6160-6193); the records of every
+  // piece append to the same buffers (they persist over pieces).  The pieces
+  // run without the pass (pq), which this loop adds.
+  const bool want_info = p->get_docid_scoring_info != 0;
+  gbgpu_params pq = *p;
+  pq.get_docid_scoring_info = 0;
+  InfoAcc acc;
+  std::vector<uint64_t> sel;
   for (int j = 0; j < ns; j++) {
     size_t total = 0;
     for (int i = 0; i < nl; i++) {
       const SplitWin &w = win[(size_t)i * ns + j];
       off[i] = total;
-      total += align256((size_t)(w.hi - w.lo) * 6 + LIST_PAD);
+      total += align256((size_t)(w.hi - w.lo) * 6 + LIST_PAD) + page_map_bytes(w.hi - w.lo);
     }
     if (q.split.ensure(std::max<size_t>(total, 256))) return ENOMEM;
     if (total) HIPCHECK(hipMemsetAsync(q.split.p, 0, total, q.stream));
@@ -4470,13 +4576,17 @@ static int query_splits(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *terms, 
       const uint32_t n = w.hi - w.lo;
       ListEntry e;
       e.d = q.split.as<uint8_t>(off[i]);
+      e.pm = reinterpret_cast<uint32_t *>(e.d + align256((size_t)n * 6 + LIST_PAD));
       e.units = n;
       e.size = n ? (int64_t)n * 6 + 6 : 0;  // as Msg2 holds it: first key 18 bytes
       e.dmin = w.dmin;
       e.dmax = w.dmax;
       e.live = true;
-      if (n)
+      if (n) {
         HIPCHECK(hipMemcpyAsync(e.d, ents[i].d + (size_t)w.lo * 6, (size_t)n * 6, hipMemcpyDeviceToDevice, q.stream));
+        int rc = build_page_map(e.d, n, e.pm, q.stream);
+        if (rc) return rc;
+      }
       we[i] = e;
     }
     if (dw == 0) {
@@ -4487,8 +4597,9 @@ static int query_splits(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *terms, 
       dw = docs_wanted(p, sz.data(), nl);
       if (dw == 0) continue;
     }
-    const int phase = clus ? ((tree_started ? 0 : TREE_INIT) | (j == ns - 1 ? TREE_FINAL : 0)) : (TREE_INIT | TREE_FINAL);
-    int rc = enqueue_entries(ctx, q, terms, nterms, we.data(), p, dw, phase);
+    const int phase = clus ? ((tree_started ? 0 : TREE_INIT) | (j == ns - 1 ? TREE_FINAL : 0) | (want_info ? TREE_EMIT : 0))
+                           : (TREE_INIT | TREE_FINAL);
+    int rc = enqueue_entries(ctx, q, terms, nterms, we.data(), &pq, dw, phase);
     if (rc) {
       q.pending = false;
       return rc;
@@ -4513,6 +4624,10 @@ static int query_splits(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *terms, 
         emitted = true;
         for (int x = 0; x < r.n; x++) top.push_back({ts[x], td[x]});
       }
+      if (want_info && replayed) {
+        rc = split_info(q, td.data(), r.n, d0[j], dmx[j], (uint32_t)r.hits, out, acc, sel);
+        if (rc) return rc;
+      }
       continue;
     }
     for (int x = 0; x < r.n; x++) top.push_back({ts[x], td[x]});
@@ -4526,6 +4641,12 @@ static int query_splits(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *terms, 
                           }),
               top.end());
     if ((int32_t)top.size() > dw) top.resize(dw);
+    if (want_info && !q.early) {
+      td.resize(top.size());
+      for (size_t x = 0; x < top.size(); x++) td[x] = top[x].second;
+      rc = split_info(q, td.data(), (int)top.size(), d0[j], dmx[j], (uint32_t)r.hits, out, acc, sel);
+      if (rc) return rc;
+    }
   }
   if (clus && tree_started && !emitted) {
     // the last piece scored nothing: the tree as the earlier pieces left it
@@ -4548,6 +4669,11 @@ static int query_splits(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *terms, 
   out->hits = hits;
   out->filtered = filtered;
   out->docs_wanted = dw;
+  if (want_info) {
+    out->n_docid_scores = acc.nd;
+    out->n_pair_scores = acc.np;
+    out->n_single_scores = acc.ns;
+  }
   if (out->hit_docids) {
     // pieces overlap by two docids (getLists' [d0, d1+2]): the set has each once
     std::sort(hit_ids.begin(), hit_ids.end());
@@ -4562,7 +4688,7 @@ static int query_splits(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *terms, 
     n++;
   }
   out->n = n;
-  return 0;
+  return want_info && !acc.room ? ENOSPC : 0;
 }
 
 // ------------------------------------------------------------------ C ABI
@@ -4622,6 +4748,7 @@ int gbgpu_open(int device, gbgpu_ctx **out) {
   }
   if (const char *pm = std::getenv("GBGPU_PROBE_MODE")) ctx->probe_mode = std::atoi(pm);
   if (const char *pw = std::getenv("GBGPU_PROBE_WAVES")) ctx->probe_waves = std::atoi(pw);
+  if (const char *rs = std::getenv("GBGPU_PROBE_RUNSPAN")) ctx->probe_runspan = std::atoi(rs);
   if (const char *sm = std::getenv("GBGPU_SCORE_MODE")) ctx->score_mode = std::atoi(sm);
   if (ctx->score_mode == 2) HIPCHECK(hipMalloc(&ctx->d_sdbg, 8192 * 64));
   if (const char *de = std::getenv("GBGPU_DEBUG_EXT")) ctx->debug_ext = std::atoi(de);

@@ -84,6 +84,7 @@ inline int range_mode(int32_t fc, int *is_int) {
 // Device image.  Lists are addressed by a dense id 0..nlists-1.
 struct DevList {
   const uint8_t *p;     // swapped list (12-byte first key), 16-B aligned, zero padded
+  const uint32_t *pm;   // its page map: run starts before each CHUNK_UNITS-unit page
   uint32_t units;       // (size-6)/6
   uint32_t group_bits;  // positive groups containing this list (+NEG_BIT if in a negative group)
   int32_t g0_array;     // index among the smallest group's candidate arrays, -1 if none

@@ -1751,7 +1751,11 @@ static int run_range(const orc_qterm *qt, const uint8_t *const *lists, const int
       }
       if (prm->min_serp_docid) { /* m_hasMaxSerpScore, Posdb.cpp:4379-4381, 7327-7347 */
         if (sortByI >= 0) {
-          const int32_t m = (int32_t)prm->max_serp_score;
+          /* (int32_t)m_maxSerpScore as x86-64 compiles it (cvttsd2si): the
+             truncation, or INT32_MIN when out of range or NaN (in C that
+             cast is undefined, so it is spelled out) */
+          const double ms = prm->max_serp_score;
+          const int32_t m = (ms > -2147483649.0 && ms < 2147483648.0) ? (int32_t)ms : INT32_MIN;
           if (intScore > m) continue;
           if (intScore == m && (int64_t)pt.docId <= prm->min_serp_docid) continue;
         } else {

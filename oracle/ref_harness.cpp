@@ -193,6 +193,10 @@ static int ref_query(const orc_qterm *terms, const uint8_t *const *lists, const 
       d1 = MAX_DOCID;
       ddd = MAX_DOCID;
     }
+    // Msg39::controlLoop hands each piece its range (Msg39.cpp:376-377): the
+    // second pass rescores only the tree's docids inside it (Posdb.cpp:6189)
+    req.m_minDocId = d0;
+    req.m_maxDocId = d1;
     int64_t docIdEnd = d1 + 1 + 1;
     if (docIdEnd > MAX_DOCID) docIdEnd = MAX_DOCID;
     for (int i = 0; i < nterms; i++) {

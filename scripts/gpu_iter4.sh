@@ -18,7 +18,7 @@ timeout -k 10 400 python $R/bench.py --steps 300 --warmup 5 --no-cpu-baseline --
 cat $O/${T}_bench.json
 [ -n "$NOPROF" ] && exit 0
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/${T}_prof -o run --output-format csv -- python3 $R/bench.py --steps 64 --warmup 2 --slots 1 --no-cpu-baseline --no-config3 --no-merge --no-ceiling ${BENCH_ARGS} > $O/${T}_prof.log 2>&1 || { echo "rocprof failed"; tail -30 $O/${T}_prof.log; exit 1; }
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/${T}_prof -o run --output-format csv -- python3 $R/bench.py --steps 64 --warmup 2 --slots 1 --no-cpu-baseline --no-config3 --no-merge --no-ceiling --no-clustering ${BENCH_ARGS} > $O/${T}_prof.log 2>&1 || { echo "rocprof failed"; tail -30 $O/${T}_prof.log; exit 1; }
 f=$(find $O/${T}_prof -name "*kernel_stats.csv" | head -1)
 python3 -c "
 import csv

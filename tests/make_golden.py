@@ -253,6 +253,29 @@ def save_sortby():
     print(f"  f_field_title: hits={r['hits']} n={len(r['docids'])}")
 
 
+def save_scoreinfo_splits():
+    """m_getDocIdScoringInfo over Msg39's docid-split pieces (the default
+    HTML /search: >= 5 splits, Msg40.cpp:696-701, score info on,
+    SearchInput.cpp:321-327): each piece's second pass scores the tree's
+    first m_docsToGet nodes inside its [m_minDocId, m_maxDocId)
+    (Posdb.cpp:6160-6193) into buffers that persist over the pieces."""
+    import posdb_py
+    N = 6000
+    ks = qkinds.kinds(N, seed=13)
+    for j, (kind, S, clus, dtg) in enumerate(((0, 5, 0, 30), (0, 5, 1, 30), (1, 2, 0, 12), (2, 5, 1, 20),
+                                               (4, 3, 0, 25), (8, 5, 1, 15), (3, 2, 1, 40))):
+        q = ks[kind]
+        q.docs_to_get = dtg
+        lists = generate(q, N, seed=5400 + j)
+        nd = len({int(d) for l in lists for d in posdb_py.docids(l)})
+        lists = posdb_py.remap_docids(lists, split_boundary_docids(nd, 40 + j, splits=(S,)))
+        p = q.params(site_clustering=clus, num_docid_splits=S)
+        p.get_docid_scoring_info = 1
+        r = save_query(f"splits{S}_c{clus}_{q.name}", q.terms, lists, p, prefix="s")
+        print(f"  s_splits{S}_c{clus}_{q.name}: n={len(r['docids'])} info={len(r['score_info'])} "
+              f"pairs={len(r['pair_scores'])} singles={len(r['single_scores'])}")
+
+
 def split_boundary_docids(n, seed, splits=(2, 5)):
     """n sorted distinct docids holding, for each piece boundary d1 of
     Msg39's docid-split loop (Msg39.cpp:362-373), d1-1 .. d1+3: d1..d1+2 are
@@ -441,6 +464,7 @@ def main():
     save_paging()
     save_whitelist()
     save_scoreinfo()
+    save_scoreinfo_splits()
     save_sortby()
     save_range()
     save_msg3a()
@@ -462,6 +486,8 @@ if __name__ == "__main__":
         save_whitelist()
     elif sys.argv[1:] == ["scoreinfo"]:
         save_scoreinfo()
+    elif sys.argv[1:] == ["scoreinfo_splits"]:
+        save_scoreinfo_splits()
     elif sys.argv[1:] == ["sortby"]:
         save_sortby()
     elif sys.argv[1:] == ["range"]:

@@ -143,3 +143,36 @@ def test_gpu_fields_clustering_vs_oracle(engine, fc, vf, vi, ints):
         assert np.array_equal(r.docids, o["docids"]), label
         assert np.array_equal(np.asarray(r.scores, np.float32).view(np.uint32),
                               np.asarray(o["scores"], np.float32).view(np.uint32)), label
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [1, 2])
+@pytest.mark.parametrize("fc", [59, 60])
+def test_gpu_int_sortby_paging_vs_oracle(engine, seed, fc):
+    """gbsortby int with the widget's paging filter (Posdb.cpp:7330-7336):
+    m_intScore against (int32_t)m_maxSerpScore -- fractional bounds of both
+    signs truncate toward zero, ties on the bound compare the docid with
+    m_minSerpDocId, and an out-of-range or NaN bound is INT32_MIN (x86-64's
+    cvttsd2si), which drops every docid above it."""
+    import qkinds
+    from numlists import number_list
+    from workload import generate
+    N = 40000
+    q = qkinds.kinds(N, seed=seed)[0]
+    lists = generate(q, N, seed=7200 + seed)
+    terms = list(q.terms)
+    t = gbgpu.QTerm(1, 0, fc, 0, -1, -1, -1, 0, max(x.qpos for x in terms) + 2, 0, -1, 1.0)
+    terms.append(t)
+    lists = list(lists) + [number_list(lists, 0.6, seed=seed, kmax=2, ints=True)]
+    base = engine.query(terms, lists, q.params(), cap=1 << 16)
+    mid = len(base.docids) // 2
+    v = int(base.int_scores[mid])
+    d = int(base.docids[mid])
+    bounds = [v + 0.75, v - 0.75, -v - 0.5, 0.25 - abs(v), 1e12, -1e12, float("nan")]
+    for b in bounds:
+        params = q.params(max_serp_score=b, min_serp_docid=d)
+        o = orc.query(terms, lists, params, cap=1 << 16)
+        r = engine.query(terms, lists, params, cap=1 << 16)
+        label = f"fc={fc} seed={seed} bound={b}"
+        assert (r.hits, r.filtered, r.docs_wanted) == (o["hits"], o["filtered"], o["docs_wanted"]), label
+        assert np.array_equal(r.docids, o["docids"]), label
