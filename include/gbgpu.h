@@ -102,9 +102,10 @@ typedef struct gbgpu_params {
   int32_t get_docid_scoring_info; /* m_getDocIdScoringInfo: the per-docid score
                                breakdown second pass (Posdb.cpp:6116-6244,
                                7554-7665, 7752-7775) into gbgpu_result's
-                               docid/pair/single score arrays.  With docid splits
-                               it returns GBGPU_EUNSUPPORTED (the adapter runs the
-                               CPU body) */
+                               docid/pair/single score arrays, also over docid
+                               splits (one second pass per piece; GBGPU_EUNSUPPORTED
+                               only where the reference's buffers would fill and
+                               kick records out, Posdb.cpp:7588-7665) */
   double  max_serp_score;   /* m_maxSerpScore  } paging of a widget's next page:   */
   int64_t min_serp_docid;   /* m_minSerpDocId  } nonzero enables the filter of
                                Posdb.cpp:4379-4381, 7327-7347 (counted in
@@ -184,8 +185,11 @@ typedef struct gbgpu_result {
   /* with gbgpu_params::get_docid_scoring_info: the second pass's records for
    * the first min(n, docs_to_get) docids of the tree, high -> low, one
    * DocIdScore each, their PairScores / SingleScores in the reference's append
-   * order.  Caller-owned arrays of *_cap entries; *_n = entries written
-   * (ENOSPC if an array is too small). */
+   * order.  With docid splits every piece's second pass appends its own
+   * records (the tree's first docs_to_get nodes inside the piece's docid
+   * range, Posdb.cpp:6160-6193), so the arrays need room for up to
+   * (pieces x docs_to_get) docids.  Caller-owned arrays of *_cap entries;
+   * *_n = entries written (ENOSPC if an array is too small). */
   gbgpu_docid_score  *docid_scores;  int32_t docid_scores_cap;  int32_t n_docid_scores;
   gbgpu_pair_score   *pair_scores;   int32_t pair_scores_cap;   int32_t n_pair_scores;
   gbgpu_single_score *single_scores; int32_t single_scores_cap; int32_t n_single_scores;

@@ -1638,6 +1638,8 @@ __device__ __forceinline__ uint64_t load6(gu8 *k) {
 struct SurvOut {
   float score;
   int32_t site_rank, doc_lang, ok;
+  int32_t ival;  // m_intScore with a gbsortby int term (DocIdScore::m_finalScore is then its double)
+  int32_t pad;
 };
 
 template <int NQ, int NS, class RP, class REC = NoRec>
@@ -1913,6 +1915,7 @@ __device__ __forceinline__ void score_survivor(const DevPlan *__restrict__ pl, c
   }
   if (so) {
     so->score = score;
+    so->ival = (int32_t)ival;
     so->site_rank = siteRank < 0 ? 0 : siteRank;
     so->doc_lang = docLang;
     so->ok = empty_pos ? -2 : ok;
@@ -2671,27 +2674,46 @@ struct TreeParams {
   int64_t ridiculous;   // m_ridiculousMax
   int64_t num_nodes;    // m_numNodes
   uint32_t init, final; // first / last piece
+  int32_t ints;          // m_useIntScores: nodes ordered by m_intScore (TopTree.cpp:216-219, 270-274)
+  int32_t pad2;
 };
 
-__device__ __forceinline__ bool node_better(float s1, uint64_t d1, float s2, uint64_t d2) {
-  return s1 > s2 || (s1 == s2 && d1 < d2);
+// Node scores: m_score, or with integer tree scores m_intScore kept as the
+// float slot's bit pattern (ints): compared as int32, and the domain tree's
+// key score cs = (uint32_t)m_intScore (TopTree.cpp:332-335)
+__device__ __forceinline__ bool sc_gt(float a, float b, bool ints) {
+  return ints ? __float_as_int(a) > __float_as_int(b) : a > b;
+}
+__device__ __forceinline__ bool sc_eq(float a, float b, bool ints) {
+  return ints ? __float_as_int(a) == __float_as_int(b) : a == b;
+}
+__device__ __forceinline__ uint32_t tree_cs(float s, bool ints) {
+  if (ints) return (uint32_t)__float_as_int(s);
+  // (uint32_t)m_score as x86-64 converts a float: the low 32 bits of its
+  // 64-bit truncation (cvttss2si; 0x8000000000000000 when out of range)
+  if (!(s > -9.2233720368547758e18f && s < 9.2233720368547758e18f)) return 0u;
+  return (uint32_t)(uint64_t)(int64_t)s;
+}
+__device__ __forceinline__ bool node_better(float s1, uint64_t d1, float s2, uint64_t d2, bool ints = false) {
+  return sc_gt(s1, s2, ints) || (sc_eq(s1, s2, ints) && d1 < d2);
 }
 __device__ __forceinline__ uint32_t dom_hash8(uint64_t d) { return (uint32_t)((d & 0x3fc0ull) >> 6); }  // Titledb.h:114-115
 
 // index of the first node (best-first order) not better than (s, d)
-__device__ uint32_t tree_lower_bound(const float *ts, const uint64_t *td, uint32_t n, float s, uint64_t d, int lane) {
+__device__ uint32_t tree_lower_bound(const float *ts, const uint64_t *td, uint32_t n, float s, uint64_t d, int lane,
+                                     bool ints) {
   uint32_t lo = 0, hi = n;
   while (hi - lo > 64) {
     const uint32_t step = (hi - lo + 63) / 64;
     const uint32_t idx = lo + lane * step;
-    const uint32_t c = (uint32_t)__popcll(__ballot(idx < hi && node_better(ts[idx], td[idx], s, d)));
+    const uint32_t c = (uint32_t)__popcll(__ballot(idx < hi && node_better(ts[idx], td[idx], s, d, ints)));
     if (c == 0) return lo;
     const uint32_t nlo = lo + (c - 1) * step + 1;
     hi = min(hi, lo + c * step);
     lo = nlo;
   }
   const uint32_t idx = lo + lane;
-  return lo + (uint32_t)__popcll(__ballot(idx < hi && node_better(ts[idx], td[idx], s, d)));
+  return lo + (uint32_t)__popcll(__ballot(idx < hi && node_better(ts[idx], td[idx], s, d, ints)));
 }
 
 // deleteNode's count bookkeeping (TopTree.cpp:543-547) and removal of node q
@@ -2725,12 +2747,13 @@ __device__ void tree_delete(float *ts, uint64_t *td, int32_t *dom, uint32_t &n, 
 __device__ void tree_add(float *ts, uint64_t *td, int32_t *dom, uint32_t &n, float &vcount, const TreeParams &tp,
                          float s, uint64_t d, uint32_t &err, int lane) {
   const uint32_t dh = dom_hash8(d);
+  const bool ints = tp.ints != 0;
   if (vcount >= tp.docs_wanted) {
-    if (!node_better(s, d, ts[n - 1], td[n - 1])) return;
+    if (!node_better(s, d, ts[n - 1], td[n - 1], ints)) return;
   }
-  const uint32_t p = tree_lower_bound(ts, td, n, s, d, lane);
-  if (p < n && ts[p] == s && td[p] == d) return;  // "if equal do not replace"
-  const uint32_t cs = (uint32_t)s;
+  const uint32_t p = tree_lower_bound(ts, td, n, s, d, lane, ints);
+  if (p < n && sc_eq(ts[p], s, ints) && td[p] == d) return;  // "if equal do not replace"
+  const uint32_t cs = tree_cs(s, ints);
   bool del = false;
   float delS = 0.0f;
   uint64_t delD = 0;
@@ -2742,7 +2765,7 @@ __device__ void tree_add(float *ts, uint64_t *td, int32_t *dom, uint32_t &n, flo
     for (uint32_t t = lane; t < n; t += 64) {
       const uint64_t dt = td[t];
       if (dom_hash8(dt) != dh) continue;
-      const uint32_t ct = (uint32_t)ts[t];
+      const uint32_t ct = tree_cs(ts[t], ints);
       if (ct < mc || (ct == mc && dt < md)) {
         mc = ct;
         md = dt;
@@ -2795,7 +2818,7 @@ __device__ void tree_add(float *ts, uint64_t *td, int32_t *dom, uint32_t &n, flo
   wave_lds_sync();
   if (dom[dh] < tp.cap) vcount += 1.0;
   else if (dom[dh] == tp.cap) vcount += tp.partial;
-  if (del) tree_delete(ts, td, dom, n, vcount, tp, tree_lower_bound(ts, td, n, delS, delD, lane), dh, lane);
+  if (del) tree_delete(ts, td, dom, n, vcount, tp, tree_lower_bound(ts, td, n, delS, delD, lane, ints), dh, lane);
   while (n > 0 && (vcount - 1.0 >= tp.docs_wanted || (int64_t)n == tp.num_nodes))
     tree_delete(ts, td, dom, n, vcount, tp, n - 1, dom_hash8(td[n - 1]), lane);
 }
@@ -2840,11 +2863,13 @@ __global__ void __launch_bounds__(64) k_tree_replay(Counters *ctr, const uint32_
     const bool serp = valid && sflag[i];
     const float B = valid ? sbound[i] : 0.0f;
     const uint64_t d = valid ? sdoc[i] : 0;
-    const float sc = key_score(key);
-    const bool live = valid && !(B <= mws);  // not skipped by the prefilters
+    const bool ints = tp.ints != 0;
+    const float sc = ints ? __int_as_float((int32_t)(key ^ 0x80000000u)) : key_score(key);
+    // (integer scores come from a gbsortby int term: the prefilters are off)
+    const bool live = valid && (ints || !(B <= mws));  // not skipped by the prefilters
     const bool ok = live && key != 0;        // scored, not filtered by paging
     const bool full = vcount >= tp.docs_wanted;
-    const bool rej = called && full && n > 0 && !node_better(sc, d, ts[n - 1], td[n - 1]);
+    const bool rej = called && full && n > 0 && !node_better(sc, d, ts[n - 1], td[n - 1], ints);
     const uint64_t slow = __ballot(ok && !rej);
     const int j = slow ? __ffsll((unsigned long long)slow) - 1 : 64;
     const uint64_t below = j >= 64 ? ~0ull : ((1ull << j) - 1);
@@ -2867,7 +2892,7 @@ __global__ void __launch_bounds__(64) k_tree_replay(Counters *ctr, const uint32_
   if (tp.final || tp.emit) {
     for (uint32_t q = lane; q < n; q += 64) {
       const uint32_t b = __float_as_uint(ts[q]);
-      uint32_t k = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+      uint32_t k = tp.ints ? (b ^ 0x80000000u) : (b & 0x80000000u) ? ~b : (b | 0x80000000u);
       out_key[q] = k ? k : 1u;
       out_doc[q] = td[q];
     }
@@ -3675,7 +3700,7 @@ static int enqueue(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *terms, int n
 // > 0 fixes TopTree::m_docsWanted (docid splits size the tree once, at the
 // first piece: Msg39.cpp:938-966).
 // TopTree::setNumNodes' sizing (TopTree.cpp:64-101) for the replay
-static TreeParams tree_params(int32_t dw, int phase) {
+static TreeParams tree_params(int32_t dw, int phase, bool ints) {
   TreeParams tp;
   std::memset(&tp, 0, sizeof tp);
   tp.docs_wanted = dw;
@@ -3687,6 +3712,7 @@ static TreeParams tree_params(int32_t dw, int phase) {
   tp.init = (phase & TREE_INIT) ? 1 : 0;
   tp.final = (phase & TREE_FINAL) ? 1 : 0;
   tp.emit = (phase & TREE_EMIT) ? 1 : 0;
+  tp.ints = ints ? 1 : 0;
   return tp;
 }
 
@@ -3720,7 +3746,7 @@ static int enqueue_tree_emit(QuerySlot &q, int32_t dw) {
                      (uint32_t)(sizeof(Counters) / 4), reinterpret_cast<uint32_t *>(dctr), 0u);
   hipLaunchKernelGGL(k_tree_replay, dim3(1), dim3(64), 0, st, dctr, (const uint32_t *)nullptr,
                      (const uint32_t *)nullptr, (const uint64_t *)nullptr, (const uint8_t *)nullptr,
-                     (const float *)nullptr, q.tree.as<TreeState>(), tree_params(dw, TREE_FINAL),
+                     (const float *)nullptr, q.tree.as<TreeState>(), tree_params(dw, TREE_FINAL, q.int_scores),
                      q.res.as<uint32_t>(res_keys_off()), q.res.as<uint64_t>(res_docs_off(q.k)));
   HIPCHECK(hipGetLastError());
   HIPCHECK(hipEventRecord(q.ev_done, st));
@@ -3824,11 +3850,6 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   P.sortby_group = hp.sortby_group;
   P.sortby_int = hp.sortby_int;
   q.int_scores = hp.sortby_int != 0;
-  // integer TopTree scores: with the domain-cap tree, the paging filter or
-  // the score info they take other reference paths (TopTree.cpp:332-333,
-  // Posdb.cpp:7330-7336, 7559-7560): not on the GPU
-  if (hp.sortby_int && (clus || p->get_docid_scoring_info || p->num_docid_splits > 1))
-    return GBGPU_EUNSUPPORTED;
   P.min_listi = hp.min_listi;
   P.all_same_wiki = 1;  // m_allInSameWikiPhrase, Posdb.cpp:5764-5778
   for (int j = 0; j < hp.ngroups; j++) {
@@ -4186,7 +4207,7 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
     hipLaunchKernelGGL(k_tree_replay, dim3(1), dim3(64), 0, st, dctr, order, q.skey.as<uint32_t>(),
                        (const uint64_t *)svdoc, q.sflag.as<uint8_t>(), q.sbound.as<float>(),
                        (tree_phase & TREE_FINAL) ? (TreeState *)q.tree.p : q.tree.as<TreeState>(),
-                       tree_params(q.docs_wanted, tree_phase), q.res.as<uint32_t>(res_keys_off()),
+                       tree_params(q.docs_wanted, tree_phase, q.int_scores), q.res.as<uint32_t>(res_keys_off()),
                        q.res.as<uint64_t>(res_docs_off(k)));
     q.replayed = true;
     if (ctx->profiling) HIPCHECK(hipEventRecord(q.ev[5], st));
@@ -4271,10 +4292,111 @@ struct InfoAcc {
   int nd = 0, np = 0, ns = 0;
   bool room = true;
 };
+// Appends each scored docid's records straight to the caller's arrays (one
+// second pass: no buffer limit is reached, enqueue checked the worst case).
+struct OutSink {
+  gbgpu_result *out;
+  InfoAcc &acc;
+  int ng;
+  bool ints;
+  int operator()(uint64_t docid, const SurvOut &inf, int cs, int cp, const gbgpu_single_score *ss,
+                 const gbgpu_pair_score *ps) {
+    gbgpu_docid_score d;
+    std::memset(&d, 0, sizeof d);
+    d.docid = (int64_t)docid;
+    d.final_score = ints ? (double)inf.ival : (double)inf.score;  // Posdb.cpp:7557-7560
+    d.site_rank = (int8_t)inf.site_rank;
+    d.doc_lang = inf.doc_lang;
+    d.num_required_terms = ng;
+    d.num_pairs = cp;
+    d.num_singles = cs;
+    d.pairs_offset = cp ? acc.np * (int32_t)sizeof(gbgpu_pair_score) : -1;
+    d.singles_offset = cs ? acc.ns * (int32_t)sizeof(gbgpu_single_score) : -1;
+    if (acc.ns + cs > out->single_scores_cap || acc.np + cp > out->pair_scores_cap ||
+        (inf.ok && acc.nd + 1 > out->docid_scores_cap))
+      acc.room = false;
+    if (acc.room) {
+      if (cs) std::memcpy(out->single_scores + acc.ns, ss, sizeof(gbgpu_single_score) * cs);
+      if (cp) std::memcpy(out->pair_scores + acc.np, ps, sizeof(gbgpu_pair_score) * cp);
+      for (int k = 0; k < cs; k++) zero_pads(out->single_scores + acc.ns + k);
+      for (int k = 0; k < cp; k++) zero_pads(out->pair_scores + acc.np + k);
+      if (inf.ok) {
+        std::memcpy(out->docid_scores + acc.nd, &d, sizeof d);
+        zero_pads(out->docid_scores + acc.nd);
+      }
+    }
+    acc.ns += cs;
+    acc.np += cp;
+    acc.nd += inf.ok ? 1 : 0;
+    return 0;
+  }
+};
+// The buffers as they stand over the docid-split pieces, in the reference's
+// SafeBufs' capacities (allocTopTree, Posdb.cpp:931-975): m_scoreInfoBuf
+// keeps at most what fits, and once it is full each new DocIdScore pushes out
+// the first one whose docid the tree no longer holds, with that docid's
+// pair / single chunks and the offsets after them (Posdb.cpp:7562-7665).
+struct SplitSink {
+  std::vector<gbgpu_docid_score> dinfo;
+  std::vector<gbgpu_pair_score> dp;
+  std::vector<gbgpu_single_score> ds;
+  int64_t cap_d = 0, cap_p = 0, cap_s = 0;  // bytes
+  int ng = 0;
+  bool ints = false;
+  std::vector<uint64_t> tree;  // the tree's docids after this piece, sorted (hasDocId)
+  int operator()(uint64_t docid, const SurvOut &inf, int cs, int cp, const gbgpu_single_score *ss,
+                 const gbgpu_pair_score *ps) {
+    constexpr int64_t DS = sizeof(gbgpu_docid_score), PS = sizeof(gbgpu_pair_score), SS = sizeof(gbgpu_single_score);
+    // a scorer whose records do not fit drops them (Posdb.cpp:3258-3264,
+    // 4213-4219): not emulated
+    if ((int64_t)(ds.size() + cs) * SS > cap_s || (int64_t)(dp.size() + cp) * PS > cap_p) return GBGPU_EUNSUPPORTED;
+    gbgpu_docid_score d;
+    std::memset(&d, 0, sizeof d);
+    d.docid = (int64_t)docid;
+    d.final_score = ints ? (double)inf.ival : (double)inf.score;  // Posdb.cpp:7557-7560
+    d.site_rank = (int8_t)inf.site_rank;
+    d.doc_lang = inf.doc_lang;
+    d.num_required_terms = ng;
+    d.num_pairs = cp;
+    d.num_singles = cs;
+    d.pairs_offset = cp ? (int32_t)(dp.size() * PS) : -1;
+    d.singles_offset = cs ? (int32_t)(ds.size() * SS) : -1;
+    for (int k = 0; k < cs; k++) {
+      ds.push_back(ss[k]);
+      zero_pads(&ds.back());
+    }
+    for (int k = 0; k < cp; k++) {
+      dp.push_back(ps[k]);
+      zero_pads(&dp.back());
+    }
+    if (!inf.ok) return 0;
+    int64_t avail = cap_d - (int64_t)dinfo.size() * DS;
+    if (avail < DS + 1) return 0;  // no room: its pair / single records stay, unreferenced
+    zero_pads(&d);
+    dinfo.push_back(d);
+    avail -= DS;
+    if (avail >= DS) return 0;
+    size_t v = 0;
+    for (; v < dinfo.size(); v++)
+      if (!std::binary_search(tree.begin(), tree.end(), (uint64_t)dinfo[v].docid)) break;
+    if (v == dinfo.size()) return 0;
+    const gbgpu_docid_score x = dinfo[v];
+    const int32_t po = x.pairs_offset, pz = x.num_pairs * (int32_t)PS;
+    const int32_t so = x.singles_offset, sz = x.num_singles * (int32_t)SS;
+    dinfo.erase(dinfo.begin() + (long)v);
+    if (pz) dp.erase(dp.begin() + po / PS, dp.begin() + (po + pz) / PS);
+    if (sz) ds.erase(ds.begin() + so / SS, ds.begin() + (so + sz) / SS);
+    for (auto &e : dinfo) {
+      if (e.pairs_offset > po) e.pairs_offset -= pz;
+      if (e.singles_offset > so) e.singles_offset -= sz;
+    }
+    return 0;
+  }
+};
 // the second pass over docs[0, n) (tree docids, high -> low) against the
-// slot's last query: DocIdScore / PairScore / SingleScore appended to out
-static int score_info_docs(QuerySlot &q, const uint64_t *docs, int n, uint32_t nsurv, gbgpu_result *out,
-                           InfoAcc &acc) {
+// slot's last query: each docid's records to `sink`
+template <class Sink>
+static int score_info_docs(QuerySlot &q, const uint64_t *docs, int n, uint32_t nsurv, Sink &sink) {
   if (!n) return 0;
   const DevPlan *hpl = reinterpret_cast<const DevPlan *>(q.h_stage);  // this query's plan (enqueue's staging copy)
   const int scap = std::max(q.info_scap, 1), pcap = std::max(q.info_pcap, 1);
@@ -4322,53 +4444,23 @@ static int score_info_docs(QuerySlot &q, const uint64_t *docs, int n, uint32_t n
   HIPCHECK(hipMemcpyAsync(hp.data(), q.si.as<uint8_t>(o_ps), sizeof(gbgpu_pair_score) * hp.size(),
                           hipMemcpyDeviceToHost, st));
   HIPCHECK(hipStreamSynchronize(st));
-  int nd = acc.nd, np = acc.np, ns = acc.ns;
-  bool room = acc.room;
   for (int t = 0; t < n; t++) {
     if (info[t].ok == -1) return GBGPU_ECORRUPT;      // a tree docid with no survivor entry
     if (info[t].ok == -2) return GBGPU_EUNSUPPORTED;  // a getWordPosList path not replayed
     if (info[t].ok == -3) return GBGPU_ECAPACITY;     // record arena exhausted
     const int cs = cnt[2 * t], cp = cnt[2 * t + 1];
     if (cs > scap || cp > pcap) return GBGPU_ECAPACITY;
-    gbgpu_docid_score d;
-    std::memset(&d, 0, sizeof d);
-    d.docid = (int64_t)docs[t];
-    d.final_score = (double)info[t].score;
-    d.site_rank = (int8_t)info[t].site_rank;
-    d.doc_lang = info[t].doc_lang;
-    d.num_required_terms = q.info_ng;
-    d.num_pairs = cp;
-    d.num_singles = cs;
-    d.pairs_offset = cp ? np * (int32_t)sizeof(gbgpu_pair_score) : -1;
-    d.singles_offset = cs ? ns * (int32_t)sizeof(gbgpu_single_score) : -1;
-    if (ns + cs > out->single_scores_cap || np + cp > out->pair_scores_cap ||
-        (info[t].ok && nd + 1 > out->docid_scores_cap))
-      room = false;
-    if (room) {
-      if (cs) std::memcpy(out->single_scores + ns, &hs[(size_t)t * scap], sizeof(gbgpu_single_score) * cs);
-      if (cp) std::memcpy(out->pair_scores + np, &hp[(size_t)t * pcap], sizeof(gbgpu_pair_score) * cp);
-      for (int k = 0; k < cs; k++) zero_pads(out->single_scores + ns + k);
-      for (int k = 0; k < cp; k++) zero_pads(out->pair_scores + np + k);
-      if (info[t].ok) {
-        std::memcpy(out->docid_scores + nd, &d, sizeof d);
-        zero_pads(out->docid_scores + nd);
-      }
-    }
-    ns += cs;
-    np += cp;
-    nd += info[t].ok ? 1 : 0;
+    const int rc = sink(docs[t], info[t], cs, cp, &hs[(size_t)t * scap], &hp[(size_t)t * pcap]);
+    if (rc) return rc;
   }
-  acc.nd = nd;
-  acc.np = np;
-  acc.ns = ns;
-  acc.room = room;
   return 0;
 }
 static int score_info(QuerySlot &q, const uint32_t *keys, const uint64_t *docs, uint32_t nsurv, gbgpu_result *out) {
   int n = 0;
   while (n < q.k && n < q.info_docs && keys[n]) n++;
   InfoAcc acc;
-  const int rc = score_info_docs(q, docs, n, nsurv, out, acc);
+  OutSink sink{out, acc, q.info_ng, q.int_scores};
+  const int rc = score_info_docs(q, docs, n, nsurv, sink);
   out->n_docid_scores = acc.nd;
   out->n_pair_scores = acc.np;
   out->n_single_scores = acc.ns;
@@ -4471,27 +4563,45 @@ constexpr uint64_t GB_MAX_DOCID = 0x3fffffffffULL;  // MAX_DOCID = DOCID_MASK (T
 // Without site clustering the tree is the best docs_wanted by (score desc,
 // docid asc), each docid once, whatever the insertion order -- so the pieces'
 // top lists merge exactly on the host.
-// One docid-split piece's second pass: the tree's first m_docsToGet nodes
-// (tree[0, n), high -> low) whose docid lies in the piece's [lo, hi) are
-// scored again against the piece's survivors.  allocTopTree reserved the
-// buffers for xx = max(docsWanted, 32) docids (Posdb.cpp:931-975); a piece
-// that could reach the kicked-out-docid path (a full m_scoreInfoBuf,
-// Posdb.cpp:7588-7665) or a pair/single overflow is refused.
+// One docid-split piece's second pass: the tree's nodes (tree[0, n), high ->
+// low) whose docid lies in the piece's [lo, hi), walked under the
+// m_docsToGet limit below, are scored again against the piece's survivors
+// into the buffers `sink` keeps over the pieces.
 static int split_info(QuerySlot &q, const int64_t *tree, int n, uint64_t lo, uint64_t hi, uint32_t nsurv,
-                      gbgpu_result *out, InfoAcc &acc, std::vector<uint64_t> &sel) {
+                      SplitSink &sink, std::vector<uint64_t> &sel) {
+  // numProcessed counts every node walked, but the docsToGet test runs only
+  // before a docid is looked for: out-of-range nodes are skipped by `goto
+  // nextNode` past it, so the first in-range node after the limit is still
+  // scored (Posdb.cpp:6163-6193)
   sel.clear();
-  for (int x = 0; x < n && x < q.info_docs; x++) {
-    const uint64_t d = (uint64_t)tree[x];
-    if (d >= lo && d < hi) sel.push_back(d);
+  int walked = 0, x = 0;
+  while (walked < q.info_docs) {
+    bool found = false;
+    while (x < n) {
+      const uint64_t d = (uint64_t)tree[x++];
+      walked++;
+      if (d >= lo && d < hi) {
+        sel.push_back(d);
+        found = true;
+        break;
+      }
+    }
+    if (!found) break;
   }
   if (sel.empty()) return 0;
-  const int64_t xx = std::max<int64_t>(q.docs_wanted, 32);
-  const int64_t nt = std::min<int64_t>(q.info_nterms, 10);
-  const int64_t pairs_ref = nt * nt / 2 * q.info_rmt * xx, singles_ref = nt * q.info_rmt * xx;
-  const int64_t m = (int64_t)sel.size();
-  if (acc.nd + m >= xx || acc.np + m * q.info_pcap > pairs_ref || acc.ns + m * q.info_scap > singles_ref)
-    return GBGPU_EUNSUPPORTED;
-  return score_info_docs(q, sel.data(), (int)m, nsurv, out, acc);
+  if (!sink.cap_d) {
+    // allocTopTree's reservations, xx = max(the tree's nodes, 32)
+    const int64_t xx = std::max<int64_t>(q.docs_wanted, 32);
+    const int64_t nt = std::min<int64_t>(q.info_nterms, 10);
+    sink.cap_d = xx * (int64_t)sizeof(gbgpu_docid_score) + 100;
+    sink.cap_p = nt * nt / 2 * q.info_rmt * xx * (int64_t)sizeof(gbgpu_pair_score);
+    sink.cap_s = nt * q.info_rmt * xx * (int64_t)sizeof(gbgpu_single_score);
+    sink.ng = q.info_ng;
+    sink.ints = q.int_scores;
+  }
+  sink.tree.assign(tree, tree + n);
+  std::sort(sink.tree.begin(), sink.tree.end());
+  return score_info_docs(q, sel.data(), (int)sel.size(), nsurv, sink);
 }
 
 static int query_splits(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *terms, int nterms,
@@ -4540,7 +4650,9 @@ static int query_splits(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *terms, 
                             q.stream));
     HIPCHECK(hipStreamSynchronize(q.stream));
   }
-  std::vector<std::pair<float, int64_t>> top;
+  // the tree's (score, docid): m_score, or m_intScore with a gbsortby int
+  // term, as a double (exact for both)
+  std::vector<std::pair<double, int64_t>> top;
   int32_t dw = 0;
   int64_t hits = 0;
   int32_t filtered = 0;
@@ -4548,6 +4660,7 @@ static int query_splits(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *terms, 
   std::vector<size_t> off(nl);
   std::vector<int64_t> td;
   std::vector<float> ts;
+  std::vector<int32_t> ti;
   std::vector<int64_t> hit_ids;
   const bool clus = p->site_clustering != 0;
   bool tree_started = false, emitted = false;
@@ -4560,7 +4673,7 @@ static int query_splits(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *terms, 
   const bool want_info = p->get_docid_scoring_info != 0;
   gbgpu_params pq = *p;
   pq.get_docid_scoring_info = 0;
-  InfoAcc acc;
+  SplitSink sink;
   std::vector<uint64_t> sel;
   for (int j = 0; j < ns; j++) {
     size_t total = 0;
@@ -4609,12 +4722,15 @@ static int query_splits(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *terms, 
     const int cap = clus ? TC : dw;
     td.assign(std::max(cap, 1), 0);
     ts.assign(std::max(cap, 1), 0.f);
+    ti.assign(std::max(cap, 1), 0);
     gbgpu_result r;
     std::memset(&r, 0, sizeof r);
     r.docids = td.data();
     r.scores = ts.data();
+    r.int_scores = ti.data();
     r.capacity = cap;
     rc = collect(ctx, q, &r, out->hit_docids ? &hit_ids : nullptr);
+    auto node_key = [&](int x) -> double { return q.int_scores ? (double)ti[x] : (double)ts[x]; };
     if (rc) return rc;
     hits += r.hits;
     filtered += r.filtered;
@@ -4622,21 +4738,21 @@ static int query_splits(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *terms, 
       // one TopTree over every piece, carried on the device between them
       if (replayed && (phase & TREE_FINAL)) {
         emitted = true;
-        for (int x = 0; x < r.n; x++) top.push_back({ts[x], td[x]});
+        for (int x = 0; x < r.n; x++) top.push_back({node_key(x), td[x]});
       }
       if (want_info && replayed) {
-        rc = split_info(q, td.data(), r.n, d0[j], dmx[j], (uint32_t)r.hits, out, acc, sel);
+        rc = split_info(q, td.data(), r.n, d0[j], dmx[j], (uint32_t)r.hits, sink, sel);
         if (rc) return rc;
       }
       continue;
     }
-    for (int x = 0; x < r.n; x++) top.push_back({ts[x], td[x]});
-    std::sort(top.begin(), top.end(), [](const std::pair<float, int64_t> &a, const std::pair<float, int64_t> &b) {
+    for (int x = 0; x < r.n; x++) top.push_back({node_key(x), td[x]});
+    std::sort(top.begin(), top.end(), [](const std::pair<double, int64_t> &a, const std::pair<double, int64_t> &b) {
       return a.first > b.first || (a.first == b.first && a.second < b.second);
     });
     // a docid read by two overlapping pieces scores the same in both
     top.erase(std::unique(top.begin(), top.end(),
-                          [](const std::pair<float, int64_t> &a, const std::pair<float, int64_t> &b) {
+                          [](const std::pair<double, int64_t> &a, const std::pair<double, int64_t> &b) {
                             return a.second == b.second;
                           }),
               top.end());
@@ -4644,7 +4760,7 @@ static int query_splits(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *terms, 
     if (want_info && !q.early) {
       td.resize(top.size());
       for (size_t x = 0; x < top.size(); x++) td[x] = top[x].second;
-      rc = split_info(q, td.data(), (int)top.size(), d0[j], dmx[j], (uint32_t)r.hits, out, acc, sel);
+      rc = split_info(q, td.data(), (int)top.size(), d0[j], dmx[j], (uint32_t)r.hits, sink, sel);
       if (rc) return rc;
     }
   }
@@ -4657,22 +4773,32 @@ static int query_splits(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *terms, 
     }
     td.assign(TC, 0);
     ts.assign(TC, 0.f);
+    ti.assign(TC, 0);
     gbgpu_result r;
     std::memset(&r, 0, sizeof r);
     r.docids = td.data();
     r.scores = ts.data();
+    r.int_scores = ti.data();
     r.capacity = TC;
     rc = collect(ctx, q, &r);
     if (rc) return rc;
-    for (int x = 0; x < r.n; x++) top.push_back({ts[x], td[x]});
+    for (int x = 0; x < r.n; x++) top.push_back({q.int_scores ? (double)ti[x] : (double)ts[x], td[x]});
   }
   out->hits = hits;
   out->filtered = filtered;
   out->docs_wanted = dw;
+  bool room = true;
   if (want_info) {
-    out->n_docid_scores = acc.nd;
-    out->n_pair_scores = acc.np;
-    out->n_single_scores = acc.ns;
+    out->n_docid_scores = (int32_t)sink.dinfo.size();
+    out->n_pair_scores = (int32_t)sink.dp.size();
+    out->n_single_scores = (int32_t)sink.ds.size();
+    room = out->n_docid_scores <= out->docid_scores_cap && out->n_pair_scores <= out->pair_scores_cap &&
+           out->n_single_scores <= out->single_scores_cap;
+    if (room) {
+      std::copy(sink.dinfo.begin(), sink.dinfo.end(), out->docid_scores);
+      std::copy(sink.dp.begin(), sink.dp.end(), out->pair_scores);
+      std::copy(sink.ds.begin(), sink.ds.end(), out->single_scores);
+    }
   }
   if (out->hit_docids) {
     // pieces overlap by two docids (getLists' [d0, d1+2]): the set has each once
@@ -4684,11 +4810,12 @@ static int query_splits(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *terms, 
   for (const auto &t : top) {
     if (n >= out->capacity) break;
     if (out->docids) out->docids[n] = t.second;
-    if (out->scores) out->scores[n] = t.first;
+    if (out->scores) out->scores[n] = q.int_scores ? 0.0f : (float)t.first;
+    if (out->int_scores) out->int_scores[n] = q.int_scores ? (int32_t)t.first : 0;
     n++;
   }
   out->n = n;
-  return want_info && !acc.room ? ENOSPC : 0;
+  return room ? 0 : ENOSPC;
 }
 
 // ------------------------------------------------------------------ C ABI

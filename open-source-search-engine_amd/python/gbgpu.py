@@ -456,10 +456,13 @@ class Engine:
     @staticmethod
     def info_arrays(params: Params, nterms: int):
         """Score-info output arrays sized for the request's worst case
-        (every group pair and group recording real_max_top entries)."""
+        (every group pair and group recording real_max_top entries; with
+        docid splits every piece's second pass appends up to docs_to_get
+        docids)."""
         if not params.get_docid_scoring_info:
             return None
-        nd = max(1, params.docs_to_get)
+        pieces = 1 if params.num_docid_splits <= 1 else params.num_docid_splits + 1
+        nd = max(1, params.docs_to_get) * pieces
         ng = max(1, min(nterms, 16))
         rmt = max(1, params.real_max_top)
         return (np.zeros(nd, DOCID_DT), np.zeros(max(1, nd * ng * (ng - 1) // 2 * rmt), PAIR_DT),

@@ -217,6 +217,7 @@ typedef struct {
   int64_t n;             /* m_numUsedNodes                               */
   double *score;         /* sorted best first (an int score is exact)     */
   int64_t *docid;
+  int ints;              /* m_useIntScores: score holds m_intScore        */
 } TTree;
 
 /* TopTree::setNumNodes, TopTree.cpp:64-101 */
@@ -259,6 +260,17 @@ static void tt_delete(TTree *t, int64_t i, uint8_t domHash) {
   t->n--;
 }
 
+/* the domain tree's key score cs (TopTree.cpp:332-335): (uint32_t)m_intScore,
+   or (uint32_t)m_score as x86-64 converts a float (the low 32 bits of its
+   64-bit truncation, cvttss2si) -- spelled out, the C casts being undefined
+   for negative values */
+static inline uint32_t tt_cs(const TTree *t, double score) {
+  if (t->ints) return (uint32_t)(int32_t)score;
+  const float f = (float)score;
+  if (!(f > -9.2233720368547758e18f && f < 9.2233720368547758e18f)) return 0; /* 0x8000000000000000 */
+  return (uint32_t)(uint64_t)(int64_t)f;
+}
+
 /* TopTree::addNode, TopTree.cpp:206-516; returns 1 if the node was added */
 static int tt_add(TTree *t, double score, int64_t docid) {
   const uint8_t domHash = domHash8(docid);
@@ -282,7 +294,7 @@ addIt:;
     pos = lo;
     if (pos < t->n && t->score[pos] == score && t->docid[pos] == docid) return 0; /* equal: not replaced */
   }
-  const uint32_t cs = (uint32_t)score;
+  const uint32_t cs = tt_cs(t, score);
   int64_t deleteMe = -1; /* docid of the domain's m_t2 minimum to delete */
   if (t->domCount[domHash] >= t->ridiculousMax) {
     /* m_domMinNode[domHash]: minimum (uint32 score, docid) of the domain */
@@ -290,7 +302,7 @@ addIt:;
     uint32_t mcs = 0;
     for (int64_t i = 0; i < t->n; i++) {
       if (domHash8(t->docid[i]) != domHash) continue;
-      const uint32_t c = (uint32_t)t->score[i];
+      const uint32_t c = tt_cs(t, t->score[i]);
       if (m < 0 || c < mcs || (c == mcs && t->docid[i] < t->docid[m])) {
         m = i;
         mcs = c;
@@ -1828,9 +1840,6 @@ int orc_query(const orc_qterm *qt, const uint8_t *const *lists, const int64_t *s
     const int fc = qt[i].field_code;
     if ((fc == F_SORTBYINT || fc == F_REVSORTBYINT) && qt[i].is_required) intMode = 1;
     if (fc == F_FACETSTR || fc == F_FACETINT || fc == F_FACETFLOAT) return ENOTSUP; /* facets: DESIGN.md */
-    /* integer tree scores with the domain caps / paging / pieces: not restated */
-    if ((fc == F_SORTBYINT || fc == F_REVSORTBYINT) && (prm->site_clustering || prm->num_docid_splits > 1))
-      return ENOTSUP;
   }
   initWeights();
 
@@ -1873,6 +1882,7 @@ int orc_query(const orc_qterm *qt, const uint8_t *const *lists, const int64_t *s
       alloced = 1;
       out->docs_wanted = (int32_t)dw;
       tt_init(&tk, (int32_t)dw, prm->site_clustering != 0);
+      tk.ints = intMode;
     }
     orc_result r;
     memset(&r, 0, sizeof r);

@@ -253,6 +253,41 @@ def save_sortby():
     print(f"  f_field_title: hits={r['hits']} n={len(r['docids'])}")
 
 
+def save_sortby_int_modes():
+    """gbsortby int (59) / gbrevsortby int (60) beyond the plain top tree:
+    site clustering (the domain tree's key score cs = (uint32_t)m_intScore,
+    TopTree.cpp:332-335, 455-463: negative ints sort above every positive
+    one there), docid splits (one tree over the pieces), and the second
+    pass's DocIdScore::m_finalScore = (double)m_intScore (Posdb.cpp:7557-
+    7560), also over splits."""
+    import posdb_py
+    N = 6000
+    ks = qkinds.kinds(N, seed=13)
+    cases = [("clus0", 0, 59, dict(site_clustering=1), 0, 100),
+             ("clus1", 4, 60, dict(site_clustering=1), 0, 30),
+             ("clus2", 1, 59, dict(site_clustering=1), 0, 12),
+             ("splits0", 0, 59, dict(num_docid_splits=2), 0, 100),
+             ("splits1", 2, 60, dict(num_docid_splits=5, site_clustering=1), 0, 20),
+             ("info0", 0, 59, {}, 1, 25),
+             ("info1", 4, 60, dict(site_clustering=1), 1, 20),
+             ("info2", 1, 59, dict(num_docid_splits=5), 1, 15)]
+    for j, (tag, kind, fc, kw, info, dtg) in enumerate(cases):
+        q = ks[kind]
+        q.docs_to_get = dtg
+        lists = generate(q, N, seed=5600 + j)
+        if kw.get("num_docid_splits", 1) > 1:
+            nd = len({int(d) for l in lists for d in posdb_py.docids(l)})
+            lists = posdb_py.remap_docids(lists, split_boundary_docids(nd, 60 + j, splits=(kw["num_docid_splits"],)))
+        terms = list(q.terms)
+        terms.append(gbgpu.QTerm(1, 0, fc, 0, -1, -1, -1, 0, max(t.qpos for t in terms) + 2, 0, -1, 1.0))
+        lists = list(lists) + [number_list(lists, 0.7, seed=120 + j, kmax=2, ints=True)]
+        p = q.params(**kw)
+        p.get_docid_scoring_info = info
+        r = save_query(f"sortbyint_{tag}_{q.name}", terms, lists, p, prefix="s" if info else "f")
+        print(f"  sortbyint_{tag}_{q.name}: n={len(r['docids'])} hits={r['hits']}"
+              + (f" info={len(r['score_info'])}" if info else ""))
+
+
 def save_scoreinfo_splits():
     """m_getDocIdScoringInfo over Msg39's docid-split pieces (the default
     HTML /search: >= 5 splits, Msg40.cpp:696-701, score info on,
@@ -466,6 +501,7 @@ def main():
     save_scoreinfo()
     save_scoreinfo_splits()
     save_sortby()
+    save_sortby_int_modes()
     save_range()
     save_msg3a()
     cases = [(0, -1), (1, -1), (0, 5000), (1, 5000), (0, 1)]
@@ -488,6 +524,8 @@ if __name__ == "__main__":
         save_scoreinfo()
     elif sys.argv[1:] == ["scoreinfo_splits"]:
         save_scoreinfo_splits()
+    elif sys.argv[1:] == ["sortby_int_modes"]:
+        save_sortby_int_modes()
     elif sys.argv[1:] == ["sortby"]:
         save_sortby()
     elif sys.argv[1:] == ["range"]:
