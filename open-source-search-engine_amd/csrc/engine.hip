@@ -99,6 +99,7 @@ struct Counters {
   uint32_t tree_err; // site clustering: the tree outgrew the replay's LDS (TC nodes)
   uint32_t unsup;    // a re-shrink would copy a misparsed run (not emulated): EUNSUPPORTED
   uint32_t pad[2];
+  uint32_t rdbg_t, rdbg_total;  // diagnostic: replay us in tree_add / in all
   unsigned long long dmax_all;  // largest survivor docid
   ListExt ext[MAXL];
   uint32_t bcnt[8];    // survivors per size bucket (k_cmp_write block 0), NBKT
@@ -112,6 +113,7 @@ struct Select {
   uint32_t na, nb;           // k_topk's gathers: A (prefix above P), B (prefix P)
   uint32_t done;             // k_topk blocks finished (the last one selects)
   uint32_t pad;
+  unsigned long long tdbg[8];  // diagnostic (GBGPU_TOPK_DEBUG): k_topk phase clocks (s_memrealtime)
 };
 
 // where a docid's run sits in one list: first unit and length in units
@@ -2615,9 +2617,19 @@ __device__ int32_t ring_best_dist(const uint8_t *ring, uint8_t m, uint8_t i, int
   return bestDist;
 }
 
+// one replay entry (16 B, docid order): score key, prefilter bound, docid
+// with bit 63 set when the paging test filtered it (k_score's sflag)
+__device__ __forceinline__ uint4 rep_entry(uint32_t key, float B, uint64_t d, bool serp) {
+  if (serp) d |= 1ull << 63;
+  return make_uint4(key, __float_as_uint(B), (uint32_t)d, (uint32_t)(d >> 32));
+}
+
+// rep != nullptr: the survivors are in docid order already, so the bound
+// goes straight into the replay entry; else into sbound for k_rank
 __global__ void __launch_bounds__(64 * BND_WAVES) k_bound(const DevPlan *__restrict__ pl, const Counters *ctr,
                                                        const uint32_t *sv_slot, const uint32_t *sv_lm,
-                                                       const Loc *sv_loc, float *sbound) {
+                                                       const Loc *sv_loc, float *sbound, const uint32_t *skey,
+                                                       const uint64_t *sdoc, const uint8_t *sflag, uint4 *rep) {
   __shared__ __attribute__((aligned(16))) uint8_t s_ring[BND_WAVES][RING];
   stage_weights(&c_weights);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -2629,7 +2641,10 @@ __global__ void __launch_bounds__(64 * BND_WAVES) k_bound(const DevPlan *__restr
     const uint32_t s = sv_slot[i], lm = sv_lm[i];
     const Loc *svl = sv_loc + (uint64_t)i * (uint32_t)pl->nlists;
     if (pl->sortby_group >= 0) {  // gbsortby: both prefilters are skipped (Posdb.cpp:6050-6051, 6350)
-      if (lane == 0) sbound[i] = INF;
+      if (lane == 0) {
+        if (rep) rep[i] = rep_entry(skey[i], INF, sdoc[i], sflag[i] != 0);
+        else sbound[i] = INF;
+      }
       continue;
     }
     // lane g: getMaxPossibleScore's scan of group g
@@ -2669,7 +2684,10 @@ __global__ void __launch_bounds__(64 * BND_WAVES) k_bound(const DevPlan *__restr
     // min over the wave
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) B = fminf(B, __shfl_xor(B, off, 64));
-    if (lane == 0) sbound[i] = B;
+    if (lane == 0) {
+      if (rep) rep[i] = rep_entry(skey[i], B, sdoc[i], sflag[i] != 0);
+      else sbound[i] = B;
+    }
   }
 }
 
@@ -2696,7 +2714,7 @@ __device__ __forceinline__ uint32_t lower_bound_u64(const uint64_t *a, uint32_t 
 }
 
 __global__ void k_rank(const DevPlan *__restrict__ pl, const Counters *ctr, const uint32_t *sv_slot, const uint64_t *sdoc,
-                       uint32_t *order) {
+                       const uint32_t *skey, const uint8_t *sflag, const float *sbound, uint4 *rep) {
   const uint32_t nsurv = (uint32_t)(ctr->surv_top >> 36);
   const int g0n = pl->g0n;
   uint32_t sb[MAXG0 + 1];
@@ -2709,7 +2727,7 @@ __global__ void k_rank(const DevPlan *__restrict__ pl, const Counters *ctr, cons
     uint32_t pos = i - sb[k];
     for (int k2 = 0; k2 < g0n; k2++)
       if (k2 != k) pos += lower_bound_u64(sdoc, sb[k2], sb[k2 + 1], d);
-    order[pos] = i;
+    rep[pos] = rep_entry(skey[i], sbound[i], d, sflag[i] != 0);
   }
 }
 
@@ -2885,14 +2903,20 @@ __device__ __forceinline__ float key_score(uint32_t key) {
 }
 
 // one wave: the docid-order loop of intersectLists10_r with the TopTree
-// (Posdb.cpp:6137-7706, minWinningScore per pass)
-__global__ void __launch_bounds__(64) k_tree_replay(Counters *ctr, const uint32_t *order, const uint32_t *skey,
-                                                    const uint64_t *sdoc, const uint8_t *sflag, const float *sbound,
-                                                    TreeState *T, TreeParams tp, uint32_t *out_key,
-                                                    uint64_t *out_doc) {
+// (Posdb.cpp:6137-7706, minWinningScore per pass).  The loop is serial, so
+// its input streams through registers: RP_BUF buffers of RP_C chunks (64
+// entries each) are in flight while one is staged in LDS and walked chunk by
+// chunk; a chunk's lanes are re-tested after every offer that changes the
+// tree (the reference's per-docid order).
+constexpr int RP_C = 16;
+constexpr int RP_BUF = 3;  // 48 loads in flight (vmcnt holds 63)
+
+__global__ void __launch_bounds__(64) k_tree_replay(Counters *ctr, const uint4 *rep, TreeState *T, TreeParams tp,
+                                                    uint32_t *out_key, uint64_t *out_doc) {
   __shared__ float ts[TC];
   __shared__ uint64_t td[TC];
   __shared__ int32_t dom[256];
+  __shared__ uint4 stage[RP_C * 64];
   const int lane = threadIdx.x;
   uint32_t n = 0;
   float vcount = 0.0f;
@@ -2909,42 +2933,110 @@ __global__ void __launch_bounds__(64) k_tree_replay(Counters *ctr, const uint32_
   }
   wave_lds_sync();
   const uint32_t ns = (uint32_t)(ctr->surv_top >> 36);
+  const bool ints = tp.ints != 0;
   float mws = -1.0f;  // minWinningScore, Posdb.cpp:6012
   bool called = false;
   uint32_t filtered = 0, err = 0;
-  for (uint32_t base = 0; base < ns && !err;) {
-    const uint32_t pidx = base + lane;
-    const bool valid = pidx < ns;
-    const uint32_t i = valid ? (order ? order[pidx] : pidx) : 0;
-    const uint32_t key = valid ? skey[i] : 0;
-    const bool serp = valid && sflag[i];
-    const float B = valid ? sbound[i] : 0.0f;
-    const uint64_t d = valid ? sdoc[i] : 0;
-    const bool ints = tp.ints != 0;
-    const float sc = ints ? __int_as_float((int32_t)(key ^ 0x80000000u)) : key_score(key);
-    // (integer scores come from a gbsortby int term: the prefilters are off)
-    const bool live = valid && (ints || !(B <= mws));  // not skipped by the prefilters
-    const bool ok = live && key != 0;        // scored, not filtered by paging
-    const bool full = vcount >= tp.docs_wanted;
-    const bool rej = called && full && n > 0 && !node_better(sc, d, ts[n - 1], td[n - 1], ints);
-    const uint64_t slow = __ballot(ok && !rej);
-    const int j = slow ? __ffsll((unsigned long long)slow) - 1 : 64;
-    const uint64_t below = j >= 64 ? ~0ull : ((1ull << j) - 1);
-    filtered += (uint32_t)__popcll(__ballot(live && serp) & below);
-    if (!slow) {
-      base += 64;
-      continue;
+  uint32_t dbg_adds = 0, dbg_nmax = 0;  // diagnostic (GBGPU_TOPK_DEBUG)
+  uint64_t dbg_t = 0;
+  const uint64_t dbg_t0 = __builtin_amdgcn_s_memrealtime();
+  float bot_s = n ? ts[n - 1] : 0.0f;  // the tree's last node
+  uint64_t bot_d = n ? td[n - 1] : 0;
+  constexpr uint32_t BATCH = RP_C * 64;
+  const uint32_t nbatch = (ns + BATCH - 1) / BATCH;
+  // one staged batch, chunk by chunk
+  auto walk = [&](uint32_t bt) {
+    for (int c = 0; c < RP_C && !err; c++) {
+      const uint32_t p = bt * BATCH + (uint32_t)c * 64 + lane;
+      if (bt * BATCH + (uint32_t)c * 64 >= ns) break;
+      const uint4 e = stage[c * 64 + lane];
+      const bool valid = p < ns;
+      const uint32_t key = e.x;
+      const float B = __uint_as_float(e.y);
+      const bool serp = valid && (e.w >> 31);
+      const uint64_t d = ((uint64_t)(e.w & 0x7fffffffu) << 32) | e.z;
+      const float sc = ints ? __int_as_float((int32_t)(key ^ 0x80000000u)) : key_score(key);
+      // (integer scores come from a gbsortby int term: the prefilters are off)
+      uint64_t from = ~0ull;  // lanes not yet decided
+      for (;;) {
+        const bool live = valid && (ints || !(B <= mws));  // not skipped by the prefilters
+        const bool ok = live && key != 0;                   // scored, not filtered by paging
+        const bool full = vcount >= tp.docs_wanted;
+        const bool rej = called && full && n > 0 && !node_better(sc, d, bot_s, bot_d, ints);
+        const uint64_t slow = __ballot(ok && !rej) & from;
+        const int j = slow ? __ffsll((unsigned long long)slow) - 1 : 64;
+        const uint64_t below = j >= 64 ? ~0ull : ((1ull << j) - 1);
+        filtered += (uint32_t)__popcll(__ballot(live && serp) & below & from);
+        if (!slow) break;
+        const float s = __shfl(sc, j, 64);
+        const uint64_t dd = __shfl(d, j, 64);
+        const uint64_t c0 = __builtin_amdgcn_s_memrealtime();
+        tree_add(ts, td, dom, n, vcount, tp, s, dd, err, lane);
+        dbg_adds++;
+        dbg_t += __builtin_amdgcn_s_memrealtime() - c0;
+        dbg_nmax = max(dbg_nmax, n);
+        if (err) break;
+        called = true;
+        if (n) {
+          bot_s = ts[n - 1];
+          bot_d = td[n - 1];
+        }
+        if (n > (uint32_t)tp.docs_wanted) mws = ts[n - 1];  // Posdb.cpp:7699-7704
+        if (j == 63) break;
+        from = ~0ull << (j + 1);
+      }
     }
-    const float s = __shfl(sc, j, 64);
-    const uint64_t dd = __shfl(d, j, 64);
-    tree_add(ts, td, dom, n, vcount, tp, s, dd, err, lane);
-    called = true;
-    if (n > (uint32_t)tp.docs_wanted) mws = ts[n - 1];  // Posdb.cpp:7699-7704
-    base += (uint32_t)j + 1;
+  };
+  // three register buffers of RP_C chunks as named values (an array or a
+  // vector would be copied out of the load registers, and wait on them)
+#define RP_EACH(M, b) M(b, 0) M(b, 1) M(b, 2) M(b, 3) M(b, 4) M(b, 5) M(b, 6) M(b, 7) \
+  M(b, 8) M(b, 9) M(b, 10) M(b, 11) M(b, 12) M(b, 13) M(b, 14) M(b, 15)
+#define RP_DECL(b, c) uint4 b##c = make_uint4(0u, 0u, 0u, 0u);
+#define RP_LOAD(b, c) b##c = rep[min(bt_ * BATCH + (uint32_t)(c) * 64 + lane, ns - 1)];
+#define RP_STAGE(b, c) stage[(c) * 64 + lane] = b##c;
+#define RP_FETCH(b, bt)        \
+  {                            \
+    const uint32_t bt_ = (bt); \
+    RP_EACH(RP_LOAD, b)        \
   }
+#define RP_CONSUME(b, bt)   \
+  RP_EACH(RP_STAGE, b)      \
+  wave_lds_sync();          \
+  walk(bt);
+  static_assert(RP_C == 16 && RP_BUF == 3, "RP_EACH names 16 chunks, three buffers");
+  RP_EACH(RP_DECL, x)
+  RP_EACH(RP_DECL, y)
+  RP_EACH(RP_DECL, z)
+  // (fetches are unconditional -- past the end they re-read the last entry --
+  // so every path reaches a use with the same loads in flight)
+  if (ns) {
+  RP_FETCH(x, 0u)
+  RP_FETCH(y, 1u)
+  RP_FETCH(z, 2u)
+  for (uint32_t bt = 0; bt < nbatch && !err; bt += RP_BUF) {
+    RP_CONSUME(x, bt)
+    RP_FETCH(x, bt + 3)
+    if (bt + 1 >= nbatch || err) break;
+    RP_CONSUME(y, bt + 1)
+    RP_FETCH(y, bt + 4)
+    if (bt + 2 >= nbatch || err) break;
+    RP_CONSUME(z, bt + 2)
+    RP_FETCH(z, bt + 5)
+  }
+  }
+#undef RP_EACH
+#undef RP_DECL
+#undef RP_LOAD
+#undef RP_STAGE
+#undef RP_FETCH
+#undef RP_CONSUME
   if (lane == 0) {
     ctr->filtered = filtered;
     if (err) ctr->tree_err = 1;
+    ctr->pad[0] = dbg_adds;
+    ctr->pad[1] = dbg_nmax;
+    ctr->rdbg_t = (uint32_t)(dbg_t / 100);
+    ctr->rdbg_total = (uint32_t)((__builtin_amdgcn_s_memrealtime() - dbg_t0) / 100);
   }
   if (tp.final || tp.emit) {
     for (uint32_t q = lane; q < n; q += 64) {
@@ -3052,6 +3144,77 @@ __device__ void top_bin(const P *h, uint32_t need, uint32_t *tmp, uint32_t *s_bi
   __syncthreads();
 }
 
+__device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+  return x;
+}
+
+// top_bin over Select::hist with coalesced 16-B loads (a thread holding 64
+// consecutive bins would make every load touch 64 lines): wave w holds bins
+// [4096 w, 4096 w + 4096) as 16 rows of 256, lane l bins 4l..4l+3 of a row;
+// the wave holding the need-th entry walks its rows, then its lanes, from
+// the top.  tmp: 16 words.
+__device__ void top_bin_hist(const uint32_t *h, uint32_t need, uint32_t *tmp, uint32_t *s_bin, uint32_t *s_above,
+                             uint32_t *s_total) {
+  static_assert(TK_THREADS == 1024 && SEL_HBINS == 16 * 4096, "16 waves of 4096 bins");
+  typedef uint32_t v4 __attribute__((ext_vector_type(4)));
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const v4 *src = reinterpret_cast<const v4 *>(h) + w * 1024 + lane;
+  v4 v[16];
+#pragma unroll
+  for (int r = 0; r < 16; r++) v[r] = src[r * 64];
+  uint32_t ls[16], lt = 0;
+#pragma unroll
+  for (int r = 0; r < 16; r++) {
+    ls[r] = v[r].x + v[r].y + v[r].z + v[r].w;
+    lt += ls[r];
+  }
+  const uint32_t wt = wave_sum(lt);
+  if (lane == 0) tmp[w] = wt;
+  __syncthreads();
+  uint32_t above = 0, total = 0;  // entries in the waves above (higher bins)
+  for (int q = 0; q < 16; q++) {
+    const uint32_t c = tmp[q];
+    total += c;
+    if (q > w) above += c;
+  }
+  if (threadIdx.x == 0) *s_total = total;
+  if (need > 0 && above < need && need <= above + wt) {  // one wave
+    uint32_t cum = above;
+#pragma unroll
+    for (int r = 15; r >= 0; r--) {
+      if (__ballot(ls[r] != 0) == 0) continue;
+      const uint32_t rs = wave_sum(ls[r]);
+      if (cum + rs >= need) {
+        uint32_t x = ls[r];  // -> entries of this row in lanes >= lane
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const uint32_t y = __shfl_down(x, o, 64);
+          if (lane + o < 64) x += y;
+        }
+        uint32_t c2 = cum + x - ls[r];
+        if (c2 < need && need <= cum + x) {
+          const uint32_t e[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
+          bool found = false;
+#pragma unroll
+          for (int c = 3; c >= 0; c--) {
+            if (!found && c2 + e[c] >= need) {
+              *s_bin = (uint32_t)(w * 4096 + r * 256 + lane * 4 + c);
+              *s_above = c2;
+              found = true;
+            }
+            c2 += e[c];
+          }
+        }
+        break;
+      }
+      cum += rs;
+    }
+  }
+  __syncthreads();
+}
+
 // write-through (sc1) stores and L2-served (sc1) loads: the cross-workgroup
 // hand-off of MI355X_MICROARCH.md (no buffer_wbl2 / buffer_inv)
 template <class T>
@@ -3083,18 +3246,21 @@ __global__ void __launch_bounds__(TK_THREADS) k_topk(const uint32_t *skey, const
   __shared__ uint32_t tmp[TK_THREADS / 64];
   __shared__ uint32_t s_bin, s_above, s_total, s_last, s_ba, s_bb;
   __shared__ uint32_t h8[256];
-  __shared__ uint32_t sk[TILE];
+  __shared__ __attribute__((aligned(16))) uint32_t sk[TILE];
   __shared__ uint64_t sd[TILE];
   const uint32_t n = (uint32_t)(ctr->surv_top >> 36);
+  const bool dbg0 = blockIdx.x == 0 && threadIdx.x == 0;
+  if (dbg0) sel->tdbg[0] = __builtin_amdgcn_s_memrealtime();
   // 1. the prefix P of the k-th key
   if (threadIdx.x == 0) {
     s_bin = 0;
     s_above = 0;
   }
   __syncthreads();
-  top_bin<TK_THREADS, SEL_HBINS>(sel->hist, k, tmp, &s_bin, &s_above, &s_total);
+  top_bin_hist(sel->hist, k, tmp, &s_bin, &s_above, &s_total);
   const bool all = s_total <= k;  // every scored key is taken
   const uint32_t P = s_bin;
+  if (dbg0) sel->tdbg[1] = __builtin_amdgcn_s_memrealtime();
   // 2. A: prefix > P (all: every scored key), B: prefix == P.  A block
   // takes TK_E keys a thread per round: flags, one block scan, ONE atomic
   // per list and round, then the writes.
@@ -3136,6 +3302,7 @@ __global__ void __launch_bounds__(TK_THREADS) k_topk(const uint32_t *skey, const
     }
     __syncthreads();  // s_ba / s_bb are rewritten next round
   }
+  if (dbg0) sel->tdbg[2] = __builtin_amdgcn_s_memrealtime();
   // 3. the last block.  Hand-off without L2 write-back (MI355X_MICROARCH.md,
   // hand-offs): every gathered entry was stored write-through (sc1), each
   // wave drains its stores, one lane per block adds to the done counter, and
@@ -3146,8 +3313,55 @@ __global__ void __launch_bounds__(TK_THREADS) k_topk(const uint32_t *skey, const
     s_last = __hip_atomic_fetch_add(&sel->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1 ? 1u : 0u;
   __syncthreads();
   if (!s_last) return;
+  if (threadIdx.x == 0) sel->tdbg[3] = __builtin_amdgcn_s_memrealtime();
   uint32_t na = ld_sc1(&sel->na);
   const uint32_t nb = ld_sc1(&sel->nb);
+  if (threadIdx.x == 0) sel->tdbg[6] = nb;
+  if (na + nb <= (uint32_t)TK_THREADS) {
+    // the usual case: A and B fit one entry a thread -- the answer is the
+    // top k of A u B (everything else ranks below bin P), each entry's
+    // output position its rank among them (docids are distinct)
+    const uint32_t m = na + nb, t = threadIdx.x;
+    uint32_t key = 0;
+    uint64_t doc = ~0ull;
+    if (t < na) {
+      key = ld_sc1(akey + t);
+      doc = ld_sc1(adoc + t);
+    } else if (t < m) {
+      key = ld_sc1(bkey + (t - na));
+      doc = ld_sc1(bdoc + (t - na));
+    }
+    sk[t] = key;  // entries past m: key 0, below every gathered key
+    sd[t] = doc;
+    __syncthreads();
+    if (t < m) {
+      typedef uint32_t v4 __attribute__((ext_vector_type(4)));
+      uint32_t rank = 0;
+      const uint32_t m4 = (m + 3) & ~3u;
+#pragma unroll 4
+      for (uint32_t j = 0; j < m4; j += 4) {
+        const v4 kq = *reinterpret_cast<const v4 *>(sk + j);
+        rank += (kq.x > key ? 1u : 0u) + (kq.y > key ? 1u : 0u) + (kq.z > key ? 1u : 0u) + (kq.w > key ? 1u : 0u);
+        if (kq.x == key) rank += sd[j] < doc ? 1u : 0u;
+        if (kq.y == key) rank += sd[j + 1] < doc ? 1u : 0u;
+        if (kq.z == key) rank += sd[j + 2] < doc ? 1u : 0u;
+        if (kq.w == key) rank += sd[j + 3] < doc ? 1u : 0u;
+      }
+      if (rank < k) {
+        out_key[rank] = key;
+        out_doc[rank] = doc;
+      }
+    }
+    for (uint32_t q = m + t; q < k; q += TK_THREADS) {
+      out_key[q] = 0u;
+      out_doc[q] = ~0ull;
+    }
+    if (threadIdx.x == 0) {
+      sel->tdbg[4] = sel->tdbg[5] = __builtin_amdgcn_s_memrealtime();
+      sel->tdbg[7] = 0;
+    }
+    return;
+  }
   uint32_t nt = 0;  // ties of T, compacted to the front of B
   if (nb) {
     // T inside B: bits 15..8, then 7..0
@@ -3180,6 +3394,7 @@ __global__ void __launch_bounds__(TK_THREADS) k_topk(const uint32_t *skey, const
       nt = block_append(key == T && i < nb, key, doc, bkey, bdoc, nt, tmp);
     }
   }
+  if (threadIdx.x == 0) sel->tdbg[4] = __builtin_amdgcn_s_memrealtime();
   // A (fewer than k entries) plus the ties, merged TILE-k at a time (ties
   // beyond one tile only with huge exact-score ties)
   __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -3204,6 +3419,10 @@ __global__ void __launch_bounds__(TK_THREADS) k_topk(const uint32_t *skey, const
   for (uint32_t t = threadIdx.x; t < k; t += TK_THREADS) {
     out_key[t] = t < kept ? sk[t] : 0u;
     out_doc[t] = t < kept ? sd[t] : ~0ull;
+  }
+  if (threadIdx.x == 0) {
+    sel->tdbg[5] = __builtin_amdgcn_s_memrealtime();
+    sel->tdbg[7] = nt;
   }
 }
 
@@ -3508,7 +3727,7 @@ struct QuerySlot {
   DevBuf tables, chunkcnt, cand, cunit, bits, loc, svslot, svlm, svu, svdoc, svloc, scratch, skey, sel, gath, res;
   DevBuf dir;           // candidate directories, epoch-tagged (never cleared per query)
   DevBuf split, swin;   // docid splits: one piece's list windows; window table
-  DevBuf blk, sflag, sbound, order, tree;  // site clustering: ordered compaction, bounds, TopTree state
+  DevBuf blk, sflag, sbound, rep, tree;  // site clustering: ordered compaction, bounds, replay entries, TopTree state
   DevBuf white, wrej;                       // "&sites=" whitelist: sorted 5-byte values; rejected slots
   DevBuf si;                                // second pass's score info (score_info)
   std::vector<uint64_t> h_white;            // its host copy (the upload's source)
@@ -3554,7 +3773,7 @@ struct QuerySlot {
     if (stream) (void)hipStreamSynchronize(stream);
     DevBuf *bufs[] = {&tables, &chunkcnt, &cand, &cunit, &bits, &loc, &svslot, &svlm, &svu, &svdoc, &svloc,
                       &scratch, &skey, &sel, &gath, &res, &dir, &split, &swin,
-                      &blk, &sflag, &sbound, &order, &tree, &white, &wrej, &si};
+                      &blk, &sflag, &sbound, &rep, &tree, &white, &wrej, &si};
     for (auto *b : bufs) b->release();
     if (h_stage) (void)hipHostFree(h_stage);
     if (h_res) (void)hipHostFree(h_res);
@@ -3801,9 +4020,8 @@ static int enqueue_tree_emit(QuerySlot &q, int32_t dw) {
   Counters *dctr = q.res.as<Counters>();
   hipLaunchKernelGGL(k_reset, dim3(1), dim3(BLOCK), 0, st, reinterpret_cast<uint32_t *>(dctr),
                      (uint32_t)(sizeof(Counters) / 4), reinterpret_cast<uint32_t *>(dctr), 0u);
-  hipLaunchKernelGGL(k_tree_replay, dim3(1), dim3(64), 0, st, dctr, (const uint32_t *)nullptr,
-                     (const uint32_t *)nullptr, (const uint64_t *)nullptr, (const uint8_t *)nullptr,
-                     (const float *)nullptr, q.tree.as<TreeState>(), tree_params(dw, TREE_FINAL, q.int_scores),
+  hipLaunchKernelGGL(k_tree_replay, dim3(1), dim3(64), 0, st, dctr, (const uint4 *)nullptr, q.tree.as<TreeState>(),
+                     tree_params(dw, TREE_FINAL, q.int_scores),
                      q.res.as<uint32_t>(res_keys_off()), q.res.as<uint64_t>(res_docs_off(q.k)));
   HIPCHECK(hipGetLastError());
   HIPCHECK(hipEventRecord(q.ev_done, st));
@@ -4108,7 +4326,7 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   if (clus) {
     rc2 |= q.sflag.ensure(slot_ub);
     rc2 |= q.sbound.ensure(4 * slot_ub);
-    if (P.g0n > 1) rc2 |= q.order.ensure(4 * slot_ub);
+    rc2 |= q.rep.ensure(16 * slot_ub);
     if (!(tree_phase & TREE_FINAL)) rc2 |= q.tree.ensure(sizeof(TreeState));
   }
   if (P.use_white) rc2 |= q.white.ensure(8 * std::max<size_t>(1, q.h_white.size()));
@@ -4252,17 +4470,20 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   if (clus) {
     // site clustering: prefilter bounds, docid order, the TopTree replay
     const uint32_t bgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((slot_ub + BND_WAVES - 1) / BND_WAVES, 4096));
+    // the replay entries: written by k_bound when the survivors are in docid
+    // order (one candidate array), else placed by k_rank
+    const bool ranked = P.g0n > 1;
     hipLaunchKernelGGL(k_bound, dim3(bgrid), dim3(64 * BND_WAVES), 0, st, dpl, dctr, (const uint32_t *)svslot,
-                       (const uint32_t *)svlm, (const Loc *)svloc, q.sbound.as<float>());
-    const uint32_t *order = nullptr;
-    if (P.g0n > 1) {
+                       (const uint32_t *)svlm, (const Loc *)svloc, q.sbound.as<float>(),
+                       (const uint32_t *)q.skey.as<uint32_t>(), (const uint64_t *)svdoc, (const uint8_t *)q.sflag.as<uint8_t>(),
+                       ranked ? nullptr : q.rep.as<uint4>());
+    if (ranked) {
       const uint32_t rgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((slot_ub + 255) / 256, 4096));
       hipLaunchKernelGGL(k_rank, dim3(rgrid), dim3(256), 0, st, dpl, dctr, (const uint32_t *)svslot,
-                         (const uint64_t *)svdoc, q.order.as<uint32_t>());
-      order = q.order.as<uint32_t>();
+                         (const uint64_t *)svdoc, (const uint32_t *)q.skey.as<uint32_t>(),
+                         (const uint8_t *)q.sflag.as<uint8_t>(), (const float *)q.sbound.as<float>(), q.rep.as<uint4>());
     }
-    hipLaunchKernelGGL(k_tree_replay, dim3(1), dim3(64), 0, st, dctr, order, q.skey.as<uint32_t>(),
-                       (const uint64_t *)svdoc, q.sflag.as<uint8_t>(), q.sbound.as<float>(),
+    hipLaunchKernelGGL(k_tree_replay, dim3(1), dim3(64), 0, st, dctr, (const uint4 *)q.rep.as<uint4>(),
                        (tree_phase & TREE_FINAL) ? (TreeState *)q.tree.p : q.tree.as<TreeState>(),
                        tree_params(q.docs_wanted, tree_phase, q.int_scores), q.res.as<uint32_t>(res_keys_off()),
                        q.res.as<uint64_t>(res_docs_off(k)));
@@ -4578,6 +4799,16 @@ static int collect(gbgpu_ctx *ctx, QuerySlot &q, gbgpu_result *out, std::vector<
           std::fclose(f);
         }
   }
+  if (std::getenv("GBGPU_TOPK_DEBUG") && q.sel.p) {
+    unsigned long long td[8];
+    if (hipMemcpy(td, q.sel.as<uint8_t>(offsetof(Select, tdbg)), sizeof td, hipMemcpyDeviceToHost) == hipSuccess)
+      std::fprintf(stderr, "topk us: hist %.2f gather %.2f wait %.2f refine %.2f sort %.2f nb %llu nt %llu\n",
+                   (td[1] - td[0]) / 100.0, (td[2] - td[1]) / 100.0, (td[3] - td[2]) / 100.0, (td[4] - td[3]) / 100.0,
+                   (td[5] - td[4]) / 100.0, td[6], td[7]);
+  }
+  if (std::getenv("GBGPU_TOPK_DEBUG") && q.replayed)
+    std::fprintf(stderr, "replay: adds %u nmax %u tree_n %u us_add %u us_total %u nsurv %u\n", c->pad[0], c->pad[1],
+                 c->tree_n, c->rdbg_t, c->rdbg_total, (uint32_t)(c->surv_top >> 36));
   if (ctx->debug_ext) {
     for (int l = 0; l < MAXL; l++)
       if (c->ext[l].units || c->ext[l].E)
