@@ -314,9 +314,10 @@ def bench_merge(eng, steps, total_keys, with_cpu):
 
 def pmc_traffic(kernel_prefix: str):
     """HBM bytes per launch of a kernel from the newest committed rocprofv3 PMC
-    pass (profiles/r02_*pmc_traffic.json), corrected per MI355X_MICROARCH.md."""
+    pass (profiles/rNN_*pmc_traffic.json, the highest round), corrected per
+    MI355X_MICROARCH.md (scripts/pmc_traffic.py)."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r02_*pmc_traffic.json")))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_*pmc_traffic.json")))
     if not files:
         return None, None
     d = json.load(open(files[-1]))
