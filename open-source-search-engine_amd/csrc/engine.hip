@@ -110,9 +110,11 @@ struct Counters {
 // top-k select state (k_score's histogram, k_topk's gathers)
 struct Select {
   uint32_t hist[SEL_HBINS];  // scored keys per top-16-bit prefix (k_score)
-  uint32_t na, nb;           // k_topk's gathers: A (prefix above P), B (prefix P)
-  uint32_t done;             // k_topk blocks finished (the last one selects)
-  uint32_t pad;
+  // k_topk's gathers and hand-off in ONE word, so a block's round takes both
+  // offsets with one atomic and the last block's done-add returns the final
+  // sizes: bits 0-15 |A| (prefix above P, < k <= MAX_K), 16-47 |B| (prefix
+  // P), 48-63 blocks finished
+  unsigned long long cnt;
   unsigned long long tdbg[8];  // diagnostic (GBGPU_TOPK_DEBUG): k_topk phase clocks (s_memrealtime)
 };
 
@@ -167,16 +169,43 @@ __device__ __forceinline__ void load_chunk(const uint8_t *list, uint32_t u0, uin
   for (int i = threadIdx.x; i < CHUNK_LOAD / 16; i += BLOCK) dst[i] = src[i];
 }
 
-// run-start bitmask of this thread's UPT units (Posdb.h:887-889 classifier)
+// run-start bitmask of this thread's UPT units (Posdb.h:887-889 classifier).
+// The thread's 48 bytes are three 16-B LDS reads (byte reads at a 48-byte
+// thread stride were 4-way bank conflicts, 16 of them per thread); unit q's
+// bytes 0-1 are the low half of word 3(q/2) (q even) or the high half of
+// word 3(q/2)+1 (q odd).
 __device__ __forceinline__ uint32_t thread_starts(const uint8_t *lds, uint32_t u0, uint32_t units) {
+  static_assert(UPT == 8, "three 16-B words per thread");
+  typedef uint32_t v4 __attribute__((ext_vector_type(4)));
+  const v4 *src = reinterpret_cast<const v4 *>(lds + threadIdx.x * UPT * 6);
+  const v4 a = src[0], b = src[1], c = src[2];
+  const uint32_t w[12] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w};
   uint32_t m = 0;
 #pragma unroll
   for (int q = 0; q < UPT; q++) {
-    uint32_t lu = threadIdx.x * UPT + q;
-    const uint8_t *k = lds + lu * 6;
-    if (u0 + lu < units && (k[1] & 0x02) && !(k[0] & 0x04)) m |= 1u << q;
+    const uint32_t h = (q & 1) ? (w[3 * (q >> 1) + 1] >> 16) : (w[3 * (q >> 1)] & 0xffffu);
+    const uint32_t lu = threadIdx.x * UPT + q;
+    if (u0 + lu < units && (h & 0x0200u) && !(h & 0x04u)) m |= 1u << q;
   }
   return m;
+}
+// the docid of the 12-byte key at LDS unit lu (bytes 7-11; Posdb.h:295) from
+// two aligned reads: lu even -> the words at 6lu+4 and 6lu+8, lu odd -> the
+// word at 6lu+6 and the half-word at 6lu+10
+__device__ __forceinline__ uint64_t lds_unit_docid(const uint8_t *lds, uint32_t lu) {
+  const uint32_t b = lu * 6;
+  uint64_t v;  // bytes 6..11 of the key in the low 48 bits
+  if (lu & 1) {
+    const uint32_t lo = *reinterpret_cast<const uint32_t *>(lds + b + 6);
+    const uint32_t hi = *reinterpret_cast<const uint16_t *>(lds + b + 10);
+    v = (uint64_t)lo | ((uint64_t)hi << 32);
+  } else {
+    const uint32_t lo = *reinterpret_cast<const uint32_t *>(lds + b + 4);
+    const uint32_t hi = *reinterpret_cast<const uint32_t *>(lds + b + 8);
+    v = ((uint64_t)lo >> 16) | ((uint64_t)hi << 16);
+  }
+  // k[7..11] = v bytes 1..5; unit_docid: ((k11 << 32) | k7..k10) >> 2
+  return ((v >> 8) & 0xffffffffffull) >> 2;
 }
 
 template <int NT = BLOCK>
@@ -359,13 +388,13 @@ __global__ void __launch_bounds__(BLOCK) k_write_runs(const DevPlan *__restrict_
     const uint32_t lu = rs_unit[o2];
     const uint32_t p2 = pos0 + o2;
     const uint64_t slot = base + p2;
-    const uint64_t d = unit_docid(lds + lu * 6);
+    const uint64_t d = lds_unit_docid(lds, lu);
     cand[slot] = d;
     cunit[slot] = c.u0 + lu;
     // directory: the first candidate of each bucket within this chunk (a
     // bucket straddling two chunks gets two writers; either names it)
     const uint64_t bkt = (d - dmin) >> sh;
-    if (o2 == 0 || ((unit_docid(lds + rs_unit[o2 - 1] * 6) - dmin) >> sh) != bkt) dir_a[bkt] = tag | p2;
+    if (o2 == 0 || ((lds_unit_docid(lds, rs_unit[o2 - 1]) - dmin) >> sh) != bkt) dir_a[bkt] = tag | p2;
     bool rej = false;
     if (pl->use_white) {
       // Posdb.cpp:5294: the 5 bytes at minRecPtr+7 (the run head's docid
@@ -1697,46 +1726,132 @@ __device__ __forceinline__ void score_survivor(const DevPlan *__restrict__ pl, c
   uint64_t sortby_raw = 0;  // gbsortby: the unmerged first key (see below)
   bool sortby_is_raw = false;
   uint32_t nrec = 0;
+  // a group's runs: cursor, end, flags (m_bigramFlags of the shrunk sublist
+  // index: lists shrunk to empty are not sublists any more)
+  struct GrpRuns {
+    uint32_t ce[NS], c0[NS];
+    uint8_t cfl[NS];
+    bool live[NS];
+    gu8 *src[NS], *xsrc[NS];
+  };
+  auto grp_runs = [&](int j, GrpRuns &g) {
+    const int gns = pl->gnsub[j];
+    int newIdx = 0;
+#pragma unroll
+    for (int x = 0; x < NS; x++) {
+      g.live[x] = false;
+      g.ce[x] = 0;
+      g.cfl[x] = 0;
+      g.src[x] = g.xsrc[x] = nullptr;
+      g.c0[x] = 0;
+      if (x < gns) {
+        const int lid = pl->gsub[j][x];
+        if (anys >> lid & 1) {
+          g.cfl[x] = pl->gsubflags[j][newIdx];
+          newIdx++;
+          // kill: sublists the second pass's lookup misses (k_scoreinfo)
+          if ((lm >> lid & 1) && !(kill && (kill[j] >> x & 1))) {
+            const SubRun sr = sub_run_at(pl, ctr, svloc[lid], lid, j, x, s);
+            g.src[x] = sr.own;
+            g.xsrc[x] = sr.ext;
+            g.c0[x] = sr.len0;
+            g.ce[x] = sr.len;
+            g.live[x] = true;
+          }
+        }
+      }
+    }
+  };
+  // Two groups (the config-2 variant): both groups' run locations, then both
+  // groups' units staged in the lane's LDS column together, one round trip
+  // each, when 2 (U0 + U1) <= cap -- the records, at most one per unit, stay
+  // below the staged units.  Otherwise each group stages its own (below).
+  constexpr bool PRE = NQ <= 2 && std::is_same<RP, LdsRecs>::value && !REC::on;
+  GrpRuns pre[PRE ? NQ : 1];
+  int preR[PRE ? NQ : 1];
+  bool pre_staged = false;
+  if constexpr (PRE) {
+    uint32_t Ut = 0, cm = 0;
+    uint32_t Uj[NQ];
+#pragma unroll
+    for (int j = 0; j < NQ; j++) {
+      Uj[j] = 0;
+      if (j < ng && !(pl->gflags0[j] & BF_NEGATIVE)) {
+        grp_runs(j, pre[j]);
+#pragma unroll
+        for (int x = 0; x < NS; x++)
+          if (pre[j].live[x]) {
+            Uj[j] += pre[j].ce[x];
+            cm = pre[j].ce[x] > cm ? pre[j].ce[x] : cm;
+          }
+      } else {
+#pragma unroll
+        for (int x = 0; x < NS; x++) pre[j].live[x] = false;
+      }
+      Ut += Uj[j];
+    }
+    if (2 * Ut <= (uint32_t)rec.cap && !(diag & 0x200)) {
+      pre_staged = true;
+      int at = rec.cap - (int)Ut;
+#pragma unroll
+      for (int j = 0; j < NQ; j++) {
+        preR[j] = at;
+        at += (int)Uj[j];
+      }
+      constexpr int SKP = 4;
+      for (uint32_t b = 0; b < cm; b += SKP) {
+        uint64_t v[NQ][NS][SKP];
+#pragma unroll
+        for (int j = 0; j < NQ; j++)
+#pragma unroll
+          for (int x = 0; x < NS; x++)
+#pragma unroll
+            for (int q = 0; q < SKP; q++) {
+              const uint32_t c = b + q;
+              const GrpRuns &g = pre[j];
+              v[j][x][q] = (g.live[x] && c < g.ce[x])
+                               ? load6(c < g.c0[x] ? g.src[x] + (size_t)c * 6 : g.xsrc[x] + (size_t)(c - g.c0[x]) * 6)
+                               : 0;
+            }
+#pragma unroll
+        for (int j = 0; j < NQ; j++) {
+          uint32_t off = 0;
+#pragma unroll
+          for (int x = 0; x < NS; x++) {
+            const GrpRuns &g = pre[j];
+#pragma unroll
+            for (int q = 0; q < SKP; q++)
+              if (g.live[x] && b + q < g.ce[x]) rec.put(preR[j] + (int)(off + b + q), v[j][x][q]);
+            off += g.live[x] ? g.ce[x] : 0;
+          }
+        }
+      }
+    }
+  }
 #pragma unroll
   for (int j = 0; j < NQ; j++) {
     dv.beg[j] = dv.end[j] = (int)nrec;
     if (j >= ng) continue;
     const uint8_t gf0 = pl->gflags0[j];
     if (gf0 & BF_NEGATIVE) continue;
-    const int gns = pl->gnsub[j];
     uint64_t ta = 0;
     if (stamp) ta = __builtin_amdgcn_s_memtime();
-    // this group's runs: cursor, end, flags (m_bigramFlags of the shrunk
-    // sublist index: lists shrunk to empty are not sublists any more)
+    GrpRuns gr;
+    if constexpr (PRE) gr = pre[j];
+    else grp_runs(j, gr);
     uint32_t cu[NS], ce[NS], c0[NS];
     uint8_t cfl[NS];
     bool live[NS];
     gu8 *src[NS], *xsrc[NS];
-    int newIdx = 0;
 #pragma unroll
     for (int x = 0; x < NS; x++) {
-      live[x] = false;
-      cu[x] = ce[x] = 0;
-      cfl[x] = 0;
-      src[x] = xsrc[x] = nullptr;
-      c0[x] = 0;
-      if (x < gns) {
-        const int lid = pl->gsub[j][x];
-        if (anys >> lid & 1) {
-          cfl[x] = pl->gsubflags[j][newIdx];
-          newIdx++;
-          // kill: sublists the second pass's lookup misses (k_scoreinfo)
-          if ((lm >> lid & 1) && !(kill && (kill[j] >> x & 1))) {
-            const SubRun sr = sub_run_at(pl, ctr, svloc[lid], lid, j, x, s);
-            src[x] = sr.own;
-            xsrc[x] = sr.ext;
-            c0[x] = sr.len0;
-            cu[x] = 0;
-            ce[x] = sr.len;
-            live[x] = true;
-          }
-        }
-      }
+      cu[x] = 0;
+      ce[x] = gr.ce[x];
+      c0[x] = gr.c0[x];
+      cfl[x] = gr.cfl[x];
+      live[x] = gr.live[x];
+      src[x] = gr.src[x];
+      xsrc[x] = gr.xsrc[x];
     }
     // Stage the group's run units in the lane's LDS column at its tail
     // [cap - U, cap), every sublist's next SK units in flight together: the
@@ -1759,8 +1874,14 @@ __device__ __forceinline__ void score_survivor(const DevPlan *__restrict__ pl, c
     }
     bool staged = false;
     int R = 0;
+    if constexpr (PRE) {
+      if (pre_staged) {
+        staged = true;
+        R = preR[j];
+      }
+    }
     if constexpr (std::is_same<RP, LdsRecs>::value) {
-      if (nrec + 2 * U <= (uint32_t)rec.cap && !(diag & 0x200)) {
+      if (!staged && nrec + 2 * U <= (uint32_t)rec.cap && !(diag & 0x200)) {
         staged = true;
         R = rec.cap - (int)U;
         for (uint32_t b = 0; b < cmax; b += SK) {
@@ -3283,8 +3404,12 @@ __global__ void __launch_bounds__(TK_THREADS) k_topk(const uint32_t *skey, const
     uint32_t tot;
     const uint32_t ex = block_exclusive_scan<TK_THREADS>(cnt, tmp, &tot);
     if (threadIdx.x == 0) {
-      s_ba = (tot & 0xffff) ? atomicAdd(&sel->na, tot & 0xffff) : 0u;
-      s_bb = (tot >> 16) ? atomicAdd(&sel->nb, tot >> 16) : 0u;
+      unsigned long long old = 0;
+      if (tot)
+        old = __hip_atomic_fetch_add(&sel->cnt, (unsigned long long)(tot & 0xffff) | ((unsigned long long)(tot >> 16) << 16),
+                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_ba = (uint32_t)(old & 0xffff);
+      s_bb = (uint32_t)(old >> 16);
     }
     __syncthreads();
     uint32_t oa = s_ba + (ex & 0xffff), ob = s_bb + (ex >> 16);
@@ -3309,13 +3434,20 @@ __global__ void __launch_bounds__(TK_THREADS) k_topk(const uint32_t *skey, const
   // the block whose add came last reads everything with sc1 loads.
   __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0)
-    s_last = __hip_atomic_fetch_add(&sel->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1 ? 1u : 0u;
+  // (the same thread made this block's gather adds on the same word before,
+  // so the last done-add returns every block's totals)
+  __shared__ unsigned long long s_fin;
+  if (threadIdx.x == 0) {
+    const unsigned long long old =
+        __hip_atomic_fetch_add(&sel->cnt, 1ull << 48, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = (old >> 48) == gridDim.x - 1 ? 1u : 0u;
+    s_fin = old;
+  }
   __syncthreads();
   if (!s_last) return;
   if (threadIdx.x == 0) sel->tdbg[3] = __builtin_amdgcn_s_memrealtime();
-  uint32_t na = ld_sc1(&sel->na);
-  const uint32_t nb = ld_sc1(&sel->nb);
+  uint32_t na = (uint32_t)(s_fin & 0xffff);
+  const uint32_t nb = (uint32_t)((s_fin >> 16) & 0xffffffffu);
   if (threadIdx.x == 0) sel->tdbg[6] = nb;
   if (na + nb <= (uint32_t)TK_THREADS) {
     // the usual case: A and B fit one entry a thread -- the answer is the
