@@ -130,6 +130,8 @@ struct G0Chunk {
 struct ProbeWork {
   uint32_t list;
   uint32_t u0, u1;
+  uint32_t has_dfirst;  // dfirst is known (the list's granule table, ListEntry::gfirst)
+  uint64_t dfirst;      // docid of the first run start at or after u0 (~0: none in the list)
 };
 
 #define HIPCHECK(x)                                                        \
@@ -563,7 +565,7 @@ __device__ __forceinline__ void wave_lds_sync() {
 // Wave-private probe state: the chunk's run starts and the matches found so
 // far (buffered so the scan loop issues no store or atomic: those would share
 // the in-order vmcnt counter with the chunk prefetches and force full drains).
-constexpr int MBUF = 256;
+constexpr int MBUF = 192;  // with the candidate ring: 4 probe blocks per CU fit in LDS
 struct ProbeLds {
   uint64_t doc[WMAX_RUNS];
   uint32_t mslot[MBUF], mu[MBUF], mlen[MBUF];
@@ -883,6 +885,219 @@ __device__ void probe_by_cand(const DevPlan *__restrict__ pl, const ProbeWork &w
   mbuf_flush(S, nbuf, po, lane);
 }
 
+// Dense list, one or two candidate arrays: the same search as probe_by_cand,
+// with the candidates streamed through a per-array LDS ring instead of
+// register windows.  Each of the two static chunk roles (A, B) owns a register
+// block of 64 candidates per array: a step writes its block -- loaded two
+// steps earlier, so the wait for it is the wait for its chunk -- into the
+// ring and loads the next 64 after the ones already issued, as long as the
+// ring has room (entries below the consumption point `lo` are free).  The
+// step's windows are then LDS reads, and no candidate load sits on the
+// step's dependency chain (a step waiting on a load issued one step before
+// it was the kernel's stall: HBM latency per chunk).  The start needs no
+// search either: the host knows the span's first run docid (ListEntry::
+// gfirst), and the directory entry of the nearest non-empty bucket below it
+// is a candidate index at or below the lower bound -- the few candidates
+// between are consumed against the runs and match none (their docids are
+// below the span's first run).
+constexpr int PRING = 256;  // candidates per array in the LDS ring (power of two)
+struct ProbeRing {
+  uint64_t c[2][PRING];
+};
+
+// first candidate index of array k at or below lower_bound(key) and close to
+// it: the directory entry of the last non-empty bucket of the 64 below key's
+__device__ uint32_t wave_start_dir(const DevPlan *__restrict__ pl, int k, const uint64_t *ck, uint32_t n, const uint64_t *dir,
+                                   uint64_t key, int lane) {
+  const uint64_t dmin = pl->g0dmin[k];
+  if (n == 0 || key <= dmin) return 0;
+  if (key > pl->g0dmax[k]) return n;
+  const uint32_t sh = pl->g0sh[k];
+  const uint64_t h = (key - dmin) >> sh;  // >= 0; buckets below h hold docids < key
+  const int64_t b = (int64_t)h - 64 + lane;
+  const uint64_t e = b >= 0 ? dir[pl->g0dir[k] + (uint64_t)b] : 0;
+  const uint64_t v = __ballot((uint32_t)(e >> 32) == pl->epoch);
+  if (v) {
+    const int f = 63 - __builtin_clzll((unsigned long long)v);
+    return (uint32_t)__shfl(e, f, 64);
+  }
+  if (h < 64) return 0;  // every bucket below key's is empty
+  return wave_lower_bound(ck, n, key, lane);
+}
+
+template <int MODE, int G0>
+__device__ void probe_by_cand_ring(const DevPlan *__restrict__ pl, const ProbeWork &w, const DevList &L, const uint64_t *cand,
+                                   const Counters *ctr, const uint64_t *dir, ProbeLds &S, ProbeRing &R, const ProbeOut &po,
+                                   int lane) {
+  static_assert(G0 >= 1 && G0 <= 2, "two ring arrays");
+  const uint8_t *lp = L.p;
+  const uint32_t last_u0 = w.u0 + ((w.u1 - w.u0 - 1) / WCH_UNITS) * WCH_UNITS;
+  WChunk cA, cB;
+  // the first two chunks do not depend on the candidates: in flight at once
+  wchunk_fetch(lp, w.u0, lane, cA);
+  wchunk_fetch(lp, min(w.u0 + WCH_UNITS, last_u0), lane, cB);
+  constexpr bool FULL = MODE == 0 || MODE >= 5;
+  uint32_t nk[G0], lo[G0], iss[G0], wr[G0], wa[G0], wb[G0];
+  uint64_t base[G0], KA[G0], KB[G0];
+  bool va[G0], vb[G0];
+  const uint64_t dfirst = !FULL ? 0 : w.has_dfirst ? w.dfirst : first_run_doc(L, w.u0, w.u1, lane);
+#pragma unroll
+  for (int k = 0; k < G0; k++) {
+    nk[k] = ctr->g0count[k];
+    base[k] = pl->g0base[k];
+    lo[k] = FULL ? wave_start_dir(pl, k, cand + base[k], nk[k], dir, dfirst, lane) : 0;
+    wr[k] = lo[k];
+  }
+  auto kload = [&](int k, uint32_t i) -> uint64_t {  // candidate i (clamped: a block past the end is never written)
+    return cand[base[k] + min(i, max(nk[k], 1u) - 1)];
+  };
+  // the first two blocks, into the two roles
+#pragma unroll
+  for (int k = 0; k < G0; k++) {
+    wa[k] = lo[k];
+    KA[k] = kload(k, lo[k] + lane);
+    va[k] = lo[k] < nk[k];
+    wb[k] = lo[k] + 64;
+    KB[k] = kload(k, lo[k] + 64 + lane);
+    vb[k] = lo[k] + 64 < nk[k];
+    iss[k] = lo[k] + 128;
+  }
+  uint32_t nbuf = 0;
+  uint64_t pend_slot = ~0ull;
+  uint32_t pend_u = 0;
+  // the window of array k: its next 64 candidates (LDS; a direct read only
+  // when the ring has fallen behind)
+  auto window = [&](int k) -> uint64_t {
+    const uint32_t i = lo[k] + lane;
+    if (i >= nk[k]) return ~0ull;
+    if (i < wr[k]) return R.c[k][i & (PRING - 1)];
+    return cand[base[k] + i];
+  };
+  auto search = [&](uint64_t d, uint32_t nrun) -> uint32_t {
+    uint32_t a = 0;
+#pragma unroll
+    for (uint32_t st = WMAX_RUNS; st > 0; st >>= 1) {
+      const uint32_t t = a + st;
+      const uint64_t v = S.doc[min(t, max(nrun, 1u)) - 1];
+      if (t <= nrun && v < d) a = t;
+    }
+    return a;
+  };
+  auto step = [&](const WChunk &c, uint32_t u0, uint64_t(&K)[G0], uint32_t(&wpos)[G0], bool(&vk)[G0]) {
+    if (MODE == 2) {
+      if (c.v[0].x == 0x557713eeu && c.v[1].y == 7u && c.v[2].z == 3u) po.bits[0] = 1;
+      return;
+    }
+    // this role's block (loaded two steps ago) into the ring, then the next
+#pragma unroll
+    for (int k = 0; k < G0; k++) {
+      if (vk[k]) {
+        R.c[k][(wpos[k] + lane) & (PRING - 1)] = K[k];
+        wr[k] = min(wpos[k] + 64, nk[k]);
+      }
+      vk[k] = iss[k] < nk[k] && iss[k] + 64 <= lo[k] + PRING;
+      wpos[k] = iss[k];
+      K[k] = kload(k, iss[k] + lane);
+      if (vk[k]) iss[k] += 64;
+    }
+    const uint32_t nrun = chunk_runs(c, u0, w.u1, lane, S);
+    if (nrun && pend_slot != ~0ull) {
+      if (nbuf + 1 > MBUF) mbuf_flush(S, nbuf, po, lane);
+      mbuf_push(S, nbuf, lane == 0, (uint32_t)pend_slot, pend_u, u0 + S.unit[0] - pend_u, lane);
+      pend_slot = ~0ull;
+    }
+    if (MODE == 1) {
+      if (nrun && S.doc[0] == 0x123456789ull) po.bits[0] = 1;
+      wave_lds_sync();
+      return;
+    }
+    if (nrun) {
+      const uint64_t dmax = S.doc[nrun - 1];
+      uint64_t dk[G0];
+      uint32_t pa[G0];
+#pragma unroll
+      for (int k = 0; k < G0; k++) dk[k] = window(k);
+      // every array's search at once (their LDS round trips overlap)
+#pragma unroll
+      for (int k = 0; k < G0; k++) pa[k] = 0;
+#pragma unroll
+      for (uint32_t st = WMAX_RUNS; st > 0 && MODE != 6; st >>= 1) {
+#pragma unroll
+        for (int k = 0; k < G0; k++) {
+          const uint32_t t = pa[k] + st;
+          const uint64_t v = S.doc[min(t, nrun) - 1];
+          if (t <= nrun && v < dk[k]) pa[k] = t;
+        }
+      }
+      if (MODE == 7) {  // diagnostic: windows searched and consumed, no settle
+#pragma unroll
+        for (int k = 0; k < G0; k++) {
+          const bool in = dk[k] <= dmax;
+          lo[k] += (uint32_t)__popcll(__ballot(in));
+          if (pa[k] == 0x7fffffffu) po.bits[1] = 1;
+        }
+        wave_lds_sync();
+        return;
+      }
+#pragma unroll
+      for (int k = 0; k < G0; k++) {
+        // the 64 candidates from lo against the runs (claims array by array,
+        // in order: a docid goes to the first array holding it)
+        auto settle = [&](uint64_t d, uint32_t a) -> uint32_t {
+          const bool in = d <= dmax;
+          bool hit = false, last = false;
+          uint32_t u = 0, len = 0;
+          if (in && a < nrun && S.doc[a] == d && !S.claim[a]) {
+            S.claim[a] = 1;
+            u = u0 + S.unit[a];
+            if (a + 1 < nrun) {
+              hit = true;
+              len = S.unit[a + 1] - S.unit[a];
+            } else {
+              last = true;  // ends at the next chunk's first run start
+            }
+          }
+          if (nbuf + 64 > MBUF) mbuf_flush(S, nbuf, po, lane);
+          mbuf_push(S, nbuf, hit, (uint32_t)(base[k] + lo[k] + lane), u, len, lane);
+          const uint64_t pm = __ballot(last);
+          if (pm) {
+            pend_slot = base[k] + lo[k] + (uint32_t)(__ffsll((unsigned long long)pm) - 1);
+            pend_u = u0 + S.unit[nrun - 1];
+          }
+          const uint32_t nin = (uint32_t)__popcll(__ballot(in));
+          lo[k] += nin;
+          return nin;
+        };
+        if (settle(dk[k], pa[k]) == 64u) {
+          // a chunk meeting more than 64 candidates: further windows
+          for (;;) {
+            const uint64_t d = window(k);
+            if (settle(d, search(d, nrun)) < 64u) break;
+          }
+        }
+      }
+    }
+    wave_lds_sync();  // the next chunk rewrites the run list; ring writes land
+  };
+  const uint32_t nch = (w.u1 - w.u0 + WCH_UNITS - 1) / WCH_UNITS;
+  uint32_t u0 = w.u0;
+  for (uint32_t it = 0; it + 2 <= nch; it += 2, u0 += 2 * WCH_UNITS) {
+    step(cA, u0, KA, wa, va);
+    wchunk_fetch(lp, min(u0 + 2 * WCH_UNITS, last_u0), lane, cA);
+    __builtin_amdgcn_sched_barrier(0);
+    step(cB, u0 + WCH_UNITS, KB, wb, vb);
+    wchunk_fetch(lp, min(u0 + 3 * WCH_UNITS, last_u0), lane, cB);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if (nch & 1) step(cA, u0, KA, wa, va);
+  if (pend_slot != ~0ull) {
+    const uint32_t len = lane == 0 ? run_end(L, pend_u + 2) - pend_u : 0;
+    if (nbuf + 1 > MBUF) mbuf_flush(S, nbuf, po, lane);
+    mbuf_push(S, nbuf, lane == 0, (uint32_t)pend_slot, pend_u, len, lane);
+  }
+  mbuf_flush(S, nbuf, po, lane);
+}
+
 // Sparse list: each run start looks its docid up in the arrays, in order;
 // the first array holding it takes the run.
 template <int G0>
@@ -966,6 +1181,7 @@ __global__ void __launch_bounds__(64 * PW) k_probe(const DevPlan *__restrict__ p
                                                    const uint64_t *cand, uint32_t *bits, uint32_t nwords, Loc *loc,
                                                    const Counters *ctr, const uint64_t *dir) {
   __shared__ ProbeLds s_lds[PW];
+  __shared__ ProbeRing s_ring[G0 <= 2 && MODE != 3 ? PW : 1];
   // the wave's index is uniform over the wave: said so, every value derived
   // from it (the work item, the list, the loop bounds) lives in SGPRs and the
   // chunk loop is a uniform one (no exec-mask loop, exact vmcnt waits)
@@ -983,7 +1199,10 @@ __global__ void __launch_bounds__(64 * PW) k_probe(const DevPlan *__restrict__ p
   if (L.probe == PROBE_BY_RUN) {
     if (MODE == 0) probe_by_run<G0>(pl, w, L, cand, ctr, dir, s_lds[wid], po, lane);
   } else {
-    probe_by_cand<MODE == 3 ? 0 : MODE, G0>(pl, w, L, cand, ctr, dir, s_lds[wid], po, lane);
+    if constexpr (G0 <= 2 && MODE != 3)
+      probe_by_cand_ring<MODE, G0>(pl, w, L, cand, ctr, dir, s_lds[wid], s_ring[wid], po, lane);
+    else
+      probe_by_cand<MODE == 3 ? 0 : MODE, G0>(pl, w, L, cand, ctr, dir, s_lds[wid], po, lane);
   }
 }
 
@@ -3199,6 +3418,9 @@ __global__ void __launch_bounds__(64) k_tree_replay(Counters *ctr, const uint4 *
 //      merges the ties in LDS.
 constexpr int TK_THREADS = 1024;
 constexpr int TK_BLOCKS = 32;
+// Select::cnt packs |A| (16 bits: < k <= MAX_K), |B| (32 bits) and the
+// blocks finished (16 bits) into one 64-bit word
+static_assert(MAX_K < 65536 && TK_BLOCKS < 65536, "Select::cnt fields");
 constexpr int TK_E = 16;  // keys per thread and gather round
 
 // bitonic sort of sk/sd[0, n) in LDS, n rounded up to a power of two with
@@ -3604,20 +3826,13 @@ __global__ void k_xpack(const Counters *ctr, const uint32_t *keys, const uint64_
 }
 
 // one wave: Msg3a::mergeLists' loop over the shards' replies (Msg3a.cpp:
-// 1315-1467).  Lane r < nranks holds shard r's head; the wave's reduction
-// picks what the reference's scan over j picks -- the highest double score,
-// on equal scores the lower docid, on equal docids the lower shard (a later
-// shard replaces maxj only if strictly better) -- so a reply need not be
-// sorted.  A docid already merged is passed over (htable, Msg3a.cpp:1381-
+// 1315-1467).  Lane r < nranks holds shard r's head; every lane then walks
+// the heads in shard order exactly as the reference's scan over j does (a
+// later head replaces maxj if its score is greater, or if it is not less and
+// not greater -- equal, or NaN on either side -- and its docid is lower), so
+// the pick is the reference's even where the comparison is not a total
+// order.  A docid already merged is passed over (htable, Msg3a.cpp:1381-
 // 1385), and the loop stops at k entries.
-__device__ __forceinline__ bool xhead_better(double s1, uint64_t d1, int l1, double s2, uint64_t d2, int l2) {
-  if (l2 >= 64) return l1 < 64;
-  if (l1 >= 64) return false;
-  if (s1 > s2) return true;
-  if (s1 < s2) return false;
-  if (d1 != d2) return d1 < d2;
-  return l1 < l2;
-}
 __global__ void __launch_bounds__(64) k_xmerge(const uint8_t *recv, int nranks, uint32_t k, size_t stride,
                                                uint8_t *out) {
   const int lane = threadIdx.x;
@@ -3639,19 +3854,22 @@ __global__ void __launch_bounds__(64) k_xmerge(const uint8_t *recv, int nranks, 
   uint32_t taken = 0;
   while (taken < k) {
     const bool has = lane < nranks && cur < n;
-    double bs = has ? rr[cur].score : 0.0;
-    uint64_t bd = has ? rr[cur].docid : ~0ull;
-    int bl = has ? lane : 64;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      const double os = __shfl_xor(bs, off, 64);
-      const uint64_t od = __shfl_xor(bd, off, 64);
-      const int ol = __shfl_xor(bl, off, 64);
-      if (xhead_better(os, od, ol, bs, bd, bl)) {
-        bs = os;
-        bd = od;
-        bl = ol;
+    const double hs = has ? rr[cur].score : 0.0;
+    const uint64_t hd = has ? rr[cur].docid : ~0ull;
+    const uint64_t hm = __ballot(has);
+    int bl = 64;
+    double bs = 0.0;
+    uint64_t bd = 0;
+    for (int j = 0; j < nranks; j++) {  // Msg3a.cpp:1323-1334, uniform over the wave
+      const double sj = __shfl(hs, j, 64);
+      const uint64_t dj = __shfl(hd, j, 64);
+      if (!((hm >> j) & 1)) continue;
+      if (bl == 64) {
+        bl = j, bs = sj, bd = dj;
+        continue;
       }
+      if (sj < bs) continue;
+      if (sj > bs || dj < bd) bl = j, bs = sj, bd = dj;
     }
     if (bl == 64) break;  // every shard exhausted
     if (lane == bl) cur++;
@@ -3807,6 +4025,9 @@ struct ListEntry {
   int64_t size = 0;   // original bytes (18-byte first key)
   uint32_t units = 0; // swapped units
   uint64_t dmin = 0, dmax = 0;  // docid of the first and of the last run
+  // first run docid at or after each WCH_UNITS-unit granule (k_gfirst; host
+  // copy, resident lists only): the probe spans' start docids
+  std::shared_ptr<const std::vector<uint64_t>> gfirst;
   bool live = false;
 };
 
@@ -3835,6 +4056,22 @@ __global__ void k_validate(const uint8_t *list, uint32_t units, uint32_t *bad) {
     }
   }
   if (__ballot(b) && (threadIdx.x & 63) == 0) atomicOr(bad, 1u);
+}
+
+// Upload-time granule table (an RdbMap-like index at 3 KiB resolution): for
+// every WCH_UNITS-unit granule of a swapped list, the docid of the first run
+// start at or after its first unit (~0: none).  One wave per granule.  The
+// host keeps a copy and gives each probe span its first run docid, so
+// k_probe starts without a dependent walk of the list.
+__global__ void __launch_bounds__(256) k_gfirst(const uint8_t *list, uint32_t units, uint32_t ngran, uint64_t *out) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t g = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (g >= ngran) return;
+  DevList L;
+  L.p = list;
+  L.units = units;
+  const uint64_t d = first_run_doc(L, g * (uint32_t)WCH_UNITS, units, lane);
+  if (lane == 0) out[g] = d;
 }
 
 // docid of the key starting at p (Posdb.h:295)
@@ -4038,8 +4275,28 @@ static int upload_list(gbgpu_ctx *ctx, const uint8_t *bytes, int64_t size, int32
     if (rc) return rc;
     HIPCHECK(hipMemcpyAsync(ctx->h_flag, ctx->d_flag, 4, hipMemcpyDeviceToHost, ctx->upload_stream));
   }
-  HIPCHECK(hipStreamSynchronize(ctx->upload_stream));
+  std::vector<uint64_t> gf;
+  DevBuf dgf;
+  if (size) {
+    const uint32_t ngran = (e.units + WCH_UNITS - 1) / WCH_UNITS;
+    gf.resize(ngran);
+    if (dgf.ensure(8 * (size_t)ngran)) return ENOMEM;
+    hipLaunchKernelGGL(k_gfirst, dim3((ngran + 3) / 4), dim3(256), 0, ctx->upload_stream, e.d, e.units, ngran,
+                       dgf.as<uint64_t>());
+    hipError_t le = hipGetLastError();
+    if (le == hipSuccess)
+      le = hipMemcpyAsync(gf.data(), dgf.p, 8 * (size_t)ngran, hipMemcpyDeviceToHost, ctx->upload_stream);
+    if (le != hipSuccess) {
+      (void)hipStreamSynchronize(ctx->upload_stream);
+      dgf.release();
+      HIPCHECK(le);
+    }
+  }
+  const hipError_t se = hipStreamSynchronize(ctx->upload_stream);
+  dgf.release();
+  HIPCHECK(se);
   if (size && *ctx->h_flag) return GBGPU_ECORRUPT;  // e.mem frees the copy
+  if (size) e.gfirst = std::make_shared<const std::vector<uint64_t>>(std::move(gf));
   if (size) {
     // the list's docid range (directory sizing): first key, last run start
     e.dmin = e.dmax = host_docid(bytes);
@@ -4267,6 +4524,7 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   }
   int dense[1024];
   uint64_t list_dmin[MAXL], list_dmax[MAXL];
+  const ListEntry *lent[MAXL] = {};
   for (int i = 0; i < nterms; i++) dense[i] = -1;
   auto dense_id = [&](int term) -> int {
     if (dense[term] >= 0) return dense[term];
@@ -4274,6 +4532,7 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
     int id = P.nlists++;
     dense[term] = id;
     const ListEntry &e = ents[term];
+    lent[id] = &e;
     P.lists[id].p = e.d;
     P.lists[id].pm = e.pm;
     P.lists[id].units = e.units;
@@ -4411,7 +4670,15 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
     // a run-driven chunk costs a few dependent lookups: one chunk per wave
     const uint32_t rspan = ctx->probe_runspan > 0 ? (uint32_t)ctx->probe_runspan : 1u;
     const uint32_t span = WCH_UNITS * (P.lists[id].probe == PROBE_BY_RUN ? rspan : S);
-    for (uint32_t u = 0; u < units; u += span) q.pw.push_back({(uint32_t)id, u, std::min(units, u + span)});
+    const std::vector<uint64_t> *gf = lent[id]->gfirst.get();
+    for (uint32_t u = 0; u < units; u += span) {
+      ProbeWork pw{(uint32_t)id, u, std::min(units, u + span), 0u, ~0ull};
+      if (gf && u / WCH_UNITS < gf->size()) {
+        pw.has_dfirst = 1;
+        pw.dfirst = (*gf)[u / WCH_UNITS];
+      }
+      q.pw.push_back(pw);
+    }
   }
   q.scan_bytes = scan;
   q.g0_bytes = 0;
@@ -4521,7 +4788,11 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
                      q.cunit.as<uint32_t>(), dctr, ng0, q.dir.as<uint64_t>());
   if (ctx->profiling) HIPCHECK(hipEventRecord(q.ev[1], st));
   if (!q.pw.empty()) {
-    auto kp = ctx->probe_mode == 5   ? k_probe<5, 2>
+    auto kp = ctx->probe_mode == 9   ? k_probe<2, 2>
+              : ctx->probe_mode == 8 ? k_probe<1, 2>
+              : ctx->probe_mode == 7 ? k_probe<7, 2>
+              : ctx->probe_mode == 6 ? k_probe<6, 2>
+              : ctx->probe_mode == 5 ? k_probe<5, 2>
               : ctx->probe_mode == 3 ? k_probe<3, MAXG0>
               : ctx->probe_mode == 2 ? k_probe<2, MAXG0>
               : ctx->probe_mode == 1 ? k_probe<1, MAXG0>
@@ -5590,6 +5861,19 @@ int gbgpu_comm_init(gbgpu_ctx *ctx, int nranks, int rank, const uint8_t *id) {
   }
   ctx->nranks = nranks;
   ctx->rank = rank;
+  // the exchange buffers at their largest (XMAX entries), so no call can fail
+  // to allocate once admitted: a failure there would skip the collective
+  const size_t stride = align256(sizeof(XHead) + sizeof(XRec) * (size_t)XMAX);
+  const size_t out_bytes = sizeof(XHead) + 16 * (size_t)XMAX;
+  if (ctx->xsend.ensure(stride) || ctx->xrecv.ensure(stride * nranks) || ctx->xout.ensure(out_bytes) ||
+      (out_bytes > ctx->h_xout_cap && (ctx->h_xout ? (void)hipHostFree(ctx->h_xout) : (void)0,
+                                       ctx->h_xout = nullptr, ctx->h_xout_cap = 0,
+                                       hipHostMalloc((void **)&ctx->h_xout, out_bytes) != hipSuccess))) {
+    (void)ncclCommDestroy(ctx->comm);
+    ctx->comm = nullptr;
+    return ENOMEM;
+  }
+  ctx->h_xout_cap = std::max(ctx->h_xout_cap, out_bytes);
   {
     std::lock_guard<std::mutex> sg(ctx->xseq.mu);
     ctx->xseq.next = 0;
@@ -5600,51 +5884,56 @@ int gbgpu_comm_init(gbgpu_ctx *ctx, int nranks, int rank, const uint8_t *id) {
 
 // One exchange, admitted by the context's sequencer: the collectives of
 // every rank run in sequence-number order whichever thread gets here first.
-static int allgather_admitted(gbgpu_ctx *ctx, QuerySlot *q, int32_t k, int64_t *docids, double *scores, int32_t *n,
-                              int64_t *hits, gbgpu_result *local) {
+// Once admitted, this rank takes part in the all-gather whatever happens: a
+// failure before it (`err`: an invalid or idle slot, a failed pack) sends an
+// empty reply, so the other ranks' exchange stays paired with theirs, and is
+// returned after the collective.  Buffers were sized at gbgpu_comm_init.
+static int allgather_admitted(gbgpu_ctx *ctx, QuerySlot *q, int err, int32_t k, int64_t *docids, double *scores,
+                              int32_t *n, int64_t *hits, gbgpu_result *local) {
   std::lock_guard<std::mutex> xg(ctx->x_mu);
-  if (!ctx->comm) return EINVAL;
+  if (!ctx->comm) return EINVAL;  // no communicator: no collective to pair
   std::unique_lock<std::mutex> lk;
   if (q) {
     lk = std::unique_lock<std::mutex>(q->mu);
-    if (!q->pending) return EINVAL;
+    if (!q->pending) {
+      if (!err) err = EINVAL;
+      lk.unlock();
+      q = nullptr;
+    }
   }
   (void)hipSetDevice(ctx->device);
   const size_t stride = align256(sizeof(XHead) + sizeof(XRec) * (size_t)k);
   const size_t out_bytes = sizeof(XHead) + 16 * (size_t)k;
-  if (ctx->xsend.ensure(stride) || ctx->xrecv.ensure(stride * ctx->nranks) || ctx->xout.ensure(out_bytes))
-    return ENOMEM;
-  if (out_bytes > ctx->h_xout_cap) {
-    if (ctx->h_xout) (void)hipHostFree(ctx->h_xout);
-    ctx->h_xout = nullptr;
-    ctx->h_xout_cap = 0;
-    HIPCHECK(hipHostMalloc((void **)&ctx->h_xout, out_bytes));
-    ctx->h_xout_cap = out_bytes;
-  }
   hipStream_t xs = ctx->xstream;
-  if (!q || q->early) {
-    HIPCHECK(hipMemsetAsync(ctx->xsend.p, 0, sizeof(XHead), xs));  // an empty reply
-  } else {
-    HIPCHECK(hipStreamWaitEvent(xs, q->ev_done, 0));
-    hipLaunchKernelGGL(k_xpack, dim3(1), dim3(256), 0, xs, q->res.as<Counters>(), q->res.as<uint32_t>(res_keys_off()),
-                       q->res.as<uint64_t>(res_docs_off(q->k)), (uint32_t)k, (uint32_t)q->k, q->int_scores ? 1 : 0,
-                       ctx->xsend.as<uint8_t>());
+  bool packed = false;
+  if (q && !q->early && !err) {
+    if (hipStreamWaitEvent(xs, q->ev_done, 0) == hipSuccess) {
+      hipLaunchKernelGGL(k_xpack, dim3(1), dim3(256), 0, xs, q->res.as<Counters>(), q->res.as<uint32_t>(res_keys_off()),
+                         q->res.as<uint64_t>(res_docs_off(q->k)), (uint32_t)k, (uint32_t)q->k, q->int_scores ? 1 : 0,
+                         ctx->xsend.as<uint8_t>());
+      packed = hipGetLastError() == hipSuccess;
+    }
+    if (!packed) err = GBGPU_EHIP;
   }
-  if (ncclAllGather(ctx->xsend.p, ctx->xrecv.p, stride, ncclUint8, ctx->comm, xs) != ncclSuccess) return GBGPU_EHIP;
+  // an empty reply (n = 0, no hits): an early-out query, no slot, or a failure
+  if (!packed && hipMemsetAsync(ctx->xsend.p, 0, sizeof(XHead), xs) != hipSuccess && !err) err = GBGPU_EHIP;
+  if (ncclAllGather(ctx->xsend.p, ctx->xrecv.p, stride, ncclUint8, ctx->comm, xs) != ncclSuccess) err = GBGPU_EHIP;
   hipLaunchKernelGGL(k_xmerge, dim3(1), dim3(64), 0, xs, ctx->xrecv.as<uint8_t>(), ctx->nranks, (uint32_t)k, stride,
                      ctx->xout.as<uint8_t>());
-  HIPCHECK(hipMemcpyAsync(ctx->h_xout, ctx->xout.p, out_bytes, hipMemcpyDeviceToHost, xs));
-  HIPCHECK(hipStreamSynchronize(xs));
-  int rc = 0;
+  if (hipMemcpyAsync(ctx->h_xout, ctx->xout.p, out_bytes, hipMemcpyDeviceToHost, xs) != hipSuccess ||
+      hipStreamSynchronize(xs) != hipSuccess)
+    err = err ? err : GBGPU_EHIP;
   if (q) {
-    // finish the slot's own query (its result block was read on the device)
+    // finish the slot's own query (its result block was read on the device);
+    // collected even after a failure, so the slot is free again
     gbgpu_result tmp;
     std::memset(&tmp, 0, sizeof tmp);
-    rc = collect(ctx, *q, local ? local : &tmp);
+    const int rc = collect(ctx, *q, local ? local : &tmp);
     lk.unlock();
     slot_released(ctx);
+    if (!err) err = rc;
   }
-  if (rc) return rc;
+  if (err) return err;
   const XHead *h = reinterpret_cast<const XHead *>(ctx->h_xout);
   const double *sc = reinterpret_cast<const double *>(ctx->h_xout + sizeof(XHead));
   const int64_t *dc = reinterpret_cast<const int64_t *>(ctx->h_xout + sizeof(XHead) + 8 * (size_t)k);
@@ -5657,17 +5946,22 @@ static int allgather_admitted(gbgpu_ctx *ctx, QuerySlot *q, int32_t k, int64_t *
   return 0;
 }
 
+// The sequence number is used up by every call that is admitted, whatever
+// its outcome; only ETIMEDOUT (not admitted) leaves it to be retried.  k must
+// be the same on every rank (it sizes the collective): a k out of range is
+// refused before admission, as a protocol error of the caller.
 int gbgpu_allgather_topk(gbgpu_ctx *ctx, int slot, uint64_t seq, int timeout_ms, int32_t k, int64_t *docids,
                          double *scores, int32_t *n, int64_t *hits, gbgpu_result *local) {
   if (!ctx || k < 1 || (uint32_t)k > XMAX || !n || !hits) return EINVAL;
   QuerySlot *q = nullptr;
+  int err = 0;
   if (slot >= 0) {
     q = slot_of(ctx, slot);
-    if (!q) return EINVAL;
+    if (!q) err = EINVAL;  // still takes part, with an empty reply
   }
   int rc = seq_enter(&ctx->xseq, seq, timeout_ms);
   if (rc) return rc;
-  rc = allgather_admitted(ctx, q, k, docids, scores, n, hits, local);
+  rc = allgather_admitted(ctx, q, err, k, docids, scores, n, hits, local);
   seq_leave(&ctx->xseq, seq);
   return rc;
 }

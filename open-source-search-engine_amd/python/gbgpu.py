@@ -8,6 +8,7 @@ the library is missing: there is no CPU fallback.
 from __future__ import annotations
 
 import ctypes
+import errno
 import os
 from dataclasses import dataclass
 from typing import List, Optional, Sequence
@@ -590,14 +591,19 @@ class Engine:
         empty reply."""
         if seq is None:
             seq = self._xseq
-        self._xseq = max(self._xseq, seq + 1)
         d = np.zeros(k, np.int64)
         sc = np.zeros(k, np.float64)
         n, h = ctypes.c_int32(), ctypes.c_int64()
-        _check(self.lib.gbgpu_allgather_topk(self.ctx, slot, seq, timeout_ms,
-                                             k, d.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
-                                             sc.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), ctypes.byref(n),
-                                             ctypes.byref(h), None), "gbgpu_allgather_topk")
+        rc = self.lib.gbgpu_allgather_topk(self.ctx, slot, seq, timeout_ms,
+                                           k, d.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                                           sc.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), ctypes.byref(n),
+                                           ctypes.byref(h), None)
+        # an admitted call uses its number up whatever its outcome (the rank
+        # took part in the collective with an empty reply on failure); only a
+        # call that was never admitted (ETIMEDOUT) leaves it to be retried
+        if rc != errno.ETIMEDOUT and not (rc == errno.EINVAL and seq < self._xseq):
+            self._xseq = max(self._xseq, seq + 1)
+        _check(rc, "gbgpu_allgather_topk")
         return d[:n.value], sc[:n.value], h.value
 
     def merge_replies_device(self, shards, k: int, shard_hits=None):

@@ -7,6 +7,8 @@ checked on its own (gbgpu_merge_replies_device) against the reference's own
 mergeLists (tests/golden/x_*.npz) and against the oracle restatement on
 seeded reply sets, and the whole collective runs as a one-rank communicator.
 The multi-rank ordering (gbgpu_seq) is covered on CPU (test_shards_gloo.py)."""
+import errno
+
 import numpy as np
 import pytest
 
@@ -40,6 +42,25 @@ def test_device_merge_matches_oracle(engine, nranks):
         ed, es = orc.msg3a_merge(shards, k)
         d, s, _ = engine.merge_replies_device(shards, k, [0] * len(shards))
         assert same(d, s, ed, es), (nranks, k)
+
+
+@pytest.mark.parametrize("nranks", [2, 3, 8])
+def test_device_merge_nan_scores_shard_order(engine, nranks):
+    # NaN scores make Msg3a's comparisons partial: its scan over the shards
+    # in order (Msg3a.cpp:1323-1334) falls through to the docid compare on
+    # any NaN, so the pick depends on the shard order -- which the device
+    # merge walks as the reference does (parity with the reference's own
+    # rules as restated by the oracle and the host merge; no reference
+    # fixture holds NaN)
+    rng = np.random.default_rng(nranks * 13 + 1)
+    for k in (5, 50, 400):
+        shards = msg3a_cases.partitioned(rng, nranks, int(rng.integers(20, 120)), int(rng.integers(1, 10)))
+        shards = [(d, np.where(rng.random(len(sc)) < 0.2, np.nan, sc)) for d, sc in shards]
+        ed, es = orc.msg3a_merge(shards, k)
+        hd, hs = gbgpu.merge_topk(shards, k)
+        d, s, _ = engine.merge_replies_device(shards, k, [0] * len(shards))
+        assert same(d, s, ed, es), (nranks, k)
+        assert same(hd, hs, ed, es), (nranks, k)
 
 
 def test_allgather_topk_one_rank():
@@ -85,3 +106,23 @@ def test_allgather_topk_one_rank():
         # sequence numbers: an explicit number already past is refused
         with pytest.raises(gbgpu.GbgpuError):
             eng.allgather_topk(10, slot=-1, seq=0, timeout_ms=0)
+
+        # a failure after admission still takes part in the collective (an
+        # empty reply) and uses its sequence number up, so the next exchange
+        # pairs with the other ranks' next one: an idle slot, a bad slot
+        nxt = eng._xseq
+        with pytest.raises(gbgpu.GbgpuError) as ei:
+            eng.allgather_topk(10, slot=0)  # slot 0 holds no query
+        assert ei.value.code == errno.EINVAL
+        with pytest.raises(gbgpu.GbgpuError):
+            eng.allgather_topk(10, slot=999)
+        assert eng._xseq == nxt + 2
+        eng.enqueue(q.terms, hs, p, slot=0)
+        d, s, h = eng.allgather_topk(q.docs_to_get, slot=0, seq=nxt + 2, timeout_ms=1000)
+        m = min(q.docs_to_get, len(exp["docids"]))
+        assert np.array_equal(d, exp["docids"][:m]) and h == exp["hits"]
+        # a number whose turn never comes times out and is not used up
+        with pytest.raises(gbgpu.GbgpuError) as ei:
+            eng.allgather_topk(10, slot=-1, seq=nxt + 5, timeout_ms=10)
+        assert ei.value.code == errno.ETIMEDOUT
+        assert eng._xseq == nxt + 3
