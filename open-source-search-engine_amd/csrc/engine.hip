@@ -581,7 +581,8 @@ struct ProbeOut {
 };
 
 // append up to 64 matches (one per lane), wave-wide
-__device__ __forceinline__ void mbuf_push(ProbeLds &S, uint32_t &nbuf, bool hit, uint32_t slot, uint32_t u,
+template <class SL>
+__device__ __forceinline__ void mbuf_push(SL &S, uint32_t &nbuf, bool hit, uint32_t slot, uint32_t u,
                                           uint32_t len, int lane) {
   const uint64_t m = __ballot(hit);
   if (hit) {
@@ -599,7 +600,8 @@ __device__ __forceinline__ void mbuf_push(ProbeLds &S, uint32_t &nbuf, bool hit,
 // candidate array), so one atomicOr goes out per word and batch
 // (out of line, with every argument by value: a by-reference counter would
 // live in scratch, and scratch loads wait on vmcnt like any global load)
-__device__ __noinline__ void mbuf_flush_n(ProbeLds *S, uint32_t nbuf, uint32_t *bits, Loc *loc, uint32_t nl,
+template <class SL>
+__device__ __noinline__ void mbuf_flush_n(SL *S, uint32_t nbuf, uint32_t *bits, Loc *loc, uint32_t nl,
                                           uint32_t l, int on, int lane) {
   wave_lds_sync();
   if (!on) nbuf = 0;  // diagnostic (GBGPU_PROBE_MODE=5): matches not published
@@ -623,7 +625,8 @@ __device__ __noinline__ void mbuf_flush_n(ProbeLds *S, uint32_t nbuf, uint32_t *
   }
   wave_lds_sync();
 }
-__device__ __forceinline__ void mbuf_flush(ProbeLds &S, uint32_t &nbuf, const ProbeOut &o, int lane) {
+template <class SL>
+__device__ __forceinline__ void mbuf_flush(SL &S, uint32_t &nbuf, const ProbeOut &o, int lane) {
   mbuf_flush_n(&S, nbuf, o.bits, o.loc, o.nl, o.l, o.on, lane);
   nbuf = 0;
 }
@@ -885,24 +888,27 @@ __device__ void probe_by_cand(const DevPlan *__restrict__ pl, const ProbeWork &w
   mbuf_flush(S, nbuf, po, lane);
 }
 
-// Dense list, one or two candidate arrays: the same search as probe_by_cand,
-// with the candidates streamed through a per-array LDS ring instead of
-// register windows.  Each of the two static chunk roles (A, B) owns a register
-// block of 64 candidates per array: a step writes its block -- loaded two
-// steps earlier, so the wait for it is the wait for its chunk -- into the
-// ring and loads the next 64 after the ones already issued, as long as the
-// ring has room (entries below the consumption point `lo` are free).  The
-// step's windows are then LDS reads, and no candidate load sits on the
-// step's dependency chain (a step waiting on a load issued one step before
-// it was the kernel's stall: HBM latency per chunk).  The start needs no
-// search either: the host knows the span's first run docid (ListEntry::
-// gfirst), and the directory entry of the nearest non-empty bucket below it
-// is a candidate index at or below the lower bound -- the few candidates
-// between are consumed against the runs and match none (their docids are
-// below the span's first run).
-constexpr int PRING = 256;  // candidates per array in the LDS ring (power of two)
-struct ProbeRing {
-  uint64_t c[2][PRING];
+// Dense list, up to four candidate arrays (HPATH): no run list and no
+// search.  The run starts stay in the registers that classified them; the
+// window of each candidate array (its next 64 candidates, one per lane) goes
+// into an LDS table of order-preserving docid buckets over the chunk's docid
+// range [dlo, dhi] (bucket = (d - dlo) >> s, fewer than HB buckets), each
+// bucket naming its first window lane; a run start then finds a candidate
+// with its docid by one table read and one read of the (at most few)
+// candidates from that lane -- two LDS round trips where the run-list search
+// took nine.  The claim order (a docid goes to the first array holding it,
+// addDocIdVotes' k-way union of group 0) is the order the arrays are tried
+// in.  A run's length ends at the next run start: the same lane's, the next
+// lane's of its piece (one bpermute per piece), a later piece's, or the next
+// chunk's (pending).  The span starts at the host-known first run docid
+// (ListEntry::gfirst) through the candidate directory (wave_start_dir).
+constexpr int HB = 512;     // docid buckets of a chunk's table
+constexpr int HPATH_G0 = 4;  // arrays the table path handles (more: probe_by_cand)
+template <int G0>
+struct HashLds {
+  uint16_t tab[G0][HB];  // bucket -> tag << 6 | the bucket's first window lane
+  uint64_t win[G0][64];  // each array's window
+  uint32_t mslot[MBUF], mu[MBUF], mlen[MBUF];
 };
 
 // first candidate index of array k at or below lower_bound(key) and close to
@@ -925,171 +931,286 @@ __device__ uint32_t wave_start_dir(const DevPlan *__restrict__ pl, int k, const 
   return wave_lower_bound(ck, n, key, lane);
 }
 
+// DPP whole-wave lane shifts (lane L reads lane L+1 / L-1; the lane with no
+// source keeps `edge`): VALU moves, no LDS round trip
+__device__ __forceinline__ uint32_t lane_next(uint32_t x, uint32_t edge) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)edge, (int)x, 0x130, 0xf, 0xf, false);  // wave_shl:1
+}
+__device__ __forceinline__ uint32_t lane_prev(uint32_t x, uint32_t edge) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)edge, (int)x, 0x138, 0xf, 0xf, false);  // wave_shr:1
+}
+
+// piece i of a chunk (wchunk_fetch's layout, as chunk_runs): the run starts
+// among the units starting in this lane's 16 bytes (at most two: a run head is
+// two units), their docids and chunk-relative units
+__device__ __forceinline__ uint32_t piece_starts(const WChunk &cur, int i, uint32_t u0, uint32_t u1, int lane, uint64_t &da,
+                                                uint64_t &db, uint32_t &ua, uint32_t &ub) {
+  uint32_t r[7];
+  r[0] = cur.v[i].x;
+  r[1] = cur.v[i].y;
+  r[2] = cur.v[i].z;
+  r[3] = cur.v[i].w;
+  uint32_t e0, e1, e2;  // lane 63: the next piece's first bytes, or the bytes after the chunk
+  if (i + 1 < WPIECES) {
+    e0 = __builtin_amdgcn_readfirstlane(cur.v[i + 1].x);
+    e1 = __builtin_amdgcn_readfirstlane(cur.v[i + 1].y);
+    e2 = __builtin_amdgcn_readfirstlane(cur.v[i + 1].z);
+  } else {
+    e0 = cur.nb.x;
+    e1 = cur.nb.y;
+    e2 = 0;
+  }
+  r[4] = lane_next(r[0], e0);
+  r[5] = lane_next(r[1], e1);
+  r[6] = lane_next(r[2], e2);
+  const uint32_t P = (uint32_t)i * 1024 + (uint32_t)lane * 16;
+  const uint32_t k0 = (P + 5) / 6;  // first unit starting in [P, P + 16)
+  const uint32_t o0 = k0 * 6 - P;
+  uint32_t a[6];
+#pragma unroll
+  for (int j = 0; j < 6; j++) a[j] = o0 == 4 ? r[j + 1] : __builtin_amdgcn_alignbyte(r[j + 1], r[j], o0);
+  auto byte = [&](int b) -> uint32_t { return (a[b >> 2] >> ((b & 3) * 8)) & 0xff; };
+  auto docid_at = [&](int q) -> uint64_t {
+    uint64_t d = 0;
+#pragma unroll
+    for (int b = 4; b >= 0; b--) d = (d << 8) | byte(6 * q + 7 + b);
+    return d >> 2;
+  };
+  uint32_t starts = 0;
+#pragma unroll
+  for (int q = 0; q < 3; q++) {
+    const bool in = 6 * q + o0 < 16 && u0 + k0 + q < u1;
+    if (in && (byte(6 * q + 1) & 0x02) && !(byte(6 * q) & 0x04)) starts |= 1u << q;
+  }
+  // starts: a subset of {0, 1, 2} with no two adjacent (a head spans 2 units)
+  const int qa = starts & 1 ? 0 : starts & 2 ? 1 : 2;
+  ua = k0 + (uint32_t)qa;
+  ub = k0 + 2;
+  const uint64_t dq0 = docid_at(0), dq1 = docid_at(1), dq2 = docid_at(2);
+  da = qa == 0 ? dq0 : qa == 1 ? dq1 : dq2;
+  db = dq2;
+  return (uint32_t)__popc(starts);
+}
+
 template <int MODE, int G0>
-__device__ void probe_by_cand_ring(const DevPlan *__restrict__ pl, const ProbeWork &w, const DevList &L, const uint64_t *cand,
-                                   const Counters *ctr, const uint64_t *dir, ProbeLds &S, ProbeRing &R, const ProbeOut &po,
-                                   int lane) {
-  static_assert(G0 >= 1 && G0 <= 2, "two ring arrays");
+__device__ void probe_by_cand_hash(const DevPlan *__restrict__ pl, const ProbeWork &w, const DevList &L,
+                                   const uint64_t *cand, const Counters *ctr, const uint64_t *dir, HashLds<G0> &S,
+                                   const ProbeOut &po, int lane) {
+  static_assert(G0 >= 1 && G0 <= HPATH_G0, "table path arrays");
   const uint8_t *lp = L.p;
   const uint32_t last_u0 = w.u0 + ((w.u1 - w.u0 - 1) / WCH_UNITS) * WCH_UNITS;
   WChunk cA, cB;
-  // the first two chunks do not depend on the candidates: in flight at once
-  wchunk_fetch(lp, w.u0, lane, cA);
-  wchunk_fetch(lp, min(w.u0 + WCH_UNITS, last_u0), lane, cB);
   constexpr bool FULL = MODE == 0 || MODE >= 5;
-  uint32_t nk[G0], lo[G0], iss[G0], wr[G0], wa[G0], wb[G0];
-  uint64_t base[G0], KA[G0], KB[G0];
-  bool va[G0], vb[G0];
+  uint32_t nk[G0], lo[G0];
+  uint64_t base[G0], cur[G0], nxt[G0];
   const uint64_t dfirst = !FULL ? 0 : w.has_dfirst ? w.dfirst : first_run_doc(L, w.u0, w.u1, lane);
-#pragma unroll
-  for (int k = 0; k < G0; k++) {
-    nk[k] = ctr->g0count[k];
-    base[k] = pl->g0base[k];
-    lo[k] = FULL ? wave_start_dir(pl, k, cand + base[k], nk[k], dir, dfirst, lane) : 0;
-    wr[k] = lo[k];
-  }
-  auto kload = [&](int k, uint32_t i) -> uint64_t {  // candidate i (clamped: a block past the end is never written)
+  auto cload = [&](int k, uint32_t i) -> uint64_t {  // candidate i of array k (clamped; validity at use)
     return cand[base[k] + min(i, max(nk[k], 1u) - 1)];
   };
-  // the first two blocks, into the two roles
+  const int g0n = G0 <= 2 ? G0 : pl->g0n;
 #pragma unroll
   for (int k = 0; k < G0; k++) {
-    wa[k] = lo[k];
-    KA[k] = kload(k, lo[k] + lane);
-    va[k] = lo[k] < nk[k];
-    wb[k] = lo[k] + 64;
-    KB[k] = kload(k, lo[k] + 64 + lane);
-    vb[k] = lo[k] + 64 < nk[k];
-    iss[k] = lo[k] + 128;
+    nk[k] = k < g0n ? ctr->g0count[k] : 0;
+    base[k] = k < g0n ? pl->g0base[k] : 0;
+    lo[k] = FULL && k < g0n ? wave_start_dir(pl, k, cand + base[k], nk[k], dir, dfirst, lane) : 0;
+    cur[k] = cload(k, lo[k] + lane);
+    nxt[k] = cload(k, lo[k] + 64 + lane);
   }
+  wchunk_fetch(lp, w.u0, lane, cA);
+  wchunk_fetch(lp, min(w.u0 + WCH_UNITS, last_u0), lane, cB);
   uint32_t nbuf = 0;
-  uint64_t pend_slot = ~0ull;
+  uint64_t pend_slot = ~0ull;  // slot whose run length waits for the next run start
   uint32_t pend_u = 0;
-  // the window of array k: its next 64 candidates (LDS; a direct read only
-  // when the ring has fallen behind)
-  auto window = [&](int k) -> uint64_t {
-    const uint32_t i = lo[k] + lane;
-    if (i >= nk[k]) return ~0ull;
-    if (i < wr[k]) return R.c[k][i & (PRING - 1)];
-    return cand[base[k] + i];
-  };
-  auto search = [&](uint64_t d, uint32_t nrun) -> uint32_t {
-    uint32_t a = 0;
-#pragma unroll
-    for (uint32_t st = WMAX_RUNS; st > 0; st >>= 1) {
-      const uint32_t t = a + st;
-      const uint64_t v = S.doc[min(t, max(nrun, 1u)) - 1];
-      if (t <= nrun && v < d) a = t;
-    }
-    return a;
-  };
-  auto step = [&](const WChunk &c, uint32_t u0, uint64_t(&K)[G0], uint32_t(&wpos)[G0], bool(&vk)[G0]) {
+  uint32_t tag = 0;  // table generation (10 bits; tables cleared when it wraps)
+  const uint64_t above = ~((2ull << lane) - 1);  // lanes after this one
+  auto step = [&](const WChunk &c, uint32_t u0) {
     if (MODE == 2) {
       if (c.v[0].x == 0x557713eeu && c.v[1].y == 7u && c.v[2].z == 3u) po.bits[0] = 1;
       return;
     }
-    // this role's block (loaded two steps ago) into the ring, then the next
+    // 1. run starts, in registers
+    uint64_t da[WPIECES], db[WPIECES];
+    uint32_t ua[WPIECES], ub[WPIECES], rc[WPIECES];
+    uint64_t mk[WPIECES];
 #pragma unroll
-    for (int k = 0; k < G0; k++) {
-      if (vk[k]) {
-        R.c[k][(wpos[k] + lane) & (PRING - 1)] = K[k];
-        wr[k] = min(wpos[k] + 64, nk[k]);
-      }
-      vk[k] = iss[k] < nk[k] && iss[k] + 64 <= lo[k] + PRING;
-      wpos[k] = iss[k];
-      K[k] = kload(k, iss[k] + lane);
-      if (vk[k]) iss[k] += 64;
+    for (int i = 0; i < WPIECES; i++) {
+      rc[i] = piece_starts(c, i, u0, w.u1, lane, da[i], db[i], ua[i], ub[i]);
+      mk[i] = __ballot(rc[i] != 0);
     }
-    const uint32_t nrun = chunk_runs(c, u0, w.u1, lane, S);
-    if (nrun && pend_slot != ~0ull) {
+    // the chunk's first and last run start; F[i]: first start unit of pieces >= i
+    uint32_t F[WPIECES + 1];
+    F[WPIECES] = 0xffffffffu;
+    uint64_t dlo = ~0ull, dhi = 0;
+#pragma unroll
+    for (int i = WPIECES - 1; i >= 0; i--) {
+      F[i] = F[i + 1];
+      if (mk[i]) {
+        const int f = __ffsll((unsigned long long)mk[i]) - 1;
+        F[i] = __builtin_amdgcn_readlane(ua[i], f);
+        const uint32_t dl = __builtin_amdgcn_readlane((uint32_t)da[i], f);
+        const uint32_t dh = __builtin_amdgcn_readlane((uint32_t)(da[i] >> 32), f);
+        dlo = ((uint64_t)dh << 32) | dl;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < WPIECES; i++) {
+      if (mk[i]) {
+        const int h = 63 - __builtin_clzll((unsigned long long)mk[i]);
+        const uint64_t x = rc[i] == 2 ? db[i] : da[i];
+        const uint32_t dl = __builtin_amdgcn_readlane((uint32_t)x, h);
+        const uint32_t dh = __builtin_amdgcn_readlane((uint32_t)(x >> 32), h);
+        dhi = ((uint64_t)dh << 32) | dl;
+      }
+    }
+    if (F[0] == 0xffffffffu) return;  // no run starts here: nothing consumed, the pending run goes on
+    if (pend_slot != ~0ull) {
       if (nbuf + 1 > MBUF) mbuf_flush(S, nbuf, po, lane);
-      mbuf_push(S, nbuf, lane == 0, (uint32_t)pend_slot, pend_u, u0 + S.unit[0] - pend_u, lane);
+      mbuf_push(S, nbuf, lane == 0, (uint32_t)pend_slot, pend_u, u0 + F[0] - pend_u, lane);
       pend_slot = ~0ull;
     }
     if (MODE == 1) {
-      if (nrun && S.doc[0] == 0x123456789ull) po.bits[0] = 1;
-      wave_lds_sync();
+      if (dlo == 0x123456789ull) po.bits[0] = 1;
       return;
     }
-    if (nrun) {
-      const uint64_t dmax = S.doc[nrun - 1];
-      uint64_t dk[G0];
-      uint32_t pa[G0];
+    // 2. where each start's run ends (chunk-relative unit; ~0: the next chunk)
+    uint32_t ea[WPIECES], eb[WPIECES];
 #pragma unroll
-      for (int k = 0; k < G0; k++) dk[k] = window(k);
-      // every array's search at once (their LDS round trips overlap)
+    for (int i = 0; i < WPIECES; i++) {
+      const uint64_t ab = mk[i] & above;
+      const int j = ab ? __ffsll((unsigned long long)ab) - 1 : lane;
+      const uint32_t nj = (uint32_t)__builtin_amdgcn_ds_bpermute(j << 2, (int)ua[i]);
+      const uint32_t nx = ab ? nj : F[i + 1];
+      ea[i] = rc[i] == 2 ? ub[i] : nx;
+      eb[i] = nx;
+    }
+    // 3. the arrays' windows into their tables, then every start looks its
+    // docid up, array by array; rounds repeat only while a window is used up
+    // inside the chunk (dense arrays), a start staying undecided while its
+    // docid lies beyond a used-up window of an array it has not yet matched
+    static_assert(HB == 512, "9-bit bucket index");
+    const uint64_t span = dhi - dlo;
+    const uint32_t sh = span >= (uint64_t)HB ? 64u - (uint32_t)__builtin_clzll(span) - 9u : 0u;  // (dhi-dlo) >> sh < HB
+    uint32_t und = 0;  // bit 2i+q: start q of piece i undecided
 #pragma unroll
-      for (int k = 0; k < G0; k++) pa[k] = 0;
+    for (int i = 0; i < WPIECES; i++) und |= (rc[i] >= 1 ? 1u : 0u) << (2 * i) | (rc[i] == 2 ? 2u : 0u) << (2 * i);
+    for (;;) {
+      if (++tag == 1024) {
+        tag = 1;
 #pragma unroll
-      for (uint32_t st = WMAX_RUNS; st > 0 && MODE != 6; st >>= 1) {
-#pragma unroll
-        for (int k = 0; k < G0; k++) {
-          const uint32_t t = pa[k] + st;
-          const uint64_t v = S.doc[min(t, nrun) - 1];
-          if (t <= nrun && v < dk[k]) pa[k] = t;
-        }
+        for (int k = 0; k < G0; k++)
+          for (int q = lane; q < HB; q += 64) S.tab[k][q] = 0;
       }
-      if (MODE == 7) {  // diagnostic: windows searched and consumed, no settle
-#pragma unroll
-        for (int k = 0; k < G0; k++) {
-          const bool in = dk[k] <= dmax;
-          lo[k] += (uint32_t)__popcll(__ballot(in));
-          if (pa[k] == 0x7fffffffu) po.bits[1] = 1;
-        }
-        wave_lds_sync();
-        return;
-      }
+      uint64_t wmax[G0];
+      bool full[G0];
 #pragma unroll
       for (int k = 0; k < G0; k++) {
-        // the 64 candidates from lo against the runs (claims array by array,
-        // in order: a docid goes to the first array holding it)
-        auto settle = [&](uint64_t d, uint32_t a) -> uint32_t {
-          const bool in = d <= dmax;
-          bool hit = false, last = false;
-          uint32_t u = 0, len = 0;
-          if (in && a < nrun && S.doc[a] == d && !S.claim[a]) {
-            S.claim[a] = 1;
-            u = u0 + S.unit[a];
-            if (a + 1 < nrun) {
-              hit = true;
-              len = S.unit[a + 1] - S.unit[a];
-            } else {
-              last = true;  // ends at the next chunk's first run start
+        const bool valid = lo[k] + lane < nk[k];
+        const uint64_t cd = valid ? cur[k] : ~0ull;
+        const bool ins = valid && cd >= dlo && cd <= dhi;
+        const uint32_t bk = ins ? (uint32_t)((cd - dlo) >> sh) : 0xffffffffu;
+        const uint32_t bp = lane_prev(bk, 0xfffffffeu);
+        if (ins && bp != bk) S.tab[k][bk] = (uint16_t)(tag << 6 | (uint32_t)lane);
+        S.win[k][lane] = cd;
+        const uint64_t wl = (uint64_t)__builtin_amdgcn_readlane((uint32_t)(cur[k] >> 32), 63) << 32 |
+                            __builtin_amdgcn_readlane((uint32_t)cur[k], 63);
+        full[k] = lo[k] + 64 <= nk[k] && wl <= dhi;  // the whole window lies in the chunk
+        wmax[k] = full[k] ? wl : ~0ull;
+      }
+      wave_lds_sync();
+      // lookups: start (i, q) of this lane
+      uint32_t hitk[2 * WPIECES], hitl[2 * WPIECES];
+#pragma unroll
+      for (int x = 0; x < 2 * WPIECES; x++) {
+        const int i = x >> 1, q = x & 1;
+        hitk[x] = 0xffu;
+        hitl[x] = 0;
+        if (!(und >> x & 1)) continue;
+        const uint64_t d = q ? db[i] : da[i];
+        const uint32_t bk = (uint32_t)((d - dlo) >> sh);
+        bool decided = true;
+#pragma unroll
+        for (int k = 0; k < G0; k++) {
+          if (k >= G0 || hitk[x] != 0xffu) break;
+          if (d > wmax[k]) {
+            decided = false;
+            break;
+          }
+          const uint32_t e = S.tab[k][bk];
+          if ((e >> 6) != tag) continue;
+          uint32_t l = e & 63;
+          for (; l < 64; l++) {
+            const uint64_t cd = S.win[k][l];
+            if (cd >= d) {
+              if (cd == d) {
+                hitk[x] = (uint32_t)k;
+                hitl[x] = l;
+              }
+              break;
             }
           }
-          if (nbuf + 64 > MBUF) mbuf_flush(S, nbuf, po, lane);
-          mbuf_push(S, nbuf, hit, (uint32_t)(base[k] + lo[k] + lane), u, len, lane);
-          const uint64_t pm = __ballot(last);
-          if (pm) {
-            pend_slot = base[k] + lo[k] + (uint32_t)(__ffsll((unsigned long long)pm) - 1);
-            pend_u = u0 + S.unit[nrun - 1];
-          }
-          const uint32_t nin = (uint32_t)__popcll(__ballot(in));
-          lo[k] += nin;
-          return nin;
-        };
-        if (settle(dk[k], pa[k]) == 64u) {
-          // a chunk meeting more than 64 candidates: further windows
-          for (;;) {
-            const uint64_t d = window(k);
-            if (settle(d, search(d, nrun)) < 64u) break;
-          }
+        }
+        if (decided) und &= ~(1u << x);
+      }
+      // 4. matches into the buffer (a run ending past the chunk waits)
+#pragma unroll
+      for (int x = 0; x < 2 * WPIECES; x++) {
+        const int i = x >> 1, q = x & 1;
+        const bool hit = hitk[x] != 0xffu;
+        if (!__ballot(hit)) continue;
+        uint64_t slot = 0;
+#pragma unroll
+        for (int k = 0; k < G0; k++)
+          if (hitk[x] == (uint32_t)k) slot = base[k] + lo[k] + hitl[x];
+        const uint32_t us = q ? ub[i] : ua[i], ue = q ? eb[i] : ea[i];
+        const bool last = hit && ue == 0xffffffffu;
+        if (nbuf + 64 > MBUF) mbuf_flush(S, nbuf, po, lane);
+        mbuf_push(S, nbuf, hit && !last, (uint32_t)slot, u0 + us, ue - us, lane);
+        const uint64_t pm = __ballot(last);
+        if (pm) {
+          const int f = __ffsll((unsigned long long)pm) - 1;
+          pend_slot = __shfl(slot, f, 64);
+          pend_u = u0 + __shfl(us, f, 64);
         }
       }
+      // 5. consumption: a used-up window moves on by 64 and the chunk goes
+      // round again; the others wait for the last round
+      bool again = false;
+#pragma unroll
+      for (int k = 0; k < G0; k++) {
+        if (full[k]) {
+          again = true;
+          lo[k] += 64;
+          cur[k] = nxt[k];
+          nxt[k] = cload(k, lo[k] + 64 + lane);
+        }
+      }
+      if (!again) break;
+      wave_lds_sync();  // the next round rewrites the tables
     }
-    wave_lds_sync();  // the next chunk rewrites the run list; ring writes land
+#pragma unroll
+    for (int k = 0; k < G0; k++) {
+      const bool valid = lo[k] + lane < nk[k];
+      const uint32_t used = (uint32_t)__popcll(__ballot(valid && cur[k] <= dhi));
+      // the next window: 64 - used candidates left in cur, the rest from nxt
+      const int sl = (lane + (int)used) & 63;
+      const uint64_t a2 = __shfl(cur[k], sl, 64), b2 = __shfl(nxt[k], sl, 64);
+      cur[k] = lane + used < 64u ? a2 : b2;
+      lo[k] += used;
+      nxt[k] = cload(k, lo[k] + 64 + lane);
+    }
+    wave_lds_sync();  // the next chunk rewrites the tables
   };
   const uint32_t nch = (w.u1 - w.u0 + WCH_UNITS - 1) / WCH_UNITS;
   uint32_t u0 = w.u0;
   for (uint32_t it = 0; it + 2 <= nch; it += 2, u0 += 2 * WCH_UNITS) {
-    step(cA, u0, KA, wa, va);
+    step(cA, u0);
     wchunk_fetch(lp, min(u0 + 2 * WCH_UNITS, last_u0), lane, cA);
     __builtin_amdgcn_sched_barrier(0);
-    step(cB, u0 + WCH_UNITS, KB, wb, vb);
+    step(cB, u0 + WCH_UNITS);
     wchunk_fetch(lp, min(u0 + 3 * WCH_UNITS, last_u0), lane, cB);
     __builtin_amdgcn_sched_barrier(0);
   }
-  if (nch & 1) step(cA, u0, KA, wa, va);
+  if (nch & 1) step(cA, u0);
   if (pend_slot != ~0ull) {
     const uint32_t len = lane == 0 ? run_end(L, pend_u + 2) - pend_u : 0;
     if (nbuf + 1 > MBUF) mbuf_flush(S, nbuf, po, lane);
@@ -1180,8 +1301,13 @@ template <int MODE, int G0>
 __global__ void __launch_bounds__(64 * PW) k_probe(const DevPlan *__restrict__ pl, const ProbeWork *work, uint32_t nwork,
                                                    const uint64_t *cand, uint32_t *bits, uint32_t nwords, Loc *loc,
                                                    const Counters *ctr, const uint64_t *dir) {
-  __shared__ ProbeLds s_lds[PW];
-  __shared__ ProbeRing s_ring[G0 <= 2 && MODE != 3 ? PW : 1];
+  constexpr bool HPATH = G0 <= HPATH_G0 && MODE != 3;
+  // a wave runs one of the paths: their LDS overlaps
+  union WaveLds {
+    ProbeLds run;
+    HashLds<HPATH ? G0 : 1> hash;
+  };
+  __shared__ WaveLds s_w[PW];
   // the wave's index is uniform over the wave: said so, every value derived
   // from it (the work item, the list, the loop bounds) lives in SGPRs and the
   // chunk loop is a uniform one (no exec-mask loop, exact vmcnt waits)
@@ -1197,12 +1323,12 @@ __global__ void __launch_bounds__(64 * PW) k_probe(const DevPlan *__restrict__ p
   po.l = w.list;
   po.on = MODE == 5 ? 0 : 1;
   if (L.probe == PROBE_BY_RUN) {
-    if (MODE == 0) probe_by_run<G0>(pl, w, L, cand, ctr, dir, s_lds[wid], po, lane);
+    if (MODE == 0) probe_by_run<G0>(pl, w, L, cand, ctr, dir, s_w[wid].run, po, lane);
   } else {
-    if constexpr (G0 <= 2 && MODE != 3)
-      probe_by_cand_ring<MODE, G0>(pl, w, L, cand, ctr, dir, s_lds[wid], s_ring[wid], po, lane);
+    if constexpr (HPATH)
+      probe_by_cand_hash<MODE, G0>(pl, w, L, cand, ctr, dir, s_w[wid].hash, po, lane);
     else
-      probe_by_cand<MODE == 3 ? 0 : MODE, G0>(pl, w, L, cand, ctr, dir, s_lds[wid], po, lane);
+      probe_by_cand<MODE == 3 ? 0 : MODE, G0>(pl, w, L, cand, ctr, dir, s_w[wid].run, po, lane);
   }
 }
 
@@ -2649,9 +2775,9 @@ struct SiList {
 };
 
 // getWordPosList(docId) over the shrunk list of U units: 1 found (the
-// docid's own run, which starts at unit `own`), 0 NULL, -1 a path not
-// replayed (a match at a negative key or off the list's start, or somewhere
-// else than `own`).  A list shared by several groups is shrunk again in
+// docid's own run, which starts at unit `own`), 0 NULL, < 0 a path not
+// replayed: -1 a match off the list's start, -2 at a negative key, -3
+// somewhere else than `own`.  A list shared by several groups is shrunk again in
 // place for each later use; that pass re-copies the runs onto themselves and
 // then parses the stale bytes after them, extending the last run by E units
 // (k_ext_walk) -- the buffer's bytes stay those of SiList::unit, only the
@@ -2667,8 +2793,8 @@ __device__ int si_word_pos_list(const SiList &L, uint64_t docId, uint32_t own, i
     const uint64_t d = ((L.unit(p + 1) >> 8) & 0xffffffffffull) >> 2;
     if (d == docId) {
       if (p < 0) return -1;
-      if (!(L.unit(p) & 0x01)) return -1;
-      return p == (int64_t)own ? 1 : -1;
+      if (!(L.unit(p) & 0x01)) return -2;
+      return p == (int64_t)own ? 1 : -3;
     }
     step >>= 1;
     step -= step % 6;
@@ -2733,6 +2859,7 @@ __global__ void __launch_bounds__(SCORE_TPB) k_scoreinfo(const DevPlan *__restri
       const int f = si_word_pos_list(L, d, L.cum[lo], U);
       if (f < 0) {
         so.ok = -2;
+        so.pad = f * 1000 - lid;  // diagnostic (GBGPU_SI_DEBUG): which path, which list
         info[t] = so;
         return;
       }
@@ -4790,8 +4917,6 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   if (!q.pw.empty()) {
     auto kp = ctx->probe_mode == 9   ? k_probe<2, 2>
               : ctx->probe_mode == 8 ? k_probe<1, 2>
-              : ctx->probe_mode == 7 ? k_probe<7, 2>
-              : ctx->probe_mode == 6 ? k_probe<6, 2>
               : ctx->probe_mode == 5 ? k_probe<5, 2>
               : ctx->probe_mode == 3 ? k_probe<3, MAXG0>
               : ctx->probe_mode == 2 ? k_probe<2, MAXG0>
@@ -5127,7 +5252,12 @@ static int score_info_docs(QuerySlot &q, const uint64_t *docs, int n, uint32_t n
   HIPCHECK(hipStreamSynchronize(st));
   for (int t = 0; t < n; t++) {
     if (info[t].ok == -1) return GBGPU_ECORRUPT;      // a tree docid with no survivor entry
-    if (info[t].ok == -2) return GBGPU_EUNSUPPORTED;  // a getWordPosList path not replayed
+    if (info[t].ok == -2) {  // a getWordPosList path not replayed
+      if (std::getenv("GBGPU_SI_DEBUG"))
+        std::fprintf(stderr, "gbgpu si decline: docid %llu path %d list %d\n", (unsigned long long)docs[t],
+                     -((-info[t].pad) / 1000), (-info[t].pad) % 1000);
+      return GBGPU_EUNSUPPORTED;
+    }
     if (info[t].ok == -3) return GBGPU_ECAPACITY;     // record arena exhausted
     const int cs = cnt[2 * t], cp = cnt[2 * t + 1];
     if (cs > scap || cp > pcap) return GBGPU_ECAPACITY;

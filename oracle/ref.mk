@@ -38,7 +38,7 @@ SKIP     := Xml.o Unicode.o geo_ip_table.o dlstubs.o
 UNITS    := $(filter-out $(SKIP),$(GB_OBJS))
 OBJS     := $(addprefix $(OBJ)/,$(UNITS))
 
-all: $(OUT)/gbref
+all: $(OUT)/gbref $(OUT)/gbref_gpu
 
 # compile, then drop the unit's global constructors/destructors
 define strip_init
@@ -66,6 +66,34 @@ $(OBJ)/ref_harness.o: oracle/ref_harness.cpp oracle/posdb_oracle.h
 
 $(OUT)/gbref: $(OBJS) $(OBJ)/ref_harness.o
 	$(CXX) -no-pie -o $@ $^ -Wl,--unresolved-symbols=ignore-all -lm -lpthread -lssl -lcrypto -lz
+
+# gbref_gpu: the same harness with INTEGRATION.md's adapter (generated into
+# $(OUT)/adapter.cpp by oracle/adapter_tu.py) and libgbgpu.so linked in; op 4
+# runs the adapter inside the reference's own Msg39 sequence
+# (tests/test_adapter.py, on the GPU box).  Mem.cpp's global operator
+# new/delete (Mem.cpp:175-360: g_mem accounting) would otherwise serve every
+# C++ allocation of the HIP runtime too, static initialisers before main
+# included; in this binary they are local to Mem's own unit (objcopy
+# --localize-symbol on a copy of its object), so every allocation pairs
+# with libstdc++'s.
+GBGPU_LIB := open-source-search-engine_amd/lib
+NEWDEL   := _Znwm _Znam _ZdlPv _ZdaPv _ZnwmRKSt9nothrow_t _ZnamRKSt9nothrow_t
+
+$(OUT)/adapter.cpp: INTEGRATION.md oracle/adapter_tu.py
+	@mkdir -p $(OUT)
+	python3 oracle/adapter_tu.py INTEGRATION.md > $@
+
+$(OBJ)/adapter.o: $(OUT)/adapter.cpp include/gbgpu.h
+	@mkdir -p $(OBJ)
+	$(CXX) $(REFFLAGS) -Iinclude -c $< -o $@
+
+$(OBJ)/Mem_local.o: $(OBJ)/Mem.o
+	objcopy $(addprefix --localize-symbol=,$(NEWDEL)) $< $@
+
+$(OUT)/gbref_gpu: $(filter-out $(OBJ)/Mem.o,$(OBJS)) $(OBJ)/Mem_local.o $(OBJ)/ref_harness.o $(OBJ)/adapter.o \
+                  $(GBGPU_LIB)/libgbgpu.so
+	$(CXX) -no-pie -o $@ $(filter %.o,$^) -Wl,--unresolved-symbols=ignore-all -L$(GBGPU_LIB) -lgbgpu \
+	  -Wl,-rpath,'$$ORIGIN/../../$(GBGPU_LIB)' -lm -lpthread -lssl -lcrypto -lz
 
 clean:
 	rm -rf $(OUT)

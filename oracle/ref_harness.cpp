@@ -73,6 +73,13 @@ __attribute__((constructor(101))) static void install_fault_handler() {
 }
 
 static bool s_inited = false;
+// INTEGRATION.md's adapter (gbgpuIntersectLists), linked only into the GPU
+// build of this harness (oracle/ref.mk: gbref_gpu); op 4 runs it in place of
+// intersectLists10_r, in the same Msg39 sequence, and falls back to the
+// unmodified CPU body where it declines -- as the adapter's caller does
+extern bool gbref_adapter_intersect(PosdbTable *pt) __attribute__((weak));
+static int s_adapter = 0;   // op 4 mode: 1 = the adapter body
+static int s_answered = 0;  // passes the adapter answered
 // the second pass's score info (Posdb.cpp:6116-6244, 7554-7665): the last
 // query's m_scoreInfoBuf / m_pairScoreBuf / m_singleScoreBuf bytes
 static std::vector<char> s_info[3];
@@ -98,6 +105,8 @@ static void ref_init() {
 
 enum { MAXT = 64 };
 
+static int32_t s_used_nodes = 0;       // the last query's TopTree::m_numUsedNodes
+static std::vector<int32_t> s_ints;    // its nodes' m_intScore, high -> low
 static int ref_query(const orc_qterm *terms, const uint8_t *const *lists, const int64_t *sizes, int nterms,
                          const orc_params *p, int64_t *docids, float *scores, int cap, orc_result *out,
                          int64_t *vote_docids, int64_t vote_cap) {
@@ -252,7 +261,8 @@ static int ref_query(const orc_qterm *terms, const uint8_t *const *lists, const 
     if (!tab->allocWhiteListTable()) return ENOMEM;
     if (!tab->setQueryTermInfo()) return ENOMEM;
     const double t0 = now_s();
-    tab->intersectLists10_r();
+    if (s_adapter && gbref_adapter_intersect && gbref_adapter_intersect(tab)) s_answered++;
+    else tab->intersectLists10_r();
     s_isect_s += now_s() - t0;
     out->hits += tab->m_docIdVoteBuf.length() / 6;
     out->filtered += tab->m_filtered;
@@ -262,11 +272,14 @@ static int ref_query(const orc_qterm *terms, const uint8_t *const *lists, const 
   // (Posdb.cpp:889-890): no tree, reported as 0 like the oracle
   out->docs_wanted = tree.m_numNodes > 0 ? tree.m_docsWanted : 0;
   int n = 0;
+  s_ints.clear();
+  s_used_nodes = tree.m_numNodes > 0 ? tree.m_numUsedNodes : 0;
   if (tree.m_numNodes > 0) {
     for (int32_t ti = tree.getHighNode(); ti >= 0 && n < cap; ti = tree.getPrev(ti)) {
       TopNode *t = tree.getNode(ti);
       docids[n] = t->m_docId;
       scores[n] = t->m_score;
+      s_ints.push_back(t->m_intScore);
       n++;
     }
   }
@@ -406,7 +419,14 @@ int main(int argc, char **argv) {
   ref_init();  // Mem's global operator new needs g_mem before any allocation
   int32_t op;
   while (fread(&op, 4, 1, stdin) == 1) {
-    if (op == 1) {
+    if (op == 1 || op == 4) {
+      // op 4: i32 mode first (0 the CPU body, 1 the GPU adapter), then op 1's
+      // request; the response adds i32 passes the adapter answered, i32
+      // m_numUsedNodes and n x i32 m_intScore
+      int32_t mode = 0;
+      if (op == 4) rd(&mode, 4);
+      s_adapter = mode;
+      s_answered = 0;
       int32_t nt;
       rd(&nt, 4);
       if (nt < 0 || nt > MAXT) return 4;
@@ -474,6 +494,15 @@ int main(int argc, char **argv) {
         wr(&nb, 8);
         wr(s_info[b].data(), (size_t)nb);
       }
+      if (op == 4) {
+        wr(&s_answered, 4);
+        wr(&s_used_nodes, 4);
+        for (int i = 0; i < r.n; i++) {
+          const int32_t v = i < (int)s_ints.size() ? s_ints[i] : 0;
+          wr(&v, 4);
+        }
+      }
+      s_adapter = 0;
     } else if (op == 2) {
       int32_t n, rm;
       int64_t mrs;

@@ -17,7 +17,10 @@ import gbgpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 EXE = os.environ.get('GBREF_EXE', os.path.join(ROOT, 'oracle', '_ref', 'gbref'))
-_proc = None
+# the same harness with INTEGRATION.md's adapter and libgbgpu.so linked in
+# (oracle/ref.mk): op 4 runs the adapter body in the reference's Msg39 sequence
+EXE_GPU = os.path.join(ROOT, 'oracle', '_ref', 'gbref_gpu')
+_procs = {}
 
 
 class OrcResult(ctypes.Structure):
@@ -25,31 +28,33 @@ class OrcResult(ctypes.Structure):
                 ("n", ctypes.c_int32), ("corrupt", ctypes.c_int32)]
 
 
-def available() -> bool:
-    return os.access(EXE, os.X_OK)
+def available(exe=None) -> bool:
+    return os.access(exe or EXE, os.X_OK)
 
 
-def _p():
-    global _proc
-    if _proc is None or _proc.poll() is not None:
-        _proc = subprocess.Popen([EXE], stdin=subprocess.PIPE, stdout=subprocess.PIPE)
-        atexit.register(close)
-    return _proc
+def _p(exe=None):
+    exe = exe or EXE
+    pr = _procs.get(exe)
+    if pr is None or pr.poll() is not None:
+        pr = subprocess.Popen([exe], stdin=subprocess.PIPE, stdout=subprocess.PIPE)
+        _procs[exe] = pr
+        if len(_procs) == 1:
+            atexit.register(close)
+    return pr
 
 
 def close():
-    global _proc
-    if _proc is not None:
+    for exe, pr in list(_procs.items()):
         try:
-            _proc.stdin.close()
-            _proc.wait(timeout=10)
+            pr.stdin.close()
+            pr.wait(timeout=10)
         except Exception:
-            _proc.kill()
-        _proc = None
+            pr.kill()
+        del _procs[exe]
 
 
-def _read(n):
-    p = _p()
+def _read(n, exe=None):
+    p = _p(exe)
     b = p.stdout.read(n)
     if len(b) != n:
         rc = p.poll()
@@ -57,12 +62,17 @@ def _read(n):
     return b
 
 
-def query(terms, lists, params, cap=4096, votes=False, reps=1, white=None):
+def query(terms, lists, params, cap=4096, votes=False, reps=1, white=None, mode=None, exe=None):
     """Same result dict as oracle_binding.query (+ 'votes', 'seconds').
-    white: the whitelist lists (Msg2::m_whiteLists) when params.use_whitelist."""
-    p = _p()
+    white: the whitelist lists (Msg2::m_whiteLists) when params.use_whitelist.
+    mode (op 4, the gbref_gpu build): 0 the CPU body, 1 INTEGRATION.md's
+    adapter; adds 'answered' (passes the adapter answered), 'used_nodes'
+    (TopTree::m_numUsedNodes) and 'int_scores' (the nodes' m_intScore)."""
+    p = _p(exe)
+    rd = lambda n: _read(n, exe)  # noqa: E731
     qt = (gbgpu.QTerm * max(1, len(terms)))(*terms)
-    req = [struct.pack("<ii", 1, len(terms)), bytes(params), bytes(qt)[:ctypes.sizeof(gbgpu.QTerm) * len(terms)]]
+    head = struct.pack("<ii", 1, len(terms)) if mode is None else struct.pack("<iii", 4, mode, len(terms))
+    req = [head, bytes(params), bytes(qt)[:ctypes.sizeof(gbgpu.QTerm) * len(terms)]]
     for l in lists:
         req.append(struct.pack("<q", len(l)))
         req.append(bytes(l))
@@ -74,21 +84,25 @@ def query(terms, lists, params, cap=4096, votes=False, reps=1, white=None):
         req.append(bytes(l))
     p.stdin.write(b"".join(req))
     p.stdin.flush()
-    r = OrcResult.from_buffer_copy(_read(ctypes.sizeof(OrcResult)))
-    d = np.frombuffer(_read(8 * r.n), np.int64).copy()
-    s = np.frombuffer(_read(4 * r.n), np.float32).copy()
-    (nv,) = struct.unpack("<q", _read(8))
-    v = np.frombuffer(_read(8 * nv), np.int64).copy()
-    (sec,) = struct.unpack("<d", _read(8))
+    r = OrcResult.from_buffer_copy(rd(ctypes.sizeof(OrcResult)))
+    d = np.frombuffer(rd(8 * r.n), np.int64).copy()
+    s = np.frombuffer(rd(4 * r.n), np.float32).copy()
+    (nv,) = struct.unpack("<q", rd(8))
+    v = np.frombuffer(rd(8 * nv), np.int64).copy()
+    (sec,) = struct.unpack("<d", rd(8))
     info = []
     for _ in range(3):  # m_scoreInfoBuf, m_pairScoreBuf, m_singleScoreBuf
-        (nb,) = struct.unpack("<q", _read(8))
-        info.append(_read(nb) if nb else b"")
+        (nb,) = struct.unpack("<q", rd(8))
+        info.append(rd(nb) if nb else b"")
+    out = dict(docids=d, scores=s, hits=r.hits, filtered=r.filtered, docs_wanted=r.docs_wanted,
+               corrupt=r.corrupt, votes=v, seconds=sec, score_info=info[0], pair_scores=info[1],
+               single_scores=info[2])
+    if mode is not None:
+        answered, used = struct.unpack("<ii", rd(8))
+        out.update(answered=answered, used_nodes=used, int_scores=np.frombuffer(rd(4 * r.n), np.int32).copy())
     if r.corrupt < 0:
         raise RuntimeError(f"gbref query rc={-r.corrupt}")
-    return dict(docids=d, scores=s, hits=r.hits, filtered=r.filtered, docs_wanted=r.docs_wanted,
-                corrupt=r.corrupt, votes=v, seconds=sec, score_info=info[0], pair_scores=info[1],
-                single_scores=info[2])
+    return out
 
 
 def posdb_merge(lists, remove_neg_keys, min_rec_sizes=-1, timed=False):
