@@ -1111,8 +1111,10 @@ __device__ void probe_by_cand_hash(const DevPlan *__restrict__ pl, const ProbeWo
         const uint32_t bp = lane_prev(bk, 0xfffffffeu);
         if (ins && bp != bk) S.tab[k][bk] = (uint16_t)(tag << 6 | (uint32_t)lane);
         S.win[k][lane] = cd;
-        const uint64_t wl = (uint64_t)__builtin_amdgcn_readlane((uint32_t)(cur[k] >> 32), 63) << 32 |
-                            __builtin_amdgcn_readlane((uint32_t)cur[k], 63);
+        // (readlane returns int: each half through uint32_t, no sign extension)
+        const uint32_t wlh = (uint32_t)__builtin_amdgcn_readlane((uint32_t)(cur[k] >> 32), 63);
+        const uint32_t wll = (uint32_t)__builtin_amdgcn_readlane((uint32_t)cur[k], 63);
+        const uint64_t wl = (uint64_t)wlh << 32 | wll;
         full[k] = lo[k] + 64 <= nk[k] && wl <= dhi;  // the whole window lies in the chunk
         wmax[k] = full[k] ? wl : ~0ull;
       }
@@ -1150,6 +1152,16 @@ __device__ void probe_by_cand_hash(const DevPlan *__restrict__ pl, const ProbeWo
           }
         }
         if (decided) und &= ~(1u << x);
+        if (pl->dbg_doc && d == pl->dbg_doc && pl->dbg_buf) {
+          // diagnostic (GBGPU_PROBE_DEBUG_DOC): up to 32 records of 16 words
+          const uint32_t o = atomicAdd(reinterpret_cast<uint32_t *>(pl->dbg_buf), 1u);
+          if (o < 32) {
+            unsigned long long *r = pl->dbg_buf + 1 + 16 * o;
+            r[0] = po.l, r[1] = u0, r[2] = (uint32_t)x, r[3] = (uint32_t)lane, r[4] = dlo, r[5] = dhi, r[6] = sh;
+            r[7] = bk, r[8] = tag, r[9] = bk < HB ? S.tab[0][bk] : 0xdead, r[10] = S.win[0][0], r[11] = S.win[0][63];
+            r[12] = lo[0], r[13] = nk[0], r[14] = (uint32_t)full[0] | (decided ? 2u : 0u), r[15] = hitk[x] << 8 | hitl[x];
+          }
+        }
       }
       // 4. matches into the buffer (a run ending past the chunk waits)
 #pragma unroll
@@ -3091,48 +3103,150 @@ __device__ __forceinline__ uint4 rep_entry(uint32_t key, float B, uint64_t d, bo
   return make_uint4(key, __float_as_uint(B), (uint32_t)d, (uint32_t)(d >> 32));
 }
 
+// The ring-buffer filter restated on a survivor's own word positions, one
+// lane per survivor: the ring after group m and the groups written before g
+// holds, for g's scan, m at the slots (wordPos mod 4096) of m's keys that no
+// group written since overwrote, and g at g's slots; the reference's scan
+// (Posdb.cpp:6445-6485) then finds the smallest distance between
+// neighbouring slots of different types -- the same as between any m slot
+// and the last g slot before it or vice versa -- and the wrap distance from
+// m's last slot round to ourFirstPos (the head slot of m's last sublist).
+// The slots go to per-lane LDS columns; a survivor with more than BL_SLOTS
+// keys in a group takes the wave's 4096-slot ring (the reference's own
+// buffer) instead.
+constexpr int BL_SLOTS = 32;
+__device__ __forceinline__ uint32_t ring_slot(gu8 *kp) {
+  return (((uint32_t)kp[2] | ((uint32_t)kp[3] << 8) | ((uint32_t)kp[4] << 16) | ((uint32_t)kp[5] << 24)) >> 14) &
+         (RING - 1);
+}
+// group g's slots into col[0..n) (column layout: entry k of lane at [k][lane]);
+// false on overflow.  first: the head slot of the last present sublist.
+__device__ bool lane_slots(const DevPlan *__restrict__ pl, const Counters *ctr, int g, uint32_t s, uint32_t lm,
+                           const Loc *svl, uint16_t (*col)[64], int lane, int &n, int &first) {
+  n = 0;
+  const int gns = pl->gnsub[g];
+  for (int x = 0; x < gns; x++) {
+    const int lid = pl->gsub[g][x];
+    if (!(lm >> lid & 1)) continue;
+    const SubRun run = sub_run_at(pl, ctr, svl[lid], lid, g, x, s);
+    for (uint32_t k = 0; k < run.len; k++) {
+      if (k == 1) continue;  // the second half of the 12-byte head
+      if (n == BL_SLOTS) return false;
+      col[n++][lane] = (uint16_t)ring_slot(run.key(k));
+    }
+    first = (int)ring_slot(run.own);
+  }
+  return true;
+}
+__device__ void lane_sort(uint16_t (*col)[64], int n, int lane) {
+  for (int a = 1; a < n; a++) {
+    const uint16_t v = col[a][lane];
+    int b = a - 1;
+    while (b >= 0 && col[b][lane] > v) {
+      col[b + 1][lane] = col[b][lane];
+      b--;
+    }
+    col[b + 1][lane] = v;
+  }
+}
+
 // rep != nullptr: the survivors are in docid order already, so the bound
-// goes straight into the replay entry; else into sbound for k_rank
+// goes straight into the replay entry; else into sbound for k_rank.  A block
+// of BND_WAVES waves, one lane per survivor (the ring restated above); the
+// survivors whose lists overflow a lane's slot columns then take the wave
+// one at a time, over the 4096-slot ring.
 __global__ void __launch_bounds__(64 * BND_WAVES) k_bound(const DevPlan *__restrict__ pl, const Counters *ctr,
                                                        const uint32_t *sv_slot, const uint32_t *sv_lm,
                                                        const Loc *sv_loc, float *sbound, const uint32_t *skey,
                                                        const uint64_t *sdoc, const uint8_t *sflag, uint4 *rep) {
   __shared__ __attribute__((aligned(16))) uint8_t s_ring[BND_WAVES][RING];
+  __shared__ uint16_t s_ms[BND_WAVES][BL_SLOTS][64], s_gs[BND_WAVES][BL_SLOTS][64];
   stage_weights(&c_weights);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   uint8_t *ring = s_ring[wid];
+  uint16_t(*ms)[64] = s_ms[wid];
+  uint16_t(*gs)[64] = s_gs[wid];
   const uint32_t nsurv = (uint32_t)(ctr->surv_top >> 36);
   const int ng = pl->ngroups, m = pl->min_listi;
   const float INF = __int_as_float(0x7f800000);
-  for (uint32_t i = blockIdx.x * BND_WAVES + wid; i < nsurv; i += gridDim.x * BND_WAVES) {
-    const uint32_t s = sv_slot[i], lm = sv_lm[i];
-    const Loc *svl = sv_loc + (uint64_t)i * (uint32_t)pl->nlists;
-    if (pl->sortby_group >= 0) {  // gbsortby: both prefilters are skipped (Posdb.cpp:6050-6051, 6350)
-      if (lane == 0) {
-        if (rep) rep[i] = rep_entry(skey[i], INF, sdoc[i], sflag[i] != 0);
-        else sbound[i] = INF;
-      }
-      continue;
-    }
-    // lane g: getMaxPossibleScore's scan of group g
-    BoundCore core{0, 0.0f};
-    if (lane < ng && !(pl->gflags0[lane] & (BF_NEGATIVE | BF_FACET)))
-      core = group_bound_core(pl, ctr, lane, s, lm, svl);
+  const float tfw_m = pl->tfw[m];
+  const bool sortby = pl->sortby_group >= 0;  // gbsortby: both prefilters are skipped (Posdb.cpp:6050-6051, 6350)
+  for (uint32_t base = (blockIdx.x * BND_WAVES + wid) * 64u; base < nsurv; base += gridDim.x * BND_WAVES * 64u) {
+    const uint32_t i = base + lane;
     float B = INF;
-    // filter 1 (m_doMaxScoreAlgo): bestDist 0, qdist 0 (Posdb.cpp:6327-6346)
-    if (pl->do_max_score && lane < ng && !(pl->gflags0[lane] & (BF_NEGATIVE | BF_FACET))) {
-      const float v = max_score_tail(pl, core, 1.0f, 0, 0);
-      if (v != -1.0f) B = v;
+    bool over = false;
+    if (i < nsurv && !sortby) {
+      const uint32_t s = sv_slot[i], lm = sv_lm[i];
+      const Loc *svl = sv_loc + (uint64_t)i * (uint32_t)pl->nlists;
+      int nm = 0, ourFirstPos = -1;
+      over = !lane_slots(pl, ctr, m, s, lm, svl, ms, lane, nm, ourFirstPos);
+      if (!over) lane_sort(ms, nm, lane);
+      for (int g = 0; g < ng && !over; g++) {
+        if (pl->gflags0[g] & (BF_NEGATIVE | BF_FACET)) continue;
+        const BoundCore core = group_bound_core(pl, ctr, g, s, lm, svl);
+        // filter 1 (m_doMaxScoreAlgo): bestDist 0, qdist 0 (Posdb.cpp:6327-6346)
+        if (pl->do_max_score) {
+          const float v = max_score_tail(pl, core, 1.0f, 0, 0);
+          if (v != -1.0f) B = fminf(B, v);
+        }
+        if (g == m) continue;
+        // filter 2 (Posdb.cpp:6364-6504): g's keys are written over the ring
+        // whatever its bound, then scanned against m's survivors there
+        int ngs = 0, dummy = -1;
+        if (!lane_slots(pl, ctr, g, s, lm, svl, gs, lane, ngs, dummy)) {
+          over = true;
+          break;
+        }
+        lane_sort(gs, ngs, lane);
+        // m slots g overwrote (both sorted): gone for this and later groups
+        for (int a = 0, b = 0; a < nm && b < ngs;) {
+          const uint16_t x = ms[a][lane], y = gs[b][lane];
+          if (x == 0xffffu) break;  // removed slots sort last
+          if (x < y) a++;
+          else if (x > y) b++;
+          else ms[a++][lane] = 0xffffu;
+        }
+        lane_sort(ms, nm, lane);
+        if (core.state < 0) continue;  // -1: not applied
+        int32_t bestDist = 0x7fffffff, hisLastPos = -1;
+        int prev = -1, ptype = -1;
+        for (int a = 0, b = 0; a < nm || b < ngs;) {
+          const int x = a < nm ? (int)ms[a][lane] : 0xffff, y = b < ngs ? (int)gs[b][lane] : 0xffff;
+          if (x == 0xffff && y == 0xffff) break;
+          int cur, t;
+          if (x < y) {
+            cur = x, t = 0, a++;
+            hisLastPos = x;
+          } else {
+            cur = y, t = 1, b++;
+          }
+          if (prev >= 0 && t != ptype) bestDist = min(bestDist, cur - prev);
+          prev = cur, ptype = t;
+        }
+        const int32_t wrapDist = ourFirstPos + (RING - hisLastPos);
+        if (wrapDist < bestDist) bestDist = wrapDist;
+        const float v = max_score_tail(pl, core, tfw_m, bestDist, pl->qpos[m] - pl->qpos[g]);
+        if (v != -1.0f) B = fminf(B, v);
+      }
     }
-    // filter 2, the ring buffer (Posdb.cpp:6364-6504): the min group's word
-    // positions mod 4096, then each other group's over them in turn (the
-    // buffer is not cleared between groups)
-    {
+    // overflowing survivors: the whole wave, one at a time, over the ring
+    for (uint64_t om = __ballot(over); om; om &= om - 1) {
+      const int j = __ffsll((unsigned long long)om) - 1;
+      const uint32_t ij = base + (uint32_t)j;
+      const uint32_t s = sv_slot[ij], lm = sv_lm[ij];
+      const Loc *svl = sv_loc + (uint64_t)ij * (uint32_t)pl->nlists;
+      // lane g: getMaxPossibleScore's scan of group g
+      BoundCore core{0, 0.0f};
+      if (lane < ng && !(pl->gflags0[lane] & (BF_NEGATIVE | BF_FACET))) core = group_bound_core(pl, ctr, lane, s, lm, svl);
+      float Bw = INF;
+      if (pl->do_max_score && lane < ng && !(pl->gflags0[lane] & (BF_NEGATIVE | BF_FACET))) {
+        const float v = max_score_tail(pl, core, 1.0f, 0, 0);
+        if (v != -1.0f) Bw = v;
+      }
       uint4 *r4 = reinterpret_cast<uint4 *>(ring);
       for (int q = lane; q < RING / 16; q += 64) r4[q] = make_uint4(~0u, ~0u, ~0u, ~0u);
       wave_lds_sync();
       const int ourFirstPos = ring_fill(pl, ctr, m, s, lm, svl, ring, (uint8_t)m, lane);
-      const float tfw_m = pl->tfw[m];
       for (int g = 0; g < ng; g++) {
         if (g == m || (pl->gflags0[g] & (BF_NEGATIVE | BF_FACET))) continue;
         wave_lds_sync();
@@ -3144,14 +3258,14 @@ __global__ void __launch_bounds__(64 * BND_WAVES) k_bound(const DevPlan *__restr
         if (cg.state < 0) continue;  // -1: not applied
         const int32_t bestDist = ring_best_dist(ring, (uint8_t)m, (uint8_t)g, ourFirstPos, lane);
         const float v = max_score_tail(pl, cg, tfw_m, bestDist, pl->qpos[m] - pl->qpos[g]);
-        if (lane == 0 && v != -1.0f) B = fminf(B, v);
+        if (lane == 0 && v != -1.0f) Bw = fminf(Bw, v);
       }
       wave_lds_sync();
-    }
-    // min over the wave
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) B = fminf(B, __shfl_xor(B, off, 64));
-    if (lane == 0) {
+      for (int off = 32; off > 0; off >>= 1) Bw = fminf(Bw, __shfl_xor(Bw, off, 64));
+      if (lane == j) B = Bw;
+    }
+    if (i < nsurv) {
       if (rep) rep[i] = rep_entry(skey[i], B, sdoc[i], sflag[i] != 0);
       else sbound[i] = B;
     }
@@ -4336,6 +4450,7 @@ struct gbgpu_ctx {
   int score_mode = 0;  // diagnostic only (GBGPU_SCORE_MODE): 1 mini-merge without scoring
   int debug_ext = 0;   // diagnostic only (GBGPU_DEBUG_EXT): print the re-shrink table per query
   uint64_t *d_sdbg = nullptr;  // GBGPU_SCORE_MODE=2: per-wave k_score timing (GBGPU_SCORE_DUMP file)
+  unsigned long long *d_pdbg = nullptr;  // GBGPU_PROBE_DEBUG_DOC: k_probe's trace of one docid
   uint32_t sdbg_grid = 0;
   std::mutex merge_mu;
   gbmerge::MergeState *merge = nullptr;  // created on first use (merge.hip)
@@ -4642,6 +4757,12 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   P.sortby_int = hp.sortby_int;
   q.int_scores = hp.sortby_int != 0;
   P.min_listi = hp.min_listi;
+  if (const char *dd = std::getenv("GBGPU_PROBE_DEBUG_DOC")) {
+    P.dbg_doc = std::strtoull(dd, nullptr, 10);
+    if (!ctx->d_pdbg && hipMalloc((void **)&ctx->d_pdbg, 8 * (1 + 16 * 32)) != hipSuccess) ctx->d_pdbg = nullptr;
+    if (ctx->d_pdbg) HIPCHECK(hipMemsetAsync(ctx->d_pdbg, 0, 8 * (1 + 16 * 32), q.stream));
+    P.dbg_buf = ctx->d_pdbg;
+  }
   P.all_same_wiki = 1;  // m_allInSameWikiPhrase, Posdb.cpp:5764-5778
   for (int j = 0; j < hp.ngroups; j++) {
     if (hp.g[j].flags[0] & (BF_NEGATIVE | BF_NUMBER | BF_FACET)) continue;
@@ -4915,7 +5036,8 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
                      q.cunit.as<uint32_t>(), dctr, ng0, q.dir.as<uint64_t>());
   if (ctx->profiling) HIPCHECK(hipEventRecord(q.ev[1], st));
   if (!q.pw.empty()) {
-    auto kp = ctx->probe_mode == 9   ? k_probe<2, 2>
+    auto kp = ctx->probe_mode == 4   ? k_probe<0, MAXG0>  // diagnostic: the run-list search path
+              : ctx->probe_mode == 9 ? k_probe<2, 2>
               : ctx->probe_mode == 8 ? k_probe<1, 2>
               : ctx->probe_mode == 5 ? k_probe<5, 2>
               : ctx->probe_mode == 3 ? k_probe<3, MAXG0>
@@ -4997,7 +5119,8 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   if (ctx->profiling) HIPCHECK(hipEventRecord(q.ev[4], st));
   if (clus) {
     // site clustering: prefilter bounds, docid order, the TopTree replay
-    const uint32_t bgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((slot_ub + BND_WAVES - 1) / BND_WAVES, 4096));
+    const uint32_t bgrid =
+        (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((slot_ub + 64 * BND_WAVES - 1) / (64 * BND_WAVES), 4096));
     // the replay entries: written by k_bound when the survivors are in docid
     // order (one candidate array), else placed by k_rank
     const bool ranked = P.g0n > 1;
@@ -5331,6 +5454,17 @@ static int collect(gbgpu_ctx *ctx, QuerySlot &q, gbgpu_result *out, std::vector<
           std::fwrite(h.data(), 8, h.size(), f);
           std::fclose(f);
         }
+  }
+  if (ctx->d_pdbg && std::getenv("GBGPU_PROBE_DEBUG_DOC")) {
+    std::vector<unsigned long long> h(1 + 16 * 32);
+    if (hipMemcpy(h.data(), ctx->d_pdbg, 8 * h.size(), hipMemcpyDeviceToHost) == hipSuccess)
+      for (unsigned long long o = 0; o < std::min<unsigned long long>(h[0] & 0xffffffffull, 32); o++) {
+        const unsigned long long *r = &h[1 + 16 * o];
+        std::fprintf(stderr,
+                     "probe dbg: list %llu u0 %llu slot %llu lane %llu dlo %llu dhi %llu sh %llu bk %llu tag %llu "
+                     "e %llx win0 %llu win63 %llu lo %llu nk %llu full|dec %llu hit %llx\n",
+                     r[0], r[1], r[2], r[3], r[4], r[5], r[6], r[7], r[8], r[9], r[10], r[11], r[12], r[13], r[14], r[15]);
+      }
   }
   if (std::getenv("GBGPU_TOPK_DEBUG") && q.sel.p) {
     unsigned long long td[8];

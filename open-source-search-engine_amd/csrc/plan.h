@@ -158,6 +158,8 @@ struct DevPlan {
   uint32_t group_lists[MAXG];  // bit l: list l is a sublist of group g
   uint32_t neg_lists;          // bit l: list l is a sublist of a negative group
   uint8_t list_mult[MAXL];     // positive groups list l is a sublist of (its runs' record copies)
+  uint64_t dbg_doc;            // diagnostic (GBGPU_PROBE_DEBUG_DOC): k_probe traces this docid's runs
+  unsigned long long *dbg_buf; // into this buffer: a count, then 16-word records
   DevList lists[MAXL];
 };
 

@@ -105,6 +105,7 @@ static void ref_init() {
 
 enum { MAXT = 64 };
 
+static std::vector<int32_t> s_plan;    // the last query's QueryTermInfos (op 4)
 static int32_t s_used_nodes = 0;       // the last query's TopTree::m_numUsedNodes
 static std::vector<int32_t> s_ints;    // its nodes' m_intScore, high -> low
 static int ref_query(const orc_qterm *terms, const uint8_t *const *lists, const int64_t *sizes, int nterms,
@@ -271,6 +272,24 @@ static int ref_query(const orc_qterm *terms, const uint8_t *const *lists, const 
   // allocTopTree returns before setNumNodes when every list is empty
   // (Posdb.cpp:889-890): no tree, reported as 0 like the oracle
   out->docs_wanted = tree.m_numNodes > 0 ? tree.m_docsWanted : 0;
+  // setQueryTermInfo's groups (Posdb.cpp:4354-4869): per QueryTermInfo its
+  // m_bigramFlags[0], m_numSubLists and each sublist's term index and flags
+  s_plan.clear();
+  if (tab) {
+    const QueryTermInfo *qip = (const QueryTermInfo *)tab->m_qiBuf.getBufStart();
+    const int32_t ng = qip ? tab->m_numQueryTermInfos : 0;
+    s_plan.push_back(ng);
+    for (int32_t g = 0; g < ng; g++) {
+      s_plan.push_back((unsigned char)qip[g].m_bigramFlags[0]);
+      s_plan.push_back(qip[g].m_numSubLists);
+      for (int32_t j = 0; j < qip[g].m_numSubLists; j++) {
+        s_plan.push_back((int32_t)(qip[g].m_subLists[j] - rl));
+        s_plan.push_back((unsigned char)qip[g].m_bigramFlags[j]);
+      }
+    }
+  } else {
+    s_plan.push_back(0);
+  }
   int n = 0;
   s_ints.clear();
   s_used_nodes = tree.m_numNodes > 0 ? tree.m_numUsedNodes : 0;
@@ -501,6 +520,10 @@ int main(int argc, char **argv) {
           const int32_t v = i < (int)s_ints.size() ? s_ints[i] : 0;
           wr(&v, 4);
         }
+        // i32 words, then the plan (ngroups; per group flags0, nsub, nsub x (term, flags))
+        const int32_t np = (int32_t)s_plan.size();
+        wr(&np, 4);
+        wr(s_plan.data(), 4 * (size_t)np);
       }
       s_adapter = 0;
     } else if (op == 2) {

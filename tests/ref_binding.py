@@ -100,6 +100,15 @@ def query(terms, lists, params, cap=4096, votes=False, reps=1, white=None, mode=
     if mode is not None:
         answered, used = struct.unpack("<ii", rd(8))
         out.update(answered=answered, used_nodes=used, int_scores=np.frombuffer(rd(4 * r.n), np.int32).copy())
+        (npl,) = struct.unpack("<i", rd(4))
+        w = list(np.frombuffer(rd(4 * npl), np.int32))
+        groups, k = [], 1
+        for _ in range(w[0] if w else 0):  # setQueryTermInfo's QueryTermInfos
+            flags0, nsub = int(w[k]), int(w[k + 1])
+            subs = [(int(w[k + 2 + 2 * x]), int(w[k + 3 + 2 * x])) for x in range(nsub)]
+            groups.append(dict(flags0=flags0, subs=subs))
+            k += 2 + 2 * nsub
+        out["plan"] = groups
     if r.corrupt < 0:
         raise RuntimeError(f"gbref query rc={-r.corrupt}")
     return out

@@ -88,6 +88,8 @@ def test_gpu_adapter_in_reference_msg39(path):
         # the body sees one docid piece per call and declines splits (they
         # are replaced at the Msg39 level): CPU body
         assert gpu["answered"] == 0, label
+    elif cpu["docs_wanted"] == 0:
+        assert gpu["answered"] == 0, label  # every list empty: Msg39 runs no pass (Msg39.cpp:945-948)
     else:
         assert gpu["answered"] == 1, (label, "the adapter declined a supported query")
     same_tree(cpu, gpu, label)

@@ -50,3 +50,19 @@ def test_adapter_compiles_against_reference_headers(tmp_path):
            "-I" + REF, "-I" + os.path.join(ROOT, "include"), str(f)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     assert r.returncode == 0, r.stderr[-4000:]
+
+
+@pytest.mark.skipif(not os.path.isdir(REF) or shutil.which("g++") is None,
+                    reason="reference tree or g++ absent (GPU box)")
+def test_adapter_has_no_null_path_at_O2(tmp_path):
+    """Compiled as the reference builds (-O2), no path of the adapter may be a
+    known null dereference: the reference's Mem.h turns malloc/calloc/realloc
+    into a crash (Mem.h:221-225), which g++ then isolates into a trap -- the
+    adapter must allocate with mmalloc/mfree as the reference's code does."""
+    f = tmp_path / "gbgpu_adapter.cpp"
+    f.write_text(adapter_source())
+    cmd = ["g++", "-O2", "-c", "-std=gnu++98", "-fpermissive", "-w", "-Wnull-dereference", "-DPTHREADS",
+           "-I" + REF, "-I" + os.path.join(ROOT, "include"), str(f), "-o", str(tmp_path / "a.o")]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-4000:]
+    assert "null pointer dereference" not in r.stderr, r.stderr[-4000:]
