@@ -453,6 +453,7 @@ constexpr int WCH_UNITS = WCH_BYTES / 6;   // units per wave chunk
 static_assert(WCH_BYTES % 6 == 0, "a chunk holds whole units");
 constexpr int WMAX_RUNS = WCH_UNITS / 2;
 constexpr uint32_t PROBE_WAVES = 256 * 16;
+constexpr uint32_t PROBE_WAVES_WIDE = 256 * 12;  // the wide path: three waves per SIMD (VGPRs)
 
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 struct WChunk {
@@ -1231,6 +1232,474 @@ __device__ void probe_by_cand_hash(const DevPlan *__restrict__ pl, const ProbeWo
   mbuf_flush(S, nbuf, po, lane);
 }
 
+// Dense list, one or two candidate arrays (the common plan: a word and its
+// bigram): probe_by_cand over 6 KiB chunks with 128-candidate windows (two
+// per lane).  A wave's dependent chain per chunk -- run-start compaction,
+// the run-list search, the settles -- is about as long for 6 KiB as for 3
+// KiB (one more search step), so each chain covers twice the bytes; the
+// lanes' two candidates search the run list interleaved.  The span starts at
+// the host-known first run docid through the directory (wave_start_dir).
+constexpr int WP6 = 6;                    // pieces (1 KiB wave loads) of a wide chunk
+constexpr int W6_BYTES = WP6 * 1024;
+constexpr int W6_UNITS = W6_BYTES / 6;    // 1024 units
+constexpr int W6_RUNS = W6_UNITS / 2;     // a run is >= 2 units
+static_assert(W6_BYTES % 6 == 0, "a wide chunk holds whole units");
+struct WChunk6 {
+  v4u v[WP6];
+  uint2 nb;
+};
+struct ProbeLds6 {
+  uint64_t doc[W6_RUNS];
+  uint32_t mslot[MBUF], mu[MBUF], mlen[MBUF];
+  uint16_t unit[W6_RUNS];
+  uint8_t claim[W6_RUNS];
+};
+__device__ __forceinline__ void wchunk6_fetch(const uint8_t *list, uint32_t u0, int lane, WChunk6 &c) {
+  const auto *src = glc<v4u>(list + (size_t)u0 * 6 + lane * 16);
+#pragma unroll
+  for (int i = 0; i < WP6; i++) c.v[i] = __builtin_nontemporal_load(src + i * 64);
+  c.nb = make_uint2(0, 0);
+  if (lane == 63) {
+    typedef uint32_t v2 __attribute__((ext_vector_type(2)));
+    const v2 t = *glc<v2>(list + (size_t)u0 * 6 + W6_BYTES);
+    c.nb = make_uint2(t.x, t.y);
+  }
+}
+// chunk_runs over WP6 pieces (its comment has the layout): the run starts of
+// the chunk into S, sorted; returns their count
+__device__ __forceinline__ uint32_t chunk6_runs(const WChunk6 &cur, uint32_t u0, uint32_t u1, int lane, ProbeLds6 &S) {
+  const uint64_t lt = (1ull << lane) - 1;
+  uint32_t nrun = 0;
+#pragma unroll
+  for (int i = 0; i < WP6; i++) {
+    uint32_t r[7];
+    r[0] = cur.v[i].x;
+    r[1] = cur.v[i].y;
+    r[2] = cur.v[i].z;
+    r[3] = cur.v[i].w;
+    uint32_t e0, e1, e2;  // lane 63: the next piece's first bytes, or the bytes after the chunk
+    if (i + 1 < WP6) {
+      e0 = __builtin_amdgcn_readfirstlane(cur.v[i + 1].x);
+      e1 = __builtin_amdgcn_readfirstlane(cur.v[i + 1].y);
+      e2 = __builtin_amdgcn_readfirstlane(cur.v[i + 1].z);
+    } else {
+      e0 = cur.nb.x;
+      e1 = cur.nb.y;
+      e2 = 0;
+    }
+    r[4] = lane_next(r[0], e0);
+    r[5] = lane_next(r[1], e1);
+    r[6] = lane_next(r[2], e2);
+    const uint32_t P = (uint32_t)i * 1024 + (uint32_t)lane * 16;
+    const uint32_t k0 = (P + 5) / 6;  // first unit starting in [P, P + 16)
+    const uint32_t o0 = k0 * 6 - P;
+    uint32_t a[6];
+#pragma unroll
+    for (int j = 0; j < 6; j++) a[j] = o0 == 4 ? r[j + 1] : __builtin_amdgcn_alignbyte(r[j + 1], r[j], o0);
+    auto byte = [&](int b) -> uint32_t { return (a[b >> 2] >> ((b & 3) * 8)) & 0xff; };
+    uint32_t starts = 0;
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+      const bool in = 6 * q + o0 < 16 && u0 + k0 + q < u1;
+      if (in && (byte(6 * q + 1) & 0x02) && !(byte(6 * q) & 0x04)) starts |= 1u << q;
+    }
+    const uint32_t cnt = __popc(starts);  // <= 2: a run head spans two units
+    const uint64_t b0 = __ballot(cnt & 1), b1 = __ballot(cnt & 2);
+    uint32_t o = nrun + (uint32_t)(__popcll(b0 & lt) + 2 * __popcll(b1 & lt));
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+      if (!(starts >> q & 1)) continue;
+      uint64_t d = 0;
+#pragma unroll
+      for (int b = 4; b >= 0; b--) d = (d << 8) | byte(6 * q + 7 + b);
+      S.doc[o] = d >> 2;
+      S.unit[o] = (uint16_t)(k0 + q);
+      S.claim[o] = 0;
+      o++;
+    }
+    nrun += (uint32_t)(__popcll(b0) + 2 * __popcll(b1));
+  }
+  wave_lds_sync();
+  return nrun;
+}
+
+template <int MODE, int G0>
+__device__ void probe_by_cand_wide(const DevPlan *__restrict__ pl, const ProbeWork &w, const DevList &L, const uint64_t *cand,
+                                   const Counters *ctr, const uint64_t *dir, ProbeLds6 &S, const ProbeOut &po, int lane) {
+  static_assert(G0 >= 1 && G0 <= 2, "wide path arrays");
+  const uint8_t *lp = L.p;
+  const uint32_t last_u0 = w.u0 + ((w.u1 - w.u0 - 1) / W6_UNITS) * W6_UNITS;
+  constexpr bool FULL = MODE == 0 || MODE == 5;
+  uint32_t nk[G0], lo[G0];
+  uint64_t base[G0];
+  uint64_t ca[G0], cb[G0], na[G0], nb2[G0];  // candidates lo + lane, lo + 64 + lane, then + 128, + 192
+  const uint64_t dfirst = !FULL ? 0 : w.has_dfirst ? w.dfirst : first_run_doc(L, w.u0, w.u1, lane);
+  auto cload = [&](int k, uint32_t i) -> uint64_t {  // candidate i of array k (clamped; validity at use)
+    return cand[base[k] + min(i, max(nk[k], 1u) - 1)];
+  };
+#pragma unroll
+  for (int k = 0; k < G0; k++) {
+    nk[k] = ctr->g0count[k];
+    base[k] = pl->g0base[k];
+    lo[k] = FULL ? wave_start_dir(pl, k, cand + base[k], nk[k], dir, dfirst, lane) : 0;
+    ca[k] = cload(k, lo[k] + lane);
+    cb[k] = cload(k, lo[k] + 64 + lane);
+    na[k] = cload(k, lo[k] + 128 + lane);
+    nb2[k] = cload(k, lo[k] + 192 + lane);
+  }
+  WChunk6 cA, cB;
+  wchunk6_fetch(lp, w.u0, lane, cA);
+  wchunk6_fetch(lp, min(w.u0 + W6_UNITS, last_u0), lane, cB);
+  uint32_t nbuf = 0;
+  uint64_t pend_slot = ~0ull;  // slot whose run length waits for the next run start
+  uint32_t pend_u = 0;
+  auto step = [&](const WChunk6 &c, uint32_t u0) {
+    if (MODE == 2) {
+      if (c.v[0].x == 0x557713eeu && c.v[1].y == 7u && c.v[2].z == 3u) po.bits[0] = 1;
+      return;
+    }
+    const uint32_t nrun = chunk6_runs(c, u0, w.u1, lane, S);
+    if (nrun && pend_slot != ~0ull) {
+      if (nbuf + 1 > MBUF) mbuf_flush(S, nbuf, po, lane);
+      mbuf_push(S, nbuf, lane == 0, (uint32_t)pend_slot, pend_u, u0 + S.unit[0] - pend_u, lane);
+      pend_slot = ~0ull;
+    }
+    if (MODE == 1) {
+      if (nrun && S.doc[0] == 0x123456789ull) po.bits[0] = 1;
+      wave_lds_sync();
+      return;
+    }
+    if (!nrun) return;  // nothing consumed; the pending run goes on
+    const uint64_t dmax = S.doc[nrun - 1];
+    auto search = [&](uint64_t d) -> uint32_t {
+      uint32_t a = 0;
+#pragma unroll
+      for (uint32_t st = W6_RUNS; st > 0; st >>= 1) {
+        const uint32_t t = a + st;
+        const uint64_t v = S.doc[min(t, nrun) - 1];
+        if (t <= nrun && v < d) a = t;
+      }
+      return a;
+    };
+    // candidate d (slot `slot`) against the runs; a its lower bound there
+    auto settle = [&](uint64_t d, uint32_t a, uint64_t slot) -> bool {
+      const bool in = d <= dmax;
+      bool hit = false, last = false;
+      uint32_t u = 0, len = 0;
+      if (in && a < nrun && S.doc[a] == d && !S.claim[a]) {
+        S.claim[a] = 1;
+        u = u0 + S.unit[a];
+        if (a + 1 < nrun) {
+          hit = true;
+          len = S.unit[a + 1] - S.unit[a];
+        } else {
+          last = true;  // ends at the next chunk's first run start
+        }
+      }
+      if (nbuf + 64 > MBUF) mbuf_flush(S, nbuf, po, lane);
+      mbuf_push(S, nbuf, hit, (uint32_t)slot, u, len, lane);
+      const uint64_t pm = __ballot(last);
+      if (pm) {
+        const int f = __ffsll((unsigned long long)pm) - 1;
+        pend_slot = __shfl(slot, f, 64);
+        pend_u = u0 + S.unit[nrun - 1];
+      }
+      return in;
+    };
+    // every array's two windows searched at once (eight independent LDS
+    // round trips a step); claims settled array by array, in order
+    uint64_t d0[G0], d1[G0];
+    uint32_t a0[G0], a1[G0];
+#pragma unroll
+    for (int k = 0; k < G0; k++) {
+      d0[k] = lo[k] + lane < nk[k] ? ca[k] : ~0ull;
+      d1[k] = lo[k] + 64 + lane < nk[k] ? cb[k] : ~0ull;
+      a0[k] = a1[k] = 0;
+    }
+#pragma unroll
+    for (uint32_t st = W6_RUNS; st > 0; st >>= 1) {
+#pragma unroll
+      for (int k = 0; k < G0; k++) {
+        const uint32_t t0 = a0[k] + st, t1 = a1[k] + st;
+        const uint64_t v0 = S.doc[min(t0, nrun) - 1], v1 = S.doc[min(t1, nrun) - 1];
+        if (t0 <= nrun && v0 < d0[k]) a0[k] = t0;
+        if (t1 <= nrun && v1 < d1[k]) a1[k] = t1;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < G0; k++) {
+      const bool in0 = settle(d0[k], a0[k], base[k] + lo[k] + lane);
+      const bool in1 = settle(d1[k], a1[k], base[k] + lo[k] + 64 + lane);
+      const uint32_t used = (uint32_t)__popcll(__ballot(in0)) + (uint32_t)__popcll(__ballot(in1));
+      if (used < 128u) {
+        // the next windows: 128 - used candidates left in ca/cb, then na/nb2
+        const uint32_t r0 = used + (uint32_t)lane, r1 = r0 + 64;
+        const int s0 = (int)(r0 & 63);
+        const uint64_t xa = __shfl(ca[k], s0, 64), xb = __shfl(cb[k], s0, 64), xc = __shfl(na[k], s0, 64),
+                       xd = __shfl(nb2[k], s0, 64);
+        const uint32_t q0 = r0 >> 6, q1 = r1 >> 6;  // source window of each: 0 ca, 1 cb, 2 na, 3 nb2
+        ca[k] = q0 == 0 ? xa : q0 == 1 ? xb : xc;
+        cb[k] = q1 == 1 ? xb : q1 == 2 ? xc : xd;
+        lo[k] += used;
+        na[k] = cload(k, lo[k] + 128 + lane);  // used one chunk later
+        nb2[k] = cload(k, lo[k] + 192 + lane);
+      } else {
+        // a chunk meeting more than 128 candidates (dense arrays): the rest
+        // 64 at a time, each window loaded and waited for at once
+        lo[k] += 128;
+        for (;;) {
+          const uint64_t d = lo[k] + lane < nk[k] ? cand[base[k] + lo[k] + lane] : ~0ull;
+          const bool in = settle(d, search(d), base[k] + lo[k] + lane);
+          const uint32_t u = (uint32_t)__popcll(__ballot(in));
+          lo[k] += u;
+          if (u < 64u) break;
+        }
+        ca[k] = cload(k, lo[k] + lane);
+        cb[k] = cload(k, lo[k] + 64 + lane);
+        na[k] = cload(k, lo[k] + 128 + lane);
+        nb2[k] = cload(k, lo[k] + 192 + lane);
+        // all used here, so the merge with the usual path leaves no load of
+        // them pending (the waitcnt pass would then wait for everything)
+        __asm__ volatile("" ::"v"(ca[k]), "v"(cb[k]), "v"(na[k]), "v"(nb2[k]));
+      }
+    }
+    wave_lds_sync();  // the next chunk rewrites the run list
+  };
+  const uint32_t nch = (w.u1 - w.u0 + W6_UNITS - 1) / W6_UNITS;
+  uint32_t u0 = w.u0;
+  for (uint32_t it = 0; it + 2 <= nch; it += 2, u0 += 2 * W6_UNITS) {
+    step(cA, u0);
+    wchunk6_fetch(lp, min(u0 + 2 * W6_UNITS, last_u0), lane, cA);
+    __builtin_amdgcn_sched_barrier(0);
+    step(cB, u0 + W6_UNITS);
+    wchunk6_fetch(lp, min(u0 + 3 * W6_UNITS, last_u0), lane, cB);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if (nch & 1) step(cA, u0);
+  if (pend_slot != ~0ull) {
+    const uint32_t len = lane == 0 ? run_end(L, pend_u + 2) - pend_u : 0;
+    if (nbuf + 1 > MBUF) mbuf_flush(S, nbuf, po, lane);
+    mbuf_push(S, nbuf, lane == 0, (uint32_t)pend_slot, pend_u, len, lane);
+  }
+  mbuf_flush(S, nbuf, po, lane);
+}
+
+// Dense list: probe_by_cand with fewer LDS and vector instructions a chunk,
+// the measured limit of that path (its LDS pipe and VALU issue, not its HBM
+// bytes: a 6 KiB-chunk variant with the same work per byte ran no faster).
+//   * a run start is ONE 64-bit LDS word, docid << 16 | unit: the search
+//     compares it with d << 16 (the unit bits cannot reorder docids), a hit
+//     reads the unit from it and the run's end from the next word (one
+//     ds_read2), so classification writes one word a start, not three;
+//   * the lane shifts of the classification are DPP moves (lane_next) and
+//     the next piece's first bytes scalar reads, not bpermutes;
+//   * claims (a docid goes to the first array holding it) are one bit a run,
+//     cleared with one store a chunk, and only with several arrays;
+//   * the span starts at the host-known first run docid (wave_start_dir).
+struct ProbeLdsP {
+  uint64_t rk[WMAX_RUNS];             // run starts: docid << 16 | unit in the chunk
+  uint32_t cbits[WMAX_RUNS / 32];     // claimed runs
+  uint32_t mslot[MBUF], mu[MBUF], mlen[MBUF];
+};
+__device__ __forceinline__ uint32_t chunk_runs_packed(const WChunk &cur, uint32_t u0, uint32_t u1, int lane, ProbeLdsP &S) {
+  const uint64_t lt = (1ull << lane) - 1;
+  uint32_t nrun = 0;
+#pragma unroll
+  for (int i = 0; i < WPIECES; i++) {
+    uint32_t r[7];
+    r[0] = cur.v[i].x;
+    r[1] = cur.v[i].y;
+    r[2] = cur.v[i].z;
+    r[3] = cur.v[i].w;
+    uint32_t e0, e1, e2;  // lane 63: the next piece's first bytes, or the bytes after the chunk
+    if (i + 1 < WPIECES) {
+      e0 = __builtin_amdgcn_readfirstlane(cur.v[i + 1].x);
+      e1 = __builtin_amdgcn_readfirstlane(cur.v[i + 1].y);
+      e2 = __builtin_amdgcn_readfirstlane(cur.v[i + 1].z);
+    } else {
+      e0 = cur.nb.x;
+      e1 = cur.nb.y;
+      e2 = 0;
+    }
+    r[4] = lane_next(r[0], e0);
+    r[5] = lane_next(r[1], e1);
+    r[6] = lane_next(r[2], e2);
+    const uint32_t P = (uint32_t)i * 1024 + (uint32_t)lane * 16;
+    const uint32_t k0 = (P + 5) / 6;  // first unit starting in [P, P + 16)
+    const uint32_t o0 = k0 * 6 - P;
+    uint32_t a[6];
+#pragma unroll
+    for (int j = 0; j < 6; j++) a[j] = o0 == 4 ? r[j + 1] : __builtin_amdgcn_alignbyte(r[j + 1], r[j], o0);
+    auto byte = [&](int b) -> uint32_t { return (a[b >> 2] >> ((b & 3) * 8)) & 0xff; };
+    auto word = [&](int q) -> uint64_t {  // docid << 16 | unit of the unit at q
+      uint64_t d = 0;
+#pragma unroll
+      for (int b = 4; b >= 0; b--) d = (d << 8) | byte(6 * q + 7 + b);
+      return ((d >> 2) << 16) | (uint64_t)(k0 + (uint32_t)q);
+    };
+    uint32_t starts = 0;
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+      const bool in = 6 * q + o0 < 16 && u0 + k0 + q < u1;
+      if (in && (byte(6 * q + 1) & 0x02) && !(byte(6 * q) & 0x04)) starts |= 1u << q;
+    }
+    // a subset of {0, 1, 2} with no two adjacent: {q} or {0, 2}
+    const uint32_t cnt = __popc(starts);
+    const uint64_t b0 = __ballot(cnt & 1), b1 = __ballot(cnt & 2);
+    const uint32_t o = nrun + (uint32_t)(__popcll(b0 & lt) + 2 * __popcll(b1 & lt));
+    const uint64_t w0 = word(0), w1 = word(1), w2 = word(2);
+    if (cnt) S.rk[o] = (starts & 1) ? w0 : (starts & 2) ? w1 : w2;
+    if (cnt == 2) S.rk[o + 1] = w2;
+    nrun += (uint32_t)(__popcll(b0) + 2 * __popcll(b1));
+  }
+  if (lane < WMAX_RUNS / 32) S.cbits[lane] = 0;
+  wave_lds_sync();
+  return nrun;
+}
+
+template <int MODE, int G0>
+__device__ void probe_by_cand_packed(const DevPlan *__restrict__ pl, const ProbeWork &w, const DevList &L, const uint64_t *cand,
+                                     const Counters *ctr, const uint64_t *dir, ProbeLdsP &S, const ProbeOut &po, int lane) {
+  const int g0n = G0 <= 2 ? G0 : pl->g0n;
+  const uint8_t *lp = L.p;
+  uint32_t nk[G0], lok[G0];
+  uint64_t base[G0], cur[G0], nxt[G0];
+  const uint32_t last_u0 = w.u0 + ((w.u1 - w.u0 - 1) / WCH_UNITS) * WCH_UNITS;
+  WChunk cA, cB;
+  constexpr bool FULL = MODE == 0 || MODE == 5;
+  const uint64_t dfirst = !FULL ? 0 : w.has_dfirst ? w.dfirst : first_run_doc(L, w.u0, w.u1, lane);
+  auto cload = [&](int k, uint32_t i) -> uint64_t {  // candidate i of array k (clamped; validity at use)
+    return cand[base[k] + min(i, max(nk[k], 1u) - 1)];
+  };
+#pragma unroll
+  for (int k = 0; k < G0; k++) {
+    nk[k] = k < g0n ? ctr->g0count[k] : 0;
+    base[k] = k < g0n ? pl->g0base[k] : 0;
+    lok[k] = (FULL && k < g0n) ? wave_start_dir(pl, k, cand + base[k], nk[k], dir, dfirst, lane) : 0;
+    cur[k] = cload(k, lok[k] + lane);
+    nxt[k] = cload(k, lok[k] + 64 + lane);
+  }
+  wchunk_fetch(lp, w.u0, lane, cA);
+  wchunk_fetch(lp, min(w.u0 + WCH_UNITS, last_u0), lane, cB);
+  uint32_t nbuf = 0;
+  uint64_t pend_slot = ~0ull;  // slot whose run length waits for the next run start
+  uint32_t pend_u = 0;
+  auto step = [&](const WChunk &c, uint32_t u0) {
+    if (MODE == 2) {
+      if (c.v[0].x == 0x557713eeu && c.v[1].y == 7u && c.v[2].z == 3u) po.bits[0] = 1;
+      return;
+    }
+    const uint32_t nrun = chunk_runs_packed(c, u0, w.u1, lane, S);
+    if (nrun && pend_slot != ~0ull) {
+      if (nbuf + 1 > MBUF) mbuf_flush(S, nbuf, po, lane);
+      mbuf_push(S, nbuf, lane == 0, (uint32_t)pend_slot, pend_u, u0 + (uint32_t)(S.rk[0] & 0xffff) - pend_u, lane);
+      pend_slot = ~0ull;
+    }
+    if (MODE == 1) {
+      if (nrun && S.rk[0] == 0x123456789ull) po.bits[0] = 1;
+      wave_lds_sync();
+      return;
+    }
+    if (!nrun) return;  // nothing consumed; the pending run goes on
+    const uint64_t kmax = S.rk[nrun - 1] | 0xffffull;  // above every key of the chunk's last docid
+    uint64_t dk[G0];
+    uint32_t pa[G0];
+#pragma unroll
+    for (int k = 0; k < G0; k++) {
+      dk[k] = (k < g0n && lok[k] + lane < nk[k]) ? cur[k] << 16 : ~0ull;
+      pa[k] = 0;
+    }
+    // branchless lower bound of d << 16 among the keys, every array at once
+#pragma unroll
+    for (uint32_t st = WMAX_RUNS; st > 0; st >>= 1) {
+#pragma unroll
+      for (int k = 0; k < G0; k++) {
+        const uint32_t t = pa[k] + st;
+        const uint64_t v = S.rk[min(t, nrun) - 1];
+        if (t <= nrun && v < dk[k]) pa[k] = t;
+      }
+    }
+    auto settle = [&](int k, uint64_t dkey, uint32_t a, uint32_t lo) -> uint32_t {
+      const bool in = dkey <= kmax;
+      bool hit = false, last = false;
+      uint32_t u = 0, len = 0;
+      if (in && a < nrun) {
+        const uint64_t v = S.rk[a], vn = S.rk[min(a + 1, nrun - 1)];
+        const bool claimed = G0 > 1 && k > 0 && ((S.cbits[a >> 5] >> (a & 31)) & 1);
+        if ((v >> 16) == (dkey >> 16) && !claimed) {
+          if (G0 > 1 && k + 1 < g0n) atomicOr(&S.cbits[a >> 5], 1u << (a & 31));
+          u = u0 + (uint32_t)(v & 0xffff);
+          if (a + 1 < nrun) {
+            hit = true;
+            len = (uint32_t)(vn & 0xffff) - (uint32_t)(v & 0xffff);
+          } else {
+            last = true;  // ends at the next chunk's first run start
+          }
+        }
+      }
+      if (nbuf + 64 > MBUF) mbuf_flush(S, nbuf, po, lane);
+      mbuf_push(S, nbuf, hit, (uint32_t)(base[k] + lo + lane), u, len, lane);
+      const uint64_t pm = __ballot(last);
+      if (pm) {
+        pend_slot = base[k] + lo + (uint32_t)(__ffsll((unsigned long long)pm) - 1);
+        pend_u = u0 + (uint32_t)(S.rk[nrun - 1] & 0xffff);
+      }
+      return (uint32_t)__popcll(__ballot(in));
+    };
+#pragma unroll
+    for (int k = 0; k < G0; k++) {
+      if (k >= g0n) break;
+      uint32_t lo = lok[k];
+      const uint32_t used = settle(k, dk[k], pa[k], lo);
+      lo += used;
+      if (used < 64u) {
+        const int sl = (lane + (int)used) & 63;
+        const uint64_t a2 = __shfl(cur[k], sl, 64), b2 = __shfl(nxt[k], sl, 64);
+        cur[k] = lane + used < 64u ? a2 : b2;
+        lok[k] = lo;
+        nxt[k] = cload(k, lo + 64 + lane);  // used one chunk later
+      } else {
+        // a chunk meeting more than 64 candidates (dense arrays)
+        for (;;) {
+          const uint64_t d = lo + lane < nk[k] ? cand[base[k] + lo + lane] << 16 : ~0ull;
+          uint32_t a = 0;
+#pragma unroll
+          for (uint32_t st = WMAX_RUNS; st > 0; st >>= 1) {
+            const uint32_t t = a + st;
+            const uint64_t v = S.rk[min(t, nrun) - 1];
+            if (t <= nrun && v < d) a = t;
+          }
+          const uint32_t u2 = settle(k, d, a, lo);
+          lo += u2;
+          if (u2 < 64u) break;
+        }
+        lok[k] = lo;
+        cur[k] = cload(k, lo + lane);
+        nxt[k] = cload(k, lo + 64 + lane);
+        __asm__ volatile("" ::"v"(cur[k]), "v"(nxt[k]));
+      }
+    }
+    wave_lds_sync();  // the next chunk rewrites the run list
+  };
+  const uint32_t nch = (w.u1 - w.u0 + WCH_UNITS - 1) / WCH_UNITS;
+  uint32_t u0 = w.u0;
+  for (uint32_t it = 0; it + 2 <= nch; it += 2, u0 += 2 * WCH_UNITS) {
+    step(cA, u0);
+    wchunk_fetch(lp, min(u0 + 2 * WCH_UNITS, last_u0), lane, cA);
+    __builtin_amdgcn_sched_barrier(0);
+    step(cB, u0 + WCH_UNITS);
+    wchunk_fetch(lp, min(u0 + 3 * WCH_UNITS, last_u0), lane, cB);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if (nch & 1) step(cA, u0);
+  if (pend_slot != ~0ull) {
+    const uint32_t len = lane == 0 ? run_end(L, pend_u + 2) - pend_u : 0;
+    if (nbuf + 1 > MBUF) mbuf_flush(S, nbuf, po, lane);
+    mbuf_push(S, nbuf, lane == 0, (uint32_t)pend_slot, pend_u, len, lane);
+  }
+  mbuf_flush(S, nbuf, po, lane);
+}
+
 // Sparse list: each run start looks its docid up in the arrays, in order;
 // the first array holding it takes the run.
 template <int G0>
@@ -1310,14 +1779,24 @@ __device__ void probe_by_run(const DevPlan *__restrict__ pl, const ProbeWork &w,
 // MODE (diagnostic, GBGPU_PROBE_MODE): 0 full, 1 stop after the run-start
 // compaction, 2 load chunks only, 3 skip the run-driven lists.
 template <int MODE, int G0>
-__global__ void __launch_bounds__(64 * PW) k_probe(const DevPlan *__restrict__ pl, const ProbeWork *work, uint32_t nwork,
+__global__ void __launch_bounds__(64 * PW, (G0 <= 2 && MODE == 11) ? 3 : 1) k_probe(const DevPlan *__restrict__ pl, const ProbeWork *work, uint32_t nwork,
                                                    const uint64_t *cand, uint32_t *bits, uint32_t nwords, Loc *loc,
                                                    const Counters *ctr, const uint64_t *dir) {
-  constexpr bool HPATH = G0 <= HPATH_G0 && MODE != 3;
+  // the bucket-table path (probe_by_cand_hash) is a measured alternative,
+  // slower than the run-list search at config 2 (188 vs 80 us): diagnostic
+  // GBGPU_PROBE_MODE=10 only
+  constexpr bool HPATH = G0 <= HPATH_G0 && MODE == 10;
   // a wave runs one of the paths: their LDS overlaps
+  constexpr bool WIDE = G0 <= 2 && MODE == 11;  // diagnostic: 6 KiB chunks (slower, see probe_by_cand_wide)
+  constexpr bool PACKED = MODE == 0 || MODE == 1 || MODE == 2 || MODE == 5;
+  struct None {
+    uint8_t x;
+  };
   union WaveLds {
     ProbeLds run;
-    HashLds<HPATH ? G0 : 1> hash;
+    typename std::conditional<HPATH, HashLds<G0 <= HPATH_G0 ? G0 : 1>, None>::type hash;
+    typename std::conditional<WIDE, ProbeLds6, None>::type wide;
+    typename std::conditional<PACKED, ProbeLdsP, None>::type packed;
   };
   __shared__ WaveLds s_w[PW];
   // the wave's index is uniform over the wave: said so, every value derived
@@ -1335,12 +1814,16 @@ __global__ void __launch_bounds__(64 * PW) k_probe(const DevPlan *__restrict__ p
   po.l = w.list;
   po.on = MODE == 5 ? 0 : 1;
   if (L.probe == PROBE_BY_RUN) {
-    if (MODE == 0) probe_by_run<G0>(pl, w, L, cand, ctr, dir, s_w[wid].run, po, lane);
+    if (MODE == 0 || MODE >= 10) probe_by_run<G0>(pl, w, L, cand, ctr, dir, s_w[wid].run, po, lane);
   } else {
     if constexpr (HPATH)
       probe_by_cand_hash<MODE, G0>(pl, w, L, cand, ctr, dir, s_w[wid].hash, po, lane);
+    else if constexpr (WIDE)
+      probe_by_cand_wide<0, G0 <= 2 ? G0 : 2>(pl, w, L, cand, ctr, dir, s_w[wid].wide, po, lane);
+    else if constexpr (PACKED)
+      probe_by_cand_packed<MODE, G0>(pl, w, L, cand, ctr, dir, s_w[wid].packed, po, lane);
     else
-      probe_by_cand<MODE == 3 ? 0 : MODE, G0>(pl, w, L, cand, ctr, dir, s_w[wid].run, po, lane);
+      probe_by_cand<(MODE == 3 || MODE == 12) ? 0 : MODE, G0>(pl, w, L, cand, ctr, dir, s_w[wid].run, po, lane);
   }
 }
 
@@ -4903,21 +5386,25 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   q.pw.clear();
   int64_t scan = 0;
   uint64_t probe_chunks = 0;
+  // candidate-driven lists walk 6 KiB chunks when the smallest group has at
+  // most two candidate arrays (probe_by_cand_wide), else 3 KiB
+  const bool wide = P.g0n <= 2 && ctx->probe_mode == 11;
+  const uint32_t cunits = wide ? (uint32_t)W6_UNITS : (uint32_t)WCH_UNITS;
   for (int id = 0; id < P.nlists; id++) {
     scan += (int64_t)P.lists[id].units * 6;
-    if (P.lists[id].probe == PROBE_BY_CAND) probe_chunks += (P.lists[id].units + WCH_UNITS - 1) / WCH_UNITS;
+    if (P.lists[id].probe == PROBE_BY_CAND) probe_chunks += (P.lists[id].units + cunits - 1) / cunits;
   }
   // one wave per span of S chunks: about PROBE_WAVES spans over all probed
   // lists, so every CU holds ~24 waves and each amortises its initial
   // candidate search over several chunks
-  const uint64_t pwaves = ctx->probe_waves ? (uint64_t)ctx->probe_waves : PROBE_WAVES;
+  const uint64_t pwaves = ctx->probe_waves ? (uint64_t)ctx->probe_waves : wide ? PROBE_WAVES_WIDE : PROBE_WAVES;
   const uint32_t S = (uint32_t)std::max<uint64_t>(1, (probe_chunks + pwaves - 1) / pwaves);
   for (int id = 0; id < P.nlists; id++) {
     if (!P.lists[id].probe) continue;
     const uint32_t units = P.lists[id].units;
     // a run-driven chunk costs a few dependent lookups: one chunk per wave
     const uint32_t rspan = ctx->probe_runspan > 0 ? (uint32_t)ctx->probe_runspan : 1u;
-    const uint32_t span = WCH_UNITS * (P.lists[id].probe == PROBE_BY_RUN ? rspan : S);
+    const uint32_t span = P.lists[id].probe == PROBE_BY_RUN ? WCH_UNITS * rspan : cunits * S;
     const std::vector<uint64_t> *gf = lent[id]->gfirst.get();
     for (uint32_t u = 0; u < units; u += span) {
       ProbeWork pw{(uint32_t)id, u, std::min(units, u + span), 0u, ~0ull};
@@ -5036,7 +5523,9 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
                      q.cunit.as<uint32_t>(), dctr, ng0, q.dir.as<uint64_t>());
   if (ctx->profiling) HIPCHECK(hipEventRecord(q.ev[1], st));
   if (!q.pw.empty()) {
-    auto kp = ctx->probe_mode == 4   ? k_probe<0, MAXG0>  // diagnostic: the run-list search path
+    auto kp = ctx->probe_mode == 11  ? (P.g0n <= 1 ? k_probe<11, 1> : k_probe<11, 2>)  // diagnostic: 6 KiB chunks
+              : ctx->probe_mode == 10 ? (P.g0n <= 2 ? k_probe<10, 2> : k_probe<10, 4>)  // diagnostic: bucket tables
+              : ctx->probe_mode == 4 ? k_probe<12, MAXG0>  // diagnostic: the unpacked run list
               : ctx->probe_mode == 9 ? k_probe<2, 2>
               : ctx->probe_mode == 8 ? k_probe<1, 2>
               : ctx->probe_mode == 5 ? k_probe<5, 2>
