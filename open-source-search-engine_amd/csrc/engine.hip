@@ -1530,28 +1530,34 @@ __device__ __forceinline__ uint32_t chunk_runs_packed(const WChunk &cur, uint32_
     uint32_t a[6];
 #pragma unroll
     for (int j = 0; j < 6; j++) a[j] = o0 == 4 ? r[j + 1] : __builtin_amdgcn_alignbyte(r[j + 1], r[j], o0);
-    auto byte = [&](int b) -> uint32_t { return (a[b >> 2] >> ((b & 3) * 8)) & 0xff; };
-    auto word = [&](int q) -> uint64_t {  // docid << 16 | unit of the unit at q
-      uint64_t d = 0;
-#pragma unroll
-      for (int b = 4; b >= 0; b--) d = (d << 8) | byte(6 * q + 7 + b);
-      return ((d >> 2) << 16) | (uint64_t)(k0 + (uint32_t)q);
-    };
-    uint32_t starts = 0;
-#pragma unroll
-    for (int q = 0; q < 3; q++) {
-      const bool in = 6 * q + o0 < 16 && u0 + k0 + q < u1;
-      if (in && (byte(6 * q + 1) & 0x02) && !(byte(6 * q) & 0x04)) starts |= 1u << q;
-    }
+    // a unit at q starts at byte 6q: bytes 0-1 (flags) are byte pair 0 of
+    // a[0] (q=0), pair 1 of a[1] (q=1), pair 0 of a[3] (q=2)
+    const uint32_t h0 = a[0], h1 = a[1] >> 16, h2 = a[3];
+    const bool in0 = o0 < 16 && u0 + k0 < u1, in1 = o0 + 6 < 16 && u0 + k0 + 1 < u1, in2 = o0 + 12 < 16 && u0 + k0 + 2 < u1;
+    const bool s0 = in0 && (h0 & 0x200u) && !(h0 & 0x4u);
+    const bool s1 = in1 && (h1 & 0x200u) && !(h1 & 0x4u);
+    const bool s2 = in2 && (h2 & 0x200u) && !(h2 & 0x4u);
     // a subset of {0, 1, 2} with no two adjacent: {q} or {0, 2}
-    const uint32_t cnt = __popc(starts);
+    const uint32_t cnt = (uint32_t)s0 + (uint32_t)s1 + (uint32_t)s2;
     const uint64_t b0 = __ballot(cnt & 1), b1 = __ballot(cnt & 2);
     const uint32_t o = nrun + (uint32_t)(__popcll(b0 & lt) + 2 * __popcll(b1 & lt));
-    const uint64_t w0 = word(0), w1 = word(1), w2 = word(2);
-    if (cnt) S.rk[o] = (starts & 1) ? w0 : (starts & 2) ? w1 : w2;
-    if (cnt == 2) S.rk[o + 1] = w2;
+    // the docid (key bytes 7..11) of the first start and of a start at q=2:
+    // q=0 bytes 7..11 = a[1].3, a[2].0-3; q=1 bytes 13..17 = a[3].1-3,
+    // a[4].0-1; q=2 bytes 19..23 = a[4].3, a[5].0-3
+    const uint32_t lo0 = s0 ? __builtin_amdgcn_alignbyte(a[2], a[1], 3) : s1 ? __builtin_amdgcn_alignbyte(a[4], a[3], 1)
+                                                                           : __builtin_amdgcn_alignbyte(a[5], a[4], 3);
+    const uint32_t hi0 = s0 ? a[2] >> 24 : s1 ? (a[4] >> 8) & 0xff : a[5] >> 24;
+    const uint32_t q0 = s0 ? 0u : s1 ? 1u : 2u;
+    const uint64_t wa = ((((uint64_t)hi0 << 32) | lo0) >> 2) << 16 | (uint64_t)(k0 + q0);
+    const uint64_t wb = ((((uint64_t)(a[5] >> 24) << 32) | __builtin_amdgcn_alignbyte(a[5], a[4], 3)) >> 2) << 16 |
+                        (uint64_t)(k0 + 2);
+    if (cnt) S.rk[o] = wa;
+    if (cnt == 2) S.rk[o + 1] = wb;
     nrun += (uint32_t)(__popcll(b0) + 2 * __popcll(b1));
   }
+  // keys past the runs read as ~0 (above every candidate key): the search
+  // needs no bounds test
+  for (uint32_t x = nrun + (uint32_t)lane; x < WMAX_RUNS; x += 64) S.rk[x] = ~0ull;
   if (lane < WMAX_RUNS / 32) S.cbits[lane] = 0;
   wave_lds_sync();
   return nrun;
@@ -1609,16 +1615,17 @@ __device__ void probe_by_cand_packed(const DevPlan *__restrict__ pl, const Probe
       dk[k] = (k < g0n && lok[k] + lane < nk[k]) ? cur[k] << 16 : ~0ull;
       pa[k] = 0;
     }
-    // branchless lower bound of d << 16 among the keys, every array at once
+    // branchless lower bound of d << 16 among the keys (padded with ~0 to
+    // WMAX_RUNS), every array at once
 #pragma unroll
-    for (uint32_t st = WMAX_RUNS; st > 0; st >>= 1) {
+    for (uint32_t st = WMAX_RUNS / 2; st > 0; st >>= 1) {
 #pragma unroll
-      for (int k = 0; k < G0; k++) {
-        const uint32_t t = pa[k] + st;
-        const uint64_t v = S.rk[min(t, nrun) - 1];
-        if (t <= nrun && v < dk[k]) pa[k] = t;
-      }
+      for (int k = 0; k < G0; k++)
+        if (S.rk[pa[k] + st - 1] < dk[k]) pa[k] += st;
     }
+#pragma unroll
+    for (int k = 0; k < G0; k++)
+      if (S.rk[pa[k]] < dk[k]) pa[k]++;  // the last position (255 at most)
     auto settle = [&](int k, uint64_t dkey, uint32_t a, uint32_t lo) -> uint32_t {
       const bool in = dkey <= kmax;
       bool hit = false, last = false;
@@ -1664,11 +1671,9 @@ __device__ void probe_by_cand_packed(const DevPlan *__restrict__ pl, const Probe
           const uint64_t d = lo + lane < nk[k] ? cand[base[k] + lo + lane] << 16 : ~0ull;
           uint32_t a = 0;
 #pragma unroll
-          for (uint32_t st = WMAX_RUNS; st > 0; st >>= 1) {
-            const uint32_t t = a + st;
-            const uint64_t v = S.rk[min(t, nrun) - 1];
-            if (t <= nrun && v < d) a = t;
-          }
+          for (uint32_t st = WMAX_RUNS / 2; st > 0; st >>= 1)
+            if (S.rk[a + st - 1] < d) a += st;
+          if (S.rk[a] < d) a++;
           const uint32_t u2 = settle(k, d, a, lo);
           lo += u2;
           if (u2 < 64u) break;
