@@ -1879,9 +1879,10 @@ __global__ void k_range_filter(const DevPlan *__restrict__ pl, uint32_t rbits, u
 // lanes run the scorers in lockstep, so its time is its largest lane's.
 // Bucket 0 holds the largest and is scored first.  Buckets 0-2 (more units
 // than a lane's rc records) are scored 8, 16 and 32 to a wave, so each
-// survivor gets 8, 4 or 2 lanes' worth of LDS records.  ORDERED (site
-// clustering: the TopTree replay walks survivors in docid order, Posdb.cpp:
-// 6137-6140) puts every survivor in one bucket, in slot order.
+// survivor gets 8, 4 or 2 lanes' worth of LDS records.  Site clustering
+// (the TopTree replay walks survivors in docid order, Posdb.cpp:6137-6140)
+// takes the same buckets plus each record's slot-order rank (sv_ord):
+// k_bound writes the replay entries in slot order from it.
 constexpr int NBKT = 8;
 __host__ __device__ __forceinline__ int size_bucket(uint32_t u, uint32_t rc) {
   return u > 4 * rc ? 0 : u > 2 * rc ? 1 : u > rc ? 2 : 2 * u > rc ? 3 : 3 * u > rc ? 4 : 4 * u > rc ? 5 : 6 * u > rc ? 6 : 7;
@@ -2074,7 +2075,6 @@ __device__ __forceinline__ void cmp_stage(const DevPlan *__restrict__ pl, const 
 // Pass 1: per block of CTILE slots (one bitmap word a thread), the survivors
 // per size bucket, the lists with a run in some survivor, the run units and
 // the re-shrink partials.
-template <bool ORDERED>
 __global__ void __launch_bounds__(CB) k_cmp_count(const DevPlan *__restrict__ pl, Counters *ctr,
                                                   const uint32_t *__restrict__ cunit, const uint32_t *__restrict__ bits,
                                                   uint32_t nwords, const Loc *__restrict__ loc,
@@ -2113,7 +2113,7 @@ __global__ void __launch_bounds__(CB) k_cmp_count(const DevPlan *__restrict__ pl
       const uint32_t lm = S.lm[i];
       const bool own = (lm >> pl->g0list[0]) & 1;
       const uint32_t u = cmp_units(pl, ctr, cunit, loc, s, lm, own);
-      atomicAdd(&s_cnt[ORDERED ? 0 : size_bucket(u, rc)], 1u);
+      atomicAdd(&s_cnt[size_bucket(u, rc)], 1u);
       any |= lm;
       usum += u;
       if (xmask) {
@@ -2189,8 +2189,8 @@ __global__ void __launch_bounds__(CB) k_cmp_count(const DevPlan *__restrict__ pl
 // its run locations ([pos][nl]), so k_score reads its survivors' data
 // contiguously.  Each block sums the counts of the blocks before it (its
 // offsets) and of all blocks (the bucket starts); block 0 publishes the
-// totals.
-template <bool ORDERED>
+// totals.  sv_ord (site clustering): each record's survivor's rank in slot
+// order, where the replay wants it.
 __global__ void __launch_bounds__(CB) k_cmp_write(const DevPlan *__restrict__ pl, Counters *__restrict__ ctr,
                                                   const uint32_t *__restrict__ cunit, const uint32_t *__restrict__ bits,
                                                   uint32_t nwords, const Loc *__restrict__ loc,
@@ -2198,7 +2198,7 @@ __global__ void __launch_bounds__(CB) k_cmp_write(const DevPlan *__restrict__ pl
                                                   const BlkInfo *__restrict__ blk, uint32_t nblk,
                                                   uint32_t *__restrict__ sv_slot, uint32_t *__restrict__ sv_lm,
                                                   uint32_t *__restrict__ sv_u, uint64_t *__restrict__ sv_doc,
-                                                  Loc *__restrict__ sv_loc) {
+                                                  Loc *__restrict__ sv_loc, uint32_t *__restrict__ sv_ord) {
   __shared__ CmpStage S;
   __shared__ uint32_t tmp[CB / 64];
   __shared__ uint32_t s_pre[NBKT], s_tot[NBKT], s_carry[NBKT];
@@ -2318,6 +2318,9 @@ __global__ void __launch_bounds__(CB) k_cmp_write(const DevPlan *__restrict__ pl
       boff[b] = s_pre[b];
     }
   }
+  uint32_t ord0 = 0;  // survivors of the blocks before this one
+#pragma unroll
+  for (int b = 0; b < NBKT; b++) ord0 += boff[b];
   const uint32_t w = blockIdx.x * CB + threadIdx.x;
   CmpWord c;
   c.surv = 0;
@@ -2339,7 +2342,7 @@ __global__ void __launch_bounds__(CB) k_cmp_write(const DevPlan *__restrict__ pl
       const uint32_t lm = act ? S.lm[i] : 0;
       const bool own = (lm >> l0) & 1;
       const uint32_t u = act ? cmp_units(pl, ctr, cunit, loc, s, lm, own) : 0;
-      const uint32_t b = ORDERED ? 0u : (uint32_t)size_bucket(u, rc);
+      const uint32_t b = (uint32_t)size_bucket(u, rc);
       uint32_t rk = 0;
 #pragma unroll
       for (int bb = 0; bb < NBKT; bb++) {
@@ -2365,6 +2368,7 @@ __global__ void __launch_bounds__(CB) k_cmp_write(const DevPlan *__restrict__ pl
         sv_lm[pos] = lm;
         sv_u[pos] = u;
         sv_doc[pos] = cand[s];
+        if (sv_ord) sv_ord[pos] = ord0 + base + i;
         for (uint32_t xm = lm; xm; xm &= xm - 1) {
           const int l = __ffs(xm) - 1;
           sv_loc[(uint64_t)pos * nl + l] = cmp_loc(pl, ctr, cunit, loc, s, l, own);
@@ -3638,15 +3642,17 @@ __device__ void lane_sort(uint16_t (*col)[64], int n, int lane) {
   }
 }
 
-// rep != nullptr: the survivors are in docid order already, so the bound
-// goes straight into the replay entry; else into sbound for k_rank.  A block
+// The replay entry of record i goes to its slot-order rank sv_ord[i]: with
+// one candidate array that is docid order (the replay's input), else k_rank
+// merges the arrays (oslot: each rank's slot).  A block
 // of BND_WAVES waves, one lane per survivor (the ring restated above); the
 // survivors whose lists overflow a lane's slot columns then take the wave
 // one at a time, over the 4096-slot ring.
 __global__ void __launch_bounds__(64 * BND_WAVES) k_bound(const DevPlan *__restrict__ pl, const Counters *ctr,
                                                        const uint32_t *sv_slot, const uint32_t *sv_lm,
-                                                       const Loc *sv_loc, float *sbound, const uint32_t *skey,
-                                                       const uint64_t *sdoc, const uint8_t *sflag, uint4 *rep) {
+                                                       const Loc *sv_loc, const uint32_t *sv_ord, const uint32_t *skey,
+                                                       const uint64_t *sdoc, const uint8_t *sflag, uint4 *rep,
+                                                       uint32_t *oslot) {
   __shared__ __attribute__((aligned(16))) uint8_t s_ring[BND_WAVES][RING];
   __shared__ uint16_t s_ms[BND_WAVES][BL_SLOTS][64], s_gs[BND_WAVES][BL_SLOTS][64];
   stage_weights(&c_weights);
@@ -3754,8 +3760,9 @@ __global__ void __launch_bounds__(64 * BND_WAVES) k_bound(const DevPlan *__restr
       if (lane == j) B = Bw;
     }
     if (i < nsurv) {
-      if (rep) rep[i] = rep_entry(skey[i], B, sdoc[i], sflag[i] != 0);
-      else sbound[i] = B;
+      const uint32_t o = sv_ord[i];
+      rep[o] = rep_entry(skey[i], B, sdoc[i], sflag[i] != 0);
+      if (oslot) oslot[o] = sv_slot[i];
     }
   }
 }
@@ -3772,31 +3779,34 @@ __device__ __forceinline__ uint32_t lower_bound_u32(const uint32_t *a, uint32_t 
   }
   return lo;
 }
-__device__ __forceinline__ uint32_t lower_bound_u64(const uint64_t *a, uint32_t lo, uint32_t hi, uint64_t v) {
+
+// repo: the entries in slot order (k_bound), oslot their slots
+__device__ __forceinline__ uint64_t rep_doc(const uint4 &e) { return ((uint64_t)(e.w & 0x7fffffffu) << 32) | e.z; }
+__device__ __forceinline__ uint32_t rep_lower(const uint4 *a, uint32_t lo, uint32_t hi, uint64_t v) {
   const uint32_t b = lo;
   while (lo < hi) {
     const uint32_t mid = (lo + hi) >> 1;
-    if (a[mid] < v) lo = mid + 1;
+    if (rep_doc(a[mid]) < v) lo = mid + 1;
     else hi = mid;
   }
   return lo - b;
 }
-
-__global__ void k_rank(const DevPlan *__restrict__ pl, const Counters *ctr, const uint32_t *sv_slot, const uint64_t *sdoc,
-                       const uint32_t *skey, const uint8_t *sflag, const float *sbound, uint4 *rep) {
+__global__ void k_rank(const DevPlan *__restrict__ pl, const Counters *ctr, const uint32_t *oslot, const uint4 *repo,
+                       uint4 *rep) {
   const uint32_t nsurv = (uint32_t)(ctr->surv_top >> 36);
   const int g0n = pl->g0n;
   uint32_t sb[MAXG0 + 1];
   for (int k = 0; k <= g0n; k++)
-    sb[k] = k == g0n ? nsurv : lower_bound_u32(sv_slot, nsurv, (uint32_t)pl->g0base[k]);
+    sb[k] = k == g0n ? nsurv : lower_bound_u32(oslot, nsurv, (uint32_t)pl->g0base[k]);
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nsurv; i += gridDim.x * blockDim.x) {
     int k = 0;
     while (k + 1 < g0n && i >= sb[k + 1]) k++;
-    const uint64_t d = sdoc[i];
+    const uint4 e = repo[i];
+    const uint64_t d = rep_doc(e);
     uint32_t pos = i - sb[k];
     for (int k2 = 0; k2 < g0n; k2++)
-      if (k2 != k) pos += lower_bound_u64(sdoc, sb[k2], sb[k2 + 1], d);
-    rep[pos] = rep_entry(skey[i], sbound[i], d, sflag[i] != 0);
+      if (k2 != k) pos += rep_lower(repo, sb[k2], sb[k2 + 1], d);
+    rep[pos] = e;
   }
 }
 
@@ -4129,6 +4139,418 @@ __global__ void __launch_bounds__(64) k_tree_replay(Counters *ctr, const uint4 *
       T->n = n;
       T->vcount = vcount;
     }
+  }
+}
+
+// ------------------------------------- site clustering: the block replay
+// k_tree_seq: the same docid-order loop as k_tree_replay for a whole-range
+// query (one pass: TREE_INIT | TREE_FINAL), split in two so that one wave's
+// serial work is only the offers that can change the tree:
+//   * all SQ_W waves of the block rule out, in parallel, the entries of a
+//     segment (SQ_SEG entries) that cannot be offered under ANY state the
+//     tree can reach from the state at the segment's start, and stage the
+//     others (the candidates) in LDS in docid order;
+//   * wave 0 (the sequencer) walks the candidates with the exact per-docid
+//     test of k_tree_replay, and publishes the new state.
+// Why skipping the others is exact: once the tree is full (m_vcount >=
+// m_docsWanted after an add), an add keeps it full (every node it deletes
+// takes at most 1.0 off m_vcount, and deletes stop below docsWanted + 1:
+// TopTree.cpp:446), and its last node never gets worse (a node is only
+// inserted above the last one, and deletes only remove nodes); so an entry
+// not better than the segment-start last node is never better than the last
+// node later, and minWinningScore, reassigned only to the last node's score
+// (Posdb.cpp:7699-7704), stays >= L = min(its value, that score).  One
+// exception: the m_numNodes delete (TopTree.cpp:446) can take m_vcount
+// below docsWanted; the sequencer then walks the rest of the segment raw.
+// The tree itself is register-resident in the sequencer: node i (best
+// first) at column i >> 6, lane i & 63, K columns; inserts and deletes are
+// DPP lane shifts, the lower bound K ballots.  A tree outgrowing 64 K nodes
+// sets tree_err = 2 and the host replays the query with k_tree_replay.
+constexpr int SQ_W = 8;                              // waves per block
+constexpr int SQ_E = 8;                              // entries per lane and segment
+constexpr uint32_t SQ_SEG = (uint32_t)SQ_W * 64 * SQ_E;  // 4096: a segment-local index fits 12 bits
+constexpr uint32_t TREE_ERR_REG = 2;                 // tree_err: the register tree overflowed
+
+__device__ __forceinline__ uint32_t rl_u32(uint32_t v, uint32_t l) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
+}
+__device__ __forceinline__ float rl_f(float v, uint32_t l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), (int)l));
+}
+__device__ __forceinline__ uint64_t rl_u64(uint64_t v, uint32_t l) {
+  return (uint64_t)rl_u32((uint32_t)(v >> 32), l) << 32 | rl_u32((uint32_t)v, l);
+}
+// lane L takes lane L-1's value, lane 0 `edge` (wave_shr:1)
+__device__ __forceinline__ uint64_t shr_u64(uint64_t x, uint64_t edge) {
+  return (uint64_t)lane_prev((uint32_t)(x >> 32), (uint32_t)(edge >> 32)) << 32 | lane_prev((uint32_t)x, (uint32_t)edge);
+}
+// lane L takes lane L+1's value, lane 63 `edge` (wave_shl:1)
+__device__ __forceinline__ uint64_t shl_u64(uint64_t x, uint64_t edge) {
+  return (uint64_t)lane_next((uint32_t)(x >> 32), (uint32_t)(edge >> 32)) << 32 | lane_next((uint32_t)x, (uint32_t)edge);
+}
+
+// A node's order key: the replay entry's score key (order-preserving uint32
+// of the float score, or of the int32 m_intScore) with -0.0 folded onto
+// +0.0, so that key order is the TopTree's score order (float compares;
+// scores are never NaN).  A -0.0 score is reported as +0.0.
+__device__ __forceinline__ uint32_t node_key(uint32_t key, bool ints) {
+  return (!ints && key == 0x7fffffffu) ? 0x80000000u : key;
+}
+__device__ __forceinline__ bool key_better(uint32_t k1, uint64_t d1, uint32_t k2, uint64_t d2) {
+  return k1 > k2 || (k1 == k2 && d1 < d2);
+}
+// tree_cs of a node key
+__device__ __forceinline__ uint32_t key_cs(uint32_t k, bool ints) {
+  return ints ? (k ^ 0x80000000u) : tree_cs(key_score(k), false);
+}
+
+template <int K, bool INTS>
+struct RegTree {
+  uint32_t kk[K];  // node keys
+  uint64_t d[K];
+  int32_t dom[4];  // m_domCount: domain h at column h >> 6, lane h & 63
+  uint32_t n;
+  float vcount;
+  uint32_t tk;     // the last node (n > 0), kept in step with the columns
+  uint64_t td;
+
+  // node i (uniform): every column read at lane i & 63, then selected -- no
+  // branches for up to four columns; a uniform branch ladder beyond
+  __device__ __forceinline__ uint32_t nk(uint32_t i) const {
+    uint32_t r = rl_u32(kk[0], i & 63);
+#pragma unroll
+    for (int k = 1; k < K; k++) {
+      if (K > 4 && (i >> 6) != (uint32_t)k) continue;
+      const uint32_t v = rl_u32(kk[k], i & 63);
+      r = (i >> 6) == (uint32_t)k ? v : r;
+    }
+    return r;
+  }
+  __device__ __forceinline__ uint64_t nd(uint32_t i) const {
+    uint64_t r = rl_u64(d[0], i & 63);
+#pragma unroll
+    for (int k = 1; k < K; k++) {
+      if (K > 4 && (i >> 6) != (uint32_t)k) continue;
+      const uint64_t v = rl_u64(d[k], i & 63);
+      r = (i >> 6) == (uint32_t)k ? v : r;
+    }
+    return r;
+  }
+  __device__ __forceinline__ int32_t domc(uint32_t h) const {
+    const uint32_t l = h & 63, c = h >> 6;
+    const int32_t c0 = (int32_t)rl_u32((uint32_t)dom[0], l), c1 = (int32_t)rl_u32((uint32_t)dom[1], l);
+    const int32_t c2 = (int32_t)rl_u32((uint32_t)dom[2], l), c3 = (int32_t)rl_u32((uint32_t)dom[3], l);
+    return c == 0 ? c0 : c == 1 ? c1 : c == 2 ? c2 : c3;
+  }
+  __device__ __forceinline__ void domadd(uint32_t h, int32_t v, int lane) {
+    const bool me = (uint32_t)lane == (h & 63);
+#pragma unroll
+    for (int c = 0; c < 4; c++) dom[c] += (me & ((h >> 6) == (uint32_t)c)) ? v : 0;
+  }
+  // nodes better than (k, dd): the insert position (the array is sorted)
+  __device__ __forceinline__ uint32_t lower(uint32_t k0, uint64_t dd, int lane) const {
+    uint32_t p = 0;
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      const uint32_t i = (uint32_t)k * 64 + (uint32_t)lane;
+      p += (uint32_t)__popcll(__ballot((i < n) & key_better(kk[k], d[k], k0, dd)));
+    }
+    return p;
+  }
+  __device__ __forceinline__ void insert(uint32_t p, uint32_t k0, uint64_t dd, int lane) {
+#pragma unroll
+    for (int k = K - 1; k >= 0; k--) {
+      if ((uint32_t)k * 64 > n || (uint32_t)(k + 1) * 64 <= p) continue;  // untouched column
+      const uint32_t ek = k > 0 ? rl_u32(kk[k > 0 ? k - 1 : 0], 63) : 0u;  // the previous column's last node
+      const uint64_t ed = k > 0 ? rl_u64(d[k > 0 ? k - 1 : 0], 63) : 0ull;
+      const uint32_t sk = lane_prev(kk[k], ek);
+      const uint64_t sd = shr_u64(d[k], ed);
+      const uint32_t i = (uint32_t)k * 64 + (uint32_t)lane;
+      kk[k] = i > p ? sk : i == p ? k0 : kk[k];
+      d[k] = i > p ? sd : i == p ? dd : d[k];
+    }
+    n++;
+  }
+  // deleteNode's count bookkeeping (TopTree.cpp:543-547) for a node of
+  // domain h
+  __device__ __forceinline__ void uncount(uint32_t h, const TreeParams &tp, int lane) {
+    const int32_t c = domc(h);
+    if (c < tp.cap) vcount -= 1.0;
+    else if (c == tp.cap) vcount -= tp.partial;
+    domadd(h, -1, lane);
+  }
+  __device__ __forceinline__ void retail() {
+    if (n) {
+      tk = nk(n - 1);
+      td = nd(n - 1);
+    }
+  }
+  // node q (not the last) out: the columns from q's shift down one
+  __device__ __forceinline__ void remove(uint32_t q, int lane) {
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      if ((uint32_t)(k + 1) * 64 <= q || (uint32_t)k * 64 >= n) continue;
+      const uint32_t ek = k + 1 < K ? rl_u32(kk[k + 1 < K ? k + 1 : k], 0) : 0u;  // the next column's first node
+      const uint64_t ed = k + 1 < K ? rl_u64(d[k + 1 < K ? k + 1 : k], 0) : 0ull;
+      const uint32_t sk = lane_next(kk[k], ek);
+      const uint64_t sd = shl_u64(d[k], ed);
+      const uint32_t i = (uint32_t)k * 64 + (uint32_t)lane;
+      kk[k] = i >= q ? sk : kk[k];
+      d[k] = i >= q ? sd : d[k];
+    }
+    n--;
+  }
+  // the domain's minimum m_t2 key (uint32 score, docid) -- m_domMinNode
+  // (TopTree.cpp:355-385) -- and that node
+  __device__ __forceinline__ void dom_min(uint32_t h, int lane, uint32_t &mc, uint64_t &md, uint32_t &mk) const {
+    mc = 0xffffffffu;
+    md = ~0ull;
+    mk = 0;
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      const uint32_t i = (uint32_t)k * 64 + (uint32_t)lane;
+      if (i >= n || dom_hash8(d[k]) != h) continue;
+      const uint32_t ct = key_cs(kk[k], INTS);
+      if (ct < mc || (ct == mc && d[k] < md)) {
+        mc = ct;
+        md = d[k];
+        mk = kk[k];
+      }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const uint32_t oc = __shfl_xor(mc, off, 64);
+      const uint64_t od = __shfl_xor(md, off, 64);
+      const uint32_t ok = __shfl_xor(mk, off, 64);
+      if (oc < mc || (oc == mc && od < md)) {
+        mc = oc;
+        md = od;
+        mk = ok;
+      }
+    }
+    // (every lane holds the minimum: read as uniform values)
+    mc = rl_u32(mc, 0);
+    md = rl_u64(md, 0);
+    mk = rl_u32(mk, 0);
+  }
+  // TopTree::addNode (TopTree.cpp:206-516), as tree_add; false: no column left
+  __device__ __forceinline__ bool add(const TreeParams &tp, uint32_t k0, uint64_t dd, int lane) {
+    const uint32_t dh = dom_hash8(dd);
+    if (vcount >= tp.docs_wanted && n > 0 && !key_better(k0, dd, tk, td)) return true;
+    // the insert position and "if equal do not replace" in one pass
+    uint32_t p = 0;
+    uint64_t eqm = 0;
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      const uint32_t i = (uint32_t)k * 64 + (uint32_t)lane;
+      const bool v = i < n;
+      p += (uint32_t)__popcll(__ballot(v & key_better(kk[k], d[k], k0, dd)));
+      eqm |= __ballot(v & (kk[k] == k0) & (d[k] == dd));
+    }
+    if (eqm) return true;
+    const int32_t c = domc(dh);
+    bool del = false;
+    uint32_t delK = 0;
+    uint64_t delD = 0;
+    if (c >= tp.ridiculous) {
+      uint32_t mc, mk;
+      uint64_t md;
+      dom_min(dh, lane, mc, md, mk);
+      const uint32_t cs = key_cs(k0, INTS);
+      if (cs < mc || (cs == mc && dd <= md)) return true;  // k <= *m_t2.getKey(min)
+      del = true;
+      delK = mk;
+      delD = md;
+    }
+    if (n >= (uint32_t)K * 64) return false;
+    const uint32_t n0 = n;
+    insert(p, k0, dd, lane);
+    if (p == n0) {
+      tk = k0;
+      td = dd;
+    }
+    domadd(dh, 1, lane);
+    if (c + 1 < tp.cap) vcount += 1.0;
+    else if (c + 1 == tp.cap) vcount += tp.partial;
+    if (del) {
+      uncount(dh, tp, lane);
+      const uint32_t q = lower(delK, delD, lane);
+      if (q + 1 < n) remove(q, lane);
+      else n--;
+      retail();
+    }
+    // the last node out while the tree holds more than it counts
+    // (TopTree.cpp:446): no shift, the new last node read back
+    while (n > 0 && (vcount - 1.0 >= tp.docs_wanted || (int64_t)n == tp.num_nodes)) {
+      uncount(dom_hash8(td), tp, lane);
+      n--;
+      retail();
+    }
+    return true;
+  }
+};
+
+// the sequencer's state as the filter reads it (published after a segment)
+struct SeqState {
+  uint32_t pref;   // the tree is full: the filter may rule entries out
+  uint32_t stop;   // the register tree overflowed: every wave leaves
+  float L;         // lower bound of minWinningScore from here on
+  uint32_t bk;     // the last node
+  uint64_t bd;
+};
+
+template <int K, bool INTS>
+__global__ void __launch_bounds__(64 * SQ_W) k_tree_seq(Counters *ctr, const uint4 *rep, TreeParams tp, uint32_t *out_key,
+                                                       uint64_t *out_doc) {
+  __shared__ uint4 s_cand[SQ_W][64 * SQ_E];
+  __shared__ uint32_t s_cnt[SQ_W];
+  __shared__ SeqState s_st;
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t lt = (1ull << lane) - 1;
+  const uint32_t ns = (uint32_t)(ctr->surv_top >> 36);
+  const uint32_t nseg = (ns + SQ_SEG - 1) / SQ_SEG;
+  // the sequencer's (wave 0's) state
+  RegTree<K, INTS> T;
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    T.kk[k] = 0;
+    T.d[k] = 0;
+  }
+#pragma unroll
+  for (int c = 0; c < 4; c++) T.dom[c] = 0;
+  T.n = 0;
+  T.vcount = 0.0f;
+  T.tk = 0;
+  T.td = 0;
+  float mws = -1.0f;  // minWinningScore, Posdb.cpp:6012
+  bool called = false;
+  uint32_t filtered = 0, err = 0, adds = 0, nmax = 0, ncand = 0;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0) s_st = SeqState{0u, 0u, 0.0f, 0u, 0ull};
+  uint4 e[SQ_E];
+  auto load = [&](uint32_t sg) {
+#pragma unroll
+    for (int j = 0; j < SQ_E; j++)
+      e[j] = rep[min(sg * SQ_SEG + (uint32_t)wid * 64 * SQ_E + (uint32_t)j * 64 + (uint32_t)lane, ns - 1)];
+  };
+  // the exact per-docid loop of k_tree_replay over one chunk of 64 entries
+  // (prefilters, paging count, offers in docid order); li: each lane's
+  // segment-local index.  Returns the local index after the add that broke
+  // the filter's premise (the rest of the segment is walked raw), else ~0u.
+  auto offer = [&](bool valid, uint4 x, uint32_t li, bool pref) -> uint32_t {
+    const uint32_t key = x.x;
+    const float B = __uint_as_float(x.y);
+    const bool serp = valid && (x.w >> 31);
+    const uint64_t d = ((uint64_t)(x.w & 0x3fu) << 32) | x.z;
+    const uint32_t k0 = node_key(key, INTS);
+    uint64_t from = ~0ull;
+    for (;;) {
+      // (integer scores come from a gbsortby int term: the prefilters are off)
+      const bool live = valid & (INTS || !(B <= mws));
+      const bool ok = live & (key != 0);
+      const bool rej = called & (T.vcount >= tp.docs_wanted) & (T.n > 0) & !key_better(k0, d, T.tk, T.td);
+      const uint64_t slow = __ballot(ok & !rej) & from;
+      const int j = slow ? __ffsll((unsigned long long)slow) - 1 : 64;
+      const uint64_t below = j >= 64 ? ~0ull : ((1ull << j) - 1);
+      filtered += (uint32_t)__popcll(__ballot(live & serp) & below & from);
+      if (!slow) return ~0u;
+      // the offer as uniform values (readlane, not a shuffle): the add's
+      // control flow is then scalar, its node indices SGPRs
+      if (!T.add(tp, rl_u32(k0, (uint32_t)j), rl_u64(d, (uint32_t)j), lane)) {
+        err = TREE_ERR_REG;
+        return ~0u;
+      }
+      adds++;
+      nmax = max(nmax, T.n);
+      called = true;
+      if (T.n > (uint32_t)tp.docs_wanted) mws = key_score(T.tk);  // Posdb.cpp:7699-7704
+      if (pref && !(T.vcount >= tp.docs_wanted)) return rl_u32(li, (uint32_t)j) + 1;
+      if (j == 63) return ~0u;
+      from = ~0ull << (j + 1);
+    }
+  };
+  if (ns) load(0);
+  for (uint32_t sg = 0; sg < nseg; sg++) {
+    __syncthreads();  // s_st published, s_cand free
+    const SeqState st = s_st;
+    if (st.stop) break;  // (uniform over the block)
+    // 1. the filter: each wave's 64 SQ_E consecutive entries
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int j = 0; j < SQ_E; j++) {
+      const uint32_t li = (uint32_t)wid * 64 * SQ_E + (uint32_t)j * 64 + (uint32_t)lane;
+      const uint4 x = e[j];
+      const bool serp = x.w >> 31;
+      bool c = (sg * SQ_SEG + li < ns) & ((x.x != 0) | serp);
+      if (st.pref) {
+        const uint64_t d = ((uint64_t)(x.w & 0x3fu) << 32) | x.z;
+        c = c & (INTS || !(__uint_as_float(x.y) <= st.L)) & (serp | key_better(node_key(x.x, INTS), d, st.bk, st.bd));
+      }
+      const uint64_t bm = __ballot(c);
+      if (c) s_cand[wid][cnt + (uint32_t)__popcll(bm & lt)] = make_uint4(x.x, x.y, x.z, (x.w & 0x8000003fu) | (li << 8));
+      cnt += (uint32_t)__popcll(bm);
+    }
+    if (lane == 0) s_cnt[wid] = cnt;
+    // the next segment's entries go out now and land while the sequencer works
+    if (sg + 1 < nseg) load(sg + 1);
+    __syncthreads();
+    if (wid != 0) continue;
+    // 2. the sequencer: the candidates in order, then the state
+    uint32_t pre[SQ_W + 1];
+    pre[0] = 0;
+#pragma unroll
+    for (int w = 0; w < SQ_W; w++) pre[w + 1] = pre[w] + __builtin_amdgcn_readfirstlane(s_cnt[w]);
+    uint32_t resume = ~0u;
+    ncand += pre[SQ_W];
+    for (uint32_t c0 = 0; c0 < pre[SQ_W] && resume == ~0u && !err; c0 += 64) {
+      const uint32_t t = c0 + (uint32_t)lane;
+      uint4 x = make_uint4(0u, 0u, 0u, 0u);
+      if (t < pre[SQ_W]) {
+        int w = 0;
+#pragma unroll
+        for (int w2 = 1; w2 < SQ_W; w2++)
+          if (t >= pre[w2]) w = w2;
+        x = s_cand[w][t - pre[w]];
+      }
+      resume = offer(t < pre[SQ_W], x, (x.w >> 8) & 0xfffu, st.pref != 0);
+    }
+    // the filter's premise broke (the m_numNodes delete): the rest raw
+    if (resume != ~0u) {
+      const uint32_t end = min(ns, (sg + 1) * SQ_SEG);
+      for (uint32_t p0 = sg * SQ_SEG + resume; p0 < end && !err; p0 += 64) {
+        const uint32_t p = p0 + (uint32_t)lane;
+        uint4 x = rep[min(p, ns - 1)];
+        x.w = (x.w & 0x8000003fu) | ((p - sg * SQ_SEG) << 8);
+        offer(p < end, x, 0u, false);
+      }
+    }
+    if (lane == 0) {
+      const bool full = called && T.vcount >= tp.docs_wanted && T.n > 0;
+      const float bs = key_score(T.tk);
+      s_st = SeqState{full ? 1u : 0u, err ? 1u : 0u, mws < bs ? mws : bs, T.tk, T.td};
+    }
+  }
+  if (wid != 0) return;
+  if (lane == 0) {
+    ctr->filtered = filtered;
+    if (err) ctr->tree_err = err;
+    ctr->pad[0] = adds;  // diagnostic (GBGPU_TOPK_DEBUG)
+    ctr->pad[1] = nmax;
+    ctr->rdbg_t = ncand;
+    ctr->rdbg_total = (uint32_t)((__builtin_amdgcn_s_memrealtime() - t0) / 100);
+  }
+  if (err) return;
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    const uint32_t i = (uint32_t)k * 64 + (uint32_t)lane;
+    if (i < T.n) {
+      out_key[i] = T.kk[k];
+      out_doc[i] = T.d[k];
+    }
+  }
+  if (lane == 0) {
+    if (T.n < TC) out_key[T.n] = 0;
+    ctr->tree_n = T.n;
   }
 }
 
@@ -4825,7 +5247,7 @@ struct QuerySlot {
   DevBuf tables, chunkcnt, cand, cunit, bits, loc, svslot, svlm, svu, svdoc, svloc, scratch, skey, sel, gath, res;
   DevBuf dir;           // candidate directories, epoch-tagged (never cleared per query)
   DevBuf split, swin;   // docid splits: one piece's list windows; window table
-  DevBuf blk, sflag, sbound, rep, tree;  // site clustering: ordered compaction, bounds, replay entries, TopTree state
+  DevBuf blk, sflag, ord, oslot, rep, tree;  // site clustering: slot-order ranks and slots, replay entries, TopTree state
   DevBuf white, wrej;                       // "&sites=" whitelist: sorted 5-byte values; rejected slots
   DevBuf si;                                // second pass's score info (score_info)
   std::vector<uint64_t> h_white;            // its host copy (the upload's source)
@@ -4841,6 +5263,7 @@ struct QuerySlot {
   // state of the in-flight query
   bool pending = false;
   bool replayed = false;  // site clustering: the pass ran the TopTree replay
+  bool seq_replay = false;  // ... as k_tree_seq (a register-tree overflow replays it with k_tree_replay)
   uint64_t slot_ub = 0;
   bool early = false;
   int k = 0;
@@ -4871,7 +5294,7 @@ struct QuerySlot {
     if (stream) (void)hipStreamSynchronize(stream);
     DevBuf *bufs[] = {&tables, &chunkcnt, &cand, &cunit, &bits, &loc, &svslot, &svlm, &svu, &svdoc, &svloc,
                       &scratch, &skey, &sel, &gath, &res, &dir, &split, &swin,
-                      &blk, &sflag, &sbound, &rep, &tree, &white, &wrej, &si};
+                      &blk, &sflag, &ord, &oslot, &rep, &tree, &white, &wrej, &si};
     for (auto *b : bufs) b->release();
     if (h_stage) (void)hipHostFree(h_stage);
     if (h_res) (void)hipHostFree(h_res);
@@ -4933,6 +5356,7 @@ struct gbgpu_ctx {
   int nslots = 0;
   bool profiling = false;
   int probe_mode = 0;  // diagnostic only (GBGPU_PROBE_MODE)
+  int replay_mode = 0;  // diagnostic only (GBGPU_REPLAY_MODE): 1 the one-wave k_tree_replay always, 3 one register column
   int probe_waves = 0;  // diagnostic: probe spans (GBGPU_PROBE_WAVES; 0 = PROBE_WAVES)
   int probe_runspan = 0;  // diagnostic: chunks per run-driven probe wave (GBGPU_PROBE_RUNSPAN; 0 = 1)
   int score_mode = 0;  // diagnostic only (GBGPU_SCORE_MODE): 1 mini-merge without scoring
@@ -5109,6 +5533,13 @@ static TreeParams tree_params(int32_t dw, int phase, bool ints) {
   tp.emit = (phase & TREE_EMIT) ? 1 : 0;
   tp.ints = ints ? 1 : 0;
   return tp;
+}
+
+// k_tree_seq's register columns (64 nodes each) for docsWanted: room for
+// the nodes above docsWanted that capped domains keep in ordinary lists; 0:
+// the one-wave replay (LDS tree)
+static int seq_columns(int32_t dw) {
+  return dw <= 200 ? 4 : dw <= 420 ? 8 : dw <= 880 ? 16 : 0;
 }
 
 // result block of a clustering query: up to TC nodes
@@ -5464,8 +5895,9 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   rc2 |= q.res.ensure(q.res_bytes);
   if (clus) {
     rc2 |= q.sflag.ensure(slot_ub);
-    rc2 |= q.sbound.ensure(4 * slot_ub);
-    rc2 |= q.rep.ensure(16 * slot_ub);
+    rc2 |= q.ord.ensure(4 * slot_ub);
+    rc2 |= q.oslot.ensure(4 * slot_ub);
+    rc2 |= q.rep.ensure((P.g0n > 1 ? 32 : 16) * slot_ub);
     if (!(tree_phase & TREE_FINAL)) rc2 |= q.tree.ensure(sizeof(TreeState));
   }
   if (P.use_white) rc2 |= q.white.ensure(8 * std::max<size_t>(1, q.h_white.size()));
@@ -5572,22 +6004,11 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   uint32_t *svslot = q.svslot.as<uint32_t>(), *svlm = q.svlm.as<uint32_t>(), *svu = q.svu.as<uint32_t>();
   uint64_t *svdoc = q.svdoc.as<uint64_t>();
   Loc *svloc = q.svloc.as<Loc>();
-  // ordered (site clustering: the replay walks the survivors in docid order)
-  // puts every survivor in one bucket, in slot order
-  if (!clus) {
-    hipLaunchKernelGGL(k_cmp_count<false>, dim3(cgrid), dim3(CB), 0, st, dpl, dctr, dcunit, bits, nwords, loc, dcand,
-                       rcap, blk);
-  } else {
-    hipLaunchKernelGGL(k_cmp_count<true>, dim3(cgrid), dim3(CB), 0, st, dpl, dctr, dcunit, bits, nwords, loc, dcand,
-                       rcap, blk);
-  }
-  if (!clus) {
-    hipLaunchKernelGGL(k_cmp_write<false>, dim3(cgrid), dim3(CB), 0, st, dpl, dctr, dcunit, bits, nwords, loc, dcand,
-                       rcap, blk, cgrid, svslot, svlm, svu, svdoc, svloc);
-  } else {
-    hipLaunchKernelGGL(k_cmp_write<true>, dim3(cgrid), dim3(CB), 0, st, dpl, dctr, dcunit, bits, nwords, loc, dcand,
-                       rcap, blk, cgrid, svslot, svlm, svu, svdoc, svloc);
-  }
+  // site clustering also records each survivor's slot-order rank (the
+  // replay walks the survivors in docid order)
+  hipLaunchKernelGGL(k_cmp_count, dim3(cgrid), dim3(CB), 0, st, dpl, dctr, dcunit, bits, nwords, loc, dcand, rcap, blk);
+  hipLaunchKernelGGL(k_cmp_write, dim3(cgrid), dim3(CB), 0, st, dpl, dctr, dcunit, bits, nwords, loc, dcand, rcap, blk,
+                     cgrid, svslot, svlm, svu, svdoc, svloc, clus ? q.ord.as<uint32_t>() : nullptr);
   const unsigned long long arena_cap = (unsigned long long)(q.scratch.cap / 8);
   if (P.reshare_mask)
     hipLaunchKernelGGL(k_ext_walk, dim3(1), dim3(64), 0, st, dpl, dctr, dcand, dcunit, bits, nwords, loc, arena_cap);
@@ -5615,23 +6036,37 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
     // site clustering: prefilter bounds, docid order, the TopTree replay
     const uint32_t bgrid =
         (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((slot_ub + 64 * BND_WAVES - 1) / (64 * BND_WAVES), 4096));
-    // the replay entries: written by k_bound when the survivors are in docid
-    // order (one candidate array), else placed by k_rank
+    // the replay entries in slot order (k_bound): docid order with one
+    // candidate array, else merged by k_rank from the second half of rep
     const bool ranked = P.g0n > 1;
+    uint4 *rep_slot = q.rep.as<uint4>() + (ranked ? slot_ub : 0);
     hipLaunchKernelGGL(k_bound, dim3(bgrid), dim3(64 * BND_WAVES), 0, st, dpl, dctr, (const uint32_t *)svslot,
-                       (const uint32_t *)svlm, (const Loc *)svloc, q.sbound.as<float>(),
+                       (const uint32_t *)svlm, (const Loc *)svloc, (const uint32_t *)q.ord.as<uint32_t>(),
                        (const uint32_t *)q.skey.as<uint32_t>(), (const uint64_t *)svdoc, (const uint8_t *)q.sflag.as<uint8_t>(),
-                       ranked ? nullptr : q.rep.as<uint4>());
+                       rep_slot, ranked ? q.oslot.as<uint32_t>() : nullptr);
     if (ranked) {
       const uint32_t rgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((slot_ub + 255) / 256, 4096));
-      hipLaunchKernelGGL(k_rank, dim3(rgrid), dim3(256), 0, st, dpl, dctr, (const uint32_t *)svslot,
-                         (const uint64_t *)svdoc, (const uint32_t *)q.skey.as<uint32_t>(),
-                         (const uint8_t *)q.sflag.as<uint8_t>(), (const float *)q.sbound.as<float>(), q.rep.as<uint4>());
+      hipLaunchKernelGGL(k_rank, dim3(rgrid), dim3(256), 0, st, dpl, dctr, (const uint32_t *)q.oslot.as<uint32_t>(),
+                         (const uint4 *)rep_slot, q.rep.as<uint4>());
     }
-    hipLaunchKernelGGL(k_tree_replay, dim3(1), dim3(64), 0, st, dctr, (const uint4 *)q.rep.as<uint4>(),
-                       (tree_phase & TREE_FINAL) ? (TreeState *)q.tree.p : q.tree.as<TreeState>(),
-                       tree_params(q.docs_wanted, tree_phase, q.int_scores), q.res.as<uint32_t>(res_keys_off()),
-                       q.res.as<uint64_t>(res_docs_off(k)));
+    // a whole-range pass: the block replay with the tree in registers
+    // (columns for the nodes docsWanted and the domain caps normally keep);
+    // a docid-split piece carries its tree in TreeState: the one-wave replay
+    const int kcol = ctx->replay_mode == 3 ? 1 : seq_columns(q.docs_wanted);  // 3: diagnostic, 64 nodes (overflows)
+    const TreeParams tp = tree_params(q.docs_wanted, tree_phase, q.int_scores);
+    q.seq_replay = tree_phase == (TREE_INIT | TREE_FINAL) && kcol > 0 && ctx->replay_mode != 1;
+    if (q.seq_replay) {
+      auto ks = q.int_scores ? (kcol == 1 ? k_tree_seq<1, true> : kcol == 4 ? k_tree_seq<4, true>
+                                : kcol == 8 ? k_tree_seq<8, true> : k_tree_seq<16, true>)
+                             : (kcol == 1 ? k_tree_seq<1, false> : kcol == 4 ? k_tree_seq<4, false>
+                                : kcol == 8 ? k_tree_seq<8, false> : k_tree_seq<16, false>);
+      hipLaunchKernelGGL(ks, dim3(1), dim3(64 * SQ_W), 0, st, dctr, (const uint4 *)q.rep.as<uint4>(), tp,
+                         q.res.as<uint32_t>(res_keys_off()), q.res.as<uint64_t>(res_docs_off(k)));
+    } else {
+      hipLaunchKernelGGL(k_tree_replay, dim3(1), dim3(64), 0, st, dctr, (const uint4 *)q.rep.as<uint4>(),
+                         (tree_phase & TREE_FINAL) ? (TreeState *)q.tree.p : q.tree.as<TreeState>(), tp,
+                         q.res.as<uint32_t>(res_keys_off()), q.res.as<uint64_t>(res_docs_off(k)));
+    }
     q.replayed = true;
     if (ctx->profiling) HIPCHECK(hipEventRecord(q.ev[5], st));
     HIPCHECK(hipEventRecord(q.ev_done, st));
@@ -5938,6 +6373,22 @@ static int collect(gbgpu_ctx *ctx, QuerySlot &q, gbgpu_result *out, std::vector<
     std::memcpy(q.stats, st, sizeof st);
   }
   if (c->corrupt) return GBGPU_ECORRUPT;
+  if (c->tree_err == TREE_ERR_REG && q.seq_replay) {
+    // the tree outgrew k_tree_seq's register columns: the same replay
+    // entries through the LDS tree (up to TC nodes)
+    q.seq_replay = false;
+    hipStream_t st = q.stream;
+    Counters *dctr = q.res.as<Counters>();
+    HIPCHECK(hipMemsetAsync(&dctr->tree_err, 0, sizeof(uint32_t), st));
+    hipLaunchKernelGGL(k_tree_replay, dim3(1), dim3(64), 0, st, dctr, (const uint4 *)q.rep.as<uint4>(),
+                       (TreeState *)q.tree.p, tree_params(q.docs_wanted, TREE_INIT | TREE_FINAL, q.int_scores),
+                       q.res.as<uint32_t>(res_keys_off()), q.res.as<uint64_t>(res_docs_off(q.k)));
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipMemcpyAsync(q.h_res, q.res.p, q.res_bytes, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipStreamSynchronize(st));
+    out->filtered = (int32_t)c->filtered;
+    q.stats[6] = (int64_t)c->tree_n;
+  }
   if (c->tree_err) return GBGPU_ECAPACITY;
   if (c->unsup) return GBGPU_EUNSUPPORTED;
   if (ctx->d_sdbg && ctx->sdbg_grid) {
@@ -5968,7 +6419,7 @@ static int collect(gbgpu_ctx *ctx, QuerySlot &q, gbgpu_result *out, std::vector<
                    (td[5] - td[4]) / 100.0, td[6], td[7]);
   }
   if (std::getenv("GBGPU_TOPK_DEBUG") && q.replayed)
-    std::fprintf(stderr, "replay: adds %u nmax %u tree_n %u us_add %u us_total %u nsurv %u\n", c->pad[0], c->pad[1],
+    std::fprintf(stderr, "replay: adds %u nmax %u tree_n %u us_add|cand %u us_total %u nsurv %u\n", c->pad[0], c->pad[1],
                  c->tree_n, c->rdbg_t, c->rdbg_total, (uint32_t)(c->surv_top >> 36));
   if (ctx->debug_ext) {
     for (int l = 0; l < MAXL; l++)
@@ -6323,6 +6774,7 @@ int gbgpu_open(int device, gbgpu_ctx **out) {
     return GBGPU_EHIP;
   }
   if (const char *pm = std::getenv("GBGPU_PROBE_MODE")) ctx->probe_mode = std::atoi(pm);
+  if (const char *rm = std::getenv("GBGPU_REPLAY_MODE")) ctx->replay_mode = std::atoi(rm);
   if (const char *pw = std::getenv("GBGPU_PROBE_WAVES")) ctx->probe_waves = std::atoi(pw);
   if (const char *rs = std::getenv("GBGPU_PROBE_RUNSPAN")) ctx->probe_runspan = std::atoi(rs);
   if (const char *sm = std::getenv("GBGPU_SCORE_MODE")) ctx->score_mode = std::atoi(sm);
