@@ -5138,22 +5138,38 @@ __global__ void k_split_windows(const uint64_t *lp, const uint64_t *units, int n
   out[t] = w;
 }
 
+// A device buffer that grows on demand.  A query slot's buffers are
+// stream-ordered (st: the slot's stream): growing one frees and allocates
+// in the stream's order from the device pool, so a query larger than the
+// slot has seen does not stall the device (hipFree synchronises it) and
+// the other slots' queries run on.
 struct DevBuf {
   void *p = nullptr;
   size_t cap = 0;
+  hipStream_t st = nullptr;
   int ensure(size_t bytes) {
     if (bytes <= cap) return 0;
-    if (p) (void)hipFree(p);
-    p = nullptr;
-    cap = 0;
-    size_t want = std::max<size_t>(bytes + bytes / 4, 1 << 16);
-    if (hipMalloc(&p, want) != hipSuccess) return ENOMEM;
+    const size_t want = std::max<size_t>(bytes + bytes / 4, 1 << 16);
+    if (st) {
+      if (p) (void)hipFreeAsync(p, st);
+      p = nullptr;
+      cap = 0;
+      if (hipMallocAsync(&p, want, st) != hipSuccess) return ENOMEM;
+    } else {
+      if (p) (void)hipFree(p);
+      p = nullptr;
+      cap = 0;
+      if (hipMalloc(&p, want) != hipSuccess) return ENOMEM;
+    }
     cap = want;
     return 0;
   }
   template <class T> T *as(size_t off = 0) const { return reinterpret_cast<T *>(static_cast<uint8_t *>(p) + off); }
   void release() {
-    if (p) (void)hipFree(p);
+    if (p) {
+      if (st) (void)hipFreeAsync(p, st);
+      else (void)hipFree(p);
+    }
     p = nullptr;
     cap = 0;
   }
@@ -5283,8 +5299,12 @@ struct QuerySlot {
   hipEvent_t ev_done = nullptr;  // the query's device work is done (the exchange waits on it)
   float last_ms[6] = {0, 0, 0, 0, 0, 0};
 
+  DevBuf *const bufs[28] = {&tables, &chunkcnt, &cand, &cunit, &bits, &loc, &svslot, &svlm, &svu, &svdoc,
+                            &svloc, &scratch, &skey, &sel, &gath, &res, &dir, &split, &swin, &blk,
+                            &sflag, &ord, &oslot, &rep, &tree, &white, &wrej, &si};
   int init() {
     if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return GBGPU_EHIP;
+    for (auto *b : bufs) b->st = stream;
     for (auto &e : ev)
       if (hipEventCreate(&e) != hipSuccess) return GBGPU_EHIP;
     if (hipEventCreateWithFlags(&ev_done, hipEventDisableTiming) != hipSuccess) return GBGPU_EHIP;
@@ -5292,10 +5312,8 @@ struct QuerySlot {
   }
   void release() {
     if (stream) (void)hipStreamSynchronize(stream);
-    DevBuf *bufs[] = {&tables, &chunkcnt, &cand, &cunit, &bits, &loc, &svslot, &svlm, &svu, &svdoc, &svloc,
-                      &scratch, &skey, &sel, &gath, &res, &dir, &split, &swin,
-                      &blk, &sflag, &ord, &oslot, &rep, &tree, &white, &wrej, &si};
     for (auto *b : bufs) b->release();
+    if (stream) (void)hipStreamSynchronize(stream);
     if (h_stage) (void)hipHostFree(h_stage);
     if (h_res) (void)hipHostFree(h_res);
     h_stage = h_res = nullptr;
@@ -6765,6 +6783,15 @@ int gbgpu_open(int device, gbgpu_ctx **out) {
   if (hipSetDevice(device) != hipSuccess) return GBGPU_ENODEVICE;
   gbgpu_ctx *ctx = new gbgpu_ctx();
   ctx->device = device;
+  {
+    // the slots' stream-ordered buffers come from the device pool: keep what
+    // they free cached there (a regrown buffer reuses it, no device sync)
+    hipMemPool_t pool;
+    if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
+      uint64_t keep = ~0ull;
+      (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+    }
+  }
   Weights w = host_weights();
   if (hipStreamCreateWithFlags(&ctx->upload_stream, hipStreamNonBlocking) != hipSuccess ||
       hipMalloc((void **)&ctx->d_flag, 4) != hipSuccess ||
