@@ -117,15 +117,17 @@ def _gbref_run(exe, req, nproc):
     return res, wall
 
 
-def cpu_baseline_query(q, lists, budget_s=20.0):
+def cpu_baseline_query(q, lists, budget_s=20.0, clustering=False):
     """The reference's own PosdbTable::intersectLists10_r (oracle/_ref/gbref,
     compiled from the unmodified sources, -O2 as its Makefile) on the SAME
     full-size lists as the GPU, timed inside the harness (list copies, which
     the reference mutates, excluded): 1 thread, then one process per host
     thread of this box's share running the same query.  Falls back to the C
-    restatement (kind "port") where the reference was not built."""
+    restatement (kind "port") where the reference was not built.  clustering:
+    the same with m_doSiteClustering (Msg39's default request: the prefilters
+    and the TopTree's domain caps, Posdb.cpp:6322-6504, TopTree.cpp:312-516)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
-    p = q.params()
+    p = q.params(site_clustering=1) if clustering else q.params()
     nbytes = sum(len(l) for l in lists)
     exe = os.path.join(ROOT, "oracle", "_ref", "gbref")
     threads = cpu_threads()
@@ -595,6 +597,8 @@ def main():
         del host
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline_query(qs[0], first_lists)
+        if "clustering" in result:
+            result["clustering"]["cpu_baseline"] = cpu_baseline_query(qs[0], first_lists, budget_s=10.0, clustering=True)
     for hs in handles:
         for h in hs:
             eng.free(h)

@@ -476,6 +476,36 @@ __device__ __forceinline__ void wchunk_fetch(const uint8_t *list, uint32_t u0, i
   }
 }
 
+// The same 3 KiB chunk as four 768-byte wave loads of 12 bytes a lane: lane
+// L of piece i holds exactly units 128i + 2L and 128i + 2L + 1, so a unit's
+// flag bytes and a run head's docid bytes sit at fixed places in the lane's
+// words (no byte realignment), and the two units cannot both start a run (a
+// run head's second half has byte 7 & 0x02 clear: posdb_key.h).
+constexpr int W12_PIECES = WCH_BYTES / 768;
+static_assert(W12_PIECES * 768 == WCH_BYTES, "a chunk is whole 12-byte-lane pieces");
+struct U3 {
+  uint32_t x, y, z;
+};
+struct WChunk12 {
+  U3 v[W12_PIECES];
+  uint2 nb;  // lane 63: the 8 bytes after the chunk (docid of a 12-byte key at unit 511)
+};
+__device__ __forceinline__ void wchunk12_fetch(const uint8_t *list, uint32_t u0, int lane, WChunk12 &c) {
+  const auto *src = glc<uint32_t>(list + (size_t)u0 * 6 + lane * 12);
+#pragma unroll
+  for (int i = 0; i < W12_PIECES; i++) {
+    c.v[i].x = __builtin_nontemporal_load(src + i * 192);
+    c.v[i].y = __builtin_nontemporal_load(src + i * 192 + 1);
+    c.v[i].z = __builtin_nontemporal_load(src + i * 192 + 2);
+  }
+  c.nb = make_uint2(0, 0);
+  if (lane == 63) {
+    typedef uint32_t v2 __attribute__((ext_vector_type(2)));
+    const v2 t = *glc<v2>(list + (size_t)u0 * 6 + WCH_BYTES);
+    c.nb = make_uint2(t.x, t.y);
+  }
+}
+
 // first index in [0,n) with a[i] >= key, cooperatively by one wave (64-ary)
 __device__ uint32_t wave_lower_bound(const uint64_t *a, uint32_t n, uint64_t key, int lane) {
   uint32_t lo = 0, hi = n;  // answer in [lo, hi]
@@ -1501,59 +1531,34 @@ struct ProbeLdsP {
   uint32_t cbits[WMAX_RUNS / 32];     // claimed runs
   uint32_t mslot[MBUF], mu[MBUF], mlen[MBUF];
 };
-__device__ __forceinline__ uint32_t chunk_runs_packed(const WChunk &cur, uint32_t u0, uint32_t u1, int lane, ProbeLdsP &S) {
+__device__ __forceinline__ uint32_t chunk_runs_packed(const WChunk12 &cur, uint32_t u0, uint32_t u1, int lane, ProbeLdsP &S) {
   const uint64_t lt = (1ull << lane) - 1;
   uint32_t nrun = 0;
 #pragma unroll
-  for (int i = 0; i < WPIECES; i++) {
-    uint32_t r[7];
-    r[0] = cur.v[i].x;
-    r[1] = cur.v[i].y;
-    r[2] = cur.v[i].z;
-    r[3] = cur.v[i].w;
-    uint32_t e0, e1, e2;  // lane 63: the next piece's first bytes, or the bytes after the chunk
-    if (i + 1 < WPIECES) {
+  for (int i = 0; i < W12_PIECES; i++) {
+    const uint32_t d0 = cur.v[i].x, d1 = cur.v[i].y, d2 = cur.v[i].z;
+    uint32_t e0, e1;  // lane 63: the next piece's first bytes, or the bytes after the chunk
+    if (i + 1 < W12_PIECES) {
       e0 = __builtin_amdgcn_readfirstlane(cur.v[i + 1].x);
       e1 = __builtin_amdgcn_readfirstlane(cur.v[i + 1].y);
-      e2 = __builtin_amdgcn_readfirstlane(cur.v[i + 1].z);
     } else {
       e0 = cur.nb.x;
       e1 = cur.nb.y;
-      e2 = 0;
     }
-    r[4] = lane_next(r[0], e0);
-    r[5] = lane_next(r[1], e1);
-    r[6] = lane_next(r[2], e2);
-    const uint32_t P = (uint32_t)i * 1024 + (uint32_t)lane * 16;
-    const uint32_t k0 = (P + 5) / 6;  // first unit starting in [P, P + 16)
-    const uint32_t o0 = k0 * 6 - P;
-    uint32_t a[6];
-#pragma unroll
-    for (int j = 0; j < 6; j++) a[j] = o0 == 4 ? r[j + 1] : __builtin_amdgcn_alignbyte(r[j + 1], r[j], o0);
-    // a unit at q starts at byte 6q: bytes 0-1 (flags) are byte pair 0 of
-    // a[0] (q=0), pair 1 of a[1] (q=1), pair 0 of a[3] (q=2)
-    const uint32_t h0 = a[0], h1 = a[1] >> 16, h2 = a[3];
-    const bool in0 = o0 < 16 && u0 + k0 < u1, in1 = o0 + 6 < 16 && u0 + k0 + 1 < u1, in2 = o0 + 12 < 16 && u0 + k0 + 2 < u1;
-    const bool s0 = in0 && (h0 & 0x200u) && !(h0 & 0x4u);
-    const bool s1 = in1 && (h1 & 0x200u) && !(h1 & 0x4u);
-    const bool s2 = in2 && (h2 & 0x200u) && !(h2 & 0x4u);
-    // a subset of {0, 1, 2} with no two adjacent: {q} or {0, 2}
-    const uint32_t cnt = (uint32_t)s0 + (uint32_t)s1 + (uint32_t)s2;
-    const uint64_t b0 = __ballot(cnt & 1), b1 = __ballot(cnt & 2);
-    const uint32_t o = nrun + (uint32_t)(__popcll(b0 & lt) + 2 * __popcll(b1 & lt));
-    // the docid (key bytes 7..11) of the first start and of a start at q=2:
-    // q=0 bytes 7..11 = a[1].3, a[2].0-3; q=1 bytes 13..17 = a[3].1-3,
-    // a[4].0-1; q=2 bytes 19..23 = a[4].3, a[5].0-3
-    const uint32_t lo0 = s0 ? __builtin_amdgcn_alignbyte(a[2], a[1], 3) : s1 ? __builtin_amdgcn_alignbyte(a[4], a[3], 1)
-                                                                           : __builtin_amdgcn_alignbyte(a[5], a[4], 3);
-    const uint32_t hi0 = s0 ? a[2] >> 24 : s1 ? (a[4] >> 8) & 0xff : a[5] >> 24;
-    const uint32_t q0 = s0 ? 0u : s1 ? 1u : 2u;
-    const uint64_t wa = ((((uint64_t)hi0 << 32) | lo0) >> 2) << 16 | (uint64_t)(k0 + q0);
-    const uint64_t wb = ((((uint64_t)(a[5] >> 24) << 32) | __builtin_amdgcn_alignbyte(a[5], a[4], 3)) >> 2) << 16 |
-                        (uint64_t)(k0 + 2);
-    if (cnt) S.rk[o] = wa;
-    if (cnt == 2) S.rk[o + 1] = wb;
-    nrun += (uint32_t)(__popcll(b0) + 2 * __popcll(b1));
+    const uint32_t n0 = lane_next(d0, e0), n1 = lane_next(d1, e1);  // the next lane's unit
+    const uint32_t k0 = (uint32_t)i * 128 + (uint32_t)lane * 2;     // the lane's first unit
+    // unit k0: flag bytes 0-1 = d0 bits 0-15; unit k0+1: bytes 6-7 = d1 bits 16-31
+    const bool s0 = (u0 + k0 < u1) & ((d0 & 0x200u) != 0) & !(d0 & 0x4u);
+    const bool s1 = (u0 + k0 + 1 < u1) & ((d1 & 0x2000000u) != 0) & !(d1 & 0x40000u);
+    // the head's docid, key bytes 7..11: d1.3 d2 (unit k0) or the next lane's
+    // bytes 1..5 (unit k0+1)
+    const uint32_t lo = s0 ? (d1 >> 24) | (d2 << 8) : (n0 >> 8) | (n1 << 24);
+    const uint32_t hi = s0 ? d2 >> 24 : (n1 >> 8) & 0xffu;
+    const uint64_t w = ((((uint64_t)hi << 32) | lo) >> 2) << 16 | (uint64_t)(k0 + (s0 ? 0u : 1u));
+    const bool st = s0 | s1;
+    const uint64_t b = __ballot(st);
+    if (st) S.rk[nrun + (uint32_t)__popcll(b & lt)] = w;
+    nrun += (uint32_t)__popcll(b);
   }
   // keys past the runs read as ~0 (above every candidate key): the search
   // needs no bounds test
@@ -1571,7 +1576,7 @@ __device__ void probe_by_cand_packed(const DevPlan *__restrict__ pl, const Probe
   uint32_t nk[G0], lok[G0];
   uint64_t base[G0], cur[G0], nxt[G0];
   const uint32_t last_u0 = w.u0 + ((w.u1 - w.u0 - 1) / WCH_UNITS) * WCH_UNITS;
-  WChunk cA, cB;
+  WChunk12 cA, cB;
   constexpr bool FULL = MODE == 0 || MODE == 5;
   const uint64_t dfirst = !FULL ? 0 : w.has_dfirst ? w.dfirst : first_run_doc(L, w.u0, w.u1, lane);
   auto cload = [&](int k, uint32_t i) -> uint64_t {  // candidate i of array k (clamped; validity at use)
@@ -1585,12 +1590,12 @@ __device__ void probe_by_cand_packed(const DevPlan *__restrict__ pl, const Probe
     cur[k] = cload(k, lok[k] + lane);
     nxt[k] = cload(k, lok[k] + 64 + lane);
   }
-  wchunk_fetch(lp, w.u0, lane, cA);
-  wchunk_fetch(lp, min(w.u0 + WCH_UNITS, last_u0), lane, cB);
+  wchunk12_fetch(lp, w.u0, lane, cA);
+  wchunk12_fetch(lp, min(w.u0 + WCH_UNITS, last_u0), lane, cB);
   uint32_t nbuf = 0;
   uint64_t pend_slot = ~0ull;  // slot whose run length waits for the next run start
   uint32_t pend_u = 0;
-  auto step = [&](const WChunk &c, uint32_t u0) {
+  auto step = [&](const WChunk12 &c, uint32_t u0) {
     if (MODE == 2) {
       if (c.v[0].x == 0x557713eeu && c.v[1].y == 7u && c.v[2].z == 3u) po.bits[0] = 1;
       return;
@@ -1690,10 +1695,10 @@ __device__ void probe_by_cand_packed(const DevPlan *__restrict__ pl, const Probe
   uint32_t u0 = w.u0;
   for (uint32_t it = 0; it + 2 <= nch; it += 2, u0 += 2 * WCH_UNITS) {
     step(cA, u0);
-    wchunk_fetch(lp, min(u0 + 2 * WCH_UNITS, last_u0), lane, cA);
+    wchunk12_fetch(lp, min(u0 + 2 * WCH_UNITS, last_u0), lane, cA);
     __builtin_amdgcn_sched_barrier(0);
     step(cB, u0 + WCH_UNITS);
-    wchunk_fetch(lp, min(u0 + 3 * WCH_UNITS, last_u0), lane, cB);
+    wchunk12_fetch(lp, min(u0 + 3 * WCH_UNITS, last_u0), lane, cB);
     __builtin_amdgcn_sched_barrier(0);
   }
   if (nch & 1) step(cA, u0);
@@ -4484,7 +4489,7 @@ __global__ void __launch_bounds__(64 * SQ_W) k_tree_seq(Counters *ctr, const uin
       bool c = (sg * SQ_SEG + li < ns) & ((x.x != 0) | serp);
       if (st.pref) {
         const uint64_t d = ((uint64_t)(x.w & 0x3fu) << 32) | x.z;
-        c = c & (INTS || !(__uint_as_float(x.y) <= st.L)) & (serp | key_better(node_key(x.x, INTS), d, st.bk, st.bd));
+        c = c && (INTS || !(__uint_as_float(x.y) <= st.L)) && (serp || key_better(node_key(x.x, INTS), d, st.bk, st.bd));
       }
       const uint64_t bm = __ballot(c);
       if (c) s_cand[wid][cnt + (uint32_t)__popcll(bm & lt)] = make_uint4(x.x, x.y, x.z, (x.w & 0x8000003fu) | (li << 8));
