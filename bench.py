@@ -546,15 +546,16 @@ def main():
             eng.collect(cap=4096, slot=0)
             cdev.append(eng.last_timings(slot=0)[0])
         eng.set_profiling(False)
-        nc = max(len(qs), args.steps // 2)
+        nc = max(4 * slots * len(qs), args.steps)  # steady state: fill and drain are a few queries
         # every slot's clustering buffers (replay entries, ranks, the TopTree
         # result block) sized before the clock starts
-        for i in range(2 * slots):
+        nw = 4 * slots
+        for i in range(nw):
             slot = i % slots
             if i >= slots:
                 eng.collect(cap=4096, slot=slot)
             eng.enqueue(qs[i % len(qs)].terms, handles[i % len(qs)], pc[i % len(qs)], slot=slot)
-        for i in range(slots, 2 * slots):
+        for i in range(nw - slots, nw):
             eng.collect(cap=4096, slot=i % slots)
         t_c = time.perf_counter()
         for i in range(nc):

@@ -36,6 +36,8 @@ for clus in [int(x) for x in os.environ.get("CLUS", "0 1").split()]:
                 a = time.perf_counter()
                 eng.enqueue(qs[i % len(qs)].terms, handles[i % len(qs)], pc[i % len(qs)], slot=s)
                 te.append(time.perf_counter() - a)
+                if te[-1] > 2e-3:
+                    print(f"  slow enqueue rep {rep} i {i} slot {s} query {i % len(qs)}: {1e3 * te[-1]:.2f} ms", flush=True)
             for i in range(max(0, nq - slots), nq):
                 eng.collect(cap=4096, slot=i % slots)
             el = time.perf_counter() - t0
