@@ -1576,7 +1576,7 @@ __device__ void probe_by_cand_packed(const DevPlan *__restrict__ pl, const Probe
   uint32_t nk[G0], lok[G0];
   uint64_t base[G0], cur[G0], nxt[G0];
   const uint32_t last_u0 = w.u0 + ((w.u1 - w.u0 - 1) / WCH_UNITS) * WCH_UNITS;
-  WChunk12 cA, cB;
+  WChunk12 cA, cB, cC;  // three chunks in flight (9 KiB a wave)
   constexpr bool FULL = MODE == 0 || MODE == 5;
   const uint64_t dfirst = !FULL ? 0 : w.has_dfirst ? w.dfirst : first_run_doc(L, w.u0, w.u1, lane);
   auto cload = [&](int k, uint32_t i) -> uint64_t {  // candidate i of array k (clamped; validity at use)
@@ -1592,12 +1592,16 @@ __device__ void probe_by_cand_packed(const DevPlan *__restrict__ pl, const Probe
   }
   wchunk12_fetch(lp, w.u0, lane, cA);
   wchunk12_fetch(lp, min(w.u0 + WCH_UNITS, last_u0), lane, cB);
+  wchunk12_fetch(lp, min(w.u0 + 2 * WCH_UNITS, last_u0), lane, cC);
   uint32_t nbuf = 0;
   uint64_t pend_slot = ~0ull;  // slot whose run length waits for the next run start
   uint32_t pend_u = 0;
   auto step = [&](const WChunk12 &c, uint32_t u0) {
-    if (MODE == 2) {
-      if (c.v[0].x == 0x557713eeu && c.v[1].y == 7u && c.v[2].z == 3u) po.bits[0] = 1;
+    if (MODE == 2) {  // every loaded word feeds the (never true) test: no load is dropped
+      uint32_t x = 0;
+#pragma unroll
+      for (int i = 0; i < W12_PIECES; i++) x ^= c.v[i].x ^ (c.v[i].y * 3u) ^ (c.v[i].z * 5u);
+      if (x == 0x557713eeu && c.nb.x == 7u) po.bits[0] = 1;
       return;
     }
     const uint32_t nrun = chunk_runs_packed(c, u0, w.u1, lane, S);
@@ -1693,15 +1697,22 @@ __device__ void probe_by_cand_packed(const DevPlan *__restrict__ pl, const Probe
   };
   const uint32_t nch = (w.u1 - w.u0 + WCH_UNITS - 1) / WCH_UNITS;
   uint32_t u0 = w.u0;
-  for (uint32_t it = 0; it + 2 <= nch; it += 2, u0 += 2 * WCH_UNITS) {
+  // static buffer roles (the in-order vmcnt then waits exactly for the
+  // chunk about to be classified)
+  for (uint32_t it = 0; it + 3 <= nch; it += 3, u0 += 3 * WCH_UNITS) {
     step(cA, u0);
-    wchunk12_fetch(lp, min(u0 + 2 * WCH_UNITS, last_u0), lane, cA);
+    wchunk12_fetch(lp, min(u0 + 3 * WCH_UNITS, last_u0), lane, cA);
     __builtin_amdgcn_sched_barrier(0);
     step(cB, u0 + WCH_UNITS);
-    wchunk12_fetch(lp, min(u0 + 3 * WCH_UNITS, last_u0), lane, cB);
+    wchunk12_fetch(lp, min(u0 + 4 * WCH_UNITS, last_u0), lane, cB);
+    __builtin_amdgcn_sched_barrier(0);
+    step(cC, u0 + 2 * WCH_UNITS);
+    wchunk12_fetch(lp, min(u0 + 5 * WCH_UNITS, last_u0), lane, cC);
     __builtin_amdgcn_sched_barrier(0);
   }
-  if (nch & 1) step(cA, u0);
+  const uint32_t rem = nch % 3;
+  if (rem >= 1) step(cA, u0);
+  if (rem == 2) step(cB, u0 + WCH_UNITS);
   if (pend_slot != ~0ull) {
     const uint32_t len = lane == 0 ? run_end(L, pend_u + 2) - pend_u : 0;
     if (nbuf + 1 > MBUF) mbuf_flush(S, nbuf, po, lane);
