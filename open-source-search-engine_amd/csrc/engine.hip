@@ -452,7 +452,7 @@ constexpr int WCH_BYTES = WPIECES * 1024;  // 3 KiB
 constexpr int WCH_UNITS = WCH_BYTES / 6;   // units per wave chunk
 static_assert(WCH_BYTES % 6 == 0, "a chunk holds whole units");
 constexpr int WMAX_RUNS = WCH_UNITS / 2;
-constexpr uint32_t PROBE_WAVES = 256 * 16;
+constexpr uint32_t PROBE_WAVES = 256 * 12;  // 3072 spans: measured best with three chunks in flight (4096: 64.1 us, 3072: 62.9)
 constexpr uint32_t PROBE_WAVES_WIDE = 256 * 12;  // the wide path: three waves per SIMD (VGPRs)
 
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
@@ -1577,6 +1577,10 @@ __device__ void probe_by_cand_packed(const DevPlan *__restrict__ pl, const Probe
   uint64_t base[G0], cur[G0], nxt[G0];
   const uint32_t last_u0 = w.u0 + ((w.u1 - w.u0 - 1) / WCH_UNITS) * WCH_UNITS;
   WChunk12 cA, cB, cC;  // three chunks in flight (9 KiB a wave)
+  // a prefetch past the span (issued unconditionally, so every step waits
+  // on a fixed load count) reads the list's first chunk, which every wave's
+  // tail shares in L2, instead of its own last chunk again from HBM
+  auto pre_u = [&](uint32_t u) -> uint32_t { return u <= last_u0 ? u : 0u; };
   constexpr bool FULL = MODE == 0 || MODE == 5;
   const uint64_t dfirst = !FULL ? 0 : w.has_dfirst ? w.dfirst : first_run_doc(L, w.u0, w.u1, lane);
   auto cload = [&](int k, uint32_t i) -> uint64_t {  // candidate i of array k (clamped; validity at use)
@@ -1591,8 +1595,8 @@ __device__ void probe_by_cand_packed(const DevPlan *__restrict__ pl, const Probe
     nxt[k] = cload(k, lok[k] + 64 + lane);
   }
   wchunk12_fetch(lp, w.u0, lane, cA);
-  wchunk12_fetch(lp, min(w.u0 + WCH_UNITS, last_u0), lane, cB);
-  wchunk12_fetch(lp, min(w.u0 + 2 * WCH_UNITS, last_u0), lane, cC);
+  wchunk12_fetch(lp, pre_u(w.u0 + WCH_UNITS), lane, cB);
+  wchunk12_fetch(lp, pre_u(w.u0 + 2 * WCH_UNITS), lane, cC);
   uint32_t nbuf = 0;
   uint64_t pend_slot = ~0ull;  // slot whose run length waits for the next run start
   uint32_t pend_u = 0;
@@ -1701,13 +1705,13 @@ __device__ void probe_by_cand_packed(const DevPlan *__restrict__ pl, const Probe
   // chunk about to be classified)
   for (uint32_t it = 0; it + 3 <= nch; it += 3, u0 += 3 * WCH_UNITS) {
     step(cA, u0);
-    wchunk12_fetch(lp, min(u0 + 3 * WCH_UNITS, last_u0), lane, cA);
+    wchunk12_fetch(lp, pre_u(u0 + 3 * WCH_UNITS), lane, cA);
     __builtin_amdgcn_sched_barrier(0);
     step(cB, u0 + WCH_UNITS);
-    wchunk12_fetch(lp, min(u0 + 4 * WCH_UNITS, last_u0), lane, cB);
+    wchunk12_fetch(lp, pre_u(u0 + 4 * WCH_UNITS), lane, cB);
     __builtin_amdgcn_sched_barrier(0);
     step(cC, u0 + 2 * WCH_UNITS);
-    wchunk12_fetch(lp, min(u0 + 5 * WCH_UNITS, last_u0), lane, cC);
+    wchunk12_fetch(lp, pre_u(u0 + 5 * WCH_UNITS), lane, cC);
     __builtin_amdgcn_sched_barrier(0);
   }
   const uint32_t rem = nch % 3;
