@@ -3177,7 +3177,7 @@ struct ScoreRec {
     ns++;
   }
   __device__ void pair(const DevPlan *__restrict__ pl, int i, int j, float best, float wts, int32_t qdist, uint64_t r1,
-                       uint64_t r2, bool fixed) {
+                       uint64_t r2, uint8_t fixed) {
     if (np < pcap) {
       gbgpu_pair_score x;
       __builtin_memset(&x, 0, sizeof x);
@@ -3203,7 +3203,7 @@ struct ScoreRec {
       x.qdist = qdist;
       x.density_rank1 = (int8_t)r_dens(r1);
       x.density_rank2 = (int8_t)r_dens(r2);
-      x.fixed_distance = fixed ? 1 : 0;
+      x.fixed_distance = (int8_t)fixed;  // 2: the reference reads its uninitialised local here
       x.qterm_num1 = pl->qterm[i];
       x.qterm_num2 = pl->qterm[j];
       x.tf_weight1 = pl->tfw[i];

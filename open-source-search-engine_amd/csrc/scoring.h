@@ -154,7 +154,7 @@ struct ScoreCtx {
 struct NoRec {
   static constexpr bool on = false;
   __device__ void single(const DevPlan *, int, float, uint64_t) {}
-  __device__ void pair(const DevPlan *, int, int, float, float, int32_t, uint64_t, uint64_t, bool) {}
+  __device__ void pair(const DevPlan *, int, int, float, float, int32_t, uint64_t, uint64_t, uint8_t) {}
 };
 
 // getSingleTermScore, Posdb.cpp:3087-3301.  bestPos = record index of the
@@ -487,8 +487,9 @@ __device__ __forceinline__ void eval_window(ScoreCtx<NQ> &c, const DocView<NQ, R
 // a bound on the slots the pair's records can fill); REC receives the top pairs
 // (pdcs path, 4195-4280) with their record indices and fixedDistance flag --
 // which the reference only assigns when dist < 50 or the distance is fixed,
-// so it carries over from the previous scored pair otherwise (false at the
-// start, where the reference's is uninitialised)
+// so it carries over from the previous scored pair of the call otherwise; a
+// pair scored before any assignment in the call reads the reference's
+// uninitialised local (Posdb.cpp:3730), recorded here as 2
 template <int NQ, class RP, class REC = NoRec, int T = MAX_TOP>
 __device__ __forceinline__ float pair_score_any(const ScoreCtx<NQ> &c, const DocView<NQ, RP> &d, int i, int j,
                                                REC *rec = nullptr) {
@@ -523,8 +524,9 @@ __device__ __forceinline__ float pair_score_any(const ScoreCtx<NQ> &c, const Doc
   float bestScores[T];
   uint32_t bestmhg1[T], bestmhg2[T];
   int bestwpi[REC::on ? T : 1], bestwpj[REC::on ? T : 1];
-  bool bestFixed[REC::on ? T : 1];
+  uint8_t bestFixed[REC::on ? T : 1];
   bool fixedDistance = false;
+  bool fixedSet = false;  // fixedDistance assigned in this call
 #pragma unroll
   for (int q = 0; q < T; q++) {
     bestScores[q] = 0.0f;
@@ -532,7 +534,7 @@ __device__ __forceinline__ float pair_score_any(const ScoreCtx<NQ> &c, const Doc
     bestmhg2[q] = 0xff;
     if constexpr (REC::on) {
       bestwpi[q] = bestwpj[q] = 0;
-      bestFixed[q] = false;
+      bestFixed[q] = 0;
     }
   }
   int numTop = 0;
@@ -558,12 +560,15 @@ __device__ __forceinline__ float pair_score_any(const ScoreCtx<NQ> &c, const Doc
         if (dist < 2) dist = 2;
         if (dist < 50) {
           fixedDistance = false;
+          fixedSet = true;
         } else if (mhg1 != mhg2) {
           dist = FIXED_DISTANCE;
           fixedDistance = true;
+          fixedSet = true;
         } else if (mhg1 == GB_HG_INLINKTEXT) {
           dist = FIXED_DISTANCE;
           fixedDistance = true;
+          fixedSet = true;
         }
         if (dist >= qdist) dist = dist - qdist;
         score = 100 * denw1 * denw2;
@@ -584,12 +589,15 @@ __device__ __forceinline__ float pair_score_any(const ScoreCtx<NQ> &c, const Doc
         if (dist < 2) dist = 2;
         if (dist < 50) {
           fixedDistance = false;
+          fixedSet = true;
         } else if (mhg1 != mhg2) {
           dist = FIXED_DISTANCE;
           fixedDistance = true;
+          fixedSet = true;
         } else if (mhg1 == GB_HG_INLINKTEXT) {
           dist = FIXED_DISTANCE;
           fixedDistance = true;
+          fixedSet = true;
         }
         if (dist >= qdist) {
           dist = dist - qdist;
@@ -636,7 +644,7 @@ __device__ __forceinline__ float pair_score_any(const ScoreCtx<NQ> &c, const Doc
           if constexpr (REC::on) {
             bestwpi[q] = wi;
             bestwpj[q] = wj;
-            bestFixed[q] = fixedDistance;
+            bestFixed[q] = fixedSet ? (fixedDistance ? 1 : 0) : 2;
           }
         }
       }

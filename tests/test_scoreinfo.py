@@ -81,12 +81,13 @@ IN_BODY = {0, 2, 3, 10}  # HASHGROUP_BODY, _HEADING, _INLIST, _INMENU (Posdb.cpp
 INLINKTEXT = 5
 
 
-def fixed_undefined(ps):
-    """PairScores whose m_fixedDistance the reference never assigns in the
-    call (getTermPairScoreForAny, Posdb.cpp:3784-3794, 3982-3992): a
-    distance of 50 or more between positions of one modified hash group
-    other than inlink text.  It then holds whatever the uninitialised local
-    held (known divergences): not compared."""
+def fixed_unassigning(ps):
+    """PairScores at which getTermPairScoreForAny leaves m_fixedDistance
+    unassigned (Posdb.cpp:3784-3794, 3982-3992): a distance of 50 or more
+    between positions of one modified hash group other than inlink text.
+    The flag then carries the value of the call's previous assignment -- or,
+    when no pair of the call assigned it yet, the uninitialised local
+    (Posdb.cpp:3730)."""
     mhg1 = np.where(np.isin(ps["hash_group1"], list(IN_BODY)), 0, ps["hash_group1"])
     mhg2 = np.where(np.isin(ps["hash_group2"], list(IN_BODY)), 0, ps["hash_group2"])
     dist = np.abs(ps["word_pos2"].astype(np.int64) - ps["word_pos1"].astype(np.int64))
@@ -103,7 +104,13 @@ def same(got, exp, label):
             g, e = g.view(f"u{g.itemsize}"), e.view(f"u{e.itemsize}")
         diff = g != e
         if f == "fixed_distance" and "hash_group1" in exp.dtype.names:
-            diff &= ~fixed_undefined(exp)
+            # the GPU carries the flag across the call's pairs as the
+            # reference does, and marks 2 the pairs scored before any
+            # assignment: only those read an undefined value, and only an
+            # unassigning pair may be one
+            und = got["fixed_distance"] == 2
+            assert not np.any(und & ~fixed_unassigning(exp)), (label, "2 at an assigning pair")
+            diff &= ~und
         bad = np.nonzero(diff)[0]
         assert not len(bad), (label, f, int(bad[0]), got[f][bad[0]], exp[f][bad[0]])
 
