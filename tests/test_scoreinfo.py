@@ -146,7 +146,14 @@ def test_reference_buffers_consistent(path):
     # getWordPosList missed the docid in a sublist (si_predict)
     missed = {doc for _, doc in si_predict.misses(lists, exp["votes"], exp["docids"][:n])}
     if any(t.field_code in (59, 60) for t in terms):
-        n = 0  # gbsortby int: m_finalScore is (double)m_intScore, m_score 0.0 (Posdb.cpp:7557-7560)
+        # gbsortby int: m_finalScore is (double)m_intScore, m_score 0.0
+        # (Posdb.cpp:7557-7560): against the reference tree's m_intScore
+        import ref_binding as ref
+        if n and ref.available():
+            ints = ref.query(terms, lists, params, cap=1 << 16, votes=False, mode=0)["int_scores"][:n]
+            keep = np.array([int(x) not in missed for x in d["docid"][:n]], bool)
+            assert np.array_equal(d["final_score"][:n][keep], ints.astype(np.float64)[keep])
+        n = 0
     keep = np.array([int(x) not in missed for x in d["docid"][:n]], bool)
     assert np.array_equal(d["final_score"][:n].astype(np.float32).view(np.uint32)[keep],
                           exp["scores"][:n].view(np.uint32)[keep])
