@@ -346,7 +346,7 @@ def main():
     ap.add_argument("--docs-per-gpu", type=int, default=0, help="0: 100M at N=1 (config 2), 125M at N>1 (config 4)")
     ap.add_argument("--docs-to-get", type=int, default=100)
     ap.add_argument("--queries", type=int, default=16, help="distinct config-2 queries the steps rotate over")
-    ap.add_argument("--slots", type=int, default=8, help="queries in flight per GPU (query slots)")
+    ap.add_argument("--slots", type=int, default=12, help="queries in flight per GPU (query slots)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-merge", action="store_true", help="skip the config-5 list merge measurement")
     ap.add_argument("--no-config3", action="store_true", help="skip the config-3 query-mix measurement")
