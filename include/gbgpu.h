@@ -338,9 +338,8 @@ int gbgpu_merge_last_key(gbgpu_ctx *ctx, uint8_t *key18);
  * pass; and the number of keys decoded and of merge tiles. */
 int gbgpu_merge_timings(gbgpu_ctx *ctx, float *ms6, int64_t *nkeys, int64_t *ntiles);
 /* The pipeline of the last merge: 2 = decoded keys (every key decoded to
- * HBM, then tiles gather them; the default), 1 = tile path (each tile decodes
- * its keys from the compressed runs into LDS: <= 28 runs, about half the HBM
- * traffic, selected with GBGPU_MERGE_PATH=tiles), 0 = none. */
+ * HBM, then tiles gather them), 0 = none.  (1, a tile pipeline decoding the
+ * compressed runs in LDS, was measured slower and retired.) */
 int gbgpu_merge_path(gbgpu_ctx *ctx);
 
 /* Per-query device timings of a slot's last query (HIP events on its stream),

@@ -33,8 +33,7 @@ int last_key(MergeState *s, uint8_t *key18);
 // tile counts.
 void last_timings(MergeState *s, float *ms6, int64_t *nkeys, int64_t *ntiles);
 
-// Which pipeline ran the last merge: 1 tile path (keys decoded into each
-// tile's LDS), 2 legacy (keys decoded to HBM), 0 none.
+// Which pipeline ran the last merge: 2 (keys decoded to HBM), 0 none.
 int last_path(MergeState *s);
 
 }  // namespace gbmerge

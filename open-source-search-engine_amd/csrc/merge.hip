@@ -225,20 +225,7 @@ __device__ __forceinline__ uint64_t rd48g(const uint8_t *p) {  // 2-B aligned gl
 }
 
 // ------------------------------------------------------------- decoding
-// Granules (the tile path's sample spacing): GU consecutive units of a run.
-// k_mcount leaves, per granule, its first key start and the chunk-local state
-// there (GLoc); k_msample2 adds the chunk carries of k_mscan and decodes
-// that key, the granule's sample.
-constexpr int GU = 64;          // units per granule
-constexpr int GPC = MCH / GU;   // granules per decode chunk
-constexpr uint32_t NONE = 0xffffffffu;
-struct GLoc {
-  uint32_t kb;      // keys of the chunk before the granule's first key start
-  uint32_t lo, hi;  // last lo / hi unit + 1 before it, in the chunk (0: none)
-  uint32_t fk;      // its unit offset in the granule, NONE: no key starts here
-};
-
-__global__ void __launch_bounds__(MB) k_mcount(const MList *lists, int n, DSum *sum, MCtl *ctl, GLoc *gl) {
+__global__ void __launch_bounds__(MB) k_mcount(const MList *lists, int n, DSum *sum, MCtl *ctl) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[WIN_BYTES];
   __shared__ uint32_t t0[MB / 64], t1[MB / 64], t2[MB / 64];
   const int li = list_of_chunk(lists, n, blockIdx.x);
@@ -247,19 +234,12 @@ __global__ void __launch_bounds__(MB) k_mcount(const MList *lists, int n, DSum *
   stage(L, u0, lds);
   __syncthreads();
   uint32_t cnt = 0, llo = 0, lhi = 0, bad = 0;
-  // the thread's first key start and the lo / hi units before it in its range
-  uint32_t fku = NONE, flo = 0, fhi = 0;
 #pragma unroll
   for (int q = 0; q < MUPT; q++) {
     const uint32_t u = u0 + threadIdx.x * MUPT + q;
     if (u >= L.units) break;
     const int t = utype(lds, u0, u);
     if (t == 0) {
-      if (fku == NONE) {
-        fku = u;
-        flo = llo;
-        fhi = lhi;
-      }
       cnt++;
       const uint32_t ku = kunits(lunit(lds, u0, u)[0]);
       if ((uint64_t)u + ku > L.units) bad |= F_CORRUPT;
@@ -273,28 +253,10 @@ __global__ void __launch_bounds__(MB) k_mcount(const MList *lists, int n, DSum *
   }
   if (bad) atomicOr(&ctl->flags, bad);
   uint32_t a, b, c;
-  const uint32_t ea = block_scan<MB>(cnt, 0u, OpAdd(), t0, &a);
-  const uint32_t eb = block_scan<MB>(llo, 0u, OpMax(), t1, &b);
-  const uint32_t ec = block_scan<MB>(lhi, 0u, OpMax(), t2, &c);
+  (void)block_scan<MB>(cnt, 0u, OpAdd(), t0, &a);
+  (void)block_scan<MB>(llo, 0u, OpMax(), t1, &b);
+  (void)block_scan<MB>(lhi, 0u, OpMax(), t2, &c);
   if (threadIdx.x == 0) sum[blockIdx.x] = DSum{a, b, c, 0};
-  if (gl) {
-    // a granule is MUPT-unit ranges of GU / MUPT consecutive lanes; its first
-    // lane with a key start writes it (or its first lane, if none has one)
-    constexpr int TPG = GU / MUPT;
-    const int lane = threadIdx.x & 63;
-    const uint64_t has = __ballot(fku != NONE);
-    const int g0 = lane & ~(TPG - 1);
-    const uint64_t grp = (has >> g0) & ((1ull << TPG) - 1);
-    const int owner = grp ? g0 + __ffsll((unsigned long long)grp) - 1 : g0;
-    if (lane == owner) {
-      GLoc x;
-      x.kb = ea;
-      x.lo = fku != NONE && flo > eb ? flo : eb;
-      x.hi = fku != NONE && fhi > ec ? fhi : ec;
-      x.fk = fku == NONE ? NONE : fku - (u0 + (threadIdx.x / TPG) * GU);
-      gl[(size_t)blockIdx.x * GPC + threadIdx.x / TPG] = x;
-    }
-  }
 }
 
 // per run (one block each): exclusive key count and lo/hi carries per chunk;
@@ -739,309 +701,6 @@ __global__ void __launch_bounds__(TB) k_mtile(const MList *lists, int n, const u
   tile_merge_emit<TB, TCAP>(s, n, tot, kbefore, t, ts, rm, arena);
 }
 
-// ------------------------------------------- tile path (no decoded keys)
-// The granule samples are ranked like the legacy samples (k_mrank); every
-// J-th one in key order is a tile boundary v_t.  Tile t holds the keys in
-// [v_t, v_t+1) of every run: in run l they lie in granules q_l(t)-1 ..
-// q_l(t+1)-1, q_l(v) being the first sample of run l >= v, so at most
-// (c_l + 1) * GU keys, c_l = run l's samples among the tile's J -- at most
-// (J + n) * GU keys in all.  The tile decodes those granules straight from
-// the compressed run into LDS, keeping the keys in its key range.
-constexpr int TB2 = 1024;                  // threads per tile block
-constexpr int TCAP2 = 2048;                // keys per tile
-constexpr int MAXN2 = TCAP2 / GU - 4;      // runs the tile path takes (J >= 4)
-
-// per (tile, run): the granules the tile decodes and where their keys go
-struct TDesc {
-  uint32_t ga;     // first granule
-  uint32_t ntask;  // granules (0: nothing to decode)
-  uint32_t kga;    // run key index of the first decoded key (= keys of the run before it)
-  uint32_t nd;     // keys decoded
-};
-// per tile: its key range [v_t, v_t+1)
-struct TKeys {
-  uint64_t lh, ll, lb, hh, hl, hb;
-};
-
-struct Tile2Lds {
-  TileLdsT<TB2, TCAP2> m;
-  // per run: LDS slot of its first decoded key, its first decoded key's
-  // run index, and its keys below v_t / inside [v_t, v_t+1)
-  uint32_t dbase[MAXN2], kga[MAXN2], low[MAXN2], kept[MAXN2];
-};
-
-// sample g (compact, runs in order): the first key of the run's granule j;
-// pad = its run key index << 32 | its unit (NONE: no key starts in j, and
-// the sample sorts after every key)
-__device__ __forceinline__ uint32_t sk_kidx(const SKey &k) { return (uint32_t)(k.pad >> 32); }
-__device__ __forceinline__ uint32_t sk_us(const SKey &k) { return (uint32_t)k.pad; }
-
-__global__ void __launch_bounds__(MB) k_msample2(const MList *lists, int n, const DSum *sum, const GLoc *gl, SKey *Sm,
-                                                 uint32_t nsamples, MCtl *ctl) {
-  const uint32_t g = blockIdx.x * MB + threadIdx.x;
-  if (g >= nsamples) return;
-  const MList &L = lists[list_of_sample(lists, n, g)];
-  const uint32_t j = g - L.soff;
-  const GLoc x = gl[(size_t)L.c0 * GPC + j];
-  const DSum d = sum[L.c0 + j / GPC];
-  const uint32_t kidx = d.nkeys + x.kb;
-  const uint32_t lo = x.lo > d.lastlo ? x.lo : d.lastlo, hi = x.hi > d.lasthi ? x.hi : d.lasthi;
-  SKey k{~0ull, ~0ull, ~0ull, ((uint64_t)kidx << 32) | NONE};
-  if (x.fk != NONE) {
-    const uint32_t us = j * GU + x.fk;
-    const uint8_t *bp = L.p + (size_t)us * 6;
-    const uint32_t ku = kunits(*gptr<uint8_t>(bp));
-    const bool ok = (ku >= 2 || lo) && (ku == 3 || hi);
-    if (!ok) atomicOr(&ctl->flags, (uint32_t)F_CORRUPT);
-    k.b = rd48g(bp);
-    k.l = ku >= 2 ? rd48g(bp + 6) : (lo ? rd48g(L.p + (size_t)(lo - 1) * 6) : 0);
-    k.h = ku == 3 ? rd48g(bp + 12) : (hi ? rd48g(L.p + (size_t)(hi - 1) * 6) : 0);
-    k.pad = ((uint64_t)kidx << 32) | us;
-  }
-  Sm[g] = k;
-}
-
-// Descriptor of (tile t, run l): q(v) = first sample of run l >= v; the tile
-// decodes granules q(v_t)-1 .. q(v_t+1)-1 (tile 0 from granule 0, the last
-// tile to the run's end).  Thread (t, 0) also writes the tile's key range.
-__global__ void __launch_bounds__(MB) k_mdesc(const MList *lists, int n, uint32_t J, const SKey *Sm,
-                                              const uint32_t *tiles, uint32_t T, TDesc *desc, TKeys *tk) {
-  const uint64_t i = (uint64_t)blockIdx.x * MB + threadIdx.x;
-  if (i >= (uint64_t)T * n) return;
-  const uint32_t t = (uint32_t)(i / n);
-  const int l = (int)(i % n);
-  const MList &L = lists[l];
-  const SKey *R = Sm + L.soff;
-  uint32_t qa = 0, qb = L.ns;
-  SKey vlo{0, 0, 0, 0}, vhi{~0ull, ~0ull, ~0ull, 0};
-  if (t > 0) {
-    vlo = Sm[tiles[(size_t)t * J]];
-    qa = (uint32_t)(sbound<false>(Sm, L.soff, (uint64_t)L.soff + L.ns, vlo.h, vlo.l, vlo.b) - L.soff);
-  }
-  if (t + 1 < T) {
-    vhi = Sm[tiles[(size_t)(t + 1) * J]];
-    qb = (uint32_t)(sbound<false>(Sm, L.soff, (uint64_t)L.soff + L.ns, vhi.h, vhi.l, vhi.b) - L.soff);
-  }
-  if (l == 0) tk[t] = TKeys{vlo.h, vlo.l, vlo.b, vhi.h, vhi.l, vhi.b};
-  TDesc d{qa ? qa - 1 : 0, 0, 0, 0};
-  if (qb > 0) {
-    const SKey A = R[d.ga];
-    d.kga = sk_kidx(A);
-    if (sk_us(A) != NONE) {
-      d.ntask = qb - d.ga;
-      d.nd = (qb < L.ns ? sk_kidx(R[qb]) : L.nkeys) - d.kga;
-    }
-  }
-  desc[i] = d;
-}
-
-// one 6-byte unit of a run (2-byte aligned global loads), 0 past its end
-__device__ __forceinline__ uint64_t gunit(const MList &L, uint32_t u) {
-  return u < L.units ? rd48g(L.p + (size_t)u * 6) : 0;
-}
-
-// A decode task's raw units, loaded before its first key start is known:
-// lane i holds unit g*GU + i, ex[] the four units after the granule (uniform).
-struct TaskUnits {
-  uint64_t x, ex[4];
-};
-// unit g*GU + off (off < GU + 4) to every lane
-__device__ __forceinline__ uint64_t unit_at(const TaskUnits &U, uint32_t off) {
-  const uint64_t v = __shfl(U.x, (int)(off & 63), 64);
-  if (off < 64) return v;
-  const uint32_t e = off - 64;
-  return e == 0 ? U.ex[0] : e == 1 ? U.ex[1] : e == 2 ? U.ex[2] : U.ex[3];
-}
-
-// Decode task: the keys starting in granule g of a run, from its first key
-// start us = g*GU + fk, by one wave (lane i: unit us + i).  Unit types need
-// the two units before; a key's lo / hi words come from its own units
-// (12/18-byte keys), the last lo / hi unit before it in the task (a lane's
-// value, shuffled), or else are the granule's first key's (its sample,
-// clo / chi).  Each key lands at LDS slot dpos + its rank in the task; keys
-// below v_t and inside [v_t, v_t+1) are counted per run.
-__device__ __forceinline__ void decode_granule(const MList &L, const TaskUnits &U, uint32_t us, uint32_t fk,
-                                               uint64_t clo, uint64_t chi, uint32_t uend, uint32_t dpos, uint8_t run,
-                                               bool open_lo, const SKey &vlo, bool open_hi, const SKey &vhi,
-                                               TileLdsT<TB2, TCAP2> &m, uint32_t *low, uint32_t *kept, bool &bad,
-                                               int lane) {
-  const uint64_t below = (1ull << lane) - 1;
-  const uint32_t u = us + lane;
-  const bool in = u < uend;
-  const uint64_t x = unit_at(U, fk + lane), x1 = unit_at(U, fk + lane + 1), x2 = unit_at(U, fk + lane + 2);
-  const uint32_t b0 = (uint32_t)x & 0xff, sb = (uint32_t)(x >> 9) & 1u;
-  const uint32_t sb1 = __shfl_up(sb, 1, 64), sb2 = __shfl_up(sb, 2, 64);
-  const uint32_t c2 = __shfl_up(b0 & 0x06, 2, 64);
-  int ty = 3;
-  if (in) {
-    if (lane == 0) ty = 0;  // the granule's first key start
-    else if (!sb) ty = sb1 ? 1 : 2;
-    else if (sb1) ty = 0;
-    else ty = (lane >= 2 && sb2 && c2 == 0) ? 2 : 0;  // utype() (lane 1: its predecessor is a key start)
-  }
-  const uint64_t bk = __ballot(ty == 0), bl = __ballot(ty == 1), bh = __ballot(ty == 2);
-  const uint64_t ml = bl & below, mh = bh & below;
-  const int sl = ml ? 63 - __clzll(ml) : 0, sh = mh ? 63 - __clzll(mh) : 0;
-  const uint64_t vl = __shfl(x, sl, 64), vh = __shfl(x, sh, 64);
-  bool keep = false, lowk = false;
-  if (ty == 0) {
-    const uint32_t ku = kunits((uint8_t)b0);
-    const uint64_t kl = ku >= 2 ? x1 : (ml ? vl : clo);
-    const uint64_t kh = ku == 3 ? x2 : (mh ? vh : chi);
-    if ((uint64_t)u + ku > L.units) bad = true;
-    lowk = !open_lo && key_lt(kh, kl, x, vlo.h, vlo.l, vlo.b);
-    keep = !lowk && (open_hi || key_lt(kh, kl, x, vhi.h, vhi.l, vhi.b));
-    const uint32_t e = dpos + (uint32_t)__popcll(bk & below);
-    m.h[e] = kh;
-    m.l[e] = kl;
-    m.b[e] = x;
-    m.run[e] = run;
-  }
-  const uint32_t nlow = (uint32_t)__popcll(__ballot(lowk)), nkeep = (uint32_t)__popcll(__ballot(keep));
-  if (lane == 0) {
-    if (nlow) atomicAdd(low, nlow);
-    if (nkeep) atomicAdd(kept, nkeep);
-  }
-}
-
-__device__ __forceinline__ uint32_t wave_excl_sum(uint32_t v, int lane) {
-  uint32_t x = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = __shfl_up(x, o, 64);
-    if (lane >= o) x += y;
-  }
-  return x - v;
-}
-
-
-// One tile of the tile path: decode every (run, granule) of the tile's
-// descriptors (one wave task each, all independent, a wave's tasks loaded
-// together), compact each run's keys inside [v_t, v_t+1) into contiguous
-// segments, then merge and emit as the legacy tile does.
-// MODE (diagnostic, GBGPU_MERGE_MODE): 0 full; stop after 1 the decode,
-// 2 the compaction, 3 the merge rounds
-template <int MODE>
-__global__ void __launch_bounds__(TB2) __attribute__((amdgpu_waves_per_eu(8, 8))) k_mtile2(const MList *lists, int n, const TDesc *desc, const TKeys *tkeys,
-                                                const SKey *Sm, uint32_t T, TileSum *ts, int rm, uint8_t *arena,
-                                                MCtl *ctl) {
-  __shared__ Tile2Lds s;
-  constexpr uint32_t W = TB2 / 64;
-  const uint32_t t = blockIdx.x;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  // every wave: the run descriptors (one lane per run) and their prefixes
-  const TDesc D = lane < n ? desc[(size_t)t * n + lane] : TDesc{0, 0, 0, 0};
-  const TKeys K = tkeys[t];
-  const SKey vlo{K.lh, K.ll, K.lb, 0}, vhi{K.hh, K.hl, K.hb, 0};
-  const uint32_t dpre = wave_excl_sum(D.nd, lane), tpre = wave_excl_sum(D.ntask, lane);
-  const uint32_t ndec = __shfl(dpre + D.nd, n - 1, 64), ntasks = __shfl(tpre + D.ntask, n - 1, 64);
-  if (ndec > TCAP2) {  // more keys than the tile holds: retry with a smaller J
-    if (threadIdx.x == 0) {
-      ts[t] = TileSum{0, 0, 0, 0, 0, 0, 0, 0};
-      atomicOr(&ctl->flags, (uint32_t)F_CAPACITY);
-    }
-    return;
-  }
-  if (wid == 0 && lane < n) {
-    s.dbase[lane] = dpre;
-    s.kga[lane] = D.kga;
-    s.low[lane] = 0;
-    s.kept[lane] = 0;
-  }
-  __syncthreads();
-  bool bad = false;
-  // the wave's tasks k = wid + W*i, two at a time: both loaded, then decoded
-  for (uint32_t k = wid; k < ntasks; k += 2 * W) {
-    const bool hb = k + W < ntasks;
-    const int la = (int)__popcll(__ballot(lane < n && tpre + D.ntask <= k));  // runs ending by k
-    const int lb = hb ? (int)__popcll(__ballot(lane < n && tpre + D.ntask <= k + W)) : la;
-    const uint32_t ga = __shfl(D.ga, la, 64) + (k - __shfl(tpre, la, 64));
-    const uint32_t gb = __shfl(D.ga, lb, 64) + (k + W - __shfl(tpre, lb, 64));
-    const MList &La = lists[la];
-    const MList &Lb = lists[lb];
-    const SKey Sa = Sm[La.soff + ga];
-    SKey Sb{0, 0, 0, NONE};
-    TaskUnits Ua, Ub;
-    Ua.x = gunit(La, ga * GU + lane);
-#pragma unroll
-    for (int e = 0; e < 4; e++) Ua.ex[e] = gunit(La, ga * GU + GU + e);
-    if (hb) {
-      Sb = Sm[Lb.soff + gb];
-      Ub.x = gunit(Lb, gb * GU + lane);
-#pragma unroll
-      for (int e = 0; e < 4; e++) Ub.ex[e] = gunit(Lb, gb * GU + GU + e);
-    }
-    if (sk_us(Sa) != NONE) {
-      const uint32_t us = sk_us(Sa);
-      decode_granule(La, Ua, us, us - ga * GU, Sa.l, Sa.h, min((ga + 1) * (uint32_t)GU, La.units),
-                     s.dbase[la] + (sk_kidx(Sa) - s.kga[la]), (uint8_t)la, t == 0, vlo, t + 1 == T, vhi, s.m,
-                     &s.low[la], &s.kept[la], bad, lane);
-    }
-    if (hb && sk_us(Sb) != NONE) {
-      const uint32_t us = sk_us(Sb);
-      decode_granule(Lb, Ub, us, us - gb * GU, Sb.l, Sb.h, min((gb + 1) * (uint32_t)GU, Lb.units),
-                     s.dbase[lb] + (sk_kidx(Sb) - s.kga[lb]), (uint8_t)lb, t == 0, vlo, t + 1 == T, vhi, s.m,
-                     &s.low[lb], &s.kept[lb], bad, lane);
-    }
-  }
-  if (bad) atomicOr(&ctl->flags, (uint32_t)F_CORRUPT);
-  __syncthreads();
-  if (MODE == 1) {
-    if (threadIdx.x == 0) ts[t] = TileSum{0, 0, s.m.h[0], 0, 0, 0, 0, 0};
-    return;
-  }
-  // segment starts (kept keys of the runs before) and the keys before the tile
-  uint64_t kbefore = 0;
-  uint32_t tot = 0;
-  for (int l = 0; l < n; l++) {
-    if (threadIdx.x == 0) s.m.seg[l] = tot;
-    tot += s.kept[l];
-    kbefore += s.kga[l] + s.low[l];
-  }
-  if (tot == 0) {
-    if (threadIdx.x == 0) ts[t] = TileSum{0, 0, 0, 0, 0, 0, 0, 0};
-    return;
-  }
-  if (threadIdx.x == 0) s.m.seg[n] = tot;
-  __syncthreads();
-  // compact: entry e of segment l comes from dbase[l] + low[l] + (e - seg[l])
-  constexpr int KC = TCAP2 / TB2;
-  uint64_t ch[KC], cl[KC], cb[KC];
-  uint8_t cr[KC];
-#pragma unroll
-  for (int j = 0; j < KC; j++) {
-    const uint32_t e = threadIdx.x + TB2 * j;
-    if (e >= tot) continue;
-    int lo = 0, hi = n - 1;
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (s.m.seg[mid] <= e) lo = mid;
-      else hi = mid - 1;
-    }
-    const uint32_t src = s.dbase[lo] + s.low[lo] + (e - s.m.seg[lo]);
-    ch[j] = s.m.h[src];
-    cl[j] = s.m.l[src];
-    cb[j] = s.m.b[src];
-    cr[j] = s.m.run[src];
-  }
-  __syncthreads();
-#pragma unroll
-  for (int j = 0; j < KC; j++) {
-    const uint32_t e = threadIdx.x + TB2 * j;
-    if (e >= tot) continue;
-    s.m.h[e] = ch[j];
-    s.m.l[e] = cl[j];
-    s.m.b[e] = cb[j];
-    s.m.run[e] = cr[j];
-  }
-  __syncthreads();
-  if (MODE == 2) {
-    if (threadIdx.x == 0) ts[t] = TileSum{0, 0, s.m.h[0], 0, 0, 0, 0, 0};
-    return;
-  }
-  tile_merge_emit<TB2, TCAP2, MODE>(s.m, n, tot, kbefore, t, ts, rm, arena);
-}
-
 // --------------------------------------------------------- tile offsets
 // Walk a thread's SCAN_TPB/MB tiles: bytes of its non-empty tiles, the first
 // key of the first one compressed against (ph, pl) when `has`, else skipped.
@@ -1265,12 +924,12 @@ struct MergeState {
   std::mutex mu;
   hipStream_t st = nullptr;
   hipEvent_t ev[6] = {};
-  Buf mlist, dsum, khi, klo, kb, shi, slo, sb, tiles, off, ts, to, bs, bo, ctl, arena, in, out, gloc, ginfo;
+  Buf mlist, dsum, khi, klo, kb, shi, slo, sb, tiles, off, ts, to, bs, bo, ctl, arena, in, out;
   MList *h_lists = nullptr;  // pinned
   MCtl *h_ctl = nullptr;     // pinned
   float ms[6] = {0, 0, 0, 0, 0, 0};
   int64_t nkeys = 0, ntiles = 0;
-  int path = 0;  // last merge: 1 tile path, 2 legacy (decoded keys)
+  int path = 0;  // last merge: 2 (the decoded-key pipeline; 1 was the retired tile path)
   bool has_last = false;
   uint8_t last_key[18] = {};
 };
@@ -1293,7 +952,7 @@ void state_free(MergeState *s) {
   if (!s) return;
   if (s->st) (void)hipStreamSynchronize(s->st);
   Buf *bufs[] = {&s->mlist, &s->dsum, &s->khi, &s->klo, &s->kb, &s->shi, &s->slo, &s->sb, &s->tiles, &s->off,
-                 &s->ts, &s->to, &s->bs, &s->bo, &s->ctl, &s->arena, &s->in, &s->out, &s->gloc, &s->ginfo};
+                 &s->ts, &s->to, &s->bs, &s->bo, &s->ctl, &s->arena, &s->in, &s->out};
   for (auto *b : bufs) b->release();
   if (s->h_lists) (void)hipHostFree(s->h_lists);
   if (s->h_ctl) (void)hipHostFree(s->h_ctl);
@@ -1350,72 +1009,7 @@ static int ensure_tile_bufs(MergeState *s, uint64_t NS, uint64_t T, int n) {
   return 0;
 }
 
-// Tile path: no decoded keys in HBM.  Count pass (+ granule state), granule
-// samples, rank, per-(tile, run) granule ranges, tiles decoding their keys
-// from the compressed runs.  RETRY: a tile overflowed at every J (keys
-// repeated inside a run), the caller runs the legacy path.
-static int run_tiles(MergeState *s, int n, uint32_t nch, uint64_t units, int rm, uint64_t maxoff, uint8_t *out,
-                     int64_t cap) {
-  hipStream_t st = s->st;
-  MList *dl = s->mlist.as<MList>();
-  MCtl *dctl = s->ctl.as<MCtl>();
-  uint64_t NS = 0;
-  for (int i = 0; i < n; i++) {
-    MList &L = s->h_lists[i];
-    L.soff = (uint32_t)NS;
-    L.ns = cdiv(L.units, GU);
-    NS += L.ns;
-  }
-  if (NS >= 0x7fffffffULL) return RETRY;
-  if (s->gloc.ensure(sizeof(GLoc) * (size_t)nch * GPC) ||
-      s->shi.ensure(sizeof(SKey) * NS) || s->arena.ensure(18 * (size_t)std::max<uint64_t>(units, 1) + 16))
-    return ENOMEM;
-  SKey *Sm = s->shi.as<SKey>();
-  const uint32_t NS32 = (uint32_t)NS;
-  MCHECK(hipEventRecord(s->ev[0], st));
-  MCHECK(hipMemcpyAsync(dl, s->h_lists, sizeof(MList) * n, hipMemcpyHostToDevice, st));
-  MCHECK(hipMemsetAsync(dctl, 0, sizeof(MCtl), st));
-  k_mcount<<<nch, MB, 0, st>>>(dl, n, s->dsum.as<DSum>(), dctl, s->gloc.as<GLoc>());
-  k_mscan<<<n, 1024, 0, st>>>(dl, s->dsum.as<DSum>());
-  k_msample2<<<cdiv(NS, MB), MB, 0, st>>>(dl, n, s->dsum.as<DSum>(), s->gloc.as<GLoc>(), Sm, NS32, dctl);
-  MCHECK(hipGetLastError());
-  MCHECK(hipEventRecord(s->ev[1], st));
-  MCHECK(hipMemcpyAsync(s->h_lists, dl, sizeof(MList) * n, hipMemcpyDeviceToHost, st));
-  MCHECK(hipMemcpyAsync(s->h_ctl, dctl, sizeof(MCtl), hipMemcpyDeviceToHost, st));
-  MCHECK(hipStreamSynchronize(st));
-  if (s->h_ctl->flags & F_FIRST) return EINVAL;  // first key must be 18 bytes
-  if (s->h_ctl->flags & F_CORRUPT) return GBGPU_ECORRUPT;
-  s->nkeys = 0;
-  for (int i = 0; i < n; i++) s->nkeys += s->h_lists[i].nkeys;
-  for (uint32_t J = (uint32_t)(TCAP2 / GU - n); J >= 1; J /= 2) {
-    const uint64_t T = (NS + J - 1) / J;
-    if ((T + 1) * (uint64_t)n >= 0xffffffffULL) return RETRY;
-    s->ntiles = (int64_t)T;
-    if (ensure_tile_bufs(s, NS, T, n) || s->off.ensure(sizeof(TDesc) * T * n) || s->ginfo.ensure(sizeof(TKeys) * T))
-      return ENOMEM;
-    Sm = s->shi.as<SKey>();
-    const uint32_t T32 = (uint32_t)T;
-    TDesc *desc = s->off.as<TDesc>();
-    TKeys *tk = s->ginfo.as<TKeys>();
-    k_mrank<<<cdiv(NS, MB), MB, 0, st>>>(dl, n, Sm, NS32, s->tiles.as<uint32_t>());
-    k_mdesc<<<cdiv(T * n, MB), MB, 0, st>>>(dl, n, J, Sm, s->tiles.as<uint32_t>(), T32, desc, tk);
-    MCHECK(hipGetLastError());
-    MCHECK(hipEventRecord(s->ev[2], st));
-    const char *mm = std::getenv("GBGPU_MERGE_MODE");  // diagnostic: stop tiles early
-    const int mode = mm ? std::atoi(mm) : 0;
-    auto kt = mode == 1 ? k_mtile2<1> : mode == 2 ? k_mtile2<2> : mode == 3 ? k_mtile2<3> : k_mtile2<0>;
-    kt<<<T32, TB2, 0, st>>>(dl, n, desc, tk, Sm, T32, s->ts.as<TileSum>(), rm, s->arena.as<uint8_t>(), dctl);
-    MCHECK(hipGetLastError());
-    MCHECK(hipEventRecord(s->ev[3], st));
-    const int rc = finish_tiles(s, T32, maxoff, cap, out, dctl);
-    if (rc != RETRY) return rc;
-    MCHECK(hipMemsetAsync(dctl, 0, sizeof(MCtl), st));
-  }
-  return RETRY;
-}
-
-// Legacy path (more runs than the tile path takes, or a tile path overflow):
-// every key decoded to 24-byte SoA in HBM, samples every S keys.
+// Every key decoded to 24-byte SoA in HBM, samples every S keys.
 static int run_legacy(MergeState *s, int n, uint32_t nch, uint64_t units, int rm, uint64_t maxoff, uint8_t *out,
                       int64_t cap) {
   hipStream_t st = s->st;
@@ -1426,7 +1020,7 @@ static int run_legacy(MergeState *s, int n, uint32_t nch, uint64_t units, int rm
   MCHECK(hipEventRecord(s->ev[0], st));
   MCHECK(hipMemcpyAsync(dl, s->h_lists, sizeof(MList) * n, hipMemcpyHostToDevice, st));
   MCHECK(hipMemsetAsync(dctl, 0, sizeof(MCtl), st));
-  k_mcount<<<nch, MB, 0, st>>>(dl, n, s->dsum.as<DSum>(), dctl, nullptr);
+  k_mcount<<<nch, MB, 0, st>>>(dl, n, s->dsum.as<DSum>(), dctl);
   k_mscan<<<n, 1024, 0, st>>>(dl, s->dsum.as<DSum>());
   k_mdecode<<<nch, MB, 0, st>>>(dl, n, s->dsum.as<DSum>(), K, dctl);
   MCHECK(hipGetLastError());
@@ -1514,18 +1108,8 @@ static int run(MergeState *s, const uint8_t *const *lists, const int64_t *sizes,
   const int64_t maxoff = std::max<int64_t>(max_offset(total, mrs, cap), 1);
   if (s->mlist.ensure(sizeof(MList) * MAXN) || s->dsum.ensure(sizeof(DSum) * nch) || s->ctl.ensure(sizeof(MCtl)))
     return ENOMEM;
-  // GBGPU_MERGE_PATH=tiles selects the tile path (keys decoded into each
-  // tile's LDS: about half the HBM bytes, measured slower)
-  const char *mp = std::getenv("GBGPU_MERGE_PATH");
-  int rc = RETRY;
-  if (n <= MAXN2 && mp && std::strcmp(mp, "tiles") == 0) {
-    s->path = 1;
-    rc = run_tiles(s, n, nch, units, rm, (uint64_t)maxoff, out, cap);
-  }
-  if (rc == RETRY) {
-    s->path = 2;
-    rc = run_legacy(s, n, nch, units, rm, (uint64_t)maxoff, out, cap);
-  }
+  s->path = 2;
+  const int rc = run_legacy(s, n, nch, units, rm, (uint64_t)maxoff, out, cap);
   if (rc) return rc;
   const uint32_t fl = s->h_ctl->flags;
   if (fl & F_CORRUPT) return GBGPU_ECORRUPT;

@@ -678,7 +678,7 @@ class Engine:
         return list(ms), nk.value, nt.value
 
     def merge_path(self):
-        """1: the last merge ran the tile path, 2: the legacy (decoded keys) path."""
+        """2: the last merge ran (the decoded-key pipeline), 0: none yet."""
         return self.lib.gbgpu_merge_path(self.ctx)
 
     def last_topk_device(self):

@@ -8,5 +8,4 @@ timeout -k 10 600 python -u -m pytest $R/tests/test_merge.py ${MERGE_FULL:+$R/te
 tail -3 $O/merge_tests.log
 timeout -k 10 300 python -u $R/scripts/merge_time.py ${MERGE_KEYS:-400000000} > $O/merge_time.log 2>&1 || { echo "timing failed"; tail -30 $O/merge_time.log; exit 1; }
 cat $O/merge_time.log
-[ -n "$MERGE_TILES_TOO" ] && { GBGPU_MERGE_PATH=tiles timeout -k 10 300 python -u $R/scripts/merge_time.py ${MERGE_KEYS:-400000000} 2 > $O/merge_time_tiles.log 2>&1 || { echo "tiles timing failed"; tail -30 $O/merge_time_tiles.log; exit 1; }; cat $O/merge_time_tiles.log; }
 exit 0

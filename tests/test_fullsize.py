@@ -97,13 +97,10 @@ def test_config4_shards_and_merge(engine):
     assert np.array_equal(s, exp["scores"][:100].astype(np.float64))
 
 
-@pytest.mark.parametrize("path", ["decoded", "tiles"])
-def test_config5_fullsize_merge(engine, path, monkeypatch):
+def test_config5_fullsize_merge(engine):
     # 400M keys in 8 tiered runs (1:2:..:128), ~4.4 GB: GPU bytes == oracle
-    # bytes, under both merge pipelines (GBGPU_MERGE_PATH)
+    # bytes
     import torch
-    if path == "tiles":
-        monkeypatch.setenv("GBGPU_MERGE_PATH", "tiles")
     m = gbgpu.MergeRuns(400_000_000, nruns=8, seed=5, nterms=20000, nthreads=16)
     try:
         sizes = [len(a) for a in m.arrays]

@@ -185,21 +185,16 @@ def test_gpu_merge_large_vs_oracle_and_properties(engine):
     assert nk > 0 and nt > 0
 
 
-@pytest.fixture(params=["decoded", "tiles"])
-def merge_path(request, monkeypatch):
-    """Run a test under both merge pipelines (GBGPU_MERGE_PATH)."""
-    if request.param == "tiles":
-        monkeypatch.setenv("GBGPU_MERGE_PATH", "tiles")
-    else:
-        monkeypatch.delenv("GBGPU_MERGE_PATH", raising=False)
-    return 1 if request.param == "tiles" else 2
+@pytest.fixture
+def merge_path():
+    """The merge pipeline every merge runs (gbgpu_merge_path): 2, the decoded
+    keys (the tile pipeline, 1, was retired in round 4: DESIGN.md §3b)."""
+    return 2
 
 
 @pytest.mark.gpu
 def test_gpu_merge_paths_agree(engine, merge_path):
-    # the tile path (<= 28 runs) and the decoded-key path give the same
-    # bytes, both equal to the oracle's; more runs than the tile path takes
-    # fall back to the decoded-key path
+    # 8 and 40 runs: the oracle's bytes, and the pipeline reported
     runs = tiered_runs(30000, nruns=8, seed=31, dup_frac=0.2, neg_frac=0.05, nterms=30)
     total = sum(map(len, runs))
     for rm in (0, 1):
@@ -224,9 +219,9 @@ def _run(term, docid, wordpos):
 @pytest.mark.gpu
 def test_gpu_merge_long_carries(engine, merge_path):
     # one docid with 30000 positions: 6-byte keys whose lo and hi units lie
-    # hundreds of granules back (the tile path decodes a granule with the
-    # run's carries, not its own bytes); a newer run interleaves docids around
-    # it and repeats some of its keys
+    # thousands of units back (the decode inherits them through the chunk
+    # carries of k_mscan); a newer run interleaves docids around it and
+    # repeats some of its keys
     d = 1 << 30
     a = _run(77, np.full(30000, d), np.arange(30000))
     b = _run(77, np.concatenate([np.arange(d - 3000, d + 3000), np.full(500, d)]),
