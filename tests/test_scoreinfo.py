@@ -139,6 +139,16 @@ def test_reference_buffers_consistent(path):
         # kicked out of the tree keep their records (Posdb.cpp:6160-6193)
         assert len(d) >= n and len(set(d["docid"].tolist())) == len(d)
         assert set(exp["docids"][:n].tolist()) <= set(d["docid"].tolist())
+        # the pieces in order (Msg39.cpp:345-457: piece j covers docids
+        # [j, j+1] x MAX_DOCID / splits), and inside a piece the tree order
+        # high -> low, which the final tree keeps for the docids still in it
+        delta = 0x3fffffffff // params.num_docid_splits
+        piece = np.minimum(d["docid"] // delta, params.num_docid_splits - 1)
+        assert np.all(np.diff(piece) >= 0), "pieces out of order"
+        rank = {int(x): i for i, x in enumerate(exp["docids"])}
+        for j in np.unique(piece):
+            r = [rank[int(x)] for x in d["docid"][piece == j] if int(x) in rank]
+            assert r == sorted(r), ("tree order inside piece", int(j))
         n = 0
     else:
         assert np.array_equal(d["docid"], exp["docids"][:n])
