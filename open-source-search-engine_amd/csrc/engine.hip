@@ -3478,8 +3478,8 @@ __device__ BoundCore group_bound_core(const DevPlan *__restrict__ pl, const Coun
     if (pl->gflags0[g] & BF_HALFSTOPWIKIBIGRAM) hs = true;
     const SubRun run = sub_run_at(pl, ctr, svl[lid], lid, g, x, s);
     if (sr == -1) {  // getSiteRank / getLangId of the 12-byte run head
-      gu8 *h = run.own;
-      const uint32_t b0 = h[0], b6 = h[6], b7 = h[7];
+      const uint64_t v0 = load6(run.own), v6 = load6(run.own + 6);  // (two 6-byte loads, not bytes)
+      const uint32_t b0 = (uint32_t)v0 & 0xff, b6 = (uint32_t)v6 & 0xff, b7 = (uint32_t)(v6 >> 8) & 0xff;
       sr = (int)(((b6 >> 5) | ((b7 & 1) << 3)) & 0x0f);
       lang = (int)((b6 & 0x1f) | ((b0 & 0x08) ? 0x20 : 0));
     }
@@ -3487,15 +3487,15 @@ __device__ BoundCore group_bound_core(const DevPlan *__restrict__ pl, const Coun
     // (Posdb.cpp:7851-7897); a body key weaker than the best ends the list
     for (int k = (int)run.len - 1; k >= 0; k--) {
       if (k == 1) continue;  // second half of the 12-byte head
-      gu8 *dc = run.key((uint32_t)k);
-      const uint32_t hg = (dc[3] >> 2) & 0x0f;
+      const uint64_t dv = load6(run.key((uint32_t)k));
+      const uint32_t hg = (uint32_t)(dv >> 26) & 0x0f;  // byte 3 >> 2
       if (hg == GB_HG_INLINKTEXT) return BoundCore{-1, 0.0f};
       const float w = W.hashgroup[hg];
       if (w < best) {
         if (hg == GB_HG_BODY) break;
         continue;
       }
-      const unsigned dr = ((uint32_t)dc[1] >> 3) & 0x1f;
+      const unsigned dr = (unsigned)(dv >> 11) & 0x1f;  // byte 1 >> 3
       if (w > best) {
         best = w;
         bestDR = dr;
@@ -3521,6 +3521,10 @@ __device__ BoundCore group_bound_core(const DevPlan *__restrict__ pl, const Coun
   return BoundCore{1, score};
 }
 
+// a key's ring-buffer slot: its word position (bytes 2-5 >> 14) mod RING
+__device__ __forceinline__ uint32_t ring_slot(gu8 *kp) {  // bytes 2-5 >> 14: the word position
+  return ((uint32_t)(load6(kp) >> 16) >> 14) & (RING - 1);
+}
 // ring-buffer slots this wave's lanes write for one group's runs (value v);
 // returns the slot of the head of the group's last run (ourFirstPos)
 __device__ int ring_fill(const DevPlan *__restrict__ pl, const Counters *ctr, int g, uint32_t s, uint32_t lm, const Loc *svl,
@@ -3533,14 +3537,9 @@ __device__ int ring_fill(const DevPlan *__restrict__ pl, const Counters *ctr, in
     const SubRun run = sub_run_at(pl, ctr, svl[lid], lid, g, x, s);
     for (uint32_t k = lane; k < run.len; k += 64) {
       if (k == 1) continue;
-      gu8 *kp = run.key(k);
-      const uint32_t wp = ((uint32_t)kp[2] | ((uint32_t)kp[3] << 8) | ((uint32_t)kp[4] << 16) |
-                           ((uint32_t)kp[5] << 24)) >> 14;
-      ring[wp & (RING - 1)] = v;
+      ring[ring_slot(run.key(k))] = v;
     }
-    gu8 *h = run.own;
-    first = (int)((((uint32_t)h[2] | ((uint32_t)h[3] << 8) | ((uint32_t)h[4] << 16) |
-                    ((uint32_t)h[5] << 24)) >> 14) & (RING - 1));
+    first = (int)ring_slot(run.own);
   }
   return first;
 }
@@ -3627,10 +3626,6 @@ __device__ __forceinline__ uint4 rep_entry(uint32_t key, float B, uint64_t d, bo
 // keys in a group takes the wave's 4096-slot ring (the reference's own
 // buffer) instead.
 constexpr int BL_SLOTS = 32;
-__device__ __forceinline__ uint32_t ring_slot(gu8 *kp) {
-  return (((uint32_t)kp[2] | ((uint32_t)kp[3] << 8) | ((uint32_t)kp[4] << 16) | ((uint32_t)kp[5] << 24)) >> 14) &
-         (RING - 1);
-}
 // group g's slots into col[0..n) (column layout: entry k of lane at [k][lane]);
 // false on overflow.  first: the head slot of the last present sublist.
 __device__ bool lane_slots(const DevPlan *__restrict__ pl, const Counters *ctr, int g, uint32_t s, uint32_t lm,
