@@ -596,6 +596,31 @@ def main():
             "note": "gbgpu_query with the lists in pageable host memory, uploaded every call; not `value`",
         }
         del host
+        # the read path into HBM (f3): the lists as one resident Posdb file
+        # image, each query cutting its termlists from it on the device
+        # (gbgpu_file_list, RdbScan's read) and freeing them after
+        blob = b"".join(first_lists)
+        fh = eng.file_upload(blob)
+        del blob
+        offs = np.cumsum([0] + [len(x) for x in first_lists[:-1]]).tolist()
+        n_fr = 20
+        for it in range(n_fr + 2):
+            if it == 2:
+                t_fr = time.perf_counter()
+            fl = [eng.file_list(fh, o, len(x)) for o, x in zip(offs, first_lists)]
+            r_fr = eng.query_resident(qs[0].terms, fl, ps[0])
+            for h in fl:
+                eng.free(h)
+            if r_fr.hits != r0.hits or not np.array_equal(r_fr.docids, r0.docids):
+                raise RuntimeError("file-cut query differs from the host-buffer query")
+        el_fr = time.perf_counter() - t_fr
+        eng.file_free(fh)
+        result["file_read"] = {
+            "queries_per_sec": round(n_fr / el_fr, 3),
+            "keys_scanned_GBps": round(qbytes[0] * n_fr / el_fr / 1e9, 3),
+            "note": "termlists cut per query from a resident Posdb file image (gbgpu_file_list: device copy, "
+                    "structure check, page map), queried, freed; one query at a time; not `value`",
+        }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline_query(qs[0], first_lists)
         if "clustering" in result:

@@ -220,6 +220,23 @@ int gbgpu_query(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms, const gbgp
  * Posdb.cpp:5671-5703 is applied to the device copy) and query it many times. */
 int gbgpu_list_upload(gbgpu_ctx *ctx, const uint8_t *bytes, int64_t size, int32_t *handle);
 int gbgpu_list_free(gbgpu_ctx *ctx, int32_t handle);
+
+/* Resident Rdb files (the read path into HBM): a Posdb file
+ * image (termlists back to back, as Msg3 reads them from disk, size a
+ * multiple of 6) is uploaded once; a termlist or a docid-range piece of one is
+ * then cut from it on the device with no host copy.  gbgpu_file_list is
+ * RdbScan's read (RdbScan.cpp:319-361) over HBM: `offset`/`size` are the byte
+ * range the caller's RdbMap gives (Msg3.cpp:534-584: RdbMap::getPageRange, getKey);
+ * when the key at `offset` is compressed (12 or 6 bytes), `key18` is the full
+ * key RdbScan writes in its place (m_startKey, the map's page key) -- it must
+ * match the stored bytes, else EINVAL; for an 18-byte first key it may be
+ * NULL.  The new list handle is a gbgpu_list_upload list (its own copy, the
+ * same checks), freed with gbgpu_list_free; the file stays until
+ * gbgpu_file_free. */
+int gbgpu_file_upload(gbgpu_ctx *ctx, const uint8_t *bytes, int64_t size, int32_t *file);
+int gbgpu_file_list(gbgpu_ctx *ctx, int32_t file, int64_t offset, int64_t size, const uint8_t *key18,
+                    int32_t *handle);
+int gbgpu_file_free(gbgpu_ctx *ctx, int32_t file);
 /* gbgpu_query and gbgpu_query_resident are re-entrant: Msg39 runs several
  * intersect threads at once (Msg39.cpp:1019-1027, Parms.cpp:12356); each call
  * takes a free query slot (its own HIP stream and buffers over the shared

@@ -5193,10 +5193,15 @@ struct DevBuf {
 // Device memory of one resident list.  Shared by the list table and every
 // query in flight that reads it: gbgpu_list_free drops the table's reference,
 // and the memory goes when the last in-flight query holding it is collected.
+// Stream-ordered on the context's upload stream (hipMallocAsync): every query
+// that reads a list holds a reference until its stream has drained
+// (QuerySlot::held), so the last reference drops with no kernel left reading
+// it and the free needs no device-wide synchronisation.
 struct ListMem {
   uint8_t *d = nullptr;
+  hipStream_t st = nullptr;
   ~ListMem() {
-    if (d) (void)hipFree(d);
+    if (d) (void)hipFreeAsync(d, st);
   }
 };
 
@@ -5342,6 +5347,15 @@ struct QuerySlot {
 
 constexpr int MAX_SLOTS = 64;
 
+// A Posdb Rdb file image resident in HBM (gbgpu_file_upload): the bytes as
+// they lie on disk, termlists back to back.  Termlists are cut from it on the
+// device (gbgpu_file_list), the read Msg3/RdbScan makes from disk.
+struct FileEntry {
+  std::shared_ptr<ListMem> mem;
+  int64_t size = 0;
+  bool live = false;
+};
+
 // Exchange sequencer (gbgpu.h "Exchange ordering"): one caller at a time,
 // admitted in increasing sequence number.
 struct gbgpu_seq {
@@ -5384,6 +5398,7 @@ struct gbgpu_ctx {
   std::condition_variable free_cv;
   std::mutex lists_mu;
   std::vector<ListEntry> lists;
+  std::vector<FileEntry> files;  // resident Rdb file images (gbgpu_file_upload), under lists_mu
   std::mutex slots_mu;  // guards growth of the slot table
   QuerySlot *slots[MAX_SLOTS] = {};
   int nslots = 0;
@@ -5429,21 +5444,35 @@ static int build_page_map(const uint8_t *d, uint32_t units, uint32_t *pm, hipStr
   return 0;
 }
 
-static int upload_list(gbgpu_ctx *ctx, const uint8_t *bytes, int64_t size, int32_t *handle) {
+// a list entry of `size` original bytes (18-byte first key), its device
+// image and page map allocated and zeroed on the upload stream
+static int alloc_list(gbgpu_ctx *ctx, int64_t size, ListEntry &e) {
   if (size < 0 || (size > 0 && size < 18) || (size > 0 && (size - 18) % 6 != 0)) return EINVAL;
   if ((size - 6) / 6 > 0xfffffff0LL) return GBGPU_ECAPACITY;
-  // the first key must be a whole 18-byte key (Posdb.cpp:5671-5703 swaps it)
-  if (size > 0 && (bytes[0] & 0x06)) return GBGPU_ECORRUPT;
-  ListEntry e;
   e.size = size;
   e.units = size ? (uint32_t)((size - 6) / 6) : 0;
   const size_t lbytes = align256((size_t)(size ? size - 6 : 0) + LIST_PAD);
   const size_t alloc = lbytes + page_map_bytes(e.units);
   e.mem = std::make_shared<ListMem>();
-  if (hipMalloc(&e.mem->d, alloc) != hipSuccess) return ENOMEM;
+  e.mem->st = ctx->upload_stream;
+  if (hipMallocAsync(reinterpret_cast<void **>(&e.mem->d), alloc, ctx->upload_stream) != hipSuccess) return ENOMEM;
   e.d = e.mem->d;
   e.pm = reinterpret_cast<uint32_t *>(e.d + lbytes);
-  HIPCHECK(hipMemsetAsync(e.d, 0, alloc, ctx->upload_stream));
+  // the image's own bytes are written next: zero the pad and the page map
+  const size_t img = (size_t)(size ? size - 6 : 0);
+  HIPCHECK(hipMemsetAsync(e.d + img, 0, alloc - img, ctx->upload_stream));
+  return 0;
+}
+
+static int finish_list(gbgpu_ctx *ctx, ListEntry &e, const uint8_t *host_bytes, const uint8_t *first18,
+                       int32_t *handle);
+
+static int upload_list(gbgpu_ctx *ctx, const uint8_t *bytes, int64_t size, int32_t *handle) {
+  ListEntry e;
+  int rc = alloc_list(ctx, size, e);
+  if (rc) return rc;
+  // the first key must be a whole 18-byte key (Posdb.cpp:5671-5703 swaps it)
+  if (size > 0 && (bytes[0] & 0x06)) return GBGPU_ECORRUPT;  // e.mem frees the image
   if (size) {
     // device image = the list after the first-key swap (Posdb.cpp:5689-5698):
     // original bytes 0..11 with the half bit set, then bytes 18..size-1
@@ -5453,6 +5482,18 @@ static int upload_list(gbgpu_ctx *ctx, const uint8_t *bytes, int64_t size, int32
     HIPCHECK(hipMemcpyAsync(e.d, first, 12, hipMemcpyHostToDevice, ctx->upload_stream));
     if (size > 18)
       HIPCHECK(hipMemcpyAsync(e.d + 12, bytes + 18, (size_t)(size - 18), hipMemcpyHostToDevice, ctx->upload_stream));
+  }
+  return finish_list(ctx, e, bytes, bytes, handle);
+}
+
+// The common tail of a list's upload once its device image is enqueued:
+// structure check, page map, granule table; then the docid range, from the
+// host bytes when the caller has them, else from the device image's last
+// granule that holds a run start.
+static int finish_list(gbgpu_ctx *ctx, ListEntry &e, const uint8_t *host_bytes, const uint8_t *first18,
+                       int32_t *handle) {
+  const int64_t size = e.size;
+  if (size) {
     HIPCHECK(hipMemsetAsync(ctx->d_flag, 0, 4, ctx->upload_stream));
     const uint32_t grid = (uint32_t)std::min<uint64_t>(4096, (e.units + 255) / 256);
     hipLaunchKernelGGL(k_validate, dim3(std::max(grid, 1u)), dim3(256), 0, ctx->upload_stream, e.d, e.units,
@@ -5483,17 +5524,37 @@ static int upload_list(gbgpu_ctx *ctx, const uint8_t *bytes, int64_t size, int32
   dgf.release();
   HIPCHECK(se);
   if (size && *ctx->h_flag) return GBGPU_ECORRUPT;  // e.mem frees the copy
-  if (size) e.gfirst = std::make_shared<const std::vector<uint64_t>>(std::move(gf));
   if (size) {
     // the list's docid range (directory sizing): first key, last run start
-    e.dmin = e.dmax = host_docid(bytes);
-    for (int64_t q = size - 6; q >= 18; q -= 6) {
-      if ((bytes[q + 1] & 0x02) && !(bytes[q] & 0x04)) {
-        e.dmax = host_docid(bytes + q);
-        break;
+    e.dmin = e.dmax = host_docid(first18);
+    if (host_bytes) {
+      for (int64_t q = size - 6; q >= 18; q -= 6) {
+        if ((host_bytes[q + 1] & 0x02) && !(host_bytes[q] & 0x04)) {
+          e.dmax = host_docid(host_bytes + q);
+          break;
+        }
+      }
+    } else {
+      // k_gfirst: gf[g] is the first run docid at or after granule g, so the
+      // last granule with one holds the last run start (its head may end one
+      // unit past the granule)
+      size_t g = gf.size();
+      while (g > 0 && gf[g - 1] == ~0ULL) g--;
+      if (g > 0) {
+        const uint32_t u0 = (uint32_t)(g - 1) * (uint32_t)WCH_UNITS;
+        const uint32_t u1 = std::min<uint32_t>(e.units, u0 + (uint32_t)WCH_UNITS + 1);
+        std::vector<uint8_t> tail(6 * (size_t)(u1 - u0));
+        HIPCHECK(hipMemcpy(tail.data(), e.d + 6 * (size_t)u0, tail.size(), hipMemcpyDeviceToHost));
+        for (int64_t q = (int64_t)tail.size() - 12; q >= 0; q -= 6) {
+          if ((tail[q + 1] & 0x02) && !(tail[q] & 0x04)) {
+            e.dmax = host_docid(tail.data() + q);
+            break;
+          }
+        }
       }
     }
   }
+  if (size) e.gfirst = std::make_shared<const std::vector<uint64_t>>(std::move(gf));
   e.live = true;
   for (size_t i = 0; i < ctx->lists.size(); i++) {
     if (!ctx->lists[i].live) {
@@ -5541,11 +5602,11 @@ static int enqueue(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *terms, int n
   int rc = snapshot_lists(ctx, terms, nterms, handles, p, ents);
   if (rc) return rc;
   if (p->num_docid_splits > 1) return GBGPU_EUNSUPPORTED;  // blocking entry points only
-  rc = enqueue_entries(ctx, q, terms, nterms, ents.data(), p, 0);
-  if (!rc)
-    for (auto &e : ents)
-      if (e.mem) q.held.push_back(e.mem);
-  return rc;
+  // held before anything is launched: a failed enqueue may have launched
+  // kernels that read the lists; the next collect on this slot drains them
+  for (auto &e : ents)
+    if (e.mem) q.held.push_back(e.mem);
+  return enqueue_entries(ctx, q, terms, nterms, ents.data(), p, 0);
 }
 
 // One PosdbTable pass over the given lists on slot q's stream.  dw_override
@@ -6375,6 +6436,7 @@ static int collect(gbgpu_ctx *ctx, QuerySlot &q, gbgpu_result *out, std::vector<
   out->n_docid_scores = out->n_pair_scores = out->n_single_scores = 0;
   out->docs_wanted = q.docs_wanted;
   if (q.early) {
+    (void)hipStreamSynchronize(q.stream);  // nothing of this query; a failed one's kernels
     q.held.clear();
     return 0;
   }
@@ -6840,6 +6902,8 @@ void gbgpu_close(gbgpu_ctx *ctx) {
   ctx->xout.release();
   if (ctx->h_xout) (void)hipHostFree(ctx->h_xout);
   ctx->lists.clear();  // the last references: ListMem frees the device copies
+  ctx->files.clear();
+  if (ctx->upload_stream) (void)hipStreamSynchronize(ctx->upload_stream);
   gbmerge::state_free(ctx->merge);
   if (ctx->d_flag) (void)hipFree(ctx->d_flag);
   if (ctx->d_sdbg) (void)hipFree(ctx->d_sdbg);
@@ -6877,6 +6941,92 @@ int gbgpu_list_upload(gbgpu_ctx *ctx, const uint8_t *bytes, int64_t size, int32_
   std::lock_guard<std::mutex> g(ctx->lists_mu);
   (void)hipSetDevice(ctx->device);
   return upload_list(ctx, bytes, size, handle);
+}
+
+int gbgpu_file_upload(gbgpu_ctx *ctx, const uint8_t *bytes, int64_t size, int32_t *fh) {
+  if (!ctx || !fh || size < 0 || (size > 0 && !bytes) || size % 6 != 0) return EINVAL;
+  std::lock_guard<std::mutex> g(ctx->lists_mu);
+  (void)hipSetDevice(ctx->device);
+  FileEntry f;
+  f.size = size;
+  f.mem = std::make_shared<ListMem>();
+  f.mem->st = ctx->upload_stream;
+  if (hipMallocAsync(reinterpret_cast<void **>(&f.mem->d), std::max<size_t>((size_t)size, 256), ctx->upload_stream) !=
+      hipSuccess)
+    return ENOMEM;
+  if (size) HIPCHECK(hipMemcpyAsync(f.mem->d, bytes, (size_t)size, hipMemcpyHostToDevice, ctx->upload_stream));
+  HIPCHECK(hipStreamSynchronize(ctx->upload_stream));
+  f.live = true;
+  for (size_t i = 0; i < ctx->files.size(); i++) {
+    if (!ctx->files[i].live) {
+      ctx->files[i] = f;
+      *fh = (int32_t)i;
+      return 0;
+    }
+  }
+  ctx->files.push_back(f);
+  *fh = (int32_t)ctx->files.size() - 1;
+  return 0;
+}
+
+int gbgpu_file_free(gbgpu_ctx *ctx, int32_t fh) {
+  if (!ctx) return EINVAL;
+  std::shared_ptr<ListMem> last;  // lists cut from it are copies: nothing else holds it
+  {
+    std::lock_guard<std::mutex> g(ctx->lists_mu);
+    if (fh < 0 || fh >= (int32_t)ctx->files.size() || !ctx->files[fh].live) return EINVAL;
+    last = std::move(ctx->files[fh].mem);
+    ctx->files[fh] = FileEntry();
+  }
+  (void)hipSetDevice(ctx->device);
+  last.reset();
+  return 0;
+}
+
+// RdbScan's read (RdbScan.cpp:319-361) on the device: bytes [offset,
+// offset+size) of a resident file; a compressed first key (12 or 6 bytes) is
+// replaced by the full key the caller's RdbMap gives for it (m_startKey), then
+// the first-key swap of Posdb.cpp:5671-5703; the image goes through the same
+// checks as gbgpu_list_upload.
+int gbgpu_file_list(gbgpu_ctx *ctx, int32_t fh, int64_t offset, int64_t size, const uint8_t *key18,
+                    int32_t *handle) {
+  if (!ctx || !handle || offset < 0 || size < 0) return EINVAL;
+  std::lock_guard<std::mutex> g(ctx->lists_mu);
+  (void)hipSetDevice(ctx->device);
+  if (fh < 0 || fh >= (int32_t)ctx->files.size() || !ctx->files[fh].live) return EINVAL;
+  const FileEntry &f = ctx->files[fh];
+  if (offset > f.size || size > f.size - offset || offset % 6 || size % 6) return EINVAL;
+  if (!size) return upload_list(ctx, nullptr, 0, handle);
+  const uint8_t *src = f.mem->d + offset;
+  uint8_t head[18] = {};
+  HIPCHECK(hipMemcpy(head, src, (size_t)std::min<int64_t>(18, size), hipMemcpyDeviceToHost));
+  if (!(head[1] & 0x02)) return GBGPU_ECORRUPT;  // not a key start (Posdb.cpp:410-412)
+  const int ks = (head[0] & 0x04) ? 6 : (head[0] & 0x02) ? 12 : 18;
+  if (size < ks) return GBGPU_ECORRUPT;
+  uint8_t full[18];
+  if (key18) {
+    // the map's key must be this key: its stored bytes, compression bits aside
+    std::memcpy(full, key18, 18);
+    if (full[0] & 0x06) return EINVAL;
+    uint8_t a[18], b[18];
+    std::memcpy(a, head, ks);
+    std::memcpy(b, full, ks);
+    a[0] &= 0xf9;
+    if (std::memcmp(a, b, ks)) return EINVAL;
+  } else {
+    if (ks != 18) return EINVAL;  // a compressed first key needs the map's key
+    std::memcpy(full, head, 18);
+  }
+  ListEntry e;
+  int rc = alloc_list(ctx, size - ks + 18, e);
+  if (rc) return rc;
+  uint8_t first[12];
+  std::memcpy(first, full, 12);
+  first[0] |= 0x02;
+  HIPCHECK(hipMemcpyAsync(e.d, first, 12, hipMemcpyHostToDevice, ctx->upload_stream));
+  if (size > ks)
+    HIPCHECK(hipMemcpyAsync(e.d + 12, src + ks, (size_t)(size - ks), hipMemcpyDeviceToDevice, ctx->upload_stream));
+  return finish_list(ctx, e, nullptr, full, handle);
 }
 
 int gbgpu_list_free(gbgpu_ctx *ctx, int32_t h) {
@@ -6962,11 +7112,15 @@ static int query_resident_on(gbgpu_ctx *ctx, QuerySlot *q, const gbgpu_qterm *te
     int rc = snapshot_lists(ctx, terms, nterms, handles, p, ents);
     if (!rc) rc = query_splits(ctx, *q, terms, nterms, ents, p, out);
     q->pending = false;
+    // on an error, launched window copies may still read the lists `ents` holds
+    if (rc) (void)hipStreamSynchronize(q->stream);
     return rc;
   }
   int rc = enqueue(ctx, *q, terms, nterms, handles, p);
   if (rc) {
     q->pending = false;
+    (void)hipStreamSynchronize(q->stream);
+    q->held.clear();
     return rc;
   }
   return collect(ctx, *q, out);

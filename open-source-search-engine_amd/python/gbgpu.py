@@ -189,6 +189,7 @@ EXPORTS = [
     "gbgpu_open", "gbgpu_close", "gbgpu_strerror", "gbgpu_abi_version", "gbgpu_docs_wanted",
     "gbgpu_tree_capacity",
     "gbgpu_query", "gbgpu_list_upload", "gbgpu_list_free", "gbgpu_query_resident",
+    "gbgpu_file_upload", "gbgpu_file_list", "gbgpu_file_free",
     "gbgpu_query_resident_enqueue", "gbgpu_query_collect", "gbgpu_stream",
     "gbgpu_last_topk_device", "gbgpu_merge_topk", "gbgpu_merge_posdb", "gbgpu_set_profiling",
     "gbgpu_last_timings", "gbgpu_set_query_slots", "gbgpu_query_slots", "gbgpu_query_slot_enqueue",
@@ -224,6 +225,9 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
                                 ctypes.POINTER(Params), ctypes.POINTER(Result)]
     lib.gbgpu_list_upload.argtypes = [vp, vp, i64, ctypes.POINTER(i32)]
     lib.gbgpu_list_free.argtypes = [vp, i32]
+    lib.gbgpu_file_upload.argtypes = [vp, vp, i64, ctypes.POINTER(i32)]
+    lib.gbgpu_file_list.argtypes = [vp, i32, i64, i64, vp, ctypes.POINTER(i32)]
+    lib.gbgpu_file_free.argtypes = [vp, i32]
     lib.gbgpu_query_resident.argtypes = [vp, ctypes.POINTER(QTerm), ctypes.c_int, ctypes.POINTER(i32),
                                          ctypes.POINTER(Params), ctypes.POINTER(Result)]
     lib.gbgpu_query_resident_enqueue.argtypes = [vp, ctypes.POINTER(QTerm), ctypes.c_int,
@@ -453,6 +457,28 @@ class Engine:
 
     def free(self, handle: int) -> None:
         _check(self.lib.gbgpu_list_free(self.ctx, handle), "free")
+
+    def file_upload(self, data: bytes) -> int:
+        """A Posdb Rdb file image into HBM; returns its file handle."""
+        h = ctypes.c_int32()
+        buf = ctypes.create_string_buffer(bytes(data), len(data))
+        _check(self.lib.gbgpu_file_upload(self.ctx, buf, len(data), ctypes.byref(h)), "file_upload")
+        return h.value
+
+    def file_list(self, fh: int, offset: int, size: int, key18: Optional[bytes] = None) -> int:
+        """RdbScan's read of [offset, offset+size) of a resident file as a
+        resident list handle; key18 = the map's full key for a compressed
+        first key."""
+        h = ctypes.c_int32()
+        k = None
+        if key18 is not None:
+            assert len(key18) == 18
+            k = ctypes.create_string_buffer(bytes(key18), 18)
+        _check(self.lib.gbgpu_file_list(self.ctx, fh, offset, size, k, ctypes.byref(h)), "file_list")
+        return h.value
+
+    def file_free(self, fh: int) -> None:
+        _check(self.lib.gbgpu_file_free(self.ctx, fh), "file_free")
 
     @staticmethod
     def info_arrays(params: Params, nterms: int):
