@@ -13,6 +13,8 @@
  *   Msg3a::mergeLists           Msg3a.cpp:971-1503     gbgpu_allgather_topk (RCCL) /
  *                                                      gbgpu_merge_topk (host lists)
  *   RdbList::posdbMerge_r       RdbList.cpp:3065-3568  gbgpu_merge_posdb
+ *   Msg3::readList -> RdbScan   Msg3.cpp:553-731,       gbgpu_file_upload /
+ *     (a Posdb file read)       RdbScan.cpp:319-361    gbgpu_file_list (in HBM)
  *
  * Conventions: plain pointers and sizes only; the caller owns
  * every input and output buffer and they are never mutated; the library owns
@@ -36,7 +38,7 @@
 extern "C" {
 #endif
 
-#define GBGPU_ABI_VERSION 9
+#define GBGPU_ABI_VERSION 10
 
 /* error codes beyond errno.h (Errno.h numbering is not reused) */
 #define GBGPU_ENODEVICE   1001 /* no HIP device / extension not usable        */
