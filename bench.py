@@ -350,6 +350,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-merge", action="store_true", help="skip the config-5 list merge measurement")
     ap.add_argument("--no-config3", action="store_true", help="skip the config-3 query-mix measurement")
+    ap.add_argument("--no-file-read", action="store_true", help="skip the resident-file read measurement")
     ap.add_argument("--no-clustering", action="store_true",
                     help="skip the config-2 rotation with site clustering (the Msg39 default)")
     ap.add_argument("--no-ceiling", action="store_true", help="skip the streaming-bandwidth ceiling")
@@ -596,6 +597,7 @@ def main():
             "note": "gbgpu_query with the lists in pageable host memory, uploaded every call; not `value`",
         }
         del host
+    if rank == 0 and world == 1 and not args.no_file_read:
         # the read path into HBM (f3): the lists as one resident Posdb file
         # image, each query cutting its termlists from it on the device
         # (gbgpu_file_list, RdbScan's read) and freeing them after

@@ -2571,6 +2571,28 @@ __device__ __forceinline__ uint64_t load6(gu8 *k) {
   return odd ? (hv | (wv << 16)) : (wv | (hv << 32));
 }
 
+// units b..b+3 of a run (b a multiple of 4) as one dwordx4 and one dwordx3
+// load from the 4-byte-aligned address at or below them, instead of eight
+// load6 halves: the run's 2-byte phase s (0 or 2) picks which fixed byte
+// offsets of the 28 loaded bytes hold each unit.  Reads up to 4 bytes past
+// the fourth unit (lists carry LIST_PAD).
+__device__ __forceinline__ void load4u(gu8 *src, uint32_t b, uint64_t *v) {
+  const uintptr_t a = (uintptr_t)src + (uintptr_t)b * 6;
+  const bool s2 = (a & 2) != 0;
+  const auto *w = (const __attribute__((address_space(1))) uint32_t *)(a & ~(uintptr_t)3);
+  uint32_t x[7];
+#pragma unroll
+  for (int i = 0; i < 7; i++) x[i] = w[i];
+  const uint32_t lo0 = s2 ? (x[0] >> 16) | (x[1] << 16) : x[0], hi0 = s2 ? x[1] >> 16 : x[1] & 0xffff;
+  const uint32_t lo1 = s2 ? x[2] : (x[1] >> 16) | (x[2] << 16), hi1 = s2 ? x[3] & 0xffff : x[2] >> 16;
+  const uint32_t lo2 = s2 ? (x[3] >> 16) | (x[4] << 16) : x[3], hi2 = s2 ? x[4] >> 16 : x[4] & 0xffff;
+  const uint32_t lo3 = s2 ? x[5] : (x[4] >> 16) | (x[5] << 16), hi3 = s2 ? x[6] & 0xffff : x[5] >> 16;
+  v[0] = lo0 | ((uint64_t)hi0 << 32);
+  v[1] = lo1 | ((uint64_t)hi1 << 32);
+  v[2] = lo2 | ((uint64_t)hi2 << 32);
+  v[3] = lo3 | ((uint64_t)hi3 << 32);
+}
+
 // what the second pass's DocIdScore takes from a scored docid (Posdb.cpp:7555-7563)
 struct SurvOut {
   float score;
@@ -2673,15 +2695,20 @@ __device__ __forceinline__ void score_survivor(const DevPlan *__restrict__ pl, c
 #pragma unroll
         for (int j = 0; j < NQ; j++)
 #pragma unroll
-          for (int x = 0; x < NS; x++)
+          for (int x = 0; x < NS; x++) {
+            const GrpRuns &g = pre[j];
+            if (g.live[x] && b < g.ce[x] && g.c0[x] == g.ce[x] && !(diag & 0x400)) {
+              load4u(g.src[x], b, v[j][x]);  // a run of its own list only
+            } else {
 #pragma unroll
-            for (int q = 0; q < SKP; q++) {
-              const uint32_t c = b + q;
-              const GrpRuns &g = pre[j];
-              v[j][x][q] = (g.live[x] && c < g.ce[x])
-                               ? load6(c < g.c0[x] ? g.src[x] + (size_t)c * 6 : g.xsrc[x] + (size_t)(c - g.c0[x]) * 6)
-                               : 0;
+              for (int q = 0; q < SKP; q++) {
+                const uint32_t c = b + q;
+                v[j][x][q] = (g.live[x] && c < g.ce[x])
+                                 ? load6(c < g.c0[x] ? g.src[x] + (size_t)c * 6 : g.xsrc[x] + (size_t)(c - g.c0[x]) * 6)
+                                 : 0;
+              }
             }
+          }
 #pragma unroll
         for (int j = 0; j < NQ; j++) {
           uint32_t off = 0;
