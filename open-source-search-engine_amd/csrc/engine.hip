@@ -2783,14 +2783,21 @@ __device__ __forceinline__ void score_survivor(const DevPlan *__restrict__ pl, c
         for (uint32_t b = 0; b < cmax; b += SK) {
           uint64_t v[NS][SK];
 #pragma unroll
-          for (int x = 0; x < NS; x++)
+          for (int x = 0; x < NS; x++) {
+            bool fast = false;
+            if constexpr (SK == 4) fast = live[x] && b < ce[x] && c0[x] == ce[x] && !(diag & 0x400);
+            if (fast) {
+              if constexpr (SK == 4) load4u(src[x], b, v[x]);  // a run of its own list only
+            } else {
 #pragma unroll
-            for (int q = 0; q < SK; q++) {
-              const uint32_t c = b + q;
-              v[x][q] = (live[x] && c < ce[x])
-                            ? load6(c < c0[x] ? src[x] + (size_t)c * 6 : xsrc[x] + (size_t)(c - c0[x]) * 6)
-                            : 0;
+              for (int q = 0; q < SK; q++) {
+                const uint32_t c = b + q;
+                v[x][q] = (live[x] && c < ce[x])
+                              ? load6(c < c0[x] ? src[x] + (size_t)c * 6 : xsrc[x] + (size_t)(c - c0[x]) * 6)
+                              : 0;
+              }
             }
+          }
 #pragma unroll
           for (int x = 0; x < NS; x++)
 #pragma unroll
