@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define GBGPU_ABI_VERSION 10
+#define GBGPU_ABI_VERSION 11
 
 /* error codes beyond errno.h (Errno.h numbering is not reused) */
 #define GBGPU_ENODEVICE   1001 /* no HIP device / extension not usable        */
@@ -330,6 +330,10 @@ int gbgpu_comm_unique_id(uint8_t *id);
 int gbgpu_comm_init(gbgpu_ctx *ctx, int nranks, int rank, const uint8_t *id);
 int gbgpu_allgather_topk(gbgpu_ctx *ctx, int slot, uint64_t seq, int timeout_ms, int32_t k, int64_t *docids,
                          double *scores, int32_t *n, int64_t *hits, gbgpu_result *local);
+/* the exchange sequence number this context admits next (a single-threaded
+ * caller's default `seq`); calls refused before admission (a bad k, a null
+ * output, ETIMEDOUT) leave it unchanged */
+uint64_t gbgpu_exchange_next(gbgpu_ctx *ctx);
 
 /* RdbList::posdbMerge_r (RdbList.cpp:3065-3568), as RdbList::merge_r
  * (RdbList.cpp:1658-1756) calls it after prepareForMerge (410-491): merge n

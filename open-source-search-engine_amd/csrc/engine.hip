@@ -751,6 +751,7 @@ __device__ uint64_t first_run_doc(const DevList &L, uint32_t u, uint32_t u1, int
   return ~0ull;
 }
 
+#ifdef GBGPU_DIAG  // probe_by_cand and the table path: measured alternatives, diagnostic builds only
 // Dense list: candidates search the run starts.  Memory pipelining under the
 // in-order vmcnt counter: two chunk buffers with static roles (the loop is
 // unrolled by two, so no in-flight register is ever copied -- a copy would
@@ -942,6 +943,8 @@ struct HashLds {
   uint32_t mslot[MBUF], mu[MBUF], mlen[MBUF];
 };
 
+#endif  // GBGPU_DIAG
+
 // first candidate index of array k at or below lower_bound(key) and close to
 // it: the directory entry of the last non-empty bucket of the 64 below key's
 __device__ uint32_t wave_start_dir(const DevPlan *__restrict__ pl, int k, const uint64_t *ck, uint32_t n, const uint64_t *dir,
@@ -971,6 +974,7 @@ __device__ __forceinline__ uint32_t lane_prev(uint32_t x, uint32_t edge) {
   return (uint32_t)__builtin_amdgcn_update_dpp((int)edge, (int)x, 0x138, 0xf, 0xf, false);  // wave_shr:1
 }
 
+#ifdef GBGPU_DIAG  // the measured alternatives (probe_by_cand_hash / _wide): diagnostic builds only
 // piece i of a chunk (wchunk_fetch's layout, as chunk_runs): the run starts
 // among the units starting in this lane's 16 bytes (at most two: a run head is
 // two units), their docids and chunk-relative units
@@ -1514,6 +1518,8 @@ __device__ void probe_by_cand_wide(const DevPlan *__restrict__ pl, const ProbeWo
   mbuf_flush(S, nbuf, po, lane);
 }
 
+#endif  // GBGPU_DIAG
+
 // Dense list: probe_by_cand with fewer LDS and vector instructions a chunk,
 // the measured limit of that path (its LDS pipe and VALU issue, not its HBM
 // bytes: a 6 KiB-chunk variant with the same work per byte ran no faster).
@@ -1807,6 +1813,7 @@ template <int MODE, int G0>
 __global__ void __launch_bounds__(64 * PW, (G0 <= 2 && MODE == 11) ? 3 : 1) k_probe(const DevPlan *__restrict__ pl, const ProbeWork *work, uint32_t nwork,
                                                    const uint64_t *cand, uint32_t *bits, uint32_t nwords, Loc *loc,
                                                    const Counters *ctr, const uint64_t *dir) {
+#ifdef GBGPU_DIAG
   // the bucket-table path (probe_by_cand_hash) is a measured alternative,
   // slower than the run-list search at config 2 (188 vs 80 us): diagnostic
   // GBGPU_PROBE_MODE=10 only
@@ -1823,6 +1830,13 @@ __global__ void __launch_bounds__(64 * PW, (G0 <= 2 && MODE == 11) ? 3 : 1) k_pr
     typename std::conditional<WIDE, ProbeLds6, None>::type wide;
     typename std::conditional<PACKED, ProbeLdsP, None>::type packed;
   };
+#else
+  static_assert(MODE == 0, "the release build has the full probe only");
+  union WaveLds {
+    ProbeLds run;
+    ProbeLdsP packed;
+  };
+#endif
   __shared__ WaveLds s_w[PW];
   // the wave's index is uniform over the wave: said so, every value derived
   // from it (the work item, the list, the loop bounds) lives in SGPRs and the
@@ -1838,6 +1852,7 @@ __global__ void __launch_bounds__(64 * PW, (G0 <= 2 && MODE == 11) ? 3 : 1) k_pr
   po.nl = (uint32_t)pl->nlists;
   po.l = w.list;
   po.on = MODE == 5 ? 0 : 1;
+#ifdef GBGPU_DIAG
   if (L.probe == PROBE_BY_RUN) {
     if (MODE == 0 || MODE >= 10) probe_by_run<G0>(pl, w, L, cand, ctr, dir, s_w[wid].run, po, lane);
   } else {
@@ -1850,6 +1865,12 @@ __global__ void __launch_bounds__(64 * PW, (G0 <= 2 && MODE == 11) ? 3 : 1) k_pr
     else
       probe_by_cand<(MODE == 3 || MODE == 12) ? 0 : MODE, G0>(pl, w, L, cand, ctr, dir, s_w[wid].run, po, lane);
   }
+#else
+  if (L.probe == PROBE_BY_RUN)
+    probe_by_run<G0>(pl, w, L, cand, ctr, dir, s_w[wid].run, po, lane);
+  else
+    probe_by_cand_packed<0, G0>(pl, w, L, cand, ctr, dir, s_w[wid].packed, po, lane);
+#endif
 }
 
 // A range term's list in a later group votes a docid only if a key of its
@@ -3878,7 +3899,7 @@ struct TreeParams {
   int64_t num_nodes;    // m_numNodes
   uint32_t init, final; // first / last piece
   int32_t ints;          // m_useIntScores: nodes ordered by m_intScore (TopTree.cpp:216-219, 270-274)
-  int32_t pad2;
+  int32_t on_reg_err;    // run only if k_tree_seq's register tree overflowed (tree_err == TREE_ERR_REG)
 };
 
 // Node scores: m_score, or with integer tree scores m_intScore kept as the
@@ -4046,6 +4067,13 @@ __global__ void __launch_bounds__(64) k_tree_replay(Counters *ctr, const uint4 *
   __shared__ int32_t dom[256];
   __shared__ uint4 stage[RP_C * 64];
   const int lane = threadIdx.x;
+  if (tp.on_reg_err) {
+    // the fallback behind k_tree_seq, on the same stream: nothing to do
+    // unless its register tree overflowed (2 = TREE_ERR_REG, defined below)
+    const uint32_t te = __builtin_amdgcn_readfirstlane(__atomic_load_n(&ctr->tree_err, __ATOMIC_RELAXED));
+    if (te != 2u) return;
+    if (lane == 0) ctr->tree_err = 0;
+  }
   uint32_t n = 0;
   float vcount = 0.0f;
   if (tp.init) {
@@ -5196,6 +5224,7 @@ struct DevBuf {
   void *p = nullptr;
   size_t cap = 0;
   hipStream_t st = nullptr;
+  hipMemPool_t pool = nullptr;  // the context's own pool (stream-ordered buffers); null: hipMalloc
   int ensure(size_t bytes) {
     if (bytes <= cap) return 0;
     const size_t want = std::max<size_t>(bytes + bytes / 4, 1 << 16);
@@ -5203,7 +5232,7 @@ struct DevBuf {
       if (p) (void)hipFreeAsync(p, st);
       p = nullptr;
       cap = 0;
-      if (hipMallocAsync(&p, want, st) != hipSuccess) return ENOMEM;
+      if (pool_alloc(&p, want, pool, st)) return ENOMEM;
     } else {
       if (p) (void)hipFree(p);
       p = nullptr;
@@ -5212,6 +5241,21 @@ struct DevBuf {
     }
     cap = want;
     return 0;
+  }
+  // stream-ordered allocation from `pool` (or the device's default pool);
+  // on failure the pool's cached free memory goes back to the device and
+  // the allocation is tried once more
+  static int pool_alloc(void **out, size_t bytes, hipMemPool_t pool, hipStream_t st) {
+    for (int t = 0; t < 2; t++) {
+      const hipError_t e = pool ? hipMallocFromPoolAsync(out, bytes, pool, st) : hipMallocAsync(out, bytes, st);
+      if (e == hipSuccess) return 0;
+      (void)hipGetLastError();
+      if (!pool || t) break;
+      (void)hipStreamSynchronize(st);
+      (void)hipMemPoolTrimTo(pool, 0);
+    }
+    *out = nullptr;
+    return ENOMEM;
   }
   template <class T> T *as(size_t off = 0) const { return reinterpret_cast<T *>(static_cast<uint8_t *>(p) + off); }
   void release() {
@@ -5223,14 +5267,6 @@ struct DevBuf {
     cap = 0;
   }
 };
-
-// Device memory of one resident list.  Shared by the list table and every
-// query in flight that reads it: gbgpu_list_free drops the table's reference,
-// and the memory goes when the last in-flight query holding it is collected.
-// Stream-ordered on the context's upload stream (hipMallocAsync): every query
-// that reads a list holds a reference until its stream has drained
-// (QuerySlot::held), so the last reference drops with no kernel left reading
-// it and the free needs no device-wide synchronisation.
 struct ListMem {
   uint8_t *d = nullptr;
   hipStream_t st = nullptr;
@@ -5356,9 +5392,12 @@ struct QuerySlot {
   DevBuf *const bufs[28] = {&tables, &chunkcnt, &cand, &cunit, &bits, &loc, &svslot, &svlm, &svu, &svdoc,
                             &svloc, &scratch, &skey, &sel, &gath, &res, &dir, &split, &swin, &blk,
                             &sflag, &ord, &oslot, &rep, &tree, &white, &wrej, &si};
-  int init() {
+  int init(hipMemPool_t pool) {
     if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return GBGPU_EHIP;
-    for (auto *b : bufs) b->st = stream;
+    for (auto *b : bufs) {
+      b->st = stream;
+      b->pool = pool;
+    }
     for (auto &e : ev)
       if (hipEventCreate(&e) != hipSuccess) return GBGPU_EHIP;
     if (hipEventCreateWithFlags(&ev_done, hipEventDisableTiming) != hipSuccess) return GBGPU_EHIP;
@@ -5380,6 +5419,7 @@ struct QuerySlot {
 };
 
 constexpr int MAX_SLOTS = 64;
+constexpr uint64_t POOL_KEEP = 16ull << 30;  // free bytes the context's pool may keep cached
 
 // A Posdb Rdb file image resident in HBM (gbgpu_file_upload): the bytes as
 // they lie on disk, termlists back to back.  Termlists are cut from it on the
@@ -5433,6 +5473,7 @@ struct gbgpu_ctx {
   std::mutex lists_mu;
   std::vector<ListEntry> lists;
   std::vector<FileEntry> files;  // resident Rdb file images (gbgpu_file_upload), under lists_mu
+  hipMemPool_t pool = nullptr;  // stream-ordered device memory of the slots, lists and files
   std::mutex slots_mu;  // guards growth of the slot table
   QuerySlot *slots[MAX_SLOTS] = {};
   int nslots = 0;
@@ -5444,7 +5485,10 @@ struct gbgpu_ctx {
   int score_mode = 0;  // diagnostic only (GBGPU_SCORE_MODE): 1 mini-merge without scoring
   int debug_ext = 0;   // diagnostic only (GBGPU_DEBUG_EXT): print the re-shrink table per query
   uint64_t *d_sdbg = nullptr;  // GBGPU_SCORE_MODE=2: per-wave k_score timing (GBGPU_SCORE_DUMP file)
-  unsigned long long *d_pdbg = nullptr;  // GBGPU_PROBE_DEBUG_DOC: k_probe's trace of one docid
+  unsigned long long *d_pdbg = nullptr;  // GBGPU_PROBE_DEBUG_DOC: k_probe's trace of one docid (one slot: the
+                                         // buffer is shared, so the trace is meaningful with one query in flight)
+  const char *probe_dbg_doc = nullptr;   // its value, read once at gbgpu_open
+  bool topk_debug = false;               // GBGPU_TOPK_DEBUG: k_topk / replay phase clocks to stderr
   uint32_t sdbg_grid = 0;
   std::mutex merge_mu;
   gbmerge::MergeState *merge = nullptr;  // created on first use (merge.hip)
@@ -5489,7 +5533,7 @@ static int alloc_list(gbgpu_ctx *ctx, int64_t size, ListEntry &e) {
   const size_t alloc = lbytes + page_map_bytes(e.units);
   e.mem = std::make_shared<ListMem>();
   e.mem->st = ctx->upload_stream;
-  if (hipMallocAsync(reinterpret_cast<void **>(&e.mem->d), alloc, ctx->upload_stream) != hipSuccess) return ENOMEM;
+  if (DevBuf::pool_alloc(reinterpret_cast<void **>(&e.mem->d), alloc, ctx->pool, ctx->upload_stream)) return ENOMEM;
   e.d = e.mem->d;
   e.pm = reinterpret_cast<uint32_t *>(e.d + lbytes);
   // the image's own bytes are written next: zero the pad and the page map
@@ -5804,12 +5848,13 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   P.sortby_int = hp.sortby_int;
   q.int_scores = hp.sortby_int != 0;
   P.min_listi = hp.min_listi;
-  if (const char *dd = std::getenv("GBGPU_PROBE_DEBUG_DOC")) {
+#ifdef GBGPU_DIAG
+  if (const char *dd = ctx->probe_dbg_doc) {
     P.dbg_doc = std::strtoull(dd, nullptr, 10);
-    if (!ctx->d_pdbg && hipMalloc((void **)&ctx->d_pdbg, 8 * (1 + 16 * 32)) != hipSuccess) ctx->d_pdbg = nullptr;
     if (ctx->d_pdbg) HIPCHECK(hipMemsetAsync(ctx->d_pdbg, 0, 8 * (1 + 16 * 32), q.stream));
     P.dbg_buf = ctx->d_pdbg;
   }
+#endif
   P.all_same_wiki = 1;  // m_allInSameWikiPhrase, Posdb.cpp:5764-5778
   for (int j = 0; j < hp.ngroups; j++) {
     if (hp.g[j].flags[0] & (BF_NEGATIVE | BF_NUMBER | BF_FACET)) continue;
@@ -5952,8 +5997,13 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   uint64_t probe_chunks = 0;
   // candidate-driven lists walk 6 KiB chunks when the smallest group has at
   // most two candidate arrays (probe_by_cand_wide), else 3 KiB
+#ifdef GBGPU_DIAG
   const bool wide = P.g0n <= 2 && ctx->probe_mode == 11;
   const uint32_t cunits = wide ? (uint32_t)W6_UNITS : (uint32_t)WCH_UNITS;
+#else
+  constexpr bool wide = false;
+  const uint32_t cunits = (uint32_t)WCH_UNITS;
+#endif
   for (int id = 0; id < P.nlists; id++) {
     scan += (int64_t)P.lists[id].units * 6;
     if (P.lists[id].probe == PROBE_BY_CAND) probe_chunks += (P.lists[id].units + cunits - 1) / cunits;
@@ -6088,6 +6138,7 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
                      q.cunit.as<uint32_t>(), dctr, ng0, q.dir.as<uint64_t>());
   if (ctx->profiling) HIPCHECK(hipEventRecord(q.ev[1], st));
   if (!q.pw.empty()) {
+#ifdef GBGPU_DIAG
     auto kp = ctx->probe_mode == 11  ? (P.g0n <= 1 ? k_probe<11, 1> : k_probe<11, 2>)  // diagnostic: 6 KiB chunks
               : ctx->probe_mode == 10 ? (P.g0n <= 2 ? k_probe<10, 2> : k_probe<10, 4>)  // diagnostic: bucket tables
               : ctx->probe_mode == 4 ? k_probe<12, MAXG0>  // diagnostic: the unpacked run list
@@ -6101,6 +6152,9 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
               : P.g0n == 2           ? k_probe<0, 2>
               : P.g0n <= 4           ? k_probe<0, 4>
                                      : k_probe<0, MAXG0>;
+#else
+    auto kp = P.g0n == 1 ? k_probe<0, 1> : P.g0n == 2 ? k_probe<0, 2> : P.g0n <= 4 ? k_probe<0, 4> : k_probe<0, MAXG0>;
+#endif
     const uint32_t nwork = (uint32_t)q.pw.size();
     hipLaunchKernelGGL(kp, dim3((nwork + PW - 1) / PW), dim3(64 * PW), 0, st, dpl, dwork, nwork,
                        q.cand.as<uint64_t>(), bits, nwords, loc, dctr, q.dir.as<uint64_t>());
@@ -6190,6 +6244,14 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
                                 : kcol == 8 ? k_tree_seq<8, false> : k_tree_seq<16, false>);
       hipLaunchKernelGGL(ks, dim3(1), dim3(64 * SQ_W), 0, st, dctr, (const uint4 *)q.rep.as<uint4>(), tp,
                          q.res.as<uint32_t>(res_keys_off()), q.res.as<uint64_t>(res_docs_off(k)));
+      // a tree that outgrew the register columns replays the same entries
+      // through the LDS tree right behind it, before ev_done: the result
+      // block is final when the exchange (k_xpack) or collect reads it
+      TreeParams tf = tp;
+      tf.on_reg_err = 1;
+      hipLaunchKernelGGL(k_tree_replay, dim3(1), dim3(64), 0, st, dctr, (const uint4 *)q.rep.as<uint4>(),
+                         (TreeState *)nullptr, tf, q.res.as<uint32_t>(res_keys_off()),
+                         q.res.as<uint64_t>(res_docs_off(k)));
     } else {
       hipLaunchKernelGGL(k_tree_replay, dim3(1), dim3(64), 0, st, dctr, (const uint4 *)q.rep.as<uint4>(),
                          (tree_phase & TREE_FINAL) ? (TreeState *)q.tree.p : q.tree.as<TreeState>(), tp,
@@ -6433,9 +6495,11 @@ static int score_info_docs(QuerySlot &q, const uint64_t *docs, int n, uint32_t n
   for (int t = 0; t < n; t++) {
     if (info[t].ok == -1) return GBGPU_ECORRUPT;      // a tree docid with no survivor entry
     if (info[t].ok == -2) {  // a getWordPosList path not replayed
+#ifdef GBGPU_DIAG
       if (std::getenv("GBGPU_SI_DEBUG"))
         std::fprintf(stderr, "gbgpu si decline: docid %llu path %d list %d\n", (unsigned long long)docs[t],
                      -((-info[t].pad) / 1000), (-info[t].pad) % 1000);
+#endif
       return GBGPU_EUNSUPPORTED;
     }
     if (info[t].ok == -3) return GBGPU_ECAPACITY;     // record arena exhausted
@@ -6502,24 +6566,9 @@ static int collect(gbgpu_ctx *ctx, QuerySlot &q, gbgpu_result *out, std::vector<
     std::memcpy(q.stats, st, sizeof st);
   }
   if (c->corrupt) return GBGPU_ECORRUPT;
-  if (c->tree_err == TREE_ERR_REG && q.seq_replay) {
-    // the tree outgrew k_tree_seq's register columns: the same replay
-    // entries through the LDS tree (up to TC nodes)
-    q.seq_replay = false;
-    hipStream_t st = q.stream;
-    Counters *dctr = q.res.as<Counters>();
-    HIPCHECK(hipMemsetAsync(&dctr->tree_err, 0, sizeof(uint32_t), st));
-    hipLaunchKernelGGL(k_tree_replay, dim3(1), dim3(64), 0, st, dctr, (const uint4 *)q.rep.as<uint4>(),
-                       (TreeState *)q.tree.p, tree_params(q.docs_wanted, TREE_INIT | TREE_FINAL, q.int_scores),
-                       q.res.as<uint32_t>(res_keys_off()), q.res.as<uint64_t>(res_docs_off(q.k)));
-    HIPCHECK(hipGetLastError());
-    HIPCHECK(hipMemcpyAsync(q.h_res, q.res.p, q.res_bytes, hipMemcpyDeviceToHost, st));
-    HIPCHECK(hipStreamSynchronize(st));
-    out->filtered = (int32_t)c->filtered;
-    q.stats[6] = (int64_t)c->tree_n;
-  }
   if (c->tree_err) return GBGPU_ECAPACITY;
   if (c->unsup) return GBGPU_EUNSUPPORTED;
+#ifdef GBGPU_DIAG
   if (ctx->d_sdbg && ctx->sdbg_grid) {
     std::vector<uint64_t> h((size_t)ctx->sdbg_grid * 8);
     if (hipMemcpy(h.data(), ctx->d_sdbg, h.size() * 8, hipMemcpyDeviceToHost) == hipSuccess)
@@ -6529,7 +6578,7 @@ static int collect(gbgpu_ctx *ctx, QuerySlot &q, gbgpu_result *out, std::vector<
           std::fclose(f);
         }
   }
-  if (ctx->d_pdbg && std::getenv("GBGPU_PROBE_DEBUG_DOC")) {
+  if (ctx->d_pdbg) {
     std::vector<unsigned long long> h(1 + 16 * 32);
     if (hipMemcpy(h.data(), ctx->d_pdbg, 8 * h.size(), hipMemcpyDeviceToHost) == hipSuccess)
       for (unsigned long long o = 0; o < std::min<unsigned long long>(h[0] & 0xffffffffull, 32); o++) {
@@ -6540,14 +6589,14 @@ static int collect(gbgpu_ctx *ctx, QuerySlot &q, gbgpu_result *out, std::vector<
                      r[0], r[1], r[2], r[3], r[4], r[5], r[6], r[7], r[8], r[9], r[10], r[11], r[12], r[13], r[14], r[15]);
       }
   }
-  if (std::getenv("GBGPU_TOPK_DEBUG") && q.sel.p) {
+  if (ctx->topk_debug && q.sel.p) {
     unsigned long long td[8];
     if (hipMemcpy(td, q.sel.as<uint8_t>(offsetof(Select, tdbg)), sizeof td, hipMemcpyDeviceToHost) == hipSuccess)
       std::fprintf(stderr, "topk us: hist %.2f gather %.2f wait %.2f refine %.2f sort %.2f nb %llu nt %llu\n",
                    (td[1] - td[0]) / 100.0, (td[2] - td[1]) / 100.0, (td[3] - td[2]) / 100.0, (td[4] - td[3]) / 100.0,
                    (td[5] - td[4]) / 100.0, td[6], td[7]);
   }
-  if (std::getenv("GBGPU_TOPK_DEBUG") && q.replayed)
+  if (ctx->topk_debug && q.replayed)
     std::fprintf(stderr, "replay: adds %u nmax %u tree_n %u us_add|cand %u us_total %u nsurv %u\n", c->pad[0], c->pad[1],
                  c->tree_n, c->rdbg_t, c->rdbg_total, (uint32_t)(c->surv_top >> 36));
   if (ctx->debug_ext) {
@@ -6556,6 +6605,7 @@ static int collect(gbgpu_ctx *ctx, QuerySlot &q, gbgpu_result *out, std::vector<
         std::fprintf(stderr, "gbgpu ext list %d units %llu dmax %llu E %u slot1 %u\n", l, c->ext[l].units,
                      c->ext[l].dmax, c->ext[l].E, c->ext[l].slot1);
   }
+#endif
   if (hits_acc || out->hit_docids) {
     std::vector<int64_t> local;
     std::vector<int64_t> &h = hits_acc ? *hits_acc : local;
@@ -6875,7 +6925,7 @@ static int grow_slots(gbgpu_ctx *ctx, int n) {
   if (n > MAX_SLOTS) return EINVAL;
   while (ctx->nslots < n) {
     QuerySlot *q = new QuerySlot();
-    int rc = q->init();
+    int rc = q->init(ctx->pool);
     if (rc) {
       q->release();
       delete q;
@@ -6895,13 +6945,25 @@ int gbgpu_open(int device, gbgpu_ctx **out) {
   gbgpu_ctx *ctx = new gbgpu_ctx();
   ctx->device = device;
   {
-    // the slots' stream-ordered buffers come from the device pool: keep what
-    // they free cached there (a regrown buffer reuses it, no device sync)
-    hipMemPool_t pool;
-    if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
-      uint64_t keep = ~0ull;
-      (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+    // the slots' stream-ordered buffers, resident lists and file images come
+    // from the context's own pool (the device's default pool and its
+    // process-wide settings are left alone): up to POOL_KEEP of what they
+    // free stays cached there (a regrown buffer reuses it with no device
+    // sync); beyond that the pool releases memory at the next sync, and a
+    // freed list or file image is trimmed back to the device at once
+    hipMemPoolProps pp;
+    std::memset(&pp, 0, sizeof pp);
+    pp.allocType = hipMemAllocationTypePinned;
+    pp.handleTypes = hipMemHandleTypeNone;
+    pp.location.type = hipMemLocationTypeDevice;
+    pp.location.id = device;
+    if (hipMemPoolCreate(&ctx->pool, &pp) != hipSuccess) {
+      ctx->pool = nullptr;
+      delete ctx;
+      return GBGPU_EHIP;
     }
+    uint64_t keep = POOL_KEEP;
+    (void)hipMemPoolSetAttribute(ctx->pool, hipMemPoolAttrReleaseThreshold, &keep);
   }
   Weights w = host_weights();
   if (hipStreamCreateWithFlags(&ctx->upload_stream, hipStreamNonBlocking) != hipSuccess ||
@@ -6911,6 +6973,9 @@ int gbgpu_open(int device, gbgpu_ctx **out) {
     gbgpu_close(ctx);
     return GBGPU_EHIP;
   }
+#ifdef GBGPU_DIAG
+  // diagnostic builds only (make diag: lib/libgbgpu_diag.so); the release
+  // library reads no environment and runs the one production path
   if (const char *pm = std::getenv("GBGPU_PROBE_MODE")) ctx->probe_mode = std::atoi(pm);
   if (const char *rm = std::getenv("GBGPU_REPLAY_MODE")) ctx->replay_mode = std::atoi(rm);
   if (const char *pw = std::getenv("GBGPU_PROBE_WAVES")) ctx->probe_waves = std::atoi(pw);
@@ -6918,6 +6983,10 @@ int gbgpu_open(int device, gbgpu_ctx **out) {
   if (const char *sm = std::getenv("GBGPU_SCORE_MODE")) ctx->score_mode = std::atoi(sm);
   if (ctx->score_mode == 2) HIPCHECK(hipMalloc(&ctx->d_sdbg, 8192 * 64));
   if (const char *de = std::getenv("GBGPU_DEBUG_EXT")) ctx->debug_ext = std::atoi(de);
+  ctx->probe_dbg_doc = std::getenv("GBGPU_PROBE_DEBUG_DOC");
+  ctx->topk_debug = std::getenv("GBGPU_TOPK_DEBUG") != nullptr;
+  if (ctx->probe_dbg_doc && hipMalloc((void **)&ctx->d_pdbg, 8 * (1 + 16 * 32)) != hipSuccess) ctx->d_pdbg = nullptr;
+#endif
   *out = ctx;
   return 0;
 }
@@ -6941,8 +7010,14 @@ void gbgpu_close(gbgpu_ctx *ctx) {
   gbmerge::state_free(ctx->merge);
   if (ctx->d_flag) (void)hipFree(ctx->d_flag);
   if (ctx->d_sdbg) (void)hipFree(ctx->d_sdbg);
+  if (ctx->d_pdbg) (void)hipFree(ctx->d_pdbg);
   if (ctx->h_flag) (void)hipHostFree(ctx->h_flag);
   if (ctx->upload_stream) (void)hipStreamDestroy(ctx->upload_stream);
+  if (ctx->pool) {
+    (void)hipDeviceSynchronize();  // every stream-ordered free has run
+    (void)hipMemPoolTrimTo(ctx->pool, 0);
+    (void)hipMemPoolDestroy(ctx->pool);
+  }
   delete ctx;
 }
 
@@ -6970,6 +7045,13 @@ int32_t gbgpu_tree_capacity(const gbgpu_params *p, const int64_t *sizes, int nte
   return (int32_t)std::min<int64_t>(tree_nodes(dw, true), TREE_CAP);
 }
 
+// a freed list or file image goes back to the device once its stream-ordered
+// free has run (TrimTo releases only memory no stream can still use); the
+// slots' cached buffers up to POOL_KEEP stay
+static void pool_trim(gbgpu_ctx *ctx) {
+  if (ctx->pool) (void)hipMemPoolTrimTo(ctx->pool, POOL_KEEP);
+}
+
 int gbgpu_list_upload(gbgpu_ctx *ctx, const uint8_t *bytes, int64_t size, int32_t *handle) {
   if (!ctx || !handle || (size > 0 && !bytes)) return EINVAL;
   std::lock_guard<std::mutex> g(ctx->lists_mu);
@@ -6985,8 +7067,8 @@ int gbgpu_file_upload(gbgpu_ctx *ctx, const uint8_t *bytes, int64_t size, int32_
   f.size = size;
   f.mem = std::make_shared<ListMem>();
   f.mem->st = ctx->upload_stream;
-  if (hipMallocAsync(reinterpret_cast<void **>(&f.mem->d), std::max<size_t>((size_t)size, 256), ctx->upload_stream) !=
-      hipSuccess)
+  if (DevBuf::pool_alloc(reinterpret_cast<void **>(&f.mem->d), std::max<size_t>((size_t)size, 256), ctx->pool,
+                         ctx->upload_stream))
     return ENOMEM;
   if (size) HIPCHECK(hipMemcpyAsync(f.mem->d, bytes, (size_t)size, hipMemcpyHostToDevice, ctx->upload_stream));
   HIPCHECK(hipStreamSynchronize(ctx->upload_stream));
@@ -7014,6 +7096,7 @@ int gbgpu_file_free(gbgpu_ctx *ctx, int32_t fh) {
   }
   (void)hipSetDevice(ctx->device);
   last.reset();
+  pool_trim(ctx);
   return 0;
 }
 
@@ -7076,6 +7159,7 @@ int gbgpu_list_free(gbgpu_ctx *ctx, int32_t h) {
   }
   (void)hipSetDevice(ctx->device);
   last.reset();
+  pool_trim(ctx);
   return 0;
 }
 
@@ -7405,6 +7489,8 @@ int gbgpu_allgather_topk(gbgpu_ctx *ctx, int slot, uint64_t seq, int timeout_ms,
   seq_leave(&ctx->xseq, seq);
   return rc;
 }
+
+uint64_t gbgpu_exchange_next(gbgpu_ctx *ctx) { return ctx ? gbgpu_seq_next(&ctx->xseq) : 0; }
 
 int gbgpu_seq_open(uint64_t first, gbgpu_seq **out) {
   if (!out) return EINVAL;

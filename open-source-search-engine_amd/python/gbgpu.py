@@ -196,18 +196,21 @@ EXPORTS = [
     "gbgpu_query_slot_collect", "gbgpu_slot_stream", "gbgpu_slot_timings", "gbgpu_slot_stats",
     "gbgpu_bandwidth_ceiling", "gbgpu_comm_unique_id", "gbgpu_comm_init", "gbgpu_allgather_topk",
     "gbgpu_merge_replies_device", "gbgpu_seq_open", "gbgpu_seq_enter", "gbgpu_seq_leave", "gbgpu_seq_next",
-    "gbgpu_seq_close",
+    "gbgpu_seq_close", "gbgpu_exchange_next",
     "gbgpu_merge_posdb_device", "gbgpu_merge_timings", "gbgpu_merge_path", "gbgpu_merge_last_key", "gb_synth_merge_runs",
     "gb_synth_lists", "gb_synth_free", "gb_synth_docid", "gb_posdb_compress", "gb_posdb_make_key",
 ]
 
-_lib: Optional[ctypes.CDLL] = None
+DIAG_LIB_PATH = os.path.join(PKG_DIR, "lib", "libgbgpu_diag.so")
+_libs = {}
 
 
 def load(path: str = LIB_PATH) -> ctypes.CDLL:
-    global _lib
-    if _lib is not None:
-        return _lib
+    """The product library (default), or the diagnostic build
+    (DIAG_LIB_PATH: the same sources with -DGBGPU_DIAG, which honours the
+    GBGPU_*_MODE switches of scripts/ and tests/test_replay.py)."""
+    if path in _libs:
+        return _libs[path]
     if not os.path.exists(path):
         raise RuntimeError(f"gbgpu native library not built: {path} (run __graft_entry__.build())")
     lib = ctypes.CDLL(path)
@@ -270,6 +273,8 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.gbgpu_seq_close.restype = None
     lib.gbgpu_comm_unique_id.argtypes = [vp]
     lib.gbgpu_comm_init.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp]
+    lib.gbgpu_exchange_next.argtypes = [vp]
+    lib.gbgpu_exchange_next.restype = ctypes.c_uint64
     lib.gbgpu_allgather_topk.argtypes = [vp, ctypes.c_int, ctypes.c_uint64, ctypes.c_int, i32, ctypes.POINTER(i64),
                                          ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i32), ctypes.POINTER(i64),
                                          ctypes.POINTER(Result)]
@@ -293,7 +298,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
                                       ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
                                       ctypes.c_int, ctypes.c_int]
     lib.gb_posdb_make_key.restype = None
-    _lib = lib
+    _libs[path] = lib
     return lib
 
 
@@ -431,8 +436,8 @@ class Engine:
     """One gbgpu context on one device: resident lists shared by its query
     slots (one HIP stream each; a context starts with one slot)."""
 
-    def __init__(self, device: int = 0):
-        self.lib = load()
+    def __init__(self, device: int = 0, diag: bool = False):
+        self.lib = load(DIAG_LIB_PATH if diag else LIB_PATH)
         self.ctx = ctypes.c_void_p()
         _check(self.lib.gbgpu_open(device, ctypes.byref(self.ctx)), "gbgpu_open")
         self._keep = {}
@@ -625,10 +630,10 @@ class Engine:
                                            sc.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), ctypes.byref(n),
                                            ctypes.byref(h), None)
         # an admitted call uses its number up whatever its outcome (the rank
-        # took part in the collective with an empty reply on failure); only a
-        # call that was never admitted (ETIMEDOUT) leaves it to be retried
-        if rc != errno.ETIMEDOUT and not (rc == errno.EINVAL and seq < self._xseq):
-            self._xseq = max(self._xseq, seq + 1)
+        # took part in the collective with an empty reply on failure); a call
+        # refused before admission (bad k, ETIMEDOUT) does not: the context's
+        # sequencer says which number comes next
+        self._xseq = int(self.lib.gbgpu_exchange_next(self.ctx))
         _check(rc, "gbgpu_allgather_topk")
         return d[:n.value], sc[:n.value], h.value
 

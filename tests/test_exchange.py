@@ -126,3 +126,54 @@ def test_allgather_topk_one_rank():
             eng.allgather_topk(10, slot=-1, seq=nxt + 5, timeout_ms=10)
         assert ei.value.code == errno.ETIMEDOUT
         assert eng._xseq == nxt + 3
+
+
+def test_allgather_refused_k_leaves_sequence():
+    """A k out of range is refused before admission: the default sequence
+    number is not used up, so the next default call is admitted at once
+    (it would wait forever on a number never entered otherwise)."""
+    with gbgpu.Engine(0) as eng:
+        eng.comm_init(1, 0, gbgpu.Engine.comm_unique_id())
+        for bad in (0, -1, 4097):
+            with pytest.raises(gbgpu.GbgpuError) as ei:
+                eng.allgather_topk(bad, slot=-1)
+            assert ei.value.code == errno.EINVAL
+            assert eng._xseq == 0
+        d, s, h = eng.allgather_topk(10, slot=-1, timeout_ms=5000)
+        assert len(d) == 0 and h == 0 and eng._xseq == 1
+
+
+@pytest.mark.parametrize("name", ["q_clus_prune_100k", "q_clus_dense", "q_clus_three_word"])
+def test_allgather_clustered_register_overflow(name):
+    """A clustered query whose TopTree outgrows k_tree_seq's register
+    columns (forced here: one column, GBGPU_REPLAY_MODE=3 in the diagnostic
+    build) replays on the device before the exchange packs the result block,
+    so the all-gathered reply is the query's final tree, not a stale one."""
+    import os
+    from test_golden import load_query
+    terms, lists, params, exp = load_query(os.path.join(os.path.dirname(__file__), "golden", name + ".npz"))
+    k = max(1, min(len(exp["docids"]), 4096))
+    old = os.environ.get("GBGPU_REPLAY_MODE")
+    os.environ["GBGPU_REPLAY_MODE"] = "3"
+    try:
+        eng = gbgpu.Engine(0, diag=True)
+    finally:
+        if old is None:
+            del os.environ["GBGPU_REPLAY_MODE"]
+        else:
+            os.environ["GBGPU_REPLAY_MODE"] = old
+    try:
+        eng.comm_init(1, 0, gbgpu.Engine.comm_unique_id())
+        hs = [eng.upload(l) for l in lists]
+        # a previous, different query leaves its result in the slot's buffers
+        other = [eng.upload(l) for l in lists[::-1]]
+        eng.enqueue(terms, other, params, slot=0)
+        eng.collect(slot=0)
+        eng.enqueue(terms, hs, params, slot=0)
+        d, s, h = eng.allgather_topk(k, slot=0)
+        m = min(k, len(exp["docids"]))
+        assert np.array_equal(d, exp["docids"][:m]), name
+        assert np.array_equal(s, exp["scores"][:m].astype(np.float64)), name
+        assert h == exp["hits"]
+    finally:
+        eng.close()

@@ -34,7 +34,7 @@ def mode_engine(request):
     old = os.environ.get("GBGPU_REPLAY_MODE")
     os.environ["GBGPU_REPLAY_MODE"] = request.param
     try:
-        e = gbgpu.Engine(0)
+        e = gbgpu.Engine(0, diag=True)  # the switch is read by the diagnostic build only
     finally:
         if old is None:
             del os.environ["GBGPU_REPLAY_MODE"]
