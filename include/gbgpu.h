@@ -356,6 +356,10 @@ int gbgpu_merge_posdb_device(gbgpu_ctx *ctx, const uint8_t *const *dev_lists, co
  * 3521-3535), from which merge_r's caller shrinks m_endKey (3544-3565).
  * 0, or ENOENT if the merge wrote no key. */
 int gbgpu_merge_last_key(gbgpu_ctx *ctx, uint8_t *key18);
+/* Whether the last merge stopped at its bound with input keys left unmerged:
+ * posdbMerge_r's numLists > 0 after its loop, the second condition (beside
+ * m_listSize >= the bound) of its m_endKey shrink (RdbList.cpp:3537-3565). */
+int gbgpu_merge_input_left(gbgpu_ctx *ctx, int32_t *left);
 /* Device timings of the last merge (HIP events), ms: [0] total, [1] decode,
  * [2] partition, [3] tile count pass, [4] tile offset scan, [5] tile write
  * pass; and the number of keys decoded and of merge tiles. */

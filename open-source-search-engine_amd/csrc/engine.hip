@@ -7629,6 +7629,15 @@ int gbgpu_merge_last_key(gbgpu_ctx *ctx, uint8_t *key18) {
   return gbmerge::last_key(m, key18);
 }
 
+int gbgpu_merge_input_left(gbgpu_ctx *ctx, int32_t *left) {
+  if (!ctx || !left) return EINVAL;
+  gbmerge::MergeState *m = merge_state(ctx);
+  if (!m) return GBGPU_EHIP;
+  *left = 0;
+  const int rc = gbmerge::last_key(m, nullptr, left);
+  return rc == ENOENT ? 0 : rc;
+}
+
 int gbgpu_merge_timings(gbgpu_ctx *ctx, float *ms6, int64_t *nkeys, int64_t *ntiles) {
   if (!ctx) return EINVAL;
   gbmerge::MergeState *m = merge_state(ctx);

@@ -24,8 +24,9 @@ int merge_host(MergeState *s, const uint8_t *const *lists, const int64_t *sizes,
                int64_t min_rec_sizes, uint8_t *out, int64_t out_cap, int64_t *out_size);
 
 // The last key the last merge wrote, decompressed (RdbList::m_lastKey):
-// 0, or ENOENT when it wrote nothing.
-int last_key(MergeState *s, uint8_t *key18);
+// 0, or ENOENT when it wrote nothing; *more (may be NULL): whether input
+// keys were left unmerged behind the cut.
+int last_key(MergeState *s, uint8_t *key18, int32_t *more = nullptr);
 
 // Phase timings of the last merge (HIP events), ms: [0] total, [1] decode
 // (count + scan + decode), [2] partition (samples, rank, offsets), [3] tile

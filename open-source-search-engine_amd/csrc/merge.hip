@@ -60,7 +60,7 @@ constexpr int TB = 256;                          // threads per merge-tile block
 constexpr int MAXN = 256;                        // runs per merge (oracle MAXL)
 constexpr int SCAN_TPB = MB * 4;                 // tiles per scan block
 
-enum : uint32_t { F_CORRUPT = 1, F_FIRST = 2, F_CAPACITY = 4 };
+enum : uint32_t { F_CORRUPT = 1, F_FIRST = 2, F_CAPACITY = 4, F_MORE = 8 };
 
 struct MList {
   const uint8_t *p;
@@ -845,6 +845,18 @@ __global__ void k_mcut(const TileSum *ts, const TileOff *to, uint32_t T, const u
   ctl->lk_b = kb & ~(uint64_t)0x06;
 }
 
+// posdbMerge_r's numLists after its loop (RdbList.cpp:3541-3542): the loop
+// stops right after writing the cut key W, so a run still holds keys iff it
+// has one ordered after W (bfcmpPosdb; keys equal to W in older runs were
+// dropped before it, and W's own run is past it).  One thread per run.
+__global__ void __launch_bounds__(256) k_mrest(const MList *lists, int n, Keys K, MCtl *ctl) {
+  const int i = threadIdx.x;
+  if (i >= n || ctl->out_end == 0) return;
+  const MList L = lists[i];
+  const uint64_t end = L.koff + L.nkeys;
+  if (gbound<true>(K, L.koff, end, ctl->lk_hi, ctl->lk_lo, ctl->lk_b) < end) atomicOr(&ctl->flags, (uint32_t)F_MORE);
+}
+
 // out[off, off + bytes) of every tile, below the cut: its first key, then its
 // arena bytes.  Byte offsets are even (keys are 6-byte multiples).
 __global__ void __launch_bounds__(MB) k_mcopy(const TileSum *ts, const TileOff *to, const uint8_t *arena,
@@ -931,6 +943,7 @@ struct MergeState {
   int64_t nkeys = 0, ntiles = 0;
   int path = 0;  // last merge: 2 (the decoded-key pipeline; 1 was the retired tile path)
   bool has_last = false;
+  bool more = false;  // input keys were left unmerged (posdbMerge_r's numLists > 0 at its end)
   uint8_t last_key[18] = {};
 };
 
@@ -978,7 +991,8 @@ static int64_t max_offset(int64_t total, int64_t mrs, int64_t cap) {
 // the tile-offset scans, the cut and the copy, shared by both paths; then
 // the result flags.  Returns 0, or RETRY when a tile overflowed.
 constexpr int RETRY = -1;
-static int finish_tiles(MergeState *s, uint32_t T32, uint64_t maxoff, int64_t cap, uint8_t *out, MCtl *dctl) {
+static int finish_tiles(MergeState *s, uint32_t T32, uint64_t maxoff, int64_t cap, uint8_t *out, MCtl *dctl, int n,
+                        const Keys &K) {
   hipStream_t st = s->st;
   const uint32_t nblk = cdiv(T32, SCAN_TPB);
   TileSum *ts = s->ts.as<TileSum>();
@@ -988,6 +1002,7 @@ static int finish_tiles(MergeState *s, uint32_t T32, uint64_t maxoff, int64_t ca
   k_tscan2<<<1, 1024, 0, st>>>(ts, s->bs.as<BlkSum>(), nblk, s->bo.as<TileOff>());
   k_tscan3<<<nblk, MB, 0, st>>>(ts, T32, s->bo.as<TileOff>(), to);
   k_mcut<<<1, 64, 0, st>>>(ts, to, T32, arena, maxoff, dctl);
+  k_mrest<<<1, 256, 0, st>>>(s->mlist.as<MList>(), n, K, dctl);
   MCHECK(hipEventRecord(s->ev[4], st));
   k_mcopy<<<cdiv(T32, MB / 64), MB, 0, st>>>(ts, to, arena, dctl, (uint64_t)cap, out, T32);
   MCHECK(hipGetLastError());
@@ -1064,7 +1079,7 @@ static int run_legacy(MergeState *s, int n, uint32_t nch, uint64_t units, int rm
     k_mtile<<<T32, TB, 0, st>>>(dl, n, s->off.as<uint32_t>(), K, s->ts.as<TileSum>(), rm, s->arena.as<uint8_t>(),
                                 dctl);
     MCHECK(hipEventRecord(s->ev[3], st));
-    const int rc = finish_tiles(s, T32, maxoff, cap, out, dctl);
+    const int rc = finish_tiles(s, T32, maxoff, cap, out, dctl, n, K);
     if (rc != RETRY) return rc;
     if (S == 1) return GBGPU_ECAPACITY;  // > S equal keys in one run
     MCHECK(hipMemsetAsync(dctl, 0, sizeof(MCtl), st));
@@ -1076,6 +1091,7 @@ static int run(MergeState *s, const uint8_t *const *lists, const int64_t *sizes,
   *out_size = 0;
   s->nkeys = s->ntiles = 0;
   s->has_last = false;
+  s->more = false;
   s->path = 0;
   std::fill(s->ms, s->ms + 6, 0.f);
   if (nin < 0 || nin > MAXN || cap < 0) return EINVAL;
@@ -1122,6 +1138,7 @@ static int run(MergeState *s, const uint8_t *const *lists, const int64_t *sizes,
     for (int i = 0; i < 3; i++)
       for (int j = 0; j < 6; j++) s->last_key[6 * i + j] = (uint8_t)(v[i] >> (8 * j));
     s->has_last = true;
+    s->more = (s->h_ctl->flags & F_MORE) != 0;
   }
   return 0;
 }
@@ -1165,10 +1182,11 @@ int merge_host(MergeState *s, const uint8_t *const *lists, const int64_t *sizes,
   return 0;
 }
 
-int last_key(MergeState *s, uint8_t *key18) {
+int last_key(MergeState *s, uint8_t *key18, int32_t *more) {
   std::lock_guard<std::mutex> g(s->mu);
+  if (more) *more = s->more ? 1 : 0;
   if (!s->has_last) return ENOENT;
-  std::memcpy(key18, s->last_key, 18);
+  if (key18) std::memcpy(key18, s->last_key, 18);
   return 0;
 }
 

@@ -197,7 +197,7 @@ EXPORTS = [
     "gbgpu_bandwidth_ceiling", "gbgpu_comm_unique_id", "gbgpu_comm_init", "gbgpu_allgather_topk",
     "gbgpu_merge_replies_device", "gbgpu_seq_open", "gbgpu_seq_enter", "gbgpu_seq_leave", "gbgpu_seq_next",
     "gbgpu_seq_close", "gbgpu_exchange_next",
-    "gbgpu_merge_posdb_device", "gbgpu_merge_timings", "gbgpu_merge_path", "gbgpu_merge_last_key", "gb_synth_merge_runs",
+    "gbgpu_merge_posdb_device", "gbgpu_merge_timings", "gbgpu_merge_path", "gbgpu_merge_last_key", "gbgpu_merge_input_left", "gb_synth_merge_runs",
     "gb_synth_lists", "gb_synth_free", "gb_synth_docid", "gb_posdb_compress", "gb_posdb_make_key",
 ]
 
@@ -248,6 +248,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.gbgpu_merge_posdb_device.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(i64), ctypes.c_int,
                                              ctypes.c_int, i64, vp, i64, ctypes.POINTER(i64)]
     lib.gbgpu_merge_last_key.argtypes = [vp, vp]
+    lib.gbgpu_merge_input_left.argtypes = [vp, ctypes.POINTER(i32)]
     lib.gbgpu_merge_path.argtypes = [vp]
     lib.gbgpu_merge_timings.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(i64),
                                         ctypes.POINTER(i64)]
@@ -622,8 +623,8 @@ class Engine:
         empty reply."""
         if seq is None:
             seq = self._xseq
-        d = np.zeros(k, np.int64)
-        sc = np.zeros(k, np.float64)
+        d = np.zeros(max(k, 1), np.int64)
+        sc = np.zeros(max(k, 1), np.float64)
         n, h = ctypes.c_int32(), ctypes.c_int64()
         rc = self.lib.gbgpu_allgather_topk(self.ctx, slot, seq, timeout_ms,
                                            k, d.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
@@ -701,6 +702,13 @@ class Engine:
             return None
         _check(rc, "gbgpu_merge_last_key")
         return k.raw
+
+    def merge_input_left(self) -> bool:
+        """Whether the last merge stopped at its bound with input keys left
+        (posdbMerge_r's numLists > 0 at its end, RdbList.cpp:3541-3542)."""
+        v = ctypes.c_int32()
+        _check(self.lib.gbgpu_merge_input_left(self.ctx, ctypes.byref(v)), "gbgpu_merge_input_left")
+        return bool(v.value)
 
     def merge_timings(self):
         ms = (ctypes.c_float * 6)()

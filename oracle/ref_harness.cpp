@@ -78,7 +78,17 @@ static bool s_inited = false;
 // intersectLists10_r, in the same Msg39 sequence, and falls back to the
 // unmodified CPU body where it declines -- as the adapter's caller does
 extern bool gbref_adapter_intersect(PosdbTable *pt) __attribute__((weak));
-static int s_adapter = 0;   // op 4 mode: 1 = the adapter body
+// the docid-split loop replaced at the Msg39 level
+// (gbgpuDocIdSplits) with the whole-range lists resident; op 4 mode 2
+extern bool gbref_adapter_splits(Msg39 *m, const uint8_t *const *lists, const int64_t *sizes)
+    __attribute__((weak));
+// gbgpuShardQuery as shard 0 of a one-rank exchange; op 7
+extern int gbref_adapter_shard(PosdbTable *pt, const uint8_t *const *lists, const int64_t *sizes, int32_t k,
+                               int64_t *docids, double *scores, int32_t *n, int64_t *hits) __attribute__((weak));
+// gbgpuMergePosdb in place of merge_r's posdbMerge_r call; op 6
+extern bool gbref_adapter_merge(RdbList *self, RdbList **lists, int32_t numLists, char *startKey, char *endKey,
+                                int32_t minRecSizes, bool removeNegRecs) __attribute__((weak));
+static int s_adapter = 0;   // op 4 mode: 1 = the adapter body, 2 = and the Msg39 split adapter
 static int s_answered = 0;  // passes the adapter answered
 // the second pass's score info (Posdb.cpp:6116-6244, 7554-7665): the last
 // query's m_scoreInfoBuf / m_pairScoreBuf / m_singleScoreBuf bytes
@@ -105,6 +115,7 @@ static void ref_init() {
 
 enum { MAXT = 64 };
 
+static PosdbTable *s_tab = NULL;       // the last query's PosdbTable
 static std::vector<int32_t> s_plan;    // the last query's QueryTermInfos (op 4)
 static int32_t s_used_nodes = 0;       // the last query's TopTree::m_numUsedNodes
 static std::vector<int32_t> s_ints;    // its nodes' m_intScore, high -> low
@@ -119,9 +130,15 @@ static int ref_query(const orc_qterm *terms, const uint8_t *const *lists, const 
   static RdbList rl[MAXT];
   static Msg2 msg2;
   static Msg39Request req;
-  static TopTree tree;
+  static TopTree s_tree;
   static float tfw[MAXT];
-  static PosdbTable *tab = NULL;
+  // mode 2 plays Msg39 itself: its m_tt is the tree, its m_posdbTable the
+  // table (Msg39.h:252,278), which gbgpuDocIdSplits fills
+  static Msg39 *s_m39 = NULL;
+  const bool msg39 = s_adapter == 2 && p->num_docid_splits > 1;
+  if (msg39 && !s_m39) s_m39 = new Msg39();
+  TopTree &tree = msg39 ? s_m39->m_tt : s_tree;
+  PosdbTable *&tab = s_tab;
 
   memset((void *)qts, 0, sizeof(qts));
   memset((void *)qws, 0, sizeof(qws));
@@ -246,12 +263,20 @@ static int ref_query(const orc_qterm *terms, const uint8_t *const *lists, const 
     // one PosdbTable over all pieces: reset per piece (Msg39::reset2,
     // Msg39.cpp:51-69), its allocTopTree buffers (m_stackBuf) kept
     if (d0 == 0) {
-      if (tab) {
+      if (tab && tab != (s_m39 ? &s_m39->m_posdbTable : NULL)) {
         tab->~PosdbTable();
         mfree(tab, sizeof(PosdbTable), "refharness");
       }
-      tab = (PosdbTable *)mmalloc(sizeof(PosdbTable), "refharness");
-      new (tab) PosdbTable();
+      if (msg39) {
+        tab = &s_m39->m_posdbTable;
+        tab->~PosdbTable();
+        new (tab) PosdbTable();
+        s_m39->m_r = &req;
+        s_m39->m_numTotalHits = 0;
+      } else {
+        tab = (PosdbTable *)mmalloc(sizeof(PosdbTable), "refharness");
+        new (tab) PosdbTable();
+      }
     }
     tab->reset();
     // Msg39::intersectLists sequence (Msg39.cpp:922-1027)
@@ -262,6 +287,15 @@ static int ref_query(const orc_qterm *terms, const uint8_t *const *lists, const 
     if (!tab->allocWhiteListTable()) return ENOMEM;
     if (!tab->setQueryTermInfo()) return ENOMEM;
     const double t0 = now_s();
+    if (msg39 && d0 == 0 && gbref_adapter_splits && gbref_adapter_splits(s_m39, lists, sizes)) {
+      // every piece answered at once (Msg39's loop skipped to phase 3):
+      // m_numTotalHits is the hits less m_filtered (Msg39.cpp:409-414)
+      s_isect_s += now_s() - t0;
+      s_answered++;
+      out->hits = s_m39->m_numTotalHits;
+      out->filtered = 0;
+      break;
+    }
     if (s_adapter && gbref_adapter_intersect && gbref_adapter_intersect(tab)) s_answered++;
     else tab->intersectLists10_r();
     s_isect_s += now_s() - t0;
@@ -359,6 +393,79 @@ static int64_t ref_posdb_merge(const uint8_t *const *lists, const int64_t *sizes
   return sz;
 }
 
+// op 6: RdbList::merge_r for posdb as Msg5::mergeLists_r / RdbMerge call it
+// (prepareForMerge, then merge_r with a start and end key), either unchanged
+// (mode 0) or with INTEGRATION.md 5's gbgpuMergePosdb where merge_r calls
+// posdbMerge_r (mode 1).  The reference is not edited, so mode 1 runs
+// merge_r's own steps before that call here (RdbList.cpp:1658-1741 for
+// RDB_POSDB: the early returns, the key range with its dangling-negative
+// fix, the key size) and then the adapter, falling back to posdbMerge_r
+// where it declines -- the body merge_r would have with the adapter in it.
+// Returns the list and what merge_r's caller reads after it: m_lastKey (and
+// whether it is valid) and m_endKey.
+static int64_t ref_posdb_merge_r(int mode, const uint8_t *const *lists, const int64_t *sizes, int n,
+                                 int remove_neg_keys, int64_t min_rec_sizes, const char *sk, const char *ek,
+                                 uint8_t *out, int64_t cap, char *last_key, int32_t *last_valid, char *end_key,
+                                 int32_t *answered) {
+  ref_init();
+  if (n < 0 || n > 256) return -EINVAL;
+  static RdbList in[256];
+  RdbList *ptrs[256];
+  for (int i = 0; i < n; i++) {
+    in[i].freeList();
+    int32_t sz = (int32_t)sizes[i];
+    char *buf = NULL;
+    if (sz > 0) {
+      buf = (char *)mmalloc(sz, "refharness");
+      memcpy(buf, lists[i], sz);
+    }
+    in[i].set(buf, sz, buf, sz, 0, true, true, 18);
+    ptrs[i] = &in[i];
+  }
+  RdbList dst;
+  dst.set(NULL, 0, NULL, 0, 0, true, true, 18);
+  char startKey[18], endKey[18];
+  memcpy(startKey, sk, 18);
+  memcpy(endKey, ek, 18);
+  const int32_t mrs = min_rec_sizes < 0 ? -1 : (int32_t)min_rec_sizes;
+  if (!dst.prepareForMerge(ptrs, n, mrs)) return -ENOMEM;
+  int32_t filtered = 0;
+  *answered = 0;
+  const double t0 = now_s();
+  bool done = false;
+  if (mode == 1 && gbref_adapter_merge) {
+    // merge_r's steps before its posdbMerge_r call (RdbList.cpp:1681-1741)
+    if (n == 0 || dst.m_mergeMinListSize == -1 || (mrs >= 0 && dst.m_listSize >= mrs)) {
+      done = true;
+    } else {
+      KEYSET(dst.m_startKey, startKey, dst.m_ks);
+      KEYSET(dst.m_endKey, endKey, dst.m_ks);
+      if (KEYCMP(dst.m_startKey, dst.m_endKey, dst.m_ks) != 0 && KEYNEG(dst.m_endKey)) KEYSUB(dst.m_endKey, 1, dst.m_ks);
+      dst.m_ks = ptrs[0]->m_ks;
+      if (mrs == 0) done = true;
+      else if (gbref_adapter_merge(&dst, ptrs, n, startKey, endKey, mrs, remove_neg_keys != 0)) {
+        *answered = 1;
+        done = true;
+      } else {
+        dst.posdbMerge_r(ptrs, n, startKey, endKey, dst.m_mergeMinListSize, remove_neg_keys != 0, &filtered,
+                         false, false, 0);
+        done = true;
+      }
+    }
+  }
+  if (!done)
+    dst.merge_r(ptrs, n, startKey, endKey, mrs, remove_neg_keys != 0, RDB_POSDB, &filtered, NULL, NULL, false, 0);
+  s_merge_s = now_s() - t0;
+  int64_t sz = dst.m_listSize;
+  if (sz > cap) return -ENOSPC;
+  memcpy(out, dst.m_list, sz);
+  memcpy(last_key, dst.m_lastKey, 18);
+  *last_valid = dst.m_lastKeyIsValid ? 1 : 0;
+  memcpy(end_key, dst.m_endKey, 18);
+  dst.freeList();
+  return sz;
+}
+
 // Msg3a::mergeLists (Msg3a.cpp:971-1503) over n fake shard replies, as
 // Msg3a::gotAllShardReplies calls it: each reply is a Msg39Reply whose
 // ptr_docIds / ptr_scores (double, Msg39.cpp:1661-1664) are the caller's
@@ -438,7 +545,7 @@ int main(int argc, char **argv) {
   ref_init();  // Mem's global operator new needs g_mem before any allocation
   int32_t op;
   while (fread(&op, 4, 1, stdin) == 1) {
-    if (op == 1 || op == 4) {
+    if (op == 1 || op == 4 || op == 7) {
       // op 4: i32 mode first (0 the CPU body, 1 the GPU adapter), then op 1's
       // request; the response adds i32 passes the adapter answered, i32
       // m_numUsedNodes and n x i32 m_intScore
@@ -513,6 +620,41 @@ int main(int argc, char **argv) {
         wr(&nb, 8);
         wr(s_info[b].data(), (size_t)nb);
       }
+      if (op == 7) {
+        // the shard's reply merged by the reference's own Msg3a::mergeLists
+        // (one shard: the TopTree's first docsToGet as Msg39 sends them,
+        // double scores), then the same query through gbgpuShardQuery
+        std::vector<double> sd(r.n > 0 ? r.n : 1);
+        // Msg39.cpp:1661-1664: m_score, or (double)m_intScore with integer tree scores
+        const bool ints = s_tab && s_tab->m_sortByTermNumInt >= 0;
+        for (int i = 0; i < r.n; i++) sd[i] = ints ? (double)s_ints[i] : (double)s[i];
+        const int64_t *dp = d.data();
+        const double *sp = sd.data();
+        const int32_t cnt = std::min<int32_t>(r.n, p.docs_to_get);
+        std::vector<int64_t> od;
+        std::vector<double> os;
+        int mrc = ref_msg3a_merge(1, p.docs_to_get, &cnt, &dp, &sp, od, os);
+        int32_t no = mrc ? -mrc : (int32_t)od.size();
+        wr(&no, 4);
+        if (no > 0) {
+          wr(od.data(), 8 * (size_t)no);
+          wr(os.data(), 8 * (size_t)no);
+        }
+        const int32_t k = p.docs_to_get;
+        std::vector<int64_t> gd(k > 0 ? k : 1);
+        std::vector<double> gs(k > 0 ? k : 1);
+        int32_t gn = 0;
+        int64_t gh = 0;
+        int32_t grc = gbref_adapter_shard ? gbref_adapter_shard(s_tab, ptrs.data(), sizes.data(), k, gd.data(),
+                                                                gs.data(), &gn, &gh)
+                                          : -1;
+        if (grc) gn = 0;
+        wr(&grc, 4);
+        wr(&gn, 4);
+        wr(&gh, 8);
+        wr(gd.data(), 8 * (size_t)gn);
+        wr(gs.data(), 8 * (size_t)gn);
+      }
       if (op == 4) {
         wr(&s_answered, 4);
         wr(&s_used_nodes, 4);
@@ -549,6 +691,45 @@ int main(int argc, char **argv) {
       wr(&sz, 8);
       if (sz > 0) wr(out.data(), sz);
       wr(&s_merge_s, 8);
+    } else if (op == 6) {
+      // merge_r with start/end keys: i32 mode (0 merge_r, 1 with the
+      // adapter), i32 n, i32 remove_neg, i64 min_rec_sizes, 18 B start key,
+      // 18 B end key, n x (i64 size, bytes)  ->  i64 size (or -errno), bytes,
+      // 18 B m_lastKey, i32 m_lastKeyIsValid, 18 B m_endKey, i32 answered
+      int32_t mode, n, rm;
+      int64_t mrs;
+      char sk[18], ek[18];
+      rd(&mode, 4);
+      rd(&n, 4);
+      rd(&rm, 4);
+      rd(&mrs, 8);
+      rd(sk, 18);
+      rd(ek, 18);
+      if (n < 0 || n > 256) return 4;
+      std::vector<std::vector<uint8_t> > bufs(n);
+      std::vector<const uint8_t *> ptrs(n);
+      std::vector<int64_t> sizes(n);
+      int64_t tot = 0;
+      for (int i = 0; i < n; i++) {
+        rd(&sizes[i], 8);
+        bufs[i].resize(sizes[i] + 1);
+        rd(bufs[i].data(), sizes[i]);
+        ptrs[i] = bufs[i].data();
+        tot += sizes[i];
+      }
+      std::vector<uint8_t> out(tot + 64);
+      char lk[18], ekey[18];
+      int32_t lv = 0, ans = 0;
+      memset(lk, 0, 18);
+      memset(ekey, 0, 18);
+      int64_t sz = ref_posdb_merge_r(mode, ptrs.data(), sizes.data(), n, rm, mrs, sk, ek, out.data(), tot + 64, lk,
+                                     &lv, ekey, &ans);
+      wr(&sz, 8);
+      if (sz > 0) wr(out.data(), sz);
+      wr(lk, 18);
+      wr(&lv, 4);
+      wr(ekey, 18);
+      wr(&ans, 4);
     } else if (op == 3) {
       // Msg3a merge: i32 nshards, i32 docs_to_get, per shard i32 n,
       // n x i64 docid, n x f64 score  ->  i32 n (or -errno), n x i64, n x f64

@@ -62,7 +62,7 @@ def _read(n, exe=None):
     return b
 
 
-def query(terms, lists, params, cap=4096, votes=False, reps=1, white=None, mode=None, exe=None):
+def query(terms, lists, params, cap=4096, votes=False, reps=1, white=None, mode=None, exe=None, op=None):
     """Same result dict as oracle_binding.query (+ 'votes', 'seconds').
     white: the whitelist lists (Msg2::m_whiteLists) when params.use_whitelist.
     mode (op 4, the gbref_gpu build): 0 the CPU body, 1 INTEGRATION.md's
@@ -71,7 +71,10 @@ def query(terms, lists, params, cap=4096, votes=False, reps=1, white=None, mode=
     p = _p(exe)
     rd = lambda n: _read(n, exe)  # noqa: E731
     qt = (gbgpu.QTerm * max(1, len(terms)))(*terms)
-    head = struct.pack("<ii", 1, len(terms)) if mode is None else struct.pack("<iii", 4, mode, len(terms))
+    if op == 7:
+        head = struct.pack("<ii", 7, len(terms))
+    else:
+        head = struct.pack("<ii", 1, len(terms)) if mode is None else struct.pack("<iii", 4, mode, len(terms))
     req = [head, bytes(params), bytes(qt)[:ctypes.sizeof(gbgpu.QTerm) * len(terms)]]
     for l in lists:
         req.append(struct.pack("<q", len(l)))
@@ -97,6 +100,16 @@ def query(terms, lists, params, cap=4096, votes=False, reps=1, white=None, mode=
     out = dict(docids=d, scores=s, hits=r.hits, filtered=r.filtered, docs_wanted=r.docs_wanted,
                corrupt=r.corrupt, votes=v, seconds=sec, score_info=info[0], pair_scores=info[1],
                single_scores=info[2])
+    if op == 7:
+        (no,) = struct.unpack("<i", rd(4))
+        if no < 0:
+            raise RuntimeError(f"gbref msg3a rc={-no}")
+        out["msg3a_docids"] = np.frombuffer(rd(8 * no), np.int64).copy()
+        out["msg3a_scores"] = np.frombuffer(rd(8 * no), np.float64).copy()
+        grc, gn, gh = struct.unpack("<iiq", rd(16))
+        out.update(shard_rc=grc, shard_hits=gh)
+        out["shard_docids"] = np.frombuffer(rd(8 * gn), np.int64).copy()
+        out["shard_scores"] = np.frombuffer(rd(8 * gn), np.float64).copy()
     if mode is not None:
         answered, used = struct.unpack("<ii", rd(8))
         out.update(answered=answered, used_nodes=used, int_scores=np.frombuffer(rd(4 * r.n), np.int32).copy())
@@ -130,6 +143,40 @@ def posdb_merge(lists, remove_neg_keys, min_rec_sizes=-1, timed=False):
     if timed:
         return out, sec
     return out
+
+
+def shard_query(terms, lists, params, white=None, exe=None):
+    """op 7 (gbref_gpu): the query through the reference's CPU body, its
+    TopTree merged by the reference's Msg3a::mergeLists as the one shard's
+    reply ('msg3a_docids' / 'msg3a_scores'), and the same query through
+    INTEGRATION.md's gbgpuShardQuery as shard 0 of a one-rank RCCL
+    exchange ('shard_rc', 'shard_docids', 'shard_scores', 'shard_hits')."""
+    return query(terms, lists, params, cap=1 << 16, white=white, exe=exe or EXE_GPU, op=7)
+
+
+def posdb_merge_r(lists, remove_neg_keys, min_rec_sizes=-1, start_key=None, end_key=None, mode=0, exe=None):
+    """op 6: RdbList::merge_r for posdb with a key range (mode 0), or with
+    INTEGRATION.md's gbgpuMergePosdb where merge_r calls posdbMerge_r (mode 1,
+    gbref_gpu).  Returns dict(list, last_key, last_valid, end_key, answered)."""
+    p = _p(exe)
+    sk = bytes(start_key) if start_key is not None else bytes(18)
+    ek = bytes(end_key) if end_key is not None else b"\xff" * 18
+    req = [struct.pack("<iiiiq", 6, mode, len(lists), 1 if remove_neg_keys else 0, min_rec_sizes), sk, ek]
+    for l in lists:
+        req.append(struct.pack("<q", len(l)))
+        req.append(bytes(l))
+    p.stdin.write(b"".join(req))
+    p.stdin.flush()
+    rd = lambda n: _read(n, exe)  # noqa: E731
+    (n,) = struct.unpack("<q", rd(8))
+    out = rd(n) if n > 0 else b""
+    lk = rd(18)
+    (lv,) = struct.unpack("<i", rd(4))
+    ek2 = rd(18)
+    (ans,) = struct.unpack("<i", rd(4))
+    if n < 0:
+        raise RuntimeError(f"gbref merge_r rc={n}")
+    return dict(list=out, last_key=lk, last_valid=lv, end_key=ek2, answered=ans)
 
 
 def msg3a_merge(shards, docs_to_get):
