@@ -526,6 +526,11 @@ static int ref_msg3a_merge(int nshards, int32_t docs_to_get, const int32_t *coun
 #include <algorithm>
 #include <vector>
 
+// the response stream: the process's original stdout, kept private; fd 1
+// itself is pointed at stderr, so anything a linked library prints (RCCL /
+// HIP banners and debug logs) cannot corrupt the protocol
+static FILE *s_proto = NULL;
+
 static void rd(void *p, size_t n) {
   if (n && fread(p, 1, n, stdin) != n) {
     fprintf(stderr, "gbref: short read\n");
@@ -533,7 +538,7 @@ static void rd(void *p, size_t n) {
   }
 }
 static void wr(const void *p, size_t n) {
-  if (n && fwrite(p, 1, n, stdout) != n) exit(3);
+  if (n && fwrite(p, 1, n, s_proto) != n) exit(3);
 }
 static double now_s() {
   struct timespec ts;
@@ -543,6 +548,12 @@ static double now_s() {
 
 int main(int argc, char **argv) {
   ref_init();  // Mem's global operator new needs g_mem before any allocation
+  {
+    const int pfd = dup(1);
+    if (pfd < 0 || dup2(2, 1) < 0) return 6;
+    s_proto = fdopen(pfd, "wb");
+    if (!s_proto) return 6;
+  }
   int32_t op;
   while (fread(&op, 4, 1, stdin) == 1) {
     if (op == 1 || op == 4 || op == 7) {
@@ -764,7 +775,7 @@ int main(int argc, char **argv) {
     } else {
       return 5;
     }
-    fflush(stdout);
+    fflush(s_proto);
   }
   return 0;
 }
