@@ -125,6 +125,21 @@ typedef struct gbgpu_params {
   int32_t use_whitelist;
   int32_t n_white_lists;
   const struct gbgpu_list *white_lists;
+  /* Boolean queries (Query::m_isBoolean): the docid set is the union of every
+   * group's sublists, negative groups included, each docid carrying the bit
+   * vector of the QueryTermInfos it occurs in (QueryTerm::m_bitNum = the
+   * group index, Posdb.cpp:4485-4721), kept where the query's expression
+   * holds for that vector (makeDocIdVoteBufForBoolQuery_r, Posdb.cpp:
+   * 8006-8249); its score is the number of bits set, times sameLangWeight on
+   * a language match (Posdb.cpp:6514-6534, 7247-7256; m_siteRankMultiplier is
+   * 0, Posdb.cpp:774).  The expression comes as its truth table: bit v
+   * (byte v >> 3, bit v & 7) = Query::matchesBoolQuery over vector v, for
+   * every v < 2^bool_ngroups; bool_ngroups must equal the plan's
+   * m_numQueryTermInfos (<= 16; more is GBGPU_EUNSUPPORTED).  The whitelist
+   * does not apply (the boolean vote never reads it).  Zero: not boolean. */
+  int32_t is_boolean;
+  int32_t bool_ngroups;
+  const uint8_t *bool_table;
 } gbgpu_params;
 
 

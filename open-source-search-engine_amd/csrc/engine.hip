@@ -2029,6 +2029,35 @@ __device__ __forceinline__ void cmp_word(const DevPlan *__restrict__ pl, const C
   for (int a = 0; a < pl->g0n; a++) valid |= range_bits(s0, pl->g0base[a], pl->g0base[a] + ctr->g0count[a]);
   c.own0 = range_bits(s0, pl->g0base[0], pl->g0base[0] + ctr->g0count[0]);
   uint32_t surv = valid;
+  if (pl->boolean) {
+    // makeDocIdVoteBufForBoolQuery_r (Posdb.cpp:8026-8231): each slot's
+    // QueryTermInfo bit vector from its lists (its canonical slot: any list
+    // bit at all), kept where the truth table holds
+    uint32_t gw[16];
+#pragma unroll
+    for (int g = 0; g < 16; g++) gw[g] = 0;
+    const int l0 = pl->g0list[0];
+    uint32_t any = 0;
+#pragma unroll
+    for (int l = 0; l < MAXL; l++) {
+      const uint32_t lb = c.bw[l] | (l == l0 ? c.own0 : 0u);
+      any |= lb;
+      const uint32_t gm = l < pl->nlists ? pl->bool_gmask[l] : 0u;
+#pragma unroll
+      for (int g = 0; g < 16; g++)
+        if (gm >> g & 1) gw[g] |= lb;
+    }
+    uint32_t pass = 0;
+    for (uint32_t m = surv & any; m; m &= m - 1) {
+      const int q = __ffs(m) - 1;
+      uint32_t v = 0;
+#pragma unroll
+      for (int g = 0; g < 16; g++) v |= ((gw[g] >> q) & 1u) << g;
+      if (pl->bool_table[v >> 3] >> (v & 7) & 1) pass |= 1u << q;
+    }
+    c.surv = pass;
+    return;
+  }
   if (surv && pl->use_rej) {  // not voted: whitelist / a range term's first group (k_write_runs)
     const v4u *r = reinterpret_cast<const v4u *>(pl->wrej + s0);
     const v4u r0 = r[0], r1 = r[1];
@@ -3103,12 +3132,25 @@ __global__ void __launch_bounds__(SCORE_TPB) k_score(const DevPlan *__restrict__
           if (e.reloc) off = e.off;
         }
       }
-      uint32_t key, nr;
+      uint32_t key, nr = 0;
       if (dbg) {
         __asm__ volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         ts1 = __builtin_amdgcn_s_memtime();
       }
-      if (units <= ((uint32_t)RC << (6 - sh))) {
+      if (pl->boolean) {
+        // a boolean query's score (Posdb.cpp:6514-6534, 7247-7256): the bits of
+        // its vector, times (siteRank * 0 + 1.0) and the same-language weight
+        // (siteRank and docLang keep their initial 0: the scorers and their
+        // siteRank/langId reads are jumped over)
+        uint32_t v = 0;
+        for (uint32_t xm = lm; xm; xm &= xm - 1) v |= pl->bool_gmask[__ffs(xm) - 1];
+        const float minScore = (float)__popc(v);
+        float score = (float)((double)minScore * ((double)(0.0f * pl->site_rank_multiplier) + 1.0));
+        score *= pl->same_lang_weight;
+        const uint32_t b = __float_as_uint(score);
+        key = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+        if (key == 0) key = 1;
+      } else if (units <= ((uint32_t)RC << (6 - sh))) {
         const LdsRecs lrec{(__attribute__((address_space(3))) uint32_t *)(s_rlo + lane),
                            (__attribute__((address_space(3))) uint16_t *)(s_rhi + lane), sh, RC << (6 - sh)};
         score_survivor<NQ, NS>(pl, ctr, s, lm, anys, svl, lrec, s_sm + lane, &key, diag, &nr,
@@ -3734,7 +3776,9 @@ __global__ void __launch_bounds__(64 * BND_WAVES) k_bound(const DevPlan *__restr
   const int ng = pl->ngroups, m = pl->min_listi;
   const float INF = __int_as_float(0x7f800000);
   const float tfw_m = pl->tfw[m];
-  const bool sortby = pl->sortby_group >= 0;  // gbsortby: both prefilters are skipped (Posdb.cpp:6050-6051, 6350)
+  // gbsortby: both prefilters are skipped (Posdb.cpp:6050-6051, 6350); a
+  // boolean query jumps over them (Posdb.cpp:6312-6316)
+  const bool sortby = pl->sortby_group >= 0 || pl->boolean;
   for (uint32_t base = (blockIdx.x * BND_WAVES + wid) * 64u; base < nsurv; base += gridDim.x * BND_WAVES * 64u) {
     const uint32_t i = base + lane;
     float B = INF;
@@ -5787,9 +5831,27 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   if (rc) return rc;
   if (dw_override > 0) hp.docs_wanted = dw_override;
   const bool clus = p->site_clustering != 0;
+  const bool boolean = p->is_boolean != 0;
+  if (boolean) {
+    // the truth table is over the plan's QueryTermInfos (m_bitNum = the
+    // group index, Posdb.cpp:4485-4721)
+    if (!p->bool_table || p->bool_ngroups != hp.ngroups) return EINVAL;
+    if (hp.ngroups > 16) return GBGPU_EUNSUPPORTED;
+    // a boolean query's gbsortby score reads a mini-merged list that may be
+    // another group's or stale (Posdb.cpp:7263-7279); its range terms vote by
+    // isInRange over the whole run (8087-8129), not restated on the device;
+    // its second pass is not replayed
+    if (hp.sortby_group >= 0 || p->get_docid_scoring_info) return GBGPU_EUNSUPPORTED;
+    for (int i = 0; i < nterms; i++) {
+      int ri = 0;
+      if (terms[i].is_required && range_mode(terms[i].field_code, &ri)) return GBGPU_EUNSUPPORTED;
+    }
+  }
   q.docs_wanted = hp.docs_wanted;
   q.k = clus ? TC : hp.docs_wanted;
-  q.early = (hp.ngroups == 0 || hp.min_list_size == 0);
+  // Posdb.cpp:5735: a boolean query goes on with an empty smallest group
+  // (allocTopTree gave it no tree only when every list is empty)
+  q.early = hp.ngroups == 0 || (boolean ? hp.docs_wanted == 0 : hp.min_list_size == 0);
   q.scan_bytes = 0;
   q.replayed = false;
   q.want_info = p->get_docid_scoring_info != 0;
@@ -5826,7 +5888,8 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   P.real_max_top = hp.real_max_top;
   P.language = p->language;
   P.same_lang_weight = p->same_lang_weight;
-  P.site_rank_multiplier = GB_SITERANKMULTIPLIER;
+  P.site_rank_multiplier = boolean ? 0.0f : (float)GB_SITERANKMULTIPLIER;  // Posdb.cpp:774
+  P.boolean = boolean ? 1 : 0;
   P.nqt = nterms;
   P.has_serp = p->min_serp_docid != 0;  // Posdb.cpp:4379-4381
   P.max_serp_score = p->max_serp_score;
@@ -5837,7 +5900,7 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
                        ? (int32_t)p->max_serp_score
                        : INT32_MIN;
   P.clustering = clus;
-  P.use_white = p->use_whitelist != 0;
+  P.use_white = p->use_whitelist != 0 && !boolean;  // the boolean vote never reads the whitelist
   if (P.use_white) {
     rc = white_set(p, q.h_white);
     if (rc) return rc;
@@ -5911,6 +5974,7 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
       int id = dense_id(g.sub_term[x]);
       if (id < 0) return GBGPU_EUNSUPPORTED;
       P.gsub[j][x] = (uint8_t)id;
+      P.bool_gmask[id] |= (uint16_t)(1u << j);
       if (rmode) {
         if (P.lists[id].uses) return GBGPU_EUNSUPPORTED;  // shared with another group
         P.lists[id].rmode = rmode;
@@ -5933,19 +5997,30 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
       }
     }
   }
-  // candidate arrays: distinct lists of the smallest group, in sublist order
-  const GroupInfo &g0 = hp.g[hp.min_listi];
+  // candidate arrays: distinct lists of the smallest group, in sublist order;
+  // for a boolean query every distinct list (the docid set is their union:
+  // a docid's slot is in the first array holding it, its other arrays'
+  // slots get no list bit and die)
   P.g0n = 0;
   uint64_t slot = 0;
-  for (int x = 0; x < g0.nsub; x++) {
-    int id = dense[g0.sub_term[x]];
-    if (P.lists[id].g0_array >= 0) continue;
+  auto add_array = [&](int id) -> int {
+    if (P.lists[id].g0_array >= 0) return 0;
     if (P.g0n >= MAXG0) return GBGPU_EUNSUPPORTED;
     P.lists[id].g0_array = P.g0n;
     P.g0list[P.g0n] = id;
     P.g0base[P.g0n] = slot;
     slot += P.lists[id].units / 2 + 1;
     P.g0n++;
+    return 0;
+  };
+  if (boolean) {
+    P.reshare_mask = 0;  // no mini merge: no re-shrunk copies
+    for (int id = 0; id < P.nlists; id++)
+      if ((rc = add_array(id))) return rc;
+  } else {
+    const GroupInfo &g0 = hp.g[hp.min_listi];
+    for (int x = 0; x < g0.nsub; x++)
+      if ((rc = add_array(dense[g0.sub_term[x]]))) return rc;
   }
   P.g0base[P.g0n] = slot;
   const uint64_t slot_ub = slot;
@@ -6050,7 +6125,9 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   const size_t o_chunks = align256(sizeof(DevPlan));
   const size_t o_afirst = o_chunks + align256(sizeof(G0Chunk) * q.g0c.size());
   const size_t o_work = o_afirst + align256(4 * MAXG0);
-  const size_t tbytes = o_work + align256(sizeof(ProbeWork) * q.pw.size());
+  const size_t o_btab = o_work + align256(sizeof(ProbeWork) * q.pw.size());
+  const size_t btab_bytes = boolean ? ((size_t)1 << hp.ngroups) / 8 + 8 : 0;
+  const size_t tbytes = o_btab + align256(btab_bytes);
   q.res_bytes = res_size(k);
   int rc2 = 0;
   rc2 |= q.tables.ensure(tbytes);
@@ -6095,6 +6172,7 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
     q.epoch = 0;
   }
   P.epoch = ++q.epoch;
+  if (boolean) P.bool_table = q.tables.as<uint8_t>(o_btab);
   if (tbytes > q.stage_cap) {
     if (q.h_stage) (void)hipHostFree(q.h_stage);
     q.h_stage = nullptr;
@@ -6115,6 +6193,10 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   std::memcpy(q.h_stage + o_chunks, q.g0c.data(), sizeof(G0Chunk) * q.g0c.size());
   std::memcpy(q.h_stage + o_afirst, q.afirst.data(), 4 * MAXG0);
   std::memcpy(q.h_stage + o_work, q.pw.data(), sizeof(ProbeWork) * q.pw.size());
+  if (boolean) {
+    std::memset(q.h_stage + o_btab, 0, btab_bytes);
+    std::memcpy(q.h_stage + o_btab, p->bool_table, ((size_t)1 << hp.ngroups) / 8 ? ((size_t)1 << hp.ngroups) / 8 : 1);
+  }
 
   hipStream_t st = q.stream;
   if (ctx->profiling) HIPCHECK(hipEventRecord(q.ev[0], st));
@@ -6173,7 +6255,7 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   int maxsub = 0;
   for (int j = 0; j < hp.ngroups; j++)
     if (!(P.gflags0[j] & BF_NEGATIVE)) maxsub = std::max(maxsub, (int)P.gnsub[j]);
-  const int variant = (hp.ngroups <= 2 && maxsub <= 2)   ? 4
+  const int variant = (boolean || (hp.ngroups <= 2 && maxsub <= 2)) ? 4  // boolean: no records scored
                       : (hp.ngroups <= 2 && maxsub <= 4) ? 0
                       : (hp.ngroups <= 4 && maxsub <= 4) ? 1
                       : (hp.ngroups <= 8 && maxsub <= 4) ? 2

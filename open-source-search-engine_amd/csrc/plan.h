@@ -158,6 +158,13 @@ struct DevPlan {
   uint32_t group_lists[MAXG];  // bit l: list l is a sublist of group g
   uint32_t neg_lists;          // bit l: list l is a sublist of a negative group
   uint8_t list_mult[MAXL];     // positive groups list l is a sublist of (its runs' record copies)
+  // boolean queries (makeDocIdVoteBufForBoolQuery_r, Posdb.cpp:8006-8249):
+  // every distinct list is a candidate array (their union is the docid set),
+  // a docid's QueryTermInfo bit vector is the OR of its lists' group masks,
+  // and it survives where the truth table has that vector's bit
+  int boolean;
+  uint16_t bool_gmask[MAXL];   // bit g: list l is a sublist of group g (negative groups too)
+  const uint8_t *bool_table;   // 2^ngroups bits (the staging buffer's tail)
   uint64_t dbg_doc;            // diagnostic (GBGPU_PROBE_DEBUG_DOC): k_probe traces this docid's runs
   unsigned long long *dbg_buf; // into this buffer: a count, then 16-word records
   DevList lists[MAXL];

@@ -62,6 +62,9 @@ class Params(ctypes.Structure):
         ("use_whitelist", ctypes.c_int32),
         ("n_white_lists", ctypes.c_int32),
         ("white_lists", ctypes.c_void_p),
+        ("is_boolean", ctypes.c_int32),
+        ("bool_ngroups", ctypes.c_int32),
+        ("bool_table", ctypes.c_void_p),
     ]
 
     def with_whitelist(self, lists):
@@ -77,6 +80,28 @@ class Params(ctypes.Structure):
         q.n_white_lists = len(lists)
         q.white_lists = ctypes.cast(arr, ctypes.c_void_p) if lists else None
         q._white = [bytes(l) for l in lists]
+        for a in ("_btok", "_btable", "_bkeep"):
+            if hasattr(self, a):
+                setattr(q, a, getattr(self, a))
+        return q
+
+    def with_boolean(self, table: bytes, ngroups: int, tokens=None):
+        """A copy of these params for a boolean query: the expression's truth
+        table over the plan's QueryTermInfo bit vectors (bit v = byte v >> 3,
+        bit v & 7), and -- for the reference harness only -- the expression
+        tokens it is built from (ref_binding: operand term >= 0, OP_OR -1,
+        OP_AND -2, OP_NOT -3, '(' -4, ')' -5)."""
+        q = Params.from_buffer_copy(self)
+        for a in ("_keep", "_white"):
+            if hasattr(self, a):
+                setattr(q, a, getattr(self, a))
+        table = bytes(table)
+        q._bkeep = ctypes.create_string_buffer(table, max(1, len(table)))
+        q.is_boolean = 1
+        q.bool_ngroups = int(ngroups)
+        q.bool_table = ctypes.cast(q._bkeep, ctypes.c_void_p)
+        q._btable = table
+        q._btok = list(tokens) if tokens is not None else getattr(self, "_btok", None)
         return q
 
 

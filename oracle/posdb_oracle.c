@@ -1308,10 +1308,12 @@ typedef struct {
   int64_t minListSize;
   int minListi;
   VoteBuf vb;
+  int64_t grand;      /* the positive groups' list bytes (m_docIdVoteBuf's boolean size) */
+  uint32_t *bvec;     /* boolean: each vote-buffer docid's QueryTermInfo bit vector (m_bt) */
 } Prep;
 
 static int prepare(const orc_qterm *qt, const uint8_t *const *lists, const int64_t *sizes, int nqt,
-                   Prep *P) {
+                   Prep *P, int boolean) {
   memset(P, 0, sizeof *P);
   P->lists = (OList *)calloc(nqt > 0 ? nqt : 1, sizeof(OList));
   P->alloc = (uint8_t **)calloc(nqt > 0 ? nqt : 1, sizeof(uint8_t *));
@@ -1329,6 +1331,10 @@ static int prepare(const orc_qterm *qt, const uint8_t *const *lists, const int64
   }
   int rc = setQueryTermInfo(qt, nqt, P->lists, P->qip, &P->nrg, &P->minListSize, &P->minListi);
   if (rc) return rc;
+  /* Posdb.cpp:4813-4826: grand = the positive groups' sizes; a boolean
+   * query's vote buffer may hold every one of their docids */
+  for (int i = 0; i < P->nrg; i++)
+    if (!(P->qip[i].bigramFlags[0] & BF_NEGATIVE)) P->grand += P->qip[i].totalSubListsSize;
   /* first-key swap, Posdb.cpp:5671-5703 */
   for (int k = 0; k < nqt; k++) {
     OList *l = &P->lists[k];
@@ -1344,6 +1350,12 @@ static int prepare(const orc_qterm *qt, const uint8_t *const *lists, const int64
     l->list = p;
   }
   int64_t need = (P->minListSize / 12) * 6 + 8;
+  if (boolean) {
+    /* Posdb.cpp:4826: grand -- but the union runs over every group, negative
+     * ones included (Posdb.cpp:8026-8153), so size for all lists here */
+    need = 8;
+    for (int i = 0; i < nqt; i++) need += P->lists[i].size + 6;
+  }
   P->vb.buf = (uint8_t *)calloc(1, (size_t)need + 16);
   if (!P->vb.buf) return ENOMEM;
   return 0;
@@ -1351,6 +1363,7 @@ static int prepare(const orc_qterm *qt, const uint8_t *const *lists, const int64
 
 static void unprepare(Prep *P, int nqt) {
   free(P->vb.buf);
+  free(P->bvec);
   free(P->qip);
   if (P->lists) free_lists(P->lists, P->alloc, nqt);
 }
@@ -1374,16 +1387,102 @@ static void votes(Prep *P, const WhiteSet *ws) {
   }
 }
 
+/* makeDocIdVoteBufForBoolQuery_r, Posdb.cpp:8006-8249: every group's
+ * sublists (negative groups too) are walked run by run; a docid takes the bit
+ * of each QueryTermInfo it occurs in (QueryTerm::m_bitNum = the group index,
+ * Posdb.cpp:4485-4721) -- a range term's run only if one of its keys is in
+ * range (isInRange, 8087-8129) -- and is voted if the expression holds for
+ * its bit vector (the truth table stands for m_ct / Query::matchesBoolQuery,
+ * 8164-8231).  The vote buffer is sorted by docid (dcmp6, 8237-8244); bvec
+ * keeps each voted docid's vector (m_bt) for the score (Posdb.cpp:6514-6534). */
+typedef struct {
+  uint64_t d;
+  uint32_t bits;
+} BEnt;
+static int bent_cmp(const void *a, const void *b) {
+  const uint64_t x = ((const BEnt *)a)->d, y = ((const BEnt *)b)->d;
+  return x < y ? -1 : x > y ? 1 : 0;
+}
+static int boolVotes(Prep *P, const orc_params *prm) {
+  QTI *qip = P->qip;
+  int64_t cap = 16, n = 0;
+  BEnt *e = (BEnt *)malloc(sizeof(BEnt) * cap);
+  if (!e) return ENOMEM;
+  for (int i = 0; i < P->nrg; i++) {
+    QTI *qti = &qip[i];
+    const int isRange = isRangeField(qti->fieldCode);
+    const uint32_t mask = 1u << i;
+    for (int j = 0; j < qti->numSubLists; j++) {
+      const OList *L = &P->lists[qti->subList[j]];
+      const uint8_t *p = L->list, *pend = L->list + L->size;
+      while (p < pend) {
+        const uint64_t d = getDocId(p);
+        int inRange = 0;
+        if (isRange && isInRange(p, qti)) inRange = 1;
+        if (p[0] & 0x02) p += 12;
+        else p += 18;
+        while (p < pend && (p[0] & 0x04)) {
+          if (isRange && isInRange(p, qti)) inRange = 1;
+          p += 6;
+        }
+        if (isRange && !inRange) continue;
+        if (n == cap) {
+          cap *= 2;
+          BEnt *ne = (BEnt *)realloc(e, sizeof(BEnt) * cap);
+          if (!ne) { free(e); return ENOMEM; }
+          e = ne;
+        }
+        e[n].d = d;
+        e[n].bits = mask;
+        n++;
+      }
+    }
+  }
+  qsort(e, (size_t)n, sizeof(BEnt), bent_cmp);
+  P->bvec = (uint32_t *)malloc(sizeof(uint32_t) * (size_t)(n ? n : 1));
+  if (!P->bvec) { free(e); return ENOMEM; }
+  int64_t nv = 0;
+  uint8_t *dst = P->vb.buf;
+  for (int64_t a = 0; a < n;) {
+    int64_t b = a;
+    uint32_t v = 0;
+    while (b < n && e[b].d == e[a].d) v |= e[b++].bits;
+    if (prm->bool_table[v >> 3] >> (v & 7) & 1) {
+      const uint64_t x = e[a].d << 2; /* a 6-byte record: docid << 2 (Posdb.cpp:8196-8209) */
+      for (int k = 0; k < 6; k++) dst[k] = (uint8_t)(x >> (8 * k));
+      dst += 6;
+      P->bvec[nv++] = v;
+    }
+    a = b;
+  }
+  P->vb.len = dst - P->vb.buf;
+  free(e);
+  return 0;
+}
+
 int64_t orc_intersect(const orc_qterm *qt, const uint8_t *const *lists, const int64_t *sizes,
                       int nqt, int64_t *docids, int64_t cap, const orc_params *prm) {
   initWeights();
   WhiteSet ws = {NULL, 0};
   if (prm && prm->use_whitelist && white_build(prm, &ws)) return -ENOMEM;
   Prep P;
-  int rc = prepare(qt, lists, sizes, nqt, &P);
+  const int boolean = prm && prm->is_boolean;
+  int rc = prepare(qt, lists, sizes, nqt, &P, boolean);
   if (rc) { unprepare(&P, nqt); free(ws.v); return -rc; }
   int64_t n = 0;
-  if (P.nrg > 0 && P.minListSize != 0) {
+  if (boolean && P.nrg > 0) {
+    if (prm->bool_ngroups != P.nrg || !prm->bool_table) { unprepare(&P, nqt); free(ws.v); return -EINVAL; }
+    rc = boolVotes(&P, prm);
+    if (rc) { unprepare(&P, nqt); free(ws.v); return -rc; }
+    n = P.vb.len / 6;
+    for (int64_t i = 0; i < n && i < cap; i++) {
+      const uint8_t *d = P.vb.buf + 6 * i;
+      uint64_t id = U32(d + 1);
+      id <<= 8;
+      id |= d[0];
+      docids[i] = (int64_t)(id >> 2);
+    }
+  } else if (P.nrg > 0 && P.minListSize != 0) {
     votes(&P, (prm && prm->use_whitelist) ? &ws : NULL);
     n = P.vb.len / 6;
     for (int64_t i = 0; i < n && i < cap; i++) {
@@ -1429,16 +1528,30 @@ static int64_t docs_wanted(const orc_params *p, const int64_t *sizes, int nqt) {
 static int run_range(const orc_qterm *qt, const uint8_t *const *lists, const int64_t *sizes, int nqt,
                      const orc_params *prm, const WhiteSet *ws, TTree *tree, orc_result *out) {
   Prep P;
-  int rc = prepare(qt, lists, sizes, nqt, &P);
+  const int boolean = prm->is_boolean != 0;
+  int rc = prepare(qt, lists, sizes, nqt, &P, boolean);
   if (rc) {
     unprepare(&P, nqt);
     return rc;
   }
   QTI *qip = P.qip;
   int nqti = P.nrg;
-  if (nqti == 0 || P.minListSize == 0) goto finish;
+  /* Posdb.cpp:5728-5735: a boolean query goes on with an empty smallest group */
+  if (nqti == 0 || (P.minListSize == 0 && !boolean)) goto finish;
 
-  votes(&P, ws);
+  if (boolean) {
+    if (prm->bool_ngroups != nqti || !prm->bool_table) {
+      unprepare(&P, nqt);
+      return EINVAL;
+    }
+    rc = boolVotes(&P, prm);
+    if (rc) {
+      unprepare(&P, nqt);
+      return rc;
+    }
+  } else {
+    votes(&P, ws);
+  }
   out->hits = P.vb.len / 6;
   for (int i = 0; i < nqti; i++) {
     if (qip[i].bigramFlags[0] & BF_NEGATIVE) continue;
@@ -1476,7 +1589,7 @@ static int run_range(const orc_qterm *qt, const uint8_t *const *lists, const int
     pt.bflags = bflags;
     pt.windowTermPtrs = winnerStack;
     pt.nqt = nqt;
-    float siteRankMultiplier = SITERANKMULTIPLIER;
+    float siteRankMultiplier = boolean ? 0.0f : SITERANKMULTIPLIER; /* Posdb.cpp:774 */
     char siteRank = 0, docLang = 0;
     float minWinningScore = -1.0; /* Posdb.cpp:6012: per pass */
     int sortByF = -1, sortByI = -1; /* m_sortByTermInfoNum(Int), Posdb.cpp:4413-4425 */
@@ -1502,6 +1615,7 @@ static int run_range(const orc_qterm *qt, const uint8_t *const *lists, const int
     uint8_t *docIdEnd = P.vb.buf + P.vb.len;
 
     for (uint8_t *docIdPtr = P.vb.buf; docIdPtr < docIdEnd; docIdPtr += 6) {
+      float minScore = 999999999.0;
       /* cursor pre-advance, Posdb.cpp:6252-6310 */
       for (int i = 0; i < nqti; i++) {
         QTI *qti = &qip[i];
@@ -1527,6 +1641,20 @@ static int run_range(const orc_qterm *qt, const uint8_t *const *lists, const int
       /* the max-score and ring-buffer prefilters, Posdb.cpp:6322-6504 (live
        * only once the TopTree holds more than docsWanted nodes, i.e. with
        * site clustering: minWinningScore is -1 until then) */
+      /* a boolean query: no prefilter, no mini merge that shows, no scorers --
+       * minScore is the number of bits of the docid's vector and siteRank /
+       * docLang keep their initial 0 (Posdb.cpp:5984-5985, 6312-6316,
+       * 6514-6534, 6833-6834 -> boolJump2 at 7247) */
+      if (boolean) {
+        uint64_t d = U32(docIdPtr + 1);
+        d <<= 8;
+        d |= docIdPtr[0];
+        pt.docId = d >> 2;
+        minScore = (float)__builtin_popcount(P.bvec[(docIdPtr - P.vb.buf) / 6]);
+        siteRank = 0;
+        docLang = 0;
+        goto boolJump2;
+      }
       /* gbsortby: both prefilters off (Posdb.cpp:6050-6051, 6350-6351) */
       if (sortByF < 0 && sortByI < 0 &&
           prefilter_skip(&mc, qip, nqti, P.minListi, prm->do_max_score_algo, minWinningScore, ringBuf,
@@ -1747,10 +1875,10 @@ static int run_range(const orc_qterm *qt, const uint8_t *const *lists, const int
       }
 
       /* final score, Posdb.cpp:7228-7257 */
-      float minScore = 999999999.0;
       if (minPairScore < minScore && minPairScore >= 0.0) minScore = minPairScore;
       if (minSingleScore < minScore) minScore = minSingleScore;
       if (minScore <= 0.0) continue;
+    boolJump2:;
       float score = minScore * (((float)siteRank) * siteRankMultiplier + 1.0);
       if (prm->language == 0 || docLang == 0 || prm->language == docLang)
         score *= prm->same_lang_weight;
@@ -1843,6 +1971,11 @@ int orc_query(const orc_qterm *qt, const uint8_t *const *lists, const int64_t *s
     const int fc = qt[i].field_code;
     if ((fc == F_SORTBYINT || fc == F_REVSORTBYINT) && qt[i].is_required) intMode = 1;
     if (fc == F_FACETSTR || fc == F_FACETINT || fc == F_FACETFLOAT) return ENOTSUP; /* facets: DESIGN.md */
+    /* a boolean query's gbsortby score reads a mini-merged list that may be
+       the next group's or stale bytes (Posdb.cpp:7263-7279): not restated */
+    if (prm->is_boolean && (fc == F_SORTBYFLOAT || fc == F_REVSORTBYFLOAT || fc == F_SORTBYINT ||
+                            fc == F_REVSORTBYINT))
+      return ENOTSUP;
   }
   initWeights();
 

@@ -56,6 +56,12 @@ typedef struct orc_params {
   int32_t use_whitelist;
   int32_t n_white_lists;
   const struct orc_list *white_lists;
+  /* boolean queries (makeDocIdVoteBufForBoolQuery_r, Posdb.cpp:8006-8249):
+   * the expression as its truth table over QueryTermInfo bit vectors
+   * (bit v = Query::matchesBoolQuery(v)), as gbgpu_params carries it */
+  int32_t is_boolean;
+  int32_t bool_ngroups;
+  const uint8_t *bool_table;
 } orc_params;
 
 typedef struct orc_list {

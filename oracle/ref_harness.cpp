@@ -116,6 +116,16 @@ static void ref_init() {
 enum { MAXT = 64 };
 
 static PosdbTable *s_tab = NULL;       // the last query's PosdbTable
+// a boolean query's expression (Query::m_qwords as Query::set2 leaves them
+// for Expression::addExpression, Query.cpp:5424-5514): tokens >= 0 are
+// operand words naming query term t (QueryWord::m_queryWordTerm), negative
+// ones the opcodes OP_OR -1, OP_AND -2, OP_NOT -3, OP_LEFTPAREN -4,
+// OP_RIGHTPAREN -5; none = not boolean
+static std::vector<int32_t> s_btok;
+// the last query's truth table over its QueryTermInfo bit vectors:
+// Query::matchesBoolQuery for every vector (bit v at byte v >> 3, bit v & 7)
+static std::vector<uint8_t> s_btable;
+static int32_t s_bgroups = -1;
 static std::vector<int32_t> s_plan;    // the last query's QueryTermInfos (op 4)
 static int32_t s_used_nodes = 0;       // the last query's TopTree::m_numUsedNodes
 static std::vector<int32_t> s_ints;    // its nodes' m_intScore, high -> low
@@ -166,7 +176,33 @@ static int ref_query(const orc_qterm *terms, const uint8_t *const *lists, const 
   }
   q.m_qterms = qts;
   q.m_numTerms = nterms;
-  q.m_isBoolean = false;
+  q.m_isBoolean = !s_btok.empty();
+  static QueryWord bws[256];
+  static char s_alpha[] = "x", s_op[] = "(";
+  if (q.m_isBoolean) {
+    const int nw = (int)s_btok.size();
+    if (nw > 256) return EINVAL;
+    memset((void *)bws, 0, sizeof(bws));
+    for (int i = 0; i < nw; i++) {
+      const int32_t t = s_btok[i];
+      QueryWord *w = &bws[i];
+      if (t >= 0) {
+        if (t >= nterms) return EINVAL;
+        w->m_word = s_alpha;  // isAlphaWord() (Query.h:269)
+        w->m_wordLen = 1;
+        w->m_queryWordTerm = &qts[t];
+      } else {
+        w->m_word = s_op;
+        w->m_wordLen = 1;
+        w->m_opcode = (char)(t == -1 ? OP_OR : t == -2 ? OP_AND : t == -3 ? OP_NOT : t == -4 ? OP_LEFTPAREN
+                                                                                           : OP_RIGHTPAREN);
+      }
+    }
+    q.m_qwords = bws;
+    q.m_numWords = nw;
+    q.m_numExpressions = 1;
+    if (!q.m_expressions[0].addExpression(0, nw, &q, 0)) return EINVAL;
+  }
 
   msg2.m_query = &q;
   msg2.m_lists = rl;
@@ -303,6 +339,23 @@ static int ref_query(const orc_qterm *terms, const uint8_t *const *lists, const 
     out->filtered += tab->m_filtered;
     if (tab->m_errno) out->corrupt = tab->m_errno;
   } while (ddd < dddEnd);
+  // a boolean query's truth table, by the reference's own evaluator over
+  // every bit vector of its QueryTermInfos (m_bitNum, Posdb.cpp:4485-4721)
+  s_btable.clear();
+  s_bgroups = -1;
+  if (q.m_isBoolean && tab) {
+    const int32_t ng = tab->m_numQueryTermInfos;
+    if (ng >= 0 && ng <= 16) {
+      s_bgroups = ng;
+      const int32_t nv = 1 << ng;
+      s_btable.assign((nv + 7) / 8, 0);
+      const int32_t vs = ng / 8 + (ng % 8 ? 1 : 0);
+      for (int32_t v = 0; v < nv; v++) {
+        unsigned char vec[4] = {(unsigned char)v, (unsigned char)(v >> 8), 0, 0};
+        if (q.matchesBoolQuery(vec, vs > 0 ? vs : 1)) s_btable[v >> 3] |= (uint8_t)(1u << (v & 7));
+      }
+    }
+  }
   // allocTopTree returns before setNumNodes when every list is empty
   // (Posdb.cpp:889-890): no tree, reported as 0 like the oracle
   out->docs_wanted = tree.m_numNodes > 0 ? tree.m_docsWanted : 0;
@@ -598,6 +651,11 @@ int main(int argc, char **argv) {
       }
       p.n_white_lists = nw;
       p.white_lists = nw ? wl.data() : NULL;
+      int32_t ntok;
+      rd(&ntok, 4);  // the boolean expression (s_btok), 0: not boolean
+      if (ntok < 0 || ntok > 256) return 4;
+      s_btok.resize(ntok);
+      rd(s_btok.data(), 4 * (size_t)ntok);
       std::vector<int64_t> d(cap > 0 ? cap : 1);
       std::vector<float> s(cap > 0 ? cap : 1);
       int64_t vcap = 0;
@@ -631,6 +689,9 @@ int main(int argc, char **argv) {
         wr(&nb, 8);
         wr(s_info[b].data(), (size_t)nb);
       }
+      // the boolean truth table (i32 groups, -1 none; then its bytes)
+      wr(&s_bgroups, 4);
+      if (s_bgroups >= 0) wr(s_btable.data(), s_btable.size());
       if (op == 7) {
         // the shard's reply merged by the reference's own Msg3a::mergeLists
         // (one shard: the TopTree's first docsToGet as Msg39 sends them,

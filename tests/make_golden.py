@@ -43,6 +43,8 @@ def save_query(name, terms, lists, params, prefix="q"):
         # the vote buffer of one whole-range pass: the exact intersection
         p1 = gbgpu.Params.from_buffer_copy(params)  # (keeps white_lists' pointer; its buffers live in params)
         p1.num_docid_splits = 1
+        if getattr(params, "_btok", None):
+            p1 = p1.with_boolean(params._btable or b"", params.bool_ngroups, params._btok)
         r["votes"] = ref.query(terms, lists, p1, votes=True, white=white)["votes"]
     sizes, blob = pack_lists(lists)
     qt = np.array([[getattr(t, f) for f in QFIELDS] for t in terms], np.int32).reshape(len(terms), len(QFIELDS))
@@ -55,7 +57,13 @@ def save_query(name, terms, lists, params, prefix="q"):
     pr = np.array([params.docs_to_get, params.real_max_top, params.language, params.site_clustering,
                    params.num_docid_splits, params.do_max_score_algo], np.int32)
     extra = {}
-    if params.get_docid_scoring_info:
+    if getattr(params, "_btok", None):
+        # a boolean query: its expression (the harness builds the Query's
+        # QueryWords from it) and the truth table the reference's own
+        # Query::matchesBoolQuery gives over the plan's QueryTermInfo vectors
+        extra["bool_tok"] = np.array(params._btok, np.int32)
+        extra["bool_groups"] = np.int32(r["bool_groups"])
+        extra["bool_table"] = np.frombuffer(r["bool_table"], np.uint8)
         # the three SafeBufs of the second pass, as the reference left them
         for k in ("score_info", "pair_scores", "single_scores"):
             extra[k] = np.frombuffer(r[k], np.uint8)
@@ -435,6 +443,62 @@ def save_paging():
             print(f"  serp {q.name} clus={clus}: n={len(r['docids'])} filtered={r['filtered']}")
 
 
+# boolean queries (makeDocIdVoteBufForBoolQuery_r, Posdb.cpp:8006-8249):
+# expressions as QueryWord tokens -- operand = query-term index, OP_OR -1,
+# OP_AND -2, OP_NOT -3, '(' -4, ')' -5 (Query.h:181-188)
+BOOL_EXPRS = {
+    "and_or": [0, -2, -4, 1, -1, 2, -5],            # a AND (b OR c)
+    "or": [0, -1, 1],                               # a OR b (c required, not in the expression)
+    "not": [-3, 0, -2, 1],                          # NOT a AND b
+    "and_not_group": [0, -2, -3, -4, 1, -1, 2, -5],  # a AND NOT (b OR c)
+    "or_or": [0, -1, 1, -1, 2],                     # a OR b OR c
+    "pairs": [-4, 0, -1, 1, -5, -2, -4, 1, -1, 2, -5],  # (a OR b) AND (b OR c)
+}
+
+
+def bool_params(p, toks):
+    return p.with_boolean(b"", 0, toks)
+
+
+def save_boolean():
+    N = 6000
+    for seed in (1, 2):
+        q = qkinds.kinds(N, seed=seed)[1]  # three_word: words a b c, bigrams ab bc
+        lists = generate(q, N, seed=3000 + seed)
+        for name, toks in BOOL_EXPRS.items():
+            r = save_query(f"bool_{name}_s{seed}", q.terms, lists, bool_params(q.params(), toks))
+            print(f"q_bool_{name}_s{seed}: hits={r['hits']} n={len(r['docids'])} table={r['bool_table'].hex()}")
+    q = qkinds.kinds(N, seed=3)[1]
+    lists = generate(q, N, seed=3100)
+    toks = BOOL_EXPRS["and_or"]
+    # the request modes around it: site clustering, docid splits, paging,
+    # a language (docLang stays 0 on the boolean path: always the weight),
+    # a whitelist (the boolean vote never reads it)
+    save_query("bool_clus", q.terms, lists, bool_params(q.params(site_clustering=1), toks))
+    save_query("bool_splits2", q.terms, lists, bool_params(q.params(num_docid_splits=2), toks))
+    save_query("bool_clus_splits5", q.terms, lists, bool_params(q.params(site_clustering=1, num_docid_splits=5),
+                                                                   BOOL_EXPRS["or_or"]))
+    full = ref.query(q.terms, lists, bool_params(q.params(), toks))
+    pos = min(40, len(full["docids"]) - 1)
+    save_query("bool_serp", q.terms, lists, bool_params(q.params(max_serp_score=float(full["scores"][pos]),
+                                                                 min_serp_docid=int(full["docids"][pos])), toks))
+    save_query("bool_lang", q.terms, lists, bool_params(q.params(language=3, same_lang_weight=7.5), toks))
+    wl = [lists[0][:600]]
+    save_query("bool_white", q.terms, lists, bool_params(q.params().with_whitelist(wl), toks))
+    # a negative term: its group's bit is in every vector (and in the score)
+    q = qkinds.kinds(N, seed=4)[3]  # negative: a b -c
+    lists = generate(q, N, seed=3200)
+    save_query("bool_negative", q.terms, lists, bool_params(q.params(), [0, -1, 1]))
+    # the smallest group empty: a boolean query still runs (Posdb.cpp:5735)
+    q = qkinds.kinds(N, seed=5)[1]
+    lists = generate(q, N, seed=3300)
+    save_query("bool_empty_a", q.terms, [b""] + list(lists[1:]), bool_params(q.params(), BOOL_EXPRS["or_or"]))
+    # synonyms: a word's synonym list is its group's sublist
+    q = qkinds.kinds(N, seed=6)[4]  # car (+synonym) cheap
+    lists = generate(q, N, seed=3400)
+    save_query("bool_synonyms", q.terms, lists, bool_params(q.params(), [-3, 0, -1, 1]))
+
+
 def save_merge(name, runs, cases):
     sizes, blob = pack_lists(runs)
     outs, osz, rms, mrss = [], [], [], []
@@ -468,6 +532,9 @@ def main():
     if not ref.available():
         sys.exit("oracle/_ref/gbref missing: run `make -f oracle/ref.mk` where /root/reference exists")
     os.makedirs(OUT, exist_ok=True)
+    if len(sys.argv) > 1:  # one family only, e.g. `make_golden.py boolean`
+        globals()["save_" + sys.argv[1]]()
+        return
     N = 6000
     for seed in (1, 2):
         for q in qkinds.kinds(N, seed=seed):
@@ -503,6 +570,7 @@ def main():
     save_sortby()
     save_sortby_int_modes()
     save_range()
+    save_boolean()
     save_msg3a()
     cases = [(0, -1), (1, -1), (0, 5000), (1, 5000), (0, 1)]
     for seed, (keys, nterms) in enumerate([(4000, 50), (12000, 3), (8000, 1)]):

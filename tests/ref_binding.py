@@ -85,6 +85,9 @@ def query(terms, lists, params, cap=4096, votes=False, reps=1, white=None, mode=
     for l in white:
         req.append(struct.pack("<q", len(l)))
         req.append(bytes(l))
+    btok = list(getattr(params, "_btok", None) or [])  # a boolean query's expression
+    req.append(struct.pack("<i", len(btok)))
+    req.append(np.asarray(btok, np.int32).tobytes())
     p.stdin.write(b"".join(req))
     p.stdin.flush()
     r = OrcResult.from_buffer_copy(rd(ctypes.sizeof(OrcResult)))
@@ -97,9 +100,11 @@ def query(terms, lists, params, cap=4096, votes=False, reps=1, white=None, mode=
     for _ in range(3):  # m_scoreInfoBuf, m_pairScoreBuf, m_singleScoreBuf
         (nb,) = struct.unpack("<q", rd(8))
         info.append(rd(nb) if nb else b"")
+    (bng,) = struct.unpack("<i", rd(4))
+    btable = rd(((1 << bng) + 7) // 8) if bng >= 0 else None
     out = dict(docids=d, scores=s, hits=r.hits, filtered=r.filtered, docs_wanted=r.docs_wanted,
                corrupt=r.corrupt, votes=v, seconds=sec, score_info=info[0], pair_scores=info[1],
-               single_scores=info[2])
+               single_scores=info[2], bool_groups=bng, bool_table=btable)
     if op == 7:
         (no,) = struct.unpack("<i", rd(4))
         if no < 0:

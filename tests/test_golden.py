@@ -44,6 +44,8 @@ def load_query(path):
                           int(z["min_serp_docid"]) if "min_serp_docid" in z else 0)
     if "use_whitelist" in z and int(z["use_whitelist"]):
         params = params.with_whitelist(split_blob(z["white_sizes"], z["white_blob"]))
+    if "bool_tok" in z:  # a boolean query: its expression and the reference's truth table
+        params = params.with_boolean(z["bool_table"].tobytes(), int(z["bool_groups"]), [int(x) for x in z["bool_tok"]])
     lists = split_blob(z["list_sizes"], z["list_blob"])
     exp = dict(docids=z["docids"], scores=z["score_bits"].view(np.float32), hits=int(z["hits"]),
                docs_wanted=int(z["docs_wanted"]), votes=z["votes"],
