@@ -15,6 +15,8 @@
  *   RdbList::posdbMerge_r       RdbList.cpp:3065-3568  gbgpu_merge_posdb
  *   Msg3::readList -> RdbScan   Msg3.cpp:553-731,       gbgpu_file_upload /
  *     (a Posdb file read)       RdbScan.cpp:319-361    gbgpu_file_list (in HBM)
+ *   Msg5::mergeLists_r          Msg5.cpp:1415-1471,    gbgpu_termlist_merge (the
+ *     (files + tree, merge_r)   1621-1795             pieces merged in HBM)
  *
  * Conventions: plain pointers and sizes only; the caller owns
  * every input and output buffer and they are never mutated; the library owns
@@ -254,6 +256,33 @@ int gbgpu_file_upload(gbgpu_ctx *ctx, const uint8_t *bytes, int64_t size, int32_
 int gbgpu_file_list(gbgpu_ctx *ctx, int32_t file, int64_t offset, int64_t size, const uint8_t *key18,
                     int32_t *handle);
 int gbgpu_file_free(gbgpu_ctx *ctx, int32_t file);
+
+/* Msg5's read of one termlist (Msg5.cpp:1415-1471 prepare, 1621-1795
+ * mergeLists_r): the termlist's range from every Posdb file (Msg3's reads,
+ * oldest file first) and the in-memory tree's list (newest, last) merged by
+ * RdbList::merge_r's posdb rules (gbgpu_merge_posdb: newest equal key wins,
+ * remove_neg_keys drops surviving delete keys -- Msg2 reads queries with it
+ * on -- and the min_rec_sizes bound) into ONE resident list, the handle a
+ * gbgpu_list_upload list would be (the same checks; free with
+ * gbgpu_list_free).  A file piece is a byte range of a resident file image
+ * with its map key when the range starts at a compressed key, as
+ * gbgpu_file_list takes it; a host piece (file < 0) is a list in host memory
+ * whose first key is 18 bytes (the tree's list, RdbTree::getList).  Every
+ * piece stays in HBM: the file cuts are device copies, the merge runs on the
+ * device.  RdbList::constrain's trim to the exact start/end keys stays with
+ * the caller (the ranges passed are the ones it keeps).  When merged_out is
+ * not NULL the merged list's bytes are also copied there (merged_cap bytes;
+ * ENOSPC if they do not fit) with their size in *merged_size.  Synchronous. */
+typedef struct gbgpu_piece {
+  int32_t file;          /* resident file handle, or -1: `bytes` in host memory */
+  int32_t pad;
+  int64_t offset, size;  /* the byte range (of the file, or of `bytes`)          */
+  const uint8_t *key18;  /* the map key at `offset` when it is compressed, or NULL */
+  const uint8_t *bytes;  /* file < 0: the host list                               */
+} gbgpu_piece;
+int gbgpu_termlist_merge(gbgpu_ctx *ctx, const gbgpu_piece *pieces, int n, int remove_neg_keys,
+                         int64_t min_rec_sizes, int32_t *handle, uint8_t *merged_out, int64_t merged_cap,
+                         int64_t *merged_size);
 /* gbgpu_query and gbgpu_query_resident are re-entrant: Msg39 runs several
  * intersect threads at once (Msg39.cpp:1019-1027, Parms.cpp:12356); each call
  * takes a free query slot (its own HIP stream and buffers over the shared

@@ -52,6 +52,7 @@
 #include <memory>
 #include <mutex>
 #include <vector>
+#include <array>
 
 #include "../../include/gbgpu.h"
 #include "merge.h"
@@ -7226,6 +7227,125 @@ int gbgpu_file_list(gbgpu_ctx *ctx, int32_t fh, int64_t offset, int64_t size, co
   if (size > ks)
     HIPCHECK(hipMemcpyAsync(e.d + 12, src + ks, (size_t)(size - ks), hipMemcpyDeviceToDevice, ctx->upload_stream));
   return finish_list(ctx, e, nullptr, full, handle);
+}
+
+static gbmerge::MergeState *merge_state(gbgpu_ctx *ctx);
+
+// Msg5::mergeLists_r over resident files (Msg5.cpp:1415-1471, 1621-1795):
+// each piece becomes a merge input run in HBM starting with an 18-byte key
+// (a file cut's compressed head replaced by the map key, as RdbScan does;
+// RdbScan.cpp:319-361), the runs are merged on the device (merge.hip), and
+// the merged list becomes a resident list (first-key swap, checks, page map)
+// with device-to-device copies only.
+int gbgpu_termlist_merge(gbgpu_ctx *ctx, const gbgpu_piece *pieces, int n, int remove_neg_keys,
+                         int64_t min_rec_sizes, int32_t *handle, uint8_t *merged_out, int64_t merged_cap,
+                         int64_t *merged_size) {
+  if (!ctx || !handle || n < 0 || n > 256 || (n && !pieces)) return EINVAL;
+  if (merged_size) *merged_size = 0;
+  (void)hipSetDevice(ctx->device);
+  gbmerge::MergeState *m = merge_state(ctx);
+  if (!m) return GBGPU_EHIP;
+  std::lock_guard<std::mutex> g(ctx->lists_mu);
+  // the runs: one 16-B aligned segment each (the merge reads whole 16-byte
+  // words), in piece order (oldest first)
+  std::vector<int64_t> rsz(n), roff(n);
+  std::vector<std::array<uint8_t, 18>> head(n);
+  std::vector<const uint8_t *> src(n);  // device bytes after the first key (file pieces)
+  std::vector<int> hks(n, 18);          // bytes the piece's first key takes in its source
+  int64_t total = 0, in_bytes = 0;
+  for (int i = 0; i < n; i++) {
+    const gbgpu_piece &pc = pieces[i];
+    if (pc.offset < 0 || pc.size < 0 || pc.size % 6) return EINVAL;
+    rsz[i] = 0;
+    roff[i] = in_bytes;
+    if (!pc.size) continue;
+    if (pc.file < 0) {
+      if (!pc.bytes || pc.size < 18) return EINVAL;
+      if (pc.bytes[pc.offset] & 0x06) return EINVAL;  // merge_r: every run starts with an 18-byte key
+      std::memcpy(head[i].data(), pc.bytes + pc.offset, 18);
+      rsz[i] = pc.size;
+    } else {
+      if (pc.file >= (int32_t)ctx->files.size() || !ctx->files[pc.file].live) return EINVAL;
+      const FileEntry &f = ctx->files[pc.file];
+      if (pc.offset > f.size || pc.size > f.size - pc.offset) return EINVAL;
+      const uint8_t *d = f.mem->d + pc.offset;
+      uint8_t h[18] = {};
+      HIPCHECK(hipMemcpy(h, d, (size_t)std::min<int64_t>(18, pc.size), hipMemcpyDeviceToHost));
+      if (!(h[1] & 0x02)) return GBGPU_ECORRUPT;  // not a key start
+      const int ks = (h[0] & 0x04) ? 6 : (h[0] & 0x02) ? 12 : 18;
+      if (pc.size < ks) return GBGPU_ECORRUPT;
+      if (pc.key18) {
+        uint8_t a[18], b[18];
+        std::memcpy(a, h, ks);
+        std::memcpy(b, pc.key18, ks);
+        a[0] &= 0xf9;
+        if ((pc.key18[0] & 0x06) || std::memcmp(a, b, ks)) return EINVAL;
+        std::memcpy(head[i].data(), pc.key18, 18);
+      } else {
+        if (ks != 18) return EINVAL;
+        std::memcpy(head[i].data(), h, 18);
+      }
+      hks[i] = ks;
+      src[i] = d + ks;
+      rsz[i] = pc.size - ks + 18;
+    }
+    total += rsz[i];
+    in_bytes += (int64_t)align256((size_t)rsz[i] + 16);
+  }
+  if (total == 0) return upload_list(ctx, nullptr, 0, handle);
+  DevBuf in, out;
+  in.st = out.st = ctx->upload_stream;
+  in.pool = out.pool = ctx->pool;
+  struct Rel {  // stream-ordered frees on every return path
+    DevBuf &b;
+    ~Rel() { b.release(); }
+  } rel_in{in}, rel_out{out};
+  if (in.ensure((size_t)in_bytes + 256) || out.ensure((size_t)total + 256)) return ENOMEM;
+  std::vector<const uint8_t *> ptrs(n);
+  for (int i = 0; i < n; i++) {
+    uint8_t *dst = in.as<uint8_t>(roff[i]);
+    ptrs[i] = dst;
+    if (!rsz[i]) continue;
+    const gbgpu_piece &pc = pieces[i];
+    if (pc.file < 0) {
+      HIPCHECK(hipMemcpyAsync(dst, pc.bytes + pc.offset, (size_t)rsz[i], hipMemcpyHostToDevice, ctx->upload_stream));
+    } else {
+      HIPCHECK(hipMemcpyAsync(dst, head[i].data(), 18, hipMemcpyHostToDevice, ctx->upload_stream));
+      if (rsz[i] > 18)
+        HIPCHECK(hipMemcpyAsync(dst + 18, src[i], (size_t)(rsz[i] - 18), hipMemcpyDeviceToDevice, ctx->upload_stream));
+    }
+    // zero the run's tail to its 16-byte word (the merge reads whole words)
+    const size_t tail = align256((size_t)rsz[i] + 16) - (size_t)rsz[i];
+    HIPCHECK(hipMemsetAsync(dst + rsz[i], 0, tail, ctx->upload_stream));
+  }
+  HIPCHECK(hipStreamSynchronize(ctx->upload_stream));  // the merge runs on its own stream
+  int64_t osz = 0;
+  int rc = gbmerge::merge_device(m, ptrs.data(), rsz.data(), n, remove_neg_keys, min_rec_sizes, out.as<uint8_t>(),
+                                 (int64_t)out.cap, &osz);
+  if (rc) return rc;
+  if (merged_out || merged_size) {
+    if (merged_size) *merged_size = osz;
+    if (merged_out) {
+      if (osz > merged_cap) return ENOSPC;
+      if (osz) HIPCHECK(hipMemcpy(merged_out, out.p, (size_t)osz, hipMemcpyDeviceToHost));
+    }
+  }
+  if (!osz) return upload_list(ctx, nullptr, 0, handle);
+  uint8_t first[18];
+  HIPCHECK(hipMemcpy(first, out.p, 18, hipMemcpyDeviceToHost));
+  if (first[0] & 0x06) return GBGPU_ECORRUPT;
+  ListEntry e;
+  rc = alloc_list(ctx, osz, e);
+  if (rc) return rc;
+  uint8_t sw[12];
+  std::memcpy(sw, first, 12);
+  sw[0] |= 0x02;  // the first-key swap (Posdb.cpp:5689-5698)
+  HIPCHECK(hipMemcpyAsync(e.d, sw, 12, hipMemcpyHostToDevice, ctx->upload_stream));
+  if (osz > 18)
+    HIPCHECK(hipMemcpyAsync(e.d + 12, out.as<uint8_t>(18), (size_t)(osz - 18), hipMemcpyDeviceToDevice,
+                            ctx->upload_stream));
+  // the merge buffers are freed stream-ordered on the upload stream, after the copies
+  return finish_list(ctx, e, nullptr, first, handle);
 }
 
 int gbgpu_list_free(gbgpu_ctx *ctx, int32_t h) {

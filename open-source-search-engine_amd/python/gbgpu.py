@@ -109,6 +109,12 @@ class ListRef(ctypes.Structure):
     _fields_ = [("bytes", ctypes.c_void_p), ("size", ctypes.c_int64)]
 
 
+class Piece(ctypes.Structure):
+    """gbgpu_piece: a file range (file >= 0) or a host list (file = -1)."""
+    _fields_ = [("file", ctypes.c_int32), ("pad", ctypes.c_int32), ("offset", ctypes.c_int64),
+                ("size", ctypes.c_int64), ("key18", ctypes.c_void_p), ("bytes", ctypes.c_void_p)]
+
+
 class PairScore(ctypes.Structure):
     """gbgpu_pair_score == the reference's PairScore (Posdb.h:767-800)."""
 
@@ -222,7 +228,7 @@ EXPORTS = [
     "gbgpu_bandwidth_ceiling", "gbgpu_comm_unique_id", "gbgpu_comm_init", "gbgpu_allgather_topk",
     "gbgpu_merge_replies_device", "gbgpu_seq_open", "gbgpu_seq_enter", "gbgpu_seq_leave", "gbgpu_seq_next",
     "gbgpu_seq_close", "gbgpu_exchange_next",
-    "gbgpu_merge_posdb_device", "gbgpu_merge_timings", "gbgpu_merge_path", "gbgpu_merge_last_key", "gbgpu_merge_input_left", "gb_synth_merge_runs",
+    "gbgpu_merge_posdb_device", "gbgpu_merge_timings", "gbgpu_merge_path", "gbgpu_merge_last_key", "gbgpu_merge_input_left", "gbgpu_termlist_merge", "gb_synth_merge_runs",
     "gb_synth_lists", "gb_synth_free", "gb_synth_docid", "gb_posdb_compress", "gb_posdb_make_key",
 ]
 
@@ -256,6 +262,8 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.gbgpu_file_upload.argtypes = [vp, vp, i64, ctypes.POINTER(i32)]
     lib.gbgpu_file_list.argtypes = [vp, i32, i64, i64, vp, ctypes.POINTER(i32)]
     lib.gbgpu_file_free.argtypes = [vp, i32]
+    lib.gbgpu_termlist_merge.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, i64, ctypes.POINTER(i32), vp, i64,
+                                         ctypes.POINTER(i64)]
     lib.gbgpu_query_resident.argtypes = [vp, ctypes.POINTER(QTerm), ctypes.c_int, ctypes.POINTER(i32),
                                          ctypes.POINTER(Params), ctypes.POINTER(Result)]
     lib.gbgpu_query_resident_enqueue.argtypes = [vp, ctypes.POINTER(QTerm), ctypes.c_int,
@@ -507,6 +515,36 @@ class Engine:
             k = ctypes.create_string_buffer(bytes(key18), 18)
         _check(self.lib.gbgpu_file_list(self.ctx, fh, offset, size, k, ctypes.byref(h)), "file_list")
         return h.value
+
+    def termlist_merge(self, pieces, remove_neg_keys: bool = True, min_rec_sizes: int = -1, want_bytes=False):
+        """Msg5's read of one termlist: pieces oldest first, each (file handle,
+        offset, size, key18-or-None) or bytes (the tree's list, newest last),
+        merged on the device into a resident list.  Returns the handle, or
+        (handle, merged bytes) with want_bytes."""
+        arr = (Piece * max(1, len(pieces)))()
+        keep = []
+        total = 0
+        for i, pc in enumerate(pieces):
+            if isinstance(pc, (bytes, bytearray)):
+                b = ctypes.create_string_buffer(bytes(pc), max(1, len(pc)))
+                keep.append(b)
+                arr[i] = Piece(-1, 0, 0, len(pc), None, ctypes.cast(b, ctypes.c_void_p))
+                total += len(pc)
+            else:
+                fh, off, size, key = pc
+                kb = None
+                if key is not None:
+                    kb = ctypes.create_string_buffer(bytes(key), 18)
+                    keep.append(kb)
+                arr[i] = Piece(fh, 0, off, size, ctypes.cast(kb, ctypes.c_void_p) if kb else None, None)
+                total += size + 18
+        h = ctypes.c_int32()
+        n = ctypes.c_int64()
+        out = ctypes.create_string_buffer(max(1, total + 64)) if want_bytes else None
+        _check(self.lib.gbgpu_termlist_merge(self.ctx, arr, len(pieces), 1 if remove_neg_keys else 0, min_rec_sizes,
+                                             ctypes.byref(h), out, total + 64 if want_bytes else 0, ctypes.byref(n)),
+               "gbgpu_termlist_merge")
+        return (h.value, out.raw[:n.value]) if want_bytes else h.value
 
     def file_free(self, fh: int) -> None:
         _check(self.lib.gbgpu_file_free(self.ctx, fh), "file_free")

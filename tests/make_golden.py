@@ -499,6 +499,82 @@ def save_boolean():
     save_query("bool_synonyms", q.terms, lists, bool_params(q.params(), [-3, 0, -1, 1]))
 
 
+def split_runs(lst, nruns, rng, dup_frac=0.08, del_frac=0.04):
+    """One termlist's keys spread over nruns runs (oldest first) the way a
+    termlist lies in tiered Posdb files plus the tree: each key in one run;
+    some keys also in a newer or older run with the delete bit possibly
+    flipped (a newer delete key removes it; an older one is overridden); some
+    keys deleted outright (a delete key in a newer run).  Each run is sorted
+    and re-compressed (RdbList::addRecord's rules)."""
+    from test_merge import key_stream
+    keys = []
+    for hi, lo, b in key_stream(lst):
+        keys.append((b & ~0x06) .to_bytes(6, "little") + lo.to_bytes(6, "little") + hi.to_bytes(6, "little"))
+    runs = [[] for _ in range(nruns)]
+    w = np.array([2.0 ** (nruns - 1 - i) for i in range(nruns)])
+    for k in keys:
+        r = int(rng.choice(nruns, p=w / w.sum()))
+        runs[r].append(k)
+        u = rng.random()
+        if u < dup_frac:
+            r2 = int(rng.integers(0, nruns))
+            if r2 != r:
+                k2 = bytes([k[0] ^ (1 if rng.random() < 0.5 else 0)]) + k[1:]
+                runs[r2].append(k2)
+        elif u < dup_frac + del_frac and r + 1 < nruns:
+            r2 = int(rng.integers(r + 1, nruns))
+            runs[r2].append(bytes([k[0] & 0xFE]) + k[1:])
+    out = []
+    for rk in runs:
+        rk.sort(key=lambda k: (k[12:18][::-1], k[6:12][::-1], (int.from_bytes(k[0:6], "little") | 7)))
+        out.append(gbgpu.compress(b"".join(rk)) if rk else b"")
+    return out
+
+
+def save_msg5():
+    """Msg5's read (Msg5.cpp:1415-1471, 1621-1795): each query term's list
+    split over three Posdb files and the tree (oldest first), the reference's
+    RdbList::merge_r with removeNegRecs (Msg2's reads) merging them, and its
+    PosdbTable on the merged lists.  Files are images of every term's range
+    back to back in termid order, as a Posdb file holds them."""
+    N = 6000
+    for j, (kind, seed, clus) in enumerate(((0, 1, 0), (1, 2, 0), (2, 3, 1), (4, 4, 0))):
+        q = qkinds.kinds(N, seed=seed)[kind]
+        lists = generate(q, N, seed=5000 + j)
+        import oracle_binding as orc
+        for attempt in range(20):
+            rng = np.random.default_rng(500 + j + 100 * attempt)
+            pieces = [split_runs(l, 4, rng) for l in lists]  # per term: file0, file1, file2, tree
+            merged = [ref.posdb_merge(pc, True, -1) for pc in pieces]
+            # a docid whose last group mini-merges empty makes the reference
+            # score stale mbuf bytes (DESIGN.md 4, undefined): such a split
+            # is not a fixture -- take the next one
+            pr = q.params(site_clustering=clus)
+            a = ref.query(q.terms, merged, pr, cap=1 << 16)
+            b = orc.query(q.terms, merged, pr, cap=1 << 16)
+            if np.array_equal(a["docids"], b["docids"]) and a["hits"] == b["hits"]:
+                break
+        # file images: terms ordered by termid (the hi key's termid bits)
+        order = sorted(range(len(lists)), key=lambda t: lists[t][12:18][::-1] if lists[t] else b"\xff" * 6)
+        fblobs, offs = [], np.zeros((len(lists), 3, 2), np.int64)
+        for f in range(3):
+            blob = b""
+            for t in order:
+                offs[t, f] = (len(blob), len(pieces[t][f]))
+                blob += pieces[t][f]
+            fblobs.append(blob)
+        tsizes, tblob = pack_lists([pc[3] for pc in pieces])
+        msizes, mblob = pack_lists(merged)
+        fsizes, fblob = pack_lists(fblobs)
+        name = f"msg5_{q.name}_{j}"
+        r = save_query(name, q.terms, merged, q.params(site_clustering=clus), prefix="r")
+        z = dict(np.load(os.path.join(OUT, f"r_{name}.npz"), allow_pickle=False))
+        z.update(file_sizes=fsizes, file_blob=fblob, file_offs=offs, tree_sizes=tsizes, tree_blob=tblob,
+                 merged_sizes=msizes, merged_blob=mblob)
+        np.savez_compressed(os.path.join(OUT, f"r_{name}.npz"), **z)
+        print(f"r_{name}: lists {[len(l) for l in lists]} merged {[len(m) for m in merged]} hits={r['hits']}")
+
+
 def save_merge(name, runs, cases):
     sizes, blob = pack_lists(runs)
     outs, osz, rms, mrss = [], [], [], []
@@ -571,6 +647,7 @@ def main():
     save_sortby_int_modes()
     save_range()
     save_boolean()
+    save_msg5()
     save_msg3a()
     cases = [(0, -1), (1, -1), (0, 5000), (1, 5000), (0, 1)]
     for seed, (keys, nterms) in enumerate([(4000, 50), (12000, 3), (8000, 1)]):

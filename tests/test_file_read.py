@@ -157,3 +157,121 @@ def test_gpu_file_list_refusals(engine):
         engine.file_free(fh)
     with pytest.raises(gbgpu.GbgpuError):
         engine.file_free(fh)  # already freed
+
+
+# --------------------------------------------------- Msg5: files + tree merged
+# tests/golden/r_msg5_*.npz (make_golden.save_msg5): every query term's list
+# spread over three Posdb files and the tree, with cross-file duplicates and
+# delete keys; the reference merged them with RdbList::merge_r (removeNegRecs,
+# as Msg2 reads for a query; Msg5.cpp:1621-1795) and ran its PosdbTable on
+# the merged lists.
+from test_golden import split_blob  # noqa: E402
+
+M5 = sorted(glob.glob(os.path.join(HERE, "golden", "r_msg5_*.npz")))
+M5_IDS = [os.path.basename(p)[2:-4] for p in M5]
+
+
+def load_msg5(path):
+    z = np.load(path, allow_pickle=False)
+    files = split_blob(z["file_sizes"], z["file_blob"])
+    tree = split_blob(z["tree_sizes"], z["tree_blob"])
+    merged = split_blob(z["merged_sizes"], z["merged_blob"])
+    return files, z["file_offs"], tree, merged
+
+
+def test_msg5_fixtures_present():
+    assert len(M5) >= 4
+
+
+@pytest.mark.parametrize("path", M5, ids=M5_IDS)
+def test_oracle_msg5_merge_vs_reference(path):
+    """the oracle's posdbMerge_r over each term's pieces (file cuts oldest
+    first, the tree last) gives the reference's merged bytes, and its
+    PosdbTable on them the reference's answer"""
+    import oracle_binding as orc
+    from test_golden import orc_merge
+    files, offs, tree, merged = load_msg5(path)
+    terms, lists, params, exp = load_query(path)
+    for t in range(len(terms)):
+        pieces = [files[f][offs[t, f, 0]:offs[t, f, 0] + offs[t, f, 1]] for f in range(3)] + [tree[t]]
+        assert orc_merge(pieces, 1, -1) == merged[t], t
+    assert lists == merged
+    r = orc.query(terms, lists, params, cap=1 << 16)
+    check(r, exp, os.path.basename(path))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("path", M5, ids=M5_IDS)
+def test_gpu_msg5_termlist_merge(engine, path):
+    """gbgpu_termlist_merge: each term's ranges cut from the three resident
+    file images and the tree's host list, merged in HBM into a resident list
+    -- byte for byte the reference's merge_r output -- then queried: the
+    reference's answer, intersected docid set included."""
+    files, offs, tree, merged = load_msg5(path)
+    terms, lists, params, exp = load_query(path)
+    fh = [engine.file_upload(f) for f in files]
+    hs = []
+    try:
+        for t in range(len(terms)):
+            pieces = [(fh[f], int(offs[t, f, 0]), int(offs[t, f, 1]), None) for f in range(3)] + [tree[t]]
+            h, mb = engine.termlist_merge(pieces, True, -1, want_bytes=True)
+            hs.append(h)
+            assert mb == merged[t], (os.path.basename(path), t)
+        r = engine.query_resident(terms, hs, params, cap=1 << 16, hit_cap=max(1, exp["hits"]))
+        check(dict(docids=r.docids, scores=r.scores, hits=r.hits, docs_wanted=r.docs_wanted, filtered=r.filtered,
+                   hit_docids=r.hit_docids), exp, os.path.basename(path))
+    finally:
+        for h in hs:
+            engine.free(h)
+        for f in fh:
+            engine.file_free(f)
+
+
+@pytest.mark.gpu
+def test_gpu_msg5_bounds_and_refusals(engine):
+    """merge_r's minRecSizes bound against the oracle; a file piece cut at a
+    compressed key takes the map key; a host piece must start with an
+    18-byte key (merge_r's rule); out-of-range cuts are refused."""
+    import gbgpu
+    from test_golden import orc_merge
+    files, offs, tree, merged = load_msg5(M5[0])
+    fh = [engine.file_upload(f) for f in files]
+    try:
+        t = 0
+        pieces = [(fh[f], int(offs[t, f, 0]), int(offs[t, f, 1]), None) for f in range(3)] + [tree[t]]
+        host = [files[f][offs[t, f, 0]:offs[t, f, 0] + offs[t, f, 1]] for f in range(3)] + [tree[t]]
+        for mrs in (1, 100, len(merged[t]) // 2):
+            h, mb = engine.termlist_merge(pieces, True, mrs, want_bytes=True)
+            engine.free(h)
+            assert mb == orc_merge_mrs(host, 1, mrs), mrs
+        # cut file 0's range after its first key: the map key restores it
+        lst = host[0]
+        st = key_starts(lst)
+        i = next(k for k in range(1, len(st)) if st[k][1] < 18)
+        off, ks = st[i]
+        key = full_key(lst, st, i)
+        p2 = [(fh[0], int(offs[t, 0, 0]) + off, len(lst) - off, key)] + pieces[1:]
+        h, mb = engine.termlist_merge(p2, True, -1, want_bytes=True)
+        engine.free(h)
+        cut = bytearray(key) + lst[off + ks:]
+        assert mb == orc_merge_mrs([bytes(cut)] + host[1:], 1, -1)
+        with pytest.raises(gbgpu.GbgpuError):  # a compressed head without its map key
+            engine.termlist_merge([(fh[0], int(offs[t, 0, 0]) + off, len(lst) - off, None)])
+        with pytest.raises(gbgpu.GbgpuError):  # past the file's end
+            engine.termlist_merge([(fh[0], len(files[0]) - 6, 12, None)])
+        with pytest.raises(gbgpu.GbgpuError):  # a host list whose first key is compressed
+            engine.termlist_merge([lst[off:]])
+    finally:
+        for f in fh:
+            engine.file_free(f)
+
+
+def orc_merge_mrs(lists, rm, mrs):
+    import ctypes
+    import oracle_binding as orc
+    keep, ptrs, sizes = orc._lists(lists)
+    cap = sum(map(len, lists)) + 64
+    out = ctypes.create_string_buffer(cap)
+    n = orc.lib().orc_posdb_merge(ptrs, sizes, len(lists), rm, mrs, out, cap)
+    assert n >= 0
+    return out.raw[:n]
