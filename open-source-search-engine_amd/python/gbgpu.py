@@ -65,7 +65,36 @@ class Params(ctypes.Structure):
         ("is_boolean", ctypes.c_int32),
         ("bool_ngroups", ctypes.c_int32),
         ("bool_table", ctypes.c_void_p),
+        ("n_facet_ranges", ctypes.c_int32),
+        ("pad_f", ctypes.c_int32),
+        ("facet_ranges", ctypes.c_void_p),
     ]
+
+    def _copy(self):
+        q = Params.from_buffer_copy(self)
+        for a in ("_keep", "_white", "_btok", "_btable", "_bkeep", "_franges", "_fkeep"):
+            if hasattr(self, a):
+                setattr(q, a, getattr(self, a))
+        return q
+
+    def with_facets(self, ranges):
+        """A copy of these params carrying gbfacetint:/gbfacetfloat: ranges:
+        [(term, A[], B[]), ...] as int32 bit patterns (floats by their bits)
+        -- QueryWord::m_facetRange{Int,Float}{A,B} (Query.h:389-393)."""
+        q = self._copy()
+        arr = (FacetRanges * max(1, len(ranges)))()
+        keep = []
+        for i, (term, a, b) in enumerate(ranges):
+            aa = (ctypes.c_int32 * max(1, len(a)))(*[int(x) for x in a])
+            bb = (ctypes.c_int32 * max(1, len(b)))(*[int(x) for x in b])
+            keep += [aa, bb]
+            arr[i] = FacetRanges(int(term), len(a), ctypes.cast(aa, ctypes.c_void_p), ctypes.cast(bb, ctypes.c_void_p))
+        keep.append(arr)
+        q._fkeep = keep
+        q.n_facet_ranges = len(ranges)
+        q.facet_ranges = ctypes.cast(arr, ctypes.c_void_p) if ranges else None
+        q._franges = [(int(t), [int(x) for x in a], [int(x) for x in b]) for t, a, b in ranges]
+        return q
 
     def with_whitelist(self, lists):
         """A copy of these params carrying the "&sites=" whitelist lists
@@ -107,6 +136,10 @@ class Params(ctypes.Structure):
 
 class ListRef(ctypes.Structure):
     _fields_ = [("bytes", ctypes.c_void_p), ("size", ctypes.c_int64)]
+
+
+class FacetRanges(ctypes.Structure):
+    _fields_ = [("term", ctypes.c_int32), ("n", ctypes.c_int32), ("a", ctypes.c_void_p), ("b", ctypes.c_void_p)]
 
 
 class Piece(ctypes.Structure):

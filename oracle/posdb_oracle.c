@@ -824,6 +824,8 @@ static int setQueryTermInfo(const orc_qterm *qt, int nqt, OList *lists, QTI *qip
       int fl = piped;
       if (qt[i].term_sign == '-') fl |= BF_NEGATIVE;
       if (isNumberField(qt[i].field_code)) fl |= BF_NUMBER; /* Posdb.cpp:4572-4594 */
+      if (qt[i].field_code == F_FACETSTR || qt[i].field_code == F_FACETINT || qt[i].field_code == F_FACETFLOAT)
+        fl |= BF_FACET; /* Posdb.cpp:4597-4602 */
       ADD(i, fl);
     }
     qti->fieldCode = qt[i].field_code;
@@ -1290,6 +1292,86 @@ static int prefilter_skip(const MaxCtx *c, QTI *qip, int nqti, int minListi, int
   return 0;
 }
 
+/* ----------------------------------------------------------------- facets */
+/* QueryTerm::m_facetHashTable (key = the facet value's 32 bits, or a range's
+ * A value) of FacetEntry (Posdb.h:401-413), per facet query term; kept over
+ * the docid-range pieces of one query (Posdb.cpp:1040, 5593) */
+typedef struct {
+  int32_t key, count, outside;
+  int64_t docid, sum;
+  int32_t max, min;
+} FEnt;
+typedef struct {
+  int live;
+  int term;
+  uint64_t docs; /* m_numDocsThatHaveFacet */
+  FEnt *e;
+  int n, cap;
+} FTable;
+#define ORC_MAXF 16
+static FTable s_ft[ORC_MAXF];
+static int s_nft = 0;
+
+static FEnt *ft_get(FTable *t, int32_t key) {
+  for (int i = 0; i < t->n; i++)
+    if (t->e[i].key == key) return &t->e[i];
+  return NULL;
+}
+static FEnt *ft_add(FTable *t, int32_t key) {
+  if (t->n == t->cap) {
+    t->cap = t->cap ? 2 * t->cap : 64;
+    t->e = (FEnt *)realloc(t->e, sizeof(FEnt) * (size_t)t->cap);
+  }
+  FEnt *f = &t->e[t->n++];
+  memset(f, 0, sizeof *f);
+  f->key = key;
+  return f;
+}
+static void ft_reset(void) {
+  for (int i = 0; i < ORC_MAXF; i++) {
+    free(s_ft[i].e);
+    memset(&s_ft[i], 0, sizeof s_ft[i]);
+  }
+  s_nft = 0;
+}
+static const orc_facet_ranges *facet_ranges_of(const orc_params *prm, int term) {
+  for (int i = 0; i < prm->n_facet_ranges; i++)
+    if (prm->facet_ranges[i].term == term) return &prm->facet_ranges[i];
+  return NULL;
+}
+static int isFacetField(int fc) { return fc == F_FACETSTR || fc == F_FACETINT || fc == F_FACETFLOAT; }
+static int cmp_fent(const void *a, const void *b) {
+  const int32_t x = ((const FEnt *)a)->key, y = ((const FEnt *)b)->key;
+  return x < y ? -1 : x > y;
+}
+int orc_last_facets(int32_t *w, int cap) {
+  int k = 0;
+  if (cap < 1) return -1;
+  w[k++] = s_nft;
+  for (int i = 0; i < s_nft; i++) {
+    FTable *t = &s_ft[i];
+    qsort(t->e, (size_t)t->n, sizeof(FEnt), cmp_fent);
+    if (k + 4 + 9 * t->n > cap) return -1;
+    w[k++] = t->term;
+    memcpy(&w[k], &t->docs, 8);
+    k += 2;
+    w[k++] = t->n;
+    for (int j = 0; j < t->n; j++) {
+      const FEnt *f = &t->e[j];
+      w[k++] = f->key;
+      w[k++] = f->count;
+      w[k++] = f->outside;
+      memcpy(&w[k], &f->docid, 8);
+      k += 2;
+      memcpy(&w[k], &f->sum, 8);
+      k += 2;
+      w[k++] = f->max;
+      w[k++] = f->min;
+    }
+  }
+  return k;
+}
+
 /* ---------------------------------------------------------------- driver */
 #define LIST_PAD 64
 
@@ -1613,6 +1695,34 @@ static int run_range(const orc_qterm *qt, const uint8_t *const *lists, const int
     uint8_t *nwp[MAX_SUBLISTS], *nwpEnd[MAX_SUBLISTS];
     char nwpFlags[MAX_SUBLISTS];
     uint8_t *docIdEnd = P.vb.buf + P.vb.len;
+    /* facet terms (allocTopTree, Posdb.cpp:1000-1067; the range buckets,
+     * 5575-5631): a table per facet query term with a non-empty list (any,
+     * over docid splits), its ranges as zeroed entries once */
+    int fgroup[ORC_MAXF], fterm[ORC_MAXF], nf = 0, hasFacet = 0;
+    for (int i = 0; i < nqt && nf < ORC_MAXF; i++) {
+      if (!isFacetField(qt[i].field_code)) continue;
+      if (sizes[i] == 0 && prm->num_docid_splits <= 1) continue;
+      int g = -1;
+      for (int k = 0; k < nqti; k++)
+        if (qip[k].qtermNum == i) g = k;
+      FTable *t = NULL;
+      for (int k = 0; k < s_nft; k++)
+        if (s_ft[k].term == i) t = &s_ft[k];
+      if (!t) {
+        t = &s_ft[s_nft++];
+        t->live = 1;
+        t->term = i;
+      }
+      hasFacet = 1;
+      if (t->n == 0) {
+        const orc_facet_ranges *fr = facet_ranges_of(prm, i);
+        for (int k = 0; fr && k < fr->n; k++)
+          if (!ft_get(t, fr->a[k])) ft_add(t, fr->a[k]);
+      }
+      fgroup[nf] = g;
+      fterm[nf] = i;
+      nf++;
+    }
 
     for (uint8_t *docIdPtr = P.vb.buf; docIdPtr < docIdEnd; docIdPtr += 6) {
       float minScore = 999999999.0;
@@ -1907,9 +2017,109 @@ static int run_range(const orc_qterm *qt, const uint8_t *const *lists, const int
         }
       }
       out->filtered--;
+      /* facet stats of every docid in the search results (Posdb.cpp:7362-7542):
+       * each key of its facet list's run, bucketed into a range with ranges,
+       * one vote per docid per entry */
+      for (int f = 0; hasFacet && f < nf; f++) {
+        const int g = fgroup[f];
+        if (g < 0 || !mml[g]) continue;
+        FTable *t = NULL;
+        for (int k = 0; k < s_nft; k++)
+          if (s_ft[k].term == fterm[f]) t = &s_ft[k];
+        const orc_facet_ranges *fr = facet_ranges_of(prm, fterm[f]);
+        const int isFloat = qt[fterm[f]].field_code == F_FACETFLOAT;
+        uint8_t *p2 = mml[g];
+        int firstTime = 1;
+        for (;;) {
+          if (p2 >= mme[g]) break;
+          if (!firstTime && !(p2[0] & 0x04)) break;
+          int32_t val32;
+          memcpy(&val32, p2 + 2, 4);
+          p2 += firstTime ? 12 : 6;
+          firstTime = 0;
+          float fv;
+          memcpy(&fv, &val32, 4);
+          FEnt *fe = NULL;
+          if (fr && fr->n > 0) {
+            for (int k = 0; k < fr->n; k++) {
+              if (isFloat) {
+                float A, B;
+                memcpy(&A, &fr->a[k], 4);
+                memcpy(&B, &fr->b[k], 4);
+                if (fv < A) continue;
+                if (fv >= B) continue;
+              } else {
+                if (val32 < fr->a[k]) continue;
+                if (val32 >= fr->b[k]) continue;
+              }
+              fe = ft_get(t, fr->a[k]);
+              break;
+            }
+          } else {
+            fe = ft_get(t, val32);
+            if (!fe) fe = ft_add(t, val32);
+          }
+          if (!fe) continue;
+          if (fe->docid == (int64_t)pt.docId) continue;
+          fe->docid = (int64_t)pt.docId;
+          fe->count++;
+          if (fe->count == 1) {
+            if (isFloat) {
+              const double z = 0.0;
+              memcpy(&fe->sum, &z, 8);
+              memcpy(&fe->min, &fv, 4);
+              memcpy(&fe->max, &fv, 4);
+            } else {
+              fe->sum = 0;
+              fe->min = val32;
+              fe->max = val32;
+            }
+          }
+          if (isFloat) {
+            double sum;
+            memcpy(&sum, &fe->sum, 8);
+            sum += fv;
+            memcpy(&fe->sum, &sum, 8);
+            float mn, mx;
+            memcpy(&mn, &fe->min, 4);
+            memcpy(&mx, &fe->max, 4);
+            if (fv < mn) memcpy(&fe->min, &fv, 4);
+            if (fv > mx) memcpy(&fe->max, &fv, 4);
+          } else {
+            fe->sum += val32;
+            if (val32 < fe->min) fe->min = val32;
+            if (val32 > fe->max) fe->max = val32;
+          }
+        }
+      }
       /* with m_useIntScores the tree orders by m_intScore (TopTree.cpp:216-219, 270-274) */
       tt_add(tree, sortByI >= 0 ? (double)intScore : (double)score, (int64_t)pt.docId);
       if (tree->n > tree->docsWanted) minWinningScore = tree->score[tree->n - 1]; /* 7699-7704 */
+    }
+    /* countUniqueDocids (Posdb.cpp:5002-5038, called at 7786-7796): the
+     * facet group's first sublist walked record by record over its whole
+     * buffer -- the shrunk runs, then the list's own bytes past them -- every
+     * record's value counted in an existing entry, the records longer than 6
+     * bytes into m_numDocsThatHaveFacet */
+    for (int f = 0; hasFacet && f < nf; f++) {
+      const int g = fgroup[f];
+      if (g < 0) continue;
+      FTable *t = NULL;
+      for (int k = 0; k < s_nft; k++)
+        if (s_ft[k].term == fterm[f]) t = &s_ft[k];
+      const OList *L = &P.lists[qip[g].subList[0]];
+      const uint8_t *rp = L->list, *end = L->list + L->size;
+      uint64_t count = 0;
+      while (rp < end) {
+        int32_t val32;
+        memcpy(&val32, rp + 2, 4);
+        FEnt *fe = ft_get(t, val32);
+        if (fe) fe->outside++;
+        const int rs = keySize(rp);
+        rp += rs;
+        if (rs > 6) count++;
+      }
+      t->docs += count;
     }
   doneAll:
     free(wikiPhraseIds); free(quotedStartIds); free(qpos); free(freqWeights);
@@ -1964,13 +2174,17 @@ static int64_t constrain_docids(const uint8_t *l, int64_t n, uint64_t d0, uint64
 int orc_query(const orc_qterm *qt, const uint8_t *const *lists, const int64_t *sizes, int nqt,
               const orc_params *prm, int64_t *docids, float *scores, int cap, orc_result *out) {
   memset(out, 0, sizeof *out);
+  ft_reset();
   if (nqt < 0 || !prm) return EINVAL;
   if (prm->real_max_top <= 0 || prm->docs_to_get <= 0 || prm->num_docid_splits <= 0) return EINVAL;
   int intMode = 0;
   for (int i = 0; i < nqt; i++) {
     const int fc = qt[i].field_code;
     if ((fc == F_SORTBYINT || fc == F_REVSORTBYINT) && qt[i].is_required) intMode = 1;
-    if (fc == F_FACETSTR || fc == F_FACETINT || fc == F_FACETFLOAT) return ENOTSUP; /* facets: DESIGN.md */
+    /* facets: restated without site clustering (the prefilter skip of
+       Posdb.cpp:6356 and the replay are not) and outside boolean queries */
+    if ((fc == F_FACETSTR || fc == F_FACETINT || fc == F_FACETFLOAT) && (prm->site_clustering || prm->is_boolean))
+      return ENOTSUP;
     /* a boolean query's gbsortby score reads a mini-merged list that may be
        the next group's or stale bytes (Posdb.cpp:7263-7279): not restated */
     if (prm->is_boolean && (fc == F_SORTBYFLOAT || fc == F_REVSORTBYFLOAT || fc == F_SORTBYINT ||

@@ -62,7 +62,26 @@ typedef struct orc_params {
   int32_t is_boolean;
   int32_t bool_ngroups;
   const uint8_t *bool_table;
+  /* gbfacetint:/gbfacetfloat: ranges (QueryWord::m_numFacetRanges,
+   * m_facetRange{Int,Float}{A,B}, Query.h:389-393), as gbgpu_params */
+  int32_t n_facet_ranges;
+  int32_t pad_f;
+  const struct orc_facet_ranges *facet_ranges;
 } orc_params;
+
+typedef struct orc_facet_ranges {
+  int32_t term;        /* the facet query term */
+  int32_t n;           /* ranges (<= 256) */
+  const int32_t *a, *b; /* [A, B) bounds: int32, or float bits for gbfacetfloat */
+} orc_facet_ranges;
+
+/* The facet tables of the last orc_query (QueryTerm::m_facetHashTable and
+ * m_numDocsThatHaveFacet, Posdb.cpp:1000-1067, 5575-5631, 7362-7542,
+ * 5002-5038 / 7786-7796), serialized into `w` (cap int32 words): i32 nterms;
+ * per facet term: i32 term, u64 docs (2 words), i32 n, n x (i32 key, i32
+ * count, i32 outside, i64 docid, i64 sum, i32 max, i32 min) with keys
+ * ascending.  Returns the words written, or -1 if cap is too small. */
+int orc_last_facets(int32_t *w, int cap);
 
 typedef struct orc_list {
   const uint8_t *bytes;

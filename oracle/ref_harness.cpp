@@ -126,6 +126,16 @@ static std::vector<int32_t> s_btok;
 // Query::matchesBoolQuery for every vector (bit v at byte v >> 3, bit v & 7)
 static std::vector<uint8_t> s_btable;
 static int32_t s_bgroups = -1;
+// gbfacetint:/gbfacetfloat: ranges (QueryWord::m_numFacetRanges and
+// m_facetRange{Int,Float}{A,B}, Query.h:389-393) per query term, and the
+// facet tables the last query left (QueryTerm::m_facetHashTable, its
+// m_numDocsThatHaveFacet; Posdb.cpp:1000-1067, 5575-5631, 7362-7542, 7786-7796)
+struct FacetRanges {
+  int32_t term, n;
+  std::vector<int32_t> a, b;
+};
+static std::vector<FacetRanges> s_franges;
+static std::vector<char> s_facets;  // i32 nterms; per facet term: i32 term, u64 docs, i32 n, n x (i32 key, FacetEntry)
 static std::vector<int32_t> s_plan;    // the last query's QueryTermInfos (op 4)
 static int32_t s_used_nodes = 0;       // the last query's TopTree::m_numUsedNodes
 static std::vector<int32_t> s_ints;    // its nodes' m_intScore, high -> low
@@ -152,6 +162,9 @@ static int ref_query(const orc_qterm *terms, const uint8_t *const *lists, const 
 
   memset((void *)qts, 0, sizeof(qts));
   memset((void *)qws, 0, sizeof(qws));
+  // QueryTerm's facet table as Query constructs it (HashTableX::HashTableX:
+  // writable, no buffer) -- a zeroed one refuses every addKey
+  for (int i = 0; i < MAXT; i++) new (&qts[i].m_facetHashTable) HashTableX();
   for (int i = 0; i < nterms; i++) {
     const orc_qterm &t = terms[i];
     QueryTerm *qt = &qts[i];
@@ -203,6 +216,19 @@ static int ref_query(const orc_qterm *terms, const uint8_t *const *lists, const 
     q.m_numExpressions = 1;
     if (!q.m_expressions[0].addExpression(0, nw, &q, 0)) return EINVAL;
   }
+  for (size_t i = 0; i < s_franges.size(); i++) {
+    const FacetRanges &fr = s_franges[i];
+    if (fr.term < 0 || fr.term >= nterms || fr.n < 0 || fr.n > MAX_FACET_RANGES) return EINVAL;
+    QueryWord *qw = &qws[fr.term];
+    qw->m_numFacetRanges = fr.n;
+    for (int k = 0; k < fr.n; k++) {
+      qw->m_facetRangeIntA[k] = fr.a[k];
+      qw->m_facetRangeIntB[k] = fr.b[k];
+      memcpy(&qw->m_facetRangeFloatA[k], &fr.a[k], 4);
+      memcpy(&qw->m_facetRangeFloatB[k], &fr.b[k], 4);
+    }
+  }
+  for (int i = 0; i < nterms; i++) qws[i].m_fieldCode = qts[i].m_fieldCode;  // QueryWord's copy (Posdb.cpp:7439-7441)
 
   msg2.m_query = &q;
   msg2.m_lists = rl;
@@ -322,6 +348,11 @@ static int ref_query(const orc_qterm *terms, const uint8_t *const *lists, const 
     alloced = true;
     if (!tab->allocWhiteListTable()) return ENOMEM;
     if (!tab->setQueryTermInfo()) return ENOMEM;
+    if (getenv("GBREF_TRACE"))
+      for (int i = 0; i < nterms; i++)
+        fprintf(stderr, "gbref: term %d fc %d slots %d used %d qti %d hasFacet %d\n", i, (int)qts[i].m_fieldCode,
+                (int)qts[i].m_facetHashTable.m_numSlots, (int)qts[i].m_facetHashTable.m_numSlotsUsed,
+                qts[i].m_queryTermInfoNum, (int)tab->m_hasFacetTerm);
     const double t0 = now_s();
     if (msg39 && d0 == 0 && gbref_adapter_splits && gbref_adapter_splits(s_m39, lists, sizes)) {
       // every piece answered at once (Msg39's loop skipped to phase 3):
@@ -339,6 +370,41 @@ static int ref_query(const orc_qterm *terms, const uint8_t *const *lists, const 
     out->filtered += tab->m_filtered;
     if (tab->m_errno) out->corrupt = tab->m_errno;
   } while (ddd < dddEnd);
+  // the facet tables (Msg39.cpp:1453-1545 serializes the same)
+  s_facets.clear();
+  {
+    int32_t nf = 0;
+    std::vector<char> body;
+    for (int i = 0; i < nterms; i++) {
+      QueryTerm *qt = &qts[i];
+      if (qt->m_fieldCode != FIELD_GBFACETSTR && qt->m_fieldCode != FIELD_GBFACETINT &&
+          qt->m_fieldCode != FIELD_GBFACETFLOAT)
+        continue;
+      HashTableX *ft = &qt->m_facetHashTable;
+      int32_t used = ft->m_numSlots ? ft->m_numSlotsUsed : 0;
+      const uint64_t docs = qt->m_numDocsThatHaveFacet;
+      const size_t at = body.size();
+      body.resize(at + 16 + (size_t)used * (4 + sizeof(FacetEntry)));
+      char *p = &body[at];
+      memcpy(p, &i, 4);
+      memcpy(p + 4, &docs, 8);
+      int32_t k2 = 0;
+      char *e = p + 16;
+      for (int32_t k = 0; k < ft->m_numSlots; k++) {
+        if (!ft->m_flags[k]) continue;
+        const int32_t key = ft->getKey32FromSlot(k);
+        memcpy(e, &key, 4);
+        memcpy(e + 4, ft->getValFromSlot(k), sizeof(FacetEntry));
+        e += 4 + sizeof(FacetEntry);
+        k2++;
+      }
+      memcpy(p + 12, &k2, 4);
+      nf++;
+    }
+    s_facets.resize(4);
+    memcpy(&s_facets[0], &nf, 4);
+    s_facets.insert(s_facets.end(), body.begin(), body.end());
+  }
   // a boolean query's truth table, by the reference's own evaluator over
   // every bit vector of its QueryTermInfos (m_bitNum, Posdb.cpp:4485-4721)
   s_btable.clear();
@@ -656,6 +722,19 @@ int main(int argc, char **argv) {
       if (ntok < 0 || ntok > 256) return 4;
       s_btok.resize(ntok);
       rd(s_btok.data(), 4 * (size_t)ntok);
+      int32_t nfr;
+      rd(&nfr, 4);  // facet ranges: per term i32 term, i32 n, n x i32 a, n x i32 b
+      if (nfr < 0 || nfr > MAXT) return 4;
+      s_franges.assign(nfr, FacetRanges());
+      for (int i = 0; i < nfr; i++) {
+        rd(&s_franges[i].term, 4);
+        rd(&s_franges[i].n, 4);
+        if (s_franges[i].n < 0 || s_franges[i].n > MAX_FACET_RANGES) return 4;
+        s_franges[i].a.resize(s_franges[i].n);
+        s_franges[i].b.resize(s_franges[i].n);
+        rd(s_franges[i].a.data(), 4 * (size_t)s_franges[i].n);
+        rd(s_franges[i].b.data(), 4 * (size_t)s_franges[i].n);
+      }
       std::vector<int64_t> d(cap > 0 ? cap : 1);
       std::vector<float> s(cap > 0 ? cap : 1);
       int64_t vcap = 0;
@@ -692,6 +771,9 @@ int main(int argc, char **argv) {
       // the boolean truth table (i32 groups, -1 none; then its bytes)
       wr(&s_bgroups, 4);
       if (s_bgroups >= 0) wr(s_btable.data(), s_btable.size());
+      if (s_facets.size() < 4) s_facets.assign(4, 0);
+      wr(s_facets.data(), s_facets.size());  // the facet tables
+      s_facets.clear();
       if (op == 7) {
         // the shard's reply merged by the reference's own Msg3a::mergeLists
         // (one shard: the TopTree's first docsToGet as Msg39 sends them,

@@ -57,6 +57,14 @@ def save_query(name, terms, lists, params, prefix="q"):
     pr = np.array([params.docs_to_get, params.real_max_top, params.language, params.site_clustering,
                    params.num_docid_splits, params.do_max_score_algo], np.int32)
     extra = {}
+    if r.get("facets"):
+        extra.update(facet_arrays(r["facets"]))
+    if getattr(params, "_franges", None):
+        fr = params._franges
+        extra["franges_term"] = np.array([t for t, a, b in fr], np.int32)
+        extra["franges_n"] = np.array([len(a) for t, a, b in fr], np.int32)
+        extra["franges_a"] = np.array([x for t, a, b in fr for x in a], np.int32)
+        extra["franges_b"] = np.array([x for t, a, b in fr for x in b], np.int32)
     if getattr(params, "_btok", None):
         # a boolean query: its expression (the harness builds the Query's
         # QueryWords from it) and the truth table the reference's own
@@ -76,6 +84,61 @@ def save_query(name, terms, lists, params, prefix="q"):
                         filtered=np.int32(r["filtered"]), docs_wanted=np.int32(r["docs_wanted"]), votes=r["votes"],
                         **white_arrays(params), **extra, **extra_num)
     return r
+
+
+def facet_arrays(facets):
+    """QueryTerm::m_facetHashTable of every facet term, flattened: the term,
+    m_numDocsThatHaveFacet, its entry count, keys ascending, and per entry
+    (m_count, m_outsideSearchResultsCount, m_docId, m_sum, m_max, m_min)"""
+    terms = sorted(facets)
+    keys, vals = [], []
+    for t in terms:
+        docs, ents = facets[t]
+        for k in sorted(ents):
+            keys.append(k)
+            vals.append(ents[k])
+    return dict(facet_term=np.array(terms, np.int32),
+                facet_docs=np.array([facets[t][0] for t in terms], np.uint64),
+                facet_n=np.array([len(facets[t][1]) for t in terms], np.int32),
+                facet_keys=np.array(keys, np.int32), facet_vals=np.array(vals, np.int64).reshape(-1, 6))
+
+
+def save_facets():
+    """gbfacetstr:/gbfacetint:/gbfacetfloat: terms (Posdb.cpp:1000-1067,
+    5575-5631, 7362-7542, 5002-5038): the per-value (or per-range) stats of
+    the docids in the search results, the values' counts over the whole
+    termlist buffer, and its docid count"""
+    import struct
+    from numlists import number_list
+    N = 6000
+    fl = lambda x: struct.unpack("<i", struct.pack("<f", x))[0]  # noqa: E731
+    cases = [
+        # (kind, seed, field code, ints, kmax, frac, ranges, params kw)
+        ("int", 0, 1, 64, True, 3, 0.8, None, {}),
+        ("int_ranges", 0, 2, 64, True, 2, 0.7, ([0, 50, 100], [50, 100, 300]), {}),
+        ("float", 1, 3, 65, False, 3, 0.9, None, {}),
+        ("float_ranges", 1, 4, 65, False, 2, 0.8, ([fl(0.0), fl(20.0), fl(55.5)], [fl(20.0), fl(55.5), fl(100.0)]), {}),
+        ("str", 2, 5, 63, True, 1, 0.6, None, {}),
+        ("int_serp", 0, 6, 64, True, 2, 0.8, None, "serp"),
+        ("int_docs10", 4, 7, 64, True, 4, 0.9, None, {"docs_to_get": 10}),
+    ]
+    for name, kind, seed, fc, ints, kmax, frac, ranges, kw in cases:
+        q = qkinds.kinds(N, seed=seed)[kind]
+        if isinstance(kw, dict) and "docs_to_get" in kw:
+            q.docs_to_get = kw["docs_to_get"]
+        lists = generate(q, N, seed=6000 + seed)
+        terms = list(q.terms)
+        terms.append(gbgpu.QTerm(1, 0, fc, 0, -1, -1, -1, 0, max(t.qpos for t in terms) + 2, 0, -1, 1.0))
+        lists = list(lists) + [number_list(lists, frac, seed=60 + seed, kmax=kmax, ints=ints)]
+        p = q.params()
+        if kw == "serp":
+            full = ref.query(terms, lists, p, cap=1 << 16)
+            pos = len(full["docids"]) // 3
+            p = q.params(max_serp_score=float(full["scores"][pos]), min_serp_docid=int(full["docids"][pos]))
+        if ranges:
+            p = p.with_facets([(len(terms) - 1, ranges[0], ranges[1])])
+        r = save_query(f"facet_{name}", terms, lists, p)
+        print(f"q_facet_{name}: hits={r['hits']} facets={ {t: (d, len(e)) for t, (d, e) in r['facets'].items()} }")
 
 
 def white_arrays(params):
@@ -647,6 +710,7 @@ def main():
     save_sortby_int_modes()
     save_range()
     save_boolean()
+    save_facets()
     save_msg5()
     save_msg3a()
     cases = [(0, -1), (1, -1), (0, 5000), (1, 5000), (0, 1)]

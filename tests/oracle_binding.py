@@ -21,6 +21,7 @@ def lib():
     global _lib
     if _lib is None:
         _lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "liboracle.so"))
+        _lib.orc_last_facets.argtypes = [ctypes.POINTER(ctypes.c_int32), ctypes.c_int]
         _lib.orc_query.argtypes = [ctypes.POINTER(gbgpu.QTerm), ctypes.POINTER(ctypes.c_void_p),
                                    ctypes.POINTER(ctypes.c_int64), ctypes.c_int, ctypes.POINTER(gbgpu.Params),
                                    ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_float), ctypes.c_int,
@@ -63,7 +64,31 @@ def query(terms, lists, params, cap=4096):
     if rc:
         raise RuntimeError(f"orc_query rc={rc}")
     return dict(docids=d[:r.n].copy(), scores=s[:r.n].copy(), hits=r.hits, filtered=r.filtered,
-                docs_wanted=r.docs_wanted, corrupt=r.corrupt)
+                docs_wanted=r.docs_wanted, corrupt=r.corrupt, facets=last_facets())
+
+
+def last_facets():
+    """the facet tables of the last orc_query: {term: (docs, {key: (count,
+    outside, docid, sum, max, min)})}, as ref_binding reads the reference's"""
+    L = lib()
+    cap = 1 << 22
+    w = np.zeros(cap, np.int32)
+    n = L.orc_last_facets(w.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), cap)
+    assert n >= 1
+    out, k = {}, 1
+    for _ in range(int(w[0])):
+        term = int(w[k])
+        docs = int(w[k + 1:k + 3].view(np.uint64)[0])
+        ne = int(w[k + 3])
+        k += 4
+        ents = {}
+        for _ in range(ne):
+            r = w[k:k + 9]
+            ents[int(r[0])] = (int(r[1]), int(r[2]), int(r[3:5].view(np.int64)[0]), int(r[5:7].view(np.int64)[0]),
+                               int(r[7]), int(r[8]))
+            k += 9
+        out[term] = (docs, ents)
+    return out
 
 
 def intersect(terms, lists, cap=1 << 24, params=None):

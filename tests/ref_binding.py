@@ -88,6 +88,12 @@ def query(terms, lists, params, cap=4096, votes=False, reps=1, white=None, mode=
     btok = list(getattr(params, "_btok", None) or [])  # a boolean query's expression
     req.append(struct.pack("<i", len(btok)))
     req.append(np.asarray(btok, np.int32).tobytes())
+    fr = list(getattr(params, "_franges", None) or [])  # facet ranges: (term, a[], b[]) as int32 bits
+    req.append(struct.pack("<i", len(fr)))
+    for term, a, b in fr:
+        req.append(struct.pack("<ii", term, len(a)))
+        req.append(np.asarray(a, np.int32).tobytes())
+        req.append(np.asarray(b, np.int32).tobytes())
     p.stdin.write(b"".join(req))
     p.stdin.flush()
     r = OrcResult.from_buffer_copy(rd(ctypes.sizeof(OrcResult)))
@@ -102,9 +108,18 @@ def query(terms, lists, params, cap=4096, votes=False, reps=1, white=None, mode=
         info.append(rd(nb) if nb else b"")
     (bng,) = struct.unpack("<i", rd(4))
     btable = rd(((1 << bng) + 7) // 8) if bng >= 0 else None
+    (nft,) = struct.unpack("<i", rd(4))
+    facets = {}
+    for _ in range(nft):  # QueryTerm::m_facetHashTable: term -> (docs, {key: FacetEntry tuple})
+        term, docs, ne = struct.unpack("<iQi", rd(16))
+        ents = {}
+        for _ in range(ne):
+            key, cnt, outside, docid, fsum, fmax, fmin = struct.unpack("<iiiqqii", rd(36))
+            ents[key] = (cnt, outside, docid, fsum, fmax, fmin)
+        facets[term] = (docs, ents)
     out = dict(docids=d, scores=s, hits=r.hits, filtered=r.filtered, docs_wanted=r.docs_wanted,
                corrupt=r.corrupt, votes=v, seconds=sec, score_info=info[0], pair_scores=info[1],
-               single_scores=info[2], bool_groups=bng, bool_table=btable)
+               single_scores=info[2], bool_groups=bng, bool_table=btable, facets=facets)
     if op == 7:
         (no,) = struct.unpack("<i", rd(4))
         if no < 0:

@@ -44,17 +44,33 @@ def load_query(path):
                           int(z["min_serp_docid"]) if "min_serp_docid" in z else 0)
     if "use_whitelist" in z and int(z["use_whitelist"]):
         params = params.with_whitelist(split_blob(z["white_sizes"], z["white_blob"]))
+    if "franges_term" in z:  # gbfacetint:/gbfacetfloat: ranges
+        fr, off = [], 0
+        for t, n in zip(z["franges_term"], z["franges_n"]):
+            fr.append((int(t), z["franges_a"][off:off + n].tolist(), z["franges_b"][off:off + n].tolist()))
+            off += int(n)
+        params = params.with_facets(fr)
     if "bool_tok" in z:  # a boolean query: its expression and the reference's truth table
         params = params.with_boolean(z["bool_table"].tobytes(), int(z["bool_groups"]), [int(x) for x in z["bool_tok"]])
     lists = split_blob(z["list_sizes"], z["list_blob"])
     exp = dict(docids=z["docids"], scores=z["score_bits"].view(np.float32), hits=int(z["hits"]),
                docs_wanted=int(z["docs_wanted"]), votes=z["votes"],
                filtered=int(z["filtered"]) if "filtered" in z else None)
+    if "facet_term" in z:
+        exp["facets"], off = {}, 0
+        for t, d, n in zip(z["facet_term"], z["facet_docs"], z["facet_n"]):
+            keys = z["facet_keys"][off:off + n]
+            vals = z["facet_vals"][off:off + n]
+            exp["facets"][int(t)] = (int(d), {int(k): tuple(int(x) for x in v) for k, v in zip(keys, vals)})
+            off += int(n)
     return terms, lists, params, exp
 
 
 def check(got, exp, label):
     assert got["hits"] == exp["hits"], label
+    if exp.get("facets") is not None and got.get("facets") is not None:
+        # QueryTerm::m_facetHashTable entry by entry, and m_numDocsThatHaveFacet
+        assert got["facets"] == exp["facets"], label
     assert got["docs_wanted"] == exp["docs_wanted"], label
     if exp.get("filtered") is not None:
         assert got["filtered"] == exp["filtered"], label
