@@ -376,7 +376,9 @@ def main():
 
     per = args.docs_per_gpu or (CFG2_DOCS if world == 1 else CFG4_DOCS_PER_GPU)
     total = per * world
-    eng = gbgpu.Engine(local_rank)
+    # GBGPU_DIAG=1: the diagnostic build (lib/libgbgpu_diag.so), whose
+    # GBGPU_*_MODE switches time kernel phases; never the measured product
+    eng = gbgpu.Engine(local_rank, diag=os.environ.get("GBGPU_DIAG") == "1")
     exchange = world > 1 or args.exchange
     if exchange and world == 1:
         eng.comm_init(1, 0, gbgpu.Engine.comm_unique_id())

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define GBGPU_ABI_VERSION 11
+#define GBGPU_ABI_VERSION 12
 
 /* error codes beyond errno.h (Errno.h numbering is not reused) */
 #define GBGPU_ENODEVICE   1001 /* no HIP device / extension not usable        */
@@ -60,7 +60,8 @@ typedef struct gbgpu_qterm {
                                        float (54/55), range terms gbmin:/gbmax:/gbequal:
                                        (56-57, 61-62, 66-67; own list only, positive),
                                        gbsortby: int (59/60: gbgpu_result::int_scores);
-                                       facets (63-65): EUNSUPPORTED */
+                                       facets gbfacetstr:/int:/float: (63-65:
+                                       gbgpu_result::facets) */
   int32_t piped;                    /* m_piped                                       */
   int32_t synonym_of;               /* index of m_synonymOf, -1 if none              */
   int32_t left_phrase_term;         /* m_leftPhraseTermNum, -1 if none               */
@@ -142,7 +143,39 @@ typedef struct gbgpu_params {
   int32_t is_boolean;
   int32_t bool_ngroups;
   const uint8_t *bool_table;
+  /* Facet terms (gbfacetstr: / gbfacetint: / gbfacetfloat:, field codes
+   * 63-65) are required terms whose termlists hold a 32-bit value where the
+   * word position is; the result carries each one's QueryTerm::
+   * m_facetHashTable (gbgpu_result::facets).  A gbfacetint:/gbfacetfloat:
+   * term may bucket its values into [A, B) ranges (QueryWord::
+   * m_numFacetRanges, m_facetRange{Int,Float}{A,B}, Query.h:389-393; floats
+   * by their 32-bit patterns).  Zero-filled: no ranges. */
+  int32_t n_facet_ranges;
+  int32_t pad_f;
+  const struct gbgpu_facet_ranges *facet_ranges;
 } gbgpu_params;
+
+typedef struct gbgpu_facet_ranges {
+  int32_t term;          /* the facet query term                       */
+  int32_t n;             /* ranges, <= 256                              */
+  const int32_t *a, *b;  /* bounds [a[k], b[k]): int32 or float bits    */
+} gbgpu_facet_ranges;
+
+/* One entry of a facet term's table: the value's (or its range's A) 32
+ * bits and Posdb.h:401-413's FacetEntry -- the search results with that
+ * value (m_count, one vote per docid), the last of them (m_docId), the sum
+ * (int64, or a double's bits for gbfacetfloat), max and min of their values,
+ * and the value's count over the whole termlist buffer
+ * (m_outsideSearchResultsCount, countUniqueDocids, Posdb.cpp:5002-5038). */
+typedef struct gbgpu_facet_entry {
+  int32_t term;     /* the facet query term                            */
+  int32_t key;      /* HashTableX key                                  */
+  int32_t count;    /* FacetEntry: m_count                             */
+  int32_t outside;  /*             m_outsideSearchResultsCount         */
+  int64_t docid;    /*             m_docId                             */
+  int64_t sum;      /*             m_sum                               */
+  int32_t max, min; /*             m_max, m_min                        */
+} gbgpu_facet_entry;
 
 
 /* The second pass's score info (m_getDocIdScoringInfo, Posdb.cpp:6116-6244,
@@ -216,6 +249,19 @@ typedef struct gbgpu_result {
    * term makes the tree use integer scores (scores[] are then 0.0, as the
    * reference's m_score); 0 otherwise.  NULL to skip. */
   int32_t *int_scores;
+  /* with facet terms: every facet term's table (Posdb.cpp:1000-1067,
+   * 5575-5631, 7362-7542), entries by term then key ascending, n_facets of
+   * them (ENOSPC when that exceeds facets_cap; NULL: not written), and
+   * facet_docs[term] = m_numDocsThatHaveFacet (countUniqueDocids' count,
+   * Posdb.cpp:7786-7796) for each of the nterms terms (0 for a term with no
+   * table: not a facet term, an empty list, or a query that ended before
+   * allocTopTree).  Both NULL: no facet pass.  Facets run without site
+   * clustering, docid splits or a boolean expression, at most 4 facet terms,
+   * each a group of its own list alone (GBGPU_EUNSUPPORTED otherwise). */
+  gbgpu_facet_entry *facets;
+  int32_t facets_cap;
+  int32_t n_facets;
+  uint64_t *facet_docs;
 } gbgpu_result;
 
 int         gbgpu_open(int device, gbgpu_ctx **out);

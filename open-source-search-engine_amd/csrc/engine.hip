@@ -71,6 +71,8 @@ constexpr int CHUNK_LOAD = CHUNK_BYTES + 16;     // + the tail of a 12-byte key
 constexpr int MAX_RUNS = CHUNK_UNITS / 2;        // a run is >= 2 units
 constexpr int TILE = 2048;                       // final top-k sort capacity
 constexpr int MAX_K = 1536;                      // TILE - MAX_K ties merged per round
+constexpr int TILE_BIG = 8192;                   // ... for a larger TopTree (k_topk<TILE_BIG>, 96 KiB of LDS)
+constexpr int MAX_K_BIG = 6144;                  // docsToGet up to 3072 (m_docsWanted = 2 docsToGet)
 constexpr int SEL_HBINS = 65536;                 // top-k histogram bins (key >> 16)
 constexpr int TREE_CAP = 4096;                   // site-clustering TopTree nodes held in LDS
 constexpr int LIST_PAD = CHUNK_LOAD + 128;
@@ -4693,7 +4695,7 @@ constexpr int TK_THREADS = 1024;
 constexpr int TK_BLOCKS = 32;
 // Select::cnt packs |A| (16 bits: < k <= MAX_K), |B| (32 bits) and the
 // blocks finished (16 bits) into one 64-bit word
-static_assert(MAX_K < 65536 && TK_BLOCKS < 65536, "Select::cnt fields");
+static_assert(MAX_K < 65536 && MAX_K_BIG < 65536 && TK_BLOCKS < 65536, "Select::cnt fields");
 constexpr int TK_E = 16;  // keys per thread and gather round
 
 // bitonic sort of sk/sd[0, n) in LDS, n rounded up to a power of two with
@@ -4855,6 +4857,9 @@ __device__ __forceinline__ uint32_t block_append(bool f, uint32_t key, uint64_t 
   return n + tot;
 }
 
+// TL: the final sort's LDS capacity (k < TL; TILE, or TILE_BIG for a TopTree
+// beyond MAX_K nodes)
+template <int TL>
 __global__ void __launch_bounds__(TK_THREADS) k_topk(const uint32_t *skey, const uint64_t *sdoc, const Counters *ctr,
                                                      Select *sel, uint32_t k, uint32_t *akey, uint64_t *adoc,
                                                      uint32_t *bkey, uint64_t *bdoc, uint32_t *out_key,
@@ -4862,8 +4867,8 @@ __global__ void __launch_bounds__(TK_THREADS) k_topk(const uint32_t *skey, const
   __shared__ uint32_t tmp[TK_THREADS / 64];
   __shared__ uint32_t s_bin, s_above, s_total, s_last, s_ba, s_bb;
   __shared__ uint32_t h8[256];
-  __shared__ __attribute__((aligned(16))) uint32_t sk[TILE];
-  __shared__ uint64_t sd[TILE];
+  __shared__ __attribute__((aligned(16))) uint32_t sk[TL];
+  __shared__ uint64_t sd[TL];
   const uint32_t n = (uint32_t)(ctr->surv_top >> 36);
   const bool dbg0 = blockIdx.x == 0 && threadIdx.x == 0;
   if (dbg0) sel->tdbg[0] = __builtin_amdgcn_s_memrealtime();
@@ -5032,7 +5037,7 @@ __global__ void __launch_bounds__(TK_THREADS) k_topk(const uint32_t *skey, const
   }
   uint32_t kept = na, tb = 0;
   for (;;) {
-    const uint32_t take = min(nt - tb, (uint32_t)TILE - kept);
+    const uint32_t take = min(nt - tb, (uint32_t)TL - kept);
     for (uint32_t t = threadIdx.x; t < take; t += TK_THREADS) {
       sk[kept + t] = ld_sc1(bkey + tb + t);
       sd[kept + t] = ld_sc1(bdoc + tb + t);
@@ -5392,6 +5397,20 @@ using namespace gbgpu;
 // One query in flight: its stream, device buffers (grown, then reused),
 // pinned staging and result state.  A context owns one or more slots; the
 // resident lists are shared by all of them.
+constexpr int MAXF = 4;                // facet terms per query
+constexpr int MAX_FACET_RANGES = 256;  // QueryWord::m_facetRange{Int,Float}{A,B}
+
+// a facet query term of the slot's query (enqueue_entries)
+struct FacetTerm {
+  int term;
+  int lid;  // its group's list, or -1 (no group: the table holds its ranges only)
+  int isfloat;
+  std::vector<int32_t> a, b;  // ranges
+  uint32_t units;
+  const uint8_t *list;
+};
+
+
 struct QuerySlot {
   std::mutex mu;
   hipStream_t stream = nullptr;
@@ -5401,6 +5420,8 @@ struct QuerySlot {
   DevBuf blk, sflag, ord, oslot, rep, tree;  // site clustering: slot-order ranks and slots, replay entries, TopTree state
   DevBuf white, wrej;                       // "&sites=" whitelist: sorted 5-byte values; rejected slots
   DevBuf si;                                // second pass's score info (score_info)
+  DevBuf fac;                               // facet tables (facet_pass)
+  std::vector<FacetTerm> facets;            // the query's facet terms with a table
   std::vector<uint64_t> h_white;            // its host copy (the upload's source)
   uint32_t epoch = 0;
   uint8_t *h_stage = nullptr;  // pinned: query tables (host -> device, one copy)
@@ -5434,9 +5455,9 @@ struct QuerySlot {
   hipEvent_t ev_done = nullptr;  // the query's device work is done (the exchange waits on it)
   float last_ms[6] = {0, 0, 0, 0, 0, 0};
 
-  DevBuf *const bufs[28] = {&tables, &chunkcnt, &cand, &cunit, &bits, &loc, &svslot, &svlm, &svu, &svdoc,
+  DevBuf *const bufs[29] = {&tables, &chunkcnt, &cand, &cunit, &bits, &loc, &svslot, &svlm, &svu, &svdoc,
                             &svloc, &scratch, &skey, &sel, &gath, &res, &dir, &split, &swin, &blk,
-                            &sflag, &ord, &oslot, &rep, &tree, &white, &wrej, &si};
+                            &sflag, &ord, &oslot, &rep, &tree, &white, &wrej, &si, &fac};
   int init(hipMemPool_t pool) {
     if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return GBGPU_EHIP;
     for (auto *b : bufs) {
@@ -5701,7 +5722,6 @@ static int snapshot_lists(gbgpu_ctx *ctx, const gbgpu_qterm *terms, int nterms, 
   ents.resize(nterms);
   std::lock_guard<std::mutex> g(ctx->lists_mu);
   for (int i = 0; i < nterms; i++) {
-    if (field_unsupported(terms[i].field_code)) return GBGPU_EUNSUPPORTED;
     int32_t h = handles[i];
     if (h < 0 || h >= (int32_t)ctx->lists.size() || !ctx->lists[h].live) return EINVAL;
     ents[i] = ctx->lists[h];
@@ -5848,6 +5868,7 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
       if (terms[i].is_required && range_mode(terms[i].field_code, &ri)) return GBGPU_EUNSUPPORTED;
     }
   }
+  q.facets.clear();
   q.docs_wanted = hp.docs_wanted;
   q.k = clus ? TC : hp.docs_wanted;
   // Posdb.cpp:5735: a boolean query goes on with an empty smallest group
@@ -5879,7 +5900,7 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
     return 0;
   }
   if (hp.ngroups > MAXG) return GBGPU_EUNSUPPORTED;
-  if (!clus && q.k > MAX_K) return GBGPU_EUNSUPPORTED;
+  if (!clus && q.k > MAX_K_BIG) return GBGPU_EUNSUPPORTED;
 
   // ---- query tables, built straight into the pinned staging buffer
   // layout: [DevPlan | G0Chunk[] | afirst[MAXG0] | ProbeWork[]]
@@ -5998,6 +6019,42 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
       }
     }
   }
+  // facet terms with a non-empty list get a table (allocTopTree, Posdb.cpp:
+  // 1000-1067); collect() fills it.  Restated without site clustering, a
+  // boolean expression or docid splits, for a facet term whose group is its
+  // own list alone, used by no other group
+  for (int i = 0; i < nterms; i++) {
+    const int32_t fc = terms[i].field_code;
+    if (fc < FIELD_GBFACETSTR || fc > FIELD_GBFACETFLOAT || ents[i].size == 0) continue;
+    if (q.facets.size() >= (size_t)MAXF || clus || boolean || p->num_docid_splits > 1 ||
+        tree_phase != (TREE_INIT | TREE_FINAL))
+      return GBGPU_EUNSUPPORTED;
+    FacetTerm ft;
+    ft.term = i;
+    ft.lid = -1;
+    ft.isfloat = fc == FIELD_GBFACETFLOAT;
+    ft.units = ents[i].units;
+    ft.list = ents[i].d;
+    for (int j = 0; j < hp.ngroups; j++) {
+      if (hp.g[j].qterm != i) continue;
+      const GroupInfo &g = hp.g[j];
+      const int id = dense[i];
+      if (g.nsub != 1 || g.sub_term[0] != i || (g.flags[0] & BF_NEGATIVE) || id < 0 || P.lists[id].uses != 1 ||
+          (P.reshare_mask >> id & 1))
+        return GBGPU_EUNSUPPORTED;
+      ft.lid = id;
+    }
+    if (p->n_facet_ranges < 0 || (p->n_facet_ranges > 0 && !p->facet_ranges)) return EINVAL;
+    for (int r = 0; r < p->n_facet_ranges; r++) {
+      const gbgpu_facet_ranges &fr = p->facet_ranges[r];
+      if (fr.term != i) continue;
+      if (fr.n < 0 || fr.n > MAX_FACET_RANGES || (fr.n > 0 && (!fr.a || !fr.b))) return EINVAL;
+      ft.a.assign(fr.a, fr.a + fr.n);
+      ft.b.assign(fr.b, fr.b + fr.n);
+      break;
+    }
+    q.facets.push_back(std::move(ft));
+  }
   // candidate arrays: distinct lists of the smallest group, in sublist order;
   // for a boolean query every distinct list (the docid set is their union:
   // a docid's slot is in the first array holding it, its other arrays'
@@ -6067,6 +6124,13 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
     q.afirst[a] = (uint32_t)q.g0c.size();
     const uint32_t units = P.lists[P.g0list[a]].units;
     for (uint32_t u = 0; u < units; u += CHUNK_UNITS) q.g0c.push_back({(uint32_t)a, u});
+  }
+  if (q.g0c.empty()) {
+    // no candidate at all: a boolean query (or docid-split piece) whose every
+    // list is empty votes nothing
+    q.early = true;
+    q.pending = true;
+    return 0;
   }
   q.pw.clear();
   int64_t scan = 0;
@@ -6147,7 +6211,7 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   rc2 |= q.skey.ensure(4 * slot_ub);
   rc2 |= q.blk.ensure(sizeof(BlkInfo) * (size_t)cgrid);
   rc2 |= q.sel.ensure(sizeof(Select));
-  rc2 |= q.gath.ensure(12 * (slot_ub + MAX_K) + 1024);
+  rc2 |= q.gath.ensure(12 * (slot_ub + MAX_K_BIG) + 1024);
   rc2 |= q.res.ensure(q.res_bytes);
   if (clus) {
     rc2 |= q.sflag.ensure(slot_ub);
@@ -6341,6 +6405,7 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
                          q.res.as<uint32_t>(res_keys_off()), q.res.as<uint64_t>(res_docs_off(k)));
     }
     q.replayed = true;
+    HIPCHECK(hipGetLastError());  // a launch refused above
     if (ctx->profiling) HIPCHECK(hipEventRecord(q.ev[5], st));
     HIPCHECK(hipEventRecord(q.ev_done, st));
     HIPCHECK(hipMemcpyAsync(q.h_res, q.res.p, q.res_bytes, hipMemcpyDeviceToHost, st));
@@ -6351,14 +6416,16 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   // top-k: radix select over the survivors' keys, then one LDS sort
   const uint32_t *skey = q.skey.as<uint32_t>();
   uint32_t *akey = q.gath.as<uint32_t>();
-  uint64_t *adoc = q.gath.as<uint64_t>(align256(4 * (size_t)MAX_K));
-  uint32_t *bkey = q.gath.as<uint32_t>(align256(4 * (size_t)MAX_K) + align256(8 * (size_t)MAX_K));
-  uint64_t *bdoc = q.gath.as<uint64_t>(align256(4 * (size_t)MAX_K) + align256(8 * (size_t)MAX_K) +
+  uint64_t *adoc = q.gath.as<uint64_t>(align256(4 * (size_t)MAX_K_BIG));
+  uint32_t *bkey = q.gath.as<uint32_t>(align256(4 * (size_t)MAX_K_BIG) + align256(8 * (size_t)MAX_K_BIG));
+  uint64_t *bdoc = q.gath.as<uint64_t>(align256(4 * (size_t)MAX_K_BIG) + align256(8 * (size_t)MAX_K_BIG) +
                                           align256(4 * slot_ub));
   const uint32_t tgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(TK_BLOCKS, (slot_ub + TK_THREADS - 1) / TK_THREADS));
-  hipLaunchKernelGGL(k_topk, dim3(tgrid), dim3(TK_THREADS), 0, st, skey, (const uint64_t *)svdoc, dctr, dsel,
+  hipLaunchKernelGGL(k <= MAX_K ? k_topk<TILE> : k_topk<TILE_BIG>, dim3(tgrid), dim3(TK_THREADS), 0, st, skey,
+                     (const uint64_t *)svdoc, dctr, dsel,
                      (uint32_t)k, akey, adoc, bkey, bdoc, q.res.as<uint32_t>(res_keys_off()),
                      q.res.as<uint64_t>(res_docs_off(k)));
+  HIPCHECK(hipGetLastError());  // a launch refused above
   if (ctx->profiling) HIPCHECK(hipEventRecord(q.ev[5], st));
   HIPCHECK(hipEventRecord(q.ev_done, st));
   HIPCHECK(hipMemcpyAsync(q.h_res, q.res.p, q.res_bytes, hipMemcpyDeviceToHost, st));
@@ -6605,6 +6672,528 @@ static int score_info(QuerySlot &q, const uint32_t *keys, const uint64_t *docs, 
   return rc ? rc : (acc.room ? 0 : ENOSPC);
 }
 
+// ------------------------------------------------------------------ facets
+// Each facet query term's QueryTerm::m_facetHashTable (Posdb.h:401-413) and
+// m_numDocsThatHaveFacet, after the scoring pass.  The reference builds them
+// inside intersectLists10_r: every docid that reaches the TopTree (after the
+// paging filter) walks its run in the facet list and votes once per entry
+// (Posdb.cpp:7362-7542), then countUniqueDocids (5002-5038, called at
+// 7786-7796) walks the facet list's whole buffer -- the survivors' runs that
+// shrinkSubLists wrote over its start, then the list's own bytes past them --
+// counting each record's value in an existing entry and each record longer
+// than 6 bytes.  Here: the votes are emitted per survivor, sorted by (facet,
+// key, docid) -- the reference's docid order, which a gbfacetfloat sum (a
+// double accumulated in that order) needs -- and reduced one wave per entry;
+// the buffer walk is the survivors' runs in parallel, the unaligned start of
+// the list's tail walked by one lane until it meets a key start, and the rest
+// of the tail in parallel (a walk that is aligned visits exactly the units
+// whose byte 1 has the 0x02 bit).
+constexpr int FAC_LDS = 4096;          // table entries counted in LDS per block
+
+struct FacetPlan {
+  int nf;
+  int lid[MAXF];      // the facet group's only list (dense id); -1: no group
+  int isfloat[MAXF];  // gbfacetfloat: ranges and stats compare as floats
+  int nr[MAXF];       // ranges
+  const int32_t *ra[MAXF], *rb[MAXF];
+  const int32_t *tkey[MAXF];  // the table's keys, ascending (k_facet_outside / k_facet_tail)
+  int tn[MAXF];
+  uint32_t tbase[MAXF];  // the table's first counter in `outside`
+  uint32_t units[MAXF];
+  const uint8_t *list[MAXF];
+};
+
+struct FacetCtr {
+  uint32_t nrec, nseg;
+  uint32_t pad[2];
+  unsigned long long B[MAXF];     // units the survivors' runs take (the shrunk buffer's size)
+  unsigned long long docs[MAXF];  // m_numDocsThatHaveFacet
+};
+
+__device__ __forceinline__ int32_t fac_val(gu8 *k) {  // Posdb::getFacetVal32: bytes 2..5
+  return (int32_t)((uint32_t)k[2] | ((uint32_t)k[3] << 8) | ((uint32_t)k[4] << 16) | ((uint32_t)k[5] << 24));
+}
+
+// the entry value v votes for (Posdb.cpp:7380-7430): the first range holding
+// it (keyed by its A value), or v itself without ranges; false: no range
+__device__ __forceinline__ bool fac_bucket(const FacetPlan &fp, int f, int32_t v, int32_t *key) {
+  const int nr = fp.nr[f];
+  if (nr == 0) {
+    *key = v;
+    return true;
+  }
+  const int32_t *ra = fp.ra[f], *rb = fp.rb[f];
+  for (int k = 0; k < nr; k++) {
+    const int32_t a = ra[k], b = rb[k];
+    if (fp.isfloat[f]) {
+      const float x = __int_as_float(v);
+      if (x < __int_as_float(a)) continue;
+      if (x >= __int_as_float(b)) continue;
+    } else {
+      if (v < a) continue;
+      if (v >= b) continue;
+    }
+    *key = a;
+    return true;
+  }
+  return false;
+}
+
+// key k of a run: its 12-byte head is units 0-1, its 6-byte keys follow
+__device__ __forceinline__ gu8 *run_key(gu8 *list, Loc lc, uint32_t k) {
+  return list + ((size_t)lc.unit + (k ? k + 1 : 0)) * 6;
+}
+
+// the survivors' votes: one record (facet, entry key, docid, value) per
+// entry a docid's run touches first (FacetEntry::m_docId == docId skips the
+// rest, 7440-7445); and each facet list's shrunk size B
+__global__ void __launch_bounds__(256) k_facet_emit(FacetPlan fp, const Counters *ctr, FacetCtr *fc, const uint32_t *skey,
+                                                    const uint64_t *sv_doc, const Loc *sv_loc, uint32_t nl,
+                                                    uint64_t *rdoc, uint64_t *rkey, int32_t *rval, uint32_t cap) {
+  const uint32_t nsurv = (uint32_t)(ctr->surv_top >> 36);
+  const int lane = threadIdx.x & 63;
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t base = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < nsurv; base += stride) {
+    const uint32_t i = base + lane;
+    const bool act = i < nsurv;
+    const bool vote = act && skey[i] != 0;
+    for (int f = 0; f < fp.nf; f++) {
+      if (fp.lid[f] < 0) continue;
+      gu8 *list = gl(fp.list[f]);
+      const Loc lc = act ? sv_loc[(uint64_t)i * nl + (uint32_t)fp.lid[f]] : Loc{0, 0};
+      unsigned long long lsum = lc.len;
+      for (int o = 32; o > 0; o >>= 1) lsum += __shfl_xor(lsum, o, 64);
+      if (lane == 0) atomicAdd(&fc->B[f], lsum);
+      const uint32_t nk = vote && lc.len >= 2 ? lc.len - 1 : 0;
+      // pass 0 counts this lane's records, pass 1 writes them
+      uint32_t n = 0, at = 0;
+      for (int pass = 0; pass < 2; pass++) {
+        if (pass == 1) {
+          uint32_t inc = n;  // inclusive scan over the wave
+          for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(inc, o, 64);
+            if (lane >= o) inc += y;
+          }
+          uint32_t wbase = 0;
+          if (lane == 63 && inc) wbase = atomicAdd(&fc->nrec, inc);
+          wbase = __shfl(wbase, 63, 64);
+          at = wbase + inc - n;
+        }
+        for (uint32_t k = 0; k < nk; k++) {
+          const int32_t v = fac_val(run_key(list, lc, k));
+          int32_t key;
+          if (!fac_bucket(fp, f, v, &key)) continue;
+          bool seen = false;
+          for (uint32_t j = 0; j < k && !seen; j++) {
+            int32_t k2;
+            seen = fac_bucket(fp, f, fac_val(run_key(list, lc, j)), &k2) && k2 == key;
+          }
+          if (seen) continue;
+          if (pass == 0) {
+            n++;
+          } else if (at < cap) {
+            rdoc[at] = sv_doc[i];
+            rkey[at] = ((uint64_t)f << 32) | (uint32_t)(key ^ (int32_t)0x80000000);
+            rval[at] = v;
+            at++;
+          }
+        }
+      }
+    }
+  }
+}
+
+__global__ void k_facet_gather(const uint32_t *idx, const uint64_t *rkey, uint32_t n, uint64_t *k2) {
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) k2[j] = rkey[idx[j]];
+}
+
+// the first record of each (facet, key) run of the sorted records
+__global__ void __launch_bounds__(256) k_facet_heads(const uint64_t *k2s, uint32_t n, FacetCtr *fc, uint32_t *segs) {
+  const int lane = threadIdx.x & 63;
+  for (uint32_t base = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < n; base += gridDim.x * blockDim.x) {
+    const uint32_t j = base + lane;
+    const bool head = j < n && (j == 0 || k2s[j] != k2s[j - 1]);
+    const uint64_t m = __ballot(head);
+    if (!m) continue;
+    uint32_t w = 0;
+    if (lane == 0) w = atomicAdd(&fc->nseg, (uint32_t)__popcll(m));
+    w = __shfl(w, 0, 64);
+    if (head) segs[w + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = j;
+  }
+}
+
+// one wave per entry: FacetEntry's count, last docid (the records are in
+// docid order), and the sum / max / min of its votes -- a gbfacetfloat
+// entry's in vote order (Posdb.cpp:7450-7540: the double sum and the float
+// compares as the reference runs them)
+__global__ void __launch_bounds__(256) k_facet_reduce(FacetPlan fp, const FacetCtr *fc, const uint64_t *k2s,
+                                                      const uint32_t *idx, uint32_t n, const uint32_t *segs,
+                                                      const uint64_t *rdoc, const int32_t *rval, gbgpu_facet_entry *out) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t nseg = fc->nseg;
+  const uint32_t nw = gridDim.x * (blockDim.x / 64);
+  for (uint32_t s = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); s < nseg; s += nw) {
+    const uint32_t st = segs[s];
+    const uint64_t key = k2s[st];
+    const int f = (int)(key >> 32);
+    const bool fl = fp.isfloat[f] != 0;
+    uint32_t cnt = 0;
+    uint64_t last = 0;
+    long long isum = 0;
+    int32_t imin = INT32_MAX, imax = INT32_MIN;
+    double fsum = 0.0;
+    float fmin = 0.0f, fmax = 0.0f;
+    for (uint32_t j0 = st;; j0 += 64) {
+      const uint32_t j = j0 + lane;
+      const bool in = j < n && k2s[j] == key;
+      const uint64_t m = __ballot(in);  // a prefix of the lanes: the run is contiguous
+      const int c = __popcll(m);
+      if (c == 0) break;
+      const uint32_t id = in ? idx[j] : 0;
+      const int32_t v = in ? rval[id] : 0;
+      const uint64_t d = in ? rdoc[id] : 0;
+      last = __shfl(d, c - 1, 64);
+      if (fl) {
+        for (int l = 0; l < c; l++) {  // every lane runs the same sequence
+          const float x = __int_as_float(__shfl(v, l, 64));
+          if (cnt == 0 && l == 0) {
+            fmin = fmax = x;
+          }
+          fsum += (double)x;
+          if (x < fmin) fmin = x;
+          if (x > fmax) fmax = x;
+        }
+      } else {
+        long long s2 = in ? (long long)v : 0;
+        int32_t mn = in ? v : INT32_MAX, mx = in ? v : INT32_MIN;
+        for (int o = 32; o > 0; o >>= 1) {
+          s2 += __shfl_xor(s2, o, 64);
+          const int32_t a = __shfl_xor(mn, o, 64), b = __shfl_xor(mx, o, 64);
+          mn = a < mn ? a : mn;
+          mx = b > mx ? b : mx;
+        }
+        isum += s2;
+        imin = mn < imin ? mn : imin;
+        imax = mx > imax ? mx : imax;
+      }
+      cnt += (uint32_t)c;
+      if (c < 64) break;
+    }
+    if (lane == 0) {
+      gbgpu_facet_entry e;
+      e.term = f;  // the facet's index here; the host names the query term
+      e.key = (int32_t)((uint32_t)key ^ 0x80000000u);
+      e.count = (int32_t)cnt;
+      e.outside = 0;
+      e.docid = (int64_t)last;
+      if (fl) {
+        e.sum = __double_as_longlong(fsum);
+        e.max = __float_as_int(fmax);
+        e.min = __float_as_int(fmin);
+      } else {
+        e.sum = isum;
+        e.max = imax;
+        e.min = imin;
+      }
+      out[s] = e;
+    }
+  }
+}
+
+// the entry of value v in facet f's table (-1: none)
+__device__ __forceinline__ int fac_find(const FacetPlan &fp, int f, int32_t v) {
+  const int32_t *t = fp.tkey[f];
+  int lo = 0, hi = fp.tn[f];
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (t[mid] < v) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo < fp.tn[f] && t[lo] == v ? lo : -1;
+}
+
+__device__ __forceinline__ void fac_count(uint32_t *lds, uint32_t *outside, bool use_lds, uint32_t e) {
+  if (use_lds) atomicAdd(lds + e, 1u);
+  else atomicAdd(outside + e, 1u);
+}
+__device__ __forceinline__ void fac_lds_init(uint32_t *lds, uint32_t et) {
+  for (uint32_t e = threadIdx.x; e < et; e += blockDim.x) lds[e] = 0;
+  __syncthreads();
+}
+__device__ __forceinline__ void fac_lds_flush(const uint32_t *lds, uint32_t et, uint32_t *outside) {
+  __syncthreads();
+  for (uint32_t e = threadIdx.x; e < et; e += blockDim.x)
+    if (lds[e]) atomicAdd(outside + e, lds[e]);
+}
+
+// countUniqueDocids over the shrunk part of the buffer: every key of every
+// survivor's run (voting or not) in an existing entry
+__global__ void __launch_bounds__(256) k_facet_outside(FacetPlan fp, const Counters *ctr, const Loc *sv_loc, uint32_t nl,
+                                                       uint32_t et, uint32_t *outside) {
+  __shared__ uint32_t s_cnt[FAC_LDS];
+  const bool use_lds = et <= (uint32_t)FAC_LDS;
+  if (use_lds) fac_lds_init(s_cnt, et);
+  const uint32_t nsurv = (uint32_t)(ctr->surv_top >> 36);
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nsurv; i += gridDim.x * blockDim.x) {
+    for (int f = 0; f < fp.nf; f++) {
+      if (fp.lid[f] < 0 || fp.tn[f] == 0) continue;
+      gu8 *list = gl(fp.list[f]);
+      const Loc lc = sv_loc[(uint64_t)i * nl + (uint32_t)fp.lid[f]];
+      const uint32_t nk = lc.len >= 2 ? lc.len - 1 : 0;
+      for (uint32_t k = 0; k < nk; k++) {
+        const int e = fac_find(fp, f, fac_val(run_key(list, lc, k)));
+        if (e >= 0) fac_count(s_cnt, outside, use_lds, fp.tbase[f] + (uint32_t)e);
+      }
+    }
+  }
+  if (use_lds) fac_lds_flush(s_cnt, et, outside);
+}
+
+// the tail's start: the walk resumes at unit B, where the list's own bytes
+// follow the shrunk runs -- possibly the second unit of a 12-byte key, read
+// as a record of the size its byte 0 claims (RdbList::getRecSize) until the
+// walk lands on a key start; one lane per facet.  tail0[f] = that start.
+__global__ void k_facet_tailhead(FacetPlan fp, const Counters *ctr, FacetCtr *fc, uint32_t *outside,
+                                 unsigned long long *tail0) {
+  const int f = threadIdx.x;
+  if (f >= fp.nf || fp.lid[f] < 0) return;
+  gu8 *list = gl(fp.list[f]);
+  const uint64_t units = fp.units[f];
+  uint64_t u = fc->B[f];
+  unsigned long long docs = ctr->surv_top >> 36;  // every survivor's run head (12 bytes)
+  while (u < units && !(list[u * 6 + 1] & 0x02)) {
+    gu8 *k = list + u * 6;
+    if (fp.tn[f]) {
+      const int e = fac_find(fp, f, fac_val(k));
+      if (e >= 0) atomicAdd(outside + fp.tbase[f] + (uint32_t)e, 1u);
+    }
+    const uint32_t rs = (k[0] & 0x04) ? 6u : (k[0] & 0x02) ? 12u : 18u;  // RdbList::getRecSize
+    if (rs > 6) docs++;
+    u += rs / 6;
+  }
+  tail0[f] = u;
+  fc->docs[f] = docs;
+}
+
+// the aligned tail: each key start from tail0 on is one record
+__global__ void __launch_bounds__(256) k_facet_tail(FacetPlan fp, FacetCtr *fc, const unsigned long long *tail0,
+                                                    uint32_t et, uint32_t *outside) {
+  __shared__ uint32_t s_cnt[FAC_LDS];
+  const bool use_lds = et <= (uint32_t)FAC_LDS;
+  if (use_lds) fac_lds_init(s_cnt, et);
+  const int lane = threadIdx.x & 63;
+  for (int f = 0; f < fp.nf; f++) {
+    if (fp.lid[f] < 0) continue;
+    gu8 *list = gl(fp.list[f]);
+    const uint64_t u0 = tail0[f], units = fp.units[f];
+    uint32_t heads = 0;
+    for (uint64_t u = u0 + blockIdx.x * blockDim.x + threadIdx.x; u < units; u += (uint64_t)gridDim.x * blockDim.x) {
+      gu8 *k = list + u * 6;
+      const uint32_t b01 = (uint32_t)k[0] | ((uint32_t)k[1] << 8);
+      if (!(b01 & 0x0200u)) continue;
+      if (!(b01 & 0x04u)) heads++;  // a 12-byte record: a new docid
+      if (fp.tn[f]) {
+        const int e = fac_find(fp, f, fac_val(k));
+        if (e >= 0) fac_count(s_cnt, outside, use_lds, fp.tbase[f] + (uint32_t)e);
+      }
+    }
+    unsigned long long h = heads;
+    for (int o = 32; o > 0; o >>= 1) h += __shfl_xor(h, o, 64);
+    if (lane == 0 && h) atomicAdd(&fc->docs[f], h);
+  }
+  if (use_lds) fac_lds_flush(s_cnt, et, outside);
+}
+
+// The facet tables of the slot's collected query (see k_facet_emit): into
+// out->facets (term then key ascending) and out->facet_docs.
+static int facet_pass(QuerySlot &q, uint32_t nsurv, gbgpu_result *out) {
+  const int nf = (int)q.facets.size();
+  hipStream_t st = q.stream;
+  FacetPlan fp;
+  std::memset(&fp, 0, sizeof fp);
+  fp.nf = nf;
+  uint64_t cap = 0;
+  size_t nranges = 0;
+  for (int f = 0; f < nf; f++) {
+    const FacetTerm &t = q.facets[f];
+    fp.lid[f] = t.lid;
+    fp.isfloat[f] = t.isfloat;
+    fp.nr[f] = (int)t.a.size();
+    fp.units[f] = t.units;
+    fp.list[f] = t.list;
+    if (t.lid >= 0) cap += t.units;
+    nranges += t.a.size();
+  }
+  const bool dev = cap > 0;
+  // entries: the votes' and the ranges' (the ranges' A values stand as
+  // entries from allocTopTree on, Posdb.cpp:5575-5631)
+  std::vector<std::vector<gbgpu_facet_entry>> tab((size_t)nf);
+  uint32_t nrec = 0, nseg = 0;
+  const DevPlan *hpl = reinterpret_cast<const DevPlan *>(q.h_stage);
+  const uint32_t nl = (uint32_t)std::max(hpl->nlists, 1);
+  size_t o_ctr = 0, o_rng = 0, o_rdoc = 0, o_rkey = 0, o_rval = 0, o_k1 = 0, o_k1s = 0, o_i0 = 0, o_i1 = 0, o_k2 = 0,
+         o_k2s = 0, o_i2 = 0, o_seg = 0, o_ent = 0, o_tkey = 0, o_out = 0, o_t0 = 0, o_tmp = 0;
+  const uint64_t ecap = cap + nranges + 1;  // table entries: distinct voted keys + ranges
+  if (dev) {
+    if (cap >= (1ull << 31)) return GBGPU_ECAPACITY;
+    size_t tmp1 = 0, tmp2 = 0;
+    HIPCHECK(si_sort_pairs(nullptr, tmp1, nullptr, nullptr, nullptr, nullptr, (uint32_t)cap, st, 38));
+    HIPCHECK(si_sort_pairs(nullptr, tmp2, nullptr, nullptr, nullptr, nullptr, (uint32_t)cap, st, 34));
+    size_t o = 0;
+    auto take = [&](size_t bytes) {
+      const size_t at = o;
+      o += align256(bytes);
+      return at;
+    };
+    o_ctr = take(sizeof(FacetCtr));
+    o_rng = take(8 * std::max<size_t>(nranges, 1));
+    o_rdoc = take(8 * cap);
+    o_rkey = take(8 * cap);
+    o_rval = take(4 * cap);
+    o_k1 = take(8 * cap);
+    o_k1s = take(8 * cap);
+    o_i0 = take(4 * cap);
+    o_i1 = take(4 * cap);
+    o_k2 = take(8 * cap);
+    o_k2s = take(8 * cap);
+    o_i2 = take(4 * cap);
+    o_seg = take(4 * cap);
+    o_ent = take(sizeof(gbgpu_facet_entry) * cap);
+    o_tkey = take(4 * ecap);
+    o_out = take(4 * ecap);
+    o_t0 = take(8 * MAXF);
+    o_tmp = take(std::max(tmp1, tmp2));
+    if (q.fac.ensure(o)) return ENOMEM;
+    std::vector<int32_t> rng;
+    size_t r = 0;
+    for (int f = 0; f < nf; f++) {
+      const FacetTerm &t = q.facets[f];
+      fp.ra[f] = q.fac.as<int32_t>(o_rng) + r;
+      rng.insert(rng.end(), t.a.begin(), t.a.end());
+      r += t.a.size();
+    }
+    for (int f = 0; f < nf; f++) {
+      const FacetTerm &t = q.facets[f];
+      fp.rb[f] = q.fac.as<int32_t>(o_rng) + r;
+      rng.insert(rng.end(), t.b.begin(), t.b.end());
+      r += t.b.size();
+    }
+    HIPCHECK(hipMemsetAsync(q.fac.as<uint8_t>(o_ctr), 0, sizeof(FacetCtr), st));
+    if (!rng.empty())
+      HIPCHECK(hipMemcpyAsync(q.fac.as<uint8_t>(o_rng), rng.data(), 4 * rng.size(), hipMemcpyHostToDevice, st));
+    FacetCtr *dfc = q.fac.as<FacetCtr>(o_ctr);
+    if (nsurv) {
+      const uint32_t g = std::max(1u, std::min<uint32_t>(2048, (nsurv + 255) / 256));
+      hipLaunchKernelGGL(k_facet_emit, dim3(g), dim3(256), 0, st, fp, (const Counters *)q.res.as<Counters>(), dfc,
+                         (const uint32_t *)q.skey.as<uint32_t>(), (const uint64_t *)q.svdoc.as<uint64_t>(),
+                         (const Loc *)q.svloc.as<Loc>(), nl, q.fac.as<uint64_t>(o_rdoc), q.fac.as<uint64_t>(o_rkey),
+                         q.fac.as<int32_t>(o_rval), (uint32_t)cap);
+      HIPCHECK(hipGetLastError());
+      HIPCHECK(hipMemcpyAsync(&nrec, &dfc->nrec, 4, hipMemcpyDeviceToHost, st));
+      HIPCHECK(hipStreamSynchronize(st));
+    }
+    if (nrec > cap) return GBGPU_ECORRUPT;  // runs are disjoint parts of the lists: not reached
+    if (nrec) {
+      const uint32_t g = std::max(1u, std::min<uint32_t>(2048, (nrec + 255) / 256));
+      // docid order, then (facet, key) order, stable: each entry's votes as the reference casts them
+      hipLaunchKernelGGL(k_si_keys, dim3(g), dim3(256), 0, st, (const uint64_t *)q.fac.as<uint64_t>(o_rdoc), nrec,
+                         q.fac.as<uint64_t>(o_k1), q.fac.as<uint32_t>(o_i0));
+      size_t tb = std::max(tmp1, tmp2);
+      HIPCHECK(si_sort_pairs(q.fac.as<uint8_t>(o_tmp), tb, q.fac.as<uint64_t>(o_k1), q.fac.as<uint64_t>(o_k1s),
+                             q.fac.as<uint32_t>(o_i0), q.fac.as<uint32_t>(o_i1), nrec, st, 38));
+      hipLaunchKernelGGL(k_facet_gather, dim3(g), dim3(256), 0, st, (const uint32_t *)q.fac.as<uint32_t>(o_i1),
+                         (const uint64_t *)q.fac.as<uint64_t>(o_rkey), nrec, q.fac.as<uint64_t>(o_k2));
+      tb = std::max(tmp1, tmp2);
+      HIPCHECK(si_sort_pairs(q.fac.as<uint8_t>(o_tmp), tb, q.fac.as<uint64_t>(o_k2), q.fac.as<uint64_t>(o_k2s),
+                             q.fac.as<uint32_t>(o_i1), q.fac.as<uint32_t>(o_i2), nrec, st, 34));
+      hipLaunchKernelGGL(k_facet_heads, dim3(g), dim3(256), 0, st, (const uint64_t *)q.fac.as<uint64_t>(o_k2s), nrec,
+                         dfc, q.fac.as<uint32_t>(o_seg));
+      hipLaunchKernelGGL(k_facet_reduce, dim3(std::max(1u, std::min<uint32_t>(4096, (nrec + 3) / 4))), dim3(256), 0, st,
+                         fp, (const FacetCtr *)dfc, (const uint64_t *)q.fac.as<uint64_t>(o_k2s),
+                         (const uint32_t *)q.fac.as<uint32_t>(o_i2), nrec, (const uint32_t *)q.fac.as<uint32_t>(o_seg),
+                         (const uint64_t *)q.fac.as<uint64_t>(o_rdoc), (const int32_t *)q.fac.as<int32_t>(o_rval),
+                         q.fac.as<gbgpu_facet_entry>(o_ent));
+      HIPCHECK(hipGetLastError());
+      HIPCHECK(hipMemcpyAsync(&nseg, &dfc->nseg, 4, hipMemcpyDeviceToHost, st));
+      HIPCHECK(hipStreamSynchronize(st));
+      if (nseg > nrec) return GBGPU_ECORRUPT;
+      std::vector<gbgpu_facet_entry> ents(nseg);
+      if (nseg) {
+        HIPCHECK(hipMemcpyAsync(ents.data(), q.fac.as<uint8_t>(o_ent), sizeof(gbgpu_facet_entry) * nseg,
+                                hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipStreamSynchronize(st));
+      }
+      for (const gbgpu_facet_entry &e : ents) tab[(size_t)e.term].push_back(e);
+    }
+  }
+  // the tables: votes and ranges, by key
+  uint32_t et = 0;
+  std::vector<int32_t> tkeys;
+  for (int f = 0; f < nf; f++) {
+    auto &t = tab[(size_t)f];
+    std::sort(t.begin(), t.end(), [](const gbgpu_facet_entry &x, const gbgpu_facet_entry &y) { return x.key < y.key; });
+    for (int32_t a : q.facets[f].a) {
+      auto it = std::lower_bound(t.begin(), t.end(), a,
+                                 [](const gbgpu_facet_entry &x, int32_t k) { return x.key < k; });
+      if (it != t.end() && it->key == a) continue;
+      gbgpu_facet_entry z;
+      std::memset(&z, 0, sizeof z);
+      z.key = a;
+      t.insert(it, z);
+    }
+    for (auto &e : t) e.term = q.facets[f].term;
+    fp.tbase[f] = et;
+    fp.tn[f] = (int)t.size();
+    for (auto &e : t) tkeys.push_back(e.key);
+    et += (uint32_t)t.size();
+  }
+  std::vector<uint32_t> outside(et, 0);
+  std::vector<uint64_t> docs((size_t)nf, 0);
+  if (dev) {
+    if (et > ecap) return GBGPU_ECORRUPT;
+    for (int f = 0; f < nf; f++) fp.tkey[f] = q.fac.as<int32_t>(o_tkey) + fp.tbase[f];
+    FacetCtr *dfc = q.fac.as<FacetCtr>(o_ctr);
+    uint32_t *dout = q.fac.as<uint32_t>(o_out);
+    if (et) {
+      HIPCHECK(hipMemcpyAsync(q.fac.as<uint8_t>(o_tkey), tkeys.data(), 4 * (size_t)et, hipMemcpyHostToDevice, st));
+      HIPCHECK(hipMemsetAsync(dout, 0, 4 * (size_t)et, st));
+    }
+    if (nsurv && et) {
+      const uint32_t g = std::max(1u, std::min<uint32_t>(1024, (nsurv + 255) / 256));
+      hipLaunchKernelGGL(k_facet_outside, dim3(g), dim3(256), 0, st, fp, (const Counters *)q.res.as<Counters>(),
+                         (const Loc *)q.svloc.as<Loc>(), nl, et, dout);
+    }
+    hipLaunchKernelGGL(k_facet_tailhead, dim3(1), dim3(64), 0, st, fp, (const Counters *)q.res.as<Counters>(), dfc,
+                       dout, q.fac.as<unsigned long long>(o_t0));
+    uint64_t tu = 0;
+    for (int f = 0; f < nf; f++) tu = std::max<uint64_t>(tu, fp.units[f]);
+    const uint32_t g = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(2048, (tu + 255) / 256));
+    hipLaunchKernelGGL(k_facet_tail, dim3(g), dim3(256), 0, st, fp, dfc,
+                       (const unsigned long long *)q.fac.as<unsigned long long>(o_t0), et, dout);
+    HIPCHECK(hipGetLastError());
+    FacetCtr hc;
+    if (et) HIPCHECK(hipMemcpyAsync(outside.data(), dout, 4 * (size_t)et, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipMemcpyAsync(&hc, dfc, sizeof hc, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipStreamSynchronize(st));
+    for (int f = 0; f < nf; f++) docs[(size_t)f] = q.facets[f].lid >= 0 ? hc.docs[f] : 0;
+  }
+  int n = 0;
+  std::vector<int> order((size_t)nf);
+  for (int f = 0; f < nf; f++) order[(size_t)f] = f;
+  std::sort(order.begin(), order.end(), [&](int x, int y) { return q.facets[x].term < q.facets[y].term; });
+  for (int f : order) {
+    auto &t = tab[(size_t)f];
+    for (size_t k = 0; k < t.size(); k++) {
+      t[k].outside = (int32_t)outside[fp.tbase[f] + k];
+      if (out->facets && n < out->facets_cap) out->facets[n] = t[k];
+      n++;
+    }
+    if (out->facet_docs) out->facet_docs[q.facets[f].term] = docs[(size_t)f];
+  }
+  out->n_facets = n;
+  return out->facets && n > out->facets_cap ? ENOSPC : 0;
+}
+
 // hits_acc: when non-null, the query's intersected docids are appended to it
 // (docid splits gather them over the pieces) instead of being written to out
 static int collect(gbgpu_ctx *ctx, QuerySlot &q, gbgpu_result *out, std::vector<int64_t> *hits_acc = nullptr) {
@@ -6616,13 +7205,19 @@ static int collect(gbgpu_ctx *ctx, QuerySlot &q, gbgpu_result *out, std::vector<
   out->n_hit_docids = 0;
   out->n_docid_scores = out->n_pair_scores = out->n_single_scores = 0;
   out->docs_wanted = q.docs_wanted;
+  out->n_facets = 0;
+  if (out->facet_docs)  // the facet pass sets the terms with a table
+    for (int t = 0; t < q.info_nterms; t++) out->facet_docs[t] = 0;
   if (q.early) {
     (void)hipStreamSynchronize(q.stream);  // nothing of this query; a failed one's kernels
     q.held.clear();
     return 0;
   }
   const hipError_t se = hipStreamSynchronize(q.stream);
-  q.held.clear();  // the lists may go now (gbgpu_list_free while in flight)
+  // the lists may go once this returns (gbgpu_list_free while in flight);
+  // the facet pass still reads them
+  std::vector<std::shared_ptr<ListMem>> held;
+  held.swap(q.held);
   if (se != hipSuccess) {
     std::fprintf(stderr, "gbgpu: query stream failed: %s\n", hipGetErrorString(se));
     return GBGPU_EHIP;
@@ -6710,6 +7305,10 @@ static int collect(gbgpu_ctx *ctx, QuerySlot &q, gbgpu_result *out, std::vector<
     n++;
   }
   out->n = n;
+  if (!q.facets.empty() && (out->facets || out->facet_docs)) {
+    const int rc = facet_pass(q, (uint32_t)out->hits, out);
+    if (rc) return rc;
+  }
   if (q.want_info) return score_info(q, keys, docs, (uint32_t)out->hits, out);
   return 0;
 }

@@ -101,7 +101,9 @@ int build_host_plan(const gbgpu_qterm *qt, int nqt, const int64_t *sizes, const 
       hp->sortby_group = nrg;
       hp->sortby_int = sortbyi;
     }
-    ok &= add(i, (uint8_t)(piped | (qt[i].term_sign == '-' ? BF_NEGATIVE : 0) | (number ? BF_NUMBER : 0)));
+    const bool facet = qt[i].field_code >= FIELD_GBFACETSTR && qt[i].field_code <= FIELD_GBFACETFLOAT;
+    ok &= add(i, (uint8_t)(piped | (qt[i].term_sign == '-' ? BF_NEGATIVE : 0) | (number ? BF_NUMBER : 0) |
+                           (facet ? BF_FACET : 0)));  // Posdb.cpp:4572-4602
     if (left >= 0 && !leftAdded) {
       ok &= add(left, piped | BF_BIGRAM);
       for (int k = 0; k < nqt; k++)

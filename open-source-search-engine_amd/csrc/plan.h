@@ -71,7 +71,6 @@ enum : int32_t {
   FIELD_GBNUMBEREQUALFLOAT = 67,
 };
 // a field code the GPU path does not implement (range, int sortby, facets)
-inline bool field_unsupported(int32_t fc) { return fc >= FIELD_GBFACETSTR && fc <= FIELD_GBFACETFLOAT; }
 // range terms: (mode, int?) of a field code, mode 0 if not one
 inline int range_mode(int32_t fc, int *is_int) {
   *is_int = fc == FIELD_GBNUMBERMININT || fc == FIELD_GBNUMBERMAXINT || fc == FIELD_GBNUMBEREQUALINT;

@@ -1,6 +1,6 @@
 // Docid sort of the survivors for the second pass's getWordPosList
-// emulation (engine.hip, score_info): a hipcub radix sort kept in its own
-// translation unit.
+// emulation (engine.hip, score_info) and of the facet votes (facet_pass): a
+// hipcub radix sort kept in its own translation unit.
 #ifndef GBGPU_SISORT_H
 #define GBGPU_SISORT_H
 
@@ -9,10 +9,10 @@
 #include <stdint.h>
 
 namespace gbgpu {
-// (docid, survivor index) pairs by docid (38-bit keys); tmp == nullptr
-// returns the scratch size in tmp_bytes
+// (key, index) pairs by the key's low end_bit bits (docids: 38), stable;
+// tmp == nullptr returns the scratch size in tmp_bytes
 hipError_t si_sort_pairs(void *tmp, size_t &tmp_bytes, const uint64_t *kin, uint64_t *kout, const uint32_t *vin,
-                         uint32_t *vout, uint32_t n, hipStream_t st);
+                         uint32_t *vout, uint32_t n, hipStream_t st, int end_bit = 38);
 }  // namespace gbgpu
 
 #endif

@@ -220,7 +220,15 @@ class Result(ctypes.Structure):
         ("single_scores", ctypes.c_void_p), ("single_scores_cap", ctypes.c_int32),
         ("n_single_scores", ctypes.c_int32),
         ("int_scores", ctypes.POINTER(ctypes.c_int32)),
+        ("facets", ctypes.c_void_p), ("facets_cap", ctypes.c_int32), ("n_facets", ctypes.c_int32),
+        ("facet_docs", ctypes.POINTER(ctypes.c_uint64)),
     ]
+
+
+# gbgpu_facet_entry: one entry of a facet term's QueryTerm::m_facetHashTable
+FACET_DT = np.dtype([("term", "<i4"), ("key", "<i4"), ("count", "<i4"), ("outside", "<i4"), ("docid", "<i8"),
+                     ("sum", "<i8"), ("max", "<i4"), ("min", "<i4")])
+FACET_FIELDS = (63, 64, 65)  # gbfacetstr: / gbfacetint: / gbfacetfloat:
 
 
 class SynthCorpus(ctypes.Structure):
@@ -497,6 +505,9 @@ class QueryResult:
     single_scores: Optional[np.ndarray] = None
     # TopNode::m_intScore under a gbsortby int term (scores are then 0.0)
     int_scores: Optional[np.ndarray] = None
+    # facet terms: {term: (m_numDocsThatHaveFacet, {key: (count, outside,
+    # docid, sum, max, min)})}, the tables QueryTerm::m_facetHashTable holds
+    facets: Optional[dict] = None
 
 
 class Engine:
@@ -597,8 +608,10 @@ class Engine:
         return (np.zeros(nd, DOCID_DT), np.zeros(max(1, nd * ng * (ng - 1) // 2 * rmt), PAIR_DT),
                 np.zeros(nd * ng * rmt, SINGLE_DT))
 
-    @staticmethod
-    def _result(cap: int, hit_cap: int = 0, info=None):
+    facet_cap = 1 << 16  # facet table entries a result holds
+
+    @classmethod
+    def _result(cls, cap: int, hit_cap: int = 0, info=None, nfacet_terms: int = 0, fterms=()):
         d = (ctypes.c_int64 * max(cap, 1))()
         s = (ctypes.c_float * max(cap, 1))()
         r = Result(ctypes.cast(d, ctypes.POINTER(ctypes.c_int64)), ctypes.cast(s, ctypes.POINTER(ctypes.c_float)),
@@ -614,7 +627,18 @@ class Engine:
             r.docid_scores, r.docid_scores_cap = info[0].ctypes.data, len(info[0])
             r.pair_scores, r.pair_scores_cap = info[1].ctypes.data, len(info[1])
             r.single_scores, r.single_scores_cap = info[2].ctypes.data, len(info[2])
+        r._fac = None
+        if nfacet_terms:
+            r._fac = (np.zeros(cls.facet_cap, FACET_DT), np.zeros(nfacet_terms, np.uint64), fterms)
+            r.facets, r.facets_cap = r._fac[0].ctypes.data, cls.facet_cap
+            r.facet_docs = r._fac[1].ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))
         return r, d, s, h
+
+    @staticmethod
+    def _facet_terms(terms):
+        """(facet_docs entries, the facet terms) of a request: its terms, when one is a facet term"""
+        ft = [i for i, t in enumerate(terms) if t.field_code in FACET_FIELDS]
+        return (len(terms) if ft else 0), ft
 
     @staticmethod
     def _pack(r, d, s, h=None, info=None) -> QueryResult:
@@ -627,6 +651,12 @@ class Engine:
             q.docid_scores = info[0][:r.n_docid_scores].copy()
             q.pair_scores = info[1][:r.n_pair_scores].copy()
             q.single_scores = info[2][:r.n_single_scores].copy()
+        if r._fac is not None:
+            ents, docs, fterms = r._fac
+            q.facets = {t: (int(docs[t]), {}) for t in fterms}
+            for e in ents[:r.n_facets]:
+                q.facets[int(e["term"])][1][int(e["key"])] = tuple(
+                    int(e[f]) for f in ("count", "outside", "docid", "sum", "max", "min"))
         return q
 
     @staticmethod
@@ -646,7 +676,7 @@ class Engine:
         qt = (QTerm * max(n, 1))(*terms)
         keep, refs = lists if isinstance(lists, tuple) else self.host_lists(lists)
         info = self.info_arrays(params, n)
-        r, d, s, h = self._result(cap, hit_cap, info)
+        r, d, s, h = self._result(cap, hit_cap, info, *self._facet_terms(terms))
         _check(self.lib.gbgpu_query(self.ctx, qt, n, refs, ctypes.byref(params), ctypes.byref(r)), "query")
         return self._pack(r, d, s, h, info)
 
@@ -656,7 +686,7 @@ class Engine:
         qt = (QTerm * max(n, 1))(*terms)
         hh = (ctypes.c_int32 * max(n, 1))(*handles)
         info = self.info_arrays(params, n)
-        r, d, s, h = self._result(cap, hit_cap, info)
+        r, d, s, h = self._result(cap, hit_cap, info, *self._facet_terms(terms))
         _check(self.lib.gbgpu_query_resident(self.ctx, qt, n, hh, ctypes.byref(params), ctypes.byref(r)), "query")
         return self._pack(r, d, s, h, info)
 
@@ -672,8 +702,9 @@ class Engine:
         hh = (ctypes.c_int32 * max(n, 1))(*handles)
         _check(self.lib.gbgpu_query_slot_enqueue(self.ctx, slot, qt, n, hh, ctypes.byref(params)), "enqueue")
 
-    def collect(self, cap: int = 4096, slot: int = 0, hit_cap: int = 0) -> QueryResult:
-        r, d, s, h = self._result(cap, hit_cap)
+    def collect(self, cap: int = 4096, slot: int = 0, hit_cap: int = 0, terms=()) -> QueryResult:
+        """terms: the enqueued query's terms, for its facet tables"""
+        r, d, s, h = self._result(cap, hit_cap, None, *self._facet_terms(terms))
         _check(self.lib.gbgpu_query_slot_collect(self.ctx, slot, ctypes.byref(r)), "collect")
         return self._pack(r, d, s, h)
 

@@ -562,6 +562,28 @@ def save_boolean():
     save_query("bool_synonyms", q.terms, lists, bool_params(q.params(), [-3, 0, -1, 1]))
 
 
+def save_capacity():
+    """Plans near the reference's own capacities: a TopTree beyond 1 536
+    nodes (docsToGet 2 000 and 3 000 make m_docsWanted 4 000 and 6 000,
+    Posdb.cpp:838-900), a 10-word query with its bigrams and synonyms (23
+    lists, 10 groups) and a 12-word one over 32 lists (12 groups of up to
+    four sublists)."""
+    from workload import Word, build_query
+    N = 20000
+    q = build_query("dense_k", [Word("x", 0.9), Word("y", 0.8)], N, seed=31)
+    lists = generate(q, N, seed=3100)
+    for dtg in (2000, 3000):
+        q.docs_to_get = dtg
+        r = save_query(f"cap_docs{dtg}", q.terms, lists, q.params())
+        print(f"q_cap_docs{dtg}: hits={r['hits']} n={len(r['docids'])} dw={r['docs_wanted']}")
+    for nw, nsyn, p in ((10, 4, 0.8), (12, 9, 0.85)):
+        words = [Word(f"w{i}", p, synonyms=(0.15,) if i < nsyn else ()) for i in range(nw)]
+        q = build_query(f"words{nw}", words, 8000, seed=32 + nw, docs_to_get=50)
+        lists = generate(q, 8000, seed=3200 + nw)
+        r = save_query(f"cap_words{nw}", q.terms, lists, q.params())
+        print(f"q_cap_words{nw}: lists={len(lists)} hits={r['hits']} n={len(r['docids'])}")
+
+
 def split_runs(lst, nruns, rng, dup_frac=0.08, del_frac=0.04):
     """One termlist's keys spread over nruns runs (oldest first) the way a
     termlist lies in tiered Posdb files plus the tree: each key in one run;
@@ -711,6 +733,7 @@ def main():
     save_range()
     save_boolean()
     save_facets()
+    save_capacity()
     save_msg5()
     save_msg3a()
     cases = [(0, -1), (1, -1), (0, 5000), (1, 5000), (0, 1)]

@@ -65,6 +65,8 @@ def same_tree(cpu, gpu, label, msg39=False):
         fields = ("hits", "filtered", "docs_wanted", "corrupt")
     for f in fields:
         assert gpu[f] == cpu[f], (label, f, gpu[f], cpu[f])
+    # the facet terms' QueryTerm::m_facetHashTable and m_numDocsThatHaveFacet
+    assert gpu["facets"] == cpu["facets"], label
 
 
 def splits(params):

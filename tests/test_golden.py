@@ -126,4 +126,4 @@ def test_gpu_query_vs_reference(engine, path):
     terms, lists, params, exp = load_query(path)
     r = engine.query(terms, lists, params, cap=1 << 16, hit_cap=max(1, exp["hits"]))
     check(dict(docids=r.docids, scores=r.scores, hits=r.hits, docs_wanted=r.docs_wanted, filtered=r.filtered,
-               hit_docids=r.hit_docids), exp, os.path.basename(path))
+               hit_docids=r.hit_docids, facets=r.facets), exp, os.path.basename(path))
