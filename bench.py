@@ -378,7 +378,9 @@ def main():
     total = per * world
     # GBGPU_DIAG=1: the diagnostic build (lib/libgbgpu_diag.so), whose
     # GBGPU_*_MODE switches time kernel phases; never the measured product
-    eng = gbgpu.Engine(local_rank, diag=os.environ.get("GBGPU_DIAG") == "1")
+    # GBGPU_LIB=alt: the A/B build (lib/libgbgpu_alt.so, Makefile `alt`)
+    eng = gbgpu.Engine(local_rank, diag=os.environ.get("GBGPU_DIAG") == "1",
+                       path=gbgpu.ALT_LIB_PATH if os.environ.get("GBGPU_LIB") == "alt" else None)
     exchange = world > 1 or args.exchange
     if exchange and world == 1:
         eng.comm_init(1, 0, gbgpu.Engine.comm_unique_id())

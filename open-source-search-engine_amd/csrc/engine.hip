@@ -2613,6 +2613,14 @@ __constant__ Weights c_weights;
 // the survivor's arena range (k_compact's prefix sum of its run units), then
 // score_doc (scoring.h) over them.
 constexpr int SCORE_TPB = 64;
+// the two-group variant's LDS records per lane and waves per SIMD it is
+// compiled for (A/B builds override them: Makefile `alt`)
+#ifndef GBGPU_SCORE_RC2
+#define GBGPU_SCORE_RC2 24
+#endif
+#ifndef GBGPU_SCORE_WAVES2
+#define GBGPU_SCORE_WAVES2 1
+#endif
 
 // a unit's 6 bytes as one u16 and one u32 load (units are 2-byte aligned;
 // which half is 4-byte aligned depends on the unit's parity)
@@ -3076,7 +3084,8 @@ __device__ __forceinline__ void hist_add(uint32_t *h, uint32_t key, int lane) {
 // data (slot, list mask, units, run locations) is read at its position, so
 // a wave's reads are contiguous; its key goes to skey at the same position.
 template <int NQ, int NS, int RC>
-__global__ void __launch_bounds__(SCORE_TPB) k_score(const DevPlan *__restrict__ pl, const uint64_t *sv_doc, Counters *ctr,
+__global__ void __launch_bounds__(SCORE_TPB, (NQ <= 2 && NS <= 2) ? GBGPU_SCORE_WAVES2 : 1)
+    k_score(const DevPlan *__restrict__ pl, const uint64_t *sv_doc, Counters *ctr,
                                                      const uint32_t *sv_slot, const uint32_t *sv_lm,
                                                      const uint32_t *sv_u, const Loc *sv_loc, uint64_t *arena,
                                                      unsigned long long arena_cap, uint32_t *skey, uint8_t *sflag,
@@ -6325,7 +6334,7 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
                       : (hp.ngroups <= 4 && maxsub <= 4) ? 1
                       : (hp.ngroups <= 8 && maxsub <= 4) ? 2
                                                          : 3;
-  static constexpr uint32_t kRC[5] = {24, 48, 64, 64, 24};  // LDS records per lane
+  static constexpr uint32_t kRC[5] = {24, 48, 64, 64, GBGPU_SCORE_RC2};  // LDS records per lane
   const uint32_t rcap = kRC[variant] / 2;  // size buckets: a column holds 2x a bucket-3 survivor's units
   const uint64_t *dcand = q.cand.as<uint64_t>();
   const uint32_t *dcunit = q.cunit.as<uint32_t>();

@@ -274,6 +274,7 @@ EXPORTS = [
 ]
 
 DIAG_LIB_PATH = os.path.join(PKG_DIR, "lib", "libgbgpu_diag.so")
+ALT_LIB_PATH = os.path.join(PKG_DIR, "lib", "libgbgpu_alt.so")  # an A/B build (Makefile `alt`), bench.py only
 _libs = {}
 
 
@@ -514,8 +515,8 @@ class Engine:
     """One gbgpu context on one device: resident lists shared by its query
     slots (one HIP stream each; a context starts with one slot)."""
 
-    def __init__(self, device: int = 0, diag: bool = False):
-        self.lib = load(DIAG_LIB_PATH if diag else LIB_PATH)
+    def __init__(self, device: int = 0, diag: bool = False, path: Optional[str] = None):
+        self.lib = load(path or (DIAG_LIB_PATH if diag else LIB_PATH))
         self.ctx = ctypes.c_void_p()
         _check(self.lib.gbgpu_open(device, ctypes.byref(self.ctx)), "gbgpu_open")
         self._keep = {}
