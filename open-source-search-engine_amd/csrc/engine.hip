@@ -95,7 +95,7 @@ struct ListExt {
 struct Counters {
   uint32_t filtered;  // m_filtered: scored docids dropped by the paging filter (Posdb.cpp:7327-7347)
   uint32_t corrupt;
-  unsigned long long surv_top;  // survivors << 36 | their run units (k_cmp_write block 0)
+  unsigned long long surv_top;  // survivors << 36 | their run units (k_cmp_scan)
   uint32_t g0count[MAXG0];
   uint32_t anysurv;  // bit l: list l has a run in some survivor
   uint32_t tree_n;   // site clustering: TopTree nodes written by k_tree_replay
@@ -105,9 +105,11 @@ struct Counters {
   uint32_t rdbg_t, rdbg_total;  // diagnostic: replay us in tree_add / in all
   unsigned long long dmax_all;  // largest survivor docid
   ListExt ext[MAXL];
-  uint32_t bcnt[8];    // survivors per size bucket (k_cmp_write block 0), NBKT
+  uint32_t bcnt[8];    // survivors per size bucket (k_cmp_scan), NBKT
   uint32_t bstart[8];  // each bucket's first survivor position
   unsigned long long arena_top;  // global record arena: units handed out (k_ext_walk, k_score, k_scoreinfo)
+  uint32_t nstale;               // survivors whose trailing group merged empty (k_score: the stale list)
+  uint32_t pad2;
 };
 
 // top-k select state (k_score's histogram, k_topk's gathers)
@@ -1909,12 +1911,15 @@ __global__ void k_range_filter(const DevPlan *__restrict__ pl, uint32_t rbits, u
 // slot is voted by its own list only through the probe, which credits a
 // docid to the first array holding it) and its bits in the probe bitmaps.
 //
-// Two passes over the slots, CB threads x CSPT consecutive slots a block:
+// Two passes over the slots, CWORDS bitmap words (CTILE slots) a block of
+// CB threads -- a word a thread for the bit-parallel vote test, then the
+// block's survivors spread over all CB threads, so each thread waits on the
+// run locations of about one survivor:
 //   k_cmp_count  survivors per size bucket of each block, the lists with a
 //                run in some survivor, the re-shrink partials (BlkInfo);
-//   k_cmp_write  each block's offset in every bucket and the bucket starts
-//                (from the counts), then every survivor's record at its
-//                final position -- buckets
+//   k_cmp_scan   one block: each block's offset in every bucket, the bucket
+//                starts and the totals;
+//   k_cmp_write  every survivor's record at its final position -- buckets
 //                in order, slot order inside a bucket: slot, list mask, run
 //                units, docid, and its run locations ([pos][nl]), so k_score
 //                reads its survivors' data contiguously.
@@ -1934,13 +1939,19 @@ __host__ __device__ __forceinline__ int size_bucket(uint32_t u, uint32_t rc) {
 __host__ __device__ __forceinline__ int bucket_shift(int b) { return b == 0 ? 3 : b == 1 ? 4 : b == 2 ? 5 : 6; }
 
 constexpr int CB = 256;            // compaction threads per block
-constexpr int CSPT = 32;           // consecutive slots per thread: one bitmap word
-constexpr int CTILE = CB * CSPT;   // 8192 slots per block (one block scan: <= 2^16 per bucket)
+constexpr int CSPT = 32;           // consecutive slots per bitmap word
+#ifndef GBGPU_CWORDS
+#define GBGPU_CWORDS 64
+#endif
+constexpr int CWORDS = GBGPU_CWORDS;  // bitmap words per block (threads 0..CWORDS-1 test them)
+static_assert(CWORDS <= CB, "a word a thread");
+constexpr int CTILE = CWORDS * CSPT;  // 2048 slots per block (one block scan: <= 2^16 per bucket)
 static_assert(CTILE < 65536, "packed 16-bit bucket counts");
 constexpr int XR = 4;              // re-shrunk lists reduced per block (more: global atomics)
 
 struct BlkInfo {
-  uint32_t cnt[NBKT];  // survivors per bucket; k_cmp_write sums them into the block's offsets
+  uint32_t cnt[NBKT];  // survivors per bucket
+  uint32_t pre[NBKT];  // k_cmp_scan: survivors per bucket in the blocks before this one
   uint32_t any, pad;   // lists with a run in some survivor of the block
   unsigned long long usum;       // the survivors' run units (their records' upper bound)
   unsigned long long dall;       // largest survivor docid (re-shrink queries)
@@ -2168,10 +2179,10 @@ __global__ void __launch_bounds__(CB) k_cmp_count(const DevPlan *__restrict__ pl
     s_dall = 0;
     s_usum = 0;
   }
-  const uint32_t w = blockIdx.x * CB + threadIdx.x;
+  const uint32_t w = blockIdx.x * CWORDS + threadIdx.x;
   CmpWord c;
   c.surv = 0;
-  if (w < nwords) cmp_word(pl, ctr, bits, nwords, w, c);
+  if (threadIdx.x < CWORDS && w < nwords) cmp_word(pl, ctr, bits, nwords, w, c);
   uint32_t total;
   const uint32_t ex = block_exclusive_scan<CB>(__popc(c.surv), tmp, &total);
   const uint32_t xmask = pl->reshare_mask;
@@ -2257,66 +2268,41 @@ __global__ void __launch_bounds__(CB) k_cmp_count(const DevPlan *__restrict__ pl
   }
 }
 
-// Pass 2: every survivor's record at its final position -- buckets in
-// order, slot order inside a bucket: slot, list mask, run units, docid, and
-// its run locations ([pos][nl]), so k_score reads its survivors' data
-// contiguously.  Each block sums the counts of the blocks before it (its
-// offsets) and of all blocks (the bucket starts); block 0 publishes the
-// totals.  sv_ord (site clustering): each record's survivor's rank in slot
-// order, where the replay wants it.
-__global__ void __launch_bounds__(CB) k_cmp_write(const DevPlan *__restrict__ pl, Counters *__restrict__ ctr,
-                                                  const uint32_t *__restrict__ cunit, const uint32_t *__restrict__ bits,
-                                                  uint32_t nwords, const Loc *__restrict__ loc,
-                                                  const uint64_t *__restrict__ cand, uint32_t rc,
-                                                  const BlkInfo *__restrict__ blk, uint32_t nblk,
-                                                  uint32_t *__restrict__ sv_slot, uint32_t *__restrict__ sv_lm,
-                                                  uint32_t *__restrict__ sv_u, uint64_t *__restrict__ sv_doc,
-                                                  Loc *__restrict__ sv_loc, uint32_t *__restrict__ sv_ord) {
-  __shared__ CmpStage S;
-  __shared__ uint32_t tmp[CB / 64];
-  __shared__ uint32_t s_pre[NBKT], s_tot[NBKT], s_carry[NBKT];
-  __shared__ uint32_t s_wc[CB / 64][NBKT];
+// One block: each compaction block's offset in every bucket (the counts of
+// the blocks before it), the bucket starts, and the totals -- counts, the
+// list union, the run units, the re-shrink sums.
+// The counts go to LDS CSCAN_CH blocks a round, in independent loads; each
+// bucket is then scanned by 128 threads, a contiguous run of blocks each.
+constexpr int CSCAN = 1024;
+constexpr int CSCAN_CH = 2048;  // blocks a round (64 KiB of counts)
+__global__ void __launch_bounds__(CSCAN) k_cmp_scan(const DevPlan *__restrict__ pl, Counters *__restrict__ ctr,
+                                                    BlkInfo *__restrict__ blk, uint32_t nblk) {
+  static_assert(CSCAN == NBKT * 128, "128 threads a bucket");
+  __shared__ uint32_t s_c[NBKT][CSCAN_CH];
+  __shared__ uint32_t s_w[CSCAN / 64];
+  __shared__ uint32_t s_any;
+  __shared__ unsigned long long s_usum, s_dall, s_xu[XR], s_xd[XR];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  if (threadIdx.x < NBKT) {
-    s_pre[threadIdx.x] = 0;
-    s_tot[threadIdx.x] = 0;
-    s_carry[threadIdx.x] = 0;
+  if (threadIdx.x == 0) {
+    s_any = 0;
+    s_usum = 0;
+    s_dall = 0;
   }
-  __syncthreads();
-  {
-    uint32_t pre[NBKT], tot[NBKT];
-#pragma unroll
-    for (int b = 0; b < NBKT; b++) pre[b] = tot[b] = 0;
-    for (uint32_t i = threadIdx.x; i < nblk; i += CB) {
-#pragma unroll
-      for (int b = 0; b < NBKT; b++) {
-        const uint32_t v = blk[i].cnt[b];
-        tot[b] += v;
-        pre[b] += i < blockIdx.x ? v : 0u;
-      }
-    }
-#pragma unroll
-    for (int b = 0; b < NBKT; b++) {
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) {
-        pre[b] += __shfl_xor(pre[b], off, 64);
-        tot[b] += __shfl_xor(tot[b], off, 64);
-      }
-    }
-    if (lane == 0) {
-#pragma unroll
-      for (int b = 0; b < NBKT; b++) {
-        if (pre[b]) atomicAdd(&s_pre[b], pre[b]);
-        if (tot[b]) atomicAdd(&s_tot[b], tot[b]);
-      }
-    }
+  if (threadIdx.x < XR) {
+    s_xu[threadIdx.x] = 0;
+    s_xd[threadIdx.x] = 0;
   }
-  if (blockIdx.x == 0) {
-    // the totals: counts, bucket starts, list union, units, re-shrink sums
-    uint32_t any = 0;
-    unsigned long long usum = 0, dall = 0, xu[XR] = {0, 0, 0, 0}, xd[XR] = {0, 0, 0, 0};
-    for (uint32_t i = threadIdx.x; i < nblk; i += CB) {
-      const BlkInfo &bi = blk[i];
+  uint32_t any = 0;
+  unsigned long long usum = 0, dall = 0, xu[XR] = {0, 0, 0, 0}, xd[XR] = {0, 0, 0, 0};
+  // bucket b = threads [128 b, 128 b + 128)
+  const int b = threadIdx.x >> 7, j = threadIdx.x & 127;
+  uint32_t carry = 0;
+  for (uint32_t c0 = 0; c0 < nblk; c0 += CSCAN_CH) {
+    const uint32_t n = min((uint32_t)CSCAN_CH, nblk - c0);
+    for (uint32_t i = threadIdx.x; i < n; i += CSCAN) {
+      const BlkInfo &bi = blk[c0 + i];
+#pragma unroll
+      for (int q = 0; q < NBKT; q++) s_c[q][i] = bi.cnt[q];
       any |= bi.any;
       usum += bi.usum;
       dall = bi.dall > dall ? bi.dall : dall;
@@ -2326,78 +2312,109 @@ __global__ void __launch_bounds__(CB) k_cmp_write(const DevPlan *__restrict__ pl
         xd[t] = bi.xd[t] > xd[t] ? bi.xd[t] : xd[t];
       }
     }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      any |= __shfl_xor(any, off, 64);
-      usum += __shfl_xor(usum, off, 64);
-      const unsigned long long o = __shfl_xor(dall, off, 64);
-      dall = o > dall ? o : dall;
-#pragma unroll
-      for (int t = 0; t < XR; t++) {
-        xu[t] += __shfl_xor(xu[t], off, 64);
-        const unsigned long long od = __shfl_xor(xd[t], off, 64);
-        xd[t] = od > xd[t] ? od : xd[t];
-      }
-    }
-    __shared__ uint32_t s_any;
-    __shared__ unsigned long long s_usum, s_dall, s_xu[XR], s_xd[XR];
-    if (threadIdx.x == 0) {
-      s_any = 0;
-      s_usum = 0;
-      s_dall = 0;
-    }
-    if (threadIdx.x < XR) {
-      s_xu[threadIdx.x] = 0;
-      s_xd[threadIdx.x] = 0;
-    }
     __syncthreads();
-    if (lane == 0) {
-      atomicOr(&s_any, any);
-      atomicAdd(&s_usum, usum);
-      atomicMax(&s_dall, dall);
+    // thread j of the bucket: blocks [j per, (j + 1) per) of the round
+    const uint32_t per = (n + 127) / 128;
+    const uint32_t i0 = min(n, (uint32_t)j * per), i1 = min(n, i0 + per);
+    uint32_t sum = 0;
+    for (uint32_t i = i0; i < i1; i++) sum += s_c[b][i];
+    uint32_t x = sum;  // inclusive scan over the wave, then over the bucket's two waves
 #pragma unroll
-      for (int t = 0; t < XR; t++) {
-        atomicAdd(&s_xu[t], xu[t]);
-        atomicMax(&s_xd[t], xd[t]);
-      }
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
     }
+    if (lane == 63) s_w[wid] = x;
     __syncthreads();
-    if (threadIdx.x == 0) {
-      uint32_t acc = 0;
-      for (int b = 0; b < NBKT; b++) {
-        ctr->bstart[b] = acc;
-        ctr->bcnt[b] = s_tot[b];
-        acc += s_tot[b];
-      }
-      ctr->surv_top = ((unsigned long long)acc << 36) | (s_usum & ((1ull << 36) - 1));
-      ctr->anysurv = s_any;
-      ctr->dmax_all = s_dall;
-      int r = 0;
-      for (uint32_t x = pl->reshare_mask; x && r < XR; x &= x - 1, r++) {
-        const int l = __ffs(x) - 1;
-        ctr->ext[l].units += s_xu[r];
-        if (s_xd[r] > ctr->ext[l].dmax) ctr->ext[l].dmax = s_xd[r];
-      }
+    const uint32_t w0 = (wid & 1) ? s_w[wid - 1] : 0u;  // the bucket's first wave, before its second
+    const uint32_t tot = s_w[wid | 1] + s_w[wid & ~1];
+    uint32_t run = carry + w0 + x - sum;
+    for (uint32_t i = i0; i < i1; i++) {
+      blk[c0 + i].pre[b] = run;
+      run += s_c[b][i];
+    }
+    carry += tot;
+    __syncthreads();  // s_c and s_w are rewritten next round
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    any |= __shfl_xor(any, off, 64);
+    usum += __shfl_xor(usum, off, 64);
+    const unsigned long long o = __shfl_xor(dall, off, 64);
+    dall = o > dall ? o : dall;
+#pragma unroll
+    for (int t = 0; t < XR; t++) {
+      xu[t] += __shfl_xor(xu[t], off, 64);
+      const unsigned long long od = __shfl_xor(xd[t], off, 64);
+      xd[t] = od > xd[t] ? od : xd[t];
     }
   }
+  if (lane == 0) {
+    atomicOr(&s_any, any);
+    atomicAdd(&s_usum, usum);
+    atomicMax(&s_dall, dall);
+#pragma unroll
+    for (int t = 0; t < XR; t++) {
+      atomicAdd(&s_xu[t], xu[t]);
+      atomicMax(&s_xd[t], xd[t]);
+    }
+  }
+  __shared__ uint32_t s_tot[NBKT];
+  if (j == 0) s_tot[b] = carry;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t acc = 0;
+    for (int q = 0; q < NBKT; q++) {
+      ctr->bstart[q] = acc;
+      ctr->bcnt[q] = s_tot[q];
+      acc += s_tot[q];
+    }
+    ctr->surv_top = ((unsigned long long)acc << 36) | (s_usum & ((1ull << 36) - 1));
+    ctr->anysurv = s_any;
+    ctr->dmax_all = s_dall;
+    int r = 0;
+    for (uint32_t xm = pl->reshare_mask; xm && r < XR; xm &= xm - 1, r++) {
+      const int l = __ffs(xm) - 1;
+      ctr->ext[l].units += s_xu[r];
+      if (s_xd[r] > ctr->ext[l].dmax) ctr->ext[l].dmax = s_xd[r];
+    }
+  }
+}
+
+// Pass 2: every survivor's record at its final position -- buckets in
+// order, slot order inside a bucket: slot, list mask, run units, docid, and
+// its run locations ([pos][nl]), so k_score reads its survivors' data
+// contiguously; the block's offsets and the bucket starts from k_cmp_scan.
+// sv_ord (site clustering): each record's survivor's rank in slot order,
+// where the replay wants it.
+__global__ void __launch_bounds__(CB) k_cmp_write(const DevPlan *__restrict__ pl, Counters *__restrict__ ctr,
+                                                  const uint32_t *__restrict__ cunit, const uint32_t *__restrict__ bits,
+                                                  uint32_t nwords, const Loc *__restrict__ loc,
+                                                  const uint64_t *__restrict__ cand, uint32_t rc,
+                                                  const BlkInfo *__restrict__ blk,
+                                                  uint32_t *__restrict__ sv_slot, uint32_t *__restrict__ sv_lm,
+                                                  uint32_t *__restrict__ sv_u, uint64_t *__restrict__ sv_doc,
+                                                  Loc *__restrict__ sv_loc, uint32_t *__restrict__ sv_ord) {
+  __shared__ CmpStage S;
+  __shared__ uint32_t tmp[CB / 64];
+  __shared__ uint32_t s_carry[NBKT];
+  __shared__ uint32_t s_wc[CB / 64][NBKT];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (threadIdx.x < NBKT) s_carry[threadIdx.x] = 0;
   __syncthreads();
   uint32_t bstart[NBKT], boff[NBKT];
-  {
-    uint32_t acc = 0;
 #pragma unroll
-    for (int b = 0; b < NBKT; b++) {
-      bstart[b] = acc;
-      acc += s_tot[b];
-      boff[b] = s_pre[b];
-    }
+  for (int b = 0; b < NBKT; b++) {
+    bstart[b] = ctr->bstart[b];
+    boff[b] = blk[blockIdx.x].pre[b];
   }
   uint32_t ord0 = 0;  // survivors of the blocks before this one
 #pragma unroll
   for (int b = 0; b < NBKT; b++) ord0 += boff[b];
-  const uint32_t w = blockIdx.x * CB + threadIdx.x;
+  const uint32_t w = blockIdx.x * CWORDS + threadIdx.x;
   CmpWord c;
   c.surv = 0;
-  if (w < nwords) cmp_word(pl, ctr, bits, nwords, w, c);
+  if (threadIdx.x < CWORDS && w < nwords) cmp_word(pl, ctr, bits, nwords, w, c);
   uint32_t total;
   const uint32_t ex = block_exclusive_scan<CB>(__popc(c.surv), tmp, &total);
   const uint32_t nl = (uint32_t)pl->nlists;
@@ -2654,6 +2671,27 @@ __device__ __forceinline__ void load4u(gu8 *src, uint32_t b, uint64_t *v) {
   v[3] = lo3 | ((uint64_t)hi3 << 32);
 }
 
+// The stale-mbuf replay (stale_fix): a docid's merges write their keys into
+// the reference's function-local mbuf from its start (Posdb.cpp:6007, 6559,
+// 6648-6778; a group's first key 12 bytes, later keys 6), so the bytes a later
+// docid's trailing empty group reads there are what earlier docids left.  A
+// tap keeps the 6 bytes at [lo, lo + 6) of one docid's writes.
+struct MbufTap {
+  uint32_t lo;
+  uint32_t got;  // bit i: b[i] written
+  uint8_t b[8];
+};
+__device__ __forceinline__ void tap_rec(MbufTap *t, uint32_t off, uint64_t lo6, uint64_t hi6, int n) {
+  for (int i = 0; i < n; i++) {
+    const uint32_t p = off + (uint32_t)i;
+    if (p >= t->lo && p < t->lo + 6) {
+      const uint64_t src = i < 6 ? lo6 : hi6;
+      t->b[p - t->lo] = (uint8_t)(src >> (8 * (i % 6)));
+      t->got |= 1u << (p - t->lo);
+    }
+  }
+}
+
 // what the second pass's DocIdScore takes from a scored docid (Posdb.cpp:7555-7563)
 struct SurvOut {
   float score;
@@ -2668,7 +2706,9 @@ __device__ __forceinline__ void score_survivor(const DevPlan *__restrict__ pl, c
                                                uint32_t *key_out, int diag, uint32_t *nrec_out,
                                                bool stamp, uint64_t &tmerge, uint64_t (&tm)[3],
                                                REC *srec = nullptr, SurvOut *so = nullptr,
-                                               const uint16_t *kill = nullptr) {
+                                               const uint16_t *kill = nullptr, uint32_t *mtot_out = nullptr,
+                                               bool *stale_out = nullptr, const uint64_t *inject = nullptr,
+                                               MbufTap *tap = nullptr) {
   const int ng = pl->ngroups;
   DocView<NQ, RP> dv;
   dv.rec = rec;
@@ -2678,6 +2718,7 @@ __device__ __forceinline__ void score_survivor(const DevPlan *__restrict__ pl, c
   uint64_t sortby_raw = 0;  // gbsortby: the unmerged first key (see below)
   bool sortby_is_raw = false;
   uint32_t nrec = 0;
+  uint32_t mtot = 0;  // mbuf bytes the docid's merges wrote (mptr - mbuf)
   // a group's runs: cursor, end, flags (m_bigramFlags of the shrunk sublist
   // index: lists shrunk to empty are not sublists any more)
   struct GrpRuns {
@@ -2926,6 +2967,7 @@ __device__ __forceinline__ void score_survivor(const DevPlan *__restrict__ pl, c
       }
     }
     const uint32_t start = nrec;
+    const uint32_t mg0 = mtot;  // the group's first byte in mbuf
     uint32_t mbytes = 0;  // emulates mptr - mbuf (cap 299000, Posdb.cpp:6007-6008)
     bool isFirstKey = true;
     uint64_t last = 0;
@@ -2966,6 +3008,7 @@ __device__ __forceinline__ void score_survivor(const DevPlan *__restrict__ pl, c
           const int sr = (int)(((b6 >> 5) | ((b7 & 1) << 3)) & 0x0f);
           const int lg = (int)((b6 & 0x1f) | ((b0 & 0x08) ? 0x20 : 0));
           r = (r & ~0xffull) | (((r & 0xff) & 0xf9) | 0x02);
+          if (tap) tap_rec(tap, mg0 + mbytes, r, hi6, 12);
           rec.put(nrec++, r);
           last = r;
           mbytes += 12;
@@ -2979,6 +3022,7 @@ __device__ __forceinline__ void score_survivor(const DevPlan *__restrict__ pl, c
                            (((last >> 24) & 0xc0) == ((r >> 24) & 0xc0));
           if (!dup) {
             r |= 0x06;
+            if (tap) tap_rec(tap, mg0 + mbytes, r, 0, 6);
             rec.put(nrec++, r);
             last = r;
             mbytes += 6;
@@ -3002,6 +3046,7 @@ __device__ __forceinline__ void score_survivor(const DevPlan *__restrict__ pl, c
       __asm__ volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       tm[2] += __builtin_amdgcn_s_memtime() - ta;
     }
+    mtot += mbytes;
     dv.beg[j] = (int)start;
     dv.end[j] = (int)nrec;
     dv.present |= 1u << j;
@@ -3009,8 +3054,21 @@ __device__ __forceinline__ void score_survivor(const DevPlan *__restrict__ pl, c
     // (do-while loops): what mbuf holds there.  When a later group writes
     // records, that is its first key (groups are merged back to back from
     // the same place), which rec[start] is here too; when none does, it is
-    // stale bytes of an earlier docid (not replayed: the docid is dropped)
+    // stale bytes of an earlier docid: the docid is dropped here and
+    // stale_fix scores it from those bytes after the pass
     empty_pos = nrec == start;
+  }
+  if (mtot_out) *mtot_out = mtot;
+  if (stale_out) *stale_out = empty_pos;
+  if (tap) {  // stale_fix: this docid's mbuf bytes only
+    *key_out = 0;
+    return;
+  }
+  if (empty_pos && inject) {
+    // stale_fix: the bytes earlier docids of the pass left where the
+    // trailing empty group points (the record store has room for one more)
+    rec.put((int)nrec, *inject);
+    empty_pos = false;
   }
   float score = 0.0f;
   *nrec_out = nrec;
@@ -3089,7 +3147,8 @@ __global__ void __launch_bounds__(SCORE_TPB, (NQ <= 2 && NS <= 2) ? GBGPU_SCORE_
                                                      const uint32_t *sv_slot, const uint32_t *sv_lm,
                                                      const uint32_t *sv_u, const Loc *sv_loc, uint64_t *arena,
                                                      unsigned long long arena_cap, uint32_t *skey, uint8_t *sflag,
-                                                     int diag, uint64_t *dbg, uint32_t *khist) {
+                                                     int diag, uint64_t *dbg, uint32_t *khist, uint32_t *sv_mb,
+                                                     uint32_t *stale) {
   static_assert(SCORE_TPB == 64, "LdsRecs columns are one wave wide");
   __shared__ float s_sm[npairs<NQ>() * SCORE_TPB];
   __shared__ uint32_t s_rlo[RC * 64];
@@ -3144,7 +3203,8 @@ __global__ void __launch_bounds__(SCORE_TPB, (NQ <= 2 && NS <= 2) ? GBGPU_SCORE_
           if (e.reloc) off = e.off;
         }
       }
-      uint32_t key, nr = 0;
+      uint32_t key, nr = 0, mt = 0;
+      bool st = false;
       if (dbg) {
         __asm__ volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         ts1 = __builtin_amdgcn_s_memtime();
@@ -3166,7 +3226,7 @@ __global__ void __launch_bounds__(SCORE_TPB, (NQ <= 2 && NS <= 2) ? GBGPU_SCORE_
         const LdsRecs lrec{(__attribute__((address_space(3))) uint32_t *)(s_rlo + lane),
                            (__attribute__((address_space(3))) uint16_t *)(s_rhi + lane), sh, RC << (6 - sh)};
         score_survivor<NQ, NS>(pl, ctr, s, lm, anys, svl, lrec, s_sm + lane, &key, diag, &nr,
-                               dbg != nullptr, ts2, tmm);
+                               dbg != nullptr, ts2, tmm, (NoRec *)nullptr, nullptr, nullptr, &mt, &st);
       } else {
         if (off == ~0ull) off = atomicAdd(&ctr->arena_top, (unsigned long long)units);
         if (off + units > arena_cap) {
@@ -3175,7 +3235,7 @@ __global__ void __launch_bounds__(SCORE_TPB, (NQ <= 2 && NS <= 2) ? GBGPU_SCORE_
         } else {
           const GlobalRecs grec{(__attribute__((address_space(1))) uint64_t *)(arena + off)};
           score_survivor<NQ, NS>(pl, ctr, s, lm, anys, svl, grec, s_sm + lane, &key, diag, &nr,
-                                 dbg != nullptr, ts2, tmm);
+                                 dbg != nullptr, ts2, tmm, (NoRec *)nullptr, nullptr, nullptr, &mt, &st);
         }
       }
       if (dbg) {
@@ -3206,6 +3266,8 @@ __global__ void __launch_bounds__(SCORE_TPB, (NQ <= 2 && NS <= 2) ? GBGPU_SCORE_
         if (filt) key = 0;
       }
       skey[i] = key;
+      sv_mb[i] = mt;
+      if (st) stale[atomicAdd(&ctr->nstale, 1u)] = i;  // scored after the pass (stale_fix)
       if (khist) hist_add(khist, key, lane);  // k_topk's first pass
       // site clustering: the replay counts m_filtered, since a docid the
       // prefilters skip never reaches the paging test (Posdb.cpp:6341-6345)
@@ -3526,6 +3588,158 @@ __global__ void __launch_bounds__(SCORE_TPB) k_scoreinfo(const DevPlan *__restri
   info[t] = so;
   counts[2 * t] = rec.ns;
   counts[2 * t + 1] = rec.np;
+}
+
+// ------------------------------------------------------ stale-mbuf replay
+// A survivor whose trailing merged group came out empty (its only keys there
+// were BF_BIGRAM keys with syn bits, Posdb.cpp:6687-6692) has every scorer
+// read the 6 mbuf bytes at that group's place, which the docid's own merges
+// never reach: the reference reads what the docids before it in the pass left
+// there (mbuf is a local of intersectLists10_r, Posdb.cpp:6007; each docid's
+// merges write it from the start, 6559).  k_score drops such survivors and
+// lists them; after the pass (stale_fix), in vote-buffer (docid) order:
+//   k_stale_find  each stale survivor's writer of each of the 6 bytes -- the
+//                 latest earlier docid whose merges wrote past it -- or none
+//                 (the stack's bytes: undefined, the docid stays dropped);
+//   k_stale_fix   the writers' merges again, tapped for those bytes, then the
+//                 survivor scored with them where its empty group points.
+__global__ void k_stale_rank(const uint32_t *order, uint32_t n, uint32_t *rank) {
+  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) rank[order[k]] = k;
+}
+
+constexpr uint32_t STALE_SCAN = 1u << 20;  // docids a writer search walks back at most (beyond: EUNSUPPORTED)
+
+__global__ void k_stale_find(Counters *ctr, const uint32_t *stale, const uint32_t *sv_mb, const uint32_t *order,
+                             const uint32_t *rank, uint32_t *wr) {
+  const uint32_t ns = ctr->nstale;
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < ns; e += gridDim.x * blockDim.x) {
+    const uint32_t si = stale[e];
+    const uint32_t O = sv_mb[si];
+    uint32_t w6[6];
+#pragma unroll
+    for (int p = 0; p < 6; p++) w6[p] = ~0u;
+    uint32_t need = 0, steps = 0;
+    for (int64_t j = (int64_t)rank[si] - 1; j >= 0 && need < 6; j--) {
+      if (++steps > STALE_SCAN) {
+        ctr->unsup = 1;
+        break;
+      }
+      const uint32_t w = order[j];
+      const uint32_t T = sv_mb[w];
+      if (T > O + need) {
+        const uint32_t upto = min(6u, T - O);
+#pragma unroll
+        for (int p = 0; p < 6; p++)
+          if ((uint32_t)p >= need && (uint32_t)p < upto) w6[p] = w;
+        need = upto;
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < 6; p++) wr[(size_t)e * 6 + p] = w6[p];
+  }
+}
+
+// a survivor's record units, as k_score sizes its store (its re-shrunk copies
+// grow by E units each)
+__device__ __forceinline__ uint32_t surv_units(const DevPlan *__restrict__ pl, const Counters *ctr, uint32_t s, uint32_t lm,
+                                               uint32_t u) {
+  for (uint32_t x = lm & pl->reshare_mask; x; x &= x - 1) {
+    const int l = __ffs(x) - 1;
+    const ListExt &e = ctr->ext[l];
+    if (e.slot1 == s + 1) u += e.E * (uint32_t)(pl->lists[l].uses - 1);
+  }
+  return u;
+}
+
+// one lane per stale survivor; okey: its key (0: undefined bytes, not
+// scored, or dropped by the paging filter); fixc[0] the fix arena's top,
+// fixc[1] the paging filter's count
+__global__ void __launch_bounds__(SCORE_TPB) k_stale_fix(const DevPlan *__restrict__ pl, Counters *ctr, const uint32_t *stale,
+                                                         const uint32_t *wr, const uint32_t *sv_mb, const uint32_t *sv_slot,
+                                                         const uint32_t *sv_lm, const uint32_t *sv_u, const uint64_t *sv_doc,
+                                                         const Loc *sv_loc, uint64_t *arena, unsigned long long arena_cap,
+                                                         unsigned long long *fixc, uint32_t *skey, uint32_t *okey) {
+  __shared__ float s_sm[npairs<MAXG>() * SCORE_TPB];
+  stage_weights(&c_weights);
+  const uint32_t e = blockIdx.x * SCORE_TPB + threadIdx.x;
+  const uint32_t ns = ctr->nstale;
+  if (e >= ns) return;
+  const uint32_t anys = ctr->anysurv;
+  const uint32_t nl = (uint32_t)pl->nlists;
+  const uint32_t i = stale[e];
+  uint32_t w6[6];
+  bool defined = true;
+#pragma unroll
+  for (int p = 0; p < 6; p++) {
+    w6[p] = wr[(size_t)e * 6 + p];
+    defined &= w6[p] != ~0u;
+  }
+  okey[e] = 0;
+  if (!defined) return;  // bytes no docid of the pass wrote: the docid stays dropped
+  // room for the largest merge this lane runs (plus the injected record)
+  uint32_t need = surv_units(pl, ctr, sv_slot[i], sv_lm[i], sv_u[i]) + 1;
+#pragma unroll
+  for (int p = 0; p < 6; p++) {
+    const uint32_t w = w6[p];
+    const uint32_t u = surv_units(pl, ctr, sv_slot[w], sv_lm[w], sv_u[w]);
+    need = u > need ? u : need;
+  }
+  const unsigned long long off = atomicAdd(&fixc[0], (unsigned long long)need);
+  if (off + need > arena_cap) {
+    ctr->unsup = 1;  // the host sized the fix arena for every stale survivor: not reached
+    return;
+  }
+  const GlobalRecs grec{(__attribute__((address_space(1))) uint64_t *)(arena + off)};
+  uint32_t key = 0, nr = 0;
+  uint64_t tmerge = 0, tm[3] = {0, 0, 0};
+  // the writers' bytes at [O, O + 6), each writer's merges once
+  const uint32_t O = sv_mb[i];
+  uint64_t inj = 0;
+  uint32_t done = 0;
+  for (int p = 0; p < 6; p++) {
+    if (done >> p & 1) continue;
+    const uint32_t w = w6[p];
+    MbufTap tap;
+    tap.lo = O;
+    tap.got = 0;
+    score_survivor<MAXG, MAXSUB>(pl, ctr, sv_slot[w], sv_lm[w], anys, sv_loc + (uint64_t)w * nl, grec,
+                                 s_sm + threadIdx.x, &key, 0, &nr, false, tmerge, tm, (NoRec *)nullptr,
+                                 (SurvOut *)nullptr, (const uint16_t *)nullptr, nullptr, nullptr, nullptr, &tap);
+    for (int q = p; q < 6; q++) {
+      if (w6[q] != w) continue;
+      if (!(tap.got >> q & 1)) {
+        ctr->unsup = 1;  // the writer wrote past the byte (sv_mb) but the tap missed it: not reached
+        return;
+      }
+      inj |= (uint64_t)tap.b[q] << (8 * q);
+      done |= 1u << q;
+    }
+  }
+  // the survivor itself, the bytes where its empty group points
+  score_survivor<MAXG, MAXSUB>(pl, ctr, sv_slot[i], sv_lm[i], anys, sv_loc + (uint64_t)i * nl, grec,
+                               s_sm + threadIdx.x, &key, 0, &nr, false, tmerge, tm, (NoRec *)nullptr,
+                               (SurvOut *)nullptr, (const uint16_t *)nullptr, nullptr, nullptr, &inj, nullptr);
+  // the paging filter (Posdb.cpp:7327-7347), as k_score applies it
+  if (pl->has_serp && key) {
+    const uint64_t d = sv_doc[i];
+    bool filt = false;
+    if (pl->sortby_group >= 0 && pl->sortby_int) {
+      const int32_t iv = (int32_t)(key ^ 0x80000000u);
+      if (iv > pl->max_serp_int) filt = true;
+      else if (iv == pl->max_serp_int && (int64_t)d <= pl->min_serp_docid) filt = true;
+    } else {
+      const uint32_t b2 = (key & 0x80000000u) ? (key & 0x7fffffffu) : ~key;
+      const float score = __uint_as_float(b2);
+      if (score > (float)pl->max_serp_score) filt = true;
+      else if ((double)score == pl->max_serp_score && (int64_t)d <= pl->min_serp_docid) filt = true;
+    }
+    if (filt) {
+      key = 0;
+      atomicAdd(&fixc[1], 1ull);
+    }
+  }
+  skey[i] = key;
+  okey[e] = key;
 }
 
 // ------------------------------------------------------- site clustering
@@ -5430,6 +5644,7 @@ struct QuerySlot {
   DevBuf white, wrej;                       // "&sites=" whitelist: sorted 5-byte values; rejected slots
   DevBuf si;                                // second pass's score info (score_info)
   DevBuf fac;                               // facet tables (facet_pass)
+  DevBuf svmb, stale;                       // survivors' mbuf bytes; the stale-mbuf survivors (stale_fix)
   std::vector<FacetTerm> facets;            // the query's facet terms with a table
   std::vector<uint64_t> h_white;            // its host copy (the upload's source)
   uint32_t epoch = 0;
@@ -5451,6 +5666,7 @@ struct QuerySlot {
   size_t res_bytes = 0;
   int32_t docs_wanted = 0;
   bool want_info = false;   // m_getDocIdScoringInfo
+  bool in_exchange = false; // collected by the exchange (its reply was packed on the device)
   bool int_scores = false;  // gbsortby int: keys are m_intScore, TopNode::m_score 0
   int info_docs = 0;        // m_docsToGet: the second pass's docid limit
   int info_nterms = 0;      // m_q->m_numTerms and m_realMaxTop (allocTopTree's reservations)
@@ -5464,9 +5680,9 @@ struct QuerySlot {
   hipEvent_t ev_done = nullptr;  // the query's device work is done (the exchange waits on it)
   float last_ms[6] = {0, 0, 0, 0, 0, 0};
 
-  DevBuf *const bufs[29] = {&tables, &chunkcnt, &cand, &cunit, &bits, &loc, &svslot, &svlm, &svu, &svdoc,
+  DevBuf *const bufs[31] = {&tables, &chunkcnt, &cand, &cunit, &bits, &loc, &svslot, &svlm, &svu, &svdoc,
                             &svloc, &scratch, &skey, &sel, &gath, &res, &dir, &split, &swin, &blk,
-                            &sflag, &ord, &oslot, &rep, &tree, &white, &wrej, &si, &fac};
+                            &sflag, &ord, &oslot, &rep, &tree, &white, &wrej, &si, &fac, &svmb, &stale};
   int init(hipMemPool_t pool) {
     if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return GBGPU_EHIP;
     for (auto *b : bufs) {
@@ -6206,7 +6422,7 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   int rc2 = 0;
   rc2 |= q.tables.ensure(tbytes);
   const uint32_t nwords = (uint32_t)((slot_ub + 31) / 32);
-  const uint32_t cgrid = std::max(1u, (uint32_t)((nwords + CB - 1) / CB));
+  const uint32_t cgrid = std::max(1u, (uint32_t)((nwords + CWORDS - 1) / CWORDS));
   rc2 |= q.cand.ensure(8 * slot_ub);
   rc2 |= q.cunit.ensure(4 * slot_ub);
   rc2 |= q.bits.ensure(4 * (size_t)nwords * (uint64_t)P.nlists);
@@ -6218,6 +6434,8 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   rc2 |= q.svloc.ensure(sizeof(Loc) * slot_ub * (uint64_t)P.nlists);
   rc2 |= q.scratch.ensure(8 * scratch_ub);
   rc2 |= q.skey.ensure(4 * slot_ub);
+  rc2 |= q.svmb.ensure(4 * slot_ub);
+  rc2 |= q.stale.ensure(4 * slot_ub);
   rc2 |= q.blk.ensure(sizeof(BlkInfo) * (size_t)cgrid);
   rc2 |= q.sel.ensure(sizeof(Select));
   rc2 |= q.gath.ensure(12 * (slot_ub + MAX_K_BIG) + 1024);
@@ -6345,8 +6563,9 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   // site clustering also records each survivor's slot-order rank (the
   // replay walks the survivors in docid order)
   hipLaunchKernelGGL(k_cmp_count, dim3(cgrid), dim3(CB), 0, st, dpl, dctr, dcunit, bits, nwords, loc, dcand, rcap, blk);
+  hipLaunchKernelGGL(k_cmp_scan, dim3(1), dim3(CSCAN), 0, st, dpl, dctr, blk, cgrid);
   hipLaunchKernelGGL(k_cmp_write, dim3(cgrid), dim3(CB), 0, st, dpl, dctr, dcunit, bits, nwords, loc, dcand, rcap, blk,
-                     cgrid, svslot, svlm, svu, svdoc, svloc, clus ? q.ord.as<uint32_t>() : nullptr);
+                     svslot, svlm, svu, svdoc, svloc, clus ? q.ord.as<uint32_t>() : nullptr);
   const unsigned long long arena_cap = (unsigned long long)(q.scratch.cap / 8);
   if (P.reshare_mask)
     hipLaunchKernelGGL(k_ext_walk, dim3(1), dim3(64), 0, st, dpl, dctr, dcand, dcunit, bits, nwords, loc, arena_cap);
@@ -6361,7 +6580,8 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
       hipLaunchKernelGGL(kern, dim3(grid), dim3(SCORE_TPB), 0, st, dpl, (const uint64_t *)svdoc, dctr,
                          (const uint32_t *)svslot, (const uint32_t *)svlm, (const uint32_t *)svu, (const Loc *)svloc,
                          q.scratch.as<uint64_t>(), arena_cap, q.skey.as<uint32_t>(), q.sflag.as<uint8_t>(),
-                         ctx->score_mode, ctx->d_sdbg, clus ? nullptr : dsel->hist);
+                         ctx->score_mode, ctx->d_sdbg, clus ? nullptr : dsel->hist, q.svmb.as<uint32_t>(),
+                         q.stale.as<uint32_t>());
     };
     if (variant == 4) launch(k_score<2, 2, kRC[4]>);  // two groups of <= 2 sublists (config 2)
     else if (variant == 0) launch(k_score<2, 4, kRC[0]>);
@@ -7203,6 +7423,86 @@ static int facet_pass(QuerySlot &q, uint32_t nsurv, gbgpu_result *out) {
   return out->facets && n > out->facets_cap ? ENOSPC : 0;
 }
 
+// The stale-mbuf survivors of the slot's pass (k_stale_find / k_stale_fix):
+// scored from the bytes earlier docids left, then merged into the top list in
+// the pinned result block (the best k by key, then docid), their paging-filter
+// drops added to *filtered.  Site clustering (the replay's prefilter skips
+// decide which docids write mbuf), the second pass and the exchange (its
+// reply is packed before collect) decline.
+static int stale_fix(QuerySlot &q, uint32_t nsurv, uint32_t nstale, int32_t *filtered) {
+  if (q.replayed || q.want_info || q.in_exchange) return GBGPU_EUNSUPPORTED;
+  const Counters *hc = reinterpret_cast<const Counters *>(q.h_res);
+  hipStream_t st = q.stream;
+  size_t sort_tmp = 0;
+  HIPCHECK(si_sort_pairs(nullptr, sort_tmp, nullptr, nullptr, nullptr, nullptr, nsurv, st));
+  size_t o = 0;
+  auto take = [&](size_t bytes) {
+    const size_t at = o;
+    o += align256(bytes);
+    return at;
+  };
+  const size_t o_key = take(8 * (size_t)nsurv), o_val = take(4 * (size_t)nsurv), o_skey = take(8 * (size_t)nsurv),
+               o_ord = take(4 * (size_t)nsurv), o_rank = take(4 * (size_t)nsurv), o_wr = take(24 * (size_t)nstale),
+               o_okey = take(4 * (size_t)nstale), o_fixc = take(16), o_tmp = take(sort_tmp);
+  // the fix arena: every stale survivor's largest merge (its own records or a
+  // writer's) is below twice the survivors' units
+  const unsigned long long usum = hc->surv_top & ((1ull << 36) - 1);
+  const unsigned long long fcap = 2 * usum + 64ull * nstale + 4096;
+  const size_t o_arena = take(8 * (size_t)fcap);
+  if (q.si.ensure(o)) return ENOMEM;
+  const uint32_t g = std::max(1u, std::min<uint32_t>(1024, (nsurv + 255) / 256));
+  hipLaunchKernelGGL(k_si_keys, dim3(g), dim3(256), 0, st, (const uint64_t *)q.svdoc.as<uint64_t>(), nsurv,
+                     q.si.as<uint64_t>(o_key), q.si.as<uint32_t>(o_val));
+  HIPCHECK(si_sort_pairs(q.si.as<uint8_t>(o_tmp), sort_tmp, q.si.as<uint64_t>(o_key), q.si.as<uint64_t>(o_skey),
+                         q.si.as<uint32_t>(o_val), q.si.as<uint32_t>(o_ord), nsurv, st));
+  hipLaunchKernelGGL(k_stale_rank, dim3(g), dim3(256), 0, st, (const uint32_t *)q.si.as<uint32_t>(o_ord), nsurv,
+                     q.si.as<uint32_t>(o_rank));
+  HIPCHECK(hipMemsetAsync(q.si.as<uint8_t>(o_fixc), 0, 16, st));
+  const uint32_t gs = std::max(1u, std::min<uint32_t>(1024, (nstale + 255) / 256));
+  Counters *dctr = q.res.as<Counters>();
+  hipLaunchKernelGGL(k_stale_find, dim3(gs), dim3(256), 0, st, dctr, (const uint32_t *)q.stale.as<uint32_t>(),
+                     (const uint32_t *)q.svmb.as<uint32_t>(), (const uint32_t *)q.si.as<uint32_t>(o_ord),
+                     (const uint32_t *)q.si.as<uint32_t>(o_rank), q.si.as<uint32_t>(o_wr));
+  hipLaunchKernelGGL(k_stale_fix, dim3((nstale + SCORE_TPB - 1) / SCORE_TPB), dim3(SCORE_TPB), 0, st,
+                     q.tables.as<DevPlan>(), dctr, (const uint32_t *)q.stale.as<uint32_t>(),
+                     (const uint32_t *)q.si.as<uint32_t>(o_wr), (const uint32_t *)q.svmb.as<uint32_t>(),
+                     (const uint32_t *)q.svslot.as<uint32_t>(), (const uint32_t *)q.svlm.as<uint32_t>(),
+                     (const uint32_t *)q.svu.as<uint32_t>(), (const uint64_t *)q.svdoc.as<uint64_t>(),
+                     (const Loc *)q.svloc.as<Loc>(), q.si.as<uint64_t>(o_arena), fcap,
+                     q.si.as<unsigned long long>(o_fixc), q.skey.as<uint32_t>(), q.si.as<uint32_t>(o_okey));
+  HIPCHECK(hipGetLastError());
+  std::vector<uint32_t> pos(nstale), okey(nstale);
+  unsigned long long fixc[2] = {0, 0};
+  uint32_t unsup = 0;
+  HIPCHECK(hipMemcpyAsync(pos.data(), q.stale.p, 4 * (size_t)nstale, hipMemcpyDeviceToHost, st));
+  HIPCHECK(hipMemcpyAsync(okey.data(), q.si.as<uint8_t>(o_okey), 4 * (size_t)nstale, hipMemcpyDeviceToHost, st));
+  HIPCHECK(hipMemcpyAsync(fixc, q.si.as<uint8_t>(o_fixc), 16, hipMemcpyDeviceToHost, st));
+  HIPCHECK(hipMemcpyAsync(&unsup, &dctr->unsup, 4, hipMemcpyDeviceToHost, st));
+  HIPCHECK(hipStreamSynchronize(st));
+  if (unsup) return GBGPU_EUNSUPPORTED;
+  *filtered += (int32_t)fixc[1];
+  // the docids of the scored ones, then the top list merged
+  std::vector<std::pair<uint32_t, uint64_t>> all;
+  std::vector<uint64_t> sd(1);
+  for (uint32_t e = 0; e < nstale; e++) {
+    if (!okey[e]) continue;
+    HIPCHECK(hipMemcpy(sd.data(), q.svdoc.as<uint64_t>() + pos[e], 8, hipMemcpyDeviceToHost));
+    all.push_back({okey[e], sd[0]});
+  }
+  if (all.empty()) return 0;
+  uint32_t *keys = reinterpret_cast<uint32_t *>(q.h_res + res_keys_off());
+  uint64_t *docs = reinterpret_cast<uint64_t *>(q.h_res + res_docs_off(q.k));
+  for (int x = 0; x < q.k && keys[x]; x++) all.push_back({keys[x], docs[x]});
+  std::sort(all.begin(), all.end(), [](const std::pair<uint32_t, uint64_t> &a, const std::pair<uint32_t, uint64_t> &b) {
+    return a.first > b.first || (a.first == b.first && a.second < b.second);
+  });
+  for (int x = 0; x < q.k; x++) {
+    keys[x] = x < (int)all.size() ? all[x].first : 0u;
+    docs[x] = x < (int)all.size() ? all[x].second : ~0ull;
+  }
+  return 0;
+}
+
 // hits_acc: when non-null, the query's intersected docids are appended to it
 // (docid splits gather them over the pieces) instead of being written to out
 static int collect(gbgpu_ctx *ctx, QuerySlot &q, gbgpu_result *out, std::vector<int64_t> *hits_acc = nullptr) {
@@ -7255,6 +7555,10 @@ static int collect(gbgpu_ctx *ctx, QuerySlot &q, gbgpu_result *out, std::vector<
   if (c->corrupt) return GBGPU_ECORRUPT;
   if (c->tree_err) return GBGPU_ECAPACITY;
   if (c->unsup) return GBGPU_EUNSUPPORTED;
+  if (c->nstale) {
+    const int rc = stale_fix(q, (uint32_t)out->hits, c->nstale, &out->filtered);
+    if (rc) return rc;
+  }
 #ifdef GBGPU_DIAG
   if (ctx->d_sdbg && ctx->sdbg_grid) {
     std::vector<uint64_t> h((size_t)ctx->sdbg_grid * 8);
@@ -8262,7 +8566,9 @@ static int allgather_admitted(gbgpu_ctx *ctx, QuerySlot *q, int err, int32_t k, 
     // collected even after a failure, so the slot is free again
     gbgpu_result tmp;
     std::memset(&tmp, 0, sizeof tmp);
+    q->in_exchange = true;
     const int rc = collect(ctx, *q, local ? local : &tmp);
+    q->in_exchange = false;
     lk.unlock();
     slot_released(ctx);
     if (!err) err = rc;

@@ -1344,6 +1344,14 @@ static int cmp_fent(const void *a, const void *b) {
   const int32_t x = ((const FEnt *)a)->key, y = ((const FEnt *)b)->key;
   return x < y ? -1 : x > y;
 }
+/* stale-mbuf docids of the last orc_query (see run_range): scored from the
+ * bytes earlier docids left, and skipped (never written in the pass) */
+static int s_stale_def = 0, s_stale_undef = 0;
+void orc_last_stale(int32_t *defined, int32_t *undefined) {
+  *defined = s_stale_def;
+  *undefined = s_stale_undef;
+}
+
 int orc_last_facets(int32_t *w, int cap) {
   int k = 0;
   if (cap < 1) return -1;
@@ -1655,6 +1663,7 @@ static int run_range(const orc_qterm *qt, const uint8_t *const *lists, const int
     float *scoreMatrix = (float *)calloc((size_t)nqt * nqt, 4);
     uint8_t *mbuf = (uint8_t *)calloc(1, 300000 + 64);
     uint8_t *mptrEnd = mbuf + 299000;
+    size_t mhwm = 0; /* mbuf bytes any docid of this pass has written */
     for (int i = 0; i < nqti; i++) {
       wikiPhraseIds[i] = qip[i].wikiPhraseId;
       quotedStartIds[i] = qip[i].quotedStartId;
@@ -1855,16 +1864,29 @@ static int run_range(const orc_qterm *qt, const uint8_t *const *lists, const int
        * Posdb.cpp:6687-6692) still has its first key read by every scorer
        * (their loops test the end after a key).  When a later group wrote
        * records, that key is the later group's first (groups are merged back
-       * to back), scored here as there.  When none did, the reference reads
-       * stale mbuf bytes of an earlier docid (undefined behaviour); defined
-       * here, as on the GPU: skip the docid. */
+       * to back), scored here as there.  When none did, the scorers read the
+       * mbuf bytes at that place as earlier docids of this pass left them
+       * (the function-local mbuf, Posdb.cpp:6007) -- mbuf here persists over
+       * the pass the same way, so they are scored from it; where no earlier
+       * docid of the pass wrote those 6 bytes they are the stack's (undefined):
+       * the docid is skipped. */
       {
         int trailingEmpty = 0;
+        size_t at = 0, end = 0;
         for (int j = 0; j < nqti; j++) {
           if (!mml[j] || rawg[j]) continue; /* an unmerged numeric group writes no records */
           trailingEmpty = (mml[j] == mme[j]);
+          at = (size_t)(mml[j] - mbuf);
+          end = (size_t)(mme[j] - mbuf);
         }
-        if (trailingEmpty) continue;
+        if (end > mhwm) mhwm = end;
+        if (trailingEmpty) {
+          if (at + 6 > mhwm) {
+            s_stale_undef++;
+            continue;
+          }
+          s_stale_def++;
+        }
       }
 
       /* non-body pair scores, Posdb.cpp:6847-6926 */
@@ -2175,6 +2197,7 @@ int orc_query(const orc_qterm *qt, const uint8_t *const *lists, const int64_t *s
               const orc_params *prm, int64_t *docids, float *scores, int cap, orc_result *out) {
   memset(out, 0, sizeof *out);
   ft_reset();
+  s_stale_def = s_stale_undef = 0;
   if (nqt < 0 || !prm) return EINVAL;
   if (prm->real_max_top <= 0 || prm->docs_to_get <= 0 || prm->num_docid_splits <= 0) return EINVAL;
   int intMode = 0;

@@ -82,6 +82,9 @@ typedef struct orc_facet_ranges {
  * count, i32 outside, i64 docid, i64 sum, i32 max, i32 min) with keys
  * ascending.  Returns the words written, or -1 if cap is too small. */
 int orc_last_facets(int32_t *w, int cap);
+/* stale-mbuf docids of the last orc_query: scored from earlier docids' bytes
+ * (defined) and skipped (bytes no docid of the pass wrote) */
+void orc_last_stale(int32_t *defined, int32_t *undefined);
 
 typedef struct orc_list {
   const uint8_t *bytes;

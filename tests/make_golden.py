@@ -584,6 +584,33 @@ def save_capacity():
         print(f"q_cap_words{nw}: lists={len(lists)} hits={r['hits']} n={len(r['docids'])}")
 
 
+def save_stale():
+    """The stale-mbuf case: the second word's list empty, so group 1 holds
+    only bigram keys, and a docid whose bigram keys all carry syn bits
+    mini-merges it empty with no group after it (Posdb.cpp:6687-6692): the
+    scorers read the mbuf bytes earlier docids of the pass left at that place
+    (the function-local mbuf, Posdb.cpp:6007).  Only seeds where every such
+    docid's 6 bytes were written earlier in the pass (none reads the stack)."""
+    import oracle_binding as orc
+    N = 6000
+    made = 0
+    for seed in range(1, 40):
+        q = qkinds.kinds(N, seed=seed)[0]
+        lists = generate(q, N, seed=2000 + seed)
+        ls = [lists[0], b"", lists[2]]
+        for dtg in (50, 200):
+            q.docs_to_get = dtg
+            r = orc.query(q.terms, ls, q.params(), cap=1 << 16)
+            if r["stale"][1] != 0 or r["stale"][0] == 0:
+                break
+            e = save_query(f"stale_s{seed}_d{dtg}", q.terms, ls, q.params())
+            assert np.array_equal(e["docids"], r["docids"]), seed
+            print(f"q_stale_s{seed}_d{dtg}: stale docids {r['stale'][0]} hits={e['hits']} n={len(e['docids'])}")
+            made += 1
+        if made >= 6:
+            break
+
+
 def split_runs(lst, nruns, rng, dup_frac=0.08, del_frac=0.04):
     """One termlist's keys spread over nruns runs (oldest first) the way a
     termlist lies in tiered Posdb files plus the tree: each key in one run;
@@ -734,6 +761,7 @@ def main():
     save_boolean()
     save_facets()
     save_capacity()
+    save_stale()
     save_msg5()
     save_msg3a()
     cases = [(0, -1), (1, -1), (0, 5000), (1, 5000), (0, 1)]

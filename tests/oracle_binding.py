@@ -22,6 +22,8 @@ def lib():
     if _lib is None:
         _lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "liboracle.so"))
         _lib.orc_last_facets.argtypes = [ctypes.POINTER(ctypes.c_int32), ctypes.c_int]
+        _lib.orc_last_stale.argtypes = [ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)]
+        _lib.orc_last_stale.restype = None
         _lib.orc_query.argtypes = [ctypes.POINTER(gbgpu.QTerm), ctypes.POINTER(ctypes.c_void_p),
                                    ctypes.POINTER(ctypes.c_int64), ctypes.c_int, ctypes.POINTER(gbgpu.Params),
                                    ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_float), ctypes.c_int,
@@ -63,8 +65,11 @@ def query(terms, lists, params, cap=4096):
                      s.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), cap, ctypes.byref(r))
     if rc:
         raise RuntimeError(f"orc_query rc={rc}")
+    sd, su = ctypes.c_int32(), ctypes.c_int32()
+    L.orc_last_stale(ctypes.byref(sd), ctypes.byref(su))
     return dict(docids=d[:r.n].copy(), scores=s[:r.n].copy(), hits=r.hits, filtered=r.filtered,
-                docs_wanted=r.docs_wanted, corrupt=r.corrupt, facets=last_facets())
+                docs_wanted=r.docs_wanted, corrupt=r.corrupt, facets=last_facets(),
+                stale=(sd.value, su.value))
 
 
 def last_facets():
