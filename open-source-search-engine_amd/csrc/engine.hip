@@ -95,7 +95,7 @@ struct ListExt {
 struct Counters {
   uint32_t filtered;  // m_filtered: scored docids dropped by the paging filter (Posdb.cpp:7327-7347)
   uint32_t corrupt;
-  unsigned long long surv_top;  // survivors << 36 | their run units (k_cmp_scan)
+  unsigned long long surv_top;  // survivors << 36 | their run units (k_cmp_write block 0)
   uint32_t g0count[MAXG0];
   uint32_t anysurv;  // bit l: list l has a run in some survivor
   uint32_t tree_n;   // site clustering: TopTree nodes written by k_tree_replay
@@ -105,7 +105,7 @@ struct Counters {
   uint32_t rdbg_t, rdbg_total;  // diagnostic: replay us in tree_add / in all
   unsigned long long dmax_all;  // largest survivor docid
   ListExt ext[MAXL];
-  uint32_t bcnt[8];    // survivors per size bucket (k_cmp_scan), NBKT
+  uint32_t bcnt[8];    // survivors per size bucket (k_cmp_write block 0), NBKT
   uint32_t bstart[8];  // each bucket's first survivor position
   unsigned long long arena_top;  // global record arena: units handed out (k_ext_walk, k_score, k_scoreinfo)
   uint32_t nstale;               // survivors whose trailing group merged empty (k_score: the stale list)
@@ -1917,9 +1917,9 @@ __global__ void k_range_filter(const DevPlan *__restrict__ pl, uint32_t rbits, u
 // run locations of about one survivor:
 //   k_cmp_count  survivors per size bucket of each block, the lists with a
 //                run in some survivor, the re-shrink partials (BlkInfo);
-//   k_cmp_scan   one block: each block's offset in every bucket, the bucket
-//                starts and the totals;
-//   k_cmp_write  every survivor's record at its final position -- buckets
+//   k_cmp_write  each block's offset in every bucket (the counts of the
+//                blocks before it, 32 B a block) and the bucket starts, then
+//                every survivor's record at its final position -- buckets
 //                in order, slot order inside a bucket: slot, list mask, run
 //                units, docid, and its run locations ([pos][nl]), so k_score
 //                reads its survivors' data contiguously.
@@ -1941,17 +1941,16 @@ __host__ __device__ __forceinline__ int bucket_shift(int b) { return b == 0 ? 3 
 constexpr int CB = 256;            // compaction threads per block
 constexpr int CSPT = 32;           // consecutive slots per bitmap word
 #ifndef GBGPU_CWORDS
-#define GBGPU_CWORDS 64
+#define GBGPU_CWORDS 128
 #endif
 constexpr int CWORDS = GBGPU_CWORDS;  // bitmap words per block (threads 0..CWORDS-1 test them)
 static_assert(CWORDS <= CB, "a word a thread");
-constexpr int CTILE = CWORDS * CSPT;  // 2048 slots per block (one block scan: <= 2^16 per bucket)
+constexpr int CTILE = CWORDS * CSPT;  // 4096 slots per block (one block scan: <= 2^16 per bucket)
 static_assert(CTILE < 65536, "packed 16-bit bucket counts");
 constexpr int XR = 4;              // re-shrunk lists reduced per block (more: global atomics)
 
 struct BlkInfo {
   uint32_t cnt[NBKT];  // survivors per bucket
-  uint32_t pre[NBKT];  // k_cmp_scan: survivors per bucket in the blocks before this one
   uint32_t any, pad;   // lists with a run in some survivor of the block
   unsigned long long usum;       // the survivors' run units (their records' upper bound)
   unsigned long long dall;       // largest survivor docid (re-shrink queries)
@@ -2163,7 +2162,7 @@ __global__ void __launch_bounds__(CB) k_cmp_count(const DevPlan *__restrict__ pl
                                                   const uint32_t *__restrict__ cunit, const uint32_t *__restrict__ bits,
                                                   uint32_t nwords, const Loc *__restrict__ loc,
                                                   const uint64_t *__restrict__ cand, uint32_t rc,
-                                                  BlkInfo *__restrict__ blk) {
+                                                  BlkInfo *__restrict__ blk, uint32_t *__restrict__ cnt8) {
   __shared__ CmpStage S;
   __shared__ uint32_t tmp[CB / 64];
   __shared__ uint32_t s_cnt[NBKT];
@@ -2255,7 +2254,10 @@ __global__ void __launch_bounds__(CB) k_cmp_count(const DevPlan *__restrict__ pl
   }
   __syncthreads();
   BlkInfo &o = blk[blockIdx.x];
-  if (threadIdx.x < NBKT) o.cnt[threadIdx.x] = s_cnt[threadIdx.x];
+  if (threadIdx.x < NBKT) {
+    o.cnt[threadIdx.x] = s_cnt[threadIdx.x];
+    cnt8[(size_t)blockIdx.x * NBKT + threadIdx.x] = s_cnt[threadIdx.x];
+  }
   if (threadIdx.x < XR) {
     o.xu[threadIdx.x] = s_xu[threadIdx.x];
     o.xd[threadIdx.x] = s_xd[threadIdx.x];
@@ -2271,38 +2273,71 @@ __global__ void __launch_bounds__(CB) k_cmp_count(const DevPlan *__restrict__ pl
 // One block: each compaction block's offset in every bucket (the counts of
 // the blocks before it), the bucket starts, and the totals -- counts, the
 // list union, the run units, the re-shrink sums.
-// The counts go to LDS CSCAN_CH blocks a round, in independent loads; each
-// bucket is then scanned by 128 threads, a contiguous run of blocks each.
-constexpr int CSCAN = 1024;
-constexpr int CSCAN_CH = 2048;  // blocks a round (64 KiB of counts)
-__global__ void __launch_bounds__(CSCAN) k_cmp_scan(const DevPlan *__restrict__ pl, Counters *__restrict__ ctr,
-                                                    BlkInfo *__restrict__ blk, uint32_t nblk) {
-  static_assert(CSCAN == NBKT * 128, "128 threads a bucket");
-  __shared__ uint32_t s_c[NBKT][CSCAN_CH];
-  __shared__ uint32_t s_w[CSCAN / 64];
-  __shared__ uint32_t s_any;
-  __shared__ unsigned long long s_usum, s_dall, s_xu[XR], s_xd[XR];
+// Pass 2: every survivor's record at its final position -- buckets in
+// order, slot order inside a bucket: slot, list mask, run units, docid, and
+// its run locations ([pos][nl]), so k_score reads its survivors' data
+// contiguously.  Each block sums the counts of the blocks before it (its
+// offsets) and of all blocks (the bucket starts) from cnt8, 32 B a block;
+// block 0 publishes the totals.  sv_ord (site clustering): each record's
+// survivor's rank in slot order, where the replay wants it.
+__global__ void __launch_bounds__(CB) k_cmp_write(const DevPlan *__restrict__ pl, Counters *__restrict__ ctr,
+                                                  const uint32_t *__restrict__ cunit, const uint32_t *__restrict__ bits,
+                                                  uint32_t nwords, const Loc *__restrict__ loc,
+                                                  const uint64_t *__restrict__ cand, uint32_t rc,
+                                                  const BlkInfo *__restrict__ blk, const uint32_t *__restrict__ cnt8,
+                                                  uint32_t nblk, uint32_t *__restrict__ sv_slot,
+                                                  uint32_t *__restrict__ sv_lm, uint32_t *__restrict__ sv_u,
+                                                  uint64_t *__restrict__ sv_doc, Loc *__restrict__ sv_loc,
+                                                  uint32_t *__restrict__ sv_ord) {
+  __shared__ CmpStage S;
+  __shared__ uint32_t tmp[CB / 64];
+  __shared__ uint32_t s_pre[NBKT], s_tot[NBKT], s_carry[NBKT];
+  __shared__ uint32_t s_wc[CB / 64][NBKT];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  if (threadIdx.x == 0) {
-    s_any = 0;
-    s_usum = 0;
-    s_dall = 0;
+  if (threadIdx.x < NBKT) {
+    s_pre[threadIdx.x] = 0;
+    s_tot[threadIdx.x] = 0;
+    s_carry[threadIdx.x] = 0;
   }
-  if (threadIdx.x < XR) {
-    s_xu[threadIdx.x] = 0;
-    s_xd[threadIdx.x] = 0;
-  }
-  uint32_t any = 0;
-  unsigned long long usum = 0, dall = 0, xu[XR] = {0, 0, 0, 0}, xd[XR] = {0, 0, 0, 0};
-  // bucket b = threads [128 b, 128 b + 128)
-  const int b = threadIdx.x >> 7, j = threadIdx.x & 127;
-  uint32_t carry = 0;
-  for (uint32_t c0 = 0; c0 < nblk; c0 += CSCAN_CH) {
-    const uint32_t n = min((uint32_t)CSCAN_CH, nblk - c0);
-    for (uint32_t i = threadIdx.x; i < n; i += CSCAN) {
-      const BlkInfo &bi = blk[c0 + i];
+  __syncthreads();
+  {
+    typedef uint32_t v4 __attribute__((ext_vector_type(4)));
+    const v4 *c4 = reinterpret_cast<const v4 *>(cnt8);
+    uint32_t pre[NBKT], tot[NBKT];
 #pragma unroll
-      for (int q = 0; q < NBKT; q++) s_c[q][i] = bi.cnt[q];
+    for (int b = 0; b < NBKT; b++) pre[b] = tot[b] = 0;
+    for (uint32_t i = threadIdx.x; i < nblk; i += CB) {
+      const v4 a = c4[2 * (size_t)i], c = c4[2 * (size_t)i + 1];
+      const uint32_t v[NBKT] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+      const bool before = i < blockIdx.x;
+#pragma unroll
+      for (int b = 0; b < NBKT; b++) {
+        tot[b] += v[b];
+        pre[b] += before ? v[b] : 0u;
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < NBKT; b++) {
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) {
+        pre[b] += __shfl_xor(pre[b], off, 64);
+        tot[b] += __shfl_xor(tot[b], off, 64);
+      }
+    }
+    if (lane == 0) {
+#pragma unroll
+      for (int b = 0; b < NBKT; b++) {
+        if (pre[b]) atomicAdd(&s_pre[b], pre[b]);
+        if (tot[b]) atomicAdd(&s_tot[b], tot[b]);
+      }
+    }
+  }
+  if (blockIdx.x == 0) {
+    // the totals: counts, bucket starts, list union, units, re-shrink sums
+    uint32_t any = 0;
+    unsigned long long usum = 0, dall = 0, xu[XR] = {0, 0, 0, 0}, xd[XR] = {0, 0, 0, 0};
+    for (uint32_t i = threadIdx.x; i < nblk; i += CB) {
+      const BlkInfo &bi = blk[i];
       any |= bi.any;
       usum += bi.usum;
       dall = bi.dall > dall ? bi.dall : dall;
@@ -2312,101 +2347,70 @@ __global__ void __launch_bounds__(CSCAN) k_cmp_scan(const DevPlan *__restrict__ 
         xd[t] = bi.xd[t] > xd[t] ? bi.xd[t] : xd[t];
       }
     }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      any |= __shfl_xor(any, off, 64);
+      usum += __shfl_xor(usum, off, 64);
+      const unsigned long long o = __shfl_xor(dall, off, 64);
+      dall = o > dall ? o : dall;
+#pragma unroll
+      for (int t = 0; t < XR; t++) {
+        xu[t] += __shfl_xor(xu[t], off, 64);
+        const unsigned long long od = __shfl_xor(xd[t], off, 64);
+        xd[t] = od > xd[t] ? od : xd[t];
+      }
+    }
+    __shared__ uint32_t s_any;
+    __shared__ unsigned long long s_usum, s_dall, s_xu[XR], s_xd[XR];
+    if (threadIdx.x == 0) {
+      s_any = 0;
+      s_usum = 0;
+      s_dall = 0;
+    }
+    if (threadIdx.x < XR) {
+      s_xu[threadIdx.x] = 0;
+      s_xd[threadIdx.x] = 0;
+    }
     __syncthreads();
-    // thread j of the bucket: blocks [j per, (j + 1) per) of the round
-    const uint32_t per = (n + 127) / 128;
-    const uint32_t i0 = min(n, (uint32_t)j * per), i1 = min(n, i0 + per);
-    uint32_t sum = 0;
-    for (uint32_t i = i0; i < i1; i++) sum += s_c[b][i];
-    uint32_t x = sum;  // inclusive scan over the wave, then over the bucket's two waves
+    if (lane == 0) {
+      atomicOr(&s_any, any);
+      atomicAdd(&s_usum, usum);
+      atomicMax(&s_dall, dall);
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(x, o, 64);
-      if (lane >= o) x += y;
+      for (int t = 0; t < XR; t++) {
+        atomicAdd(&s_xu[t], xu[t]);
+        atomicMax(&s_xd[t], xd[t]);
+      }
     }
-    if (lane == 63) s_w[wid] = x;
     __syncthreads();
-    const uint32_t w0 = (wid & 1) ? s_w[wid - 1] : 0u;  // the bucket's first wave, before its second
-    const uint32_t tot = s_w[wid | 1] + s_w[wid & ~1];
-    uint32_t run = carry + w0 + x - sum;
-    for (uint32_t i = i0; i < i1; i++) {
-      blk[c0 + i].pre[b] = run;
-      run += s_c[b][i];
-    }
-    carry += tot;
-    __syncthreads();  // s_c and s_w are rewritten next round
-  }
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    any |= __shfl_xor(any, off, 64);
-    usum += __shfl_xor(usum, off, 64);
-    const unsigned long long o = __shfl_xor(dall, off, 64);
-    dall = o > dall ? o : dall;
-#pragma unroll
-    for (int t = 0; t < XR; t++) {
-      xu[t] += __shfl_xor(xu[t], off, 64);
-      const unsigned long long od = __shfl_xor(xd[t], off, 64);
-      xd[t] = od > xd[t] ? od : xd[t];
+    if (threadIdx.x == 0) {
+      uint32_t acc = 0;
+      for (int b = 0; b < NBKT; b++) {
+        ctr->bstart[b] = acc;
+        ctr->bcnt[b] = s_tot[b];
+        acc += s_tot[b];
+      }
+      ctr->surv_top = ((unsigned long long)acc << 36) | (s_usum & ((1ull << 36) - 1));
+      ctr->anysurv = s_any;
+      ctr->dmax_all = s_dall;
+      int r = 0;
+      for (uint32_t x = pl->reshare_mask; x && r < XR; x &= x - 1, r++) {
+        const int l = __ffs(x) - 1;
+        ctr->ext[l].units += s_xu[r];
+        if (s_xd[r] > ctr->ext[l].dmax) ctr->ext[l].dmax = s_xd[r];
+      }
     }
   }
-  if (lane == 0) {
-    atomicOr(&s_any, any);
-    atomicAdd(&s_usum, usum);
-    atomicMax(&s_dall, dall);
-#pragma unroll
-    for (int t = 0; t < XR; t++) {
-      atomicAdd(&s_xu[t], xu[t]);
-      atomicMax(&s_xd[t], xd[t]);
-    }
-  }
-  __shared__ uint32_t s_tot[NBKT];
-  if (j == 0) s_tot[b] = carry;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t acc = 0;
-    for (int q = 0; q < NBKT; q++) {
-      ctr->bstart[q] = acc;
-      ctr->bcnt[q] = s_tot[q];
-      acc += s_tot[q];
-    }
-    ctr->surv_top = ((unsigned long long)acc << 36) | (s_usum & ((1ull << 36) - 1));
-    ctr->anysurv = s_any;
-    ctr->dmax_all = s_dall;
-    int r = 0;
-    for (uint32_t xm = pl->reshare_mask; xm && r < XR; xm &= xm - 1, r++) {
-      const int l = __ffs(xm) - 1;
-      ctr->ext[l].units += s_xu[r];
-      if (s_xd[r] > ctr->ext[l].dmax) ctr->ext[l].dmax = s_xd[r];
-    }
-  }
-}
-
-// Pass 2: every survivor's record at its final position -- buckets in
-// order, slot order inside a bucket: slot, list mask, run units, docid, and
-// its run locations ([pos][nl]), so k_score reads its survivors' data
-// contiguously; the block's offsets and the bucket starts from k_cmp_scan.
-// sv_ord (site clustering): each record's survivor's rank in slot order,
-// where the replay wants it.
-__global__ void __launch_bounds__(CB) k_cmp_write(const DevPlan *__restrict__ pl, Counters *__restrict__ ctr,
-                                                  const uint32_t *__restrict__ cunit, const uint32_t *__restrict__ bits,
-                                                  uint32_t nwords, const Loc *__restrict__ loc,
-                                                  const uint64_t *__restrict__ cand, uint32_t rc,
-                                                  const BlkInfo *__restrict__ blk,
-                                                  uint32_t *__restrict__ sv_slot, uint32_t *__restrict__ sv_lm,
-                                                  uint32_t *__restrict__ sv_u, uint64_t *__restrict__ sv_doc,
-                                                  Loc *__restrict__ sv_loc, uint32_t *__restrict__ sv_ord) {
-  __shared__ CmpStage S;
-  __shared__ uint32_t tmp[CB / 64];
-  __shared__ uint32_t s_carry[NBKT];
-  __shared__ uint32_t s_wc[CB / 64][NBKT];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  if (threadIdx.x < NBKT) s_carry[threadIdx.x] = 0;
   __syncthreads();
   uint32_t bstart[NBKT], boff[NBKT];
+  {
+    uint32_t acc = 0;
 #pragma unroll
-  for (int b = 0; b < NBKT; b++) {
-    bstart[b] = ctr->bstart[b];
-    boff[b] = blk[blockIdx.x].pre[b];
+    for (int b = 0; b < NBKT; b++) {
+      bstart[b] = acc;
+      acc += s_tot[b];
+      boff[b] = s_pre[b];
+    }
   }
   uint32_t ord0 = 0;  // survivors of the blocks before this one
 #pragma unroll
@@ -2700,7 +2704,9 @@ struct SurvOut {
   int32_t pad;
 };
 
-template <int NQ, int NS, class RP, class REC = NoRec>
+// MB (the stale-mbuf replay only): count the docid's mbuf bytes (mtot_out),
+// tap them (tap: merge only, no scoring), or score with the injected record
+template <int NQ, int NS, class RP, class REC = NoRec, bool MB = false>
 __device__ __forceinline__ void score_survivor(const DevPlan *__restrict__ pl, const Counters *ctr, uint32_t s, uint32_t lm,
                                                uint32_t anys, const Loc *svloc, RP rec, float *smcol,
                                                uint32_t *key_out, int diag, uint32_t *nrec_out,
@@ -3008,7 +3014,8 @@ __device__ __forceinline__ void score_survivor(const DevPlan *__restrict__ pl, c
           const int sr = (int)(((b6 >> 5) | ((b7 & 1) << 3)) & 0x0f);
           const int lg = (int)((b6 & 0x1f) | ((b0 & 0x08) ? 0x20 : 0));
           r = (r & ~0xffull) | (((r & 0xff) & 0xf9) | 0x02);
-          if (tap) tap_rec(tap, mg0 + mbytes, r, hi6, 12);
+          if constexpr (MB)
+            if (tap) tap_rec(tap, mg0 + mbytes, r, hi6, 12);
           rec.put(nrec++, r);
           last = r;
           mbytes += 12;
@@ -3022,7 +3029,8 @@ __device__ __forceinline__ void score_survivor(const DevPlan *__restrict__ pl, c
                            (((last >> 24) & 0xc0) == ((r >> 24) & 0xc0));
           if (!dup) {
             r |= 0x06;
-            if (tap) tap_rec(tap, mg0 + mbytes, r, 0, 6);
+            if constexpr (MB)
+              if (tap) tap_rec(tap, mg0 + mbytes, r, 0, 6);
             rec.put(nrec++, r);
             last = r;
             mbytes += 6;
@@ -3046,7 +3054,7 @@ __device__ __forceinline__ void score_survivor(const DevPlan *__restrict__ pl, c
       __asm__ volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       tm[2] += __builtin_amdgcn_s_memtime() - ta;
     }
-    mtot += mbytes;
+    if constexpr (MB) mtot += mbytes;
     dv.beg[j] = (int)start;
     dv.end[j] = (int)nrec;
     dv.present |= 1u << j;
@@ -3058,17 +3066,19 @@ __device__ __forceinline__ void score_survivor(const DevPlan *__restrict__ pl, c
     // stale_fix scores it from those bytes after the pass
     empty_pos = nrec == start;
   }
-  if (mtot_out) *mtot_out = mtot;
   if (stale_out) *stale_out = empty_pos;
-  if (tap) {  // stale_fix: this docid's mbuf bytes only
-    *key_out = 0;
-    return;
-  }
-  if (empty_pos && inject) {
-    // stale_fix: the bytes earlier docids of the pass left where the
-    // trailing empty group points (the record store has room for one more)
-    rec.put((int)nrec, *inject);
-    empty_pos = false;
+  if constexpr (MB) {
+    if (mtot_out) *mtot_out = mtot;
+    if (tap) {  // stale_fix: this docid's mbuf bytes only
+      *key_out = 0;
+      return;
+    }
+    if (empty_pos && inject) {
+      // stale_fix: the bytes earlier docids of the pass left where the
+      // trailing empty group points (the record store has room for one more)
+      rec.put((int)nrec, *inject);
+      empty_pos = false;
+    }
   }
   float score = 0.0f;
   *nrec_out = nrec;
@@ -3147,8 +3157,7 @@ __global__ void __launch_bounds__(SCORE_TPB, (NQ <= 2 && NS <= 2) ? GBGPU_SCORE_
                                                      const uint32_t *sv_slot, const uint32_t *sv_lm,
                                                      const uint32_t *sv_u, const Loc *sv_loc, uint64_t *arena,
                                                      unsigned long long arena_cap, uint32_t *skey, uint8_t *sflag,
-                                                     int diag, uint64_t *dbg, uint32_t *khist, uint32_t *sv_mb,
-                                                     uint32_t *stale) {
+                                                     int diag, uint64_t *dbg, uint32_t *khist) {
   static_assert(SCORE_TPB == 64, "LdsRecs columns are one wave wide");
   __shared__ float s_sm[npairs<NQ>() * SCORE_TPB];
   __shared__ uint32_t s_rlo[RC * 64];
@@ -3203,7 +3212,7 @@ __global__ void __launch_bounds__(SCORE_TPB, (NQ <= 2 && NS <= 2) ? GBGPU_SCORE_
           if (e.reloc) off = e.off;
         }
       }
-      uint32_t key, nr = 0, mt = 0;
+      uint32_t key, nr = 0;
       bool st = false;
       if (dbg) {
         __asm__ volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -3226,7 +3235,7 @@ __global__ void __launch_bounds__(SCORE_TPB, (NQ <= 2 && NS <= 2) ? GBGPU_SCORE_
         const LdsRecs lrec{(__attribute__((address_space(3))) uint32_t *)(s_rlo + lane),
                            (__attribute__((address_space(3))) uint16_t *)(s_rhi + lane), sh, RC << (6 - sh)};
         score_survivor<NQ, NS>(pl, ctr, s, lm, anys, svl, lrec, s_sm + lane, &key, diag, &nr,
-                               dbg != nullptr, ts2, tmm, (NoRec *)nullptr, nullptr, nullptr, &mt, &st);
+                               dbg != nullptr, ts2, tmm, (NoRec *)nullptr, nullptr, nullptr, nullptr, &st);
       } else {
         if (off == ~0ull) off = atomicAdd(&ctr->arena_top, (unsigned long long)units);
         if (off + units > arena_cap) {
@@ -3235,7 +3244,7 @@ __global__ void __launch_bounds__(SCORE_TPB, (NQ <= 2 && NS <= 2) ? GBGPU_SCORE_
         } else {
           const GlobalRecs grec{(__attribute__((address_space(1))) uint64_t *)(arena + off)};
           score_survivor<NQ, NS>(pl, ctr, s, lm, anys, svl, grec, s_sm + lane, &key, diag, &nr,
-                                 dbg != nullptr, ts2, tmm, (NoRec *)nullptr, nullptr, nullptr, &mt, &st);
+                                 dbg != nullptr, ts2, tmm, (NoRec *)nullptr, nullptr, nullptr, nullptr, &st);
         }
       }
       if (dbg) {
@@ -3266,8 +3275,7 @@ __global__ void __launch_bounds__(SCORE_TPB, (NQ <= 2 && NS <= 2) ? GBGPU_SCORE_
         if (filt) key = 0;
       }
       skey[i] = key;
-      sv_mb[i] = mt;
-      if (st) stale[atomicAdd(&ctr->nstale, 1u)] = i;  // scored after the pass (stale_fix)
+      if (st) atomicAdd(&ctr->nstale, 1u);  // scored after the pass (stale_fix)
       if (khist) hist_add(khist, key, lane);  // k_topk's first pass
       // site clustering: the replay counts m_filtered, since a docid the
       // prefilters skip never reaches the paging test (Posdb.cpp:6341-6345)
@@ -3651,6 +3659,38 @@ __device__ __forceinline__ uint32_t surv_units(const DevPlan *__restrict__ pl, c
   return u;
 }
 
+// every survivor's mbuf bytes (its merges again, no scoring), one lane each:
+// only for a pass with stale survivors
+__global__ void __launch_bounds__(SCORE_TPB) k_stale_mb(const DevPlan *__restrict__ pl, Counters *ctr, uint32_t nsurv,
+                                                        const uint32_t *sv_slot, const uint32_t *sv_lm, const uint32_t *sv_u,
+                                                        const Loc *sv_loc, uint64_t *arena, unsigned long long arena_cap,
+                                                        unsigned long long *fixc, uint32_t *sv_mb, uint32_t *stale) {
+  __shared__ float s_sm[npairs<MAXG>() * SCORE_TPB];
+  stage_weights(&c_weights);
+  const uint32_t i = blockIdx.x * SCORE_TPB + threadIdx.x;
+  if (i >= nsurv) return;
+  const uint32_t nl = (uint32_t)pl->nlists;
+  const uint32_t need = surv_units(pl, ctr, sv_slot[i], sv_lm[i], sv_u[i]) + 1;
+  const unsigned long long off = atomicAdd(&fixc[0], (unsigned long long)need);
+  if (off + need > arena_cap) {
+    ctr->unsup = 1;  // the host sized the arena for every survivor: not reached
+    return;
+  }
+  const GlobalRecs grec{(__attribute__((address_space(1))) uint64_t *)(arena + off)};
+  uint32_t key = 0, nr = 0, mt = 0;
+  bool st = false;
+  uint64_t tmerge = 0, tm[3] = {0, 0, 0};
+  MbufTap tap;
+  tap.lo = ~0u - 8;  // no byte: the count only
+  tap.got = 0;
+  score_survivor<MAXG, MAXSUB, GlobalRecs, NoRec, true>(pl, ctr, sv_slot[i], sv_lm[i], ctr->anysurv,
+                                                        sv_loc + (uint64_t)i * nl, grec, s_sm + threadIdx.x, &key, 0,
+                                                        &nr, false, tmerge, tm, nullptr, nullptr, nullptr, &mt, &st,
+                                                        nullptr, &tap);
+  sv_mb[i] = mt;
+  if (st) stale[atomicAdd((uint32_t *)&fixc[1], 1u)] = i;  // the list k_stale_find walks
+}
+
 // one lane per stale survivor; okey: its key (0: undefined bytes, not
 // scored, or dropped by the paging filter); fixc[0] the fix arena's top,
 // fixc[1] the paging filter's count
@@ -3702,9 +3742,9 @@ __global__ void __launch_bounds__(SCORE_TPB) k_stale_fix(const DevPlan *__restri
     MbufTap tap;
     tap.lo = O;
     tap.got = 0;
-    score_survivor<MAXG, MAXSUB>(pl, ctr, sv_slot[w], sv_lm[w], anys, sv_loc + (uint64_t)w * nl, grec,
-                                 s_sm + threadIdx.x, &key, 0, &nr, false, tmerge, tm, (NoRec *)nullptr,
-                                 (SurvOut *)nullptr, (const uint16_t *)nullptr, nullptr, nullptr, nullptr, &tap);
+    score_survivor<MAXG, MAXSUB, GlobalRecs, NoRec, true>(pl, ctr, sv_slot[w], sv_lm[w], anys, sv_loc + (uint64_t)w * nl,
+                                                          grec, s_sm + threadIdx.x, &key, 0, &nr, false, tmerge, tm,
+                                                          nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, &tap);
     for (int q = p; q < 6; q++) {
       if (w6[q] != w) continue;
       if (!(tap.got >> q & 1)) {
@@ -3716,9 +3756,9 @@ __global__ void __launch_bounds__(SCORE_TPB) k_stale_fix(const DevPlan *__restri
     }
   }
   // the survivor itself, the bytes where its empty group points
-  score_survivor<MAXG, MAXSUB>(pl, ctr, sv_slot[i], sv_lm[i], anys, sv_loc + (uint64_t)i * nl, grec,
-                               s_sm + threadIdx.x, &key, 0, &nr, false, tmerge, tm, (NoRec *)nullptr,
-                               (SurvOut *)nullptr, (const uint16_t *)nullptr, nullptr, nullptr, &inj, nullptr);
+  score_survivor<MAXG, MAXSUB, GlobalRecs, NoRec, true>(pl, ctr, sv_slot[i], sv_lm[i], anys, sv_loc + (uint64_t)i * nl,
+                                                        grec, s_sm + threadIdx.x, &key, 0, &nr, false, tmerge, tm,
+                                                        nullptr, nullptr, nullptr, nullptr, nullptr, &inj, nullptr);
   // the paging filter (Posdb.cpp:7327-7347), as k_score applies it
   if (pl->has_serp && key) {
     const uint64_t d = sv_doc[i];
@@ -5666,7 +5706,8 @@ struct QuerySlot {
   size_t res_bytes = 0;
   int32_t docs_wanted = 0;
   bool want_info = false;   // m_getDocIdScoringInfo
-  bool in_exchange = false; // collected by the exchange (its reply was packed on the device)
+  bool stale_done = false;  // stale_fix ran for the pending query (before the exchange packed it)
+  int32_t stale_filt = 0;   // ... and the paging filter's drops among its survivors
   bool int_scores = false;  // gbsortby int: keys are m_intScore, TopNode::m_score 0
   int info_docs = 0;        // m_docsToGet: the second pass's docid limit
   int info_nterms = 0;      // m_q->m_numTerms and m_realMaxTop (allocTopTree's reservations)
@@ -6094,6 +6135,8 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
     }
   }
   q.facets.clear();
+  q.stale_done = false;
+  q.stale_filt = 0;
   q.docs_wanted = hp.docs_wanted;
   q.k = clus ? TC : hp.docs_wanted;
   // Posdb.cpp:5735: a boolean query goes on with an empty smallest group
@@ -6434,9 +6477,7 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   rc2 |= q.svloc.ensure(sizeof(Loc) * slot_ub * (uint64_t)P.nlists);
   rc2 |= q.scratch.ensure(8 * scratch_ub);
   rc2 |= q.skey.ensure(4 * slot_ub);
-  rc2 |= q.svmb.ensure(4 * slot_ub);
-  rc2 |= q.stale.ensure(4 * slot_ub);
-  rc2 |= q.blk.ensure(sizeof(BlkInfo) * (size_t)cgrid);
+  rc2 |= q.blk.ensure(align256(sizeof(BlkInfo) * (size_t)cgrid) + 4 * NBKT * (size_t)cgrid);
   rc2 |= q.sel.ensure(sizeof(Select));
   rc2 |= q.gath.ensure(12 * (slot_ub + MAX_K_BIG) + 1024);
   rc2 |= q.res.ensure(q.res_bytes);
@@ -6562,10 +6603,12 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   Loc *svloc = q.svloc.as<Loc>();
   // site clustering also records each survivor's slot-order rank (the
   // replay walks the survivors in docid order)
-  hipLaunchKernelGGL(k_cmp_count, dim3(cgrid), dim3(CB), 0, st, dpl, dctr, dcunit, bits, nwords, loc, dcand, rcap, blk);
-  hipLaunchKernelGGL(k_cmp_scan, dim3(1), dim3(CSCAN), 0, st, dpl, dctr, blk, cgrid);
+  uint32_t *cnt8 = reinterpret_cast<uint32_t *>(q.blk.as<uint8_t>(align256(sizeof(BlkInfo) * (size_t)cgrid)));
+  hipLaunchKernelGGL(k_cmp_count, dim3(cgrid), dim3(CB), 0, st, dpl, dctr, dcunit, bits, nwords, loc, dcand, rcap, blk,
+                     cnt8);
   hipLaunchKernelGGL(k_cmp_write, dim3(cgrid), dim3(CB), 0, st, dpl, dctr, dcunit, bits, nwords, loc, dcand, rcap, blk,
-                     svslot, svlm, svu, svdoc, svloc, clus ? q.ord.as<uint32_t>() : nullptr);
+                     (const uint32_t *)cnt8, cgrid, svslot, svlm, svu, svdoc, svloc,
+                     clus ? q.ord.as<uint32_t>() : nullptr);
   const unsigned long long arena_cap = (unsigned long long)(q.scratch.cap / 8);
   if (P.reshare_mask)
     hipLaunchKernelGGL(k_ext_walk, dim3(1), dim3(64), 0, st, dpl, dctr, dcand, dcunit, bits, nwords, loc, arena_cap);
@@ -6580,8 +6623,7 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
       hipLaunchKernelGGL(kern, dim3(grid), dim3(SCORE_TPB), 0, st, dpl, (const uint64_t *)svdoc, dctr,
                          (const uint32_t *)svslot, (const uint32_t *)svlm, (const uint32_t *)svu, (const Loc *)svloc,
                          q.scratch.as<uint64_t>(), arena_cap, q.skey.as<uint32_t>(), q.sflag.as<uint8_t>(),
-                         ctx->score_mode, ctx->d_sdbg, clus ? nullptr : dsel->hist, q.svmb.as<uint32_t>(),
-                         q.stale.as<uint32_t>());
+                         ctx->score_mode, ctx->d_sdbg, clus ? nullptr : dsel->hist);
     };
     if (variant == 4) launch(k_score<2, 2, kRC[4]>);  // two groups of <= 2 sublists (config 2)
     else if (variant == 0) launch(k_score<2, 4, kRC[0]>);
@@ -7425,12 +7467,12 @@ static int facet_pass(QuerySlot &q, uint32_t nsurv, gbgpu_result *out) {
 
 // The stale-mbuf survivors of the slot's pass (k_stale_find / k_stale_fix):
 // scored from the bytes earlier docids left, then merged into the top list in
-// the pinned result block (the best k by key, then docid), their paging-filter
-// drops added to *filtered.  Site clustering (the replay's prefilter skips
-// decide which docids write mbuf), the second pass and the exchange (its
-// reply is packed before collect) decline.
-static int stale_fix(QuerySlot &q, uint32_t nsurv, uint32_t nstale, int32_t *filtered) {
-  if (q.replayed || q.want_info || q.in_exchange) return GBGPU_EUNSUPPORTED;
+// the pinned result block (the best k by key, then docid) and in the device
+// one (the exchange packs from it), their paging-filter drops kept in
+// q.stale_filt.  Site clustering (the replay's prefilter skips decide which
+// docids write mbuf) and the second pass decline.  The slot's stream is idle.
+static int stale_fix(QuerySlot &q, uint32_t nsurv, uint32_t nstale) {
+  if (q.replayed || q.want_info) return GBGPU_EUNSUPPORTED;
   const Counters *hc = reinterpret_cast<const Counters *>(q.h_res);
   hipStream_t st = q.stream;
   size_t sort_tmp = 0;
@@ -7444,10 +7486,10 @@ static int stale_fix(QuerySlot &q, uint32_t nsurv, uint32_t nstale, int32_t *fil
   const size_t o_key = take(8 * (size_t)nsurv), o_val = take(4 * (size_t)nsurv), o_skey = take(8 * (size_t)nsurv),
                o_ord = take(4 * (size_t)nsurv), o_rank = take(4 * (size_t)nsurv), o_wr = take(24 * (size_t)nstale),
                o_okey = take(4 * (size_t)nstale), o_fixc = take(16), o_tmp = take(sort_tmp);
-  // the fix arena: every stale survivor's largest merge (its own records or a
-  // writer's) is below twice the survivors' units
+  // the fix arena: every survivor's merges once (k_stale_mb), then every
+  // stale survivor's largest merge (its own records or a writer's)
   const unsigned long long usum = hc->surv_top & ((1ull << 36) - 1);
-  const unsigned long long fcap = 2 * usum + 64ull * nstale + 4096;
+  const unsigned long long fcap = 2 * usum + 64ull * nsurv + 4096;
   const size_t o_arena = take(8 * (size_t)fcap);
   if (q.si.ensure(o)) return ENOMEM;
   const uint32_t g = std::max(1u, std::min<uint32_t>(1024, (nsurv + 255) / 256));
@@ -7457,9 +7499,16 @@ static int stale_fix(QuerySlot &q, uint32_t nsurv, uint32_t nstale, int32_t *fil
                          q.si.as<uint32_t>(o_val), q.si.as<uint32_t>(o_ord), nsurv, st));
   hipLaunchKernelGGL(k_stale_rank, dim3(g), dim3(256), 0, st, (const uint32_t *)q.si.as<uint32_t>(o_ord), nsurv,
                      q.si.as<uint32_t>(o_rank));
+  Counters *dctr = q.res.as<Counters>();
+  if (q.svmb.ensure(4 * (size_t)nsurv) || q.stale.ensure(4 * (size_t)nstale)) return ENOMEM;
+  HIPCHECK(hipMemsetAsync(q.si.as<uint8_t>(o_fixc), 0, 16, st));
+  hipLaunchKernelGGL(k_stale_mb, dim3((nsurv + SCORE_TPB - 1) / SCORE_TPB), dim3(SCORE_TPB), 0, st,
+                     q.tables.as<DevPlan>(), dctr, nsurv, (const uint32_t *)q.svslot.as<uint32_t>(),
+                     (const uint32_t *)q.svlm.as<uint32_t>(), (const uint32_t *)q.svu.as<uint32_t>(),
+                     (const Loc *)q.svloc.as<Loc>(), q.si.as<uint64_t>(o_arena), fcap,
+                     q.si.as<unsigned long long>(o_fixc), q.svmb.as<uint32_t>(), q.stale.as<uint32_t>());
   HIPCHECK(hipMemsetAsync(q.si.as<uint8_t>(o_fixc), 0, 16, st));
   const uint32_t gs = std::max(1u, std::min<uint32_t>(1024, (nstale + 255) / 256));
-  Counters *dctr = q.res.as<Counters>();
   hipLaunchKernelGGL(k_stale_find, dim3(gs), dim3(256), 0, st, dctr, (const uint32_t *)q.stale.as<uint32_t>(),
                      (const uint32_t *)q.svmb.as<uint32_t>(), (const uint32_t *)q.si.as<uint32_t>(o_ord),
                      (const uint32_t *)q.si.as<uint32_t>(o_rank), q.si.as<uint32_t>(o_wr));
@@ -7480,7 +7529,7 @@ static int stale_fix(QuerySlot &q, uint32_t nsurv, uint32_t nstale, int32_t *fil
   HIPCHECK(hipMemcpyAsync(&unsup, &dctr->unsup, 4, hipMemcpyDeviceToHost, st));
   HIPCHECK(hipStreamSynchronize(st));
   if (unsup) return GBGPU_EUNSUPPORTED;
-  *filtered += (int32_t)fixc[1];
+  q.stale_filt = (int32_t)fixc[1];
   // the docids of the scored ones, then the top list merged
   std::vector<std::pair<uint32_t, uint64_t>> all;
   std::vector<uint64_t> sd(1);
@@ -7500,6 +7549,9 @@ static int stale_fix(QuerySlot &q, uint32_t nsurv, uint32_t nstale, int32_t *fil
     keys[x] = x < (int)all.size() ? all[x].first : 0u;
     docs[x] = x < (int)all.size() ? all[x].second : ~0ull;
   }
+  HIPCHECK(hipMemcpyAsync(q.res.as<uint8_t>(res_keys_off()), keys, 4 * (size_t)q.k, hipMemcpyHostToDevice, st));
+  HIPCHECK(hipMemcpyAsync(q.res.as<uint8_t>(res_docs_off(q.k)), docs, 8 * (size_t)q.k, hipMemcpyHostToDevice, st));
+  HIPCHECK(hipStreamSynchronize(st));
   return 0;
 }
 
@@ -7556,8 +7608,11 @@ static int collect(gbgpu_ctx *ctx, QuerySlot &q, gbgpu_result *out, std::vector<
   if (c->tree_err) return GBGPU_ECAPACITY;
   if (c->unsup) return GBGPU_EUNSUPPORTED;
   if (c->nstale) {
-    const int rc = stale_fix(q, (uint32_t)out->hits, c->nstale, &out->filtered);
-    if (rc) return rc;
+    if (!q.stale_done) {
+      const int rc = stale_fix(q, (uint32_t)out->hits, c->nstale);
+      if (rc) return rc;
+    }
+    out->filtered += q.stale_filt;
   }
 #ifdef GBGPU_DIAG
   if (ctx->d_sdbg && ctx->sdbg_grid) {
@@ -8545,6 +8600,16 @@ static int allgather_admitted(gbgpu_ctx *ctx, QuerySlot *q, int err, int32_t k, 
   hipStream_t xs = ctx->xstream;
   bool packed = false;
   if (q && !q->early && !err) {
+    // stale-mbuf survivors are scored on the host's word after the pass: the
+    // reply waits for them (the pass done, its result block read)
+    if (hipStreamSynchronize(q->stream) != hipSuccess) err = GBGPU_EHIP;
+    const Counters *hc = reinterpret_cast<const Counters *>(q->h_res);
+    if (!err && hc->nstale && !hc->corrupt && !hc->tree_err && !hc->unsup) {
+      err = stale_fix(*q, (uint32_t)(hc->surv_top >> 36), hc->nstale);
+      if (!err) q->stale_done = true;
+    }
+  }
+  if (q && !q->early && !err) {
     if (hipStreamWaitEvent(xs, q->ev_done, 0) == hipSuccess) {
       hipLaunchKernelGGL(k_xpack, dim3(1), dim3(256), 0, xs, q->res.as<Counters>(), q->res.as<uint32_t>(res_keys_off()),
                          q->res.as<uint64_t>(res_docs_off(q->k)), (uint32_t)k, (uint32_t)q->k, q->int_scores ? 1 : 0,
@@ -8566,9 +8631,7 @@ static int allgather_admitted(gbgpu_ctx *ctx, QuerySlot *q, int err, int32_t k, 
     // collected even after a failure, so the slot is free again
     gbgpu_result tmp;
     std::memset(&tmp, 0, sizeof tmp);
-    q->in_exchange = true;
     const int rc = collect(ctx, *q, local ? local : &tmp);
-    q->in_exchange = false;
     lk.unlock();
     slot_released(ctx);
     if (!err) err = rc;

@@ -14,6 +14,7 @@ import os
 import numpy as np
 import pytest
 
+import gbgpu
 from test_golden import check, load_query
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -113,8 +114,19 @@ def test_gpu_file_pieces_match_host_upload(engine, path, kind):
         for (c, k18), o, x in zip(cuts, offs, lists):
             hd.append(engine.file_list(fh, o + c, len(x) - c, k18))
         hh = [engine.upload(x) for x in host]
-        a = engine.query_resident(terms, hd, params, cap=1 << 16, hit_cap=1 << 20)
-        b = engine.query_resident(terms, hh, params, cap=1 << 16, hit_cap=1 << 20)
+
+        def run(hs):
+            try:
+                return engine.query_resident(terms, hs, params, cap=1 << 16, hit_cap=1 << 20)
+            except gbgpu.GbgpuError as e:
+                return e.code
+
+        a, b = run(hd), run(hh)
+        if isinstance(a, int) or isinstance(b, int):
+            # a cut can leave docids whose trailing group merges empty (the
+            # stale-mbuf case), which site clustering declines: both alike
+            assert a == b == gbgpu.GBGPU_EUNSUPPORTED and params.site_clustering
+            return
         assert a.hits == b.hits and a.docs_wanted == b.docs_wanted and a.filtered == b.filtered
         assert np.array_equal(a.docids, b.docids)
         assert np.array_equal(a.scores.view(np.uint32), b.scores.view(np.uint32))
