@@ -1941,11 +1941,11 @@ __host__ __device__ __forceinline__ int bucket_shift(int b) { return b == 0 ? 3 
 constexpr int CB = 256;            // compaction threads per block
 constexpr int CSPT = 32;           // consecutive slots per bitmap word
 #ifndef GBGPU_CWORDS
-#define GBGPU_CWORDS 128
+#define GBGPU_CWORDS 256
 #endif
 constexpr int CWORDS = GBGPU_CWORDS;  // bitmap words per block (threads 0..CWORDS-1 test them)
 static_assert(CWORDS <= CB, "a word a thread");
-constexpr int CTILE = CWORDS * CSPT;  // 4096 slots per block (one block scan: <= 2^16 per bucket)
+constexpr int CTILE = CWORDS * CSPT;  // 8192 slots per block (one block scan: <= 2^16 per bucket)
 static_assert(CTILE < 65536, "packed 16-bit bucket counts");
 constexpr int XR = 4;              // re-shrunk lists reduced per block (more: global atomics)
 
