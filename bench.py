@@ -620,12 +620,33 @@ def main():
             if r_fr.hits != r0.hits or not np.array_equal(r_fr.docids, r0.docids):
                 raise RuntimeError("file-cut query differs from the host-buffer query")
         el_fr = time.perf_counter() - t_fr
+        # the same with queries in flight: the next query's termlists are cut
+        # (upload stream) while earlier ones run on their slots
+        fs = min(4, slots)
+        n_fq = 60
+        live = {}
+        t_fq = time.perf_counter()
+        for i in range(n_fq + fs):
+            sl = i % fs
+            if sl in live:
+                r_fq = eng.collect(cap=4096, slot=sl)
+                for h in live.pop(sl):
+                    eng.free(h)
+                if r_fq.hits != r0.hits or not np.array_equal(r_fq.docids, r0.docids):
+                    raise RuntimeError("file-cut query differs from the host-buffer query")
+            if i < n_fq:
+                fl = [eng.file_list(fh, o, len(x)) for o, x in zip(offs, first_lists)]
+                eng.enqueue(qs[0].terms, fl, ps[0], slot=sl)
+                live[sl] = fl
+        el_fq = time.perf_counter() - t_fq
         eng.file_free(fh)
         result["file_read"] = {
             "queries_per_sec": round(n_fr / el_fr, 3),
             "keys_scanned_GBps": round(qbytes[0] * n_fr / el_fr / 1e9, 3),
+            "in_flight": {"queries": fs, "queries_per_sec": round(n_fq / el_fq, 3)},
             "note": "termlists cut per query from a resident Posdb file image (gbgpu_file_list: device copy, "
-                    "structure check, page map), queried, freed; one query at a time; not `value`",
+                    "one structure/page-map/granule pass), queried, freed; one query at a time, and with "
+                    "`in_flight.queries` queries in flight; not `value`",
         }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline_query(qs[0], first_lists)

@@ -5595,53 +5595,122 @@ struct ListEntry {
   int64_t size = 0;   // original bytes (18-byte first key)
   uint32_t units = 0; // swapped units
   uint64_t dmin = 0, dmax = 0;  // docid of the first and of the last run
-  // first run docid at or after each WCH_UNITS-unit granule (k_gfirst; host
+  // first run docid at or after each WCH_UNITS-unit granule (k_list_scan; host
   // copy, resident lists only): the probe spans' start docids
   std::shared_ptr<const std::vector<uint64_t>> gfirst;
   bool live = false;
 };
 
-// Upload-time check of a swapped list's unit structure.  A valid list
-// classifies every unit independently (Posdb.h:887-889): a unit with the
-// half bit (byte1 & 0x02) starts a key, and a key start is either a 12-byte
-// run head (byte0 & 0x06 == 0x02), which the next unit (its docid half,
-// whose byte-1 bit is the mandatory zero, Posdb.cpp:410-412) must follow, or
-// a 6-byte key (byte0 & 0x04).  A key start with neither compression bit is
-// an 18-byte key inside the list -- the corruption intersectLists10_r bails
-// on (Posdb.cpp:6289-6302); a run head followed by a key start, or ending the
-// list, is a truncated key.  Either sets *bad, so no scan kernel ever sees a
-// list whose run count could exceed units/2 (the sizing of every run buffer).
-__global__ void k_validate(const uint8_t *list, uint32_t units, uint32_t *bad) {
-  gu8 *p = gl(list);
-  uint32_t b = 0;
-  for (uint32_t u = blockIdx.x * blockDim.x + threadIdx.x; u < units; u += gridDim.x * blockDim.x) {
-    const uint8_t b0 = p[(size_t)u * 6], b1 = p[(size_t)u * 6 + 1];
+// An uploaded (or cut) list's one pass over its bytes, a 2048-unit page a
+// block, from the page staged in LDS: the structure check (every unit
+// classified alone, Posdb.h:887-889: a unit with the half bit byte1 & 0x02
+// starts a key, which must carry a size bit in byte 0, and a 12-byte key's
+// second unit must not look like a key start; the list starts with a key), the
+// page's run starts (the page map), the first run docid of each of its four
+// granules (the granule table: ~0 where the page has none from there on; the
+// suffix over pages is k_list_tail's), and the last run docid (dmax).
+struct ListHdr {
+  uint32_t bad;
+  uint32_t pad;
+  unsigned long long dmax;
+};
+static_assert(CHUNK_UNITS == 4 * WCH_UNITS, "four granules a page");
+__global__ void __launch_bounds__(BLOCK) k_list_scan(const uint8_t *__restrict__ list, uint32_t units,
+                                                     uint32_t *__restrict__ pm, uint64_t *__restrict__ gf,
+                                                     ListHdr *hdr) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[CHUNK_LOAD];
+  __shared__ uint32_t tmp[BLOCK / 64];
+  __shared__ uint32_t s_first[4], s_last;
+  const uint32_t u0 = blockIdx.x * (uint32_t)CHUNK_UNITS;
+  if (threadIdx.x < 4) s_first[threadIdx.x] = ~0u;
+  if (threadIdx.x == 0) s_last = 0;
+  load_chunk(list, u0, lds);
+  __syncthreads();
+  const uint32_t m = thread_starts(lds, u0, units);
+  uint32_t bad = 0;
+#pragma unroll
+  for (int q = 0; q < UPT; q++) {
+    const uint32_t lu = threadIdx.x * UPT + q, u = u0 + lu;
+    if (u >= units) break;
+    const uint32_t b0 = lds[lu * 6], b1 = lds[lu * 6 + 1];
     if (!(b1 & 0x02)) {
-      if (u == 0) b = 1;  // the list must start with a key
+      if (u == 0) bad = 1;  // the list must start with a key
       continue;
     }
-    if (!(b0 & 0x06)) b = 1;
-    if (!(b0 & 0x04)) {
-      if (u + 1 >= units || (p[(size_t)(u + 1) * 6 + 1] & 0x02)) b = 1;
-    }
+    if (!(b0 & 0x06)) bad = 1;
+    if (!(b0 & 0x04) && (u + 1 >= units || (lds[(lu + 1) * 6 + 1] & 0x02))) bad = 1;
   }
-  if (__ballot(b) && (threadIdx.x & 63) == 0) atomicOr(bad, 1u);
+  if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(&hdr->bad, 1u);
+  if (m) {
+    const uint32_t f = threadIdx.x * UPT + (uint32_t)(__ffs(m) - 1);
+    atomicMin(&s_first[f / WCH_UNITS], f);
+    atomicMax(&s_last, threadIdx.x * UPT + (uint32_t)(31 - __clz(m)) + 1);
+  }
+  uint32_t tot;
+  block_exclusive_scan(__popc(m), tmp, &tot);  // its barriers order the LDS atomics
+  if (threadIdx.x == 0) pm[blockIdx.x] = tot;
+  if (threadIdx.x < 4) {
+    uint32_t f = ~0u;  // the first run start at or after the granule, in this page
+    for (int g = 3; g >= (int)threadIdx.x; g--) f = s_first[g] != ~0u ? s_first[g] : f;
+    gf[(size_t)blockIdx.x * 4 + threadIdx.x] = f == ~0u ? ~0ull : lds_unit_docid(lds, f);
+  }
+  if (threadIdx.x == 0 && s_last) atomicMax(&hdr->dmax, (unsigned long long)lds_unit_docid(lds, s_last - 1));
 }
 
-// Upload-time granule table (an RdbMap-like index at 3 KiB resolution): for
-// every WCH_UNITS-unit granule of a swapped list, the docid of the first run
-// start at or after its first unit (~0: none).  One wave per granule.  The
-// host keeps a copy and gives each probe span its first run docid, so
-// k_probe starts without a dependent walk of the list.
-__global__ void __launch_bounds__(256) k_gfirst(const uint8_t *list, uint32_t units, uint32_t ngran, uint64_t *out) {
-  const int lane = threadIdx.x & 63;
-  const uint32_t g = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (g >= ngran) return;
-  DevList L;
-  L.p = list;
-  L.units = units;
-  const uint64_t d = first_run_doc(L, g * (uint32_t)WCH_UNITS, units, lane);
-  if (lane == 0) out[g] = d;
+// one block: the page map's exclusive scan (total at pm[npages]) and the
+// granule table's suffix over pages (a granule with no run start after it in
+// its page takes the next page's first)
+__global__ void __launch_bounds__(1024) k_list_tail(uint32_t npages, uint32_t *pm, uint64_t *gf, uint32_t ngran) {
+  __shared__ uint32_t tmp[16];
+  __shared__ uint32_t carry;
+  __shared__ unsigned long long s_next[16], s_carry;
+  if (threadIdx.x == 0) {
+    carry = 0;
+    s_carry = ~0ull;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (uint32_t base = 0; base < npages; base += 1024) {
+    const uint32_t i = base + threadIdx.x;
+    const uint32_t v = i < npages ? pm[i] : 0;
+    uint32_t x = v;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) tmp[wid] = x;
+    __syncthreads();
+    uint32_t pre = 0;
+    for (int w = 0; w < wid; w++) pre += tmp[w];
+    const uint32_t incl = carry + pre + x;
+    __syncthreads();
+    if (i < npages) pm[i] = incl - v;
+    if (threadIdx.x == 1023) carry = incl;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) pm[npages] = carry;
+  // suffix minimum over the granules (docids ascend, ~0 = none), from the end,
+  // 1024 granules a round
+  const uint32_t rounds = (ngran + 1023) / 1024;
+  for (uint32_t r = 0; r < rounds; r++) {
+    const uint32_t base = (rounds - 1 - r) * 1024;
+    const uint32_t i = base + threadIdx.x;
+    unsigned long long v = i < ngran ? gf[i] : ~0ull;
+    // suffix min within the wave (lanes above)
+    for (int o = 1; o < 64; o <<= 1) {
+      const unsigned long long y = __shfl_down(v, o, 64);
+      if (lane + o < 64 && y < v) v = y;
+    }
+    if (lane == 0) s_next[wid] = v;  // the wave's minimum
+    __syncthreads();
+    unsigned long long after = s_carry;  // the rounds after this one
+    for (int w = wid + 1; w < 16; w++) after = s_next[w] < after ? s_next[w] : after;
+    if (after < v) v = after;
+    if (i < ngran) gf[i] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) s_carry = v;  // thread 0 holds the round's minimum
+    __syncthreads();
+  }
 }
 
 // docid of the key starting at p (Posdb.h:295)
@@ -5903,66 +5972,37 @@ static int upload_list(gbgpu_ctx *ctx, const uint8_t *bytes, int64_t size, int32
 static int finish_list(gbgpu_ctx *ctx, ListEntry &e, const uint8_t *host_bytes, const uint8_t *first18,
                        int32_t *handle) {
   const int64_t size = e.size;
-  if (size) {
-    HIPCHECK(hipMemsetAsync(ctx->d_flag, 0, 4, ctx->upload_stream));
-    const uint32_t grid = (uint32_t)std::min<uint64_t>(4096, (e.units + 255) / 256);
-    hipLaunchKernelGGL(k_validate, dim3(std::max(grid, 1u)), dim3(256), 0, ctx->upload_stream, e.d, e.units,
-                       ctx->d_flag);
-    HIPCHECK(hipGetLastError());
-    int rc = build_page_map(e.d, e.units, e.pm, ctx->upload_stream);
-    if (rc) return rc;
-    HIPCHECK(hipMemcpyAsync(ctx->h_flag, ctx->d_flag, 4, hipMemcpyDeviceToHost, ctx->upload_stream));
-  }
   std::vector<uint64_t> gf;
-  DevBuf dgf;
   if (size) {
-    const uint32_t ngran = (e.units + WCH_UNITS - 1) / WCH_UNITS;
+    // one pass over the bytes (k_list_scan), the page scan and granule
+    // suffix (k_list_tail), then ONE synchronisation for the check, the
+    // granule table and the last run docid
+    const uint32_t np = (e.units + CHUNK_UNITS - 1) / CHUNK_UNITS;
+    const uint32_t ngran = np * 4;
     gf.resize(ngran);
-    if (dgf.ensure(8 * (size_t)ngran)) return ENOMEM;
-    hipLaunchKernelGGL(k_gfirst, dim3((ngran + 3) / 4), dim3(256), 0, ctx->upload_stream, e.d, e.units, ngran,
-                       dgf.as<uint64_t>());
-    hipError_t le = hipGetLastError();
-    if (le == hipSuccess)
-      le = hipMemcpyAsync(gf.data(), dgf.p, 8 * (size_t)ngran, hipMemcpyDeviceToHost, ctx->upload_stream);
-    if (le != hipSuccess) {
-      (void)hipStreamSynchronize(ctx->upload_stream);
-      dgf.release();
-      HIPCHECK(le);
+    DevBuf dgf;
+    if (dgf.ensure(align256(8 * (size_t)ngran) + sizeof(ListHdr))) return ENOMEM;
+    ListHdr *dh = reinterpret_cast<ListHdr *>(dgf.as<uint8_t>(align256(8 * (size_t)ngran)));
+    hipError_t le = hipMemsetAsync(dh, 0, sizeof(ListHdr), ctx->upload_stream);
+    if (le == hipSuccess) {
+      hipLaunchKernelGGL(k_list_scan, dim3(np), dim3(BLOCK), 0, ctx->upload_stream, e.d, e.units, e.pm,
+                         dgf.as<uint64_t>(), dh);
+      hipLaunchKernelGGL(k_list_tail, dim3(1), dim3(1024), 0, ctx->upload_stream, np, e.pm, dgf.as<uint64_t>(), ngran);
+      le = hipGetLastError();
     }
-  }
-  const hipError_t se = hipStreamSynchronize(ctx->upload_stream);
-  dgf.release();
-  HIPCHECK(se);
-  if (size && *ctx->h_flag) return GBGPU_ECORRUPT;  // e.mem frees the copy
-  if (size) {
-    // the list's docid range (directory sizing): first key, last run start
-    e.dmin = e.dmax = host_docid(first18);
-    if (host_bytes) {
-      for (int64_t q = size - 6; q >= 18; q -= 6) {
-        if ((host_bytes[q + 1] & 0x02) && !(host_bytes[q] & 0x04)) {
-          e.dmax = host_docid(host_bytes + q);
-          break;
-        }
-      }
-    } else {
-      // k_gfirst: gf[g] is the first run docid at or after granule g, so the
-      // last granule with one holds the last run start (its head may end one
-      // unit past the granule)
-      size_t g = gf.size();
-      while (g > 0 && gf[g - 1] == ~0ULL) g--;
-      if (g > 0) {
-        const uint32_t u0 = (uint32_t)(g - 1) * (uint32_t)WCH_UNITS;
-        const uint32_t u1 = std::min<uint32_t>(e.units, u0 + (uint32_t)WCH_UNITS + 1);
-        std::vector<uint8_t> tail(6 * (size_t)(u1 - u0));
-        HIPCHECK(hipMemcpy(tail.data(), e.d + 6 * (size_t)u0, tail.size(), hipMemcpyDeviceToHost));
-        for (int64_t q = (int64_t)tail.size() - 12; q >= 0; q -= 6) {
-          if ((tail[q + 1] & 0x02) && !(tail[q] & 0x04)) {
-            e.dmax = host_docid(tail.data() + q);
-            break;
-          }
-        }
-      }
-    }
+    ListHdr hh;
+    if (le == hipSuccess) le = hipMemcpyAsync(gf.data(), dgf.p, 8 * (size_t)ngran, hipMemcpyDeviceToHost, ctx->upload_stream);
+    if (le == hipSuccess) le = hipMemcpyAsync(&hh, dh, sizeof hh, hipMemcpyDeviceToHost, ctx->upload_stream);
+    const hipError_t se = hipStreamSynchronize(ctx->upload_stream);
+    dgf.release();
+    HIPCHECK(le);
+    HIPCHECK(se);
+    if (hh.bad) return GBGPU_ECORRUPT;  // e.mem frees the copy
+    // granules past the list's units (the last page's tail) hold ~0
+    gf.resize((e.units + WCH_UNITS - 1) / WCH_UNITS);
+    e.dmin = host_docid(first18);  // the first key (the list starts with a run)
+    e.dmax = hh.dmax;
+    (void)host_bytes;
   }
   if (size) e.gfirst = std::make_shared<const std::vector<uint64_t>>(std::move(gf));
   e.live = true;
