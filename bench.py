@@ -79,6 +79,7 @@ def _gbref_requests(terms, lists, params, reps):
         req.append(struct.pack("<q", len(l)))
         req.append(bytes(l))
     req.append(struct.pack("<iiii", 128, 0, reps, 0))  # no whitelist lists
+    req.append(struct.pack("<ii", 0, 0))  # no boolean expression, no facet ranges
     return b"".join(req)
 
 

@@ -5608,7 +5608,8 @@ struct ListEntry {
 // second unit must not look like a key start; the list starts with a key), the
 // page's run starts (the page map), the first run docid of each of its four
 // granules (the granule table: ~0 where the page has none from there on; the
-// suffix over pages is k_list_tail's), and the last run docid (dmax).
+// host carries the next page's first into those), and the last run docid
+// (dmax).
 struct ListHdr {
   uint32_t bad;
   uint32_t pad;
@@ -5657,17 +5658,11 @@ __global__ void __launch_bounds__(BLOCK) k_list_scan(const uint8_t *__restrict__
   if (threadIdx.x == 0 && s_last) atomicMax(&hdr->dmax, (unsigned long long)lds_unit_docid(lds, s_last - 1));
 }
 
-// one block: the page map's exclusive scan (total at pm[npages]) and the
-// granule table's suffix over pages (a granule with no run start after it in
-// its page takes the next page's first)
-__global__ void __launch_bounds__(1024) k_list_tail(uint32_t npages, uint32_t *pm, uint64_t *gf, uint32_t ngran) {
+// one block: the page map's exclusive scan (total at pm[npages])
+__global__ void __launch_bounds__(1024) k_list_tail(uint32_t npages, uint32_t *pm) {
   __shared__ uint32_t tmp[16];
   __shared__ uint32_t carry;
-  __shared__ unsigned long long s_next[16], s_carry;
-  if (threadIdx.x == 0) {
-    carry = 0;
-    s_carry = ~0ull;
-  }
+  if (threadIdx.x == 0) carry = 0;
   __syncthreads();
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   for (uint32_t base = 0; base < npages; base += 1024) {
@@ -5689,28 +5684,6 @@ __global__ void __launch_bounds__(1024) k_list_tail(uint32_t npages, uint32_t *p
     __syncthreads();
   }
   if (threadIdx.x == 0) pm[npages] = carry;
-  // suffix minimum over the granules (docids ascend, ~0 = none), from the end,
-  // 1024 granules a round
-  const uint32_t rounds = (ngran + 1023) / 1024;
-  for (uint32_t r = 0; r < rounds; r++) {
-    const uint32_t base = (rounds - 1 - r) * 1024;
-    const uint32_t i = base + threadIdx.x;
-    unsigned long long v = i < ngran ? gf[i] : ~0ull;
-    // suffix min within the wave (lanes above)
-    for (int o = 1; o < 64; o <<= 1) {
-      const unsigned long long y = __shfl_down(v, o, 64);
-      if (lane + o < 64 && y < v) v = y;
-    }
-    if (lane == 0) s_next[wid] = v;  // the wave's minimum
-    __syncthreads();
-    unsigned long long after = s_carry;  // the rounds after this one
-    for (int w = wid + 1; w < 16; w++) after = s_next[w] < after ? s_next[w] : after;
-    if (after < v) v = after;
-    if (i < ngran) gf[i] = v;
-    __syncthreads();
-    if (threadIdx.x == 0) s_carry = v;  // thread 0 holds the round's minimum
-    __syncthreads();
-  }
 }
 
 // docid of the key starting at p (Posdb.h:295)
@@ -5974,9 +5947,9 @@ static int finish_list(gbgpu_ctx *ctx, ListEntry &e, const uint8_t *host_bytes, 
   const int64_t size = e.size;
   std::vector<uint64_t> gf;
   if (size) {
-    // one pass over the bytes (k_list_scan), the page scan and granule
-    // suffix (k_list_tail), then ONE synchronisation for the check, the
-    // granule table and the last run docid
+    // one pass over the bytes (k_list_scan), the page scan (k_list_tail),
+    // then ONE synchronisation for the check, the granule table and the last
+    // run docid
     const uint32_t np = (e.units + CHUNK_UNITS - 1) / CHUNK_UNITS;
     const uint32_t ngran = np * 4;
     gf.resize(ngran);
@@ -5987,7 +5960,7 @@ static int finish_list(gbgpu_ctx *ctx, ListEntry &e, const uint8_t *host_bytes, 
     if (le == hipSuccess) {
       hipLaunchKernelGGL(k_list_scan, dim3(np), dim3(BLOCK), 0, ctx->upload_stream, e.d, e.units, e.pm,
                          dgf.as<uint64_t>(), dh);
-      hipLaunchKernelGGL(k_list_tail, dim3(1), dim3(1024), 0, ctx->upload_stream, np, e.pm, dgf.as<uint64_t>(), ngran);
+      hipLaunchKernelGGL(k_list_tail, dim3(1), dim3(1024), 0, ctx->upload_stream, np, e.pm);
       le = hipGetLastError();
     }
     ListHdr hh;
@@ -5998,7 +5971,11 @@ static int finish_list(gbgpu_ctx *ctx, ListEntry &e, const uint8_t *host_bytes, 
     HIPCHECK(le);
     HIPCHECK(se);
     if (hh.bad) return GBGPU_ECORRUPT;  // e.mem frees the copy
-    // granules past the list's units (the last page's tail) hold ~0
+    // a granule with no run start after it in its page takes the next
+    // page's first (docids ascend; ~0: none); granules past the list's units
+    // (the last page's tail) hold ~0
+    for (size_t g = ngran - 1; g-- > 0;)
+      if (gf[g] == ~0ull) gf[g] = gf[g + 1];
     gf.resize((e.units + WCH_UNITS - 1) / WCH_UNITS);
     e.dmin = host_docid(first18);  // the first key (the list starts with a run)
     e.dmax = hh.dmax;
