@@ -3611,6 +3611,10 @@ __global__ void __launch_bounds__(SCORE_TPB) k_scoreinfo(const DevPlan *__restri
 //                 (the stack's bytes: undefined, the docid stays dropped);
 //   k_stale_fix   the writers' merges again, tapped for those bytes, then the
 //                 survivor scored with them where its empty group points.
+__global__ void k_gather_docs(const uint64_t *doc, const uint32_t *pos, const Counters *ctr, uint64_t *out) {
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < ctr->nstale; e += gridDim.x * blockDim.x) out[e] = doc[pos[e]];
+}
+
 __global__ void k_stale_rank(const uint32_t *order, uint32_t n, uint32_t *rank) {
   for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) rank[order[k]] = k;
 }
@@ -7502,7 +7506,8 @@ static int stale_fix(QuerySlot &q, uint32_t nsurv, uint32_t nstale) {
   };
   const size_t o_key = take(8 * (size_t)nsurv), o_val = take(4 * (size_t)nsurv), o_skey = take(8 * (size_t)nsurv),
                o_ord = take(4 * (size_t)nsurv), o_rank = take(4 * (size_t)nsurv), o_wr = take(24 * (size_t)nstale),
-               o_okey = take(4 * (size_t)nstale), o_fixc = take(16), o_tmp = take(sort_tmp);
+               o_okey = take(4 * (size_t)nstale), o_sdoc = take(8 * (size_t)nstale), o_fixc = take(16),
+               o_tmp = take(sort_tmp);
   // the fix arena: every survivor's merges once (k_stale_mb), then every
   // stale survivor's largest merge (its own records or a writer's)
   const unsigned long long usum = hc->surv_top & ((1ull << 36) - 1);
@@ -7536,11 +7541,14 @@ static int stale_fix(QuerySlot &q, uint32_t nsurv, uint32_t nstale) {
                      (const uint32_t *)q.svu.as<uint32_t>(), (const uint64_t *)q.svdoc.as<uint64_t>(),
                      (const Loc *)q.svloc.as<Loc>(), q.si.as<uint64_t>(o_arena), fcap,
                      q.si.as<unsigned long long>(o_fixc), q.skey.as<uint32_t>(), q.si.as<uint32_t>(o_okey));
+  hipLaunchKernelGGL(k_gather_docs, dim3(gs), dim3(256), 0, st, (const uint64_t *)q.svdoc.as<uint64_t>(),
+                     (const uint32_t *)q.stale.as<uint32_t>(), (const Counters *)dctr, q.si.as<uint64_t>(o_sdoc));
   HIPCHECK(hipGetLastError());
-  std::vector<uint32_t> pos(nstale), okey(nstale);
+  std::vector<uint32_t> okey(nstale);
+  std::vector<uint64_t> sdoc(nstale);
   unsigned long long fixc[2] = {0, 0};
   uint32_t unsup = 0;
-  HIPCHECK(hipMemcpyAsync(pos.data(), q.stale.p, 4 * (size_t)nstale, hipMemcpyDeviceToHost, st));
+  HIPCHECK(hipMemcpyAsync(sdoc.data(), q.si.as<uint8_t>(o_sdoc), 8 * (size_t)nstale, hipMemcpyDeviceToHost, st));
   HIPCHECK(hipMemcpyAsync(okey.data(), q.si.as<uint8_t>(o_okey), 4 * (size_t)nstale, hipMemcpyDeviceToHost, st));
   HIPCHECK(hipMemcpyAsync(fixc, q.si.as<uint8_t>(o_fixc), 16, hipMemcpyDeviceToHost, st));
   HIPCHECK(hipMemcpyAsync(&unsup, &dctr->unsup, 4, hipMemcpyDeviceToHost, st));
@@ -7549,12 +7557,8 @@ static int stale_fix(QuerySlot &q, uint32_t nsurv, uint32_t nstale) {
   q.stale_filt = (int32_t)fixc[1];
   // the docids of the scored ones, then the top list merged
   std::vector<std::pair<uint32_t, uint64_t>> all;
-  std::vector<uint64_t> sd(1);
-  for (uint32_t e = 0; e < nstale; e++) {
-    if (!okey[e]) continue;
-    HIPCHECK(hipMemcpy(sd.data(), q.svdoc.as<uint64_t>() + pos[e], 8, hipMemcpyDeviceToHost));
-    all.push_back({okey[e], sd[0]});
-  }
+  for (uint32_t e = 0; e < nstale; e++)
+    if (okey[e]) all.push_back({okey[e], sdoc[e]});
   if (all.empty()) return 0;
   uint32_t *keys = reinterpret_cast<uint32_t *>(q.h_res + res_keys_off());
   uint64_t *docs = reinterpret_cast<uint64_t *>(q.h_res + res_docs_off(q.k));
@@ -8183,7 +8187,8 @@ int gbgpu_file_list(gbgpu_ctx *ctx, int32_t fh, int64_t offset, int64_t size, co
   if (!size) return upload_list(ctx, nullptr, 0, handle);
   const uint8_t *src = f.mem->d + offset;
   uint8_t head[18] = {};
-  HIPCHECK(hipMemcpy(head, src, (size_t)std::min<int64_t>(18, size), hipMemcpyDeviceToHost));
+  HIPCHECK(hipMemcpyAsync(head, src, (size_t)std::min<int64_t>(18, size), hipMemcpyDeviceToHost, ctx->upload_stream));
+  HIPCHECK(hipStreamSynchronize(ctx->upload_stream));
   if (!(head[1] & 0x02)) return GBGPU_ECORRUPT;  // not a key start (Posdb.cpp:410-412)
   const int ks = (head[0] & 0x04) ? 6 : (head[0] & 0x02) ? 12 : 18;
   if (size < ks) return GBGPU_ECORRUPT;
