@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import subprocess
 import sys
@@ -200,7 +201,9 @@ def bench_config3(eng, num_docs, steps, slots, with_cpu):
         for i in range(max(0, nq - slots), nq):
             eng.collect(cap=4096, slot=i % slots)
 
-    run(len(qs))
+    # warm-up: every (slot, query) pair the timed rotation meets, so no slot
+    # grows its buffers inside the timed region
+    run(len(qs) * slots // math.gcd(len(qs), slots))
     eng.set_profiling(True)
     dev = []
     for j, q in enumerate(qs):
@@ -379,9 +382,12 @@ def main():
     total = per * world
     # GBGPU_DIAG=1: the diagnostic build (lib/libgbgpu_diag.so), whose
     # GBGPU_*_MODE switches time kernel phases; never the measured product
-    # GBGPU_LIB=alt: the A/B build (lib/libgbgpu_alt.so, Makefile `alt`)
+    # GBGPU_LIB=alt: the A/B build (lib/libgbgpu_alt.so, Makefile `alt`);
+    # GBGPU_LIB=<name>.so: another A/B build under lib/ (scripts/bisect_libs.sh)
+    lib = os.environ.get("GBGPU_LIB", "")
     eng = gbgpu.Engine(local_rank, diag=os.environ.get("GBGPU_DIAG") == "1",
-                       path=gbgpu.ALT_LIB_PATH if os.environ.get("GBGPU_LIB") == "alt" else None)
+                       path=gbgpu.ALT_LIB_PATH if lib == "alt" else
+                       os.path.join(gbgpu.PKG_DIR, "lib", lib) if lib.endswith(".so") else None)
     exchange = world > 1 or args.exchange
     if exchange and world == 1:
         eng.comm_init(1, 0, gbgpu.Engine.comm_unique_id())

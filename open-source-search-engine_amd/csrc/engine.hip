@@ -1849,7 +1849,19 @@ __global__ void __launch_bounds__(64 * PW, (G0 <= 2 && MODE == 11) ? 3 : 1) k_pr
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t wi = blockIdx.x * PW + wid;
   if (wi >= nwork) return;  // the whole wave: no block barrier follows
-  const ProbeWork w = work[wi];
+  ProbeWork w;
+  if (wi < pl->nwork_cand) {
+    w = work[wi];
+  } else {
+    const uint32_t i = wi - pl->nwork_cand;
+    uint32_t sg = 0;
+    while (sg + 1 < pl->nrseg && i >= pl->rseg_wbase[sg + 1]) sg++;
+    w.list = pl->rseg_list[sg];
+    w.u0 = (i - pl->rseg_wbase[sg]) * pl->run_span;
+    w.u1 = min(pl->lists[w.list].units, w.u0 + pl->run_span);
+    w.has_dfirst = 0;  // probe_by_run starts from the chunk's own run heads
+    w.dfirst = ~0ull;
+  }
   const DevList &L = pl->lists[w.list];
   ProbeOut po;
   po.bits = bits + (uint64_t)w.list * nwords;
@@ -5040,7 +5052,7 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
 // [4096 w, 4096 w + 4096) as 16 rows of 256, lane l bins 4l..4l+3 of a row;
 // the wave holding the need-th entry walks its rows, then its lanes, from
 // the top.  tmp: 16 words.
-__device__ void top_bin_hist(const uint32_t *h, uint32_t need, uint32_t *tmp, uint32_t *s_bin, uint32_t *s_above,
+__device__ __forceinline__ void top_bin_hist(const uint32_t *h, uint32_t need, uint32_t *tmp, uint32_t *s_bin, uint32_t *s_above,
                              uint32_t *s_total) {
   static_assert(TK_THREADS == 1024 && SEL_HBINS == 16 * 4096, "16 waves of 4096 bins");
   typedef uint32_t v4 __attribute__((ext_vector_type(4)));
@@ -5584,11 +5596,23 @@ struct DevBuf {
     cap = 0;
   }
 };
+// GBGPU_LIST_MALLOC (A/B knob): resident lists from hipMalloc instead of the
+// context's stream-ordered pool
+#ifndef GBGPU_LIST_MALLOC
+#define GBGPU_LIST_MALLOC 0
+#endif
+// GBGPU_DEFAULT_POOL (A/B knob): the device's default pool instead of the
+// context's own
+#ifndef GBGPU_DEFAULT_POOL
+#define GBGPU_DEFAULT_POOL 0
+#endif
 struct ListMem {
   uint8_t *d = nullptr;
   hipStream_t st = nullptr;
+  bool malloced = false;
   ~ListMem() {
-    if (d) (void)hipFreeAsync(d, st);
+    if (d && malloced) (void)hipFree(d);
+    else if (d) (void)hipFreeAsync(d, st);
   }
 };
 
@@ -5631,19 +5655,33 @@ __global__ void __launch_bounds__(BLOCK) k_list_scan(const uint8_t *__restrict__
   if (threadIdx.x == 0) s_last = 0;
   load_chunk(list, u0, lds);
   __syncthreads();
-  const uint32_t m = thread_starts(lds, u0, units);
-  uint32_t bad = 0;
+  // the thread's units' bytes 0-1 from three 16-B LDS reads (as thread_starts)
+  // and the next thread's first unit's from one aligned word: byte reads at
+  // the 48-byte thread stride were 4-way bank conflicts
+  uint32_t h[UPT + 1];
+  {
+    typedef uint32_t v4 __attribute__((ext_vector_type(4)));
+    const v4 *src = reinterpret_cast<const v4 *>(lds + threadIdx.x * UPT * 6);
+    const v4 a = src[0], b = src[1], c = src[2];
+    const uint32_t w[12] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w};
+#pragma unroll
+    for (int q = 0; q < UPT; q++) h[q] = (q & 1) ? (w[3 * (q >> 1) + 1] >> 16) : (w[3 * (q >> 1)] & 0xffffu);
+    h[UPT] = *reinterpret_cast<const uint32_t *>(lds + (threadIdx.x + 1) * UPT * 6) & 0xffffu;  // < CHUNK_LOAD
+  }
+  uint32_t m = 0, bad = 0;
 #pragma unroll
   for (int q = 0; q < UPT; q++) {
-    const uint32_t lu = threadIdx.x * UPT + q, u = u0 + lu;
+    const uint32_t u = u0 + threadIdx.x * UPT + q;
     if (u >= units) break;
-    const uint32_t b0 = lds[lu * 6], b1 = lds[lu * 6 + 1];
-    if (!(b1 & 0x02)) {
+    if (!(h[q] & 0x0200u)) {
       if (u == 0) bad = 1;  // the list must start with a key
       continue;
     }
-    if (!(b0 & 0x06)) bad = 1;
-    if (!(b0 & 0x04) && (u + 1 >= units || (lds[(lu + 1) * 6 + 1] & 0x02))) bad = 1;
+    if (!(h[q] & 0x06u)) bad = 1;
+    if (!(h[q] & 0x04u)) {
+      m |= 1u << q;  // a 12-byte key: a run start
+      if (u + 1 >= units || (h[q + 1] & 0x0200u)) bad = 1;
+    }
   }
   if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(&hdr->bad, 1u);
   if (m) {
@@ -5739,7 +5777,8 @@ struct QuerySlot {
   uint8_t *h_res = nullptr;    // pinned: counters + top list (device -> host, one copy)
   size_t hres_cap = 0;
   std::vector<G0Chunk> g0c;
-  std::vector<ProbeWork> pw;
+  std::vector<ProbeWork> pw;  // the candidate-driven probe waves (DevPlan::nwork_cand)
+  uint32_t nwork = 0;         // k_probe waves: pw, then the run-driven segments
   std::vector<uint32_t> afirst;
   std::vector<std::shared_ptr<ListMem>> held;  // lists the in-flight query reads
   // state of the in-flight query
@@ -5911,7 +5950,16 @@ static int alloc_list(gbgpu_ctx *ctx, int64_t size, ListEntry &e) {
   const size_t alloc = lbytes + page_map_bytes(e.units);
   e.mem = std::make_shared<ListMem>();
   e.mem->st = ctx->upload_stream;
-  if (DevBuf::pool_alloc(reinterpret_cast<void **>(&e.mem->d), alloc, ctx->pool, ctx->upload_stream)) return ENOMEM;
+  if (GBGPU_LIST_MALLOC) {
+    if (hipMalloc(reinterpret_cast<void **>(&e.mem->d), alloc) != hipSuccess) {
+      (void)hipGetLastError();
+      e.mem->d = nullptr;
+      return ENOMEM;
+    }
+    e.mem->malloced = true;
+  } else if (DevBuf::pool_alloc(reinterpret_cast<void **>(&e.mem->d), alloc, ctx->pool, ctx->upload_stream)) {
+    return ENOMEM;
+  }
   e.d = e.mem->d;
   e.pm = reinterpret_cast<uint32_t *>(e.d + lbytes);
   // the image's own bytes are written next: zero the pad and the page map
@@ -6442,12 +6490,23 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   // candidate search over several chunks
   const uint64_t pwaves = ctx->probe_waves ? (uint64_t)ctx->probe_waves : wide ? PROBE_WAVES_WIDE : PROBE_WAVES;
   const uint32_t S = (uint32_t)std::max<uint64_t>(1, (probe_chunks + pwaves - 1) / pwaves);
+  // a run-driven chunk costs a few dependent lookups: one chunk per wave,
+  // its work computed by the wave itself (DevPlan::rseg_*)
+  const uint32_t rspan = ctx->probe_runspan > 0 ? (uint32_t)ctx->probe_runspan : 1u;
+  P.run_span = WCH_UNITS * rspan;
+  P.nrseg = 0;
+  uint64_t rwaves = 0;
   for (int id = 0; id < P.nlists; id++) {
-    if (!P.lists[id].probe) continue;
+    if (P.lists[id].probe != PROBE_BY_RUN || !P.lists[id].units) continue;
+    P.rseg_list[P.nrseg] = (uint32_t)id;
+    P.rseg_wbase[P.nrseg++] = (uint32_t)rwaves;
+    rwaves += (P.lists[id].units + P.run_span - 1) / P.run_span;
+  }
+  P.rseg_wbase[P.nrseg] = (uint32_t)rwaves;
+  for (int id = 0; id < P.nlists; id++) {
+    if (P.lists[id].probe != PROBE_BY_CAND) continue;
     const uint32_t units = P.lists[id].units;
-    // a run-driven chunk costs a few dependent lookups: one chunk per wave
-    const uint32_t rspan = ctx->probe_runspan > 0 ? (uint32_t)ctx->probe_runspan : 1u;
-    const uint32_t span = P.lists[id].probe == PROBE_BY_RUN ? WCH_UNITS * rspan : cunits * S;
+    const uint32_t span = cunits * S;
     const std::vector<uint64_t> *gf = lent[id]->gfirst.get();
     for (uint32_t u = 0; u < units; u += span) {
       ProbeWork pw{(uint32_t)id, u, std::min(units, u + span), 0u, ~0ull};
@@ -6458,6 +6517,8 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
       q.pw.push_back(pw);
     }
   }
+  P.nwork_cand = (uint32_t)q.pw.size();
+  q.nwork = P.nwork_cand + (uint32_t)rwaves;
   q.scan_bytes = scan;
   q.g0_bytes = 0;
   q.probe_bytes = 0;
@@ -6573,7 +6634,7 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   hipLaunchKernelGGL(k_write_runs, dim3(ng0), dim3(BLOCK), 0, st, dpl, dchunks, q.cand.as<uint64_t>(),
                      q.cunit.as<uint32_t>(), dctr, ng0, q.dir.as<uint64_t>());
   if (ctx->profiling) HIPCHECK(hipEventRecord(q.ev[1], st));
-  if (!q.pw.empty()) {
+  if (q.nwork) {
 #ifdef GBGPU_DIAG
     auto kp = ctx->probe_mode == 11  ? (P.g0n <= 1 ? k_probe<11, 1> : k_probe<11, 2>)  // diagnostic: 6 KiB chunks
               : ctx->probe_mode == 10 ? (P.g0n <= 2 ? k_probe<10, 2> : k_probe<10, 4>)  // diagnostic: bucket tables
@@ -6591,7 +6652,7 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
 #else
     auto kp = P.g0n == 1 ? k_probe<0, 1> : P.g0n == 2 ? k_probe<0, 2> : P.g0n <= 4 ? k_probe<0, 4> : k_probe<0, MAXG0>;
 #endif
-    const uint32_t nwork = (uint32_t)q.pw.size();
+    const uint32_t nwork = q.nwork;
     hipLaunchKernelGGL(kp, dim3((nwork + PW - 1) / PW), dim3(64 * PW), 0, st, dpl, dwork, nwork,
                        q.cand.as<uint64_t>(), bits, nwords, loc, dctr, q.dir.as<uint64_t>());
   }
@@ -8015,7 +8076,7 @@ int gbgpu_open(int device, gbgpu_ctx **out) {
   if (hipSetDevice(device) != hipSuccess) return GBGPU_ENODEVICE;
   gbgpu_ctx *ctx = new gbgpu_ctx();
   ctx->device = device;
-  {
+  if (!GBGPU_DEFAULT_POOL) {
     // the slots' stream-ordered buffers, resident lists and file images come
     // from the context's own pool (the device's default pool and its
     // process-wide settings are left alone): up to POOL_KEEP of what they

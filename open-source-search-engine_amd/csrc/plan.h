@@ -167,6 +167,16 @@ struct DevPlan {
   uint64_t dbg_doc;            // diagnostic (GBGPU_PROBE_DEBUG_DOC): k_probe traces this docid's runs
   unsigned long long *dbg_buf; // into this buffer: a count, then 16-word records
   DevList lists[MAXL];
+  // run-driven probe work (PROBE_BY_RUN lists) without a per-wave table:
+  // wave nwork_cand + i scans run_span units of list rseg_list[s], the
+  // segment s with rseg_wbase[s] <= i < rseg_wbase[s + 1], from unit
+  // (i - rseg_wbase[s]) * run_span; the candidate-driven waves come first
+  // and read the staged ProbeWork array
+  uint32_t nwork_cand;
+  uint32_t nrseg;
+  uint32_t run_span;
+  uint32_t rseg_list[MAXL];
+  uint32_t rseg_wbase[MAXL + 1];
 };
 
 // setQueryTermInfo + minListi; returns 0 or error.

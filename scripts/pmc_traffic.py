@@ -14,7 +14,7 @@ import sys
 
 
 # kernels whose HBM reads are 16-B lane loads (v4 chunk / window loads)
-WIDE = {"k_probe", "k_write_runs", "k_page_count", "k_validate", "k_stream_read", "k_stream_copy"}
+WIDE = {"k_probe", "k_write_runs", "k_page_count", "k_validate", "k_list_scan", "k_stream_read", "k_stream_copy"}
 
 
 def is_wide(k):
