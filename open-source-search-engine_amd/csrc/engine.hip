@@ -2695,12 +2695,12 @@ __device__ __forceinline__ void load4u(gu8 *src, uint32_t b, uint64_t *v) {
 struct MbufTap {
   uint32_t lo;
   uint32_t got;  // bit i: b[i] written
-  uint8_t b[8];
+  uint8_t b[12];
 };
 __device__ __forceinline__ void tap_rec(MbufTap *t, uint32_t off, uint64_t lo6, uint64_t hi6, int n) {
   for (int i = 0; i < n; i++) {
     const uint32_t p = off + (uint32_t)i;
-    if (p >= t->lo && p < t->lo + 6) {
+    if (p >= t->lo && p < t->lo + 12) {
       const uint64_t src = i < 6 ? lo6 : hi6;
       t->b[p - t->lo] = (uint8_t)(src >> (8 * (i % 6)));
       t->got |= 1u << (p - t->lo);
@@ -3081,15 +3081,30 @@ __device__ __forceinline__ void score_survivor(const DevPlan *__restrict__ pl, c
   if (stale_out) *stale_out = empty_pos;
   if constexpr (MB) {
     if (mtot_out) *mtot_out = mtot;
-    if (tap) {  // stale_fix: this docid's mbuf bytes only
-      *key_out = 0;
+    if (tap) {  // stale_fix: this docid's mbuf bytes only; key_out 1: no plain group gave a key
+      *key_out = siteRank < 0 ? 1u : 0u;
       return;
     }
     if (empty_pos && inject) {
-      // stale_fix: the bytes earlier docids of the pass left where the
-      // trailing empty group points (the record store has room for one more)
-      rec.put((int)nrec, *inject);
+      // stale_fix / k_si_stale: the bytes earlier docids of the call left
+      // where the trailing empty group points (the record store has room
+      // for one more): inject[0] its bytes 0-5; inject[1] bytes 6-11 with bit
+      // 63 set when known.  A docid no plain group gave a key takes siteRank
+      // and langId from there too (the group's list pointer, Posdb.cpp:
+      // 6984-7003)
+      rec.put((int)nrec, inject[0]);
       empty_pos = false;
+      if (siteRank < 0 && (inject[1] >> 63)) {
+        bool plain = false;
+        for (int j = 0; j < ng; j++)
+          if (!(pl->gflags0[j] & (BF_NEGATIVE | BF_NUMBER | BF_FACET))) plain = true;
+        if (plain) {
+          const uint32_t b0 = (uint32_t)(inject[0] & 0xff), b6 = (uint32_t)(inject[1] & 0xff),
+                         b7 = (uint32_t)((inject[1] >> 8) & 0xff);
+          siteRank = (int)(((b6 >> 5) | ((b7 & 1) << 3)) & 0x0f);
+          docLang = (int)((b6 & 0x1f) | ((b0 & 0x08) ? 0x20 : 0));
+        }
+      }
     }
   }
   float score = 0.0f;
@@ -3130,6 +3145,7 @@ __device__ __forceinline__ void score_survivor(const DevPlan *__restrict__ pl, c
     so->site_rank = siteRank < 0 ? 0 : siteRank;
     so->doc_lang = docLang;
     so->ok = empty_pos ? -2 : ok;
+    if (siteRank < 0) so->pad = 1;  // no plain group gave a key (a stale docid's siteRank is in mbuf)
   }
   uint32_t key = 0;
   if (ok) {
@@ -3528,38 +3544,12 @@ __device__ int si_word_pos_list(const SiList &L, uint64_t docId, uint32_t own, i
   return -1;
 }
 
-// one lane per tree docid: the first pass's score_survivor again, with the
-// recorder, over the survivor's arena range (k_score's fallback store)
-__global__ void __launch_bounds__(SCORE_TPB) k_scoreinfo(const DevPlan *__restrict__ pl, Counters *ctr, const uint32_t *sv_slot,
-                                                         const uint32_t *sv_lm, const uint32_t *sv_u,
-                                                         const Loc *sv_loc, uint64_t *arena,
-                                                         unsigned long long arena_cap, const uint64_t *tdoc,
-                                                         const uint64_t *sdoc, const uint32_t *sperm,
-                                                         const uint32_t *cum, uint32_t nsurv,
-                                                         uint32_t n, SurvOut *info, int32_t *counts,
-                                                         gbgpu_single_score *ss, int scap, gbgpu_pair_score *ps,
-                                                         int pcap) {
-  __shared__ float s_sm[npairs<MAXG>() * SCORE_TPB];
-  stage_weights(&c_weights);
-  const uint32_t t = blockIdx.x * SCORE_TPB + threadIdx.x;
-  if (t >= n) return;
-  SurvOut so{0.0f, 0, 0, -1};
-  const uint64_t d = tdoc[t];
-  uint32_t lo = 0, hi = nsurv;
-  while (lo < hi) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (sdoc[mid] < d) lo = mid + 1;
-    else hi = mid;
-  }
-  if (lo >= nsurv || sdoc[lo] != d) {  // not a survivor: reported as ECORRUPT
-    info[t] = so;
-    return;
-  }
-  const uint32_t i = sperm[lo];
-  const uint32_t s = sv_slot[i];
-  // the sublists getWordPosList finds the docid in (Posdb.cpp:6195-6241)
-  const uint32_t lm = sv_lm[i];
-  uint16_t kill[MAXG];
+// the sublists getWordPosList finds docid d in (Posdb.cpp:6195-6241): kill
+// bit x of group j where it misses; d is the survivor of docid-order rank lo
+// with list mask lm.  < 0: a path not replayed (*blid: the list)
+__device__ int si_kill(const DevPlan *__restrict__ pl, const Counters *ctr, const Loc *sv_loc, const uint32_t *sperm,
+                       const uint32_t *cum, uint32_t nsurv, uint64_t d, uint32_t lo, uint32_t lm, uint16_t *kill,
+                       int *blid) {
   for (int j = 0; j < MAXG; j++) kill[j] = 0;
   const uint32_t anys = ctr->anysurv;
   for (int j = 0; j < pl->ngroups; j++) {
@@ -3573,26 +3563,83 @@ __global__ void __launch_bounds__(SCORE_TPB) k_scoreinfo(const DevPlan *__restri
       const int64_t U = (int64_t)L.cum[nsurv] + ((later && ctr->ext[lid].slot1) ? ctr->ext[lid].E : 0);
       const int f = si_word_pos_list(L, d, L.cum[lo], U);
       if (f < 0) {
-        so.ok = -2;
-        so.pad = f * 1000 - lid;  // diagnostic (GBGPU_SI_DEBUG): which path, which list
-        info[t] = so;
-        return;
+        *blid = lid;
+        return f;
       }
       if (f == 0) kill[j] |= (uint16_t)(1u << x);
     }
   }
-  // the records go to a range of the global arena (a re-shrunk copy's
-  // relocated range where k_ext_walk gave it one)
-  uint32_t units = sv_u[i];
-  unsigned long long off = ~0ull;
+  return 0;
+}
+
+// docid-order rank of tree docid d among the survivors (sdoc sorted), or nsurv
+__device__ __forceinline__ uint32_t si_rank(const uint64_t *sdoc, uint32_t nsurv, uint64_t d) {
+  uint32_t lo = 0, hi = nsurv;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (sdoc[mid] < d) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo < nsurv && sdoc[lo] == d ? lo : nsurv;
+}
+
+// a survivor's record units, as k_score sizes its store (its re-shrunk copies
+// grow by E units each), and the arena offset of a relocated copy (~0: none)
+__device__ __forceinline__ uint32_t surv_units_off(const DevPlan *__restrict__ pl, const Counters *ctr, uint32_t s,
+                                                   uint32_t lm, uint32_t u, unsigned long long *off) {
+  *off = ~0ull;
   for (uint32_t x = lm & pl->reshare_mask; x; x &= x - 1) {
     const int l = __ffs(x) - 1;
     const ListExt &e = ctr->ext[l];
     if (e.slot1 == s + 1) {
-      units += e.E * (uint32_t)(pl->lists[l].uses - 1);
-      if (e.reloc) off = e.off;
+      u += e.E * (uint32_t)(pl->lists[l].uses - 1);
+      if (e.reloc) *off = e.off;
     }
   }
+  return u;
+}
+
+// one lane per tree docid: the first pass's score_survivor again, with the
+// recorder, over the survivor's arena range (k_score's fallback store); mt:
+// the mbuf bytes its merges write (the second pass's stale-byte replay,
+// k_si_stale); a docid whose last merged group comes out empty is ok = -4
+__global__ void __launch_bounds__(SCORE_TPB) k_scoreinfo(const DevPlan *__restrict__ pl, Counters *ctr, const uint32_t *sv_slot,
+                                                         const uint32_t *sv_lm, const uint32_t *sv_u,
+                                                         const Loc *sv_loc, uint64_t *arena,
+                                                         unsigned long long arena_cap, const uint64_t *tdoc,
+                                                         const uint64_t *sdoc, const uint32_t *sperm,
+                                                         const uint32_t *cum, uint32_t nsurv,
+                                                         uint32_t n, SurvOut *info, int32_t *counts,
+                                                         gbgpu_single_score *ss, int scap, gbgpu_pair_score *ps,
+                                                         int pcap, uint32_t *mt) {
+  __shared__ float s_sm[npairs<MAXG>() * SCORE_TPB];
+  stage_weights(&c_weights);
+  const uint32_t t = blockIdx.x * SCORE_TPB + threadIdx.x;
+  if (t >= n) return;
+  SurvOut so{0.0f, 0, 0, -1};
+  mt[t] = 0;
+  const uint64_t d = tdoc[t];
+  const uint32_t lo = si_rank(sdoc, nsurv, d);
+  if (lo >= nsurv) {  // not a survivor: reported as ECORRUPT
+    info[t] = so;
+    return;
+  }
+  const uint32_t i = sperm[lo];
+  const uint32_t s = sv_slot[i];
+  const uint32_t lm = sv_lm[i];
+  uint16_t kill[MAXG];
+  int blid = 0;
+  const int f = si_kill(pl, ctr, sv_loc, sperm, cum, nsurv, d, lo, lm, kill, &blid);
+  if (f < 0) {
+    so.ok = -2;
+    so.pad = f * 1000 - blid;  // diagnostic (GBGPU_SI_DEBUG): which path, which list
+    info[t] = so;
+    return;
+  }
+  // the records go to a range of the global arena (a re-shrunk copy's
+  // relocated range where k_ext_walk gave it one)
+  unsigned long long off;
+  const uint32_t units = surv_units_off(pl, ctr, s, lm, sv_u[i], &off);
   if (off == ~0ull) off = atomicAdd(&ctr->arena_top, (unsigned long long)units);
   if (off + units > arena_cap) {
     so.ok = -3;  // arena exhausted (not reached: the host sizes it for every survivor)
@@ -3600,14 +3647,124 @@ __global__ void __launch_bounds__(SCORE_TPB) k_scoreinfo(const DevPlan *__restri
     return;
   }
   ScoreRec rec{ss + (size_t)t * scap, ps + (size_t)t * pcap, 0, 0, scap, pcap};
-  uint32_t key, nr;
+  uint32_t key, nr, mtot = 0;
+  bool stale = false;
   uint64_t tmerge = 0, tm[3] = {0, 0, 0};
   const GlobalRecs grec{(__attribute__((address_space(1))) uint64_t *)(arena + off)};
-  score_survivor<MAXG, MAXSUB>(pl, ctr, s, lm, anys, sv_loc + (uint64_t)i * (uint32_t)pl->nlists, grec,
-                               s_sm + threadIdx.x, &key, 0, &nr, false, tmerge, tm, &rec, &so, kill);
+  score_survivor<MAXG, MAXSUB, GlobalRecs, ScoreRec, true>(pl, ctr, s, lm, ctr->anysurv,
+                                                           sv_loc + (uint64_t)i * (uint32_t)pl->nlists, grec,
+                                                           s_sm + threadIdx.x, &key, 0, &nr, false, tmerge, tm, &rec, &so,
+                                                           kill, &mtot, &stale);
+  if (stale) so.ok = -4;
+  mt[t] = mtot;
   info[t] = so;
   counts[2 * t] = rec.ns;
   counts[2 * t + 1] = rec.np;
+}
+
+// The second pass's stale-byte docids (ok = -4 above): its docids run in tree
+// order after the first pass in the same call (Posdb.cpp:6116-6160), so the 6
+// bytes a stale docid's scorers read are those of the latest earlier docid of
+// the second pass whose merges (getWordPosList's sublists) reached them, else
+// of the first pass's last docid (vote-buffer order) that did.  One lane per
+// stale docid: each writer's merge again, tapped for its bytes, then the docid
+// scored and recorded with them.
+struct SiStale {
+  uint32_t t;      // its position in the second pass
+  uint32_t O;      // its mbuf bytes (where its empty group points)
+  uint32_t nb;     // bytes read there: 6, or 12 when no plain group gave it a key (siteRank, langId)
+  uint32_t w[12];  // each byte's writer: a second-pass position, or 0x80000000 | a first-pass survivor index
+};
+__global__ void __launch_bounds__(SCORE_TPB) k_si_stale(const DevPlan *__restrict__ pl, Counters *ctr,
+                                                        const uint32_t *sv_slot, const uint32_t *sv_lm,
+                                                        const uint32_t *sv_u, const Loc *sv_loc, uint64_t *arena,
+                                                        unsigned long long arena_cap, unsigned long long *fixc,
+                                                        const uint64_t *tdoc, const uint64_t *sdoc,
+                                                        const uint32_t *sperm, const uint32_t *cum, uint32_t nsurv,
+                                                        const SiStale *ent, uint32_t ne, SurvOut *info,
+                                                        int32_t *counts, gbgpu_single_score *ss, int scap,
+                                                        gbgpu_pair_score *ps, int pcap) {
+  __shared__ float s_sm[npairs<MAXG>() * SCORE_TPB];
+  stage_weights(&c_weights);
+  const uint32_t e = blockIdx.x * SCORE_TPB + threadIdx.x;
+  if (e >= ne) return;
+  const SiStale E = ent[e];
+  const uint32_t anys = ctr->anysurv;
+  const uint32_t nl = (uint32_t)pl->nlists;
+  SurvOut so{0.0f, 0, 0, -3};  // -3 on a failed replay (capacity / a tap that missed): the host declines
+  // survivor index and kill mask of second-pass position t (false: not replayable)
+  auto second = [&](uint32_t t, uint32_t &i, uint16_t *kill) -> bool {
+    const uint64_t d = tdoc[t];
+    const uint32_t lo = si_rank(sdoc, nsurv, d);
+    if (lo >= nsurv) return false;
+    i = sperm[lo];
+    int blid = 0;
+    return si_kill(pl, ctr, sv_loc, sperm, cum, nsurv, d, lo, sv_lm[i], kill, &blid) == 0;
+  };
+  // room for the largest merge this lane runs (plus the injected record)
+  uint32_t me = 0;
+  uint16_t kill[MAXG];
+  if (!second(E.t, me, kill)) {
+    info[E.t] = so;
+    return;
+  }
+  unsigned long long roff;
+  uint32_t need = surv_units_off(pl, ctr, sv_slot[me], sv_lm[me], sv_u[me], &roff) + 1;
+  uint32_t wi[12];
+  for (uint32_t p = 0; p < E.nb; p++) {
+    uint16_t k2[MAXG];
+    wi[p] = E.w[p] & 0x7fffffffu;
+    if (!(E.w[p] & 0x80000000u) && !second(E.w[p], wi[p], k2)) {
+      info[E.t] = so;
+      return;
+    }
+    const uint32_t u = surv_units_off(pl, ctr, sv_slot[wi[p]], sv_lm[wi[p]], sv_u[wi[p]], &roff);
+    need = u > need ? u : need;
+  }
+  const unsigned long long off = atomicAdd(&fixc[0], (unsigned long long)need);
+  if (off + need > arena_cap) {
+    info[E.t] = so;
+    return;
+  }
+  const GlobalRecs grec{(__attribute__((address_space(1))) uint64_t *)(arena + off)};
+  uint32_t key = 0, nr = 0;
+  uint64_t tmerge = 0, tm[3] = {0, 0, 0};
+  uint64_t inj[2] = {0, 0};
+  uint32_t done = 0;
+  for (uint32_t p = 0; p < E.nb; p++) {
+    if (done >> p & 1) continue;
+    const uint32_t w = wi[p];
+    const bool first = (E.w[p] & 0x80000000u) != 0;
+    uint16_t k2[MAXG];
+    uint32_t wdummy = 0;
+    if (!first) (void)second(E.w[p], wdummy, k2);
+    MbufTap tap;
+    tap.lo = E.O;
+    tap.got = 0;
+    score_survivor<MAXG, MAXSUB, GlobalRecs, NoRec, true>(pl, ctr, sv_slot[w], sv_lm[w], anys, sv_loc + (uint64_t)w * nl,
+                                                          grec, s_sm + threadIdx.x, &key, 0, &nr, false, tmerge, tm,
+                                                          nullptr, nullptr, first ? nullptr : k2, nullptr, nullptr,
+                                                          nullptr, &tap);
+    for (uint32_t q2 = p; q2 < E.nb; q2++) {
+      if (E.w[q2] != E.w[p]) continue;
+      if (!(tap.got >> q2 & 1)) {
+        info[E.t] = so;  // the writer's count said it reached the byte but the tap missed it: not reached
+        return;
+      }
+      inj[q2 / 6] |= (uint64_t)tap.b[q2] << (8 * (q2 % 6));
+      done |= 1u << q2;
+    }
+  }
+  if (E.nb == 12) inj[1] |= 1ull << 63;
+  ScoreRec rec{ss + (size_t)E.t * scap, ps + (size_t)E.t * pcap, 0, 0, scap, pcap};
+  SurvOut so2{0.0f, 0, 0, -1};
+  score_survivor<MAXG, MAXSUB, GlobalRecs, ScoreRec, true>(pl, ctr, sv_slot[me], sv_lm[me], anys,
+                                                           sv_loc + (uint64_t)me * nl, grec, s_sm + threadIdx.x, &key, 0,
+                                                           &nr, false, tmerge, tm, &rec, &so2, kill, nullptr, nullptr,
+                                                           inj, nullptr);
+  info[E.t] = so2;
+  counts[2 * E.t] = rec.ns;
+  counts[2 * E.t + 1] = rec.np;
 }
 
 // ------------------------------------------------------ stale-mbuf replay
@@ -3624,7 +3781,7 @@ __global__ void __launch_bounds__(SCORE_TPB) k_scoreinfo(const DevPlan *__restri
 //   k_stale_fix   the writers' merges again, tapped for those bytes, then the
 //                 survivor scored with them where its empty group points.
 __global__ void k_gather_docs(const uint64_t *doc, const uint32_t *pos, const Counters *ctr, uint64_t *out) {
-  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < ctr->nstale; e += gridDim.x * blockDim.x) out[e] = doc[pos[e]];
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < ctr->nstale; e += gridDim.x * blockDim.x) out[e] = doc[pos[e] & 0x7fffffffu];
 }
 
 __global__ void k_stale_rank(const uint32_t *order, uint32_t n, uint32_t *rank) {
@@ -3637,13 +3794,14 @@ __global__ void k_stale_find(Counters *ctr, const uint32_t *stale, const uint32_
                              const uint32_t *rank, uint32_t *wr) {
   const uint32_t ns = ctr->nstale;
   for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < ns; e += gridDim.x * blockDim.x) {
-    const uint32_t si = stale[e];
+    const uint32_t si = stale[e] & 0x7fffffffu;
+    const uint32_t nb = (stale[e] >> 31) ? 12u : 6u;  // 12: its siteRank / langId are read there too
     const uint32_t O = sv_mb[si];
-    uint32_t w6[6];
+    uint32_t w12[12];
 #pragma unroll
-    for (int p = 0; p < 6; p++) w6[p] = ~0u;
+    for (int p = 0; p < 12; p++) w12[p] = ~0u;
     uint32_t need = 0, steps = 0;
-    for (int64_t j = (int64_t)rank[si] - 1; j >= 0 && need < 6; j--) {
+    for (int64_t j = (int64_t)rank[si] - 1; j >= 0 && need < nb; j--) {
       if (++steps > STALE_SCAN) {
         ctr->unsup = 1;
         break;
@@ -3651,15 +3809,15 @@ __global__ void k_stale_find(Counters *ctr, const uint32_t *stale, const uint32_
       const uint32_t w = order[j];
       const uint32_t T = sv_mb[w];
       if (T > O + need) {
-        const uint32_t upto = min(6u, T - O);
+        const uint32_t upto = min(nb, T - O);
 #pragma unroll
-        for (int p = 0; p < 6; p++)
-          if ((uint32_t)p >= need && (uint32_t)p < upto) w6[p] = w;
+        for (int p = 0; p < 12; p++)
+          if ((uint32_t)p >= need && (uint32_t)p < upto) w12[p] = w;
         need = upto;
       }
     }
 #pragma unroll
-    for (int p = 0; p < 6; p++) wr[(size_t)e * 6 + p] = w6[p];
+    for (int p = 0; p < 12; p++) wr[(size_t)e * 12 + p] = w12[p];
   }
 }
 
@@ -3704,7 +3862,9 @@ __global__ void __launch_bounds__(SCORE_TPB) k_stale_mb(const DevPlan *__restric
                                                         &nr, false, tmerge, tm, nullptr, nullptr, nullptr, &mt, &st,
                                                         nullptr, &tap);
   sv_mb[i] = mt;
-  if (st) stale[atomicAdd((uint32_t *)&fixc[1], 1u)] = i;  // the list k_stale_find walks
+  // the list k_stale_find walks (bit 31: no plain group gave a key, so its
+  // siteRank / langId come from the stale bytes too)
+  if (st) stale[atomicAdd((uint32_t *)&fixc[1], 1u)] = i | (key ? 0x80000000u : 0u);
 }
 
 // one lane per stale survivor; okey: its key (0: undefined bytes, not
@@ -3722,20 +3882,20 @@ __global__ void __launch_bounds__(SCORE_TPB) k_stale_fix(const DevPlan *__restri
   if (e >= ns) return;
   const uint32_t anys = ctr->anysurv;
   const uint32_t nl = (uint32_t)pl->nlists;
-  const uint32_t i = stale[e];
-  uint32_t w6[6];
+  const uint32_t i = stale[e] & 0x7fffffffu;
+  const uint32_t nb = (stale[e] >> 31) ? 12u : 6u;
+  uint32_t w6[12];
   bool defined = true;
 #pragma unroll
-  for (int p = 0; p < 6; p++) {
-    w6[p] = wr[(size_t)e * 6 + p];
-    defined &= w6[p] != ~0u;
+  for (int p = 0; p < 12; p++) {
+    w6[p] = wr[(size_t)e * 12 + p];
+    defined &= (uint32_t)p >= nb || w6[p] != ~0u;
   }
   okey[e] = 0;
   if (!defined) return;  // bytes no docid of the pass wrote: the docid stays dropped
   // room for the largest merge this lane runs (plus the injected record)
   uint32_t need = surv_units(pl, ctr, sv_slot[i], sv_lm[i], sv_u[i]) + 1;
-#pragma unroll
-  for (int p = 0; p < 6; p++) {
+  for (uint32_t p = 0; p < nb; p++) {
     const uint32_t w = w6[p];
     const uint32_t u = surv_units(pl, ctr, sv_slot[w], sv_lm[w], sv_u[w]);
     need = u > need ? u : need;
@@ -3750,9 +3910,9 @@ __global__ void __launch_bounds__(SCORE_TPB) k_stale_fix(const DevPlan *__restri
   uint64_t tmerge = 0, tm[3] = {0, 0, 0};
   // the writers' bytes at [O, O + 6), each writer's merges once
   const uint32_t O = sv_mb[i];
-  uint64_t inj = 0;
+  uint64_t inj[2] = {0, 0};  // bytes 0-5, 6-11
   uint32_t done = 0;
-  for (int p = 0; p < 6; p++) {
+  for (uint32_t p = 0; p < nb; p++) {
     if (done >> p & 1) continue;
     const uint32_t w = w6[p];
     MbufTap tap;
@@ -3761,20 +3921,21 @@ __global__ void __launch_bounds__(SCORE_TPB) k_stale_fix(const DevPlan *__restri
     score_survivor<MAXG, MAXSUB, GlobalRecs, NoRec, true>(pl, ctr, sv_slot[w], sv_lm[w], anys, sv_loc + (uint64_t)w * nl,
                                                           grec, s_sm + threadIdx.x, &key, 0, &nr, false, tmerge, tm,
                                                           nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, &tap);
-    for (int q = p; q < 6; q++) {
+    for (uint32_t q = p; q < nb; q++) {
       if (w6[q] != w) continue;
       if (!(tap.got >> q & 1)) {
         ctr->unsup = 1;  // the writer wrote past the byte (sv_mb) but the tap missed it: not reached
         return;
       }
-      inj |= (uint64_t)tap.b[q] << (8 * q);
+      inj[q / 6] |= (uint64_t)tap.b[q] << (8 * (q % 6));
       done |= 1u << q;
     }
   }
+  if (nb == 12) inj[1] |= 1ull << 63;
   // the survivor itself, the bytes where its empty group points
   score_survivor<MAXG, MAXSUB, GlobalRecs, NoRec, true>(pl, ctr, sv_slot[i], sv_lm[i], anys, sv_loc + (uint64_t)i * nl,
                                                         grec, s_sm + threadIdx.x, &key, 0, &nr, false, tmerge, tm,
-                                                        nullptr, nullptr, nullptr, nullptr, nullptr, &inj, nullptr);
+                                                        nullptr, nullptr, nullptr, nullptr, nullptr, inj, nullptr);
   // the paging filter (Posdb.cpp:7327-7347), as k_score applies it
   if (pl->has_serp && key) {
     const uint64_t d = sv_doc[i];
@@ -5769,6 +5930,7 @@ struct QuerySlot {
   DevBuf si;                                // second pass's score info (score_info)
   DevBuf fac;                               // facet tables (facet_pass)
   DevBuf svmb, stale;                       // survivors' mbuf bytes; the stale-mbuf survivors (stale_fix)
+  DevBuf si2;                               // the second pass's stale-byte replay (k_si_stale)
   std::vector<FacetTerm> facets;            // the query's facet terms with a table
   std::vector<uint64_t> h_white;            // its host copy (the upload's source)
   uint32_t epoch = 0;
@@ -5806,9 +5968,9 @@ struct QuerySlot {
   hipEvent_t ev_done = nullptr;  // the query's device work is done (the exchange waits on it)
   float last_ms[6] = {0, 0, 0, 0, 0, 0};
 
-  DevBuf *const bufs[31] = {&tables, &chunkcnt, &cand, &cunit, &bits, &loc, &svslot, &svlm, &svu, &svdoc,
+  DevBuf *const bufs[32] = {&tables, &chunkcnt, &cand, &cunit, &bits, &loc, &svslot, &svlm, &svu, &svdoc,
                             &svloc, &scratch, &skey, &sel, &gath, &res, &dir, &split, &swin, &blk,
-                            &sflag, &ord, &oslot, &rep, &tree, &white, &wrej, &si, &fac, &svmb, &stale};
+                            &sflag, &ord, &oslot, &rep, &tree, &white, &wrej, &si, &fac, &svmb, &stale, &si2};
   int init(hipMemPool_t pool) {
     if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return GBGPU_EHIP;
     for (auto *b : bufs) {
@@ -6965,7 +7127,8 @@ static int score_info_docs(QuerySlot &q, const uint64_t *docs, int n, uint32_t n
   const size_t o_cnt = o_info + align256(sizeof(SurvOut) * (size_t)n);
   const size_t o_ss = o_cnt + align256(8 * (size_t)n);
   const size_t o_ps = o_ss + align256(sizeof(gbgpu_single_score) * (size_t)n * scap);
-  const size_t total = o_ps + sizeof(gbgpu_pair_score) * (size_t)n * pcap;
+  const size_t o_mt = o_ps + align256(sizeof(gbgpu_pair_score) * (size_t)n * pcap);
+  const size_t total = o_mt + 4 * (size_t)n;
   if (q.si.ensure(total)) return ENOMEM;
   hipStream_t st = q.stream;
   const uint32_t g = std::max(1u, std::min<uint32_t>(1024, (nsurv + 255) / 256));
@@ -6982,19 +7145,131 @@ static int score_info_docs(QuerySlot &q, const uint64_t *docs, int n, uint32_t n
                      (unsigned long long)(q.scratch.cap / 8), q.si.as<uint64_t>(o_tdoc), q.si.as<uint64_t>(o_skey), q.si.as<uint32_t>(o_sval),
                      q.si.as<uint32_t>(o_cum), nsurv, (uint32_t)n, q.si.as<SurvOut>(o_info),
                      q.si.as<int32_t>(o_cnt), q.si.as<gbgpu_single_score>(o_ss), scap,
-                     q.si.as<gbgpu_pair_score>(o_ps), pcap);
+                     q.si.as<gbgpu_pair_score>(o_ps), pcap, q.si.as<uint32_t>(o_mt));
   HIPCHECK(hipGetLastError());
   std::vector<SurvOut> info((size_t)n);
   std::vector<int32_t> cnt(2 * (size_t)n);
+  std::vector<uint32_t> mt((size_t)n);
   std::vector<gbgpu_single_score> hs((size_t)n * scap);
   std::vector<gbgpu_pair_score> hp((size_t)n * pcap);
-  HIPCHECK(hipMemcpyAsync(info.data(), q.si.as<uint8_t>(o_info), sizeof(SurvOut) * (size_t)n, hipMemcpyDeviceToHost, st));
-  HIPCHECK(hipMemcpyAsync(cnt.data(), q.si.as<uint8_t>(o_cnt), 8 * (size_t)n, hipMemcpyDeviceToHost, st));
-  HIPCHECK(hipMemcpyAsync(hs.data(), q.si.as<uint8_t>(o_ss), sizeof(gbgpu_single_score) * hs.size(),
-                          hipMemcpyDeviceToHost, st));
-  HIPCHECK(hipMemcpyAsync(hp.data(), q.si.as<uint8_t>(o_ps), sizeof(gbgpu_pair_score) * hp.size(),
-                          hipMemcpyDeviceToHost, st));
-  HIPCHECK(hipStreamSynchronize(st));
+  auto fetch = [&]() -> int {
+    HIPCHECK(hipMemcpyAsync(info.data(), q.si.as<uint8_t>(o_info), sizeof(SurvOut) * (size_t)n, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipMemcpyAsync(cnt.data(), q.si.as<uint8_t>(o_cnt), 8 * (size_t)n, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipMemcpyAsync(hs.data(), q.si.as<uint8_t>(o_ss), sizeof(gbgpu_single_score) * hs.size(),
+                            hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipMemcpyAsync(hp.data(), q.si.as<uint8_t>(o_ps), sizeof(gbgpu_pair_score) * hp.size(),
+                            hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipStreamSynchronize(st));
+    return 0;
+  };
+  HIPCHECK(hipMemcpyAsync(mt.data(), q.si.as<uint8_t>(o_mt), 4 * (size_t)n, hipMemcpyDeviceToHost, st));
+  if (int rc = fetch()) return rc;
+  // docids whose last merged group comes out empty read the mbuf bytes
+  // earlier docids left (k_si_stale): their writers, the second pass's first
+  std::vector<SiStale> ents;
+  bool need_first = false;
+  for (int t = 0; t < n; t++) {
+    if (info[t].ok != -4) continue;
+    SiStale E;
+    E.t = (uint32_t)t;
+    E.O = mt[t];
+    E.nb = info[t].pad == 1 ? 12 : 6;
+    uint32_t need = 0;
+    for (int p = 0; p < 12; p++) E.w[p] = ~0u;
+    for (int t2 = t - 1; t2 >= 0 && need < E.nb; t2--) {
+      const uint32_t T = mt[t2];
+      if (T > E.O + need) {
+        const uint32_t upto = std::min<uint32_t>(E.nb, T - E.O);
+        for (uint32_t p = need; p < upto; p++) E.w[p] = (uint32_t)t2;
+        need = upto;
+      }
+    }
+    if (need < E.nb) need_first = true;
+    ents.push_back(E);
+  }
+  if (!ents.empty()) {
+    for (int t = 0; t < n; t++) {
+      if (info[t].ok == -1) return GBGPU_ECORRUPT;
+      if (info[t].ok == -2) return GBGPU_EUNSUPPORTED;
+      if (info[t].ok == -3) return GBGPU_ECAPACITY;
+    }
+    const Counters *hc = reinterpret_cast<const Counters *>(q.h_res);
+    const unsigned long long usum = hc->surv_top & ((1ull << 36) - 1);
+    const size_t ne = ents.size();
+    const unsigned long long mcap = need_first ? usum + 64ull * nsurv + 4096 : 0;
+    const unsigned long long fcap = (unsigned long long)ne * (usum + 4096) + 4096;
+    size_t o = 0;
+    auto take = [&](size_t bytes) {
+      const size_t at = o;
+      o += align256(bytes);
+      return at;
+    };
+    const size_t o_fixc = take(16), o_ent = take(sizeof(SiStale) * ne), o_lst = take(4 * (size_t)nsurv + 4),
+                 o_marena = take(8 * (size_t)mcap), o_farena = take(8 * (size_t)fcap);
+    if (q.si2.ensure(o) || q.svmb.ensure(4 * (size_t)nsurv + 4)) return ENOMEM;
+    Counters *dctr = q.res.as<Counters>();
+    if (need_first) {
+      // the first pass's residue: every survivor's mbuf bytes (its merges
+      // again), and its writers in vote-buffer (docid) order.  With site
+      // clustering the prefilter's skips decide which docids wrote: declined
+      if (q.replayed) return GBGPU_EUNSUPPORTED;
+      HIPCHECK(hipMemsetAsync(q.si2.as<uint8_t>(o_fixc), 0, 16, st));
+      hipLaunchKernelGGL(k_stale_mb, dim3((nsurv + SCORE_TPB - 1) / SCORE_TPB), dim3(SCORE_TPB), 0, st,
+                         q.tables.as<DevPlan>(), dctr, nsurv, (const uint32_t *)q.svslot.as<uint32_t>(),
+                         (const uint32_t *)q.svlm.as<uint32_t>(), (const uint32_t *)q.svu.as<uint32_t>(),
+                         (const Loc *)q.svloc.as<Loc>(), q.si2.as<uint64_t>(o_marena), mcap,
+                         q.si2.as<unsigned long long>(o_fixc), q.svmb.as<uint32_t>(), q.si2.as<uint32_t>(o_lst));
+      HIPCHECK(hipGetLastError());
+      std::vector<uint32_t> mb(nsurv), perm(nsurv);
+      uint32_t unsup = 0;
+      HIPCHECK(hipMemcpyAsync(mb.data(), q.svmb.p, 4 * (size_t)nsurv, hipMemcpyDeviceToHost, st));
+      HIPCHECK(hipMemcpyAsync(perm.data(), q.si.as<uint8_t>(o_sval), 4 * (size_t)nsurv, hipMemcpyDeviceToHost, st));
+      HIPCHECK(hipMemcpyAsync(&unsup, reinterpret_cast<uint8_t *>(dctr) + offsetof(Counters, unsup), 4,
+                              hipMemcpyDeviceToHost, st));
+      HIPCHECK(hipStreamSynchronize(st));
+      if (unsup) return GBGPU_EUNSUPPORTED;
+      for (auto &E : ents) {
+        uint32_t need = 0;
+        while (need < E.nb && E.w[need] != ~0u) need++;
+        for (int64_t k = (int64_t)nsurv - 1; k >= 0 && need < E.nb; k--) {
+          const uint32_t i = perm[(size_t)k];
+          const uint32_t T = mb[i];
+          if (T > E.O + need) {
+            const uint32_t upto = std::min<uint32_t>(E.nb, T - E.O);
+            for (uint32_t p = need; p < upto; p++) E.w[p] = 0x80000000u | i;
+            need = upto;
+          }
+        }
+        if (need < E.nb) return GBGPU_EUNSUPPORTED;  // bytes no docid of the call wrote: the stack's
+      }
+    }
+#ifdef GBGPU_DIAG
+    if (std::getenv("GBGPU_SI_DEBUG")) {
+      for (const auto &E : ents)
+        std::fprintf(stderr, "gbgpu si stale: t %u docid %llu O %u nb %u writers %x %x %x %x %x %x %x %x\n", E.t,
+                     (unsigned long long)docs[E.t], E.O, E.nb, E.w[0], E.w[1], E.w[5], E.w[6], E.w[7], E.w[8], E.w[10],
+                     E.w[11]);
+      for (int t = 0; t < n; t++)
+        std::fprintf(stderr, "gbgpu si mt: t %d docid %llu mt %u ok %d\n", t, (unsigned long long)docs[t], mt[t],
+                     info[t].ok);
+    }
+#endif
+    HIPCHECK(hipMemcpyAsync(q.si2.as<uint8_t>(o_ent), ents.data(), sizeof(SiStale) * ne, hipMemcpyHostToDevice, st));
+    HIPCHECK(hipMemsetAsync(q.si2.as<uint8_t>(o_fixc), 0, 16, st));
+    hipLaunchKernelGGL(k_si_stale, dim3((uint32_t)((ne + SCORE_TPB - 1) / SCORE_TPB)), dim3(SCORE_TPB), 0, st,
+                       q.tables.as<DevPlan>(), dctr, (const uint32_t *)q.svslot.as<uint32_t>(),
+                       (const uint32_t *)q.svlm.as<uint32_t>(), (const uint32_t *)q.svu.as<uint32_t>(),
+                       (const Loc *)q.svloc.as<Loc>(), q.si2.as<uint64_t>(o_farena), fcap,
+                       q.si2.as<unsigned long long>(o_fixc), (const uint64_t *)q.si.as<uint64_t>(o_tdoc),
+                       (const uint64_t *)q.si.as<uint64_t>(o_skey), (const uint32_t *)q.si.as<uint32_t>(o_sval),
+                       (const uint32_t *)q.si.as<uint32_t>(o_cum), nsurv, (const SiStale *)q.si2.as<SiStale>(o_ent),
+                       (uint32_t)ne, q.si.as<SurvOut>(o_info), q.si.as<int32_t>(o_cnt),
+                       q.si.as<gbgpu_single_score>(o_ss), scap, q.si.as<gbgpu_pair_score>(o_ps), pcap);
+    HIPCHECK(hipGetLastError());
+    if (int rc = fetch()) return rc;
+    for (const auto &E : ents)
+      if (info[E.t].ok == -3 || info[E.t].ok == -4) return GBGPU_EUNSUPPORTED;  // a replay that failed
+  }
   for (int t = 0; t < n; t++) {
     if (info[t].ok == -1) return GBGPU_ECORRUPT;      // a tree docid with no survivor entry
     if (info[t].ok == -2) {  // a getWordPosList path not replayed
@@ -7566,7 +7841,7 @@ static int stale_fix(QuerySlot &q, uint32_t nsurv, uint32_t nstale) {
     return at;
   };
   const size_t o_key = take(8 * (size_t)nsurv), o_val = take(4 * (size_t)nsurv), o_skey = take(8 * (size_t)nsurv),
-               o_ord = take(4 * (size_t)nsurv), o_rank = take(4 * (size_t)nsurv), o_wr = take(24 * (size_t)nstale),
+               o_ord = take(4 * (size_t)nsurv), o_rank = take(4 * (size_t)nsurv), o_wr = take(48 * (size_t)nstale),
                o_okey = take(4 * (size_t)nstale), o_sdoc = take(8 * (size_t)nstale), o_fixc = take(16),
                o_tmp = take(sort_tmp);
   // the fix arena: every survivor's merges once (k_stale_mb), then every

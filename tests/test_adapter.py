@@ -113,8 +113,8 @@ def test_gpu_adapter_score_info_in_reference_msg39(path):
     m_pairScoreBuf, m_singleScoreBuf) against the CPU body's, field by field
     (test_scoreinfo.same: m_termFreq* and padding excepted); over docid
     splits through gbgpuDocIdSplits.  The adapter declines exactly the
-    fixtures the library declines (EXPECTED_DECLINE: the stale-bytes case,
-    DESIGN.md 4), and answers every other."""
+    fixtures the library declines (test_scoreinfo.EXPECTED_DECLINE: none; the
+    stale-bytes fixtures are replayed), and answers every other."""
     from test_scoreinfo import EXPECTED_DECLINE, same
     cpu, exp, params = run(path, 0, info=True)
     gpu, _, _ = run(path, 2, info=True)

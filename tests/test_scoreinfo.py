@@ -22,15 +22,19 @@ SCASES = sorted(glob.glob(os.path.join(HERE, "golden", "s_*.npz")))
 IDS = [os.path.basename(p)[2:-4] for p in SCASES]
 SKIP = {"term_freq1", "term_freq2", "term_freq", "pair_scores", "single_scores"}
 DECLINED = set()
-# The fixtures whose second pass the GPU declines (GBGPU_EUNSUPPORTED): each
-# has a tree docid whose LAST merged group's mini-merged list comes out empty
-# after getWordPosList misses, so the reference's scorers read stale mbuf
-# bytes of an earlier docid (known divergences) -- and only those.
-# test_decline_set_is_the_stale_bytes_set derives the set from the
-# reference's own QueryTermInfo groups (gbref) and si_predict's restated
-# lookups; the GPU test requires exactly this set.
-EXPECTED_DECLINE = {"clus2_synonyms", "piped", "sortbyint_info1_synonyms", "sortbyint_info2_three_word",
-                    "splits2_c0_three_word", "three_word", "wiki_halfstop"}
+# The fixtures with a tree docid whose LAST merged group's mini-merged list
+# comes out empty in the second pass (getWordPosList misses), so the
+# reference's scorers read the mbuf bytes an earlier docid of the call left
+# there.  test_decline_set_is_the_stale_bytes_set derives the
+# set from the reference's own QueryTermInfo groups (gbref) and si_predict's
+# restated lookups.  The GPU replays those bytes (k_si_stale: the latest
+# earlier second-pass docid that wrote them, else the first pass's last) and
+# is compared with the reference's buffers on them like on every other.
+STALE_BYTES = {"clus2_synonyms", "piped", "sortbyint_info1_synonyms", "sortbyint_info2_three_word",
+               "splits2_c0_three_word", "three_word", "wiki_halfstop"}
+# the fixtures the GPU declines (GBGPU_EUNSUPPORTED: bytes no docid of the
+# call wrote, or a first-pass writer under site clustering): none
+EXPECTED_DECLINE = set()
 BF_HALF, BF_SYN, BF_NEG, BF_BIGRAM, BF_NUM, BF_FACET = 0x01, 0x04, 0x08, 0x10, 0x20, 0x40
 
 
@@ -189,10 +193,10 @@ def test_gpu_scoreinfo_vs_reference(engine, path):
         r = engine.query(terms, lists, params, cap=1 << 16)
     except gbgpu.GbgpuError as e:
         assert e.code == gbgpu.GBGPU_EUNSUPPORTED, label
-        assert label[2:-4] in EXPECTED_DECLINE, (label, "declined outside the stale-bytes set")
+        assert label[2:-4] in EXPECTED_DECLINE, (label, "declined outside the expected set")
         DECLINED.add(label[2:-4])
         return
-    assert label[2:-4] not in EXPECTED_DECLINE, (label, "answered a stale-bytes case")
+    assert label[2:-4] not in EXPECTED_DECLINE, (label, "answered an expected decline")
     check(dict(docids=r.docids, scores=r.scores, hits=r.hits, docs_wanted=r.docs_wanted, filtered=r.filtered),
           exp, label)
     d, p, s = ref_buffers(path)
@@ -204,14 +208,14 @@ def test_gpu_scoreinfo_vs_reference(engine, path):
 @pytest.mark.gpu
 def test_gpu_scoreinfo_declines_exactly(engine):
     """Runs after the parametrized cases: the GPU declined exactly the
-    stale-bytes fixtures."""
+    expected fixtures (none: the stale-bytes ones are replayed)."""
     if not SCASES:
         pytest.skip("no fixtures")
     assert DECLINED == EXPECTED_DECLINE, sorted(DECLINED ^ EXPECTED_DECLINE)
 
 
 def test_decline_set_is_the_stale_bytes_set():
-    """EXPECTED_DECLINE from the reference: without docid splits exactly the
+    """STALE_BYTES from the reference: without docid splits exactly the
     fixtures with a stale-bytes docid; a split fixture in the set has one in
     its whole-range view (each piece's second pass sees its own lists)."""
     import ref_binding as ref
@@ -225,9 +229,9 @@ def test_decline_set_is_the_stale_bytes_set():
             split_names.add(name)
         if st:
             (split if ns > 1 else plain).add(name)
-    exp_plain = EXPECTED_DECLINE - split_names
+    exp_plain = STALE_BYTES - split_names
     assert plain == exp_plain, sorted(plain ^ exp_plain)
-    assert EXPECTED_DECLINE - exp_plain <= split, sorted((EXPECTED_DECLINE - exp_plain) - split)
+    assert STALE_BYTES - exp_plain <= split, sorted((STALE_BYTES - exp_plain) - split)
 
 
 @pytest.mark.gpu
