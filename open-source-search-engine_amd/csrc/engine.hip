@@ -5802,12 +5802,12 @@ struct ListEntry {
 struct ListHdr {
   uint32_t bad;
   uint32_t pad;
-  unsigned long long dmax;
+  unsigned long long dmax;  // unused (the pages' last docids carry it)
 };
 static_assert(CHUNK_UNITS == 4 * WCH_UNITS, "four granules a page");
 __global__ void __launch_bounds__(BLOCK) k_list_scan(const uint8_t *__restrict__ list, uint32_t units,
                                                      uint32_t *__restrict__ pm, uint64_t *__restrict__ gf,
-                                                     ListHdr *hdr) {
+                                                     uint64_t *__restrict__ lastd, ListHdr *hdr) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[CHUNK_LOAD];
   __shared__ uint32_t tmp[BLOCK / 64];
   __shared__ uint32_t s_first[4], s_last;
@@ -5858,7 +5858,9 @@ __global__ void __launch_bounds__(BLOCK) k_list_scan(const uint8_t *__restrict__
     for (int g = 3; g >= (int)threadIdx.x; g--) f = s_first[g] != ~0u ? s_first[g] : f;
     gf[(size_t)blockIdx.x * 4 + threadIdx.x] = f == ~0u ? ~0ull : lds_unit_docid(lds, f);
   }
-  if (threadIdx.x == 0 && s_last) atomicMax(&hdr->dmax, (unsigned long long)lds_unit_docid(lds, s_last - 1));
+  // the page's last run docid (~0: no run start in the page); the host takes
+  // the list's last (one global atomic a page serialised the launch)
+  if (threadIdx.x == 0) lastd[blockIdx.x] = s_last ? lds_unit_docid(lds, s_last - 1) : ~0ull;
 }
 
 // one block: the page map's exclusive scan (total at pm[npages])
@@ -6167,18 +6169,26 @@ static int finish_list(gbgpu_ctx *ctx, ListEntry &e, const uint8_t *host_bytes, 
     const uint32_t np = (e.units + CHUNK_UNITS - 1) / CHUNK_UNITS;
     const uint32_t ngran = np * 4;
     gf.resize(ngran);
+    // stream-ordered from the context's pool (a hipMalloc / hipFree pair a
+    // cut synchronised the whole device, every query in flight included)
     DevBuf dgf;
-    if (dgf.ensure(align256(8 * (size_t)ngran) + sizeof(ListHdr))) return ENOMEM;
-    ListHdr *dh = reinterpret_cast<ListHdr *>(dgf.as<uint8_t>(align256(8 * (size_t)ngran)));
+    dgf.st = ctx->upload_stream;
+    dgf.pool = ctx->pool;
+    const size_t o_last = align256(8 * (size_t)ngran), o_hdr = o_last + align256(8 * (size_t)np);
+    if (dgf.ensure(o_hdr + sizeof(ListHdr))) return ENOMEM;
+    ListHdr *dh = reinterpret_cast<ListHdr *>(dgf.as<uint8_t>(o_hdr));
+    std::vector<uint64_t> lastd(np);
     hipError_t le = hipMemsetAsync(dh, 0, sizeof(ListHdr), ctx->upload_stream);
     if (le == hipSuccess) {
       hipLaunchKernelGGL(k_list_scan, dim3(np), dim3(BLOCK), 0, ctx->upload_stream, e.d, e.units, e.pm,
-                         dgf.as<uint64_t>(), dh);
+                         dgf.as<uint64_t>(), dgf.as<uint64_t>(o_last), dh);
       hipLaunchKernelGGL(k_list_tail, dim3(1), dim3(1024), 0, ctx->upload_stream, np, e.pm);
       le = hipGetLastError();
     }
     ListHdr hh;
     if (le == hipSuccess) le = hipMemcpyAsync(gf.data(), dgf.p, 8 * (size_t)ngran, hipMemcpyDeviceToHost, ctx->upload_stream);
+    if (le == hipSuccess)
+      le = hipMemcpyAsync(lastd.data(), dgf.as<uint8_t>(o_last), 8 * (size_t)np, hipMemcpyDeviceToHost, ctx->upload_stream);
     if (le == hipSuccess) le = hipMemcpyAsync(&hh, dh, sizeof hh, hipMemcpyDeviceToHost, ctx->upload_stream);
     const hipError_t se = hipStreamSynchronize(ctx->upload_stream);
     dgf.release();
@@ -6192,7 +6202,12 @@ static int finish_list(gbgpu_ctx *ctx, ListEntry &e, const uint8_t *host_bytes, 
       if (gf[g] == ~0ull) gf[g] = gf[g + 1];
     gf.resize((e.units + WCH_UNITS - 1) / WCH_UNITS);
     e.dmin = host_docid(first18);  // the first key (the list starts with a run)
-    e.dmax = hh.dmax;
+    e.dmax = 0;
+    for (size_t pg = np; pg-- > 0;)
+      if (lastd[pg] != ~0ull) {
+        e.dmax = lastd[pg];
+        break;
+      }
     (void)host_bytes;
   }
   if (size) e.gfirst = std::make_shared<const std::vector<uint64_t>>(std::move(gf));
