@@ -4240,7 +4240,7 @@ __global__ void __launch_bounds__(64 * BND_WAVES) k_bound(const DevPlan *__restr
           const float v = max_score_tail(pl, core, 1.0f, 0, 0);
           if (v != -1.0f) B = fminf(B, v);
         }
-        if (g == m) continue;
+        if (g == m || pl->has_facet) continue;  // a facet term skips filter 2 (Posdb.cpp:6353-6356)
         // filter 2 (Posdb.cpp:6364-6504): g's keys are written over the ring
         // whatever its bound, then scanned against m's survivors there
         int ngs = 0, dummy = -1;
@@ -4298,7 +4298,7 @@ __global__ void __launch_bounds__(64 * BND_WAVES) k_bound(const DevPlan *__restr
       for (int q = lane; q < RING / 16; q += 64) r4[q] = make_uint4(~0u, ~0u, ~0u, ~0u);
       wave_lds_sync();
       const int ourFirstPos = ring_fill(pl, ctr, m, s, lm, svl, ring, (uint8_t)m, lane);
-      for (int g = 0; g < ng; g++) {
+      for (int g = 0; g < ng && !pl->has_facet; g++) {
         if (g == m || (pl->gflags0[g] & (BF_NEGATIVE | BF_FACET))) continue;
         wave_lds_sync();
         ring_fill(pl, ctr, g, s, lm, svl, ring, (uint8_t)g, lane);
@@ -4387,6 +4387,10 @@ struct TreeParams {
   uint32_t init, final; // first / last piece
   int32_t ints;          // m_useIntScores: nodes ordered by m_intScore (TopTree.cpp:216-219, 270-274)
   int32_t on_reg_err;    // run only if k_tree_seq's register tree overflowed (tree_err == TREE_ERR_REG)
+  // facet terms with site clustering: every minWinningScore assignment as
+  // {docid lo, docid hi, score bits, 0} from [1], the count in [0].x (the
+  // facet votes of the docids the prefilter did not skip, k_facet_live)
+  uint4 *mwsl;
 };
 
 // Node scores: m_score, or with integer tree scores m_intScore kept as the
@@ -4578,6 +4582,7 @@ __global__ void __launch_bounds__(64) k_tree_replay(Counters *ctr, const uint4 *
   const uint32_t ns = (uint32_t)(ctr->surv_top >> 36);
   const bool ints = tp.ints != 0;
   float mws = -1.0f;  // minWinningScore, Posdb.cpp:6012
+  uint32_t nmws = 0;  // its assignments recorded (tp.mwsl)
   bool called = false;
   uint32_t filtered = 0, err = 0;
   uint32_t dbg_adds = 0, dbg_nmax = 0;  // diagnostic (GBGPU_TOPK_DEBUG)
@@ -4624,7 +4629,11 @@ __global__ void __launch_bounds__(64) k_tree_replay(Counters *ctr, const uint4 *
           bot_s = ts[n - 1];
           bot_d = td[n - 1];
         }
-        if (n > (uint32_t)tp.docs_wanted) mws = ts[n - 1];  // Posdb.cpp:7699-7704
+        if (n > (uint32_t)tp.docs_wanted) {
+          mws = ts[n - 1];  // Posdb.cpp:7699-7704
+          if (tp.mwsl && lane == 0)
+            tp.mwsl[1 + nmws++] = make_uint4((uint32_t)dd, (uint32_t)(dd >> 32), __float_as_uint(mws), 0u);
+        }
         if (j == 63) break;
         from = ~0ull << (j + 1);
       }
@@ -4676,6 +4685,7 @@ __global__ void __launch_bounds__(64) k_tree_replay(Counters *ctr, const uint4 *
   if (lane == 0) {
     ctr->filtered = filtered;
     if (err) ctr->tree_err = 1;
+    if (tp.mwsl) tp.mwsl[0] = make_uint4(nmws, 0u, 0u, 0u);
     ctr->pad[0] = dbg_adds;
     ctr->pad[1] = dbg_nmax;
     ctr->rdbg_t = (uint32_t)(dbg_t / 100);
@@ -4987,6 +4997,7 @@ __global__ void __launch_bounds__(64 * SQ_W) k_tree_seq(Counters *ctr, const uin
   T.tk = 0;
   T.td = 0;
   float mws = -1.0f;  // minWinningScore, Posdb.cpp:6012
+  uint32_t nmws = 0;  // its assignments recorded (tp.mwsl)
   bool called = false;
   uint32_t filtered = 0, err = 0, adds = 0, nmax = 0, ncand = 0;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -5027,7 +5038,14 @@ __global__ void __launch_bounds__(64 * SQ_W) k_tree_seq(Counters *ctr, const uin
       adds++;
       nmax = max(nmax, T.n);
       called = true;
-      if (T.n > (uint32_t)tp.docs_wanted) mws = key_score(T.tk);  // Posdb.cpp:7699-7704
+      if (T.n > (uint32_t)tp.docs_wanted) {
+        mws = key_score(T.tk);  // Posdb.cpp:7699-7704
+        if (tp.mwsl) {
+          const uint64_t dj = rl_u64(d, (uint32_t)j);
+          if (lane == 0) tp.mwsl[1 + nmws] = make_uint4((uint32_t)dj, (uint32_t)(dj >> 32), __float_as_uint(mws), 0u);
+          nmws++;
+        }
+      }
       if (pref && !(T.vcount >= tp.docs_wanted)) return rl_u32(li, (uint32_t)j) + 1;
       if (j == 63) return ~0u;
       from = ~0ull << (j + 1);
@@ -5098,6 +5116,7 @@ __global__ void __launch_bounds__(64 * SQ_W) k_tree_seq(Counters *ctr, const uin
   if (lane == 0) {
     ctr->filtered = filtered;
     if (err) ctr->tree_err = err;
+    if (tp.mwsl) tp.mwsl[0] = make_uint4(nmws, 0u, 0u, 0u);
     ctr->pad[0] = adds;  // diagnostic (GBGPU_TOPK_DEBUG)
     ctr->pad[1] = nmax;
     ctr->rdbg_t = ncand;
@@ -5933,6 +5952,8 @@ struct QuerySlot {
   DevBuf fac;                               // facet tables (facet_pass)
   DevBuf svmb, stale;                       // survivors' mbuf bytes; the stale-mbuf survivors (stale_fix)
   DevBuf si2;                               // the second pass's stale-byte replay (k_si_stale)
+  DevBuf mwsl;                              // facets with site clustering: minWinningScore's assignments
+  uint64_t rep_off = 0;                     // the replay entries in slot order: q.rep + rep_off (k_bound)
   std::vector<FacetTerm> facets;            // the query's facet terms with a table
   std::vector<uint64_t> h_white;            // its host copy (the upload's source)
   uint32_t epoch = 0;
@@ -5970,9 +5991,9 @@ struct QuerySlot {
   hipEvent_t ev_done = nullptr;  // the query's device work is done (the exchange waits on it)
   float last_ms[6] = {0, 0, 0, 0, 0, 0};
 
-  DevBuf *const bufs[32] = {&tables, &chunkcnt, &cand, &cunit, &bits, &loc, &svslot, &svlm, &svu, &svdoc,
+  DevBuf *const bufs[33] = {&tables, &chunkcnt, &cand, &cunit, &bits, &loc, &svslot, &svlm, &svu, &svdoc,
                             &svloc, &scratch, &skey, &sel, &gath, &res, &dir, &split, &swin, &blk,
-                            &sflag, &ord, &oslot, &rep, &tree, &white, &wrej, &si, &fac, &svmb, &stale, &si2};
+                            &sflag, &ord, &oslot, &rep, &tree, &white, &wrej, &si, &fac, &svmb, &stale, &si2, &mwsl};
   int init(hipMemPool_t pool) {
     if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return GBGPU_EHIP;
     for (auto *b : bufs) {
@@ -6540,8 +6561,7 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   for (int i = 0; i < nterms; i++) {
     const int32_t fc = terms[i].field_code;
     if (fc < FIELD_GBFACETSTR || fc > FIELD_GBFACETFLOAT || ents[i].size == 0) continue;
-    if (q.facets.size() >= (size_t)MAXF || clus || boolean || p->num_docid_splits > 1 ||
-        tree_phase != (TREE_INIT | TREE_FINAL))
+    if (q.facets.size() >= (size_t)MAXF || boolean || p->num_docid_splits > 1 || tree_phase != (TREE_INIT | TREE_FINAL))
       return GBGPU_EUNSUPPORTED;
     FacetTerm ft;
     ft.term = i;
@@ -6569,6 +6589,7 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
     }
     q.facets.push_back(std::move(ft));
   }
+  P.has_facet = q.facets.empty() ? 0 : 1;
   // candidate arrays: distinct lists of the smallest group, in sublist order;
   // for a boolean query every distinct list (the docid set is their union:
   // a docid's slot is in the first array holding it, its other arrays'
@@ -6746,6 +6767,7 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
     rc2 |= q.oslot.ensure(4 * slot_ub);
     rc2 |= q.rep.ensure((P.g0n > 1 ? 32 : 16) * slot_ub);
     if (!(tree_phase & TREE_FINAL)) rc2 |= q.tree.ensure(sizeof(TreeState));
+    if (!q.facets.empty()) rc2 |= q.mwsl.ensure(16 * (slot_ub + 2));
   }
   if (P.use_white) rc2 |= q.white.ensure(8 * std::max<size_t>(1, q.h_white.size()));
   if (P.use_rej) rc2 |= q.wrej.ensure(align256(slot_ub));  // k_cmp_* read it 32 slots at a time
@@ -6912,7 +6934,9 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
     // (columns for the nodes docsWanted and the domain caps normally keep);
     // a docid-split piece carries its tree in TreeState: the one-wave replay
     const int kcol = ctx->replay_mode == 3 ? 1 : seq_columns(q.docs_wanted);  // 3: diagnostic, 64 nodes (overflows)
-    const TreeParams tp = tree_params(q.docs_wanted, tree_phase, q.int_scores);
+    TreeParams tp = tree_params(q.docs_wanted, tree_phase, q.int_scores);
+    if (!q.facets.empty()) tp.mwsl = q.mwsl.as<uint4>();
+    q.rep_off = ranked ? slot_ub : 0;
     q.seq_replay = tree_phase == (TREE_INIT | TREE_FINAL) && kcol > 0 && ctx->replay_mode != 1;
     if (q.seq_replay) {
       auto ks = q.int_scores ? (kcol == 1 ? k_tree_seq<1, true> : kcol == 4 ? k_tree_seq<4, true>
@@ -7390,6 +7414,30 @@ __device__ __forceinline__ gu8 *run_key(gu8 *list, Loc lc, uint32_t k) {
 // the survivors' votes: one record (facet, entry key, docid, value) per
 // entry a docid's run touches first (FacetEntry::m_docId == docId skips the
 // rest, 7440-7445); and each facet list's shrunk size B
+// Site clustering: only the docids the prefilter did not skip reach the
+// facet votes (Posdb.cpp:6341-6345 jump back to docIdLoop).  A docid is skipped
+// when its bound B <= minWinningScore as the replay had it on reaching the
+// docid: the last assignment (tp.mwsl, docid order) of a lower docid.  fkey:
+// skey with the skipped docids' keys cleared.
+__global__ void k_facet_live(uint32_t nsurv, const uint64_t *sdoc, const uint32_t *sv_ord, const uint4 *rep_slot,
+                             const uint4 *mwsl, int ints, const uint32_t *skey, uint32_t *fkey) {
+  const uint32_t nm = mwsl[0].x;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nsurv; i += gridDim.x * blockDim.x) {
+    const uint64_t d = sdoc[i];
+    const float B = __uint_as_float(rep_slot[sv_ord[i]].y);
+    uint32_t lo = 0, hi = nm;  // assignments at docids < d: [1, 1 + lo)
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      const uint4 e = mwsl[1 + mid];
+      if ((((uint64_t)e.y << 32) | e.x) < d) lo = mid + 1;
+      else hi = mid;
+    }
+    const float mws = lo ? __uint_as_float(mwsl[lo].z) : -1.0f;
+    const bool live = ints || !(B <= mws);
+    fkey[i] = live ? skey[i] : 0u;
+  }
+}
+
 __global__ void __launch_bounds__(256) k_facet_emit(FacetPlan fp, const Counters *ctr, FacetCtr *fc, const uint32_t *skey,
                                                     const uint64_t *sv_doc, const Loc *sv_loc, uint32_t nl,
                                                     uint64_t *rdoc, uint64_t *rkey, int32_t *rval, uint32_t cap) {
@@ -7675,7 +7723,7 @@ static int facet_pass(QuerySlot &q, uint32_t nsurv, gbgpu_result *out) {
   const DevPlan *hpl = reinterpret_cast<const DevPlan *>(q.h_stage);
   const uint32_t nl = (uint32_t)std::max(hpl->nlists, 1);
   size_t o_ctr = 0, o_rng = 0, o_rdoc = 0, o_rkey = 0, o_rval = 0, o_k1 = 0, o_k1s = 0, o_i0 = 0, o_i1 = 0, o_k2 = 0,
-         o_k2s = 0, o_i2 = 0, o_seg = 0, o_ent = 0, o_tkey = 0, o_out = 0, o_t0 = 0, o_tmp = 0;
+         o_k2s = 0, o_i2 = 0, o_seg = 0, o_ent = 0, o_tkey = 0, o_out = 0, o_t0 = 0, o_tmp = 0, o_fkey = 0;
   const uint64_t ecap = cap + nranges + 1;  // table entries: distinct voted keys + ranges
   if (dev) {
     if (cap >= (1ull << 31)) return GBGPU_ECAPACITY;
@@ -7689,6 +7737,7 @@ static int facet_pass(QuerySlot &q, uint32_t nsurv, gbgpu_result *out) {
       return at;
     };
     o_ctr = take(sizeof(FacetCtr));
+    o_fkey = take(4 * (size_t)nsurv + 4);
     o_rng = take(8 * std::max<size_t>(nranges, 1));
     o_rdoc = take(8 * cap);
     o_rkey = take(8 * cap);
@@ -7727,8 +7776,17 @@ static int facet_pass(QuerySlot &q, uint32_t nsurv, gbgpu_result *out) {
     FacetCtr *dfc = q.fac.as<FacetCtr>(o_ctr);
     if (nsurv) {
       const uint32_t g = std::max(1u, std::min<uint32_t>(2048, (nsurv + 255) / 256));
+      // the votes' keys: the scores (0: not scored or dropped by the paging
+      // filter), with site clustering also 0 where the prefilter skipped
+      const uint32_t *vkey = q.skey.as<uint32_t>();
+      if (q.replayed) {
+        hipLaunchKernelGGL(k_facet_live, dim3(g), dim3(256), 0, st, nsurv, (const uint64_t *)q.svdoc.as<uint64_t>(),
+                           (const uint32_t *)q.ord.as<uint32_t>(), (const uint4 *)(q.rep.as<uint4>() + q.rep_off),
+                           (const uint4 *)q.mwsl.as<uint4>(), q.int_scores ? 1 : 0, vkey, q.fac.as<uint32_t>(o_fkey));
+        vkey = q.fac.as<uint32_t>(o_fkey);
+      }
       hipLaunchKernelGGL(k_facet_emit, dim3(g), dim3(256), 0, st, fp, (const Counters *)q.res.as<Counters>(), dfc,
-                         (const uint32_t *)q.skey.as<uint32_t>(), (const uint64_t *)q.svdoc.as<uint64_t>(),
+                         vkey, (const uint64_t *)q.svdoc.as<uint64_t>(),
                          (const Loc *)q.svloc.as<Loc>(), nl, q.fac.as<uint64_t>(o_rdoc), q.fac.as<uint64_t>(o_rkey),
                          q.fac.as<int32_t>(o_rval), (uint32_t)cap);
       HIPCHECK(hipGetLastError());

@@ -130,6 +130,7 @@ struct DevPlan {
   uint32_t reshare_mask;   // bit l: list l is shrunk more than once (uses >= 2)
   int clustering;
   int do_max_score;        // m_doMaxScoreAlgo
+  int has_facet;           // m_hasFacetTerm: the scoring filter is skipped (Posdb.cpp:6353-6356)
   int min_listi;           // m_minListi (group whose positions seed the ring buffer)
   int all_same_wiki;       // m_allInSameWikiPhrase (Posdb.cpp:5764-5778)
   // groups, in QueryTermInfo order

@@ -1208,7 +1208,7 @@ static float getMaxPossibleScore(const MaxCtx *c, QTI *qti, int32_t bestDist, in
 /* The two prefilters of the per-docid loop, Posdb.cpp:6322-6504: 1 if the
  * docid is skipped (its bound cannot beat minWinningScore). */
 static int prefilter_skip(const MaxCtx *c, QTI *qip, int nqti, int minListi, int doMaxScoreAlgo,
-                          float minWinningScore, unsigned char *ringBuf, int32_t *ourFirstPos) {
+                          float minWinningScore, unsigned char *ringBuf, int32_t *ourFirstPos, int hasFacet) {
   const int nnn = doMaxScoreAlgo ? nqti : 0;
   for (int i = 0; i < nnn; i++) {
     if (qip[i].bigramFlags[0] & (BF_NEGATIVE | BF_FACET)) continue;
@@ -1216,6 +1216,9 @@ static int prefilter_skip(const MaxCtx *c, QTI *qip, int nqti, int minListi, int
     if (maxScore == -1.0) continue;
     if (maxScore <= minWinningScore) return 1;
   }
+  /* a query with a facet term skips the scoring filter: facet stats are over
+     every result (Posdb.cpp:6353-6356) */
+  if (hasFacet) return 0;
   memset(ringBuf, 0xff, RINGBUFSIZE);
   QTI *qtx = &qip[minListi];
   for (int k = 0; k < qtx->numNewSubLists; k++) {
@@ -1777,7 +1780,7 @@ static int run_range(const orc_qterm *qt, const uint8_t *const *lists, const int
       /* gbsortby: both prefilters off (Posdb.cpp:6050-6051, 6350-6351) */
       if (sortByF < 0 && sortByI < 0 &&
           prefilter_skip(&mc, qip, nqti, P.minListi, prm->do_max_score_algo, minWinningScore, ringBuf,
-                         &ourFirstPos))
+                         &ourFirstPos, hasFacet))
         continue;
 
       /* mini merges, Posdb.cpp:6559-6778 */
@@ -2204,10 +2207,8 @@ int orc_query(const orc_qterm *qt, const uint8_t *const *lists, const int64_t *s
   for (int i = 0; i < nqt; i++) {
     const int fc = qt[i].field_code;
     if ((fc == F_SORTBYINT || fc == F_REVSORTBYINT) && qt[i].is_required) intMode = 1;
-    /* facets: restated without site clustering (the prefilter skip of
-       Posdb.cpp:6356 and the replay are not) and outside boolean queries */
-    if ((fc == F_FACETSTR || fc == F_FACETINT || fc == F_FACETFLOAT) && (prm->site_clustering || prm->is_boolean))
-      return ENOTSUP;
+    /* facets: restated outside boolean queries */
+    if ((fc == F_FACETSTR || fc == F_FACETINT || fc == F_FACETFLOAT) && prm->is_boolean) return ENOTSUP;
     /* a boolean query's gbsortby score reads a mini-merged list that may be
        the next group's or stale bytes (Posdb.cpp:7263-7279): not restated */
     if (prm->is_boolean && (fc == F_SORTBYFLOAT || fc == F_REVSORTBYFLOAT || fc == F_SORTBYINT ||

@@ -121,6 +121,12 @@ def save_facets():
         ("str", 2, 5, 63, True, 1, 0.6, None, {}),
         ("int_serp", 0, 6, 64, True, 2, 0.8, None, "serp"),
         ("int_docs10", 4, 7, 64, True, 4, 0.9, None, {"docs_to_get": 10}),
+        # with site clustering (the Msg39 default): the prefilters skip docids
+        # (no votes), and a facet term turns the scoring filter off
+        ("int_clus", 0, 8, 64, True, 3, 0.8, None, {"docs_to_get": 10, "site_clustering": 1}),
+        ("float_ranges_clus", 1, 9, 65, False, 2, 0.8, ([fl(0.0), fl(20.0), fl(55.5)], [fl(20.0), fl(55.5), fl(100.0)]),
+         {"docs_to_get": 10, "site_clustering": 1}),
+        ("str_clus", 3, 10, 63, True, 1, 0.6, None, {"docs_to_get": 20, "site_clustering": 1}),
     ]
     for name, kind, seed, fc, ints, kmax, frac, ranges, kw in cases:
         q = qkinds.kinds(N, seed=seed)[kind]
@@ -130,7 +136,7 @@ def save_facets():
         terms = list(q.terms)
         terms.append(gbgpu.QTerm(1, 0, fc, 0, -1, -1, -1, 0, max(t.qpos for t in terms) + 2, 0, -1, 1.0))
         lists = list(lists) + [number_list(lists, frac, seed=60 + seed, kmax=kmax, ints=ints)]
-        p = q.params()
+        p = q.params(site_clustering=1) if isinstance(kw, dict) and kw.get("site_clustering") else q.params()
         if kw == "serp":
             full = ref.query(terms, lists, p, cap=1 << 16)
             pos = len(full["docids"]) // 3

@@ -14,8 +14,9 @@ Parity: the reference's own fixtures (tests/golden/q_facet_*.npz: int, str
 and float facets, ranges of both, the paging filter, docsToGet 10) pin the
 oracle (test_golden.py runs them on CPU and GPU); here the GPU runs against
 the oracle on seeded corpora over several query kinds, facet shapes and
-range sets, through gbgpu_query, the resident path and enqueue/collect, and
-the modes the library does not restate fail loudly."""
+range sets, with and without site clustering, through gbgpu_query, the
+resident path and enqueue/collect, and the modes the library does not
+restate fail loudly."""
 import struct
 
 import numpy as np
@@ -125,6 +126,23 @@ def test_gpu_facets_vs_oracle(engine, kind, shape):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("shape", ["int", "float_ranges", "str"])
+@pytest.mark.parametrize("kind", [0, 1, 3])
+def test_gpu_facets_with_site_clustering(engine, kind, shape):
+    """Site clustering (the Msg39 default): the prefilters skip docids, which
+    then cast no facet vote, and a facet term turns the scoring filter off
+    (Posdb.cpp:6353-6356); small docsToGet so minWinningScore goes live early"""
+    q = qkinds.kinds(20000, seed=11)[kind]
+    lists = generate(q, 20000, seed=1100 + kind)
+    terms, fl_, fr = facet_query(q, lists, shape, seed=110 + kind)
+    for dtg in (10, 50):
+        p = params_of(q, fr, docs_to_get=dtg, site_clustering=1)
+        exp = orc.query(terms, fl_, p, cap=1 << 16)
+        r = engine.query(terms, fl_, p, cap=1 << 16)
+        same(r, exp, f"{q.name} {shape} clustered docs {dtg}")
+
+
+@pytest.mark.gpu
 def test_gpu_facets_paging_and_two_terms(engine):
     """the paging filter (only the docids that reach the tree vote) and two
     facet terms in one query, through the resident path and enqueue/collect"""
@@ -176,10 +194,9 @@ def test_gpu_facets_capacity_and_refusals(engine):
         assert ei.value.code == 28  # ENOSPC
     finally:
         gbgpu.Engine.facet_cap = old
-    for kw in (dict(site_clustering=1), dict(num_docid_splits=3)):
-        with pytest.raises(gbgpu.GbgpuError) as ei:
-            engine.query(terms, fl_, params_of(q, fr, **kw), cap=1 << 16)
-        assert ei.value.code == gbgpu.GBGPU_EUNSUPPORTED, kw
+    with pytest.raises(gbgpu.GbgpuError) as ei:
+        engine.query(terms, fl_, params_of(q, fr, num_docid_splits=3), cap=1 << 16)
+    assert ei.value.code == gbgpu.GBGPU_EUNSUPPORTED
     ng = sum(1 for t in terms if t.is_required)
     tb = bytes([0xff]) * max(1, (1 << ng) // 8)
     with pytest.raises(gbgpu.GbgpuError) as ei:
