@@ -52,6 +52,7 @@
 #include <memory>
 #include <mutex>
 #include <vector>
+#include <map>
 #include <array>
 
 #include "../../include/gbgpu.h"
@@ -5940,6 +5941,13 @@ struct FacetTerm {
 };
 
 
+// docid splits: each facet query term's table and docid count over the
+// pieces (Msg39 runs one Query, whose QueryTerms keep them), by query term
+struct FacetAcc {
+  std::map<int, std::map<int32_t, gbgpu_facet_entry>> tab;
+  std::map<int, uint64_t> docs;
+};
+
 struct QuerySlot {
   std::mutex mu;
   hipStream_t stream = nullptr;
@@ -5953,6 +5961,7 @@ struct QuerySlot {
   DevBuf svmb, stale;                       // survivors' mbuf bytes; the stale-mbuf survivors (stale_fix)
   DevBuf si2;                               // the second pass's stale-byte replay (k_si_stale)
   DevBuf mwsl;                              // facets with site clustering: minWinningScore's assignments
+  FacetAcc *facc = nullptr;                 // docid splits: the facet tables over the pieces (facet_pass)
   uint64_t rep_off = 0;                     // the replay entries in slot order: q.rep + rep_off (k_bound)
   std::vector<FacetTerm> facets;            // the query's facet terms with a table
   std::vector<uint64_t> h_white;            // its host copy (the upload's source)
@@ -6561,8 +6570,7 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   for (int i = 0; i < nterms; i++) {
     const int32_t fc = terms[i].field_code;
     if (fc < FIELD_GBFACETSTR || fc > FIELD_GBFACETFLOAT || ents[i].size == 0) continue;
-    if (q.facets.size() >= (size_t)MAXF || boolean || p->num_docid_splits > 1 || tree_phase != (TREE_INIT | TREE_FINAL))
-      return GBGPU_EUNSUPPORTED;
+    if (q.facets.size() >= (size_t)MAXF || boolean || (p->num_docid_splits > 1 && !q.facc)) return GBGPU_EUNSUPPORTED;
     FacetTerm ft;
     ft.term = i;
     ft.lid = -1;
@@ -6589,7 +6597,13 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
     }
     q.facets.push_back(std::move(ft));
   }
-  P.has_facet = q.facets.empty() ? 0 : 1;
+  // m_hasFacetTerm: a facet term with a list, or any over docid splits
+  // (Posdb.cpp:1013-1023)
+  P.has_facet = 0;
+  for (int i = 0; i < nterms; i++)
+    if (terms[i].field_code >= FIELD_GBFACETSTR && terms[i].field_code <= FIELD_GBFACETFLOAT &&
+        (ents[i].size > 0 || p->num_docid_splits > 1))
+      P.has_facet = 1;
   // candidate arrays: distinct lists of the smallest group, in sublist order;
   // for a boolean query every distinct list (the docid set is their union:
   // a docid's slot is in the first array holding it, its other arrays'
@@ -7368,6 +7382,11 @@ struct FacetPlan {
   uint32_t tbase[MAXF];  // the table's first counter in `outside`
   uint32_t units[MAXF];
   const uint8_t *list[MAXF];
+  // docid splits: the tables as the pieces before left them (the Query's
+  // QueryTerms keep them over the pieces), facet f's entries by key at
+  // prev[prev_off[f], prev_off[f + 1]); null: the first piece or no splits
+  const gbgpu_facet_entry *prev;
+  uint32_t prev_off[MAXF + 1];
 };
 
 struct FacetCtr {
@@ -7534,7 +7553,37 @@ __global__ void __launch_bounds__(256) k_facet_reduce(FacetPlan fp, const FacetC
     int32_t imin = INT32_MAX, imax = INT32_MIN;
     double fsum = 0.0;
     float fmin = 0.0f, fmax = 0.0f;
-    for (uint32_t j0 = st;; j0 += 64) {
+    uint32_t from = st;
+    if (fp.prev) {
+      // the entry as the earlier pieces left it: its votes go on from there,
+      // and the docid that voted last there (pieces overlap by two docids)
+      // is not counted again (Posdb.cpp:7509: fe->m_docId == m_docId)
+      const int32_t k32 = (int32_t)((uint32_t)key ^ 0x80000000u);
+      uint32_t lo = fp.prev_off[f], hi = fp.prev_off[f + 1];
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (fp.prev[mid].key < k32) lo = mid + 1;
+        else hi = mid;
+      }
+      if (lo < fp.prev_off[f + 1] && fp.prev[lo].key == k32) {
+        const gbgpu_facet_entry pv = fp.prev[lo];
+        cnt = (uint32_t)pv.count;
+        last = (uint64_t)pv.docid;
+        if (cnt) {
+          if (fl) {
+            fsum = __longlong_as_double(pv.sum);
+            fmin = __int_as_float(pv.min);
+            fmax = __int_as_float(pv.max);
+          } else {
+            isum = pv.sum;
+            imin = pv.min;
+            imax = pv.max;
+          }
+          if (rdoc[idx[st]] == last) from = st + 1;
+        }
+      }
+    }
+    for (uint32_t j0 = from;; j0 += 64) {
       const uint32_t j = j0 + lane;
       const bool in = j < n && k2s[j] == key;
       const uint64_t m = __ballot(in);  // a prefix of the lanes: the run is contiguous
@@ -7715,6 +7764,18 @@ static int facet_pass(QuerySlot &q, uint32_t nsurv, gbgpu_result *out) {
     if (t.lid >= 0) cap += t.units;
     nranges += t.a.size();
   }
+  // docid splits: the tables the pieces before left (the entries' votes go
+  // on from there, and this piece's records count in every entry they hold)
+  std::vector<gbgpu_facet_entry> prev;
+  if (q.facc) {
+    for (int f = 0; f < nf; f++) {
+      fp.prev_off[f] = (uint32_t)prev.size();
+      auto it = q.facc->tab.find(q.facets[f].term);
+      if (it != q.facc->tab.end())
+        for (const auto &kv : it->second) prev.push_back(kv.second);
+    }
+    fp.prev_off[nf] = (uint32_t)prev.size();
+  }
   const bool dev = cap > 0;
   // entries: the votes' and the ranges' (the ranges' A values stand as
   // entries from allocTopTree on, Posdb.cpp:5575-5631)
@@ -7723,8 +7784,8 @@ static int facet_pass(QuerySlot &q, uint32_t nsurv, gbgpu_result *out) {
   const DevPlan *hpl = reinterpret_cast<const DevPlan *>(q.h_stage);
   const uint32_t nl = (uint32_t)std::max(hpl->nlists, 1);
   size_t o_ctr = 0, o_rng = 0, o_rdoc = 0, o_rkey = 0, o_rval = 0, o_k1 = 0, o_k1s = 0, o_i0 = 0, o_i1 = 0, o_k2 = 0,
-         o_k2s = 0, o_i2 = 0, o_seg = 0, o_ent = 0, o_tkey = 0, o_out = 0, o_t0 = 0, o_tmp = 0, o_fkey = 0;
-  const uint64_t ecap = cap + nranges + 1;  // table entries: distinct voted keys + ranges
+         o_k2s = 0, o_i2 = 0, o_seg = 0, o_ent = 0, o_tkey = 0, o_out = 0, o_t0 = 0, o_tmp = 0, o_fkey = 0, o_prev = 0;
+  const uint64_t ecap = cap + nranges + prev.size() + 1;  // table entries: voted keys + ranges (+ earlier pieces')
   if (dev) {
     if (cap >= (1ull << 31)) return GBGPU_ECAPACITY;
     size_t tmp1 = 0, tmp2 = 0;
@@ -7738,6 +7799,7 @@ static int facet_pass(QuerySlot &q, uint32_t nsurv, gbgpu_result *out) {
     };
     o_ctr = take(sizeof(FacetCtr));
     o_fkey = take(4 * (size_t)nsurv + 4);
+    o_prev = take(sizeof(gbgpu_facet_entry) * std::max<size_t>(prev.size(), 1));
     o_rng = take(8 * std::max<size_t>(nranges, 1));
     o_rdoc = take(8 * cap);
     o_rkey = take(8 * cap);
@@ -7769,6 +7831,11 @@ static int facet_pass(QuerySlot &q, uint32_t nsurv, gbgpu_result *out) {
       fp.rb[f] = q.fac.as<int32_t>(o_rng) + r;
       rng.insert(rng.end(), t.b.begin(), t.b.end());
       r += t.b.size();
+    }
+    if (!prev.empty()) {
+      HIPCHECK(hipMemcpyAsync(q.fac.as<uint8_t>(o_prev), prev.data(), sizeof(gbgpu_facet_entry) * prev.size(),
+                              hipMemcpyHostToDevice, st));
+      fp.prev = q.fac.as<gbgpu_facet_entry>(o_prev);
     }
     HIPCHECK(hipMemsetAsync(q.fac.as<uint8_t>(o_ctr), 0, sizeof(FacetCtr), st));
     if (!rng.empty())
@@ -7843,6 +7910,24 @@ static int facet_pass(QuerySlot &q, uint32_t nsurv, gbgpu_result *out) {
       t.insert(it, z);
     }
     for (auto &e : t) e.term = q.facets[f].term;
+    if (q.facc) {
+      // this piece's entries over the earlier pieces' (a voted entry came
+      // back merged; a range entry nobody voted keeps what it had), then the
+      // whole table, by key, for this piece's record counts
+      auto &A = q.facc->tab[q.facets[f].term];
+      for (const auto &e : t) {
+        auto it = A.find(e.key);
+        if (it == A.end()) {
+          A[e.key] = e;
+        } else if (e.count) {
+          const int32_t o = it->second.outside;
+          it->second = e;
+          it->second.outside = o;
+        }
+      }
+      t.clear();
+      for (const auto &kv : A) t.push_back(kv.second);
+    }
     fp.tbase[f] = et;
     fp.tn[f] = (int)t.size();
     for (auto &e : t) tkeys.push_back(e.key);
@@ -7877,6 +7962,15 @@ static int facet_pass(QuerySlot &q, uint32_t nsurv, gbgpu_result *out) {
     HIPCHECK(hipMemcpyAsync(&hc, dfc, sizeof hc, hipMemcpyDeviceToHost, st));
     HIPCHECK(hipStreamSynchronize(st));
     for (int f = 0; f < nf; f++) docs[(size_t)f] = q.facets[f].lid >= 0 ? hc.docs[f] : 0;
+  }
+  if (q.facc) {  // a docid-split piece: the counts go on over the pieces
+    for (int f = 0; f < nf; f++) {
+      auto &A = q.facc->tab[q.facets[f].term];
+      const auto &t = tab[(size_t)f];
+      for (size_t k = 0; k < t.size(); k++) A[t[k].key].outside += (int32_t)outside[fp.tbase[f] + k];
+      q.facc->docs[q.facets[f].term] += docs[(size_t)f];
+    }
+    return 0;
   }
   int n = 0;
   std::vector<int> order((size_t)nf);
@@ -8103,7 +8197,7 @@ static int collect(gbgpu_ctx *ctx, QuerySlot &q, gbgpu_result *out, std::vector<
     n++;
   }
   out->n = n;
-  if (!q.facets.empty() && (out->facets || out->facet_docs)) {
+  if (!q.facets.empty() && (out->facets || out->facet_docs || q.facc)) {
     const int rc = facet_pass(q, (uint32_t)out->hits, out);
     if (rc) return rc;
   }
@@ -8233,6 +8327,17 @@ static int query_splits(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *terms, 
   gbgpu_params pq = *p;
   pq.get_docid_scoring_info = 0;
   SplitSink sink;
+  // facet terms: their tables and docid counts go on over the pieces
+  // (facet_pass with q.facc); written out after the last
+  FacetAcc facc;
+  struct FaccGuard {
+    QuerySlot &q;
+    ~FaccGuard() { q.facc = nullptr; }
+  } facc_guard{q};
+  bool any_facet = false;
+  for (int i = 0; i < nterms; i++)
+    if (terms[i].field_code >= FIELD_GBFACETSTR && terms[i].field_code <= FIELD_GBFACETFLOAT) any_facet = true;
+  if (any_facet && (out->facets || out->facet_docs)) q.facc = &facc;
   std::vector<uint64_t> sel;
   for (int j = 0; j < ns; j++) {
     size_t total = 0;
@@ -8346,6 +8451,43 @@ static int query_splits(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *terms, 
   out->hits = hits;
   out->filtered = filtered;
   out->docs_wanted = dw;
+  out->n_facets = 0;
+  if (q.facc) {
+    if (out->facet_docs)
+      for (int i = 0; i < nterms; i++) out->facet_docs[i] = 0;
+    // every facet term has its table (allocTopTree over docid splits makes
+    // one even for an empty list, its ranges as zeroed entries, Posdb.cpp:
+    // 1013-1067), by term, then key
+    for (int i = 0; i < nterms; i++) {
+      if (terms[i].field_code < FIELD_GBFACETSTR || terms[i].field_code > FIELD_GBFACETFLOAT) continue;
+      auto &A = facc.tab[i];
+      for (int r = 0; r < p->n_facet_ranges; r++) {
+        const gbgpu_facet_ranges &fr = p->facet_ranges[r];
+        if (fr.term != i) continue;
+        for (int k = 0; k < fr.n; k++)
+          if (!A.count(fr.a[k])) {
+            gbgpu_facet_entry z;
+            std::memset(&z, 0, sizeof z);
+            z.term = i;
+            z.key = fr.a[k];
+            A[fr.a[k]] = z;
+          }
+      }
+    }
+    int nfe = 0;
+    for (const auto &tv : facc.tab) {
+      for (const auto &kv : tv.second) {
+        if (out->facets && nfe < out->facets_cap) {
+          out->facets[nfe] = kv.second;
+          out->facets[nfe].term = tv.first;
+        }
+        nfe++;
+      }
+      if (out->facet_docs) out->facet_docs[tv.first] = facc.docs[tv.first];
+    }
+    out->n_facets = nfe;
+    if (out->facets && nfe > out->facets_cap) return ENOSPC;
+  }
   bool room = true;
   if (want_info) {
     out->n_docid_scores = (int32_t)sink.dinfo.size();

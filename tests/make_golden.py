@@ -127,6 +127,12 @@ def save_facets():
         ("float_ranges_clus", 1, 9, 65, False, 2, 0.8, ([fl(0.0), fl(20.0), fl(55.5)], [fl(20.0), fl(55.5), fl(100.0)]),
          {"docs_to_get": 10, "site_clustering": 1}),
         ("str_clus", 3, 10, 63, True, 1, 0.6, None, {"docs_to_get": 20, "site_clustering": 1}),
+        # over docid splits (the default /search request): the tables go on
+        # over the pieces, with and without site clustering
+        ("int_splits", 0, 11, 64, True, 3, 0.8, None, {"num_docid_splits": 3}),
+        ("float_ranges_splits_clus", 1, 12, 65, False, 2, 0.8,
+         ([fl(0.0), fl(20.0), fl(55.5)], [fl(20.0), fl(55.5), fl(100.0)]),
+         {"docs_to_get": 10, "site_clustering": 1, "num_docid_splits": 5}),
     ]
     for name, kind, seed, fc, ints, kmax, frac, ranges, kw in cases:
         q = qkinds.kinds(N, seed=seed)[kind]
@@ -136,7 +142,8 @@ def save_facets():
         terms = list(q.terms)
         terms.append(gbgpu.QTerm(1, 0, fc, 0, -1, -1, -1, 0, max(t.qpos for t in terms) + 2, 0, -1, 1.0))
         lists = list(lists) + [number_list(lists, frac, seed=60 + seed, kmax=kmax, ints=ints)]
-        p = q.params(site_clustering=1) if isinstance(kw, dict) and kw.get("site_clustering") else q.params()
+        pkw = {k: kw[k] for k in ("site_clustering", "num_docid_splits") if isinstance(kw, dict) and k in kw}
+        p = q.params(**pkw)
         if kw == "serp":
             full = ref.query(terms, lists, p, cap=1 << 16)
             pos = len(full["docids"]) // 3

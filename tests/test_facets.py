@@ -143,6 +143,25 @@ def test_gpu_facets_with_site_clustering(engine, kind, shape):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("shape", ["int", "int_ranges", "float", "str"])
+@pytest.mark.parametrize("kind", [0, 1, 3])
+def test_gpu_facets_over_docid_splits(engine, kind, shape):
+    """Docid splits (the default /search request): each piece's votes go on
+    from the tables the pieces before left -- an entry's last voter is not
+    counted again where the pieces overlap, a float sum keeps accumulating in
+    docid order -- and each piece's records count in every entry the table
+    holds; with and without site clustering"""
+    q = qkinds.kinds(20000, seed=12)[kind]
+    lists = generate(q, 20000, seed=1200 + kind)
+    terms, fl_, fr = facet_query(q, lists, shape, seed=120 + kind)
+    for kw in (dict(num_docid_splits=3), dict(num_docid_splits=5, site_clustering=1, docs_to_get=10)):
+        p = params_of(q, fr, **kw)
+        exp = orc.query(terms, fl_, p, cap=1 << 16)
+        r = engine.query(terms, fl_, p, cap=1 << 16)
+        same(r, exp, f"{q.name} {shape} {kw}")
+
+
+@pytest.mark.gpu
 def test_gpu_facets_paging_and_two_terms(engine):
     """the paging filter (only the docids that reach the tree vote) and two
     facet terms in one query, through the resident path and enqueue/collect"""
@@ -194,9 +213,6 @@ def test_gpu_facets_capacity_and_refusals(engine):
         assert ei.value.code == 28  # ENOSPC
     finally:
         gbgpu.Engine.facet_cap = old
-    with pytest.raises(gbgpu.GbgpuError) as ei:
-        engine.query(terms, fl_, params_of(q, fr, num_docid_splits=3), cap=1 << 16)
-    assert ei.value.code == gbgpu.GBGPU_EUNSUPPORTED
     ng = sum(1 for t in terms if t.is_required)
     tb = bytes([0xff]) * max(1, (1 << ng) // 8)
     with pytest.raises(gbgpu.GbgpuError) as ei:
