@@ -6570,7 +6570,7 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   for (int i = 0; i < nterms; i++) {
     const int32_t fc = terms[i].field_code;
     if (fc < FIELD_GBFACETSTR || fc > FIELD_GBFACETFLOAT || ents[i].size == 0) continue;
-    if (q.facets.size() >= (size_t)MAXF || boolean || (p->num_docid_splits > 1 && !q.facc)) return GBGPU_EUNSUPPORTED;
+    if (q.facets.size() >= (size_t)MAXF || boolean) return GBGPU_EUNSUPPORTED;
     FacetTerm ft;
     ft.term = i;
     ft.lid = -1;
