@@ -100,11 +100,6 @@ def test_gpu_adapter_in_reference_msg39(path):
     check(cpu, exp, label)  # the CPU body of this binary is the fixture's reference
     if cpu["docs_wanted"] == 0:
         assert gpu["answered"] == 0, label  # every list empty: Msg39 runs no pass (Msg39.cpp:945-948)
-    elif "facet" in label and splits(params):
-        # gbgpuDocIdSplits passes no facet buffers: the
-        # library answers facets over splits (test_facets.py), the adapter
-        # leaves them to the per-piece loop
-        assert gpu["answered"] == 0, (label, "expected the split adapter to decline facets")
     else:
         assert gpu["answered"] == 1, (label, "the adapter declined a supported query")
     same_tree(cpu, gpu, label, msg39=splits(params) and gpu["answered"] == 1)
