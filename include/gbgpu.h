@@ -11,7 +11,9 @@
  *   PosdbTable::intersectLists10_r Posdb.cpp:5437-7806 gbgpu_query / _resident
  *   TopTree::addNode / getHighNode TopTree.cpp:195-516 gbgpu_result (high -> low)
  *   Msg3a::mergeLists           Msg3a.cpp:971-1503     gbgpu_allgather_topk (RCCL) /
- *                                                      gbgpu_merge_topk (host lists)
+ *                                                      gbgpu_merge_topk (host lists);
+ *     (site cap, facet merge)                          gbgpu_allgather_replies (RCCL) /
+ *                                                      gbgpu_merge_replies(_device)
  *   RdbList::posdbMerge_r       RdbList.cpp:3065-3568  gbgpu_merge_posdb
  *   Msg3::readList -> RdbScan   Msg3.cpp:553-731,       gbgpu_file_upload /
  *     (a Posdb file read)       RdbScan.cpp:319-361    gbgpu_file_list (in HBM)
@@ -40,7 +42,7 @@
 extern "C" {
 #endif
 
-#define GBGPU_ABI_VERSION 12
+#define GBGPU_ABI_VERSION 13
 
 /* error codes beyond errno.h (Errno.h numbering is not reused) */
 #define GBGPU_ENODEVICE   1001 /* no HIP device / extension not usable        */
@@ -375,9 +377,9 @@ int gbgpu_merge_topk(const int64_t *const *shard_docids, const double *const *sh
  * given from the host (one per shard: counts[r] entries as Msg39 sends them,
  * double scores, and the shard's hit count); for checking the merge without
  * a multi-GPU node.  Same rules as gbgpu_merge_topk. */
-int gbgpu_merge_replies_device(gbgpu_ctx *ctx, int nranks, int32_t k, const int32_t *counts, const int64_t *shard_hits,
-                               const int64_t *const *shard_docids, const double *const *shard_scores,
-                               int64_t *docids, double *scores, int32_t *n, int64_t *hits);
+int gbgpu_merge_topk_device(gbgpu_ctx *ctx, int nranks, int32_t k, const int32_t *counts, const int64_t *shard_hits,
+                            const int64_t *const *shard_docids, const double *const *shard_scores,
+                            int64_t *docids, double *scores, int32_t *n, int64_t *hits);
 
 /* Exchange ordering.  Every rank must issue its collectives in the same
  * order, but a process runs several INTERSECT threads (Msg39.cpp:1019-1027,
@@ -420,6 +422,73 @@ int gbgpu_comm_unique_id(uint8_t *id);
 int gbgpu_comm_init(gbgpu_ctx *ctx, int nranks, int rank, const uint8_t *id);
 int gbgpu_allgather_topk(gbgpu_ctx *ctx, int slot, uint64_t seq, int timeout_ms, int32_t k, int64_t *docids,
                          double *scores, int32_t *n, int64_t *hits, gbgpu_result *local);
+/* Msg3a::mergeLists whole (Msg3a.cpp:971-1503) over full Msg39Replies: the
+ * shards' CR_OK nodes with their 12-byte clusterdb records, as Msg39 builds
+ * the reply after Msg51 and setClusterLevels (Msg39.cpp:1201-1344,
+ * 1346-1684), and their facet lists.  On top of gbgpu_merge_topk's rules:
+ * with site clustering a head whose record has n0 and n1 both non-zero is
+ * dropped when familyFilter is on and it is adult, or when its 26-bit site
+ * hash (non-zero) already has 2 results -- 1 with hideAllClustered -- and is
+ * counted against its site otherwise, before the docid test (1342-1385);
+ * each term's facet entries from every reply are merged into its table
+ * (1089-1240: count, outside count, int64 sums, double sums in reply order,
+ * min/max by the reference's count-zero rule; a list naming a termid the
+ * query lacks ends the walk, for that reply and every later one; m_docId: the first entry's -- the
+ * reference picks one at random, 1232-1233); and the hits and every term's
+ * m_numDocsThatHaveFacet are summed as gotAllShardReplies does (792-802).
+ * The caller keeps Msg3a::sortFacetEntries (923-962), which orders its
+ * hash table for display. */
+typedef struct gbgpu_reply {       /* one Msg39Reply (Msg39.h:169-208)          */
+  int32_t n;                       /* m_numDocIds                               */
+  int32_t hits;                    /* m_estimatedHits (an int32 on the wire)    */
+  const int64_t *docids;           /* ptr_docIds, n                             */
+  const double  *scores;           /* ptr_scores, n                             */
+  const uint8_t *cluster_recs;     /* ptr_clusterRecs, n x 12-byte key_t; NULL
+                                      when size_clusterRecs is 0                 */
+  const uint8_t *facet_list;       /* ptr_facetHashList: per facet term i64
+                                      termid, i32 n, n x (i32 key, FacetEntry)  */
+  int32_t facet_list_size;         /* size_facetHashList                        */
+  int32_t nqt;                     /* m_nqt (must equal the request's)           */
+  const int64_t *facet_docs;       /* ptr_numDocsThatHaveFacetList (nqt), or NULL */
+} gbgpu_reply;
+typedef struct gbgpu_merge_req {   /* what mergeLists reads of Msg3a / the request */
+  int32_t docs_to_get;             /* Msg3a::m_docsToGet (> 0, <= 4096 on the device) */
+  int32_t site_clustering;         /* m_r->m_doSiteClustering                   */
+  int32_t hide_all_clustered;      /* m_r->m_hideAllClustered                   */
+  int32_t family_filter;           /* m_r->m_familyFilter                        */
+  int32_t nqt;                     /* m_q->m_numTerms (<= 64)                    */
+  int32_t pad;
+  const int64_t *term_ids;         /* m_q->m_qterms[i].m_termId                  */
+  const int32_t *field_codes;      /* m_q->m_qterms[i].m_fieldCode               */
+} gbgpu_merge_req;
+typedef struct gbgpu_merged {      /* what mergeLists and gotAllShardReplies leave */
+  int64_t *docids;                 /* m_docIds, cap entries                      */
+  double  *scores;                 /* m_scores                                   */
+  uint8_t *cluster_recs;           /* m_clusterRecs (12 bytes each; with site
+                                      clustering), or NULL                       */
+  int32_t  cap;
+  int32_t  n;                      /* m_numDocIds                                */
+  int64_t  hits;                   /* m_numTotalEstimatedHits                    */
+  int64_t *facet_docs;             /* nqt: QueryTerm::m_numDocsThatHaveFacet, or NULL */
+  gbgpu_facet_entry *facets;       /* every term's m_facetHashTable, by term then
+                                      key; ENOSPC past facets_cap (n_facets set) */
+  int32_t  facets_cap;
+  int32_t  n_facets;
+} gbgpu_merged;
+/* on the host */
+int gbgpu_merge_replies(const gbgpu_merge_req *req, const gbgpu_reply *replies, int nshards, gbgpu_merged *out);
+/* the same merge on the device, over replies given from the host */
+int gbgpu_merge_replies_device(gbgpu_ctx *ctx, const gbgpu_merge_req *req, const gbgpu_reply *replies,
+                               int nshards, gbgpu_merged *out);
+/* The exchange of full replies over RCCL: every rank passes its own shard's
+ * reply (after Msg51 and the CR_OK filter), the replies are all-gathered
+ * over xGMI (a fixed-size head, then the bodies at the largest one's size)
+ * and merged on the device; every rank receives the same merged result.
+ * Sequenced like gbgpu_allgather_topk (one sequence for both); `mine` may
+ * be NULL (an empty reply: a shard whose query failed still takes part). */
+int gbgpu_allgather_replies(gbgpu_ctx *ctx, uint64_t seq, int timeout_ms, const gbgpu_merge_req *req,
+                            const gbgpu_reply *mine, gbgpu_merged *out);
+
 /* the exchange sequence number this context admits next (a single-threaded
  * caller's default `seq`); calls refused before admission (a bad k, a null
  * output, ETIMEDOUT) leave it unchanged */

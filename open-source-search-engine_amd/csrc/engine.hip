@@ -61,6 +61,7 @@
 #include "posdb_key.h"
 #include "scoring.h"
 #include "sisort.h"
+#include "exchange.h"
 
 namespace gbgpu {
 
@@ -9260,9 +9261,9 @@ uint64_t gbgpu_seq_next(const gbgpu_seq *s) {
 }
 void gbgpu_seq_close(gbgpu_seq *s) { delete s; }
 
-int gbgpu_merge_replies_device(gbgpu_ctx *ctx, int nranks, int32_t k, const int32_t *counts, const int64_t *shard_hits,
-                               const int64_t *const *shard_docids, const double *const *shard_scores,
-                               int64_t *docids, double *scores, int32_t *n, int64_t *hits) {
+int gbgpu_merge_topk_device(gbgpu_ctx *ctx, int nranks, int32_t k, const int32_t *counts, const int64_t *shard_hits,
+                            const int64_t *const *shard_docids, const double *const *shard_scores,
+                            int64_t *docids, double *scores, int32_t *n, int64_t *hits) {
   if (!ctx || nranks < 1 || nranks > 64 || k < 1 || (uint32_t)k > XMAX || !counts || !n || !hits) return EINVAL;
   (void)hipSetDevice(ctx->device);
   const size_t stride = align256(sizeof(XHead) + sizeof(XRec) * (size_t)k);
@@ -9339,6 +9340,133 @@ int gbgpu_merge_topk(const int64_t *const *sd, const double *const *ss, const in
   }
   *on = n;
   return 0;
+}
+
+// ---- Msg3a::mergeLists whole over full replies (exchange.hip)
+int gbgpu_merge_replies(const gbgpu_merge_req *req, const gbgpu_reply *replies, int nshards, gbgpu_merged *out) {
+  return gbx::merge_host(req, replies, nshards, out);
+}
+
+// the replies' packs, `stride` apart (the layout the all-gather leaves)
+static int pack_all(const gbgpu_merge_req *req, const gbgpu_reply *replies, int nshards, std::vector<uint8_t> &buf,
+                    size_t &stride, std::vector<int32_t> &fbytes) {
+  stride = 256;
+  for (int j = 0; j < nshards; j++) {
+    const gbgpu_reply &r = replies[j];
+    const size_t b = gbx::pack_bytes(&r);
+    if (!b || r.nqt != req->nqt || (req->site_clustering && r.n > 0 && !r.cluster_recs) ||
+        (r.n > 0 && (!r.docids || !r.scores)))
+      return EINVAL;
+    stride = std::max(stride, align256(b));
+  }
+  buf.assign(stride * nshards, 0);
+  fbytes.assign(nshards, 0);
+  for (int j = 0; j < nshards; j++) {
+    gbx::pack_reply(&replies[j], req->nqt, buf.data() + stride * j);
+    fbytes[j] = replies[j].facet_list ? replies[j].facet_list_size : 0;
+  }
+  return 0;
+}
+
+int gbgpu_merge_replies_device(gbgpu_ctx *ctx, const gbgpu_merge_req *req, const gbgpu_reply *replies, int nshards,
+                               gbgpu_merged *out) {
+  gbx::XFReq rq;
+  if (!ctx || !out || nshards < 1 || nshards > 64 || !replies) return EINVAL;
+  int rc = gbx::make_req(req, &rq);
+  if (rc) return rc;
+  if ((uint32_t)req->docs_to_get > gbx::XFMAX) return EINVAL;
+  std::vector<uint8_t> buf;
+  std::vector<int32_t> fb;
+  size_t stride = 0;
+  if ((rc = pack_all(req, replies, nshards, buf, stride, fb))) return rc;
+  std::lock_guard<std::mutex> xg(ctx->x_mu);
+  (void)hipSetDevice(ctx->device);
+  if (!ctx->xstream && hipStreamCreateWithFlags(&ctx->xstream, hipStreamNonBlocking) != hipSuccess) return GBGPU_EHIP;
+  hipStream_t xs = ctx->xstream;
+  uint8_t *d = nullptr;
+  if (hipMallocAsync(reinterpret_cast<void **>(&d), buf.size(), xs) != hipSuccess) return ENOMEM;
+  if (hipMemcpyAsync(d, buf.data(), buf.size(), hipMemcpyHostToDevice, xs) != hipSuccess) rc = GBGPU_EHIP;
+  if (!rc) rc = gbx::merge_device(xs, d, nshards, stride, rq, fb.data(), out);
+  (void)hipFreeAsync(d, xs);
+  if (hipStreamSynchronize(xs) != hipSuccess && !rc) rc = GBGPU_EHIP;
+  return rc;
+}
+
+// One exchange of full replies, admitted by the sequencer.  Three
+// collectives, so no rank is left waiting whatever fails: the heads (fixed
+// size), then every rank's verdict on the buffers the largest pack needs
+// (a min all-reduce), then the packs at that size.
+static int allgather_replies_admitted(gbgpu_ctx *ctx, const gbgpu_merge_req *req, const gbx::XFReq &rq,
+                                      const gbgpu_reply *mine, int err, gbgpu_merged *out) {
+  std::lock_guard<std::mutex> xg(ctx->x_mu);
+  if (!ctx->comm) return EINVAL;
+  (void)hipSetDevice(ctx->device);
+  hipStream_t xs = ctx->xstream;
+  const int nr = ctx->nranks;
+  const size_t mb = err ? sizeof(gbx::XFHead) : gbx::pack_bytes(mine);
+  std::vector<uint8_t> pk(std::max<size_t>(mb, sizeof(gbx::XFHead)), 0);
+  gbx::pack_reply(err ? nullptr : mine, rq.nqt, pk.data());
+  std::vector<uint8_t> heads(sizeof(gbx::XFHead) * nr);
+  int rc = 0;
+  int32_t ok = 1;
+  size_t stride = 256;
+  std::vector<int32_t> fb(nr, 0);
+  // 1: the heads (the send and receive buffers hold at least XMAX records
+  // since gbgpu_comm_init, so this never allocates)
+  if (hipMemcpyAsync(ctx->xsend.p, pk.data(), sizeof(gbx::XFHead), hipMemcpyHostToDevice, xs) != hipSuccess) rc = GBGPU_EHIP;
+  if (ncclAllGather(ctx->xsend.p, ctx->xrecv.p, sizeof(gbx::XFHead), ncclUint8, ctx->comm, xs) != ncclSuccess) rc = GBGPU_EHIP;
+  if (hipMemcpyAsync(heads.data(), ctx->xrecv.p, heads.size(), hipMemcpyDeviceToHost, xs) != hipSuccess ||
+      hipStreamSynchronize(xs) != hipSuccess)
+    rc = GBGPU_EHIP;
+  if (!rc) {
+    for (int r = 0; r < nr; r++) {
+      gbx::XFHead h;
+      std::memcpy(&h, heads.data() + sizeof h * r, sizeof h);
+      if (h.empty) continue;
+      gbgpu_reply x;
+      std::memset(&x, 0, sizeof x);
+      x.n = h.n;
+      x.nqt = h.nqt;
+      x.facet_list_size = h.facet_bytes;
+      stride = std::max(stride, align256(gbx::pack_bytes(&x)));
+      fb[r] = h.facet_bytes;
+    }
+  }
+  // 2: every rank can hold the packs
+  if (rc || ctx->xsend.ensure(stride) || ctx->xrecv.ensure(stride * nr)) ok = 0;
+  int32_t *dok = reinterpret_cast<int32_t *>(ctx->xout.p);
+  if (hipMemcpyAsync(dok, &ok, 4, hipMemcpyHostToDevice, xs) != hipSuccess) rc = rc ? rc : GBGPU_EHIP;
+  if (ncclAllReduce(dok, dok, 1, ncclInt32, ncclMin, ctx->comm, xs) != ncclSuccess) rc = rc ? rc : GBGPU_EHIP;
+  int32_t all_ok = 0;
+  if (hipMemcpyAsync(&all_ok, dok, 4, hipMemcpyDeviceToHost, xs) != hipSuccess || hipStreamSynchronize(xs) != hipSuccess)
+    rc = rc ? rc : GBGPU_EHIP;
+  if (rc) return rc;
+  if (!all_ok) return ENOMEM;
+  // 3: the packs
+  if (hipMemcpyAsync(ctx->xsend.p, pk.data(), pk.size(), hipMemcpyHostToDevice, xs) != hipSuccess) rc = GBGPU_EHIP;
+  if (ncclAllGather(ctx->xsend.p, ctx->xrecv.p, stride, ncclUint8, ctx->comm, xs) != ncclSuccess) rc = GBGPU_EHIP;
+  if (!rc) rc = gbx::merge_device(xs, ctx->xrecv.as<uint8_t>(), nr, stride, rq, fb.data(), out);
+  if (hipStreamSynchronize(xs) != hipSuccess && !rc) rc = GBGPU_EHIP;
+  if (err) return err;
+  (void)req;
+  return rc;
+}
+
+int gbgpu_allgather_replies(gbgpu_ctx *ctx, uint64_t seq, int timeout_ms, const gbgpu_merge_req *req,
+                            const gbgpu_reply *mine, gbgpu_merged *out) {
+  gbx::XFReq rq;
+  if (!ctx || !out || gbx::make_req(req, &rq) || (uint32_t)req->docs_to_get > gbx::XFMAX) return EINVAL;
+  // a reply this rank cannot pack still takes part, as an empty one
+  int err = 0;
+  if (mine && (!gbx::pack_bytes(mine) || mine->nqt != req->nqt ||
+               (req->site_clustering && mine->n > 0 && !mine->cluster_recs) ||
+               (mine->n > 0 && (!mine->docids || !mine->scores))))
+    err = EINVAL;
+  int rc = seq_enter(&ctx->xseq, seq, timeout_ms);
+  if (rc) return rc;
+  rc = allgather_replies_admitted(ctx, req, rq, mine, err, out);
+  seq_leave(&ctx->xseq, seq);
+  return rc;
 }
 
 static gbmerge::MergeState *merge_state(gbgpu_ctx *ctx) {

@@ -231,6 +231,84 @@ FACET_DT = np.dtype([("term", "<i4"), ("key", "<i4"), ("count", "<i4"), ("outsid
 FACET_FIELDS = (63, 64, 65)  # gbfacetstr: / gbfacetint: / gbfacetfloat:
 
 
+class Reply(ctypes.Structure):
+    """gbgpu_reply: one Msg39Reply (Msg39.h:169-208)"""
+    _fields_ = [("n", ctypes.c_int32), ("hits", ctypes.c_int32), ("docids", ctypes.c_void_p),
+                ("scores", ctypes.c_void_p), ("cluster_recs", ctypes.c_void_p), ("facet_list", ctypes.c_void_p),
+                ("facet_list_size", ctypes.c_int32), ("nqt", ctypes.c_int32), ("facet_docs", ctypes.c_void_p)]
+
+
+class MergeReq(ctypes.Structure):
+    _fields_ = [("docs_to_get", ctypes.c_int32), ("site_clustering", ctypes.c_int32),
+                ("hide_all_clustered", ctypes.c_int32), ("family_filter", ctypes.c_int32), ("nqt", ctypes.c_int32),
+                ("pad", ctypes.c_int32), ("term_ids", ctypes.c_void_p), ("field_codes", ctypes.c_void_p)]
+
+
+class Merged(ctypes.Structure):
+    _fields_ = [("docids", ctypes.c_void_p), ("scores", ctypes.c_void_p), ("cluster_recs", ctypes.c_void_p),
+                ("cap", ctypes.c_int32), ("n", ctypes.c_int32), ("hits", ctypes.c_int64),
+                ("facet_docs", ctypes.c_void_p), ("facets", ctypes.c_void_p), ("facets_cap", ctypes.c_int32),
+                ("n_facets", ctypes.c_int32)]
+
+
+# gbgpu_facet_entry (40 bytes)
+FACET_ENTRY = np.dtype([("term", "<i4"), ("key", "<i4"), ("count", "<i4"), ("outside", "<i4"), ("docid", "<i8"),
+                        ("sum", "<i8"), ("max", "<i4"), ("min", "<i4")])
+
+
+class FullReplies:
+    """ctypes views of a Msg3a request and its shards' full replies (dicts of
+    docids, scores, recs (bytes or None), hits, facets (bytes), fcounts
+    (int64[nqt] or None); tests/msg3a_cases.py) and the output buffers."""
+
+    def __init__(self, req, shards, cap=None, facets_cap=None):
+        self.keep = []
+        nqt = len(req["tids"])
+        self.tids = np.ascontiguousarray(req["tids"], np.int64)
+        self.fcs = np.ascontiguousarray(req["fcs"], np.int32)
+        self.req = MergeReq(req["docs_to_get"], req["clus"], req["hide"], req["family"], nqt, 0,
+                            self.tids.ctypes.data, self.fcs.ctypes.data)
+        self.reps = (Reply * max(1, len(shards)))()
+        for j, s in enumerate(shards):
+            d = np.ascontiguousarray(s["docids"], np.int64)
+            sc = np.ascontiguousarray(s["scores"], np.float64)
+            rec = ctypes.create_string_buffer(s["recs"], max(1, len(s["recs"]))) if s["recs"] is not None else None
+            fl = ctypes.create_string_buffer(s["facets"], max(1, len(s["facets"])))
+            fc = np.ascontiguousarray(s["fcounts"], np.int64) if s.get("fcounts") is not None else None
+            self.keep += [d, sc, rec, fl, fc]
+            self.reps[j] = Reply(len(d), s["hits"], d.ctypes.data, sc.ctypes.data,
+                                 ctypes.cast(rec, ctypes.c_void_p) if rec is not None else None,
+                                 ctypes.cast(fl, ctypes.c_void_p) if s["facets"] else None, len(s["facets"]), nqt,
+                                 fc.ctypes.data if fc is not None else None)
+        self.n = len(shards)
+        cap = cap if cap is not None else max(1, req["docs_to_get"])
+        fcap = facets_cap if facets_cap is not None else sum(len(s["facets"]) // 36 for s in shards) + 1
+        self.od = np.zeros(cap, np.int64)
+        self.os = np.zeros(cap, np.float64)
+        self.orec = np.zeros(12 * cap, np.uint8)
+        self.ofd = np.zeros(max(1, nqt), np.int64)
+        self.ofac = np.zeros(max(1, fcap), FACET_ENTRY)
+        self.out = Merged(self.od.ctypes.data, self.os.ctypes.data, self.orec.ctypes.data, cap, 0, 0,
+                          self.ofd.ctypes.data, self.ofac.ctypes.data, fcap, 0)
+        self.nqt = nqt
+        self.clus = req["clus"]
+
+    def result(self):
+        """-> dict(docids, scores, recs (bytes or None), hits, fdocs, facets (FACET_ENTRY[]))"""
+        n = self.out.n
+        return dict(docids=self.od[:n].copy(), scores=self.os[:n].copy(),
+                    recs=self.orec[:12 * n].tobytes() if self.clus else None, hits=self.out.hits,
+                    fdocs=self.ofd[:self.nqt].copy(), facets=self.ofac[:self.out.n_facets].copy(),
+                    n_facets=self.out.n_facets)
+
+
+def merge_replies(req, shards, **kw):
+    """gbgpu_merge_replies: Msg3a::mergeLists whole on the host"""
+    x = FullReplies(req, shards, **kw)
+    _check(load().gbgpu_merge_replies(ctypes.byref(x.req), x.reps, x.n, ctypes.byref(x.out)), "gbgpu_merge_replies")
+    return x.result()
+
+
 class SynthCorpus(ctypes.Structure):
     _fields_ = [
         ("num_docs", ctypes.c_int64),
@@ -267,8 +345,9 @@ EXPORTS = [
     "gbgpu_last_timings", "gbgpu_set_query_slots", "gbgpu_query_slots", "gbgpu_query_slot_enqueue",
     "gbgpu_query_slot_collect", "gbgpu_slot_stream", "gbgpu_slot_timings", "gbgpu_slot_stats",
     "gbgpu_bandwidth_ceiling", "gbgpu_comm_unique_id", "gbgpu_comm_init", "gbgpu_allgather_topk",
-    "gbgpu_merge_replies_device", "gbgpu_seq_open", "gbgpu_seq_enter", "gbgpu_seq_leave", "gbgpu_seq_next",
-    "gbgpu_seq_close", "gbgpu_exchange_next",
+    "gbgpu_merge_topk_device", "gbgpu_seq_open", "gbgpu_seq_enter", "gbgpu_seq_leave", "gbgpu_seq_next",
+    "gbgpu_seq_close", "gbgpu_exchange_next", "gbgpu_merge_replies", "gbgpu_merge_replies_device",
+    "gbgpu_allgather_replies",
     "gbgpu_merge_posdb_device", "gbgpu_merge_timings", "gbgpu_merge_path", "gbgpu_merge_last_key", "gbgpu_merge_input_left", "gbgpu_termlist_merge", "gb_synth_merge_runs",
     "gb_synth_lists", "gb_synth_free", "gb_synth_docid", "gb_posdb_compress", "gb_posdb_make_key",
 ]
@@ -354,11 +433,17 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.gbgpu_allgather_topk.argtypes = [vp, ctypes.c_int, ctypes.c_uint64, ctypes.c_int, i32, ctypes.POINTER(i64),
                                          ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i32), ctypes.POINTER(i64),
                                          ctypes.POINTER(Result)]
-    lib.gbgpu_merge_replies_device.argtypes = [vp, ctypes.c_int, i32, ctypes.POINTER(i32), ctypes.POINTER(i64),
+    lib.gbgpu_merge_topk_device.argtypes = [vp, ctypes.c_int, i32, ctypes.POINTER(i32), ctypes.POINTER(i64),
                                                ctypes.POINTER(ctypes.POINTER(i64)),
                                                ctypes.POINTER(ctypes.POINTER(ctypes.c_double)),
                                                ctypes.POINTER(i64), ctypes.POINTER(ctypes.c_double),
                                                ctypes.POINTER(i32), ctypes.POINTER(i64)]
+    lib.gbgpu_merge_replies.argtypes = [ctypes.POINTER(MergeReq), ctypes.POINTER(Reply), ctypes.c_int,
+                                        ctypes.POINTER(Merged)]
+    lib.gbgpu_merge_replies_device.argtypes = [vp, ctypes.POINTER(MergeReq), ctypes.POINTER(Reply), ctypes.c_int,
+                                               ctypes.POINTER(Merged)]
+    lib.gbgpu_allgather_replies.argtypes = [vp, ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(MergeReq),
+                                            ctypes.POINTER(Reply), ctypes.POINTER(Merged)]
     lib.gbgpu_bandwidth_ceiling.argtypes = [vp, i64, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                             ctypes.POINTER(ctypes.c_double)]
     lib.gb_synth_lists.argtypes = [ctypes.POINTER(SynthCorpus), ctypes.POINTER(SynthTerm), ctypes.c_int,
@@ -766,7 +851,7 @@ class Engine:
         _check(rc, "gbgpu_allgather_topk")
         return d[:n.value], sc[:n.value], h.value
 
-    def merge_replies_device(self, shards, k: int, shard_hits=None):
+    def merge_topk_device(self, shards, k: int, shard_hits=None):
         ns = len(shards)
         keep = []
         dptrs = (ctypes.POINTER(ctypes.c_int64) * ns)()
@@ -783,11 +868,30 @@ class Engine:
         od = np.zeros(k, np.int64)
         osc = np.zeros(k, np.float64)
         n, h = ctypes.c_int32(), ctypes.c_int64()
-        _check(self.lib.gbgpu_merge_replies_device(self.ctx, ns, k, cnts, hh, dptrs, sptrs,
+        _check(self.lib.gbgpu_merge_topk_device(self.ctx, ns, k, cnts, hh, dptrs, sptrs,
                                                    od.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
                                                    osc.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
-                                                   ctypes.byref(n), ctypes.byref(h)), "gbgpu_merge_replies_device")
+                                                   ctypes.byref(n), ctypes.byref(h)), "gbgpu_merge_topk_device")
         return od[:n.value], osc[:n.value], h.value
+
+    def merge_replies_device(self, req, shards, **kw):
+        """gbgpu_merge_replies_device: Msg3a::mergeLists whole on the device"""
+        x = FullReplies(req, shards, **kw)
+        _check(self.lib.gbgpu_merge_replies_device(self.ctx, ctypes.byref(x.req), x.reps, x.n, ctypes.byref(x.out)),
+               "gbgpu_merge_replies_device")
+        return x.result()
+
+    def allgather_replies(self, req, shard, seq: Optional[int] = None, timeout_ms: int = -1, **kw):
+        """gbgpu_allgather_replies: this rank's full reply (None: an empty
+        one) exchanged over RCCL and merged on the device"""
+        if seq is None:
+            seq = self._xseq
+        x = FullReplies(req, [shard] if shard is not None else [], **kw)
+        rc = self.lib.gbgpu_allgather_replies(self.ctx, seq, timeout_ms, ctypes.byref(x.req),
+                                              x.reps if shard is not None else None, ctypes.byref(x.out))
+        self._xseq = int(self.lib.gbgpu_exchange_next(self.ctx))
+        _check(rc, "gbgpu_allgather_replies")
+        return x.result()
 
     def stream(self) -> int:
         return self.lib.gbgpu_stream(self.ctx) or 0

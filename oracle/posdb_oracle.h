@@ -125,6 +125,36 @@ int64_t orc_posdb_merge(const uint8_t *const *lists, const int64_t *sizes, int n
 int32_t orc_msg3a_merge(const int64_t *const *docids, const double *const *scores, const int32_t *counts,
                         int nshards, int32_t docs_to_get, int64_t *out_docids, double *out_scores);
 
+/* Msg3a::mergeLists whole (Msg3a.cpp:971-1503) over full Msg39Replies
+ * (Msg39.h:169-208; the layout of gbgpu_reply): the <=2-per-site cap over
+ * cluster records (1342-1379), the facet-table merge (1089-1240) and the
+ * per-term facet doc counts and hits gotAllShardReplies sums (792-802).
+ * Merged facet entries go out by term, then key ascending, with the first
+ * merged entry's m_docId (the reference picks one at random, 1232-1233).
+ * Returns 0 or an errno-style code. */
+typedef struct orc_reply {
+  int32_t n, hits;
+  const int64_t *docids;
+  const double *scores;
+  const uint8_t *cluster_recs; /* n x 12 bytes, or NULL */
+  const uint8_t *facet_list;
+  int32_t facet_list_size, nqt;
+  const int64_t *facet_docs;   /* nqt, or NULL */
+} orc_reply;
+typedef struct orc_merge_req {
+  int32_t docs_to_get, site_clustering, hide_all_clustered, family_filter, nqt, pad;
+  const int64_t *term_ids;
+  const int32_t *field_codes;
+} orc_merge_req;
+typedef struct orc_facet_entry {
+  int32_t term, key, count, outside;
+  int64_t docid, sum;
+  int32_t max, min;
+} orc_facet_entry;
+int orc_msg3a_full(const orc_merge_req *rq, const orc_reply *rep, int nshards, int64_t *out_docids,
+                   double *out_scores, uint8_t *out_recs, int32_t *out_n, int64_t *out_hits, int64_t *out_fdocs,
+                   orc_facet_entry *facets, int32_t facets_cap, int32_t *n_facets);
+
 void orc_weights(float *density32, float *wordspam16, float *linker16, float *hashgroup11,
                  float *diversity16);
 

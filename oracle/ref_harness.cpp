@@ -628,6 +628,250 @@ static int ref_msg3a_merge(int nshards, int32_t docs_to_get, const int32_t *coun
   return 0;
 }
 
+// ---- a24 whole: Msg39's reply with cluster records and facet lists, and
+// Msg3a::mergeLists over such replies -- the ≤2-per-site cap
+// (Msg3a.cpp:1342-1379), the facet-table merge (1089-1240) and the facet
+// doc counts gotAllShardReplies sums (794-802).
+#include <algorithm>
+#include <stdlib.h>
+#include "Clusterdb.h"
+#include "Msg51.h"
+
+// one shard's Msg39Reply (Msg39.h:169-208): its fixed fields and the
+// variable parts serializeMsg lays out
+struct ShardReply {
+  std::vector<int64_t> docids;   // ptr_docIds
+  std::vector<double> scores;    // ptr_scores
+  std::vector<char> recs;        // ptr_clusterRecs: n x 12-byte key_t; empty = size_clusterRecs 0
+  int32_t hits;                  // m_estimatedHits (int32 on the wire)
+  std::vector<char> facets;      // ptr_facetHashList (Msg39.cpp:1457-1555 layout)
+  std::vector<int64_t> fcounts;  // ptr_numDocsThatHaveFacetList, one per query term
+};
+// what Msg3a leaves: m_docIds / m_scores / m_clusterRecs, the summed hits,
+// each QueryTerm's m_numDocsThatHaveFacet and m_facetHashTable
+struct MergedOut {
+  int32_t rc;
+  std::vector<int64_t> docids;
+  std::vector<double> scores;
+  std::vector<char> recs;
+  int64_t hits;
+  std::vector<int64_t> fdocs;
+  std::vector<std::vector<char> > tables;  // per query term: (i32 key, FacetEntry) by key
+};
+
+// a query term table read out in key order (its slot order is the hash's)
+static std::vector<char> table_by_key(HashTableX *ft) {
+  std::vector<std::pair<int32_t, int32_t> > slots;
+  for (int32_t k = 0; ft->m_numSlots && k < ft->m_numSlots; k++)
+    if (ft->m_flags[k]) slots.push_back(std::make_pair(ft->getKey32FromSlot(k), k));
+  std::sort(slots.begin(), slots.end());
+  std::vector<char> t(slots.size() * (4 + sizeof(FacetEntry)));
+  for (size_t i = 0; i < slots.size(); i++) {
+    memcpy(&t[i * 36], &slots[i].first, 4);
+    memcpy(&t[i * 36 + 4], ft->getValFromSlot(slots[i].second), sizeof(FacetEntry));
+  }
+  return t;
+}
+
+// INTEGRATION.md §4's Msg3a-side block (gbgpuFillMsg3a over the exchange's
+// merged result) -- linked only into gbref_gpu
+struct gbgpu_merge_req;
+struct gbgpu_reply;
+extern int gbref_adapter_exchange(Msg3a *m, const gbgpu_reply *mine) __attribute__((weak));
+
+static Msg3a *s_m3a = NULL;
+static Msg39Request s_m3req;
+static Query s_m3q;
+static QueryTerm s_m3qt[MAXT];
+
+// Msg3a set up as Msg3a::getDocIds leaves it for mergeLists: the query's
+// terms (m_termId, m_fieldCode: what the facet merge reads), the request's
+// clustering flags
+static void msg3a_setup(int32_t docs_to_get, bool clus, bool hide_all, bool family,
+                        const std::vector<int64_t> &tids, const std::vector<int32_t> &fcs) {
+  ref_init();
+  if (!s_m3a) {
+    s_m3a = new Msg3a();
+    for (int i = 0; i < MAXT; i++) new (&s_m3qt[i].m_facetHashTable) HashTableX();
+  }
+  s_m3req.reset();
+  s_m3req.m_doSiteClustering = clus;
+  s_m3req.m_hideAllClustered = hide_all;
+  s_m3req.m_familyFilter = family;
+  s_m3req.m_getDocIdScoringInfo = false;
+  // sortFacetEntries truncates each term's index to m_maxFacets (reset(): -1)
+  s_m3req.m_maxFacets = 1 << 20;
+  const int nqt = (int)tids.size();
+  for (int i = 0; i < nqt; i++) {
+    s_m3qt[i].m_termId = tids[i];
+    s_m3qt[i].m_fieldCode = (char)fcs[i];
+    s_m3qt[i].m_numDocsThatHaveFacet = 0;
+  }
+  s_m3q.m_qterms = s_m3qt;
+  s_m3q.m_numTerms = nqt;
+  s_m3a->m_q = &s_m3q;
+  s_m3a->m_r = &s_m3req;
+  s_m3a->m_debug = 0;
+  s_m3a->m_docsToGet = docs_to_get;
+}
+
+static void msg3a_read(MergedOut &o) {
+  Msg3a *m = s_m3a;
+  o.docids.assign(m->m_docIds, m->m_docIds + m->m_numDocIds);
+  o.scores.assign(m->m_scores, m->m_scores + m->m_numDocIds);
+  o.recs.clear();
+  if (m->m_r->m_doSiteClustering)
+    o.recs.assign((char *)m->m_clusterRecs, (char *)m->m_clusterRecs + 12 * (size_t)m->m_numDocIds);
+  o.fdocs.clear();
+  o.tables.clear();
+  for (int i = 0; i < m->m_q->m_numTerms; i++) {
+    o.fdocs.push_back(m->m_q->m_qterms[i].m_numDocsThatHaveFacet);
+    o.tables.push_back(table_by_key(&m->m_q->m_qterms[i].m_facetHashTable));
+  }
+}
+
+// mode 0: the reference's Msg3a::mergeLists over the replies; mode 1 (one
+// reply, gbref_gpu): INTEGRATION.md's exchange of it as a one-rank RCCL
+// collective and its fill of Msg3a
+static int ref_msg3a_full(int mode, std::vector<ShardReply> &sh, int32_t docs_to_get, bool clus, bool hide_all,
+                          bool family, const std::vector<int64_t> &tids, const std::vector<int32_t> &fcs,
+                          MergedOut &o) {
+  const int ns = (int)sh.size();
+  const int nqt = (int)tids.size();
+  if (ns < 0 || ns > MAX_SHARDS || docs_to_get <= 0 || nqt > MAXT || (mode == 1 && ns != 1)) return EINVAL;
+  msg3a_setup(docs_to_get, clus, hide_all, family, tids, fcs);
+  Msg3a *m = s_m3a;
+  static Msg39Reply rep[MAX_SHARDS];
+  m->m_numHosts = ns;
+  o.hits = 0;
+  for (int j = 0; j < ns; j++) {
+    ShardReply &s = sh[j];
+    Msg39Reply &r = rep[j];
+    memset((void *)&r, 0, sizeof r);
+    const int32_t n = (int32_t)s.docids.size();
+    r.m_numDocIds = n;
+    r.m_nqt = nqt;
+    r.m_estimatedHits = s.hits;
+    r.ptr_docIds = (char *)s.docids.data();
+    r.size_docIds = 8 * n;
+    r.ptr_scores = (char *)s.scores.data();
+    r.size_scores = 8 * n;
+    r.ptr_clusterRecs = s.recs.empty() ? NULL : (char *)s.recs.data();
+    r.size_clusterRecs = (int32_t)s.recs.size();
+    r.ptr_facetHashList = s.facets.empty() ? NULL : (char *)s.facets.data();
+    r.size_facetHashList = (int32_t)s.facets.size();
+    s.fcounts.resize(nqt, 0);
+    r.ptr_numDocsThatHaveFacetList = (char *)s.fcounts.data();
+    r.size_numDocsThatHaveFacetList = 8 * nqt;
+    m->m_reply[j] = &r;
+  }
+  if (mode == 0) {
+    // Msg3a::gotAllShardReplies (Msg3a.cpp:792-802): the hits and each
+    // term's facet doc count summed over the replies, then mergeLists
+    for (int j = 0; j < ns; j++) {
+      o.hits += rep[j].m_estimatedHits;
+      const int64_t *fc = (const int64_t *)rep[j].ptr_numDocsThatHaveFacetList;
+      for (int k = 0; k < rep[j].m_nqt && k < s_m3q.m_numTerms; k++) s_m3qt[k].m_numDocsThatHaveFacet += fc[k];
+    }
+    srand(1);  // the facet merge picks m_docId with rand() (Msg3a.cpp:1232-1233)
+    m->mergeLists();
+  } else {
+    if (!gbref_adapter_exchange) return ENOSYS;
+    int rc = gbref_adapter_exchange(m, (const gbgpu_reply *)&rep[0]);
+    if (rc) {
+      for (int j = 0; j < ns; j++) m->m_reply[j] = NULL;
+      return rc;
+    }
+    o.hits = m->m_numTotalEstimatedHits;
+  }
+  msg3a_read(o);
+  for (int j = 0; j < ns; j++) m->m_reply[j] = NULL;  // not Msg3a's to free
+  return 0;
+}
+
+// Msg51's clusterdb lookup (Msg51.cpp:380-416) over a synthetic clusterdb:
+// the record of docid d has site hash d mod nsites (0 included), docids with
+// d % 11 == 3 have none (CR_ERROR_CLUSTERDB, the record left 0), d % 13 == 5
+// is adult, and d % 17 == 7 has the record of another docid (the mismatch
+// keeps CR_ERROR_CLUSTERDB but the record is stored, Msg51.cpp:400-413)
+static void fake_clusterdb(int64_t d, int32_t nsites, key_t *rec, char *level) {
+  rec->n0 = 0;
+  rec->n1 = 0;
+  *level = CR_ERROR_CLUSTERDB;
+  if (d % 11 == 3) return;
+  const int64_t owner = d % 17 == 7 ? d ^ 0x40 : d;
+  const int32_t sh = (int32_t)((uint64_t)(d * 2654435761ULL >> 7) % (uint64_t)(nsites > 0 ? nsites : 1));
+  *rec = g_clusterdb.makeClusterRecKey(owner, d % 13 == 5, (uint8_t)(d % 5), sh, false);
+  if (g_clusterdb.getDocId(rec) != d) return;
+  *level = CR_OK;
+}
+
+// Msg39 after the intersection, as Msg39::setClusterRecs / gotClusterRecs
+// (Msg39.cpp:1201-1344: Msg51's records, then the reference's own
+// setClusterLevels with 2 docids per site) and estimateHitsAndSendReply
+// (1346-1684: CR_OK nodes only, at most docsToGet, double scores or
+// (double)m_intScore; the facet lists of every facet term; each term's
+// m_numDocsThatHaveFacet; m_estimatedHits = hits less filtered, 409-414)
+// build the reply, from the tree read high -> low
+static void ref_msg39_reply(const int64_t *docids, const float *scores, int n, const orc_params *p, bool family,
+                            int32_t nsites, int64_t hits, ShardReply &s) {
+  const bool clus = p->site_clustering != 0;
+  const bool ints = s_tab && s_tab->m_sortByTermNumInt >= 0;
+  std::vector<key_t> recs(n > 0 ? n : 1);
+  std::vector<char> levels(n > 0 ? n : 1, CR_OK);
+  int32_t visible = n;
+  if (clus && n > 0) {
+    std::vector<int64_t> d(docids, docids + n);
+    for (int i = 0; i < n; i++) fake_clusterdb(docids[i], nsites, &recs[i], &levels[i]);
+    setClusterLevels(&recs[0], &d[0], n, 2, true, family, 0, false, &levels[0]);
+    visible = 0;
+    for (int i = 0; i < n; i++) visible += levels[i] == CR_OK;
+  }
+  int32_t nd = visible < p->docs_to_get ? visible : p->docs_to_get;
+  s.docids.clear();
+  s.scores.clear();
+  s.recs.clear();
+  for (int i = 0; i < n && (int32_t)s.docids.size() < nd; i++) {
+    if (clus && levels[i] != CR_OK) continue;
+    s.docids.push_back(docids[i]);
+    s.scores.push_back(ints ? (double)s_ints[i] : (double)scores[i]);
+    if (clus) s.recs.insert(s.recs.end(), (char *)&recs[i], (char *)&recs[i] + 12);
+  }
+  s.hits = (int32_t)hits;
+  s.facets.clear();
+  s.fcounts.clear();
+  Query *q = s_tab ? s_tab->m_q : NULL;
+  const int nqt = q ? q->m_numTerms : 0;
+  for (int i = 0; i < nqt; i++) {
+    QueryTerm *qt = &q->m_qterms[i];
+    s.fcounts.push_back(qt->m_numDocsThatHaveFacet);
+    if (qt->m_fieldCode != FIELD_GBFACETSTR && qt->m_fieldCode != FIELD_GBFACETINT &&
+        qt->m_fieldCode != FIELD_GBFACETFLOAT)
+      continue;
+    HashTableX *ft = &qt->m_facetHashTable;
+    if (!ft->m_numSlots || ft->m_numSlotsUsed == 0) continue;
+    int32_t used = ft->getNumSlotsUsed();
+    if (used > 20000) used = 20000;  // MAX_FACETS, Msg39.cpp:1449, 1518-1519
+    const size_t at = s.facets.size();
+    s.facets.resize(at + 12 + (size_t)used * 36);
+    char *w = &s.facets[at];
+    memcpy(w, &qt->m_termId, 8);
+    memcpy(w + 8, &used, 4);
+    w += 12;
+    int32_t count = 0;
+    for (int32_t k = 0; k < ft->m_numSlots; k++) {
+      if (!ft->m_flags[k]) continue;
+      const int32_t key = ft->getKey32FromSlot(k);
+      memcpy(w, &key, 4);
+      memcpy(w + 4, ft->getValFromSlot(k), sizeof(FacetEntry));
+      w += 36;
+      if (++count >= 20000) break;
+    }
+  }
+}
+
+static void write_merged(const MergedOut &o);
+
 // ------------------------------------------------------------------ driver
 // Binary request on stdin, response on stdout (little-endian, host layout):
 //   op=1 query: i32 nterms, orc_params (its white_lists pointer ignored), nterms x orc_qterm,
@@ -659,6 +903,28 @@ static void rd(void *p, size_t n) {
 static void wr(const void *p, size_t n) {
   if (n && fwrite(p, 1, n, s_proto) != n) exit(3);
 }
+// op 8 / 9 response: i32 n (or -errno), n x i64 docid, n x f64 score,
+// i32 recs (0/1) then n x 12-byte cluster rec, i64 hits, i32 nqt, nqt x i64
+// m_numDocsThatHaveFacet, per term i32 entries then (i32 key, FacetEntry) by key
+static void write_merged(const MergedOut &o) {
+  int32_t n = o.rc ? -o.rc : (int32_t)o.docids.size();
+  wr(&n, 4);
+  if (o.rc) return;
+  wr(o.docids.data(), 8 * (size_t)n);
+  wr(o.scores.data(), 8 * (size_t)n);
+  const int32_t hr = o.recs.empty() ? 0 : 1;
+  wr(&hr, 4);
+  if (hr) wr(o.recs.data(), o.recs.size());
+  wr(&o.hits, 8);
+  const int32_t nqt = (int32_t)o.fdocs.size();
+  wr(&nqt, 4);
+  wr(o.fdocs.data(), 8 * (size_t)nqt);
+  for (int i = 0; i < nqt; i++) {
+    const int32_t ne = (int32_t)(o.tables[i].size() / 36);
+    wr(&ne, 4);
+    wr(o.tables[i].data(), o.tables[i].size());
+  }
+}
 static double now_s() {
   struct timespec ts;
   clock_gettime(CLOCK_MONOTONIC, &ts);
@@ -675,12 +941,19 @@ int main(int argc, char **argv) {
   }
   int32_t op;
   while (fread(&op, 4, 1, stdin) == 1) {
-    if (op == 1 || op == 4 || op == 7) {
+    if (op == 1 || op == 4 || op == 7 || op == 9) {
       // op 4: i32 mode first (0 the CPU body, 1 the GPU adapter), then op 1's
       // request; the response adds i32 passes the adapter answered, i32
-      // m_numUsedNodes and n x i32 m_intScore
-      int32_t mode = 0;
-      if (op == 4) rd(&mode, 4);
+      // m_numUsedNodes and n x i32 m_intScore.
+      // op 9: i32 mode, i32 familyFilter, i32 hideAllClustered, i32 nsites,
+      // then op 1's request: the query (mode 0 the CPU body, 1 the adapter),
+      // Msg39's reply from its tree over the synthetic clusterdb
+      // (fake_clusterdb), and that one reply merged (mode 0 the reference's
+      // Msg3a::mergeLists, 1 INTEGRATION.md's exchange): op 1's response,
+      // then write_merged's
+      int32_t mode = 0, o9[3] = {0, 0, 0};
+      if (op == 4 || op == 9) rd(&mode, 4);
+      if (op == 9) rd(o9, 12);
       s_adapter = mode;
       s_answered = 0;
       int32_t nt;
@@ -809,6 +1082,28 @@ int main(int argc, char **argv) {
         wr(gd.data(), 8 * (size_t)gn);
         wr(gs.data(), 8 * (size_t)gn);
       }
+      if (op == 9) {
+        MergedOut o;
+        o.rc = 0;
+        o.hits = 0;
+        std::vector<int64_t> tids(nt);
+        std::vector<int32_t> fcs(nt);
+        for (int i = 0; i < nt; i++) {
+          // distinct termids: Msg39's facet lists name their term by it and
+          // Msg3a finds it with getQueryTermByTermId64 (Msg3a.cpp:1156)
+          tids[i] = 1000003LL * (i + 1);
+          fcs[i] = t[i].field_code;
+          if (s_tab && i < s_tab->m_q->m_numTerms) s_tab->m_q->m_qterms[i].m_termId = tids[i];
+        }
+        std::vector<ShardReply> sh(1);
+        if (rc == 0) {
+          ref_msg39_reply(d.data(), s.data(), r.n, &p, o9[0] != 0, o9[2], r.hits - r.filtered, sh[0]);
+          o.rc = ref_msg3a_full(mode, sh, p.docs_to_get, p.site_clustering != 0, o9[1] != 0, o9[0] != 0, tids, fcs, o);
+        } else {
+          o.rc = rc;
+        }
+        write_merged(o);
+      }
       if (op == 4) {
         wr(&s_answered, 4);
         wr(&s_used_nodes, 4);
@@ -915,6 +1210,49 @@ int main(int argc, char **argv) {
         wr(od.data(), 8 * (size_t)n);
         wr(os.data(), 8 * (size_t)n);
       }
+    } else if (op == 8) {
+      // Msg3a over full replies: i32 nshards, i32 docs_to_get, i32
+      // doSiteClustering, i32 hideAllClustered, i32 familyFilter, i32 nqt,
+      // nqt x i64 m_termId, nqt x i32 m_fieldCode; per shard i32 n, i32 recs
+      // (0/1), n x i64 docid, n x f64 score, [n x 12-byte cluster rec], i32
+      // m_estimatedHits, i32 facet list bytes + bytes, i32 counts (0/1) +
+      // nqt x i64  ->  write_merged
+      int32_t h[6];
+      rd(h, sizeof h);
+      const int32_t ns = h[0], nqt = h[5];
+      if (ns < 0 || ns > MAX_SHARDS || nqt < 0 || nqt > MAXT) return 4;
+      std::vector<int64_t> tids(nqt);
+      std::vector<int32_t> fcs(nqt);
+      rd(tids.data(), 8 * (size_t)nqt);
+      rd(fcs.data(), 4 * (size_t)nqt);
+      std::vector<ShardReply> sh(ns);
+      for (int j = 0; j < ns; j++) {
+        int32_t n, hr, fb, hc;
+        rd(&n, 4);
+        rd(&hr, 4);
+        if (n < 0) return 4;
+        sh[j].docids.resize(n);
+        sh[j].scores.resize(n);
+        rd(sh[j].docids.data(), 8 * (size_t)n);
+        rd(sh[j].scores.data(), 8 * (size_t)n);
+        if (hr) {
+          sh[j].recs.resize(12 * (size_t)n);
+          rd(sh[j].recs.data(), 12 * (size_t)n);
+        }
+        rd(&sh[j].hits, 4);
+        rd(&fb, 4);
+        if (fb < 0) return 4;
+        sh[j].facets.resize(fb);
+        rd(sh[j].facets.data(), fb);
+        rd(&hc, 4);
+        if (hc) {
+          sh[j].fcounts.resize(nqt);
+          rd(sh[j].fcounts.data(), 8 * (size_t)nqt);
+        }
+      }
+      MergedOut o;
+      o.rc = ref_msg3a_full(0, sh, h[1], h[2] != 0, h[3] != 0, h[4] != 0, tids, fcs, o);
+      write_merged(o);
     } else {
       return 5;
     }

@@ -729,6 +729,20 @@ def save_msg3a():
         print(f"x_{name}: shards={len(shards)} k={k} merged={len(d)}")
 
 
+def save_msg3a_full():
+    """Msg3a::mergeLists whole: the reference's own mergeLists (op 8) over
+    the full-reply sets of msg3a_cases.full_cases -- cluster records and the
+    site cap, facet lists and the table merge, summed hits and facet counts
+    (x3_<name>.npz)"""
+    import msg3a_cases
+    for name, req, shards in msg3a_cases.full_cases():
+        exp = ref.msg3a_full(req, shards)
+        assert exp["rc"] == 0, (name, exp["rc"])
+        msg3a_cases.save_full(os.path.join(OUT, f"x3_{name}.npz"), name, req, shards, exp)
+        print(f"x3_{name}: shards={len(shards)} k={req['docs_to_get']} merged={len(exp['docids'])} "
+              f"facets={[len(t) for t in exp['tables']]}")
+
+
 def main():
     if not ref.available():
         sys.exit("oracle/_ref/gbref missing: run `make -f oracle/ref.mk` where /root/reference exists")
@@ -777,6 +791,7 @@ def main():
     save_stale()
     save_msg5()
     save_msg3a()
+    save_msg3a_full()
     cases = [(0, -1), (1, -1), (0, 5000), (1, 5000), (0, 1)]
     for seed, (keys, nterms) in enumerate([(4000, 50), (12000, 3), (8000, 1)]):
         save_merge(f"tiered_s{seed}", tiered_runs(keys, seed=seed, nterms=nterms), cases)
@@ -805,5 +820,7 @@ if __name__ == "__main__":
         save_range()
     elif sys.argv[1:] == ["msg3a"]:
         save_msg3a()
+    elif sys.argv[1:] == ["msg3a_full"]:
+        save_msg3a_full()
     else:
         main()

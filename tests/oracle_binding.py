@@ -137,3 +137,24 @@ def msg3a_merge(shards, docs_to_get):
     if n < 0:
         raise RuntimeError(f"orc_msg3a_merge rc={n}")
     return od[:n].copy(), os_[:n].copy()
+
+
+def msg3a_full(req, shards):
+    """oracle/msg3a_oracle.c orc_msg3a_full: Msg3a::mergeLists whole over full
+    replies (msg3a_cases.full_cases); the same dict as gbgpu.merge_replies."""
+    L = lib()
+    if not getattr(L, "_full", False):
+        vp = ctypes.c_void_p
+        L.orc_msg3a_full.argtypes = [ctypes.POINTER(gbgpu.MergeReq), ctypes.POINTER(gbgpu.Reply), ctypes.c_int,
+                                     vp, vp, vp, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int64),
+                                     vp, vp, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32)]
+        L._full = True
+    x = gbgpu.FullReplies(req, shards)
+    n, h, nf = ctypes.c_int32(), ctypes.c_int64(), ctypes.c_int32()
+    rc = L.orc_msg3a_full(ctypes.byref(x.req), x.reps, x.n, x.od.ctypes.data, x.os.ctypes.data, x.orec.ctypes.data,
+                          ctypes.byref(n), ctypes.byref(h), x.ofd.ctypes.data, x.ofac.ctypes.data, x.out.facets_cap,
+                          ctypes.byref(nf))
+    if rc:
+        raise RuntimeError(f"orc_msg3a_full rc={rc}")
+    x.out.n, x.out.hits, x.out.n_facets = n.value, h.value, nf.value
+    return x.result()

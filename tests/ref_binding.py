@@ -218,3 +218,48 @@ def msg3a_merge(shards, docs_to_get):
     d = np.frombuffer(_read(8 * n), np.int64).copy()
     s = np.frombuffer(_read(8 * n), np.float64).copy()
     return d, s
+
+
+def _read_merged(rd):
+    """write_merged's response -> dict(docids, scores, recs, hits, fdocs, tables)"""
+    from msg3a_cases import FE
+    (n,) = struct.unpack("<i", rd(4))
+    if n < 0:
+        return dict(rc=-n)
+    d = np.frombuffer(rd(8 * n), np.int64).copy()
+    s = np.frombuffer(rd(8 * n), np.float64).copy()
+    (hr,) = struct.unpack("<i", rd(4))
+    recs = rd(12 * n) if hr else None
+    (hits, nqt) = struct.unpack("<qi", rd(12))
+    fdocs = np.frombuffer(rd(8 * nqt), np.int64).copy()
+    tables = []
+    for _ in range(nqt):
+        (ne,) = struct.unpack("<i", rd(4))
+        tables.append(np.frombuffer(rd(36 * ne), FE).copy())
+    return dict(rc=0, docids=d, scores=s, recs=recs, hits=hits, fdocs=fdocs, tables=tables)
+
+
+def msg3a_full(req, shards, exe=None):
+    """op 8: the reference's own Msg3a::mergeLists over full Msg39Replies
+    (cluster records, facet lists, facet counts; msg3a_cases.full_cases),
+    with the hits and facet counts summed as gotAllShardReplies does."""
+    p = _p(exe)
+    nqt = len(req["tids"])
+    out = [struct.pack("<7i", 8, len(shards), req["docs_to_get"], req["clus"], req["hide"], req["family"], nqt),
+           np.asarray(req["tids"], np.int64).tobytes(), np.asarray(req["fcs"], np.int32).tobytes()]
+    for s in shards:
+        n = len(s["docids"])
+        out.append(struct.pack("<ii", n, 1 if s["recs"] is not None else 0))
+        out += [np.asarray(s["docids"], np.int64).tobytes(), np.asarray(s["scores"], np.float64).tobytes()]
+        if s["recs"] is not None:
+            assert len(s["recs"]) == 12 * n
+            out.append(s["recs"])
+        out.append(struct.pack("<ii", s["hits"], len(s["facets"])))
+        out.append(s["facets"])
+        fc = s.get("fcounts")
+        out.append(struct.pack("<i", 1 if fc is not None else 0))
+        if fc is not None:
+            out.append(np.asarray(fc, np.int64).tobytes())
+    p.stdin.write(b"".join(out))
+    p.stdin.flush()
+    return _read_merged(lambda n: _read(n, exe))

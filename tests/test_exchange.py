@@ -3,7 +3,7 @@
 gbgpu_allgather_topk all-gathers every shard's reply over RCCL and merges
 them on the device (k_xmerge) by Msg3a::mergeLists' rules (Msg3a.cpp:
 971-1503).  One GPU box cannot run several ranks, so the device merge is
-checked on its own (gbgpu_merge_replies_device) against the reference's own
+checked on its own (gbgpu_merge_topk_device) against the reference's own
 mergeLists (tests/golden/x_*.npz) and against the oracle restatement on
 seeded reply sets, and the whole collective runs as a one-rank communicator.
 The multi-rank ordering (gbgpu_seq) is covered on CPU (test_shards_gloo.py)."""
@@ -26,7 +26,7 @@ pytestmark = pytest.mark.gpu
 def test_device_merge_matches_reference_fixture(engine, path):
     shards, k, ed, es = load_fixture(path)
     hits = list(range(1, len(shards) + 1))
-    d, s, h = engine.merge_replies_device(shards, k, hits)
+    d, s, h = engine.merge_topk_device(shards, k, hits)
     assert h == sum(hits)
     assert same(d, s, ed, es)
 
@@ -40,7 +40,7 @@ def test_device_merge_matches_oracle(engine, nranks):
         if it == 3:  # replicas
             shards = (shards + shards)[:max(nranks, 2)]
         ed, es = orc.msg3a_merge(shards, k)
-        d, s, _ = engine.merge_replies_device(shards, k, [0] * len(shards))
+        d, s, _ = engine.merge_topk_device(shards, k, [0] * len(shards))
         assert same(d, s, ed, es), (nranks, k)
 
 
@@ -58,7 +58,7 @@ def test_device_merge_nan_scores_shard_order(engine, nranks):
         shards = [(d, np.where(rng.random(len(sc)) < 0.2, np.nan, sc)) for d, sc in shards]
         ed, es = orc.msg3a_merge(shards, k)
         hd, hs = gbgpu.merge_topk(shards, k)
-        d, s, _ = engine.merge_replies_device(shards, k, [0] * len(shards))
+        d, s, _ = engine.merge_topk_device(shards, k, [0] * len(shards))
         assert same(d, s, ed, es), (nranks, k)
         assert same(hd, hs, ed, es), (nranks, k)
 

@@ -87,7 +87,7 @@ def test_config4_shards_and_merge(engine):
         replies.append((res.docids[:n], res.scores[:n].astype(np.float64)))
         hits.append(res.hits)
         del lists
-    d, s, h = engine.merge_replies_device(replies, 100, hits)
+    d, s, h = engine.merge_topk_device(replies, 100, hits)
     ed, es = orc.msg3a_merge(replies, 100)
     assert np.array_equal(d, ed) and np.array_equal(s, es)
     full = generate(q, total, threads=16)
