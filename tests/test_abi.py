@@ -26,7 +26,7 @@ def test_exports_every_declared_symbol():
 
 def test_abi_version_and_errors():
     lib = gbgpu.load()
-    assert lib.gbgpu_abi_version() == 12
+    assert lib.gbgpu_abi_version() == 13
     assert b"unsupported" in lib.gbgpu_strerror(gbgpu.GBGPU_EUNSUPPORTED) or \
         b"not supported" in lib.gbgpu_strerror(gbgpu.GBGPU_EUNSUPPORTED)
 
