@@ -214,7 +214,7 @@ struct XFSec {
   uint32_t off;   // byte offset of the section's first entry in recv
   int32_t nh;     // entries
   int32_t term;   // query term
-  uint32_t base;  // global index of its first entry
+  uint32_t base;  // index of its first entry among its reply's entries
 };
 
 __global__ void __launch_bounds__(64) k_xf_sections(const uint8_t *recv, int nranks, size_t stride, XFReq rq,
@@ -281,13 +281,14 @@ __global__ void __launch_bounds__(64) k_xf_sections(const uint8_t *recv, int nra
     nsec[lane] = ns;
     rbase[lane] = x - cnt;
   }
+  // the shuffles run with every lane active: a lane read by ds_bpermute must
+  // be in the exec mask, or the read returns 0
   const uint64_t eb = __ballot(e != 0);
+  const uint32_t tot = __shfl(x, 63, 64);
+  const int e0 = __shfl(e, eb ? __builtin_ctzll(eb) : 0, 64);
   if (lane == 0) {
-    *total = __shfl(x, 63, 64);
-    *err = eb ? __shfl(e, __builtin_ctzll(eb), 64) : 0;
-  } else {
-    (void)__shfl(x, 63, 64);
-    if (eb) (void)__shfl(e, __builtin_ctzll(eb), 64);
+    *total = tot;
+    *err = eb ? e0 : 0;
   }
 }
 
@@ -305,9 +306,10 @@ __global__ void k_xf_keys(const uint8_t *recv, int nranks, const XFSec *sec, con
   int r = 0;
   while (r + 1 < nranks && rbase[r + 1] <= i) r++;
   const XFSec *s = sec + r * MAXSEC;
+  const uint32_t li = i - rbase[r];  // the entry's index inside its reply
   int k = 0;
-  while (k + 1 < nsec[r] && s[k + 1].base <= i) k++;
-  const uint32_t off = s[k].off + 36 * (i - s[k].base);
+  while (k + 1 < nsec[r] && s[k + 1].base <= li) k++;
+  const uint32_t off = s[k].off + 36 * (li - s[k].base);
   const uint32_t key = rd32(recv + off);
   keys[i] = ((uint64_t)(uint32_t)s[k].term << 32) | (key ^ 0x80000000u);  // signed key order
   vals[i] = off;
