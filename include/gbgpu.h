@@ -256,10 +256,14 @@ typedef struct gbgpu_result {
    * them (ENOSPC when that exceeds facets_cap; NULL: not written), and
    * facet_docs[term] = m_numDocsThatHaveFacet (countUniqueDocids' count,
    * Posdb.cpp:7786-7796) for each of the nterms terms (0 for a term with no
-   * table: not a facet term, an empty list, or a query that ended before
-   * allocTopTree).  Both NULL: no facet pass.  Facets run without site
-   * clustering, docid splits or a boolean expression, at most 4 facet terms,
-   * each a group of its own list alone (GBGPU_EUNSUPPORTED otherwise). */
+   * table: not a facet term, or a query that ended before allocTopTree; over
+   * docid splits a facet term with an empty list still has its table, as the
+   * Query's tables go on over the pieces).  Both NULL: no facet pass.  Facets
+   * run with site clustering and over docid splits; not inside a boolean
+   * expression, at most 4 facet terms, each a group of its own list alone
+   * (GBGPU_EUNSUPPORTED otherwise).  ENOSPC: only n_facets is valid (over docid
+   * splits the call returns before the tree and the score-info outputs are
+   * written): call again with facets_cap >= n_facets. */
   gbgpu_facet_entry *facets;
   int32_t facets_cap;
   int32_t n_facets;

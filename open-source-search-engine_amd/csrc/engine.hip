@@ -2654,7 +2654,7 @@ constexpr int SCORE_TPB = 64;
 #define GBGPU_SCORE_RC2 24
 #endif
 #ifndef GBGPU_SCORE_WAVES2
-#define GBGPU_SCORE_WAVES2 1
+#define GBGPU_SCORE_WAVES2 4
 #endif
 
 // a unit's 6 bytes as one u16 and one u32 load (units are 2-byte aligned;
@@ -2820,7 +2820,13 @@ __device__ __forceinline__ void score_survivor(const DevPlan *__restrict__ pl, c
           for (int x = 0; x < NS; x++) {
             const GrpRuns &g = pre[j];
             if (g.live[x] && b < g.ce[x] && g.c0[x] == g.ce[x] && !(diag & 0x400)) {
-              load4u(g.src[x], b, v[j][x]);  // a run of its own list only
+              gu8 *sp = g.src[x];
+              if (diag & 0x800) {  // diagnostic: every lane reads the first lane's run (no gather, and no divergence)
+                const uintptr_t a = (uintptr_t)sp;
+                sp = (gu8 *)(((uintptr_t)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)) << 32) |
+                             (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)a));
+              }
+              load4u(sp, b, v[j][x]);  // a run of its own list only
             } else {
 #pragma unroll
               for (int q = 0; q < SKP; q++) {
@@ -3119,19 +3125,12 @@ __device__ __forceinline__ void score_survivor(const DevPlan *__restrict__ pl, c
     *key_out = nrec + 1;
     return;
   }
-  // the scorers' top lists fill at most min(m_realMaxTop, records) slots
-  // (a pair's merge walk scores fewer steps than both lists' records; an
-  // empty list is read once): when every lane of the wave has at most
-  // SMALL_TOP records, the bookkeeping runs over SMALL_TOP register slots
-  constexpr int SMALL_TOP = 4;
+  // (the scorers bound their top-list slot loops by the wave's largest
+  // fillable count, wave_max15 in scoring.h)
   bool ok = false;
   if (!empty_pos) {
     const int sr = siteRank < 0 ? 0 : siteRank;
-    if (!REC::on && __ballot(nrec > (uint32_t)SMALL_TOP) == 0)
-      ok = score_doc<NQ, RP, REC, SMALL_TOP>(&c_weights, pl, dv, sr, docLang, smcol, SCORE_TPB, &score, diag & 0xff,
-                                             srec);
-    else
-      ok = score_doc<NQ, RP, REC>(&c_weights, pl, dv, sr, docLang, smcol, SCORE_TPB, &score, diag & 0xff, srec);
+    ok = score_doc<NQ, RP, REC>(&c_weights, pl, dv, sr, docLang, smcol, SCORE_TPB, &score, diag & 0xff, srec);
   }
   // gbsortby: the score is the float of the group's first key, bytes 2..5 as
   // the mini-merge left them (Posdb.cpp:7265-7269)
@@ -6765,6 +6764,17 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   rc2 |= q.cunit.ensure(4 * slot_ub);
   rc2 |= q.bits.ensure(4 * (size_t)nwords * (uint64_t)P.nlists);
   rc2 |= q.loc.ensure(sizeof(Loc) * slot_ub * (uint64_t)P.nlists);
+  // k_score variant: group / sublist capacity and LDS records per lane
+  int maxsub = 0;
+  for (int j = 0; j < hp.ngroups; j++)
+    if (!(P.gflags0[j] & BF_NEGATIVE)) maxsub = std::max(maxsub, (int)P.gnsub[j]);
+  const int variant = (boolean || (hp.ngroups <= 2 && maxsub <= 2)) ? 4  // boolean: no records scored
+                      : (hp.ngroups <= 2 && maxsub <= 4) ? 0
+                      : (hp.ngroups <= 4 && maxsub <= 4) ? 1
+                      : (hp.ngroups <= 8 && maxsub <= 4) ? 2
+                                                         : 3;
+  static constexpr uint32_t kRC[5] = {24, 48, 64, 64, GBGPU_SCORE_RC2};  // LDS records per lane
+  const uint32_t rcap = kRC[variant] / 2;  // size buckets: a column holds 2x a bucket-3 survivor's units
   rc2 |= q.svslot.ensure(4 * slot_ub);
   rc2 |= q.svlm.ensure(4 * slot_ub);
   rc2 |= q.svu.ensure(4 * slot_ub);
@@ -6880,17 +6890,6 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
     }
   }
   if (ctx->profiling) HIPCHECK(hipEventRecord(q.ev[2], st));
-  // k_score variant: group / sublist capacity and LDS records per lane
-  int maxsub = 0;
-  for (int j = 0; j < hp.ngroups; j++)
-    if (!(P.gflags0[j] & BF_NEGATIVE)) maxsub = std::max(maxsub, (int)P.gnsub[j]);
-  const int variant = (boolean || (hp.ngroups <= 2 && maxsub <= 2)) ? 4  // boolean: no records scored
-                      : (hp.ngroups <= 2 && maxsub <= 4) ? 0
-                      : (hp.ngroups <= 4 && maxsub <= 4) ? 1
-                      : (hp.ngroups <= 8 && maxsub <= 4) ? 2
-                                                         : 3;
-  static constexpr uint32_t kRC[5] = {24, 48, 64, 64, GBGPU_SCORE_RC2};  // LDS records per lane
-  const uint32_t rcap = kRC[variant] / 2;  // size buckets: a column holds 2x a bucket-3 survivor's units
   const uint64_t *dcand = q.cand.as<uint64_t>();
   const uint32_t *dcunit = q.cunit.as<uint32_t>();
   BlkInfo *blk = q.blk.as<BlkInfo>();

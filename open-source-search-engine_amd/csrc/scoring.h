@@ -88,6 +88,33 @@ __device__ __forceinline__ void rset(T (&a)[N], int i, T v) {
     if (q == i) a[q] = v;
 }
 
+// The largest v (0..15) among the wave's active lanes, as a wave-uniform
+// value (four ballots).  The scorers' top lists bound their unrolled slot
+// loops with it: a lane fills at most min(m_realMaxTop, steps) slots, so the
+// slots past the wave's largest such count are never touched and their
+// iterations are skipped with one scalar branch each.
+__device__ __forceinline__ int wave_max15(int v) {
+  int m = 0;
+#pragma unroll
+  for (int s = 8; s >= 1; s >>= 1)
+    if (__ballot(v >= m + s)) m += s;
+  return m;
+}
+
+// The top lists' modified hash groups, packed 4 bits a slot (hash groups are
+// 4-bit fields): the lowest slot below n whose nibble equals v is found with
+// the zero-nibble test on pm ^ v*0x11..1 -- a borrow can only flag nibbles
+// ABOVE a zero one, so the lowest flag is exact -- instead of a per-slot loop.
+constexpr uint64_t NIB1 = 0x1111111111111111ull, NIB8 = 0x8888888888888888ull;
+__device__ __forceinline__ uint64_t nib_match(uint64_t pm, uint32_t v, int n) {
+  const uint64_t x = pm ^ ((uint64_t)v * NIB1);
+  const uint64_t z = (x - NIB1) & ~x & NIB8;
+  return n >= 16 ? z : z & ((1ull << (4 * n)) - 1);
+}
+__device__ __forceinline__ uint64_t nib_set(uint64_t pm, int q, uint32_t v) {
+  return (pm & ~(0xfull << (4 * q))) | ((uint64_t)v << (4 * q));
+}
+
 // index of pair (i, j), i < j, in the upper triangle of an NQ x NQ matrix
 template <int NQ>
 __device__ __forceinline__ int pair_index(int i, int j) {
@@ -164,20 +191,19 @@ struct NoRec {
 // unrolled bookkeeping below costs T steps per record, not MAX_TOP.
 template <int NQ, class RP, class REC = NoRec, int T = MAX_TOP>
 __device__ __forceinline__ float single_term_score(const ScoreCtx<NQ> &c, const DocView<NQ, RP> &d, int i, int *bestPos,
-                                                  REC *rec = nullptr) {
+                                                  REC *rec = nullptr, int tw = T) {
   const Weights &W = s_weights;
   float nonBodyMax = -1.0;
   int minx = 0;
   float minv = 0.0f;  // bestScores[minx]
   float bestScores[T];
   int bestwpi[REC::on ? T : 1];
-  uint32_t bestmhg[T];
+  uint64_t bestmhg = 0;  // slot q's modified hash group: nibble q (slots < numTop)
   uint32_t besths = 0;  // bit q: slot q's key is a half-stop wiki bigram (r_hswb)
 #pragma unroll
   for (int q = 0; q < T; q++) {
     bestScores[q] = 0.0f;
     if constexpr (REC::on) bestwpi[q] = 0;
-    bestmhg[q] = 0xff;
   }
   int numTop = 0;
   int bp = -1;
@@ -217,11 +243,13 @@ __device__ __forceinline__ float single_term_score(const ScoreCtx<NQ> &c, const 
     int bro = -1;
     float broScore = 0.0f;
     if (hg != GB_HG_INLINKTEXT) {
+      const uint64_t z = nib_match(bestmhg, mhg, numTop);  // lowest matching slot
+      if (z) {
+        bro = (int)(__builtin_ctzll(z) >> 2);
 #pragma unroll
-      for (int q = T - 1; q >= 0; q--) {
-        if (q < numTop && bestmhg[q] == mhg) {  // lowest matching slot
-          bro = q;
-          broScore = bestScores[q];
+        for (int q = 0; q < T; q++) {
+          if (q >= tw) break;  // wave-uniform: no lane holds slot q
+          if (q == bro) broScore = bestScores[q];
         }
       }
     }
@@ -239,15 +267,18 @@ __device__ __forceinline__ float single_term_score(const ScoreCtx<NQ> &c, const 
       if (q == slot) {
         bestScores[q] = score;
         if constexpr (REC::on) bestwpi[q] = r;
-        bestmhg[q] = mhg;
       }
     }
-    if (slot >= 0) besths = (besths & ~(1u << slot)) | (r_hswb(k) << slot);
+    if (slot >= 0) {
+      besths = (besths & ~(1u << slot)) | (r_hswb(k) << slot);
+      bestmhg = nib_set(bestmhg, slot, mhg);
+    }
     if (numTop >= rmt) {
       minx = 0;
       minv = bestScores[0];
 #pragma unroll
       for (int q = 1; q < T; q++) {
+        if (q >= tw) break;  // rmt <= numTop <= tw here
         if (q < rmt && !(bestScores[q] > minv)) {
           minx = q;
           minv = bestScores[q];
@@ -263,6 +294,7 @@ __device__ __forceinline__ float single_term_score(const ScoreCtx<NQ> &c, const 
   float sum = 0.0;
 #pragma unroll
   for (int q = 0; q < T; q++) {
+    if (q >= tw) break;
     if (q < numTop) {
       if (besths >> q & 1)
         sum += (bestScores[q] * GB_WIKI_BIGRAM_WEIGHT * GB_WIKI_BIGRAM_WEIGHT);
@@ -492,7 +524,7 @@ __device__ __forceinline__ void eval_window(ScoreCtx<NQ> &c, const DocView<NQ, R
 // uninitialised local (Posdb.cpp:3730), recorded here as 2
 template <int NQ, class RP, class REC = NoRec, int T = MAX_TOP>
 __device__ __forceinline__ float pair_score_any(const ScoreCtx<NQ> &c, const DocView<NQ, RP> &d, int i, int j,
-                                               REC *rec = nullptr) {
+                                               REC *rec = nullptr, int tw = T) {
   const Weights &W = s_weights;
   const DevPlan *pl = c.pl;
   float wts;
@@ -522,7 +554,7 @@ __device__ __forceinline__ float pair_score_any(const ScoreCtx<NQ> &c, const Doc
   int minx = -1;
   float minv = 0.0f;  // bestScores[minx]
   float bestScores[T];
-  uint32_t bestmhg1[T], bestmhg2[T];
+  uint64_t bestmhg1 = 0, bestmhg2 = 0;  // nibble q: slot q's modified hash groups
   int bestwpi[REC::on ? T : 1], bestwpj[REC::on ? T : 1];
   uint8_t bestFixed[REC::on ? T : 1];
   bool fixedDistance = false;
@@ -530,8 +562,6 @@ __device__ __forceinline__ float pair_score_any(const ScoreCtx<NQ> &c, const Doc
 #pragma unroll
   for (int q = 0; q < T; q++) {
     bestScores[q] = 0.0f;
-    bestmhg1[q] = 0xff;
-    bestmhg2[q] = 0xff;
     if constexpr (REC::on) {
       bestwpi[q] = bestwpj[q] = 0;
       bestFixed[q] = 0;
@@ -618,12 +648,16 @@ __device__ __forceinline__ float pair_score_any(const ScoreCtx<NQ> &c, const Doc
     if (scored) {  // the topScores block, Posdb.cpp:3875-3922
       int bro = -1;
       float broScore = 0.0f;
+      // the lowest slot matching either modified hash group (not inlink text)
+      uint64_t z = 0;
+      if (hg1 != GB_HG_INLINKTEXT) z |= nib_match(bestmhg1, mhg1, numTop);
+      if (hg2 != GB_HG_INLINKTEXT) z |= nib_match(bestmhg2, mhg2, numTop);
+      if (z) {
+        bro = (int)(__builtin_ctzll(z) >> 2);
 #pragma unroll
-      for (int q = T - 1; q >= 0; q--) {
-        if (q < numTop && ((bestmhg1[q] == mhg1 && hg1 != GB_HG_INLINKTEXT) ||
-                           (bestmhg2[q] == mhg2 && hg2 != GB_HG_INLINKTEXT))) {
-          bro = q;  // lowest matching slot
-          broScore = bestScores[q];
+        for (int q = 0; q < T; q++) {
+          if (q >= tw) break;  // wave-uniform: no lane holds slot q
+          if (q == bro) broScore = bestScores[q];
         }
       }
       int slot = -1;
@@ -639,8 +673,6 @@ __device__ __forceinline__ float pair_score_any(const ScoreCtx<NQ> &c, const Doc
       for (int q = 0; q < T; q++) {
         if (q == slot) {
           bestScores[q] = score;
-          bestmhg1[q] = mhg1;
-          bestmhg2[q] = mhg2;
           if constexpr (REC::on) {
             bestwpi[q] = wi;
             bestwpj[q] = wj;
@@ -648,11 +680,16 @@ __device__ __forceinline__ float pair_score_any(const ScoreCtx<NQ> &c, const Doc
           }
         }
       }
+      if (slot >= 0) {
+        bestmhg1 = nib_set(bestmhg1, slot, mhg1);
+        bestmhg2 = nib_set(bestmhg2, slot, mhg2);
+      }
       if (numTop >= rmt) {
         minx = 0;
         minv = bestScores[0];
 #pragma unroll
         for (int q = 1; q < T; q++) {
+          if (q >= tw) break;  // rmt <= numTop <= tw here
           if (q < rmt && !(bestScores[q] > minv)) {
             minx = q;
             minv = bestScores[q];
@@ -680,8 +717,10 @@ __device__ __forceinline__ float pair_score_any(const ScoreCtx<NQ> &c, const Doc
   }
   float sum = 0.0;
 #pragma unroll
-  for (int q = 0; q < T; q++)
+  for (int q = 0; q < T; q++) {
+    if (q >= tw) break;
     if (q < numTop) sum += bestScores[q];
+  }
   sum *= wts;
   sum *= pl->tfw[i];
   sum *= pl->tfw[j];
@@ -753,7 +792,10 @@ __device__ __forceinline__ bool score_doc(const Weights *w, const DevPlan *pl, c
   for (int i = 0; i < c.nq; i++) {
     if ((c.excl >> i & 1)) continue;
     int bp;
-    const float sts = single_term_score<NQ, RP, REC, T>(c, d, i, &bp, rec);
+    // the do-while reads at least one record, and fills a slot a record at most
+    const int ni = rget(d.end, i) - rget(d.beg, i);
+    const int tw = wave_max15(min(c.realMaxTop, max(ni, 1)));
+    const float sts = single_term_score<NQ, RP, REC, T>(c, d, i, &bp, rec, tw);
     rset(bestPos, i, bp);
     if (sts < minSingleScore) minSingleScore = sts;
   }
@@ -930,7 +972,10 @@ __device__ __forceinline__ bool score_doc(const Weights *w, const DevPlan *pl, c
       if ((c.excl >> j & 1)) continue;
       if (!(d.present >> i & 1)) continue;
       if (!(d.present >> j & 1)) continue;
-      const float score = pair_score_any<NQ, RP, REC, T>(c, d, i, j, rec);
+      // each step advances one cursor and fills a slot at most: n_i + n_j - 1 steps
+      const int nij = (rget(d.end, i) - rget(d.beg, i)) + (rget(d.end, j) - rget(d.beg, j)) - 1;
+      const int tw = wave_max15(min(c.realMaxTop, max(nij, 1)));
+      const float score = pair_score_any<NQ, RP, REC, T>(c, d, i, j, rec, tw);
       if (score >= minPairScore && minPairScore >= 0.0) continue;
       minPairScore = score;
     }

@@ -763,7 +763,9 @@ class Engine:
         keep, refs = lists if isinstance(lists, tuple) else self.host_lists(lists)
         info = self.info_arrays(params, n)
         r, d, s, h = self._result(cap, hit_cap, info, *self._facet_terms(terms))
-        _check(self.lib.gbgpu_query(self.ctx, qt, n, refs, ctypes.byref(params), ctypes.byref(r)), "query")
+        rc = self.lib.gbgpu_query(self.ctx, qt, n, refs, ctypes.byref(params), ctypes.byref(r))
+        self.last_n_facets = r.n_facets  # the table size after ENOSPC (call again with room)
+        _check(rc, "query")
         return self._pack(r, d, s, h, info)
 
     def query_resident(self, terms: Sequence[QTerm], handles: Sequence[int], params: Params,
@@ -773,7 +775,9 @@ class Engine:
         hh = (ctypes.c_int32 * max(n, 1))(*handles)
         info = self.info_arrays(params, n)
         r, d, s, h = self._result(cap, hit_cap, info, *self._facet_terms(terms))
-        _check(self.lib.gbgpu_query_resident(self.ctx, qt, n, hh, ctypes.byref(params), ctypes.byref(r)), "query")
+        rc = self.lib.gbgpu_query_resident(self.ctx, qt, n, hh, ctypes.byref(params), ctypes.byref(r))
+        self.last_n_facets = r.n_facets
+        _check(rc, "query")
         return self._pack(r, d, s, h, info)
 
     def set_slots(self, n: int) -> None:

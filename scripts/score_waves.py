@@ -22,7 +22,7 @@ from workload import config_two_term, generate  # noqa: E402
 N = int(os.environ.get("SW_DOCS", 100_000_000))
 q = config_two_term(N, docs_to_get=100, seed=1)
 lists = generate(q, N, threads=16)
-with gbgpu.Engine(0) as eng:
+with gbgpu.Engine(0, diag=True) as eng:
     hs = [eng.upload(l) for l in lists]
     for _ in range(3):
         eng.query_resident(q.terms, hs, q.params(), cap=128)

@@ -162,6 +162,42 @@ def test_gpu_facets_over_docid_splits(engine, kind, shape):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("resident", [False, True])
+def test_gpu_facets_over_splits_enospc_then_room(engine, resident):
+    """INTEGRATION.md 3b's retry: the adapter sizes the facet buffer from the
+    first piece's lists; when the whole range's tables hold more entries the
+    call returns ENOSPC with n_facets set (and nothing else valid), and the
+    call again with room for n_facets entries answers exactly.  The facet
+    list's records sit mostly in the last piece, as the retry meets them."""
+    q = qkinds.kinds(20000, seed=13)[1]
+    lists = generate(q, 20000, seed=1301)
+    terms, fl_, fr = facet_query(q, lists, "int", seed=131)
+    for kw in (dict(num_docid_splits=4), dict(num_docid_splits=5, site_clustering=1, docs_to_get=10)):
+        p = params_of(q, fr, **kw)
+        exp = orc.query(terms, fl_, p, cap=1 << 16)
+        n = sum(len(v[1]) for v in exp["facets"].values())
+        assert n > 8
+        old = gbgpu.Engine.facet_cap
+        hs = [engine.upload(x) for x in fl_] if resident else None
+        try:
+            gbgpu.Engine.facet_cap = 3  # what a first piece's lists might size
+            with pytest.raises(gbgpu.GbgpuError) as ei:
+                if resident:
+                    engine.query_resident(terms, hs, p, cap=1 << 16)
+                else:
+                    engine.query(terms, fl_, p, cap=1 << 16)
+            assert ei.value.code == 28  # ENOSPC
+            assert engine.last_n_facets == n, (engine.last_n_facets, n)
+            gbgpu.Engine.facet_cap = engine.last_n_facets  # exactly the room asked for
+            r = engine.query_resident(terms, hs, p, cap=1 << 16) if resident else engine.query(terms, fl_, p, cap=1 << 16)
+            same(r, exp, f"retry {kw}")
+        finally:
+            gbgpu.Engine.facet_cap = old
+            for h in hs or ():
+                engine.free(h)
+
+
+@pytest.mark.gpu
 def test_gpu_facets_paging_and_two_terms(engine):
     """the paging filter (only the docids that reach the tree vote) and two
     facet terms in one query, through the resident path and enqueue/collect"""
