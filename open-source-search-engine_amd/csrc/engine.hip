@@ -94,6 +94,29 @@ struct ListExt {
   uint32_t pad;
 };
 
+// The buckets are narrow where a wave's lanes are one survivor each: a
+// lane's merge loop and scorers run for as many steps as its survivor has
+// units and records, and the wave for as many as its largest lane, so the
+// lanes of one wave should hold survivors of one size.  Buckets 5..15 are
+// the unit counts rc, rc - 1, ... (rc <= 12: one count a bucket; wider
+// steps for larger rc), 2..4 the thirds of (rc, 2rc] (two lanes a
+// survivor), 1 (2rc, 4rc] and 0 above (four and eight lanes).
+constexpr int NBKT = 16;
+static_assert(NBKT % 4 == 0, "count rows are read as 16-byte vectors");
+__host__ __device__ __forceinline__ int size_bucket(uint32_t u, uint32_t rc) {
+  if (u > 4 * rc) return 0;
+  if (u > 2 * rc) return 1;
+  if (u > rc) {
+    const uint32_t d = u - rc - 1;  // 0 .. rc - 1
+    const uint32_t t = (3 * d) / rc;
+    return 4 - (int)(t < 2 ? t : 2u);
+  }
+  const uint32_t w = rc <= 12 ? 1u : (rc + 10) / 11;
+  const uint32_t k = (rc - u) / w;
+  return 5 + (int)(k < 10 ? k : 10u);
+}
+__host__ __device__ __forceinline__ int bucket_shift(int b) { return b == 0 ? 3 : b == 1 ? 4 : b <= 4 ? 5 : 6; }
+
 struct Counters {
   uint32_t filtered;  // m_filtered: scored docids dropped by the paging filter (Posdb.cpp:7327-7347)
   uint32_t corrupt;
@@ -107,8 +130,8 @@ struct Counters {
   uint32_t rdbg_t, rdbg_total;  // diagnostic: replay us in tree_add / in all
   unsigned long long dmax_all;  // largest survivor docid
   ListExt ext[MAXL];
-  uint32_t bcnt[8];    // survivors per size bucket (k_cmp_write block 0), NBKT
-  uint32_t bstart[8];  // each bucket's first survivor position
+  uint32_t bcnt[NBKT];    // survivors per size bucket (k_cmp_write block 0)
+  uint32_t bstart[NBKT];  // each bucket's first survivor position
   unsigned long long arena_top;  // global record arena: units handed out (k_ext_walk, k_score, k_scoreinfo)
   uint32_t nstale;               // survivors whose trailing group merged empty (k_score: the stale list)
   uint32_t pad2;
@@ -1932,7 +1955,7 @@ __global__ void k_range_filter(const DevPlan *__restrict__ pl, uint32_t rbits, u
 //   k_cmp_count  survivors per size bucket of each block, the lists with a
 //                run in some survivor, the re-shrink partials (BlkInfo);
 //   k_cmp_write  each block's offset in every bucket (the counts of the
-//                blocks before it, 32 B a block) and the bucket starts, then
+//                blocks before it, 4 B a bucket a block) and the bucket starts, then
 //                every survivor's record at its final position -- buckets
 //                in order, slot order inside a bucket: slot, list mask, run
 //                units, docid, and its run locations ([pos][nl]), so k_score
@@ -1940,17 +1963,12 @@ __global__ void k_range_filter(const DevPlan *__restrict__ pl, uint32_t rbits, u
 // Survivors are counted by size (their run units, an upper bound on their
 // records) so k_score can give each wave survivors of one size: a wave's
 // lanes run the scorers in lockstep, so its time is its largest lane's.
-// Bucket 0 holds the largest and is scored first.  Buckets 0-2 (more units
-// than a lane's rc records) are scored 8, 16 and 32 to a wave, so each
-// survivor gets 8, 4 or 2 lanes' worth of LDS records.  Site clustering
+// Bucket 0 holds the largest and is scored first.  Buckets 0, 1 and 2-4
+// (more units than a lane's rc records) are scored 8, 16 and 32 to a wave,
+// so each survivor gets 8, 4 or 2 lanes' worth of LDS records (size_bucket).  Site clustering
 // (the TopTree replay walks survivors in docid order, Posdb.cpp:6137-6140)
 // takes the same buckets plus each record's slot-order rank (sv_ord):
 // k_bound writes the replay entries in slot order from it.
-constexpr int NBKT = 8;
-__host__ __device__ __forceinline__ int size_bucket(uint32_t u, uint32_t rc) {
-  return u > 4 * rc ? 0 : u > 2 * rc ? 1 : u > rc ? 2 : 2 * u > rc ? 3 : 3 * u > rc ? 4 : 4 * u > rc ? 5 : 6 * u > rc ? 6 : 7;
-}
-__host__ __device__ __forceinline__ int bucket_shift(int b) { return b == 0 ? 3 : b == 1 ? 4 : b == 2 ? 5 : 6; }
 
 constexpr int CB = 256;            // compaction threads per block
 constexpr int CSPT = 32;           // consecutive slots per bitmap word
@@ -2291,7 +2309,7 @@ __global__ void __launch_bounds__(CB) k_cmp_count(const DevPlan *__restrict__ pl
 // order, slot order inside a bucket: slot, list mask, run units, docid, and
 // its run locations ([pos][nl]), so k_score reads its survivors' data
 // contiguously.  Each block sums the counts of the blocks before it (its
-// offsets) and of all blocks (the bucket starts) from cnt8, 32 B a block;
+// offsets) and of all blocks (the bucket starts) from cnt8, 4 B a bucket a block;
 // block 0 publishes the totals.  sv_ord (site clustering): each record's
 // survivor's rank in slot order, where the replay wants it.
 __global__ void __launch_bounds__(CB) k_cmp_write(const DevPlan *__restrict__ pl, Counters *__restrict__ ctr,
@@ -2321,8 +2339,15 @@ __global__ void __launch_bounds__(CB) k_cmp_write(const DevPlan *__restrict__ pl
 #pragma unroll
     for (int b = 0; b < NBKT; b++) pre[b] = tot[b] = 0;
     for (uint32_t i = threadIdx.x; i < nblk; i += CB) {
-      const v4 a = c4[2 * (size_t)i], c = c4[2 * (size_t)i + 1];
-      const uint32_t v[NBKT] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+      uint32_t v[NBKT];
+#pragma unroll
+      for (int r = 0; r < NBKT / 4; r++) {
+        const v4 a = c4[(NBKT / 4) * (size_t)i + r];
+        v[4 * r] = a.x;
+        v[4 * r + 1] = a.y;
+        v[4 * r + 2] = a.z;
+        v[4 * r + 3] = a.w;
+      }
       const bool before = i < blockIdx.x;
 #pragma unroll
       for (int b = 0; b < NBKT; b++) {
@@ -2416,19 +2441,19 @@ __global__ void __launch_bounds__(CB) k_cmp_write(const DevPlan *__restrict__ pl
     }
   }
   __syncthreads();
-  uint32_t bstart[NBKT], boff[NBKT];
+  // each bucket's first position for this block: the bucket's start plus
+  // the blocks before it
+  __shared__ uint32_t s_base[NBKT];
+  uint32_t ord0 = 0;  // survivors of the blocks before this one
   {
     uint32_t acc = 0;
 #pragma unroll
     for (int b = 0; b < NBKT; b++) {
-      bstart[b] = acc;
+      if (threadIdx.x == b) s_base[b] = acc + s_pre[b];
       acc += s_tot[b];
-      boff[b] = s_pre[b];
+      ord0 += s_pre[b];
     }
   }
-  uint32_t ord0 = 0;  // survivors of the blocks before this one
-#pragma unroll
-  for (int b = 0; b < NBKT; b++) ord0 += boff[b];
   const uint32_t w = blockIdx.x * CWORDS + threadIdx.x;
   CmpWord c;
   c.surv = 0;
@@ -2451,27 +2476,22 @@ __global__ void __launch_bounds__(CB) k_cmp_write(const DevPlan *__restrict__ pl
       const bool own = (lm >> l0) & 1;
       const uint32_t u = act ? cmp_units(pl, ctr, cunit, loc, s, lm, own) : 0;
       const uint32_t b = (uint32_t)size_bucket(u, rc);
-      uint32_t rk = 0;
+      // the wave's lanes with the same bucket: 4 ballots on its bits; the
+      // first of them writes their count
+      static_assert(NBKT == 16, "four bucket bits");
+      uint64_t peers = __ballot(act);
 #pragma unroll
-      for (int bb = 0; bb < NBKT; bb++) {
-        const uint64_t m = __ballot(act && b == (uint32_t)bb);
-        if (b == (uint32_t)bb) rk = (uint32_t)__popcll(m & lt);
-        if (lane == 0) s_wc[wid][bb] = (uint32_t)__popcll(m);
+      for (int bit = 0; bit < 4; bit++) {
+        const uint64_t m = __ballot((b >> bit) & 1u);
+        peers &= ((b >> bit) & 1u) ? m : ~m;
       }
+      const uint32_t rk = (uint32_t)__popcll(peers & lt);
+      if (lane < NBKT) s_wc[wid][lane] = 0;
+      if (act && rk == 0) s_wc[wid][b] = (uint32_t)__popcll(peers);
       __syncthreads();
-      uint32_t wpre = 0;
-#pragma unroll
-      for (int bb = 0; bb < NBKT; bb++)
-        if (b == (uint32_t)bb) {
-          for (int w2 = 0; w2 < wid; w2++) wpre += s_wc[w2][bb];
-          wpre += s_carry[bb];
-        }
       if (act) {
-        uint32_t pos = 0;
-#pragma unroll
-        for (int bb = 0; bb < NBKT; bb++)
-          if (b == (uint32_t)bb) pos = bstart[bb] + boff[bb];
-        pos += wpre + rk;
+        uint32_t pos = s_base[b] + s_carry[b] + rk;
+        for (int w2 = 0; w2 < wid; w2++) pos += s_wc[w2][b];
         sv_slot[pos] = (uint32_t)s;
         sv_lm[pos] = lm;
         sv_u[pos] = u;
