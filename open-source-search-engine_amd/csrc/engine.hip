@@ -6113,6 +6113,11 @@ struct gbgpu_ctx {
   int replay_mode = 0;  // diagnostic only (GBGPU_REPLAY_MODE): 1 the one-wave k_tree_replay always, 3 one register column
   int probe_waves = 0;  // diagnostic: probe spans (GBGPU_PROBE_WAVES; 0 = PROBE_WAVES)
   int probe_runspan = 0;  // diagnostic: chunks per run-driven probe wave (GBGPU_PROBE_RUNSPAN; 0 = 1)
+  // candidates a 3 KiB chunk meets above which a list is probed run-driven
+  // (GBGPU_PROBE_DIR_T in the diagnostic build): config 3's probe phase at
+  // 64 / 128 / 256 / 384 / 768 / 1024: 0.457 / 0.339 / 0.263 / 0.240 / 0.342
+  // / 0.394 ms a query (scripts/r06_c3dir.sh); config 2 meets ~36 either way
+  double probe_dir_t = 384.0;
   int score_mode = 0;  // diagnostic only (GBGPU_SCORE_MODE): 1 mini-merge without scoring
   int debug_ext = 0;   // diagnostic only (GBGPU_DEBUG_EXT): print the re-shrink table per query
   uint64_t *d_sdbg = nullptr;  // GBGPU_SCORE_MODE=2: per-wave k_score timing (GBGPU_SCORE_DUMP file)
@@ -6674,8 +6679,9 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
     P.g0dir[a] = dir_entries;
     dir_entries += ((hi - lo) >> sh) + 1;
   }
-  // probe direction per list: candidate-driven while a 3 KiB chunk meets
-  // about one wave-width of candidates, else run-driven
+  // probe direction per list: candidate-driven while a 3 KiB chunk meets at
+  // most probe_dir_t candidates (several 64-lane windows a chunk still beat
+  // a directory lookup per run), else run-driven
   for (int id = 0; id < P.nlists; id++)
     P.list_mult[id] = (uint8_t)__builtin_popcount(P.lists[id].group_bits & P.pos_mask & ~NEG_BIT);
   P.probed_mask = 0;
@@ -6683,7 +6689,7 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
     P.lists[id].probe = 0;
     if (P.lists[id].g0_array == 0) continue;
     const double per_chunk = (double)slot_ub * WCH_UNITS / std::max<uint32_t>(1, P.lists[id].units);
-    P.lists[id].probe = per_chunk > 64.0 ? PROBE_BY_RUN : PROBE_BY_CAND;
+    P.lists[id].probe = per_chunk > ctx->probe_dir_t ? PROBE_BY_RUN : PROBE_BY_CAND;
     P.probed_mask |= 1u << id;
   }
 
@@ -8622,6 +8628,7 @@ int gbgpu_open(int device, gbgpu_ctx **out) {
   if (const char *rm = std::getenv("GBGPU_REPLAY_MODE")) ctx->replay_mode = std::atoi(rm);
   if (const char *pw = std::getenv("GBGPU_PROBE_WAVES")) ctx->probe_waves = std::atoi(pw);
   if (const char *rs = std::getenv("GBGPU_PROBE_RUNSPAN")) ctx->probe_runspan = std::atoi(rs);
+  if (const char *dt = std::getenv("GBGPU_PROBE_DIR_T")) ctx->probe_dir_t = std::atof(dt);
   if (const char *sm = std::getenv("GBGPU_SCORE_MODE")) ctx->score_mode = std::atoi(sm);
   if (ctx->score_mode == 2) HIPCHECK(hipMalloc(&ctx->d_sdbg, 8192 * 64));
   if (const char *de = std::getenv("GBGPU_DEBUG_EXT")) ctx->debug_ext = std::atoi(de);
