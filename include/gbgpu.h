@@ -259,8 +259,8 @@ typedef struct gbgpu_result {
    * table: not a facet term, or a query that ended before allocTopTree; over
    * docid splits a facet term with an empty list still has its table, as the
    * Query's tables go on over the pieces).  Both NULL: no facet pass.  Facets
-   * run with site clustering and over docid splits; not inside a boolean
-   * expression, at most 4 facet terms, each a group of its own list alone
+   * run with site clustering, over docid splits and in boolean queries, at
+   * most 4 facet terms, each a group of its own list alone
    * (GBGPU_EUNSUPPORTED otherwise).  ENOSPC: only n_facets is valid (over docid
    * splits the call returns before the tree and the score-info outputs are
    * written): call again with facets_cap >= n_facets. */

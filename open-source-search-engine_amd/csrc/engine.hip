@@ -6595,7 +6595,7 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   for (int i = 0; i < nterms; i++) {
     const int32_t fc = terms[i].field_code;
     if (fc < FIELD_GBFACETSTR || fc > FIELD_GBFACETFLOAT || ents[i].size == 0) continue;
-    if (q.facets.size() >= (size_t)MAXF || boolean) return GBGPU_EUNSUPPORTED;
+    if (q.facets.size() >= (size_t)MAXF) return GBGPU_EUNSUPPORTED;
     FacetTerm ft;
     ft.term = i;
     ft.lid = -1;
@@ -7420,6 +7420,7 @@ struct FacetCtr {
   uint32_t pad[2];
   unsigned long long B[MAXF];     // units the survivors' runs take (the shrunk buffer's size)
   unsigned long long docs[MAXF];  // m_numDocsThatHaveFacet
+  unsigned long long heads[MAXF]; // survivors with a run in the facet list (the shrunk buffer's 12-byte keys)
 };
 
 __device__ __forceinline__ int32_t fac_val(gu8 *k) {  // Posdb::getFacetVal32: bytes 2..5
@@ -7484,7 +7485,8 @@ __global__ void k_facet_live(uint32_t nsurv, const uint64_t *sdoc, const uint32_
 }
 
 __global__ void __launch_bounds__(256) k_facet_emit(FacetPlan fp, const Counters *ctr, FacetCtr *fc, const uint32_t *skey,
-                                                    const uint64_t *sv_doc, const Loc *sv_loc, uint32_t nl,
+                                                    const uint64_t *sv_doc, const uint32_t *sv_lm, const Loc *sv_loc,
+                                                    uint32_t nl,
                                                     uint64_t *rdoc, uint64_t *rkey, int32_t *rval, uint32_t cap) {
   const uint32_t nsurv = (uint32_t)(ctr->surv_top >> 36);
   const int lane = threadIdx.x & 63;
@@ -7496,10 +7498,15 @@ __global__ void __launch_bounds__(256) k_facet_emit(FacetPlan fp, const Counters
     for (int f = 0; f < fp.nf; f++) {
       if (fp.lid[f] < 0) continue;
       gu8 *list = gl(fp.list[f]);
-      const Loc lc = act ? sv_loc[(uint64_t)i * nl + (uint32_t)fp.lid[f]] : Loc{0, 0};
+      // (a boolean expression may admit a docid the facet list does not hold)
+      const Loc lc = act && (sv_lm[i] >> fp.lid[f] & 1) ? sv_loc[(uint64_t)i * nl + (uint32_t)fp.lid[f]] : Loc{0, 0};
       unsigned long long lsum = lc.len;
       for (int o = 32; o > 0; o >>= 1) lsum += __shfl_xor(lsum, o, 64);
-      if (lane == 0) atomicAdd(&fc->B[f], lsum);
+      const unsigned long long nh = (unsigned long long)__popcll(__ballot(lc.len > 0));
+      if (lane == 0) {
+        atomicAdd(&fc->B[f], lsum);
+        atomicAdd(&fc->heads[f], nh);
+      }
       const uint32_t nk = vote && lc.len >= 2 ? lc.len - 1 : 0;
       // pass 0 counts this lane's records, pass 1 writes them
       uint32_t n = 0, at = 0;
@@ -7694,15 +7701,15 @@ __device__ __forceinline__ void fac_lds_flush(const uint32_t *lds, uint32_t et, 
 
 // countUniqueDocids over the shrunk part of the buffer: every key of every
 // survivor's run (voting or not) in an existing entry
-__global__ void __launch_bounds__(256) k_facet_outside(FacetPlan fp, const Counters *ctr, const Loc *sv_loc, uint32_t nl,
-                                                       uint32_t et, uint32_t *outside) {
+__global__ void __launch_bounds__(256) k_facet_outside(FacetPlan fp, const Counters *ctr, const uint32_t *sv_lm,
+                                                       const Loc *sv_loc, uint32_t nl, uint32_t et, uint32_t *outside) {
   __shared__ uint32_t s_cnt[FAC_LDS];
   const bool use_lds = et <= (uint32_t)FAC_LDS;
   if (use_lds) fac_lds_init(s_cnt, et);
   const uint32_t nsurv = (uint32_t)(ctr->surv_top >> 36);
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nsurv; i += gridDim.x * blockDim.x) {
     for (int f = 0; f < fp.nf; f++) {
-      if (fp.lid[f] < 0 || fp.tn[f] == 0) continue;
+      if (fp.lid[f] < 0 || fp.tn[f] == 0 || !(sv_lm[i] >> fp.lid[f] & 1)) continue;
       gu8 *list = gl(fp.list[f]);
       const Loc lc = sv_loc[(uint64_t)i * nl + (uint32_t)fp.lid[f]];
       const uint32_t nk = lc.len >= 2 ? lc.len - 1 : 0;
@@ -7726,7 +7733,7 @@ __global__ void k_facet_tailhead(FacetPlan fp, const Counters *ctr, FacetCtr *fc
   gu8 *list = gl(fp.list[f]);
   const uint64_t units = fp.units[f];
   uint64_t u = fc->B[f];
-  unsigned long long docs = ctr->surv_top >> 36;  // every survivor's run head (12 bytes)
+  unsigned long long docs = fc->heads[f];  // every survivor run's head (12 bytes)
   while (u < units && !(list[u * 6 + 1] & 0x02)) {
     gu8 *k = list + u * 6;
     if (fp.tn[f]) {
@@ -7879,7 +7886,7 @@ static int facet_pass(QuerySlot &q, uint32_t nsurv, gbgpu_result *out) {
         vkey = q.fac.as<uint32_t>(o_fkey);
       }
       hipLaunchKernelGGL(k_facet_emit, dim3(g), dim3(256), 0, st, fp, (const Counters *)q.res.as<Counters>(), dfc,
-                         vkey, (const uint64_t *)q.svdoc.as<uint64_t>(),
+                         vkey, (const uint64_t *)q.svdoc.as<uint64_t>(), (const uint32_t *)q.svlm.as<uint32_t>(),
                          (const Loc *)q.svloc.as<Loc>(), nl, q.fac.as<uint64_t>(o_rdoc), q.fac.as<uint64_t>(o_rkey),
                          q.fac.as<int32_t>(o_rval), (uint32_t)cap);
       HIPCHECK(hipGetLastError());
@@ -7973,7 +7980,7 @@ static int facet_pass(QuerySlot &q, uint32_t nsurv, gbgpu_result *out) {
     if (nsurv && et) {
       const uint32_t g = std::max(1u, std::min<uint32_t>(1024, (nsurv + 255) / 256));
       hipLaunchKernelGGL(k_facet_outside, dim3(g), dim3(256), 0, st, fp, (const Counters *)q.res.as<Counters>(),
-                         (const Loc *)q.svloc.as<Loc>(), nl, et, dout);
+                         (const uint32_t *)q.svlm.as<uint32_t>(), (const Loc *)q.svloc.as<Loc>(), nl, et, dout);
     }
     hipLaunchKernelGGL(k_facet_tailhead, dim3(1), dim3(64), 0, st, fp, (const Counters *)q.res.as<Counters>(), dfc,
                        dout, q.fac.as<unsigned long long>(o_t0));

@@ -100,7 +100,7 @@ class Params(ctypes.Structure):
         """A copy of these params carrying the "&sites=" whitelist lists
         (Msg2::m_whiteLists; Posdb.cpp:793-835, 5294).  The copy keeps the
         list buffers alive."""
-        q = Params.from_buffer_copy(self)
+        q = self._copy()
         q._keep = [ctypes.create_string_buffer(bytes(l), max(1, len(l))) for l in lists]
         arr = (ListRef * max(1, len(lists)))(*[ListRef(ctypes.cast(k, ctypes.c_void_p), len(l))
                                                for k, l in zip(q._keep, lists)])
@@ -120,10 +120,7 @@ class Params(ctypes.Structure):
         bit v & 7), and -- for the reference harness only -- the expression
         tokens it is built from (ref_binding: operand term >= 0, OP_OR -1,
         OP_AND -2, OP_NOT -3, '(' -4, ')' -5)."""
-        q = Params.from_buffer_copy(self)
-        for a in ("_keep", "_white"):
-            if hasattr(self, a):
-                setattr(q, a, getattr(self, a))
+        q = self._copy()  # keeps the buffers the pointers name (facet ranges, whitelist)
         table = bytes(table)
         q._bkeep = ctypes.create_string_buffer(table, max(1, len(table)))
         q.is_boolean = 1

@@ -1775,6 +1775,29 @@ static int run_range(const orc_qterm *qt, const uint8_t *const *lists, const int
         minScore = (float)__builtin_popcount(P.bvec[(docIdPtr - P.vb.buf) / 6]);
         siteRank = 0;
         docLang = 0;
+        /* the mini merge runs in a boolean query too (Posdb.cpp:6512-6778);
+         * only the facet votes read its lists there: a facet group's one
+         * sublist is the termlist's run itself (6638-6647), and a group the
+         * docid is not in (the expression did not need it) is empty */
+        for (int j = 0; hasFacet && j < nqti; j++) {
+          QTI *qti = &qip[j];
+          if (!(qti->bigramFlags[0] & BF_FACET)) continue;
+          int nsub = 0;
+          uint8_t *a = NULL, *e = NULL;
+          char fl = 0;
+          for (int k = 0; k < qti->numNewSubLists; k++) {
+            if (!qti->savedCursor[k]) continue;
+            a = qti->savedCursor[k];
+            e = qti->cursor[k];
+            fl = qti->bigramFlags[k];
+            nsub++;
+          }
+          mml[j] = NULL;
+          if (nsub == 1 && !(fl & (BF_SYNONYM | BF_HALFSTOPWIKIBIGRAM))) {
+            mml[j] = a;
+            mme[j] = e;
+          }
+        }
         goto boolJump2;
       }
       /* gbsortby: both prefilters off (Posdb.cpp:6050-6051, 6350-6351) */
@@ -2207,8 +2230,11 @@ int orc_query(const orc_qterm *qt, const uint8_t *const *lists, const int64_t *s
   for (int i = 0; i < nqt; i++) {
     const int fc = qt[i].field_code;
     if ((fc == F_SORTBYINT || fc == F_REVSORTBYINT) && qt[i].is_required) intMode = 1;
-    /* facets: restated outside boolean queries */
-    if ((fc == F_FACETSTR || fc == F_FACETINT || fc == F_FACETFLOAT) && prm->is_boolean) return ENOTSUP;
+    /* facets in a boolean query: restated for a facet term without synonyms
+     * (its group one sublist, the run itself) */
+    if ((fc == F_FACETSTR || fc == F_FACETINT || fc == F_FACETFLOAT) && prm->is_boolean)
+      for (int k = 0; k < nqt; k++)
+        if (qt[k].synonym_of == i) return ENOTSUP;
     /* a boolean query's gbsortby score reads a mini-merged list that may be
        the next group's or stale bytes (Posdb.cpp:7263-7279): not restated */
     if (prm->is_boolean && (fc == F_SORTBYFLOAT || fc == F_REVSORTBYFLOAT || fc == F_SORTBYINT ||

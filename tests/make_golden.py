@@ -575,6 +575,43 @@ def save_boolean():
     save_query("bool_synonyms", q.terms, lists, bool_params(q.params(), [-3, 0, -1, 1]))
 
 
+def save_bool_facets():
+    """Facet terms in a boolean query (Posdb.cpp:5575-5631, 7362-7542 with
+    m_isBoolean): the mini merge still runs (6512-6778), so the facet group's
+    run is there to vote from; the vote buffer is the expression's (8006-8249)
+    and a docid the expression admits without the facet term casts no vote.
+    The facet term is a required term outside the expression, or an operand
+    of it."""
+    import struct
+    from numlists import number_list
+    N = 6000
+    fl = lambda x: struct.unpack("<i", struct.pack("<f", x))[0]  # noqa: E731
+    cases = [
+        # (name, q seed, list seed, field code, ints, kmax, frac, ranges, toks, params kw)
+        ("and_or_int", 1, 1, 64, True, 3, 0.8, None, "and_or", {}),
+        ("or_str", 2, 2, 63, True, 1, 0.6, None, "or", {}),
+        ("or_facet_operand", 1, 3, 64, True, 2, 0.5, None, [0, -1, 1, -2, 5], {}),
+        ("not_float_ranges", 2, 4, 65, False, 2, 0.8, ([fl(0.0), fl(20.0), fl(55.5)], [fl(20.0), fl(55.5), fl(100.0)]),
+         "not", {}),
+        ("or_or_int_clus", 3, 5, 64, True, 3, 0.8, None, "or_or", {"docs_to_get": 10, "site_clustering": 1}),
+        ("and_or_int_splits", 3, 6, 64, True, 3, 0.8, None, "and_or", {"num_docid_splits": 3}),
+    ]
+    for name, qseed, seed, fc, ints, kmax, frac, ranges, toks, kw in cases:
+        q = qkinds.kinds(N, seed=qseed)[1]  # three_word: words a b c, bigrams ab bc
+        if "docs_to_get" in kw:
+            q.docs_to_get = kw["docs_to_get"]
+        lists = generate(q, N, seed=7000 + seed)
+        terms = list(q.terms)
+        terms.append(gbgpu.QTerm(1, 0, fc, 0, -1, -1, -1, 0, max(t.qpos for t in terms) + 2, 0, -1, 1.0))
+        lists = list(lists) + [number_list(lists, frac, seed=70 + seed, kmax=kmax, ints=ints)]
+        pkw = {k: kw[k] for k in ("site_clustering", "num_docid_splits") if k in kw}
+        p = bool_params(q.params(**pkw), BOOL_EXPRS[toks] if isinstance(toks, str) else toks)
+        if ranges:
+            p = p.with_facets([(len(terms) - 1, ranges[0], ranges[1])])
+        r = save_query(f"bool_facet_{name}", terms, lists, p)
+        print(f"q_bool_facet_{name}: hits={r['hits']} facets={ {t: (d, len(e)) for t, (d, e) in r['facets'].items()} }")
+
+
 def save_capacity():
     """Plans near the reference's own capacities: a TopTree beyond 1 536
     nodes (docsToGet 2 000 and 3 000 make m_docsWanted 4 000 and 6 000,
@@ -787,6 +824,7 @@ def main():
     save_range()
     save_boolean()
     save_facets()
+    save_bool_facets()
     save_capacity()
     save_stale()
     save_msg5()

@@ -198,6 +198,28 @@ def test_gpu_facets_over_splits_enospc_then_room(engine, resident):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("shape", ["int", "float_ranges", "str"])
+def test_gpu_facets_in_boolean_queries(engine, shape):
+    """A facet term in a boolean query (the reference's q_bool_facet_*
+    fixtures pin the mode): the expression's vote buffer, the facet group's
+    run voted from where the docid has one -- a docid the truth table admits
+    without it casts no vote -- on random truth tables over the groups"""
+    q = qkinds.kinds(20000, seed=14)[1]
+    lists = generate(q, 20000, seed=1400)
+    terms, fl_, fr = facet_query(q, lists, shape, seed=140)
+    ng = sum(1 for t in terms if t.is_required)
+    rng = np.random.default_rng(141)
+    for it in range(4):
+        bits = rng.integers(0, 2, 1 << ng)
+        bits[0] = 0  # a docid in no group is never voted
+        tb = np.packbits(bits.astype(np.uint8), bitorder="little").tobytes()
+        tb = tb + bytes(max(0, (1 << ng) // 8 - len(tb)))
+        p = params_of(q, fr).with_boolean(tb, ng)
+        exp = orc.query(terms, fl_, p, cap=1 << 16)
+        same(engine.query(terms, fl_, p, cap=1 << 16), exp, f"{shape} table {it}")
+
+
+@pytest.mark.gpu
 def test_gpu_facets_paging_and_two_terms(engine):
     """the paging filter (only the docids that reach the tree vote) and two
     facet terms in one query, through the resident path and enqueue/collect"""
@@ -249,11 +271,6 @@ def test_gpu_facets_capacity_and_refusals(engine):
         assert ei.value.code == 28  # ENOSPC
     finally:
         gbgpu.Engine.facet_cap = old
-    ng = sum(1 for t in terms if t.is_required)
-    tb = bytes([0xff]) * max(1, (1 << ng) // 8)
-    with pytest.raises(gbgpu.GbgpuError) as ei:
-        engine.query(terms, fl_, q.params().with_boolean(tb, ng), cap=1 << 16)
-    assert ei.value.code == gbgpu.GBGPU_EUNSUPPORTED
     big = list(range(300))
     with pytest.raises(gbgpu.GbgpuError) as ei:
         engine.query(terms, fl_, q.params().with_facets([(len(terms) - 1, big, [x + 1 for x in big])]), cap=1 << 16)
