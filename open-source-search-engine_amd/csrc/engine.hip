@@ -6428,8 +6428,7 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
     // a boolean query's gbsortby score reads a mini-merged list that may be
     // another group's or stale (Posdb.cpp:7263-7279); its range terms vote by
     // isInRange over the whole run (8087-8129), not restated on the device;
-    // its second pass is not replayed
-    if (hp.sortby_group >= 0 || p->get_docid_scoring_info) return GBGPU_EUNSUPPORTED;
+    if (hp.sortby_group >= 0) return GBGPU_EUNSUPPORTED;
     for (int i = 0; i < nterms; i++) {
       int ri = 0;
       if (terms[i].is_required && range_mode(terms[i].field_code, &ri)) return GBGPU_EUNSUPPORTED;
@@ -7367,12 +7366,59 @@ static int score_info_docs(QuerySlot &q, const uint64_t *docs, int n, uint32_t n
   }
   return 0;
 }
+// A boolean query's second pass (Posdb.cpp:6116-6244 with m_isBoolean): the
+// loop still walks the tree's nodes (numProcessed, the docid-range skips),
+// but the boolean block at boolJump1 (6514-6534) sets m_docId again from
+// docIdPtr, which the second pass restarted at the vote buffer's start
+// (6119) and advances once a docid (7732); the scorers are jumped over
+// (6833), so the t-th DocIdScore is the t-th vote-buffer docid (ascending)
+// with its boolean score -- unless the paging filter drops it -- with
+// siteRank and docLang 0 and no pair or single records.  m: the docids the
+// pass processes (at most the vote buffer's).
+template <class Sink>
+static int bool_info_docs(QuerySlot &q, int m, uint32_t nsurv, Sink &sink) {
+  m = std::min<int>(m, (int)nsurv);
+  if (m <= 0) return 0;
+  size_t sort_tmp = 0;
+  HIPCHECK(si_sort_pairs(nullptr, sort_tmp, nullptr, nullptr, nullptr, nullptr, nsurv, q.stream));
+  const size_t o_key = 0;
+  const size_t o_val = o_key + align256(8 * (size_t)nsurv);
+  const size_t o_skey = o_val + align256(4 * (size_t)nsurv);
+  const size_t o_sval = o_skey + align256(8 * (size_t)nsurv);
+  const size_t o_tmp = o_sval + align256(4 * (size_t)nsurv);
+  if (q.si.ensure(o_tmp + align256(sort_tmp))) return ENOMEM;
+  hipStream_t st = q.stream;
+  const uint32_t g = std::max(1u, std::min<uint32_t>(1024, (nsurv + 255) / 256));
+  hipLaunchKernelGGL(k_si_keys, dim3(g), dim3(256), 0, st, q.svdoc.as<uint64_t>(), nsurv,
+                     q.si.as<uint64_t>(o_key), q.si.as<uint32_t>(o_val));
+  HIPCHECK(si_sort_pairs(q.si.as<uint8_t>(o_tmp), sort_tmp, q.si.as<uint64_t>(o_key), q.si.as<uint64_t>(o_skey),
+                         q.si.as<uint32_t>(o_val), q.si.as<uint32_t>(o_sval), nsurv, st));
+  std::vector<uint64_t> doc((size_t)m);
+  std::vector<uint32_t> pos((size_t)m), key((size_t)nsurv);
+  HIPCHECK(hipMemcpyAsync(doc.data(), q.si.as<uint8_t>(o_skey), 8 * (size_t)m, hipMemcpyDeviceToHost, st));
+  HIPCHECK(hipMemcpyAsync(pos.data(), q.si.as<uint8_t>(o_sval), 4 * (size_t)m, hipMemcpyDeviceToHost, st));
+  HIPCHECK(hipMemcpyAsync(key.data(), q.skey.p, 4 * (size_t)nsurv, hipMemcpyDeviceToHost, st));
+  HIPCHECK(hipStreamSynchronize(st));
+  for (int t = 0; t < m; t++) {
+    const uint32_t k = key[pos[(size_t)t]];
+    SurvOut inf;
+    std::memset(&inf, 0, sizeof inf);
+    const uint32_t b = (k & 0x80000000u) ? (k & 0x7fffffffu) : ~k;
+    std::memcpy(&inf.score, &b, 4);
+    inf.ok = k != 0;  // 0: the paging filter dropped it (7327-7347)
+    const int rc = sink(doc[(size_t)t], inf, 0, 0, nullptr, nullptr);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
 static int score_info(QuerySlot &q, const uint32_t *keys, const uint64_t *docs, uint32_t nsurv, gbgpu_result *out) {
   int n = 0;
   while (n < q.k && n < q.info_docs && keys[n]) n++;
   InfoAcc acc;
   OutSink sink{out, acc, q.info_ng, q.int_scores};
-  const int rc = score_info_docs(q, docs, n, nsurv, sink);
+  const int rc = reinterpret_cast<const DevPlan *>(q.h_stage)->boolean ? bool_info_docs(q, n, nsurv, sink)
+                                                                       : score_info_docs(q, docs, n, nsurv, sink);
   out->n_docid_scores = acc.nd;
   out->n_pair_scores = acc.np;
   out->n_single_scores = acc.ns;
@@ -8287,6 +8333,7 @@ static int split_info(QuerySlot &q, const int64_t *tree, int n, uint64_t lo, uin
   }
   sink.tree.assign(tree, tree + n);
   std::sort(sink.tree.begin(), sink.tree.end());
+  if (reinterpret_cast<const DevPlan *>(q.h_stage)->boolean) return bool_info_docs(q, (int)sel.size(), nsurv, sink);
   return score_info_docs(q, sel.data(), (int)sel.size(), nsurv, sink);
 }
 

@@ -230,6 +230,33 @@ def save_scoreinfo():
         print(f"  s_v{j}_{q.name}: n={len(r['docids'])} info={len(r['score_info'])}")
 
 
+def save_bool_scoreinfo():
+    """A boolean query's second pass (Posdb.cpp:6116-6244 with m_isBoolean):
+    the boolean block (6514-6534) takes m_docId from docIdPtr, which the
+    second pass restarted at the vote buffer (6119), so the DocIdScores are
+    the vote buffer's first docids with their boolean scores; no pair or
+    single records.  Plain, paging, site clustering, 3 and 5 docid splits
+    (the buffers' kick-out rule, 7588-7665)."""
+    N = 6000
+    q = qkinds.kinds(N, seed=21)[1]  # three_word
+    lists = generate(q, N, seed=5400)
+    for name, toks, kw in (("and_or", "and_or", {}), ("or_or", "or_or", {}), ("not", "not", {}),
+                           ("clus", "and_or", {"site_clustering": 1}),
+                           ("splits3", "or_or", {"num_docid_splits": 3}),
+                           ("splits5_clus", "and_or", {"num_docid_splits": 5, "site_clustering": 1})):
+        p = bool_params(q.params(**kw), BOOL_EXPRS[toks])
+        p.get_docid_scoring_info = 1
+        r = save_query(f"bool_{name}", q.terms, lists, p, prefix="s")
+        print(f"  s_bool_{name}: n={len(r['docids'])} info={len(r['score_info'])}")
+    full = ref.query(q.terms, lists, bool_params(q.params(), BOOL_EXPRS["or_or"]))
+    pos = min(30, len(full["docids"]) - 1)
+    p = bool_params(q.params(max_serp_score=float(full["scores"][pos]), min_serp_docid=int(full["docids"][pos])),
+                    BOOL_EXPRS["or_or"])
+    p.get_docid_scoring_info = 1
+    r = save_query("bool_serp", q.terms, lists, p, prefix="s")
+    print(f"  s_bool_serp: n={len(r['docids'])} info={len(r['score_info'])}")
+
+
 def sortby_list(lists, frac, seed, termid=0x5A5A5A5A5A5, neg_frac=0.0):
     """A numeric gbsortby: termlist (Posdb.cpp:4572-4577): one key per docid
     for a `frac` share of the query's docids, a float where the word position
@@ -819,6 +846,7 @@ def main():
     save_whitelist()
     save_scoreinfo()
     save_scoreinfo_splits()
+    save_bool_scoreinfo()
     save_sortby()
     save_sortby_int_modes()
     save_range()

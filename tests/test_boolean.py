@@ -97,11 +97,6 @@ def test_gpu_boolean_refused_modes(engine):
     with pytest.raises(gbgpu.GbgpuError) as e:  # the table must be over the plan's groups
         engine.query(q.terms, lists, q.params().with_boolean(tab, 2))
     assert e.value.code == 22  # EINVAL
-    p = q.params().with_boolean(tab, 3)
-    p.get_docid_scoring_info = 1  # the second pass is not replayed for boolean queries
-    with pytest.raises(gbgpu.GbgpuError) as e:
-        engine.query(q.terms, lists, p)
-    assert e.value.code == gbgpu.GBGPU_EUNSUPPORTED
     terms = list(q.terms)
     terms[0] = gbgpu.QTerm(*[getattr(terms[0], f) for f, _ in gbgpu.QTerm._fields_])
     terms[0].field_code = 54  # gbsortby: reads a mini-merged list that may be stale
