@@ -3172,7 +3172,12 @@ __device__ __forceinline__ void score_survivor(const DevPlan *__restrict__ pl, c
   if (ok) {
     const uint32_t b = __float_as_uint(score);
     key = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
-    if (pl->sortby_group >= 0 && pl->sortby_int) key = ival ^ 0x80000000u;  // int32 order
+    if (pl->sortby_group >= 0 && pl->sortby_int) {
+      key = ival ^ 0x80000000u;  // int32 order
+      // m_intScore INT32_MIN would travel as key 0 ("not scored"): the query
+      // is declined (GBGPU_EUNSUPPORTED), never answered with INT32_MIN + 1
+      if (key == 0) const_cast<Counters *>(ctr)->unsup = 1;
+    }
     if (key == 0) key = 1;
   }
   *key_out = key;

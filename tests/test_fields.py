@@ -182,3 +182,56 @@ def test_gpu_int_sortby_paging_vs_oracle(engine, seed, fc):
         label = f"fc={fc} seed={seed} bound={b}"
         assert (r.hits, r.filtered, r.docs_wanted) == (o["hits"], o["filtered"], o["docs_wanted"]), label
         assert np.array_equal(r.docids, o["docids"]), label
+
+
+@pytest.mark.gpu
+def test_gpu_int_sortby_int32_min_declined(engine):
+    """m_intScore INT32_MIN (Posdb.cpp:7271-7279) has no survivor key of its
+    own on the device (key 0 means "not scored"): a query that scores such a
+    docid is declined (EUNSUPPORTED, the adapter runs the CPU body) instead
+    of reporting INT32_MIN + 1; INT32_MIN + 1 itself, and INT32_MIN on keys
+    no scored docid holds, are answered exactly."""
+    import struct
+    import posdb_py
+    import qkinds
+    from numlists import number_list
+    from workload import generate
+    N = 20000
+    q = qkinds.kinds(N, seed=3)[0]
+    lists = generate(q, N, seed=7300)
+    terms = list(q.terms)
+    terms.append(gbgpu.QTerm(1, 0, 59, 0, -1, -1, -1, 0, max(x.qpos for x in terms) + 2, 0, -1, 1.0))
+    nl = number_list(lists, 0.6, seed=3, kmax=2, ints=True)
+    keys = posdb_py.full_keys(nl)
+
+    def with_values(pick):
+        ks = []
+        for k in keys:
+            k = bytearray(k)
+            v = pick(int.from_bytes(k[7:12], "little") >> 2, struct.unpack("<i", bytes(k[2:6]))[0])
+            k[2:6] = struct.pack("<i", v)
+            ks.append(bytes(k))
+        return posdb_py.encode_keys(ks)
+
+    p = q.params()
+    base = orc.query(terms, list(lists) + [nl], p, cap=1 << 16)
+    assert len(base["docids"]) > 10
+    top = int(base["docids"][0])
+    # INT32_MIN + 1 everywhere: answered, as the oracle
+    l1 = list(lists) + [with_values(lambda d, v: -(1 << 31) + 1)]
+    r = engine.query(terms, l1, p, cap=1 << 16)
+    o = orc.query(terms, l1, p, cap=1 << 16)
+    assert np.array_equal(r.docids, o["docids"]) and r.hits == o["hits"]
+    # INT32_MIN on a scored docid: declined
+    l2 = list(lists) + [with_values(lambda d, v: -(1 << 31) if d == top else v)]
+    with pytest.raises(gbgpu.GbgpuError) as ei:
+        engine.query(terms, l2, p, cap=1 << 16)
+    assert ei.value.code == gbgpu.GBGPU_EUNSUPPORTED
+    # INT32_MIN on a docid the query does not score (not voted): answered
+    voted = set(int(x) for x in orc.intersect(terms, list(lists) + [nl], params=p))
+    other = next(int.from_bytes(k[7:12], "little") >> 2 for k in keys
+                 if (int.from_bytes(k[7:12], "little") >> 2) not in voted)
+    l3 = list(lists) + [with_values(lambda d, v: -(1 << 31) if d == other else v)]
+    r = engine.query(terms, l3, p, cap=1 << 16)
+    o = orc.query(terms, l3, p, cap=1 << 16)
+    assert np.array_equal(r.docids, o["docids"]) and r.hits == o["hits"]
