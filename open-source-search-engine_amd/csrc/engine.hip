@@ -6142,6 +6142,25 @@ struct gbgpu_ctx {
   DevBuf xsend, xrecv, xout;
   uint8_t *h_xout = nullptr;
   size_t h_xout_cap = 0;
+  // the full-reply merge's device scratch and its pinned host stage (the
+  // heads, the pack, the merged block): plain allocations the exchange owns,
+  // grown between calls, so no copy touches pageable memory
+  DevBuf xscratch;
+  uint8_t *h_xf = nullptr;
+  size_t h_xf_cap = 0;
+  int ensure_h_xf(size_t bytes) {
+    if (bytes <= h_xf_cap) return 0;
+    if (h_xf) (void)hipHostFree(h_xf);
+    h_xf = nullptr;
+    h_xf_cap = 0;
+    const size_t want = std::max<size_t>(bytes + bytes / 4, 1 << 18);
+    if (hipHostMalloc(reinterpret_cast<void **>(&h_xf), want) != hipSuccess) {
+      h_xf = nullptr;
+      return ENOMEM;
+    }
+    h_xf_cap = want;
+    return 0;
+  }
 };
 
 // result block layout: [Counters | keys k | docids k]
@@ -8711,7 +8730,9 @@ void gbgpu_close(gbgpu_ctx *ctx) {
   ctx->xsend.release();
   ctx->xrecv.release();
   ctx->xout.release();
+  ctx->xscratch.release();
   if (ctx->h_xout) (void)hipHostFree(ctx->h_xout);
+  if (ctx->h_xf) (void)hipHostFree(ctx->h_xf);
   ctx->lists.clear();  // the last references: ListMem frees the device copies
   ctx->files.clear();
   if (ctx->upload_stream) (void)hipStreamSynchronize(ctx->upload_stream);
@@ -9464,15 +9485,23 @@ int gbgpu_merge_replies_device(gbgpu_ctx *ctx, const gbgpu_merge_req *req, const
   std::vector<int32_t> fb;
   size_t stride = 0;
   if ((rc = pack_all(req, replies, nshards, buf, stride, fb))) return rc;
+  const size_t sb = gbx::merge_scratch_bytes(nshards, fb.data());
+  if (!sb) return GBGPU_ECAPACITY;
   std::lock_guard<std::mutex> xg(ctx->x_mu);
   (void)hipSetDevice(ctx->device);
   if (!ctx->xstream && hipStreamCreateWithFlags(&ctx->xstream, hipStreamNonBlocking) != hipSuccess) return GBGPU_EHIP;
   hipStream_t xs = ctx->xstream;
-  uint8_t *d = nullptr;
-  if (hipMallocAsync(reinterpret_cast<void **>(&d), buf.size(), xs) != hipSuccess) return ENOMEM;
-  if (hipMemcpyAsync(d, buf.data(), buf.size(), hipMemcpyHostToDevice, xs) != hipSuccess) rc = GBGPU_EHIP;
-  if (!rc) rc = gbx::merge_device(xs, d, nshards, stride, rq, fb.data(), out);
-  (void)hipFreeAsync(d, xs);
+  // the packs go where an all-gather would leave them (the receive buffer),
+  // staged through pinned memory
+  if (ctx->xrecv.ensure(buf.size()) || ctx->xscratch.ensure(sb) ||
+      ctx->ensure_h_xf(std::max(buf.size(), gbx::merge_stage_bytes())))
+    return ENOMEM;
+  std::memcpy(ctx->h_xf, buf.data(), buf.size());
+  if (hipMemcpyAsync(ctx->xrecv.p, ctx->h_xf, buf.size(), hipMemcpyHostToDevice, xs) != hipSuccess ||
+      hipStreamSynchronize(xs) != hipSuccess)
+    return GBGPU_EHIP;
+  rc = gbx::merge_device(xs, ctx->xrecv.as<uint8_t>(), nshards, stride, rq, fb.data(), ctx->xscratch.as<uint8_t>(),
+                         ctx->xscratch.cap, ctx->h_xf, out);
   if (hipStreamSynchronize(xs) != hipSuccess && !rc) rc = GBGPU_EHIP;
   return rc;
 }
@@ -9481,59 +9510,83 @@ int gbgpu_merge_replies_device(gbgpu_ctx *ctx, const gbgpu_merge_req *req, const
 // collectives, so no rank is left waiting whatever fails: the heads (fixed
 // size), then every rank's verdict on the buffers the largest pack needs
 // (a min all-reduce), then the packs at that size.
-static int allgather_replies_admitted(gbgpu_ctx *ctx, const gbgpu_merge_req *req, const gbx::XFReq &rq,
-                                      const gbgpu_reply *mine, int err, gbgpu_merged *out) {
+static int allgather_replies_admitted(gbgpu_ctx *ctx, const gbx::XFReq &rq, const gbgpu_reply *mine, int err,
+                                      gbgpu_merged *out) {
   std::lock_guard<std::mutex> xg(ctx->x_mu);
   if (!ctx->comm) return EINVAL;
   (void)hipSetDevice(ctx->device);
   hipStream_t xs = ctx->xstream;
   const int nr = ctx->nranks;
-  const size_t mb = err ? sizeof(gbx::XFHead) : gbx::pack_bytes(mine);
-  std::vector<uint8_t> pk(std::max<size_t>(mb, sizeof(gbx::XFHead)), 0);
+  const size_t mb = std::max(err ? sizeof(gbx::XFHead) : gbx::pack_bytes(mine), sizeof(gbx::XFHead));
+  std::vector<uint8_t> pk(mb, 0);
   gbx::pack_reply(err ? nullptr : mine, rq.nqt, pk.data());
-  std::vector<uint8_t> heads(sizeof(gbx::XFHead) * nr);
   int rc = 0;
   int32_t ok = 1;
   size_t stride = 256;
   std::vector<int32_t> fb(nr, 0);
+  // the flags go through the small result buffer (xout, sized at
+  // gbgpu_comm_init and never reallocated): a rank whose pack buffers
+  // could not grow still takes part in every collective
+  uint8_t *dflag = ctx->xout.as<uint8_t>();
+  uint8_t *dflags = dflag + 256;
+  static_assert(256 + 4 * 64 <= sizeof(XHead) + 16 * (size_t)XMAX, "flags fit xout");
   // 1: the heads (the send and receive buffers hold at least XMAX records
-  // since gbgpu_comm_init, so this never allocates)
-  if (hipMemcpyAsync(ctx->xsend.p, pk.data(), sizeof(gbx::XFHead), hipMemcpyHostToDevice, xs) != hipSuccess) rc = GBGPU_EHIP;
+  // since gbgpu_comm_init, so this never allocates), staged through the
+  // pinned result buffer
+  uint8_t *hx = ctx->h_xout;
+  std::memcpy(hx, pk.data(), sizeof(gbx::XFHead));
+  if (hipMemcpyAsync(ctx->xsend.p, hx, sizeof(gbx::XFHead), hipMemcpyHostToDevice, xs) != hipSuccess) rc = GBGPU_EHIP;
   if (ncclAllGather(ctx->xsend.p, ctx->xrecv.p, sizeof(gbx::XFHead), ncclUint8, ctx->comm, xs) != ncclSuccess) rc = GBGPU_EHIP;
-  if (hipMemcpyAsync(heads.data(), ctx->xrecv.p, heads.size(), hipMemcpyDeviceToHost, xs) != hipSuccess ||
+  if (hipMemcpyAsync(hx, ctx->xrecv.p, sizeof(gbx::XFHead) * nr, hipMemcpyDeviceToHost, xs) != hipSuccess ||
       hipStreamSynchronize(xs) != hipSuccess)
     rc = GBGPU_EHIP;
   if (!rc) {
     for (int r = 0; r < nr; r++) {
       gbx::XFHead h;
-      std::memcpy(&h, heads.data() + sizeof h * r, sizeof h);
+      std::memcpy(&h, hx + sizeof h * r, sizeof h);
       if (h.empty) continue;
       gbgpu_reply x;
       std::memset(&x, 0, sizeof x);
       x.n = h.n;
       x.nqt = h.nqt;
       x.facet_list_size = h.facet_bytes;
-      stride = std::max(stride, align256(gbx::pack_bytes(&x)));
+      const size_t b = gbx::pack_bytes(&x);
+      if (!b) {
+        rc = GBGPU_ECORRUPT;
+        break;
+      }
+      stride = std::max(stride, align256(b));
       fb[r] = h.facet_bytes;
     }
   }
-  // 2: every rank can hold the packs
-  if (rc || ctx->xsend.ensure(stride) || ctx->xrecv.ensure(stride * nr)) ok = 0;
-  int32_t *dok = reinterpret_cast<int32_t *>(ctx->xout.p);
-  if (hipMemcpyAsync(dok, &ok, 4, hipMemcpyHostToDevice, xs) != hipSuccess) rc = rc ? rc : GBGPU_EHIP;
-  if (ncclAllReduce(dok, dok, 1, ncclInt32, ncclMin, ctx->comm, xs) != ncclSuccess) rc = rc ? rc : GBGPU_EHIP;
-  int32_t all_ok = 0;
-  if (hipMemcpyAsync(&all_ok, dok, 4, hipMemcpyDeviceToHost, xs) != hipSuccess || hipStreamSynchronize(xs) != hipSuccess)
+  // 2: every rank can hold the packs and the merge's scratch (an all-gather
+  // of the verdicts)
+  const size_t sb = rc ? 0 : gbx::merge_scratch_bytes(nr, fb.data());
+  if (rc || !sb || pk.size() > stride || ctx->xsend.ensure(stride) || ctx->xrecv.ensure(stride * nr) ||
+      ctx->xscratch.ensure(sb) || ctx->ensure_h_xf(std::max(stride, gbx::merge_stage_bytes())))
+    ok = 0;
+  std::memcpy(hx, &ok, 4);
+  if (hipMemcpyAsync(dflag, hx, 4, hipMemcpyHostToDevice, xs) != hipSuccess) rc = rc ? rc : GBGPU_EHIP;
+  if (ncclAllGather(dflag, dflags, 4, ncclUint8, ctx->comm, xs) != ncclSuccess) rc = rc ? rc : GBGPU_EHIP;
+  if (hipMemcpyAsync(hx, dflags, 4 * (size_t)nr, hipMemcpyDeviceToHost, xs) != hipSuccess ||
+      hipStreamSynchronize(xs) != hipSuccess)
     rc = rc ? rc : GBGPU_EHIP;
   if (rc) return rc;
-  if (!all_ok) return ENOMEM;
+  for (int r = 0; r < nr; r++) {
+    int32_t f;
+    std::memcpy(&f, hx + 4 * r, 4);
+    if (!f) return ENOMEM;
+  }
   // 3: the packs
-  if (hipMemcpyAsync(ctx->xsend.p, pk.data(), pk.size(), hipMemcpyHostToDevice, xs) != hipSuccess) rc = GBGPU_EHIP;
+  std::memcpy(ctx->h_xf, pk.data(), pk.size());
+  if (hipMemcpyAsync(ctx->xsend.p, ctx->h_xf, pk.size(), hipMemcpyHostToDevice, xs) != hipSuccess) rc = GBGPU_EHIP;
   if (ncclAllGather(ctx->xsend.p, ctx->xrecv.p, stride, ncclUint8, ctx->comm, xs) != ncclSuccess) rc = GBGPU_EHIP;
-  if (!rc) rc = gbx::merge_device(xs, ctx->xrecv.as<uint8_t>(), nr, stride, rq, fb.data(), out);
+  if (hipStreamSynchronize(xs) != hipSuccess) rc = GBGPU_EHIP;
+  if (!rc)
+    rc = gbx::merge_device(xs, ctx->xrecv.as<uint8_t>(), nr, stride, rq, fb.data(), ctx->xscratch.as<uint8_t>(),
+                           ctx->xscratch.cap, ctx->h_xf, out);
   if (hipStreamSynchronize(xs) != hipSuccess && !rc) rc = GBGPU_EHIP;
   if (err) return err;
-  (void)req;
   return rc;
 }
 
@@ -9549,7 +9602,7 @@ int gbgpu_allgather_replies(gbgpu_ctx *ctx, uint64_t seq, int timeout_ms, const 
     err = EINVAL;
   int rc = seq_enter(&ctx->xseq, seq, timeout_ms);
   if (rc) return rc;
-  rc = allgather_replies_admitted(ctx, req, rq, mine, err, out);
+  rc = allgather_replies_admitted(ctx, rq, mine, err, out);
   seq_leave(&ctx->xseq, seq);
   return rc;
 }

@@ -53,10 +53,19 @@ void pack_reply(const gbgpu_reply *r, int32_t nqt, uint8_t *dst);
 // checks a request; fills the device view
 int make_req(const gbgpu_merge_req *req, XFReq *x);
 
+// device scratch merge_device needs for nranks packs holding facet_bytes[r]
+// bytes of facet lists (0: more entries than it handles)
+size_t merge_scratch_bytes(int nranks, const int32_t *facet_bytes);
+// pinned host bytes merge_device reads its result through
+size_t merge_stage_bytes();
+
 // device merge of nranks packs laid `stride` bytes apart in d_recv (device
-// memory), synchronously on stream st; result into `out` (host arrays)
+// memory), synchronously on stream st; result into `out` (host arrays).
+// The caller owns the scratch (device, merge_scratch_bytes) and the stage
+// (pinned host, merge_stage_bytes): the merge allocates nothing.
 int merge_device(hipStream_t st, const uint8_t *d_recv, int nranks, size_t stride, const XFReq &req,
-                 const int32_t *facet_bytes, gbgpu_merged *out);
+                 const int32_t *facet_bytes, uint8_t *scratch, size_t scratch_bytes, uint8_t *stage,
+                 gbgpu_merged *out);
 
 // the same merge on the host
 int merge_host(const gbgpu_merge_req *req, const gbgpu_reply *replies, int nshards, gbgpu_merged *out);

@@ -481,96 +481,113 @@ int make_req(const gbgpu_merge_req *req, XFReq *x) {
   return 0;
 }
 
+namespace {
+// the scratch a merge of these packs lays out (device)
+struct Layout {
+  uint32_t emax = 0, nb = 0;
+  size_t sort_tmp = 0, o_out = 0, o_sec = 0, o_nsec = 0, o_rbase = 0, o_misc = 0, o_k = 0, o_ks = 0, o_v = 0,
+         o_vs = 0, o_bc = 0, o_fac = 0, o_tmp = 0, bytes = 0;
+  bool set(int nranks, const int32_t *facet_bytes) {
+    uint64_t e = 1;
+    for (int r = 0; r < nranks; r++) e += (uint64_t)std::max(0, facet_bytes[r]) / 36;
+    if (e > (1u << 30)) return false;
+    emax = (uint32_t)e;
+    nb = (emax + 255) / 256;
+    (void)gbgpu::si_sort_pairs(nullptr, sort_tmp, nullptr, nullptr, nullptr, nullptr, emax, nullptr, 40);
+    o_out = 0;
+    o_sec = o_out + al256(OUT_BYTES);
+    o_nsec = o_sec + al256(sizeof(XFSec) * 64 * MAXSEC);
+    o_rbase = o_nsec + 256;
+    o_misc = o_rbase + 256;  // err, total
+    o_k = o_misc + 256;
+    o_ks = o_k + al256(8 * (size_t)emax);
+    o_v = o_ks + al256(8 * (size_t)emax);
+    o_vs = o_v + al256(4 * (size_t)emax);
+    o_bc = o_vs + al256(4 * (size_t)emax);
+    o_fac = o_bc + al256(4 * ((size_t)nb + 1));
+    o_tmp = o_fac + al256(sizeof(gbgpu_facet_entry) * (size_t)emax);
+    bytes = o_tmp + al256(sort_tmp);
+    return true;
+  }
+};
+// the stage: the merged block, then the section walk's error and entry
+// count, then the table size
+constexpr size_t ST_MISC = OUT_BYTES;
+constexpr size_t ST_NFAC = OUT_BYTES + 8;
+constexpr size_t ST_BYTES = OUT_BYTES + 16;
+}  // namespace
+
+size_t merge_scratch_bytes(int nranks, const int32_t *facet_bytes) {
+  Layout L;
+  return nranks >= 1 && nranks <= 64 && L.set(nranks, facet_bytes) ? L.bytes : 0;
+}
+
+size_t merge_stage_bytes() { return ST_BYTES; }
+
 int merge_device(hipStream_t st, const uint8_t *d_recv, int nranks, size_t stride, const XFReq &rq,
-                 const int32_t *facet_bytes, gbgpu_merged *out) {
-  if (nranks < 1 || nranks > 64 || (uint32_t)rq.docs_to_get > XFMAX || !out) return EINVAL;
-  uint64_t emax64 = 1;
-  for (int r = 0; r < nranks; r++) emax64 += (uint64_t)std::max(0, facet_bytes[r]) / 36;
-  if (emax64 > (1u << 30)) return GBGPU_ECAPACITY;
-  const uint32_t emax = (uint32_t)emax64;
-  const uint32_t nb = (emax + 255) / 256;
-  size_t sort_tmp = 0;
-  (void)gbgpu::si_sort_pairs(nullptr, sort_tmp, nullptr, nullptr, nullptr, nullptr, emax, st, 40);
-  // scratch: merged block, sections, keys/values (in, sorted), block counts, sort scratch
-  const size_t o_out = 0;
-  const size_t o_sec = o_out + al256(OUT_BYTES);
-  const size_t o_nsec = o_sec + al256(sizeof(XFSec) * 64 * MAXSEC);
-  const size_t o_rbase = o_nsec + 256;
-  const size_t o_misc = o_rbase + 256;  // err, total
-  const size_t o_k = o_misc + 256;
-  const size_t o_ks = o_k + al256(8 * (size_t)emax);
-  const size_t o_v = o_ks + al256(8 * (size_t)emax);
-  const size_t o_vs = o_v + al256(4 * (size_t)emax);
-  const size_t o_bc = o_vs + al256(4 * (size_t)emax);
-  const size_t o_fac = o_bc + al256(4 * ((size_t)nb + 1));
-  const size_t o_tmp = o_fac + al256(sizeof(gbgpu_facet_entry) * (size_t)emax);
-  const size_t bytes = o_tmp + al256(sort_tmp);
-  uint8_t *s = nullptr;
+                 const int32_t *facet_bytes, uint8_t *s, size_t scratch_bytes, uint8_t *stage, gbgpu_merged *out) {
+  if (nranks < 1 || nranks > 64 || (uint32_t)rq.docs_to_get > XFMAX || !out || !s || !stage) return EINVAL;
+  Layout L;
+  if (!L.set(nranks, facet_bytes)) return GBGPU_ECAPACITY;
+  if (scratch_bytes < L.bytes) return EINVAL;
+  const uint32_t emax = L.emax, nb = L.nb;
   int rc = 0;
-  XFOut ho;
-  std::vector<uint8_t> hb;
-  if (hipMallocAsync(reinterpret_cast<void **>(&s), bytes, st) != hipSuccess) return ENOMEM;
   {
-    hipLaunchKernelGGL(k_xf_merge, dim3(1), dim3(64), 0, st, d_recv, nranks, stride, rq, s + o_out);
+    hipLaunchKernelGGL(k_xf_merge, dim3(1), dim3(64), 0, st, d_recv, nranks, stride, rq, s + L.o_out);
     XCHECK(hipGetLastError());
-    int32_t *derr = reinterpret_cast<int32_t *>(s + o_misc);
-    uint32_t *dtot = reinterpret_cast<uint32_t *>(s + o_misc + 4);
+    int32_t *derr = reinterpret_cast<int32_t *>(s + L.o_misc);
+    uint32_t *dtot = reinterpret_cast<uint32_t *>(s + L.o_misc + 4);
     hipLaunchKernelGGL(k_xf_sections, dim3(1), dim3(64), 0, st, d_recv, nranks, stride, rq,
-                       reinterpret_cast<XFSec *>(s + o_sec), reinterpret_cast<int32_t *>(s + o_nsec),
-                       reinterpret_cast<uint32_t *>(s + o_rbase), derr, dtot);
+                       reinterpret_cast<XFSec *>(s + L.o_sec), reinterpret_cast<int32_t *>(s + L.o_nsec),
+                       reinterpret_cast<uint32_t *>(s + L.o_rbase), derr, dtot);
     XCHECK(hipGetLastError());
-    uint64_t *k = reinterpret_cast<uint64_t *>(s + o_k), *ks = reinterpret_cast<uint64_t *>(s + o_ks);
-    uint32_t *v = reinterpret_cast<uint32_t *>(s + o_v), *vs = reinterpret_cast<uint32_t *>(s + o_vs);
-    uint32_t *bc = reinterpret_cast<uint32_t *>(s + o_bc);
-    gbgpu_facet_entry *fac = reinterpret_cast<gbgpu_facet_entry *>(s + o_fac);
-    hipLaunchKernelGGL(k_xf_keys, dim3(nb), dim3(256), 0, st, d_recv, nranks, reinterpret_cast<XFSec *>(s + o_sec),
-                       reinterpret_cast<int32_t *>(s + o_nsec), reinterpret_cast<uint32_t *>(s + o_rbase), dtot, emax,
-                       k, v);
+    uint64_t *k = reinterpret_cast<uint64_t *>(s + L.o_k), *ks = reinterpret_cast<uint64_t *>(s + L.o_ks);
+    uint32_t *v = reinterpret_cast<uint32_t *>(s + L.o_v), *vs = reinterpret_cast<uint32_t *>(s + L.o_vs);
+    uint32_t *bc = reinterpret_cast<uint32_t *>(s + L.o_bc);
+    gbgpu_facet_entry *fac = reinterpret_cast<gbgpu_facet_entry *>(s + L.o_fac);
+    hipLaunchKernelGGL(k_xf_keys, dim3(nb), dim3(256), 0, st, d_recv, nranks, reinterpret_cast<XFSec *>(s + L.o_sec),
+                       reinterpret_cast<int32_t *>(s + L.o_nsec), reinterpret_cast<uint32_t *>(s + L.o_rbase), dtot,
+                       emax, k, v);
     XCHECK(hipGetLastError());
-    XCHECK(gbgpu::si_sort_pairs(s + o_tmp, sort_tmp, k, ks, v, vs, emax, st, 40));
+    size_t tmp = L.sort_tmp;
+    XCHECK(gbgpu::si_sort_pairs(s + L.o_tmp, tmp, k, ks, v, vs, emax, st, 40));
     hipLaunchKernelGGL(k_xf_heads, dim3(nb), dim3(256), 0, st, ks, dtot, emax, bc);
     hipLaunchKernelGGL(k_xf_bscan, dim3(1), dim3(1024), 0, st, bc, nb);
     hipLaunchKernelGGL(k_xf_emit, dim3(nb), dim3(256), 0, st, d_recv, ks, vs, dtot, emax, bc, rq, fac);
     XCHECK(hipGetLastError());
-    // the merged head, the section walk's error and the table size
-    uint32_t misc[2], nfac = 0;
-    XCHECK(hipMemcpyAsync(&ho, s + o_out, sizeof ho, hipMemcpyDeviceToHost, st));
-    XCHECK(hipMemcpyAsync(misc, s + o_misc, 8, hipMemcpyDeviceToHost, st));
-    XCHECK(hipMemcpyAsync(&nfac, bc + nb, 4, hipMemcpyDeviceToHost, st));
+    // the merged block, the section walk's error and the table size, in one
+    // round trip through the pinned stage
+    XCHECK(hipMemcpyAsync(stage, s + L.o_out, OUT_BYTES, hipMemcpyDeviceToHost, st));
+    XCHECK(hipMemcpyAsync(stage + ST_MISC, s + L.o_misc, 8, hipMemcpyDeviceToHost, st));
+    XCHECK(hipMemcpyAsync(stage + ST_NFAC, bc + nb, 4, hipMemcpyDeviceToHost, st));
     XCHECK(hipStreamSynchronize(st));
-    if (ho.err) {
-      rc = ho.err;
-      goto done;
-    }
-    if (misc[0]) {
-      rc = (int)misc[0];
-      goto done;
-    }
+    XFOut ho;
+    std::memcpy(&ho, stage, sizeof ho);
+    int32_t serr;
+    uint32_t nfac;
+    std::memcpy(&serr, stage + ST_MISC, 4);
+    std::memcpy(&nfac, stage + ST_NFAC, 4);
+    if (ho.err) return ho.err;
+    if (serr) return serr;
     out->n = ho.n;
     out->hits = ho.hits;
     out->n_facets = (int32_t)nfac;
     const size_t n = (size_t)ho.n;
-    const size_t need = OUT_FDOCS + 8 * (size_t)MAXQT;
-    hb.resize(need);
-    XCHECK(hipMemcpyAsync(hb.data(), s + o_out, need, hipMemcpyDeviceToHost, st));
     const bool fit = !out->facets || (int32_t)nfac <= out->facets_cap;
-    if (out->facets && fit && nfac)
+    if (out->facets && fit && nfac) {
       XCHECK(hipMemcpyAsync(out->facets, fac, sizeof(gbgpu_facet_entry) * nfac, hipMemcpyDeviceToHost, st));
-    XCHECK(hipStreamSynchronize(st));
-    if ((int32_t)n > out->cap) {
-      rc = ENOSPC;
-      goto done;
+      XCHECK(hipStreamSynchronize(st));
     }
+    if ((int32_t)n > out->cap) return ENOSPC;
     for (size_t i = 0; i < n; i++) {
-      if (out->docids) std::memcpy(&out->docids[i], hb.data() + OUT_DOCS + 8 * i, 8);
-      if (out->scores) std::memcpy(&out->scores[i], hb.data() + OUT_SCORES + 8 * i, 8);
+      if (out->docids) std::memcpy(&out->docids[i], stage + OUT_DOCS + 8 * i, 8);
+      if (out->scores) std::memcpy(&out->scores[i], stage + OUT_SCORES + 8 * i, 8);
     }
-    if (out->cluster_recs && rq.clus) std::memcpy(out->cluster_recs, hb.data() + OUT_RECS, 12 * n);
-    if (out->facet_docs) std::memcpy(out->facet_docs, hb.data() + OUT_FDOCS, 8 * (size_t)rq.nqt);
+    if (out->cluster_recs && rq.clus) std::memcpy(out->cluster_recs, stage + OUT_RECS, 12 * n);
+    if (out->facet_docs) std::memcpy(out->facet_docs, stage + OUT_FDOCS, 8 * (size_t)rq.nqt);
     if (!fit) rc = ENOSPC;
   }
 done:
-  (void)hipFreeAsync(s, st);
   if (rc == GBGPU_EHIP) (void)hipStreamSynchronize(st);
   return rc;
 }

@@ -675,9 +675,7 @@ static std::vector<char> table_by_key(HashTableX *ft) {
 
 // INTEGRATION.md §4's Msg3a-side block (gbgpuFillMsg3a over the exchange's
 // merged result) -- linked only into gbref_gpu
-struct gbgpu_merge_req;
-struct gbgpu_reply;
-extern int gbref_adapter_exchange(Msg3a *m, const gbgpu_reply *mine) __attribute__((weak));
+extern int gbref_adapter_exchange(Msg3a *m, const Msg39Reply *mine) __attribute__((weak));
 
 static Msg3a *s_m3a = NULL;
 static Msg39Request s_m3req;
@@ -713,6 +711,7 @@ static void msg3a_setup(int32_t docs_to_get, bool clus, bool hide_all, bool fami
   s_m3a->m_r = &s_m3req;
   s_m3a->m_debug = 0;
   s_m3a->m_docsToGet = docs_to_get;
+  s_m3a->m_numTotalEstimatedHits = 0;
 }
 
 static void msg3a_read(MergedOut &o) {
@@ -777,7 +776,7 @@ static int ref_msg3a_full(int mode, std::vector<ShardReply> &sh, int32_t docs_to
     m->mergeLists();
   } else {
     if (!gbref_adapter_exchange) return ENOSYS;
-    int rc = gbref_adapter_exchange(m, (const gbgpu_reply *)&rep[0]);
+    int rc = gbref_adapter_exchange(m, &rep[0]);
     if (rc) {
       for (int j = 0; j < ns; j++) m->m_reply[j] = NULL;
       return rc;

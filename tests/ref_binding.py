@@ -62,7 +62,8 @@ def _read(n, exe=None):
     return b
 
 
-def query(terms, lists, params, cap=4096, votes=False, reps=1, white=None, mode=None, exe=None, op=None):
+def query(terms, lists, params, cap=4096, votes=False, reps=1, white=None, mode=None, exe=None, op=None,
+          op9=(0, 0, 3)):
     """Same result dict as oracle_binding.query (+ 'votes', 'seconds').
     white: the whitelist lists (Msg2::m_whiteLists) when params.use_whitelist.
     mode (op 4, the gbref_gpu build): 0 the CPU body, 1 INTEGRATION.md's
@@ -73,6 +74,8 @@ def query(terms, lists, params, cap=4096, votes=False, reps=1, white=None, mode=
     qt = (gbgpu.QTerm * max(1, len(terms)))(*terms)
     if op == 7:
         head = struct.pack("<ii", 7, len(terms))
+    elif op == 9:
+        head = struct.pack("<iiiiii", 9, mode, *op9, len(terms))
     else:
         head = struct.pack("<ii", 1, len(terms)) if mode is None else struct.pack("<iii", 4, mode, len(terms))
     req = [head, bytes(params), bytes(qt)[:ctypes.sizeof(gbgpu.QTerm) * len(terms)]]
@@ -130,7 +133,9 @@ def query(terms, lists, params, cap=4096, votes=False, reps=1, white=None, mode=
         out.update(shard_rc=grc, shard_hits=gh)
         out["shard_docids"] = np.frombuffer(rd(8 * gn), np.int64).copy()
         out["shard_scores"] = np.frombuffer(rd(8 * gn), np.float64).copy()
-    if mode is not None:
+    if op == 9:
+        out["merged"] = _read_merged(rd)
+    elif mode is not None:
         answered, used = struct.unpack("<ii", rd(8))
         out.update(answered=answered, used_nodes=used, int_scores=np.frombuffer(rd(4 * r.n), np.int32).copy())
         (npl,) = struct.unpack("<i", rd(4))
@@ -145,6 +150,17 @@ def query(terms, lists, params, cap=4096, votes=False, reps=1, white=None, mode=
     if r.corrupt < 0:
         raise RuntimeError(f"gbref query rc={-r.corrupt}")
     return out
+
+
+def shard_msg3a(terms, lists, params, mode, family=0, hide=0, nsites=3, white=None, exe=None):
+    """op 9 (gbref_gpu): the query through Msg39 (mode 0 the CPU body, 1
+    INTEGRATION.md's adapter), its reply built as Msg39 builds it over a
+    synthetic clusterdb (CR_OK nodes, cluster records, facet lists), and
+    that reply merged by Msg3a (mode 0 the reference's gotAllShardReplies
+    sums and mergeLists, 1 INTEGRATION.md 4b's gbgpuMsg3aReplies over the
+    one-rank exchange).  Returns the query result with 'merged'."""
+    return query(terms, lists, params, cap=1 << 16, white=white, mode=mode, exe=exe or EXE_GPU, op=9,
+                 op9=(family, hide, nsites))
 
 
 def posdb_merge(lists, remove_neg_keys, min_rec_sizes=-1, timed=False):

@@ -154,6 +154,38 @@ def test_gpu_adapter_shard_query(path):
     assert r["shard_hits"] == r["hits"], label
 
 
+# ------------------------------ Msg3a over full replies
+# every query fixture -- site-clustered and facet ones included -- as one
+# shard: the reply Msg39 builds (CR_OK nodes, cluster records over gbref's
+# synthetic clusterdb, facet lists and counts), merged by Msg3a; the GPU
+# side is the adapter body plus gbgpuMsg3aReplies (the one-rank exchange)
+REPLY_CASES = [p for p in QCASES if "splits" not in os.path.basename(p)]
+
+
+@pytest.mark.gpu
+@needs_gpu_build
+@pytest.mark.parametrize("path", REPLY_CASES, ids=[os.path.basename(p)[:-4] for p in REPLY_CASES])
+def test_gpu_adapter_msg3a_replies(path):
+    terms, lists, params, exp = load_query(path)
+    label = os.path.basename(path)
+    white = getattr(params, "_white", None)
+    for family, hide, nsites in ((0, 0, 3), (1, 1, 5)):
+        cpu = ref.shard_msg3a(terms, lists, params, 0, family, hide, nsites, white=white)["merged"]
+        gpu = ref.shard_msg3a(terms, lists, params, 1, family, hide, nsites, white=white)["merged"]
+        tag = (label, family, hide, nsites)
+        assert cpu["rc"] == 0, tag
+        assert gpu["rc"] == 0, (tag, gpu["rc"])
+        assert np.array_equal(gpu["docids"], cpu["docids"]), tag
+        assert np.array_equal(gpu["scores"].view(np.uint64), cpu["scores"].view(np.uint64)), tag
+        assert gpu["recs"] == cpu["recs"], tag
+        assert gpu["hits"] == cpu["hits"], tag
+        assert np.array_equal(gpu["fdocs"], cpu["fdocs"]), tag
+        for a, b in zip(gpu["tables"], cpu["tables"]):
+            # m_docId of a merged entry is the reference's rand() pick; one
+            # reply: the entry itself
+            assert np.array_equal(a, b), tag
+
+
 # -------------------------------------------- the merge
 def _merge_cases():
     from test_golden import MCASES, split_blob

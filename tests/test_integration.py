@@ -2,7 +2,7 @@
 
 Every ```cpp block of INTEGRATION.md is concatenated, in order, after the
 reference headers the adapter's host files include (Posdb.cpp:1-11,
-Msg39.cpp, RdbList.cpp) and compiled with the reference's own flags
+Msg39.cpp, RdbList.cpp, Msg3a.cpp) and compiled with the reference's own flags
 (Makefile:101: gnu++98, -fpermissive, -DPTHREADS), syntax only.  Needs the
 reference tree, so it runs in the build container only (skipped elsewhere).
 """
@@ -24,6 +24,7 @@ PRELUDE = """\
 #include "Msg39.h"
 #include "TopTree.h"
 #include "RdbList.h"
+#include "Msg3a.h"
 #include "Conf.h"
 """
 
