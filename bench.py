@@ -655,6 +655,54 @@ def main():
                     "one structure/page-map/granule pass), queried, freed; one query at a time, and with "
                     "`in_flight.queries` queries in flight; not `value`",
         }
+        # Msg5's read of a termlist (f3, gbgpu_termlist_merge): three resident
+        # files, each holding a third of config 2's docid range, cut and merged
+        # on the device with the tree's list (the first 1 000 docs again: the
+        # newest copies of keys the first file holds, replaced in the merge),
+        # into resident lists the query then reads.  The merged lists are
+        # config 2's own, so the answer must be r0's.
+        thirds = [generate(qs[0], total, doc_begin=j * per // 3, doc_end=(j + 1) * per // 3, threads=16)
+                  for j in range(3)]
+        tree = generate(qs[0], total, doc_begin=0, doc_end=1000, threads=1)
+        fhs, offs3 = [], []
+        for fl in thirds:
+            fhs.append(eng.file_upload(b"".join(fl)))
+            offs3.append(np.cumsum([0] + [len(x) for x in fl[:-1]]).tolist())
+
+        def pieces(t):
+            return [(fhs[j], int(offs3[j][t]), len(thirds[j][t]), None) for j in range(3) if thirds[j][t]] + \
+                   ([tree[t]] if tree[t] else [])
+
+        nt = len(first_lists)
+        in_bytes = sum(len(thirds[j][t]) for j in range(3) for t in range(nt)) + sum(len(x) for x in tree)
+        n_m = 20
+        for it in range(n_m + 2):  # merge + query, checked
+            if it == 2:
+                t_mq = time.perf_counter()
+            hl = [eng.termlist_merge(pieces(t)) for t in range(nt)]
+            r_m = eng.query_resident(qs[0].terms, hl, ps[0])
+            for h in hl:
+                eng.free(h)
+            if r_m.hits != r0.hits or not np.array_equal(r_m.docids, r0.docids):
+                raise RuntimeError("Msg5-merged query differs from the host-buffer query")
+        el_mq = time.perf_counter() - t_mq
+        t_m = time.perf_counter()
+        for it in range(n_m):  # the merges alone
+            for t in range(nt):
+                eng.free(eng.termlist_merge(pieces(t)))
+        el_m = time.perf_counter() - t_m
+        for fh in fhs:
+            eng.file_free(fh)
+        del thirds, tree
+        result["msg5_merge"] = {
+            "queries_per_sec": round(n_m / el_mq, 3),
+            "merge_only_per_sec": round(n_m / el_m, 3),
+            "merge_in_GBps": round(in_bytes * n_m / el_m / 1e9, 3),
+            "bytes_in_per_query": in_bytes,
+            "note": "each config-2 termlist merged on the device (gbgpu_termlist_merge: three file cuts, "
+                    "docid thirds, plus a 1 000-doc tree list) into a resident list, then queried; one query "
+                    "at a time; merge_only_per_sec: the merges without the query; not `value`",
+        }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline_query(qs[0], first_lists)
         if "clustering" in result:

@@ -135,6 +135,7 @@ struct Counters {
   unsigned long long arena_top;  // global record arena: units handed out (k_ext_walk, k_score, k_scoreinfo)
   uint32_t nstale;               // survivors whose trailing group merged empty (k_score: the stale list)
   uint32_t pad2;
+  uint32_t sq_dbg[4];  // diagnostic (GBGPU_DIAG + GBGPU_TOPK_DEBUG): k_tree_seq clocks, 10 ns units
 };
 
 // top-k select state (k_score's histogram, k_topk's gathers)
@@ -5027,6 +5028,7 @@ __global__ void __launch_bounds__(64 * SQ_W) k_tree_seq(Counters *ctr, const uin
   bool called = false;
   uint32_t filtered = 0, err = 0, adds = 0, nmax = 0, ncand = 0;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  uint64_t t_add = 0, t_seq = 0, t_filt = 0;  // diagnostic clocks (GBGPU_DIAG)
   if (threadIdx.x == 0) s_st = SeqState{0u, 0u, 0.0f, 0u, 0ull};
   uint4 e[SQ_E];
   auto load = [&](uint32_t sg) {
@@ -5057,7 +5059,14 @@ __global__ void __launch_bounds__(64 * SQ_W) k_tree_seq(Counters *ctr, const uin
       if (!slow) return ~0u;
       // the offer as uniform values (readlane, not a shuffle): the add's
       // control flow is then scalar, its node indices SGPRs
-      if (!T.add(tp, rl_u32(k0, (uint32_t)j), rl_u64(d, (uint32_t)j), lane)) {
+#ifdef GBGPU_DIAG
+      const uint64_t ta = __builtin_amdgcn_s_memrealtime();
+#endif
+      const bool added = T.add(tp, rl_u32(k0, (uint32_t)j), rl_u64(d, (uint32_t)j), lane);
+#ifdef GBGPU_DIAG
+      t_add += __builtin_amdgcn_s_memrealtime() - ta;
+#endif
+      if (!added) {
         err = TREE_ERR_REG;
         return ~0u;
       }
@@ -5080,6 +5089,9 @@ __global__ void __launch_bounds__(64 * SQ_W) k_tree_seq(Counters *ctr, const uin
   if (ns) load(0);
   for (uint32_t sg = 0; sg < nseg; sg++) {
     __syncthreads();  // s_st published, s_cand free
+#ifdef GBGPU_DIAG
+    const uint64_t tf = __builtin_amdgcn_s_memrealtime();
+#endif
     const SeqState st = s_st;
     if (st.stop) break;  // (uniform over the block)
     // 1. the filter: each wave's 64 SQ_E consecutive entries
@@ -5103,6 +5115,10 @@ __global__ void __launch_bounds__(64 * SQ_W) k_tree_seq(Counters *ctr, const uin
     if (sg + 1 < nseg) load(sg + 1);
     __syncthreads();
     if (wid != 0) continue;
+#ifdef GBGPU_DIAG
+    const uint64_t ts = __builtin_amdgcn_s_memrealtime();
+    t_filt += ts - tf;
+#endif
     // 2. the sequencer: the candidates in order, then the state
     uint32_t pre[SQ_W + 1];
     pre[0] = 0;
@@ -5137,6 +5153,9 @@ __global__ void __launch_bounds__(64 * SQ_W) k_tree_seq(Counters *ctr, const uin
       const float bs = key_score(T.tk);
       s_st = SeqState{full ? 1u : 0u, err ? 1u : 0u, mws < bs ? mws : bs, T.tk, T.td};
     }
+#ifdef GBGPU_DIAG
+    t_seq += __builtin_amdgcn_s_memrealtime() - ts;
+#endif
   }
   if (wid != 0) return;
   if (lane == 0) {
@@ -5147,6 +5166,10 @@ __global__ void __launch_bounds__(64 * SQ_W) k_tree_seq(Counters *ctr, const uin
     ctr->pad[1] = nmax;
     ctr->rdbg_t = ncand;
     ctr->rdbg_total = (uint32_t)((__builtin_amdgcn_s_memrealtime() - t0) / 100);
+    ctr->sq_dbg[0] = (uint32_t)t_add;
+    ctr->sq_dbg[1] = (uint32_t)t_seq;
+    ctr->sq_dbg[2] = (uint32_t)t_filt;
+    ctr->sq_dbg[3] = nseg;
   }
   if (err) return;
 #pragma unroll
@@ -8270,8 +8293,10 @@ static int collect(gbgpu_ctx *ctx, QuerySlot &q, gbgpu_result *out, std::vector<
                    (td[5] - td[4]) / 100.0, td[6], td[7]);
   }
   if (ctx->topk_debug && q.replayed)
-    std::fprintf(stderr, "replay: adds %u nmax %u tree_n %u us_add|cand %u us_total %u nsurv %u\n", c->pad[0], c->pad[1],
-                 c->tree_n, c->rdbg_t, c->rdbg_total, (uint32_t)(c->surv_top >> 36));
+    std::fprintf(stderr, "replay: adds %u nmax %u tree_n %u us_add|cand %u us_total %u nsurv %u "
+                 "seq: us_in_add %.1f us_seq %.1f us_filt %.1f nseg %u\n", c->pad[0], c->pad[1],
+                 c->tree_n, c->rdbg_t, c->rdbg_total, (uint32_t)(c->surv_top >> 36), c->sq_dbg[0] / 100.0,
+                 c->sq_dbg[1] / 100.0, c->sq_dbg[2] / 100.0, c->sq_dbg[3]);
   if (ctx->debug_ext) {
     for (int l = 0; l < MAXL; l++)
       if (c->ext[l].units || c->ext[l].E)

@@ -180,6 +180,7 @@ def test_gpu_adapter_msg3a_replies(path):
         assert gpu["recs"] == cpu["recs"], tag
         assert gpu["hits"] == cpu["hits"], tag
         assert np.array_equal(gpu["fdocs"], cpu["fdocs"]), tag
+        assert len(gpu["tables"]) == len(cpu["tables"]), tag
         for a, b in zip(gpu["tables"], cpu["tables"]):
             # m_docId of a merged entry is the reference's rand() pick; one
             # reply: the entry itself
