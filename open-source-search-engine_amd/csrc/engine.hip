@@ -2747,7 +2747,7 @@ __device__ __forceinline__ void score_survivor(const DevPlan *__restrict__ pl, c
                                                uint32_t *key_out, int diag, uint32_t *nrec_out,
                                                bool stamp, uint64_t &tmerge, uint64_t (&tm)[3],
                                                REC *srec = nullptr, SurvOut *so = nullptr,
-                                               const uint16_t *kill = nullptr, uint32_t *mtot_out = nullptr,
+                                               const uint32_t *kill = nullptr, uint32_t *mtot_out = nullptr,
                                                bool *stale_out = nullptr, const uint64_t *inject = nullptr,
                                                MbufTap *tap = nullptr) {
   const int ng = pl->ngroups;
@@ -3575,7 +3575,7 @@ __device__ int si_word_pos_list(const SiList &L, uint64_t docId, uint32_t own, i
 // bit x of group j where it misses; d is the survivor of docid-order rank lo
 // with list mask lm.  < 0: a path not replayed (*blid: the list)
 __device__ int si_kill(const DevPlan *__restrict__ pl, const Counters *ctr, const Loc *sv_loc, const uint32_t *sperm,
-                       const uint32_t *cum, uint32_t nsurv, uint64_t d, uint32_t lo, uint32_t lm, uint16_t *kill,
+                       const uint32_t *cum, uint32_t nsurv, uint64_t d, uint32_t lo, uint32_t lm, uint32_t *kill,
                        int *blid) {
   for (int j = 0; j < MAXG; j++) kill[j] = 0;
   const uint32_t anys = ctr->anysurv;
@@ -3593,7 +3593,7 @@ __device__ int si_kill(const DevPlan *__restrict__ pl, const Counters *ctr, cons
         *blid = lid;
         return f;
       }
-      if (f == 0) kill[j] |= (uint16_t)(1u << x);
+      if (f == 0) kill[j] |= 1u << x;
     }
   }
   return 0;
@@ -3654,7 +3654,7 @@ __global__ void __launch_bounds__(SCORE_TPB) k_scoreinfo(const DevPlan *__restri
   const uint32_t i = sperm[lo];
   const uint32_t s = sv_slot[i];
   const uint32_t lm = sv_lm[i];
-  uint16_t kill[MAXG];
+  uint32_t kill[MAXG];
   int blid = 0;
   const int f = si_kill(pl, ctr, sv_loc, sperm, cum, nsurv, d, lo, lm, kill, &blid);
   if (f < 0) {
@@ -3720,7 +3720,7 @@ __global__ void __launch_bounds__(SCORE_TPB) k_si_stale(const DevPlan *__restric
   const uint32_t nl = (uint32_t)pl->nlists;
   SurvOut so{0.0f, 0, 0, -3};  // -3 on a failed replay (capacity / a tap that missed): the host declines
   // survivor index and kill mask of second-pass position t (false: not replayable)
-  auto second = [&](uint32_t t, uint32_t &i, uint16_t *kill) -> bool {
+  auto second = [&](uint32_t t, uint32_t &i, uint32_t *kill) -> bool {
     const uint64_t d = tdoc[t];
     const uint32_t lo = si_rank(sdoc, nsurv, d);
     if (lo >= nsurv) return false;
@@ -3730,7 +3730,7 @@ __global__ void __launch_bounds__(SCORE_TPB) k_si_stale(const DevPlan *__restric
   };
   // room for the largest merge this lane runs (plus the injected record)
   uint32_t me = 0;
-  uint16_t kill[MAXG];
+  uint32_t kill[MAXG];
   if (!second(E.t, me, kill)) {
     info[E.t] = so;
     return;
@@ -3739,7 +3739,7 @@ __global__ void __launch_bounds__(SCORE_TPB) k_si_stale(const DevPlan *__restric
   uint32_t need = surv_units_off(pl, ctr, sv_slot[me], sv_lm[me], sv_u[me], &roff) + 1;
   uint32_t wi[12];
   for (uint32_t p = 0; p < E.nb; p++) {
-    uint16_t k2[MAXG];
+    uint32_t k2[MAXG];
     wi[p] = E.w[p] & 0x7fffffffu;
     if (!(E.w[p] & 0x80000000u) && !second(E.w[p], wi[p], k2)) {
       info[E.t] = so;
@@ -3762,7 +3762,7 @@ __global__ void __launch_bounds__(SCORE_TPB) k_si_stale(const DevPlan *__restric
     if (done >> p & 1) continue;
     const uint32_t w = wi[p];
     const bool first = (E.w[p] & 0x80000000u) != 0;
-    uint16_t k2[MAXG];
+    uint32_t k2[MAXG];
     uint32_t wdummy = 0;
     if (!first) (void)second(E.w[p], wdummy, k2);
     MbufTap tap;

@@ -55,7 +55,10 @@ constexpr int MUPT = 8;                          // units per thread (decode)
 constexpr int MCH = MB * MUPT;                   // 2048 units = 12 KiB per decode chunk
 constexpr int WIN_LO = 16;                       // bytes staged before a chunk (2 units + pad)
 constexpr int WIN_BYTES = WIN_LO + MCH * 6 + 16; // + 2 units after it
-constexpr int TCAP = 512;                        // keys per merge tile
+#ifndef GBGPU_TCAP
+#define GBGPU_TCAP 512
+#endif
+constexpr int TCAP = GBGPU_TCAP;                 // keys per merge tile
 constexpr int TB = 256;                          // threads per merge-tile block
 constexpr int MAXN = 256;                        // runs per merge (oracle MAXL)
 constexpr int SCAN_TPB = MB * 4;                 // tiles per scan block

@@ -25,7 +25,7 @@ constexpr uint8_t BF_EXCLUDE = BF_PIPED | BF_NEGATIVE | BF_NUMBER | BF_FACET;
 constexpr int REF_MAX_SUBLISTS = 50;  // Posdb.h:417
 // GPU-path capacities (EUNSUPPORTED beyond)
 constexpr int MAXG = 16;     // QueryTermInfos (required term groups)
-constexpr int MAXSUB = 16;   // sublists per group
+constexpr int MAXSUB = 32;   // sublists per group (MAXL: one group may hold every list)
 constexpr int MAXL = 32;     // distinct lists referenced by one query
 constexpr int MAXG0 = 8;     // sublists of the smallest group (candidate arrays)
 constexpr uint32_t NEG_BIT = 0x80000000u;

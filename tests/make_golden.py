@@ -661,6 +661,23 @@ def save_capacity():
         print(f"q_cap_words{nw}: lists={len(lists)} hits={r['hits']} n={len(r['docids'])}")
 
 
+def save_sublists():
+    """A group past 16 sublists (the GPU's old MAXSUB): one word with 20 and
+    with 29 synonyms, so its QueryTermInfo holds the word, its synonyms and
+    the bigram (22 and 31 sublists, Posdb.cpp:4354-4869; MAX_SUBLISTS is 50,
+    Posdb.h:417), 23 and 32 lists in all; also with site clustering."""
+    from workload import Word, build_query
+    N = 6000
+    for nsyn, seed in ((20, 41), (29, 42)):
+        words = [Word("w0", 0.5, synonyms=(0.04,) * nsyn), Word("w1", 0.6)]
+        q = build_query(f"sub{nsyn}", words, N, seed=seed, docs_to_get=50)
+        lists = generate(q, N, seed=4100 + nsyn)
+        r = save_query(f"cap_sub{nsyn}", q.terms, lists, q.params())
+        print(f"q_cap_sub{nsyn}: lists={len(lists)} hits={r['hits']} n={len(r['docids'])}")
+        r = save_query(f"cap_sub{nsyn}_clus", q.terms, lists, q.params(site_clustering=1))
+        print(f"q_cap_sub{nsyn}_clus: hits={r['hits']} n={len(r['docids'])}")
+
+
 def save_stale():
     """The stale-mbuf case: the second word's list empty, so group 1 holds
     only bigram keys, and a docid whose bigram keys all carry syn bits
@@ -854,6 +871,7 @@ def main():
     save_facets()
     save_bool_facets()
     save_capacity()
+    save_sublists()
     save_stale()
     save_msg5()
     save_msg3a()
@@ -867,7 +885,9 @@ def main():
 
 
 if __name__ == "__main__":
-    if sys.argv[1:] == ["splits"]:
+    if sys.argv[1:] == ["sublists"]:
+        save_sublists()
+    elif sys.argv[1:] == ["splits"]:
         save_splits()
     elif sys.argv[1:] == ["clustering"]:
         save_clustering()
