@@ -120,7 +120,7 @@ __host__ __device__ __forceinline__ int bucket_shift(int b) { return b == 0 ? 3 
 struct Counters {
   uint32_t filtered;  // m_filtered: scored docids dropped by the paging filter (Posdb.cpp:7327-7347)
   uint32_t corrupt;
-  unsigned long long surv_top;  // survivors << 36 | their run units (k_cmp_write block 0)
+  unsigned long long surv_top;  // survivors << 36 | their run units (k_cmp_place block 0)
   uint32_t g0count[MAXG0];
   uint32_t anysurv;  // bit l: list l has a run in some survivor
   uint32_t tree_n;   // site clustering: TopTree nodes written by k_tree_replay
@@ -130,7 +130,7 @@ struct Counters {
   uint32_t rdbg_t, rdbg_total;  // diagnostic: replay us in tree_add / in all
   unsigned long long dmax_all;  // largest survivor docid
   ListExt ext[MAXL];
-  uint32_t bcnt[NBKT];    // survivors per size bucket (k_cmp_write block 0)
+  uint32_t bcnt[NBKT];    // survivors per size bucket (k_cmp_place block 0)
   uint32_t bstart[NBKT];  // each bucket's first survivor position
   unsigned long long arena_top;  // global record arena: units handed out (k_ext_walk, k_score, k_scoreinfo)
   uint32_t nstale;               // survivors whose trailing group merged empty (k_score: the stale list)
@@ -1949,18 +1949,22 @@ __global__ void k_range_filter(const DevPlan *__restrict__ pl, uint32_t rbits, u
 // slot is voted by its own list only through the probe, which credits a
 // docid to the first array holding it) and its bits in the probe bitmaps.
 //
-// Two passes over the slots, CWORDS bitmap words (CTILE slots) a block of
-// CB threads -- a word a thread for the bit-parallel vote test, then the
-// block's survivors spread over all CB threads, so each thread waits on the
-// run locations of about one survivor:
-//   k_cmp_count  survivors per size bucket of each block, the lists with a
-//                run in some survivor, the re-shrink partials (BlkInfo);
-//   k_cmp_write  each block's offset in every bucket (the counts of the
-//                blocks before it, 4 B a bucket a block) and the bucket starts, then
-//                every survivor's record at its final position -- buckets
-//                in order, slot order inside a bucket: slot, list mask, run
-//                units, docid, and its run locations ([pos][nl]), so k_score
-//                reads its survivors' data contiguously.
+// Two launches, CWORDS bitmap words (CTILE slots) a block of CB threads; the
+// survivors are derived once:
+//   k_cmp_count  a word a thread for the bit-parallel vote test, then the
+//                block's survivors spread over all CB threads (each thread
+//                waits on the run locations of about one survivor): their
+//                count per size bucket, the lists with a run in some
+//                survivor, the re-shrink partials (BlkInfo), and each
+//                survivor's (slot, list mask, run units) staged in slot order
+//                at the block's CTILE-slot place;
+//   k_cmp_place  each block's offset in every bucket (the counts of the
+//                blocks before it, 4 B a bucket a block) and the bucket
+//                starts, then every staged survivor's record at its final
+//                position -- buckets in order, slot order inside a bucket:
+//                slot, list mask, run units, docid, and its run locations
+//                ([pos][nl]), so k_score reads its survivors' data
+//                contiguously.
 // Survivors are counted by size (their run units, an upper bound on their
 // records) so k_score can give each wave survivors of one size: a wave's
 // lanes run the scorers in lockstep, so its time is its largest lane's.
@@ -2195,7 +2199,9 @@ __global__ void __launch_bounds__(CB) k_cmp_count(const DevPlan *__restrict__ pl
                                                   const uint32_t *__restrict__ cunit, const uint32_t *__restrict__ bits,
                                                   uint32_t nwords, const Loc *__restrict__ loc,
                                                   const uint64_t *__restrict__ cand, uint32_t rc,
-                                                  BlkInfo *__restrict__ blk, uint32_t *__restrict__ cnt8) {
+                                                  BlkInfo *__restrict__ blk, uint32_t *__restrict__ cnt8,
+                                                  uint32_t *__restrict__ st_slot, uint32_t *__restrict__ st_lm,
+                                                  uint32_t *__restrict__ st_u) {
   __shared__ CmpStage S;
   __shared__ uint32_t tmp[CB / 64];
   __shared__ uint32_t s_cnt[NBKT];
@@ -2230,6 +2236,12 @@ __global__ void __launch_bounds__(CB) k_cmp_count(const DevPlan *__restrict__ pl
       const bool own = (lm >> pl->g0list[0]) & 1;
       const uint32_t u = cmp_units(pl, ctr, cunit, loc, s, lm, own);
       atomicAdd(&s_cnt[size_bucket(u, rc)], 1u);
+      // the block's survivors in slot order for k_cmp_place (block b's at
+      // b * CTILE: a block holds at most its CTILE slots' survivors)
+      const size_t si = (size_t)blockIdx.x * CTILE + base + i;
+      st_slot[si] = (uint32_t)s;
+      st_lm[si] = lm;
+      st_u[si] = u;
       any |= lm;
       usum += u;
       if (xmask) {
@@ -2313,17 +2325,16 @@ __global__ void __launch_bounds__(CB) k_cmp_count(const DevPlan *__restrict__ pl
 // offsets) and of all blocks (the bucket starts) from cnt8, 4 B a bucket a block;
 // block 0 publishes the totals.  sv_ord (site clustering): each record's
 // survivor's rank in slot order, where the replay wants it.
-__global__ void __launch_bounds__(CB) k_cmp_write(const DevPlan *__restrict__ pl, Counters *__restrict__ ctr,
-                                                  const uint32_t *__restrict__ cunit, const uint32_t *__restrict__ bits,
-                                                  uint32_t nwords, const Loc *__restrict__ loc,
+__global__ void __launch_bounds__(CB) k_cmp_place(const DevPlan *__restrict__ pl, Counters *__restrict__ ctr,
+                                                  const uint32_t *__restrict__ cunit, const Loc *__restrict__ loc,
                                                   const uint64_t *__restrict__ cand, uint32_t rc,
                                                   const BlkInfo *__restrict__ blk, const uint32_t *__restrict__ cnt8,
-                                                  uint32_t nblk, uint32_t *__restrict__ sv_slot,
+                                                  uint32_t nblk, const uint32_t *__restrict__ st_slot,
+                                                  const uint32_t *__restrict__ st_lm, const uint32_t *__restrict__ st_u,
+                                                  uint32_t *__restrict__ sv_slot,
                                                   uint32_t *__restrict__ sv_lm, uint32_t *__restrict__ sv_u,
                                                   uint64_t *__restrict__ sv_doc, Loc *__restrict__ sv_loc,
                                                   uint32_t *__restrict__ sv_ord) {
-  __shared__ CmpStage S;
-  __shared__ uint32_t tmp[CB / 64];
   __shared__ uint32_t s_pre[NBKT], s_tot[NBKT], s_carry[NBKT];
   __shared__ uint32_t s_wc[CB / 64][NBKT];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -2455,27 +2466,25 @@ __global__ void __launch_bounds__(CB) k_cmp_write(const DevPlan *__restrict__ pl
       ord0 += s_pre[b];
     }
   }
-  const uint32_t w = blockIdx.x * CWORDS + threadIdx.x;
-  CmpWord c;
-  c.surv = 0;
-  if (threadIdx.x < CWORDS && w < nwords) cmp_word(pl, ctr, bits, nwords, w, c);
-  uint32_t total;
-  const uint32_t ex = block_exclusive_scan<CB>(__popc(c.surv), tmp, &total);
+  // this block's survivors (its row of counts), staged by k_cmp_count
+  uint32_t total = 0;
+#pragma unroll
+  for (int b = 0; b < NBKT; b++) total += cnt8[(size_t)blockIdx.x * NBKT + b];
   const uint32_t nl = (uint32_t)pl->nlists;
   const int l0 = pl->g0list[0];
   const uint64_t lt = (1ull << lane) - 1;
-  for (uint32_t base = 0; base < total; base += CSV) {
-    cmp_stage(pl, c, w, ex, base, S);
-    __syncthreads();
-    const uint32_t nr = min((uint32_t)CSV, total - base);
-    // in steps of CB survivors, in order: ranks inside each bucket
+  const size_t sb = (size_t)blockIdx.x * CTILE;
+  {
+    const uint32_t base = 0;
+    const uint32_t nr = total;
+    // in steps of CB survivors, in slot order: ranks inside each bucket
     for (uint32_t i0 = 0; i0 < nr; i0 += CB) {
       const uint32_t i = i0 + threadIdx.x;
       const bool act = i < nr;
-      const uint64_t s = act ? S.slot[i] : 0;
-      const uint32_t lm = act ? S.lm[i] : 0;
+      const uint64_t s = act ? st_slot[sb + i] : 0;
+      const uint32_t lm = act ? st_lm[sb + i] : 0;
       const bool own = (lm >> l0) & 1;
-      const uint32_t u = act ? cmp_units(pl, ctr, cunit, loc, s, lm, own) : 0;
+      const uint32_t u = act ? st_u[sb + i] : 0;
       const uint32_t b = (uint32_t)size_bucket(u, rc);
       // the wave's lanes with the same bucket: 4 ballots on its bits; the
       // first of them writes their count
@@ -3197,7 +3206,7 @@ __device__ __forceinline__ void hist_add(uint32_t *h, uint32_t key, int lane) {
   }
 }
 
-// Scored in size-bucket order (k_cmp_write's positions), so a wave's
+// Scored in size-bucket order (k_cmp_place's positions), so a wave's
 // survivors have similar work (its lanes run the scorers in lockstep).
 // Waves of buckets 3-7 score 64 survivors, one per lane, each keeping its
 // records in its lane's column of the wave's LDS record arrays (RC records);
@@ -6971,10 +6980,13 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   // site clustering also records each survivor's slot-order rank (the
   // replay walks the survivors in docid order)
   uint32_t *cnt8 = reinterpret_cast<uint32_t *>(q.blk.as<uint8_t>(align256(sizeof(BlkInfo) * (size_t)cgrid)));
+  // the staged survivors (slot, list mask, units) live in the top-k gather
+  // buffer, which is free until k_topk: 12 bytes a slot
+  uint32_t *stslot = q.gath.as<uint32_t>(), *stlm = stslot + slot_ub, *stu = stlm + slot_ub;
   hipLaunchKernelGGL(k_cmp_count, dim3(cgrid), dim3(CB), 0, st, dpl, dctr, dcunit, bits, nwords, loc, dcand, rcap, blk,
-                     cnt8);
-  hipLaunchKernelGGL(k_cmp_write, dim3(cgrid), dim3(CB), 0, st, dpl, dctr, dcunit, bits, nwords, loc, dcand, rcap, blk,
-                     (const uint32_t *)cnt8, cgrid, svslot, svlm, svu, svdoc, svloc,
+                     cnt8, stslot, stlm, stu);
+  hipLaunchKernelGGL(k_cmp_place, dim3(cgrid), dim3(CB), 0, st, dpl, dctr, dcunit, loc, dcand, rcap, blk,
+                     (const uint32_t *)cnt8, cgrid, stslot, stlm, stu, svslot, svlm, svu, svdoc, svloc,
                      clus ? q.ord.as<uint32_t>() : nullptr);
   const unsigned long long arena_cap = (unsigned long long)(q.scratch.cap / 8);
   if (P.reshare_mask)
