@@ -1840,8 +1840,11 @@ __device__ void probe_by_run(const DevPlan *__restrict__ pl, const ProbeWork &w,
 // barrier).  The direction is per list (the host's choice, DevList::probe).
 // MODE (diagnostic, GBGPU_PROBE_MODE): 0 full, 1 stop after the run-start
 // compaction, 2 load chunks only, 3 skip the run-driven lists.
+#ifndef GBGPU_PROBE_MINB
+#define GBGPU_PROBE_MINB 1
+#endif
 template <int MODE, int G0>
-__global__ void __launch_bounds__(64 * PW, (G0 <= 2 && MODE == 11) ? 3 : 1) k_probe(const DevPlan *__restrict__ pl, const ProbeWork *work, uint32_t nwork,
+__global__ void __launch_bounds__(64 * PW, (G0 <= 2 && MODE == 11) ? 3 : (G0 <= 2 ? GBGPU_PROBE_MINB : 1)) k_probe(const DevPlan *__restrict__ pl, const ProbeWork *work, uint32_t nwork,
                                                    const uint64_t *cand, uint32_t *bits, uint32_t nwords, Loc *loc,
                                                    const Counters *ctr, const uint64_t *dir) {
 #ifdef GBGPU_DIAG
@@ -3467,7 +3470,7 @@ struct ScoreRec {
 // resolves to the previous run).  A miss drops that sublist from the
 // docid's mini merge.  shrinkSubLists (Posdb.cpp:5334-5428) made each
 // sublist the survivors' runs in docid order, in place, so the search is
-// replayed over a directory: survivors sorted by docid (k_si_keys + hipcub),
+// replayed over a directory: survivors sorted by docid (k_si_keys + sisort),
 // and per list the exclusive prefix of their run units (k_si_dir).  Past the
 // shrunk end the in-place buffer still holds the list's own bytes.
 __global__ void k_si_keys(const uint64_t *sv_doc, uint32_t nsurv, uint64_t *key, uint32_t *val) {
