@@ -6011,7 +6011,7 @@ struct FacetAcc {
 struct QuerySlot {
   std::mutex mu;
   hipStream_t stream = nullptr;
-  DevBuf tables, chunkcnt, cand, cunit, bits, loc, svslot, svlm, svu, svdoc, svloc, scratch, skey, sel, gath, res;
+  DevBuf tables, chunkcnt, cand, cunit, bits, loc, svslot, svlm, svu, svdoc, svloc, scratch, skey, sel, gath, res, stg;
   DevBuf dir;           // candidate directories, epoch-tagged (never cleared per query)
   DevBuf split, swin;   // docid splits: one piece's list windows; window table
   DevBuf blk, sflag, ord, oslot, rep, tree;  // site clustering: slot-order ranks and slots, replay entries, TopTree state
@@ -6060,9 +6060,10 @@ struct QuerySlot {
   hipEvent_t ev_done = nullptr;  // the query's device work is done (the exchange waits on it)
   float last_ms[6] = {0, 0, 0, 0, 0, 0};
 
-  DevBuf *const bufs[33] = {&tables, &chunkcnt, &cand, &cunit, &bits, &loc, &svslot, &svlm, &svu, &svdoc,
+  DevBuf *const bufs[34] = {&tables, &chunkcnt, &cand, &cunit, &bits, &loc, &svslot, &svlm, &svu, &svdoc,
                             &svloc, &scratch, &skey, &sel, &gath, &res, &dir, &split, &swin, &blk,
-                            &sflag, &ord, &oslot, &rep, &tree, &white, &wrej, &si, &fac, &svmb, &stale, &si2, &mwsl};
+                            &sflag, &ord, &oslot, &rep, &tree, &white, &wrej, &si, &fac, &svmb, &stale, &si2, &mwsl,
+                            &stg};
   int init(hipMemPool_t pool) {
     if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return GBGPU_EHIP;
     for (auto *b : bufs) {
@@ -6869,6 +6870,7 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   rc2 |= q.blk.ensure(align256(sizeof(BlkInfo) * (size_t)cgrid) + 4 * NBKT * (size_t)cgrid);
   rc2 |= q.sel.ensure(sizeof(Select));
   rc2 |= q.gath.ensure(12 * (slot_ub + MAX_K_BIG) + 1024);
+  rc2 |= q.stg.ensure(12 * slot_ub + 256);
   rc2 |= q.res.ensure(q.res_bytes);
   if (clus) {
     rc2 |= q.sflag.ensure(slot_ub);
@@ -6983,9 +6985,8 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   // site clustering also records each survivor's slot-order rank (the
   // replay walks the survivors in docid order)
   uint32_t *cnt8 = reinterpret_cast<uint32_t *>(q.blk.as<uint8_t>(align256(sizeof(BlkInfo) * (size_t)cgrid)));
-  // the staged survivors (slot, list mask, units) live in the top-k gather
-  // buffer, which is free until k_topk: 12 bytes a slot
-  uint32_t *stslot = q.gath.as<uint32_t>(), *stlm = stslot + slot_ub, *stu = stlm + slot_ub;
+  // the staged survivors (slot, list mask, units): 12 bytes a slot
+  uint32_t *stslot = q.stg.as<uint32_t>(), *stlm = stslot + slot_ub, *stu = stlm + slot_ub;
   hipLaunchKernelGGL(k_cmp_count, dim3(cgrid), dim3(CB), 0, st, dpl, dctr, dcunit, bits, nwords, loc, dcand, rcap, blk,
                      cnt8, stslot, stlm, stu);
   hipLaunchKernelGGL(k_cmp_place, dim3(cgrid), dim3(CB), 0, st, dpl, dctr, dcunit, loc, dcand, rcap, blk,
