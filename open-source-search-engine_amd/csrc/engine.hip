@@ -4204,7 +4204,10 @@ __device__ __forceinline__ uint4 rep_entry(uint32_t key, float B, uint64_t d, bo
 // The slots go to per-lane LDS columns; a survivor with more than BL_SLOTS
 // keys in a group takes the wave's 4096-slot ring (the reference's own
 // buffer) instead.
-constexpr int BL_SLOTS = 32;
+#ifndef GBGPU_BL_SLOTS
+#define GBGPU_BL_SLOTS 32
+#endif
+constexpr int BL_SLOTS = GBGPU_BL_SLOTS;
 // group g's slots into col[0..n) (column layout: entry k of lane at [k][lane]);
 // false on overflow.  first: the head slot of the last present sublist.
 __device__ bool lane_slots(const DevPlan *__restrict__ pl, const Counters *ctr, int g, uint32_t s, uint32_t lm,
