@@ -59,7 +59,10 @@ constexpr int WIN_BYTES = WIN_LO + MCH * 6 + 16; // + 2 units after it
 #define GBGPU_TCAP 512
 #endif
 constexpr int TCAP = GBGPU_TCAP;                 // keys per merge tile
-constexpr int TB = 256;                          // threads per merge-tile block
+#ifndef GBGPU_TB
+#define GBGPU_TB 256
+#endif
+constexpr int TB = GBGPU_TB;                     // threads per merge-tile block
 constexpr int MAXN = 256;                        // runs per merge (oracle MAXL)
 constexpr int SCAN_TPB = MB * 4;                 // tiles per scan block
 
