@@ -20,10 +20,11 @@
 //        g>0 / rmDocIdVotes, Posdb.cpp:5086-5171, 4871-4946.  A hit sets the
 //        list's bit in the candidate's list mask and records (unit, length)
 //        of the docid's run.
-//   k_compact
+//   k_cmp_count, k_cmp_place (+ k_ext_walk)
 //        survivors = candidates whose lists cover every positive group and
 //        no negative one (the final m_docIdVoteBuf), plus the shrunk-sublist
-//        non-empty flags (shrinkSubLists, Posdb.cpp:5334-5428).
+//        non-empty flags (shrinkSubLists, Posdb.cpp:5334-5428), placed by
+//        size bucket for k_score.
 //   k_score<NQ, NS>
 //        one lane per survivor: mini-merge of each group (Posdb.cpp:6559-
 //        6778) into the survivor's arena records, then the scorers of
@@ -2678,7 +2679,7 @@ __constant__ Weights c_weights;
 
 // Per-survivor work, one lane per survivor (Posdb.cpp:6252-7257): for each
 // group, mini-merge (Posdb.cpp:6559-6778) its sublist runs into records in
-// the survivor's arena range (k_compact's prefix sum of its run units), then
+// the survivor's arena range (its run units, handed out from Counters::arena_top), then
 // score_doc (scoring.h) over them.
 constexpr int SCORE_TPB = 64;
 // the two-group variant's LDS records per lane and waves per SIMD it is
@@ -6723,7 +6724,7 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
   P.use_rej = P.use_white;
   for (int a = 0; a < P.g0n; a++)
     if (P.lists[P.g0list[a]].rmode) P.use_rej = 1;
-  if (slot_ub >= (1ull << 28)) return GBGPU_ECAPACITY;  // k_compact's packed bump pointer
+  if (slot_ub >= (1ull << 28)) return GBGPU_ECAPACITY;  // 28-bit slot indices (survivor records, replay entries)
   q.slot_ub = slot_ub;
   // directories: about 8 units (2-4 docids) per bucket, power-of-two count
   uint64_t dir_entries = 0;
