@@ -3830,8 +3830,10 @@ __global__ void k_stale_rank(const uint32_t *order, uint32_t n, uint32_t *rank) 
 
 constexpr uint32_t STALE_SCAN = 1u << 20;  // docids a writer search walks back at most (beyond: EUNSUPPORTED)
 
+// skip (site clustering; null: none): survivors the replay's prefilter
+// skipped, which run no merges and write no mbuf byte (Posdb.cpp:6341-6345)
 __global__ void k_stale_find(Counters *ctr, const uint32_t *stale, const uint32_t *sv_mb, const uint32_t *order,
-                             const uint32_t *rank, uint32_t *wr) {
+                             const uint32_t *rank, uint32_t *wr, const uint8_t *skip) {
   const uint32_t ns = ctr->nstale;
   for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < ns; e += gridDim.x * blockDim.x) {
     const uint32_t si = stale[e] & 0x7fffffffu;
@@ -3847,6 +3849,7 @@ __global__ void k_stale_find(Counters *ctr, const uint32_t *stale, const uint32_
         break;
       }
       const uint32_t w = order[j];
+      if (skip && skip[w]) continue;
       const uint32_t T = sv_mb[w];
       if (T > O + need) {
         const uint32_t upto = min(nb, T - O);
@@ -3914,7 +3917,8 @@ __global__ void __launch_bounds__(SCORE_TPB) k_stale_fix(const DevPlan *__restri
                                                          const uint32_t *wr, const uint32_t *sv_mb, const uint32_t *sv_slot,
                                                          const uint32_t *sv_lm, const uint32_t *sv_u, const uint64_t *sv_doc,
                                                          const Loc *sv_loc, uint64_t *arena, unsigned long long arena_cap,
-                                                         unsigned long long *fixc, uint32_t *skey, uint32_t *okey) {
+                                                         unsigned long long *fixc, uint32_t *skey, uint32_t *okey,
+                                                         uint8_t *sflag) {
   __shared__ float s_sm[npairs<MAXG>() * SCORE_TPB];
   stage_weights(&c_weights);
   const uint32_t e = blockIdx.x * SCORE_TPB + threadIdx.x;
@@ -3932,7 +3936,11 @@ __global__ void __launch_bounds__(SCORE_TPB) k_stale_fix(const DevPlan *__restri
     defined &= (uint32_t)p >= nb || w6[p] != ~0u;
   }
   okey[e] = 0;
-  if (!defined) return;  // bytes no docid of the pass wrote: the docid stays dropped
+  if (sflag) sflag[i] = 0;
+  if (!defined) {  // bytes no docid of the pass wrote: the docid stays dropped
+    skey[i] = 0;
+    return;
+  }
   // room for the largest merge this lane runs (plus the injected record)
   uint32_t need = surv_units(pl, ctr, sv_slot[i], sv_lm[i], sv_u[i]) + 1;
   for (uint32_t p = 0; p < nb; p++) {
@@ -3993,10 +4001,33 @@ __global__ void __launch_bounds__(SCORE_TPB) k_stale_fix(const DevPlan *__restri
     if (filt) {
       key = 0;
       atomicAdd(&fixc[1], 1ull);
+      if (sflag) sflag[i] = 1;  // site clustering: the replay counts it (m_filtered)
     }
   }
   skey[i] = key;
   okey[e] = key;
+}
+
+// site clustering: which survivors the replay's prefilter skipped -- its
+// bound B <= minWinningScore at its turn, the value the last add of an
+// earlier docid assigned (the replay records each assignment with that
+// docid, in docid order; before the first one -1.0, Posdb.cpp:6012)
+__global__ void k_stale_skip(uint32_t nsurv, const uint64_t *sv_doc, const uint32_t *sv_ord, const uint4 *rep_slot,
+                             const uint4 *mwsl, int ints, uint8_t *skip) {
+  const uint32_t nm = mwsl[0].x;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nsurv; i += gridDim.x * blockDim.x) {
+    const uint64_t d = sv_doc[i];
+    const float B = __uint_as_float(rep_slot[sv_ord[i]].y);
+    uint32_t lo = 0, hi = nm;  // assignments from docids below d
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      const uint4 a = mwsl[1 + mid];
+      if ((((uint64_t)a.y << 32) | a.x) < d) lo = mid + 1;
+      else hi = mid;
+    }
+    const float mws = lo ? __uint_as_float(mwsl[lo].z) : -1.0f;
+    skip[i] = (!ints && B <= mws) ? 1 : 0;
+  }
 }
 
 // ------------------------------------------------------- site clustering
@@ -6043,6 +6074,7 @@ struct QuerySlot {
   bool pending = false;
   bool replayed = false;  // site clustering: the pass ran the TopTree replay
   bool seq_replay = false;  // ... as k_tree_seq (a register-tree overflow replays it with k_tree_replay)
+  bool whole_range = false; // ... over the whole docid range in one pass (no docid-split pieces)
   uint64_t slot_ub = 0;
   bool early = false;
   int k = 0;
@@ -7043,7 +7075,8 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
     TreeParams tp = tree_params(q.docs_wanted, tree_phase, q.int_scores);
     if (!q.facets.empty()) tp.mwsl = q.mwsl.as<uint4>();
     q.rep_off = ranked ? slot_ub : 0;
-    q.seq_replay = tree_phase == (TREE_INIT | TREE_FINAL) && kcol > 0 && ctx->replay_mode != 1;
+    q.whole_range = tree_phase == (TREE_INIT | TREE_FINAL);
+    q.seq_replay = q.whole_range && kcol > 0 && ctx->replay_mode != 1;
     if (q.seq_replay) {
       auto ks = q.int_scores ? (kcol == 1 ? k_tree_seq<1, true> : kcol == 4 ? k_tree_seq<4, true>
                                 : kcol == 8 ? k_tree_seq<8, true> : k_tree_seq<16, true>)
@@ -8182,14 +8215,15 @@ static int stale_fix(QuerySlot &q, uint32_t nsurv, uint32_t nstale) {
   const uint32_t gs = std::max(1u, std::min<uint32_t>(1024, (nstale + 255) / 256));
   hipLaunchKernelGGL(k_stale_find, dim3(gs), dim3(256), 0, st, dctr, (const uint32_t *)q.stale.as<uint32_t>(),
                      (const uint32_t *)q.svmb.as<uint32_t>(), (const uint32_t *)q.si.as<uint32_t>(o_ord),
-                     (const uint32_t *)q.si.as<uint32_t>(o_rank), q.si.as<uint32_t>(o_wr));
+                     (const uint32_t *)q.si.as<uint32_t>(o_rank), q.si.as<uint32_t>(o_wr), (const uint8_t *)nullptr);
   hipLaunchKernelGGL(k_stale_fix, dim3((nstale + SCORE_TPB - 1) / SCORE_TPB), dim3(SCORE_TPB), 0, st,
                      q.tables.as<DevPlan>(), dctr, (const uint32_t *)q.stale.as<uint32_t>(),
                      (const uint32_t *)q.si.as<uint32_t>(o_wr), (const uint32_t *)q.svmb.as<uint32_t>(),
                      (const uint32_t *)q.svslot.as<uint32_t>(), (const uint32_t *)q.svlm.as<uint32_t>(),
                      (const uint32_t *)q.svu.as<uint32_t>(), (const uint64_t *)q.svdoc.as<uint64_t>(),
                      (const Loc *)q.svloc.as<Loc>(), q.si.as<uint64_t>(o_arena), fcap,
-                     q.si.as<unsigned long long>(o_fixc), q.skey.as<uint32_t>(), q.si.as<uint32_t>(o_okey));
+                     q.si.as<unsigned long long>(o_fixc), q.skey.as<uint32_t>(), q.si.as<uint32_t>(o_okey),
+                     (uint8_t *)nullptr);
   hipLaunchKernelGGL(k_gather_docs, dim3(gs), dim3(256), 0, st, (const uint64_t *)q.svdoc.as<uint64_t>(),
                      (const uint32_t *)q.stale.as<uint32_t>(), (const Counters *)dctr, q.si.as<uint64_t>(o_sdoc));
   HIPCHECK(hipGetLastError());
@@ -8223,6 +8257,131 @@ static int stale_fix(QuerySlot &q, uint32_t nsurv, uint32_t nstale) {
   HIPCHECK(hipMemcpyAsync(q.res.as<uint8_t>(res_docs_off(q.k)), docs, 8 * (size_t)q.k, hipMemcpyHostToDevice, st));
   HIPCHECK(hipStreamSynchronize(st));
   return 0;
+}
+
+// Site clustering (a whole-range pass through k_tree_seq): the stale
+// survivors' bytes come from the latest earlier docid that the replay's
+// prefilter did not skip, and which docids it skips depends on the tree the
+// stale survivors' own scores feed.  So: score them with the writers of an
+// unskipped pass, replay (recording minWinningScore's assignments), derive
+// the skips, find the writers again among the unskipped docids and score
+// again -- until the scores the replay used are the ones its skips give
+// (usually at once; at most STALE_ROUNDS replays, else EUNSUPPORTED).
+constexpr int STALE_ROUNDS = 4;
+static int stale_fix_clustered(QuerySlot &q, uint32_t nsurv, uint32_t nstale) {
+  if (q.want_info || !q.facets.empty() || !q.whole_range) return GBGPU_EUNSUPPORTED;
+  const Counters *hc = reinterpret_cast<const Counters *>(q.h_res);
+  hipStream_t st = q.stream;
+  const uint64_t slot_ub = q.slot_ub;
+  size_t sort_tmp = 0;
+  HIPCHECK(si_sort_pairs(nullptr, sort_tmp, nullptr, nullptr, nullptr, nullptr, nsurv, st));
+  size_t o = 0;
+  auto take = [&](size_t bytes) {
+    const size_t at = o;
+    o += align256(bytes);
+    return at;
+  };
+  const size_t o_key = take(8 * (size_t)nsurv), o_val = take(4 * (size_t)nsurv), o_skey = take(8 * (size_t)nsurv),
+               o_ord = take(4 * (size_t)nsurv), o_rank = take(4 * (size_t)nsurv), o_wr = take(48 * (size_t)nstale),
+               o_okey = take(4 * (size_t)nstale), o_fixc = take(16), o_skip = take((size_t)nsurv),
+               o_tmp = take(sort_tmp);
+  const unsigned long long usum = hc->surv_top & ((1ull << 36) - 1);
+  const unsigned long long fcap = 2 * usum + 64ull * nsurv + 4096;
+  const size_t o_arena = take(8 * (size_t)fcap);
+  if (q.si.ensure(o) || q.svmb.ensure(4 * (size_t)nsurv) || q.stale.ensure(4 * (size_t)nstale) ||
+      q.mwsl.ensure(16 * (slot_ub + 2)))
+    return ENOMEM;
+  const DevPlan *dpl = q.tables.as<DevPlan>();
+  Counters *dctr = q.res.as<Counters>();
+  const uint32_t g = std::max(1u, std::min<uint32_t>(1024, (nsurv + 255) / 256));
+  // the survivors in docid order, every survivor's mbuf length, the stale list
+  hipLaunchKernelGGL(k_si_keys, dim3(g), dim3(256), 0, st, (const uint64_t *)q.svdoc.as<uint64_t>(), nsurv,
+                     q.si.as<uint64_t>(o_key), q.si.as<uint32_t>(o_val));
+  HIPCHECK(si_sort_pairs(q.si.as<uint8_t>(o_tmp), sort_tmp, q.si.as<uint64_t>(o_key), q.si.as<uint64_t>(o_skey),
+                         q.si.as<uint32_t>(o_val), q.si.as<uint32_t>(o_ord), nsurv, st));
+  hipLaunchKernelGGL(k_stale_rank, dim3(g), dim3(256), 0, st, (const uint32_t *)q.si.as<uint32_t>(o_ord), nsurv,
+                     q.si.as<uint32_t>(o_rank));
+  HIPCHECK(hipMemsetAsync(q.si.as<uint8_t>(o_fixc), 0, 16, st));
+  hipLaunchKernelGGL(k_stale_mb, dim3((nsurv + SCORE_TPB - 1) / SCORE_TPB), dim3(SCORE_TPB), 0, st, dpl, dctr, nsurv,
+                     (const uint32_t *)q.svslot.as<uint32_t>(), (const uint32_t *)q.svlm.as<uint32_t>(),
+                     (const uint32_t *)q.svu.as<uint32_t>(), (const Loc *)q.svloc.as<Loc>(), q.si.as<uint64_t>(o_arena),
+                     fcap, q.si.as<unsigned long long>(o_fixc), q.svmb.as<uint32_t>(), q.stale.as<uint32_t>());
+  // the replay as enqueue() launched it
+  const bool ranked = q.rep_off != 0;
+  uint4 *rep_slot = q.rep.as<uint4>() + q.rep_off;
+  const uint32_t bgrid =
+      (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((slot_ub + 64 * BND_WAVES - 1) / (64 * BND_WAVES), 4096));
+  const int kcol = seq_columns(q.docs_wanted);
+  TreeParams tp = tree_params(q.docs_wanted, TREE_INIT | TREE_FINAL, q.int_scores);
+  tp.mwsl = q.mwsl.as<uint4>();
+  auto ks = q.int_scores ? (kcol == 1 ? k_tree_seq<1, true> : kcol == 4 ? k_tree_seq<4, true>
+                            : kcol == 8 ? k_tree_seq<8, true> : k_tree_seq<16, true>)
+                         : (kcol == 1 ? k_tree_seq<1, false> : kcol == 4 ? k_tree_seq<4, false>
+                            : kcol == 8 ? k_tree_seq<8, false> : k_tree_seq<16, false>);
+  const int k = q.k;
+  uint8_t *skip = q.si.as<uint8_t>(o_skip);
+  const uint32_t gs = std::max(1u, std::min<uint32_t>(1024, (nstale + 255) / 256));
+  std::vector<uint32_t> okey(nstale), prev;
+  for (int round = 0; round <= STALE_ROUNDS; round++) {
+    // the stale survivors' writers (none skipped in the first round) and scores
+    HIPCHECK(hipMemsetAsync(q.si.as<uint8_t>(o_fixc), 0, 16, st));
+    hipLaunchKernelGGL(k_stale_find, dim3(gs), dim3(256), 0, st, dctr, (const uint32_t *)q.stale.as<uint32_t>(),
+                       (const uint32_t *)q.svmb.as<uint32_t>(), (const uint32_t *)q.si.as<uint32_t>(o_ord),
+                       (const uint32_t *)q.si.as<uint32_t>(o_rank), q.si.as<uint32_t>(o_wr),
+                       round ? (const uint8_t *)skip : (const uint8_t *)nullptr);
+    hipLaunchKernelGGL(k_stale_fix, dim3((nstale + SCORE_TPB - 1) / SCORE_TPB), dim3(SCORE_TPB), 0, st, dpl, dctr,
+                       (const uint32_t *)q.stale.as<uint32_t>(), (const uint32_t *)q.si.as<uint32_t>(o_wr),
+                       (const uint32_t *)q.svmb.as<uint32_t>(), (const uint32_t *)q.svslot.as<uint32_t>(),
+                       (const uint32_t *)q.svlm.as<uint32_t>(), (const uint32_t *)q.svu.as<uint32_t>(),
+                       (const uint64_t *)q.svdoc.as<uint64_t>(), (const Loc *)q.svloc.as<Loc>(),
+                       q.si.as<uint64_t>(o_arena), fcap, q.si.as<unsigned long long>(o_fixc), q.skey.as<uint32_t>(),
+                       q.si.as<uint32_t>(o_okey), q.sflag.as<uint8_t>());
+    HIPCHECK(hipGetLastError());
+    uint32_t unsup = 0;
+    HIPCHECK(hipMemcpyAsync(okey.data(), q.si.as<uint8_t>(o_okey), 4 * (size_t)nstale, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipMemcpyAsync(&unsup, &dctr->unsup, 4, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipStreamSynchronize(st));
+    if (unsup) return GBGPU_EUNSUPPORTED;
+    if (round > 0 && okey == prev) {
+      // the replay ran with these scores: its skips give them back
+      HIPCHECK(hipMemcpyAsync(q.h_res, q.res.p, q.res_bytes, hipMemcpyDeviceToHost, st));
+      HIPCHECK(hipStreamSynchronize(st));
+      q.stale_filt = 0;  // the replay counted the paging filter's drops
+      return hc->tree_err ? GBGPU_ECAPACITY : 0;
+    }
+    if (round == STALE_ROUNDS) break;
+    prev = okey;
+    // the replay again with these scores, recording minWinningScore
+    HIPCHECK(hipMemsetAsync(&dctr->tree_err, 0, 4, st));
+    hipLaunchKernelGGL(k_bound, dim3(bgrid), dim3(64 * BND_WAVES), 0, st, dpl, dctr, (const uint32_t *)q.svslot.as<uint32_t>(),
+                       (const uint32_t *)q.svlm.as<uint32_t>(), (const Loc *)q.svloc.as<Loc>(),
+                       (const uint32_t *)q.ord.as<uint32_t>(), (const uint32_t *)q.skey.as<uint32_t>(),
+                       (const uint64_t *)q.svdoc.as<uint64_t>(), (const uint8_t *)q.sflag.as<uint8_t>(), rep_slot,
+                       ranked ? q.oslot.as<uint32_t>() : nullptr);
+    if (ranked) {
+      const uint32_t rgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((slot_ub + 255) / 256, 4096));
+      hipLaunchKernelGGL(k_rank, dim3(rgrid), dim3(256), 0, st, dpl, dctr, (const uint32_t *)q.oslot.as<uint32_t>(),
+                         (const uint4 *)rep_slot, q.rep.as<uint4>());
+    }
+    if (q.seq_replay) {
+      hipLaunchKernelGGL(ks, dim3(1), dim3(64 * SQ_W), 0, st, dctr, (const uint4 *)q.rep.as<uint4>(), tp,
+                         q.res.as<uint32_t>(res_keys_off()), q.res.as<uint64_t>(res_docs_off(k)));
+      TreeParams tf = tp;
+      tf.on_reg_err = 1;
+      hipLaunchKernelGGL(k_tree_replay, dim3(1), dim3(64), 0, st, dctr, (const uint4 *)q.rep.as<uint4>(),
+                         (TreeState *)nullptr, tf, q.res.as<uint32_t>(res_keys_off()),
+                         q.res.as<uint64_t>(res_docs_off(k)));
+    } else {  // the one-wave replay (diagnostic GBGPU_REPLAY_MODE=1, or a tree past the register columns)
+      hipLaunchKernelGGL(k_tree_replay, dim3(1), dim3(64), 0, st, dctr, (const uint4 *)q.rep.as<uint4>(),
+                         (TreeState *)q.tree.p, tp, q.res.as<uint32_t>(res_keys_off()),
+                         q.res.as<uint64_t>(res_docs_off(k)));
+    }
+    hipLaunchKernelGGL(k_stale_skip, dim3(g), dim3(256), 0, st, nsurv, (const uint64_t *)q.svdoc.as<uint64_t>(),
+                       (const uint32_t *)q.ord.as<uint32_t>(), (const uint4 *)rep_slot, (const uint4 *)q.mwsl.as<uint4>(),
+                       q.int_scores ? 1 : 0, skip);
+    HIPCHECK(hipGetLastError());
+  }
+  return GBGPU_EUNSUPPORTED;  // the scores did not settle
 }
 
 // hits_acc: when non-null, the query's intersected docids are appended to it
@@ -8279,8 +8438,10 @@ static int collect(gbgpu_ctx *ctx, QuerySlot &q, gbgpu_result *out, std::vector<
   if (c->unsup) return GBGPU_EUNSUPPORTED;
   if (c->nstale) {
     if (!q.stale_done) {
-      const int rc = stale_fix(q, (uint32_t)out->hits, c->nstale);
+      const int rc = q.replayed ? stale_fix_clustered(q, (uint32_t)out->hits, c->nstale)
+                                : stale_fix(q, (uint32_t)out->hits, c->nstale);
       if (rc) return rc;
+      out->filtered = (int32_t)c->filtered;  // (a clustered replay counted them again)
     }
     out->filtered += q.stale_filt;
   }
@@ -9330,7 +9491,8 @@ static int allgather_admitted(gbgpu_ctx *ctx, QuerySlot *q, int err, int32_t k, 
     if (hipStreamSynchronize(q->stream) != hipSuccess) err = GBGPU_EHIP;
     const Counters *hc = reinterpret_cast<const Counters *>(q->h_res);
     if (!err && hc->nstale && !hc->corrupt && !hc->tree_err && !hc->unsup) {
-      err = stale_fix(*q, (uint32_t)(hc->surv_top >> 36), hc->nstale);
+      err = q->replayed ? stale_fix_clustered(*q, (uint32_t)(hc->surv_top >> 36), hc->nstale)
+                        : stale_fix(*q, (uint32_t)(hc->surv_top >> 36), hc->nstale);
       if (!err) q->stale_done = true;
     }
   }

@@ -705,6 +705,28 @@ def save_stale():
             break
 
 
+def save_stale_clus():
+    """The stale-mbuf case under site clustering (Msg39's default): the
+    writers of a stale docid's bytes are the earlier docids the replay's
+    prefilter did not skip (Posdb.cpp:6341-6345), so the scores feed back
+    into which docids write.  Seeds whose stale docids all have defined
+    bytes; 20 000 docs so the tree fills and minWinningScore moves."""
+    import oracle_binding as orc
+    from test_stale import stale_case
+    for seed in (1, 5, 6):
+        q, ls = stale_case(seed, n=20000)
+        for dtg in (50, 200):
+            q.docs_to_get = dtg
+            p = q.params(site_clustering=1)
+            r = orc.query(q.terms, ls, p, cap=1 << 16)
+            if r["stale"][1] != 0:
+                continue
+            e = save_query(f"stale_clus_s{seed}_d{dtg}", q.terms, ls, p)
+            assert np.array_equal(e["docids"], r["docids"]), seed
+            assert np.array_equal(e["scores"].view(np.uint32), r["scores"].view(np.uint32)), seed
+            print(f"q_stale_clus_s{seed}_d{dtg}: stale docids {r['stale'][0]} hits={e['hits']} n={len(e['docids'])}")
+
+
 def split_runs(lst, nruns, rng, dup_frac=0.08, del_frac=0.04):
     """One termlist's keys spread over nruns runs (oldest first) the way a
     termlist lies in tiered Posdb files plus the tree: each key in one run;
@@ -873,6 +895,7 @@ def main():
     save_capacity()
     save_sublists()
     save_stale()
+    save_stale_clus()
     save_msg5()
     save_msg3a()
     save_msg3a_full()
@@ -887,6 +910,8 @@ def main():
 if __name__ == "__main__":
     if sys.argv[1:] == ["sublists"]:
         save_sublists()
+    elif sys.argv[1:] == ["stale_clus"]:
+        save_stale_clus()
     elif sys.argv[1:] == ["splits"]:
         save_splits()
     elif sys.argv[1:] == ["clustering"]:

@@ -132,7 +132,7 @@ def test_gpu_adapter_score_info_in_reference_msg39(path):
 # ------------------------------------------------ the shard
 # one shard's whole-range pass: a docid-split fixture's hit count is the
 # pieces' sum with their overlap (Msg39.cpp:409-414), the shard's the exact one
-SHARD_CASES = [p for p in QCASES if not os.path.basename(p).startswith(("q_clus", "f_sortbyint_clus"))
+SHARD_CASES = [p for p in QCASES if not os.path.basename(p).startswith(("q_clus", "f_sortbyint_clus", "q_stale_clus"))
                and "splits" not in os.path.basename(p)]
 
 

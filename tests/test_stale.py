@@ -12,8 +12,9 @@ word's list empty, so half the hits are stale docids, each with defined
 bytes) pin the oracle, which keeps a real mbuf over the pass (test_golden.py
 runs them on CPU and GPU); here the GPU (k_stale_find / k_stale_fix after the
 pass) runs against the oracle on seeded corpora, defined and undefined
-bytes alike, with paging and over docid splits, and the modes it does not
-replay decline."""
+bytes alike, with paging and over docid splits, and with site clustering
+(the writers among the docids the replay's prefilter did not skip); the
+modes it does not replay (clustering over docid splits) decline."""
 import numpy as np
 import pytest
 
@@ -73,10 +74,44 @@ def test_gpu_stale_paging_and_splits(engine):
 
 
 @pytest.mark.gpu
-def test_gpu_stale_declines_with_clustering(engine):
+@pytest.mark.parametrize("seed", list(range(1, 9)))
+def test_gpu_stale_with_clustering_vs_oracle(engine, seed):
     """with site clustering the replay's prefilter skips decide which docids
-    write mbuf: not restated, declined"""
+    write mbuf: the stale survivors are scored with the writers among the
+    docids the replay did not skip, and replayed until the scores settle
+    (stale_fix_clustered); the oracle keeps a real mbuf over the sequential
+    pass"""
+    q, lists = stale_case(seed, n=20000)
+    for dtg in (50, 200):
+        q.docs_to_get = dtg
+        p = q.params(site_clustering=1)
+        exp = orc.query(q.terms, lists, p, cap=1 << 16)
+        label = f"seed {seed} docs {dtg} stale {exp['stale']}"
+        r = engine.query(q.terms, lists, p, cap=1 << 16)
+        assert r.hits == exp["hits"], label
+        assert r.filtered == exp["filtered"], label
+        assert np.array_equal(r.docids, exp["docids"]), label
+        assert np.array_equal(r.scores.view(np.uint32), exp["scores"].view(np.uint32)), label
+
+
+@pytest.mark.gpu
+def test_gpu_stale_with_clustering_paging(engine):
+    q, lists = stale_case(3, n=20000)
+    full = orc.query(q.terms, lists, q.params(site_clustering=1), cap=1 << 16)
+    pos = len(full["docids"]) // 2
+    p = q.params(site_clustering=1, max_serp_score=float(full["scores"][pos]), min_serp_docid=int(full["docids"][pos]))
+    exp = orc.query(q.terms, lists, p, cap=1 << 16)
+    r = engine.query(q.terms, lists, p, cap=1 << 16)
+    assert (r.hits, r.filtered) == (exp["hits"], exp["filtered"])
+    assert np.array_equal(r.docids, exp["docids"])
+    assert np.array_equal(r.scores.view(np.uint32), exp["scores"].view(np.uint32))
+
+
+@pytest.mark.gpu
+def test_gpu_stale_declines_with_clustering_over_splits(engine):
+    """docid splits carry the tree between pieces (the one-wave replay): a
+    stale survivor there is still declined"""
     q, lists = stale_case(1, n=20000)
     with pytest.raises(gbgpu.GbgpuError) as ei:
-        engine.query(q.terms, lists, q.params(site_clustering=1), cap=1 << 16)
+        engine.query(q.terms, lists, q.params(site_clustering=1, num_docid_splits=3), cap=1 << 16)
     assert ei.value.code == gbgpu.GBGPU_EUNSUPPORTED
