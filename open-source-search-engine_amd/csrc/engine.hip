@@ -6050,6 +6050,7 @@ struct QuerySlot {
   DevBuf dir;           // candidate directories, epoch-tagged (never cleared per query)
   DevBuf split, swin;   // docid splits: one piece's list windows; window table
   DevBuf blk, sflag, ord, oslot, rep, tree;  // site clustering: slot-order ranks and slots, replay entries, TopTree state
+  DevBuf tree_bak;                          // ... the state before a docid-split piece's replay (stale_fix_clustered)
   DevBuf white, wrej;                       // "&sites=" whitelist: sorted 5-byte values; rejected slots
   DevBuf si;                                // second pass's score info (score_info)
   DevBuf fac;                               // facet tables (facet_pass)
@@ -6075,6 +6076,7 @@ struct QuerySlot {
   bool replayed = false;  // site clustering: the pass ran the TopTree replay
   bool seq_replay = false;  // ... as k_tree_seq (a register-tree overflow replays it with k_tree_replay)
   bool whole_range = false; // ... over the whole docid range in one pass (no docid-split pieces)
+  int tree_phase = 0;       // ... its TREE_* phase (a docid-split piece: not both INIT and FINAL)
   uint64_t slot_ub = 0;
   bool early = false;
   int k = 0;
@@ -6096,10 +6098,10 @@ struct QuerySlot {
   hipEvent_t ev_done = nullptr;  // the query's device work is done (the exchange waits on it)
   float last_ms[6] = {0, 0, 0, 0, 0, 0};
 
-  DevBuf *const bufs[34] = {&tables, &chunkcnt, &cand, &cunit, &bits, &loc, &svslot, &svlm, &svu, &svdoc,
+  DevBuf *const bufs[35] = {&tables, &chunkcnt, &cand, &cunit, &bits, &loc, &svslot, &svlm, &svu, &svdoc,
                             &svloc, &scratch, &skey, &sel, &gath, &res, &dir, &split, &swin, &blk,
                             &sflag, &ord, &oslot, &rep, &tree, &white, &wrej, &si, &fac, &svmb, &stale, &si2, &mwsl,
-                            &stg};
+                            &stg, &tree_bak};
   int init(hipMemPool_t pool) {
     if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return GBGPU_EHIP;
     for (auto *b : bufs) {
@@ -6914,6 +6916,9 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
     rc2 |= q.oslot.ensure(4 * slot_ub);
     rc2 |= q.rep.ensure((P.g0n > 1 ? 32 : 16) * slot_ub);
     if (!(tree_phase & TREE_FINAL)) rc2 |= q.tree.ensure(sizeof(TreeState));
+    // a later docid-split piece keeps the tree it starts from: a stale-mbuf
+    // fix replays the piece again from it (stale_fix_clustered)
+    if (!(tree_phase & TREE_INIT)) rc2 |= q.tree_bak.ensure(sizeof(TreeState));
     if (!q.facets.empty()) rc2 |= q.mwsl.ensure(16 * (slot_ub + 2));
   }
   if (P.use_white) rc2 |= q.white.ensure(8 * std::max<size_t>(1, q.h_white.size()));
@@ -7076,6 +7081,9 @@ static int enqueue_entries(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *term
     if (!q.facets.empty()) tp.mwsl = q.mwsl.as<uint4>();
     q.rep_off = ranked ? slot_ub : 0;
     q.whole_range = tree_phase == (TREE_INIT | TREE_FINAL);
+    q.tree_phase = tree_phase;
+    if (!(tree_phase & TREE_INIT))
+      HIPCHECK(hipMemcpyAsync(q.tree_bak.p, q.tree.p, sizeof(TreeState), hipMemcpyDeviceToDevice, st));
     q.seq_replay = q.whole_range && kcol > 0 && ctx->replay_mode != 1;
     if (q.seq_replay) {
       auto ks = q.int_scores ? (kcol == 1 ? k_tree_seq<1, true> : kcol == 4 ? k_tree_seq<4, true>
@@ -8269,7 +8277,7 @@ static int stale_fix(QuerySlot &q, uint32_t nsurv, uint32_t nstale) {
 // (usually at once; at most STALE_ROUNDS replays, else EUNSUPPORTED).
 constexpr int STALE_ROUNDS = 4;
 static int stale_fix_clustered(QuerySlot &q, uint32_t nsurv, uint32_t nstale) {
-  if (q.want_info || !q.facets.empty() || !q.whole_range) return GBGPU_EUNSUPPORTED;
+  if (q.want_info || !q.facets.empty() || (q.tree_phase & TREE_EMIT)) return GBGPU_EUNSUPPORTED;
   const Counters *hc = reinterpret_cast<const Counters *>(q.h_res);
   hipStream_t st = q.stream;
   const uint64_t slot_ub = q.slot_ub;
@@ -8312,7 +8320,7 @@ static int stale_fix_clustered(QuerySlot &q, uint32_t nsurv, uint32_t nstale) {
   const uint32_t bgrid =
       (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((slot_ub + 64 * BND_WAVES - 1) / (64 * BND_WAVES), 4096));
   const int kcol = seq_columns(q.docs_wanted);
-  TreeParams tp = tree_params(q.docs_wanted, TREE_INIT | TREE_FINAL, q.int_scores);
+  TreeParams tp = tree_params(q.docs_wanted, q.tree_phase, q.int_scores);
   tp.mwsl = q.mwsl.as<uint4>();
   auto ks = q.int_scores ? (kcol == 1 ? k_tree_seq<1, true> : kcol == 4 ? k_tree_seq<4, true>
                             : kcol == 8 ? k_tree_seq<8, true> : k_tree_seq<16, true>)
@@ -8371,10 +8379,15 @@ static int stale_fix_clustered(QuerySlot &q, uint32_t nsurv, uint32_t nstale) {
       hipLaunchKernelGGL(k_tree_replay, dim3(1), dim3(64), 0, st, dctr, (const uint4 *)q.rep.as<uint4>(),
                          (TreeState *)nullptr, tf, q.res.as<uint32_t>(res_keys_off()),
                          q.res.as<uint64_t>(res_docs_off(k)));
-    } else {  // the one-wave replay (diagnostic GBGPU_REPLAY_MODE=1, or a tree past the register columns)
+    } else {
+      // the one-wave replay: a docid-split piece (from the tree the piece
+      // started with), a tree past the register columns, or the diagnostic
+      // GBGPU_REPLAY_MODE=1
+      if (!(q.tree_phase & TREE_INIT))
+        HIPCHECK(hipMemcpyAsync(q.tree.p, q.tree_bak.p, sizeof(TreeState), hipMemcpyDeviceToDevice, st));
       hipLaunchKernelGGL(k_tree_replay, dim3(1), dim3(64), 0, st, dctr, (const uint4 *)q.rep.as<uint4>(),
-                         (TreeState *)q.tree.p, tp, q.res.as<uint32_t>(res_keys_off()),
-                         q.res.as<uint64_t>(res_docs_off(k)));
+                         (q.tree_phase & TREE_FINAL) ? (TreeState *)q.tree.p : q.tree.as<TreeState>(), tp,
+                         q.res.as<uint32_t>(res_keys_off()), q.res.as<uint64_t>(res_docs_off(k)));
     }
     hipLaunchKernelGGL(k_stale_skip, dim3(g), dim3(256), 0, st, nsurv, (const uint64_t *)q.svdoc.as<uint64_t>(),
                        (const uint32_t *)q.ord.as<uint32_t>(), (const uint4 *)rep_slot, (const uint4 *)q.mwsl.as<uint4>(),

@@ -13,8 +13,8 @@ bytes) pin the oracle, which keeps a real mbuf over the pass (test_golden.py
 runs them on CPU and GPU); here the GPU (k_stale_find / k_stale_fix after the
 pass) runs against the oracle on seeded corpora, defined and undefined
 bytes alike, with paging and over docid splits, and with site clustering
-(the writers among the docids the replay's prefilter did not skip); the
-modes it does not replay (clustering over docid splits) decline."""
+(the writers among the docids the replay's prefilter did not skip), over
+docid splits too."""
 import numpy as np
 import pytest
 
@@ -108,10 +108,18 @@ def test_gpu_stale_with_clustering_paging(engine):
 
 
 @pytest.mark.gpu
-def test_gpu_stale_declines_with_clustering_over_splits(engine):
-    """docid splits carry the tree between pieces (the one-wave replay): a
-    stale survivor there is still declined"""
-    q, lists = stale_case(1, n=20000)
-    with pytest.raises(gbgpu.GbgpuError) as ei:
-        engine.query(q.terms, lists, q.params(site_clustering=1, num_docid_splits=3), cap=1 << 16)
-    assert ei.value.code == gbgpu.GBGPU_EUNSUPPORTED
+@pytest.mark.parametrize("seed", [1, 3, 6])
+def test_gpu_stale_with_clustering_over_splits(engine, seed):
+    """Msg39's default request: site clustering over docid splits, the tree
+    carried between the pieces; each piece's mbuf is its own call's, and a
+    stale fix replays the piece again from the tree it started with"""
+    q, lists = stale_case(seed, n=20000)
+    for dtg in (50, 200):
+        q.docs_to_get = dtg
+        p = q.params(site_clustering=1, num_docid_splits=3)
+        exp = orc.query(q.terms, lists, p, cap=1 << 16)
+        label = f"seed {seed} docs {dtg} stale {exp['stale']}"
+        r = engine.query(q.terms, lists, p, cap=1 << 16)
+        assert (r.hits, r.filtered) == (exp["hits"], exp["filtered"]), label
+        assert np.array_equal(r.docids, exp["docids"]), label
+        assert np.array_equal(r.scores.view(np.uint32), exp["scores"].view(np.uint32)), label
