@@ -302,6 +302,40 @@ __global__ void k_reset(uint32_t *a, uint32_t na, uint32_t *b, uint32_t nb, uint
   }
 }
 
+// A termlist cut from a resident file (gbgpu_file_list): the swapped list
+// image, its first 12 bytes the map key's (k0..k2, half bit set), then the
+// file's bytes [src, src + n).  One dword a lane, lanes on consecutive dwords;
+// src is 2-byte aligned (file offsets and key sizes are even), so an odd
+// half-dword source is two dword loads joined.  One launch writes the whole
+// image, the map key included (no host-to-device copy per cut).
+__global__ void __launch_bounds__(256) k_cut_copy(const uint8_t *__restrict__ file, uint64_t fsize, uint64_t src,
+                                                  uint64_t n, uint32_t k0, uint32_t k1, uint32_t k2,
+                                                  uint32_t *__restrict__ dst) {
+  const uint64_t len = 12 + n;  // image bytes; the dwords past it are the zeroed pad
+  const uint64_t nd = (len + 3) / 4;
+  const uint32_t *fw = reinterpret_cast<const uint32_t *>(file);
+  const uint64_t fmax = (fsize + 3) / 4 - 1;  // the last file dword
+  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nd; j += (uint64_t)gridDim.x * blockDim.x) {
+    uint32_t v;
+    if (j < 3) {
+      v = j == 0 ? k0 : j == 1 ? k1 : k2;
+    } else {
+      const uint64_t fb = src + 4 * j - 12;  // the file byte at image byte 4j
+      const uint64_t a = fb >> 2;
+      const uint32_t lo = fw[min(a, fmax)];
+      if (fb & 2) {
+        const uint32_t hi = fw[min(a + 1, fmax)];
+        v = (lo >> 16) | (hi << 16);
+      } else {
+        v = lo;
+      }
+      const uint64_t left = len - 4 * j;  // image bytes in this dword (the last one may hold fewer)
+      if (left < 4) v &= (1u << (8 * left)) - 1;
+    }
+    dst[j] = v;
+  }
+}
+
 // ----------------------------------------------- candidate extraction (G0)
 // The page map, RdbMap's role (RdbMap.h:48: a list's pages and where each
 // begins) for the GPU: per CHUNK_UNITS-unit page of a swapped list, the run
@@ -5830,6 +5864,28 @@ struct DevBuf {
   size_t cap = 0;
   hipStream_t st = nullptr;
   hipMemPool_t pool = nullptr;  // the context's own pool (stream-ordered buffers); null: hipMalloc
+  // GBGPU_CANARY=1 (debug): a guard of CANARY bytes of 0xA5 after every
+  // stream-ordered buffer, checked by canary_ok (collect reports a buffer
+  // whose guard a kernel overwrote)
+  static constexpr size_t CANARY = 1 << 20;
+  static int canary_level() {
+    static const int lv = [] {
+      const char *s = std::getenv("GBGPU_CANARY");
+      return s ? std::atoi(s) : 0;
+    }();
+    return lv;
+  }
+  static bool canary_on() { return canary_level() != 0; }
+  bool canary_ok() const {
+    if (!p || !st || !canary_on()) return true;
+    std::vector<uint8_t> h(CANARY);
+    if (hipMemcpyAsync(h.data(), static_cast<uint8_t *>(p) + cap, CANARY, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+      return false;
+    for (uint8_t b : h)
+      if (b != 0xA5) return false;
+    return true;
+  }
   int ensure(size_t bytes) {
     if (bytes <= cap) return 0;
     const size_t want = std::max<size_t>(bytes + bytes / 4, 1 << 16);
@@ -5837,7 +5893,9 @@ struct DevBuf {
       if (p) (void)hipFreeAsync(p, st);
       p = nullptr;
       cap = 0;
-      if (pool_alloc(&p, want, pool, st)) return ENOMEM;
+      const size_t guard = canary_on() ? CANARY : 0;
+      if (pool_alloc(&p, want + guard, pool, st)) return ENOMEM;
+      if (guard) (void)hipMemsetAsync(static_cast<uint8_t *>(p) + want, 0xA5, guard, st);
     } else {
       if (p) (void)hipFree(p);
       p = nullptr;
@@ -5872,23 +5930,132 @@ struct DevBuf {
     cap = 0;
   }
 };
-// GBGPU_LIST_MALLOC (A/B knob): resident lists from hipMalloc instead of the
-// context's stream-ordered pool
-#ifndef GBGPU_LIST_MALLOC
-#define GBGPU_LIST_MALLOC 0
-#endif
 // GBGPU_DEFAULT_POOL (A/B knob): the device's default pool instead of the
 // context's own
 #ifndef GBGPU_DEFAULT_POOL
 #define GBGPU_DEFAULT_POOL 0
 #endif
+
+// Resident lists and file images live in a context-owned arena of hipMalloc'd
+// chunks, carved first-fit on the host.  They came from the stream-ordered
+// pool until round 6, where a list freed and re-cut at once (the file-read
+// path) was sometimes scanned from stale bytes: the granule table its upload
+// read back differed run to run while the image itself compared equal
+// afterwards, and the queries over it went astray (wrong top docids, 1-9 s
+// probes; scripts/r06_fqbug.py).  hipMalloc'd lists never showed it; the
+// arena keeps that memory and reuses it with no allocator call per list.
+// A list's memory returns to the arena when its last reference goes: every
+// query that read it has been collected (synchronised) by then, and the
+// upload stream's own work on it is ordered before the next cut.
+struct ListArena {
+  static constexpr size_t ALIGN = 256;
+  static constexpr size_t CHUNK = 1ull << 30;  // the smallest chunk a growth maps
+  struct Chunk {
+    uint8_t *base = nullptr;
+    size_t size = 0, used = 0;
+    std::map<size_t, size_t> free_;  // offset -> bytes, coalesced
+  };
+  std::mutex mu;
+  std::vector<Chunk> chunks;
+  int device = 0;
+  uint8_t *alloc(size_t bytes) {
+    bytes = (std::max<size_t>(bytes, 1) + ALIGN - 1) / ALIGN * ALIGN;
+    std::lock_guard<std::mutex> g(mu);
+    for (auto &c : chunks)
+      for (auto it = c.free_.begin(); it != c.free_.end(); ++it)
+        if (it->second >= bytes) {
+          const size_t off = it->first, len = it->second;
+          c.free_.erase(it);
+          if (len > bytes) c.free_[off + bytes] = len - bytes;
+          c.used += bytes;
+          return c.base + off;
+        }
+    Chunk c;
+    c.size = std::max(bytes, CHUNK);
+    (void)hipSetDevice(device);
+    if (hipMalloc(reinterpret_cast<void **>(&c.base), c.size) != hipSuccess) {
+      (void)hipGetLastError();
+      // no room for a new chunk: the wholly free ones go back first
+      trim_locked(0);
+      if (hipMalloc(reinterpret_cast<void **>(&c.base), c.size) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+      }
+    }
+    if (c.size > bytes) c.free_[bytes] = c.size - bytes;
+    c.used = bytes;
+    chunks.push_back(std::move(c));
+    return chunks.back().base;
+  }
+  void free(uint8_t *p, size_t bytes) {
+    bytes = (std::max<size_t>(bytes, 1) + ALIGN - 1) / ALIGN * ALIGN;
+    std::lock_guard<std::mutex> g(mu);
+    for (auto &c : chunks) {
+      if (p < c.base || p >= c.base + c.size) continue;
+      size_t off = (size_t)(p - c.base), len = bytes;
+      auto nx = c.free_.lower_bound(off);
+      if (nx != c.free_.end() && nx->first == off + len) {
+        len += nx->second;
+        nx = c.free_.erase(nx);
+      }
+      if (nx != c.free_.begin()) {
+        auto pv = std::prev(nx);
+        if (pv->first + pv->second == off) {
+          off = pv->first;
+          len += pv->second;
+          c.free_.erase(pv);
+        }
+      }
+      c.free_[off] = len;
+      c.used -= bytes;
+      return;
+    }
+  }
+  // wholly free chunks beyond `keep` bytes of them go back to the device
+  void trim_locked(size_t keep) {
+    size_t kept = 0;
+    for (size_t i = 0; i < chunks.size();) {
+      Chunk &c = chunks[i];
+      if (c.used == 0 && kept + c.size > keep) {
+        (void)hipFree(c.base);
+        chunks.erase(chunks.begin() + (long)i);
+        continue;
+      }
+      if (c.used == 0) kept += c.size;
+      i++;
+    }
+  }
+  void trim(size_t keep) {
+    std::lock_guard<std::mutex> g(mu);
+    trim_locked(keep);
+  }
+  ~ListArena() {
+    for (auto &c : chunks) (void)hipFree(c.base);
+  }
+};
+
 struct ListMem {
   uint8_t *d = nullptr;
-  hipStream_t st = nullptr;
-  bool malloced = false;
+  size_t bytes = 0;
+  std::shared_ptr<ListArena> arena;  // owner of d
+  size_t dbg_len = 0;     // GBGPU_CANARY: bytes hashed (image, pad, page map)
+  uint64_t dbg_hash = 0;  // and their hash when the list was finished
+  uint64_t hash(hipStream_t s) const {
+    std::vector<uint64_t> h((dbg_len + 7) / 8, 0);
+    if (hipMemcpyAsync(h.data(), d, dbg_len, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+      return 0;
+    uint64_t x = 1469598103934665603ull;
+    for (uint64_t v : h) x = (x ^ v) * 1099511628211ull;
+    return x;
+  }
+  int alloc(const std::shared_ptr<ListArena> &a, size_t n) {
+    arena = a;
+    bytes = n;
+    d = a->alloc(n);
+    return d ? 0 : ENOMEM;
+  }
   ~ListMem() {
-    if (d && malloced) (void)hipFree(d);
-    else if (d) (void)hipFreeAsync(d, st);
+    if (d && arena) arena->free(d, bytes);
   }
 };
 
@@ -6050,7 +6217,6 @@ struct QuerySlot {
   DevBuf dir;           // candidate directories, epoch-tagged (never cleared per query)
   DevBuf split, swin;   // docid splits: one piece's list windows; window table
   DevBuf blk, sflag, ord, oslot, rep, tree;  // site clustering: slot-order ranks and slots, replay entries, TopTree state
-  DevBuf tree_bak;                          // ... the state before a docid-split piece's replay (stale_fix_clustered)
   DevBuf white, wrej;                       // "&sites=" whitelist: sorted 5-byte values; rejected slots
   DevBuf si;                                // second pass's score info (score_info)
   DevBuf fac;                               // facet tables (facet_pass)
@@ -6076,7 +6242,6 @@ struct QuerySlot {
   bool replayed = false;  // site clustering: the pass ran the TopTree replay
   bool seq_replay = false;  // ... as k_tree_seq (a register-tree overflow replays it with k_tree_replay)
   bool whole_range = false; // ... over the whole docid range in one pass (no docid-split pieces)
-  int tree_phase = 0;       // ... its TREE_* phase (a docid-split piece: not both INIT and FINAL)
   uint64_t slot_ub = 0;
   bool early = false;
   int k = 0;
@@ -6098,6 +6263,10 @@ struct QuerySlot {
   hipEvent_t ev_done = nullptr;  // the query's device work is done (the exchange waits on it)
   float last_ms[6] = {0, 0, 0, 0, 0, 0};
 
+  // site clustering over docid splits: the tree a piece started from
+  // (stale_fix_clustered replays the piece from it), the piece's TREE_* phase
+  DevBuf tree_bak;
+  int tree_phase = 0;
   DevBuf *const bufs[35] = {&tables, &chunkcnt, &cand, &cunit, &bits, &loc, &svslot, &svlm, &svu, &svdoc,
                             &svloc, &scratch, &skey, &sel, &gath, &res, &dir, &split, &swin, &blk,
                             &sflag, &ord, &oslot, &rep, &tree, &white, &wrej, &si, &fac, &svmb, &stale, &si2, &mwsl,
@@ -6222,6 +6391,26 @@ struct gbgpu_ctx {
   DevBuf xscratch;
   uint8_t *h_xf = nullptr;
   size_t h_xf_cap = 0;
+  // a list upload's readbacks (granule table, pages' last docids, header):
+  // pinned, grown between uploads (under lists_mu)
+  uint8_t *h_lst = nullptr;
+  size_t h_lst_cap = 0;
+  DevBuf lscan;                              // and their device side (k_list_scan's outputs)
+  DevBuf min_runs, mout;                     // gbgpu_termlist_merge's runs and merged list
+  std::shared_ptr<ListArena> arena = std::make_shared<ListArena>();  // lists and file images
+  int ensure_h_lst(size_t bytes) {
+    if (bytes <= h_lst_cap) return 0;
+    if (h_lst) (void)hipHostFree(h_lst);
+    h_lst = nullptr;
+    h_lst_cap = 0;
+    const size_t want = std::max<size_t>(bytes + bytes / 4, 1 << 16);
+    if (hipHostMalloc(reinterpret_cast<void **>(&h_lst), want) != hipSuccess) {
+      h_lst = nullptr;
+      return ENOMEM;
+    }
+    h_lst_cap = want;
+    return 0;
+  }
   int ensure_h_xf(size_t bytes) {
     if (bytes <= h_xf_cap) return 0;
     if (h_xf) (void)hipHostFree(h_xf);
@@ -6266,17 +6455,7 @@ static int alloc_list(gbgpu_ctx *ctx, int64_t size, ListEntry &e) {
   const size_t lbytes = align256((size_t)(size ? size - 6 : 0) + LIST_PAD);
   const size_t alloc = lbytes + page_map_bytes(e.units);
   e.mem = std::make_shared<ListMem>();
-  e.mem->st = ctx->upload_stream;
-  if (GBGPU_LIST_MALLOC) {
-    if (hipMalloc(reinterpret_cast<void **>(&e.mem->d), alloc) != hipSuccess) {
-      (void)hipGetLastError();
-      e.mem->d = nullptr;
-      return ENOMEM;
-    }
-    e.mem->malloced = true;
-  } else if (DevBuf::pool_alloc(reinterpret_cast<void **>(&e.mem->d), alloc, ctx->pool, ctx->upload_stream)) {
-    return ENOMEM;
-  }
+  if (e.mem->alloc(ctx->arena, alloc)) return ENOMEM;
   e.d = e.mem->d;
   e.pm = reinterpret_cast<uint32_t *>(e.d + lbytes);
   // the image's own bytes are written next: zero the pad and the page map
@@ -6322,11 +6501,8 @@ static int finish_list(gbgpu_ctx *ctx, ListEntry &e, const uint8_t *host_bytes, 
     const uint32_t np = (e.units + CHUNK_UNITS - 1) / CHUNK_UNITS;
     const uint32_t ngran = np * 4;
     gf.resize(ngran);
-    // stream-ordered from the context's pool (a hipMalloc / hipFree pair a
-    // cut synchronised the whole device, every query in flight included)
-    DevBuf dgf;
-    dgf.st = ctx->upload_stream;
-    dgf.pool = ctx->pool;
+    // the context's scan buffer, grown between uploads (under lists_mu)
+    DevBuf &dgf = ctx->lscan;
     const size_t o_last = align256(8 * (size_t)ngran), o_hdr = o_last + align256(8 * (size_t)np);
     if (dgf.ensure(o_hdr + sizeof(ListHdr))) return ENOMEM;
     ListHdr *dh = reinterpret_cast<ListHdr *>(dgf.as<uint8_t>(o_hdr));
@@ -6339,12 +6515,16 @@ static int finish_list(gbgpu_ctx *ctx, ListEntry &e, const uint8_t *host_bytes, 
       le = hipGetLastError();
     }
     ListHdr hh;
-    if (le == hipSuccess) le = hipMemcpyAsync(gf.data(), dgf.p, 8 * (size_t)ngran, hipMemcpyDeviceToHost, ctx->upload_stream);
-    if (le == hipSuccess)
-      le = hipMemcpyAsync(lastd.data(), dgf.as<uint8_t>(o_last), 8 * (size_t)np, hipMemcpyDeviceToHost, ctx->upload_stream);
-    if (le == hipSuccess) le = hipMemcpyAsync(&hh, dh, sizeof hh, hipMemcpyDeviceToHost, ctx->upload_stream);
+    // one readback through the pinned stage
+    const size_t need = o_hdr + sizeof(ListHdr);
+    if (le == hipSuccess && ctx->ensure_h_lst(need)) le = hipErrorOutOfMemory;
+    if (le == hipSuccess) le = hipMemcpyAsync(ctx->h_lst, dgf.p, need, hipMemcpyDeviceToHost, ctx->upload_stream);
     const hipError_t se = hipStreamSynchronize(ctx->upload_stream);
-    dgf.release();
+    if (le == hipSuccess && se == hipSuccess) {
+      std::memcpy(gf.data(), ctx->h_lst, 8 * (size_t)ngran);
+      std::memcpy(lastd.data(), ctx->h_lst + o_last, 8 * (size_t)np);
+      std::memcpy(&hh, ctx->h_lst + o_hdr, sizeof hh);
+    }
     HIPCHECK(le);
     HIPCHECK(se);
     if (hh.bad) return GBGPU_ECORRUPT;  // e.mem frees the copy
@@ -6364,6 +6544,17 @@ static int finish_list(gbgpu_ctx *ctx, ListEntry &e, const uint8_t *host_bytes, 
     (void)host_bytes;
   }
   if (size) e.gfirst = std::make_shared<const std::vector<uint64_t>>(std::move(gf));
+  if (DevBuf::canary_level() == 5 && size) {
+    uint64_t x = 1469598103934665603ull;
+    for (uint64_t v : *e.gfirst) x = (x ^ v) * 1099511628211ull;
+    std::fprintf(stderr, "gbgpu: list %p size %lld units %u dmin %llu dmax %llu gf %zu %016llx\n", (void *)e.d,
+                 (long long)size, e.units, (unsigned long long)e.dmin, (unsigned long long)e.dmax, e.gfirst->size(),
+                 (unsigned long long)x);
+  }
+  if ((DevBuf::canary_level() == 1 || DevBuf::canary_level() == 2) && size) {
+    e.mem->dbg_len = (size_t)(reinterpret_cast<uint8_t *>(e.pm) - e.d) + page_map_bytes(e.units);
+    e.mem->dbg_hash = e.mem->hash(ctx->upload_stream);
+  }
   e.live = true;
   for (size_t i = 0; i < ctx->lists.size(); i++) {
     if (!ctx->lists[i].live) {
@@ -6413,7 +6604,16 @@ static int enqueue(gbgpu_ctx *ctx, QuerySlot &q, const gbgpu_qterm *terms, int n
   // held before anything is launched: a failed enqueue may have launched
   // kernels that read the lists; the next collect on this slot drains them
   for (auto &e : ents)
-    if (e.mem) q.held.push_back(e.mem);
+    if (e.mem) {
+      q.held.push_back(e.mem);
+      if (DevBuf::canary_level() == 3) {
+        std::vector<uint8_t> one(64);
+        (void)hipMemcpyAsync(one.data(), e.mem->d, 64, hipMemcpyDeviceToHost, q.stream);
+        (void)hipStreamSynchronize(q.stream);
+      }
+      if (e.mem->dbg_len && e.mem->hash(q.stream) != e.mem->dbg_hash)
+        std::fprintf(stderr, "gbgpu: canary: list %p changed before enqueue\n", (void *)e.mem->d);
+    }
   return enqueue_entries(ctx, q, terms, nterms, ents.data(), p, 0);
 }
 
@@ -8425,6 +8625,14 @@ static int collect(gbgpu_ctx *ctx, QuerySlot &q, gbgpu_result *out, std::vector<
     std::fprintf(stderr, "gbgpu: query stream failed: %s\n", hipGetErrorString(se));
     return GBGPU_EHIP;
   }
+  if (DevBuf::canary_on())
+    for (size_t i = 0; i < sizeof q.bufs / sizeof q.bufs[0]; i++)
+      if (!q.bufs[i]->canary_ok())
+        std::fprintf(stderr, "gbgpu: canary: slot buffer #%zu (cap %zu) overrun\n", i, q.bufs[i]->cap);
+  if (DevBuf::canary_on())
+    for (auto &m : held)
+      if (m->dbg_len && m->hash(q.stream) != m->dbg_hash)
+        std::fprintf(stderr, "gbgpu: canary: list %p changed during the query\n", (void *)m->d);
   if (ctx->profiling) {
     float t;
     (void)hipEventElapsedTime(&t, q.ev[0], q.ev[6]);
@@ -8909,14 +9117,26 @@ int gbgpu_open(int device, gbgpu_ctx **out) {
     }
     uint64_t keep = POOL_KEEP;
     (void)hipMemPoolSetAttribute(ctx->pool, hipMemPoolAttrReleaseThreshold, &keep);
+    if (const char *s = std::getenv("GBGPU_POOL_STRICT"); s && *s == '1') {
+      // A/B: memory a stream freed is reused by that stream only
+      int off = 0;
+      (void)hipMemPoolSetAttribute(ctx->pool, hipMemPoolReuseAllowOpportunistic, &off);
+      (void)hipMemPoolSetAttribute(ctx->pool, hipMemPoolReuseAllowInternalDependencies, &off);
+      (void)hipMemPoolSetAttribute(ctx->pool, hipMemPoolReuseFollowEventDependencies, &off);
+    }
   }
   Weights w = host_weights();
+  ctx->arena->device = device;
   if (hipStreamCreateWithFlags(&ctx->upload_stream, hipStreamNonBlocking) != hipSuccess ||
       hipMalloc((void **)&ctx->d_flag, 4) != hipSuccess ||
       hipHostMalloc((void **)&ctx->h_flag, 4) != hipSuccess ||
       hipMemcpyToSymbol(HIP_SYMBOL(c_weights), &w, sizeof w) != hipSuccess || grow_slots(ctx, 1) != 0) {
     gbgpu_close(ctx);
     return GBGPU_EHIP;
+  }
+  for (DevBuf *b : {&ctx->lscan, &ctx->min_runs, &ctx->mout}) {
+    b->st = ctx->upload_stream;
+    b->pool = ctx->pool;
   }
 #ifdef GBGPU_DIAG
   // diagnostic builds only (make diag: lib/libgbgpu_diag.so); the release
@@ -8950,8 +9170,12 @@ void gbgpu_close(gbgpu_ctx *ctx) {
   ctx->xrecv.release();
   ctx->xout.release();
   ctx->xscratch.release();
+  ctx->lscan.release();
+  ctx->min_runs.release();
+  ctx->mout.release();
   if (ctx->h_xout) (void)hipHostFree(ctx->h_xout);
   if (ctx->h_xf) (void)hipHostFree(ctx->h_xf);
+  if (ctx->h_lst) (void)hipHostFree(ctx->h_lst);
   ctx->lists.clear();  // the last references: ListMem frees the device copies
   ctx->files.clear();
   if (ctx->upload_stream) (void)hipStreamSynchronize(ctx->upload_stream);
@@ -8998,6 +9222,7 @@ int32_t gbgpu_tree_capacity(const gbgpu_params *p, const int64_t *sizes, int nte
 // slots' cached buffers up to POOL_KEEP stay
 static void pool_trim(gbgpu_ctx *ctx) {
   if (ctx->pool) (void)hipMemPoolTrimTo(ctx->pool, POOL_KEEP);
+  ctx->arena->trim(POOL_KEEP);
 }
 
 int gbgpu_list_upload(gbgpu_ctx *ctx, const uint8_t *bytes, int64_t size, int32_t *handle) {
@@ -9014,10 +9239,7 @@ int gbgpu_file_upload(gbgpu_ctx *ctx, const uint8_t *bytes, int64_t size, int32_
   FileEntry f;
   f.size = size;
   f.mem = std::make_shared<ListMem>();
-  f.mem->st = ctx->upload_stream;
-  if (DevBuf::pool_alloc(reinterpret_cast<void **>(&f.mem->d), std::max<size_t>((size_t)size, 256), ctx->pool,
-                         ctx->upload_stream))
-    return ENOMEM;
+  if (f.mem->alloc(ctx->arena, std::max<size_t>((size_t)size, 256))) return ENOMEM;
   if (size) HIPCHECK(hipMemcpyAsync(f.mem->d, bytes, (size_t)size, hipMemcpyHostToDevice, ctx->upload_stream));
   HIPCHECK(hipStreamSynchronize(ctx->upload_stream));
   f.live = true;
@@ -9089,10 +9311,28 @@ int gbgpu_file_list(gbgpu_ctx *ctx, int32_t fh, int64_t offset, int64_t size, co
   uint8_t first[12];
   std::memcpy(first, full, 12);
   first[0] |= 0x02;
-  HIPCHECK(hipMemcpyAsync(e.d, first, 12, hipMemcpyHostToDevice, ctx->upload_stream));
-  if (size > ks)
-    HIPCHECK(hipMemcpyAsync(e.d + 12, src + ks, (size_t)(size - ks), hipMemcpyDeviceToDevice, ctx->upload_stream));
-  return finish_list(ctx, e, nullptr, full, handle);
+  {
+    uint32_t k[3];
+    std::memcpy(k, first, 12);
+    const uint64_t n = (uint64_t)(size - ks), nd = (12 + n + 3) / 4;
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((nd + 255) / 256, 8192);
+    hipLaunchKernelGGL(k_cut_copy, dim3(grid), dim3(256), 0, ctx->upload_stream, f.mem->d, (uint64_t)f.size,
+                       (uint64_t)(offset + ks), n, k[0], k[1], k[2], reinterpret_cast<uint32_t *>(e.d));
+    HIPCHECK(hipGetLastError());
+  }
+  const int frc = finish_list(ctx, e, nullptr, full, handle);
+  if (!frc && DevBuf::canary_level() == 1 && size > ks) {
+    std::vector<uint8_t> a((size_t)(size - ks)), b((size_t)(size - ks));
+    HIPCHECK(hipMemcpy(a.data(), e.d + 12, a.size(), hipMemcpyDeviceToHost));
+    HIPCHECK(hipMemcpy(b.data(), src + ks, b.size(), hipMemcpyDeviceToHost));
+    if (a != b) {
+      size_t i = 0;
+      while (a[i] == b[i]) i++;
+      std::fprintf(stderr, "gbgpu: canary: cut %lld+%lld differs from the file at byte %zu\n", (long long)offset,
+                   (long long)size, i);
+    }
+  }
+  return frc;
 }
 
 static gbmerge::MergeState *merge_state(gbgpu_ctx *ctx);
@@ -9159,13 +9399,8 @@ int gbgpu_termlist_merge(gbgpu_ctx *ctx, const gbgpu_piece *pieces, int n, int r
     in_bytes += (int64_t)align256((size_t)rsz[i] + 16);
   }
   if (total == 0) return upload_list(ctx, nullptr, 0, handle);
-  DevBuf in, out;
-  in.st = out.st = ctx->upload_stream;
-  in.pool = out.pool = ctx->pool;
-  struct Rel {  // stream-ordered frees on every return path
-    DevBuf &b;
-    ~Rel() { b.release(); }
-  } rel_in{in}, rel_out{out};
+  // the context's merge buffers, grown between calls (under lists_mu)
+  DevBuf &in = ctx->min_runs, &out = ctx->mout;
   if (in.ensure((size_t)in_bytes + 256) || out.ensure((size_t)total + 256)) return ENOMEM;
   std::vector<const uint8_t *> ptrs(n);
   for (int i = 0; i < n; i++) {
@@ -9210,7 +9445,6 @@ int gbgpu_termlist_merge(gbgpu_ctx *ctx, const gbgpu_piece *pieces, int n, int r
   if (osz > 18)
     HIPCHECK(hipMemcpyAsync(e.d + 12, out.as<uint8_t>(18), (size_t)(osz - 18), hipMemcpyDeviceToDevice,
                             ctx->upload_stream));
-  // the merge buffers are freed stream-ordered on the upload stream, after the copies
   return finish_list(ctx, e, nullptr, first, handle);
 }
 

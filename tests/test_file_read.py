@@ -138,6 +138,50 @@ def test_gpu_file_pieces_match_host_upload(engine, path, kind):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("slots", [1, 3])
+def test_gpu_recut_lists_answer_as_resident(engine, slots):
+    """Termlists cut, queried, freed and cut again from one resident file, as
+    the read path serves query after query (bench.py's file_read leg): every
+    answer equals the same lists' uploaded once.  The big list re-cut into
+    the memory its predecessor just left was scanned from stale bytes while
+    lists came from the stream-ordered pool (round 6: wrong top docids and
+    second-long probes in 1-in-2 queries at config 2's 180 MB list)."""
+    from workload import config_two_term, generate
+    n = 30_000_000
+    q = config_two_term(n, docs_to_get=100, seed=7)
+    lists = generate(q, n, doc_begin=0, doc_end=n, threads=8)
+    p = q.params()
+    hs = [engine.upload(x) for x in lists]
+    blob, offs = _file(lists)
+    fh = engine.file_upload(blob)
+    del blob
+    engine.set_slots(max(slots, engine.slots()))
+    live = {}
+    try:
+        ref = engine.query_resident(q.terms, hs, p)
+        for i in range(12 + slots):
+            sl = i % slots
+            if sl in live:
+                r = engine.collect(cap=4096, slot=sl)
+                for h in live.pop(sl):
+                    engine.free(h)
+                assert r.hits == ref.hits and np.array_equal(r.docids, ref.docids), i
+                assert np.array_equal(r.scores.view(np.uint32), ref.scores.view(np.uint32)), i
+            if i < 12:
+                fl = [engine.file_list(fh, o, len(x)) for o, x in zip(offs, lists)]
+                engine.enqueue(q.terms, fl, p, slot=sl)
+                live[sl] = fl
+    finally:
+        for sl, fl in live.items():
+            engine.collect(cap=4096, slot=sl)
+            for h in fl:
+                engine.free(h)
+        for h in hs:
+            engine.free(h)
+        engine.file_free(fh)
+
+
+@pytest.mark.gpu
 def test_gpu_file_list_refusals(engine):
     import gbgpu
     terms, lists, params, exp = load_query(FIX[0])
