@@ -302,40 +302,6 @@ __global__ void k_reset(uint32_t *a, uint32_t na, uint32_t *b, uint32_t nb, uint
   }
 }
 
-// A termlist cut from a resident file (gbgpu_file_list): the swapped list
-// image, its first 12 bytes the map key's (k0..k2, half bit set), then the
-// file's bytes [src, src + n).  One dword a lane, lanes on consecutive dwords;
-// src is 2-byte aligned (file offsets and key sizes are even), so an odd
-// half-dword source is two dword loads joined.  One launch writes the whole
-// image, the map key included (no host-to-device copy per cut).
-__global__ void __launch_bounds__(256) k_cut_copy(const uint8_t *__restrict__ file, uint64_t fsize, uint64_t src,
-                                                  uint64_t n, uint32_t k0, uint32_t k1, uint32_t k2,
-                                                  uint32_t *__restrict__ dst) {
-  const uint64_t len = 12 + n;  // image bytes; the dwords past it are the zeroed pad
-  const uint64_t nd = (len + 3) / 4;
-  const uint32_t *fw = reinterpret_cast<const uint32_t *>(file);
-  const uint64_t fmax = (fsize + 3) / 4 - 1;  // the last file dword
-  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nd; j += (uint64_t)gridDim.x * blockDim.x) {
-    uint32_t v;
-    if (j < 3) {
-      v = j == 0 ? k0 : j == 1 ? k1 : k2;
-    } else {
-      const uint64_t fb = src + 4 * j - 12;  // the file byte at image byte 4j
-      const uint64_t a = fb >> 2;
-      const uint32_t lo = fw[min(a, fmax)];
-      if (fb & 2) {
-        const uint32_t hi = fw[min(a + 1, fmax)];
-        v = (lo >> 16) | (hi << 16);
-      } else {
-        v = lo;
-      }
-      const uint64_t left = len - 4 * j;  // image bytes in this dword (the last one may hold fewer)
-      if (left < 4) v &= (1u << (8 * left)) - 1;
-    }
-    dst[j] = v;
-  }
-}
-
 // ----------------------------------------------- candidate extraction (G0)
 // The page map, RdbMap's role (RdbMap.h:48: a list's pages and where each
 // begins) for the GPU: per CHUNK_UNITS-unit page of a swapped list, the run
@@ -6087,16 +6053,56 @@ struct ListHdr {
   unsigned long long dmax;  // unused (the pages' last docids carry it)
 };
 static_assert(CHUNK_UNITS == 4 * WCH_UNITS, "four granules a page");
+// A termlist cut from a resident file (gbgpu_file_list): the swapped list
+// image is the map key's first 12 bytes (k, half bit set), then the file's
+// bytes [src, src + n).  src is 2-byte aligned (file offsets and key sizes
+// are even), so an odd half-dword source is two dword loads joined.
+struct CutSrc {
+  const uint8_t *file;
+  uint64_t fsize, src, n;
+  uint32_t k[3];
+  uint32_t *dst;  // the list image
+};
+__device__ __forceinline__ uint32_t cut_dword(const CutSrc &c, uint64_t j) {
+  const uint64_t len = 12 + c.n;
+  if (4 * j >= len) return 0;  // the zeroed pad
+  if (j < 3) return c.k[j];
+  const uint32_t *fw = reinterpret_cast<const uint32_t *>(c.file);
+  const uint64_t fmax = (c.fsize + 3) / 4 - 1;
+  const uint64_t fb = c.src + 4 * j - 12, a = fb >> 2;
+  uint32_t v = fw[min(a, fmax)];
+  if (fb & 2) v = (v >> 16) | (fw[min(a + 1, fmax)] << 16);
+  const uint64_t left = len - 4 * j;
+  if (left < 4) v &= (1u << (8 * left)) - 1;
+  return v;
+}
+
+// CUT: the block builds its page from the file instead of reading the list
+// (the dwords staged in LDS and its own page's written to the list image),
+// so a cut is one pass over its bytes
+template <bool CUT>
 __global__ void __launch_bounds__(BLOCK) k_list_scan(const uint8_t *__restrict__ list, uint32_t units,
                                                      uint32_t *__restrict__ pm, uint64_t *__restrict__ gf,
-                                                     uint64_t *__restrict__ lastd, ListHdr *hdr) {
+                                                     uint64_t *__restrict__ lastd, ListHdr *hdr, CutSrc cut) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[CHUNK_LOAD];
   __shared__ uint32_t tmp[BLOCK / 64];
   __shared__ uint32_t s_first[4], s_last;
   const uint32_t u0 = blockIdx.x * (uint32_t)CHUNK_UNITS;
   if (threadIdx.x < 4) s_first[threadIdx.x] = ~0u;
   if (threadIdx.x == 0) s_last = 0;
-  load_chunk(list, u0, lds);
+  if constexpr (CUT) {
+    static_assert(CHUNK_BYTES % 4 == 0 && CHUNK_LOAD % 4 == 0, "whole dwords a page");
+    const uint64_t j0 = (uint64_t)u0 * 6 / 4;
+    uint32_t *ld = reinterpret_cast<uint32_t *>(lds);
+    uint32_t *img = cut.dst;
+    for (int i = threadIdx.x; i < CHUNK_LOAD / 4; i += BLOCK) {
+      const uint32_t v = cut_dword(cut, j0 + i);
+      ld[i] = v;
+      if (i < CHUNK_BYTES / 4) img[j0 + i] = v;
+    }
+  } else {
+    load_chunk(list, u0, lds);
+  }
   __syncthreads();
   // the thread's units' bytes 0-1 from three 16-B LDS reads (as thread_starts)
   // and the next thread's first unit's from one aligned word: byte reads at
@@ -6465,7 +6471,7 @@ static int alloc_list(gbgpu_ctx *ctx, int64_t size, ListEntry &e) {
 }
 
 static int finish_list(gbgpu_ctx *ctx, ListEntry &e, const uint8_t *host_bytes, const uint8_t *first18,
-                       int32_t *handle);
+                       int32_t *handle, const CutSrc *cut = nullptr);
 
 static int upload_list(gbgpu_ctx *ctx, const uint8_t *bytes, int64_t size, int32_t *handle) {
   ListEntry e;
@@ -6491,7 +6497,7 @@ static int upload_list(gbgpu_ctx *ctx, const uint8_t *bytes, int64_t size, int32
 // host bytes when the caller has them, else from the device image's last
 // granule that holds a run start.
 static int finish_list(gbgpu_ctx *ctx, ListEntry &e, const uint8_t *host_bytes, const uint8_t *first18,
-                       int32_t *handle) {
+                       int32_t *handle, const CutSrc *cut) {
   const int64_t size = e.size;
   std::vector<uint64_t> gf;
   if (size) {
@@ -6509,8 +6515,12 @@ static int finish_list(gbgpu_ctx *ctx, ListEntry &e, const uint8_t *host_bytes, 
     std::vector<uint64_t> lastd(np);
     hipError_t le = hipMemsetAsync(dh, 0, sizeof(ListHdr), ctx->upload_stream);
     if (le == hipSuccess) {
-      hipLaunchKernelGGL(k_list_scan, dim3(np), dim3(BLOCK), 0, ctx->upload_stream, e.d, e.units, e.pm,
-                         dgf.as<uint64_t>(), dgf.as<uint64_t>(o_last), dh);
+      if (cut)
+        hipLaunchKernelGGL(k_list_scan<true>, dim3(np), dim3(BLOCK), 0, ctx->upload_stream, e.d, e.units, e.pm,
+                           dgf.as<uint64_t>(), dgf.as<uint64_t>(o_last), dh, *cut);
+      else
+        hipLaunchKernelGGL(k_list_scan<false>, dim3(np), dim3(BLOCK), 0, ctx->upload_stream, e.d, e.units, e.pm,
+                           dgf.as<uint64_t>(), dgf.as<uint64_t>(o_last), dh, CutSrc{});
       hipLaunchKernelGGL(k_list_tail, dim3(1), dim3(1024), 0, ctx->upload_stream, np, e.pm);
       le = hipGetLastError();
     }
@@ -9311,16 +9321,15 @@ int gbgpu_file_list(gbgpu_ctx *ctx, int32_t fh, int64_t offset, int64_t size, co
   uint8_t first[12];
   std::memcpy(first, full, 12);
   first[0] |= 0x02;
-  {
-    uint32_t k[3];
-    std::memcpy(k, first, 12);
-    const uint64_t n = (uint64_t)(size - ks), nd = (12 + n + 3) / 4;
-    const uint32_t grid = (uint32_t)std::min<uint64_t>((nd + 255) / 256, 8192);
-    hipLaunchKernelGGL(k_cut_copy, dim3(grid), dim3(256), 0, ctx->upload_stream, f.mem->d, (uint64_t)f.size,
-                       (uint64_t)(offset + ks), n, k[0], k[1], k[2], reinterpret_cast<uint32_t *>(e.d));
-    HIPCHECK(hipGetLastError());
-  }
-  const int frc = finish_list(ctx, e, nullptr, full, handle);
+  // the image is built by the list scan itself (k_list_scan<true>): one pass
+  CutSrc cs;
+  cs.file = f.mem->d;
+  cs.fsize = (uint64_t)f.size;
+  cs.src = (uint64_t)(offset + ks);
+  cs.n = (uint64_t)(size - ks);
+  std::memcpy(cs.k, first, 12);
+  cs.dst = reinterpret_cast<uint32_t *>(e.d);
+  const int frc = finish_list(ctx, e, nullptr, full, handle, &cs);
   if (!frc && DevBuf::canary_level() == 1 && size > ks) {
     std::vector<uint8_t> a((size_t)(size - ks)), b((size_t)(size - ks));
     HIPCHECK(hipMemcpy(a.data(), e.d + 12, a.size(), hipMemcpyDeviceToHost));
