@@ -620,7 +620,7 @@ def main():
         for it in range(n_fr + 2):
             if it == 2:
                 t_fr = time.perf_counter()
-            fl = [eng.file_list(fh, o, len(x)) for o, x in zip(offs, first_lists)]
+            fl = eng.file_lists(fh, offs, [len(x) for x in first_lists])  # the query's reads together
             r_fr = eng.query_resident(qs[0].terms, fl, ps[0])
             for h in fl:
                 eng.free(h)
@@ -643,7 +643,7 @@ def main():
                 if r_fq.hits != r0.hits or not np.array_equal(r_fq.docids, r0.docids):
                     raise RuntimeError("file-cut query differs from the host-buffer query")
             if i < n_fq + w_fq:
-                fl = [eng.file_list(fh, o, len(x)) for o, x in zip(offs, first_lists)]
+                fl = eng.file_lists(fh, offs, [len(x) for x in first_lists])
                 eng.enqueue(qs[0].terms, fl, ps[0], slot=sl)
                 live[sl] = fl
         el_fq = time.perf_counter() - t_fq
@@ -652,8 +652,8 @@ def main():
             "queries_per_sec": round(n_fr / el_fr, 3),
             "keys_scanned_GBps": round(qbytes[0] * n_fr / el_fr / 1e9, 3),
             "in_flight": {"queries": fs, "queries_per_sec": round(n_fq / el_fq, 3)},
-            "note": "termlists cut per query from a resident Posdb file image (gbgpu_file_list: device copy, "
-                    "one structure/page-map/granule pass), queried, freed; one query at a time, and with "
+            "note": "termlists cut per query from a resident Posdb file image (gbgpu_file_lists: the query's "
+                    "cuts together, each image built by its structure/page-map/granule pass), queried, freed; one query at a time, and with "
                     "`in_flight.queries` queries in flight; not `value`",
         }
         # Msg5's read of a termlist (f3, gbgpu_termlist_merge): three resident

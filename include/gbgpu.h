@@ -307,6 +307,13 @@ int gbgpu_list_free(gbgpu_ctx *ctx, int32_t handle);
 int gbgpu_file_upload(gbgpu_ctx *ctx, const uint8_t *bytes, int64_t size, int32_t *file);
 int gbgpu_file_list(gbgpu_ctx *ctx, int32_t file, int64_t offset, int64_t size, const uint8_t *key18,
                     int32_t *handle);
+/* The termlists of one query cut together (Msg2 hands Msg3 all of a query's
+ * reads at once): n cuts as gbgpu_file_list's, key18s NULL or n entries each
+ * NULL or a map key; one device round trip for the heads and one for the
+ * checks whatever n is.  All or nothing: on an error no handle is created and
+ * handles[] holds -1. */
+int gbgpu_file_lists(gbgpu_ctx *ctx, int32_t file, int n, const int64_t *offsets, const int64_t *sizes,
+                     const uint8_t *const *key18s, int32_t *handles);
 int gbgpu_file_free(gbgpu_ctx *ctx, int32_t file);
 
 /* Msg5's read of one termlist (Msg5.cpp:1415-1471 prepare, 1621-1795

@@ -6496,72 +6496,46 @@ static int upload_list(gbgpu_ctx *ctx, const uint8_t *bytes, int64_t size, int32
 // structure check, page map, granule table; then the docid range, from the
 // host bytes when the caller has them, else from the device image's last
 // granule that holds a run start.
-static int finish_list(gbgpu_ctx *ctx, ListEntry &e, const uint8_t *host_bytes, const uint8_t *first18,
-                       int32_t *handle, const CutSrc *cut) {
-  const int64_t size = e.size;
-  std::vector<uint64_t> gf;
-  if (size) {
-    // one pass over the bytes (k_list_scan), the page scan (k_list_tail),
-    // then ONE synchronisation for the check, the granule table and the last
-    // run docid
-    const uint32_t np = (e.units + CHUNK_UNITS - 1) / CHUNK_UNITS;
-    const uint32_t ngran = np * 4;
-    gf.resize(ngran);
-    // the context's scan buffer, grown between uploads (under lists_mu)
-    DevBuf &dgf = ctx->lscan;
-    const size_t o_last = align256(8 * (size_t)ngran), o_hdr = o_last + align256(8 * (size_t)np);
-    if (dgf.ensure(o_hdr + sizeof(ListHdr))) return ENOMEM;
-    ListHdr *dh = reinterpret_cast<ListHdr *>(dgf.as<uint8_t>(o_hdr));
-    std::vector<uint64_t> lastd(np);
-    hipError_t le = hipMemsetAsync(dh, 0, sizeof(ListHdr), ctx->upload_stream);
-    if (le == hipSuccess) {
-      if (cut)
-        hipLaunchKernelGGL(k_list_scan<true>, dim3(np), dim3(BLOCK), 0, ctx->upload_stream, e.d, e.units, e.pm,
-                           dgf.as<uint64_t>(), dgf.as<uint64_t>(o_last), dh, *cut);
-      else
-        hipLaunchKernelGGL(k_list_scan<false>, dim3(np), dim3(BLOCK), 0, ctx->upload_stream, e.d, e.units, e.pm,
-                           dgf.as<uint64_t>(), dgf.as<uint64_t>(o_last), dh, CutSrc{});
-      hipLaunchKernelGGL(k_list_tail, dim3(1), dim3(1024), 0, ctx->upload_stream, np, e.pm);
-      le = hipGetLastError();
+// the scan's outputs read back (granule table, pages' last docids, header)
+// into the entry: the structure check, the granule table, dmin / dmax
+static int scan_result(ListEntry &e, const uint8_t *h_gf, const uint8_t *h_last, const uint8_t *h_hdr, uint32_t np,
+                       const uint8_t *first18) {
+  ListHdr hh;
+  std::memcpy(&hh, h_hdr, sizeof hh);
+  if (hh.bad) return GBGPU_ECORRUPT;  // e.mem frees the copy
+  const size_t ngran = (size_t)np * 4;
+  std::vector<uint64_t> gf(ngran);
+  std::memcpy(gf.data(), h_gf, 8 * ngran);
+  // a granule with no run start after it in its page takes the next
+  // page's first (docids ascend; ~0: none); granules past the list's units
+  // (the last page's tail) hold ~0
+  for (size_t g = ngran - 1; g-- > 0;)
+    if (gf[g] == ~0ull) gf[g] = gf[g + 1];
+  gf.resize((e.units + WCH_UNITS - 1) / WCH_UNITS);
+  e.dmin = host_docid(first18);  // the first key (the list starts with a run)
+  e.dmax = 0;
+  for (size_t pg = np; pg-- > 0;) {
+    uint64_t d;
+    std::memcpy(&d, h_last + 8 * pg, 8);
+    if (d != ~0ull) {
+      e.dmax = d;
+      break;
     }
-    ListHdr hh;
-    // one readback through the pinned stage
-    const size_t need = o_hdr + sizeof(ListHdr);
-    if (le == hipSuccess && ctx->ensure_h_lst(need)) le = hipErrorOutOfMemory;
-    if (le == hipSuccess) le = hipMemcpyAsync(ctx->h_lst, dgf.p, need, hipMemcpyDeviceToHost, ctx->upload_stream);
-    const hipError_t se = hipStreamSynchronize(ctx->upload_stream);
-    if (le == hipSuccess && se == hipSuccess) {
-      std::memcpy(gf.data(), ctx->h_lst, 8 * (size_t)ngran);
-      std::memcpy(lastd.data(), ctx->h_lst + o_last, 8 * (size_t)np);
-      std::memcpy(&hh, ctx->h_lst + o_hdr, sizeof hh);
-    }
-    HIPCHECK(le);
-    HIPCHECK(se);
-    if (hh.bad) return GBGPU_ECORRUPT;  // e.mem frees the copy
-    // a granule with no run start after it in its page takes the next
-    // page's first (docids ascend; ~0: none); granules past the list's units
-    // (the last page's tail) hold ~0
-    for (size_t g = ngran - 1; g-- > 0;)
-      if (gf[g] == ~0ull) gf[g] = gf[g + 1];
-    gf.resize((e.units + WCH_UNITS - 1) / WCH_UNITS);
-    e.dmin = host_docid(first18);  // the first key (the list starts with a run)
-    e.dmax = 0;
-    for (size_t pg = np; pg-- > 0;)
-      if (lastd[pg] != ~0ull) {
-        e.dmax = lastd[pg];
-        break;
-      }
-    (void)host_bytes;
   }
-  if (size) e.gfirst = std::make_shared<const std::vector<uint64_t>>(std::move(gf));
-  if (DevBuf::canary_level() == 5 && size) {
+  e.gfirst = std::make_shared<const std::vector<uint64_t>>(std::move(gf));
+  return 0;
+}
+
+// a checked list into the context's table
+static int register_list(gbgpu_ctx *ctx, ListEntry &e, int32_t *handle) {
+  if (DevBuf::canary_level() == 5 && e.size) {
     uint64_t x = 1469598103934665603ull;
     for (uint64_t v : *e.gfirst) x = (x ^ v) * 1099511628211ull;
     std::fprintf(stderr, "gbgpu: list %p size %lld units %u dmin %llu dmax %llu gf %zu %016llx\n", (void *)e.d,
-                 (long long)size, e.units, (unsigned long long)e.dmin, (unsigned long long)e.dmax, e.gfirst->size(),
+                 (long long)e.size, e.units, (unsigned long long)e.dmin, (unsigned long long)e.dmax, e.gfirst->size(),
                  (unsigned long long)x);
   }
-  if ((DevBuf::canary_level() == 1 || DevBuf::canary_level() == 2) && size) {
+  if ((DevBuf::canary_level() == 1 || DevBuf::canary_level() == 2) && e.size) {
     e.mem->dbg_len = (size_t)(reinterpret_cast<uint8_t *>(e.pm) - e.d) + page_map_bytes(e.units);
     e.mem->dbg_hash = e.mem->hash(ctx->upload_stream);
   }
@@ -6576,6 +6550,37 @@ static int finish_list(gbgpu_ctx *ctx, ListEntry &e, const uint8_t *host_bytes, 
   ctx->lists.push_back(e);
   *handle = (int32_t)ctx->lists.size() - 1;
   return 0;
+}
+
+static int finish_list(gbgpu_ctx *ctx, ListEntry &e, const uint8_t *host_bytes, const uint8_t *first18,
+                       int32_t *handle, const CutSrc *cut) {
+  (void)host_bytes;
+  if (e.size) {
+    // one pass over the bytes (k_list_scan), the page scan (k_list_tail),
+    // then ONE synchronisation for the check, the granule table and the last
+    // run docid, read back through the pinned stage
+    const uint32_t np = (e.units + CHUNK_UNITS - 1) / CHUNK_UNITS;
+    const uint32_t ngran = np * 4;
+    DevBuf &dgf = ctx->lscan;  // the context's scan buffer, grown between uploads (under lists_mu)
+    const size_t o_last = align256(8 * (size_t)ngran), o_hdr = o_last + align256(8 * (size_t)np);
+    const size_t need = o_hdr + sizeof(ListHdr);
+    if (dgf.ensure(need) || ctx->ensure_h_lst(need)) return ENOMEM;
+    ListHdr *dh = reinterpret_cast<ListHdr *>(dgf.as<uint8_t>(o_hdr));
+    HIPCHECK(hipMemsetAsync(dh, 0, sizeof(ListHdr), ctx->upload_stream));
+    if (cut)
+      hipLaunchKernelGGL(k_list_scan<true>, dim3(np), dim3(BLOCK), 0, ctx->upload_stream, e.d, e.units, e.pm,
+                         dgf.as<uint64_t>(), dgf.as<uint64_t>(o_last), dh, *cut);
+    else
+      hipLaunchKernelGGL(k_list_scan<false>, dim3(np), dim3(BLOCK), 0, ctx->upload_stream, e.d, e.units, e.pm,
+                         dgf.as<uint64_t>(), dgf.as<uint64_t>(o_last), dh, CutSrc{});
+    hipLaunchKernelGGL(k_list_tail, dim3(1), dim3(1024), 0, ctx->upload_stream, np, e.pm);
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipMemcpyAsync(ctx->h_lst, dgf.p, need, hipMemcpyDeviceToHost, ctx->upload_stream));
+    HIPCHECK(hipStreamSynchronize(ctx->upload_stream));
+    const int rc = scan_result(e, ctx->h_lst, ctx->h_lst + o_last, ctx->h_lst + o_hdr, np, first18);
+    if (rc) return rc;
+  }
+  return register_list(ctx, e, handle);
 }
 
 // Validates a request and copies the list-table entries it names (the table
@@ -9284,64 +9289,134 @@ int gbgpu_file_free(gbgpu_ctx *ctx, int32_t fh) {
 // offset+size) of a resident file; a compressed first key (12 or 6 bytes) is
 // replaced by the full key the caller's RdbMap gives for it (m_startKey), then
 // the first-key swap of Posdb.cpp:5671-5703; the image goes through the same
-// checks as gbgpu_list_upload.
-int gbgpu_file_list(gbgpu_ctx *ctx, int32_t fh, int64_t offset, int64_t size, const uint8_t *key18,
-                    int32_t *handle) {
-  if (!ctx || !handle || offset < 0 || size < 0) return EINVAL;
+// checks as gbgpu_list_upload.  A query's termlists are cut together (Msg2
+// asks Msg3 for all of them at once): one round trip for the cuts' heads, one
+// for their scans' outputs, whatever their number.
+int gbgpu_file_lists(gbgpu_ctx *ctx, int32_t fh, int n, const int64_t *offsets, const int64_t *sizes,
+                     const uint8_t *const *key18s, int32_t *handles) {
+  if (!ctx || !handles || n < 0 || (n && (!offsets || !sizes)) || n > 4096) return EINVAL;
+  for (int i = 0; i < n; i++) handles[i] = -1;
   std::lock_guard<std::mutex> g(ctx->lists_mu);
   (void)hipSetDevice(ctx->device);
   if (fh < 0 || fh >= (int32_t)ctx->files.size() || !ctx->files[fh].live) return EINVAL;
   const FileEntry &f = ctx->files[fh];
-  if (offset > f.size || size > f.size - offset || offset % 6 || size % 6) return EINVAL;
-  if (!size) return upload_list(ctx, nullptr, 0, handle);
-  const uint8_t *src = f.mem->d + offset;
-  uint8_t head[18] = {};
-  HIPCHECK(hipMemcpyAsync(head, src, (size_t)std::min<int64_t>(18, size), hipMemcpyDeviceToHost, ctx->upload_stream));
+  for (int i = 0; i < n; i++)
+    if (offsets[i] < 0 || sizes[i] < 0 || offsets[i] > f.size || sizes[i] > f.size - offsets[i] || offsets[i] % 6 ||
+        sizes[i] % 6)
+      return EINVAL;
+  struct Cut {
+    int ks = 18;
+    uint8_t full[18];
+    ListEntry e;
+    CutSrc cs;
+    uint32_t np = 0, ngran = 0;
+    size_t o = 0, o_last = 0, o_hdr = 0;
+  };
+  std::vector<Cut> cut((size_t)n);
+  // the heads, one round trip
+  if (n && ctx->ensure_h_lst(32 * (size_t)n)) return ENOMEM;
+  for (int i = 0; i < n; i++)
+    if (sizes[i])
+      HIPCHECK(hipMemcpyAsync(ctx->h_lst + 32 * (size_t)i, f.mem->d + offsets[i], (size_t)std::min<int64_t>(18, sizes[i]),
+                              hipMemcpyDeviceToHost, ctx->upload_stream));
   HIPCHECK(hipStreamSynchronize(ctx->upload_stream));
-  if (!(head[1] & 0x02)) return GBGPU_ECORRUPT;  // not a key start (Posdb.cpp:410-412)
-  const int ks = (head[0] & 0x04) ? 6 : (head[0] & 0x02) ? 12 : 18;
-  if (size < ks) return GBGPU_ECORRUPT;
-  uint8_t full[18];
-  if (key18) {
-    // the map's key must be this key: its stored bytes, compression bits aside
-    std::memcpy(full, key18, 18);
-    if (full[0] & 0x06) return EINVAL;
-    uint8_t a[18], b[18];
-    std::memcpy(a, head, ks);
-    std::memcpy(b, full, ks);
-    a[0] &= 0xf9;
-    if (std::memcmp(a, b, ks)) return EINVAL;
-  } else {
-    if (ks != 18) return EINVAL;  // a compressed first key needs the map's key
-    std::memcpy(full, head, 18);
-  }
-  ListEntry e;
-  int rc = alloc_list(ctx, size - ks + 18, e);
-  if (rc) return rc;
-  uint8_t first[12];
-  std::memcpy(first, full, 12);
-  first[0] |= 0x02;
-  // the image is built by the list scan itself (k_list_scan<true>): one pass
-  CutSrc cs;
-  cs.file = f.mem->d;
-  cs.fsize = (uint64_t)f.size;
-  cs.src = (uint64_t)(offset + ks);
-  cs.n = (uint64_t)(size - ks);
-  std::memcpy(cs.k, first, 12);
-  cs.dst = reinterpret_cast<uint32_t *>(e.d);
-  const int frc = finish_list(ctx, e, nullptr, full, handle, &cs);
-  if (!frc && DevBuf::canary_level() == 1 && size > ks) {
-    std::vector<uint8_t> a((size_t)(size - ks)), b((size_t)(size - ks));
-    HIPCHECK(hipMemcpy(a.data(), e.d + 12, a.size(), hipMemcpyDeviceToHost));
-    HIPCHECK(hipMemcpy(b.data(), src + ks, b.size(), hipMemcpyDeviceToHost));
-    if (a != b) {
-      size_t i = 0;
-      while (a[i] == b[i]) i++;
-      std::fprintf(stderr, "gbgpu: canary: cut %lld+%lld differs from the file at byte %zu\n", (long long)offset,
-                   (long long)size, i);
+  for (int i = 0; i < n; i++) {
+    if (!sizes[i]) continue;
+    const uint8_t *head = ctx->h_lst + 32 * (size_t)i;
+    if (!(head[1] & 0x02)) return GBGPU_ECORRUPT;  // not a key start (Posdb.cpp:410-412)
+    Cut &c = cut[(size_t)i];
+    c.ks = (head[0] & 0x04) ? 6 : (head[0] & 0x02) ? 12 : 18;
+    if (sizes[i] < c.ks) return GBGPU_ECORRUPT;
+    const uint8_t *key18 = key18s ? key18s[i] : nullptr;
+    if (key18) {
+      // the map's key must be this key: its stored bytes, compression bits aside
+      std::memcpy(c.full, key18, 18);
+      if (c.full[0] & 0x06) return EINVAL;
+      uint8_t a[18], b[18];
+      std::memcpy(a, head, c.ks);
+      std::memcpy(b, c.full, c.ks);
+      a[0] &= 0xf9;
+      if (std::memcmp(a, b, c.ks)) return EINVAL;
+    } else {
+      if (c.ks != 18) return EINVAL;  // a compressed first key needs the map's key
+      std::memcpy(c.full, head, 18);
     }
   }
-  return frc;
+  // the images and their scans (k_list_scan<true> builds each image as it
+  // scans it: one pass), the outputs side by side in the context's buffer
+  size_t total = 0;
+  for (int i = 0; i < n; i++) {
+    if (!sizes[i]) continue;
+    Cut &c = cut[(size_t)i];
+    int rc = alloc_list(ctx, sizes[i] - c.ks + 18, c.e);
+    if (rc) return rc;  // the cuts' entries free their images
+    c.np = (c.e.units + CHUNK_UNITS - 1) / CHUNK_UNITS;
+    c.ngran = c.np * 4;
+    c.o = total;
+    c.o_last = c.o + align256(8 * (size_t)c.ngran);
+    c.o_hdr = c.o_last + align256(8 * (size_t)c.np);
+    total = c.o_hdr + align256(sizeof(ListHdr));
+    uint8_t first[12];
+    std::memcpy(first, c.full, 12);
+    first[0] |= 0x02;
+    c.cs.file = f.mem->d;
+    c.cs.fsize = (uint64_t)f.size;
+    c.cs.src = (uint64_t)(offsets[i] + c.ks);
+    c.cs.n = (uint64_t)(sizes[i] - c.ks);
+    std::memcpy(c.cs.k, first, 12);
+    c.cs.dst = reinterpret_cast<uint32_t *>(c.e.d);
+  }
+  if (total) {
+    DevBuf &dgf = ctx->lscan;
+    if (dgf.ensure(total) || ctx->ensure_h_lst(total)) return ENOMEM;
+    for (int i = 0; i < n; i++) {
+      if (!sizes[i]) continue;
+      Cut &c = cut[(size_t)i];
+      ListHdr *dh = reinterpret_cast<ListHdr *>(dgf.as<uint8_t>(c.o_hdr));
+      HIPCHECK(hipMemsetAsync(dh, 0, sizeof(ListHdr), ctx->upload_stream));
+      hipLaunchKernelGGL(k_list_scan<true>, dim3(c.np), dim3(BLOCK), 0, ctx->upload_stream, c.e.d, c.e.units, c.e.pm,
+                         dgf.as<uint64_t>(c.o), dgf.as<uint64_t>(c.o_last), dh, c.cs);
+      hipLaunchKernelGGL(k_list_tail, dim3(1), dim3(1024), 0, ctx->upload_stream, c.np, c.e.pm);
+      HIPCHECK(hipGetLastError());
+    }
+    HIPCHECK(hipMemcpyAsync(ctx->h_lst, dgf.p, total, hipMemcpyDeviceToHost, ctx->upload_stream));
+    HIPCHECK(hipStreamSynchronize(ctx->upload_stream));
+    for (int i = 0; i < n; i++) {
+      if (!sizes[i]) continue;
+      Cut &c = cut[(size_t)i];
+      int rc = scan_result(c.e, ctx->h_lst + c.o, ctx->h_lst + c.o_last, ctx->h_lst + c.o_hdr, c.np, c.full);
+      if (rc) return rc;
+    }
+  }
+  if (DevBuf::canary_level() == 1)
+    for (int i = 0; i < n; i++) {
+      if (sizes[i] <= cut[(size_t)i].ks) continue;
+      const Cut &c = cut[(size_t)i];
+      std::vector<uint8_t> a((size_t)c.cs.n), b((size_t)c.cs.n);
+      HIPCHECK(hipMemcpy(a.data(), c.e.d + 12, a.size(), hipMemcpyDeviceToHost));
+      HIPCHECK(hipMemcpy(b.data(), f.mem->d + c.cs.src, b.size(), hipMemcpyDeviceToHost));
+      if (a != b)
+        std::fprintf(stderr, "gbgpu: canary: cut %lld+%lld differs from the file\n", (long long)offsets[i],
+                     (long long)sizes[i]);
+    }
+  // every cut checked: the handles
+  for (int i = 0; i < n; i++) {
+    int rc = sizes[i] ? register_list(ctx, cut[(size_t)i].e, &handles[i]) : upload_list(ctx, nullptr, 0, &handles[i]);
+    if (rc) {
+      for (int j = 0; j < i; j++) {
+        ctx->lists[handles[j]] = ListEntry();
+        handles[j] = -1;
+      }
+      return rc;
+    }
+  }
+  return 0;
+}
+
+int gbgpu_file_list(gbgpu_ctx *ctx, int32_t fh, int64_t offset, int64_t size, const uint8_t *key18,
+                    int32_t *handle) {
+  if (!ctx || !handle || offset < 0 || size < 0) return EINVAL;
+  return gbgpu_file_lists(ctx, fh, 1, &offset, &size, &key18, handle);
 }
 
 static gbmerge::MergeState *merge_state(gbgpu_ctx *ctx);

@@ -336,7 +336,7 @@ EXPORTS = [
     "gbgpu_open", "gbgpu_close", "gbgpu_strerror", "gbgpu_abi_version", "gbgpu_docs_wanted",
     "gbgpu_tree_capacity",
     "gbgpu_query", "gbgpu_list_upload", "gbgpu_list_free", "gbgpu_query_resident",
-    "gbgpu_file_upload", "gbgpu_file_list", "gbgpu_file_free",
+    "gbgpu_file_upload", "gbgpu_file_list", "gbgpu_file_lists", "gbgpu_file_free",
     "gbgpu_query_resident_enqueue", "gbgpu_query_collect", "gbgpu_stream",
     "gbgpu_last_topk_device", "gbgpu_merge_topk", "gbgpu_merge_posdb", "gbgpu_set_profiling",
     "gbgpu_last_timings", "gbgpu_set_query_slots", "gbgpu_query_slots", "gbgpu_query_slot_enqueue",
@@ -379,6 +379,8 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.gbgpu_list_free.argtypes = [vp, i32]
     lib.gbgpu_file_upload.argtypes = [vp, vp, i64, ctypes.POINTER(i32)]
     lib.gbgpu_file_list.argtypes = [vp, i32, i64, i64, vp, ctypes.POINTER(i32)]
+    lib.gbgpu_file_lists.argtypes = [vp, i32, ctypes.c_int, ctypes.POINTER(i64), ctypes.POINTER(i64), vp,
+                                     ctypes.POINTER(i32)]
     lib.gbgpu_file_free.argtypes = [vp, i32]
     lib.gbgpu_termlist_merge.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, i64, ctypes.POINTER(i32), vp, i64,
                                          ctypes.POINTER(i64)]
@@ -642,6 +644,23 @@ class Engine:
             k = ctypes.create_string_buffer(bytes(key18), 18)
         _check(self.lib.gbgpu_file_list(self.ctx, fh, offset, size, k, ctypes.byref(h)), "file_list")
         return h.value
+
+    def file_lists(self, fh: int, offsets, sizes, key18s=None):
+        """gbgpu_file_lists: a query's cuts together (all or nothing); key18s
+        None or one entry a cut, each None or the map's full key."""
+        n = len(offsets)
+        assert len(sizes) == n and (key18s is None or len(key18s) == n)
+        off = (ctypes.c_int64 * max(n, 1))(*offsets)
+        sz = (ctypes.c_int64 * max(n, 1))(*sizes)
+        hs = (ctypes.c_int32 * max(n, 1))()
+        keys, kp = None, None
+        if key18s is not None:
+            keys = [None if k is None else ctypes.create_string_buffer(bytes(k), 18) for k in key18s]
+            for k in key18s:
+                assert k is None or len(k) == 18
+            kp = (ctypes.c_void_p * max(n, 1))(*[None if k is None else ctypes.addressof(k) for k in keys])
+        _check(self.lib.gbgpu_file_lists(self.ctx, fh, n, off, sz, kp, hs), "file_lists")
+        return list(hs)[:n]
 
     def termlist_merge(self, pieces, remove_neg_keys: bool = True, min_rec_sizes: int = -1, want_bytes=False):
         """Msg5's read of one termlist: pieces oldest first, each (file handle,

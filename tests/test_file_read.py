@@ -168,7 +168,10 @@ def test_gpu_recut_lists_answer_as_resident(engine, slots):
                 assert r.hits == ref.hits and np.array_equal(r.docids, ref.docids), i
                 assert np.array_equal(r.scores.view(np.uint32), ref.scores.view(np.uint32)), i
             if i < 12:
-                fl = [engine.file_list(fh, o, len(x)) for o, x in zip(offs, lists)]
+                if i % 2:  # a query's cuts together (gbgpu_file_lists) and one by one
+                    fl = engine.file_lists(fh, offs, [len(x) for x in lists])
+                else:
+                    fl = [engine.file_list(fh, o, len(x)) for o, x in zip(offs, lists)]
                 engine.enqueue(q.terms, fl, p, slot=sl)
                 live[sl] = fl
     finally:
@@ -177,6 +180,65 @@ def test_gpu_recut_lists_answer_as_resident(engine, slots):
             for h in fl:
                 engine.free(h)
         for h in hs:
+            engine.free(h)
+        engine.file_free(fh)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("path", PIECE_FIX[:4], ids=IDS[::3][:4])
+def test_gpu_file_lists_batch(engine, path):
+    """gbgpu_file_lists: a query's cuts together -- pieces at compressed keys
+    with their map keys, whole lists without, an empty one -- answer what the
+    same cuts made one by one answer; a batch with one bad cut creates no
+    handle (the next cut gets the handle a leak would have taken)."""
+    terms, lists, params, exp = load_query(path)
+    blob, offs = _file(lists)
+    rng = np.random.default_rng(len(blob) + 1)
+    cut_o, cut_s, keys = [], [], []
+    for o, x in zip(offs, lists):
+        st = key_starts(x) if x else []
+        cand = [i for i, (_, k) in enumerate(st) if k < 18 and i >= len(st) // 2]
+        if cand and rng.random() < 0.7:
+            i = int(rng.choice(cand))
+            cut_o.append(o + st[i][0])
+            cut_s.append(len(x) - st[i][0])
+            keys.append(full_key(x, st, i))
+        else:
+            cut_o.append(o)
+            cut_s.append(len(x))
+            keys.append(None)
+    fh = engine.file_upload(blob)
+    hb, hs = [], []
+    try:
+        hb = engine.file_lists(fh, cut_o, cut_s, keys)
+        hs = [engine.file_list(fh, o, n, k) for o, n, k in zip(cut_o, cut_s, keys)]
+
+        def run(h):
+            try:
+                return engine.query_resident(terms, h, params, cap=1 << 16, hit_cap=1 << 20)
+            except gbgpu.GbgpuError as e:
+                return e.code
+
+        a, b = run(hb), run(hs)
+        if isinstance(a, int) or isinstance(b, int):
+            assert a == b
+        else:
+            assert a.hits == b.hits and np.array_equal(a.docids, b.docids)
+            assert np.array_equal(a.scores.view(np.uint32), b.scores.view(np.uint32))
+            assert np.array_equal(a.hit_docids, b.hit_docids)
+        # all or nothing
+        probe = engine.file_list(fh, cut_o[0], cut_s[0], keys[0])
+        engine.free(probe)
+        bad_o = list(cut_o) + [cut_o[0] + 1]  # off a key boundary: EINVAL
+        bad_s = list(cut_s) + [6]
+        with pytest.raises(gbgpu.GbgpuError):
+            engine.file_lists(fh, bad_o, bad_s, list(keys) + [None])
+        again = engine.file_list(fh, cut_o[0], cut_s[0], keys[0])
+        engine.free(again)
+        assert again == probe
+        assert engine.file_lists(fh, [], [], None) == []
+    finally:
+        for h in hb + hs:
             engine.free(h)
         engine.file_free(fh)
 
