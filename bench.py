@@ -629,7 +629,7 @@ def main():
         el_fr = time.perf_counter() - t_fr
         # the same with queries in flight: the next query's termlists are cut
         # (upload stream) while earlier ones run on their slots
-        fs = min(4, slots)
+        fs = min(int(os.environ.get("GBGPU_FR_INFLIGHT", "4")), slots)
         n_fq, w_fq = 120, 2 * fs  # the first 2*fs queries warm the slots (untimed)
         live = {}
         for i in range(n_fq + w_fq + fs):

@@ -9142,7 +9142,13 @@ int gbgpu_open(int device, gbgpu_ctx **out) {
   }
   Weights w = host_weights();
   ctx->arena->device = device;
-  if (hipStreamCreateWithFlags(&ctx->upload_stream, hipStreamNonBlocking) != hipSuccess ||
+  // the upload stream at the device's greatest priority (GBGPU_UPLOAD_PRIO=0:
+  // the default): a cut's scan, which the host waits on, is dispatched ahead
+  // of the queries in flight
+  int prio_lo = 0, prio_hi = 0;
+  (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+  if (const char *s = std::getenv("GBGPU_UPLOAD_PRIO"); s && *s == '0') prio_hi = prio_lo;
+  if (hipStreamCreateWithPriority(&ctx->upload_stream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
       hipMalloc((void **)&ctx->d_flag, 4) != hipSuccess ||
       hipHostMalloc((void **)&ctx->h_flag, 4) != hipSuccess ||
       hipMemcpyToSymbol(HIP_SYMBOL(c_weights), &w, sizeof w) != hipSuccess || grow_slots(ctx, 1) != 0) {
